@@ -1,0 +1,112 @@
+/*
+ * REFERENCE HARNESS — TEST INFRASTRUCTURE ONLY.
+ *
+ * Thin driver over the srsLTE reference FEC code compiled from its own sources in
+ * /root/reference/lib (recipe: oracle/Makefile, target `ref`; output oracle/_ref/). It exposes
+ * the same entry-point shapes as tdec_oracle.h so tests can check the restatement against the
+ * real reference, and tests/golden/make_golden.py can record golden vectors from it.
+ * Nothing here is product code and no reference source is copied into this repository.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "srslte/phy/fec/cbsegm.h"
+#include "srslte/phy/fec/crc.h"
+#include "srslte/phy/fec/tc_interl.h"
+#include "srslte/phy/fec/turbocoder.h"
+#include "srslte/phy/fec/turbodecoder.h"
+
+/* Same call sequence as turbodecoder_test.c:200-266 / sch.c:356-366: init, (force_not_sb),
+ * new_cb, then one srslte_tdec_iteration per half-iteration (each returns the decision). */
+int ref_tdec_run(int impl, int sb_layout, const int16_t *input, uint32_t K, uint32_t nof_halfits,
+                 uint8_t *decisions, int16_t *final_app1, int16_t *final_ext1) {
+  srslte_tdec_t h;
+  if (srslte_tdec_init_manual(&h, SRSLTE_TCOD_MAX_LEN_CB, (srslte_tdec_impl_type_t)impl)) return -1;
+  if (!sb_layout) srslte_tdec_force_not_sb(&h);
+  /* the reference writes tail copies into the input padding: give it a private copy */
+  size_t n = 3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 64;
+  int16_t *buf = NULL;
+  if (posix_memalign((void **)&buf, 64, n * sizeof(int16_t))) return -1;
+  memset(buf, 0, n * sizeof(int16_t));
+  int sb_eff = sb_layout && impl == SRSLTE_TDEC_AUTO && srslte_tdec_autoimp_get_subblocks(K) > 0;
+  size_t in_len = sb_eff ? 3 * (K + 32) + 12 : 3 * K + 12;
+  memcpy(buf, input, in_len * sizeof(int16_t));
+  if (srslte_tdec_new_cb(&h, K)) {
+    free(buf);
+    srslte_tdec_free(&h);
+    return -1;
+  }
+  uint8_t tmp[SRSLTE_TCOD_MAX_LEN_CB / 8];
+  for (uint32_t i = 0; i < nof_halfits; i++) {
+    srslte_tdec_iteration(&h, buf, decisions ? decisions + (size_t)i * (K / 8) : tmp);
+  }
+  if (final_app1) memcpy(final_app1, h.app1, K * sizeof(int16_t));
+  if (final_ext1) memcpy(final_ext1, h.ext1, K * sizeof(int16_t));
+  free(buf);
+  srslte_tdec_free(&h);
+  return 0;
+}
+
+/* srslte_tdec_run_all over many CBs with ONE decoder object (the CPU baseline loop of
+ * BASELINE.md §3). inputs: n x stride int16, natural layout (force_not_sb), outputs n x K/8. */
+int ref_tdec_run_all_many(int impl, const int16_t *inputs, size_t stride, uint32_t K, uint32_t n,
+                          uint32_t nof_halfits, uint8_t *outputs) {
+  srslte_tdec_t h;
+  if (srslte_tdec_init_manual(&h, SRSLTE_TCOD_MAX_LEN_CB, (srslte_tdec_impl_type_t)impl)) return -1;
+  srslte_tdec_force_not_sb(&h);
+  int16_t *buf = NULL;
+  size_t len = 3 * K + 12;
+  if (posix_memalign((void **)&buf, 64, (len + 64) * sizeof(int16_t))) return -1;
+  for (uint32_t c = 0; c < n; c++) {
+    memcpy(buf, inputs + (size_t)c * stride, len * sizeof(int16_t));
+    srslte_tdec_run_all(&h, buf, outputs + (size_t)c * (K / 8), nof_halfits, K);
+  }
+  free(buf);
+  srslte_tdec_free(&h);
+  return 0;
+}
+
+int ref_interl(uint32_t K, uint32_t nsb, uint16_t *fwd, uint16_t *rev) {
+  srslte_tc_interl_t t;
+  if (srslte_tc_interl_init(&t, SRSLTE_TCOD_MAX_LEN_CB)) return -1;
+  int r = srslte_tc_interl_LTE_gen_interl(&t, K, nsb);
+  if (!r) {
+    memcpy(fwd, t.forward, K * sizeof(uint16_t));
+    memcpy(rev, t.reverse, K * sizeof(uint16_t));
+  }
+  srslte_tc_interl_free(&t);
+  return r;
+}
+
+int ref_tcod_encode(const uint8_t *in_bits, uint8_t *out_bits, uint32_t K) {
+  srslte_tcod_t t;
+  if (srslte_tcod_init(&t, SRSLTE_TCOD_MAX_LEN_CB)) return -1;
+  uint8_t *in = malloc(K);
+  memcpy(in, in_bits, K);
+  int r = srslte_tcod_encode(&t, in, out_bits, K);
+  free(in);
+  /* srslte_tcod_free would tear down the shared static tables; keep them for reuse */
+  free(t.temp);
+  return r;
+}
+
+uint32_t ref_crc_checksum_byte(uint32_t poly, int order, const uint8_t *data, uint32_t len_bits) {
+  srslte_crc_t c;
+  if (srslte_crc_init(&c, poly, order)) return 0xffffffff;
+  return srslte_crc_checksum_byte(&c, (uint8_t *)data, (int)len_bits);
+}
+
+int ref_cbsegm(uint32_t tbs, uint32_t *out6) {
+  srslte_cbsegm_t s;
+  int r = srslte_cbsegm(&s, tbs);
+  out6[0] = s.C;
+  out6[1] = s.C1;
+  out6[2] = s.K1;
+  out6[3] = s.C2;
+  out6[4] = s.K2;
+  out6[5] = s.F;
+  return r;
+}
+
+uint32_t ref_autoimp_subblocks(uint32_t K) { return srslte_tdec_autoimp_get_subblocks(K); }
