@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X turbo-decoder hot path (BASELINE.json configs[1]).
+
+One "step" = decode one batch of 4096 code blocks of K=6144 bits with 8 half-iterations
+(srslte_tdec_run_all semantics, AUTO decoder = AVX16 window, 16 sub-blocks), inputs resident in
+HBM, through the C ABI (srsgpu_tdec_batch_run_dev). Synthetic traffic: random bits -> turbo
+encoder -> BPSK/AWGN -> int16 LLRs (turbodecoder_test.c:236-252 quantisation).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 run under torch.distributed.run: one rank per GPU, each decodes its own batch
+(independent code blocks, no data-path collective) -> weak scaling.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "empower-srslte_amd"))
+
+METRIC = "turbo-decoded Mbps + subframes/s, 20 MHz 64QAM, 1/2/4/8 MI355X"
+K = 6144
+NCB = 4096
+NHALF = 8
+EBNO_DB = 4.5            # reference convention (noise std sqrt(1/(Es/N0))), error-free region
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SF_BITS = 75376          # 20 MHz, MCS 28 transport block (13 x K=5824): subframe equivalent
+# Algorithmic bytes of one constituent-decoder launch (one half-iteration) per info bit:
+# read x (systematic/app, int16) + y (parity, int16), write the LLR (int16) = 6 B/bit.
+ALG_BYTES_PER_BIT_HALFIT = 6
+
+
+def make_inputs(n, seed, tcod):
+    """n code blocks: random bits, srslte_tcod_encode (product encoder), AWGN, int16 LLRs."""
+    rng = np.random.default_rng(seed)
+    ntmpl = min(n, 256)
+    bits = rng.integers(0, 2, (ntmpl, K), dtype=np.uint8)
+    coded = np.stack([tcod.encode(b) for b in bits])
+    idx = np.arange(n) % ntmpl
+    esno = EBNO_DB + 10 * np.log10(1.0 / 3.0)
+    sigma = np.float32(np.sqrt(1.0 / 10 ** (esno / 10)))
+    llr = np.empty((n, 3 * K + 12), np.int16)
+    for c0 in range(0, n, 512):
+        c1 = min(n, c0 + 512)
+        sym = np.where(coded[idx[c0:c1]].astype(bool), np.float32(1), np.float32(-1))
+        y = sym + sigma * rng.standard_normal(sym.shape, dtype=np.float32)
+        llr[c0:c1] = (np.float32(100) * y).astype(np.int16)
+    return bits, idx, llr
+
+
+def cpu_baseline(llr, nthreads):
+    """Reference AVX2 AUTO decoder (oracle/_ref, compiled from the reference's own sources) on
+    the host cores: one srslte_tdec_t per thread, srslte_tdec_run_all over a bounded sample of
+    the same code blocks. Falls back to the scalar oracle port if _ref is absent."""
+    ref = os.path.join(REPO, "oracle", "_ref", "libsrsref.so")
+    port = os.path.join(REPO, "oracle", "liboracle.so")
+    kind = "reference" if os.path.exists(ref) else "port"
+    lib = ctypes.CDLL(ref if kind == "reference" else port)
+    i16p = ctypes.POINTER(ctypes.c_int16)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    if kind == "reference":
+        fn = lib.ref_tdec_run_all_many
+        fn.argtypes = [ctypes.c_int, i16p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                       ctypes.c_uint32, u8p]
+
+        def work(rows, out):
+            fn(0, rows.ctypes.data_as(i16p), rows.shape[1], K, rows.shape[0], NHALF,
+               out.ctypes.data_as(u8p))
+    else:
+        fn = lib.orc_tdec_run
+        fn.argtypes = [ctypes.c_int, ctypes.c_int, i16p, ctypes.c_uint32, ctypes.c_uint32, u8p,
+                       i16p, i16p]
+        dec = np.zeros((NHALF, K // 8), np.uint8)
+
+        def work(rows, out):
+            for r in rows:
+                fn(0, 0, r.ctypes.data_as(i16p), K, NHALF, dec.ctypes.data_as(u8p), None, None)
+    # calibrate on two blocks, then size the sample to ~15 s of CPU work: each thread decodes
+    # its own slice of the batch R times
+    scratch = np.zeros((4, K // 8), np.uint8)
+    work(llr[:1], scratch)  # first call pays the decoder's table set-up
+    t0 = time.perf_counter()
+    work(llr[:4], scratch)
+    per_cb = (time.perf_counter() - t0) / 4
+    per_thread = max(1, llr.shape[0] // nthreads)
+    reps = int(max(1, min(64, round(15.0 / nthreads / max(per_cb * per_thread, 1e-6)))))
+
+    def thread_fn(i, out):
+        rows = llr[i * per_thread:(i + 1) * per_thread]
+        for _ in range(reps):
+            work(rows, out)
+
+    outs = [np.zeros((per_thread, K // 8), np.uint8) for _ in range(nthreads)]
+    ths = [threading.Thread(target=thread_fn, args=(i, outs[i])) for i in range(nthreads)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    wall = time.perf_counter() - t0
+    ncb = per_thread * nthreads * reps
+    return {"value": round(ncb * K / wall / 1e6, 2), "unit": "Mbps", "cores": nthreads,
+            "kind": kind,
+            "sample": "%d CB decodes of K=%d (%d threads x %d CBs x %d passes), %d half-iterations, "
+                      "AUTO (AVX2) decoder, natural layout, one srslte_tdec_t per thread, %.1f s wall"
+                      % (ncb, K, nthreads, per_thread, reps, NHALF, wall)}
+
+
+def load_pmc_traffic(workload):
+    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 PMC summary
+    (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py), if one matches."""
+    pdir = os.path.join(REPO, "profiles")
+    best = None
+    if os.path.isdir(pdir):
+        for f in sorted(os.listdir(pdir)):
+            if "pmc_traffic" in f and f.endswith(".json"):
+                try:
+                    d = json.load(open(os.path.join(pdir, f)))
+                except Exception:
+                    continue
+                if d.get("workload") == workload:
+                    best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import srsgpu_phy as s
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    tcod = s.Tcod(K)
+    bits, idx, llr = make_inputs(NCB, 1234 + rank, tcod)
+    d_in = torch.from_numpy(llr).to(dev)
+    d_out = torch.zeros((NCB, K // 8), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    batch = s.TdecBatch(NCB, K, stream=stream.cuda_stream)
+    stride = 3 * K + 12
+
+    def step():
+        r = batch.run_dev(0, 0, d_in.data_ptr(), stride, K, NCB, NHALF, d_out.data_ptr(), K // 8)
+        if r != 0:
+            raise RuntimeError("srsgpu_tdec_batch_run_dev failed")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # sanity: the decoded bits equal the transmitted ones (error-free SNR)
+    got = d_out.cpu().numpy()
+    expect = np.packbits(bits, axis=1)[idx]
+    bit_errors = int(np.unpackbits(got ^ expect).sum())
+
+    s.prof_reset()
+    s.prof_enable(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    s.prof_enable(False)
+    kern_ms, kern_n = s.prof_get("k_win_dec")
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([bit_errors], device=dev, dtype=torch.int64)
+        dist.all_reduce(e)
+        bit_errors = int(e.item())
+
+    nranks = max(1, world)
+    bits_total = nranks * NCB * K * args.steps
+    mbps = bits_total / elapsed / 1e6
+    result = None
+    if rank == 0:
+        workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
+        avg_launch_ms = kern_ms / max(kern_n, 1)
+        alg_bytes = ALG_BYTES_PER_BIT_HALFIT * NCB * K
+        achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
+        pmc = load_pmc_traffic(workload)
+        roofline = {"bound": "hbm", "kernel": "k_win_dec",
+                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                    "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(avg_launch_ms, 4),
+                    "launches": kern_n}
+        result = {
+            "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": nranks,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int16", "data": "synthetic",
+            "config": {"workload": workload, "code_blocks_per_gpu": NCB, "K": K,
+                       "half_iterations": NHALF, "decoder": "AUTO (AVX16 window, 16 sub-blocks)",
+                       "ebno_db_ref_convention": EBNO_DB, "parallelism": "dp%d" % nranks,
+                       "subframes_per_s_equiv": round(bits_total / elapsed / SF_BITS, 1),
+                       "bit_errors": bit_errors},
+            "roofline": roofline,
+        }
+    if rank == 0 and not args.no_cpu_baseline and nranks == 1:
+        result["cpu_baseline"] = cpu_baseline(llr, int(os.environ.get("SRSGPU_CPU_THREADS",
+                                                                       min(16, os.cpu_count() or 1))))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    batch.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

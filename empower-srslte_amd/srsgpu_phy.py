@@ -1,0 +1,240 @@
+"""Python host-side mirror of the srsLTE turbo-decoder API on the MI355X engine.
+
+Loads lib/libsrsgpu_phy.so (built by `make -C empower-srslte_amd`, C ABI in
+include/srslte/phy/fec/turbodecoder.h and include/srsgpu/tdec_batch.h) through ctypes.
+
+  Tdec       one srslte_tdec_t object (reference: lib/src/phy/fec/turbodecoder.c:133-564):
+             init/new_cb/iteration/run_all/get_nof_iterations/free, same return codes.
+  TdecBatch  the batched extension: many code blocks of one size per call, host arrays or
+             device pointers (e.g. torch.cuda tensors' data_ptr()).
+
+There is no CPU fallback: if the library is missing this module raises at import time.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libsrsgpu_phy.so")
+
+SRSLTE_TDEC_AUTO, SRSLTE_TDEC_GENERIC, SRSLTE_TDEC_SSE = 0, 1, 2
+SRSLTE_TDEC_SSE_WINDOW, SRSLTE_TDEC_AVX_WINDOW = 3, 4
+SRSLTE_TDEC_SSE8_WINDOW, SRSLTE_TDEC_AVX8_WINDOW = 5, 6
+SRSLTE_SUCCESS, SRSLTE_ERROR = 0, -1
+CRC24A, CRC24B = 0x1864CFB, 0x1800063
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("srsgpu: %s not found — build it with `make -C empower-srslte_amd` "
+                      "(no CPU fallback exists)" % LIB_PATH)
+
+_lib = ctypes.CDLL(LIB_PATH)
+_vp, _sz, _u32, _i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+_i16p = ctypes.POINTER(ctypes.c_int16)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+class srslte_tdec_t(ctypes.Structure):
+    """Layout of srslte_tdec_t in include/srslte/phy/fec/turbodecoder.h."""
+    _fields_ = [("max_long_cb", ctypes.c_uint32), ("dec_type", ctypes.c_int),
+                ("force_not_sb", ctypes.c_bool), ("current_long_cb", ctypes.c_uint32),
+                ("current_cbidx", ctypes.c_int), ("n_iter", ctypes.c_int), ("gpu", ctypes.c_void_p)]
+
+
+class srslte_tcod_t(ctypes.Structure):
+    """Layout of srslte_tcod_t in include/srslte/phy/fec/turbocoder.h."""
+    _fields_ = [("max_long_cb", ctypes.c_uint32), ("temp", ctypes.c_void_p)]
+
+
+_P = ctypes.POINTER(srslte_tdec_t)
+_PC = ctypes.POINTER(srslte_tcod_t)
+_sig = {
+    "srslte_tdec_init": (_i32, [_P, _u32]),
+    "srslte_tdec_init_manual": (_i32, [_P, _u32, _i32]),
+    "srslte_tdec_free": (None, [_P]),
+    "srslte_tdec_force_not_sb": (None, [_P]),
+    "srslte_tdec_new_cb": (_i32, [_P, _u32]),
+    "srslte_tdec_get_nof_iterations": (_i32, [_P]),
+    "srslte_tdec_autoimp_get_subblocks": (_u32, [_u32]),
+    "srslte_tdec_autoimp_get_subblocks_8bit": (_u32, [_u32]),
+    "srslte_tdec_iteration": (None, [_P, _i16p, _u8p]),
+    "srslte_tdec_run_all": (_i32, [_P, _i16p, _u8p, _u32, _u32]),
+    "srslte_tdec_iteration_8bit": (None, [_P, ctypes.POINTER(ctypes.c_int8), _u8p]),
+    "srslte_tdec_run_all_8bit": (_i32, [_P, ctypes.POINTER(ctypes.c_int8), _u8p, _u32, _u32]),
+    "srslte_tcod_init": (_i32, [_PC, _u32]),
+    "srslte_tcod_free": (None, [_PC]),
+    "srslte_tcod_encode": (_i32, [_PC, _u8p, _u8p, _u32]),
+    "srsgpu_tdec_batch_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32]),
+    "srsgpu_tdec_batch_destroy": (None, [_vp]),
+    "srsgpu_tdec_batch_set_stream": (None, [_vp, _vp]),
+    "srsgpu_tdec_batch_run_dev": (_i32, [_vp, _i32, _i32, _vp, _sz, _u32, _u32, _u32, _vp, _sz]),
+    "srsgpu_tdec_batch_decode_dev": (_i32, [_vp, _i32, _i32, _vp, _sz, _u32, _u32, _u32, _u32,
+                                            _u32, _vp, _sz, _vp, _vp]),
+    "srsgpu_tdec_batch_run": (_i32, [_vp, _i32, _i32, ctypes.POINTER(_vp), _u32, _u32, _u32,
+                                     ctypes.POINTER(_vp)]),
+    "srsgpu_tdec_batch_decode": (_i32, [_vp, _i32, _i32, ctypes.POINTER(_vp), _u32, _u32, _u32,
+                                        _u32, _u32, ctypes.POINTER(_vp), _u8p, _u32p]),
+    "srsgpu_tdec_input_len": (_u32, [_i32, _i32, _u32]),
+    "srsgpu_prof_enable": (None, [_i32]),
+    "srsgpu_prof_reset": (None, []),
+    "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_uint64)]),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(_lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+EXPORTED = tuple(_sig)
+
+
+def _i16(a):
+    return a.ctypes.data_as(_i16p)
+
+
+def _u8(a):
+    return a.ctypes.data_as(_u8p)
+
+
+def input_len(impl, sb_layout, K):
+    return _lib.srsgpu_tdec_input_len(impl, sb_layout, K)
+
+
+def autoimp_get_subblocks(K):
+    return _lib.srslte_tdec_autoimp_get_subblocks(K)
+
+
+class Tdec:
+    """srslte_tdec_t (one code block at a time, one half-iteration per iteration() call)."""
+
+    def __init__(self, max_long_cb=6144, dec_type=SRSLTE_TDEC_AUTO):
+        self.h = srslte_tdec_t()
+        r = _lib.srslte_tdec_init_manual(ctypes.byref(self.h), max_long_cb, dec_type)
+        if r != SRSLTE_SUCCESS:
+            raise RuntimeError("srslte_tdec_init_manual failed (%d)" % r)
+
+    def force_not_sb(self):
+        _lib.srslte_tdec_force_not_sb(ctypes.byref(self.h))
+
+    def new_cb(self, K):
+        return _lib.srslte_tdec_new_cb(ctypes.byref(self.h), K)
+
+    def iteration(self, inp, out):
+        _lib.srslte_tdec_iteration(ctypes.byref(self.h), _i16(inp), _u8(out))
+
+    def run_all(self, inp, out, nof_iterations, K):
+        return _lib.srslte_tdec_run_all(ctypes.byref(self.h), _i16(inp), _u8(out), nof_iterations, K)
+
+    def get_nof_iterations(self):
+        return _lib.srslte_tdec_get_nof_iterations(ctypes.byref(self.h))
+
+    def free(self):
+        if self.h.gpu:
+            _lib.srslte_tdec_free(ctypes.byref(self.h))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class TdecBatch:
+    """srsgpu_tdec_batch_t: batched decoding of code blocks of one size."""
+
+    def __init__(self, max_cbs, max_long_cb=6144, stream=None):
+        self.q = _vp()
+        r = _lib.srsgpu_tdec_batch_create(ctypes.byref(self.q), max_cbs, max_long_cb)
+        if r != 0:
+            raise RuntimeError("srsgpu_tdec_batch_create failed")
+        if stream is not None:
+            self.set_stream(stream)
+
+    def set_stream(self, stream):
+        _lib.srsgpu_tdec_batch_set_stream(self.q, _vp(stream))
+
+    # ---- device pointers (ints) ----
+    def run_dev(self, impl, sb, d_in, in_stride, K, n, nhalf, d_out, out_stride):
+        return _lib.srsgpu_tdec_batch_run_dev(self.q, impl, sb, _vp(d_in), in_stride, K, n, nhalf,
+                                              _vp(d_out), out_stride)
+
+    def decode_dev(self, impl, sb, d_in, in_stride, K, n, maxh, poly, crc_len, d_out, out_stride,
+                   d_ok=None, d_noi=None):
+        return _lib.srsgpu_tdec_batch_decode_dev(self.q, impl, sb, _vp(d_in), in_stride, K, n,
+                                                 maxh, poly, crc_len, _vp(d_out), out_stride,
+                                                 _vp(d_ok), _vp(d_noi))
+
+    # ---- host numpy arrays ----
+    def run(self, impl, sb, inputs, K, nhalf):
+        n = len(inputs)
+        ins = [np.ascontiguousarray(x, np.int16) for x in inputs]
+        outs = [np.zeros(K // 8, np.uint8) for _ in range(n)]
+        ip = (_vp * n)(*[x.ctypes.data for x in ins])
+        op = (_vp * n)(*[x.ctypes.data for x in outs])
+        r = _lib.srsgpu_tdec_batch_run(self.q, impl, sb, ip, K, n, nhalf, op)
+        if r != 0:
+            raise RuntimeError("srsgpu_tdec_batch_run failed")
+        return np.stack(outs)
+
+    def decode(self, impl, sb, inputs, K, maxh, poly, crc_len):
+        n = len(inputs)
+        ins = [np.ascontiguousarray(x, np.int16) for x in inputs]
+        outs = [np.zeros(K // 8, np.uint8) for _ in range(n)]
+        ok = np.zeros(n, np.uint8)
+        noi = np.zeros(n, np.uint32)
+        ip = (_vp * n)(*[x.ctypes.data for x in ins])
+        op = (_vp * n)(*[x.ctypes.data for x in outs])
+        r = _lib.srsgpu_tdec_batch_decode(self.q, impl, sb, ip, K, n, maxh, poly, crc_len, op,
+                                          ok.ctypes.data_as(_u8p), noi.ctypes.data_as(_u32p))
+        if r != 0:
+            raise RuntimeError("srsgpu_tdec_batch_decode failed")
+        return np.stack(outs), ok, noi
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_tdec_batch_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Tcod:
+    """srslte_tcod_t bit encoder (host): bits in, [s,p0,p1]*K + 12 tail bits out."""
+
+    def __init__(self, max_long_cb=6144):
+        self.h = srslte_tcod_t()
+        if _lib.srslte_tcod_init(ctypes.byref(self.h), max_long_cb) != 0:
+            raise RuntimeError("srslte_tcod_init failed")
+
+    def encode(self, bits):
+        bits = np.ascontiguousarray(bits, np.uint8)
+        out = np.zeros(3 * bits.size + 12, np.uint8)
+        if _lib.srslte_tcod_encode(ctypes.byref(self.h), _u8(bits), _u8(out), bits.size) != 0:
+            raise RuntimeError("srslte_tcod_encode failed")
+        return out
+
+    def __del__(self):
+        try:
+            _lib.srslte_tcod_free(ctypes.byref(self.h))
+        except Exception:
+            pass
+
+
+def prof_enable(on=True):
+    _lib.srsgpu_prof_enable(1 if on else 0)
+
+
+def prof_reset():
+    _lib.srsgpu_prof_reset()
+
+
+def prof_get(name):
+    t = ctypes.c_double(0)
+    c = ctypes.c_uint64(0)
+    _lib.srsgpu_prof_get(name.encode() if name else None, ctypes.byref(t), ctypes.byref(c))
+    return t.value, c.value

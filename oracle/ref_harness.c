@@ -110,3 +110,33 @@ int ref_cbsegm(uint32_t tbs, uint32_t *out6) {
 }
 
 uint32_t ref_autoimp_subblocks(uint32_t K) { return srslte_tdec_autoimp_get_subblocks(K); }
+
+/* decode_tb_cb inner loop for one code block (sch.c:356-391): srslte_tdec_iteration then
+ * srslte_crc_checksum_byte until the CRC passes or max_halfits half-iterations ran. */
+int ref_tdec_decode_cb(int impl, int sb_layout, const int16_t *input, uint32_t K,
+                       uint32_t max_halfits, uint32_t crc_poly, uint32_t crc_len_bits,
+                       uint8_t *out_bytes, uint32_t *noi) {
+  srslte_tdec_t h;
+  srslte_crc_t crc;
+  if (srslte_crc_init(&crc, crc_poly, 24)) return -1;
+  if (srslte_tdec_init_manual(&h, SRSLTE_TCOD_MAX_LEN_CB, (srslte_tdec_impl_type_t)impl)) return -1;
+  if (!sb_layout) srslte_tdec_force_not_sb(&h);
+  size_t n = 3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 64;
+  int16_t *buf = NULL;
+  if (posix_memalign((void **)&buf, 64, n * sizeof(int16_t))) return -1;
+  memset(buf, 0, n * sizeof(int16_t));
+  int sb_eff = sb_layout && impl == SRSLTE_TDEC_AUTO && srslte_tdec_autoimp_get_subblocks(K) > 0;
+  memcpy(buf, input, (sb_eff ? 3 * (K + 32) + 12 : 3 * K + 12) * sizeof(int16_t));
+  srslte_tdec_new_cb(&h, K);
+  int ok = 0;
+  uint32_t it = 0;
+  do {
+    srslte_tdec_iteration(&h, buf, out_bytes);
+    it++;
+    if (!srslte_crc_checksum_byte(&crc, out_bytes, (int)crc_len_bits)) ok = 1;
+  } while (it < max_halfits && !ok);
+  *noi = it;
+  free(buf);
+  srslte_tdec_free(&h);
+  return ok;
+}

@@ -1,0 +1,30 @@
+import os
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "empower-srslte_amd"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from srsgpu_testlib import Oracle
+    return Oracle()
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    import numpy as np
+    z = np.load(os.path.join(HERE, "golden", "tdec_golden.npz"))
+    manifest = json.loads(bytes(z["manifest"]).decode())
+    return z, manifest

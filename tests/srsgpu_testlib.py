@@ -153,3 +153,21 @@ def make_cb(K, ebno_db, seed, oracle=None):
     o = oracle or Oracle()
     coded = o.tcod_encode(bits)
     return bits, awgn_llr(coded, ebno_db, rng)
+
+
+def pack_bits(bits):
+    """bits (0/1, MSB first) -> bytes, as srslte_bit_pack_vector."""
+    return np.packbits(np.asarray(bits, np.uint8))
+
+
+def make_crc_cb(K, ebno_db, seed, poly=CRC24B, oracle=None):
+    """Code block whose last 24 bits are the CRC of the first K-24 (TS 36.212 5.1.1/5.1.2),
+    so the CRC over all K decoded bits is 0 exactly when decoding succeeds."""
+    o = oracle or Oracle()
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 2, K - 24, dtype=np.uint8)
+    crc = o.crc(poly, pack_bits(data), K - 24)
+    crcbits = np.array([(crc >> (23 - i)) & 1 for i in range(24)], np.uint8)
+    bits = np.concatenate([data, crcbits])
+    coded = o.tcod_encode(bits)
+    return bits, awgn_llr(coded, ebno_db, rng)
