@@ -186,7 +186,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     s.prof_enable(False)
-    kern_ms, kern_n = s.prof_get("k_win_dec")
+    kern_ms, kern_n = s.prof_get("k_win_halfit")
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -205,7 +205,7 @@ def main():
         alg_bytes = ALG_BYTES_PER_BIT_HALFIT * NCB * K
         achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
         pmc = load_pmc_traffic(workload)
-        roofline = {"bound": "hbm", "kernel": "k_win_dec",
+        roofline = {"bound": "hbm", "kernel": "k_win_halfit",
                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                     "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,

@@ -2,13 +2,11 @@
 // C ABI (include/srsgpu/tdec_batch.h + the drop-in include/srslte/phy/fec/turbodecoder.h).
 //
 // Schedule per code-block batch (all CBs share K; mirrors turbodecoder_iter.h:283-357):
-//   load                     user layout -> pair-interleaved syst/par0/par1 + tails
-//   n even: prep_even(n)     app1 = deinterleave(ext2) - ext1 (n>0); x = syst (+) app1
-//           dec -> ext1      constituent decoder 1
-//   n odd:  prep_odd(n)      ext1 -= app1 (n>1); x = interleave(ext1)
-//           dec -> ext2      constituent decoder 2
-//   decide(n)                hard decision (ext1 after DEC1, deinterleaved ext2 after DEC2)
-//   crc(n)                   only with early stop (sch.c:361-391)
+//   load          user layout -> pair-interleaved syst/par0 (SP0), par1 (XP1), tails; A = 0
+//   halfit(n)     one constituent decoder run: DEC1 for even n, DEC2 for odd n, with the
+//                 interleave / subtract glue fused into its output stage (tdec_kernels.hip)
+//   decide(n)     hard decision after half-iteration n (+ CRC and early-stop flags when asked,
+//                 sch.c:361-391)
 #include <hip/hip_runtime.h>
 
 #include <map>
@@ -128,10 +126,8 @@ struct Engine {
   hipStream_t st = nullptr;
   uint32_t cap_cbs = 0, cap_K = 0;
   size_t cap_pairs = 0;
-  // pair-interleaved short2 arrays [pairs][K]
-  void *S = nullptr, *P0 = nullptr, *P1 = nullptr, *T = nullptr, *A = nullptr, *X2 = nullptr;
-  void *E[2] = {nullptr, nullptr};
-  void *XY = nullptr;      // short4 [pairs][K]
+  // pair-interleaved arrays [pairs][K]: SP0, XP1 short4; A short2; T short2 [pairs][12]
+  void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr;
   void *scratch = nullptr; // checkpoints (windowed) / alpha-beta (sequential)
   size_t scratch_bytes = 0;
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
@@ -141,7 +137,7 @@ struct Engine {
   std::map<std::pair<uint32_t, uint32_t>, std::pair<uint16_t *, uint16_t *>> interl;
   // current job
   uint32_t K = 0;
-  int impl_r = 0, nb = 1, ncb = 0, npairs = 0, ecur = 0;
+  int impl_r = 0, nb = 1, ncb = 0, npairs = 0;
   const uint16_t *fwd = nullptr, *rev = nullptr;
 
   int create(uint32_t max_cbs, uint32_t max_K) {
@@ -158,14 +154,9 @@ struct Engine {
     cap_K = max_K;
     cap_pairs = (max_cbs + 1) / 2;
     const size_t arr = cap_pairs * max_K * 4;
-    HIPCHK(hipMalloc(&S, arr));
-    HIPCHK(hipMalloc(&P0, arr));
-    HIPCHK(hipMalloc(&P1, arr));
+    HIPCHK(hipMalloc(&SP0, arr * 2));
+    HIPCHK(hipMalloc(&XP1, arr * 2));
     HIPCHK(hipMalloc(&A, arr));
-    HIPCHK(hipMalloc(&X2, arr));
-    HIPCHK(hipMalloc(&E[0], arr));
-    HIPCHK(hipMalloc(&E[1], arr));
-    HIPCHK(hipMalloc(&XY, arr * 2));
     HIPCHK(hipMalloc(&T, cap_pairs * 12 * 4));
     size_t ck = 0;
     for (int nbv : {8, 16}) {
@@ -181,7 +172,7 @@ struct Engine {
   }
 
   void destroy() {
-    for (void *p : {S, P0, P1, A, X2, E[0], E[1], XY, T, scratch})
+    for (void *p : {SP0, XP1, A, T, scratch})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
                     (void *)out_stage})
@@ -243,10 +234,9 @@ struct Engine {
     nb = nbv;
     ncb = (int)n;
     npairs = (ncb + 1) / 2;
-    ecur = 0;
     if (get_interleaver(K, (uint32_t)nb)) return -1;
     const int sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nb > 1;
-    HIPCHK(srsgpu::launch_load(d_in, in_stride, sb_input, (int)K, nb, ncb, S, P0, P1, T, st));
+    HIPCHK(srsgpu::launch_load(d_in, in_stride, sb_input, (int)K, nb, ncb, SP0, XP1, A, T, st));
     HIPCHK(hipMemsetAsync(cb_done, 0, cap_pairs * 2, st));
     HIPCHK(hipMemsetAsync(cb_ok, 0, cap_pairs * 2, st));
     HIPCHK(hipMemsetAsync(pair_done, 0, cap_pairs, st));
@@ -255,32 +245,17 @@ struct Engine {
 
   int halfit(int n, bool early) {
     const uint8_t *pd = early ? pair_done : nullptr;
-    const int wrap_mode = nb == 1; // SSE / generic add app with wrapping arithmetic
-    if ((n & 1) == 0) {
-      HIPCHK(srsgpu::launch_prep_even(n, (int)K, npairs, rev, S, P0, X2, E[ecur], A, XY, wrap_mode, pd, st));
-      ProfScope ps(nb > 1 ? "k_win_dec" : (impl_r == SRSLTE_TDEC_SSE ? "k_sse_dec" : "k_gen_dec"), st);
-      HIPCHK(dec(0, E[ecur], pd));
-    } else {
-      int eo = ecur;
-      if (n > 1) eo = ecur ^ 1;
-      HIPCHK(srsgpu::launch_prep_odd(n, (int)K, npairs, fwd, P1, E[ecur], A, E[eo], XY, pd, st));
-      ecur = eo;
-      ProfScope ps(nb > 1 ? "k_win_dec" : (impl_r == SRSLTE_TDEC_SSE ? "k_sse_dec" : "k_gen_dec"), st);
-      HIPCHK(dec(6, X2, pd));
-    }
+    const int seq = impl_r == SRSLTE_TDEC_SSE ? 0 : 1;
+    ProfScope ps(nb > 1 ? "k_win_halfit" : (seq == 0 ? "k_sse_halfit" : "k_gen_halfit"), st);
+    HIPCHK(srsgpu::launch_halfit(n, nb, seq, SP0, XP1, A, T, fwd, rev, scratch, pd, (int)K, npairs, st));
     return 0;
   }
 
-  hipError_t dec(int tail_xoff, void *out, const uint8_t *pd) {
-    if (nb > 1) return srsgpu::launch_win_dec(nb, XY, T, tail_xoff, out, scratch, pd, (int)K, npairs, st);
-    if (impl_r == SRSLTE_TDEC_SSE)
-      return srsgpu::launch_sse_dec(XY, T, tail_xoff, out, scratch, pd, (int)K, npairs, st);
-    return srsgpu::launch_gen_dec(XY, T, tail_xoff, out, scratch, pd, (int)K, npairs, st);
-  }
-
-  int decide(int n, uint8_t *d_out, size_t out_stride, bool early) {
-    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, rev, E[ecur], X2, d_out, out_stride,
-                                 early ? cb_done : nullptr, st));
+  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t poly = 0,
+             uint32_t crc_bytes = 0, uint32_t maxh = 0) {
+    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, rev, A, XP1, d_out, out_stride,
+                                 early ? cb_done : nullptr, cb_ok, noi, early ? (int)crc_bytes : 0,
+                                 poly, (int)maxh, pair_done, st));
     return 0;
   }
 
@@ -306,9 +281,7 @@ struct Engine {
     if (load(impl, sb_layout, d_in, in_stride, Kv, n)) return -1;
     for (uint32_t h = 0; h < maxh; h++) {
       if (halfit((int)h, true)) return -1;
-      if (decide((int)h, d_out, out_stride, true)) return -1;
-      HIPCHK(srsgpu::launch_crc_check((int)h, ncb, (int)(crc_len / 8), poly, d_out, out_stride, cb_done,
-                                      cb_ok, noi, (int)maxh, pair_done, st));
+      if (decide((int)h, d_out, out_stride, true, poly, crc_len / 8, maxh)) return -1;
     }
     if (d_ok) HIPCHK(hipMemcpyAsync(d_ok, cb_ok, (size_t)n, hipMemcpyDeviceToDevice, st));
     if (d_noi) HIPCHK(hipMemcpyAsync(d_noi, noi, (size_t)n * 4, hipMemcpyDeviceToDevice, st));

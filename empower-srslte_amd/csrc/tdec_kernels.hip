@@ -4,22 +4,33 @@
 //     SSE16: 8 sub-blocks + output >>1), saturating int16
 //   * SSE non-window     src/phy/fec/turbodecoder_sse.c (halved branch metrics, wrapping int16)
 //   * generic            src/phy/fec/turbodecoder_gen.c (wrapping int16)
-// and the half-iteration glue of include/srslte/phy/fec/turbodecoder_iter.h:283-357.
+// with the half-iteration glue of include/srslte/phy/fec/turbodecoder_iter.h:283-357 fused into
+// the decoder's output stage (no separate interleave/subtract passes).
 //
-// Data layout (HBM): code blocks are processed in PAIRS. Every per-CB int16 array is stored
-// pair-interleaved as short2 [npairs][K] — element j of CB 2p sits in .x, of CB 2p+1 in .y —
-// so one packed VALU op (v_pk_add_i16 clamp, v_pk_max_i16) advances both chains of a lane.
-// Inside a code block the index j is the reference's sub-block (SB) index: j = k*NB + d holds
-// natural position d*(K/NB) + k (rm_turbo.c:239-264), so the 16 (or 8) chains of one pair that
-// run in lockstep at step k touch NB consecutive short2, and, because QPP interleavers are
-// contention-free for every window length dividing K, the interleaver gathers of one step also
-// hit NB consecutive elements.
+// ---- Data layout in HBM ---------------------------------------------------------------------
+// Code blocks are processed in PAIRS: every per-CB int16 array is stored pair-interleaved
+// (element j of CB 2p in .x, of CB 2p+1 in .y) so one packed VALU op (v_pk_add_i16 clamp,
+// v_pk_max_i16) advances both chains of a lane. Within a CB the index j is the reference's
+// sub-block (SB) index: j = k*NB + d holds natural position d*(K/NB) + k (rm_turbo.c:239-264).
+// The NB chains of one pair run in lockstep over k, so a step's loads touch NB consecutive
+// elements; and since QPP interleavers are contention-free for every window length dividing K
+// (pi(x + tW) = pi(x) mod W), the interleaver scatters of one step also land on NB consecutive
+// elements (permuted) — every global access is a 64/128-byte coalesced group.
+//   SP0[pair][K]  short4 (syst.a, syst.b, par0.a, par0.b)          static
+//   XP1[pair][K]  short4 (app2.a, app2.b, par1.a, par1.b)          app2 rewritten by DEC1
+//   A  [pair][K]  short2  app1 - ext1 ("a priori" of DEC1), 0 before the first half-iteration
+//   T  [pair][12] short2  tail values as in the reference input (s,p0)x3 (app2,p1)x3
+// Half-iteration n even (DEC1): x = syst (+) A, y = par0; the LLR L gives E' = L - A, scattered
+//   to app2[rev[j]] (the reference's ext1 -= app1 and vec_lut interleave).
+// n odd (DEC2): x = app2, y = par1; A[fwd[j]] = L - app2[j] (vec_lut deinterleave, app1 -= ext1).
+// Hard decision after either: bit(p) = A + app2[rev] at j(p) > 0 (= ext1 after DEC1, app1 after
+// DEC2, because both subtractions are exactly invertible modulo 2^16).
 //
-// Windowed decoder mapping: one lane = one sub-block chain of one CB pair; a 64-lane wave
-// carries 64/NB pairs. The backward (beta) pass keeps only every W-th state metric (plus the
-// one at L) in a coalesced global checkpoint buffer; the forward (alpha) pass recomputes the W
-// betas of each segment from its checkpoint into registers (exact: integer recursion) and
-// emits the LLRs. This avoids streaming 16 B/bit/half-iteration of beta through HBM.
+// ---- Windowed decoder mapping ---------------------------------------------------------------
+// One lane = one sub-block chain of one CB pair, a 64-lane wave = 64/NB pairs. The backward pass
+// keeps every 8th state metric (and the one at L) in a coalesced global checkpoint buffer; the
+// forward pass recomputes the 8 betas of each segment from its checkpoint into registers (exact:
+// integer recursion) and emits LLRs. All inputs are software-pipelined one 8-step chunk ahead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,20 +43,22 @@ typedef short s4 __attribute__((ext_vector_type(4)));
 
 #define TD_INF 10000  // turbodecoder_win.h:63 / _sse.c:51 / _gen.c:41
 #define TD_OVERLAP 40 // turbodecoder_win.h:59 win_overlap_len
+#define TD_W 8        // checkpoint period / chunk length (steps)
 
 __device__ __forceinline__ s2 sadd(s2 a, s2 b) { return __builtin_elementwise_add_sat(a, b); }
 __device__ __forceinline__ s2 ssub(s2 a, s2 b) { return __builtin_elementwise_sub_sat(a, b); }
 __device__ __forceinline__ s2 smax(s2 a, s2 b) { return __builtin_elementwise_max(a, b); }
 // wrapping int16 arithmetic on packed halves (v_pk_add_u16 / v_pk_sub_u16)
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ s2 wadd(s2 a, s2 b) {
-  typedef unsigned short u2 __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(s2, __builtin_bit_cast(u2, a) + __builtin_bit_cast(u2, b));
 }
 __device__ __forceinline__ s2 wsub(s2 a, s2 b) {
-  typedef unsigned short u2 __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(s2, __builtin_bit_cast(u2, a) - __builtin_bit_cast(u2, b));
 }
 __device__ __forceinline__ s2 splat(short v) { return s2{v, v}; }
+__device__ __forceinline__ s2 lo2(s4 v) { return s2{v.x, v.y}; }
+__device__ __forceinline__ s2 hi2(s4 v) { return s2{v.z, v.w}; }
 
 struct St8 {
   s2 s[8];
@@ -133,125 +146,233 @@ __device__ __forceinline__ void st_fill(St8 &o, short v0, short v) {
   for (int i = 1; i < 8; i++) o.s[i] = splat(v);
 }
 
-// checkpoint slot of stored-beta index k (k = L or a multiple of W)
-template <int W>
-__device__ __forceinline__ int ck_slot(int k) { return (k + W - 1) / W; }
-
 __device__ __forceinline__ void ck_store(s4 *ck, size_t off, const St8 &o) {
-  s4 a = {o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
-  s4 b = {o.s[2].x, o.s[2].y, o.s[3].x, o.s[3].y};
-  s4 c = {o.s[4].x, o.s[4].y, o.s[5].x, o.s[5].y};
-  s4 d = {o.s[6].x, o.s[6].y, o.s[7].x, o.s[7].y};
-  ck[off * 4 + 0] = a;
-  ck[off * 4 + 1] = b;
-  ck[off * 4 + 2] = c;
-  ck[off * 4 + 3] = d;
+  s4 *p = ck + off * 4;
+  p[0] = s4{o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
+  p[1] = s4{o.s[2].x, o.s[2].y, o.s[3].x, o.s[3].y};
+  p[2] = s4{o.s[4].x, o.s[4].y, o.s[5].x, o.s[5].y};
+  p[3] = s4{o.s[6].x, o.s[6].y, o.s[7].x, o.s[7].y};
 }
-__device__ __forceinline__ void ck_load(const s4 *ck, size_t off, St8 &o) {
-  s4 a = ck[off * 4 + 0], b = ck[off * 4 + 1], c = ck[off * 4 + 2], d = ck[off * 4 + 3];
-  o.s[0] = s2{a.x, a.y};
-  o.s[1] = s2{a.z, a.w};
-  o.s[2] = s2{b.x, b.y};
-  o.s[3] = s2{b.z, b.w};
-  o.s[4] = s2{c.x, c.y};
-  o.s[5] = s2{c.z, c.w};
-  o.s[6] = s2{d.x, d.y};
-  o.s[7] = s2{d.z, d.w};
+struct Ck {
+  s4 v[4];
+};
+__device__ __forceinline__ void ck_load(const s4 *ck, size_t off, Ck &c) {
+  const s4 *p = ck + off * 4;
+  c.v[0] = p[0];
+  c.v[1] = p[1];
+  c.v[2] = p[2];
+  c.v[3] = p[3];
+}
+__device__ __forceinline__ void ck_unpack(const Ck &c, St8 &o) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    o.s[2 * i] = lo2(c.v[i]);
+    o.s[2 * i + 1] = hi2(c.v[i]);
+  }
 }
 
-// One constituent MAP decoder run (turbodecoder_win.h:614-622) for every sub-block chain of
-// every CB pair. xy: short4 [npairs][K] = (x.a, x.b, y.a, y.b) at SB index; tail: short2
-// [npairs][12]; out: short2 [npairs][K]; ck: checkpoint scratch.
-template <int NB, int DIV, int W>
-__global__ __launch_bounds__(256) void k_win_dec(const s4 *__restrict__ xy,
-                                                 const s2 *__restrict__ tail, int tail_xoff,
-                                                 s2 *__restrict__ out, s4 *__restrict__ ck,
-                                                 const uint8_t *__restrict__ pair_done, int K,
-                                                 int npairs) {
+// ------------------------------------------------------------------ input policy ----
+// Per-step inputs of one constituent decoder run. DEC1: x = syst (+) A, y = par0, operand of
+// the output stage = A, scatter table = rev. DEC2: x = app2, y = par1, operand = app2, table =
+// fwd. WRAP selects the SSE/generic wrapping add for x (tdec_sse_gamma :321-325, gen.c:72-74)
+// instead of the windowed decoders' saturating one (win.h:390-393).
+struct StepIn {
+  s2 x, y, e;
+};
+
+template <bool DEC2, bool WRAP>
+__device__ __forceinline__ StepIn load_step(const s4 *__restrict__ sp0, const s4 *__restrict__ xp1,
+                                            const s2 *__restrict__ A, int i) {
+  StepIn r;
+  if (DEC2) {
+    s4 v = xp1[i];
+    r.x = lo2(v);
+    r.y = hi2(v);
+    r.e = r.x;
+  } else {
+    s4 v = sp0[i];
+    s2 a = A[i];
+    r.x = WRAP ? wadd(lo2(v), a) : sadd(a, lo2(v));
+    r.y = hi2(v);
+    r.e = a;
+  }
+  return r;
+}
+
+// Output stage (turbodecoder_iter.h:315-341): DEC1 ext1 -> app2 (interleave, minus app1);
+// DEC2 ext2 -> A (deinterleave, minus the a priori it was fed).
+template <bool DEC2>
+__device__ __forceinline__ void store_out(s4 *__restrict__ xp1, s2 *__restrict__ A, int t, s2 llr,
+                                          s2 e) {
+  s2 v = wsub(llr, e);
+  if (DEC2)
+    A[t] = v;
+  else
+    reinterpret_cast<s2 *>(xp1)[2 * t] = v;
+}
+
+// 8-step chunk of inputs (+ scatter indices + the segment's beta checkpoint) in registers
+struct Chunk {
+  s2 x[TD_W], y[TD_W], e[TD_W];
+  int t[TD_W];
+  Ck ck;
+};
+
+// ------------------------------------------------------------------ windowed decoder ----
+template <int NB, int DIV, bool DEC2>
+__global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+                                                    s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                    const uint16_t *__restrict__ tbl,
+                                                    s4 *__restrict__ ck,
+                                                    const uint8_t *__restrict__ pair_done, int K,
+                                                    int npairs) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int pair = g / NB;
   const int d = g % NB;
   if (pair >= npairs) return;
   if (pair_done && pair_done[pair]) return;
   const int L = K / NB;
+  const int nc = (L + TD_W - 1) / TD_W;
   const int nlanes = npairs * NB;
-  const s4 *in = xy + (size_t)pair * K;
-  s2 *o_out = out + (size_t)pair * K;
-  const s2 *tl = tail + (size_t)pair * 12;
+  const size_t base = (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s4 *xp1 = XP1 + base;
+  s2 *A = Aarr + base;
+  const s2 *tl = T + (size_t)pair * 12;
+  const int tail_xoff = DEC2 ? 6 : 0;
 
-  // ---------------- beta ----------------
+  // loads of chunk q of a walk: steps k0 .. k0+7 (clamped into the sub-block) of column col
+  auto load_xy = [&](Chunk &c, int col, int k0) {
+#pragma unroll
+    for (int j = 0; j < TD_W; j++) {
+      int k = min(k0 + j, L - 1);
+      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + col);
+      c.x[j] = s.x;
+      c.y[j] = s.y;
+    }
+  };
+
+  // ================= beta =================
   St8 o;
   {
     // turbodecoder_win.h:376-384,386-433 (loop_len = 40): estimate the state at the start of
     // sub-block d+1 from all-unknown states; move_right (:333-366) hands it to sub-block d.
-    st_fill(o, -TD_INF, -TD_INF);
     const int dn = d + 1 < NB ? d + 1 : d; // last lane: result replaced by the tail trellis
-#pragma unroll 8
-    for (int k = TD_OVERLAP - 1; k >= 0; k--) {
-      s4 v = in[k * NB + dn];
-      win_beta_step(o, s2{v.x, v.y}, s2{v.z, v.w});
-      win_norm(k, o);
+    st_fill(o, -TD_INF, -TD_INF);
+    Chunk c0, c1;
+    load_xy(c0, dn, 32);
+    for (int q = 4; q >= 0; q -= 2) {
+      if (q > 0) load_xy(c1, dn, 8 * (q - 1));
+#pragma unroll
+      for (int j = TD_W - 1; j >= 0; j--) {
+        win_beta_step(o, c0.x[j], c0.y[j]);
+        win_norm(8 * q + j, o);
+      }
+      if (q == 0) break;
+      if (q > 1) load_xy(c0, dn, 8 * (q - 2));
+#pragma unroll
+      for (int j = TD_W - 1; j >= 0; j--) {
+        win_beta_step(o, c1.x[j], c1.y[j]);
+        win_norm(8 * (q - 1) + j, o);
+      }
     }
     St8 t;
     win_tail_trellis(tl, tail_xoff, t); // :350-355 last sub-block starts from the tail
     if (d == NB - 1) o = t;
   }
-  ck_store(ck, (size_t)ck_slot<W>(L) * nlanes + g, o); // :372-374 beta[L]
-  for (int k = L - 1; k >= 0; k--) {
-    s4 v = in[k * NB + d];
-    win_beta_step(o, s2{v.x, v.y}, s2{v.z, v.w});
-    if ((k % W) == 0 && k != 0) ck_store(ck, (size_t)(k / W) * nlanes + g, o); // pre-normalise
-    win_norm(k, o);
+  ck_store(ck, (size_t)nc * nlanes + g, o); // :372-374 beta[L] (slot ceil(L/8))
+  {
+    Chunk c0, c1;
+    load_xy(c0, d, TD_W * (nc - 1));
+    for (int q = nc - 1; q >= 0; q -= 2) {
+      if (q > 0) load_xy(c1, d, TD_W * (q - 1));
+      {
+        const int n = min(TD_W, L - TD_W * q);
+#pragma unroll
+        for (int j = TD_W - 1; j >= 0; j--) {
+          if (j < n) {
+            win_beta_step(o, c0.x[j], c0.y[j]);
+            if (j == 0 && q > 0) ck_store(ck, (size_t)q * nlanes + g, o); // beta[8q] pre-norm
+            win_norm(TD_W * q + j, o);
+          }
+        }
+      }
+      if (q == 0) break;
+      if (q > 1) load_xy(c0, d, TD_W * (q - 2));
+#pragma unroll
+      for (int j = TD_W - 1; j >= 0; j--) {
+        win_beta_step(o, c1.x[j], c1.y[j]);
+        if (j == 0 && q - 1 > 0) ck_store(ck, (size_t)(q - 1) * nlanes + g, o);
+        win_norm(TD_W * (q - 1) + j, o);
+      }
+    }
   }
 
-  // ---------------- alpha + LLR ----------------
+  // ================= alpha + LLR + output stage =================
   {
     // :501-506,512-584 (loop_len = 40) over the last 40 steps of sub-block d-1; move_left
     // (:469-495) hands the estimate to sub-block d; sub-block 0 starts in state 0 (:496-500).
-    st_fill(o, -TD_INF, -TD_INF);
     const int dp = d > 0 ? d - 1 : 0;
-#pragma unroll 8
-    for (int k = 0; k < TD_OVERLAP; k++) {
-      s4 v = in[(L - TD_OVERLAP + k) * NB + dp];
-      win_alpha_step(o, s2{v.x, v.y}, s2{v.z, v.w});
-      win_norm(k, o);
+    st_fill(o, -TD_INF, -TD_INF);
+    Chunk c0, c1;
+    load_xy(c0, dp, L - TD_OVERLAP);
+    for (int q = 0; q < 5; q += 2) {
+      if (q < 4) load_xy(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
+#pragma unroll
+      for (int j = 0; j < TD_W; j++) {
+        win_alpha_step(o, c0.x[j], c0.y[j]);
+        win_norm(8 * q + j, o);
+      }
+      if (q == 4) break;
+      if (q < 3) load_xy(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
+#pragma unroll
+      for (int j = 0; j < TD_W; j++) {
+        win_alpha_step(o, c1.x[j], c1.y[j]);
+        win_norm(8 * (q + 1) + j, o);
+      }
     }
     if (d == 0) st_fill(o, 0, -TD_INF);
   }
-  for (int s0 = 0; s0 < L; s0 += W) {
-    const int s1 = s0 + W < L ? s0 + W : L;
-    const int n = s1 - s0;
-    s2 xs[W], ys[W];
+
+  auto load_seg = [&](Chunk &c, int q) {
 #pragma unroll
-    for (int j = 0; j < W; j++) {
-      if (j < n) {
-        s4 v = in[(s0 + j) * NB + d];
-        xs[j] = s2{v.x, v.y};
-        ys[j] = s2{v.z, v.w};
-      }
+    for (int j = 0; j < TD_W; j++) {
+      int k = min(TD_W * q + j, L - 1);
+      int i = k * NB + d;
+      StepIn s = load_step<DEC2, false>(sp0, xp1, A, i);
+      c.x[j] = s.x;
+      c.y[j] = s.y;
+      c.e[j] = s.e;
+      c.t[j] = tbl[i];
     }
-    // betas stored at indices s0+1 .. s1 (bst[j] = stored beta[s0+1+j])
-    St8 bst[W];
+    ck_load(ck, (size_t)(q + 1) * nlanes + g, c.ck); // beta stored at min(8q+8, L)
+  };
+
+  auto seg = [&](Chunk &c, int q) {
+    const int s0 = TD_W * q;
+    const int n = min(TD_W, L - s0);
+    const int s1 = s0 + n;
+    St8 bst[TD_W]; // bst[j] = stored beta[s0+1+j]
     St8 run;
-    ck_load(ck, (size_t)ck_slot<W>(s1) * nlanes + g, run);
+    ck_unpack(c.ck, run);
 #pragma unroll
-    for (int j = W - 1; j >= 0; j--) {
+    for (int j = TD_W - 1; j >= 0; j--) {
       if (j == n - 1) bst[j] = run;
     }
-    if (s1 != L) win_norm(s1, run); // running state continues from the normalised value
+    if (s1 != L) win_norm(s1, run); // the running state continues from the normalised value
 #pragma unroll
-    for (int j = W - 2; j >= 0; j--) {
+    for (int j = TD_W - 2; j >= 0; j--) {
       if (j <= n - 2) {
-        win_beta_step(run, xs[j + 1], ys[j + 1]);
+        win_beta_step(run, c.x[j + 1], c.y[j + 1]);
         bst[j] = run;
         win_norm(s0 + 1 + j, run);
       }
     }
 #pragma unroll
-    for (int j = 0; j < W; j++) {
+    for (int j = 0; j < TD_W; j++) {
       if (j < n) {
         s2 mb[8], nw[8];
-        win_alpha_branches(o, xs[j], ys[j], mb, nw);
+        win_alpha_branches(o, c.x[j], c.y[j], mb, nw);
         s2 m0 = sadd(bst[j].s[0], mb[0]);
         s2 m1 = sadd(bst[j].s[0], nw[0]);
 #pragma unroll
@@ -261,32 +382,47 @@ __global__ __launch_bounds__(256) void k_win_dec(const s4 *__restrict__ xy,
         }
         s2 v = ssub(m1, m0);
         if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
-        o_out[(s0 + j) * NB + d] = v;
+        store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
 #pragma unroll
         for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
         win_norm(s0 + j, o);
       }
     }
+  };
+
+  {
+    Chunk c0, c1;
+    load_seg(c0, 0);
+    for (int q = 0; q < nc; q += 2) {
+      if (q + 1 < nc) load_seg(c1, q + 1);
+      seg(c0, q);
+      if (q + 1 >= nc) break;
+      if (q + 2 < nc) load_seg(c0, q + 2);
+      seg(c1, q + 1);
+    }
   }
 }
 
 // ------------------------------------------------------------------ SSE non-window ----
-// turbodecoder_sse.c:97-407, one lane per CB pair, natural index. x/app/par come through
-// the xy stream (x already contains app, wrapping, as tdec_sse_gamma :321-325 does) — the
-// caller builds it with wrapping adds for this decoder. Tail gammas use C division.
-// scratch: alpha (K+1)*8 short2 per pair.
-__global__ __launch_bounds__(64) void k_sse_dec(const s4 *__restrict__ xy,
-                                                const s2 *__restrict__ tail, int tail_xoff,
-                                                s2 *__restrict__ out, s2 *__restrict__ scratch,
-                                                const uint8_t *__restrict__ pair_done, int K,
-                                                int npairs) {
+// turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
+// x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
+// scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
+template <bool DEC2>
+__global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   const uint16_t *__restrict__ tbl,
+                                                   s2 *__restrict__ scratch,
+                                                   const uint8_t *__restrict__ pair_done, int K,
+                                                   int npairs) {
   const int pair = blockIdx.x * blockDim.x + threadIdx.x;
   if (pair >= npairs) return;
   if (pair_done && pair_done[pair]) return;
-  const s4 *in = xy + (size_t)pair * K;
-  s2 *o_out = out + (size_t)pair * K;
-  const s2 *tl = tail + (size_t)pair * 12;
-  // alpha in scratch, lane-interleaved so that consecutive pairs are contiguous
+  const size_t base = (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s4 *xp1 = XP1 + base;
+  s2 *A = Aarr + base;
+  const s2 *tl = T + (size_t)pair * 12;
+  const int tail_xoff = DEC2 ? 6 : 0;
   auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   s2 a[8];
   a[0] = splat(0);
@@ -295,9 +431,8 @@ __global__ __launch_bounds__(64) void k_sse_dec(const s4 *__restrict__ xy,
 #pragma unroll
   for (int i = 0; i < 8; i++) AL(0, i) = a[i];
   for (int k = 0; k < K; k++) { // :211-297
-    s4 v = in[k];
-    s2 x = s2{v.x, v.y}, y = s2{v.z, v.w};
-    s2 g1 = wadd(x, y) >> 1, g0 = wsub(x, y) >> 1;
+    StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+    s2 g1 = wadd(s.x, s.y) >> 1, g0 = wsub(s.x, s.y) >> 1;
     s2 n[8];
     n[0] = smax(wadd(a[1], g1), wsub(a[0], g1));
     n[1] = smax(wadd(a[2], g0), wsub(a[3], g0));
@@ -323,16 +458,16 @@ __global__ __launch_bounds__(64) void k_sse_dec(const s4 *__restrict__ xy,
 #pragma unroll
   for (int i = 1; i < 8; i++) b[i] = splat(-TD_INF);
   for (int k = K + 2; k >= 0; k--) { // :105-206
-    s2 g0, g1;
-    if (k >= K) { // :349-352 C division truncates toward zero
+    s2 g0, g1, e = splat(0);
+    if (k >= K) {
       s2 x = tl[tail_xoff + 2 * (k - K)], y = tl[tail_xoff + 2 * (k - K) + 1];
       g0 = s2{(short)(((int)x.x - y.x) / 2), (short)(((int)x.y - y.y) / 2)};
       g1 = s2{(short)(((int)x.x + y.x) / 2), (short)(((int)x.y + y.y) / 2)};
     } else {
-      s4 v = in[k];
-      s2 x = s2{v.x, v.y}, y = s2{v.z, v.w};
-      g1 = wadd(x, y) >> 1;
-      g0 = wsub(x, y) >> 1;
+      StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+      g1 = wadd(s.x, s.y) >> 1;
+      g0 = wsub(s.x, s.y) >> 1;
+      e = s.e;
     }
     s2 bp[8] = {wadd(b[4], g1), wadd(b[0], g1), wadd(b[1], g0), wadd(b[5], g0),
                 wadd(b[6], g0), wadd(b[2], g0), wadd(b[3], g1), wadd(b[7], g1)};
@@ -348,8 +483,9 @@ __global__ __launch_bounds__(64) void k_sse_dec(const s4 *__restrict__ xy,
         mp = smax(mp, wadd(bp[i], al));
         mn = smax(mn, wadd(bn[i], al));
       }
-      // hMax(bn) - hMax(bp) with hMax(v) = 0x7FFF - max(v) (minpos_epu16 trick)
-      o_out[k] = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
+      // hMax(bn) - hMax(bp) with hMax(v) = 0x7FFF - max(v) (minpos_epu16 trick, :97-102)
+      s2 llr = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
+      store_out<DEC2>(xp1, A, tbl[k], llr, e);
       if ((k & 3) == 0) {
         s2 z = b[0];
 #pragma unroll
@@ -360,21 +496,25 @@ __global__ __launch_bounds__(64) void k_sse_dec(const s4 *__restrict__ xy,
 }
 
 // ------------------------------------------------------------------ generic ----
-// turbodecoder_gen.c:59-236, one lane per CB pair, natural index, wrapping int16.
-// The xy stream carries x = syst (+) app with a wrapping add (gen.c:72-74,120-122 add app only
-// for k < K, which is exactly the stream's range); tail x/y come from the tail array.
+// turbodecoder_gen.c:59-236, one lane per CB pair, natural index, wrapping int16; app is added
+// for k < K only (:72-74), which is exactly the range the input policy covers.
 // scratch: beta (K+4)*8 short2 per pair.
-__global__ __launch_bounds__(64) void k_gen_dec(const s4 *__restrict__ xy,
-                                                const s2 *__restrict__ tail, int tail_xoff,
-                                                s2 *__restrict__ out, s2 *__restrict__ scratch,
-                                                const uint8_t *__restrict__ pair_done, int K,
-                                                int npairs) {
+template <bool DEC2>
+__global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   const uint16_t *__restrict__ tbl,
+                                                   s2 *__restrict__ scratch,
+                                                   const uint8_t *__restrict__ pair_done, int K,
+                                                   int npairs) {
   const int pair = blockIdx.x * blockDim.x + threadIdx.x;
   if (pair >= npairs) return;
   if (pair_done && pair_done[pair]) return;
-  const s4 *in = xy + (size_t)pair * K;
-  s2 *o_out = out + (size_t)pair * K;
-  const s2 *tl = tail + (size_t)pair * 12;
+  const size_t base = (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s4 *xp1 = XP1 + base;
+  s2 *A = Aarr + base;
+  const s2 *tl = T + (size_t)pair * 12;
+  const int tail_xoff = DEC2 ? 6 : 0;
   auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   const int end = K + 3;
   s2 o[8];
@@ -387,9 +527,9 @@ __global__ __launch_bounds__(64) void k_gen_dec(const s4 *__restrict__ xy,
       x = tl[tail_xoff + 2 * (k - K)];
       y = tl[tail_xoff + 2 * (k - K) + 1];
     } else {
-      s4 v = in[k];
-      x = s2{v.x, v.y};
-      y = s2{v.z, v.w};
+      StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+      x = s.x;
+      y = s.y;
     }
     s2 xy_ = wadd(x, y);
     s2 mb[8] = {wadd(o[4], xy_), o[4], wadd(o[5], y), wadd(o[5], x),
@@ -412,8 +552,8 @@ __global__ __launch_bounds__(64) void k_gen_dec(const s4 *__restrict__ xy,
 #pragma unroll
   for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
   for (int k = 1; k < K + 1; k++) {
-    s4 v = in[k - 1];
-    s2 x = s2{v.x, v.y}, y = s2{v.z, v.w}, xy_ = wadd(x, y);
+    StepIn s = load_step<DEC2, true>(sp0, xp1, A, k - 1);
+    s2 x = s.x, y = s.y, xy_ = wadd(x, y);
     s2 mb[8] = {a[0], wadd(a[3], y), wadd(a[4], y), a[7],
                 a[1], wadd(a[2], y), wadd(a[5], y), a[6]};
     s2 nw[8] = {wadd(a[1], xy_), wadd(a[2], x), wadd(a[5], x), wadd(a[6], xy_),
@@ -432,170 +572,144 @@ __global__ __launch_bounds__(64) void k_gen_dec(const s4 *__restrict__ xy,
 #pragma unroll
       for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
     }
-    o_out[k - 1] = wsub(m1, m0);
+    store_out<DEC2>(xp1, A, tbl[k - 1], wsub(m1, m0), s.e);
   }
 }
 
-// ------------------------------------------------------------------ glue kernels ----
-
-// Input load: user layout -> pair-interleaved syst/par0/par1 (SB index when NB > 1) + tails.
-// Natural input: [s,p0,p1]*K + 12 tail (turbodecoder_gen.c:240-259, win.h:634-674);
-// SB input: streams at s*(K+32), tails at 3*(K+32) (turbodecoder_iter.h:271-280).
-__global__ void k_load(const int16_t *__restrict__ in, size_t in_stride, int sb_input, int K,
-                       int NB, int ncb, s2 *__restrict__ S, s2 *__restrict__ P0,
-                       s2 *__restrict__ P1, s2 *__restrict__ T) {
+// ------------------------------------------------------------------ load ----
+// User layout -> SP0 / XP1.par1 / T, A = 0. Natural input ([s,p0,p1]*K + 12 tail;
+// turbodecoder_gen.c:240-259, win.h:634-674) is transposed through LDS: a workgroup takes 64
+// consecutive steps k of all NB sub-blocks of one pair, reads NB runs of 64 natural positions
+// (coalesced), and writes the 64*NB SB-ordered elements contiguously. SB input (rm_turbo's
+// layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280) is a straight copy.
+#define LOAD_KT 64
+__global__ __launch_bounds__(256) void k_load(const int16_t *__restrict__ in, size_t in_stride,
+                                              int sb_input, int K, int NB, int ncb,
+                                              s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+                                              s2 *__restrict__ Aarr, s2 *__restrict__ T) {
+  __shared__ short lds[2][3][LOAD_KT * 16 + 1];
   const int npairs = (ncb + 1) / 2;
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int per = K + 12;
-  if (tid >= (size_t)npairs * per) return;
-  const int pair = (int)(tid / per);
-  const int j = (int)(tid % per);
-  const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
-  const int16_t *a = in + (size_t)c0 * in_stride, *b = in + (size_t)c1 * in_stride;
-  if (j < K) {
-    // j is the destination index (SB index when NB > 1)
-    int s, p0, p1;
-    if (sb_input) {
-      s = j;
-      p0 = (K + 32) + j;
-      p1 = 2 * (K + 32) + j;
-    } else {
-      int p = j;
-      if (NB > 1) {
-        const int L = K / NB;
-        p = (j % NB) * L + j / NB; // SB index -> natural position
-      }
-      s = 3 * p;
-      p0 = 3 * p + 1;
-      p1 = 3 * p + 2;
-    }
-    S[(size_t)pair * K + j] = s2{a[s], b[s]};
-    P0[(size_t)pair * K + j] = s2{a[p0], b[p0]};
-    P1[(size_t)pair * K + j] = s2{a[p1], b[p1]};
-  } else {
-    const int t = j - K;
-    const int base = sb_input ? 3 * (K + 32) : 3 * K;
-    T[(size_t)pair * 12 + t] = s2{a[base + t], b[base + t]};
-  }
-}
-
-// Even half-iteration prologue (turbodecoder_iter.h:315-324): app1 = deinterleave(ext2)
-// - ext1 (wrapping) for n > 0, decoder input x = syst (+) app1.
-// mode: 0 = saturating add (windowed), 1 = wrapping add (SSE/generic).
-__global__ void k_prep_even(int n, int K, int npairs, const uint16_t *__restrict__ rev,
-                            const s2 *__restrict__ S, const s2 *__restrict__ P0,
-                            const s2 *__restrict__ X2, const s2 *__restrict__ E,
-                            s2 *__restrict__ A, s4 *__restrict__ XY, int wrap_mode,
-                            const uint8_t *__restrict__ pair_done) {
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (size_t)npairs * K) return;
-  const int pair = (int)(tid / K);
-  if (pair_done && pair_done[pair]) return;
-  const int j = (int)(tid % K);
-  const size_t base = (size_t)pair * K;
-  s2 x = S[base + j];
-  if (n > 0) {
-    s2 app = wsub(X2[base + rev[j]], E[base + j]);
-    A[base + j] = app;
-    x = wrap_mode ? wadd(x, app) : sadd(app, x);
-  }
-  s2 y = P0[base + j];
-  XY[base + j] = s4{x.x, x.y, y.x, y.y};
-}
-
-// Odd half-iteration prologue (turbodecoder_iter.h:327-333): ext1 -= app1 for n > 1, then
-// app2 = interleave(ext1): app2[m] = ext1[fwd[m]]. E is double-buffered (Ein -> Eout).
-__global__ void k_prep_odd(int n, int K, int npairs, const uint16_t *__restrict__ fwd,
-                           const s2 *__restrict__ P1, const s2 *__restrict__ Ein,
-                           const s2 *__restrict__ A, s2 *__restrict__ Eout,
-                           s4 *__restrict__ XY, const uint8_t *__restrict__ pair_done) {
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= (size_t)npairs * K) return;
-  const int pair = (int)(tid / K);
-  if (pair_done && pair_done[pair]) return;
-  const int m = (int)(tid % K);
-  const size_t base = (size_t)pair * K;
-  const int f = fwd[m];
-  s2 x;
-  if (n > 1) {
-    Eout[base + m] = wsub(Ein[base + m], A[base + m]);
-    x = wsub(Ein[base + f], A[base + f]);
-  } else {
-    x = Ein[base + f];
-  }
-  s2 y = P1[base + m];
-  XY[base + m] = s4{x.x, x.y, y.x, y.y};
-}
-
-// Hard decision after half-iteration n (turbodecoder.c:353-360 + decision_byte): bits from
-// ext1 after DEC1 (n even) or from app1 = deinterleave(ext2) after DEC2 (n odd), natural order,
-// MSB first. One thread per output byte. Skips CBs already finished (early stop).
-__global__ void k_decide(int n, int K, int NB, int ncb, const uint16_t *__restrict__ rev,
-                         const s2 *__restrict__ E, const s2 *__restrict__ X2,
-                         uint8_t *__restrict__ outb, size_t out_stride,
-                         const uint8_t *__restrict__ cb_done) {
-  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int nbytes = K / 8;
-  if (tid >= (size_t)ncb * nbytes) return;
-  const int cb = (int)(tid / nbytes);
-  if (cb_done && cb_done[cb]) return;
-  const int byte = (int)(tid % nbytes);
-  const int pair = cb >> 1, half = cb & 1;
-  const size_t base = (size_t)pair * K;
   const int L = K / NB;
-  uint8_t r = 0;
-#pragma unroll
-  for (int b = 0; b < 8; b++) {
-    const int p = 8 * byte + b;
-    const int j = NB > 1 ? (p % L) * NB + p / L : p;
-    s2 v = (n & 1) ? X2[base + rev[j]] : E[base + j];
-    short s = half ? v.y : v.x;
-    if (s > 0) r |= (uint8_t)(0x80 >> b);
+  const int ktiles = (L + LOAD_KT - 1) / LOAD_KT;
+  const int pair = blockIdx.x / ktiles;
+  const int kt = blockIdx.x % ktiles;
+  if (pair >= npairs) return;
+  const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
+  const int16_t *src[2] = {in + (size_t)c0 * in_stride, in + (size_t)c1 * in_stride};
+  const size_t base = (size_t)pair * K;
+  const int k0 = kt * LOAD_KT;
+  const int kn = min(LOAD_KT, L - k0);
+  if (sb_input) {
+    for (int e = threadIdx.x; e < kn * NB; e += blockDim.x) {
+      const int i = k0 * NB + e;
+      s2 s = s2{src[0][i], src[1][i]};
+      s2 p0 = s2{src[0][K + 32 + i], src[1][K + 32 + i]};
+      s2 p1 = s2{src[0][2 * (K + 32) + i], src[1][2 * (K + 32) + i]};
+      SP0[base + i] = s4{s.x, s.y, p0.x, p0.y};
+      XP1[base + i] = s4{0, 0, p1.x, p1.y};
+      Aarr[base + i] = splat(0);
+    }
+  } else {
+    // read: for each sub-block d, natural positions d*L + k0 .. + kn-1, 3 values each
+    for (int h = 0; h < 2; h++) {
+      for (int e = threadIdx.x; e < NB * kn * 3; e += blockDim.x) {
+        const int dd = e / (kn * 3), r = e % (kn * 3);
+        const int kk = r / 3, s = r % 3;
+        lds[h][s][kk * 16 + dd] = src[h][3 * (dd * L + k0) + r];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kn * NB; e += blockDim.x) {
+      const int kk = e / NB, dd = e % NB;
+      const int i = (k0 + kk) * NB + dd;
+      const int li = kk * 16 + dd;
+      SP0[base + i] = s4{lds[0][0][li], lds[1][0][li], lds[0][1][li], lds[1][1][li]};
+      XP1[base + i] = s4{0, 0, lds[0][2][li], lds[1][2][li]};
+      Aarr[base + i] = splat(0);
+    }
   }
-  outb[(size_t)cb * out_stride + byte] = r;
+  if (kt == 0 && threadIdx.x < 12) {
+    const int t = threadIdx.x;
+    const int tb = sb_input ? 3 * (K + 32) : 3 * K;
+    T[(size_t)pair * 12 + t] = s2{src[0][tb + t], src[1][tb + t]};
+  }
 }
 
-// CRC check + early-stop bookkeeping (sch.c:361-391): one wave per CB; the byte-serial table
-// CRC (crc.c:144-155) is split over 64 lanes as 64 partial CRCs combined by shifting through
-// the zero-extension operator, done here by a simple sequential fold on lane 0 of the partial
-// remainders (each partial is a table CRC of its 1/64 slice followed by zero bytes).
-__global__ void k_crc_check(int n, int ncb, int nbytes_total, uint32_t poly,
-                            const uint8_t *__restrict__ outb, size_t out_stride,
-                            uint8_t *__restrict__ cb_done, uint8_t *__restrict__ cb_ok,
-                            uint32_t *__restrict__ noi, int max_halfits) {
+// ------------------------------------------------------------------ decide (+ CRC) ----
+// Hard decision after half-iteration n (turbodecoder.c:353-360 + decision_byte): bit(p) =
+// A[j] + app2[rev[j]] > 0 at the SB index j of natural position p, MSB first. One workgroup
+// per CB pair: bits gathered into an LDS bitmap, then written as bytes. With early stop the
+// same workgroup checks the CRC (crc.c:144-155, sch.c:361-391) and updates the done flags.
+__global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
+                                                const uint16_t *__restrict__ rev,
+                                                const s2 *__restrict__ Aarr,
+                                                const s4 *__restrict__ XP1, uint8_t *__restrict__ outb,
+                                                size_t out_stride, uint8_t *__restrict__ cb_done,
+                                                uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
+                                                int crc_bytes, uint32_t poly, int max_halfits) {
+  __shared__ uint32_t bits[2][6144 / 32];
   __shared__ uint32_t table[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    uint32_t crc = (uint32_t)i << 16;
-    for (int j = 0; j < 8; j++) {
-      uint32_t bit = crc & 0x800000u;
-      crc <<= 1;
-      if (bit) crc ^= poly;
+  const int pair = blockIdx.x;
+  const int npairs = (ncb + 1) / 2;
+  if (pair >= npairs) return;
+  const int cbs[2] = {2 * pair, 2 * pair + 1 < ncb ? 2 * pair + 1 : -1};
+  const bool skip0 = cb_done && cb_done[cbs[0]];
+  const bool skip1 = cbs[1] < 0 || (cb_done && cb_done[cbs[1]]);
+  if (skip0 && skip1) return;
+  const int nw = (K + 31) / 32;
+  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+    bits[0][w] = 0;
+    bits[1][w] = 0;
+  }
+  if (crc_bytes) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+      uint32_t crc = (uint32_t)i << 16;
+      for (int j = 0; j < 8; j++) {
+        uint32_t bit = crc & 0x800000u;
+        crc <<= 1;
+        if (bit) crc ^= poly;
+      }
+      table[i] = crc & 0xFFFFFFu;
     }
-    table[i] = crc & 0xFFFFFFu;
   }
   __syncthreads();
-  const int cb = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-  const int lane = threadIdx.x & 63;
-  if (cb >= ncb) return;
-  if (cb_done[cb]) return;
-  // lane 0 walks the bytes (K/8 <= 768 table steps); other lanes idle. Simple and exact.
-  if (lane == 0) {
-    const uint8_t *p = outb + (size_t)cb * out_stride;
-    uint32_t crc = 0;
-    for (int i = 0; i < nbytes_total; i++) {
-      crc = ((crc << 8) ^ table[((crc >> 16) & 0xff) ^ p[i]]) & 0xFFFFFFu;
-    }
-    noi[cb] = (uint32_t)(n + 1);
-    if (crc == 0) {
-      cb_ok[cb] = 1;
-      cb_done[cb] = 1;
-    } else if (n + 1 >= max_halfits) {
-      cb_done[cb] = 1;
+  const size_t base = (size_t)pair * K;
+  const int L = K / NB;
+  const s2 *x2 = reinterpret_cast<const s2 *>(XP1 + base);
+  for (int j = threadIdx.x; j < K; j += blockDim.x) {
+    s2 v = wadd(Aarr[base + j], x2[2 * rev[j]]);
+    const int p = NB > 1 ? (j % NB) * L + j / NB : j;
+    const uint32_t m = 1u << (8 * ((p >> 3) & 3) + 7 - (p & 7)); // byte p/8, bit 7-p%8
+    if (v.x > 0) atomicOr(&bits[0][p >> 5], m);
+    if (v.y > 0) atomicOr(&bits[1][p >> 5], m);
+  }
+  __syncthreads();
+  for (int h = 0; h < 2; h++) {
+    if (h ? skip1 : skip0) continue;
+    uint8_t *o = outb + (size_t)cbs[h] * out_stride;
+    const uint8_t *by = reinterpret_cast<const uint8_t *>(bits[h]);
+    for (int b = threadIdx.x; b < K / 8; b += blockDim.x) o[b] = by[b];
+  }
+  if (crc_bytes && threadIdx.x < 2) {
+    const int h = threadIdx.x;
+    if (!(h ? skip1 : skip0)) {
+      const uint8_t *by = reinterpret_cast<const uint8_t *>(bits[h]);
+      uint32_t crc = 0;
+      for (int i = 0; i < crc_bytes; i++)
+        crc = ((crc << 8) ^ table[((crc >> 16) & 0xff) ^ by[i]]) & 0xFFFFFFu;
+      const int cb = cbs[h];
+      noi[cb] = (uint32_t)(n + 1);
+      if (crc == 0) {
+        cb_ok[cb] = 1;
+        cb_done[cb] = 1;
+      } else if (n + 1 >= max_halfits) {
+        cb_done[cb] = 1;
+      }
     }
   }
 }
 
-// pair_done = cb_done[2p] && cb_done[2p+1]
+// pair_done = both code blocks finished
 __global__ void k_pair_done(int ncb, const uint8_t *__restrict__ cb_done,
                             uint8_t *__restrict__ pair_done) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -610,89 +724,74 @@ __global__ void k_pair_done(int ncb, const uint8_t *__restrict__ cb_done,
 static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
-                       void *S, void *P0, void *P1, void *T, hipStream_t st) {
+                       void *SP0, void *XP1, void *A, void *T, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
-  size_t n = (size_t)npairs * (K + 12);
-  hipLaunchKernelGGL(k_load, dim3(nblk(n, 256)), dim3(256), 0, st, in, in_stride, sb_input, K, NB,
-                     ncb, (s2 *)S, (s2 *)P0, (s2 *)P1, (s2 *)T);
-  return hipGetLastError();
-}
-
-hipError_t launch_prep_even(int n, int K, int npairs, const uint16_t *rev, const void *S,
-                            const void *P0, const void *X2, const void *E, void *A, void *XY,
-                            int wrap_mode, const uint8_t *pair_done, hipStream_t st) {
-  size_t tot = (size_t)npairs * K;
-  hipLaunchKernelGGL(k_prep_even, dim3(nblk(tot, 256)), dim3(256), 0, st, n, K, npairs, rev,
-                     (const s2 *)S, (const s2 *)P0, (const s2 *)X2, (const s2 *)E, (s2 *)A,
-                     (s4 *)XY, wrap_mode, pair_done);
-  return hipGetLastError();
-}
-
-hipError_t launch_prep_odd(int n, int K, int npairs, const uint16_t *fwd, const void *P1,
-                           const void *Ein, const void *A, void *Eout, void *XY,
-                           const uint8_t *pair_done, hipStream_t st) {
-  size_t tot = (size_t)npairs * K;
-  hipLaunchKernelGGL(k_prep_odd, dim3(nblk(tot, 256)), dim3(256), 0, st, n, K, npairs, fwd,
-                     (const s2 *)P1, (const s2 *)Ein, (const s2 *)A, (s2 *)Eout, (s4 *)XY,
-                     pair_done);
+  const int L = K / NB;
+  const int ktiles = (L + LOAD_KT - 1) / LOAD_KT;
+  hipLaunchKernelGGL(k_load, dim3((unsigned)(npairs * ktiles)), dim3(256), 0, st, in, in_stride,
+                     sb_input, K, NB, ncb, (s4 *)SP0, (s4 *)XP1, (s2 *)A, (s2 *)T);
   return hipGetLastError();
 }
 
 size_t win_ck_bytes(int K, int NB, int npairs) {
   const int L = K / NB;
-  const int W = TD_CK_W;
-  size_t slots = (size_t)(L + W - 1) / W + 1;
+  size_t slots = (size_t)(L + TD_W - 1) / TD_W + 1;
   return slots * (size_t)npairs * NB * 8 * sizeof(s2);
-}
-
-hipError_t launch_win_dec(int NB, const void *XY, const void *T, int tail_xoff, void *out,
-                          void *ck, const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
-  size_t lanes = (size_t)npairs * NB;
-  dim3 grid(nblk(lanes, 256)), blk(256);
-  if (NB == 16) {
-    hipLaunchKernelGGL((k_win_dec<16, 0, TD_CK_W>), grid, blk, 0, st, (const s4 *)XY,
-                       (const s2 *)T, tail_xoff, (s2 *)out, (s4 *)ck, pair_done, K, npairs);
-  } else if (NB == 8) {
-    hipLaunchKernelGGL((k_win_dec<8, 1, TD_CK_W>), grid, blk, 0, st, (const s4 *)XY,
-                       (const s2 *)T, tail_xoff, (s2 *)out, (s4 *)ck, pair_done, K, npairs);
-  } else {
-    return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 size_t seq_scratch_bytes(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs * sizeof(s2); }
 
-hipError_t launch_sse_dec(const void *XY, const void *T, int tail_xoff, void *out, void *scratch,
-                          const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
-  hipLaunchKernelGGL(k_sse_dec, dim3(nblk(npairs, 64)), dim3(64), 0, st, (const s4 *)XY,
-                     (const s2 *)T, tail_xoff, (s2 *)out, (s2 *)scratch, pair_done, K, npairs);
+hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, const void *T,
+                         const uint16_t *fwd, const uint16_t *rev, void *scratch,
+                         const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
+  const bool dec2 = n & 1;
+  const uint16_t *tbl = dec2 ? fwd : rev;
+  const s4 *sp0 = (const s4 *)SP0;
+  s4 *xp1 = (s4 *)XP1;
+  s2 *a = (s2 *)A;
+  const s2 *t = (const s2 *)T;
+  if (NB > 1) {
+    dim3 grid(nblk((size_t)npairs * NB, 256)), blk(256);
+    s4 *ck = (s4 *)scratch;
+#define WIN(nb, div, d2)                                                                           \
+  hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, t, tbl, ck,        \
+                     pair_done, K, npairs)
+    if (NB == 16) {
+      if (dec2) WIN(16, 0, true); else WIN(16, 0, false);
+    } else if (NB == 8) {
+      if (dec2) WIN(8, 1, true); else WIN(8, 1, false);
+    } else {
+      return hipErrorInvalidValue;
+    }
+#undef WIN
+  } else {
+    dim3 grid(nblk(npairs, 64)), blk(64);
+    s2 *sc = (s2 *)scratch;
+    if (impl_seq == 0) { // SSE non-window
+      if (dec2)
+        hipLaunchKernelGGL(k_sse_halfit<true>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+      else
+        hipLaunchKernelGGL(k_sse_halfit<false>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+    } else {
+      if (dec2)
+        hipLaunchKernelGGL(k_gen_halfit<true>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+      else
+        hipLaunchKernelGGL(k_gen_halfit<false>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+    }
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_gen_dec(const void *XY, const void *T, int tail_xoff, void *out, void *scratch,
-                          const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
-  hipLaunchKernelGGL(k_gen_dec, dim3(nblk(npairs, 64)), dim3(64), 0, st, (const s4 *)XY,
-                     (const s2 *)T, tail_xoff, (s2 *)out, (s2 *)scratch, pair_done, K, npairs);
-  return hipGetLastError();
-}
-
-hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *E,
-                         const void *X2, uint8_t *outb, size_t out_stride, const uint8_t *cb_done,
-                         hipStream_t st) {
-  size_t tot = (size_t)ncb * (K / 8);
-  hipLaunchKernelGGL(k_decide, dim3(nblk(tot, 256)), dim3(256), 0, st, n, K, NB, ncb, rev,
-                     (const s2 *)E, (const s2 *)X2, outb, out_stride, cb_done);
-  return hipGetLastError();
-}
-
-hipError_t launch_crc_check(int n, int ncb, int nbytes, uint32_t poly, const uint8_t *outb,
-                            size_t out_stride, uint8_t *cb_done, uint8_t *cb_ok, uint32_t *noi,
-                            int max_halfits, uint8_t *pair_done, hipStream_t st) {
-  hipLaunchKernelGGL(k_crc_check, dim3(nblk(ncb, 4)), dim3(256), 0, st, n, ncb, nbytes, poly,
-                     outb, out_stride, cb_done, cb_ok, noi, max_halfits);
-  hipLaunchKernelGGL(k_pair_done, dim3(nblk((ncb + 1) / 2, 256)), dim3(256), 0, st, ncb, cb_done,
-                     pair_done);
+hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *A,
+                         const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
+                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, uint32_t poly,
+                         int max_halfits, uint8_t *pair_done, hipStream_t st) {
+  const int npairs = (ncb + 1) / 2;
+  hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, rev, (const s2 *)A,
+                     (const s4 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, poly,
+                     max_halfits);
+  if (crc_bytes && pair_done)
+    hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
   return hipGetLastError();
 }
 

@@ -24,6 +24,15 @@ SRSLTE_TDEC_SSE8_WINDOW, SRSLTE_TDEC_AVX8_WINDOW = 5, 6
 SRSLTE_SUCCESS, SRSLTE_ERROR = 0, -1
 CRC24A, CRC24B = 0x1864CFB, 0x1800063
 
+try:
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64/libhsa-runtime64
+    # with the same SONAME as /opt/rocm's. Loading torch first makes the library bind to that
+    # runtime; loading the library first would put two HSA runtimes in the process and torch
+    # then sees no GPU.
+    import torch  # noqa: F401
+except ImportError:  # C-only users: the library uses the system ROCm runtime
+    torch = None
+
 if not os.path.exists(LIB_PATH):
     raise ImportError("srsgpu: %s not found — build it with `make -C empower-srslte_amd` "
                       "(no CPU fallback exists)" % LIB_PATH)
