@@ -241,15 +241,24 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = DEC2 ? 6 : 0;
 
-  // loads of chunk q of a walk: steps k0 .. k0+7 (clamped into the sub-block) of column col
+  // loads of one 8-step chunk of column col: steps k0 .. k0+7, clamped into the sub-block
   auto load_xy = [&](Chunk &c, int col, int k0) {
 #pragma unroll
     for (int j = 0; j < TD_W; j++) {
-      int k = min(k0 + j, L - 1);
+      int k = min(max(k0 + j, 0), L - 1);
       StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + col);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
+  };
+  // state-0 normalisation operand at step k = 8q + j (win.h:244-261: k even and k != 0);
+  // subtracting 0 (saturating) is the identity, which keeps the steady-state loops branch-free
+  auto norm_op = [&](const St8 &o, int q, int j) -> s2 {
+    return (j == 0 && q == 0) ? splat(0) : o.s[0];
+  };
+  auto norm_by = [&](St8 &o, s2 z) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], z);
   };
 
   // ================= beta =================
@@ -261,6 +270,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     st_fill(o, -TD_INF, -TD_INF);
     Chunk c0, c1;
     load_xy(c0, dn, 32);
+#pragma unroll
     for (int q = 4; q >= 0; q -= 2) {
       if (q > 0) load_xy(c1, dn, 8 * (q - 1));
 #pragma unroll
@@ -268,12 +278,13 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
         win_beta_step(o, c0.x[j], c0.y[j]);
         win_norm(8 * q + j, o);
       }
-      if (q == 0) break;
-      if (q > 1) load_xy(c0, dn, 8 * (q - 2));
+      if (q > 0) {
+        if (q > 1) load_xy(c0, dn, 8 * (q - 2));
 #pragma unroll
-      for (int j = TD_W - 1; j >= 0; j--) {
-        win_beta_step(o, c1.x[j], c1.y[j]);
-        win_norm(8 * (q - 1) + j, o);
+        for (int j = TD_W - 1; j >= 0; j--) {
+          win_beta_step(o, c1.x[j], c1.y[j]);
+          win_norm(8 * (q - 1) + j, o);
+        }
       }
     }
     St8 t;
@@ -282,30 +293,38 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   }
   ck_store(ck, (size_t)nc * nlanes + g, o); // :372-374 beta[L] (slot ceil(L/8))
   {
-    Chunk c0, c1;
-    load_xy(c0, d, TD_W * (nc - 1));
-    for (int q = nc - 1; q >= 0; q -= 2) {
-      if (q > 0) load_xy(c1, d, TD_W * (q - 1));
-      {
-        const int n = min(TD_W, L - TD_W * q);
-#pragma unroll
-        for (int j = TD_W - 1; j >= 0; j--) {
-          if (j < n) {
-            win_beta_step(o, c0.x[j], c0.y[j]);
-            if (j == 0 && q > 0) ck_store(ck, (size_t)q * nlanes + g, o); // beta[8q] pre-norm
-            win_norm(TD_W * q + j, o);
-          }
-        }
-      }
-      if (q == 0) break;
-      if (q > 1) load_xy(c0, d, TD_W * (q - 2));
+    // full chunk q (steps 8q+7 .. 8q): checkpoint beta[8q] before its normalisation (:420-424)
+    auto beta_full = [&](Chunk &c, int q) {
 #pragma unroll
       for (int j = TD_W - 1; j >= 0; j--) {
-        win_beta_step(o, c1.x[j], c1.y[j]);
-        if (j == 0 && q - 1 > 0) ck_store(ck, (size_t)(q - 1) * nlanes + g, o);
-        win_norm(TD_W * (q - 1) + j, o);
+        win_beta_step(o, c.x[j], c.y[j]);
+        if (j == 0) ck_store(ck, (size_t)q * nlanes + g, o); // slot 0 is never read
+        if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+      }
+    };
+    Chunk c0, c1;
+    const int qt = nc - 1; // top chunk, possibly partial (L % 8 != 0); nc >= 7 since L > 40
+    load_xy(c0, d, TD_W * qt);
+    load_xy(c1, d, TD_W * (qt - 1));
+    {
+      const int n = L - TD_W * qt;
+#pragma unroll
+      for (int j = TD_W - 1; j >= 0; j--) {
+        if (j < n) {
+          win_beta_step(o, c0.x[j], c0.y[j]);
+          if (j == 0) ck_store(ck, (size_t)qt * nlanes + g, o);
+          win_norm(TD_W * qt + j, o);
+        }
       }
     }
+    int q = qt - 1; // chunk q is in c1
+    for (; q >= 1; q -= 2) {
+      load_xy(c0, d, TD_W * (q - 1));
+      beta_full(c1, q);
+      load_xy(c1, d, TD_W * (q - 2));
+      beta_full(c0, q - 1);
+    }
+    if (q == 0) beta_full(c1, 0);
   }
 
   // ================= alpha + LLR + output stage =================
@@ -316,6 +335,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     st_fill(o, -TD_INF, -TD_INF);
     Chunk c0, c1;
     load_xy(c0, dp, L - TD_OVERLAP);
+#pragma unroll
     for (int q = 0; q < 5; q += 2) {
       if (q < 4) load_xy(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
 #pragma unroll
@@ -323,12 +343,13 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
         win_alpha_step(o, c0.x[j], c0.y[j]);
         win_norm(8 * q + j, o);
       }
-      if (q == 4) break;
-      if (q < 3) load_xy(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
+      if (q < 4) {
+        if (q < 3) load_xy(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
 #pragma unroll
-      for (int j = 0; j < TD_W; j++) {
-        win_alpha_step(o, c1.x[j], c1.y[j]);
-        win_norm(8 * (q + 1) + j, o);
+        for (int j = 0; j < TD_W; j++) {
+          win_alpha_step(o, c1.x[j], c1.y[j]);
+          win_norm(8 * (q + 1) + j, o);
+        }
       }
     }
     if (d == 0) st_fill(o, 0, -TD_INF);
@@ -348,18 +369,55 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     ck_load(ck, (size_t)(q + 1) * nlanes + g, c.ck); // beta stored at min(8q+8, L)
   };
 
-  auto seg = [&](Chunk &c, int q) {
+  // one LLR step at position k = 8q+j from the forward state o and stored beta[k+1]
+  auto llr_step = [&](const Chunk &c, const St8 &b, int j) {
+    s2 mb[8], nw[8];
+    win_alpha_branches(o, c.x[j], c.y[j], mb, nw);
+    s2 m0 = sadd(b.s[0], mb[0]);
+    s2 m1 = sadd(b.s[0], nw[0]);
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      m0 = smax(m0, sadd(b.s[i], mb[i]));
+      m1 = smax(m1, sadd(b.s[i], nw[i]));
+    }
+    s2 v = ssub(m1, m0);
+    if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
+    store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+  };
+
+  // full segment q (8 steps, s1 = 8q+8 < L): branch-free
+  auto seg_full = [&](Chunk &c, int q) {
+    St8 bst[TD_W]; // bst[j] = stored beta[8q+1+j]
+    St8 run;
+    ck_unpack(c.ck, run);
+    bst[TD_W - 1] = run;
+    norm_by(run, run.s[0]); // s1 = 8q+8: even, non-zero
+#pragma unroll
+    for (int j = TD_W - 2; j >= 0; j--) {
+      win_beta_step(run, c.x[j + 1], c.y[j + 1]);
+      bst[j] = run;
+      if (((j + 1) & 1) == 0) norm_by(run, run.s[0]); // k = 8q+1+j >= 1
+    }
+#pragma unroll
+    for (int j = 0; j < TD_W; j++) {
+      llr_step(c, bst[j], j);
+      if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+    }
+  };
+
+  // last segment (steps 8q .. L-1, 1..8 of them)
+  auto seg_last = [&](Chunk &c, int q) {
     const int s0 = TD_W * q;
-    const int n = min(TD_W, L - s0);
-    const int s1 = s0 + n;
-    St8 bst[TD_W]; // bst[j] = stored beta[s0+1+j]
+    const int n = L - s0;
+    St8 bst[TD_W];
     St8 run;
     ck_unpack(c.ck, run);
 #pragma unroll
     for (int j = TD_W - 1; j >= 0; j--) {
       if (j == n - 1) bst[j] = run;
     }
-    if (s1 != L) win_norm(s1, run); // the running state continues from the normalised value
 #pragma unroll
     for (int j = TD_W - 2; j >= 0; j--) {
       if (j <= n - 2) {
@@ -371,20 +429,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
 #pragma unroll
     for (int j = 0; j < TD_W; j++) {
       if (j < n) {
-        s2 mb[8], nw[8];
-        win_alpha_branches(o, c.x[j], c.y[j], mb, nw);
-        s2 m0 = sadd(bst[j].s[0], mb[0]);
-        s2 m1 = sadd(bst[j].s[0], nw[0]);
-#pragma unroll
-        for (int i = 1; i < 8; i++) {
-          m0 = smax(m0, sadd(bst[j].s[i], mb[i]));
-          m1 = smax(m1, sadd(bst[j].s[i], nw[i]));
-        }
-        s2 v = ssub(m1, m0);
-        if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
-        store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
-#pragma unroll
-        for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+        llr_step(c, bst[j], j);
         win_norm(s0 + j, o);
       }
     }
@@ -392,13 +437,20 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
 
   {
     Chunk c0, c1;
+    int q = 0;
     load_seg(c0, 0);
-    for (int q = 0; q < nc; q += 2) {
-      if (q + 1 < nc) load_seg(c1, q + 1);
-      seg(c0, q);
-      if (q + 1 >= nc) break;
-      if (q + 2 < nc) load_seg(c0, q + 2);
-      seg(c1, q + 1);
+    for (; q + 2 < nc; q += 2) { // segments q and q+1 are full
+      load_seg(c1, q + 1);
+      seg_full(c0, q);
+      load_seg(c0, q + 2);
+      seg_full(c1, q + 1);
+    }
+    if (q == nc - 2) {
+      load_seg(c1, q + 1);
+      seg_full(c0, q);
+      seg_last(c1, q + 1);
+    } else {
+      seg_last(c0, q);
     }
   }
 }
