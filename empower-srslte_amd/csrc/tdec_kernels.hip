@@ -33,6 +33,7 @@
 // integer recursion) and emits LLRs. All inputs are software-pipelined one 8-step chunk ahead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "tdec_kernels.h"
 
@@ -44,6 +45,9 @@ typedef short s4 __attribute__((ext_vector_type(4)));
 #define TD_INF 10000  // turbodecoder_win.h:63 / _sse.c:51 / _gen.c:41
 #define TD_OVERLAP 40 // turbodecoder_win.h:59 win_overlap_len
 #define TD_W 8        // checkpoint period / chunk length (steps)
+#ifndef TD_BIDIR_CW
+#define TD_BIDIR_CW 16 // checkpoint period of the bidirectional decoder (LDS checkpoints)
+#endif
 
 __device__ __forceinline__ s2 sadd(s2 a, s2 b) { return __builtin_elementwise_add_sat(a, b); }
 __device__ __forceinline__ s2 ssub(s2 a, s2 b) { return __builtin_elementwise_sub_sat(a, b); }
@@ -455,6 +459,338 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   }
 }
 
+// ------------------------------------------------------------------ windowed, bidirectional ----
+// Same arithmetic as k_win_halfit, two waves per 64 sub-block chains: wave 0 runs the forward
+// (alpha) recursion, wave 1 the backward (beta) recursion, both starting at their end of the
+// sub-block and meeting at M (a multiple of CW near L/2). In its first half each wave only
+// recurses and checkpoints its metric every CW steps into LDS (alpha: entering state; beta: the
+// value the reference stores, before normalisation); after a workgroup barrier each wave emits
+// the LLRs of the other wave's first half, recomputing the other metric CW steps at a time from
+// those checkpoints. Every position is visited once per direction with the reference's
+// normalisation schedule, so all metrics are the reference's; the serial chain is half as long
+// and the checkpoints never touch HBM.
+template <int CW>
+struct ChunkW {
+  s2 x[CW], y[CW], e[CW];
+  int t[CW];
+};
+
+template <int NB, int DIV, bool DEC2, int CW>
+__global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   const uint16_t *__restrict__ tbl,
+                                                   const uint8_t *__restrict__ pair_done, int K,
+                                                   int npairs) {
+  // checkpoint slots in (dynamic) LDS, [slot][half][lane] x 16 B (conflict-free b128 accesses);
+  // nc + 1 slots of 2 KiB: 50 KiB at K = 6144 with 16 sub-blocks
+  extern __shared__ s4 cks[];
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
+  const int lane = threadIdx.x & 63;
+  const int gl = blockIdx.x * 64 + lane;
+  const int nlanes = npairs * NB;
+  const bool live = gl < nlanes;
+  const int g = live ? gl : nlanes - 1; // dead lanes compute on valid data, store nothing
+  const int pair = g / NB;
+  const int d = g % NB;
+  {
+    // whole block finished (early stop): both waves leave before the barrier
+    const int p0 = (blockIdx.x * 64) / NB;
+    const int p1 = min((blockIdx.x * 64 + 63) / NB, npairs - 1);
+    bool all_done = pair_done != nullptr;
+    if (pair_done)
+      for (int p = p0; p <= p1; p++) all_done = all_done && pair_done[p];
+    if (all_done) return;
+  }
+  const bool wr = live && !(pair_done && pair_done[pair]);
+  const int L = K / NB;
+  const int nc = (L + CW - 1) / CW;
+  const int qm = nc / 2; // meeting chunk: M = CW*qm
+  const size_t base = (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s4 *xp1 = XP1 + base;
+  s2 *A = Aarr + base;
+  const s2 *tl = T + (size_t)pair * 12;
+  const int tail_xoff = DEC2 ? 6 : 0;
+
+  auto ck_put = [&](int slot, const St8 &o) {
+    s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
+    p[0] = s4{o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
+    p[1] = s4{o.s[2].x, o.s[2].y, o.s[3].x, o.s[3].y};
+    s4 *q = &cks[((slot * 2 + 1) * 64 + lane) * 2];
+    q[0] = s4{o.s[4].x, o.s[4].y, o.s[5].x, o.s[5].y};
+    q[1] = s4{o.s[6].x, o.s[6].y, o.s[7].x, o.s[7].y};
+  };
+  auto ck_get = [&](int slot, St8 &o) {
+    const s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
+    const s4 *q = &cks[((slot * 2 + 1) * 64 + lane) * 2];
+    s4 a = p[0], b = p[1], c = q[0], e = q[1];
+    o.s[0] = lo2(a);
+    o.s[1] = hi2(a);
+    o.s[2] = lo2(b);
+    o.s[3] = hi2(b);
+    o.s[4] = lo2(c);
+    o.s[5] = hi2(c);
+    o.s[6] = lo2(e);
+    o.s[7] = hi2(e);
+  };
+  auto load_x8 = [&](ChunkW<8> &c, int col, int k0) { // prepass chunks
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      int k = min(max(k0 + j, 0), L - 1);
+      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + col);
+      c.x[j] = s.x;
+      c.y[j] = s.y;
+    }
+  };
+  auto load_xy = [&](ChunkW<CW> &c, int q) {
+#pragma unroll
+    for (int j = 0; j < CW; j++) {
+      int k = min(max(CW * q + j, 0), L - 1);
+      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + d);
+      c.x[j] = s.x;
+      c.y[j] = s.y;
+    }
+  };
+  auto load_full = [&](ChunkW<CW> &c, int q) {
+#pragma unroll
+    for (int j = 0; j < CW; j++) {
+      int k = min(max(CW * q + j, 0), L - 1);
+      int i = k * NB + d;
+      StepIn s = load_step<DEC2, false>(sp0, xp1, A, i);
+      c.x[j] = s.x;
+      c.y[j] = s.y;
+      c.e[j] = s.e;
+      c.t[j] = tbl[i];
+    }
+  };
+  auto norm_by = [&](St8 &o, s2 z) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], z);
+  };
+  // normalisation operand at step k = CW*q + j, k even (win.h:244-261: never at k == 0)
+  auto norm_op = [&](const St8 &o, int q, int j) -> s2 {
+    return (j == 0 && q == 0) ? splat(0) : o.s[0];
+  };
+  // LLR at position k from alpha_k (al), the chunk's inputs and stored beta[k+1] (be)
+  auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, s2 mb[8], s2 nw[8]) {
+    win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
+    s2 m0 = sadd(be.s[0], mb[0]);
+    s2 m1 = sadd(be.s[0], nw[0]);
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      m0 = smax(m0, sadd(be.s[i], mb[i]));
+      m1 = smax(m1, sadd(be.s[i], nw[i]));
+    }
+    s2 v = ssub(m1, m0);
+    if (DIV) v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
+    if (wr) store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
+  };
+
+  St8 o;
+  if (role == 0) {
+    // ================= forward wave =================
+    {
+      // win.h:501-506,512-584 (loop_len = 40) over the last 40 steps of sub-block d-1;
+      // move_left (:469-495); sub-block 0 starts in state 0 (:496-500)
+      const int dp = d > 0 ? d - 1 : 0;
+      st_fill(o, -TD_INF, -TD_INF);
+      ChunkW<8> c0, c1;
+      load_x8(c0, dp, L - TD_OVERLAP);
+#pragma unroll
+      for (int q = 0; q < 5; q += 2) {
+        if (q < 4) load_x8(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          win_alpha_step(o, c0.x[j], c0.y[j]);
+          win_norm(8 * q + j, o);
+        }
+        if (q < 4) {
+          if (q < 3) load_x8(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            win_alpha_step(o, c1.x[j], c1.y[j]);
+            win_norm(8 * (q + 1) + j, o);
+          }
+        }
+      }
+      if (d == 0) st_fill(o, 0, -TD_INF);
+    }
+    // first half: chunks 0 .. qm-1, checkpoint the entering state of each
+    {
+      auto fwd_chunk = [&](ChunkW<CW> &c, int q) {
+        ck_put(q, o);
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+          win_alpha_step(o, c.x[j], c.y[j]);
+          if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+        }
+      };
+      ChunkW<CW> c0, c1;
+      int q = 0;
+      load_xy(c0, 0);
+      for (; q + 1 < qm; q += 2) {
+        load_xy(c1, q + 1);
+        fwd_chunk(c0, q);
+        load_xy(c0, q + 2);
+        fwd_chunk(c1, q + 1);
+      }
+      if (q < qm) fwd_chunk(c0, q);
+    }
+    __syncthreads();
+    // second half: segments qm .. nc-1 with betas recomputed from the backward checkpoints
+    {
+      auto seg = [&](ChunkW<CW> &c, int q, bool last) {
+        const int s0 = CW * q;
+        const int n = last ? L - s0 : CW;
+        St8 bst[CW]; // bst[j] = stored beta[s0+1+j]
+        St8 run;
+        ck_get(min(q + 1, nc), run);
+#pragma unroll
+        for (int j = CW - 1; j >= 0; j--)
+          if (j == n - 1) bst[j] = run;
+        if (!last) norm_by(run, run.s[0]); // s1 = s0+CW < L: even, non-zero
+#pragma unroll
+        for (int j = CW - 2; j >= 0; j--) {
+          if (j <= n - 2) {
+            win_beta_step(run, c.x[j + 1], c.y[j + 1]);
+            bst[j] = run;
+            if (((j + 1) & 1) == 0) norm_by(run, run.s[0]); // k = s0+1+j >= 1
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+          if (j < n) {
+            s2 mb[8], nw[8];
+            llr_out(c, o, bst[j], j, mb, nw);
+#pragma unroll
+            for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+            if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+          }
+        }
+      };
+      ChunkW<CW> c0, c1;
+      int q = qm;
+      load_full(c0, q);
+      for (; q + 2 < nc; q += 2) {
+        load_full(c1, q + 1);
+        seg(c0, q, false);
+        load_full(c0, q + 2);
+        seg(c1, q + 1, false);
+      }
+      if (q == nc - 2) {
+        load_full(c1, q + 1);
+        seg(c0, q, false);
+        seg(c1, q + 1, true);
+      } else {
+        seg(c0, q, true);
+      }
+    }
+  } else {
+    // ================= backward wave =================
+    {
+      // win.h:376-384,386-433 (loop_len = 40) over the first 40 steps of sub-block d+1;
+      // move_right (:333-366); the last sub-block starts from the tail trellis (:350-355)
+      const int dn = d + 1 < NB ? d + 1 : d;
+      st_fill(o, -TD_INF, -TD_INF);
+      ChunkW<8> c0, c1;
+      load_x8(c0, dn, 32);
+#pragma unroll
+      for (int q = 4; q >= 0; q -= 2) {
+        if (q > 0) load_x8(c1, dn, 8 * (q - 1));
+#pragma unroll
+        for (int j = 7; j >= 0; j--) {
+          win_beta_step(o, c0.x[j], c0.y[j]);
+          win_norm(8 * q + j, o);
+        }
+        if (q > 0) {
+          if (q > 1) load_x8(c0, dn, 8 * (q - 2));
+#pragma unroll
+          for (int j = 7; j >= 0; j--) {
+            win_beta_step(o, c1.x[j], c1.y[j]);
+            win_norm(8 * (q - 1) + j, o);
+          }
+        }
+      }
+      St8 t;
+      win_tail_trellis(tl, tail_xoff, t);
+      if (d == NB - 1) o = t;
+    }
+    ck_put(nc, o); // beta[L] (win.h:372-374)
+    // first half: chunks nc-1 .. qm (steps L-1 .. M); bpre ends as beta[M] before normalisation
+    St8 bpre;
+    {
+      auto bwd_chunk = [&](ChunkW<CW> &c, int q, int n, bool keep) { // q > 0: norm never at 0
+#pragma unroll
+        for (int j = CW - 1; j >= 0; j--) {
+          if (j < n) {
+            win_beta_step(o, c.x[j], c.y[j]);
+            if (j == 0) {
+              if (keep)
+                bpre = o;
+              else
+                ck_put(q, o);
+            }
+            if ((j & 1) == 0) norm_by(o, o.s[0]);
+          }
+        }
+      };
+      ChunkW<CW> c0, c1;
+      const int qt = nc - 1; // top chunk, possibly partial; qt > qm
+      load_xy(c0, qt);
+      load_xy(c1, qt - 1);
+      bwd_chunk(c0, qt, L - CW * qt, false);
+      int q = qt - 1; // in c1
+      for (; q - 1 > qm; q -= 2) {
+        load_xy(c0, q - 1);
+        bwd_chunk(c1, q, CW, false);
+        load_xy(c1, q - 2);
+        bwd_chunk(c0, q - 1, CW, false);
+      }
+      if (q > qm) {
+        load_xy(c0, q - 1);
+        bwd_chunk(c1, q, CW, false);
+        bwd_chunk(c0, qm, CW, true);
+      } else {
+        bwd_chunk(c1, qm, CW, true);
+      }
+    }
+    __syncthreads();
+    // second half: segments qm-1 .. 0 (full), alphas recomputed from the forward checkpoints
+    {
+      auto seg = [&](ChunkW<CW> &c, int q) {
+        St8 ast[CW]; // ast[j] = alpha entering step CW*q+j
+        ck_get(q, ast[0]);
+#pragma unroll
+        for (int j = 0; j < CW - 1; j++) {
+          ast[j + 1] = ast[j];
+          win_alpha_step(ast[j + 1], c.x[j], c.y[j]);
+          if ((j & 1) == 0) norm_by(ast[j + 1], norm_op(ast[j + 1], q, j));
+        }
+#pragma unroll
+        for (int j = CW - 1; j >= 0; j--) {
+          s2 mb[8], nw[8];
+          llr_out(c, ast[j], bpre, j, mb, nw); // bpre = stored beta[k+1]
+          // running beta at k+1 (normalised when k+1 is even; k+1 >= 1), then beta[k]
+          St8 run = bpre;
+          if (((j + 1) & 1) == 0) norm_by(run, run.s[0]);
+          win_beta_step(run, c.x[j], c.y[j]);
+          bpre = run;
+        }
+      };
+      ChunkW<CW> c0, c1;
+      int q = qm - 1;
+      load_full(c0, q);
+      for (; q - 1 >= 0; q -= 2) {
+        load_full(c1, q - 1);
+        seg(c0, q);
+        load_full(c0, q - 2);
+        seg(c1, q - 1);
+      }
+      if (q == 0) seg(c0, 0);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ SSE non-window ----
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
@@ -775,6 +1111,11 @@ __global__ void k_pair_done(int ncb, const uint8_t *__restrict__ cb_done,
 
 static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
+// dynamic LDS above 64 KiB (the 8-sub-block decoder at large K) needs the per-kernel opt-in
+static void allow_big_lds(const void *f) {
+  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
 hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
                        void *SP0, void *XP1, void *A, void *T, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
@@ -808,14 +1149,29 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
 #define WIN(nb, div, d2)                                                                           \
   hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, t, tbl, ck,        \
                      pair_done, K, npairs)
+#define BIDIR(nb, div, d2)                                                                         \
+  allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW>));                                \
+  hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW>), dim3(nblk((size_t)npairs * NB, 64)),   \
+                     dim3(128), bidir_lds, st, sp0, xp1, a, t, tbl, pair_done, K, npairs)
+    static const bool unidir = getenv("SRSGPU_TDEC_UNIDIR") != nullptr;
+    const size_t bidir_lds = (size_t)((K / NB + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
     if (NB == 16) {
-      if (dec2) WIN(16, 0, true); else WIN(16, 0, false);
+      if (unidir) {
+        if (dec2) WIN(16, 0, true); else WIN(16, 0, false);
+      } else {
+        if (dec2) BIDIR(16, 0, true); else BIDIR(16, 0, false);
+      }
     } else if (NB == 8) {
-      if (dec2) WIN(8, 1, true); else WIN(8, 1, false);
+      if (unidir) {
+        if (dec2) WIN(8, 1, true); else WIN(8, 1, false);
+      } else {
+        if (dec2) BIDIR(8, 1, true); else BIDIR(8, 1, false);
+      }
     } else {
       return hipErrorInvalidValue;
     }
 #undef WIN
+#undef BIDIR
   } else {
     dim3 grid(nblk(npairs, 64)), blk(64);
     s2 *sc = (s2 *)scratch;
