@@ -1150,9 +1150,11 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
   hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, t, tbl, ck,        \
                      pair_done, K, npairs)
 #define BIDIR(nb, div, d2)                                                                         \
-  allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW>));                                \
-  hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW>), dim3(nblk((size_t)npairs * NB, 64)),   \
-                     dim3(128), bidir_lds, st, sp0, xp1, a, t, tbl, pair_done, K, npairs)
+  do {                                                                                             \
+    allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW>));                          \
+    hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW>), dim3(nblk((size_t)npairs * NB, 64)), \
+                       dim3(128), bidir_lds, st, sp0, xp1, a, t, tbl, pair_done, K, npairs);         \
+  } while (0)
     static const bool unidir = getenv("SRSGPU_TDEC_UNIDIR") != nullptr;
     const size_t bidir_lds = (size_t)((K / NB + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
     if (NB == 16) {
