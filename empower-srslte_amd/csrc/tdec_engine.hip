@@ -2,7 +2,7 @@
 // C ABI (include/srsgpu/tdec_batch.h + the drop-in include/srslte/phy/fec/turbodecoder.h).
 //
 // Schedule per code-block batch (all CBs share K; mirrors turbodecoder_iter.h:283-357):
-//   load          user layout -> pair-interleaved syst/par0 (SP0), par1 (XP1), tails; A = 0
+//   load          user layout -> pair-interleaved syst/par0 (SP0), par1 (P1 plane of XP1), tails
 //   halfit(n)     one constituent decoder run: DEC1 for even n, DEC2 for odd n, with the
 //                 interleave / subtract glue fused into its output stage (tdec_kernels.hip)
 //   decide(n)     hard decision after half-iteration n (+ CRC and early-stop flags when asked,
@@ -126,7 +126,8 @@ struct Engine {
   hipStream_t st = nullptr;
   uint32_t cap_cbs = 0, cap_K = 0;
   size_t cap_pairs = 0;
-  // pair-interleaved arrays [pairs][K]: SP0, XP1 short4; A short2; T short2 [pairs][12]
+  // pair-interleaved arrays [pairs][K]: SP0 short4; XP1 = X2, P1 short2 planes; A short2;
+  // T short2 [pairs][12]
   void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr;
   void *scratch = nullptr; // checkpoints (windowed) / alpha-beta (sequential)
   size_t scratch_bytes = 0;
@@ -236,7 +237,7 @@ struct Engine {
     npairs = (ncb + 1) / 2;
     if (get_interleaver(K, (uint32_t)nb)) return -1;
     const int sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nb > 1;
-    HIPCHK(srsgpu::launch_load(d_in, in_stride, sb_input, (int)K, nb, ncb, SP0, XP1, A, T, st));
+    HIPCHK(srsgpu::launch_load(d_in, in_stride, sb_input, (int)K, nb, ncb, SP0, XP1, T, st));
     HIPCHK(hipMemsetAsync(cb_done, 0, cap_pairs * 2, st));
     HIPCHK(hipMemsetAsync(cb_ok, 0, cap_pairs * 2, st));
     HIPCHK(hipMemsetAsync(pair_done, 0, cap_pairs, st));

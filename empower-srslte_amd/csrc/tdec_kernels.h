@@ -6,9 +6,10 @@
 #include <stdint.h>
 
 namespace srsgpu {
-// user input -> SP0 (short4), XP1 (short4, par1 half), A = 0 (short2), T (short2 x 12) per pair
+// user input -> SP0 (short4), P1 plane of XP1 (short2), T (short2 x 12) per pair. XP1 holds
+// two [npairs][K] short2 planes: X2 (app2) then P1 (par1).
 hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
-                       void *SP0, void *XP1, void *A, void *T, hipStream_t st);
+                       void *SP0, void *XP1, void *T, hipStream_t st);
 size_t win_ck_bytes(int K, int NB, int npairs);
 size_t seq_scratch_bytes(int K, int npairs);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n). NB > 1: windowed decoder;

@@ -17,8 +17,11 @@
 // (pi(x + tW) = pi(x) mod W), the interleaver scatters of one step also land on NB consecutive
 // elements (permuted) — every global access is a 64/128-byte coalesced group.
 //   SP0[pair][K]  short4 (syst.a, syst.b, par0.a, par0.b)          static
-//   XP1[pair][K]  short4 (app2.a, app2.b, par1.a, par1.b)          app2 rewritten by DEC1
-//   A  [pair][K]  short2  app1 - ext1 ("a priori" of DEC1), 0 before the first half-iteration
+//   X2 [pair][K]  short2  app2 (DEC2 input), rewritten by every DEC1 (dense, so the scattered
+//                 DEC1 stores fill whole cache lines)
+//   P1 [pair][K]  short2  par1                                      static (X2 + npairs*K)
+//   A  [pair][K]  short2  app1 - ext1 ("a priori" of DEC1); the first DEC1 neither reads it nor
+//                 needs it zeroed (MODE 2), DEC2 writes every element
 //   T  [pair][12] short2  tail values as in the reference input (s,p0)x3 (app2,p1)x3
 // Half-iteration n even (DEC1): x = syst (+) A, y = par0; the LLR L gives E' = L - A, scattered
 //   to app2[rev[j]] (the reference's ext1 -= app1 and vec_lut interleave).
@@ -184,18 +187,20 @@ struct StepIn {
   s2 x, y, e;
 };
 
-template <bool DEC2, bool WRAP>
-__device__ __forceinline__ StepIn load_step(const s4 *__restrict__ sp0, const s4 *__restrict__ xp1,
-                                            const s2 *__restrict__ A, int i) {
+// MODE: 0 = DEC1, 1 = DEC2, 2 = DEC1 of the first half-iteration (app1 is still all zero, so
+// A is neither read nor needed: turbodecoder_iter.h:318-323 passes NULL as app).
+template <int MODE, bool WRAP>
+__device__ __forceinline__ StepIn load_step(const s4 *__restrict__ sp0, const s2 *__restrict__ x2,
+                                            const s2 *__restrict__ p1, const s2 *__restrict__ A,
+                                            int i) {
   StepIn r;
-  if (DEC2) {
-    s4 v = xp1[i];
-    r.x = lo2(v);
-    r.y = hi2(v);
+  if (MODE == 1) {
+    r.x = x2[i];
+    r.y = p1[i];
     r.e = r.x;
   } else {
     s4 v = sp0[i];
-    s2 a = A[i];
+    s2 a = MODE == 2 ? splat(0) : A[i];
     r.x = WRAP ? wadd(lo2(v), a) : sadd(a, lo2(v));
     r.y = hi2(v);
     r.e = a;
@@ -206,13 +211,13 @@ __device__ __forceinline__ StepIn load_step(const s4 *__restrict__ sp0, const s4
 // Output stage (turbodecoder_iter.h:315-341): DEC1 ext1 -> app2 (interleave, minus app1);
 // DEC2 ext2 -> A (deinterleave, minus the a priori it was fed).
 template <bool DEC2>
-__device__ __forceinline__ void store_out(s4 *__restrict__ xp1, s2 *__restrict__ A, int t, s2 llr,
+__device__ __forceinline__ void store_out(s2 *__restrict__ x2, s2 *__restrict__ A, int t, s2 llr,
                                           s2 e) {
   s2 v = wsub(llr, e);
   if (DEC2)
     A[t] = v;
   else
-    reinterpret_cast<s2 *>(xp1)[2 * t] = v;
+    x2[t] = v;
 }
 
 // 8-step chunk of inputs (+ scatter indices + the segment's beta checkpoint) in registers
@@ -223,8 +228,8 @@ struct Chunk {
 };
 
 // ------------------------------------------------------------------ windowed decoder ----
-template <int NB, int DIV, bool DEC2>
-__global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+template <int NB, int DIV, int MODE>
+__global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                     s2 *__restrict__ Aarr, const s2 *__restrict__ T,
                                                     const uint16_t *__restrict__ tbl,
                                                     s4 *__restrict__ ck,
@@ -240,17 +245,18 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   const int nlanes = npairs * NB;
   const size_t base = (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s4 *xp1 = XP1 + base;
+  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
+  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
   const s2 *tl = T + (size_t)pair * 12;
-  const int tail_xoff = DEC2 ? 6 : 0;
+  const int tail_xoff = MODE == 1 ? 6 : 0;
 
   // loads of one 8-step chunk of column col: steps k0 .. k0+7, clamped into the sub-block
   auto load_xy = [&](Chunk &c, int col, int k0) {
 #pragma unroll
     for (int j = 0; j < TD_W; j++) {
       int k = min(max(k0 + j, 0), L - 1);
-      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + col);
+      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + col);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     for (int j = 0; j < TD_W; j++) {
       int k = min(TD_W * q + j, L - 1);
       int i = k * NB + d;
-      StepIn s = load_step<DEC2, false>(sp0, xp1, A, i);
+      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
       c.x[j] = s.x;
       c.y[j] = s.y;
       c.e[j] = s.e;
@@ -386,7 +392,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     }
     s2 v = ssub(m1, m0);
     if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
-    store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
+    store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
 #pragma unroll
     for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
   };
@@ -475,8 +481,8 @@ struct ChunkW {
   int t[CW];
 };
 
-template <int NB, int DIV, bool DEC2, int CW>
-__global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+template <int NB, int DIV, int MODE, int CW>
+__global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    const uint8_t *__restrict__ pair_done, int K,
@@ -507,10 +513,11 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
   const int qm = nc / 2; // meeting chunk: M = CW*qm
   const size_t base = (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s4 *xp1 = XP1 + base;
+  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
+  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
   const s2 *tl = T + (size_t)pair * 12;
-  const int tail_xoff = DEC2 ? 6 : 0;
+  const int tail_xoff = MODE == 1 ? 6 : 0;
 
   auto ck_put = [&](int slot, const St8 &o) {
     s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
@@ -537,7 +544,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       int k = min(max(k0 + j, 0), L - 1);
-      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + col);
+      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + col);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
@@ -546,7 +553,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 #pragma unroll
     for (int j = 0; j < CW; j++) {
       int k = min(max(CW * q + j, 0), L - 1);
-      StepIn s = load_step<DEC2, false>(sp0, xp1, A, k * NB + d);
+      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + d);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
@@ -556,7 +563,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
     for (int j = 0; j < CW; j++) {
       int k = min(max(CW * q + j, 0), L - 1);
       int i = k * NB + d;
-      StepIn s = load_step<DEC2, false>(sp0, xp1, A, i);
+      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
       c.x[j] = s.x;
       c.y[j] = s.y;
       c.e[j] = s.e;
@@ -574,16 +581,23 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
   // LLR at position k from alpha_k (al), the chunk's inputs and stored beta[k+1] (be)
   auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, s2 mb[8], s2 nw[8]) {
     win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
-    s2 m0 = sadd(be.s[0], mb[0]);
-    s2 m1 = sadd(be.s[0], nw[0]);
+    // max over the 8 branches as a tree (max is exact, so any order is the reference's)
+    s2 t0[8], t1[8];
 #pragma unroll
-    for (int i = 1; i < 8; i++) {
-      m0 = smax(m0, sadd(be.s[i], mb[i]));
-      m1 = smax(m1, sadd(be.s[i], nw[i]));
+    for (int i = 0; i < 8; i++) {
+      t0[i] = sadd(be.s[i], mb[i]);
+      t1[i] = sadd(be.s[i], nw[i]);
     }
-    s2 v = ssub(m1, m0);
+#pragma unroll
+    for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+      for (int i = 0; i < w; i++) {
+        t0[i] = smax(t0[i], t0[i + w]);
+        t1[i] = smax(t1[i], t1[i + w]);
+      }
+    s2 v = ssub(t1[0], t0[0]);
     if (DIV) v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
-    if (wr) store_out<DEC2>(xp1, A, c.t[j], v, c.e[j]);
+    if (wr) store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
   };
 
   St8 o;
@@ -795,8 +809,8 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
 // scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
-template <bool DEC2>
-__global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+template <int MODE>
+__global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    s2 *__restrict__ scratch,
@@ -807,10 +821,11 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
   if (pair_done && pair_done[pair]) return;
   const size_t base = (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s4 *xp1 = XP1 + base;
+  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
+  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
   const s2 *tl = T + (size_t)pair * 12;
-  const int tail_xoff = DEC2 ? 6 : 0;
+  const int tail_xoff = MODE == 1 ? 6 : 0;
   auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   s2 a[8];
   a[0] = splat(0);
@@ -819,7 +834,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
 #pragma unroll
   for (int i = 0; i < 8; i++) AL(0, i) = a[i];
   for (int k = 0; k < K; k++) { // :211-297
-    StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+    StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k);
     s2 g1 = wadd(s.x, s.y) >> 1, g0 = wsub(s.x, s.y) >> 1;
     s2 n[8];
     n[0] = smax(wadd(a[1], g1), wsub(a[0], g1));
@@ -852,7 +867,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
       g0 = s2{(short)(((int)x.x - y.x) / 2), (short)(((int)x.y - y.y) / 2)};
       g1 = s2{(short)(((int)x.x + y.x) / 2), (short)(((int)x.y + y.y) / 2)};
     } else {
-      StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+      StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k);
       g1 = wadd(s.x, s.y) >> 1;
       g0 = wsub(s.x, s.y) >> 1;
       e = s.e;
@@ -873,7 +888,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
       }
       // hMax(bn) - hMax(bp) with hMax(v) = 0x7FFF - max(v) (minpos_epu16 trick, :97-102)
       s2 llr = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
-      store_out<DEC2>(xp1, A, tbl[k], llr, e);
+      store_out<MODE == 1>(xp1, A, tbl[k], llr, e);
       if ((k & 3) == 0) {
         s2 z = b[0];
 #pragma unroll
@@ -887,8 +902,8 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
 // turbodecoder_gen.c:59-236, one lane per CB pair, natural index, wrapping int16; app is added
 // for k < K only (:72-74), which is exactly the range the input policy covers.
 // scratch: beta (K+4)*8 short2 per pair.
-template <bool DEC2>
-__global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s4 *__restrict__ XP1,
+template <int MODE>
+__global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    s2 *__restrict__ scratch,
@@ -899,10 +914,11 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
   if (pair_done && pair_done[pair]) return;
   const size_t base = (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s4 *xp1 = XP1 + base;
+  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
+  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
   const s2 *tl = T + (size_t)pair * 12;
-  const int tail_xoff = DEC2 ? 6 : 0;
+  const int tail_xoff = MODE == 1 ? 6 : 0;
   auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   const int end = K + 3;
   s2 o[8];
@@ -915,7 +931,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
       x = tl[tail_xoff + 2 * (k - K)];
       y = tl[tail_xoff + 2 * (k - K) + 1];
     } else {
-      StepIn s = load_step<DEC2, true>(sp0, xp1, A, k);
+      StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k);
       x = s.x;
       y = s.y;
     }
@@ -940,7 +956,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
 #pragma unroll
   for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
   for (int k = 1; k < K + 1; k++) {
-    StepIn s = load_step<DEC2, true>(sp0, xp1, A, k - 1);
+    StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k - 1);
     s2 x = s.x, y = s.y, xy_ = wadd(x, y);
     s2 mb[8] = {a[0], wadd(a[3], y), wadd(a[4], y), a[7],
                 a[1], wadd(a[2], y), wadd(a[5], y), a[6]};
@@ -960,66 +976,95 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
 #pragma unroll
       for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
     }
-    store_out<DEC2>(xp1, A, tbl[k - 1], wsub(m1, m0), s.e);
+    store_out<MODE == 1>(xp1, A, tbl[k - 1], wsub(m1, m0), s.e);
   }
 }
 
 // ------------------------------------------------------------------ load ----
-// User layout -> SP0 / XP1.par1 / T, A = 0. Natural input ([s,p0,p1]*K + 12 tail;
+// User layout -> SP0 / P1 / T. Natural input ([s,p0,p1]*K + 12 tail;
 // turbodecoder_gen.c:240-259, win.h:634-674) is transposed through LDS: a workgroup takes 64
 // consecutive steps k of all NB sub-blocks of one pair, reads NB runs of 64 natural positions
 // (coalesced), and writes the 64*NB SB-ordered elements contiguously. SB input (rm_turbo's
 // layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280) is a straight copy.
 #define LOAD_KT 64
-__global__ __launch_bounds__(256) void k_load(const int16_t *__restrict__ in, size_t in_stride,
-                                              int sb_input, int K, int NB, int ncb,
-                                              s4 *__restrict__ SP0, s4 *__restrict__ XP1,
-                                              s2 *__restrict__ Aarr, s2 *__restrict__ T) {
-  __shared__ short lds[2][3][LOAD_KT * 16 + 1];
+// NB and the tile are compile-time so the run/offset arithmetic is shifts and multiplies; VEC
+// reads the natural runs as dwords (in, in_stride and L even).
+template <int NB, bool VEC>
+__global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in, size_t in_stride,
+                                                  int K, int ncb, s4 *__restrict__ SP0,
+                                                  s2 *__restrict__ P1, s2 *__restrict__ T) {
+  constexpr int RUN = 3 * LOAD_KT; // int16 per (CB, sub-block) run of one tile
+  __shared__ short lds[2][3][LOAD_KT * NB];
   const int npairs = (ncb + 1) / 2;
   const int L = K / NB;
   const int ktiles = (L + LOAD_KT - 1) / LOAD_KT;
   const int pair = blockIdx.x / ktiles;
-  const int kt = blockIdx.x % ktiles;
+  const int kt = blockIdx.x - pair * ktiles;
   if (pair >= npairs) return;
   const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
-  const int16_t *src[2] = {in + (size_t)c0 * in_stride, in + (size_t)c1 * in_stride};
-  const size_t base = (size_t)pair * K;
   const int k0 = kt * LOAD_KT;
   const int kn = min(LOAD_KT, L - k0);
-  if (sb_input) {
-    for (int e = threadIdx.x; e < kn * NB; e += blockDim.x) {
-      const int i = k0 * NB + e;
-      s2 s = s2{src[0][i], src[1][i]};
-      s2 p0 = s2{src[0][K + 32 + i], src[1][K + 32 + i]};
-      s2 p1 = s2{src[0][2 * (K + 32) + i], src[1][2 * (K + 32) + i]};
-      SP0[base + i] = s4{s.x, s.y, p0.x, p0.y};
-      XP1[base + i] = s4{0, 0, p1.x, p1.y};
-      Aarr[base + i] = splat(0);
-    }
-  } else {
-    // read: for each sub-block d, natural positions d*L + k0 .. + kn-1, 3 values each
-    for (int h = 0; h < 2; h++) {
-      for (int e = threadIdx.x; e < NB * kn * 3; e += blockDim.x) {
-        const int dd = e / (kn * 3), r = e % (kn * 3);
-        const int kk = r / 3, s = r % 3;
-        lds[h][s][kk * 16 + dd] = src[h][3 * (dd * L + k0) + r];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int16_t *src = in + (size_t)(h ? c1 : c0) * in_stride + 3 * k0;
+    if (VEC) {
+      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
+      for (int w = threadIdx.x; w < NB * RUN / 2; w += 256) {
+        const int dd = w / (RUN / 2), r = 2 * (w - dd * (RUN / 2));
+        if (r < 3 * kn) {
+          const uint32_t v = s32[(dd * 3 * L) / 2 + r / 2];
+          const int kk = r / 3, sidx = r - 3 * kk;
+          lds[h][sidx][kk * NB + dd] = (short)(v & 0xffff);
+          const int r1 = r + 1, kk1 = r1 / 3, s1 = r1 - 3 * kk1;
+          lds[h][s1][kk1 * NB + dd] = (short)(v >> 16);
+        }
+      }
+    } else {
+      for (int e = threadIdx.x; e < NB * RUN; e += 256) {
+        const int dd = e / RUN, r = e - dd * RUN;
+        if (r < 3 * kn) {
+          const int kk = r / 3, sidx = r - 3 * kk;
+          lds[h][sidx][kk * NB + dd] = src[dd * 3 * L + r];
+        }
       }
     }
-    __syncthreads();
-    for (int e = threadIdx.x; e < kn * NB; e += blockDim.x) {
-      const int kk = e / NB, dd = e % NB;
-      const int i = (k0 + kk) * NB + dd;
-      const int li = kk * 16 + dd;
-      SP0[base + i] = s4{lds[0][0][li], lds[1][0][li], lds[0][1][li], lds[1][1][li]};
-      XP1[base + i] = s4{0, 0, lds[0][2][li], lds[1][2][li]};
-      Aarr[base + i] = splat(0);
-    }
+  }
+  __syncthreads();
+  const size_t base = (size_t)pair * K + (size_t)k0 * NB;
+  for (int e = threadIdx.x; e < kn * NB; e += 256) {
+    SP0[base + e] = s4{lds[0][0][e], lds[1][0][e], lds[0][1][e], lds[1][1][e]};
+    P1[base + e] = s2{lds[0][2][e], lds[1][2][e]};
   }
   if (kt == 0 && threadIdx.x < 12) {
     const int t = threadIdx.x;
-    const int tb = sb_input ? 3 * (K + 32) : 3 * K;
-    T[(size_t)pair * 12 + t] = s2{src[0][tb + t], src[1][tb + t]};
+    T[(size_t)pair * 12 + t] = s2{in[(size_t)c0 * in_stride + 3 * K + t],
+                                  in[(size_t)c1 * in_stride + 3 * K + t]};
+  }
+}
+
+// SB input (rm_turbo's layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280):
+// already in SB index order, a straight pair-interleaving copy, two elements per thread.
+__global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in, size_t in_stride,
+                                                 int K, int ncb, s4 *__restrict__ SP0,
+                                                 s2 *__restrict__ P1, s2 *__restrict__ T) {
+  const int npairs = (ncb + 1) / 2;
+  const int per = K / 2;
+  const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int pair = (int)(gid / per);
+  if (pair >= npairs) return;
+  const int i = 2 * (int)(gid - (size_t)pair * per);
+  const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
+  const int16_t *a = in + (size_t)c0 * in_stride, *b = in + (size_t)c1 * in_stride;
+  const size_t o = (size_t)pair * K + i;
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    SP0[o + u] = s4{a[i + u], b[i + u], a[K + 32 + i + u], b[K + 32 + i + u]};
+    P1[o + u] = s2{a[2 * (K + 32) + i + u], b[2 * (K + 32) + i + u]};
+  }
+  if (i < 12) {
+    const int tb = 3 * (K + 32);
+    T[(size_t)pair * 12 + i] = s2{a[tb + i], b[tb + i]};
+    T[(size_t)pair * 12 + i + 1] = s2{a[tb + i + 1], b[tb + i + 1]};
   }
 }
 
@@ -1031,7 +1076,7 @@ __global__ __launch_bounds__(256) void k_load(const int16_t *__restrict__ in, si
 __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
                                                 const uint16_t *__restrict__ rev,
                                                 const s2 *__restrict__ Aarr,
-                                                const s4 *__restrict__ XP1, uint8_t *__restrict__ outb,
+                                                const s2 *__restrict__ XP1, uint8_t *__restrict__ outb,
                                                 size_t out_stride, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
                                                 int crc_bytes, uint32_t poly, int max_halfits) {
@@ -1063,9 +1108,10 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
   __syncthreads();
   const size_t base = (size_t)pair * K;
   const int L = K / NB;
-  const s2 *x2 = reinterpret_cast<const s2 *>(XP1 + base);
+  const s2 *x2 = XP1 + base;
   for (int j = threadIdx.x; j < K; j += blockDim.x) {
-    s2 v = wadd(Aarr[base + j], x2[2 * rev[j]]);
+    // after the first half-iteration A (app1 - ext1) is still zero and was never written
+    s2 v = n == 0 ? x2[rev[j]] : wadd(Aarr[base + j], x2[rev[j]]);
     const int p = NB > 1 ? (j % NB) * L + j / NB : j;
     const uint32_t m = 1u << (8 * ((p >> 3) & 3) + 7 - (p & 7)); // byte p/8, bit 7-p%8
     if (v.x > 0) atomicOr(&bits[0][p >> 5], m);
@@ -1117,12 +1163,33 @@ static void allow_big_lds(const void *f) {
 }
 
 hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
-                       void *SP0, void *XP1, void *A, void *T, hipStream_t st) {
+                       void *SP0, void *XP1, void *T, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
+  s4 *sp0 = (s4 *)SP0;
+  s2 *p1 = (s2 *)XP1 + (size_t)npairs * K;
+  s2 *t = (s2 *)T;
+  if (sb_input) {
+    hipLaunchKernelGGL(k_load_sb, dim3(nblk((size_t)npairs * (K / 2), 256)), dim3(256), 0, st, in,
+                       in_stride, K, ncb, sp0, p1, t);
+    return hipGetLastError();
+  }
   const int L = K / NB;
-  const int ktiles = (L + LOAD_KT - 1) / LOAD_KT;
-  hipLaunchKernelGGL(k_load, dim3((unsigned)(npairs * ktiles)), dim3(256), 0, st, in, in_stride,
-                     sb_input, K, NB, ncb, (s4 *)SP0, (s4 *)XP1, (s2 *)A, (s2 *)T);
+  const unsigned grid = (unsigned)(npairs * ((L + LOAD_KT - 1) / LOAD_KT));
+  const bool vec = ((uintptr_t)in % 4 == 0) && (in_stride % 2 == 0) && (L % 2 == 0);
+#define LOADNAT(nb)                                                                                \
+  do {                                                                                             \
+    if (vec)                                                                                       \
+      hipLaunchKernelGGL((k_load_nat<nb, true>), dim3(grid), dim3(256), 0, st, in, in_stride, K,    \
+                         ncb, sp0, p1, t);                                                         \
+    else                                                                                           \
+      hipLaunchKernelGGL((k_load_nat<nb, false>), dim3(grid), dim3(256), 0, st, in, in_stride, K,   \
+                         ncb, sp0, p1, t);                                                         \
+  } while (0)
+  if (NB == 16) LOADNAT(16);
+  else if (NB == 8) LOADNAT(8);
+  else if (NB == 1) LOADNAT(1);
+  else return hipErrorInvalidValue;
+#undef LOADNAT
   return hipGetLastError();
 }
 
@@ -1138,9 +1205,10 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
                          const uint16_t *fwd, const uint16_t *rev, void *scratch,
                          const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
   const bool dec2 = n & 1;
+  const int mode = dec2 ? 1 : (n == 0 ? 2 : 0);
   const uint16_t *tbl = dec2 ? fwd : rev;
   const s4 *sp0 = (const s4 *)SP0;
-  s4 *xp1 = (s4 *)XP1;
+  s2 *xp1 = (s2 *)XP1;
   s2 *a = (s2 *)A;
   const s2 *t = (const s2 *)T;
   if (NB > 1) {
@@ -1159,15 +1227,15 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
     const size_t bidir_lds = (size_t)((K / NB + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
     if (NB == 16) {
       if (unidir) {
-        if (dec2) WIN(16, 0, true); else WIN(16, 0, false);
+        if (mode == 1) WIN(16, 0, 1); else if (mode == 2) WIN(16, 0, 2); else WIN(16, 0, 0);
       } else {
-        if (dec2) BIDIR(16, 0, true); else BIDIR(16, 0, false);
+        if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
       }
     } else if (NB == 8) {
       if (unidir) {
-        if (dec2) WIN(8, 1, true); else WIN(8, 1, false);
+        if (mode == 1) WIN(8, 1, 1); else if (mode == 2) WIN(8, 1, 2); else WIN(8, 1, 0);
       } else {
-        if (dec2) BIDIR(8, 1, true); else BIDIR(8, 1, false);
+        if (mode == 1) BIDIR(8, 1, 1); else if (mode == 2) BIDIR(8, 1, 2); else BIDIR(8, 1, 0);
       }
     } else {
       return hipErrorInvalidValue;
@@ -1178,15 +1246,11 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
     dim3 grid(nblk(npairs, 64)), blk(64);
     s2 *sc = (s2 *)scratch;
     if (impl_seq == 0) { // SSE non-window
-      if (dec2)
-        hipLaunchKernelGGL(k_sse_halfit<true>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
-      else
-        hipLaunchKernelGGL(k_sse_halfit<false>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+#define SEQ(kern, m) hipLaunchKernelGGL(kern<m>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs)
+      if (mode == 1) SEQ(k_sse_halfit, 1); else if (mode == 2) SEQ(k_sse_halfit, 2); else SEQ(k_sse_halfit, 0);
     } else {
-      if (dec2)
-        hipLaunchKernelGGL(k_gen_halfit<true>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
-      else
-        hipLaunchKernelGGL(k_gen_halfit<false>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs);
+      if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
+#undef SEQ
     }
   }
   return hipGetLastError();
@@ -1198,7 +1262,7 @@ hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, con
                          int max_halfits, uint8_t *pair_done, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, rev, (const s2 *)A,
-                     (const s4 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, poly,
+                     (const s2 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, poly,
                      max_halfits);
   if (crc_bytes && pair_done)
     hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);

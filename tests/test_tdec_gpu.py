@@ -186,3 +186,30 @@ def test_error_behaviour(s, batch):
     assert s._lib.srslte_tdec_run_all_8bit(None, None, None, 1, 40) == -1
     d.free()
     d2.free()
+
+
+@pytest.mark.parametrize("impl,K,sb", [(AUTO, 6144, 0), (AUTO, 6144, 1), (AUTO, 512, 0), (SSE, 1024, 0)])
+def test_device_input_odd_stride(s, oracle, impl, K, sb):
+    """Device inputs at an odd int16 stride and an odd element offset (unaligned dword reads
+    are not allowed: the loader must take its element-wise path) decode like the oracle."""
+    import torch
+    rng = np.random.default_rng(K + sb)
+    n = 5
+    ins = []
+    for i in range(n):
+        _, llr = make_cb(K, float(rng.uniform(1.0, 5.0)), int(rng.integers(1 << 30)), oracle)
+        ins.append(_sb_input(oracle, llr, K, sb) if impl == AUTO else llr)
+    ln = len(ins[0])
+    stride = ln + 3
+    host = np.zeros(1 + n * stride, np.int16)
+    for i, x in enumerate(ins):
+        host[1 + i * stride:1 + i * stride + ln] = x
+    d_in = torch.from_numpy(host).cuda()
+    d_out = torch.zeros((n, K // 8), dtype=torch.uint8, device="cuda")
+    b = s.TdecBatch(n, K, stream=torch.cuda.current_stream().cuda_stream)
+    assert b.run_dev(impl, sb, d_in.data_ptr() + 2, stride, K, n, 3, d_out.data_ptr(), K // 8) == 0
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for i in range(n):
+        assert (out[i] == oracle.tdec_run(impl, sb, ins[i], K, 3)[0][-1]).all(), i
+    b.close()
