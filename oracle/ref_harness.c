@@ -140,3 +140,106 @@ int ref_tdec_decode_cb(int impl, int sb_layout, const int16_t *input, uint32_t K
   srslte_tdec_free(&h);
   return ok;
 }
+
+/* ---------------------------------------------------------------- DL-SCH (sch.c) ---------- */
+#include "srslte/phy/fec/rm_turbo.h"
+#include "srslte/phy/fec/softbuffer.h"
+#include "srslte/phy/phch/pdsch_cfg.h"
+#include "srslte/phy/phch/sch.h"
+
+/* srslte_rm_turbo_rx_lut_ (rm_turbo.c:394-430): out += de-rate-matched in; sb_layout selects the
+ * sub-block table the decoder expects (enable_input_tdec). */
+int ref_rm_turbo_rx(const int16_t *input, int16_t *output, uint32_t in_len, uint32_t K,
+                    uint32_t rv, int sb_layout) {
+  srslte_rm_turbo_gentables();
+  int idx = srslte_cbsegm_cbindex(K);
+  if (idx < 0) return -1;
+  int16_t *in = NULL;
+  if (posix_memalign((void **)&in, 64, (in_len + 32) * sizeof(int16_t))) return -1;
+  memcpy(in, input, in_len * sizeof(int16_t));
+  int r = srslte_rm_turbo_rx_lut_(in, output, in_len, (uint32_t)idx, rv, sb_layout != 0);
+  free(in);
+  return r;
+}
+
+static srslte_sch_t ref_sch;
+static int ref_sch_ready = 0;
+
+static int ref_sch_get(void) {
+  if (!ref_sch_ready) {
+    if (srslte_sch_init(&ref_sch)) return -1;
+    ref_sch_ready = 1;
+  }
+  return 0;
+}
+
+static void ref_cfg(srslte_pdsch_cfg_t *cfg, uint32_t tbs, uint32_t rv, uint32_t Qm,
+                    uint32_t nof_e_bits) {
+  memset(cfg, 0, sizeof(*cfg));
+  srslte_cbsegm(&cfg->cb_segm[0], tbs);
+  cfg->grant.tb_en[0] = true;
+  cfg->grant.Qm[0] = Qm;
+  cfg->nbits[0].nof_bits = nof_e_bits;
+  cfg->rv[0] = rv;
+  cfg->nof_layers = 1;
+}
+
+/* srslte_dlsch_encode2 (sch.c:543-): data (tbs/8 bytes) -> packed e bits (nof_e_bits). */
+int ref_dlsch_encode(uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_e_bits,
+                     const uint8_t *data, uint8_t *e_packed, uint32_t nof_prb) {
+  if (ref_sch_get()) return -1;
+  srslte_pdsch_cfg_t cfg;
+  ref_cfg(&cfg, tbs, rv, Qm, nof_e_bits);
+  srslte_softbuffer_tx_t sb;
+  if (srslte_softbuffer_tx_init(&sb, nof_prb)) return -1;
+  srslte_softbuffer_tx_reset(&sb);
+  uint8_t *d = calloc(tbs / 8 + 16, 1);
+  memcpy(d, data, tbs / 8);
+  /* srslte_rm_turbo_tx_lut fills the circular buffer only at rv 0 (rm_turbo.c:332-343); a
+   * retransmission reuses it, so encode rv 0 first as a HARQ process would */
+  int r = 0;
+  if (rv != 0) {
+    srslte_pdsch_cfg_t cfg0;
+    ref_cfg(&cfg0, tbs, 0, Qm, nof_e_bits);
+    r = srslte_dlsch_encode2(&ref_sch, &cfg0, &sb, d, e_packed, 0);
+  }
+  if (!r) r = srslte_dlsch_encode2(&ref_sch, &cfg, &sb, d, e_packed, 0);
+  free(d);
+  srslte_softbuffer_tx_free(&sb);
+  return r;
+}
+
+/* A persistent rx softbuffer per HARQ slot, as a UE keeps one per process. */
+#define REF_NSLOT 8
+static srslte_softbuffer_rx_t ref_sbrx[REF_NSLOT];
+static int ref_sbrx_ready[REF_NSLOT];
+
+int ref_softbuffer_reset(int slot, uint32_t nof_prb) {
+  if (slot < 0 || slot >= REF_NSLOT) return -1;
+  if (!ref_sbrx_ready[slot]) {
+    if (srslte_softbuffer_rx_init(&ref_sbrx[slot], nof_prb)) return -1;
+    ref_sbrx_ready[slot] = 1;
+  }
+  srslte_softbuffer_rx_reset(&ref_sbrx[slot]);
+  return 0;
+}
+
+/* srslte_dlsch_decode2 (sch.c:500-512 -> decode_tb -> decode_tb_cb): int16 e bits -> data.
+ * Returns the reference's return code; *noi = srslte_sch_last_noi; cb_crc[] copied out. */
+int ref_dlsch_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_e_bits,
+                     const int16_t *e_bits, uint8_t *data, uint32_t max_halfits, uint32_t *noi,
+                     uint8_t *cb_crc) {
+  if (ref_sch_get()) return -100;
+  if (slot < 0 || slot >= REF_NSLOT || !ref_sbrx_ready[slot]) return -100;
+  srslte_pdsch_cfg_t cfg;
+  ref_cfg(&cfg, tbs, rv, Qm, nof_e_bits);
+  srslte_sch_set_max_noi(&ref_sch, max_halfits);
+  int16_t *e = NULL;
+  if (posix_memalign((void **)&e, 64, (nof_e_bits + 64) * sizeof(int16_t))) return -100;
+  memcpy(e, e_bits, nof_e_bits * sizeof(int16_t));
+  int r = srslte_dlsch_decode2(&ref_sch, &cfg, &ref_sbrx[slot], e, data, 0);
+  free(e);
+  *noi = srslte_sch_last_noi(&ref_sch);
+  for (uint32_t i = 0; i < cfg.cb_segm[0].C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
+  return r;
+}

@@ -97,6 +97,79 @@ class Oracle(_Lib):
         return tuple(x.value for x in v)
 
 
+class OrcSoftbuffer(ctypes.Structure):
+    _fields_ = [("max_cb", ctypes.c_uint32), ("buffer", _i16p), ("data", _u8p),
+                ("cb_crc", _u8p), ("tb_crc", ctypes.c_uint8)]
+
+
+SOFTBUFFER_SIZE = 18600
+
+
+class DlschOracle:
+    """Bindings of oracle/dlsch_oracle.c (rate matching, TB encode/decode with softbuffer)."""
+
+    def __init__(self, oracle):
+        L = self.lib = oracle.lib
+        u32 = ctypes.c_uint32
+        L.orc_rm_turbo_rx_table.argtypes = [u32, u32, u32, _u16p]
+        L.orc_rm_turbo_rx.argtypes = [_i16p, _i16p, u32, u32, u32, u32]
+        L.orc_rm_turbo_tx.argtypes = [_u8p, u32, u32, _u8p, u32]
+        L.orc_dlsch_encode.argtypes = [u32, u32, u32, u32, _u8p, _u8p]
+        L.orc_softbuffer_init.argtypes = [ctypes.POINTER(OrcSoftbuffer), u32]
+        L.orc_softbuffer_reset.argtypes = [ctypes.POINTER(OrcSoftbuffer)]
+        L.orc_softbuffer_free.argtypes = [ctypes.POINTER(OrcSoftbuffer)]
+        L.orc_dlsch_decode.argtypes = [ctypes.POINTER(OrcSoftbuffer), u32, u32, u32, u32, _i16p,
+                                       _u8p, u32, _u32p]
+
+    def rx_table(self, K, rv, nsb):
+        t = np.zeros(3 * K + 12, np.uint16)
+        assert self.lib.orc_rm_turbo_rx_table(K, rv, nsb, _ptr(t, _u16p)) == 0
+        return t
+
+    def rm_rx(self, e, out, K, rv, nsb):
+        e = np.ascontiguousarray(e, np.int16)
+        assert self.lib.orc_rm_turbo_rx(_ptr(e, _i16p), _ptr(out, _i16p), e.size, K, rv, nsb) == 0
+        return out
+
+    def rm_tx(self, coded, K, rv, E):
+        coded = np.ascontiguousarray(coded, np.uint8)
+        e = np.zeros(E, np.uint8)
+        assert self.lib.orc_rm_turbo_tx(_ptr(coded, _u8p), K, rv, _ptr(e, _u8p), E) == 0
+        return e
+
+    def encode(self, tbs, rv, Qm, nbits, data):
+        data = np.ascontiguousarray(data, np.uint8)
+        e = np.zeros(nbits, np.uint8)
+        assert self.lib.orc_dlsch_encode(tbs, rv, Qm, nbits, _ptr(data, _u8p), _ptr(e, _u8p)) == 0
+        return e
+
+    def softbuffer(self, max_cb):
+        sb = OrcSoftbuffer()
+        assert self.lib.orc_softbuffer_init(ctypes.byref(sb), max_cb) == 0
+        return sb
+
+    def reset(self, sb):
+        self.lib.orc_softbuffer_reset(ctypes.byref(sb))
+
+    def free(self, sb):
+        self.lib.orc_softbuffer_free(ctypes.byref(sb))
+
+    def decode(self, sb, tbs, rv, Qm, e, max_halfits):
+        e = np.ascontiguousarray(e, np.int16)
+        data = np.zeros(tbs // 8 + 8, np.uint8)
+        noi = ctypes.c_uint32(0)
+        r = self.lib.orc_dlsch_decode(ctypes.byref(sb), tbs, rv, Qm, e.size, _ptr(e, _i16p),
+                                      _ptr(data, _u8p), max_halfits, ctypes.byref(noi))
+        C = self.lib_segm_C(tbs)
+        cb_crc = np.ctypeslib.as_array(sb.cb_crc, shape=(sb.max_cb,))[:C].copy()
+        return r, data, noi.value, cb_crc
+
+    def lib_segm_C(self, tbs):
+        v = [ctypes.c_uint32(0) for _ in range(6)]
+        self.lib.orc_cbsegm(tbs, *[ctypes.byref(x) for x in v])
+        return v[0].value
+
+
 class Ref(_Lib):
     def __init__(self):
         super().__init__(REF_SO, "ref_")
@@ -109,6 +182,46 @@ class Ref(_Lib):
         o = np.zeros(6, np.uint32)
         assert self.lib.ref_cbsegm(tbs, _ptr(o, _u32p)) == 0
         return tuple(int(x) for x in o)
+
+    # ---- DL-SCH (sch.c through ref_harness.c) ----
+    def _dl_sigs(self):
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.ref_rm_turbo_rx.argtypes = [_i16p, _i16p, u32, u32, u32, ctypes.c_int]
+        L.ref_dlsch_encode.argtypes = [u32, u32, u32, u32, _u8p, _u8p, u32]
+        L.ref_softbuffer_reset.argtypes = [ctypes.c_int, u32]
+        L.ref_dlsch_decode.argtypes = [ctypes.c_int, u32, u32, u32, u32, _i16p, _u8p, u32, _u32p,
+                                       _u8p]
+
+    def rm_rx(self, e, out, K, rv, sb):
+        self._dl_sigs()
+        e = np.ascontiguousarray(e, np.int16)
+        assert self.lib.ref_rm_turbo_rx(_ptr(e, _i16p), _ptr(out, _i16p), e.size, K, rv, sb) == 0
+        return out
+
+    def encode(self, tbs, rv, Qm, nbits, data, nof_prb=100):
+        """-> unpacked e bits (the reference packs them, sch.c:281)"""
+        self._dl_sigs()
+        data = np.ascontiguousarray(data, np.uint8)
+        e = np.zeros((nbits + 7) // 8 + 8, np.uint8)
+        assert self.lib.ref_dlsch_encode(tbs, rv, Qm, nbits, _ptr(data, _u8p), _ptr(e, _u8p),
+                                         nof_prb) == 0
+        return np.unpackbits(e)[:nbits]
+
+    def sb_reset(self, slot, nof_prb=100):
+        self._dl_sigs()
+        assert self.lib.ref_softbuffer_reset(slot, nof_prb) == 0
+
+    def decode(self, slot, tbs, rv, Qm, e, max_halfits):
+        self._dl_sigs()
+        e = np.ascontiguousarray(e, np.int16)
+        data = np.zeros(tbs // 8 + 8, np.uint8)
+        noi = ctypes.c_uint32(0)
+        crc = np.zeros(64, np.uint8)
+        r = self.lib.ref_dlsch_decode(slot, tbs, rv, Qm, e.size, _ptr(e, _i16p), _ptr(data, _u8p),
+                                      max_halfits, ctypes.byref(noi), _ptr(crc, _u8p))
+        C = self.cbsegm(tbs)[0]
+        return r, data, noi.value, crc[:C]
 
 
 def have_ref():
