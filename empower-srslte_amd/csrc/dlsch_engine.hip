@@ -1,0 +1,469 @@
+// Host side of the MI355X DL-SCH transport-block decoder (include/srsgpu/dlsch_batch.h).
+//
+// One call = many transport blocks:
+//   host      code block segmentation and the per-CB receive parameters of decode_tb_cb
+//             (sch.c:325-341), grouping of the CBs by (K, CRC) for the turbo decoder
+//   k_derm    de-rate-matching + HARQ combining of every CB into its softbuffer row
+//   decoder   per (K, CRC) group: TdecEngine::decode on the softbuffer rows themselves (row
+//             pointer table, SB layout), CRC early stop per half-iteration, CBs that passed in an
+//             earlier transmission start out "done"
+//   k_tb_finish  TB bytes, cb_crc / saved bytes, nof_iterations, TB CRC
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string.h>
+#include <tuple>
+#include <vector>
+
+#include "dlsch_kernels.h"
+#include "srsgpu/dlsch_batch.h"
+#include "tdec_engine.h"
+
+namespace srsgpu {
+
+// ------------------------------------------------------------------ segmentation ----
+struct Segm {
+  uint32_t tbs = 0, C = 0, C1 = 0, K1 = 0, C2 = 0, K2 = 0, F = 0;
+};
+
+// srslte_cbsegm (cbsegm.c:58-112): C = ceil(B / 6120) (B > 6144), K1 = smallest table size
+// >= ceil(B'/C), K2 = the next smaller one, C2 = (C*K1 - B') / (K1 - K2)
+static int segm(uint32_t tbs, Segm &s) {
+  s = Segm();
+  s.tbs = tbs;
+  if (tbs == 0) return 0;
+  const uint32_t B = tbs + 24;
+  uint32_t Bp;
+  if (B <= 6144) {
+    s.C = 1;
+    Bp = B;
+  } else {
+    s.C = (B + 6119) / 6120;
+    Bp = B + 24 * s.C;
+  }
+  const uint32_t target = (Bp - 1) / s.C + 1;
+  int idx = -1;
+  for (int i = 0; i < SRSGPU_NOF_CB_SIZES; i++)
+    if (srsgpu_qpp_table[i][0] >= target) {
+      idx = i;
+      break;
+    }
+  if (idx < 0) return -1;
+  s.K1 = srsgpu_qpp_table[idx][0];
+  if (s.C == 1) {
+    s.K2 = 0;
+    s.C2 = 0;
+    s.C1 = 1;
+  } else {
+    s.K2 = idx > 0 ? srsgpu_qpp_table[idx - 1][0] : s.K1;
+    s.C2 = s.K1 > s.K2 ? (s.C * s.K1 - Bp) / (s.K1 - s.K2) : 0;
+    s.C1 = s.C - s.C2;
+  }
+  s.F = s.C1 * s.K1 + s.C2 * s.K2 - Bp;
+  return 0;
+}
+
+// ------------------------------------------------------------------ rate-matching table ----
+// Receive table of 36.212 5.1.4.1 for (K, rv): entry m = decoder-input index of the m-th
+// non-<NULL> bit of the circular buffer read from k0 (rm_turbo.c:163-228). Built forward: the
+// buffer holds v0 (systematic), then v1/v2 interleaved, each the column-permuted R x 32 matrix
+// with ND leading dummies; v2 uses pi(k) = (P[k/R] + 32(k%R) + 1) mod Kp. Decoder index of
+// stream s, position k: 3k+s (natural) or, for the windowed decoders, the sub-block layout
+// s*(K+32) + (k % (K/nsb))*nsb + k/(K/nsb), tails at 3*(K+32) (rm_turbo.c:231-257).
+static const uint8_t RM_PERM[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30,
+                                    1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31};
+
+static void rm_rx_table(uint32_t K, uint32_t rv, uint32_t nsb, std::vector<uint16_t> &t) {
+  const uint32_t D = K + 4, R = (D + 31) / 32, Kp = 32 * R, ND = Kp - D, Ncb = 3 * Kp;
+  auto dec_index = [&](uint32_t d) -> uint32_t { // d = 3k + s, natural index
+    if (!nsb) return d;
+    if (d >= 3 * K) return d - 3 * K + 3 * (K + 32);
+    const uint32_t k = d / 3, s = d % 3, L = K / nsb;
+    return s * (K + 32) + (k % L) * nsb + k / L;
+  };
+  auto entry = [&](uint32_t w) -> int64_t { // circular-buffer position -> d or -1 (<NULL>)
+    if (w < Kp) {
+      const uint32_t y = (w % R) * 32 + RM_PERM[w / R];
+      return y < ND ? -1 : (int64_t)(3 * (y - ND));
+    }
+    const uint32_t k = (w - Kp) / 2;
+    if (((w - Kp) & 1) == 0) {
+      const uint32_t y = (k % R) * 32 + RM_PERM[k / R];
+      return y < ND ? -1 : (int64_t)(3 * (y - ND) + 1);
+    }
+    const uint32_t p = (RM_PERM[k / R] + 32 * (k % R) + 1) % Kp;
+    return p < ND ? -1 : (int64_t)(3 * (p - ND) + 2);
+  };
+  const uint32_t N = 3 * K + 12, k0 = R * (24 * rv + 2);
+  t.resize(N);
+  uint32_t m = 0;
+  for (uint32_t j = 0; m < N; j++) {
+    const int64_t v = entry((k0 + j) % Ncb);
+    if (v >= 0) t[m++] = (uint16_t)dec_index((uint32_t)v);
+  }
+}
+
+// ------------------------------------------------------------------ engine ----
+struct DlschEngine {
+  hipStream_t st = nullptr;
+  uint32_t nslots = 0, max_cb = 0, cap = 0;
+  int16_t *soft = nullptr;   // [nslots * max_cb][SOFTBUFFER_SIZE]
+  uint8_t *saved = nullptr;  // [nslots * max_cb][768]
+  uint8_t *cbcrc = nullptr;  // [nslots * max_cb]
+  // per-call device arrays (capacity cap CBs / cap TBs)
+  DermItem *d_items = nullptr;
+  TbItem *d_tbs = nullptr;
+  const int16_t **d_rows = nullptr;
+  uint32_t *d_cbmap = nullptr;
+  uint8_t *d_init = nullptr, *d_dec = nullptr, *d_ok = nullptr;
+  uint32_t *d_noi = nullptr;
+  int32_t *d_ret_stage = nullptr;
+  uint32_t *d_noi_stage = nullptr;
+  // pinned staging for the per-call descriptors, reused once the previous copies completed
+  DermItem *h_items = nullptr;
+  TbItem *h_tbs = nullptr;
+  const int16_t **h_rows = nullptr;
+  uint32_t *h_cbmap = nullptr;
+  hipEvent_t staged = nullptr;
+  bool staged_pending = false;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables;
+  TdecEngine tdec;
+  // host-pointer API staging
+  int16_t *e_stage = nullptr;
+  uint8_t *data_stage = nullptr;
+  size_t e_stage_len = 0, data_stage_len = 0;
+
+  int create(uint32_t slots, uint32_t mcb, uint32_t cap_cbs) {
+    if (!slots || !mcb || !cap_cbs) return -1;
+    nslots = slots;
+    max_cb = mcb;
+    cap = cap_cbs;
+    const size_t rows = (size_t)slots * mcb;
+    HIPCHK(hipMalloc(&soft, rows * SRSGPU_SOFTBUFFER_SIZE * 2));
+    HIPCHK(hipMemset(soft, 0, rows * SRSGPU_SOFTBUFFER_SIZE * 2));
+    HIPCHK(hipMalloc(&saved, rows * 768));
+    HIPCHK(hipMemset(saved, 0, rows * 768));
+    HIPCHK(hipMalloc(&cbcrc, rows));
+    HIPCHK(hipMemset(cbcrc, 0, rows));
+    HIPCHK(hipMalloc(&d_items, sizeof(DermItem) * cap));
+    HIPCHK(hipMalloc(&d_tbs, sizeof(TbItem) * cap));
+    HIPCHK(hipMalloc(&d_rows, sizeof(int16_t *) * cap));
+    HIPCHK(hipMalloc(&d_cbmap, sizeof(uint32_t) * cap));
+    HIPCHK(hipMalloc(&d_init, cap));
+    HIPCHK(hipMalloc(&d_dec, (size_t)cap * 768));
+    HIPCHK(hipMalloc(&d_ok, cap));
+    HIPCHK(hipMalloc(&d_noi, sizeof(uint32_t) * cap));
+    HIPCHK(hipMalloc(&d_ret_stage, sizeof(int32_t) * cap));
+    HIPCHK(hipMalloc(&d_noi_stage, sizeof(uint32_t) * cap));
+    HIPCHK(hipHostMalloc(&h_items, sizeof(DermItem) * cap));
+    HIPCHK(hipHostMalloc(&h_tbs, sizeof(TbItem) * cap));
+    HIPCHK(hipHostMalloc(&h_rows, sizeof(int16_t *) * cap));
+    HIPCHK(hipHostMalloc(&h_cbmap, sizeof(uint32_t) * cap));
+    HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
+    return tdec.create(cap, 6144);
+  }
+
+  void destroy() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)d_items, (void *)d_tbs,
+                    (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
+                    (void *)d_noi, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
+                    (void *)data_stage})
+      if (p) (void)hipFree(p);
+    for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap})
+      if (p) (void)hipHostFree(p);
+    for (auto &kv : tables) (void)hipFree(kv.second);
+    tables.clear();
+    if (staged) (void)hipEventDestroy(staged);
+    tdec.destroy();
+  }
+
+  const uint16_t *table(uint32_t K, uint32_t rv, uint32_t nsb) {
+    auto key = std::make_tuple(K, rv, nsb);
+    auto it = tables.find(key);
+    if (it != tables.end()) return it->second;
+    std::vector<uint16_t> t;
+    rm_rx_table(K, rv, nsb, t);
+    uint16_t *d = nullptr;
+    if (hipMalloc(&d, t.size() * 2) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    tables.emplace(key, d);
+    return d;
+  }
+
+  int16_t *row(uint32_t slot, uint32_t cb) {
+    return soft + ((size_t)slot * max_cb + cb) * SRSGPU_SOFTBUFFER_SIZE;
+  }
+
+  int reset(uint32_t slot, uint32_t ncb) {
+    if (slot >= nslots) return -1;
+    ncb = std::min(ncb, max_cb);
+    HIPCHK(hipMemsetAsync(row(slot, 0), 0, (size_t)ncb * SRSGPU_SOFTBUFFER_SIZE * 2, st));
+    HIPCHK(hipMemsetAsync(cbcrc + (size_t)slot * max_cb, 0, max_cb, st));
+    return 0;
+  }
+
+  int decode(const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const int16_t *const *e_ptr,
+             uint8_t *const *data_ptr, uint32_t maxh, int32_t *d_ret, uint32_t *d_noi_out) {
+    if (ntb > cap) {
+      fprintf(stderr, "srsgpu: %u transport blocks exceed the capacity %u\n", ntb, cap);
+      return -1;
+    }
+    if (maxh == 0) {
+      fprintf(stderr, "srsgpu: max_halfits must be > 0\n");
+      return -1;
+    }
+    tdec.st = st;
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    // ---- host: segmentation, CB list in TB order, groups by (K, CRC) ----
+    struct Cb {
+      uint32_t K, poly, crclen, u;
+    };
+    std::vector<Cb> cbs;
+    uint32_t ncb = 0, max_n = 0;
+    for (uint32_t b = 0; b < ntb; b++) {
+      const srsgpu_dlsch_tb_t &t = tb[b];
+      TbItem &ti = h_tbs[b];
+      memset(&ti, 0, sizeof(ti));
+      ti.data = data_ptr[b];
+      ti.ret = d_ret + b;
+      ti.noi = d_noi_out + b;
+      Segm s;
+      if (t.softbuffer >= nslots || t.rv > 3 || t.Qm == 0 || segm(t.tbs, s)) {
+        fprintf(stderr, "srsgpu: invalid transport block %u (tbs=%u rv=%u Qm=%u softbuffer=%u)\n", b,
+                t.tbs, t.rv, t.Qm, t.softbuffer);
+        return -1;
+      }
+      if (s.tbs == 0 || s.C == 0) { // sch.c:451-453
+        ti.preset_ret = 0;
+        continue;
+      }
+      if (s.F || s.C > max_cb) { // sch.c:455-463
+        fprintf(stderr, s.F ? "Error filler bits are not supported. Use standard TBS\n"
+                            : "Error number of CB (%d) exceeds soft buffer size (%d CBs)\n",
+                s.C, max_cb);
+        ti.preset_ret = -2;
+        continue;
+      }
+      if (ncb + s.C > cap) {
+        fprintf(stderr, "srsgpu: code blocks of this call exceed the capacity %u\n", cap);
+        return -1;
+      }
+      ti.tbs = s.tbs;
+      ti.C = s.C;
+      ti.C1 = s.C1;
+      ti.K1 = s.K1;
+      ti.K2 = s.K2;
+      ti.first = ncb;
+      ti.cb_crc = cbcrc + (size_t)t.softbuffer * max_cb;
+      ti.saved = saved + (size_t)t.softbuffer * max_cb * 768;
+      const uint32_t Gp = t.nof_e_bits / t.Qm;
+      const uint32_t gamma = Gp % s.C;
+      const uint32_t n_e = t.Qm * (Gp / s.C);
+      for (uint32_t i = 0; i < s.C; i++, ncb++) {
+        const uint32_t K = i < s.C1 ? s.K1 : s.K2;
+        uint32_t rp = i * n_e, ne = n_e;
+        if (i > s.C - gamma) { // sch.c:339-342
+          ne = n_e + t.Qm;
+          rp = (s.C - gamma) * n_e + (i - (s.C - gamma)) * ne;
+        }
+        const uint32_t nsb = auto_subblocks(K);
+        const uint16_t *tab = table(K, t.rv, nsb);
+        if (!tab) return -1;
+        DermItem &it = h_items[ncb];
+        it.e = e_ptr[b] + rp;
+        it.ne = ne;
+        it.N = 3 * K + 12;
+        it.table = tab;
+        it.row = row(t.softbuffer, i);
+        it.cb_crc = ti.cb_crc + i;
+        max_n = std::max(max_n, std::min(ne, it.N));
+        cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
+      }
+    }
+    std::vector<uint32_t> order(cbs.size());
+    for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      return std::tie(cbs[a].K, cbs[a].poly, cbs[a].crclen) <
+             std::tie(cbs[b].K, cbs[b].poly, cbs[b].crclen);
+    });
+    for (uint32_t p = 0; p < order.size(); p++) {
+      const uint32_t u = cbs[order[p]].u;
+      h_cbmap[u] = p;
+      h_items[u].pos = p;
+      h_rows[p] = h_items[u].row;
+    }
+    // ---- device ----
+    if (ncb) {
+      HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(DermItem) * ncb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(d_rows, h_rows, sizeof(int16_t *) * ncb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(d_cbmap, h_cbmap, sizeof(uint32_t) * ncb, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipMemcpyAsync(d_tbs, h_tbs, sizeof(TbItem) * ntb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    {
+      ProfScope ps("k_derm", st);
+      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st));
+    }
+    for (uint32_t p0 = 0; p0 < order.size();) {
+      const Cb &c = cbs[order[p0]];
+      uint32_t p1 = p0 + 1;
+      while (p1 < order.size() && cbs[order[p1]].K == c.K && cbs[order[p1]].poly == c.poly &&
+             cbs[order[p1]].crclen == c.crclen)
+        p1++;
+      if (tdec.decode(SRSLTE_TDEC_AUTO, 1, nullptr, 0, c.K, p1 - p0, maxh, c.poly, c.crclen,
+                      d_dec + (size_t)p0 * 768, 768, d_ok + p0, d_noi + p0,
+                      (const int16_t *const *)(d_rows + p0), 1, d_init + p0))
+        return -1;
+      p0 = p1;
+    }
+    {
+      ProfScope ps("k_tb_finish", st);
+      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, st));
+    }
+    return 0;
+  }
+};
+
+} // namespace srsgpu
+
+using srsgpu::DlschEngine;
+
+struct srsgpu_dlsch {
+  DlschEngine e;
+};
+
+extern "C" {
+
+int srsgpu_dlsch_create(srsgpu_dlsch_t **q, uint32_t nslots, uint32_t max_cb, uint32_t cap) {
+  if (!q) return -1;
+  auto *d = new srsgpu_dlsch();
+  if (d->e.create(nslots, max_cb, cap)) {
+    d->e.destroy();
+    delete d;
+    *q = nullptr;
+    return -1;
+  }
+  *q = d;
+  return 0;
+}
+
+void srsgpu_dlsch_destroy(srsgpu_dlsch_t *q) {
+  if (!q) return;
+  q->e.destroy();
+  delete q;
+}
+
+void srsgpu_dlsch_set_stream(srsgpu_dlsch_t *q, void *s) {
+  if (q) q->e.st = (hipStream_t)s;
+}
+
+int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t slot) {
+  return q ? q->e.reset(slot, q->e.max_cb) : -1;
+}
+
+int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t slot, uint32_t tbs) {
+  return q ? q->e.reset(slot, (tbs + 24) / 6120 + 1) : -1; // softbuffer.c:113-116
+}
+
+int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,
+                            const int16_t *d_e, uint8_t *d_data, uint32_t maxh, int32_t *d_ret,
+                            uint32_t *d_noi) {
+  if (!q || (!tb && ntb) || !d_e || !d_data || !d_ret || !d_noi) return -1;
+  if (ntb == 0) return 0;
+  std::vector<const int16_t *> e(ntb);
+  std::vector<uint8_t *> d(ntb);
+  for (uint32_t i = 0; i < ntb; i++) {
+    e[i] = d_e + tb[i].e_offset;
+    d[i] = d_data + tb[i].data_offset;
+  }
+  return q->e.decode(tb, ntb, e.data(), d.data(), maxh, d_ret, d_noi);
+}
+
+int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,
+                        const int16_t *const *e_bits, uint8_t *const *data, uint32_t maxh,
+                        int32_t *ret, uint32_t *noi) {
+  if (!q || (!tb && ntb) || !e_bits || !data || !ret || !noi) return -1;
+  if (ntb == 0) return 0;
+  DlschEngine &E = q->e;
+  if (ntb > E.cap) return -1;
+  size_t elen = 0, dlen = 0;
+  for (uint32_t i = 0; i < ntb; i++) {
+    elen += tb[i].nof_e_bits;
+    dlen += SRSGPU_DLSCH_DATA_LEN(tb[i].tbs);
+  }
+  if (elen > E.e_stage_len) {
+    if (E.e_stage) (void)hipFree(E.e_stage);
+    E.e_stage = nullptr;
+    HIPCHK(hipMalloc(&E.e_stage, elen * 2 + 64));
+    E.e_stage_len = elen;
+  }
+  if (dlen > E.data_stage_len) {
+    if (E.data_stage) (void)hipFree(E.data_stage);
+    E.data_stage = nullptr;
+    HIPCHK(hipMalloc(&E.data_stage, dlen + 64));
+    E.data_stage_len = dlen;
+  }
+  std::vector<srsgpu_dlsch_tb_t> t(tb, tb + ntb);
+  size_t eo = 0, dof = 0;
+  for (uint32_t i = 0; i < ntb; i++) {
+    t[i].e_offset = eo;
+    t[i].data_offset = dof;
+    if (tb[i].nof_e_bits)
+      HIPCHK(hipMemcpyAsync(E.e_stage + eo, e_bits[i], (size_t)tb[i].nof_e_bits * 2,
+                            hipMemcpyHostToDevice, E.st));
+    eo += tb[i].nof_e_bits;
+    dof += SRSGPU_DLSCH_DATA_LEN(tb[i].tbs);
+  }
+  HIPCHK(hipMemsetAsync(E.data_stage, 0, dlen, E.st));
+  if (srsgpu_dlsch_decode_dev(q, t.data(), ntb, E.e_stage, E.data_stage, maxh, E.d_ret_stage,
+                              E.d_noi_stage))
+    return -1;
+  for (uint32_t i = 0; i < ntb; i++)
+    HIPCHK(hipMemcpyAsync(data[i], E.data_stage + t[i].data_offset, SRSGPU_DLSCH_DATA_LEN(tb[i].tbs),
+                          hipMemcpyDeviceToHost, E.st));
+  HIPCHK(hipMemcpyAsync(ret, E.d_ret_stage, sizeof(int32_t) * ntb, hipMemcpyDeviceToHost, E.st));
+  HIPCHK(hipMemcpyAsync(noi, E.d_noi_stage, sizeof(uint32_t) * ntb, hipMemcpyDeviceToHost, E.st));
+  HIPCHK(hipStreamSynchronize(E.st));
+  return 0;
+}
+
+int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t slot, int16_t *rows, uint8_t *cb_crc) {
+  if (!q || slot >= q->e.nslots) return -1;
+  DlschEngine &E = q->e;
+  if (rows)
+    HIPCHK(hipMemcpyAsync(rows, E.row(slot, 0), (size_t)E.max_cb * SRSGPU_SOFTBUFFER_SIZE * 2,
+                          hipMemcpyDeviceToHost, E.st));
+  if (cb_crc)
+    HIPCHK(hipMemcpyAsync(cb_crc, E.cbcrc + (size_t)slot * E.max_cb, E.max_cb, hipMemcpyDeviceToHost,
+                          E.st));
+  HIPCHK(hipStreamSynchronize(E.st));
+  return 0;
+}
+
+int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
+                           uint32_t K, uint32_t rv, int sb_layout) {
+  if (!q || !d_in || !d_out || rv > 3 || srsgpu::cb_index(K) < 0) return -1;
+  DlschEngine &E = q->e;
+  if (E.staged_pending) HIPCHK(hipEventSynchronize(E.staged));
+  const uint16_t *tab = E.table(K, rv, sb_layout ? srsgpu::auto_subblocks(K) : 0);
+  if (!tab) return -1;
+  srsgpu::DermItem &it = E.h_items[0];
+  it.e = d_in;
+  it.ne = in_len;
+  it.N = 3 * K + 12;
+  it.table = tab;
+  it.row = d_out;
+  it.cb_crc = nullptr;
+  it.pos = 0;
+  HIPCHK(hipMemcpyAsync(E.d_items, E.h_items, sizeof(srsgpu::DermItem), hipMemcpyHostToDevice, E.st));
+  HIPCHK(hipEventRecord(E.staged, E.st));
+  E.staged_pending = true;
+  HIPCHK(srsgpu::launch_derm(E.d_items, 1, std::min(in_len, 3 * K + 12), E.d_init, E.st));
+  return 0;
+}
+
+} // extern "C"

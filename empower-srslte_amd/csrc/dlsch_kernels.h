@@ -1,0 +1,40 @@
+// Internal launch interface of the DL-SCH kernels (dlsch_kernels.hip).
+#ifndef SRSGPU_DLSCH_KERNELS_H
+#define SRSGPU_DLSCH_KERNELS_H
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace srsgpu {
+
+// one code block to de-rate-match into its softbuffer row
+struct DermItem {
+  const int16_t *e;       // its E received LLRs (sch.c:330-341 rp / n_e2)
+  uint32_t ne;            // E
+  uint32_t N;             // 3K + 12 (table length)
+  const uint16_t *table;  // receive table for (K, rv), decoder layout
+  int16_t *row;           // softbuffer row (SOFTBUFFER_SIZE int16)
+  const uint8_t *cb_crc;  // softbuffer cb_crc[i]: already decoded -> skipped
+  uint32_t pos;           // position in the decoder's (K-grouped) CB order
+};
+
+// one transport block's epilogue
+struct TbItem {
+  uint8_t *data;      // output bytes
+  uint8_t *cb_crc;    // softbuffer cb_crc[0..C)
+  uint8_t *saved;     // softbuffer saved bytes [C][768]
+  int32_t *ret;       // SRSLTE_SUCCESS / SRSLTE_ERROR
+  uint32_t *noi;      // nof_iterations (sum over decoded CBs / C)
+  uint32_t tbs, C, C1, K1, K2;
+  uint32_t first;     // index of CB 0 in the call's CB list
+  int32_t preset_ret; // result when C == 0 (tbs == 0 or invalid inputs)
+};
+
+hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
+                       hipStream_t st);
+// dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
+hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
+                            size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
+                            const uint32_t *noi, hipStream_t st);
+} // namespace srsgpu
+#endif

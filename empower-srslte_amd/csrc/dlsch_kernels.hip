@@ -1,0 +1,154 @@
+// MI355X DL-SCH kernels around the turbo decoder (paths relative to /root/reference/lib):
+//   k_derm        srslte_rm_turbo_rx_lut (src/phy/fec/rm_turbo.c:394-430): soft-combine a code
+//                 block's E received LLRs into its HARQ softbuffer row, out[t[i % N]] += in[i]
+//                 (int16 wrap). Written as a gather over the N = 3K+12 table entries: entry m
+//                 sums in[m], in[m+N], ... (repetition) and adds once, so every row element is
+//                 owned by one thread (the table is a bijection) and no atomics are needed.
+//   k_tb_finish   decode_tb / decode_tb_cb epilogue (src/phy/phch/sch.c:393-491): TB bytes from
+//                 the per-CB decisions (or from the softbuffer's saved bytes for CBs that passed
+//                 in an earlier transmission), cb_crc / saved-data update, nof_iterations and
+//                 the TB CRC24A check.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dlsch_kernels.h"
+
+namespace srsgpu {
+
+__global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
+                                              uint8_t *__restrict__ init_done) {
+  const int g = blockIdx.y;
+  if (g >= nitems) return;
+  const DermItem it = items[g];
+  const uint8_t skip = it.cb_crc ? *it.cb_crc : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) init_done[it.pos] = skip;
+  if (skip) return; // sch.c:323: blocks whose CRC passed before are not combined again
+  const uint32_t N = it.N;
+  const uint32_t lim = it.ne < N ? it.ne : N;
+  for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < lim; m += gridDim.x * 256) {
+    uint32_t acc = 0;
+    for (uint32_t i = m; i < it.ne; i += N) acc += (uint16_t)it.e[i];
+    const uint32_t o = it.table[m];
+    it.row[o] = (int16_t)(uint16_t)((uint16_t)it.row[o] + acc);
+  }
+}
+
+// MSB-first CRC24 byte table (crc.c:43-62 gen_crc_table for order 24)
+__device__ static void crc24_table(uint32_t *table, uint32_t poly) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    uint32_t crc = (uint32_t)i << 16;
+    for (int j = 0; j < 8; j++) {
+      const uint32_t bit = crc & 0x800000u;
+      crc <<= 1;
+      if (bit) crc ^= poly;
+    }
+    table[i] = crc & 0xFFFFFFu;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tbs_, int ntb,
+                                                   const uint32_t *__restrict__ cbmap,
+                                                   const uint8_t *__restrict__ dec, size_t dec_stride,
+                                                   const uint8_t *__restrict__ cb_ok_in,
+                                                   const uint8_t *__restrict__ init_done,
+                                                   const uint32_t *__restrict__ noi_in) {
+  __shared__ uint32_t table[256];
+  __shared__ int all_ok;
+  __shared__ uint32_t noi_sum;
+  const int b = blockIdx.x;
+  if (b >= ntb) return;
+  const TbItem t = tbs_[b];
+  if (t.C == 0) { // tbs == 0 (sch.c:451-453) or invalid inputs: result set on the host
+    if (threadIdx.x == 0) {
+      *t.ret = t.preset_ret;
+      *t.noi = 0;
+    }
+    return;
+  }
+  crc24_table(table, 0x1864CFBu);
+  if (threadIdx.x == 0) {
+    all_ok = 1;
+    noi_sum = 0;
+  }
+  __syncthreads();
+  // 1. TB bytes: CB i owns [i*rlen/8, (i+1)*rlen/8); the last CB also writes its 3 CRC bytes,
+  //    as its full K/8-byte decision lands last in the reference (sch.c:363-366)
+  for (uint32_t i = 0; i < t.C; i++) {
+    const uint32_t K = i < t.C1 ? t.K1 : t.K2;
+    const uint32_t rlen = t.C == 1 ? K : K - 24;
+    const uint32_t g = cbmap[t.first + i];
+    uint8_t *dst = t.data + (size_t)i * (rlen / 8);
+    if (init_done[g]) {
+      const uint8_t *src = t.saved + (size_t)i * 768;
+      for (uint32_t j = threadIdx.x; j < rlen / 8; j += blockDim.x) dst[j] = src[j];
+    } else {
+      const uint32_t nb = (i == t.C - 1) ? K / 8 : rlen / 8;
+      const uint8_t *src = dec + (size_t)g * dec_stride;
+      for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) dst[j] = src[j];
+    }
+  }
+  __syncthreads();
+  // 2. cb_crc flags, tb_crc, nof_iterations (sch.c:394-419)
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    int ok = 1;
+    for (uint32_t i = 0; i < t.C; i++) {
+      const uint32_t g = cbmap[t.first + i];
+      if (!init_done[g]) {
+        s += noi_in[g];
+        if (cb_ok_in[g]) t.cb_crc[i] = 1;
+      }
+      ok = ok && t.cb_crc[i];
+    }
+    all_ok = ok;
+    noi_sum = s;
+  }
+  __syncthreads();
+  if (!all_ok) {
+    // keep the bytes of the blocks that passed for the retransmission (sch.c:407-416)
+    for (uint32_t i = 0; i < t.C; i++) {
+      if (!t.cb_crc[i]) continue;
+      const uint32_t K = i < t.C1 ? t.K1 : t.K2;
+      const uint32_t rlen = t.C == 1 ? K : K - 24;
+      const uint8_t *src = t.data + (size_t)i * (rlen / 8);
+      uint8_t *dst = t.saved + (size_t)i * 768;
+      for (uint32_t j = threadIdx.x; j < rlen / 8; j += blockDim.x) dst[j] = src[j];
+    }
+  }
+  if (threadIdx.x == 0) {
+    *t.noi = noi_sum / t.C;
+    int ret = -1;
+    if (all_ok) { // TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491)
+      uint32_t crc = 0;
+      const uint32_t nbytes = t.tbs / 8;
+      for (uint32_t i = 0; i < nbytes; i++)
+        crc = ((crc << 8) ^ table[((crc >> 16) & 0xff) ^ t.data[i]]) & 0xFFFFFFu;
+      const uint32_t tx = ((uint32_t)t.data[nbytes] << 16) | ((uint32_t)t.data[nbytes + 1] << 8) |
+                          t.data[nbytes + 2];
+      ret = (crc == tx && crc) ? 0 : -1;
+    }
+    *t.ret = ret;
+  }
+}
+
+static inline unsigned cdiv(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
+                       hipStream_t st) {
+  if (nitems <= 0) return hipSuccess;
+  const unsigned gx = cdiv(max_n, 256) < 32 ? cdiv(max_n, 256) : 32;
+  hipLaunchKernelGGL(k_derm, dim3(gx ? gx : 1, (unsigned)nitems), dim3(256), 0, st, d_items, nitems,
+                     init_done);
+  return hipGetLastError();
+}
+
+hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
+                            size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
+                            const uint32_t *noi, hipStream_t st) {
+  if (ntb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
+                     dec_stride, cb_ok, init_done, noi);
+  return hipGetLastError();
+}
+
+} // namespace srsgpu

@@ -21,19 +21,9 @@
 #include "srsgpu/qpp_table.h"
 #include "srsgpu/tdec_batch.h"
 #include "srslte/phy/fec/turbodecoder.h"
-#include "tdec_kernels.h"
+#include "tdec_engine.h"
 
-#define HIPCHK(x)                                                                                 \
-  do {                                                                                            \
-    hipError_t e_ = (x);                                                                          \
-    if (e_ != hipSuccess) {                                                                       \
-      fprintf(stderr, "srsgpu: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__,      \
-              __LINE__);                                                                          \
-      return -1;                                                                                  \
-    }                                                                                             \
-  } while (0)
-
-namespace {
+namespace srsgpu {
 
 // ------------------------------------------------------------------ profiling ----
 struct ProfRec {
@@ -60,24 +50,11 @@ struct Prof {
   }
 } g_prof;
 
-struct ProfScope {
-  hipEvent_t a = nullptr, b = nullptr;
-  const char *name;
-  hipStream_t st;
-  ProfScope(const char *n, hipStream_t s) : name(n), st(s) {
-    if (g_prof.on) {
-      if (hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
-        (void)hipEventRecord(a, st);
-    }
-  }
-  ~ProfScope() {
-    if (a && b) {
-      (void)hipEventRecord(b, st);
-      std::lock_guard<std::mutex> g(g_prof.mu);
-      g_prof.pending.push_back({name, a, b});
-    }
-  }
-};
+bool prof_on() { return g_prof.on; }
+void prof_push(const char *name, hipEvent_t a, hipEvent_t b) {
+  std::lock_guard<std::mutex> g(g_prof.mu);
+  g_prof.pending.push_back({name, a, b});
+}
 
 // ------------------------------------------------------------------ tables ----
 int cb_index(uint32_t K) {
@@ -121,187 +98,15 @@ void gen_interleaver(uint32_t K, uint32_t nb, std::vector<uint16_t> &fwd, std::v
   }
 }
 
-// ------------------------------------------------------------------ engine ----
-struct Engine {
-  hipStream_t st = nullptr;
-  uint32_t cap_cbs = 0, cap_K = 0;
-  size_t cap_pairs = 0;
-  // pair-interleaved arrays [pairs][K]: SP0 short4; XP1 = X2, P1 short2 planes; A short2;
-  // T short2 [pairs][12]
-  void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr;
-  void *scratch = nullptr; // checkpoints (windowed) / alpha-beta (sequential)
-  size_t scratch_bytes = 0;
-  uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
-  uint32_t *noi = nullptr;
-  int16_t *in_stage = nullptr; // host-pointer API staging
-  uint8_t *out_stage = nullptr;
-  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint16_t *, uint16_t *>> interl;
-  // current job
-  uint32_t K = 0;
-  int impl_r = 0, nb = 1, ncb = 0, npairs = 0;
-  const uint16_t *fwd = nullptr, *rev = nullptr;
+} // namespace srsgpu
 
-  int create(uint32_t max_cbs, uint32_t max_K) {
-    if (max_cbs == 0 || max_K == 0 || max_K > SRSLTE_TCOD_MAX_LEN_CB) {
-      fprintf(stderr, "srsgpu: invalid batch capacity %u x %u\n", max_cbs, max_K);
-      return -1;
-    }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
-      fprintf(stderr, "srsgpu: no HIP device available\n");
-      return -1;
-    }
-    cap_cbs = max_cbs;
-    cap_K = max_K;
-    cap_pairs = (max_cbs + 1) / 2;
-    const size_t arr = cap_pairs * max_K * 4;
-    HIPCHK(hipMalloc(&SP0, arr * 2));
-    HIPCHK(hipMalloc(&XP1, arr * 2));
-    HIPCHK(hipMalloc(&A, arr));
-    HIPCHK(hipMalloc(&T, cap_pairs * 12 * 4));
-    size_t ck = 0;
-    for (int nbv : {8, 16}) {
-      if (max_K / nbv > 40) ck = std::max(ck, srsgpu::win_ck_bytes((int)max_K, nbv, (int)cap_pairs));
-    }
-    scratch_bytes = std::max(ck, srsgpu::seq_scratch_bytes((int)max_K, (int)cap_pairs));
-    HIPCHK(hipMalloc(&scratch, scratch_bytes));
-    HIPCHK(hipMalloc(&cb_done, cap_pairs * 2));
-    HIPCHK(hipMalloc(&cb_ok, cap_pairs * 2));
-    HIPCHK(hipMalloc(&pair_done, cap_pairs));
-    HIPCHK(hipMalloc(&noi, cap_pairs * 2 * 4));
-    return 0;
-  }
-
-  void destroy() {
-    for (void *p : {SP0, XP1, A, T, scratch})
-      if (p) (void)hipFree(p);
-    for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
-                    (void *)out_stage})
-      if (p) (void)hipFree(p);
-    for (auto &kv : interl) {
-      (void)hipFree(kv.second.first);
-      (void)hipFree(kv.second.second);
-    }
-    interl.clear();
-  }
-
-  int get_interleaver(uint32_t Kv, uint32_t nbv) {
-    auto key = std::make_pair(Kv, nbv);
-    auto it = interl.find(key);
-    if (it == interl.end()) {
-      std::vector<uint16_t> f, r;
-      gen_interleaver(Kv, nbv, f, r);
-      uint16_t *df = nullptr, *dr = nullptr;
-      HIPCHK(hipMalloc(&df, Kv * 2));
-      HIPCHK(hipMalloc(&dr, Kv * 2));
-      HIPCHK(hipMemcpy(df, f.data(), Kv * 2, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(dr, r.data(), Kv * 2, hipMemcpyHostToDevice));
-      it = interl.emplace(key, std::make_pair(df, dr)).first;
-    }
-    fwd = it->second.first;
-    rev = it->second.second;
-    return 0;
-  }
-
-  // validate + bind a job, load inputs into the internal layout
-  int load(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n) {
-    if (cb_index(Kv) < 0) {
-      fprintf(stderr, "srsgpu: invalid code block size K=%u\n", Kv);
-      return -1;
-    }
-    if (Kv > cap_K || n > cap_cbs || n == 0) {
-      fprintf(stderr, "srsgpu: batch of %u x K=%u exceeds capacity %u x %u\n", n, Kv, cap_cbs, cap_K);
-      return -1;
-    }
-    if (impl < SRSLTE_TDEC_AUTO || impl > SRSLTE_TDEC_AVX_WINDOW) {
-      fprintf(stderr, "srsgpu: decoder type %d not supported\n", impl);
-      return -1;
-    }
-    const int r = resolve_impl(impl, Kv);
-    const int nbv = impl_nb(r);
-    if (nbv > 1 && (Kv % nbv || Kv / nbv <= 40)) {
-      // the reference windowed decoders need K/nb > win_overlap_len (turbodecoder_win.h:59);
-      // at K/nb == 40 its estimation pass doubles as the final pass (:331, :469) — a manual-
-      // mode-only corner (AUTO never selects it) that is rejected here
-      fprintf(stderr, "srsgpu: K=%u not supported by the %d-sub-block window decoder\n", Kv, nbv);
-      return -1;
-    }
-    if (in_stride < srsgpu_tdec_input_len(impl, sb_layout, Kv)) {
-      fprintf(stderr, "srsgpu: input stride %zu too small\n", in_stride);
-      return -1;
-    }
-    K = Kv;
-    impl_r = r;
-    nb = nbv;
-    ncb = (int)n;
-    npairs = (ncb + 1) / 2;
-    if (get_interleaver(K, (uint32_t)nb)) return -1;
-    const int sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nb > 1;
-    HIPCHK(srsgpu::launch_load(d_in, in_stride, sb_input, (int)K, nb, ncb, SP0, XP1, T, st));
-    HIPCHK(hipMemsetAsync(cb_done, 0, cap_pairs * 2, st));
-    HIPCHK(hipMemsetAsync(cb_ok, 0, cap_pairs * 2, st));
-    HIPCHK(hipMemsetAsync(pair_done, 0, cap_pairs, st));
-    return 0;
-  }
-
-  int halfit(int n, bool early) {
-    const uint8_t *pd = early ? pair_done : nullptr;
-    const int seq = impl_r == SRSLTE_TDEC_SSE ? 0 : 1;
-    ProfScope ps(nb > 1 ? "k_win_halfit" : (seq == 0 ? "k_sse_halfit" : "k_gen_halfit"), st);
-    HIPCHK(srsgpu::launch_halfit(n, nb, seq, SP0, XP1, A, T, fwd, rev, scratch, pd, (int)K, npairs, st));
-    return 0;
-  }
-
-  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t poly = 0,
-             uint32_t crc_bytes = 0, uint32_t maxh = 0) {
-    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, rev, A, XP1, d_out, out_stride,
-                                 early ? cb_done : nullptr, cb_ok, noi, early ? (int)crc_bytes : 0,
-                                 poly, (int)maxh, pair_done, st));
-    return 0;
-  }
-
-  int run(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
-          uint32_t nhalf, uint8_t *d_out, size_t out_stride) {
-    if (nhalf == 0) {
-      fprintf(stderr, "srsgpu: nof_halfits must be > 0\n");
-      return -1;
-    }
-    if (load(impl, sb_layout, d_in, in_stride, Kv, n)) return -1;
-    for (uint32_t h = 0; h < nhalf; h++)
-      if (halfit((int)h, false)) return -1;
-    return decide((int)nhalf - 1, d_out, out_stride, false);
-  }
-
-  int decode(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
-             uint32_t maxh, uint32_t poly, uint32_t crc_len, uint8_t *d_out, size_t out_stride,
-             uint8_t *d_ok, uint32_t *d_noi) {
-    if (maxh == 0 || crc_len == 0 || crc_len % 8 || crc_len > Kv) {
-      fprintf(stderr, "srsgpu: invalid early-stop parameters (max_halfits=%u crc_len=%u)\n", maxh, crc_len);
-      return -1;
-    }
-    if (load(impl, sb_layout, d_in, in_stride, Kv, n)) return -1;
-    for (uint32_t h = 0; h < maxh; h++) {
-      if (halfit((int)h, true)) return -1;
-      if (decide((int)h, d_out, out_stride, true, poly, crc_len / 8, maxh)) return -1;
-    }
-    if (d_ok) HIPCHK(hipMemcpyAsync(d_ok, cb_ok, (size_t)n, hipMemcpyDeviceToDevice, st));
-    if (d_noi) HIPCHK(hipMemcpyAsync(d_noi, noi, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
-    return 0;
-  }
-
-  int stage(uint32_t n, uint32_t Kv, size_t in_len) {
-    if (!in_stage) {
-      HIPCHK(hipMalloc(&in_stage, (size_t)cap_cbs * (3 * (cap_K + 32) + 12) * 2));
-      HIPCHK(hipMalloc(&out_stage, (size_t)cap_cbs * (cap_K / 8)));
-    }
-    (void)n;
-    (void)Kv;
-    (void)in_len;
-    return 0;
-  }
-};
-
-} // namespace
+using srsgpu::TdecEngine;
+using srsgpu::g_prof;
+using srsgpu::auto_subblocks;
+using srsgpu::cb_index;
+using srsgpu::impl_nb;
+using srsgpu::resolve_impl;
+typedef TdecEngine Engine;
 
 struct srsgpu_tdec_batch {
   Engine e;

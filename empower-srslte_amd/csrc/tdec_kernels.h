@@ -8,8 +8,11 @@
 namespace srsgpu {
 // user input -> SP0 (short4), P1 plane of XP1 (short2), T (short2 x 12) per pair. XP1 holds
 // two [npairs][K] short2 planes: X2 (app2) then P1 (par1).
-hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
-                       void *SP0, void *XP1, void *T, hipStream_t st);
+// rows != NULL: code block c's input starts at rows[c] (device array; rows_aligned: every row
+// is 4-byte aligned), else at in + c * in_stride.
+hipError_t launch_load(const int16_t *in, size_t in_stride, const int16_t *const *rows,
+                       int rows_aligned, int sb_input, int K, int NB, int ncb, void *SP0, void *XP1,
+                       void *T, hipStream_t st);
 size_t win_ck_bytes(int K, int NB, int npairs);
 size_t seq_scratch_bytes(int K, int npairs);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n). NB > 1: windowed decoder;
@@ -22,5 +25,7 @@ hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, con
                          const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int crc_bytes, uint32_t poly,
                          int max_halfits, uint8_t *pair_done, hipStream_t st);
+// pair_done[p] = both CBs of pair p done
+hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done, hipStream_t st);
 } // namespace srsgpu
 #endif

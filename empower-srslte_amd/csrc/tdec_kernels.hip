@@ -987,10 +987,16 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
 // (coalesced), and writes the 64*NB SB-ordered elements contiguously. SB input (rm_turbo's
 // layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280) is a straight copy.
 #define LOAD_KT 64
+// input row of code block c: strided rows, or a per-CB pointer table (DL-SCH softbuffer rows)
+__device__ __forceinline__ const int16_t *cb_row(const int16_t *in, size_t stride,
+                                                 const int16_t *const *rows, int c) {
+  return rows ? rows[c] : in + (size_t)c * stride;
+}
 // NB and the tile are compile-time so the run/offset arithmetic is shifts and multiplies; VEC
 // reads the natural runs as dwords (in, in_stride and L even).
 template <int NB, bool VEC>
 __global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in, size_t in_stride,
+                                                  const int16_t *const *__restrict__ rows,
                                                   int K, int ncb, s4 *__restrict__ SP0,
                                                   s2 *__restrict__ P1, s2 *__restrict__ T) {
   constexpr int RUN = 3 * LOAD_KT; // int16 per (CB, sub-block) run of one tile
@@ -1006,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in
   const int kn = min(LOAD_KT, L - k0);
 #pragma unroll
   for (int h = 0; h < 2; h++) {
-    const int16_t *src = in + (size_t)(h ? c1 : c0) * in_stride + 3 * k0;
+    const int16_t *src = cb_row(in, in_stride, rows, h ? c1 : c0) + 3 * k0;
     if (VEC) {
       const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
       for (int w = threadIdx.x; w < NB * RUN / 2; w += 256) {
@@ -1037,14 +1043,15 @@ __global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in
   }
   if (kt == 0 && threadIdx.x < 12) {
     const int t = threadIdx.x;
-    T[(size_t)pair * 12 + t] = s2{in[(size_t)c0 * in_stride + 3 * K + t],
-                                  in[(size_t)c1 * in_stride + 3 * K + t]};
+    T[(size_t)pair * 12 + t] = s2{cb_row(in, in_stride, rows, c0)[3 * K + t],
+                                  cb_row(in, in_stride, rows, c1)[3 * K + t]};
   }
 }
 
 // SB input (rm_turbo's layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280):
 // already in SB index order, a straight pair-interleaving copy, two elements per thread.
 __global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in, size_t in_stride,
+                                                 const int16_t *const *__restrict__ rows,
                                                  int K, int ncb, s4 *__restrict__ SP0,
                                                  s2 *__restrict__ P1, s2 *__restrict__ T) {
   const int npairs = (ncb + 1) / 2;
@@ -1054,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in,
   if (pair >= npairs) return;
   const int i = 2 * (int)(gid - (size_t)pair * per);
   const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
-  const int16_t *a = in + (size_t)c0 * in_stride, *b = in + (size_t)c1 * in_stride;
+  const int16_t *a = cb_row(in, in_stride, rows, c0), *b = cb_row(in, in_stride, rows, c1);
   const size_t o = (size_t)pair * K + i;
 #pragma unroll
   for (int u = 0; u < 2; u++) {
@@ -1162,27 +1169,29 @@ static void allow_big_lds(const void *f) {
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-hipError_t launch_load(const int16_t *in, size_t in_stride, int sb_input, int K, int NB, int ncb,
-                       void *SP0, void *XP1, void *T, hipStream_t st) {
+hipError_t launch_load(const int16_t *in, size_t in_stride, const int16_t *const *rows,
+                       int rows_aligned, int sb_input, int K, int NB, int ncb, void *SP0, void *XP1,
+                       void *T, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
   s4 *sp0 = (s4 *)SP0;
   s2 *p1 = (s2 *)XP1 + (size_t)npairs * K;
   s2 *t = (s2 *)T;
   if (sb_input) {
     hipLaunchKernelGGL(k_load_sb, dim3(nblk((size_t)npairs * (K / 2), 256)), dim3(256), 0, st, in,
-                       in_stride, K, ncb, sp0, p1, t);
+                       in_stride, rows, K, ncb, sp0, p1, t);
     return hipGetLastError();
   }
   const int L = K / NB;
   const unsigned grid = (unsigned)(npairs * ((L + LOAD_KT - 1) / LOAD_KT));
-  const bool vec = ((uintptr_t)in % 4 == 0) && (in_stride % 2 == 0) && (L % 2 == 0);
+  const bool vec = (rows ? rows_aligned != 0 : ((uintptr_t)in % 4 == 0 && in_stride % 2 == 0)) &&
+                   (L % 2 == 0);
 #define LOADNAT(nb)                                                                                \
   do {                                                                                             \
     if (vec)                                                                                       \
-      hipLaunchKernelGGL((k_load_nat<nb, true>), dim3(grid), dim3(256), 0, st, in, in_stride, K,    \
+      hipLaunchKernelGGL((k_load_nat<nb, true>), dim3(grid), dim3(256), 0, st, in, in_stride, rows, K, \
                          ncb, sp0, p1, t);                                                         \
     else                                                                                           \
-      hipLaunchKernelGGL((k_load_nat<nb, false>), dim3(grid), dim3(256), 0, st, in, in_stride, K,   \
+      hipLaunchKernelGGL((k_load_nat<nb, false>), dim3(grid), dim3(256), 0, st, in, in_stride, rows, K, \
                          ncb, sp0, p1, t);                                                         \
   } while (0)
   if (NB == 16) LOADNAT(16);
@@ -1253,6 +1262,12 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
 #undef SEQ
     }
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done, hipStream_t st) {
+  const int npairs = (ncb + 1) / 2;
+  hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
   return hipGetLastError();
 }
 

@@ -56,6 +56,20 @@ class srslte_tcod_t(ctypes.Structure):
     _fields_ = [("max_long_cb", ctypes.c_uint32), ("temp", ctypes.c_void_p)]
 
 
+class srsgpu_dlsch_tb_t(ctypes.Structure):
+    """include/srsgpu/dlsch_batch.h"""
+    _fields_ = [("tbs", ctypes.c_uint32), ("rv", ctypes.c_uint32), ("Qm", ctypes.c_uint32),
+                ("nof_e_bits", ctypes.c_uint32), ("softbuffer", ctypes.c_uint32),
+                ("e_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64)]
+
+
+SOFTBUFFER_SIZE = 18600
+
+
+def dlsch_data_len(tbs):
+    return tbs // 8 + 6
+
+
 _P = ctypes.POINTER(srslte_tdec_t)
 _PC = ctypes.POINTER(srslte_tcod_t)
 _sig = {
@@ -85,6 +99,18 @@ _sig = {
     "srsgpu_tdec_batch_decode": (_i32, [_vp, _i32, _i32, ctypes.POINTER(_vp), _u32, _u32, _u32,
                                         _u32, _u32, ctypes.POINTER(_vp), _u8p, _u32p]),
     "srsgpu_tdec_input_len": (_u32, [_i32, _i32, _u32]),
+    "srsgpu_dlsch_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32, _u32]),
+    "srsgpu_dlsch_destroy": (None, [_vp]),
+    "srsgpu_dlsch_set_stream": (None, [_vp, _vp]),
+    "srsgpu_dlsch_softbuffer_reset": (_i32, [_vp, _u32]),
+    "srsgpu_dlsch_softbuffer_reset_tbs": (_i32, [_vp, _u32, _u32]),
+    "srsgpu_dlsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp, _u32,
+                                       _vp, _vp]),
+    "srsgpu_dlsch_decode": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32,
+                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u32,
+                                   ctypes.POINTER(ctypes.c_int32), _u32p]),
+    "srsgpu_dlsch_softbuffer_read": (_i32, [_vp, _u32, _i16p, _u8p]),
+    "srsgpu_rm_turbo_rx_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
     "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -230,6 +256,76 @@ class Tcod:
     def __del__(self):
         try:
             _lib.srslte_tcod_free(ctypes.byref(self.h))
+        except Exception:
+            pass
+
+
+class Dlsch:
+    """srsgpu_dlsch_t: batched transport-block decoding (de-RM + HARQ, turbo decoding with CRC
+    early stop, TB CRC) with device-resident softbuffers."""
+
+    def __init__(self, nof_softbuffers, max_cb=13, max_cbs_per_call=1024, stream=None):
+        self.q = _vp()
+        self.max_cb = max_cb
+        if _lib.srsgpu_dlsch_create(ctypes.byref(self.q), nof_softbuffers, max_cb,
+                                    max_cbs_per_call) != 0:
+            raise RuntimeError("srsgpu_dlsch_create failed")
+        if stream is not None:
+            _lib.srsgpu_dlsch_set_stream(self.q, _vp(stream))
+
+    @staticmethod
+    def _tbs(tbs_list):
+        arr = (srsgpu_dlsch_tb_t * len(tbs_list))()
+        for i, t in enumerate(tbs_list):
+            for k, v in t.items():
+                setattr(arr[i], k, v)
+        return arr
+
+    def reset(self, slot, tbs=None):
+        r = (_lib.srsgpu_dlsch_softbuffer_reset(self.q, slot) if tbs is None
+             else _lib.srsgpu_dlsch_softbuffer_reset_tbs(self.q, slot, tbs))
+        if r != 0:
+            raise RuntimeError("softbuffer reset failed")
+
+    def decode(self, tbs_list, e_bits, max_halfits=8):
+        """tbs_list: dicts {tbs, rv, Qm, nof_e_bits, softbuffer}; e_bits: int16 arrays.
+        Returns (ret[], data[], noi[])."""
+        n = len(tbs_list)
+        arr = self._tbs(tbs_list)
+        es = [np.ascontiguousarray(e, np.int16) for e in e_bits]
+        outs = [np.zeros(dlsch_data_len(t["tbs"]), np.uint8) for t in tbs_list]
+        ep = (_vp * n)(*[e.ctypes.data for e in es])
+        op = (_vp * n)(*[o.ctypes.data for o in outs])
+        ret = (ctypes.c_int32 * n)()
+        noi = np.zeros(n, np.uint32)
+        if _lib.srsgpu_dlsch_decode(self.q, arr, n, ep, op, max_halfits, ret,
+                                    noi.ctypes.data_as(_u32p)) != 0:
+            raise RuntimeError("srsgpu_dlsch_decode failed")
+        return list(ret), outs, noi
+
+    def decode_dev(self, tbs_list, d_e, d_data, max_halfits, d_ret, d_noi):
+        arr = self._tbs(tbs_list)
+        return _lib.srsgpu_dlsch_decode_dev(self.q, arr, len(tbs_list), _vp(d_e), _vp(d_data),
+                                            max_halfits, _vp(d_ret), _vp(d_noi))
+
+    def read_softbuffer(self, slot):
+        rows = np.zeros((self.max_cb, SOFTBUFFER_SIZE), np.int16)
+        crc = np.zeros(self.max_cb, np.uint8)
+        if _lib.srsgpu_dlsch_softbuffer_read(self.q, slot, _i16(rows), _u8(crc)) != 0:
+            raise RuntimeError("softbuffer read failed")
+        return rows, crc
+
+    def rm_rx_dev(self, d_in, d_out, in_len, K, rv, sb_layout):
+        return _lib.srsgpu_rm_turbo_rx_dev(self.q, _vp(d_in), _vp(d_out), in_len, K, rv, sb_layout)
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_dlsch_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:
             pass
 

@@ -1,0 +1,86 @@
+/*
+ * srsgpu batched DL-SCH transport-block decoder — C ABI of the MI355X (gfx950) path from
+ * descrambled int16 LLRs to transport blocks.
+ *
+ * One call decodes many transport blocks. That covers a subframe's TBs, or the TBs of many
+ * subframes and cells. Each TB goes through the reference's receive chain
+ * (reference: lib/src/phy/phch/sch.c:307-517, decode_tb / decode_tb_cb):
+ *   - code block segmentation (cbsegm.c:58-140);
+ *   - per code block, de-rate-matching with HARQ soft combining into the TB's softbuffer
+ *     (srslte_rm_turbo_rx_lut, rm_turbo.c:378-430; sub-block layout for the windowed decoders);
+ *   - turbo decoding with CRC early stop per half-iteration (CRC24B over K when C > 1, CRC24A over
+ *     TBS+24 when C == 1) up to max_halfits half-iterations; blocks that passed in an earlier
+ *     transmission are not decoded again but copied from the softbuffer;
+ *   - TB assembly and the TB CRC24A check.
+ * The results match srslte_dlsch_decode2 bit for bit: return code, data bytes, nof_iterations
+ * and the softbuffer's cb_crc state.
+ *
+ * Softbuffers live in device memory, indexed 0 .. nof_softbuffers-1. Each holds max_cb rows of
+ * SRSGPU_SOFTBUFFER_SIZE int16 (softbuffer.h SOFTBUFFER_SIZE), cb_crc flags and saved bytes. As in
+ * the reference, the caller resets a softbuffer before a new transport block
+ * (srslte_softbuffer_rx_reset).
+ */
+#ifndef SRSGPU_DLSCH_BATCH_H
+#define SRSGPU_DLSCH_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRSGPU_SOFTBUFFER_SIZE 18600
+
+typedef struct srsgpu_dlsch srsgpu_dlsch_t;
+
+typedef struct {
+  uint32_t tbs;         /* transport block size in bits (cb_segm.tbs) */
+  uint32_t rv;          /* redundancy version 0..3 */
+  uint32_t Qm;          /* modulation order x layers factor, as srslte_dlsch_decode2 passes it */
+  uint32_t nof_e_bits;  /* received coded bits of this TB */
+  uint32_t softbuffer;  /* softbuffer index */
+  uint64_t e_offset;    /* first LLR of this TB in the e-bits buffer (int16 elements) */
+  uint64_t data_offset; /* first output byte of this TB in the data buffer */
+} srsgpu_dlsch_tb_t;
+
+/* Output bytes one TB needs: (tbs+24)/8 plus the last code block's 3 CRC bytes (C > 1). */
+#define SRSGPU_DLSCH_DATA_LEN(tbs) ((tbs) / 8 + 6)
+
+int srsgpu_dlsch_create(srsgpu_dlsch_t **q, uint32_t nof_softbuffers, uint32_t max_cb,
+                        uint32_t max_cbs_per_call);
+void srsgpu_dlsch_destroy(srsgpu_dlsch_t *q);
+void srsgpu_dlsch_set_stream(srsgpu_dlsch_t *q, void *hip_stream);
+
+/* srslte_softbuffer_rx_reset (softbuffer.c:125-150): zero the soft bits and the cb_crc flags. */
+int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t softbuffer);
+/* srslte_softbuffer_rx_reset_tbs: only the first (tbs+24)/6120+1 code blocks. */
+int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t softbuffer, uint32_t tbs);
+
+/* Device pointers, asynchronous on the handle's stream. d_ret[i]: 0 TB decoded and CRC OK,
+ * -1 CRC error, -2 invalid inputs (filler bits, too many CBs) — sch.c's return values.
+ * d_noi[i]: srslte_sch_last_noi after TB i. The host array tb[] may be reused on return. */
+int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
+                            const int16_t *d_e_bits, uint8_t *d_data, uint32_t max_halfits,
+                            int32_t *d_ret, uint32_t *d_noi);
+
+/* Host pointers: e_bits[i] / data[i] per TB (offsets in tb[] ignored); synchronises. */
+int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
+                        const int16_t *const *e_bits, uint8_t *const *data, uint32_t max_halfits,
+                        int32_t *ret, uint32_t *noi);
+
+/* Copy a softbuffer's state to the host (tests / debugging): rows [max_cb][SOFTBUFFER_SIZE]
+ * int16 and cb_crc [max_cb]; either may be NULL. */
+int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t softbuffer, int16_t *rows,
+                                 uint8_t *cb_crc);
+
+/* De-rate-matching alone (srslte_rm_turbo_rx_lut_ semantics, rm_turbo.c:394-430) on device
+ * buffers: d_out[t[i % (3K+12)]] += d_in[i] for i < in_len, with the sub-block table the AUTO
+ * decoder expects when sb_layout != 0 (srslte_tdec_autoimp_get_subblocks(K) > 0). */
+int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
+                           uint32_t K, uint32_t rv, int sb_layout);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

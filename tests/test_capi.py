@@ -7,9 +7,8 @@ import re
 from conftest import REPO
 
 LIB = os.path.join(REPO, "empower-srslte_amd", "lib", "libsrsgpu_phy.so")
-HEADERS = [os.path.join(REPO, "include", "srslte", "phy", "fec", "turbodecoder.h"),
-           os.path.join(REPO, "include", "srslte", "phy", "fec", "turbocoder.h"),
-           os.path.join(REPO, "include", "srsgpu", "tdec_batch.h")]
+HEADERS = sorted(os.path.join(d, f) for d, _, fs in os.walk(os.path.join(REPO, "include"))
+                 for f in fs if f.endswith(".h") and f != "qpp_table.h")
 
 
 def declared_functions(path):

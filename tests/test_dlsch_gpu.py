@@ -1,0 +1,185 @@
+"""Parity of the MI355X DL-SCH transport-block decoder (libsrsgpu_phy.so, srsgpu_dlsch_*) with
+the golden HARQ sequences recorded from the srsLTE reference (sch.c decode_tb) and with the CPU
+oracle: return codes, TB bytes, nof_iterations, softbuffer cb_crc flags and soft bits."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from srsgpu_testlib import DlschOracle, SOFTBUFFER_SIZE
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def s():
+    import srsgpu_phy
+    return srsgpu_phy
+
+
+@pytest.fixture(scope="module")
+def dgold():
+    z = np.load(os.path.join(HERE, "golden", "dlsch_golden.npz"))
+    return z, json.loads(bytes(z["manifest"]))
+
+
+@pytest.fixture(scope="module")
+def dl(oracle):
+    return DlschOracle(oracle)
+
+
+def _tb(tbs, rv, Qm, nbits, slot):
+    return dict(tbs=tbs, rv=rv, Qm=Qm, nof_e_bits=nbits, softbuffer=slot)
+
+
+def test_golden_harq_sequences(s, dgold):
+    """Each golden TB in its own softbuffer; every transmission matches the reference."""
+    z, man = dgold
+    tbc = [c for c in man if c["kind"] == "tb"]
+    g = s.Dlsch(len(tbc), 16, 64)
+    for slot, c in enumerate(tbc):
+        g.reset(slot)
+        for t, st in enumerate(c["steps"]):
+            sk = "%s_t%d" % (c["key"], t)
+            ret, data, noi = g.decode([_tb(c["tbs"], st["rv"], c["Qm"], c["nbits"], slot)],
+                                      [z[sk + "_llr"]], c["max_halfits"])
+            nbytes = (c["tbs"] + 24) // 8
+            assert ret[0] == st["ret"] and noi[0] == st["noi"], (sk, ret, noi, st)
+            assert (data[0][:nbytes] == z[sk + "_out"]).all(), sk
+            _, crc = g.read_softbuffer(slot)
+            assert (crc[:c["C"]] == z[sk + "_cbcrc"]).all(), sk
+    g.close()
+
+
+def test_golden_all_first_transmissions_one_call(s, dgold):
+    """All golden TBs' first transmissions in ONE call (mixed K, C, CRC types)."""
+    z, man = dgold
+    tbc = [c for c in man if c["kind"] == "tb"]
+    g = s.Dlsch(len(tbc), 16, 128)
+    for slot in range(len(tbc)):
+        g.reset(slot)
+    tbl = [_tb(c["tbs"], c["steps"][0]["rv"], c["Qm"], c["nbits"], i) for i, c in enumerate(tbc)]
+    ret, data, noi = g.decode(tbl, [z["%s_t0_llr" % c["key"]] for c in tbc], 8)
+    for i, c in enumerate(tbc):
+        st = c["steps"][0]
+        assert ret[i] == st["ret"] and noi[i] == st["noi"], c["key"]
+        assert (data[i][:(c["tbs"] + 24) // 8] == z["%s_t0_out" % c["key"]]).all(), c["key"]
+    g.close()
+
+
+def test_softbuffer_soft_bits_vs_oracle(s, dl, dgold):
+    """After a failed first transmission the device softbuffer rows equal the oracle's."""
+    z, man = dgold
+    c = [c for c in man if c["kind"] == "tb" and c["C"] > 1 and c["steps"][0]["ret"] != 0][0]
+    g = s.Dlsch(1, 16, 32)
+    g.reset(0)
+    llr = z["%s_t0_llr" % c["key"]]
+    g.decode([_tb(c["tbs"], 0, c["Qm"], c["nbits"], 0)], [llr], 8)
+    rows, crc = g.read_softbuffer(0)
+    sb = dl.softbuffer(16)
+    dl.reset(sb)
+    dl.decode(sb, c["tbs"], 0, c["Qm"], llr, 8)
+    orows = np.ctypeslib.as_array(sb.buffer, shape=(16 * SOFTBUFFER_SIZE,)).reshape(16, -1)
+    assert (rows[:c["C"]] == orows[:c["C"]]).all()
+    dl.free(sb)
+    g.close()
+
+
+def test_rate_dematching_dev_golden(s, oracle, dgold):
+    import torch
+    z, man = dgold
+    g = s.Dlsch(1, 1, 4)
+    for c in man:
+        if c["kind"] != "rm":
+            continue
+        K = c["K"]
+        d_in = torch.from_numpy(np.ascontiguousarray(z[c["key"] + "_in"])).cuda()
+        d_out = torch.zeros(3 * (K + 32) + 12, dtype=torch.int16, device="cuda")
+        assert g.rm_rx_dev(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), K, c["rv"], c["sb"]) == 0
+        torch.cuda.synchronize()
+        assert (d_out.cpu().numpy() == z[c["key"] + "_out"]).all(), c["key"]
+    g.close()
+
+
+def test_random_harq_batches_vs_oracle(s, dl, oracle):
+    """Batches of random TBs (varied TBS/Qm/E/SNR/rv) across several HARQ rounds, one call per
+    round, against the oracle with its own softbuffers."""
+    rng = np.random.default_rng(77)
+    good = [t for t in list(range(16, 6200, 24)) + list(range(6200, 80000, 312))
+            if oracle.cbsegm(t)[5] == 0]
+    n = 12
+    g = s.Dlsch(n, 16, 256)
+    osb = [dl.softbuffer(16) for _ in range(n)]
+    tbl, datas = [], []
+    for i in range(n):
+        tbs, Qm = int(rng.choice(good)), int(rng.choice([2, 4, 6]))
+        C = oracle.cbsegm(tbs)[0]
+        nb = int(3.1 * tbs * rng.uniform(0.4, 1.5))
+        nb = max(nb - nb % Qm, Qm * C)
+        tbl.append(_tb(tbs, 0, Qm, nb, i))
+        datas.append(rng.integers(0, 256, tbs // 8).astype(np.uint8))
+        g.reset(i)
+        dl.reset(osb[i])
+    snr = rng.uniform(-0.5, 3.0, n)
+    for rnd, rv in enumerate((0, 2, 3, 1)):
+        llrs = []
+        for i, t in enumerate(tbl):
+            t["rv"] = rv
+            e = dl.encode(t["tbs"], rv, t["Qm"], t["nof_e_bits"], datas[i])
+            y = np.where(e == 1, 1.0, -1.0) + 10 ** (-snr[i] / 20) * rng.standard_normal(e.size)
+            llrs.append((100 * y).astype(np.float32).astype(np.int16))
+        ret, data, noi = g.decode(tbl, llrs, 8)
+        for i, t in enumerate(tbl):
+            r, od, onoi, ocrc = dl.decode(osb[i], t["tbs"], rv, t["Qm"], llrs[i], 8)
+            nbytes = (t["tbs"] + 24) // 8
+            assert ret[i] == r and noi[i] == onoi, (rnd, i, ret[i], r, noi[i], onoi)
+            assert (data[i][:nbytes] == od[:nbytes]).all(), (rnd, i)
+            _, crc = g.read_softbuffer(i)
+            assert (crc[:len(ocrc)] == ocrc).all(), (rnd, i)
+    for b in osb:
+        dl.free(b)
+    g.close()
+
+
+def test_full_subframe_batch_device(s, dl):
+    """C3 shape: 64 x TBS 75376 (13 x K=5824, 64QAM, 90000 coded bits), noiseless LLRs, device
+    pointers: every TB decodes with nof_iterations 1 (CRC after the first half-iteration)."""
+    import torch
+    n, tbs, nb = 64, 75376, 90000
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (4, tbs // 8)).astype(np.uint8)
+    e = np.stack([np.where(dl.encode(tbs, 0, 6, nb, d) == 1, 100, -100) for d in data]).astype(np.int16)
+    e_all = e[np.arange(n) % 4]
+    d_e = torch.from_numpy(np.ascontiguousarray(e_all)).cuda()
+    dl_len = tbs // 8 + 6
+    d_data = torch.zeros(n * dl_len, dtype=torch.uint8, device="cuda")
+    d_ret = torch.full((n,), 7, dtype=torch.int32, device="cuda")
+    d_noi = torch.zeros(n, dtype=torch.int32, device="cuda")
+    g = s.Dlsch(n, 13, n * 13, stream=torch.cuda.current_stream().cuda_stream)
+    for i in range(n):
+        g.reset(i)
+    tbl = [dict(tbs=tbs, rv=0, Qm=6, nof_e_bits=nb, softbuffer=i, e_offset=i * nb,
+                data_offset=i * dl_len) for i in range(n)]
+    assert g.decode_dev(tbl, d_e.data_ptr(), d_data.data_ptr(), 8, d_ret.data_ptr(),
+                        d_noi.data_ptr()) == 0
+    torch.cuda.synchronize()
+    assert (d_ret.cpu().numpy() == 0).all()
+    assert (d_noi.cpu().numpy() == 1).all()
+    out = d_data.cpu().numpy().reshape(n, dl_len)
+    assert (out[:, :tbs // 8] == data[np.arange(n) % 4]).all()
+    g.close()
+
+
+def test_invalid_and_empty_tbs(s):
+    g = s.Dlsch(2, 13, 16)
+    g.reset(0)
+    g.reset(1)
+    e = np.zeros(3000, np.int16)
+    # 1001 bits: B' = 1025 is not a code block size -> filler bits -> SRSLTE_ERROR_INVALID_INPUTS
+    ret, _, noi = g.decode([_tb(1001, 0, 2, 3000, 0), _tb(0, 0, 2, 3000, 1)], [e, e], 8)
+    assert ret == [-2, 0] and list(noi) == [0, 0]
+    with pytest.raises(RuntimeError):
+        g.decode([_tb(1000, 0, 2, 3000, 5)], [e], 8)  # no such softbuffer
+    g.close()
