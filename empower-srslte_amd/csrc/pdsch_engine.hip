@@ -1,0 +1,323 @@
+// Host side of the MI355X PDSCH receiver (include/srsgpu/pdsch_batch.h): RE maps, scrambling
+// sequence tables, per-call descriptors; the compute is pdsch_kernels.hip + the DL-SCH engine.
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <stdio.h>
+#include <string.h>
+#include <string>
+#include <vector>
+
+#include "pdsch_kernels.h"
+#include "srsgpu/pdsch_batch.h"
+#include "tdec_engine.h"
+
+namespace srsgpu {
+
+// ------------------------------------------------------------------ RE map ----
+// Gather order of srslte_pdsch_cp in read mode (pdsch.c:95-234): slots, OFDM symbols, allocated
+// PRBs; PSS/SSS (subframes 0/5, slot 0, last two symbols) and PBCH (subframe 0, slot 1, first 4
+// symbols) cut the 6 (or, for odd nof_prb, 7) central PRBs; in symbols carrying CRS the
+// reference REs are skipped with prb_cp_ref's interval walk (prb_dl.c:51-82).
+static void re_map(const srsgpu_cell_t &c, uint32_t lstart_grant, uint32_t sf_idx,
+                   const uint8_t prb[2][110], std::vector<uint32_t> &m) {
+  const uint32_t N = c.nof_prb, ns = 7, nref = c.nof_ports == 1 ? 2 : 4;
+  m.clear();
+  auto refsym = [&](uint32_t l) { return (l == 1 && c.nof_ports == 4) || l == 0 || l == ns - 3; };
+  // prb_cp_ref: 'offset' REs, then (intervals-1) x [skip 1, take ri], then [skip 1, take ri-offset]
+  auto take_ref = [&](uint32_t &in, int offset, int intervals) {
+    const int ri = 12 / (int)nref - 1;
+    for (int j = 0; j < offset; j++) m.push_back(in++);
+    for (int i = 0; i < intervals - 1; i++) {
+      in++;
+      for (int j = 0; j < ri; j++) m.push_back(in++);
+    }
+    if (ri - offset > 0) {
+      in++;
+      for (int j = 0; j < ri - offset; j++) m.push_back(in++);
+    }
+  };
+  uint32_t offset = 0;
+  for (uint32_t s = 0; s < 2; s++)
+    for (uint32_t l = 0; l < ns; l++)
+      for (uint32_t n = 0; n < N; n++) {
+        if (!prb[s][n]) continue;
+        uint32_t lst = s == 0 ? lstart_grant : 0, lend = ns;
+        const bool centre = n >= N / 2 - 3 && n < N / 2 + 3 + (N % 2);
+        const bool sss = s == 0 && (sf_idx == 0 || sf_idx == 5) && centre;
+        const bool pbch = s == 1 && sf_idx == 0 && centre;
+        if (sss) lend = ns - 2;
+        if (pbch) lst = 4;
+        uint32_t in = ((l + s * ns) * N + n) * 12;
+        if (l >= lst && l < lend) {
+          if (refsym(l)) {
+            offset = nref == 2 ? (l == 0 ? c.id % 6 : (c.id + 3) % 6) : c.id % 3;
+            take_ref(in, (int)offset, (int)nref);
+          } else {
+            for (int j = 0; j < 12; j++) m.push_back(in++);
+          }
+        }
+        if ((N % 2) && ((pbch && l < lst) || (sss && l >= lend))) {
+          if (n == N / 2 - 3 || n == N / 2 + 3) {
+            if (n == N / 2 + 3) in += 6;
+            if (refsym(l))
+              take_ref(in, (int)offset, (int)nref / 2);
+            else
+              for (int j = 0; j < 6; j++) m.push_back(in++);
+          }
+        }
+      }
+}
+
+static const int kQm[4] = {1, 2, 4, 6};
+
+// ------------------------------------------------------------------ engine ----
+struct PdschEngine {
+  hipStream_t st = nullptr;
+  srsgpu_cell_t cell{};
+  uint32_t max_sf = 0;
+  bool csi = false;
+  srsgpu_dlsch_t *dl = nullptr;
+  // Gold tables: x1 and the 31 x2 basis sequences, bits 0 .. 32*words-1
+  uint32_t gold_words = 0;
+  uint32_t *d_x1 = nullptr, *d_x2b = nullptr;
+  std::map<std::string, std::pair<uint32_t *, uint32_t>> maps; // device RE maps
+  // per-call buffers
+  GoldItem *h_gold = nullptr, *d_gold = nullptr;
+  LlrItem *h_llr = nullptr, *d_llr = nullptr;
+  srsgpu_dlsch_tb_t *h_tb = nullptr;
+  uint32_t *d_c = nullptr;   // [max_sf][cwords]
+  float *d_csi = nullptr;    // [max_sf][max_re]
+  uint32_t *d_csimax = nullptr;
+  int16_t *d_e = nullptr;    // [max_sf][max_bits]
+  uint32_t max_re = 0, max_bits = 0, cwords = 0;
+  hipEvent_t staged = nullptr;
+  bool staged_pending = false;
+
+  int create(const srsgpu_cell_t &c, uint32_t nsb, uint32_t max_cb, uint32_t msf) {
+    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !msf ||
+        (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4) || c.nof_rx_ant < 1 ||
+        c.nof_rx_ant > 2) {
+      fprintf(stderr, "srsgpu: invalid cell (nof_prb=%u id=%u ports=%u rx=%u)\n", c.nof_prb, c.id,
+              c.nof_ports, c.nof_rx_ant);
+      return -1;
+    }
+    cell = c;
+    max_sf = msf;
+    max_re = c.nof_prb * 12 * 14;
+    max_bits = max_re * 6;
+    cwords = (max_bits + 31) / 32 + 1;
+    if (srsgpu_dlsch_create(&dl, nsb, max_cb, msf * max_cb)) return -1;
+    // Gold tables (36.211 7.2): x1(n+31) = x1(n+3) + x1(n), x1 = 1,0,0..; x2 basis i: seed 1 << i
+    gold_words = (1600 + max_bits + 64) / 32 + 2;
+    const uint32_t nbits = gold_words * 32;
+    std::vector<uint8_t> a(nbits + 31);
+    std::vector<uint32_t> x1w(gold_words, 0), x2w((size_t)31 * gold_words, 0);
+    a.assign(nbits + 31, 0);
+    a[0] = 1;
+    for (uint32_t n = 0; n < nbits; n++) a[n + 31] = (a[n + 3] + a[n]) & 1;
+    for (uint32_t n = 0; n < nbits; n++) x1w[n / 32] |= (uint32_t)a[n] << (n % 32);
+    for (int i = 0; i < 31; i++) {
+      a.assign(nbits + 31, 0);
+      a[i] = 1;
+      for (uint32_t n = 0; n < nbits; n++) a[n + 31] = (a[n + 3] + a[n + 2] + a[n + 1] + a[n]) & 1;
+      for (uint32_t n = 0; n < nbits; n++) x2w[(size_t)i * gold_words + n / 32] |= (uint32_t)a[n] << (n % 32);
+    }
+    HIPCHK(hipMalloc(&d_x1, x1w.size() * 4));
+    HIPCHK(hipMalloc(&d_x2b, x2w.size() * 4));
+    HIPCHK(hipMemcpy(d_x1, x1w.data(), x1w.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_x2b, x2w.data(), x2w.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipHostMalloc(&h_gold, sizeof(GoldItem) * msf));
+    HIPCHK(hipHostMalloc(&h_llr, sizeof(LlrItem) * msf));
+    HIPCHK(hipHostMalloc(&h_tb, sizeof(srsgpu_dlsch_tb_t) * msf));
+    HIPCHK(hipMalloc(&d_gold, sizeof(GoldItem) * msf));
+    HIPCHK(hipMalloc(&d_llr, sizeof(LlrItem) * msf));
+    HIPCHK(hipMalloc(&d_c, (size_t)msf * cwords * 4));
+    HIPCHK(hipMalloc(&d_csi, (size_t)msf * max_re * 4));
+    HIPCHK(hipMalloc(&d_csimax, (size_t)msf * 4));
+    HIPCHK(hipMalloc(&d_e, (size_t)msf * max_bits * 2));
+    HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
+    return 0;
+  }
+
+  void destroy() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (void *p : {(void *)d_x1, (void *)d_x2b, (void *)d_gold, (void *)d_llr, (void *)d_c,
+                    (void *)d_csi, (void *)d_csimax, (void *)d_e})
+      if (p) (void)hipFree(p);
+    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb})
+      if (p) (void)hipHostFree(p);
+    for (auto &kv : maps) (void)hipFree(kv.second.first);
+    maps.clear();
+    if (staged) (void)hipEventDestroy(staged);
+    if (dl) srsgpu_dlsch_destroy(dl);
+    dl = nullptr;
+  }
+
+  // device RE map of a grant, cached; returns its RE count
+  const uint32_t *map(const srsgpu_pdsch_sf_t &s, uint32_t *nre) {
+    const uint32_t cls = s.sf_idx == 0 ? 0 : s.sf_idx == 5 ? 5 : 1;
+    std::string key((const char *)s.prb_idx, 2 * 110);
+    key += (char)cls;
+    key += (char)s.lstart;
+    auto it = maps.find(key);
+    if (it == maps.end()) {
+      std::vector<uint32_t> m;
+      re_map(cell, s.lstart, cls, s.prb_idx, m);
+      uint32_t *d = nullptr;
+      if (hipMalloc(&d, std::max<size_t>(m.size(), 1) * 4) != hipSuccess) return nullptr;
+      if (!m.empty() && hipMemcpy(d, m.data(), m.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return nullptr;
+      it = maps.emplace(key, std::make_pair(d, (uint32_t)m.size())).first;
+    }
+    *nre = it->second.second;
+    return it->second.first;
+  }
+
+  int llr(const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid, const float *d_ce,
+          size_t ant_stride, int16_t *const *e_ptr) {
+    if (n > max_sf) {
+      fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
+      return -1;
+    }
+    if (cell.nof_ports != 1) {
+      fprintf(stderr, "srsgpu: only single-port (SISO) PDSCH is supported\n");
+      return -1;
+    }
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    uint32_t mre = 0, mbits = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const srsgpu_pdsch_sf_t &s = sf[i];
+      if (s.mod > 3 || s.sf_idx > 9 || s.lstart > 4) {
+        fprintf(stderr, "srsgpu: invalid subframe %u (mod=%u sf_idx=%u lstart=%u)\n", i, s.mod, s.sf_idx,
+                s.lstart);
+        return -1;
+      }
+      uint32_t nre = 0;
+      const uint32_t *m = map(s, &nre);
+      if (!m) return -1;
+      if (nre != s.nof_re) { // pdsch.c:886-890
+        fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
+        return -1;
+      }
+      const int q = kQm[s.mod];
+      GoldItem &g = h_gold[i];
+      g.seed = ((uint32_t)s.rnti << 14) + ((2 * s.sf_idx / 2) << 9) + cell.id; // q = 0 (codeword 0)
+      g.len = nre * q;
+      g.c = d_c + (size_t)i * cwords;
+      LlrItem &t = h_llr[i];
+      memset(&t, 0, sizeof(t));
+      for (uint32_t a = 0; a < cell.nof_rx_ant; a++) {
+        t.y[a] = (const float2 *)d_grid + s.grid_offset + a * ant_stride;
+        t.h[a] = (const float2 *)d_ce + s.grid_offset + a * ant_stride;
+      }
+      t.map = m;
+      t.c = g.c;
+      t.e = e_ptr[i];
+      t.csi = d_csi + (size_t)i * max_re;
+      t.csi_max = d_csimax + i;
+      t.nof_re = nre;
+      t.qm = q;
+      t.mod = (int)s.mod;
+      t.nrx = (int)cell.nof_rx_ant;
+      t.csi_mode = csi ? 1 : 0;
+      t.noise = s.noise_estimate;
+      t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
+      t.inv_scaling = 1.0f / t.scaling;
+      mre = std::max(mre, nre);
+      mbits = std::max(mbits, nre * q);
+    }
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)n * 4, st));
+    {
+      ProfScope ps("k_gold", st);
+      HIPCHK(launch_gold(d_gold, (int)n, mbits, d_x1, d_x2b, gold_words, st));
+    }
+    ProfScope ps("k_pdsch_llr", st);
+    HIPCHK(launch_pdsch_llr(d_llr, (int)n, mre, csi, st));
+    return 0;
+  }
+};
+
+} // namespace srsgpu
+
+using srsgpu::PdschEngine;
+
+struct srsgpu_pdsch {
+  PdschEngine e;
+};
+
+extern "C" {
+
+int srsgpu_pdsch_create(srsgpu_pdsch_t **q, const srsgpu_cell_t *cell, uint32_t nsb, uint32_t max_cb,
+                        uint32_t max_sf) {
+  if (!q || !cell) return -1;
+  auto *p = new srsgpu_pdsch();
+  if (p->e.create(*cell, nsb, max_cb, max_sf)) {
+    p->e.destroy();
+    delete p;
+    *q = nullptr;
+    return -1;
+  }
+  *q = p;
+  return 0;
+}
+
+void srsgpu_pdsch_destroy(srsgpu_pdsch_t *q) {
+  if (!q) return;
+  q->e.destroy();
+  delete q;
+}
+
+void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *s) {
+  if (!q) return;
+  q->e.st = (hipStream_t)s;
+  srsgpu_dlsch_set_stream(q->e.dl, s);
+}
+
+void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {
+  if (q) q->e.csi = enable != 0;
+}
+
+srsgpu_dlsch_t *srsgpu_pdsch_get_dlsch(srsgpu_pdsch_t *q) { return q ? q->e.dl : nullptr; }
+
+int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf) {
+  if (!cell || !sf) return -1;
+  std::vector<uint32_t> m;
+  srsgpu::re_map(*cell, sf->lstart, sf->sf_idx, sf->prb_idx, m);
+  return (int)m.size();
+}
+
+int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
+                         const float *d_ce, size_t ant_stride, int16_t *d_e, const uint64_t *e_offset) {
+  if (!q || (!sf && n) || !d_grid || !d_ce || !d_e || !e_offset) return -1;
+  std::vector<int16_t *> e(n);
+  for (uint32_t i = 0; i < n; i++) e[i] = d_e + e_offset[i];
+  return q->e.llr(sf, n, d_grid, d_ce, ant_stride, e.data());
+}
+
+int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
+                            const float *d_ce, size_t ant_stride, uint8_t *d_data, uint32_t maxh,
+                            int32_t *d_ret, uint32_t *d_noi) {
+  if (!q || (!sf && n) || !d_grid || !d_ce || !d_data || !d_ret || !d_noi) return -1;
+  PdschEngine &E = q->e;
+  std::vector<int16_t *> e(n);
+  for (uint32_t i = 0; i < n; i++) e[i] = E.d_e + (size_t)i * E.max_bits;
+  if (E.llr(sf, n, d_grid, d_ce, ant_stride, e.data())) return -1;
+  for (uint32_t i = 0; i < n; i++) {
+    srsgpu_dlsch_tb_t &t = E.h_tb[i];
+    t.tbs = sf[i].tbs;
+    t.rv = sf[i].rv;
+    t.Qm = (uint32_t)srsgpu::kQm[sf[i].mod];
+    t.nof_e_bits = sf[i].nof_re * t.Qm;
+    t.softbuffer = sf[i].softbuffer;
+    t.e_offset = (uint64_t)i * E.max_bits;
+    t.data_offset = sf[i].data_offset;
+  }
+  return srsgpu_dlsch_decode_dev(E.dl, E.h_tb, n, E.d_e, d_data, maxh, d_ret, d_noi);
+}
+
+} // extern "C"

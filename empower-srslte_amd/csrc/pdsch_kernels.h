@@ -1,0 +1,36 @@
+// Internal launch interface of the PDSCH receive kernels (pdsch_kernels.hip).
+#ifndef SRSGPU_PDSCH_KERNELS_H
+#define SRSGPU_PDSCH_KERNELS_H
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+namespace srsgpu {
+
+// one codeword's scrambling sequence: len bits of c(n) for c_init = seed, packed LSB first
+struct GoldItem {
+  uint32_t seed, len;
+  uint32_t *c;
+};
+
+// one codeword: gather + equalise + demap + descramble (+ CSI)
+struct LlrItem {
+  const float2 *y[2];      // received grid of each rx antenna
+  const float2 *h[2];      // channel estimate (port 0) of each rx antenna, same layout
+  const uint32_t *map;     // RE j -> grid position
+  const uint32_t *c;       // packed scrambling bits
+  int16_t *e;              // LLRs out (nof_re * qm)
+  float *csi;              // per-RE CSI (csi_mode)
+  uint32_t *csi_max;       // max CSI as float bits (csi_mode; zeroed before the launch)
+  uint32_t nof_re;
+  int qm, mod, nrx, csi_mode;
+  float noise, inv_scaling, scaling;
+};
+
+hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,
+                       const uint32_t *x2b, uint32_t words, hipStream_t st);
+hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st);
+} // namespace srsgpu
+#endif

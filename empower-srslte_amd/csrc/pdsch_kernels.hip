@@ -1,0 +1,258 @@
+// MI355X PDSCH receive kernels between the channel estimate and the DL-SCH decoder (paths
+// relative to /root/reference/lib), fused into one pass per resource element (RE):
+//   gather      srslte_pdsch_get (src/phy/phch/pdsch.c:95-234): RE j of the codeword reads grid
+//               position map[j] of the received grid and of the channel estimate (the map is
+//               built on the host for each (cell, grant, lstart, sf_idx) class)
+//   equalise    SISO ZF/MMSE srslte_predecoding_single_multi (src/phy/mimo/precoding.c:154-352):
+//               x = y conj(h) / (|h|^2 + n0) * (1/scaling), summed over 1-2 rx antennas, with the
+//               reference's operation order and no FMA contraction, so x is the reference's float
+//               (CSI mode: csi = |h|^2 + n0, x = y conj(h) (1/scaling) / csi)
+//   demap       srslte_demod_soft_demodulate_s (src/phy/modem/demod_soft.c): the SSE/AVX2
+//               integer path (round-to-nearest, saturating pack, integer offsets) for REs inside
+//               the reference's SIMD blocks and its scalar C tail for the rest
+//   descramble  srslte_scrambling_s_offset with the PDSCH Gold sequence (scrambling.c:48-51,
+//               sequence.c:51-80): LLR negated where c(n) = 1
+//   CSI         pdsch.c:676-776 csi_correction (second pass, needs the codeword's max CSI)
+// The Gold sequence of each codeword is produced by k_gold from two device tables (x1 and the
+// 31 x2 basis sequences of unit seeds, packed 32 bits per word): c = x1 ^ XOR_{seed bit i} x2_i,
+// since x2 is linear in its seed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pdsch_kernels.h"
+
+namespace srsgpu {
+
+__device__ __forceinline__ int16_t sat16(int32_t v) {
+  return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v);
+}
+__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+// x86 cvtps_epi32 / cvttps_epi32: NaN and out-of-range give 0x80000000
+__device__ __forceinline__ int32_t cvt_rn(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)__builtin_rintf(v);
+}
+__device__ __forceinline__ int32_t cvt_rz(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)v;
+}
+__device__ __forceinline__ int16_t abs16(int16_t v) { return wrap16(v < 0 ? -(int32_t)v : v); }
+
+// ------------------------------------------------------------------ Gold sequence ----
+__global__ __launch_bounds__(256) void k_gold(const GoldItem *__restrict__ items, int nitems,
+                                              const uint32_t *__restrict__ x1,
+                                              const uint32_t *__restrict__ x2b, uint32_t words) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  const GoldItem g = items[it];
+  const uint32_t nw = (g.len + 31) / 32;
+  for (uint32_t w = blockIdx.x * 256 + threadIdx.x; w < nw; w += gridDim.x * 256) {
+    // bits n = 32w .. 32w+31 of c are bits 1600 + n of x1 ^ x2 (36.211 7.2)
+    const uint32_t b = 1600 + 32 * w, q = b / 32, r = b % 32;
+    auto word = [&](uint32_t k) {
+      uint32_t v = x1[k];
+      uint32_t s = g.seed;
+      while (s) {
+        const int i = __builtin_ctz(s);
+        v ^= x2b[(size_t)i * words + k];
+        s &= s - 1;
+      }
+      return v;
+    };
+    const uint32_t lo = word(q);
+    const uint32_t v = r ? (lo >> r) | (word(q + 1) << (32 - r)) : lo;
+    g.c[w] = v;
+  }
+}
+
+// ------------------------------------------------------------------ equalise + demap ----
+struct Eq {
+  float xr, xi, csi;
+};
+
+__device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t j) {
+  Eq e;
+  if (!t.csi_mode && (t.nof_re <= 32 || j >= 16 * (t.nof_re / 16))) { // AVX only above 32 (:330)
+    // symbols after the last whole 16 take the reference's C path (precoding.c:231-240), whose
+    // conj() is the double one: products and sums in double, rounded into float accumulators,
+    // then r / ((hh + n0) * scaling)
+    float hh = 0.f, rr = 0.f, ri = 0.f;
+    for (int a = 0; a < t.nrx; a++) {
+      const float2 y = t.y[a][pos], h = t.h[a][pos];
+      const double yr = y.x, yi = y.y, hr = h.x, hi = h.y;
+      rr = (float)__dadd_rn((double)rr, __dsub_rn(__dmul_rn(yr, hr), __dmul_rn(yi, -hi)));
+      ri = (float)__dadd_rn((double)ri, __dadd_rn(__dmul_rn(yr, -hi), __dmul_rn(yi, hr)));
+      hh = (float)__dadd_rn((double)hh, __dadd_rn(__dmul_rn(hr, hr), __dmul_rn(hi, hi)));
+    }
+    const float d = __fmul_rn(__fadd_rn(hh, t.noise), t.scaling);
+    e.csi = d;
+    e.xr = __fdiv_rn(rr, d);
+    e.xi = __fdiv_rn(ri, d);
+    return e;
+  }
+  float hh = 0.f, rr = 0.f, ri = 0.f;
+  for (int a = 0; a < t.nrx; a++) {
+    const float2 y = t.y[a][pos], h = t.h[a][pos];
+    // |h|^2 as hadd(h*h) (precoding.c:179-187), antenna sums in order
+    hh = __fadd_rn(hh, __fadd_rn(__fmul_rn(h.x, h.x), __fmul_rn(h.y, h.y)));
+    // y * conj(h) as PROD_AVX (addsub of products, :150): re = yr*hr - yi*(-hi)
+    rr = __fadd_rn(rr, __fsub_rn(__fmul_rn(y.x, h.x), __fmul_rn(y.y, -h.y)));
+    ri = __fadd_rn(ri, __fadd_rn(__fmul_rn(y.y, h.x), __fmul_rn(y.x, -h.y)));
+  }
+  if (t.csi_mode) { // precoding.c:256-296
+    e.csi = __fadd_rn(hh, t.noise);
+    const float ir = __frcp_rn(e.csi);
+    e.xr = __fmul_rn(__fmul_rn(rr, t.inv_scaling), ir);
+    e.xi = __fmul_rn(__fmul_rn(ri, t.inv_scaling), ir);
+  } else {
+    const float d = t.noise > 0.f ? __fadd_rn(hh, t.noise) : hh;
+    e.csi = d;
+    e.xr = __fmul_rn(__fdiv_rn(rr, d), t.inv_scaling);
+    e.xi = __fmul_rn(__fdiv_rn(ri, d), t.inv_scaling);
+  }
+  return e;
+}
+
+// LLRs of symbol j (q per symbol) into out[0..q)
+__device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr, float xi,
+                                      int16_t *o) {
+  switch (mod) {
+  case 0: // BPSK demod_bpsk_lte_s (demod_soft.c:56-60)
+    o[0] = (int16_t)(int32_t)((double)(-100.0f * (xr + xi)) / 1.4142135623730951);
+    break;
+  case 1: { // QPSK srslte_vec_convert_fi(-100 sqrt 2): 16-float SIMD blocks, C tail
+    const float sc = -141.42135623730951f;
+    const bool simd = 2 * j + 1 < 16 * ((2 * n) / 16);
+    const float a = __fmul_rn(xr, sc), b = __fmul_rn(xi, sc);
+    o[0] = simd ? sat16(cvt_rz(a)) : wrap16(cvt_rz(a));
+    o[1] = simd ? sat16(cvt_rz(b)) : wrap16(cvt_rz(b));
+    break;
+  }
+  case 2: { // 16QAM demod_16qam_lte_s_sse (:96-155)
+    if (j < 4 * (n / 4)) {
+      const int16_t re = sat16(cvt_rn(__fmul_rn(xr, -400.f)));
+      const int16_t im = sat16(cvt_rn(__fmul_rn(xi, -400.f)));
+      o[0] = re;
+      o[1] = im;
+      o[2] = wrap16(abs16(re) - 252);
+      o[3] = wrap16(abs16(im) - 252);
+    } else {
+      const int16_t yre = wrap16(cvt_rz(__fmul_rn(400.f, xr)));
+      const int16_t yim = wrap16(cvt_rz(__fmul_rn(400.f, xi)));
+      o[0] = wrap16(-(int32_t)yre);
+      o[1] = wrap16(-(int32_t)yim);
+      o[2] = wrap16((int32_t)((double)abs(yre) - 252.98221281347036));
+      o[3] = wrap16((int32_t)((double)abs(yim) - 252.98221281347036));
+    }
+    break;
+  }
+  default: { // 64QAM demod_64qam_lte_s_sse (:242-304)
+    if (j < 4 * (n / 4)) {
+      const int16_t re = sat16(cvt_rn(__fmul_rn(xr, -700.f)));
+      const int16_t im = sat16(cvt_rn(__fmul_rn(xi, -700.f)));
+      const int16_t a1r = wrap16(abs16(re) - 432), a1i = wrap16(abs16(im) - 432);
+      o[0] = re;
+      o[1] = im;
+      o[2] = a1r;
+      o[3] = a1i;
+      o[4] = wrap16(abs16(a1r) - 216);
+      o[5] = wrap16(abs16(a1i) - 216);
+    } else {
+      const float yre = (float)wrap16(cvt_rz(__fmul_rn(700.f, xr)));
+      const float yim = (float)wrap16(cvt_rz(__fmul_rn(700.f, xi)));
+      o[0] = wrap16((int32_t)-yre);
+      o[1] = wrap16((int32_t)-yim);
+      o[2] = wrap16((int32_t)((double)abs((int)yre) - 432.04937989385187));
+      o[3] = wrap16((int32_t)((double)abs((int)yim) - 432.04937989385187));
+      o[4] = wrap16((int32_t)((double)abs((int)o[2]) - 216.02468994692594));
+      o[5] = wrap16((int32_t)((double)abs((int)o[3]) - 216.02468994692594));
+    }
+  }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ items, int nitems) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  const LlrItem t = items[it];
+  const int q = t.qm;
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
+    const uint32_t pos = t.map[j];
+    const Eq e = equalise(t, pos, j);
+    int16_t o[6];
+    demap(t.mod, j, t.nof_re, e.xr, e.xi, o);
+    const uint32_t b0 = j * q;
+    for (int k = 0; k < q; k++) {
+      const uint32_t n = b0 + k;
+      const uint32_t c = (t.c[n >> 5] >> (n & 31)) & 1;
+      t.e[n] = c ? wrap16(-(int32_t)o[k]) : o[k]; // _mm256_sign_epi16 by c_short = 1 - 2c
+    }
+    if (t.csi_mode) {
+      t.csi[j] = e.csi;
+      atomicMax(t.csi_max, __float_as_uint(e.csi)); // csi >= 0: uint order == float order
+    }
+  }
+}
+
+// pdsch.c:676-776 (16-bit path): SIMD part mulhi by cvtps(csi * 32767/csi_max) with the
+// reference's lane-to-symbol assignment (QPSK and 64QAM blend the neighbouring symbol's CSI into
+// half of each 4-LLR group), scalar tail (int16)(e * (csi / csi_max)).
+__global__ __launch_bounds__(256) void k_csi_correct(const LlrItem *__restrict__ items, int nitems) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  const LlrItem t = items[it];
+  const uint32_t nbits = t.nof_re * t.qm;
+  const float cmax = __uint_as_float(*t.csi_max);
+  const float scale = __fdiv_rn(32767.f, cmax);
+  uint32_t simd_bits = 0; // bits covered by the SIMD loop
+  if (t.mod == 1 || t.mod == 2)
+    simd_bits = nbits >= 4 ? ((nbits - 4) / 4 + 1) * 4 : 0;
+  else if (t.mod == 3)
+    simd_bits = nbits >= 12 ? ((nbits - 12) / 12 + 1) * 12 : 0;
+  for (uint32_t n = blockIdx.x * 256 + threadIdx.x; n < nbits; n += gridDim.x * 256) {
+    int16_t v = t.e[n];
+    if (n < simd_bits) {
+      uint32_t sym;
+      if (t.mod == 1) { // 4 LLRs = symbols 2g, 2g+1; lanes 0,1 take csi[2g+1], lanes 2,3 csi[2g]
+        const uint32_t g = n / 4, l = n % 4;
+        sym = 2 * g + (l < 2 ? 1 : 0);
+      } else if (t.mod == 2) {
+        sym = n / 4;
+      } else { // 12 LLRs = symbols 2g, 2g+1: e0 <- csi[2g], e1 lanes 0,1 <- csi[2g+1], lanes 2,3
+               // <- csi[2g], e2 <- csi[2g+1]
+        const uint32_t g = n / 12, l = n % 12;
+        sym = l < 4 ? 2 * g : l < 6 ? 2 * g + 1 : l < 8 ? 2 * g : 2 * g + 1;
+      }
+      const int16_t s = sat16(cvt_rn(__fmul_rn(t.csi[sym], scale)));
+      v = (int16_t)(((int32_t)v * (int32_t)s) >> 16);
+    } else {
+      const float c = __fdiv_rn(t.csi[n / t.qm], cmax);
+      v = wrap16(cvt_rz(__fmul_rn((float)v, c)));
+    }
+    t.e[n] = v;
+  }
+}
+
+static inline unsigned cdiv(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,
+                       const uint32_t *x2b, uint32_t words, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned gx = std::min(cdiv(cdiv(max_len, 32), 256), 16u);
+  hipLaunchKernelGGL(k_gold, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n, x1, x2b,
+                     words);
+  return hipGetLastError();
+}
+
+hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned gx = std::min(cdiv(max_re, 256), 64u);
+  hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+  if (csi) {
+    const unsigned gb = std::min(cdiv((size_t)max_re * 6, 256), 256u);
+    hipLaunchKernelGGL(k_csi_correct, dim3(gb ? gb : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+  }
+  return hipGetLastError();
+}
+
+} // namespace srsgpu

@@ -66,6 +66,22 @@ class srsgpu_dlsch_tb_t(ctypes.Structure):
 SOFTBUFFER_SIZE = 18600
 
 
+class srsgpu_cell_t(ctypes.Structure):
+    """include/srsgpu/pdsch_batch.h"""
+    _fields_ = [("nof_prb", ctypes.c_uint32), ("id", ctypes.c_uint32),
+                ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32)]
+
+
+class srsgpu_pdsch_sf_t(ctypes.Structure):
+    """include/srsgpu/pdsch_batch.h"""
+    _fields_ = [("sf_idx", ctypes.c_uint32), ("lstart", ctypes.c_uint32),
+                ("prb_idx", (ctypes.c_uint8 * 110) * 2), ("mod", ctypes.c_uint32),
+                ("nof_re", ctypes.c_uint32), ("rnti", ctypes.c_uint16),
+                ("noise_estimate", ctypes.c_float), ("scaling", ctypes.c_float),
+                ("tbs", ctypes.c_uint32), ("rv", ctypes.c_uint32), ("softbuffer", ctypes.c_uint32),
+                ("grid_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64)]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -111,6 +127,17 @@ _sig = {
                                    ctypes.POINTER(ctypes.c_int32), _u32p]),
     "srsgpu_dlsch_softbuffer_read": (_i32, [_vp, _u32, _i16p, _u8p]),
     "srsgpu_rm_turbo_rx_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
+    "srsgpu_pdsch_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32, _u32,
+                                   _u32]),
+    "srsgpu_pdsch_destroy": (None, [_vp]),
+    "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
+    "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
+    "srsgpu_pdsch_get_dlsch": (_vp, [_vp]),
+    "srsgpu_pdsch_llr_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz, _vp,
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_pdsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz,
+                                       _vp, _u32, _vp, _vp]),
+    "srsgpu_pdsch_nof_re": (_i32, [ctypes.POINTER(srsgpu_cell_t), ctypes.POINTER(srsgpu_pdsch_sf_t)]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
     "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -321,6 +348,68 @@ class Dlsch:
     def close(self):
         if self.q:
             _lib.srsgpu_dlsch_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_sf(sf_idx=1, lstart=1, prb=None, nof_prb=100, mod=3, nof_re=0, rnti=1234, noise=0.0,
+            scaling=1.0, tbs=0, rv=0, softbuffer=0, grid_offset=0, data_offset=0):
+    """srsgpu_pdsch_sf_t from keyword arguments; prb: None (all) or a (2, nof_prb) 0/1 array."""
+    s = srsgpu_pdsch_sf_t()
+    s.sf_idx, s.lstart, s.mod, s.nof_re, s.rnti = sf_idx, lstart, mod, nof_re, rnti
+    s.noise_estimate, s.scaling, s.tbs, s.rv, s.softbuffer = noise, scaling, tbs, rv, softbuffer
+    s.grid_offset, s.data_offset = grid_offset, data_offset
+    m = np.ones((2, nof_prb), np.uint8) if prb is None else np.asarray(prb, np.uint8)
+    for sl in range(2):
+        for n in range(m.shape[1]):
+            s.prb_idx[sl][n] = int(m[sl, n])
+    return s
+
+
+class Pdsch:
+    """srsgpu_pdsch_t: batched PDSCH receive (RE extraction, SISO equalisation, demapping,
+    descrambling, CSI, DL-SCH decoding) on device grids."""
+
+    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, nof_softbuffers=16, max_cb=13,
+                 max_sf=64, stream=None):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+        self.q = _vp()
+        if _lib.srsgpu_pdsch_create(ctypes.byref(self.q), ctypes.byref(self.cell), nof_softbuffers,
+                                    max_cb, max_sf) != 0:
+            raise RuntimeError("srsgpu_pdsch_create failed")
+        if stream is not None:
+            _lib.srsgpu_pdsch_set_stream(self.q, _vp(stream))
+        self.dlsch_q = _lib.srsgpu_pdsch_get_dlsch(self.q)
+
+    def set_csi(self, on):
+        _lib.srsgpu_pdsch_set_csi(self.q, 1 if on else 0)
+
+    def reset_softbuffer(self, slot):
+        if _lib.srsgpu_dlsch_softbuffer_reset(_vp(self.dlsch_q), slot) != 0:
+            raise RuntimeError("softbuffer reset failed")
+
+    def nof_re(self, sf):
+        return _lib.srsgpu_pdsch_nof_re(ctypes.byref(self.cell), ctypes.byref(sf))
+
+    def llr_dev(self, sfs, d_grid, d_ce, ant_stride, d_e, e_offsets):
+        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+        offs = (ctypes.c_uint64 * len(sfs))(*e_offsets)
+        return _lib.srsgpu_pdsch_llr_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
+                                         _vp(d_e), offs)
+
+    def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_data, max_halfits, d_ret, d_noi):
+        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+        return _lib.srsgpu_pdsch_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
+                                            _vp(d_data), max_halfits, _vp(d_ret), _vp(d_noi))
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_pdsch_destroy(self.q)
             self.q = _vp()
 
     def __del__(self):

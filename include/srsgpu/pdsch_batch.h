@@ -1,0 +1,84 @@
+/*
+ * srsgpu batched PDSCH receiver — C ABI of the MI355X (gfx950) path from the received resource
+ * grid and its channel estimate to decoded transport blocks.
+ *
+ * Per subframe and codeword, this follows the reference's srslte_pdsch_decode
+ * (reference: lib/src/phy/phch/pdsch.c:868-1007, srslte_pdsch_codeword_decode :778-835):
+ *   - RE extraction of the grant (srslte_pdsch_get, pdsch.c:95-234);
+ *   - SISO ZF/MMSE equalisation over 1-2 rx antennas (srslte_predecoding_single_multi,
+ *     mimo/precoding.c:243-352), optionally with CSI;
+ *   - soft demapping to int16 LLRs (srslte_demod_soft_demodulate_s, modem/demod_soft.c);
+ *   - descrambling with the PDSCH Gold sequence (scrambling.c:48-51, sequences.c:64-66);
+ *   - optional CSI weighting (csi_correction, pdsch.c:676-776);
+ *   - DL-SCH decoding into the softbuffers of include/srsgpu/dlsch_batch.h.
+ * Everything for a batch of subframes runs as a few fused kernel launches on the handle's
+ * stream.
+ *
+ * Grid layout (as srslte_ofdm_rx_sf produces and srslte_chest_dl_estimate consumes): per
+ * subframe and rx antenna, 14 OFDM symbols x nof_prb*12 subcarriers of complex float. The
+ * channel estimate of CRS port 0 uses the same layout.
+ */
+#ifndef SRSGPU_PDSCH_BATCH_H
+#define SRSGPU_PDSCH_BATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "srsgpu/dlsch_batch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct srsgpu_pdsch srsgpu_pdsch_t;
+
+typedef struct {
+  uint32_t nof_prb;    /* cell bandwidth in PRB (6..110) */
+  uint32_t id;         /* physical cell id (0..503) */
+  uint32_t nof_ports;  /* CRS ports: the RE map skips their reference signals; SISO decoding
+                          needs 1 port */
+  uint32_t nof_rx_ant; /* 1 or 2 */
+} srsgpu_cell_t;
+
+typedef struct {
+  uint32_t sf_idx;          /* subframe index 0..9 */
+  uint32_t lstart;          /* first PDSCH OFDM symbol (srslte_ra_nbits_t.lstart) */
+  uint8_t prb_idx[2][110];  /* srslte_ra_dl_grant_t.prb_idx: PRB allocation per slot */
+  uint32_t mod;             /* srslte_mod_t: 0 BPSK, 1 QPSK, 2 16QAM, 3 64QAM */
+  uint32_t nof_re;          /* srslte_ra_nbits_t.nof_re: must equal the grant's RE count */
+  uint16_t rnti;
+  float noise_estimate;     /* MMSE term (0 = ZF) */
+  float scaling;            /* pdsch_scaling (rho_a, 1.0 by default) */
+  uint32_t tbs, rv, softbuffer;
+  uint64_t grid_offset;     /* this subframe's grid in d_grid / d_ce (complex elements) */
+  uint64_t data_offset;     /* first output byte in d_data */
+} srsgpu_pdsch_sf_t;
+
+/* nof_softbuffers HARQ softbuffers of max_cb code blocks; up to max_sf subframes per call. */
+int srsgpu_pdsch_create(srsgpu_pdsch_t **q, const srsgpu_cell_t *cell, uint32_t nof_softbuffers,
+                        uint32_t max_cb, uint32_t max_sf);
+void srsgpu_pdsch_destroy(srsgpu_pdsch_t *q);
+void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *hip_stream);
+void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable); /* srslte_pdsch_enable_csi */
+/* the DL-SCH engine owning the softbuffers (reset them with srsgpu_dlsch_softbuffer_reset) */
+srsgpu_dlsch_t *srsgpu_pdsch_get_dlsch(srsgpu_pdsch_t *q);
+
+/* LLRs only: d_e receives sf[i].nof_re * Qm descrambled int16 LLRs per subframe at e_offset[i]
+ * (host array). d_grid: [rx antenna] planes of ant_stride complex elements each. */
+int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
+                         const float *d_grid, const float *d_ce, size_t ant_stride, int16_t *d_e,
+                         const uint64_t *e_offset);
+
+/* Full decode: LLRs then DL-SCH. d_ack[i] = 1 when TB i decoded with a good CRC, d_noi[i] =
+ * nof_iterations. Returns -1 on invalid input (RE count mismatch: pdsch.c:886-890). */
+int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
+                            const float *d_grid, const float *d_ce, size_t ant_stride,
+                            uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
+
+/* RE count of a grant (srslte_pdsch_get's return value). */
+int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,239 @@
+/*
+ * CPU ORACLE — TEST INFRASTRUCTURE ONLY. Plain-C restatement of the srsLTE PDSCH receive steps
+ * between the channel estimate and the DL-SCH decoder (paths relative to /root/reference/lib):
+ *   - RE extraction srslte_pdsch_get / srslte_pdsch_cp (src/phy/phch/pdsch.c:95-234) with the
+ *     PRB copy helpers of src/phy/phch/prb_dl.c:51-97, returned as a gather index list;
+ *   - SISO ZF/MMSE equalisation srslte_predecoding_single_multi (src/phy/mimo/precoding.c:
+ *     243-352), plain and with CSI;
+ *   - soft demapping srslte_demod_soft_demodulate_s (src/phy/modem/demod_soft.c:52-456): the
+ *     SSE/AVX2 integer paths (round-to-nearest conversion, saturating pack, integer offsets) for
+ *     whole SIMD blocks and the scalar C tail for the rest, exactly as the reference splits them;
+ *   - the PDSCH scrambling sequence (src/phy/common/sequence.c:51-80, phch/sequences.c:64-66)
+ *     and srslte_scrambling_s_offset (src/phy/scrambling/scrambling.c:48-51).
+ * Only tests/, __graft_entry__.smoke() and bench.py's CPU baseline may use this code.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "pdsch_oracle.h"
+
+/* ---------------------------------------------------------------- RE extraction ---------- */
+/* prb_dl.c:51-82 prb_cp_ref in read mode: skips one input RE before each interval */
+static void cp_ref(uint32_t *in, uint32_t **out, int offset, int nof_refs, int nof_intervals) {
+  const int ri = 12 / nof_refs - 1;
+  for (int j = 0; j < offset; j++) *(*out)++ = (*in)++;
+  for (int i = 0; i < nof_intervals - 1; i++) {
+    (*in)++;
+    for (int j = 0; j < ri; j++) *(*out)++ = (*in)++;
+  }
+  if (ri - offset > 0) {
+    (*in)++;
+    for (int j = 0; j < ri - offset; j++) *(*out)++ = (*in)++;
+  }
+}
+
+static int has_ref(uint32_t l, uint32_t nof_ports) { /* phy_common.h:132-134, normal CP */
+  return (l == 1 && nof_ports == 4) || l == 0 || l == 7 - 3;
+}
+
+int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart_grant,
+                     uint32_t sf_idx, const uint8_t *prb_mask, uint32_t *idx) {
+  const uint32_t nsymb = 7, nof_refs = nof_ports == 1 ? 2 : 4;
+  uint32_t *out = idx;
+  uint32_t offset = 0;
+  for (uint32_t s = 0; s < 2; s++) {
+    for (uint32_t l = 0; l < nsymb; l++) {
+      for (uint32_t n = 0; n < nof_prb; n++) {
+        if (!prb_mask[s * nof_prb + n]) continue;
+        uint32_t lstart = s == 0 ? lstart_grant : 0, lend = nsymb;
+        int is_pbch = 0, is_sss = 0;
+        const int centre = n >= nof_prb / 2 - 3 && n < nof_prb / 2 + 3 + (nof_prb % 2);
+        if (s == 0 && (sf_idx == 0 || sf_idx == 5) && centre) {
+          lend = nsymb - 2;
+          is_sss = 1;
+        }
+        if (s == 1 && sf_idx == 0 && centre) {
+          lstart = 4;
+          is_pbch = 1;
+        }
+        const uint32_t lp = l + s * nsymb;
+        uint32_t in = (lp * nof_prb + n) * 12;
+        if (l >= lstart && l < lend) {
+          if (has_ref(l, nof_ports)) {
+            offset = nof_refs == 2 ? (l == 0 ? cell_id % 6 : (cell_id + 3) % 6) : cell_id % 3;
+            cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs);
+          } else {
+            for (int j = 0; j < 12; j++) *out++ = in++;
+          }
+        }
+        if ((nof_prb % 2) && ((is_pbch && l < lstart) || (is_sss && l >= lend))) {
+          if (n == nof_prb / 2 - 3) {
+            if (has_ref(l, nof_ports))
+              cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs / 2);
+            else
+              for (int j = 0; j < 6; j++) *out++ = in++;
+          } else if (n == nof_prb / 2 + 3) {
+            in += 6;
+            if (has_ref(l, nof_ports))
+              cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs / 2);
+            else
+              for (int j = 0; j < 6; j++) *out++ = in++;
+          }
+        }
+      }
+    }
+  }
+  return (int)(out - idx);
+}
+
+/* ---------------------------------------------------------------- equalisation ---------- */
+void orc_predecode_single(const float *y, const float *h, float *x, float *csi, int n,
+                          float scaling, float noise) {
+  /* float operations in the order of srslte_predecoding_single_avx (:154-230): |h|^2 = hr*hr +
+   * hi*hi, y*conj(h) via the addsub product, divide, then times 1/scaling; symbols past the last
+   * whole 16 use the C path r / ((hh + n0) * scaling) (:231-240) whose conj() is the double
+   * one. CSI mode (:256-296) uses an exact reciprocal where the reference's rcpps is
+   * approximate (tests compare it with a tolerance). */
+  const float inv = 1.0f / scaling;
+  const int simd = n > 32 ? 16 * (n / 16) : 0; /* :330-338: the AVX kernel only above 32 */
+  for (int i = 0; i < n; i++) {
+    const float yr = y[2 * i], yi = y[2 * i + 1], hr = h[2 * i], hi = h[2 * i + 1];
+    const float p1 = hr * hr, p2 = hi * hi;
+    const float hh = p1 + p2;
+    const float a1 = yr * hr, a2 = yi * -hi, b1 = yi * hr, b2 = yr * -hi;
+    const float rr = a1 - a2, ri = b1 + b2;
+    if (csi) {
+      const float c = hh + noise;
+      csi[i] = c;
+      const float r = 1.0f / c;
+      x[2 * i] = rr * inv * r;
+      x[2 * i + 1] = ri * inv * r;
+    } else if (i < simd) {
+      const float d = noise > 0 ? hh + noise : hh;
+      x[2 * i] = rr / d * inv;
+      x[2 * i + 1] = ri / d * inv;
+    } else {
+      /* the C tail multiplies by conj() of double complex: products and sums in double, then
+       * rounded to the float accumulators */
+      const float hd = (float)((double)hr * hr + (double)hi * hi);
+      const float rd = (float)((double)yr * hr - (double)yi * -(double)hi);
+      const float id = (float)((double)yr * -(double)hi + (double)yi * hr);
+      const float d = (hd + noise) * scaling;
+      x[2 * i] = rd / d;
+      x[2 * i + 1] = id / d;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- soft demapping ---------- */
+static int16_t sat16(int64_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
+static int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+
+/* cvtps_epi32 (round to nearest even, MXCSR default) / cvttps_epi32 (truncate): out-of-range
+ * and NaN give the "integer indefinite" 0x80000000 */
+static int32_t cvt_rn(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)rintf(v);
+}
+static int32_t cvt_rz(float v) {
+  if (!(v >= -2147483648.0f && v < 2147483648.0f)) return INT32_MIN;
+  return (int32_t)v;
+}
+static int16_t abs16(int16_t v) { return wrap16(v < 0 ? -(int32_t)v : v); } /* _mm_abs_epi16 */
+
+int orc_demod_s(int mod, const float *sym, int nsym, int16_t *llr) {
+  switch (mod) {
+  case 0: /* BPSK demod_bpsk_lte_s :56-60 */
+    for (int i = 0; i < nsym; i++)
+      llr[i] = (int16_t)(int32_t)(-100 * (sym[2 * i] + sym[2 * i + 1]) / sqrt(2));
+    return 0;
+  case 1: { /* QPSK: srslte_vec_convert_fi(x, -100*sqrt(2)) (vector_simd.c:394-429) */
+    const float scale = (float)(-100 * sqrt(2));
+    const int len = 2 * nsym, simd = 16 * (len / 16);
+    for (int i = 0; i < simd; i++) llr[i] = sat16(cvt_rz(sym[i] * scale));
+    for (int i = simd; i < len; i++) llr[i] = wrap16(cvt_rz(sym[i] * scale));
+    return 0;
+  }
+  case 2: { /* 16QAM demod_16qam_lte_s_sse :96-155 */
+    const int16_t off = (int16_t)(2 * 400 / sqrt(10));
+    const int simd = 4 * (nsym / 4);
+    for (int i = 0; i < simd; i++) {
+      const int16_t re = sat16(cvt_rn(sym[2 * i] * -400.0f));
+      const int16_t im = sat16(cvt_rn(sym[2 * i + 1] * -400.0f));
+      llr[4 * i + 0] = re;
+      llr[4 * i + 1] = im;
+      llr[4 * i + 2] = wrap16(abs16(re) - off);
+      llr[4 * i + 3] = wrap16(abs16(im) - off);
+    }
+    for (int i = simd; i < nsym; i++) {
+      const int16_t yre = (int16_t)(int32_t)(400 * sym[2 * i]);
+      const int16_t yim = (int16_t)(int32_t)(400 * sym[2 * i + 1]);
+      llr[4 * i + 0] = (int16_t)-yre;
+      llr[4 * i + 1] = (int16_t)-yim;
+      llr[4 * i + 2] = (int16_t)(int32_t)(abs(yre) - 2 * 400 / sqrt(10));
+      llr[4 * i + 3] = (int16_t)(int32_t)(abs(yim) - 2 * 400 / sqrt(10));
+    }
+    return 0;
+  }
+  case 3: { /* 64QAM demod_64qam_lte_s_sse :242-304 */
+    const int16_t off1 = (int16_t)(4 * 700 / sqrt(42)), off2 = (int16_t)(2 * 700 / sqrt(42));
+    const int simd = 4 * (nsym / 4);
+    for (int i = 0; i < simd; i++) {
+      const int16_t re = sat16(cvt_rn(sym[2 * i] * -700.0f));
+      const int16_t im = sat16(cvt_rn(sym[2 * i + 1] * -700.0f));
+      const int16_t a1r = wrap16(abs16(re) - off1), a1i = wrap16(abs16(im) - off1);
+      llr[6 * i + 0] = re;
+      llr[6 * i + 1] = im;
+      llr[6 * i + 2] = a1r;
+      llr[6 * i + 3] = a1i;
+      llr[6 * i + 4] = wrap16(abs16(a1r) - off2);
+      llr[6 * i + 5] = wrap16(abs16(a1i) - off2);
+    }
+    for (int i = simd; i < nsym; i++) {
+      const float yre = (int16_t)(int32_t)(700 * sym[2 * i]);
+      const float yim = (int16_t)(int32_t)(700 * sym[2 * i + 1]);
+      llr[6 * i + 0] = (int16_t)(int32_t)-yre;
+      llr[6 * i + 1] = (int16_t)(int32_t)-yim;
+      llr[6 * i + 2] = (int16_t)(int32_t)(abs((int)yre) - 4 * 700 / sqrt(42));
+      llr[6 * i + 3] = (int16_t)(int32_t)(abs((int)yim) - 4 * 700 / sqrt(42));
+      llr[6 * i + 4] = (int16_t)(int32_t)(abs(llr[6 * i + 2]) - 2 * 700 / sqrt(42));
+      llr[6 * i + 5] = (int16_t)(int32_t)(abs(llr[6 * i + 3]) - 2 * 700 / sqrt(42));
+    }
+    return 0;
+  }
+  default:
+    return -1;
+  }
+}
+
+/* ---------------------------------------------------------------- scrambling ---------- */
+int orc_sequence(uint32_t seed, uint32_t len, uint8_t *c) { /* 36.211 7.2, Nc = 1600 */
+  const uint32_t Nc = 1600, tot = Nc + len + 31;
+  uint8_t *x1 = calloc(tot, 1), *x2 = calloc(tot, 1);
+  if (!x1 || !x2) return -1;
+  for (int n = 0; n < 31; n++) x2[n] = (seed >> n) & 1;
+  x1[0] = 1;
+  for (uint32_t n = 0; n < Nc + len; n++) {
+    x1[n + 31] = (x1[n + 3] + x1[n]) & 1;
+    x2[n + 31] = (x2[n + 3] + x2[n + 2] + x2[n + 1] + x2[n]) & 1;
+  }
+  for (uint32_t n = 0; n < len; n++) c[n] = (x1[n + Nc] + x2[n + Nc]) & 1;
+  free(x1);
+  free(x2);
+  return 0;
+}
+
+uint32_t orc_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id) {
+  return ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((nslot / 2) << 9) + cell_id;
+}
+
+int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len) {
+  uint8_t *c = malloc(len + 1);
+  if (!c || orc_sequence(seed, len, c)) return -1;
+  for (uint32_t i = 0; i < len; i++)
+    if (c[i]) llr[i] = wrap16(-(int32_t)llr[i]); /* _mm256_sign_epi16 with c_short = -1 */
+  free(c);
+  return 0;
+}

@@ -1,0 +1,14 @@
+/* CPU ORACLE — TEST INFRASTRUCTURE ONLY (see pdsch_oracle.c). */
+#ifndef SRSGPU_PDSCH_ORACLE_H
+#define SRSGPU_PDSCH_ORACLE_H
+#include <stdint.h>
+
+int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart,
+                     uint32_t sf_idx, const uint8_t *prb_mask, uint32_t *idx);
+void orc_predecode_single(const float *y, const float *h, float *x, float *csi, int n,
+                          float scaling, float noise);
+int orc_demod_s(int mod, const float *sym, int nsym, int16_t *llr);
+int orc_sequence(uint32_t seed, uint32_t len, uint8_t *c);
+uint32_t orc_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
+int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len);
+#endif

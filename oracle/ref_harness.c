@@ -243,3 +243,89 @@ int ref_dlsch_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t 
   for (uint32_t i = 0; i < cfg.cb_segm[0].C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
   return r;
 }
+
+/* ---------------------------------------------------------------- PDSCH front-end ---------- */
+#include "srslte/phy/mimo/precoding.h"
+#include "srslte/phy/modem/demod_soft.h"
+#include "srslte/phy/phch/pdsch.h"
+#include "srslte/phy/common/sequence.h"
+#include "srslte/phy/scrambling/scrambling.h"
+
+/* srslte_demod_soft_demodulate_s (demod_soft.c:437-456): symbols interleaved re/im float32 */
+int ref_demod_s(int mod, const float *sym, int nsym, int16_t *llr) {
+  cf_t *s = NULL;
+  int16_t *l = NULL;
+  if (posix_memalign((void **)&s, 64, (nsym + 16) * sizeof(cf_t))) return -1;
+  if (posix_memalign((void **)&l, 64, (6 * nsym + 64) * sizeof(int16_t))) return -1;
+  memcpy(s, sym, nsym * sizeof(cf_t));
+  int r = srslte_demod_soft_demodulate_s((srslte_mod_t)mod, s, l, nsym);
+  const int bps = mod == SRSLTE_MOD_BPSK ? 1 : mod == SRSLTE_MOD_QPSK ? 2 : mod == SRSLTE_MOD_16QAM ? 4 : 6;
+  memcpy(llr, l, (size_t)bps * nsym * sizeof(int16_t));
+  free(s);
+  free(l);
+  return r;
+}
+
+/* srslte_sequence_pdsch (sequences.c:64-66) bits */
+int ref_sequence_pdsch(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id, uint32_t len, uint8_t *c) {
+  srslte_sequence_t seq;
+  memset(&seq, 0, sizeof(seq));
+  if (srslte_sequence_pdsch(&seq, rnti, q, nslot, cell_id, len)) return -1;
+  memcpy(c, seq.c, len);
+  srslte_sequence_free(&seq);
+  return 0;
+}
+
+/* srslte_scrambling_s_offset (scrambling.c:48-51) with the PDSCH sequence */
+int ref_scramble_pdsch_s(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id, int16_t *llr, uint32_t len) {
+  srslte_sequence_t seq;
+  memset(&seq, 0, sizeof(seq));
+  if (srslte_sequence_pdsch(&seq, rnti, q, nslot, cell_id, len)) return -1;
+  int16_t *l = NULL;
+  if (posix_memalign((void **)&l, 64, (len + 32) * sizeof(int16_t))) return -1;
+  memcpy(l, llr, len * sizeof(int16_t));
+  srslte_scrambling_s_offset(&seq, l, 0, len);
+  memcpy(llr, l, len * sizeof(int16_t));
+  free(l);
+  srslte_sequence_free(&seq);
+  return 0;
+}
+
+/* srslte_predecoding_single_multi, one rx antenna (precoding.c:330-352); csi may be NULL */
+int ref_predecode_single(const float *y, const float *h, float *x, float *csi, int n, float scaling, float noise) {
+  cf_t *yy = NULL, *hh = NULL, *xx = NULL;
+  float *cc = NULL;
+  size_t sz = (n + 32) * sizeof(cf_t);
+  if (posix_memalign((void **)&yy, 64, sz) || posix_memalign((void **)&hh, 64, sz) ||
+      posix_memalign((void **)&xx, 64, sz) || posix_memalign((void **)&cc, 64, sz))
+    return -1;
+  memcpy(yy, y, n * sizeof(cf_t));
+  memcpy(hh, h, n * sizeof(cf_t));
+  cf_t *ya[SRSLTE_MAX_PORTS] = {yy}, *ha[SRSLTE_MAX_PORTS] = {hh};
+  float *ca[SRSLTE_MAX_CODEWORDS] = {csi ? cc : NULL, NULL};
+  int r = srslte_predecoding_single_multi(ya, ha, xx, ca, 1, n, scaling, noise);
+  memcpy(x, xx, n * sizeof(cf_t));
+  if (csi) memcpy(csi, cc, n * sizeof(float));
+  free(yy);
+  free(hh);
+  free(xx);
+  free(cc);
+  return r;
+}
+
+/* srslte_pdsch_get (pdsch.c:95-234, 250-255): RE extraction of one grant from a subframe grid
+ * (nof_prb*12 x 14 cf32); prb_mask[s*nof_prb + n] marks PRB n allocated in slot s. */
+int ref_pdsch_get(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart,
+                  uint32_t sf_idx, const uint8_t *prb_mask, const float *grid, float *out) {
+  srslte_pdsch_t q;
+  memset(&q, 0, sizeof(q));
+  q.cell.nof_prb = nof_prb;
+  q.cell.id = cell_id;
+  q.cell.nof_ports = nof_ports;
+  q.cell.cp = SRSLTE_CP_NORM;
+  srslte_ra_dl_grant_t g;
+  memset(&g, 0, sizeof(g));
+  for (uint32_t s = 0; s < 2; s++)
+    for (uint32_t n = 0; n < nof_prb; n++) g.prb_idx[s][n] = prb_mask[s * nof_prb + n] != 0;
+  return srslte_pdsch_get(&q, (cf_t *)grid, (cf_t *)out, &g, lstart, sf_idx);
+}

@@ -284,3 +284,73 @@ def make_crc_cb(K, ebno_db, seed, poly=CRC24B, oracle=None):
     bits = np.concatenate([data, crcbits])
     coded = o.tcod_encode(bits)
     return bits, awgn_llr(coded, ebno_db, rng)
+
+
+# ------------------------------------------------------------------ PDSCH front-end ----
+_f32p = ctypes.POINTER(ctypes.c_float)
+MOD_BPSK, MOD_QPSK, MOD_16QAM, MOD_64QAM = 0, 1, 2, 3
+BITS_PER_SYMBOL = {MOD_BPSK: 1, MOD_QPSK: 2, MOD_16QAM: 4, MOD_64QAM: 6}
+
+
+class PdschOracle:
+    """Bindings of oracle/pdsch_oracle.c (RE map, SISO equaliser, soft demapper, scrambling)."""
+
+    def __init__(self, oracle):
+        L = self.lib = oracle.lib
+        u32 = ctypes.c_uint32
+        L.orc_pdsch_re_map.argtypes = [u32, u32, u32, u32, u32, _u8p, _u32p]
+        L.orc_predecode_single.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_float,
+                                           ctypes.c_float]
+        L.orc_demod_s.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i16p]
+        L.orc_sequence.argtypes = [u32, u32, _u8p]
+        L.orc_pdsch_seed.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32]
+        L.orc_pdsch_seed.restype = u32
+        L.orc_scramble_s.argtypes = [u32, _i16p, u32]
+
+    def re_map(self, nof_prb, cell_id, nof_ports, lstart, sf_idx, prb_mask):
+        m = np.ascontiguousarray(prb_mask, np.uint8).reshape(-1)
+        idx = np.zeros(nof_prb * 12 * 14, np.uint32)
+        n = self.lib.orc_pdsch_re_map(nof_prb, cell_id, nof_ports, lstart, sf_idx, _ptr(m, _u8p),
+                                      _ptr(idx, _u32p))
+        return idx[:n]
+
+    def predecode(self, y, h, scaling=1.0, noise=0.0, csi=False):
+        y = np.ascontiguousarray(y, np.complex64)
+        h = np.ascontiguousarray(h, np.complex64)
+        x = np.zeros_like(y)
+        c = np.zeros(y.size, np.float32) if csi else None
+        self.lib.orc_predecode_single(y.ctypes.data_as(_f32p), h.ctypes.data_as(_f32p),
+                                      x.ctypes.data_as(_f32p), _ptr(c, _f32p), y.size, scaling, noise)
+        return (x, c) if csi else x
+
+    def demod(self, mod, sym):
+        sym = np.ascontiguousarray(sym, np.complex64)
+        llr = np.zeros(sym.size * BITS_PER_SYMBOL[mod], np.int16)
+        assert self.lib.orc_demod_s(mod, sym.ctypes.data_as(_f32p), sym.size, _ptr(llr, _i16p)) == 0
+        return llr
+
+    def seed(self, rnti, q, nslot, cell_id):
+        return self.lib.orc_pdsch_seed(rnti, q, nslot, cell_id)
+
+    def sequence(self, seed, n):
+        c = np.zeros(n, np.uint8)
+        assert self.lib.orc_sequence(seed, n, _ptr(c, _u8p)) == 0
+        return c
+
+    def scramble(self, seed, llr):
+        llr = np.array(llr, np.int16)
+        assert self.lib.orc_scramble_s(seed, _ptr(llr, _i16p), llr.size) == 0
+        return llr
+
+
+def ref_pdsch(ref):
+    """Attach the PDSCH front-end harness signatures to a Ref instance."""
+    L = ref.lib
+    u32 = ctypes.c_uint32
+    L.ref_demod_s.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i16p]
+    L.ref_sequence_pdsch.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32, u32, _u8p]
+    L.ref_scramble_pdsch_s.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32, _i16p, u32]
+    L.ref_predecode_single.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_float,
+                                       ctypes.c_float]
+    L.ref_pdsch_get.argtypes = [u32, u32, u32, u32, u32, _u8p, _f32p, _f32p]
+    return L
