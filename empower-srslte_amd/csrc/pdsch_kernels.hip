@@ -21,6 +21,10 @@
 
 #include "pdsch_kernels.h"
 
+// The equaliser must round like the reference's separate SSE/AVX multiplies and adds: no FMA
+// contraction anywhere in this file (HIP's __fmul_rn is a plain '*').
+#pragma clang fp contract(off)
+
 namespace srsgpu {
 
 __device__ __forceinline__ int16_t sat16(int32_t v) {

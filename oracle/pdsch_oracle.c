@@ -237,3 +237,48 @@ int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len) {
   free(c);
   return 0;
 }
+
+/* ---------------------------------------------------------------- CSI weighting ---------- */
+/* pdsch.c:676-776 csi_correction, 16-bit path: the SSE loop scales groups of 4 LLRs with
+ * _mm_mulhi_pi16(e, cvtps_pi16(csi * (INT16_MAX / csi_max))) — QPSK and 64QAM blend the next
+ * symbol's CSI into lanes 0-1 of the mixed groups (_mm_blend_ps(.., 3)) — and the C tail does
+ * (int16)(e * (csi / csi_max)). csi_max = max over the codeword's symbols. */
+int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e) {
+  const int qm = mod == 0 ? 1 : mod == 1 ? 2 : mod == 2 ? 4 : 6;
+  const int nbits = nsym * qm;
+  float cmax = -INFINITY;
+  for (int i = 0; i < nsym; i++)
+    if (csi[i] > cmax) cmax = csi[i];
+  if (nsym == 0) cmax = 1.0f;
+  const float scale = 32767.0f / cmax;
+  int i = 0;
+#define MULHI(k, c) e[k] = (int16_t)(((int32_t)e[k] * (int32_t)sat16(cvt_rn((c) * scale))) >> 16)
+  if (mod == 1) {
+    for (; i < nbits - 3; i += 4) {
+      const float c1 = csi[i / 2], c2 = csi[i / 2 + 1];
+      MULHI(i, c2);
+      MULHI(i + 1, c2);
+      MULHI(i + 2, c1);
+      MULHI(i + 3, c1);
+    }
+  } else if (mod == 2) {
+    for (; i < nbits - 3; i += 4)
+      for (int k = 0; k < 4; k++) MULHI(i + k, csi[i / 4]);
+  } else if (mod == 3) {
+    for (; i < nbits - 11; i += 12) {
+      const float c1 = csi[i / 6], c3 = csi[i / 6 + 1];
+      for (int k = 0; k < 4; k++) MULHI(i + k, c1);
+      MULHI(i + 4, c3);
+      MULHI(i + 5, c3);
+      MULHI(i + 6, c1);
+      MULHI(i + 7, c1);
+      for (int k = 8; k < 12; k++) MULHI(i + k, c3);
+    }
+  }
+#undef MULHI
+  for (int sy = i / qm; sy < nsym; sy++) {
+    const float c = csi[sy] / cmax;
+    for (int k = 0; k < qm; k++) e[qm * sy + k] = wrap16(cvt_rz((float)e[qm * sy + k] * c));
+  }
+  return 0;
+}

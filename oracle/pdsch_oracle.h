@@ -11,4 +11,5 @@ int orc_demod_s(int mod, const float *sym, int nsym, int16_t *llr);
 int orc_sequence(uint32_t seed, uint32_t len, uint8_t *c);
 uint32_t orc_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
 int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len);
+int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e);
 #endif

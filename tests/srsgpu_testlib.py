@@ -306,6 +306,13 @@ class PdschOracle:
         L.orc_pdsch_seed.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32]
         L.orc_pdsch_seed.restype = u32
         L.orc_scramble_s.argtypes = [u32, _i16p, u32]
+        L.orc_csi_correction.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i16p]
+
+    def csi_correction(self, mod, csi, llr):
+        csi = np.ascontiguousarray(csi, np.float32)
+        llr = np.array(llr, np.int16)
+        assert self.lib.orc_csi_correction(mod, csi.ctypes.data_as(_f32p), csi.size, _ptr(llr, _i16p)) == 0
+        return llr
 
     def re_map(self, nof_prb, cell_id, nof_ports, lstart, sf_idx, prb_mask):
         m = np.ascontiguousarray(prb_mask, np.uint8).reshape(-1)
