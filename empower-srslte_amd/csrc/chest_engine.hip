@@ -1,0 +1,173 @@
+// Host side of the MI355X CRS channel estimator (include/srsgpu/chest_batch.h): cell-specific
+// reference-signal table and per-call descriptors.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <vector>
+
+#include "chest_kernels.h"
+#include "srsgpu/chest_batch.h"
+#include "tdec_engine.h"
+
+namespace srsgpu {
+
+// CRS of ports 0/1, normal CP (refsignal_dl.c:265-318, 36.211 6.10.1.1): for slot ns and OFDM
+// symbol lp in {0, 4}, c_init = 2^10 (7(ns+1) + lp + 1)(2 N_ID + 1) + 2 N_ID + 1 and
+// r(m) = ((1 - 2c(2m')) + j(1 - 2c(2m'+1))) / sqrt(2), m' = m + 110 - nof_prb.
+static void crs_table(uint32_t nprb, uint32_t id, std::vector<float> &t) {
+  const uint32_t np = 2 * nprb, len = 4 * 110, Nc = 1600;
+  t.assign((size_t)10 * 4 * np * 2, 0.f);
+  std::vector<uint8_t> x1(Nc + len + 31), x2(Nc + len + 31);
+  for (uint32_t ns = 0; ns < 20; ns++)
+    for (uint32_t l = 0; l < 2; l++) {
+      const uint32_t lp = l ? 4 : 0;
+      const uint32_t cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * id + 1) + 2 * id + 1;
+      std::fill(x1.begin(), x1.end(), 0);
+      std::fill(x2.begin(), x2.end(), 0);
+      x1[0] = 1;
+      for (int n = 0; n < 31; n++) x2[n] = (cinit >> n) & 1;
+      for (uint32_t n = 0; n < Nc + len; n++) {
+        x1[n + 31] = (x1[n + 3] + x1[n]) & 1;
+        x2[n + 31] = (x2[n + 3] + x2[n + 2] + x2[n + 1] + x2[n]) & 1;
+      }
+      const uint32_t sf = ns / 2, sym = (ns % 2) * 2 + l;
+      for (uint32_t m = 0; m < np; m++) {
+        const uint32_t mp = m + 110 - nprb;
+        const uint8_t c0 = (x1[2 * mp + Nc] + x2[2 * mp + Nc]) & 1;
+        const uint8_t c1 = (x1[2 * mp + 1 + Nc] + x2[2 * mp + 1 + Nc]) & 1;
+        const size_t o = (((size_t)sf * 4 + sym) * np + m) * 2;
+        t[o] = (float)((1 - 2 * (float)c0) / sqrt(2));
+        t[o + 1] = (float)((1 - 2 * (float)c1) / sqrt(2));
+      }
+    }
+}
+
+struct ChestEngine {
+  hipStream_t st = nullptr;
+  srsgpu_cell_t cell{};
+  uint32_t cap = 0;
+  float2 *d_crs = nullptr;
+  float *d_filt = nullptr;
+  int flen = 3;
+  float filt[16] = {0.1f, 1 - 2 * 0.1f, 0.1f};
+  bool filt_dirty = true;
+  ChestItem *h_items = nullptr, *d_items = nullptr;
+  hipEvent_t staged = nullptr;
+  bool staged_pending = false;
+
+  int create(const srsgpu_cell_t &c, uint32_t n) {
+    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n) {
+      fprintf(stderr, "srsgpu: invalid cell for channel estimation\n");
+      return -1;
+    }
+    cell = c;
+    cap = n;
+    std::vector<float> t;
+    crs_table(c.nof_prb, c.id, t);
+    HIPCHK(hipMalloc(&d_crs, t.size() * 4));
+    HIPCHK(hipMemcpy(d_crs, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&d_filt, 16 * 4));
+    HIPCHK(hipHostMalloc(&h_items, sizeof(ChestItem) * n));
+    HIPCHK(hipMalloc(&d_items, sizeof(ChestItem) * n));
+    HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
+    return 0;
+  }
+
+  void destroy() {
+    if (st) (void)hipStreamSynchronize(st);
+    for (void *p : {(void *)d_crs, (void *)d_filt, (void *)d_items})
+      if (p) (void)hipFree(p);
+    if (h_items) (void)hipHostFree(h_items);
+    if (staged) (void)hipEventDestroy(staged);
+  }
+
+  int estimate(const uint32_t *sf_idx, uint32_t n, const float *d_grid, size_t stride, float *d_ce,
+               float *d_noise) {
+    if (n > cap) {
+      fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
+      return -1;
+    }
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    if (filt_dirty) {
+      HIPCHK(hipMemcpy(d_filt, filt, sizeof(filt), hipMemcpyHostToDevice));
+      filt_dirty = false;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+      if (sf_idx[i] > 9) return -1;
+      ChestItem &t = h_items[i];
+      t.grid = (const float2 *)d_grid + i * stride;
+      t.ce = (float2 *)d_ce + i * stride;
+      t.noise = d_noise ? d_noise + i : nullptr;
+      t.sf_idx = sf_idx[i];
+    }
+    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    // chest_dl.c:620-621: no smoothing for an empty filter or a 3-tap one with w == 0
+    const int fl = (flen == 3 && filt[0] == 0.f) ? 0 : flen;
+    ProfScope ps("k_chest", st);
+    HIPCHK(launch_chest(d_items, (int)n, (int)cell.nof_prb, (int)cell.id, d_crs, d_filt, fl, st));
+    return 0;
+  }
+};
+
+} // namespace srsgpu
+
+struct srsgpu_chest {
+  srsgpu::ChestEngine e;
+};
+
+extern "C" {
+
+int srsgpu_chest_create(srsgpu_chest_t **q, const srsgpu_cell_t *cell, uint32_t n) {
+  if (!q || !cell) return -1;
+  auto *c = new srsgpu_chest();
+  if (c->e.create(*cell, n)) {
+    c->e.destroy();
+    delete c;
+    *q = nullptr;
+    return -1;
+  }
+  *q = c;
+  return 0;
+}
+
+void srsgpu_chest_destroy(srsgpu_chest_t *q) {
+  if (!q) return;
+  q->e.destroy();
+  delete q;
+}
+
+void srsgpu_chest_set_stream(srsgpu_chest_t *q, void *s) {
+  if (q) q->e.st = (hipStream_t)s;
+}
+
+int srsgpu_chest_set_smooth_filter(srsgpu_chest_t *q, const float *f, uint32_t len) {
+  if (!q || len >= 16 || (len && !(len % 2)) || (len && !f)) {
+    fprintf(stderr, "srsgpu: smoothing filter must have an odd length below 16\n");
+    return -1;
+  }
+  q->e.flen = (int)len;
+  for (uint32_t i = 0; i < len; i++) q->e.filt[i] = f[i];
+  q->e.filt_dirty = true;
+  return 0;
+}
+
+void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w) { // chest_dl.c:464-469
+  if (!q) return;
+  q->e.flen = 3;
+  q->e.filt[0] = w;
+  q->e.filt[2] = w;
+  q->e.filt[1] = 1 - 2 * w;
+  q->e.filt_dirty = true;
+}
+
+int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, const float *d_grid,
+                              size_t stride, float *d_ce, float *d_noise) {
+  if (!q || (!sf_idx && n) || !d_grid || !d_ce) return -1;
+  return q->e.estimate(sf_idx, n, d_grid, stride, d_ce, d_noise);
+}
+
+} // extern "C"

@@ -138,6 +138,12 @@ _sig = {
     "srsgpu_pdsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz,
                                        _vp, _u32, _vp, _vp]),
     "srsgpu_pdsch_nof_re": (_i32, [ctypes.POINTER(srsgpu_cell_t), ctypes.POINTER(srsgpu_pdsch_sf_t)]),
+    "srsgpu_chest_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32]),
+    "srsgpu_chest_destroy": (None, [_vp]),
+    "srsgpu_chest_set_stream": (None, [_vp, _vp]),
+    "srsgpu_chest_set_smooth_filter": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _u32]),
+    "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
+    "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
     "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -410,6 +416,43 @@ class Pdsch:
     def close(self):
         if self.q:
             _lib.srsgpu_pdsch_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Chest:
+    """srsgpu_chest_t: batched CRS channel estimation (port 0, normal CP) on device grids."""
+
+    def __init__(self, nof_prb, cell_id, max_grids=64, stream=None):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, 1, 1)
+        self.q = _vp()
+        if _lib.srsgpu_chest_create(ctypes.byref(self.q), ctypes.byref(self.cell), max_grids) != 0:
+            raise RuntimeError("srsgpu_chest_create failed")
+        if stream is not None:
+            _lib.srsgpu_chest_set_stream(self.q, _vp(stream))
+
+    def set_filter(self, taps):
+        arr = (ctypes.c_float * max(1, len(taps)))(*taps)
+        if _lib.srsgpu_chest_set_smooth_filter(self.q, arr, len(taps)) != 0:
+            raise RuntimeError("invalid smoothing filter")
+
+    def set_filter3(self, w):
+        _lib.srsgpu_chest_set_smooth_filter3_coeff(self.q, w)
+
+    def estimate_dev(self, sf_idx, d_grid, stride, d_ce, d_noise=None):
+        n = len(sf_idx)
+        arr = (ctypes.c_uint32 * n)(*sf_idx)
+        return _lib.srsgpu_chest_estimate_dev(self.q, arr, n, _vp(d_grid), stride, _vp(d_ce),
+                                              _vp(d_noise) if d_noise else None)
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_chest_destroy(self.q)
             self.q = _vp()
 
     def __del__(self):

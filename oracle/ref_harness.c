@@ -329,3 +329,34 @@ int ref_pdsch_get(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32
     for (uint32_t n = 0; n < nof_prb; n++) g.prb_idx[s][n] = prb_mask[s * nof_prb + n] != 0;
   return srslte_pdsch_get(&q, (cf_t *)grid, (cf_t *)out, &g, lstart, sf_idx);
 }
+
+/* ---------------------------------------------------------------- CRS (refsignal_dl.c) ---------- */
+#include "srslte/phy/ch_estimation/refsignal_dl.h"
+
+/* port 0/1 CRS of subframe sf_idx: 4 symbols x 2*nof_prb (refsignal_dl.c:265-318) */
+int ref_crs_pilots(uint32_t nof_prb, uint32_t cell_id, uint32_t sf_idx, float *out) {
+  srslte_refsignal_t q;
+  memset(&q, 0, sizeof(q));
+  if (srslte_refsignal_cs_init(&q, nof_prb)) return -1;
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = 1;
+  cell.cp = SRSLTE_CP_NORM;
+  if (srslte_refsignal_cs_set_cell(&q, cell)) return -1;
+  memcpy(out, q.pilots[0][sf_idx], 4 * 2 * nof_prb * sizeof(cf_t));
+  srslte_refsignal_free(&q);
+  return 0;
+}
+
+/* srslte_refsignal_cs_get_sf (refsignal_dl.c:404-430) */
+int ref_crs_get_sf(uint32_t nof_prb, uint32_t cell_id, uint32_t port, const float *grid, float *out) {
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = port < 2 ? 2 : 4;
+  cell.cp = SRSLTE_CP_NORM;
+  return srslte_refsignal_cs_get_sf(cell, port, (cf_t *)grid, (cf_t *)out);
+}
