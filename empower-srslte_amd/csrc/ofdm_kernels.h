@@ -1,0 +1,14 @@
+// Internal launch interface of the OFDM receive FFT (ofdm_kernels.hip).
+#ifndef SRSGPU_OFDM_KERNELS_H
+#define SRSGPU_OFDM_KERNELS_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srsgpu {
+// nsf subframes: in + i*in_stride (15 N samples), out + i*out_stride (14 x nre); tw: N twiddles
+// e^{-2 pi i k / N}; radices: 4-bit radix per stage (first stage in the low nibble)
+hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
+                          int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
+                          hipStream_t st);
+} // namespace srsgpu
+#endif

@@ -144,6 +144,12 @@ _sig = {
     "srsgpu_chest_set_smooth_filter": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _u32]),
     "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
+    "srsgpu_symbol_sz": (_i32, [_u32, _i32]),
+    "srsgpu_ofdm_rx_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32]),
+    "srsgpu_ofdm_rx_destroy": (None, [_vp]),
+    "srsgpu_ofdm_rx_set_stream": (None, [_vp, _vp]),
+    "srsgpu_ofdm_rx_set_normalize": (None, [_vp, _i32]),
+    "srsgpu_ofdm_rx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
     "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -453,6 +459,36 @@ class Chest:
     def close(self):
         if self.q:
             _lib.srsgpu_chest_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def symbol_sz(nof_prb, standard_rates=False):
+    return _lib.srsgpu_symbol_sz(nof_prb, 1 if standard_rates else 0)
+
+
+class OfdmRx:
+    """srsgpu_ofdm_t: batched OFDM receive FFT (normal CP) on device sample buffers."""
+
+    def __init__(self, nof_prb, symbol_size, normalize=False, stream=None):
+        self.q = _vp()
+        if _lib.srsgpu_ofdm_rx_create(ctypes.byref(self.q), nof_prb, symbol_size) != 0:
+            raise RuntimeError("srsgpu_ofdm_rx_create failed")
+        _lib.srsgpu_ofdm_rx_set_normalize(self.q, 1 if normalize else 0)
+        if stream is not None:
+            _lib.srsgpu_ofdm_rx_set_stream(self.q, _vp(stream))
+
+    def rx_dev(self, n, d_in, in_stride, d_out, out_stride):
+        return _lib.srsgpu_ofdm_rx_sf_dev(self.q, n, _vp(d_in), in_stride, _vp(d_out), out_stride)
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_ofdm_rx_destroy(self.q)
             self.q = _vp()
 
     def __del__(self):
