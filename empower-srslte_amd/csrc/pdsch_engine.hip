@@ -77,6 +77,7 @@ struct PdschEngine {
   srsgpu_cell_t cell{};
   uint32_t max_sf = 0;
   bool csi = false;
+  const float *noise_dev = nullptr; // per-subframe chest noise estimates (nof_rx_ant each)
   srsgpu_dlsch_t *dl = nullptr;
   // Gold tables: x1 and the 31 x2 basis sequences, bits 0 .. 32*words-1
   uint32_t gold_words = 0;
@@ -222,6 +223,7 @@ struct PdschEngine {
       t.nrx = (int)cell.nof_rx_ant;
       t.csi_mode = csi ? 1 : 0;
       t.noise = s.noise_estimate;
+      t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant : nullptr;
       t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
       t.inv_scaling = 1.0f / t.scaling;
       mre = std::max(mre, nre);
@@ -276,6 +278,10 @@ void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *s) {
   if (!q) return;
   q->e.st = (hipStream_t)s;
   srsgpu_dlsch_set_stream(q->e.dl, s);
+}
+
+void srsgpu_pdsch_set_noise_dev(srsgpu_pdsch_t *q, const float *d_noise) {
+  if (q) q->e.noise_dev = d_noise;
 }
 
 void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {

@@ -27,6 +27,7 @@ struct LlrItem {
   uint32_t nof_re;
   int qm, mod, nrx, csi_mode;
   float noise, inv_scaling, scaling;
+  const float *noise_dev; // if set: noise = mean over rx antennas of noise_dev[a] (chest output)
 };
 
 hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,

@@ -178,7 +178,12 @@ __device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr,
 __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ items, int nitems) {
   const int it = blockIdx.y;
   if (it >= nitems) return;
-  const LlrItem t = items[it];
+  LlrItem t = items[it];
+  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750), one port
+    float n = 0.f;
+    for (int a = 0; a < t.nrx; a++) n += t.noise_dev[a] / 1.0f;
+    t.noise = n / (float)t.nrx;
+  }
   const int q = t.qm;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
     const uint32_t pos = t.map[j];

@@ -132,6 +132,7 @@ _sig = {
     "srsgpu_pdsch_destroy": (None, [_vp]),
     "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
+    "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
     "srsgpu_pdsch_get_dlsch": (_vp, [_vp]),
     "srsgpu_pdsch_llr_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz, _vp,
                                     ctypes.POINTER(ctypes.c_uint64)]),
@@ -400,6 +401,9 @@ class Pdsch:
 
     def set_csi(self, on):
         _lib.srsgpu_pdsch_set_csi(self.q, 1 if on else 0)
+
+    def set_noise_dev(self, d_noise):
+        _lib.srsgpu_pdsch_set_noise_dev(self.q, _vp(d_noise) if d_noise else None)
 
     def reset_softbuffer(self, slot):
         if _lib.srsgpu_dlsch_softbuffer_reset(_vp(self.dlsch_q), slot) != 0:

@@ -60,6 +60,10 @@ int srsgpu_pdsch_create(srsgpu_pdsch_t **q, const srsgpu_cell_t *cell, uint32_t 
 void srsgpu_pdsch_destroy(srsgpu_pdsch_t *q);
 void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *hip_stream);
 void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable); /* srslte_pdsch_enable_csi */
+/* Take the MMSE noise term from device memory instead of sf[i].noise_estimate: subframe i of a
+ * call uses the mean of d_noise[i*nof_rx_ant + a] (the channel estimator's per-antenna outputs,
+ * as srslte_chest_dl_get_noise_estimate averages them). NULL restores sf[i].noise_estimate. */
+void srsgpu_pdsch_set_noise_dev(srsgpu_pdsch_t *q, const float *d_noise);
 /* the DL-SCH engine owning the softbuffers (reset them with srsgpu_dlsch_softbuffer_reset) */
 srsgpu_dlsch_t *srsgpu_pdsch_get_dlsch(srsgpu_pdsch_t *q);
 
@@ -69,8 +73,9 @@ int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_
                          const float *d_grid, const float *d_ce, size_t ant_stride, int16_t *d_e,
                          const uint64_t *e_offset);
 
-/* Full decode: LLRs then DL-SCH. d_ack[i] = 1 when TB i decoded with a good CRC, d_noi[i] =
- * nof_iterations. Returns -1 on invalid input (RE count mismatch: pdsch.c:886-890). */
+/* Full decode: LLRs then DL-SCH. d_ret[i] = srslte_dlsch_decode2's result for TB i (0: decoded
+ * with a good CRC, i.e. ack; -1: CRC error; -2: invalid TB), d_noi[i] = nof_iterations. Returns
+ * -1 on invalid input (RE count mismatch: pdsch.c:886-890). */
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
                             const float *d_grid, const float *d_ce, size_t ant_stride,
                             uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
