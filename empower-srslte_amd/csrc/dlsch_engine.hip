@@ -112,6 +112,7 @@ struct DlschEngine {
   int16_t *soft = nullptr;   // [nslots * max_cb][SOFTBUFFER_SIZE]
   uint8_t *saved = nullptr;  // [nslots * max_cb][768]
   uint8_t *cbcrc = nullptr;  // [nslots * max_cb]
+  uint8_t *fresh = nullptr;  // [nslots * max_cb]: row reset since last use (counts as zero)
   // per-call device arrays (capacity cap CBs / cap TBs)
   DermItem *d_items = nullptr;
   TbItem *d_tbs = nullptr;
@@ -147,6 +148,8 @@ struct DlschEngine {
     HIPCHK(hipMemset(saved, 0, rows * 768));
     HIPCHK(hipMalloc(&cbcrc, rows));
     HIPCHK(hipMemset(cbcrc, 0, rows));
+    HIPCHK(hipMalloc(&fresh, rows));
+    HIPCHK(hipMemset(fresh, 1, rows));
     HIPCHK(hipMalloc(&d_items, sizeof(DermItem) * cap));
     HIPCHK(hipMalloc(&d_tbs, sizeof(TbItem) * cap));
     HIPCHK(hipMalloc(&d_rows, sizeof(int16_t *) * cap));
@@ -167,7 +170,7 @@ struct DlschEngine {
 
   void destroy() {
     if (st) (void)hipStreamSynchronize(st);
-    for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)d_items, (void *)d_tbs,
+    for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
                     (void *)d_noi, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
                     (void *)data_stage})
@@ -197,11 +200,17 @@ struct DlschEngine {
     return soft + ((size_t)slot * max_cb + cb) * SRSGPU_SOFTBUFFER_SIZE;
   }
 
-  int reset(uint32_t slot, uint32_t ncb) {
-    if (slot >= nslots) return -1;
-    ncb = std::min(ncb, max_cb);
-    HIPCHK(hipMemsetAsync(row(slot, 0), 0, (size_t)ncb * SRSGPU_SOFTBUFFER_SIZE * 2, st));
-    HIPCHK(hipMemsetAsync(cbcrc + (size_t)slot * max_cb, 0, max_cb, st));
+  // srslte_softbuffer_rx_reset(_cb): cb_crc cleared now; the soft bits are zeroed lazily (the
+  // next de-rate-matching pass treats a fresh softbuffer's rows as zero and rewrites them whole)
+  int reset(uint32_t slot, uint32_t count, uint32_t ncb) {
+    if (slot + count > nslots) return -1;
+    if (ncb < max_cb) { // reset_tbs: the first ncb rows only
+      for (uint32_t s = slot; s < slot + count; s++)
+        HIPCHK(hipMemsetAsync(fresh + (size_t)s * max_cb, 1, ncb, st));
+    } else {
+      HIPCHK(hipMemsetAsync(fresh + (size_t)slot * max_cb, 1, (size_t)count * max_cb, st));
+    }
+    HIPCHK(hipMemsetAsync(cbcrc + (size_t)slot * max_cb, 0, (size_t)count * max_cb, st));
     return 0;
   }
 
@@ -279,6 +288,8 @@ struct DlschEngine {
         it.table = tab;
         it.row = row(t.softbuffer, i);
         it.cb_crc = ti.cb_crc + i;
+        it.rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
+        it.fresh = fresh + (size_t)t.softbuffer * max_cb + i;
         max_n = std::max(max_n, std::min(ne, it.N));
         cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
       }
@@ -362,11 +373,17 @@ void srsgpu_dlsch_set_stream(srsgpu_dlsch_t *q, void *s) {
 }
 
 int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t slot) {
-  return q ? q->e.reset(slot, q->e.max_cb) : -1;
+  return q ? q->e.reset(slot, 1, q->e.max_cb) : -1;
+}
+
+int srsgpu_dlsch_softbuffer_reset_range(srsgpu_dlsch_t *q, uint32_t first, uint32_t count) {
+  return q ? q->e.reset(first, count, q->e.max_cb) : -1;
 }
 
 int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t slot, uint32_t tbs) {
-  return q ? q->e.reset(slot, (tbs + 24) / 6120 + 1) : -1; // softbuffer.c:113-116
+  if (!q) return -1;
+  const uint32_t n = (tbs + 24) / 6120 + 1; // softbuffer.c:113-116
+  return q->e.reset(slot, 1, n < q->e.max_cb ? n : q->e.max_cb);
 }
 
 int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,
@@ -434,9 +451,14 @@ int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t
 int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t slot, int16_t *rows, uint8_t *cb_crc) {
   if (!q || slot >= q->e.nslots) return -1;
   DlschEngine &E = q->e;
+  std::vector<uint8_t> fr(E.max_cb);
+  HIPCHK(hipMemcpyAsync(fr.data(), E.fresh + (size_t)slot * E.max_cb, E.max_cb, hipMemcpyDeviceToHost, E.st));
   if (rows)
     HIPCHK(hipMemcpyAsync(rows, E.row(slot, 0), (size_t)E.max_cb * SRSGPU_SOFTBUFFER_SIZE * 2,
                           hipMemcpyDeviceToHost, E.st));
+  HIPCHK(hipStreamSynchronize(E.st));
+  for (uint32_t i = 0; rows && i < E.max_cb; i++) // lazily reset rows read as zero
+    if (fr[i]) memset(rows + (size_t)i * SRSGPU_SOFTBUFFER_SIZE, 0, SRSGPU_SOFTBUFFER_SIZE * 2);
   if (cb_crc)
     HIPCHK(hipMemcpyAsync(cb_crc, E.cbcrc + (size_t)slot * E.max_cb, E.max_cb, hipMemcpyDeviceToHost,
                           E.st));
@@ -459,10 +481,11 @@ int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_ou
   it.row = d_out;
   it.cb_crc = nullptr;
   it.pos = 0;
+  it.fresh = nullptr;
   HIPCHK(hipMemcpyAsync(E.d_items, E.h_items, sizeof(srsgpu::DermItem), hipMemcpyHostToDevice, E.st));
   HIPCHK(hipEventRecord(E.staged, E.st));
   E.staged_pending = true;
-  HIPCHK(srsgpu::launch_derm(E.d_items, 1, std::min(in_len, 3 * K + 12), E.d_init, E.st));
+  HIPCHK(srsgpu::launch_derm_rmw(E.d_items, std::min(in_len, 3 * K + 12), E.st));
   return 0;
 }
 

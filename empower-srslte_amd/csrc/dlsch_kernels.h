@@ -16,6 +16,8 @@ struct DermItem {
   int16_t *row;           // softbuffer row (SOFTBUFFER_SIZE int16)
   const uint8_t *cb_crc;  // softbuffer cb_crc[i]: already decoded -> skipped
   uint32_t pos;           // position in the decoder's (K-grouped) CB order
+  uint32_t rowlen;        // decoder-input length of the row: 3(K+32)+12 (SB) or 3K+12
+  uint8_t *fresh;         // row reset since its last use: content counts as zero (cleared here)
 };
 
 // one transport block's epilogue
@@ -32,6 +34,7 @@ struct TbItem {
 
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
                        hipStream_t st);
+hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,

@@ -13,16 +13,42 @@
 
 #include "dlsch_kernels.h"
 
+#include <algorithm>
+
 namespace srsgpu {
 
+// One workgroup per code block: the softbuffer row is staged in LDS (or starts at zero when the
+// row was reset since its last use: lazy reset, no memset pass over the softbuffers), the
+// E LLRs are scatter-added there and the row is written back with coalesced stores.
+#define DERM_MAXROW (3 * (6144 + 32) + 12)
 __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
                                               uint8_t *__restrict__ init_done) {
-  const int g = blockIdx.y;
+  __shared__ int16_t row[DERM_MAXROW];
+  const int g = blockIdx.x;
   if (g >= nitems) return;
   const DermItem it = items[g];
   const uint8_t skip = it.cb_crc ? *it.cb_crc : 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) init_done[it.pos] = skip;
+  if (threadIdx.x == 0) init_done[it.pos] = skip;
   if (skip) return; // sch.c:323: blocks whose CRC passed before are not combined again
+  const bool fresh = it.fresh && *it.fresh;
+  for (uint32_t p = threadIdx.x; p < it.rowlen; p += blockDim.x) row[p] = fresh ? 0 : it.row[p];
+  __syncthreads();
+  const uint32_t N = it.N;
+  const uint32_t lim = it.ne < N ? it.ne : N;
+  for (uint32_t m = threadIdx.x; m < lim; m += blockDim.x) {
+    uint32_t acc = 0;
+    for (uint32_t i = m; i < it.ne; i += N) acc += (uint16_t)it.e[i];
+    const uint32_t o = it.table[m]; // a bijection: no two m share o
+    row[o] = (int16_t)(uint16_t)((uint16_t)row[o] + acc);
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < it.rowlen; p += blockDim.x) it.row[p] = row[p];
+  if (fresh && threadIdx.x == 0) *it.fresh = 0; // the row now holds real soft bits
+}
+
+// srsgpu_rm_turbo_rx_dev: arbitrary output buffers, read-modify-write in place (one block)
+__global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ items) {
+  const DermItem it = items[0];
   const uint32_t N = it.N;
   const uint32_t lim = it.ne < N ? it.ne : N;
   for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < lim; m += gridDim.x * 256) {
@@ -136,9 +162,14 @@ static inline unsigned cdiv(size_t n, unsigned b) { return (unsigned)((n + b - 1
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
                        hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
-  const unsigned gx = cdiv(max_n, 256) < 32 ? cdiv(max_n, 256) : 32;
-  hipLaunchKernelGGL(k_derm, dim3(gx ? gx : 1, (unsigned)nitems), dim3(256), 0, st, d_items, nitems,
-                     init_done);
+  (void)max_n;
+  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done);
+  return hipGetLastError();
+}
+
+hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st) {
+  const unsigned gx = std::min(cdiv(n, 256), 64u);
+  hipLaunchKernelGGL(k_derm_rmw, dim3(gx ? gx : 1), dim3(256), 0, st, d_item);
   return hipGetLastError();
 }
 

@@ -24,6 +24,50 @@ __device__ __forceinline__ cf mul_mi(cf a) { return {a.y, -a.x}; } // a * (-i)
 
 #define OFDM_MAXN 2048
 
+// one Stockham radix-R pass: d1[(j/Ns) Ns R + j%Ns + r Ns] = DFT_R(tw^(r k) d0[j + r N/R])
+template <int R>
+__device__ __forceinline__ void stage(const cf *__restrict__ d0, cf *__restrict__ d1, int N, int Ns,
+                                      const float2 *__restrict__ tw) {
+  const int nb = N / R;
+  for (int j = threadIdx.x; j < nb; j += blockDim.x) {
+    const int k = j % Ns;
+    const int tstep = k * (N / (Ns * R)); // e^{-2 pi i r k / (Ns R)} = tw[r tstep]
+    cf v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      cf a = d0[j + r * nb];
+      if (r) {
+        const float2 w = tw[r * tstep];
+        a = cmul(a, cf{w.x, w.y});
+      }
+      v[r] = a;
+    }
+    cf y[R];
+    if constexpr (R == 4) {
+      const cf s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+      const cf s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+      y[0] = cadd(s02, s13);
+      y[2] = csub(s02, s13);
+      y[1] = cadd(d02, d13);
+      y[3] = csub(d02, d13);
+    } else if constexpr (R == 2) {
+      y[0] = cadd(v[0], v[1]);
+      y[1] = csub(v[0], v[1]);
+    } else { // R == 3, w = e^{-2 pi i / 3}
+      const float c = -0.5f, sn = -0.86602540378443865f;
+      const cf t = cadd(v[1], v[2]), u = csub(v[1], v[2]);
+      y[0] = cadd(v[0], t);
+      const cf m = {v[0].x + c * t.x, v[0].y + c * t.y};
+      const cf q = {-sn * u.y, sn * u.x}; // i * sn * u
+      y[1] = cadd(m, q);
+      y[2] = csub(m, q);
+    }
+    const int o = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; r++) d1[o + r * Ns] = y[r];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_ofdm_rx(const float2 *__restrict__ in, size_t in_stride,
                                                  float2 *__restrict__ out, size_t out_stride, int N,
                                                  int nre, int cp0, int cp, const float2 *__restrict__ tw,
@@ -37,44 +81,14 @@ __global__ __launch_bounds__(256) void k_ofdm_rx(const float2 *__restrict__ in, 
   for (int n = threadIdx.x; n < N; n += blockDim.x) buf[0][n] = src[n];
   __syncthreads();
   int cur = 0, Ns = 1;
-  for (int s = 0; s < nstages; s++) {
-    const int R = (radices >> (4 * s)) & 15;
-    const int nb = N / R;
-    const cf *d0 = buf[cur];
-    cf *d1 = buf[cur ^ 1];
-    for (int j = threadIdx.x; j < nb; j += blockDim.x) {
-      const int k = j % Ns;
-      // twiddle e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
-      const int tstep = k * (N / (Ns * R));
-      cf v[4];
-      for (int r = 0; r < R; r++) {
-        cf a = d0[j + r * nb];
-        if (r) a = cmul(a, cf{tw[r * tstep].x, tw[r * tstep].y});
-        v[r] = a;
-      }
-      cf y[4];
-      if (R == 4) {
-        const cf s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
-        const cf s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
-        y[0] = cadd(s02, s13);
-        y[2] = csub(s02, s13);
-        y[1] = cadd(d02, d13);
-        y[3] = csub(d02, d13);
-      } else if (R == 2) {
-        y[0] = cadd(v[0], v[1]);
-        y[1] = csub(v[0], v[1]);
-      } else { // R == 3, w = e^{-2 pi i / 3}
-        const float c = -0.5f, sn = -0.86602540378443865f;
-        const cf t = cadd(v[1], v[2]), u = csub(v[1], v[2]);
-        y[0] = cadd(v[0], t);
-        const cf m = {v[0].x + c * t.x, v[0].y + c * t.y};
-        const cf q = {-sn * u.y, sn * u.x}; // i * sn * u
-        y[1] = cadd(m, q);
-        y[2] = csub(m, q);
-      }
-      const int o = (j / Ns) * Ns * R + k;
-      for (int r = 0; r < R; r++) d1[o + r * Ns] = y[r];
-    }
+  for (int st = 0; st < nstages; st++) {
+    const int R = (radices >> (4 * st)) & 15;
+    if (R == 4)
+      stage<4>(buf[cur], buf[cur ^ 1], N, Ns, tw);
+    else if (R == 2)
+      stage<2>(buf[cur], buf[cur ^ 1], N, Ns, tw);
+    else
+      stage<3>(buf[cur], buf[cur ^ 1], N, Ns, tw);
     __syncthreads();
     cur ^= 1;
     Ns *= R;

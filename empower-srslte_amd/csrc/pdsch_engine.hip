@@ -107,7 +107,7 @@ struct PdschEngine {
     max_sf = msf;
     max_re = c.nof_prb * 12 * 14;
     max_bits = max_re * 6;
-    cwords = (max_bits + 31) / 32 + 1;
+    cwords = (max_bits + 31) / 32 + 2;
     if (srsgpu_dlsch_create(&dl, nsb, max_cb, msf * max_cb)) return -1;
     // Gold tables (36.211 7.2): x1(n+31) = x1(n+3) + x1(n), x1 = 1,0,0..; x2 basis i: seed 1 << i
     gold_words = (1600 + max_bits + 64) / 32 + 2;
@@ -222,6 +222,7 @@ struct PdschEngine {
       t.mod = (int)s.mod;
       t.nrx = (int)cell.nof_rx_ant;
       t.csi_mode = csi ? 1 : 0;
+      t.aligned = ((uintptr_t)t.e % 4) == 0;
       t.noise = s.noise_estimate;
       t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant : nullptr;
       t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;

@@ -26,6 +26,7 @@ struct LlrItem {
   uint32_t *csi_max;       // max CSI as float bits (csi_mode; zeroed before the launch)
   uint32_t nof_re;
   int qm, mod, nrx, csi_mode;
+  int aligned;             // e is 4-byte aligned: LLR pairs stored as 32-bit words
   float noise, inv_scaling, scaling;
   const float *noise_dev; // if set: noise = mean over rx antennas of noise_dev[a] (chest output)
 };

@@ -81,8 +81,9 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
     // conj() is the double one: products and sums in double, rounded into float accumulators,
     // then r / ((hh + n0) * scaling)
     float hh = 0.f, rr = 0.f, ri = 0.f;
-    for (int a = 0; a < t.nrx; a++) {
-      const float2 y = t.y[a][pos], h = t.h[a][pos];
+    for (int a = 0; a < 2; a++) {
+      if (a == 1 && t.nrx < 2) break;
+      const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[1][pos] : t.h[0][pos];
       const double yr = y.x, yi = y.y, hr = h.x, hi = h.y;
       rr = (float)__dadd_rn((double)rr, __dsub_rn(__dmul_rn(yr, hr), __dmul_rn(yi, -hi)));
       ri = (float)__dadd_rn((double)ri, __dadd_rn(__dmul_rn(yr, -hi), __dmul_rn(yi, hr)));
@@ -95,8 +96,9 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
     return e;
   }
   float hh = 0.f, rr = 0.f, ri = 0.f;
-  for (int a = 0; a < t.nrx; a++) {
-    const float2 y = t.y[a][pos], h = t.h[a][pos];
+  for (int a = 0; a < 2; a++) {
+    if (a == 1 && t.nrx < 2) break;
+    const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[1][pos] : t.h[0][pos];
     // |h|^2 as hadd(h*h) (precoding.c:179-187), antenna sums in order
     hh = __fadd_rn(hh, __fadd_rn(__fmul_rn(h.x, h.x), __fmul_rn(h.y, h.y)));
     // y * conj(h) as PROD_AVX (addsub of products, :150): re = yr*hr - yi*(-hi)
@@ -175,31 +177,50 @@ __device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr,
   }
 }
 
-__global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ items, int nitems) {
-  const int it = blockIdx.y;
-  if (it >= nitems) return;
-  LlrItem t = items[it];
-  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750), one port
-    float n = 0.f;
-    for (int a = 0; a < t.nrx; a++) n += t.noise_dev[a] / 1.0f;
-    t.noise = n / (float)t.nrx;
-  }
-  const int q = t.qm;
+template <int MOD>
+__device__ __forceinline__ void llr_body(const LlrItem &t) {
+  constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
     const uint32_t pos = t.map[j];
     const Eq e = equalise(t, pos, j);
-    int16_t o[6];
-    demap(t.mod, j, t.nof_re, e.xr, e.xi, o);
-    const uint32_t b0 = j * q;
-    for (int k = 0; k < q; k++) {
-      const uint32_t n = b0 + k;
-      const uint32_t c = (t.c[n >> 5] >> (n & 31)) & 1;
-      t.e[n] = c ? wrap16(-(int32_t)o[k]) : o[k]; // _mm256_sign_epi16 by c_short = 1 - 2c
+    int16_t o[Q];
+    demap(MOD, j, t.nof_re, e.xr, e.xi, o);
+    // scrambling bits b0 .. b0+Q-1 (may straddle two words)
+    const uint32_t b0 = j * Q, w = b0 >> 5, sh = b0 & 31;
+    const uint64_t cw = (uint64_t)t.c[w] | ((uint64_t)t.c[w + 1] << 32);
+    const uint32_t cb = (uint32_t)(cw >> sh);
+#pragma unroll
+    for (int k = 0; k < Q; k++)
+      if ((cb >> k) & 1) o[k] = wrap16(-(int32_t)o[k]); // _mm256_sign_epi16 by c_short = 1 - 2c
+    if (Q % 2 == 0 && t.aligned) {
+      uint32_t *dst = reinterpret_cast<uint32_t *>(t.e + b0);
+#pragma unroll
+      for (int k = 0; k < Q; k += 2) dst[k / 2] = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < Q; k++) t.e[b0 + k] = o[k];
     }
     if (t.csi_mode) {
       t.csi[j] = e.csi;
       atomicMax(t.csi_max, __float_as_uint(e.csi)); // csi >= 0: uint order == float order
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ items, int nitems) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  LlrItem t = items[it];
+  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750), one port
+    float n = t.noise_dev[0];
+    if (t.nrx > 1) n += t.noise_dev[1];
+    t.noise = n / (float)t.nrx;
+  }
+  switch (t.mod) {
+  case 0: llr_body<0>(t); break;
+  case 1: llr_body<1>(t); break;
+  case 2: llr_body<2>(t); break;
+  default: llr_body<3>(t); break;
   }
 }
 

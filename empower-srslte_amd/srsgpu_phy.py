@@ -120,6 +120,7 @@ _sig = {
     "srsgpu_dlsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_dlsch_softbuffer_reset": (_i32, [_vp, _u32]),
     "srsgpu_dlsch_softbuffer_reset_tbs": (_i32, [_vp, _u32, _u32]),
+    "srsgpu_dlsch_softbuffer_reset_range": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp, _u32,
                                        _vp, _vp]),
     "srsgpu_dlsch_decode": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32,
@@ -405,8 +406,10 @@ class Pdsch:
     def set_noise_dev(self, d_noise):
         _lib.srsgpu_pdsch_set_noise_dev(self.q, _vp(d_noise) if d_noise else None)
 
-    def reset_softbuffer(self, slot):
-        if _lib.srsgpu_dlsch_softbuffer_reset(_vp(self.dlsch_q), slot) != 0:
+    def reset_softbuffer(self, slot, count=None):
+        r = (_lib.srsgpu_dlsch_softbuffer_reset(_vp(self.dlsch_q), slot) if count is None else
+             _lib.srsgpu_dlsch_softbuffer_reset_range(_vp(self.dlsch_q), slot, count))
+        if r != 0:
             raise RuntimeError("softbuffer reset failed")
 
     def nof_re(self, sf):

@@ -54,6 +54,8 @@ void srsgpu_dlsch_set_stream(srsgpu_dlsch_t *q, void *hip_stream);
 
 /* srslte_softbuffer_rx_reset (softbuffer.c:125-150): zero the soft bits and the cb_crc flags. */
 int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t softbuffer);
+/* Reset softbuffers first .. first+count-1 in one pass (a batch of new transport blocks). */
+int srsgpu_dlsch_softbuffer_reset_range(srsgpu_dlsch_t *q, uint32_t first, uint32_t count);
 /* srslte_softbuffer_rx_reset_tbs: only the first (tbs+24)/6120+1 code blocks. */
 int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t softbuffer, uint32_t tbs);
 
