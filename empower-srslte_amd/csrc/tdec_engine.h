@@ -70,6 +70,7 @@ struct TdecEngine {
   int16_t *in_stage = nullptr; // host-pointer API staging
   uint8_t *out_stage = nullptr;
   std::map<std::pair<uint32_t, uint32_t>, std::pair<uint16_t *, uint16_t *>> interl;
+  std::map<uint32_t, uint32_t *> crc_tables; // poly -> x^(d+24) mod poly, d < 6144 (k_decide)
   // current job
   uint32_t K = 0;
   int impl_r = 0, nb = 1, ncb = 0, npairs = 0;
@@ -112,6 +113,8 @@ struct TdecEngine {
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
                     (void *)out_stage})
       if (p) (void)hipFree(p);
+    for (auto &kv : crc_tables) (void)hipFree(kv.second);
+    crc_tables.clear();
     for (auto &kv : interl) {
       (void)hipFree(kv.second.first);
       (void)hipFree(kv.second.second);
@@ -197,11 +200,34 @@ struct TdecEngine {
     return 0;
   }
 
+  const uint32_t *crc_table(uint32_t poly) {
+    auto it = crc_tables.find(poly);
+    if (it != crc_tables.end()) return it->second;
+    std::vector<uint32_t> t(6144);
+    uint32_t r = 1u << 23; // x^23; one shift below gives x^24 mod P
+    for (int d = 0; d < 6144; d++) {
+      const uint32_t top = r & 0x800000u;
+      r = (r << 1) & 0xFFFFFFu;
+      if (top) r ^= poly & 0xFFFFFFu;
+      t[d] = r; // x^(d + 24) mod P
+    }
+    uint32_t *dt = nullptr;
+    if (hipMalloc(&dt, t.size() * 4) != hipSuccess) return nullptr;
+    if (hipMemcpy(dt, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    crc_tables.emplace(poly, dt);
+    return dt;
+  }
+
   int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t poly = 0,
              uint32_t crc_bytes = 0, uint32_t maxh = 0) {
+    const uint32_t *pw = nullptr;
+    if (early && crc_bytes) {
+      pw = crc_table(poly);
+      if (!pw) return -1;
+    }
     HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, rev, A, XP1, d_out, out_stride,
                                  early ? cb_done : nullptr, cb_ok, noi, early ? (int)crc_bytes : 0,
-                                 poly, (int)maxh, pair_done, st));
+                                 pw, (int)maxh, pair_done, st));
     return 0;
   }
 

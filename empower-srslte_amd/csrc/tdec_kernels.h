@@ -23,8 +23,10 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
 // hard decision after half-iteration n; with crc_bytes > 0 also CRC + early-stop bookkeeping
 hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *A,
                          const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
-                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, uint32_t poly,
+                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
                          int max_halfits, uint8_t *pair_done, hipStream_t st);
+// crc_pw[d] = x^(d + 24) mod poly (24-bit CRC), d < 6144: the checksum of a crc_bits-bit message is
+// the XOR of crc_pw[crc_bits - 1 - p] over its set bits p
 // pair_done[p] = both CBs of pair p done
 hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done, hipStream_t st);
 } // namespace srsgpu

@@ -1086,9 +1086,10 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
                                                 const s2 *__restrict__ XP1, uint8_t *__restrict__ outb,
                                                 size_t out_stride, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
-                                                int crc_bytes, uint32_t poly, int max_halfits) {
+                                                int crc_bytes, const uint32_t *__restrict__ crc_pw,
+                                                int max_halfits) {
   __shared__ uint32_t bits[2][6144 / 32];
-  __shared__ uint32_t table[256];
+  __shared__ uint32_t red[2][256];
   const int pair = blockIdx.x;
   const int npairs = (ncb + 1) / 2;
   if (pair >= npairs) return;
@@ -1101,21 +1102,15 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
     bits[0][w] = 0;
     bits[1][w] = 0;
   }
-  if (crc_bytes) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-      uint32_t crc = (uint32_t)i << 16;
-      for (int j = 0; j < 8; j++) {
-        uint32_t bit = crc & 0x800000u;
-        crc <<= 1;
-        if (bit) crc ^= poly;
-      }
-      table[i] = crc & 0xFFFFFFu;
-    }
-  }
   __syncthreads();
   const size_t base = (size_t)pair * K;
   const int L = K / NB;
   const s2 *x2 = XP1 + base;
+  // CRC (crc.c:144-155, MSB-first, zero init) is linear: the checksum of the first crc_bits bits
+  // is the XOR over set bits p of x^(crc_bits - 1 - p + 24) mod P = crc_pw[crc_bits - 1 - p], so
+  // every thread folds its own bits and a tree reduction replaces the byte-serial loop.
+  const int crc_bits = 8 * crc_bytes;
+  uint32_t c0 = 0, c1 = 0;
   for (int j = threadIdx.x; j < K; j += blockDim.x) {
     // after the first half-iteration A (app1 - ext1) is still zero and was never written
     s2 v = n == 0 ? x2[rev[j]] : wadd(Aarr[base + j], x2[rev[j]]);
@@ -1123,6 +1118,15 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
     const uint32_t m = 1u << (8 * ((p >> 3) & 3) + 7 - (p & 7)); // byte p/8, bit 7-p%8
     if (v.x > 0) atomicOr(&bits[0][p >> 5], m);
     if (v.y > 0) atomicOr(&bits[1][p >> 5], m);
+    if (p < crc_bits) {
+      const uint32_t w = crc_pw[crc_bits - 1 - p];
+      if (v.x > 0) c0 ^= w;
+      if (v.y > 0) c1 ^= w;
+    }
+  }
+  if (crc_bytes) {
+    red[0][threadIdx.x] = c0;
+    red[1][threadIdx.x] = c1;
   }
   __syncthreads();
   for (int h = 0; h < 2; h++) {
@@ -1131,13 +1135,18 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
     const uint8_t *by = reinterpret_cast<const uint8_t *>(bits[h]);
     for (int b = threadIdx.x; b < K / 8; b += blockDim.x) o[b] = by[b];
   }
-  if (crc_bytes && threadIdx.x < 2) {
+  if (!crc_bytes) return;
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      red[0][threadIdx.x] ^= red[0][threadIdx.x + st];
+      red[1][threadIdx.x] ^= red[1][threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2) {
     const int h = threadIdx.x;
     if (!(h ? skip1 : skip0)) {
-      const uint8_t *by = reinterpret_cast<const uint8_t *>(bits[h]);
-      uint32_t crc = 0;
-      for (int i = 0; i < crc_bytes; i++)
-        crc = ((crc << 8) ^ table[((crc >> 16) & 0xff) ^ by[i]]) & 0xFFFFFFu;
+      const uint32_t crc = red[h][0];
       const int cb = cbs[h];
       noi[cb] = (uint32_t)(n + 1);
       if (crc == 0) {
@@ -1273,11 +1282,11 @@ hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done,
 
 hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *A,
                          const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
-                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, uint32_t poly,
+                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
                          int max_halfits, uint8_t *pair_done, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, rev, (const s2 *)A,
-                     (const s2 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, poly,
+                     (const s2 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, crc_pw,
                      max_halfits);
   if (crc_bytes && pair_done)
     hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
