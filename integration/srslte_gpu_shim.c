@@ -1,0 +1,239 @@
+/*
+ * Reference-side binding: routes the srsLTE receive API onto libsrsgpu_phy.so.
+ *
+ * A maintainer adds this file to srsLTE's srslte_phy library (lib/src/phy/CMakeLists.txt) and
+ * compiles it against srsLTE's own headers. It is not part of this repository's product library.
+ * The GPU side is reached only through this repository's C ABI (include/srsgpu/ headers). The file
+ * defines the receive entry points that srsLTE's ue_dl.c / pdsch_test.c call:
+ *
+ *   srslte_ofdm_rx_sf(q)                 (replaces dft/ofdm.c:460-470 for normal-CP subframes)
+ *   srslte_chest_dl_estimate(q, in, ce, sf_idx)   (chest_dl.c:696-715, CRS port 0)
+ *   srslte_pdsch_decode(q, cfg, sb, sf_symbols, ce, noise, rnti, data, acks)
+ *                                        (pdsch.c:868-1007, SISO / single antenna port)
+ *
+ * Build it with -DSRSGPU_SHIM and drop the three replaced functions from their reference
+ * translation units. The reference objects keep their own state. This file keeps one GPU handle
+ * per object in a small registry keyed by the object's address, because the reference structs
+ * have no spare field. Calls that are out of the GPU path's scope (MBSFN, extended CP, more
+ * than one antenna port) return SRSLTE_ERROR and print a message. There is no hidden CPU path
+ * behind them.
+ * Each call moves one subframe host -> device -> host, as the reference API is per subframe.
+ * Batch users call include/srsgpu/ headers directly and keep the data in HBM.
+ */
+#include <stdbool.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "srslte/phy/ch_estimation/chest_dl.h"
+#include "srslte/phy/dft/ofdm.h"
+#include "srslte/phy/phch/pdsch.h"
+
+#include "srsgpu/chest_batch.h"
+#include "srsgpu/dlsch_batch.h"
+#include "srsgpu/ofdm_batch.h"
+#include "srsgpu/pdsch_batch.h"
+
+/* ---- HIP runtime entry points used for the host <-> device staging (libamdhip64) ---- */
+typedef int hipError_t;
+extern hipError_t hipMalloc(void **ptr, size_t size);
+extern hipError_t hipFree(void *ptr);
+extern hipError_t hipMemcpy(void *dst, const void *src, size_t n, int kind);
+extern hipError_t hipDeviceSynchronize(void);
+#define SHIM_MARK 0x5a5a
+#define H2D 1
+#define D2H 2
+
+/* ---- object registry ---- */
+#define SHIM_MAX 64
+typedef struct {
+  const void *owner;
+  void *gpu;          /* srsgpu_ofdm_t / srsgpu_chest_t / srsgpu_pdsch_t */
+  float *d_a, *d_b, *d_c, *d_d;
+  uint32_t nof_prb, cell_id, symbol_sz;
+  const void *sb[SHIM_MAX]; /* pdsch: softbuffer object -> GPU softbuffer index */
+} shim_entry_t;
+static shim_entry_t shim[SHIM_MAX];
+
+static shim_entry_t *shim_get(const void *owner, bool create) {
+  for (int i = 0; i < SHIM_MAX; i++)
+    if (shim[i].owner == owner) return &shim[i];
+  if (!create) return NULL;
+  for (int i = 0; i < SHIM_MAX; i++)
+    if (!shim[i].owner) {
+      memset(&shim[i], 0, sizeof(shim[i]));
+      shim[i].owner = owner;
+      return &shim[i];
+    }
+  return NULL;
+}
+
+static void shim_drop(shim_entry_t *e) {
+  if (e->d_a) hipFree(e->d_a);
+  if (e->d_b) hipFree(e->d_b);
+  if (e->d_c) hipFree(e->d_c);
+  if (e->d_d) hipFree(e->d_d);
+  memset(e, 0, sizeof(*e));
+}
+
+/* ------------------------------------------------------------------ OFDM ---- */
+void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
+  if (q->cp != SRSLTE_CP_NORM || q->mbsfn_subframe || q->freq_shift) {
+    fprintf(stderr, "srsgpu shim: only normal-CP, non-MBSFN, unshifted OFDM runs on the GPU\n");
+    return;
+  }
+  const uint32_t nof_prb = q->nof_re / SRSLTE_NRE;
+  shim_entry_t *e = shim_get(q, true);
+  if (!e) return;
+  if (e->symbol_sz != q->symbol_sz || e->nof_prb != nof_prb) {
+    if (e->gpu) srsgpu_ofdm_rx_destroy((srsgpu_ofdm_t *)e->gpu);
+    shim_drop(e);
+    e->owner = q;
+    if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz)) return;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * q->sf_sz);
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp));
+    e->symbol_sz = q->symbol_sz;
+    e->nof_prb = nof_prb;
+  }
+  srsgpu_ofdm_rx_set_normalize((srsgpu_ofdm_t *)e->gpu, q->fft_plan.norm);
+  hipMemcpy(e->d_a, q->in_buffer, sizeof(cf_t) * q->sf_sz, H2D);
+  srsgpu_ofdm_rx_sf_dev((srsgpu_ofdm_t *)e->gpu, 1, e->d_a, q->sf_sz, e->d_b,
+                        SRSLTE_SF_LEN_RE(nof_prb, q->cp));
+  hipMemcpy(q->out_buffer, e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp), D2H);
+}
+
+/* ------------------------------------------------------------------ channel estimation ---- */
+int srslte_chest_dl_estimate(srslte_chest_dl_t *q, cf_t *input, cf_t *ce[SRSLTE_MAX_PORTS],
+                             uint32_t sf_idx) {
+  if (q->cell.nof_ports != 1 || q->cell.cp != SRSLTE_CP_NORM || q->average_subframe ||
+      q->noise_alg != SRSLTE_NOISE_ALG_REFS || q->smooth_filter_auto) {
+    fprintf(stderr, "srsgpu shim: GPU channel estimation covers port 0, normal CP, REFS noise\n");
+    return SRSLTE_ERROR;
+  }
+  shim_entry_t *e = shim_get(q, true);
+  if (!e) return SRSLTE_ERROR;
+  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || !e->gpu) {
+    if (e->gpu) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
+    shim_drop(e);
+    e->owner = q;
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, 1, 1};
+    if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 1)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n);
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n);
+    hipMalloc((void **)&e->d_c, sizeof(float));
+    e->nof_prb = q->cell.nof_prb;
+    e->cell_id = q->cell.id;
+  }
+  if (srsgpu_chest_set_smooth_filter((srsgpu_chest_t *)e->gpu, q->smooth_filter, q->smooth_filter_len))
+    return SRSLTE_ERROR;
+  hipMemcpy(e->d_a, input, sizeof(cf_t) * n, H2D);
+  if (srsgpu_chest_estimate_dev((srsgpu_chest_t *)e->gpu, &sf_idx, 1, e->d_a, n, e->d_b, e->d_c))
+    return SRSLTE_ERROR;
+  hipMemcpy(ce[0], e->d_b, sizeof(cf_t) * n, D2H);
+  hipMemcpy(&q->noise_estimate[0][0], e->d_c, sizeof(float), D2H);
+  q->last_nof_antennas = 1;
+  return SRSLTE_SUCCESS;
+}
+
+/* ------------------------------------------------------------------ PDSCH ---- */
+int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
+                        srslte_softbuffer_rx_t *softbuffers[SRSLTE_MAX_CODEWORDS],
+                        cf_t *sf_symbols[SRSLTE_MAX_PORTS], cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS],
+                        float noise_estimate, uint16_t rnti, uint8_t *data[SRSLTE_MAX_CODEWORDS],
+                        bool acks[SRSLTE_MAX_CODEWORDS]) {
+  if (!q || !cfg || !sf_symbols || !data) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (q->cell.nof_ports != 1 || cfg->mimo_type != SRSLTE_MIMO_TYPE_SINGLE_ANTENNA ||
+      q->nof_rx_antennas > 2 || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit) {
+    fprintf(stderr, "srsgpu shim: GPU PDSCH covers single-antenna-port, normal-CP, 16-bit LLRs\n");
+    return SRSLTE_ERROR;
+  }
+  if (!cfg->grant.tb_en[0] || acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
+  shim_entry_t *e = shim_get(q, true);
+  if (!e) return SRSLTE_ERROR;
+  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || !e->gpu) {
+    if (e->gpu) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
+    shim_drop(e);
+    e->owner = q;
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, 1, q->nof_rx_antennas};
+    const uint32_t max_tbs = (uint32_t)srslte_ra_tbs_from_idx(26, q->cell.nof_prb);
+    const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
+    if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2); /* [rx antenna][n] */
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 2);
+    hipMalloc((void **)&e->d_c, SRSGPU_DLSCH_DATA_LEN(max_tbs) + 16);
+    hipMalloc((void **)&e->d_d, 2 * sizeof(int32_t));
+    e->nof_prb = q->cell.nof_prb;
+    e->cell_id = q->cell.id;
+  }
+  srsgpu_pdsch_t *g = (srsgpu_pdsch_t *)e->gpu;
+  srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(g);
+  srslte_softbuffer_rx_t *sb = softbuffers[0];
+  /* softbuffer object -> GPU softbuffer index; a new object starts reset (softbuffer_rx_init) */
+  int slot = -1;
+  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
+    if (e->sb[i] == sb) slot = i;
+  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
+    if (!e->sb[i]) {
+      e->sb[i] = sb;
+      slot = i;
+      srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)i);
+    }
+  if (slot < 0) return SRSLTE_ERROR;
+  /* The soft bits live in HBM; the host rows only carry a marker in element 0 of each code block
+   * row, written after every decode. srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb
+   * (softbuffer.c:127-150) zero a prefix of the rows, so the zeroed prefix length is exactly the
+   * number of rows the caller reset since the last decode. */
+  uint32_t nreset = 0;
+  while (nreset < sb->max_cb && sb->buffer_f[nreset] && sb->buffer_f[nreset][0] != SHIM_MARK) nreset++;
+  if (nreset == sb->max_cb)
+    srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)slot);
+  else if (nreset > 0)
+    srsgpu_dlsch_softbuffer_reset_tbs(dl, (uint32_t)slot, (nreset - 1) * (SRSLTE_TCOD_MAX_LEN_CB - 24));
+
+  srsgpu_pdsch_sf_t sf;
+  memset(&sf, 0, sizeof(sf));
+  sf.sf_idx = cfg->sf_idx;
+  sf.lstart = cfg->nbits[0].lstart;
+  for (int s = 0; s < 2; s++)
+    for (uint32_t p = 0; p < q->cell.nof_prb; p++) sf.prb_idx[s][p] = cfg->grant.prb_idx[s][p];
+  sf.mod = (uint32_t)cfg->grant.mcs[0].mod;
+  sf.nof_re = cfg->nbits[0].nof_re;
+  sf.rnti = rnti;
+  sf.noise_estimate = noise_estimate;
+  sf.scaling = q->rho_a != 0.0f ? q->rho_a : 1.0f;
+  sf.tbs = (uint32_t)cfg->grant.mcs[0].tbs;
+  sf.rv = cfg->rv[0];
+  sf.softbuffer = (uint32_t)slot;
+  for (uint32_t a = 0; a < q->nof_rx_antennas; a++) {
+    hipMemcpy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D);
+    hipMemcpy(e->d_b + 2 * (size_t)a * n, ce[0][a], sizeof(cf_t) * n, H2D);
+  }
+  srsgpu_pdsch_set_csi(g, q->csi_enabled);
+  int32_t *d_ret = (int32_t *)e->d_d;
+  uint32_t *d_noi = (uint32_t *)e->d_d + 1;
+  if (srsgpu_pdsch_decode_dev(g, &sf, 1, e->d_a, e->d_b, (size_t)n, (uint8_t *)e->d_c,
+                              q->dl_sch.max_iterations, d_ret, d_noi))
+    return SRSLTE_ERROR; /* RE count mismatch: pdsch.c:886-890 */
+  int32_t ret = -1;
+  uint32_t noi = 0;
+  hipMemcpy(data[0], e->d_c, (size_t)sf.tbs / 8, D2H);
+  hipMemcpy(&ret, d_ret, sizeof(ret), D2H);
+  hipMemcpy(&noi, d_noi, sizeof(noi), D2H);
+  q->last_nof_iterations[0] = noi;
+  /* srslte_pdsch_codeword_decode (pdsch.c:811-822): ack on a good TB CRC; srslte_pdsch_decode
+   * returns SRSLTE_SUCCESS whatever the codeword result (pdsch.c:966-985) */
+  acks[0] = ret == SRSLTE_SUCCESS;
+  if (ret != SRSLTE_ERROR_INVALID_INPUTS) {
+    /* mirror the code block CRC flags and tb_crc (sch.c:404-408) into the reference object */
+    uint8_t crc[SHIM_MAX];
+    if (srsgpu_dlsch_softbuffer_read(dl, (uint32_t)slot, NULL, crc) == 0) {
+      for (uint32_t i = 0; i < sb->max_cb && i < SHIM_MAX; i++) sb->cb_crc[i] = crc[i] != 0;
+      sb->tb_crc = true;
+      for (uint32_t i = 0; i < cfg->cb_segm[0].C && sb->tb_crc; i++) sb->tb_crc = sb->cb_crc[i];
+    }
+  }
+  for (uint32_t i = 0; i < sb->max_cb; i++)
+    if (sb->buffer_f[i]) sb->buffer_f[i][0] = SHIM_MARK;
+  return SRSLTE_SUCCESS;
+}

@@ -1,0 +1,50 @@
+"""Reference-side binding (integration/srslte_gpu_shim.c).
+
+CPU: the shim type-checks against the reference's own headers (when /root/reference exists).
+GPU: oracle/_ref/shim_check decodes every subframe with the reference's CPU srslte_pdsch_decode
+(pdsch.c:868-1007) and with the shim's GPU version on the same srslte_pdsch_t, grids and HARQ
+sequence (rv 0, 2, 3, 1), and requires identical return value, ack, data bytes,
+last_nof_iterations and softbuffer cb_crc / tb_crc for every transmission. With CSI enabled
+the reference's approximate reciprocal (rcpps) makes failed blocks' bit errors CPU-dependent, so
+their data bytes are compared only when the TB is acked.
+"""
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_INC = "/root/reference/lib/include"
+SHIM = os.path.join(REPO, "integration", "srslte_gpu_shim.c")
+CHECK = os.path.join(REPO, "oracle", "_ref", "shim_check")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INC), reason="reference headers not present")
+def test_shim_typechecks_against_reference_headers():
+    r = subprocess.run(["gcc", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-std=gnu99",
+                        "-I" + REF_INC, "-I" + os.path.join(REPO, "include"), SHIM],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+# nof_prb, cell_id, mcs, cfi, nof_rx, csi, nof_tb, snr_db, seed
+CASES = [
+    (6, 1, 9, 3, 1, 0, 8, 3.0, 1),      # QPSK, 6 PRB, includes subframes 0 and 5
+    (15, 77, 16, 2, 2, 1, 8, 9.0, 2),   # 16QAM, odd PRB count (PBCH half PRBs), 2 rx, CSI
+    (25, 301, 22, 1, 1, 0, 6, 14.0, 3),  # 64QAM, 25 PRB
+    (15, 77, 16, 2, 2, 0, 8, 9.0, 6),   # 2 rx without CSI: every transmission bit-exact
+    (50, 503, 27, 2, 2, 1, 4, 18.0, 4),  # 64QAM, 2 rx, CSI, several code blocks
+    (100, 12, 28, 2, 1, 0, 4, 21.0, 5),  # 100 PRB, 13 code blocks
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[f"prb{c[0]}_mcs{c[2]}_rx{c[4]}_csi{c[5]}" for c in CASES])
+def test_shim_pdsch_decode_matches_reference(case):
+    if not os.path.exists(CHECK):
+        pytest.skip("oracle/_ref/shim_check not built (needs /root/reference at build time)")
+    r = subprocess.run([CHECK] + [str(v) for v in case], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    stats = dict(kv.split("=") for kv in r.stdout.split())
+    assert int(stats["mismatches"]) == 0 and int(stats["tx"]) >= case[6]
