@@ -63,18 +63,22 @@ struct TdecEngine {
   // pair-interleaved arrays [pairs][K]: SP0 short4; XP1 = X2, P1 short2 planes; A short2;
   // T short2 [pairs][12]
   void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr;
+  void *D = nullptr; // [pairs][NB][ceil(K/NB/16)] uint32: packed hard decisions (k_decide input)
   void *scratch = nullptr; // checkpoints (windowed) / alpha-beta (sequential)
   size_t scratch_bytes = 0;
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
   uint32_t *noi = nullptr;
   int16_t *in_stage = nullptr; // host-pointer API staging
   uint8_t *out_stage = nullptr;
-  std::map<std::pair<uint32_t, uint32_t>, std::pair<uint16_t *, uint16_t *>> interl;
+  struct Interl {
+    uint16_t *fwd, *rev, *dmap;
+  };
+  std::map<std::pair<uint32_t, uint32_t>, Interl> interl;
   std::map<uint32_t, uint32_t *> crc_tables; // poly -> x^(d+24) mod poly, d < 6144 (k_decide)
   // current job
   uint32_t K = 0;
   int impl_r = 0, nb = 1, ncb = 0, npairs = 0;
-  const uint16_t *fwd = nullptr, *rev = nullptr;
+  const uint16_t *fwd = nullptr, *rev = nullptr, *dmap = nullptr;
 
   int create(uint32_t max_cbs, uint32_t max_K) {
     if (max_cbs == 0 || max_K == 0 || max_K > SRSLTE_TCOD_MAX_LEN_CB) {
@@ -93,6 +97,7 @@ struct TdecEngine {
     HIPCHK(hipMalloc(&SP0, arr * 2));
     HIPCHK(hipMalloc(&XP1, arr * 2));
     HIPCHK(hipMalloc(&A, arr));
+    HIPCHK(hipMalloc(&D, cap_pairs * (max_K / 16 + 16) * 4));
     HIPCHK(hipMalloc(&T, cap_pairs * 12 * 4));
     size_t ck = 0;
     for (int nbv : {8, 16}) {
@@ -108,17 +113,15 @@ struct TdecEngine {
   }
 
   void destroy() {
-    for (void *p : {SP0, XP1, A, T, scratch})
+    for (void *p : {SP0, XP1, A, D, T, scratch})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
                     (void *)out_stage})
       if (p) (void)hipFree(p);
     for (auto &kv : crc_tables) (void)hipFree(kv.second);
     crc_tables.clear();
-    for (auto &kv : interl) {
-      (void)hipFree(kv.second.first);
-      (void)hipFree(kv.second.second);
-    }
+    for (auto &kv : interl)
+      for (uint16_t *p : {kv.second.fwd, kv.second.rev, kv.second.dmap}) (void)hipFree(p);
     interl.clear();
   }
 
@@ -126,17 +129,26 @@ struct TdecEngine {
     auto key = std::make_pair(Kv, nbv);
     auto it = interl.find(key);
     if (it == interl.end()) {
-      std::vector<uint16_t> f, r;
+      std::vector<uint16_t> f, r, m(Kv);
       gen_interleaver(Kv, nbv, f, r);
-      uint16_t *df = nullptr, *dr = nullptr;
-      HIPCHK(hipMalloc(&df, Kv * 2));
-      HIPCHK(hipMalloc(&dr, Kv * 2));
-      HIPCHK(hipMemcpy(df, f.data(), Kv * 2, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(dr, r.data(), Kv * 2, hipMemcpyHostToDevice));
-      it = interl.emplace(key, std::make_pair(df, dr)).first;
+      // dmap[p]: natural position p -> SB index j -> interleaved index i = rev[j], which DEC2
+      // decodes as step i / NB of chain i % NB: chain-major decision index (k_decide)
+      const uint32_t L = Kv / nbv, G16 = (L + 15) / 16;
+      for (uint32_t p = 0; p < Kv; p++) {
+        const uint32_t j = nbv > 1 ? (p % L) * nbv + p / L : p;
+        const uint32_t i = r[j];
+        m[p] = (uint16_t)((i % nbv) * 16 * G16 + i / nbv);
+      }
+      Interl t{};
+      for (uint16_t **pp : {&t.fwd, &t.rev, &t.dmap}) HIPCHK(hipMalloc(pp, Kv * 2));
+      HIPCHK(hipMemcpy(t.fwd, f.data(), Kv * 2, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(t.rev, r.data(), Kv * 2, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(t.dmap, m.data(), Kv * 2, hipMemcpyHostToDevice));
+      it = interl.emplace(key, t).first;
     }
-    fwd = it->second.first;
-    rev = it->second.second;
+    fwd = it->second.fwd;
+    rev = it->second.rev;
+    dmap = it->second.dmap;
     return 0;
   }
 
@@ -192,11 +204,12 @@ struct TdecEngine {
     return 0;
   }
 
-  int halfit(int n, bool early) {
+  // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)
+  int halfit(int n, bool early, bool dec = true) {
     const uint8_t *pd = early ? pair_done : nullptr;
     const int seq = impl_r == SRSLTE_TDEC_SSE ? 0 : 1;
     ProfScope ps(nb > 1 ? "k_win_halfit" : (seq == 0 ? "k_sse_halfit" : "k_gen_halfit"), st);
-    HIPCHK(srsgpu::launch_halfit(n, nb, seq, SP0, XP1, A, T, fwd, rev, scratch, pd, (int)K, npairs, st));
+    HIPCHK(srsgpu::launch_halfit(n, nb, seq, SP0, XP1, A, dec ? D : nullptr, T, fwd, rev, scratch, pd, (int)K, npairs, st));
     return 0;
   }
 
@@ -225,7 +238,7 @@ struct TdecEngine {
       pw = crc_table(poly);
       if (!pw) return -1;
     }
-    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, rev, A, XP1, d_out, out_stride,
+    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, dmap, D, d_out, out_stride,
                                  early ? cb_done : nullptr, cb_ok, noi, early ? (int)crc_bytes : 0,
                                  pw, (int)maxh, pair_done, st));
     return 0;
@@ -239,7 +252,7 @@ struct TdecEngine {
     }
     if (load(impl, sb_layout, d_in, in_stride, Kv, n)) return -1;
     for (uint32_t h = 0; h < nhalf; h++)
-      if (halfit((int)h, false)) return -1;
+      if (halfit((int)h, false, h + 1 == nhalf)) return -1;
     return decide((int)nhalf - 1, d_out, out_stride, false);
   }
 

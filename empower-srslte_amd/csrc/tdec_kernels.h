@@ -17,12 +17,14 @@ size_t win_ck_bytes(int K, int NB, int npairs);
 size_t seq_scratch_bytes(int K, int npairs);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n). NB > 1: windowed decoder;
 // NB == 1: impl_seq 0 = SSE non-window, 1 = generic.
-hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, const void *T,
+hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, void *D,
+                         const void *T,
                          const uint16_t *fwd, const uint16_t *rev, void *scratch,
                          const uint8_t *pair_done, int K, int npairs, hipStream_t st);
 // hard decision after half-iteration n; with crc_bytes > 0 also CRC + early-stop bookkeeping
-hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *A,
-                         const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
+// dmap: natural position -> chain-major decision index after DEC2 (see tdec_engine.h)
+hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *dmap, const void *D,
+                         uint8_t *outb, size_t out_stride, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
                          int max_halfits, uint8_t *pair_done, hipStream_t st);
 // crc_pw[d] = x^(d + 24) mod poly (24-bit CRC), d < 6144: the checksum of a crc_bits-bit message is

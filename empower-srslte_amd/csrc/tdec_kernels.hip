@@ -220,6 +220,17 @@ __device__ __forceinline__ void store_out(s2 *__restrict__ x2, s2 *__restrict__ 
     x2[t] = v;
 }
 
+// Decision plane D: the hard decisions of the half-iteration, packed in the decoder's own
+// order (chain d, step k): word [pair][d][k / 16] holds CB x's decisions of steps 16h..16h+15 in
+// bits 0-15 and CB y's in bits 16-31. llr > 0 is the reference's decision on ext1 / app1
+// (turbodecoder.c:353-360), since A + app2 reproduces llr exactly modulo 2^16. k_decide maps
+// natural positions onto it (directly after DEC1, through dmap after DEC2).
+// dec_bits: 1 at bit 0 (x) / bit 16 (y) where llr > 0 (two packed ops)
+__device__ __forceinline__ uint32_t dec_bits(s2 llr) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(smax(llr, splat(0)), splat(1)));
+}
+__device__ __forceinline__ int dec_words(int K, int NB) { return NB * ((K / NB + 15) / 16); }
+
 // 8-step chunk of inputs (+ scatter indices + the segment's beta checkpoint) in registers
 struct Chunk {
   s2 x[TD_W], y[TD_W], e[TD_W];
@@ -230,7 +241,8 @@ struct Chunk {
 // ------------------------------------------------------------------ windowed decoder ----
 template <int NB, int DIV, int MODE>
 __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                    s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                    const s2 *__restrict__ T,
                                                     const uint16_t *__restrict__ tbl,
                                                     s4 *__restrict__ ck,
                                                     const uint8_t *__restrict__ pair_done, int K,
@@ -248,6 +260,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
   const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = MODE == 1 ? 6 : 0;
 
@@ -380,7 +393,15 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
   };
 
   // one LLR step at position k = 8q+j from the forward state o and stored beta[k+1]
-  auto llr_step = [&](const Chunk &c, const St8 &b, int j) {
+  uint32_t dacc = 0; // decisions of the current 16-step group
+  const int G16 = (L + 15) / 16;
+  auto dec_flush = [&](int q, bool last) {
+    if (D && ((q & 1) || last)) {
+      D[d * G16 + q / 2] = dacc;
+      dacc = 0;
+    }
+  };
+  auto llr_step = [&](const Chunk &c, const St8 &b, int j, int q) {
     s2 mb[8], nw[8];
     win_alpha_branches(o, c.x[j], c.y[j], mb, nw);
     s2 m0 = sadd(b.s[0], mb[0]);
@@ -393,6 +414,7 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     s2 v = ssub(m1, m0);
     if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
     store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
+    if (D) dacc |= dec_bits(v) << ((q & 1) * 8 + j);
 #pragma unroll
     for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
   };
@@ -412,9 +434,10 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
     }
 #pragma unroll
     for (int j = 0; j < TD_W; j++) {
-      llr_step(c, bst[j], j);
+      llr_step(c, bst[j], j, q);
       if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
     }
+    dec_flush(q, false);
   };
 
   // last segment (steps 8q .. L-1, 1..8 of them)
@@ -439,10 +462,11 @@ __global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, 
 #pragma unroll
     for (int j = 0; j < TD_W; j++) {
       if (j < n) {
-        llr_step(c, bst[j], j);
+        llr_step(c, bst[j], j, q);
         win_norm(s0 + j, o);
       }
     }
+    dec_flush(q, true);
   };
 
   {
@@ -481,9 +505,10 @@ struct ChunkW {
   int t[CW];
 };
 
-template <int NB, int DIV, int MODE, int CW>
+template <int NB, int DIV, int MODE, int CW, bool DOUT>
 __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                   const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    const uint8_t *__restrict__ pair_done, int K,
                                                    int npairs) {
@@ -516,6 +541,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
   s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
   const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = MODE == 1 ? 6 : 0;
 
@@ -579,7 +605,10 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
     return (j == 0 && q == 0) ? splat(0) : o.s[0];
   };
   // LLR at position k from alpha_k (al), the chunk's inputs and stored beta[k+1] (be)
-  auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, s2 mb[8], s2 nw[8]) {
+  static_assert(CW == 16, "decision words hold 16 steps");
+  const int G16 = (L + 15) / 16;
+  auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, uint32_t &dacc,
+                     s2 mb[8], s2 nw[8]) {
     win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
     // max over the 8 branches as a tree (max is exact, so any order is the reference's)
     s2 t0[8], t1[8];
@@ -598,6 +627,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
     s2 v = ssub(t1[0], t0[0]);
     if (DIV) v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
     if (wr) store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
+    if (DOUT) dacc |= dec_bits(v) << j;
   };
 
   St8 o;
@@ -657,6 +687,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
         const int s0 = CW * q;
         const int n = last ? L - s0 : CW;
         St8 bst[CW]; // bst[j] = stored beta[s0+1+j]
+        uint32_t dacc = 0;
         St8 run;
         ck_get(min(q + 1, nc), run);
 #pragma unroll
@@ -675,12 +706,13 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
         for (int j = 0; j < CW; j++) {
           if (j < n) {
             s2 mb[8], nw[8];
-            llr_out(c, o, bst[j], j, mb, nw);
+            llr_out(c, o, bst[j], j, dacc, mb, nw);
 #pragma unroll
             for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
             if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
           }
         }
+        if (DOUT && wr) D[d * G16 + q] = dacc;
       };
       ChunkW<CW> c0, c1;
       int q = qm;
@@ -773,6 +805,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
     {
       auto seg = [&](ChunkW<CW> &c, int q) {
         St8 ast[CW]; // ast[j] = alpha entering step CW*q+j
+        uint32_t dacc = 0;
         ck_get(q, ast[0]);
 #pragma unroll
         for (int j = 0; j < CW - 1; j++) {
@@ -783,13 +816,14 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--) {
           s2 mb[8], nw[8];
-          llr_out(c, ast[j], bpre, j, mb, nw); // bpre = stored beta[k+1]
+          llr_out(c, ast[j], bpre, j, dacc, mb, nw); // bpre = stored beta[k+1]
           // running beta at k+1 (normalised when k+1 is even; k+1 >= 1), then beta[k]
           St8 run = bpre;
           if (((j + 1) & 1) == 0) norm_by(run, run.s[0]);
           win_beta_step(run, c.x[j], c.y[j]);
           bpre = run;
         }
+        if (DOUT && wr) D[d * G16 + q] = dacc;
       };
       ChunkW<CW> c0, c1;
       int q = qm - 1;
@@ -811,7 +845,8 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 // scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
 template <int MODE>
 __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                   const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    s2 *__restrict__ scratch,
                                                    const uint8_t *__restrict__ pair_done, int K,
@@ -824,6 +859,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
   s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
   const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, 1) : nullptr;
   const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = MODE == 1 ? 6 : 0;
   auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
@@ -860,6 +896,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
   b[0] = splat(0);
 #pragma unroll
   for (int i = 1; i < 8; i++) b[i] = splat(-TD_INF);
+  uint32_t dacc = 0;
   for (int k = K + 2; k >= 0; k--) { // :105-206
     s2 g0, g1, e = splat(0);
     if (k >= K) {
@@ -889,6 +926,13 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
       // hMax(bn) - hMax(bp) with hMax(v) = 0x7FFF - max(v) (minpos_epu16 trick, :97-102)
       s2 llr = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
       store_out<MODE == 1>(xp1, A, tbl[k], llr, e);
+      if (D) { // k descends: flush each 16-step group at its first step
+        dacc |= dec_bits(llr) << (k & 15);
+        if ((k & 15) == 0) {
+          D[k >> 4] = dacc;
+          dacc = 0;
+        }
+      }
       if ((k & 3) == 0) {
         s2 z = b[0];
 #pragma unroll
@@ -904,7 +948,8 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
 // scratch: beta (K+4)*8 short2 per pair.
 template <int MODE>
 __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                   s2 *__restrict__ Aarr, const s2 *__restrict__ T,
+                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                   const s2 *__restrict__ T,
                                                    const uint16_t *__restrict__ tbl,
                                                    s2 *__restrict__ scratch,
                                                    const uint8_t *__restrict__ pair_done, int K,
@@ -917,6 +962,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
   s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
   const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
   s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, 1) : nullptr;
   const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = MODE == 1 ? 6 : 0;
   auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
@@ -955,6 +1001,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
   a[0] = splat(0);
 #pragma unroll
   for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
+  uint32_t dacc = 0;
   for (int k = 1; k < K + 1; k++) {
     StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k - 1);
     s2 x = s.x, y = s.y, xy_ = wadd(x, y);
@@ -977,6 +1024,13 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
       for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
     }
     store_out<MODE == 1>(xp1, A, tbl[k - 1], wsub(m1, m0), s.e);
+    if (D) {
+      dacc |= dec_bits(wsub(m1, m0)) << ((k - 1) & 15);
+      if (((k - 1) & 15) == 15 || k == K) {
+        D[(k - 1) >> 4] = dacc;
+        dacc = 0;
+      }
+    }
   }
 }
 
@@ -1076,20 +1130,25 @@ __global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in,
 }
 
 // ------------------------------------------------------------------ decide (+ CRC) ----
-// Hard decision after half-iteration n (turbodecoder.c:353-360 + decision_byte): bit(p) =
-// A[j] + app2[rev[j]] > 0 at the SB index j of natural position p, MSB first. One workgroup
-// per CB pair: bits gathered into an LDS bitmap, then written as bytes. With early stop the
-// same workgroup checks the CRC (crc.c:144-155, sch.c:361-391) and updates the done flags.
+// Hard decision after half-iteration n (turbodecoder.c:353-360 + decision_byte), MSB first,
+// from the decoders' packed decision words D (see dec_bits). One workgroup per CB pair:
+//   1. the pair's words (K/16 of them, 1.5 KB at K = 6144) are staged in LDS;
+//   2. each wave takes 64 consecutive natural positions p. After DEC1 (even n) position
+//      p = d L + k is step k of chain d; after DEC2 dmap[p] gives the chain-major index of the
+//      interleaved position that carries it. Two ballots give the 64 decision bits of each CB,
+//      lanes 0-15 write the 8+8 output bytes, and the CRC (crc.c:144-155, MSB-first, zero
+//      init) is folded from coalesced reads of crc_pw (see below) and reduced.
+// With early stop the same workgroup updates the done flags (sch.c:361-391).
 __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
-                                                const uint16_t *__restrict__ rev,
-                                                const s2 *__restrict__ Aarr,
-                                                const s2 *__restrict__ XP1, uint8_t *__restrict__ outb,
+                                                const uint16_t *__restrict__ dmap,
+                                                const uint32_t *__restrict__ Darr,
+                                                uint8_t *__restrict__ outb,
                                                 size_t out_stride, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
                                                 int crc_bytes, const uint32_t *__restrict__ crc_pw,
                                                 int max_halfits) {
-  __shared__ uint32_t bits[2][6144 / 32];
-  __shared__ uint32_t red[2][256];
+  __shared__ uint32_t dw[6144 / 16 + 16];
+  __shared__ uint32_t red[2][4];
   const int pair = blockIdx.x;
   const int npairs = (ncb + 1) / 2;
   if (pair >= npairs) return;
@@ -1097,56 +1156,69 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
   const bool skip0 = cb_done && cb_done[cbs[0]];
   const bool skip1 = cbs[1] < 0 || (cb_done && cb_done[cbs[1]]);
   if (skip0 && skip1) return;
-  const int nw = (K + 31) / 32;
-  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
-    bits[0][w] = 0;
-    bits[1][w] = 0;
-  }
+  const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
+  const uint32_t *src = Darr + (size_t)pair * nw;
+  for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
   __syncthreads();
-  const size_t base = (size_t)pair * K;
-  const int L = K / NB;
-  const s2 *x2 = XP1 + base;
-  // CRC (crc.c:144-155, MSB-first, zero init) is linear: the checksum of the first crc_bits bits
-  // is the XOR over set bits p of x^(crc_bits - 1 - p + 24) mod P = crc_pw[crc_bits - 1 - p], so
-  // every thread folds its own bits and a tree reduction replaces the byte-serial loop.
+  const bool dec2 = n & 1;
+  // DEC1: p = d L + k -> d * 16 G16 + k; d from a float reciprocal (exact: p < 6144, so the
+  // fraction of (p + 0.5) / L stays >= 1 / (2 L) away from an integer)
+  const float invL = 1.0f / (float)L;
+  const int gap = 16 * G16 - L;
+  auto chain_index = [&](int p) -> int {
+    if (dec2) return (int)dmap[p];
+    const int d = (int)(((float)p + 0.5f) * invL);
+    return p + d * gap;
+  };
+  // CRC is linear: the checksum of the first crc_bits bits is the XOR over set bits p of
+  // x^(crc_bits - 1 - p + 24) mod P = crc_pw[crc_bits - 1 - p].
   const int crc_bits = 8 * crc_bytes;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t c0 = 0, c1 = 0;
-  for (int j = threadIdx.x; j < K; j += blockDim.x) {
-    // after the first half-iteration A (app1 - ext1) is still zero and was never written
-    s2 v = n == 0 ? x2[rev[j]] : wadd(Aarr[base + j], x2[rev[j]]);
-    const int p = NB > 1 ? (j % NB) * L + j / NB : j;
-    const uint32_t m = 1u << (8 * ((p >> 3) & 3) + 7 - (p & 7)); // byte p/8, bit 7-p%8
-    if (v.x > 0) atomicOr(&bits[0][p >> 5], m);
-    if (v.y > 0) atomicOr(&bits[1][p >> 5], m);
-    if (p < crc_bits) {
-      const uint32_t w = crc_pw[crc_bits - 1 - p];
-      if (v.x > 0) c0 ^= w;
-      if (v.y > 0) c1 ^= w;
+  // 4 groups of 64 positions per wave and round, loads issued before use (latency hiding)
+  for (int r0 = wv * 64; r0 < K; r0 += 4 * blockDim.x) {
+    uint32_t dd[4], ww[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int p = r0 + u * blockDim.x + lane;
+      if (p < K) {
+        const int c = chain_index(p);
+        const uint32_t w = dw[c >> 4] >> (c & 15);
+        dd[u] = (w & 1u) | ((w >> 15) & 2u);
+      } else {
+        dd[u] = 0u;
+      }
+      ww[u] = p < crc_bits ? crc_pw[crc_bits - 1 - p] : 0u;
     }
-  }
-  if (crc_bytes) {
-    red[0][threadIdx.x] = c0;
-    red[1][threadIdx.x] = c1;
-  }
-  __syncthreads();
-  for (int h = 0; h < 2; h++) {
-    if (h ? skip1 : skip0) continue;
-    uint8_t *o = outb + (size_t)cbs[h] * out_stride;
-    const uint8_t *by = reinterpret_cast<const uint8_t *>(bits[h]);
-    for (int b = threadIdx.x; b < K / 8; b += blockDim.x) o[b] = by[b];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int p0 = r0 + u * blockDim.x;
+      if (p0 >= K) break;
+      const uint64_t m0 = __ballot(dd[u] & 1u), m1 = __ballot(dd[u] & 2u);
+      if (dd[u] & 1u) c0 ^= ww[u];
+      if (dd[u] & 2u) c1 ^= ww[u];
+      const int h = lane >> 3, b = lane & 7;
+      if (lane < 16 && p0 + 8 * b < K && !(h ? skip1 : skip0)) {
+        const uint32_t v = (uint32_t)(((h ? m1 : m0) >> (8 * b)) & 0xffu);
+        outb[(size_t)cbs[h] * out_stride + (p0 >> 3) + b] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
+      }
+    }
   }
   if (!crc_bytes) return;
-  for (int st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st) {
-      red[0][threadIdx.x] ^= red[0][threadIdx.x + st];
-      red[1][threadIdx.x] ^= red[1][threadIdx.x + st];
-    }
-    __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    c0 ^= __shfl_xor(c0, o);
+    c1 ^= __shfl_xor(c1, o);
   }
+  if (lane == 0) {
+    red[0][wv] = c0;
+    red[1][wv] = c1;
+  }
+  __syncthreads();
   if (threadIdx.x < 2) {
     const int h = threadIdx.x;
     if (!(h ? skip1 : skip0)) {
-      const uint32_t crc = red[h][0];
+      uint32_t crc = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); w++) crc ^= red[h][w];
       const int cb = cbs[h];
       noi[cb] = (uint32_t)(n + 1);
       if (crc == 0) {
@@ -1219,7 +1291,8 @@ size_t win_ck_bytes(int K, int NB, int npairs) {
 
 size_t seq_scratch_bytes(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs * sizeof(s2); }
 
-hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, const void *T,
+hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, void *D,
+                         const void *T,
                          const uint16_t *fwd, const uint16_t *rev, void *scratch,
                          const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
   const bool dec2 = n & 1;
@@ -1228,18 +1301,24 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
   const s4 *sp0 = (const s4 *)SP0;
   s2 *xp1 = (s2 *)XP1;
   s2 *a = (s2 *)A;
+  uint32_t *dp = (uint32_t *)D;
   const s2 *t = (const s2 *)T;
   if (NB > 1) {
     dim3 grid(nblk((size_t)npairs * NB, 256)), blk(256);
     s4 *ck = (s4 *)scratch;
 #define WIN(nb, div, d2)                                                                           \
-  hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, t, tbl, ck,        \
+  hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, dp, t, tbl, ck,    \
                      pair_done, K, npairs)
+#define BIDIR1(nb, div, d2, dout)                                                                  \
+  do {                                                                                             \
+    allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW, dout>));                    \
+    hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW, dout>),                              \
+                       dim3(nblk((size_t)npairs * NB, 64)), dim3(128), bidir_lds, st, sp0, xp1, a, \
+                       dp, t, tbl, pair_done, K, npairs);                                          \
+  } while (0)
 #define BIDIR(nb, div, d2)                                                                         \
   do {                                                                                             \
-    allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW>));                          \
-    hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW>), dim3(nblk((size_t)npairs * NB, 64)), \
-                       dim3(128), bidir_lds, st, sp0, xp1, a, t, tbl, pair_done, K, npairs);         \
+    if (dp) BIDIR1(nb, div, d2, true); else BIDIR1(nb, div, d2, false);                            \
   } while (0)
     static const bool unidir = getenv("SRSGPU_TDEC_UNIDIR") != nullptr;
     const size_t bidir_lds = (size_t)((K / NB + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
@@ -1260,11 +1339,12 @@ hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void
     }
 #undef WIN
 #undef BIDIR
+#undef BIDIR1
   } else {
     dim3 grid(nblk(npairs, 64)), blk(64);
     s2 *sc = (s2 *)scratch;
     if (impl_seq == 0) { // SSE non-window
-#define SEQ(kern, m) hipLaunchKernelGGL(kern<m>, grid, blk, 0, st, sp0, xp1, a, t, tbl, sc, pair_done, K, npairs)
+#define SEQ(kern, m) hipLaunchKernelGGL(kern<m>, grid, blk, 0, st, sp0, xp1, a, dp, t, tbl, sc, pair_done, K, npairs)
       if (mode == 1) SEQ(k_sse_halfit, 1); else if (mode == 2) SEQ(k_sse_halfit, 2); else SEQ(k_sse_halfit, 0);
     } else {
       if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
@@ -1280,13 +1360,13 @@ hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done,
   return hipGetLastError();
 }
 
-hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *rev, const void *A,
-                         const void *XP1, uint8_t *outb, size_t out_stride, uint8_t *cb_done,
+hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *dmap, const void *D,
+                         uint8_t *outb, size_t out_stride, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
                          int max_halfits, uint8_t *pair_done, hipStream_t st) {
   const int npairs = (ncb + 1) / 2;
-  hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, rev, (const s2 *)A,
-                     (const s2 *)XP1, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, crc_pw,
+  hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, dmap,
+                     (const uint32_t *)D, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, crc_pw,
                      max_halfits);
   if (crc_bytes && pair_done)
     hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
