@@ -209,6 +209,24 @@ def run_pipeline(s, torch, dev, steps, warmup):
             "data": "synthetic 64QAM symbols (not codewords: every CB runs 8 half-iterations)"}
 
 
+def reduce_over_ranks(dist, dev, elapsed, bit_errors):
+    """Job time = the slowest rank's timed region (it is bracketed by barriers); bit errors are
+    summed. Identity on a single process."""
+    if not dist:
+        return elapsed, bit_errors
+    import torch
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    e = torch.tensor([bit_errors], device=dev, dtype=torch.int64)
+    dist.all_reduce(e)
+    return float(t.item()), int(e.item())
+
+
+def decoded_mbps(nranks, ncb, k, steps, elapsed):
+    """Whole-job decoded Mbps: every rank decodes its own ncb code blocks per step (weak scaling)."""
+    return nranks * ncb * k * steps / elapsed / 1e6
+
+
 def load_pmc_traffic(workload):
     """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 PMC summary
     (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py), if one matches."""
@@ -285,17 +303,11 @@ def main():
     elapsed = time.perf_counter() - t0
     s.prof_enable(False)
     kern_ms, kern_n = s.prof_get("k_win_halfit")
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        e = torch.tensor([bit_errors], device=dev, dtype=torch.int64)
-        dist.all_reduce(e)
-        bit_errors = int(e.item())
+    elapsed, bit_errors = reduce_over_ranks(dist, dev, elapsed, bit_errors)
 
     nranks = max(1, world)
     bits_total = nranks * NCB * K * args.steps
-    mbps = bits_total / elapsed / 1e6
+    mbps = decoded_mbps(nranks, NCB, K, args.steps, elapsed)
     result = None
     if rank == 0:
         workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
@@ -326,9 +338,8 @@ def main():
     if not args.no_pipeline:
         pipe = run_pipeline(s, torch, dev, max(1, args.steps // 2), 1)
         if dist:
-            t = torch.tensor([pipe["ms_per_batch"]], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            pipe["subframes_per_s"] = round(nranks * C3_SF / (float(t.item()) / 1e3), 1)
+            ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
+            pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
     if rank == 0 and pipe:
         result["config"]["subframes_per_s"] = pipe["subframes_per_s"]
