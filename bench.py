@@ -81,35 +81,39 @@ def cpu_baseline(llr, nthreads):
         def work(rows, out):
             for r in rows:
                 fn(0, 0, r.ctypes.data_as(i16p), K, NHALF, dec.ctypes.data_as(u8p), None, None)
-    # calibrate on two blocks, then size the sample to ~15 s of CPU work: each thread decodes
-    # its own slice of the batch R times
-    scratch = np.zeros((4, K // 8), np.uint8)
+    # size the sample to ~20 s of CPU work (thread-seconds): one threaded pass over the batch
+    # calibrates, then the timed run repeats it R times
+    scratch = np.zeros((1, K // 8), np.uint8)
     work(llr[:1], scratch)  # first call pays the decoder's table set-up
-    t0 = time.perf_counter()
-    work(llr[:4], scratch)
-    per_cb = (time.perf_counter() - t0) / 4
     per_thread = max(1, llr.shape[0] // nthreads)
-    reps = int(max(1, min(64, round(15.0 / nthreads / max(per_cb * per_thread, 1e-6)))))
-
-    def thread_fn(i, out):
-        rows = llr[i * per_thread:(i + 1) * per_thread]
-        for _ in range(reps):
-            work(rows, out)
-
     outs = [np.zeros((per_thread, K // 8), np.uint8) for _ in range(nthreads)]
-    ths = [threading.Thread(target=thread_fn, args=(i, outs[i])) for i in range(nthreads)]
-    t0 = time.perf_counter()
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    wall = time.perf_counter() - t0
+
+    def threaded(reps):
+        def thread_fn(i):
+            rows = llr[i * per_thread:(i + 1) * per_thread]
+            for _ in range(reps):
+                work(rows, outs[i])
+        ths = [threading.Thread(target=thread_fn, args=(i,)) for i in range(nthreads)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        return time.perf_counter() - t0
+
+    reps = 1
+    while True:  # grow R until one timed run holds >= 10 thread-seconds (target 20)
+        wall = threaded(reps)
+        if wall * nthreads >= 10.0 or reps >= 400:
+            break
+        reps = int(min(400, max(reps + 1, np.ceil(reps * 20.0 / (wall * nthreads)))))
     ncb = per_thread * nthreads * reps
     return {"value": round(ncb * K / wall / 1e6, 2), "unit": "Mbps", "cores": nthreads,
             "kind": kind,
             "sample": "%d CB decodes of K=%d (%d threads x %d CBs x %d passes), %d half-iterations, "
-                      "AUTO (AVX2) decoder, natural layout, one srslte_tdec_t per thread, %.1f s wall"
-                      % (ncb, K, nthreads, per_thread, reps, NHALF, wall)}
+                      "AUTO (AVX2) decoder, natural layout, one srslte_tdec_t per thread, %.1f s wall "
+                      "(%.0f thread-seconds)" % (ncb, K, nthreads, per_thread, reps, NHALF, wall,
+                                                 wall * nthreads)}
 
 
 # ---------------------------------------------------------------- C3 subframe pipeline ----
