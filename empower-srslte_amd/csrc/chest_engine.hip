@@ -58,12 +58,13 @@ struct ChestEngine {
   bool staged_pending = false;
 
   int create(const srsgpu_cell_t &c, uint32_t n) {
-    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n) {
-      fprintf(stderr, "srsgpu: invalid cell for channel estimation\n");
+    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || c.nof_ports < 1 || c.nof_ports > 2) {
+      fprintf(stderr, "srsgpu: invalid cell for channel estimation (1 or 2 CRS ports)\n");
       return -1;
     }
     cell = c;
     cap = n;
+    n *= c.nof_ports; // one work item per (grid, port)
     std::vector<float> t;
     crs_table(c.nof_prb, c.id, t);
     HIPCHK(hipMalloc(&d_crs, t.size() * 4));
@@ -94,21 +95,25 @@ struct ChestEngine {
       HIPCHK(hipMemcpy(d_filt, filt, sizeof(filt), hipMemcpyHostToDevice));
       filt_dirty = false;
     }
+    const uint32_t np = cell.nof_ports;
     for (uint32_t i = 0; i < n; i++) {
       if (sf_idx[i] > 9) return -1;
-      ChestItem &t = h_items[i];
-      t.grid = (const float2 *)d_grid + i * stride;
-      t.ce = (float2 *)d_ce + i * stride;
-      t.noise = d_noise ? d_noise + i : nullptr;
-      t.sf_idx = sf_idx[i];
+      for (uint32_t p = 0; p < np; p++) { // srslte_chest_dl_estimate_multi: every port per rx
+        ChestItem &t = h_items[i * np + p];
+        t.grid = (const float2 *)d_grid + i * stride;
+        t.ce = (float2 *)d_ce + (i * np + p) * stride;
+        t.noise = d_noise ? d_noise + i * np + p : nullptr;
+        t.sf_idx = sf_idx[i];
+        t.port = p;
+      }
     }
-    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
     // chest_dl.c:620-621: no smoothing for an empty filter or a 3-tap one with w == 0
     const int fl = (flen == 3 && filt[0] == 0.f) ? 0 : flen;
     ProfScope ps("k_chest", st);
-    HIPCHK(launch_chest(d_items, (int)n, (int)cell.nof_prb, (int)cell.id, d_crs, d_filt, fl, st));
+    HIPCHK(launch_chest(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, d_crs, d_filt, fl, st));
     return 0;
   }
 };

@@ -5,12 +5,13 @@
 #include <stdint.h>
 
 namespace srsgpu {
-// one (subframe, rx antenna): grid and ce are 14 x 12*nof_prb complex planes
+// one (subframe, rx antenna, CRS port): grid and ce are 14 x 12*nof_prb complex planes
 struct ChestItem {
   const float2 *grid;
   float2 *ce;
   float *noise; // noise estimate out (NULL: not computed)
   uint32_t sf_idx;
+  uint32_t port; // 0 or 1: frequency shift v (refsignal_dl.c:40-57)
 };
 // crs: [10 subframes][4 CRS symbols][2*nof_prb] port-0/1 pilots; filt: flen taps (0: no smoothing)
 hipError_t launch_chest(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,

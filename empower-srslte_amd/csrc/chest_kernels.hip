@@ -1,5 +1,5 @@
-// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port for the normal-CP,
-// non-MBSFN, per-symbol (average_subframe off) configuration
+// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0 and 1) for the
+// normal-CP, non-MBSFN, per-symbol (average_subframe off) configuration
 // (reference: lib/src/phy/ch_estimation/chest_dl.c:641-694 and the helpers it calls):
 //   1. least squares   pilots received at the CRS REs of symbols 0/4/7/11 (refsignal_cs_get_sf,
 //                      refsignal_dl.c:404-430) times conj(CRS) (refsignal_dl.c:265-318)
@@ -10,7 +10,7 @@
 //   4. frequency       srslte_interp_linear_offset per CRS symbol (interp.c:245-272), M = 6
 //   5. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:392-397,
 //                      interp.c:150-173): running sums of (ce_b - ce_a) / d
-// One workgroup per (subframe, rx antenna): pilots and their smoothed copy stay in LDS, each
+// One workgroup per (subframe, rx antenna, port): pilots and their smoothed copy stay in LDS, each
 // thread then produces whole subcarrier columns (14 symbols) in registers and streams them out.
 // Float arithmetic in the reference's operation order; the stage is checked with a tolerance
 // (float stages 1e-4 relative).
@@ -48,17 +48,19 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   const c32 *grid = (const c32 *)t.grid;
   const c32 *pil = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);
   const int sym[4] = {0, 4, 7, 11};
-  // 1. LS: port 0, v = 0 (even CRS symbols) / 3 (odd), fidx = (v + id % 6) % 6
+  const int port = (int)t.port;
+  // 1. LS: v = 0 / 3 alternating over the CRS symbols (port 1: 3 / 0), fidx = (v + id % 6) % 6;
+  //    ports 0 and 1 share the pilot sequence (csr_refs.pilots[port / 2])
   for (int e = threadIdx.x; e < 4 * np; e += blockDim.x) {
     const int l = e / np, m = e % np;
-    const int f = ((l & 1 ? 3 : 0) + cell_id % 6) % 6;
+    const int f = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
     ls[l][m] = cmulconj(grid[sym[l] * nsc + f + 6 * m], pil[l * np + m]);
   }
   __syncthreads();
   // 2. noise (REFS): residual of the last CRS symbol against its 4 staggered neighbours in the
   //    symbols around it (bottom one extrapolated as 2 ls[2] - ls[0]), power / 4 * sqrt(5)
   if (t.noise) {
-    const int f0 = (cell_id % 6) % 6;
+    const int f0 = ((port ? 3 : 0) + cell_id % 6) % 6; // srslte_refsignal_cs_fidx(cell, 0, port, 0)
     const int off = f0 < 3 ? 0 : 1; // ((fidx < 3) ^ (4 & 1)) ? 0 : 1
     float acc = 0.f;
     for (int k = threadIdx.x; k < np; k += blockDim.x) {
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   for (int k = threadIdx.x; k < nsc; k += blockDim.x) {
     c32 f[4];
     for (int l = 0; l < 4; l++) {
-      const int fo = ((l & 1 ? 3 : 0) + cell_id % 6) % 6;
+      const int fo = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
       const c32 *in = sm[l];
       if (k < fo) { // output[fo-j-1] = in[0] - (j+1) (in[1]-in[0]) / M
         const int j = fo - 1 - k;

@@ -439,10 +439,11 @@ class Pdsch:
 
 
 class Chest:
-    """srsgpu_chest_t: batched CRS channel estimation (port 0, normal CP) on device grids."""
+    """srsgpu_chest_t: batched CRS channel estimation (ports 0/1, normal CP) on device grids.
+    With nof_ports = 2 grid i yields estimates i*2 (port 0) and i*2 + 1 (port 1)."""
 
-    def __init__(self, nof_prb, cell_id, max_grids=64, stream=None):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, 1, 1)
+    def __init__(self, nof_prb, cell_id, max_grids=64, stream=None, nof_ports=1):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1)
         self.q = _vp()
         if _lib.srsgpu_chest_create(ctypes.byref(self.q), ctypes.byref(self.cell), max_grids) != 0:
             raise RuntimeError("srsgpu_chest_create failed")

@@ -3,7 +3,7 @@
  * estimation (reference: lib/src/phy/ch_estimation/chest_dl.c, srslte_chest_dl_estimate_port
  * :641-664 and the helpers it calls).
  *
- * Supported: CRS port 0 (SISO), normal cyclic prefix, per-symbol estimation
+ * Supported: CRS ports 0 and 1 (cell.nof_ports 1 or 2), normal cyclic prefix, per-symbol estimation
  * (average_subframe off), REFS noise estimation. Processing per grid:
  *   - least-squares pilot estimates;
  *   - optional frequency smoothing (srslte_chest_dl_set_smooth_filter /
@@ -36,8 +36,10 @@ int srsgpu_chest_set_smooth_filter(srsgpu_chest_t *q, const float *filter, uint3
 void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w);
 
 /* Estimate nof_grids grids: grid i (subframe index sf_idx[i], host array) at d_grid + i*stride
- * complex elements, estimate written at d_ce + i*stride, noise estimate at d_noise[i] (may be
- * NULL). Grids of one subframe's rx antennas are simply separate grids. */
+ * complex elements. For every CRS port p of the cell (srslte_chest_dl_estimate_multi order), the
+ * estimate is written at d_ce + (i*nof_ports + p)*stride and the noise estimate at
+ * d_noise[i*nof_ports + p] (d_noise may be NULL). Grids of one subframe's rx antennas are simply
+ * separate grids, so a subframe's estimates come out as [rx antenna][port] planes. */
 int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t nof_grids,
                               const float *d_grid, size_t stride, float *d_ce, float *d_noise);
 

@@ -1,5 +1,5 @@
 """CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's downlink CRS
-channel estimation for port 0, normal CP, per-symbol mode (paths relative to
+channel estimation for CRS ports 0 and 1, normal CP, per-symbol mode (paths relative to
 /root/reference/lib/src/phy):
 
   crs_pilots        ch_estimation/refsignal_dl.c:265-318 (Gold sequence per slot/symbol)
@@ -49,23 +49,24 @@ def crs_pilots(nof_prb, cell_id, sf_idx):
 SYMS = (0, 4, 7, 11)
 
 
-def fidx(cell_id, l):
-    return ((3 if l % 2 else 0) + cell_id % 6) % 6
+def fidx(cell_id, l, port=0):
+    """refsignal_dl.c:40-95: v = 0 / 3 alternating over the CRS symbols, port 1 shifted by 3"""
+    return ((3 if (l % 2) ^ port else 0) + cell_id % 6) % 6
 
 
-def ls_estimates(grid, nof_prb, cell_id, sf_idx):
+def ls_estimates(grid, nof_prb, cell_id, sf_idx, port=0):
     g = grid.reshape(14, 12 * nof_prb)
-    pil = crs_pilots(nof_prb, cell_id, sf_idx)
+    pil = crs_pilots(nof_prb, cell_id, sf_idx)  # ports 0 and 1 share the sequence (pilots[p/2])
     est = np.zeros_like(pil)
     for l, s in enumerate(SYMS):
-        est[l] = g[s, fidx(cell_id, l) + 6 * np.arange(2 * nof_prb)] * np.conj(pil[l])
+        est[l] = g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] * np.conj(pil[l])
     return est
 
 
-def noise_refs(est, cell_id):
+def noise_refs(est, cell_id, port=0):
     n = est.shape[1]
     row3, prev, nxt = est[3], est[2], 2 * est[2] - est[0]
-    off = 0 if fidx(cell_id, 0) < 3 else 1
+    off = 0 if fidx(cell_id, 0, port) < 3 else 1
     tmp = row3.copy()
     for r in (prev, nxt):
         tmp[off:] += r[:n - off]
@@ -110,15 +111,15 @@ def interp_freq(x, off_st, M=6):
     return out
 
 
-def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1)):
-    """-> (ce grid [14 * 12*nof_prb] complex128, noise estimate)"""
-    est = ls_estimates(grid, nof_prb, cell_id, sf_idx)
-    noise = noise_refs(est, cell_id)
+def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0):
+    """-> (ce grid [14 * 12*nof_prb] complex128, noise estimate) of CRS port `port`"""
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+    noise = noise_refs(est, cell_id, port)
     f = np.asarray(filt, np.float64)
     sm = est if (len(f) == 0 or (len(f) == 3 and f[0] == 0)) else np.stack([smooth(r, f) for r in est])
     ce = np.zeros((14, 12 * nof_prb), np.complex128)
     for l, s in enumerate(SYMS):
-        ce[s] = interp_freq(sm[l], fidx(cell_id, l))
+        ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
     for a, b, d, first, cnt in ((0, 4, 4, 1, 3), (4, 7, 3, 5, 2), (7, 11, 4, 8, 3), (7, 11, 4, 12, 2)):
         diff = (ce[b] - ce[a]) / d
         prev = ce[b] if first == 12 else ce[a]

@@ -127,6 +127,82 @@ void orc_predecode_single(const float *y, const float *h, float *x, float *csi, 
   }
 }
 
+/* ---------------------------------------------------------------- TM3: CDD 2x2 MMSE ---------- */
+/* complex float arithmetic in the order gcc evaluates the reference's cf_t expressions (ISO C,
+ * no contraction): (a+bi)(c+di) = (ac - bd) + (ad + bc)i */
+typedef struct {
+  float r, i;
+} orc_cf;
+static orc_cf cf_mul(orc_cf a, orc_cf b) { return (orc_cf){a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+static orc_cf cf_add(orc_cf a, orc_cf b) { return (orc_cf){a.r + b.r, a.i + b.i}; }
+static orc_cf cf_sub(orc_cf a, orc_cf b) { return (orc_cf){a.r - b.r, a.i - b.i}; }
+static orc_cf cf_conj(orc_cf a) { return (orc_cf){a.r, -a.i}; }
+static orc_cf cf_neg(orc_cf a) { return (orc_cf){-a.r, -a.i}; }
+
+/* srslte_mat_2x2_mmse_csi_gen (utils/mat.c:63-98) */
+static void mmse_csi_gen(orc_cf y0, orc_cf y1, orc_cf h00, orc_cf h01, orc_cf h10, orc_cf h11,
+                         orc_cf *x0, orc_cf *x1, float *csi0, float *csi1, float noise, float norm) {
+  const orc_cf _h00 = cf_conj(h00), _h01 = cf_conj(h01), _h10 = cf_conj(h10), _h11 = cf_conj(h11);
+  orc_cf a00 = cf_add(cf_mul(_h00, h00), cf_mul(_h10, h10));
+  a00.r = a00.r + noise;
+  const orc_cf a01 = cf_add(cf_mul(_h00, h01), cf_mul(_h10, h11));
+  const orc_cf a10 = cf_add(cf_mul(_h01, h00), cf_mul(_h11, h10));
+  orc_cf a11 = cf_add(cf_mul(_h01, h01), cf_mul(_h11, h11));
+  a11.r = a11.r + noise;
+  /* srslte_mat_cf_recip_gen(srslte_mat_2x2_det_gen(...)) (mat.c:35-42): conj(a) / |a|^2 */
+  const orc_cf det = cf_sub(cf_mul(a00, a11), cf_mul(a01, a10));
+  const float m2 = det.r * det.r + det.i * det.i;
+  const orc_cf rcp = {det.r / m2, -det.i / m2};
+  const orc_cf nrm = {norm * rcp.r, norm * rcp.i};
+  const orc_cf b00 = cf_mul(a11, nrm), b01 = cf_mul(cf_neg(a01), nrm);
+  const orc_cf b10 = cf_mul(cf_neg(a10), nrm), b11 = cf_mul(a00, nrm);
+  const orc_cf w00 = cf_add(cf_mul(b00, _h00), cf_mul(b01, _h01));
+  const orc_cf w01 = cf_add(cf_mul(b00, _h10), cf_mul(b01, _h11));
+  const orc_cf w10 = cf_add(cf_mul(b10, _h00), cf_mul(b11, _h01));
+  const orc_cf w11 = cf_add(cf_mul(b10, _h10), cf_mul(b11, _h11));
+  *x0 = cf_add(cf_mul(y0, w00), cf_mul(y1, w01));
+  *x1 = cf_add(cf_mul(y0, w10), cf_mul(y1, w11));
+  *csi0 = 1.0f / b00.r;
+  *csi1 = 1.0f / b11.r;
+}
+
+void orc_predecode_ccd_2x2(const float *y0, const float *y1, const float *h00, const float *h01,
+                           const float *h10, const float *h11, float *x0, float *x1, float *csi0,
+                           float *csi1, int n, float scaling, float noise) {
+  /* srslte_predecoding_ccd_2x2_mmse(_csi) (mimo/precoding.c:930-1019, 1021-1072): h[port][rx]
+   * (h01 = port 0 / rx 1, h10 = port 1 / rx 0), CDD precoder alternating per RE: even RE
+   * H = [[h00 + h10, h00 - h10], [h01 + h11, h01 - h11]], odd RE the columns swap. Restated as
+   * the reference's C loop (the exact tail); its AVX body uses rcpps, so the reference's first
+   * 8*(n/8) REs agree with this only to the rcpps tolerance. */
+  const float norm = 2.0f / scaling;
+  for (int i = 0; i < n; i++) {
+    const orc_cf p00 = {h00[2 * i], h00[2 * i + 1]}, p01 = {h01[2 * i], h01[2 * i + 1]};
+    const orc_cf p10 = {h10[2 * i], h10[2 * i + 1]}, p11 = {h11[2 * i], h11[2 * i + 1]};
+    orc_cf g00, g01, g10, g11;
+    if (i % 2 == 0) {
+      g00 = cf_add(p00, p10);
+      g10 = cf_add(p01, p11);
+      g01 = cf_sub(p00, p10);
+      g11 = cf_sub(p01, p11);
+    } else {
+      g00 = cf_sub(p00, p10);
+      g10 = cf_sub(p01, p11);
+      g01 = cf_add(p00, p10);
+      g11 = cf_add(p01, p11);
+    }
+    orc_cf a, b;
+    float c0, c1;
+    mmse_csi_gen((orc_cf){y0[2 * i], y0[2 * i + 1]}, (orc_cf){y1[2 * i], y1[2 * i + 1]}, g00, g01,
+                 g10, g11, &a, &b, &c0, &c1, noise, norm);
+    x0[2 * i] = a.r;
+    x0[2 * i + 1] = a.i;
+    x1[2 * i] = b.r;
+    x1[2 * i + 1] = b.i;
+    if (csi0) csi0[i] = c0;
+    if (csi1) csi1[i] = c1;
+  }
+}
+
 /* ---------------------------------------------------------------- soft demapping ---------- */
 static int16_t sat16(int64_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
 static int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }

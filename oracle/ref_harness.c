@@ -313,6 +313,51 @@ int ref_predecode_single(const float *y, const float *h, float *x, float *csi, i
   return r;
 }
 
+/* precoding.c:1074 defines this without a declaration in precoding.h: declare it, or C99 would
+ * call it through an implicit int() prototype and pass the floats as doubles */
+int srslte_predecoding_ccd_mmse(cf_t *y[SRSLTE_MAX_PORTS], cf_t *h[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS],
+                                cf_t *x[SRSLTE_MAX_LAYERS], float *csi[SRSLTE_MAX_CODEWORDS],
+                                int nof_rxant, int nof_ports, int nof_layers, int nof_symbols,
+                                float scaling, float noise_estimate);
+
+/* srslte_predecoding_ccd_mmse, 2 ports x 2 rx, 2 layers (precoding.c:1074-1097); h[port][rx];
+ * csi0/csi1 may be NULL (non-CSI variant) */
+int ref_predecode_ccd(const float *y0, const float *y1, const float *h00, const float *h01,
+                      const float *h10, const float *h11, float *x0, float *x1, float *csi0,
+                      float *csi1, int n, float scaling, float noise) {
+  size_t sz = (n + 32) * sizeof(cf_t);
+  cf_t *b[8] = {NULL};
+  float *c[2] = {NULL};
+  for (int i = 0; i < 8; i++)
+    if (posix_memalign((void **)&b[i], 64, sz)) return -1;
+  for (int i = 0; i < 2; i++)
+    if (posix_memalign((void **)&c[i], 64, sz)) return -1;
+  memcpy(b[0], y0, n * sizeof(cf_t));
+  memcpy(b[1], y1, n * sizeof(cf_t));
+  memcpy(b[2], h00, n * sizeof(cf_t));
+  memcpy(b[3], h01, n * sizeof(cf_t));
+  memcpy(b[4], h10, n * sizeof(cf_t));
+  memcpy(b[5], h11, n * sizeof(cf_t));
+  cf_t *ya[SRSLTE_MAX_PORTS] = {b[0], b[1]};
+  cf_t *ha[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{b[2], b[3]}, {b[4], b[5]}};
+  cf_t *xa[SRSLTE_MAX_LAYERS] = {b[6], b[7]};
+  float *ca[SRSLTE_MAX_CODEWORDS] = {csi0 ? c[0] : NULL, csi0 ? c[1] : NULL};
+  int r = srslte_predecoding_ccd_mmse(ya, ha, xa, ca, 2, 2, 2, n, scaling, noise);
+  memcpy(x0, b[6], n * sizeof(cf_t));
+  memcpy(x1, b[7], n * sizeof(cf_t));
+  if (csi0) {
+    memcpy(csi0, c[0], n * sizeof(float));
+    memcpy(csi1, c[1], n * sizeof(float));
+  }
+  for (int i = 0; i < 8; i++) free(b[i]);
+  for (int i = 0; i < 2; i++) free(c[i]);
+  return r;
+}
+
+/* defined in pdsch.c:229 without a declaration in pdsch.h */
+int srslte_pdsch_get(srslte_pdsch_t *q, cf_t *sf_symbols, cf_t *symbols, srslte_ra_dl_grant_t *grant,
+                     uint32_t lstart, uint32_t subframe);
+
 /* srslte_pdsch_get (pdsch.c:95-234, 250-255): RE extraction of one grant from a subframe grid
  * (nof_prb*12 x 14 cf32); prb_mask[s*nof_prb + n] marks PRB n allocated in slot s. */
 int ref_pdsch_get(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart,

@@ -307,6 +307,18 @@ class PdschOracle:
         L.orc_pdsch_seed.restype = u32
         L.orc_scramble_s.argtypes = [u32, _i16p, u32]
         L.orc_csi_correction.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i16p]
+        L.orc_predecode_ccd_2x2.argtypes = [_f32p] * 10 + [ctypes.c_int, ctypes.c_float, ctypes.c_float]
+
+    def predecode_ccd(self, y, h, scaling=1.0, noise=0.0, csi=False):
+        """TM3 CDD 2x2 MMSE: y [2 rx][n], h [2 ports][2 rx][n] -> x [2 layers][n] (+ csi [2][n])"""
+        y = [np.ascontiguousarray(v, np.complex64) for v in y]
+        hh = [np.ascontiguousarray(h[p][a], np.complex64) for p in (0, 1) for a in (0, 1)]
+        n = y[0].size
+        x = [np.zeros(n, np.complex64) for _ in range(2)]
+        c = [np.zeros(n, np.float32) for _ in range(2)] if csi else [None, None]
+        self.lib.orc_predecode_ccd_2x2(*[v.ctypes.data_as(_f32p) for v in y + hh + x],
+                                       _ptr(c[0], _f32p), _ptr(c[1], _f32p), n, scaling, noise)
+        return (x, c) if csi else x
 
     def csi_correction(self, mod, csi, llr):
         csi = np.ascontiguousarray(csi, np.float32)
@@ -360,4 +372,17 @@ def ref_pdsch(ref):
     L.ref_predecode_single.argtypes = [_f32p, _f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_float,
                                        ctypes.c_float]
     L.ref_pdsch_get.argtypes = [u32, u32, u32, u32, u32, _u8p, _f32p, _f32p]
+    L.ref_predecode_ccd.argtypes = [_f32p] * 10 + [ctypes.c_int, ctypes.c_float, ctypes.c_float]
     return L
+
+
+def ref_predecode_ccd(L, y, h, scaling=1.0, noise=0.0, csi=False):
+    """the reference's srslte_predecoding_ccd_mmse (AVX2 body + C tail) on the same arguments"""
+    y = [np.ascontiguousarray(v, np.complex64) for v in y]
+    hh = [np.ascontiguousarray(h[p][a], np.complex64) for p in (0, 1) for a in (0, 1)]
+    n = y[0].size
+    x = [np.zeros(n, np.complex64) for _ in range(2)]
+    c = [np.zeros(n, np.float32) for _ in range(2)] if csi else [None, None]
+    assert L.ref_predecode_ccd(*[v.ctypes.data_as(_f32p) for v in y + hh + x],
+                               _ptr(c[0], _f32p), _ptr(c[1], _f32p), n, scaling, noise) == 0
+    return (x, c) if csi else x

@@ -102,3 +102,30 @@ def test_equaliser_and_demapper_vs_reference(po):
                 llr = np.zeros(n * bps, np.int16)
                 L.ref_demod_s(mod, s.ctypes.data_as(f32), n, llr.ctypes.data_as(i16))
                 assert (po.demod(mod, s) == llr).all(), (n, mod, sc)
+
+
+@needs_ref
+def test_cdd_equaliser_vs_reference(po):
+    """TM3 CDD 2x2 MMSE (precoding.c:930-1072). The reference's C tail (the last n % 8 REs) is
+    the oracle's formula and must agree bit for bit; its AVX body uses rcpps and must agree to
+    the rcpps tolerance (<= 1e-3 relative)."""
+    from srsgpu_testlib import ref_predecode_ccd
+    L = ref_pdsch(Ref())
+    rng = np.random.default_rng(5)
+    for n in (2, 6, 8, 14, 1000, 14406):
+        y = [(rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64) for _ in range(2)]
+        h = [[(rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+              for _ in range(2)] for _ in range(2)]
+        for noise, scaling, csi in ((0.1, 1.0, False), (0.01, 0.8, True), (0.5, 1.0, True)):
+            got = po.predecode_ccd(y, h, scaling, noise, csi)
+            ref = ref_predecode_ccd(L, y, h, scaling, noise, csi)
+            xg, xr = (got[0], ref[0]) if csi else (got, ref)
+            tail = 8 * (n // 8)
+            for lay in (0, 1):
+                assert (xg[lay][tail:] == xr[lay][tail:]).all(), (n, lay)
+                scale = np.abs(xr[lay][:tail]) + 1.0
+                assert (np.abs(xg[lay][:tail] - xr[lay][:tail]) / scale).max(initial=0) < 1e-3, (n, lay)
+                if csi:
+                    cg, cr = got[1][lay], ref[1][lay]
+                    assert (cg[tail:] == cr[tail:]).all()
+                    assert (np.abs(cg[:tail] - cr[:tail]) / np.abs(cr[:tail])).max(initial=0) < 2e-3
