@@ -108,7 +108,7 @@ struct PdschEngine {
     max_re = c.nof_prb * 12 * 14;
     max_bits = max_re * 6;
     cwords = (max_bits + 31) / 32 + 2;
-    if (srsgpu_dlsch_create(&dl, nsb, max_cb, msf * max_cb)) return -1;
+    if (srsgpu_dlsch_create(&dl, nsb, max_cb, 2 * msf * max_cb)) return -1;
     // Gold tables (36.211 7.2): x1(n+31) = x1(n+3) + x1(n), x1 = 1,0,0..; x2 basis i: seed 1 << i
     gold_words = (1600 + max_bits + 64) / 32 + 2;
     const uint32_t nbits = gold_words * 32;
@@ -128,15 +128,16 @@ struct PdschEngine {
     HIPCHK(hipMalloc(&d_x2b, x2w.size() * 4));
     HIPCHK(hipMemcpy(d_x1, x1w.data(), x1w.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_x2b, x2w.data(), x2w.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipHostMalloc(&h_gold, sizeof(GoldItem) * msf));
-    HIPCHK(hipHostMalloc(&h_llr, sizeof(LlrItem) * msf));
-    HIPCHK(hipHostMalloc(&h_tb, sizeof(srsgpu_dlsch_tb_t) * msf));
-    HIPCHK(hipMalloc(&d_gold, sizeof(GoldItem) * msf));
-    HIPCHK(hipMalloc(&d_llr, sizeof(LlrItem) * msf));
-    HIPCHK(hipMalloc(&d_c, (size_t)msf * cwords * 4));
-    HIPCHK(hipMalloc(&d_csi, (size_t)msf * max_re * 4));
-    HIPCHK(hipMalloc(&d_csimax, (size_t)msf * 4));
-    HIPCHK(hipMalloc(&d_e, (size_t)msf * max_bits * 2));
+    const uint32_t mtb = 2 * msf; // up to 2 TBs per subframe (CDD)
+    HIPCHK(hipHostMalloc(&h_gold, sizeof(GoldItem) * mtb));
+    HIPCHK(hipHostMalloc(&h_llr, sizeof(LlrItem) * mtb));
+    HIPCHK(hipHostMalloc(&h_tb, sizeof(srsgpu_dlsch_tb_t) * mtb));
+    HIPCHK(hipMalloc(&d_gold, sizeof(GoldItem) * mtb));
+    HIPCHK(hipMalloc(&d_llr, sizeof(LlrItem) * mtb));
+    HIPCHK(hipMalloc(&d_c, (size_t)mtb * cwords * 4));
+    HIPCHK(hipMalloc(&d_csi, (size_t)mtb * max_re * 4));
+    HIPCHK(hipMalloc(&d_csimax, (size_t)mtb * 4));
+    HIPCHK(hipMalloc(&d_e, (size_t)mtb * max_bits * 2));
     HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
     return 0;
   }
@@ -175,25 +176,48 @@ struct PdschEngine {
     return it->second.first;
   }
 
+  // TBs of a call in order: (subframe, tb); tb t of a CDD subframe sits on codeword
+  // cw = t ^ tb_cw_swap (pdsch.c:959-995)
+  static uint32_t nof_tb(const srsgpu_pdsch_sf_t &s) { return s.mimo_type == SRSGPU_MIMO_CDD ? 2 : 1; }
+
+  int check(const srsgpu_pdsch_sf_t &s, uint32_t i) {
+    const uint32_t nt = nof_tb(s);
+    bool ok = s.sf_idx <= 9 && s.lstart <= 4;
+    for (uint32_t t = 0; t < nt; t++) ok = ok && s.mod[t] <= 3;
+    if (!ok) {
+      fprintf(stderr, "srsgpu: invalid subframe %u (mod=%u sf_idx=%u lstart=%u)\n", i, s.mod[0], s.sf_idx,
+              s.lstart);
+      return -1;
+    }
+    if (s.mimo_type == SRSGPU_MIMO_SINGLE_ANTENNA) {
+      if (cell.nof_ports != 1) {
+        fprintf(stderr, "srsgpu: single-antenna PDSCH needs a 1-port cell\n");
+        return -1;
+      }
+    } else if (s.mimo_type == SRSGPU_MIMO_CDD) { // precoding.c:1085-1097
+      if (cell.nof_ports != 2 || cell.nof_rx_ant != 2) {
+        fprintf(stderr, "Error predecoding CCD: Invalid combination of ports %u and rx antennax %u\n",
+                cell.nof_ports, cell.nof_rx_ant);
+        return -1;
+      }
+    } else {
+      fprintf(stderr, "srsgpu: MIMO type %u is not supported on the GPU\n", s.mimo_type);
+      return -1;
+    }
+    return 0;
+  }
+
   int llr(const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid, const float *d_ce,
           size_t ant_stride, int16_t *const *e_ptr) {
     if (n > max_sf) {
       fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
       return -1;
     }
-    if (cell.nof_ports != 1) {
-      fprintf(stderr, "srsgpu: only single-port (SISO) PDSCH is supported\n");
-      return -1;
-    }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
-    uint32_t mre = 0, mbits = 0;
+    uint32_t mre = 0, mbits = 0, k = 0;
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
-      if (s.mod > 3 || s.sf_idx > 9 || s.lstart > 4) {
-        fprintf(stderr, "srsgpu: invalid subframe %u (mod=%u sf_idx=%u lstart=%u)\n", i, s.mod, s.sf_idx,
-                s.lstart);
-        return -1;
-      }
+      if (check(s, i)) return -1;
       uint32_t nre = 0;
       const uint32_t *m = map(s, &nre);
       if (!m) return -1;
@@ -201,47 +225,61 @@ struct PdschEngine {
         fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
         return -1;
       }
-      const int q = kQm[s.mod];
-      GoldItem &g = h_gold[i];
-      g.seed = ((uint32_t)s.rnti << 14) + ((2 * s.sf_idx / 2) << 9) + cell.id; // q = 0 (codeword 0)
-      g.len = nre * q;
-      g.c = d_c + (size_t)i * cwords;
-      LlrItem &t = h_llr[i];
-      memset(&t, 0, sizeof(t));
-      for (uint32_t a = 0; a < cell.nof_rx_ant; a++) {
-        t.y[a] = (const float2 *)d_grid + s.grid_offset + a * ant_stride;
-        t.h[a] = (const float2 *)d_ce + s.grid_offset + a * ant_stride;
+      const uint32_t nt = nof_tb(s);
+      for (uint32_t tb = 0; tb < nt; tb++, k++) {
+        const uint32_t cw = nt == 2 ? (tb ^ (s.tb_cw_swap ? 1u : 0u)) : 0u;
+        const int q = kQm[s.mod[tb]];
+        GoldItem &g = h_gold[k]; // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID
+        g.seed = ((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id;
+        g.len = nre * q;
+        g.c = d_c + (size_t)k * cwords;
+        LlrItem &t = h_llr[k];
+        memset(&t, 0, sizeof(t));
+        for (uint32_t a = 0; a < cell.nof_rx_ant; a++) {
+          t.y[a] = (const float2 *)d_grid + s.grid_offset + a * ant_stride;
+          for (uint32_t p = 0; p < cell.nof_ports && p < 2; p++)
+            t.h[p][a] = (const float2 *)d_ce + s.ce_offset + (a * cell.nof_ports + p) * ant_stride;
+        }
+        t.map = m;
+        t.c = g.c;
+        t.e = e_ptr[k];
+        t.csi = d_csi + (size_t)k * max_re;
+        t.csi_max = d_csimax + k;
+        t.nof_re = nre;
+        t.qm = q;
+        t.mod = (int)s.mod[tb];
+        t.nrx = (int)cell.nof_rx_ant;
+        t.nports = (int)cell.nof_ports;
+        t.cdd = s.mimo_type == SRSGPU_MIMO_CDD;
+        t.layer = (int)cw;
+        t.csi_mode = csi ? 1 : 0;
+        t.aligned = ((uintptr_t)t.e % 4) == 0;
+        t.noise = s.noise_estimate;
+        t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant * cell.nof_ports : nullptr;
+        t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
+        t.inv_scaling = 1.0f / t.scaling;
+        mre = std::max(mre, nre);
+        mbits = std::max(mbits, nre * q);
       }
-      t.map = m;
-      t.c = g.c;
-      t.e = e_ptr[i];
-      t.csi = d_csi + (size_t)i * max_re;
-      t.csi_max = d_csimax + i;
-      t.nof_re = nre;
-      t.qm = q;
-      t.mod = (int)s.mod;
-      t.nrx = (int)cell.nof_rx_ant;
-      t.csi_mode = csi ? 1 : 0;
-      t.aligned = ((uintptr_t)t.e % 4) == 0;
-      t.noise = s.noise_estimate;
-      t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant : nullptr;
-      t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
-      t.inv_scaling = 1.0f / t.scaling;
-      mre = std::max(mre, nre);
-      mbits = std::max(mbits, nre * q);
     }
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * k, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * k, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)n * 4, st));
+    if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)k * 4, st));
     {
       ProfScope ps("k_gold", st);
-      HIPCHK(launch_gold(d_gold, (int)n, mbits, d_x1, d_x2b, gold_words, st));
+      HIPCHK(launch_gold(d_gold, (int)k, mbits, d_x1, d_x2b, gold_words, st));
     }
     ProfScope ps("k_pdsch_llr", st);
-    HIPCHK(launch_pdsch_llr(d_llr, (int)n, mre, csi, st));
+    HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st));
     return 0;
+  }
+
+  uint32_t count_tb(const srsgpu_pdsch_sf_t *sf, uint32_t n) const {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++) k += nof_tb(sf[i]);
+    return k;
   }
 };
 
@@ -301,8 +339,9 @@ int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf) 
 int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
                          const float *d_ce, size_t ant_stride, int16_t *d_e, const uint64_t *e_offset) {
   if (!q || (!sf && n) || !d_grid || !d_ce || !d_e || !e_offset) return -1;
-  std::vector<int16_t *> e(n);
-  for (uint32_t i = 0; i < n; i++) e[i] = d_e + e_offset[i];
+  const uint32_t k = q->e.count_tb(sf, n);
+  std::vector<int16_t *> e(k);
+  for (uint32_t i = 0; i < k; i++) e[i] = d_e + e_offset[i];
   return q->e.llr(sf, n, d_grid, d_ce, ant_stride, e.data());
 }
 
@@ -311,20 +350,23 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
                             int32_t *d_ret, uint32_t *d_noi) {
   if (!q || (!sf && n) || !d_grid || !d_ce || !d_data || !d_ret || !d_noi) return -1;
   PdschEngine &E = q->e;
-  std::vector<int16_t *> e(n);
-  for (uint32_t i = 0; i < n; i++) e[i] = E.d_e + (size_t)i * E.max_bits;
+  const uint32_t k = E.count_tb(sf, n);
+  std::vector<int16_t *> e(k);
+  for (uint32_t i = 0; i < k; i++) e[i] = E.d_e + (size_t)i * E.max_bits;
   if (E.llr(sf, n, d_grid, d_ce, ant_stride, e.data())) return -1;
-  for (uint32_t i = 0; i < n; i++) {
-    srsgpu_dlsch_tb_t &t = E.h_tb[i];
-    t.tbs = sf[i].tbs;
-    t.rv = sf[i].rv;
-    t.Qm = (uint32_t)srsgpu::kQm[sf[i].mod];
-    t.nof_e_bits = sf[i].nof_re * t.Qm;
-    t.softbuffer = sf[i].softbuffer;
-    t.e_offset = (uint64_t)i * E.max_bits;
-    t.data_offset = sf[i].data_offset;
-  }
-  return srsgpu_dlsch_decode_dev(E.dl, E.h_tb, n, E.d_e, d_data, maxh, d_ret, d_noi);
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t tb = 0; tb < PdschEngine::nof_tb(sf[i]); tb++, j++) {
+      srsgpu_dlsch_tb_t &t = E.h_tb[j];
+      t.tbs = sf[i].tbs[tb];
+      t.rv = sf[i].rv[tb];
+      t.Qm = (uint32_t)srsgpu::kQm[sf[i].mod[tb]];
+      t.nof_e_bits = sf[i].nof_re * t.Qm;
+      t.softbuffer = sf[i].softbuffer[tb];
+      t.e_offset = (uint64_t)j * E.max_bits;
+      t.data_offset = sf[i].data_offset[tb];
+    }
+  return srsgpu_dlsch_decode_dev(E.dl, E.h_tb, k, E.d_e, d_data, maxh, d_ret, d_noi);
 }
 
 } // extern "C"

@@ -15,10 +15,10 @@ struct GoldItem {
   uint32_t *c;
 };
 
-// one codeword: gather + equalise + demap + descramble (+ CSI)
+// one transport block: gather + equalise + demap + descramble (+ CSI)
 struct LlrItem {
   const float2 *y[2];      // received grid of each rx antenna
-  const float2 *h[2];      // channel estimate (port 0) of each rx antenna, same layout
+  const float2 *h[2][2];   // channel estimate [port][rx antenna], same layout
   const uint32_t *map;     // RE j -> grid position
   const uint32_t *c;       // packed scrambling bits
   int16_t *e;              // LLRs out (nof_re * qm)
@@ -26,9 +26,11 @@ struct LlrItem {
   uint32_t *csi_max;       // max CSI as float bits (csi_mode; zeroed before the launch)
   uint32_t nof_re;
   int qm, mod, nrx, csi_mode;
+  int cdd, layer;          // TM3 CDD 2x2 MMSE: this TB's codeword / layer (0 or 1)
   int aligned;             // e is 4-byte aligned: LLR pairs stored as 32-bit words
   float noise, inv_scaling, scaling;
-  const float *noise_dev; // if set: noise = mean over rx antennas of noise_dev[a] (chest output)
+  const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does
+  int nports;              // ports in noise_dev
 };
 
 hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,

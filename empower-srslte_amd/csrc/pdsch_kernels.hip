@@ -6,7 +6,9 @@
 //   equalise    SISO ZF/MMSE srslte_predecoding_single_multi (src/phy/mimo/precoding.c:154-352):
 //               x = y conj(h) / (|h|^2 + n0) * (1/scaling), summed over 1-2 rx antennas, with the
 //               reference's operation order and no FMA contraction, so x is the reference's float
-//               (CSI mode: csi = |h|^2 + n0, x = y conj(h) (1/scaling) / csi)
+//               (CSI mode: csi = |h|^2 + n0, x = y conj(h) (1/scaling) / csi);
+//               TM3 CDD 2x2 MMSE srslte_predecoding_ccd_mmse (precoding.c:930-1097) in the
+//               order of srslte_mat_2x2_mmse_csi_gen (utils/mat.c:63-98), exact reciprocals
 //   demap       srslte_demod_soft_demodulate_s (src/phy/modem/demod_soft.c): the SSE/AVX2
 //               integer path (round-to-nearest, saturating pack, integer offsets) for REs inside
 //               the reference's SIMD blocks and its scalar C tail for the rest
@@ -83,7 +85,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
     float hh = 0.f, rr = 0.f, ri = 0.f;
     for (int a = 0; a < 2; a++) {
       if (a == 1 && t.nrx < 2) break;
-      const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[1][pos] : t.h[0][pos];
+      const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[0][1][pos] : t.h[0][0][pos];
       const double yr = y.x, yi = y.y, hr = h.x, hi = h.y;
       rr = (float)__dadd_rn((double)rr, __dsub_rn(__dmul_rn(yr, hr), __dmul_rn(yi, -hi)));
       ri = (float)__dadd_rn((double)ri, __dadd_rn(__dmul_rn(yr, -hi), __dmul_rn(yi, hr)));
@@ -98,7 +100,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
   float hh = 0.f, rr = 0.f, ri = 0.f;
   for (int a = 0; a < 2; a++) {
     if (a == 1 && t.nrx < 2) break;
-    const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[1][pos] : t.h[0][pos];
+    const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[0][1][pos] : t.h[0][0][pos];
     // |h|^2 as hadd(h*h) (precoding.c:179-187), antenna sums in order
     hh = __fadd_rn(hh, __fadd_rn(__fmul_rn(h.x, h.x), __fmul_rn(h.y, h.y)));
     // y * conj(h) as PROD_AVX (addsub of products, :150): re = yr*hr - yi*(-hi)
@@ -116,6 +118,73 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
     e.xr = __fmul_rn(__fdiv_rn(rr, d), t.inv_scaling);
     e.xi = __fmul_rn(__fdiv_rn(ri, d), t.inv_scaling);
   }
+  return e;
+}
+
+// complex float arithmetic in the order gcc evaluates the reference's cf_t expressions
+struct cf {
+  float r, i;
+};
+__device__ __forceinline__ cf c_mul(cf a, cf b) { return {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+__device__ __forceinline__ cf c_add(cf a, cf b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cf c_sub(cf a, cf b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cf c_conj(cf a) { return {a.r, -a.i}; }
+__device__ __forceinline__ cf c_neg(cf a) { return {-a.r, -a.i}; }
+__device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
+  const float2 v = p[pos];
+  return {v.x, v.y};
+}
+
+// TM3 large-delay CDD, 2 ports x 2 rx antennas, 2 layers (precoding.c:930-1019): the precoder
+// alternates per RE (even: H = [[h00+h10, h00-h10], [h01+h11, h01-h11]] with h[port][rx], odd: the
+// columns swap); MMSE row `layer` of B = (H'H + n0 I)^-1 (2/scaling), then x = (B H') y
+// (srslte_mat_2x2_mmse_csi_gen, mat.c:63-98) and csi = 1 / Re(B[layer][layer]).
+__device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint32_t j) {
+  const cf p00 = c_ld(t.h[0][0], pos), p01 = c_ld(t.h[0][1], pos);
+  const cf p10 = c_ld(t.h[1][0], pos), p11 = c_ld(t.h[1][1], pos);
+  cf h00, h01, h10, h11;
+  if ((j & 1) == 0) {
+    h00 = c_add(p00, p10);
+    h10 = c_add(p01, p11);
+    h01 = c_sub(p00, p10);
+    h11 = c_sub(p01, p11);
+  } else {
+    h00 = c_sub(p00, p10);
+    h10 = c_sub(p01, p11);
+    h01 = c_add(p00, p10);
+    h11 = c_add(p01, p11);
+  }
+  const cf _h00 = c_conj(h00), _h01 = c_conj(h01), _h10 = c_conj(h10), _h11 = c_conj(h11);
+  cf a00 = c_add(c_mul(_h00, h00), c_mul(_h10, h10));
+  a00.r = a00.r + t.noise;
+  const cf a01 = c_add(c_mul(_h00, h01), c_mul(_h10, h11));
+  const cf a10 = c_add(c_mul(_h01, h00), c_mul(_h11, h10));
+  cf a11 = c_add(c_mul(_h01, h01), c_mul(_h11, h11));
+  a11.r = a11.r + t.noise;
+  const cf det = c_sub(c_mul(a00, a11), c_mul(a01, a10));
+  const float m2 = det.r * det.r + det.i * det.i;
+  const cf rcp = {det.r / m2, -det.i / m2};
+  const float norm = 2.0f / t.scaling;
+  const cf nrm = {norm * rcp.r, norm * rcp.i};
+  cf bd, bo; // diagonal and off-diagonal entries of row `layer` of B
+  if (t.layer == 0) {
+    bd = c_mul(a11, nrm);          // b00
+    bo = c_mul(c_neg(a01), nrm);   // b01
+  } else {
+    bo = c_mul(c_neg(a10), nrm);   // b10
+    bd = c_mul(a00, nrm);          // b11
+  }
+  // row 0: w00 = b00 _h00 + b01 _h01, w01 = b00 _h10 + b01 _h11
+  // row 1: w10 = b10 _h00 + b11 _h01, w11 = b10 _h10 + b11 _h11
+  const cf b0 = t.layer == 0 ? bd : bo, b1 = t.layer == 0 ? bo : bd;
+  const cf wa = c_add(c_mul(b0, _h00), c_mul(b1, _h01));
+  const cf wb = c_add(c_mul(b0, _h10), c_mul(b1, _h11));
+  const cf y0 = c_ld(t.y[0], pos), y1 = c_ld(t.y[1], pos);
+  const cf x = c_add(c_mul(y0, wa), c_mul(y1, wb));
+  Eq e;
+  e.xr = x.r;
+  e.xi = x.i;
+  e.csi = 1.0f / bd.r;
   return e;
 }
 
@@ -182,7 +251,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
     const uint32_t pos = t.map[j];
-    const Eq e = equalise(t, pos, j);
+    const Eq e = t.cdd ? equalise_cdd(t, pos, j) : equalise(t, pos, j);
     int16_t o[Q];
     demap(MOD, j, t.nof_re, e.xr, e.xi, o);
     // scrambling bits b0 .. b0+Q-1 (may straddle two words)
@@ -211,9 +280,14 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
   const int it = blockIdx.y;
   if (it >= nitems) return;
   LlrItem t = items[it];
-  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750), one port
-    float n = t.noise_dev[0];
-    if (t.nrx > 1) n += t.noise_dev[1];
+  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
+                     // the mean over ports, then the mean over antennas
+    float n = 0.f;
+    for (int a = 0; a < t.nrx; a++) {
+      float acc = 0.f;
+      for (int p = 0; p < t.nports; p++) acc += t.noise_dev[a * t.nports + p];
+      n += acc / (float)t.nports;
+    }
     t.noise = n / (float)t.nrx;
   }
   switch (t.mod) {

@@ -72,14 +72,19 @@ class srsgpu_cell_t(ctypes.Structure):
                 ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32)]
 
 
+MIMO_SINGLE_ANTENNA, MIMO_CDD = 0, 3
+
+
 class srsgpu_pdsch_sf_t(ctypes.Structure):
     """include/srsgpu/pdsch_batch.h"""
     _fields_ = [("sf_idx", ctypes.c_uint32), ("lstart", ctypes.c_uint32),
-                ("prb_idx", (ctypes.c_uint8 * 110) * 2), ("mod", ctypes.c_uint32),
-                ("nof_re", ctypes.c_uint32), ("rnti", ctypes.c_uint16),
-                ("noise_estimate", ctypes.c_float), ("scaling", ctypes.c_float),
-                ("tbs", ctypes.c_uint32), ("rv", ctypes.c_uint32), ("softbuffer", ctypes.c_uint32),
-                ("grid_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64)]
+                ("prb_idx", (ctypes.c_uint8 * 110) * 2), ("nof_re", ctypes.c_uint32),
+                ("rnti", ctypes.c_uint16), ("noise_estimate", ctypes.c_float),
+                ("scaling", ctypes.c_float), ("mimo_type", ctypes.c_uint32),
+                ("tb_cw_swap", ctypes.c_uint32), ("mod", ctypes.c_uint32 * 2),
+                ("tbs", ctypes.c_uint32 * 2), ("rv", ctypes.c_uint32 * 2),
+                ("softbuffer", ctypes.c_uint32 * 2), ("grid_offset", ctypes.c_uint64),
+                ("ce_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64 * 2)]
 
 
 def dlsch_data_len(tbs):
@@ -372,12 +377,20 @@ class Dlsch:
 
 
 def make_sf(sf_idx=1, lstart=1, prb=None, nof_prb=100, mod=3, nof_re=0, rnti=1234, noise=0.0,
-            scaling=1.0, tbs=0, rv=0, softbuffer=0, grid_offset=0, data_offset=0):
-    """srsgpu_pdsch_sf_t from keyword arguments; prb: None (all) or a (2, nof_prb) 0/1 array."""
+            scaling=1.0, tbs=0, rv=0, softbuffer=0, grid_offset=0, data_offset=0, mimo=0,
+            ce_offset=None, tb_cw_swap=0):
+    """srsgpu_pdsch_sf_t from keyword arguments; prb: None (all) or a (2, nof_prb) 0/1 array.
+    Per-TB fields (mod, tbs, rv, softbuffer, data_offset) take a value or a (tb0, tb1) pair;
+    ce_offset defaults to grid_offset (1-port cells: one estimate plane per rx antenna)."""
     s = srsgpu_pdsch_sf_t()
-    s.sf_idx, s.lstart, s.mod, s.nof_re, s.rnti = sf_idx, lstart, mod, nof_re, rnti
-    s.noise_estimate, s.scaling, s.tbs, s.rv, s.softbuffer = noise, scaling, tbs, rv, softbuffer
-    s.grid_offset, s.data_offset = grid_offset, data_offset
+    s.sf_idx, s.lstart, s.nof_re, s.rnti = sf_idx, lstart, nof_re, rnti
+    s.noise_estimate, s.scaling, s.mimo_type, s.tb_cw_swap = noise, scaling, mimo, tb_cw_swap
+    for name, v in (("mod", mod), ("tbs", tbs), ("rv", rv), ("softbuffer", softbuffer),
+                    ("data_offset", data_offset)):
+        pair = tuple(v) if isinstance(v, (tuple, list)) else (v, 0)
+        getattr(s, name)[0], getattr(s, name)[1] = pair
+    s.grid_offset = grid_offset
+    s.ce_offset = grid_offset if ce_offset is None else ce_offset
     m = np.ones((2, nof_prb), np.uint8) if prb is None else np.asarray(prb, np.uint8)
     for sl in range(2):
         for n in range(m.shape[1]):
@@ -417,7 +430,7 @@ class Pdsch:
 
     def llr_dev(self, sfs, d_grid, d_ce, ant_stride, d_e, e_offsets):
         arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
-        offs = (ctypes.c_uint64 * len(sfs))(*e_offsets)
+        offs = (ctypes.c_uint64 * len(e_offsets))(*e_offsets)  # one per TB
         return _lib.srsgpu_pdsch_llr_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                          _vp(d_e), offs)
 

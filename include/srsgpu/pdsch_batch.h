@@ -6,7 +6,8 @@
  * (reference: lib/src/phy/phch/pdsch.c:868-1007, srslte_pdsch_codeword_decode :778-835):
  *   - RE extraction of the grant (srslte_pdsch_get, pdsch.c:95-234);
  *   - SISO ZF/MMSE equalisation over 1-2 rx antennas (srslte_predecoding_single_multi,
- *     mimo/precoding.c:243-352), optionally with CSI;
+ *     mimo/precoding.c:243-352), or TM3 large-delay CDD 2x2 MMSE over 2 ports and 2 rx antennas
+ *     (srslte_predecoding_ccd_mmse, precoding.c:930-1097), optionally with CSI;
  *   - soft demapping to int16 LLRs (srslte_demod_soft_demodulate_s, modem/demod_soft.c);
  *   - descrambling with the PDSCH Gold sequence (scrambling.c:48-51, sequences.c:64-66);
  *   - optional CSI weighting (csi_correction, pdsch.c:676-776);
@@ -15,8 +16,14 @@
  * stream.
  *
  * Grid layout (as srslte_ofdm_rx_sf produces and srslte_chest_dl_estimate consumes): per
- * subframe and rx antenna, 14 OFDM symbols x nof_prb*12 subcarriers of complex float. The
- * channel estimate of CRS port 0 uses the same layout.
+ * subframe and rx antenna, 14 OFDM symbols x nof_prb*12 subcarriers of complex float. Channel
+ * estimates use the same plane layout, one plane per (rx antenna, port) in that order, which is
+ * the order srsgpu_chest_estimate_dev writes them. Plane a of the grid starts at
+ * d_grid + grid_offset + a*ant_stride; plane (a, p) of the estimate at
+ * d_ce + ce_offset + (a*nof_ports + p)*ant_stride.
+ *
+ * Transport blocks of a call are numbered in subframe order, TB 0 then TB 1 of a CDD subframe:
+ * d_ret / d_noi / e_offset have one entry per TB in that order.
  */
 #ifndef SRSGPU_PDSCH_BATCH_H
 #define SRSGPU_PDSCH_BATCH_H
@@ -40,18 +47,26 @@ typedef struct {
   uint32_t nof_rx_ant; /* 1 or 2 */
 } srsgpu_cell_t;
 
+/* srslte_mimo_type_t values accepted by the GPU receiver */
+#define SRSGPU_MIMO_SINGLE_ANTENNA 0 /* 1 CRS port, 1 layer, 1 TB (TM1), 1-2 rx antennas */
+#define SRSGPU_MIMO_CDD 3            /* TM3 large-delay CDD: 2 ports, 2 layers, 2 TBs, 2 rx antennas */
+
 typedef struct {
   uint32_t sf_idx;          /* subframe index 0..9 */
   uint32_t lstart;          /* first PDSCH OFDM symbol (srslte_ra_nbits_t.lstart) */
   uint8_t prb_idx[2][110];  /* srslte_ra_dl_grant_t.prb_idx: PRB allocation per slot */
-  uint32_t mod;             /* srslte_mod_t: 0 BPSK, 1 QPSK, 2 16QAM, 3 64QAM */
   uint32_t nof_re;          /* srslte_ra_nbits_t.nof_re: must equal the grant's RE count */
   uint16_t rnti;
   float noise_estimate;     /* MMSE term (0 = ZF) */
   float scaling;            /* pdsch_scaling (rho_a, 1.0 by default) */
-  uint32_t tbs, rv, softbuffer;
-  uint64_t grid_offset;     /* this subframe's grid in d_grid / d_ce (complex elements) */
-  uint64_t data_offset;     /* first output byte in d_data */
+  uint32_t mimo_type;       /* SRSGPU_MIMO_SINGLE_ANTENNA or SRSGPU_MIMO_CDD */
+  uint32_t tb_cw_swap;      /* srslte_pdsch_cfg_t.tb_cw_swap (CDD): TB 0 on codeword 1 */
+  /* per transport block (index 1 only with CDD) */
+  uint32_t mod[2];          /* srslte_mod_t: 0 BPSK, 1 QPSK, 2 16QAM, 3 64QAM */
+  uint32_t tbs[2], rv[2], softbuffer[2];
+  uint64_t grid_offset;     /* this subframe's [rx antenna] grid planes in d_grid (complex elements) */
+  uint64_t ce_offset;       /* this subframe's [rx antenna][port] estimate planes in d_ce */
+  uint64_t data_offset[2];  /* first output byte of each TB in d_data */
 } srsgpu_pdsch_sf_t;
 
 /* nof_softbuffers HARQ softbuffers of max_cb code blocks; up to max_sf subframes per call. */
@@ -67,15 +82,15 @@ void srsgpu_pdsch_set_noise_dev(srsgpu_pdsch_t *q, const float *d_noise);
 /* the DL-SCH engine owning the softbuffers (reset them with srsgpu_dlsch_softbuffer_reset) */
 srsgpu_dlsch_t *srsgpu_pdsch_get_dlsch(srsgpu_pdsch_t *q);
 
-/* LLRs only: d_e receives sf[i].nof_re * Qm descrambled int16 LLRs per subframe at e_offset[i]
- * (host array). d_grid: [rx antenna] planes of ant_stride complex elements each. */
+/* LLRs only: d_e receives nof_re * Qm descrambled int16 LLRs per TB at e_offset[tb] (host array,
+ * one entry per TB of the call). */
 int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
                          const float *d_grid, const float *d_ce, size_t ant_stride, int16_t *d_e,
                          const uint64_t *e_offset);
 
-/* Full decode: LLRs then DL-SCH. d_ret[i] = srslte_dlsch_decode2's result for TB i (0: decoded
- * with a good CRC, i.e. ack; -1: CRC error; -2: invalid TB), d_noi[i] = nof_iterations. Returns
- * -1 on invalid input (RE count mismatch: pdsch.c:886-890). */
+/* Full decode: LLRs then DL-SCH. d_ret[t] = srslte_dlsch_decode2's result for TB t (0: decoded
+ * with a good CRC, i.e. ack; -1: CRC error; -2: invalid TB), d_noi[t] = nof_iterations. Returns
+ * -1 on invalid input (RE count mismatch: pdsch.c:886-890; a MIMO type the cell cannot carry). */
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
                             const float *d_grid, const float *d_ce, size_t ant_stride,
                             uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);

@@ -7,15 +7,15 @@
  * defines the receive entry points that srsLTE's ue_dl.c / pdsch_test.c call:
  *
  *   srslte_ofdm_rx_sf(q)                 (replaces dft/ofdm.c:460-470 for normal-CP subframes)
- *   srslte_chest_dl_estimate(q, in, ce, sf_idx)   (chest_dl.c:696-715, CRS port 0)
+ *   srslte_chest_dl_estimate(_multi)(q, in, ce, sf_idx[, nof_rx])  (chest_dl.c:681-715, ports 0-1)
  *   srslte_pdsch_decode(q, cfg, sb, sf_symbols, ce, noise, rnti, data, acks)
- *                                        (pdsch.c:868-1007, SISO / single antenna port)
+ *                                        (pdsch.c:868-1007, TM1 single antenna port and TM3 CDD)
  *
  * Build it with -DSRSGPU_SHIM and drop the three replaced functions from their reference
  * translation units. The reference objects keep their own state. This file keeps one GPU handle
  * per object in a small registry keyed by the object's address, because the reference structs
- * have no spare field. Calls that are out of the GPU path's scope (MBSFN, extended CP, more
- * than one antenna port) return SRSLTE_ERROR and print a message. There is no hidden CPU path
+ * have no spare field. Calls that are out of the GPU path's scope (MBSFN, extended CP, transmit
+ * diversity, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a message. There is no hidden CPU path
  * behind them.
  * Each call moves one subframe host -> device -> host, as the reference API is per subframe.
  * Batch users call include/srsgpu/ headers directly and keep the data in HBM.
@@ -49,7 +49,7 @@ typedef struct {
   const void *owner;
   void *gpu;          /* srsgpu_ofdm_t / srsgpu_chest_t / srsgpu_pdsch_t */
   float *d_a, *d_b, *d_c, *d_d;
-  uint32_t nof_prb, cell_id, symbol_sz;
+  uint32_t nof_prb, cell_id, aux; /* aux: FFT size (OFDM) or CRS port count (chest, PDSCH) */
   const void *sb[SHIM_MAX]; /* pdsch: softbuffer object -> GPU softbuffer index */
 } shim_entry_t;
 static shim_entry_t shim[SHIM_MAX];
@@ -84,14 +84,14 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
   const uint32_t nof_prb = q->nof_re / SRSLTE_NRE;
   shim_entry_t *e = shim_get(q, true);
   if (!e) return;
-  if (e->symbol_sz != q->symbol_sz || e->nof_prb != nof_prb) {
+  if (e->aux != q->symbol_sz || e->nof_prb != nof_prb) {
     if (e->gpu) srsgpu_ofdm_rx_destroy((srsgpu_ofdm_t *)e->gpu);
     shim_drop(e);
     e->owner = q;
     if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz)) return;
     hipMalloc((void **)&e->d_a, sizeof(cf_t) * q->sf_sz);
     hipMalloc((void **)&e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp));
-    e->symbol_sz = q->symbol_sz;
+    e->aux = q->symbol_sz;
     e->nof_prb = nof_prb;
   }
   srsgpu_ofdm_rx_set_normalize((srsgpu_ofdm_t *)e->gpu, q->fft_plan.norm);
@@ -102,84 +102,74 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
 }
 
 /* ------------------------------------------------------------------ channel estimation ---- */
-int srslte_chest_dl_estimate(srslte_chest_dl_t *q, cf_t *input, cf_t *ce[SRSLTE_MAX_PORTS],
-                             uint32_t sf_idx) {
-  if (q->cell.nof_ports != 1 || q->cell.cp != SRSLTE_CP_NORM || q->average_subframe ||
-      q->noise_alg != SRSLTE_NOISE_ALG_REFS || q->smooth_filter_auto) {
-    fprintf(stderr, "srsgpu shim: GPU channel estimation covers port 0, normal CP, REFS noise\n");
+/* srslte_chest_dl_estimate_multi (chest_dl.c:681-694): every rx antenna x every CRS port */
+int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_PORTS],
+                                   cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], uint32_t sf_idx,
+                                   uint32_t nof_rx_antennas) {
+  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->average_subframe ||
+      q->noise_alg != SRSLTE_NOISE_ALG_REFS || q->smooth_filter_auto || nof_rx_antennas > 2) {
+    fprintf(stderr, "srsgpu shim: GPU channel estimation covers ports 0-1, normal CP, REFS noise\n");
     return SRSLTE_ERROR;
   }
   shim_entry_t *e = shim_get(q, true);
   if (!e) return SRSLTE_ERROR;
-  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
-  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || !e->gpu) {
+  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
     if (e->gpu) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
     shim_drop(e);
     e->owner = q;
-    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, 1, 1};
-    if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 1)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n);
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n);
-    hipMalloc((void **)&e->d_c, sizeof(float));
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, 1};
+    if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 2)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
+    hipMalloc((void **)&e->d_c, sizeof(float) * 4);
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
+    e->aux = np;
   }
   if (srsgpu_chest_set_smooth_filter((srsgpu_chest_t *)e->gpu, q->smooth_filter, q->smooth_filter_len))
     return SRSLTE_ERROR;
-  hipMemcpy(e->d_a, input, sizeof(cf_t) * n, H2D);
-  if (srsgpu_chest_estimate_dev((srsgpu_chest_t *)e->gpu, &sf_idx, 1, e->d_a, n, e->d_b, e->d_c))
+  uint32_t sfs[2] = {sf_idx, sf_idx};
+  for (uint32_t a = 0; a < nof_rx_antennas; a++)
+    hipMemcpy(e->d_a + 2 * (size_t)a * n, input[a], sizeof(cf_t) * n, H2D);
+  if (srsgpu_chest_estimate_dev((srsgpu_chest_t *)e->gpu, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c))
     return SRSLTE_ERROR;
-  hipMemcpy(ce[0], e->d_b, sizeof(cf_t) * n, D2H);
-  hipMemcpy(&q->noise_estimate[0][0], e->d_c, sizeof(float), D2H);
-  q->last_nof_antennas = 1;
+  float noise[4];
+  hipMemcpy(noise, e->d_c, sizeof(float) * nof_rx_antennas * np, D2H);
+  for (uint32_t a = 0; a < nof_rx_antennas; a++)
+    for (uint32_t p = 0; p < np; p++) { /* GPU order [rx][port]; reference ce[port][rx] */
+      hipMemcpy(ce[p][a], e->d_b + 2 * (size_t)(a * np + p) * n, sizeof(cf_t) * n, D2H);
+      q->noise_estimate[a][p] = noise[a * np + p];
+    }
+  q->last_nof_antennas = (int)nof_rx_antennas;
   return SRSLTE_SUCCESS;
 }
 
+/* srslte_chest_dl_estimate (chest_dl.c:696-715): one rx antenna */
+int srslte_chest_dl_estimate(srslte_chest_dl_t *q, cf_t *input, cf_t *ce[SRSLTE_MAX_PORTS],
+                             uint32_t sf_idx) {
+  cf_t *in[SRSLTE_MAX_PORTS] = {input};
+  cf_t *ce2[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS];
+  memset(ce2, 0, sizeof(ce2));
+  for (uint32_t p = 0; p < q->cell.nof_ports && p < SRSLTE_MAX_PORTS; p++) ce2[p][0] = ce[p];
+  return srslte_chest_dl_estimate_multi(q, in, ce2, sf_idx, 1);
+}
+
 /* ------------------------------------------------------------------ PDSCH ---- */
-int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
-                        srslte_softbuffer_rx_t *softbuffers[SRSLTE_MAX_CODEWORDS],
-                        cf_t *sf_symbols[SRSLTE_MAX_PORTS], cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS],
-                        float noise_estimate, uint16_t rnti, uint8_t *data[SRSLTE_MAX_CODEWORDS],
-                        bool acks[SRSLTE_MAX_CODEWORDS]) {
-  if (!q || !cfg || !sf_symbols || !data) return SRSLTE_ERROR_INVALID_INPUTS;
-  if (q->cell.nof_ports != 1 || cfg->mimo_type != SRSLTE_MIMO_TYPE_SINGLE_ANTENNA ||
-      q->nof_rx_antennas > 2 || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit) {
-    fprintf(stderr, "srsgpu shim: GPU PDSCH covers single-antenna-port, normal-CP, 16-bit LLRs\n");
-    return SRSLTE_ERROR;
-  }
-  if (!cfg->grant.tb_en[0] || acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
-  shim_entry_t *e = shim_get(q, true);
-  if (!e) return SRSLTE_ERROR;
-  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
-  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || !e->gpu) {
-    if (e->gpu) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
-    shim_drop(e);
-    e->owner = q;
-    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, 1, q->nof_rx_antennas};
-    const uint32_t max_tbs = (uint32_t)srslte_ra_tbs_from_idx(26, q->cell.nof_prb);
-    const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
-    if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2); /* [rx antenna][n] */
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 2);
-    hipMalloc((void **)&e->d_c, SRSGPU_DLSCH_DATA_LEN(max_tbs) + 16);
-    hipMalloc((void **)&e->d_d, 2 * sizeof(int32_t));
-    e->nof_prb = q->cell.nof_prb;
-    e->cell_id = q->cell.id;
-  }
-  srsgpu_pdsch_t *g = (srsgpu_pdsch_t *)e->gpu;
-  srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(g);
-  srslte_softbuffer_rx_t *sb = softbuffers[0];
-  /* softbuffer object -> GPU softbuffer index; a new object starts reset (softbuffer_rx_init) */
+/* GPU softbuffer index of a reference softbuffer; the last index is a scratch buffer for TBs the
+ * caller already acked (the reference skips them, pdsch.c:963-965) */
+#define SHIM_SCRATCH (SHIM_MAX - 1)
+static int shim_softbuffer(shim_entry_t *e, srsgpu_dlsch_t *dl, srslte_softbuffer_rx_t *sb) {
   int slot = -1;
-  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
+  for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
     if (e->sb[i] == sb) slot = i;
-  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
-    if (!e->sb[i]) {
+  for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
+    if (!e->sb[i]) { /* a new object starts reset (softbuffer_rx_init) */
       e->sb[i] = sb;
       slot = i;
       srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)i);
     }
-  if (slot < 0) return SRSLTE_ERROR;
+  if (slot < 0) return -1;
   /* The soft bits live in HBM; the host rows only carry a marker in element 0 of each code block
    * row, written after every decode. srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb
    * (softbuffer.c:127-150) zero a prefix of the rows, so the zeroed prefix length is exactly the
@@ -190,6 +180,49 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)slot);
   else if (nreset > 0)
     srsgpu_dlsch_softbuffer_reset_tbs(dl, (uint32_t)slot, (nreset - 1) * (SRSLTE_TCOD_MAX_LEN_CB - 24));
+  return slot;
+}
+
+int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
+                        srslte_softbuffer_rx_t *softbuffers[SRSLTE_MAX_CODEWORDS],
+                        cf_t *sf_symbols[SRSLTE_MAX_PORTS], cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS],
+                        float noise_estimate, uint16_t rnti, uint8_t *data[SRSLTE_MAX_CODEWORDS],
+                        bool acks[SRSLTE_MAX_CODEWORDS]) {
+  if (!q || !cfg || !sf_symbols || !data) return SRSLTE_ERROR_INVALID_INPUTS;
+  const uint32_t nof_tb = SRSLTE_RA_DL_GRANT_NOF_TB(&cfg->grant);
+  const bool siso = cfg->mimo_type == SRSLTE_MIMO_TYPE_SINGLE_ANTENNA && q->cell.nof_ports == 1 &&
+                    nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
+  const bool cdd = cfg->mimo_type == SRSLTE_MIMO_TYPE_CDD && q->cell.nof_ports == 2 && nof_tb == 2 &&
+                   cfg->nof_layers == 2 && q->nof_rx_antennas == 2;
+  if ((!siso && !cdd) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit) {
+    fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port) and TM3 CDD (2 ports, 2 layers, "
+                    "2 rx), normal CP, 16-bit LLRs\n");
+    return SRSLTE_ERROR;
+  }
+  if (siso && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
+  if (cdd && acks[0] && acks[1]) return SRSLTE_SUCCESS;
+  shim_entry_t *e = shim_get(q, true);
+  if (!e) return SRSLTE_ERROR;
+  const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
+  const uint32_t max_tbs = (uint32_t)srslte_ra_tbs_from_idx(26, q->cell.nof_prb);
+  const size_t dlen = SRSGPU_DLSCH_DATA_LEN(max_tbs) + 16;
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
+    if (e->gpu) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
+    shim_drop(e);
+    e->owner = q;
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, q->nof_rx_antennas};
+    const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
+    if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
+    hipMalloc((void **)&e->d_c, 2 * dlen);
+    hipMalloc((void **)&e->d_d, 4 * sizeof(int32_t));
+    e->nof_prb = q->cell.nof_prb;
+    e->cell_id = q->cell.id;
+    e->aux = np;
+  }
+  srsgpu_pdsch_t *g = (srsgpu_pdsch_t *)e->gpu;
+  srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(g);
 
   srsgpu_pdsch_sf_t sf;
   memset(&sf, 0, sizeof(sf));
@@ -197,43 +230,60 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   sf.lstart = cfg->nbits[0].lstart;
   for (int s = 0; s < 2; s++)
     for (uint32_t p = 0; p < q->cell.nof_prb; p++) sf.prb_idx[s][p] = cfg->grant.prb_idx[s][p];
-  sf.mod = (uint32_t)cfg->grant.mcs[0].mod;
   sf.nof_re = cfg->nbits[0].nof_re;
   sf.rnti = rnti;
   sf.noise_estimate = noise_estimate;
-  sf.scaling = q->rho_a != 0.0f ? q->rho_a : 1.0f;
-  sf.tbs = (uint32_t)cfg->grant.mcs[0].tbs;
-  sf.rv = cfg->rv[0];
-  sf.softbuffer = (uint32_t)slot;
+  sf.scaling = q->rho_a != 0.0f ? q->rho_a : 1.0f; /* pdsch.c:924-927 */
+  sf.mimo_type = cdd ? SRSGPU_MIMO_CDD : SRSGPU_MIMO_SINGLE_ANTENNA;
+  sf.tb_cw_swap = cfg->tb_cw_swap ? 1 : 0;
+  sf.grid_offset = 0;
+  sf.ce_offset = 0;
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    const int slot = acks[t] ? SHIM_SCRATCH : shim_softbuffer(e, dl, softbuffers[t]);
+    if (slot < 0) return SRSLTE_ERROR;
+    if (acks[t]) srsgpu_dlsch_softbuffer_reset(dl, SHIM_SCRATCH);
+    sf.mod[t] = (uint32_t)cfg->grant.mcs[t].mod;
+    sf.tbs[t] = (uint32_t)cfg->grant.mcs[t].tbs;
+    sf.rv[t] = cfg->rv[t];
+    sf.softbuffer[t] = (uint32_t)slot;
+    sf.data_offset[t] = t * dlen;
+  }
   for (uint32_t a = 0; a < q->nof_rx_antennas; a++) {
     hipMemcpy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D);
-    hipMemcpy(e->d_b + 2 * (size_t)a * n, ce[0][a], sizeof(cf_t) * n, H2D);
+    for (uint32_t p = 0; p < np; p++) /* reference ce[port][rx] -> GPU [rx][port] planes */
+      hipMemcpy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D);
   }
   srsgpu_pdsch_set_csi(g, q->csi_enabled);
   int32_t *d_ret = (int32_t *)e->d_d;
-  uint32_t *d_noi = (uint32_t *)e->d_d + 1;
+  uint32_t *d_noi = (uint32_t *)e->d_d + 2;
   if (srsgpu_pdsch_decode_dev(g, &sf, 1, e->d_a, e->d_b, (size_t)n, (uint8_t *)e->d_c,
                               q->dl_sch.max_iterations, d_ret, d_noi))
     return SRSLTE_ERROR; /* RE count mismatch: pdsch.c:886-890 */
-  int32_t ret = -1;
-  uint32_t noi = 0;
-  hipMemcpy(data[0], e->d_c, (size_t)sf.tbs / 8, D2H);
-  hipMemcpy(&ret, d_ret, sizeof(ret), D2H);
-  hipMemcpy(&noi, d_noi, sizeof(noi), D2H);
-  q->last_nof_iterations[0] = noi;
-  /* srslte_pdsch_codeword_decode (pdsch.c:811-822): ack on a good TB CRC; srslte_pdsch_decode
-   * returns SRSLTE_SUCCESS whatever the codeword result (pdsch.c:966-985) */
-  acks[0] = ret == SRSLTE_SUCCESS;
-  if (ret != SRSLTE_ERROR_INVALID_INPUTS) {
-    /* mirror the code block CRC flags and tb_crc (sch.c:404-408) into the reference object */
-    uint8_t crc[SHIM_MAX];
-    if (srsgpu_dlsch_softbuffer_read(dl, (uint32_t)slot, NULL, crc) == 0) {
-      for (uint32_t i = 0; i < sb->max_cb && i < SHIM_MAX; i++) sb->cb_crc[i] = crc[i] != 0;
-      sb->tb_crc = true;
-      for (uint32_t i = 0; i < cfg->cb_segm[0].C && sb->tb_crc; i++) sb->tb_crc = sb->cb_crc[i];
+  int32_t ret[2] = {-1, -1};
+  uint32_t noi[2] = {0, 0};
+  hipMemcpy(ret, d_ret, sizeof(int32_t) * nof_tb, D2H);
+  hipMemcpy(noi, d_noi, sizeof(uint32_t) * nof_tb, D2H);
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    if (acks[t]) continue; /* already acked: the reference does not touch it */
+    srslte_softbuffer_rx_t *sb = softbuffers[t];
+    hipMemcpy(data[t], (uint8_t *)e->d_c + t * dlen, (size_t)sf.tbs[t] / 8, D2H);
+    /* last_nof_iterations is indexed by codeword (pdsch.c:815) */
+    const uint32_t cw = cdd ? (t ^ sf.tb_cw_swap) : 0;
+    q->last_nof_iterations[cw] = noi[t];
+    /* srslte_pdsch_codeword_decode (pdsch.c:811-822): ack on a good TB CRC; srslte_pdsch_decode
+     * returns SRSLTE_SUCCESS whatever the codeword result (pdsch.c:966-985) */
+    acks[t] = ret[t] == SRSLTE_SUCCESS;
+    if (ret[t] != SRSLTE_ERROR_INVALID_INPUTS) {
+      /* mirror the code block CRC flags and tb_crc (sch.c:404-408) into the reference object */
+      uint8_t crc[SHIM_MAX];
+      if (srsgpu_dlsch_softbuffer_read(dl, sf.softbuffer[t], NULL, crc) == 0) {
+        for (uint32_t i = 0; i < sb->max_cb && i < SHIM_MAX; i++) sb->cb_crc[i] = crc[i] != 0;
+        sb->tb_crc = true;
+        for (uint32_t i = 0; i < cfg->cb_segm[t].C && sb->tb_crc; i++) sb->tb_crc = sb->cb_crc[i];
+      }
     }
+    for (uint32_t i = 0; i < sb->max_cb; i++)
+      if (sb->buffer_f[i]) sb->buffer_f[i][0] = SHIM_MARK;
   }
-  for (uint32_t i = 0; i < sb->max_cb; i++)
-    if (sb->buffer_f[i]) sb->buffer_f[i][0] = SHIM_MARK;
   return SRSLTE_SUCCESS;
 }

@@ -12,8 +12,12 @@
  *
  * Built by `make -C oracle shim` into oracle/_ref/shim_check (needs /root/reference and
  * empower-srslte_amd/lib/libsrsgpu_phy.so); tests/test_integration.py runs it on the GPU.
- * Usage: shim_check nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed
- * Prints one line "tx=<n> acks=<n> mismatches=<n>"; the exit status is 0 only when nothing differs.
+ * Usage: shim_check nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm
+ *   tm 1: single antenna port (TM1); tm 3: 2 CRS ports, CDD with 2 layers and 2 TBs (nof_rx 2).
+ * Prints "tx=<n> acks=<n> mismatches=<n> soft=<n> tbs=<n>". In the exact configurations (TM1
+ * without CSI) every compared field must agree (mismatches). Where the reference equaliser uses
+ * rcpps (CSI, TM3 MMSE) LLRs agree only to its tolerance: data bytes are compared on acks, and
+ * ack / iteration-count differences near the decoding threshold are counted as "soft".
  */
 #include <complex.h>
 #include <math.h>
@@ -41,10 +45,12 @@ static double urand(void) {
 static float gauss(void) { return (float)(sqrt(-2.0 * log(urand())) * cos(2.0 * M_PI * urand())); }
 
 int main(int argc, char **argv) {
-  if (argc != 10) {
-    fprintf(stderr, "usage: %s nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed\n", argv[0]);
+  if (argc != 11) {
+    fprintf(stderr, "usage: %s nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm\n", argv[0]);
     return 2;
   }
+  const int tm = atoi(argv[10]);
+  const uint32_t nports = tm == 3 ? 2 : 1, ntb = tm == 3 ? 2 : 1;
   const uint32_t nof_prb = atoi(argv[1]), cell_id = atoi(argv[2]), mcs = atoi(argv[3]);
   const uint32_t cfi = atoi(argv[4]), nof_rx = atoi(argv[5]), nof_tb = atoi(argv[7]);
   const int csi = atoi(argv[6]);
@@ -52,7 +58,7 @@ int main(int argc, char **argv) {
   rng = (uint64_t)atoll(argv[9]) * 2654435761ULL + 7;
   const uint16_t rnti = 0x1234;
 
-  srslte_cell_t cell = {nof_prb, 1, cell_id, SRSLTE_CP_NORM, SRSLTE_PHICH_NORM, SRSLTE_PHICH_R_1};
+  srslte_cell_t cell = {nof_prb, nports, cell_id, SRSLTE_CP_NORM, SRSLTE_PHICH_NORM, SRSLTE_PHICH_R_1};
   srslte_pdsch_t tx, rx;
   if (srslte_pdsch_init_enb(&tx, nof_prb) || srslte_pdsch_set_cell(&tx, cell) ||
       srslte_pdsch_set_rnti(&tx, rnti) || srslte_pdsch_init_ue(&rx, nof_prb, nof_rx) ||
@@ -65,86 +71,123 @@ int main(int argc, char **argv) {
   grant.nof_prb = nof_prb;
   for (uint32_t s = 0; s < 2; s++)
     for (uint32_t p = 0; p < nof_prb; p++) grant.prb_idx[s][p] = true;
-  grant.tb_en[0] = true;
-  grant.mcs[0].idx = mcs;
-  grant.mcs[0].mod = srslte_ra_mod_from_mcs(mcs);
-  grant.mcs[0].tbs = srslte_ra_tbs_from_idx(srslte_ra_tbs_idx_from_mcs(mcs), nof_prb);
-  grant.Qm[0] = srslte_mod_bits_x_symbol(grant.mcs[0].mod);
+  for (uint32_t t = 0; t < ntb; t++) { /* TB 1 two MCS below TB 0 */
+    const uint32_t m = t ? (mcs >= 2 ? mcs - 2 : mcs) : mcs;
+    grant.tb_en[t] = true;
+    grant.mcs[t].idx = m;
+    grant.mcs[t].mod = srslte_ra_mod_from_mcs(m);
+    grant.mcs[t].tbs = srslte_ra_tbs_from_idx(srslte_ra_tbs_idx_from_mcs(m), nof_prb);
+    grant.Qm[t] = srslte_mod_bits_x_symbol(grant.mcs[t].mod);
+  }
   const uint32_t tbs = (uint32_t)grant.mcs[0].tbs;
 
   const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
-  cf_t *txgrid = srslte_vec_malloc(sizeof(cf_t) * n);
+  cf_t *txg[SRSLTE_MAX_PORTS] = {NULL};
+  for (uint32_t p = 0; p < nports; p++) txg[p] = srslte_vec_malloc(sizeof(cf_t) * n);
   cf_t *y[SRSLTE_MAX_PORTS] = {NULL}, *h[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
   for (uint32_t a = 0; a < nof_rx; a++) {
     y[a] = srslte_vec_malloc(sizeof(cf_t) * n);
-    h[0][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nports; p++) h[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
   }
-  uint8_t *data_tx = calloc(tbs / 8 + 16, 1), *da = calloc(tbs / 8 + 16, 1), *db = calloc(tbs / 8 + 16, 1);
-  srslte_softbuffer_tx_t sbt;
-  srslte_softbuffer_rx_t sra, srb;
-  if (srslte_softbuffer_tx_init(&sbt, nof_prb) || srslte_softbuffer_rx_init(&sra, nof_prb) ||
-      srslte_softbuffer_rx_init(&srb, nof_prb))
-    return 2;
-  srslte_softbuffer_tx_t *sbt_p[SRSLTE_MAX_CODEWORDS] = {&sbt, NULL};
-  srslte_softbuffer_rx_t *sra_p[SRSLTE_MAX_CODEWORDS] = {&sra, NULL};
-  srslte_softbuffer_rx_t *srb_p[SRSLTE_MAX_CODEWORDS] = {&srb, NULL};
-  uint8_t *dtx_p[SRSLTE_MAX_CODEWORDS] = {data_tx, NULL};
-  uint8_t *da_p[SRSLTE_MAX_CODEWORDS] = {da, NULL}, *db_p[SRSLTE_MAX_CODEWORDS] = {db, NULL};
-  cf_t *tx_p[SRSLTE_MAX_PORTS] = {txgrid, NULL};
+  const size_t dl = tbs / 8 + 16;
+  srslte_softbuffer_tx_t sbt[2];
+  srslte_softbuffer_rx_t sra[2], srb[2];
+  srslte_softbuffer_tx_t *sbt_p[SRSLTE_MAX_CODEWORDS] = {NULL};
+  srslte_softbuffer_rx_t *sra_p[SRSLTE_MAX_CODEWORDS] = {NULL}, *srb_p[SRSLTE_MAX_CODEWORDS] = {NULL};
+  uint8_t *dtx_p[SRSLTE_MAX_CODEWORDS] = {NULL}, *da_p[SRSLTE_MAX_CODEWORDS] = {NULL};
+  uint8_t *db_p[SRSLTE_MAX_CODEWORDS] = {NULL};
+  for (uint32_t t = 0; t < ntb; t++) {
+    if (srslte_softbuffer_tx_init(&sbt[t], nof_prb) || srslte_softbuffer_rx_init(&sra[t], nof_prb) ||
+        srslte_softbuffer_rx_init(&srb[t], nof_prb))
+      return 2;
+    sbt_p[t] = &sbt[t];
+    sra_p[t] = &sra[t];
+    srb_p[t] = &srb[t];
+    dtx_p[t] = calloc(dl, 1);
+    da_p[t] = calloc(dl, 1);
+    db_p[t] = calloc(dl, 1);
+  }
+  const int exact = tm == 1 && !csi;
 
   const uint32_t rvs[4] = {0, 2, 3, 1};
-  uint32_t ntx = 0, nacks = 0, nbad = 0;
-  for (uint32_t t = 0; t < nof_tb; t++) {
-    const uint32_t sf_idx = (t * 3 + 1) % 10;
-    for (uint32_t i = 0; i < tbs / 8; i++) data_tx[i] = (uint8_t)(urand() * 256);
-    srslte_softbuffer_tx_reset(&sbt);
-    srslte_softbuffer_rx_reset(&sra);
-    srslte_softbuffer_rx_reset(&srb);
+  uint32_t ntx = 0, nacks = 0, nbad = 0, nsoft = 0;
+  for (uint32_t k = 0; k < nof_tb; k++) {
+    const uint32_t sf_idx = (k * 3 + 1) % 10;
+    for (uint32_t t = 0; t < ntb; t++) {
+      for (uint32_t i = 0; i < (uint32_t)grant.mcs[t].tbs / 8; i++) dtx_p[t][i] = (uint8_t)(urand() * 256);
+      srslte_softbuffer_tx_reset(&sbt[t]);
+      srslte_softbuffer_rx_reset(&sra[t]);
+      srslte_softbuffer_rx_reset(&srb[t]);
+    }
     /* the SNR steps down every third TB so that some need retransmissions */
-    const float snr = snr_db - 3.0f * (float)(t % 3);
+    const float snr = snr_db - 3.0f * (float)(k % 3);
     const float sigma2 = powf(10.0f, -snr / 10.0f);
     bool acka[SRSLTE_MAX_CODEWORDS] = {false, false}, ackb[SRSLTE_MAX_CODEWORDS] = {false, false};
-    for (uint32_t r = 0; r < 4 && !acka[0]; r++) {
+    for (uint32_t r = 0; r < 4 && !(acka[0] && (ntb == 1 || acka[1])); r++) {
       srslte_pdsch_cfg_t cfg;
       memset(&cfg, 0, sizeof(cfg));
-      if (srslte_pdsch_cfg(&cfg, cell, &grant, cfi, sf_idx, (int)rvs[r])) return 2;
-      memset(txgrid, 0, sizeof(cf_t) * n);
-      if (srslte_pdsch_encode(&tx, &cfg, sbt_p, dtx_p, rnti, tx_p)) return 2;
+      int rv2[SRSLTE_MAX_CODEWORDS] = {(int)rvs[r], (int)rvs[r]};
+      if (srslte_pdsch_cfg_mimo(&cfg, cell, &grant, cfi, sf_idx, rv2,
+                                tm == 3 ? SRSLTE_MIMO_TYPE_CDD : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA, 0))
+        return 2;
+      for (uint32_t p = 0; p < nports; p++) memset(txg[p], 0, sizeof(cf_t) * n);
+      if (srslte_pdsch_encode(&tx, &cfg, sbt_p, dtx_p, rnti, txg)) return 2;
       for (uint32_t a = 0; a < nof_rx; a++) {
-        const float amp = 0.5f + (float)urand(), ph = (float)(2 * M_PI * urand());
-        const float slope = (float)(0.02 * (urand() - 0.5));
-        for (uint32_t k = 0; k < n; k++) {
-          const uint32_t sc = k % (nof_prb * SRSLTE_NRE);
-          h[0][a][k] = amp * cexpf(I * (ph + slope * (float)sc));
-          y[a][k] = h[0][a][k] * txgrid[k] +
-                    sqrtf(sigma2 / 2) * (gauss() + I * gauss());
+        for (uint32_t p = 0; p < nports; p++) {
+          const float amp = 0.5f + (float)urand(), ph = (float)(2 * M_PI * urand());
+          const float slope = (float)(0.02 * (urand() - 0.5));
+          for (uint32_t i = 0; i < n; i++) {
+            const uint32_t sc = i % (nof_prb * SRSLTE_NRE);
+            h[p][a][i] = amp * cexpf(I * (ph + slope * (float)sc));
+          }
+        }
+        for (uint32_t i = 0; i < n; i++) {
+          cf_t v = sqrtf(sigma2 / 2) * (gauss() + I * gauss());
+          for (uint32_t p = 0; p < nports; p++) v += h[p][a][i] * txg[p][i];
+          y[a][i] = v;
         }
       }
-      memset(da, 0, tbs / 8 + 16);
-      memset(db, 0, tbs / 8 + 16);
-      const int ra = srslte_pdsch_decode(&rx, &cfg, sra_p, y, h, sigma2, rnti, da_p, acka);
-      const uint32_t noia = rx.last_nof_iterations[0];
-      const int rb = srsgpu_shim_pdsch_decode(&rx, &cfg, srb_p, y, h, sigma2, rnti, db_p, ackb);
-      const uint32_t noib = rx.last_nof_iterations[0];
-      /* with CSI the reference equaliser uses the SSE approximate reciprocal (rcpps, precoding.c
-       * CSI path), whose bits differ between CPU models; the GPU computes the exact quotient.
-       * Undecodable blocks then leave different bit errors, so data is compared on acks only. */
-      const int data_bad = (!csi || acka[0]) && memcmp(da, db, tbs / 8) != 0;
-      int bad = ra != rb || acka[0] != ackb[0] || noia != noib || data_bad || sra.tb_crc != srb.tb_crc;
-      for (uint32_t i = 0; i < cfg.cb_segm[0].C; i++) bad |= sra.cb_crc[i] != srb.cb_crc[i];
-      if (bad)
-        fprintf(stderr, "mismatch tb %u rv %u sf %u: ret %d/%d ack %d/%d noi %u/%u data %d tb_crc %d/%d\n",
-                t, rvs[r], sf_idx, ra, rb, acka[0], ackb[0], noia, noib, data_bad,
-                sra.tb_crc, srb.tb_crc);
-      nbad += bad;
-      ntx++;
-      nacks += acka[0];
-      if (acka[0] && memcmp(da, data_tx, tbs / 8)) {
-        fprintf(stderr, "tb %u: reference acked wrong data\n", t);
-        nbad++;
+      bool acka0[2] = {acka[0], acka[1]};
+      for (uint32_t t = 0; t < ntb; t++) {
+        memset(da_p[t], 0, dl);
+        memset(db_p[t], 0, dl);
       }
+      const int ra = srslte_pdsch_decode(&rx, &cfg, sra_p, y, h, sigma2, rnti, da_p, acka);
+      uint32_t noia[2] = {rx.last_nof_iterations[0], rx.last_nof_iterations[1]};
+      const int rb = srsgpu_shim_pdsch_decode(&rx, &cfg, srb_p, y, h, sigma2, rnti, db_p, ackb);
+      uint32_t noib[2] = {rx.last_nof_iterations[0], rx.last_nof_iterations[1]};
+      int bad = ra != rb, soft = 0;
+      for (uint32_t t = 0; t < ntb; t++) {
+        if (acka0[t]) continue; /* acked before this transmission: neither decoder touched it */
+        const size_t nb = (size_t)grant.mcs[t].tbs / 8;
+        const int dbad = (exact || (acka[t] && ackb[t])) && memcmp(da_p[t], db_p[t], nb) != 0;
+        int crcbad = sra[t].tb_crc != srb[t].tb_crc;
+        for (uint32_t i = 0; i < cfg.cb_segm[t].C; i++) crcbad |= sra[t].cb_crc[i] != srb[t].cb_crc[i];
+        const int cw = tm == 3 ? (int)(t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
+        const int state = acka[t] != ackb[t] || noia[cw] != noib[cw] || crcbad;
+        if (exact)
+          bad |= dbad || state;
+        else {
+          bad |= dbad;
+          soft |= state;
+        }
+        if (dbad || state)
+          fprintf(stderr, "%s tb %u/%u rv %u sf %u: ret %d/%d ack %d/%d noi %u/%u data %d crc %d\n",
+                  exact ? "mismatch" : "differs", k, t, rvs[r], sf_idx, ra, rb, acka[t], ackb[t],
+                  noia[cw], noib[cw], dbad, crcbad);
+        nacks += acka[t];
+        if (acka[t] && memcmp(da_p[t], dtx_p[t], nb)) {
+          fprintf(stderr, "tb %u/%u: reference acked wrong data\n", k, t);
+          bad = 1;
+        }
+        /* keep the two decoders on the same HARQ path */
+        ackb[t] = acka[t];
+      }
+      nbad += bad;
+      nsoft += soft;
+      ntx++;
     }
   }
-  printf("tx=%u acks=%u mismatches=%u tbs=%u\n", ntx, nacks, nbad, tbs);
+  printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u\n", ntx, nacks, nbad, nsoft, tbs);
   return nbad ? 1 : 0;
 }

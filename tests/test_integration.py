@@ -4,9 +4,11 @@ CPU: the shim type-checks against the reference's own headers (when /root/refere
 GPU: oracle/_ref/shim_check decodes every subframe with the reference's CPU srslte_pdsch_decode
 (pdsch.c:868-1007) and with the shim's GPU version on the same srslte_pdsch_t, grids and HARQ
 sequence (rv 0, 2, 3, 1), and requires identical return value, ack, data bytes,
-last_nof_iterations and softbuffer cb_crc / tb_crc for every transmission. With CSI enabled
-the reference's approximate reciprocal (rcpps) makes failed blocks' bit errors CPU-dependent, so
-their data bytes are compared only when the TB is acked.
+last_nof_iterations and softbuffer cb_crc / tb_crc for every transmission of TM1 without CSI.
+With CSI, and in TM3 (whose MMSE inverts with rcpps in the reference), the reference's
+approximate reciprocal makes LLRs agree only to its tolerance: data bytes must agree whenever
+both decoders ack, and ack / iteration-count differences at the decoding threshold ("soft") must
+stay rare.
 """
 import os
 import subprocess
@@ -27,19 +29,23 @@ def test_shim_typechecks_against_reference_headers():
     assert r.returncode == 0, r.stderr
 
 
-# nof_prb, cell_id, mcs, cfi, nof_rx, csi, nof_tb, snr_db, seed
+# nof_prb, cell_id, mcs, cfi, nof_rx, csi, nof_tb, snr_db, seed, tm
 CASES = [
-    (6, 1, 9, 3, 1, 0, 8, 3.0, 1),      # QPSK, 6 PRB, includes subframes 0 and 5
-    (15, 77, 16, 2, 2, 1, 8, 9.0, 2),   # 16QAM, odd PRB count (PBCH half PRBs), 2 rx, CSI
-    (25, 301, 22, 1, 1, 0, 6, 14.0, 3),  # 64QAM, 25 PRB
-    (15, 77, 16, 2, 2, 0, 8, 9.0, 6),   # 2 rx without CSI: every transmission bit-exact
-    (50, 503, 27, 2, 2, 1, 4, 18.0, 4),  # 64QAM, 2 rx, CSI, several code blocks
-    (100, 12, 28, 2, 1, 0, 4, 21.0, 5),  # 100 PRB, 13 code blocks
+    (6, 1, 9, 3, 1, 0, 8, 3.0, 1, 1),      # QPSK, 6 PRB, includes subframes 0 and 5
+    (15, 77, 16, 2, 2, 1, 8, 9.0, 2, 1),   # 16QAM, odd PRB count (PBCH half PRBs), 2 rx, CSI
+    (25, 301, 22, 1, 1, 0, 6, 14.0, 3, 1),  # 64QAM, 25 PRB
+    (15, 77, 16, 2, 2, 0, 8, 9.0, 6, 1),   # 2 rx without CSI: every transmission bit-exact
+    (50, 503, 27, 2, 2, 1, 4, 18.0, 4, 1),  # 64QAM, 2 rx, CSI, several code blocks
+    (100, 12, 28, 2, 1, 0, 4, 21.0, 5, 1),  # 100 PRB, 13 code blocks
+    (25, 7, 16, 2, 2, 0, 8, 16.0, 7, 3),   # TM3 CDD 2x2, two 16QAM TBs
+    (50, 150, 26, 1, 2, 1, 6, 25.0, 8, 3),  # TM3, 64QAM, CSI
+    (100, 1, 28, 1, 2, 0, 4, 27.0, 9, 3),  # TM3 20 MHz, two 64QAM TBs (BASELINE configs[3] shape)
 ]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", CASES, ids=[f"prb{c[0]}_mcs{c[2]}_rx{c[4]}_csi{c[5]}" for c in CASES])
+@pytest.mark.parametrize("case", CASES,
+                         ids=[f"tm{c[9]}_prb{c[0]}_mcs{c[2]}_rx{c[4]}_csi{c[5]}" for c in CASES])
 def test_shim_pdsch_decode_matches_reference(case):
     if not os.path.exists(CHECK):
         pytest.skip("oracle/_ref/shim_check not built (needs /root/reference at build time)")
@@ -48,3 +54,5 @@ def test_shim_pdsch_decode_matches_reference(case):
     assert r.returncode == 0, r.stdout + r.stderr
     stats = dict(kv.split("=") for kv in r.stdout.split())
     assert int(stats["mismatches"]) == 0 and int(stats["tx"]) >= case[6]
+    assert int(stats["soft"]) <= max(1, int(stats["tx"]) // 10), r.stdout + r.stderr
+    assert int(stats["acks"]) > 0

@@ -173,3 +173,67 @@ def test_re_count_mismatch_is_an_error(s):
     sf = s.make_sf(sf_idx=1, lstart=1, nof_prb=25, mod=1, nof_re=123)
     assert p.llr_dev([sf], d.data_ptr(), d.data_ptr(), 25 * 12 * 14, d.data_ptr(), [0]) == -1
     p.close()
+
+
+@pytest.mark.parametrize("nof_prb,cell_id,swap,csi", [(100, 3, 0, False), (25, 101, 1, False),
+                                                       (50, 7, 0, True), (15, 400, 1, True)])
+def test_llr_cdd_vs_oracle(s, po, nof_prb, cell_id, swap, csi):
+    """TM3 CDD 2x2 MMSE (2 ports, 2 rx, 2 TBs per subframe): every TB's LLRs equal the oracle
+    (exact-reciprocal restatement of srslte_mat_2x2_mmse_csi_gen) bit for bit, codeword / layer /
+    scrambling q chosen through tb_cw_swap as pdsch.c:959-995 does; CSI weighting per codeword."""
+    import torch
+    rng = np.random.default_rng(3 * nof_prb + cell_id)
+    size = nof_prb * 12 * 14
+    n_sf = 6
+    y = (rng.standard_normal((n_sf, 2, size)) + 1j * rng.standard_normal((n_sf, 2, size))).astype(np.complex64)
+    h = (rng.standard_normal((n_sf, 2, 2, size)) + 1j * rng.standard_normal((n_sf, 2, 2, size))).astype(np.complex64)
+    p = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=2, max_sf=n_sf)
+    p.set_csi(csi)
+    sfs, expect, offs, off = [], [], [], 0
+    for i in range(n_sf):
+        sf_idx = [0, 1, 5][i % 3]
+        lstart = 1 + i % 3
+        mask = np.ones((2, nof_prb), np.uint8) if i % 2 == 0 else (rng.random((2, nof_prb)) < 0.6).astype(np.uint8)
+        mods = ([3, 2], [1, 3], [2, 2])[i % 3]
+        noise = 0.05 + 0.05 * (i % 2)
+        rnti = int(rng.integers(1, 65535))
+        idx = po.re_map(nof_prb, cell_id, 2, lstart, sf_idx, mask)
+        sf = s.make_sf(sf_idx=sf_idx, lstart=lstart, prb=mask, nof_prb=nof_prb, mod=mods,
+                       nof_re=idx.size, rnti=rnti, noise=noise, grid_offset=i * 2 * size,
+                       ce_offset=i * 4 * size, mimo=s.MIMO_CDD, tb_cw_swap=swap)
+        assert p.nof_re(sf) == idx.size
+        sfs.append(sf)
+        # h[sf][rx][port] planes on the device; the oracle takes h[port][rx]
+        hp = [[h[i, a, port][idx] for a in (0, 1)] for port in (0, 1)]
+        xs = po.predecode_ccd([y[i, 0][idx], y[i, 1][idx]], hp, 1.0, noise, csi)
+        x, c = (xs if csi else (xs, None))
+        for tb in (0, 1):
+            cw = tb ^ swap
+            e = po.demod(mods[tb], x[cw])
+            e = po.scramble(po.seed(rnti, cw, 2 * sf_idx, cell_id), e)
+            if csi:
+                e = po.csi_correction(mods[tb], c[cw], e)
+            expect.append(e)
+            offs.append(off)
+            off += e.size
+    d_y = torch.from_numpy(y.reshape(-1)).cuda()
+    d_h = torch.from_numpy(h.reshape(-1)).cuda()
+    d_e = torch.zeros(off + 8, dtype=torch.int16, device="cuda")
+    assert p.llr_dev(sfs, d_y.data_ptr(), d_h.data_ptr(), size, d_e.data_ptr(), offs) == 0
+    torch.cuda.synchronize()
+    e = d_e.cpu().numpy()
+    for k in range(len(expect)):
+        got = e[offs[k]:offs[k] + expect[k].size]
+        assert (got == expect[k]).all(), (k, np.nonzero(got != expect[k])[0][:5])
+    p.close()
+
+
+def test_cdd_needs_two_port_cell(s):
+    """a CDD subframe on a 1-port cell is refused (precoding.c:1085-1097)"""
+    import torch
+    p = s.Pdsch(25, 1, max_sf=1)
+    sf = s.make_sf(sf_idx=1, lstart=1, nof_prb=25, mod=(1, 1), nof_re=1, mimo=s.MIMO_CDD)
+    d = torch.zeros(25 * 12 * 14 * 4, dtype=torch.complex64, device="cuda")
+    d_e = torch.zeros(100000, dtype=torch.int16, device="cuda")
+    assert p.llr_dev([sf], d.data_ptr(), d.data_ptr(), 25 * 12 * 14, d_e.data_ptr(), [0, 0]) == -1
+    p.close()
