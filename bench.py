@@ -120,69 +120,83 @@ def cpu_baseline(llr, nthreads):
 C3_PRB, C3_CELL, C3_TBS, C3_SF = 100, 1, 75376, 1024   # BASELINE configs[2]: 20 MHz SISO 64QAM
 
 
-def pipeline_inputs(s, n_sf, rng):
-    """n_sf time-domain 20 MHz subframes (N = 2048, 15 N samples): random 64QAM symbols on every
-    RE through a frequency-selective channel plus AWGN, built with numpy only. The symbols are not
-    codewords, so every code block runs the full 8 half-iterations (the fixed-8 throughput case;
-    early stop never triggers)."""
+def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1):
+    """n_sf time-domain 20 MHz subframes per rx antenna (N = 2048, 15 N samples): random 64QAM
+    symbols on every RE of each layer through frequency-selective channels plus AWGN, built with
+    numpy only -> [n_sf][nrx][15 N]. The symbols are not codewords, so every code block runs the
+    full 8 half-iterations (the fixed-8 throughput case; early stop never triggers)."""
     N = s.symbol_sz(C3_PRB, True)
     nsc = 12 * C3_PRB
     k = np.arange(nsc)
-    h = (1 + 0.3 * np.cos(2 * np.pi * k / nsc)) * np.exp(0.5j * np.sin(2 * np.pi * k / nsc))
     lev = np.array([-7, -5, -3, -1, 1, 3, 5, 7], np.float32) / np.sqrt(42)
     cp0, cp = int(np.ceil(160 * N / 2048)), int(np.ceil(144 * N / 2048))
     ntmpl = min(n_sf, 16)
-    tmpl = np.zeros((ntmpl, 15 * N), np.complex64)
+    tmpl = np.zeros((ntmpl, nrx, 15 * N), np.complex64)
     for t in range(ntmpl):
-        g = (lev[rng.integers(0, 8, (14, nsc))] + 1j * lev[rng.integers(0, 8, (14, nsc))]) * h
-        X = np.zeros((14, N), np.complex64)
-        X[:, N - nsc // 2:] = g[:, :nsc // 2]
-        X[:, 1:1 + nsc // 2] = g[:, nsc // 2:]
-        sym = np.fft.ifft(X, axis=1).astype(np.complex64)
-        pos = 0
-        for i in range(14):
-            c = cp0 if i % 7 == 0 else cp
-            tmpl[t, pos:pos + c] = sym[i, N - c:]
-            tmpl[t, pos + c:pos + c + N] = sym[i]
-            pos += c + N
+        layers = [lev[rng.integers(0, 8, (14, nsc))] + 1j * lev[rng.integers(0, 8, (14, nsc))]
+                  for _ in range(nports)]
+        for a in range(nrx):
+            g = np.zeros((14, nsc), np.complex128)
+            for p, lay in enumerate(layers):
+                ph = 0.5 + 0.7 * a + 1.3 * p
+                h = (1 + 0.3 * np.cos(2 * np.pi * k / nsc + ph)) * np.exp(0.5j * np.sin(2 * np.pi * k / nsc + ph))
+                g += lay * h / np.sqrt(nports)
+            X = np.zeros((14, N), np.complex64)
+            X[:, N - nsc // 2:] = g[:, :nsc // 2]
+            X[:, 1:1 + nsc // 2] = g[:, nsc // 2:]
+            sym = np.fft.ifft(X, axis=1).astype(np.complex64)
+            pos = 0
+            for i in range(14):
+                c = cp0 if i % 7 == 0 else cp
+                tmpl[t, a, pos:pos + c] = sym[i, N - c:]
+                tmpl[t, a, pos + c:pos + c + N] = sym[i]
+                pos += c + N
     x = tmpl[np.arange(n_sf) % ntmpl]
     x += (1e-3 / np.sqrt(N)) * (rng.standard_normal(x.shape) + 1j * rng.standard_normal(x.shape)).astype(np.complex64)
     return N, x
 
 
-def run_pipeline(s, torch, dev, steps, warmup):
-    """BASELINE configs[2]: one step = 1024 subframes through OFDM FFT -> CRS channel estimation
-    -> PDSCH (RE extraction, MMSE, 64QAM demap, descramble) -> DL-SCH (de-RM, turbo decoding with
-    CRC early stop up to 8 half-iterations, TB CRC) for TBS 75376 (13 x K=5824)."""
+def run_pipeline(s, torch, dev, steps, warmup, tm=1):
+    """tm 1 — BASELINE configs[2]: one step = 1024 subframes through OFDM FFT -> CRS channel
+    estimation -> PDSCH (RE extraction, MMSE, 64QAM demap, descramble) -> DL-SCH (de-RM, turbo
+    decoding with CRC early stop up to 8 half-iterations, TB CRC) for TBS 75376 (13 x K=5824).
+    tm 3 — the per-GPU shard of BASELINE configs[3]: 1024 TM3 subframes (2 CRS ports, 2 rx
+    antennas, CDD 2x2 MMSE, two MCS-28 TBs per subframe) through the same stages."""
+    nrx = nports = 2 if tm == 3 else 1
+    ntb = 2 if tm == 3 else 1
     rng = np.random.default_rng(99)
-    N, x = pipeline_inputs(s, C3_SF, rng)
+    N, x = pipeline_inputs(s, C3_SF, rng, nrx, nports)
     stream = torch.cuda.current_stream(dev).cuda_stream
     gsz = 14 * 12 * C3_PRB
+    ngrid = C3_SF * nrx
     ofdm = s.OfdmRx(C3_PRB, N, stream=stream)
-    chest = s.Chest(C3_PRB, C3_CELL, max_grids=C3_SF, stream=stream)
-    pd = s.Pdsch(C3_PRB, C3_CELL, nof_softbuffers=C3_SF, max_cb=13, max_sf=C3_SF, stream=stream)
+    chest = s.Chest(C3_PRB, C3_CELL, max_grids=ngrid, stream=stream, nof_ports=nports)
+    pd = s.Pdsch(C3_PRB, C3_CELL, nof_ports=nports, nof_rx_ant=nrx, nof_softbuffers=C3_SF * ntb,
+                 max_cb=13, max_sf=C3_SF, stream=stream)
     d_x = torch.from_numpy(x.reshape(-1)).to(dev)
     del x
-    d_grid = torch.zeros(C3_SF * gsz, dtype=torch.complex64, device=dev)
-    d_ce = torch.zeros_like(d_grid)
-    d_noise = torch.zeros(C3_SF, dtype=torch.float32, device=dev)
+    d_grid = torch.zeros(ngrid * gsz, dtype=torch.complex64, device=dev)
+    d_ce = torch.zeros(ngrid * nports * gsz, dtype=torch.complex64, device=dev)
+    d_noise = torch.zeros(ngrid * nports, dtype=torch.float32, device=dev)
     dlen = C3_TBS // 8 + 6
-    d_data = torch.zeros(C3_SF * dlen, dtype=torch.uint8, device=dev)
-    d_ret = torch.zeros(C3_SF, dtype=torch.int32, device=dev)
-    d_noi = torch.zeros(C3_SF, dtype=torch.int32, device=dev)
+    d_data = torch.zeros(C3_SF * ntb * dlen, dtype=torch.uint8, device=dev)
+    d_ret = torch.zeros(C3_SF * ntb, dtype=torch.int32, device=dev)
+    d_noi = torch.zeros(C3_SF * ntb, dtype=torch.int32, device=dev)
     pd.set_noise_dev(d_noise.data_ptr())
     sf_idx = [1 + (i % 4) for i in range(C3_SF)]  # subframes without PSS/SSS/PBCH
-    probe = s.make_sf(sf_idx=1, lstart=1, nof_prb=C3_PRB, mod=3)
-    nre = pd.nof_re(probe)
-    sfs = [s.make_sf(sf_idx=sf_idx[i], lstart=1, nof_prb=C3_PRB, mod=3, nof_re=nre, rnti=1234,
-                     tbs=C3_TBS, softbuffer=i, grid_offset=i * gsz, data_offset=i * dlen)
+    mimo = s.MIMO_CDD if tm == 3 else s.MIMO_SINGLE_ANTENNA
+    nre = pd.nof_re(s.make_sf(sf_idx=1, lstart=1, nof_prb=C3_PRB, mod=3))
+    sfs = [s.make_sf(sf_idx=sf_idx[i], lstart=1, nof_prb=C3_PRB, mod=(3, 3), nof_re=nre, rnti=1234,
+                     tbs=(C3_TBS, C3_TBS), softbuffer=(ntb * i, ntb * i + 1), mimo=mimo,
+                     grid_offset=i * nrx * gsz, ce_offset=i * nrx * nports * gsz,
+                     data_offset=(ntb * i * dlen, (ntb * i + 1) * dlen))
            for i in range(C3_SF)]
-    sf_list = sf_idx
+    grid_sf = [v for v in sf_idx for _ in range(nrx)]
 
     def step():
-        pd.reset_softbuffer(0, C3_SF)  # new TBs: one softbuffer reset pass
-        assert ofdm.rx_dev(C3_SF, d_x.data_ptr(), 15 * N, d_grid.data_ptr(), gsz) == 0
-        assert chest.estimate_dev(sf_list, d_grid.data_ptr(), gsz, d_ce.data_ptr(), d_noise.data_ptr()) == 0
+        pd.reset_softbuffer(0, C3_SF * ntb)  # new TBs: one softbuffer reset pass
+        assert ofdm.rx_dev(ngrid, d_x.data_ptr(), 15 * N, d_grid.data_ptr(), gsz) == 0
+        assert chest.estimate_dev(grid_sf, d_grid.data_ptr(), gsz, d_ce.data_ptr(), d_noise.data_ptr()) == 0
         assert pd.decode_dev(sfs, d_grid.data_ptr(), d_ce.data_ptr(), gsz, d_data.data_ptr(), 8,
                              d_ret.data_ptr(), d_noi.data_ptr()) == 0
 
@@ -205,10 +219,11 @@ def run_pipeline(s, torch, dev, steps, warmup):
     noi = d_noi.cpu().numpy()
     for o in (ofdm, chest, pd):
         o.close()
-    return {"workload": "c3_pdsch_pipeline_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS),
+    name = "c3_pdsch_pipeline" if tm == 1 else "c4_tm3_cdd2x2_pipeline"
+    return {"workload": "%s_%dsf_20MHz_64QAM_%dx_tbs%d" % (name, C3_SF, ntb, C3_TBS),
             "subframes_per_s": round(C3_SF * steps / el, 1),
-            "tb_mbps": round(C3_SF * steps * C3_TBS / el / 1e6, 1),
-            "ms_per_batch": round(el / steps * 1e3, 3), "symbol_size": N,
+            "tb_mbps": round(C3_SF * ntb * steps * C3_TBS / el / 1e6, 1),
+            "ms_per_batch": round(el / steps * 1e3, 3), "symbol_size": N, "rx_antennas": nrx,
             "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
             "data": "synthetic 64QAM symbols (not codewords: every CB runs 8 half-iterations)"}
 
@@ -345,9 +360,19 @@ def main():
             ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
             pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
+    pipe3 = None
+    if not args.no_pipeline:
+        pipe3 = run_pipeline(s, torch, dev, max(1, args.steps // 2), 1, tm=3)
+        if dist:
+            ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
+            pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            pipe3["tb_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
     if rank == 0 and pipe:
         result["config"]["subframes_per_s"] = pipe["subframes_per_s"]
         result["pipeline"] = pipe
+    if rank == 0 and pipe3:
+        result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
+        result["pipeline_tm3"] = pipe3
     if rank == 0 and not args.no_cpu_baseline and nranks == 1:
         result["cpu_baseline"] = cpu_baseline(llr, int(os.environ.get("SRSGPU_CPU_THREADS",
                                                                        min(16, os.cpu_count() or 1))))
