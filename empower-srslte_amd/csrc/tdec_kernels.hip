@@ -505,6 +505,20 @@ struct ChunkW {
   int t[CW];
 };
 
+#ifdef TD_TIMING
+// debug build only (make timing): shader-clock stamps per wave of the bidirectional decoder
+__device__ unsigned long long td_times[2048 * 8];
+#define TD_T(k)                                                                                    \
+  do {                                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                                           \
+      td_times[(blockIdx.x * 2 + role) * 8 + (k)] = clock64();                                     \
+      if ((k) == 0 || (k) == 4) td_times[(blockIdx.x * 2 + role) * 8 + 5 + (k) / 4] = wall_clock64(); \
+    }                                                                                              \
+  } while (0)
+#else
+#define TD_T(k)
+#endif
+
 template <int NB, int DIV, int MODE, int CW, bool DOUT>
 __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
@@ -516,6 +530,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
   // nc + 1 slots of 2 KiB: 50 KiB at K = 6144 with 16 sub-blocks
   extern __shared__ s4 cks[];
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
+  TD_T(0);
   const int lane = threadIdx.x & 63;
   const int gl = blockIdx.x * 64 + lane;
   const int nlanes = npairs * NB;
@@ -659,6 +674,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
       }
       if (d == 0) st_fill(o, 0, -TD_INF);
     }
+    TD_T(1);
     // first half: chunks 0 .. qm-1, checkpoint the entering state of each
     {
       auto fwd_chunk = [&](ChunkW<CW> &c, int q) {
@@ -680,7 +696,9 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
       }
       if (q < qm) fwd_chunk(c0, q);
     }
+    TD_T(2);
     __syncthreads();
+    TD_T(3);
     // second half: segments qm .. nc-1 with betas recomputed from the backward checkpoints
     {
       auto seg = [&](ChunkW<CW> &c, int q, bool last) {
@@ -762,6 +780,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
       if (d == NB - 1) o = t;
     }
     ck_put(nc, o); // beta[L] (win.h:372-374)
+    TD_T(1);
     // first half: chunks nc-1 .. qm (steps L-1 .. M); bpre ends as beta[M] before normalisation
     St8 bpre;
     {
@@ -800,7 +819,9 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
         bwd_chunk(c1, qm, CW, true);
       }
     }
+    TD_T(2);
     __syncthreads();
+    TD_T(3);
     // second half: segments qm-1 .. 0 (full), alphas recomputed from the forward checkpoints
     {
       auto seg = [&](ChunkW<CW> &c, int q) {
@@ -837,6 +858,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
       if (q == 0) seg(c0, 0);
     }
   }
+  TD_T(4);
 }
 
 // ------------------------------------------------------------------ SSE non-window ----
@@ -1374,3 +1396,12 @@ hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *dmap, co
 }
 
 } // namespace srsgpu
+
+#ifdef TD_TIMING
+extern "C" int srsgpu_debug_td_times(unsigned long long *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srsgpu::td_times), sizeof(unsigned long long) * n) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
