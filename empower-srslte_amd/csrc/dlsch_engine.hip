@@ -131,6 +131,9 @@ struct DlschEngine {
   bool staged_pending = false;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables;
   TdecEngine tdec;
+  // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
+  EncItem *h_enc = nullptr, *d_enc = nullptr;
+  uint32_t *d_crc_a = nullptr;
   // host-pointer API staging
   int16_t *e_stage = nullptr;
   uint8_t *data_stage = nullptr;
@@ -173,9 +176,9 @@ struct DlschEngine {
     for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
                     (void *)d_noi, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
-                    (void *)data_stage})
+                    (void *)data_stage, (void *)d_enc, (void *)d_crc_a})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap})
+    for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc})
       if (p) (void)hipHostFree(p);
     for (auto &kv : tables) (void)hipFree(kv.second);
     tables.clear();
@@ -194,6 +197,70 @@ struct DlschEngine {
     if (hipMemcpy(d, t.data(), t.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
     tables.emplace(key, d);
     return d;
+  }
+
+  // encode_tb_off (sch.c:187-296) for a batch of TBs: CB i < C2 has K2 (the encoder's order),
+  // E per CB by sch.c:237-241, e bits unpacked (one per byte) at e_offset
+  static constexpr uint32_t CRC_A_LEN = 131072; // > 24 + the largest TBS (110 PRB, 2 layers)
+  int encode(const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const uint8_t *d_data, uint8_t *d_e) {
+    if (!h_enc) {
+      HIPCHK(hipHostMalloc(&h_enc, sizeof(EncItem) * cap));
+      HIPCHK(hipMalloc(&d_enc, sizeof(EncItem) * cap));
+      std::vector<uint32_t> t(CRC_A_LEN);
+      uint32_t r = 1u << 23;
+      for (uint32_t d = 0; d < CRC_A_LEN; d++) { // x^(d+24) mod 0x1864CFB
+        const uint32_t top = r & 0x800000u;
+        r = (r << 1) & 0xFFFFFFu;
+        if (top) r ^= 0x864CFBu;
+        t[d] = r;
+      }
+      HIPCHK(hipMalloc(&d_crc_a, CRC_A_LEN * 4));
+      HIPCHK(hipMemcpy(d_crc_a, t.data(), CRC_A_LEN * 4, hipMemcpyHostToDevice));
+    }
+    const uint32_t *crc_b = tdec.crc_table(0x1800063);
+    if (!crc_b) return -1;
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    uint32_t n = 0;
+    for (uint32_t b = 0; b < ntb; b++) {
+      const srsgpu_dlsch_tb_t &x = tb[b];
+      Segm sg;
+      if (x.tbs == 0) continue;
+      if (segm(x.tbs, sg) || sg.F || x.tbs + 24 > CRC_A_LEN || x.rv > 3 || !x.Qm) {
+        fprintf(stderr, "Error filler bits are not supported. Use standard TBS\n"); // sch.c:203-206
+        return -1;
+      }
+      if (n + sg.C > cap) {
+        fprintf(stderr, "srsgpu: %u code blocks exceed the capacity %u\n", n + sg.C, cap);
+        return -1;
+      }
+      const uint32_t Gp = x.nof_e_bits / x.Qm, gamma = Gp % sg.C;
+      uint32_t rp = 0, wp = 0;
+      for (uint32_t i = 0; i < sg.C; i++, n++) {
+        const uint32_t K = i < sg.C2 ? sg.K2 : sg.K1;
+        EncItem &e = h_enc[n];
+        e.data = d_data + x.data_offset;
+        e.tbs = x.tbs;
+        e.K = K;
+        e.rlen = sg.C > 1 ? K - 24 : K;
+        e.rp = rp;
+        e.ne = i <= sg.C - gamma - 1 ? x.Qm * (Gp / sg.C) : x.Qm * ((Gp + sg.C - 1) / sg.C);
+        e.N = 3 * K + 12;
+        e.table = table(K, x.rv, 0);
+        if (!e.table || tdec.get_interleaver(K, 1)) return -1;
+        e.pi = tdec.fwd;
+        e.last = i == sg.C - 1;
+        e.crc_cb = sg.C > 1;
+        e.e = d_e + x.e_offset + wp;
+        rp += e.rlen;
+        wp += e.ne;
+      }
+    }
+    HIPCHK(hipMemcpyAsync(d_enc, h_enc, sizeof(EncItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    ProfScope ps("k_dlsch_encode", st);
+    HIPCHK(launch_dlsch_encode(d_enc, (int)n, d_crc_a, crc_b, st));
+    return 0;
   }
 
   int16_t *row(uint32_t slot, uint32_t cb) {
@@ -464,6 +531,12 @@ int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t slot, int16_t *rows
                           E.st));
   HIPCHK(hipStreamSynchronize(E.st));
   return 0;
+}
+
+int srsgpu_dlsch_encode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
+                            const uint8_t *d_data, uint8_t *d_e_bits) {
+  if (!q || (!tb && nof_tb) || !d_data || !d_e_bits) return -1;
+  return q->e.encode(tb, nof_tb, d_data, d_e_bits);
 }
 
 int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,

@@ -32,6 +32,17 @@ struct TbItem {
   int32_t preset_ret; // result when C == 0 (tbs == 0 or invalid inputs)
 };
 
+// one code block to encode and rate-match (transmit side)
+struct EncItem {
+  const uint8_t *data;     // TB bytes (MSB first)
+  uint8_t *e;              // ne output bits, one per byte
+  const uint16_t *table;   // receive table (K, rv), natural layout, N entries
+  const uint16_t *pi;      // QPP interleaver pi(i)
+  uint32_t tbs, K, rlen, rp, ne, N;
+  uint32_t last;           // carries the TB CRC
+  uint32_t crc_cb;         // C > 1: CB CRC24B
+};
+
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
                        hipStream_t st);
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
@@ -39,5 +50,8 @@ hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
                             const uint32_t *noi, hipStream_t st);
+// crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
+hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
+                               const uint32_t *crc_b, hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -182,4 +182,92 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ transmit ----
+// encode_tb_off (sch.c:187-296) for one code block per workgroup: the code block's bits are
+// assembled in LDS (TB bits, the TB CRC24A on the last block, the CB CRC24B when C > 1; both
+// CRCs as XOR folds of x^(d+24) mod P over the set bits, crc.c:144-155 being linear), the two
+// RSC encoders of srslte_tcod_encode (turbocoder.c:82-193) run in one lane each over LDS, and
+// rate matching reads the circular buffer through the receive table: e[m] = coded[table[m mod N]]
+// (rm_turbo.c:332-376 is the inverse of the receive mapping).
+__device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); w++) r ^= red[w];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_dlsch_encode(const EncItem *__restrict__ items, int nitems,
+                                                      const uint32_t *__restrict__ crc_a,
+                                                      const uint32_t *__restrict__ crc_b) {
+  __shared__ uint8_t bits[6144];
+  __shared__ uint8_t coded[3 * 6144 + 12];
+  __shared__ uint32_t red[4];
+  const int it = blockIdx.x;
+  if (it >= nitems) return;
+  const EncItem t = items[it];
+  auto data_bit = [&](uint32_t p) -> uint32_t { return (t.data[p >> 3] >> (7 - (p & 7))) & 1u; };
+  uint32_t tcrc = 0;
+  if (t.last) { // TB CRC24A over tbs bits
+    uint32_t acc = 0;
+    for (uint32_t p = threadIdx.x; p < t.tbs; p += blockDim.x)
+      if (data_bit(p)) acc ^= crc_a[t.tbs - 1 - p];
+    tcrc = wg_xor(acc, red);
+  }
+  for (uint32_t j = threadIdx.x; j < t.rlen; j += blockDim.x) {
+    const uint32_t p = t.rp + j;
+    bits[j] = (uint8_t)(p < t.tbs ? data_bit(p) : (tcrc >> (23 - (p - t.tbs))) & 1u);
+  }
+  __syncthreads();
+  if (t.crc_cb) { // CB CRC24B over the rlen bits
+    uint32_t acc = 0;
+    for (uint32_t j = threadIdx.x; j < t.rlen; j += blockDim.x)
+      if (bits[j]) acc ^= crc_b[t.rlen - 1 - j];
+    const uint32_t c = wg_xor(acc, red);
+    if (threadIdx.x < 24) bits[t.rlen + threadIdx.x] = (uint8_t)((c >> (23 - threadIdx.x)) & 1u);
+    __syncthreads();
+  }
+  // turbocoder.c:123-131: fb = u ^ s2 ^ s1, parity = s2 ^ s0 ^ fb; tails :160-177
+  if (threadIdx.x == 0 || threadIdx.x == 64) {
+    const bool second = threadIdx.x == 64;
+    uint32_t s0 = 0, s1 = 0, s2 = 0;
+    for (uint32_t i = 0; i < t.K; i++) {
+      const uint32_t u = second ? bits[t.pi[i]] : bits[i];
+      const uint32_t fb = u ^ s2 ^ s1;
+      const uint32_t par = s2 ^ s0 ^ fb;
+      s2 = s1;
+      s1 = s0;
+      s0 = fb;
+      if (second) {
+        coded[3 * i + 2] = (uint8_t)par;
+      } else {
+        coded[3 * i] = (uint8_t)u;
+        coded[3 * i + 1] = (uint8_t)par;
+      }
+    }
+    const uint32_t o = 3 * t.K + (second ? 6 : 0);
+    for (int j = 0; j < 3; j++) {
+      const uint32_t u = s2 ^ s1; // drives the register to zero
+      const uint32_t fb = u ^ s2 ^ s1;
+      const uint32_t par = s2 ^ s0 ^ fb;
+      s2 = s1;
+      s1 = s0;
+      s0 = fb;
+      coded[o + 2 * j] = (uint8_t)u;
+      coded[o + 2 * j + 1] = (uint8_t)par;
+    }
+  }
+  __syncthreads();
+  for (uint32_t m = threadIdx.x; m < t.ne; m += blockDim.x) t.e[m] = coded[t.table[m % t.N]];
+}
+
+hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
+                               const uint32_t *crc_b, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dlsch_encode, dim3((unsigned)n), dim3(256), 0, st, d_items, n, crc_a, crc_b);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

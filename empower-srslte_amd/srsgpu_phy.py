@@ -133,6 +133,7 @@ _sig = {
                                    ctypes.POINTER(ctypes.c_int32), _u32p]),
     "srsgpu_dlsch_softbuffer_read": (_i32, [_vp, _u32, _i16p, _u8p]),
     "srsgpu_rm_turbo_rx_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
+    "srsgpu_dlsch_encode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp]),
     "srsgpu_pdsch_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32, _u32,
                                    _u32]),
     "srsgpu_pdsch_destroy": (None, [_vp]),
@@ -360,6 +361,12 @@ class Dlsch:
         if _lib.srsgpu_dlsch_softbuffer_read(self.q, slot, _i16(rows), _u8(crc)) != 0:
             raise RuntimeError("softbuffer read failed")
         return rows, crc
+
+    def encode_dev(self, tbs_list, d_data, d_e):
+        """srsgpu_dlsch_encode_dev: tbs_list as for decode (dicts with tbs, rv, Qm, nof_e_bits,
+        e_offset, data_offset)"""
+        arr = self._tbs(tbs_list)
+        return _lib.srsgpu_dlsch_encode_dev(self.q, arr, len(tbs_list), _vp(d_data), _vp(d_e))
 
     def rm_rx_dev(self, d_in, d_out, in_len, K, rv, sb_layout):
         return _lib.srsgpu_rm_turbo_rx_dev(self.q, _vp(d_in), _vp(d_out), in_len, K, rv, sb_layout)

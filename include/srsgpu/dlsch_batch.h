@@ -76,6 +76,15 @@ int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t
 int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t softbuffer, int16_t *rows,
                                  uint8_t *cb_crc);
 
+/* Transmit side (srslte_dlsch_encode2, sch.c:540-; encode_tb_off :187-296), used to synthesise
+ * traffic on the device: per TB, the TB CRC24A, code block segmentation with CRC24B, turbo
+ * encoding (srslte_tcod_encode) and rate matching for tb[i].rv (as the reference produces it
+ * after its rv 0 transmission filled the circular buffer). d_data + data_offset holds tbs/8 bytes;
+ * the nof_e_bits coded bits are written unpacked (one 0/1 byte each) at d_e_bits + e_offset.
+ * Returns -1 for TB sizes with filler bits (sch.c:203-206). */
+int srsgpu_dlsch_encode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
+                            const uint8_t *d_data, uint8_t *d_e_bits);
+
 /* De-rate-matching alone (srslte_rm_turbo_rx_lut_ semantics, rm_turbo.c:394-430) on device
  * buffers: d_out[t[i % (3K+12)]] += d_in[i] for i < in_len, with the sub-block table the AUTO
  * decoder expects when sb_layout != 0 (srslte_tdec_autoimp_get_subblocks(K) > 0). */
