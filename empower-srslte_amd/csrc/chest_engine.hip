@@ -116,6 +116,31 @@ struct ChestEngine {
     HIPCHK(launch_chest(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, d_crs, d_filt, fl, st));
     return 0;
   }
+
+  int put_crs(const uint32_t *sf_idx, uint32_t n, float *d_grid, size_t stride) {
+    if (n > cap) {
+      fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
+      return -1;
+    }
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    const uint32_t np = cell.nof_ports;
+    for (uint32_t i = 0; i < n; i++) {
+      if (sf_idx[i] > 9) return -1;
+      for (uint32_t p = 0; p < np; p++) {
+        ChestItem &t = h_items[i * np + p];
+        t.grid = nullptr;
+        t.ce = (float2 *)d_grid + (i * np + p) * stride;
+        t.noise = nullptr;
+        t.sf_idx = sf_idx[i];
+        t.port = p;
+      }
+    }
+    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    HIPCHK(launch_crs_put(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, d_crs, st));
+    return 0;
+  }
 };
 
 } // namespace srsgpu
@@ -173,6 +198,12 @@ int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_
                               size_t stride, float *d_ce, float *d_noise) {
   if (!q || (!sf_idx && n) || !d_grid || !d_ce) return -1;
   return q->e.estimate(sf_idx, n, d_grid, stride, d_ce, d_noise);
+}
+
+int srsgpu_chest_put_crs_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, float *d_grid,
+                             size_t stride) {
+  if (!q || (!sf_idx && n) || !d_grid) return -1;
+  return q->e.put_crs(sf_idx, n, d_grid, stride);
 }
 
 } // extern "C"

@@ -16,5 +16,8 @@ struct ChestItem {
 // crs: [10 subframes][4 CRS symbols][2*nof_prb] port-0/1 pilots; filt: flen taps (0: no smoothing)
 hipError_t launch_chest(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
                         const float *filt, int flen, hipStream_t st);
+// items[i].ce is the grid plane the port's CRS is written into
+hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
+                          hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -165,4 +165,29 @@ hipError_t launch_chest(const ChestItem *d_items, int n, int nprb, int cell_id, 
   return hipGetLastError();
 }
 
+// srslte_refsignal_cs_put_sf (refsignal_dl.c:380-402): the CRS of a port into its grid plane at
+// symbols 0/4/7/11, subcarriers fidx + 6m
+__global__ __launch_bounds__(256) void k_crs_put(const ChestItem *__restrict__ items, int nitems, int nprb,
+                                                 int cell_id, const float2 *__restrict__ crs) {
+  const int it = blockIdx.x;
+  if (it >= nitems) return;
+  const ChestItem t = items[it];
+  const int np = 2 * nprb, nsc = 12 * nprb, port = (int)t.port;
+  const int sym[4] = {0, 4, 7, 11};
+  const float2 *pil = crs + (size_t)t.sf_idx * 4 * np;
+  float2 *g = t.ce; // the grid plane written
+  for (int e = threadIdx.x; e < 4 * np; e += blockDim.x) {
+    const int l = e / np, m = e % np;
+    const int f = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
+    g[sym[l] * nsc + f + 6 * m] = pil[l * np + m];
+  }
+}
+
+hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
+                          hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_crs_put, dim3((unsigned)n), dim3(256), 0, st, d_items, n, nprb, cell_id, crs);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

@@ -98,4 +98,16 @@ int srsgpu_ofdm_rx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, 
   return 0;
 }
 
+int srsgpu_ofdm_tx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
+                          float *d_out, size_t out_stride) {
+  if (!q || !d_in || !d_out) return -1;
+  if (out_stride < 15 * (size_t)q->N || in_stride < 14 * 12 * (size_t)q->nof_prb) return -1;
+  const float scale = q->normalize ? 1.0f / sqrtf((float)q->N) : 1.0f;
+  srsgpu::ProfScope ps("k_ofdm_tx", q->st);
+  HIPCHK(srsgpu::launch_ofdm_tx((const float2 *)d_in, in_stride, (float2 *)d_out, out_stride, (int)nof_sf,
+                                (int)q->N, (int)(12 * q->nof_prb), q->d_tw, q->radices, q->nstages, scale,
+                                q->st));
+  return 0;
+}
+
 } // extern "C"

@@ -10,5 +10,9 @@ namespace srsgpu {
 hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
                           int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
                           hipStream_t st);
+// transmit: nsf grids (14 x nre at in + i*in_stride) -> 15 N time samples at out + i*out_stride
+hipError_t launch_ofdm_tx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
+                          int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
+                          hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -112,4 +112,58 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
   return hipGetLastError();
 }
 
+// srslte_ofdm_tx_sf (ofdm.c:491-598), normal CP: per symbol the grid row goes to bins
+// [1, 1 + nre/2) (upper half) and [N - nre/2, N) (lower half), DC and guards zero, an
+// unnormalised backward DFT (FFTW backward: e^{+2 pi i k n / N}, here conj(FFT(conj(x)))), the
+// optional 1/sqrt(N) scaling, and the last cp samples copied in front of the symbol.
+__global__ __launch_bounds__(256) void k_ofdm_tx(const float2 *__restrict__ in, size_t in_stride,
+                                                 float2 *__restrict__ out, size_t out_stride, int N,
+                                                 int nre, int cp0, int cp, const float2 *__restrict__ tw,
+                                                 const uint32_t radices, int nstages, float scale) {
+  __shared__ cf buf[2][OFDM_MAXN];
+  const int sym = blockIdx.x % 14, sf = blockIdx.x / 14;
+  const int slot = sym / 7, l = sym % 7;
+  const cf *src = (const cf *)(in + (size_t)sf * in_stride + (size_t)sym * nre);
+  const int h = nre / 2;
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    cf v = {0.f, 0.f};
+    if (n >= 1 && n < 1 + h)
+      v = src[h + n - 1];
+    else if (n >= N - h)
+      v = src[n - (N - h)];
+    buf[0][n] = cf{v.x, -v.y};
+  }
+  __syncthreads();
+  int cur = 0, Ns = 1;
+  for (int st = 0; st < nstages; st++) {
+    const int R = (radices >> (4 * st)) & 15;
+    if (R == 4)
+      stage<4>(buf[cur], buf[cur ^ 1], N, Ns, tw);
+    else if (R == 2)
+      stage<2>(buf[cur], buf[cur ^ 1], N, Ns, tw);
+    else
+      stage<3>(buf[cur], buf[cur ^ 1], N, Ns, tw);
+    __syncthreads();
+    cur ^= 1;
+    Ns *= R;
+  }
+  const int c = l == 0 ? cp0 : cp;
+  const size_t start = (size_t)slot * (N * 15 / 2) + (l ? cp0 + N + (size_t)(l - 1) * (N + cp) : 0);
+  cf *dst = (cf *)(out + (size_t)sf * out_stride + start);
+  for (int n = threadIdx.x; n < N + c; n += blockDim.x) {
+    const cf v = buf[cur][n < c ? N - c + n : n - c];
+    dst[n] = cf{v.x * scale, -v.y * scale};
+  }
+}
+
+hipError_t launch_ofdm_tx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
+                          int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
+                          hipStream_t st) {
+  if (nsf <= 0) return hipSuccess;
+  const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
+  hipLaunchKernelGGL(k_ofdm_tx, dim3((unsigned)nsf * 14), dim3(256), 0, st, in, in_stride, out, out_stride,
+                     N, nre, cp0, cp, tw, radices, nstages, scale);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

@@ -94,6 +94,10 @@ struct PdschEngine {
   uint32_t max_re = 0, max_bits = 0, cwords = 0;
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
+  // transmit side (lazily allocated)
+  TxItem *h_tx = nullptr, *d_tx = nullptr;
+  uint8_t *d_ebits = nullptr; // [2 max_sf][max_bits] coded bits
+  float2 *d_mod = nullptr;    // constellation tables
 
   int create(const srsgpu_cell_t &c, uint32_t nsb, uint32_t max_cb, uint32_t msf) {
     if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !msf ||
@@ -145,9 +149,10 @@ struct PdschEngine {
   void destroy() {
     if (st) (void)hipStreamSynchronize(st);
     for (void *p : {(void *)d_x1, (void *)d_x2b, (void *)d_gold, (void *)d_llr, (void *)d_c,
-                    (void *)d_csi, (void *)d_csimax, (void *)d_e})
+                    (void *)d_csi, (void *)d_csimax, (void *)d_e, (void *)d_tx, (void *)d_ebits,
+                    (void *)d_mod})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb})
+    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb, (void *)h_tx})
       if (p) (void)hipHostFree(p);
     for (auto &kv : maps) (void)hipFree(kv.second.first);
     maps.clear();
@@ -276,6 +281,88 @@ struct PdschEngine {
     return 0;
   }
 
+  // srslte_pdsch_encode (pdsch.c:1048-1131), single antenna port: DL-SCH encoding of each TB,
+  // then scrambling, modulation and RE mapping into the subframe's grid (other REs untouched)
+  int encode(const srsgpu_pdsch_sf_t *sf, uint32_t n, const uint8_t *d_data, float *d_grid) {
+    if (n > max_sf) {
+      fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
+      return -1;
+    }
+    if (!h_tx) {
+      HIPCHK(hipHostMalloc(&h_tx, sizeof(TxItem) * max_sf));
+      HIPCHK(hipMalloc(&d_tx, sizeof(TxItem) * max_sf));
+      HIPCHK(hipMalloc(&d_ebits, (size_t)max_sf * max_bits + 64));
+      // modem/lte_tables.c: levels k / sqrt(N) in double, stored as float; 36.211 7.1 bit order
+      std::vector<float2> t;
+      const float b = (float)(1 / sqrt(2.0));
+      t.push_back(make_float2(b, b));
+      t.push_back(make_float2(-b, -b));
+      for (int i = 0; i < 4; i++) t.push_back(make_float2(i & 2 ? -b : b, i & 1 ? -b : b));
+      const float l16[2] = {(float)(1 / sqrt(10.0)), (float)(3 / sqrt(10.0))};
+      for (int i = 0; i < 16; i++) { // b0 b1 signs, b2 b3 levels
+        const float re = l16[(i >> 1) & 1], im = l16[i & 1];
+        t.push_back(make_float2(i & 8 ? -re : re, i & 4 ? -im : im));
+      }
+      const float l64[4] = {(float)(3 / sqrt(42.0)), (float)(1 / sqrt(42.0)), (float)(5 / sqrt(42.0)),
+                            (float)(7 / sqrt(42.0))}; // (b2 b4) / (b3 b5) = 00 01 10 11
+      for (int i = 0; i < 64; i++) {
+        const int bi = ((i >> 3) & 1) << 1 | ((i >> 1) & 1), bq = ((i >> 2) & 1) << 1 | (i & 1);
+        t.push_back(make_float2(i & 32 ? -l64[bi] : l64[bi], i & 16 ? -l64[bq] : l64[bq]));
+      }
+      HIPCHK(hipMalloc(&d_mod, t.size() * sizeof(float2)));
+      HIPCHK(hipMemcpy(d_mod, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
+    }
+    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    uint32_t mre = 0, mbits = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const srsgpu_pdsch_sf_t &s = sf[i];
+      if (check(s, i)) return -1;
+      if (s.mimo_type != SRSGPU_MIMO_SINGLE_ANTENNA) {
+        fprintf(stderr, "srsgpu: the GPU transmitter covers single-antenna PDSCH\n");
+        return -1;
+      }
+      uint32_t nre = 0;
+      const uint32_t *m = map(s, &nre);
+      if (!m) return -1;
+      if (nre != s.nof_re) {
+        fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
+        return -1;
+      }
+      const int q = kQm[s.mod[0]];
+      srsgpu_dlsch_tb_t &t = h_tb[i];
+      t.tbs = s.tbs[0];
+      t.rv = s.rv[0];
+      t.Qm = (uint32_t)q;
+      t.nof_e_bits = nre * q;
+      t.softbuffer = 0;
+      t.e_offset = (uint64_t)i * max_bits;
+      t.data_offset = s.data_offset[0];
+      GoldItem &g = h_gold[i];
+      g.seed = ((uint32_t)s.rnti << 14) + ((2 * s.sf_idx / 2) << 9) + cell.id;
+      g.len = nre * q;
+      g.c = d_c + (size_t)i * cwords;
+      TxItem &x = h_tx[i];
+      x.e = d_ebits + (size_t)i * max_bits;
+      x.c = g.c;
+      x.map = m;
+      x.grid = (float2 *)d_grid + s.grid_offset;
+      x.nof_re = nre;
+      x.qm = q;
+      x.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
+      mre = std::max(mre, nre);
+      mbits = std::max(mbits, nre * q);
+    }
+    if (srsgpu_dlsch_encode_dev(dl, h_tb, n, d_data, d_ebits)) return -1;
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(staged, st));
+    staged_pending = true;
+    HIPCHK(launch_gold(d_gold, (int)n, mbits, d_x1, d_x2b, gold_words, st));
+    ProfScope ps("k_pdsch_tx", st);
+    HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));
+    return 0;
+  }
+
   uint32_t count_tb(const srsgpu_pdsch_sf_t *sf, uint32_t n) const {
     uint32_t k = 0;
     for (uint32_t i = 0; i < n; i++) k += nof_tb(sf[i]);
@@ -343,6 +430,12 @@ int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_
   std::vector<int16_t *> e(k);
   for (uint32_t i = 0; i < k; i++) e[i] = d_e + e_offset[i];
   return q->e.llr(sf, n, d_grid, d_ce, ant_stride, e.data());
+}
+
+int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n,
+                            const uint8_t *d_data, float *d_grid) {
+  if (!q || (!sf && n) || !d_data || !d_grid) return -1;
+  return q->e.encode(sf, n, d_data, d_grid);
 }
 
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,

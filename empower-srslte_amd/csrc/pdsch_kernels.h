@@ -33,8 +33,22 @@ struct LlrItem {
   int nports;              // ports in noise_dev
 };
 
+// one codeword to transmit: scramble + modulate + map
+struct TxItem {
+  const uint8_t *e;        // nof_re * qm coded bits, one per byte
+  const uint32_t *c;       // packed scrambling bits
+  const uint32_t *map;     // RE j -> grid position
+  float2 *grid;            // port-0 grid of the subframe
+  uint32_t nof_re;
+  int qm;
+  float scaling;
+};
+
 hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,
                        const uint32_t *x2b, uint32_t words, hipStream_t st);
 hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st);
+// tables: 2 BPSK + 4 QPSK + 16 16QAM + 64 64QAM constellation points (lte_tables.c order)
+hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const float2 *tables,
+                           hipStream_t st);
 } // namespace srsgpu
 #endif

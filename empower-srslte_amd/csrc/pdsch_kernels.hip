@@ -359,4 +359,34 @@ hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ transmit ----
+// srslte_pdsch_encode for one single-antenna codeword (pdsch.c:1048-1131): scrambling of the
+// coded bits (srslte_scrambling_bytes), modulation (srslte_mod_modulate_bytes with the LTE tables
+// of modem/lte_tables.c: index = bits MSB first), optional rho_a scaling, RE mapping (pdsch_put).
+__global__ __launch_bounds__(256) void k_pdsch_tx(const TxItem *__restrict__ items, int nitems,
+                                                  const float2 *__restrict__ tables) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  const TxItem t = items[it];
+  const float2 *tab = tables + (t.qm == 1 ? 0 : t.qm == 2 ? 2 : t.qm == 4 ? 6 : 22);
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
+    const uint32_t b0 = j * (uint32_t)t.qm, w = b0 >> 5, sh = b0 & 31;
+    const uint64_t cw = (uint64_t)t.c[w] | ((uint64_t)t.c[w + 1] << 32);
+    const uint32_t cb = (uint32_t)(cw >> sh);
+    uint32_t idx = 0;
+    for (int k = 0; k < t.qm; k++) idx = (idx << 1) | ((t.e[b0 + k] ^ (cb >> k)) & 1u);
+    float2 v = tab[idx];
+    if (t.scaling != 1.0f) v = make_float2(v.x * t.scaling, v.y * t.scaling);
+    t.grid[t.map[j]] = v;
+  }
+}
+
+hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const float2 *tables,
+                           hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned gx = std::min(cdiv(max_re, 256), 64u);
+  hipLaunchKernelGGL(k_pdsch_tx, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n, tables);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

@@ -158,6 +158,9 @@ _sig = {
     "srsgpu_ofdm_rx_set_stream": (None, [_vp, _vp]),
     "srsgpu_ofdm_rx_set_normalize": (None, [_vp, _i32]),
     "srsgpu_ofdm_rx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
+    "srsgpu_ofdm_tx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
+    "srsgpu_chest_put_crs_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz]),
+    "srsgpu_pdsch_encode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
     "srsgpu_prof_get": (_i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -441,6 +444,11 @@ class Pdsch:
         return _lib.srsgpu_pdsch_llr_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                          _vp(d_e), offs)
 
+    def encode_dev(self, sfs, d_data, d_grid):
+        """srsgpu_pdsch_encode_dev: TB bytes (data_offset[0]) -> PDSCH REs of each grid"""
+        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+        return _lib.srsgpu_pdsch_encode_dev(self.q, arr, len(sfs), _vp(d_data), _vp(d_grid))
+
     def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_data, max_halfits, d_ret, d_noi):
         arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
         return _lib.srsgpu_pdsch_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
@@ -478,6 +486,11 @@ class Chest:
     def set_filter3(self, w):
         _lib.srsgpu_chest_set_smooth_filter3_coeff(self.q, w)
 
+    def put_crs_dev(self, sf_idx, d_grid, stride):
+        n = len(sf_idx)
+        arr = (ctypes.c_uint32 * n)(*sf_idx)
+        return _lib.srsgpu_chest_put_crs_dev(self.q, arr, n, _vp(d_grid), stride)
+
     def estimate_dev(self, sf_idx, d_grid, stride, d_ce, d_noise=None):
         n = len(sf_idx)
         arr = (ctypes.c_uint32 * n)(*sf_idx)
@@ -513,6 +526,10 @@ class OfdmRx:
 
     def rx_dev(self, n, d_in, in_stride, d_out, out_stride):
         return _lib.srsgpu_ofdm_rx_sf_dev(self.q, n, _vp(d_in), in_stride, _vp(d_out), out_stride)
+
+    def tx_dev(self, n, d_in, in_stride, d_out, out_stride):
+        """srsgpu_ofdm_tx_sf_dev: grids -> time-domain subframes (same handle)"""
+        return _lib.srsgpu_ofdm_tx_sf_dev(self.q, n, _vp(d_in), in_stride, _vp(d_out), out_stride)
 
     def close(self):
         if self.q:

@@ -43,6 +43,12 @@ void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w);
 int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t nof_grids,
                               const float *d_grid, size_t stride, float *d_ce, float *d_noise);
 
+/* Transmit side (srslte_refsignal_cs_put_sf, refsignal_dl.c:380-402): the CRS of every port of
+ * the cell into nof_grids grids; port p of grid i is the plane d_grid + (i*nof_ports + p)*stride.
+ * Used to synthesise traffic on the device. */
+int srsgpu_chest_put_crs_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t nof_grids,
+                             float *d_grid, size_t stride);
+
 #ifdef __cplusplus
 }
 #endif

@@ -35,6 +35,13 @@ void srsgpu_ofdm_rx_set_normalize(srsgpu_ofdm_t *q, int enable);
 int srsgpu_ofdm_rx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
                           float *d_out, size_t out_stride);
 
+/* Transmit direction on the same handle (srslte_ofdm_tx_sf, ofdm.c:491-598; tx plans are
+ * unnormalised by default, ofdm.c:276; srsgpu_ofdm_rx_set_normalize applies 1/sqrt(N) here too):
+ * grid i at d_in + i*in_stride (14 x 12 nof_prb) -> 15 symbol_sz samples with CPs at
+ * d_out + i*out_stride. Used to synthesise traffic on the device. */
+int srsgpu_ofdm_tx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
+                          float *d_out, size_t out_stride);
+
 #ifdef __cplusplus
 }
 #endif

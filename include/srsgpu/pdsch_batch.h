@@ -95,6 +95,14 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
                             const float *d_grid, const float *d_ce, size_t ant_stride,
                             uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
 
+/* Transmit side, used to synthesise traffic on the device (srslte_pdsch_encode, pdsch.c:1048-1131,
+ * single antenna port): per subframe, DL-SCH encoding of TB 0 (srsgpu_dlsch_encode_dev, rv from
+ * sf[i].rv[0]), scrambling, modulation (modem/lte_tables.c), rho_a scaling and RE mapping into
+ * the port-0 grid at d_grid + grid_offset. REs outside the grant (CRS, control region) are left
+ * as they are: srsgpu_chest_put_crs_dev writes the CRS. */
+int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
+                            const uint8_t *d_data, float *d_grid);
+
 /* RE count of a grant (srslte_pdsch_get's return value). */
 int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf);
 
