@@ -228,6 +228,53 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1):
             "data": "synthetic 64QAM symbols (not codewords: every CB runs 8 half-iterations)"}
 
 
+def run_traffic(s, torch, dev, steps, warmup, kind):
+    """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
+    with CRC early stop (max 8 half-iterations, srsUE's default):
+    kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes interleaved over cells of
+      6/25/50/100 PRB, random allocation and MCS 0..28 (K 40..6144), all cells' TBs in one
+      DL-SCH call; AWGN at 20 dB.
+    kind "c3_coded" — the C3 subframe (100 PRB, MCS 28, TBS 75376) as real codewords at 30 dB
+      (the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst case."""
+    import srsgpu_traffic as tr
+    table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    if kind == "c5":
+        m = tr.MixedCells(table, C3_SF, torch, dev, seed=21, stream=stream, snr_db=20.0)
+    else:
+        m = tr.MixedCells(table, C3_SF, torch, dev, prbs=(100,), seed=22, stream=stream,
+                          snr_db=30.0, mcs=28, full_band=True)
+    for _ in range(warmup):
+        m.step()
+    torch.cuda.synchronize()
+    s.prof_reset()
+    s.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    s.prof_enable(False)
+    stages = {}
+    for name in ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_win_halfit",
+                 "k_sse_halfit", "k_tb_finish"):
+        ms, cnt = s.prof_get(name)
+        if cnt:
+            stages[name] = round(ms / steps, 4)
+    acks, good, noi = m.check()
+    ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in m.tb_list})
+    out = {"workload": ("c5_mixed_bw_%dsf_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
+                        "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS)),
+           "subframes_per_s": round(C3_SF * steps / el, 1),
+           "tb_mbps": round(m.bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+           "code_blocks": m.ncb, "distinct_K": len(ks), "K_range": [ks[0], ks[-1]],
+           "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": m.ntb, "nof_iterations_mean": noi,
+           "stage_ms_per_batch": stages,
+           "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % ("20" if kind == "c5" else "30")}
+    m.close()
+    return out
+
+
 def reduce_over_ranks(dist, dev, elapsed, bit_errors):
     """Job time = the slowest rank's timed region (it is bracketed by barriers); bit errors are
     summed. Identity on a single process."""
@@ -367,12 +414,26 @@ def main():
             ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
             pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe3["tb_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
+    extra = {}
+    if not args.no_pipeline:
+        for kind in ("c3_coded", "c5"):
+            r = run_traffic(s, torch, dev, max(1, args.steps // 2), 1, kind)
+            if dist:
+                ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
+                r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)
+                r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            extra[kind] = r
     if rank == 0 and pipe:
         result["config"]["subframes_per_s"] = pipe["subframes_per_s"]
         result["pipeline"] = pipe
     if rank == 0 and pipe3:
         result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
         result["pipeline_tm3"] = pipe3
+    if rank == 0 and extra:
+        result["config"]["subframes_per_s_coded"] = extra["c3_coded"]["subframes_per_s"]
+        result["config"]["subframes_per_s_c5"] = extra["c5"]["subframes_per_s"]
+        result["pipeline_coded"] = extra["c3_coded"]
+        result["pipeline_c5"] = extra["c5"]
     if rank == 0 and not args.no_cpu_baseline and nranks == 1:
         result["cpu_baseline"] = cpu_baseline(llr, int(os.environ.get("SRSGPU_CPU_THREADS",
                                                                        min(16, os.cpu_count() or 1))))

@@ -4,9 +4,10 @@
 //   host      code block segmentation and the per-CB receive parameters of decode_tb_cb
 //             (sch.c:325-341), grouping of the CBs by (K, CRC) for the turbo decoder
 //   k_derm    de-rate-matching + HARQ combining of every CB into its softbuffer row
-//   decoder   per (K, CRC) group: TdecEngine::decode on the softbuffer rows themselves (row
-//             pointer table, SB layout), CRC early stop per half-iteration, CBs that passed in an
-//             earlier transmission start out "done"
+//   decoder   ONE TdecEngine job over all (K, CRC) groups (one launch per decoder variant and
+//             half-iteration, however many sizes) on the softbuffer rows themselves (row pointer
+//             table, SB layout), CRC early stop per half-iteration, CBs that passed in an earlier
+//             transmission start out "done"
 //   k_tb_finish  TB bytes, cb_crc / saved bytes, nof_iterations, TB CRC
 #include <hip/hip_runtime.h>
 
@@ -168,7 +169,20 @@ struct DlschEngine {
     HIPCHK(hipHostMalloc(&h_rows, sizeof(int16_t *) * cap));
     HIPCHK(hipHostMalloc(&h_cbmap, sizeof(uint32_t) * cap));
     HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
-    return tdec.create(cap, 6144);
+    if (tdec.create(cap, 6144)) return -1;
+    // x^(d+24) mod 0x1864CFB for every bit distance d of a TB: the TB CRC24A as a parallel XOR
+    // fold (k_tb_finish, k_dlsch_encode)
+    std::vector<uint32_t> t(CRC_A_LEN);
+    uint32_t r = 1u << 23;
+    for (uint32_t d = 0; d < CRC_A_LEN; d++) {
+      const uint32_t top = r & 0x800000u;
+      r = (r << 1) & 0xFFFFFFu;
+      if (top) r ^= 0x864CFBu;
+      t[d] = r;
+    }
+    HIPCHK(hipMalloc(&d_crc_a, CRC_A_LEN * 4));
+    HIPCHK(hipMemcpy(d_crc_a, t.data(), CRC_A_LEN * 4, hipMemcpyHostToDevice));
+    return 0;
   }
 
   void destroy() {
@@ -201,21 +215,11 @@ struct DlschEngine {
 
   // encode_tb_off (sch.c:187-296) for a batch of TBs: CB i < C2 has K2 (the encoder's order),
   // E per CB by sch.c:237-241, e bits unpacked (one per byte) at e_offset
-  static constexpr uint32_t CRC_A_LEN = 131072; // > 24 + the largest TBS (110 PRB, 2 layers)
+  static constexpr uint32_t CRC_A_LEN = 400000; // > 24 + the largest TBS (391656, 36.213)
   int encode(const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const uint8_t *d_data, uint8_t *d_e) {
     if (!h_enc) {
       HIPCHK(hipHostMalloc(&h_enc, sizeof(EncItem) * cap));
       HIPCHK(hipMalloc(&d_enc, sizeof(EncItem) * cap));
-      std::vector<uint32_t> t(CRC_A_LEN);
-      uint32_t r = 1u << 23;
-      for (uint32_t d = 0; d < CRC_A_LEN; d++) { // x^(d+24) mod 0x1864CFB
-        const uint32_t top = r & 0x800000u;
-        r = (r << 1) & 0xFFFFFFu;
-        if (top) r ^= 0x864CFBu;
-        t[d] = r;
-      }
-      HIPCHK(hipMalloc(&d_crc_a, CRC_A_LEN * 4));
-      HIPCHK(hipMemcpy(d_crc_a, t.data(), CRC_A_LEN * 4, hipMemcpyHostToDevice));
     }
     const uint32_t *crc_b = tdec.crc_table(0x1800063);
     if (!crc_b) return -1;
@@ -246,8 +250,9 @@ struct DlschEngine {
         e.ne = i <= sg.C - gamma - 1 ? x.Qm * (Gp / sg.C) : x.Qm * ((Gp + sg.C - 1) / sg.C);
         e.N = 3 * K + 12;
         e.table = table(K, x.rv, 0);
-        if (!e.table || tdec.get_interleaver(K, 1)) return -1;
-        e.pi = tdec.fwd;
+        const TdecEngine::Interl *il = e.table ? tdec.get_interleaver(K, 1) : nullptr;
+        if (!il) return -1;
+        e.pi = il->fwd;
         e.last = i == sg.C - 1;
         e.crc_cb = sg.C > 1;
         e.e = d_e + x.e_offset + wp;
@@ -386,21 +391,24 @@ struct DlschEngine {
       ProfScope ps("k_derm", st);
       HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st));
     }
+    // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
+    std::vector<TdSpec> specs;
     for (uint32_t p0 = 0; p0 < order.size();) {
       const Cb &c = cbs[order[p0]];
       uint32_t p1 = p0 + 1;
       while (p1 < order.size() && cbs[order[p1]].K == c.K && cbs[order[p1]].poly == c.poly &&
              cbs[order[p1]].crclen == c.crclen)
         p1++;
-      if (tdec.decode(SRSLTE_TDEC_AUTO, 1, nullptr, 0, c.K, p1 - p0, maxh, c.poly, c.crclen,
-                      d_dec + (size_t)p0 * 768, 768, d_ok + p0, d_noi + p0,
-                      (const int16_t *const *)(d_rows + p0), 1, d_init + p0))
-        return -1;
+      specs.push_back(TdSpec{c.K, p1 - p0, c.poly, c.crclen, p0});
       p0 = p1;
     }
+    if (!specs.empty() &&
+        tdec.decode_multi(SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
+                          (const int16_t *const *)d_rows, 1, d_init, maxh, d_dec, 768, d_ok, d_noi))
+      return -1;
     {
       ProfScope ps("k_tb_finish", st);
-      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, st));
+      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st));
     }
     return 0;
   }

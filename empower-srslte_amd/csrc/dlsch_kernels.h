@@ -47,9 +47,10 @@ hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint
                        hipStream_t st);
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
+// crc_a[d] = x^(d+24) mod P_24A for d < the largest TBS + 24
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
-                            const uint32_t *noi, hipStream_t st);
+                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st);
 // crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
 hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
                                const uint32_t *crc_b, hipStream_t st);

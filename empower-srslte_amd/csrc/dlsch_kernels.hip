@@ -59,17 +59,15 @@ __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ i
   }
 }
 
-// MSB-first CRC24 byte table (crc.c:43-62 gen_crc_table for order 24)
-__device__ static void crc24_table(uint32_t *table, uint32_t poly) {
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    uint32_t crc = (uint32_t)i << 16;
-    for (int j = 0; j < 8; j++) {
-      const uint32_t bit = crc & 0x800000u;
-      crc <<= 1;
-      if (bit) crc ^= poly;
-    }
-    table[i] = crc & 0xFFFFFFu;
-  }
+// XOR-reduce one value per thread over the workgroup
+__device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
+  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t r = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); w++) r ^= red[w];
+  __syncthreads();
+  return r;
 }
 
 __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tbs_, int ntb,
@@ -77,8 +75,9 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint8_t *__restrict__ dec, size_t dec_stride,
                                                    const uint8_t *__restrict__ cb_ok_in,
                                                    const uint8_t *__restrict__ init_done,
-                                                   const uint32_t *__restrict__ noi_in) {
-  __shared__ uint32_t table[256];
+                                                   const uint32_t *__restrict__ noi_in,
+                                                   const uint32_t *__restrict__ crc_a) {
+  __shared__ uint32_t red[4];
   __shared__ int all_ok;
   __shared__ uint32_t noi_sum;
   const int b = blockIdx.x;
@@ -91,7 +90,6 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
     }
     return;
   }
-  crc24_table(table, 0x1864CFBu);
   if (threadIdx.x == 0) {
     all_ok = 1;
     noi_sum = 0;
@@ -141,14 +139,26 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       for (uint32_t j = threadIdx.x; j < rlen / 8; j += blockDim.x) dst[j] = src[j];
     }
   }
+  // TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491), as a parallel XOR fold:
+  // crc.c:144-155 is linear, the checksum is the XOR of x^(tbs-1-p+24) mod P over set bits p
+  uint32_t crc = 0;
+  if (all_ok) {
+    uint32_t acc = 0;
+    const uint32_t nbytes = t.tbs / 8;
+    for (uint32_t j = threadIdx.x; j < nbytes; j += blockDim.x) {
+      const uint32_t v = t.data[j];
+      const uint32_t *w = crc_a + (t.tbs - 1 - 8 * j); // w[-b]: bit b (MSB first) of byte j
+#pragma unroll
+      for (int b = 0; b < 8; b++)
+        if ((v >> (7 - b)) & 1u) acc ^= *(w - b);
+    }
+    crc = wg_xor(acc, red);
+  }
   if (threadIdx.x == 0) {
     *t.noi = noi_sum / t.C;
     int ret = -1;
-    if (all_ok) { // TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491)
-      uint32_t crc = 0;
+    if (all_ok) {
       const uint32_t nbytes = t.tbs / 8;
-      for (uint32_t i = 0; i < nbytes; i++)
-        crc = ((crc << 8) ^ table[((crc >> 16) & 0xff) ^ t.data[i]]) & 0xFFFFFFu;
       const uint32_t tx = ((uint32_t)t.data[nbytes] << 16) | ((uint32_t)t.data[nbytes + 1] << 8) |
                           t.data[nbytes + 2];
       ret = (crc == tx && crc) ? 0 : -1;
@@ -175,10 +185,10 @@ hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st) {
 
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
-                            const uint32_t *noi, hipStream_t st) {
+                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi);
+                     dec_stride, cb_ok, init_done, noi, crc_a);
   return hipGetLastError();
 }
 
@@ -189,16 +199,6 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
 // RSC encoders of srslte_tcod_encode (turbocoder.c:82-193) run in one lane each over LDS, and
 // rate matching reads the circular buffer through the receive table: e[m] = coded[table[m mod N]]
 // (rm_turbo.c:332-376 is the inverse of the receive mapping).
-__device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
-  for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t r = 0;
-  for (int w = 0; w < (int)(blockDim.x >> 6); w++) r ^= red[w];
-  __syncthreads();
-  return r;
-}
-
 __global__ __launch_bounds__(256) void k_dlsch_encode(const EncItem *__restrict__ items, int nitems,
                                                       const uint32_t *__restrict__ crc_a,
                                                       const uint32_t *__restrict__ crc_b) {

@@ -8,6 +8,7 @@
 #include <map>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 #include <utility>
 #include <vector>
 
@@ -56,16 +57,22 @@ int impl_nb(int r);
 void gen_interleaver(uint32_t K, uint32_t nb, std::vector<uint16_t> &fwd, std::vector<uint16_t> &rev);
 
 // ------------------------------------------------------------------ engine ----
+// A job = code blocks of one or many sizes. TdSpec lists them in the caller's numbering: spec i
+// holds n code blocks of size K numbered cb0 .. cb0+n-1 (input rows, outputs and per-CB flags use
+// that number) and the CRC its early stop checks. The engine turns the specs into device groups
+// (tdec_kernels.h), ordered by decoder variant, and runs every half-iteration as one launch per
+// variant plus one decide launch, whatever the number of distinct sizes.
+struct TdSpec {
+  uint32_t K, n, poly, crc_len, cb0;
+};
+
 struct TdecEngine {
   hipStream_t st = nullptr;
   uint32_t cap_cbs = 0, cap_K = 0;
-  size_t cap_pairs = 0;
-  // pair-interleaved arrays [pairs][K]: SP0 short4; XP1 = X2, P1 short2 planes; A short2;
-  // T short2 [pairs][12]
-  void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr;
-  void *D = nullptr; // [pairs][NB][ceil(K/NB/16)] uint32: packed hard decisions (k_decide input)
-  void *scratch = nullptr; // checkpoints (windowed) / alpha-beta (sequential)
-  size_t scratch_bytes = 0;
+  size_t cap_pairs = 0, cap_elems = 0, cap_dw = 0, cap_sc = 0;
+  // concatenated per-group arrays: SP0 short4; XP1 = X2, P1 short2 planes of cap_elems; A short2;
+  // T short2 [pairs][12]; D packed decisions; scratch (sequential decoders)
+  void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr, *D = nullptr, *scratch = nullptr;
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
   uint32_t *noi = nullptr;
   int16_t *in_stage = nullptr; // host-pointer API staging
@@ -74,11 +81,22 @@ struct TdecEngine {
     uint16_t *fwd, *rev, *dmap;
   };
   std::map<std::pair<uint32_t, uint32_t>, Interl> interl;
-  std::map<uint32_t, uint32_t *> crc_tables; // poly -> x^(d+24) mod poly, d < 6144 (k_decide)
-  // current job
+  std::map<uint32_t, uint32_t *> crc_tables; // poly -> x^(d+24) mod P, d < 6144 (k_decide)
+  // current job (one pass)
+  std::vector<TdGroup> groups; // kind order
+  TdGroup *d_groups = nullptr, *h_groups = nullptr;
+  size_t groups_cap = 0, uploaded = 0;
+  hipEvent_t gev = nullptr;
+  bool gev_pending = false;
+  int kind_g0[TD_NKIND + 1] = {0};
+  int kind_blocks[TD_NKIND] = {0};
+  size_t kind_lds[TD_NKIND] = {0};
+  int total_pairs = 0;
+  // K and interleaver of the last single-size job (the drop-in srslte_tdec_* path)
   uint32_t K = 0;
-  int impl_r = 0, nb = 1, ncb = 0, npairs = 0;
   const uint16_t *fwd = nullptr, *rev = nullptr, *dmap = nullptr;
+
+  static constexpr size_t EXTRA_PAIRS = 256; // odd groups each add half a pair
 
   int create(uint32_t max_cbs, uint32_t max_K) {
     if (max_cbs == 0 || max_K == 0 || max_K > SRSLTE_TCOD_MAX_LEN_CB) {
@@ -92,32 +110,33 @@ struct TdecEngine {
     }
     cap_cbs = max_cbs;
     cap_K = max_K;
-    cap_pairs = (max_cbs + 1) / 2;
-    const size_t arr = cap_pairs * max_K * 4;
-    HIPCHK(hipMalloc(&SP0, arr * 2));
-    HIPCHK(hipMalloc(&XP1, arr * 2));
-    HIPCHK(hipMalloc(&A, arr));
-    HIPCHK(hipMalloc(&D, cap_pairs * (max_K / 16 + 16) * 4));
+    cap_pairs = (max_cbs + 1) / 2 + EXTRA_PAIRS;
+    cap_elems = (size_t)((max_cbs + 1) / 2) * max_K + EXTRA_PAIRS * std::min<uint32_t>(max_K, 1024);
+    cap_dw = cap_elems / 16 + cap_pairs * 16;
+    cap_sc = (cap_elems + 4 * cap_pairs) * 8;
+    HIPCHK(hipMalloc(&SP0, cap_elems * 8));
+    HIPCHK(hipMalloc(&XP1, cap_elems * 8));
+    HIPCHK(hipMalloc(&A, cap_elems * 4));
+    HIPCHK(hipMalloc(&D, cap_dw * 4));
     HIPCHK(hipMalloc(&T, cap_pairs * 12 * 4));
-    size_t ck = 0;
-    for (int nbv : {8, 16}) {
-      if (max_K / nbv > 40) ck = std::max(ck, srsgpu::win_ck_bytes((int)max_K, nbv, (int)cap_pairs));
-    }
-    scratch_bytes = std::max(ck, srsgpu::seq_scratch_bytes((int)max_K, (int)cap_pairs));
-    HIPCHK(hipMalloc(&scratch, scratch_bytes));
-    HIPCHK(hipMalloc(&cb_done, cap_pairs * 2));
-    HIPCHK(hipMalloc(&cb_ok, cap_pairs * 2));
+    HIPCHK(hipMalloc(&scratch, cap_sc * 4));
+    HIPCHK(hipMalloc(&cb_done, cap_cbs));
+    HIPCHK(hipMalloc(&cb_ok, cap_cbs));
     HIPCHK(hipMalloc(&pair_done, cap_pairs));
-    HIPCHK(hipMalloc(&noi, cap_pairs * 2 * 4));
+    HIPCHK(hipMalloc(&noi, (size_t)cap_cbs * 4));
+    HIPCHK(hipEventCreateWithFlags(&gev, hipEventDisableTiming));
     return 0;
   }
 
   void destroy() {
-    for (void *p : {SP0, XP1, A, D, T, scratch})
+    if (gev_pending) (void)hipEventSynchronize(gev);
+    for (void *p : {SP0, XP1, A, D, T, scratch, (void *)d_groups})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
                     (void *)out_stage})
       if (p) (void)hipFree(p);
+    if (h_groups) (void)hipHostFree(h_groups);
+    if (gev) (void)hipEventDestroy(gev);
     for (auto &kv : crc_tables) (void)hipFree(kv.second);
     crc_tables.clear();
     for (auto &kv : interl)
@@ -125,7 +144,9 @@ struct TdecEngine {
     interl.clear();
   }
 
-  int get_interleaver(uint32_t Kv, uint32_t nbv) {
+  TdArrays arrays() const { return TdArrays{SP0, XP1, A, D, T, scratch, cap_elems}; }
+
+  const Interl *get_interleaver(uint32_t Kv, uint32_t nbv) {
     auto key = std::make_pair(Kv, nbv);
     auto it = interl.find(key);
     if (it == interl.end()) {
@@ -140,77 +161,15 @@ struct TdecEngine {
         m[p] = (uint16_t)((i % nbv) * 16 * G16 + i / nbv);
       }
       Interl t{};
-      for (uint16_t **pp : {&t.fwd, &t.rev, &t.dmap}) HIPCHK(hipMalloc(pp, Kv * 2));
-      HIPCHK(hipMemcpy(t.fwd, f.data(), Kv * 2, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(t.rev, r.data(), Kv * 2, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(t.dmap, m.data(), Kv * 2, hipMemcpyHostToDevice));
+      for (uint16_t **pp : {&t.fwd, &t.rev, &t.dmap})
+        if (hipMalloc(pp, Kv * 2) != hipSuccess) return nullptr;
+      if (hipMemcpy(t.fwd, f.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(t.rev, r.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(t.dmap, m.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess)
+        return nullptr;
       it = interl.emplace(key, t).first;
     }
-    fwd = it->second.fwd;
-    rev = it->second.rev;
-    dmap = it->second.dmap;
-    return 0;
-  }
-
-  // validate + bind a job, load inputs into the internal layout
-  // rows: optional device table of per-CB input pointers (in place of d_in + c * in_stride);
-  // init_done: optional device flags of CBs that are already decoded (skipped, noi 0)
-  int load(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
-           const int16_t *const *rows = nullptr, int rows_aligned = 0,
-           const uint8_t *init_done = nullptr) {
-    if (cb_index(Kv) < 0) {
-      fprintf(stderr, "srsgpu: invalid code block size K=%u\n", Kv);
-      return -1;
-    }
-    if (Kv > cap_K || n > cap_cbs || n == 0) {
-      fprintf(stderr, "srsgpu: batch of %u x K=%u exceeds capacity %u x %u\n", n, Kv, cap_cbs, cap_K);
-      return -1;
-    }
-    if (impl < SRSLTE_TDEC_AUTO || impl > SRSLTE_TDEC_AVX_WINDOW) {
-      fprintf(stderr, "srsgpu: decoder type %d not supported\n", impl);
-      return -1;
-    }
-    const int r = resolve_impl(impl, Kv);
-    const int nbv = impl_nb(r);
-    if (nbv > 1 && (Kv % nbv || Kv / nbv <= 40)) {
-      // the reference windowed decoders need K/nb > win_overlap_len (turbodecoder_win.h:59);
-      // at K/nb == 40 its estimation pass doubles as the final pass (:331, :469) — a manual-
-      // mode-only corner (AUTO never selects it) that is rejected here
-      fprintf(stderr, "srsgpu: K=%u not supported by the %d-sub-block window decoder\n", Kv, nbv);
-      return -1;
-    }
-    if (!rows && in_stride < srsgpu_tdec_input_len(impl, sb_layout, Kv)) {
-      fprintf(stderr, "srsgpu: input stride %zu too small\n", in_stride);
-      return -1;
-    }
-    K = Kv;
-    impl_r = r;
-    nb = nbv;
-    ncb = (int)n;
-    npairs = (ncb + 1) / 2;
-    if (get_interleaver(K, (uint32_t)nb)) return -1;
-    const int sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nb > 1;
-    HIPCHK(srsgpu::launch_load(d_in, in_stride, rows, rows_aligned, sb_input, (int)K, nb, ncb, SP0,
-                               XP1, T, st));
-    HIPCHK(hipMemsetAsync(cb_done, 0, cap_pairs * 2, st));
-    HIPCHK(hipMemsetAsync(cb_ok, 0, cap_pairs * 2, st));
-    HIPCHK(hipMemsetAsync(noi, 0, cap_pairs * 2 * 4, st));
-    if (init_done) {
-      HIPCHK(hipMemcpyAsync(cb_done, init_done, n, hipMemcpyDeviceToDevice, st));
-      HIPCHK(srsgpu::launch_pair_done(ncb, cb_done, pair_done, st));
-    } else {
-      HIPCHK(hipMemsetAsync(pair_done, 0, cap_pairs, st));
-    }
-    return 0;
-  }
-
-  // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)
-  int halfit(int n, bool early, bool dec = true) {
-    const uint8_t *pd = early ? pair_done : nullptr;
-    const int seq = impl_r == SRSLTE_TDEC_SSE ? 0 : 1;
-    ProfScope ps(nb > 1 ? "k_win_halfit" : (seq == 0 ? "k_sse_halfit" : "k_gen_halfit"), st);
-    HIPCHK(srsgpu::launch_halfit(n, nb, seq, SP0, XP1, A, dec ? D : nullptr, T, fwd, rev, scratch, pd, (int)K, npairs, st));
-    return 0;
+    return &it->second;
   }
 
   const uint32_t *crc_table(uint32_t poly) {
@@ -231,16 +190,200 @@ struct TdecEngine {
     return dt;
   }
 
-  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t poly = 0,
-             uint32_t crc_bytes = 0, uint32_t maxh = 0) {
-    const uint32_t *pw = nullptr;
-    if (early && crc_bytes) {
-      pw = crc_table(poly);
-      if (!pw) return -1;
+  static int kind_of(int r) {
+    const int nbv = impl_nb(r);
+    return nbv == 16 ? TD_KIND_W16 : nbv == 8 ? TD_KIND_W8 : r == SRSLTE_TDEC_SSE ? TD_KIND_SSE : TD_KIND_GEN;
+  }
+
+  int check_spec(int impl, uint32_t Kv, uint32_t n) {
+    if (cb_index(Kv) < 0) {
+      fprintf(stderr, "srsgpu: invalid code block size K=%u\n", Kv);
+      return -1;
     }
-    HIPCHK(srsgpu::launch_decide(n, (int)K, nb, ncb, dmap, D, d_out, out_stride,
-                                 early ? cb_done : nullptr, cb_ok, noi, early ? (int)crc_bytes : 0,
-                                 pw, (int)maxh, pair_done, st));
+    if (Kv > cap_K || n > cap_cbs || n == 0) {
+      fprintf(stderr, "srsgpu: batch of %u x K=%u exceeds capacity %u x %u\n", n, Kv, cap_cbs, cap_K);
+      return -1;
+    }
+    if (impl < SRSLTE_TDEC_AUTO || impl > SRSLTE_TDEC_AVX_WINDOW) {
+      fprintf(stderr, "srsgpu: decoder type %d not supported\n", impl);
+      return -1;
+    }
+    const int nbv = impl_nb(resolve_impl(impl, Kv));
+    if (nbv > 1 && (Kv % nbv || Kv / nbv <= 40)) {
+      // the reference windowed decoders need K/nb > win_overlap_len (turbodecoder_win.h:59);
+      // at K/nb == 40 its estimation pass doubles as the final pass (:331, :469) — a manual-
+      // mode-only corner (AUTO never selects it) that is rejected here
+      fprintf(stderr, "srsgpu: K=%u not supported by the %d-sub-block window decoder\n", Kv, nbv);
+      return -1;
+    }
+    return 0;
+  }
+
+  // Lay out specs[0..ns) as device groups. Returns 1 (nothing launched) if they do not fit.
+  int plan(int impl, int sb_layout, const TdSpec *specs, size_t ns) {
+    std::vector<size_t> order(ns);
+    for (size_t i = 0; i < ns; i++) order[i] = i;
+    std::vector<int> kind(ns);
+    for (size_t i = 0; i < ns; i++) kind[i] = kind_of(resolve_impl(impl, specs[i].K));
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+      return std::make_pair(kind[a], specs[a].K) < std::make_pair(kind[b], specs[b].K);
+    });
+    groups.assign(ns, TdGroup{});
+    size_t elems = 0, dw = 0, sc = 0;
+    int pairs = 0;
+    for (int k = 0; k <= TD_NKIND; k++) kind_g0[k] = (int)ns;
+    for (int k = 0; k < TD_NKIND; k++) {
+      kind_blocks[k] = 0;
+      kind_lds[k] = 0;
+    }
+    for (size_t gi = 0; gi < ns; gi++) {
+      const TdSpec &sp = specs[order[gi]];
+      const int r = resolve_impl(impl, sp.K);
+      const int nbv = impl_nb(r), kd = kind[order[gi]];
+      if (kind_g0[kd] == (int)ns) kind_g0[kd] = (int)gi;
+      TdGroup &g = groups[gi];
+      g.K = (int)sp.K;
+      g.nb = nbv;
+      g.ncb = (int)sp.n;
+      g.npairs = (int)((sp.n + 1) / 2);
+      g.cb0 = (int)sp.cb0;
+      g.pair0 = pairs;
+      g.elem0 = (int64_t)elems;
+      g.dw0 = (int64_t)dw;
+      g.sc0 = (int64_t)sc;
+      g.sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nbv > 1;
+      g.blk_half = kind_blocks[kd];
+      kind_blocks[kd] += halfit_blocks(nbv, g.npairs);
+      if (nbv > 1) kind_lds[kd] = std::max(kind_lds[kd], bidir_lds_bytes(g.K, nbv));
+      const Interl *it = get_interleaver(sp.K, (uint32_t)nbv);
+      if (!it) return -1;
+      g.fwd = it->fwd;
+      g.rev = it->rev;
+      g.dmap = it->dmap;
+      g.crc_bytes = (int)(sp.crc_len / 8);
+      g.crc_pw = nullptr;
+      if (g.crc_bytes) {
+        g.crc_pw = crc_table(sp.poly);
+        if (!g.crc_pw) return -1;
+      }
+      pairs += g.npairs;
+      elems += (size_t)g.npairs * sp.K;
+      dw += (size_t)g.npairs * dec_words_host(g.K, nbv);
+      if (nbv == 1) sc += seq_scratch_elems(g.K, g.npairs);
+    }
+    for (int k = TD_NKIND - 1; k >= 0; k--) kind_g0[k] = std::min(kind_g0[k], kind_g0[k + 1]);
+    // load launches: runs of groups with the same loader (nb, sb_input)
+    for (size_t g0 = 0; g0 < ns;) {
+      size_t g1 = g0;
+      int blocks = 0;
+      while (g1 < ns && groups[g1].nb == groups[g0].nb && groups[g1].sb_input == groups[g0].sb_input) {
+        groups[g1].blk_load = blocks;
+        blocks += load_blocks(groups[g1].K, groups[g1].nb, groups[g1].npairs, groups[g1].sb_input);
+        g1++;
+      }
+      g0 = g1;
+    }
+    if ((size_t)pairs > cap_pairs || elems > cap_elems || dw > cap_dw || sc > cap_sc) return 1;
+    total_pairs = pairs;
+    return 0;
+  }
+
+  int upload_groups() {
+    const size_t ng = groups.size();
+    if (ng > groups_cap) {
+      if (gev_pending) HIPCHK(hipEventSynchronize(gev));
+      gev_pending = false;
+      if (d_groups) HIPCHK(hipFree(d_groups));
+      if (h_groups) HIPCHK(hipHostFree(h_groups));
+      groups_cap = std::max<size_t>(ng, 64);
+      HIPCHK(hipMalloc(&d_groups, groups_cap * sizeof(TdGroup)));
+      HIPCHK(hipHostMalloc(&h_groups, groups_cap * sizeof(TdGroup)));
+      uploaded = 0;
+    }
+    if (uploaded == ng && memcmp(h_groups, groups.data(), ng * sizeof(TdGroup)) == 0) return 0;
+    if (gev_pending) HIPCHK(hipEventSynchronize(gev));
+    memcpy(h_groups, groups.data(), ng * sizeof(TdGroup));
+    HIPCHK(hipMemcpyAsync(d_groups, h_groups, ng * sizeof(TdGroup), hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(gev, st));
+    gev_pending = true;
+    uploaded = ng;
+    return 0;
+  }
+
+  // load the inputs of the planned groups; first: reset the per-CB flags of the whole job
+  // (total_cbs code blocks; init_done seeds cb_done: blocks already decoded are skipped, noi 0)
+  int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
+                   int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs) {
+    if (upload_groups()) return -1;
+    const TdArrays a = arrays();
+    const size_t ng = groups.size();
+    for (size_t g0 = 0; g0 < ng;) {
+      const TdGroup &f = groups[g0];
+      size_t g1 = g0;
+      int blocks = 0;
+      bool vec = rows ? rows_aligned != 0 : ((uintptr_t)d_in % 4 == 0 && in_stride % 2 == 0);
+      while (g1 < ng && groups[g1].nb == f.nb && groups[g1].sb_input == f.sb_input) {
+        blocks += load_blocks(groups[g1].K, groups[g1].nb, groups[g1].npairs, groups[g1].sb_input);
+        vec = vec && (groups[g1].K / groups[g1].nb) % 2 == 0;
+        g1++;
+      }
+      HIPCHK(launch_load(d_groups + g0, (int)(g1 - g0), blocks, f.nb, f.sb_input, vec, d_in, in_stride,
+                         rows, a, st));
+      g0 = g1;
+    }
+    if (first) {
+      HIPCHK(hipMemsetAsync(cb_ok, 0, total_cbs, st));
+      HIPCHK(hipMemsetAsync(noi, 0, (size_t)total_cbs * 4, st));
+      if (init_done)
+        HIPCHK(hipMemcpyAsync(cb_done, init_done, total_cbs, hipMemcpyDeviceToDevice, st));
+      else
+        HIPCHK(hipMemsetAsync(cb_done, 0, total_cbs, st));
+    }
+    if (init_done)
+      HIPCHK(launch_pair_done(d_groups, (int)ng, total_pairs, cb_done, pair_done, st));
+    else
+      HIPCHK(hipMemsetAsync(pair_done, 0, (size_t)total_pairs, st));
+    return 0;
+  }
+
+  // single-size job (batch API and the drop-in srslte_tdec_* path)
+  int load(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
+           const int16_t *const *rows = nullptr, int rows_aligned = 0,
+           const uint8_t *init_done = nullptr, uint32_t poly = 0, uint32_t crc_len = 0) {
+    if (check_spec(impl, Kv, n)) return -1;
+    if (!rows && in_stride < srsgpu_tdec_input_len(impl, sb_layout, Kv)) {
+      fprintf(stderr, "srsgpu: input stride %zu too small\n", in_stride);
+      return -1;
+    }
+    const TdSpec sp{Kv, n, poly, crc_len, 0};
+    const int r = plan(impl, sb_layout, &sp, 1);
+    if (r) {
+      if (r > 0) fprintf(stderr, "srsgpu: batch of %u x K=%u exceeds capacity\n", n, Kv);
+      return -1;
+    }
+    K = Kv;
+    fwd = groups[0].fwd;
+    rev = groups[0].rev;
+    dmap = groups[0].dmap;
+    return load_planned(d_in, in_stride, rows, rows_aligned, init_done, true, n);
+  }
+
+  // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)
+  int halfit(int n, bool early, bool dec = true) {
+    const uint8_t *pd = early ? pair_done : nullptr;
+    const TdArrays a = arrays();
+    for (int k = 0; k < TD_NKIND; k++) {
+      const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+      if (g1 <= g0) continue;
+      ProfScope ps(k <= TD_KIND_W8 ? "k_win_halfit" : (k == TD_KIND_SSE ? "k_sse_halfit" : "k_gen_halfit"), st);
+      HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
+    }
+    return 0;
+  }
+
+  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t maxh = 0) {
+    HIPCHK(launch_decide(n, d_groups, (int)groups.size(), total_pairs, arrays(), d_out, out_stride,
+                         early, cb_done, cb_ok, noi, (int)maxh, pair_done, st));
     return 0;
   }
 
@@ -256,22 +399,64 @@ struct TdecEngine {
     return decide((int)nhalf - 1, d_out, out_stride, false);
   }
 
+  // early-stop decoding of one pass (planned groups) — maxh half-iterations at most
+  int decode_planned(uint32_t maxh, uint8_t *d_out, size_t out_stride) {
+    for (uint32_t h = 0; h < maxh; h++) {
+      if (halfit((int)h, true)) return -1;
+      if (decide((int)h, d_out, out_stride, true, maxh)) return -1;
+    }
+    return 0;
+  }
+
+  // Mixed sizes: specs in any order (cb0 ranges disjoint, < total_cbs); CB c's input at rows[c]
+  // (or d_in + c * in_stride), its decision bytes at d_out + c * out_stride. Specs that do not fit
+  // the arrays together are decoded in several passes.
+  int decode_multi(int impl, int sb_layout, const std::vector<TdSpec> &specs, uint32_t total_cbs,
+                   const int16_t *d_in, size_t in_stride, const int16_t *const *rows, int rows_aligned,
+                   const uint8_t *init_done, uint32_t maxh, uint8_t *d_out, size_t out_stride,
+                   uint8_t *d_ok, uint32_t *d_noi) {
+    if (maxh == 0 || total_cbs > cap_cbs) {
+      fprintf(stderr, "srsgpu: invalid early-stop job (max_halfits=%u, %u code blocks)\n", maxh, total_cbs);
+      return -1;
+    }
+    for (const TdSpec &sp : specs) {
+      if (check_spec(impl, sp.K, sp.n)) return -1;
+      if (sp.crc_len == 0 || sp.crc_len % 8 || sp.crc_len > sp.K || sp.cb0 + sp.n > total_cbs) {
+        fprintf(stderr, "srsgpu: invalid early-stop parameters (crc_len=%u K=%u)\n", sp.crc_len, sp.K);
+        return -1;
+      }
+      if (!rows && in_stride < srsgpu_tdec_input_len(impl, sb_layout, sp.K)) {
+        fprintf(stderr, "srsgpu: input stride %zu too small\n", in_stride);
+        return -1;
+      }
+    }
+    bool first = true;
+    for (size_t s0 = 0; s0 < specs.size();) {
+      size_t s1 = specs.size();
+      int r;
+      while ((r = plan(impl, sb_layout, specs.data() + s0, s1 - s0)) == 1 && s1 - s0 > 1)
+        s1 = s0 + (s1 - s0 + 1) / 2;
+      if (r) {
+        if (r > 0) fprintf(stderr, "srsgpu: code block group exceeds the decoder capacity\n");
+        return -1;
+      }
+      if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs)) return -1;
+      if (decode_planned(maxh, d_out, out_stride)) return -1;
+      first = false;
+      s0 = s1;
+    }
+    if (d_ok) HIPCHK(hipMemcpyAsync(d_ok, cb_ok, total_cbs, hipMemcpyDeviceToDevice, st));
+    if (d_noi) HIPCHK(hipMemcpyAsync(d_noi, noi, (size_t)total_cbs * 4, hipMemcpyDeviceToDevice, st));
+    return 0;
+  }
+
   int decode(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
              uint32_t maxh, uint32_t poly, uint32_t crc_len, uint8_t *d_out, size_t out_stride,
              uint8_t *d_ok, uint32_t *d_noi, const int16_t *const *rows = nullptr,
              int rows_aligned = 0, const uint8_t *init_done = nullptr) {
-    if (maxh == 0 || crc_len == 0 || crc_len % 8 || crc_len > Kv) {
-      fprintf(stderr, "srsgpu: invalid early-stop parameters (max_halfits=%u crc_len=%u)\n", maxh, crc_len);
-      return -1;
-    }
-    if (load(impl, sb_layout, d_in, in_stride, Kv, n, rows, rows_aligned, init_done)) return -1;
-    for (uint32_t h = 0; h < maxh; h++) {
-      if (halfit((int)h, true)) return -1;
-      if (decide((int)h, d_out, out_stride, true, poly, crc_len / 8, maxh)) return -1;
-    }
-    if (d_ok) HIPCHK(hipMemcpyAsync(d_ok, cb_ok, (size_t)n, hipMemcpyDeviceToDevice, st));
-    if (d_noi) HIPCHK(hipMemcpyAsync(d_noi, noi, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
-    return 0;
+    const std::vector<TdSpec> sp{TdSpec{Kv, n, poly, crc_len, 0}};
+    return decode_multi(impl, sb_layout, sp, n, d_in, in_stride, rows, rows_aligned, init_done, maxh,
+                        d_out, out_stride, d_ok, d_noi);
   }
 
   int stage(uint32_t n, uint32_t Kv, size_t in_len) {
@@ -285,7 +470,6 @@ struct TdecEngine {
     return 0;
   }
 };
-
 
 } // namespace srsgpu
 #endif

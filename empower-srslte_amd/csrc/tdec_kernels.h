@@ -1,4 +1,11 @@
 // Internal launch interface of the turbo-decoder kernels (tdec_kernels.hip).
+//
+// A decoder job is a list of GROUPS: code blocks of one size K and one decoder variant (AUTO
+// picks the variant from K, turbodecoder.c:364-422), plus the CRC the early stop checks. Mixed
+// sizes (many cells, many TBs) decode together: one launch per variant and half-iteration covers
+// every group of that variant; a workgroup finds its group by binary search over the groups'
+// first-workgroup numbers (wave-uniform scalar loads), so launch count does not grow with the
+// number of distinct K.
 #ifndef SRSGPU_TDEC_KERNELS_H
 #define SRSGPU_TDEC_KERNELS_H
 #include <hip/hip_runtime.h>
@@ -6,30 +13,53 @@
 #include <stdint.h>
 
 namespace srsgpu {
-// user input -> SP0 (short4), P1 plane of XP1 (short2), T (short2 x 12) per pair. XP1 holds
-// two [npairs][K] short2 planes: X2 (app2) then P1 (par1).
-// rows != NULL: code block c's input starts at rows[c] (device array; rows_aligned: every row
-// is 4-byte aligned), else at in + c * in_stride.
-hipError_t launch_load(const int16_t *in, size_t in_stride, const int16_t *const *rows,
-                       int rows_aligned, int sb_input, int K, int NB, int ncb, void *SP0, void *XP1,
-                       void *T, hipStream_t st);
-size_t win_ck_bytes(int K, int NB, int npairs);
-size_t seq_scratch_bytes(int K, int npairs);
-// one half-iteration n (DEC1 for even n, DEC2 for odd n). NB > 1: windowed decoder;
-// NB == 1: impl_seq 0 = SSE non-window, 1 = generic.
-hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, void *D,
-                         const void *T,
-                         const uint16_t *fwd, const uint16_t *rev, void *scratch,
-                         const uint8_t *pair_done, int K, int npairs, hipStream_t st);
-// hard decision after half-iteration n; with crc_bytes > 0 also CRC + early-stop bookkeeping
-// dmap: natural position -> chain-major decision index after DEC2 (see tdec_engine.h)
-hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *dmap, const void *D,
-                         uint8_t *outb, size_t out_stride, uint8_t *cb_done,
-                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
-                         int max_halfits, uint8_t *pair_done, hipStream_t st);
-// crc_pw[d] = x^(d + 24) mod poly (24-bit CRC), d < 6144: the checksum of a crc_bits-bit message is
-// the XOR of crc_pw[crc_bits - 1 - p] over its set bits p
-// pair_done[p] = both CBs of pair p done
-hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done, hipStream_t st);
+
+// decoder variants, in the order groups are laid out in a job
+enum { TD_KIND_W16 = 0, TD_KIND_W8 = 1, TD_KIND_SSE = 2, TD_KIND_GEN = 3, TD_NKIND = 4 };
+
+struct TdGroup {
+  int32_t K, nb, ncb, npairs; // nb: 16 / 8 windowed sub-blocks, 1 sequential
+  int32_t cb0;                // first code block of the group in the caller's numbering (rows,
+                              // outputs, cb_done / cb_ok / noi)
+  int32_t pair0;              // first pair (T, pair_done; monotonic over the group list)
+  int32_t blk_load, blk_half; // first workgroup of the group in its load / half-iteration launch
+  int64_t elem0;              // first element of the group's [pair][K] arrays (SP0, X2, P1, A)
+  int64_t dw0;                // first packed decision word (D)
+  int64_t sc0;                // first short2 of the sequential decoders' scratch
+  const uint16_t *fwd, *rev, *dmap;
+  const uint32_t *crc_pw;     // x^(d+24) mod P of the group's CRC (early stop)
+  int32_t crc_bytes;          // CRC-checked prefix in bytes (0: no CRC)
+  int32_t sb_input;           // input rows in rm_turbo's sub-block layout
+};
+
+struct TdArrays {
+  void *SP0, *XP1, *A, *D, *T, *scratch;
+  size_t plane; // elements of the X2 plane: P1 starts at XP1 + plane
+};
+
+// user input -> SP0 / P1 / T for groups [0, ng) of dg (all with the same nb and sb_input).
+// rows != NULL: code block c's input starts at rows[c], else at in + c * in_stride.
+// vec: natural rows may be read as dwords.
+hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_input, bool vec,
+                       const int16_t *in, size_t in_stride, const int16_t *const *rows,
+                       const TdArrays &a, hipStream_t st);
+// workgroups a group needs in the load / half-iteration launch of its kind
+int load_blocks(int K, int nb, int npairs, int sb_input);
+int halfit_blocks(int nb, int npairs);
+size_t seq_scratch_elems(int K, int npairs); // short2 elements
+size_t bidir_lds_bytes(int K, int nb);
+int dec_words_host(int K, int nb);
+// one half-iteration n (DEC1 for even n, DEC2 for odd n) of every group of one kind
+hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
+                         bool dec, const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
+// hard decision after half-iteration n for every pair of the job (npairs in total); early: also
+// the CRC, cb_done / cb_ok / noi and pair_done (turbodecoder.c:353-360, sch.c:361-391)
+hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,
+                         uint8_t *outb, size_t out_stride, bool early, uint8_t *cb_done,
+                         uint8_t *cb_ok, uint32_t *noi, int max_halfits, uint8_t *pair_done,
+                         hipStream_t st);
+// pair_done[p] = both code blocks of pair p done (after cb_done was seeded)
+hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *cb_done,
+                            uint8_t *pair_done, hipStream_t st);
 } // namespace srsgpu
 #endif

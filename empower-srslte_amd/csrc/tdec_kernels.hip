@@ -29,11 +29,14 @@
 // Hard decision after either: bit(p) = A + app2[rev] at j(p) > 0 (= ext1 after DEC1, app1 after
 // DEC2, because both subtractions are exactly invertible modulo 2^16).
 //
+// ---- Groups ---------------------------------------------------------------------------------
+// A job holds groups of code blocks (one K and decoder variant each, tdec_kernels.h). Every
+// [pair][K] array above is the concatenation of the groups' arrays (group g from element elem0);
+// pair-indexed arrays (T, pair_done) use the global pair index pair0 + p, CB-indexed ones (rows,
+// outputs, flags) the caller's index cb0 + c. One launch per variant covers all its groups.
+//
 // ---- Windowed decoder mapping ---------------------------------------------------------------
-// One lane = one sub-block chain of one CB pair, a 64-lane wave = 64/NB pairs. The backward pass
-// keeps every 8th state metric (and the one at L) in a coalesced global checkpoint buffer; the
-// forward pass recomputes the 8 betas of each segment from its checkpoint into registers (exact:
-// integer recursion) and emits LLRs. All inputs are software-pipelined one 8-step chunk ahead.
+// One lane = one sub-block chain of one CB pair, a 64-lane wave = 64/NB pairs (k_win_bidir).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -47,7 +50,6 @@ typedef short s4 __attribute__((ext_vector_type(4)));
 
 #define TD_INF 10000  // turbodecoder_win.h:63 / _sse.c:51 / _gen.c:41
 #define TD_OVERLAP 40 // turbodecoder_win.h:59 win_overlap_len
-#define TD_W 8        // checkpoint period / chunk length (steps)
 #ifndef TD_BIDIR_CW
 #define TD_BIDIR_CW 16 // checkpoint period of the bidirectional decoder (LDS checkpoints)
 #endif
@@ -70,6 +72,33 @@ __device__ __forceinline__ s2 hi2(s4 v) { return s2{v.z, v.w}; }
 struct St8 {
   s2 s[8];
 };
+
+// Pointers read from a group descriptor are generic (flat) to the compiler; tables are global
+// memory, and flat loads would count against both vmcnt and lgkmcnt. gptr() restores that.
+template <typename T> using gptr_t = const T __attribute__((address_space(1))) *;
+template <typename T> __device__ __forceinline__ gptr_t<T> gptr(const T *p) {
+  return (gptr_t<T>)(const __attribute__((address_space(1))) void *)(uintptr_t)p;
+}
+template <typename T> using gmut_t = T __attribute__((address_space(1))) *;
+template <typename T> __device__ __forceinline__ gmut_t<T> gmut(void *p) {
+  return (gmut_t<T>)(__attribute__((address_space(1))) void *)(uintptr_t)p;
+}
+
+// group of workgroup b in a launch: the last group whose first workgroup (field F) is <= b
+enum { GF_LOAD, GF_HALF, GF_PAIR };
+template <int F>
+__device__ __forceinline__ int grp_find(const TdGroup *__restrict__ g, int ng, int b) {
+  int lo = 0, hi = ng - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    const int v = F == GF_LOAD ? g[mid].blk_load : F == GF_HALF ? g[mid].blk_half : g[mid].pair0;
+    if (v <= b)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
 
 // ------------------------------------------------------------------ windowed steps ----
 
@@ -153,31 +182,6 @@ __device__ __forceinline__ void st_fill(St8 &o, short v0, short v) {
   for (int i = 1; i < 8; i++) o.s[i] = splat(v);
 }
 
-__device__ __forceinline__ void ck_store(s4 *ck, size_t off, const St8 &o) {
-  s4 *p = ck + off * 4;
-  p[0] = s4{o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
-  p[1] = s4{o.s[2].x, o.s[2].y, o.s[3].x, o.s[3].y};
-  p[2] = s4{o.s[4].x, o.s[4].y, o.s[5].x, o.s[5].y};
-  p[3] = s4{o.s[6].x, o.s[6].y, o.s[7].x, o.s[7].y};
-}
-struct Ck {
-  s4 v[4];
-};
-__device__ __forceinline__ void ck_load(const s4 *ck, size_t off, Ck &c) {
-  const s4 *p = ck + off * 4;
-  c.v[0] = p[0];
-  c.v[1] = p[1];
-  c.v[2] = p[2];
-  c.v[3] = p[3];
-}
-__device__ __forceinline__ void ck_unpack(const Ck &c, St8 &o) {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    o.s[2 * i] = lo2(c.v[i]);
-    o.s[2 * i + 1] = hi2(c.v[i]);
-  }
-}
-
 // ------------------------------------------------------------------ input policy ----
 // Per-step inputs of one constituent decoder run. DEC1: x = syst (+) A, y = par0, operand of
 // the output stage = A, scatter table = rev. DEC2: x = app2, y = par1, operand = app2, table =
@@ -231,266 +235,8 @@ __device__ __forceinline__ uint32_t dec_bits(s2 llr) {
 }
 __device__ __forceinline__ int dec_words(int K, int NB) { return NB * ((K / NB + 15) / 16); }
 
-// 8-step chunk of inputs (+ scatter indices + the segment's beta checkpoint) in registers
-struct Chunk {
-  s2 x[TD_W], y[TD_W], e[TD_W];
-  int t[TD_W];
-  Ck ck;
-};
-
-// ------------------------------------------------------------------ windowed decoder ----
-template <int NB, int DIV, int MODE>
-__global__ __launch_bounds__(256) void k_win_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
-                                                    const s2 *__restrict__ T,
-                                                    const uint16_t *__restrict__ tbl,
-                                                    s4 *__restrict__ ck,
-                                                    const uint8_t *__restrict__ pair_done, int K,
-                                                    int npairs) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int pair = g / NB;
-  const int d = g % NB;
-  if (pair >= npairs) return;
-  if (pair_done && pair_done[pair]) return;
-  const int L = K / NB;
-  const int nc = (L + TD_W - 1) / TD_W;
-  const int nlanes = npairs * NB;
-  const size_t base = (size_t)pair * K;
-  const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
-  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
-  s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, NB) : nullptr;
-  const s2 *tl = T + (size_t)pair * 12;
-  const int tail_xoff = MODE == 1 ? 6 : 0;
-
-  // loads of one 8-step chunk of column col: steps k0 .. k0+7, clamped into the sub-block
-  auto load_xy = [&](Chunk &c, int col, int k0) {
-#pragma unroll
-    for (int j = 0; j < TD_W; j++) {
-      int k = min(max(k0 + j, 0), L - 1);
-      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + col);
-      c.x[j] = s.x;
-      c.y[j] = s.y;
-    }
-  };
-  // state-0 normalisation operand at step k = 8q + j (win.h:244-261: k even and k != 0);
-  // subtracting 0 (saturating) is the identity, which keeps the steady-state loops branch-free
-  auto norm_op = [&](const St8 &o, int q, int j) -> s2 {
-    return (j == 0 && q == 0) ? splat(0) : o.s[0];
-  };
-  auto norm_by = [&](St8 &o, s2 z) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], z);
-  };
-
-  // ================= beta =================
-  St8 o;
-  {
-    // turbodecoder_win.h:376-384,386-433 (loop_len = 40): estimate the state at the start of
-    // sub-block d+1 from all-unknown states; move_right (:333-366) hands it to sub-block d.
-    const int dn = d + 1 < NB ? d + 1 : d; // last lane: result replaced by the tail trellis
-    st_fill(o, -TD_INF, -TD_INF);
-    Chunk c0, c1;
-    load_xy(c0, dn, 32);
-#pragma unroll
-    for (int q = 4; q >= 0; q -= 2) {
-      if (q > 0) load_xy(c1, dn, 8 * (q - 1));
-#pragma unroll
-      for (int j = TD_W - 1; j >= 0; j--) {
-        win_beta_step(o, c0.x[j], c0.y[j]);
-        win_norm(8 * q + j, o);
-      }
-      if (q > 0) {
-        if (q > 1) load_xy(c0, dn, 8 * (q - 2));
-#pragma unroll
-        for (int j = TD_W - 1; j >= 0; j--) {
-          win_beta_step(o, c1.x[j], c1.y[j]);
-          win_norm(8 * (q - 1) + j, o);
-        }
-      }
-    }
-    St8 t;
-    win_tail_trellis(tl, tail_xoff, t); // :350-355 last sub-block starts from the tail
-    if (d == NB - 1) o = t;
-  }
-  ck_store(ck, (size_t)nc * nlanes + g, o); // :372-374 beta[L] (slot ceil(L/8))
-  {
-    // full chunk q (steps 8q+7 .. 8q): checkpoint beta[8q] before its normalisation (:420-424)
-    auto beta_full = [&](Chunk &c, int q) {
-#pragma unroll
-      for (int j = TD_W - 1; j >= 0; j--) {
-        win_beta_step(o, c.x[j], c.y[j]);
-        if (j == 0) ck_store(ck, (size_t)q * nlanes + g, o); // slot 0 is never read
-        if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
-      }
-    };
-    Chunk c0, c1;
-    const int qt = nc - 1; // top chunk, possibly partial (L % 8 != 0); nc >= 7 since L > 40
-    load_xy(c0, d, TD_W * qt);
-    load_xy(c1, d, TD_W * (qt - 1));
-    {
-      const int n = L - TD_W * qt;
-#pragma unroll
-      for (int j = TD_W - 1; j >= 0; j--) {
-        if (j < n) {
-          win_beta_step(o, c0.x[j], c0.y[j]);
-          if (j == 0) ck_store(ck, (size_t)qt * nlanes + g, o);
-          win_norm(TD_W * qt + j, o);
-        }
-      }
-    }
-    int q = qt - 1; // chunk q is in c1
-    for (; q >= 1; q -= 2) {
-      load_xy(c0, d, TD_W * (q - 1));
-      beta_full(c1, q);
-      load_xy(c1, d, TD_W * (q - 2));
-      beta_full(c0, q - 1);
-    }
-    if (q == 0) beta_full(c1, 0);
-  }
-
-  // ================= alpha + LLR + output stage =================
-  {
-    // :501-506,512-584 (loop_len = 40) over the last 40 steps of sub-block d-1; move_left
-    // (:469-495) hands the estimate to sub-block d; sub-block 0 starts in state 0 (:496-500).
-    const int dp = d > 0 ? d - 1 : 0;
-    st_fill(o, -TD_INF, -TD_INF);
-    Chunk c0, c1;
-    load_xy(c0, dp, L - TD_OVERLAP);
-#pragma unroll
-    for (int q = 0; q < 5; q += 2) {
-      if (q < 4) load_xy(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
-#pragma unroll
-      for (int j = 0; j < TD_W; j++) {
-        win_alpha_step(o, c0.x[j], c0.y[j]);
-        win_norm(8 * q + j, o);
-      }
-      if (q < 4) {
-        if (q < 3) load_xy(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
-#pragma unroll
-        for (int j = 0; j < TD_W; j++) {
-          win_alpha_step(o, c1.x[j], c1.y[j]);
-          win_norm(8 * (q + 1) + j, o);
-        }
-      }
-    }
-    if (d == 0) st_fill(o, 0, -TD_INF);
-  }
-
-  auto load_seg = [&](Chunk &c, int q) {
-#pragma unroll
-    for (int j = 0; j < TD_W; j++) {
-      int k = min(TD_W * q + j, L - 1);
-      int i = k * NB + d;
-      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
-      c.x[j] = s.x;
-      c.y[j] = s.y;
-      c.e[j] = s.e;
-      c.t[j] = tbl[i];
-    }
-    ck_load(ck, (size_t)(q + 1) * nlanes + g, c.ck); // beta stored at min(8q+8, L)
-  };
-
-  // one LLR step at position k = 8q+j from the forward state o and stored beta[k+1]
-  uint32_t dacc = 0; // decisions of the current 16-step group
-  const int G16 = (L + 15) / 16;
-  auto dec_flush = [&](int q, bool last) {
-    if (D && ((q & 1) || last)) {
-      D[d * G16 + q / 2] = dacc;
-      dacc = 0;
-    }
-  };
-  auto llr_step = [&](const Chunk &c, const St8 &b, int j, int q) {
-    s2 mb[8], nw[8];
-    win_alpha_branches(o, c.x[j], c.y[j], mb, nw);
-    s2 m0 = sadd(b.s[0], mb[0]);
-    s2 m1 = sadd(b.s[0], nw[0]);
-#pragma unroll
-    for (int i = 1; i < 8; i++) {
-      m0 = smax(m0, sadd(b.s[i], mb[i]));
-      m1 = smax(m1, sadd(b.s[i], nw[i]));
-    }
-    s2 v = ssub(m1, m0);
-    if (DIV) v = v >> 1; // :565-567 srai 1 (SSE16 window)
-    store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
-    if (D) dacc |= dec_bits(v) << ((q & 1) * 8 + j);
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
-  };
-
-  // full segment q (8 steps, s1 = 8q+8 < L): branch-free
-  auto seg_full = [&](Chunk &c, int q) {
-    St8 bst[TD_W]; // bst[j] = stored beta[8q+1+j]
-    St8 run;
-    ck_unpack(c.ck, run);
-    bst[TD_W - 1] = run;
-    norm_by(run, run.s[0]); // s1 = 8q+8: even, non-zero
-#pragma unroll
-    for (int j = TD_W - 2; j >= 0; j--) {
-      win_beta_step(run, c.x[j + 1], c.y[j + 1]);
-      bst[j] = run;
-      if (((j + 1) & 1) == 0) norm_by(run, run.s[0]); // k = 8q+1+j >= 1
-    }
-#pragma unroll
-    for (int j = 0; j < TD_W; j++) {
-      llr_step(c, bst[j], j, q);
-      if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
-    }
-    dec_flush(q, false);
-  };
-
-  // last segment (steps 8q .. L-1, 1..8 of them)
-  auto seg_last = [&](Chunk &c, int q) {
-    const int s0 = TD_W * q;
-    const int n = L - s0;
-    St8 bst[TD_W];
-    St8 run;
-    ck_unpack(c.ck, run);
-#pragma unroll
-    for (int j = TD_W - 1; j >= 0; j--) {
-      if (j == n - 1) bst[j] = run;
-    }
-#pragma unroll
-    for (int j = TD_W - 2; j >= 0; j--) {
-      if (j <= n - 2) {
-        win_beta_step(run, c.x[j + 1], c.y[j + 1]);
-        bst[j] = run;
-        win_norm(s0 + 1 + j, run);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TD_W; j++) {
-      if (j < n) {
-        llr_step(c, bst[j], j, q);
-        win_norm(s0 + j, o);
-      }
-    }
-    dec_flush(q, true);
-  };
-
-  {
-    Chunk c0, c1;
-    int q = 0;
-    load_seg(c0, 0);
-    for (; q + 2 < nc; q += 2) { // segments q and q+1 are full
-      load_seg(c1, q + 1);
-      seg_full(c0, q);
-      load_seg(c0, q + 2);
-      seg_full(c1, q + 1);
-    }
-    if (q == nc - 2) {
-      load_seg(c1, q + 1);
-      seg_full(c0, q);
-      seg_last(c1, q + 1);
-    } else {
-      seg_last(c0, q);
-    }
-  }
-}
-
 // ------------------------------------------------------------------ windowed, bidirectional ----
-// Same arithmetic as k_win_halfit, two waves per 64 sub-block chains: wave 0 runs the forward
+// Windowed decoder (turbodecoder_win.h), two waves per 64 sub-block chains: wave 0 runs the forward
 // (alpha) recursion, wave 1 the backward (beta) recursion, both starting at their end of the
 // sub-block and meeting at M (a multiple of CW near L/2). In its first half each wave only
 // recurses and checkpoints its metric every CW steps into LDS (alpha: entering state; beta: the
@@ -519,45 +265,17 @@ __device__ unsigned long long td_times[2048 * 8];
 #define TD_T(k)
 #endif
 
+// The body of k_win_bidir: every pointer a __restrict__ parameter, so the scoped no-alias
+// facts survive inlining (the group tables would otherwise hide them from the scheduler).
 template <int NB, int DIV, int MODE, int CW, bool DOUT>
-__global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
-                                                   const s2 *__restrict__ T,
-                                                   const uint16_t *__restrict__ tbl,
-                                                   const uint8_t *__restrict__ pair_done, int K,
-                                                   int npairs) {
-  // checkpoint slots in (dynamic) LDS, [slot][half][lane] x 16 B (conflict-free b128 accesses);
-  // nc + 1 slots of 2 KiB: 50 KiB at K = 6144 with 16 sub-blocks
-  extern __shared__ s4 cks[];
-  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
-  TD_T(0);
-  const int lane = threadIdx.x & 63;
-  const int gl = blockIdx.x * 64 + lane;
-  const int nlanes = npairs * NB;
-  const bool live = gl < nlanes;
-  const int g = live ? gl : nlanes - 1; // dead lanes compute on valid data, store nothing
-  const int pair = g / NB;
-  const int d = g % NB;
-  {
-    // whole block finished (early stop): both waves leave before the barrier
-    const int p0 = (blockIdx.x * 64) / NB;
-    const int p1 = min((blockIdx.x * 64 + 63) / NB, npairs - 1);
-    bool all_done = pair_done != nullptr;
-    if (pair_done)
-      for (int p = p0; p <= p1; p++) all_done = all_done && pair_done[p];
-    if (all_done) return;
-  }
-  const bool wr = live && !(pair_done && pair_done[pair]);
+__device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *__restrict__ xp1,
+                                               const s2 *__restrict__ p1, s2 *__restrict__ A,
+                                               uint32_t *__restrict__ D, const s2 *__restrict__ tl,
+                                               gptr_t<uint16_t> __restrict__ tbl, s4 *__restrict__ cks,
+                                               int K, int d, bool wr, int role, int lane) {
   const int L = K / NB;
   const int nc = (L + CW - 1) / CW;
   const int qm = nc / 2; // meeting chunk: M = CW*qm
-  const size_t base = (size_t)pair * K;
-  const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
-  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
-  s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, NB) : nullptr;
-  const s2 *tl = T + (size_t)pair * 12;
   const int tail_xoff = MODE == 1 ? 6 : 0;
 
   auto ck_put = [&](int slot, const St8 &o) {
@@ -858,6 +576,49 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
       if (q == 0) seg(c0, 0);
     }
   }
+}
+
+template <int NB, int DIV, int MODE, int CW, bool DOUT>
+__global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
+                                                   const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                   const s2 *__restrict__ T, size_t plane,
+                                                   const uint8_t *__restrict__ pair_done) {
+  // checkpoint slots in (dynamic) LDS, [slot][half][lane] x 16 B (conflict-free b128 accesses);
+  // nc + 1 slots of 2 KiB: 50 KiB at K = 6144 with 16 sub-blocks
+  extern __shared__ s4 cks[];
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
+  TD_T(0);
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, npairs = G.npairs;
+  const int blk = blockIdx.x - G.blk_half;
+  const int lane = threadIdx.x & 63;
+  const int gl = blk * 64 + lane;
+  const int nlanes = npairs * NB;
+  const bool live = gl < nlanes;
+  const int g = live ? gl : nlanes - 1; // dead lanes compute on valid data, store nothing
+  const int pair = g / NB;              // within the group
+  const int d = g % NB;
+  const uint8_t *pdone = pair_done ? pair_done + G.pair0 : nullptr;
+  {
+    // whole block finished (early stop): both waves leave before the barrier
+    const int p0 = (blk * 64) / NB;
+    const int p1 = min((blk * 64 + 63) / NB, npairs - 1);
+    bool all_done = pdone != nullptr;
+    if (pdone)
+      for (int p = p0; p <= p1; p++) all_done = all_done && pdone[p];
+    if (all_done) return;
+  }
+  const bool wr = live && !(pdone && pdone[pair]);
+  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
+  const s2 *p1 = XP1 + plane + base;     // par1
+  s2 *A = Aarr + base;
+  uint32_t *D = DOUT ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
+  win_bidir_body<NB, DIV, MODE, CW, DOUT>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, wr, role, lane);
   TD_T(4);
 }
 
@@ -866,23 +627,26 @@ __global__ __launch_bounds__(128) void k_win_bidir(const s4 *__restrict__ SP0, s
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
 // scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
 template <int MODE>
-__global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+__global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ groups, int ngroups,
+                                                   const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
-                                                   const s2 *__restrict__ T,
-                                                   const uint16_t *__restrict__ tbl,
-                                                   s2 *__restrict__ scratch,
-                                                   const uint8_t *__restrict__ pair_done, int K,
-                                                   int npairs) {
-  const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   const s2 *__restrict__ T, size_t plane,
+                                                   s2 *__restrict__ scratch_base,
+                                                   const uint8_t *__restrict__ pair_done) {
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, npairs = G.npairs;
+  const int pair = (blockIdx.x - G.blk_half) * blockDim.x + threadIdx.x; // within the group
   if (pair >= npairs) return;
-  if (pair_done && pair_done[pair]) return;
-  const size_t base = (size_t)pair * K;
+  if (pair_done && pair_done[G.pair0 + pair]) return;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
-  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
+  s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
+  const s2 *p1 = XP1 + plane + base;     // par1
   s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, 1) : nullptr;
-  const s2 *tl = T + (size_t)pair * 12;
+  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, 1) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
+  s2 *scratch = scratch_base + G.sc0;
   const int tail_xoff = MODE == 1 ? 6 : 0;
   auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   s2 a[8];
@@ -969,23 +733,26 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const s4 *__restrict__ SP0, s
 // for k < K only (:72-74), which is exactly the range the input policy covers.
 // scratch: beta (K+4)*8 short2 per pair.
 template <int MODE>
-__global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+__global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ groups, int ngroups,
+                                                   const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
-                                                   const s2 *__restrict__ T,
-                                                   const uint16_t *__restrict__ tbl,
-                                                   s2 *__restrict__ scratch,
-                                                   const uint8_t *__restrict__ pair_done, int K,
-                                                   int npairs) {
-  const int pair = blockIdx.x * blockDim.x + threadIdx.x;
+                                                   const s2 *__restrict__ T, size_t plane,
+                                                   s2 *__restrict__ scratch_base,
+                                                   const uint8_t *__restrict__ pair_done) {
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, npairs = G.npairs;
+  const int pair = (blockIdx.x - G.blk_half) * blockDim.x + threadIdx.x; // within the group
   if (pair >= npairs) return;
-  if (pair_done && pair_done[pair]) return;
-  const size_t base = (size_t)pair * K;
+  if (pair_done && pair_done[G.pair0 + pair]) return;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
   const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;                              // app2 (DEC1 output)
-  const s2 *p1 = XP1 + (size_t)npairs * K + base;     // par1
+  s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
+  const s2 *p1 = XP1 + plane + base;     // par1
   s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + (size_t)pair * dec_words(K, 1) : nullptr;
-  const s2 *tl = T + (size_t)pair * 12;
+  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, 1) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
+  s2 *scratch = scratch_base + G.sc0;
   const int tail_xoff = MODE == 1 ? 6 : 0;
   auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
   const int end = K + 3;
@@ -1064,33 +831,35 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const s4 *__restrict__ SP0, s
 // layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280) is a straight copy.
 #define LOAD_KT 64
 // input row of code block c: strided rows, or a per-CB pointer table (DL-SCH softbuffer rows)
-__device__ __forceinline__ const int16_t *cb_row(const int16_t *in, size_t stride,
-                                                 const int16_t *const *rows, int c) {
-  return rows ? rows[c] : in + (size_t)c * stride;
+__device__ __forceinline__ gptr_t<int16_t> cb_row(const int16_t *in, size_t stride,
+                                                  const int16_t *const *rows, int c) {
+  return gptr(rows ? rows[c] : in + (size_t)c * stride);
 }
 // NB and the tile are compile-time so the run/offset arithmetic is shifts and multiplies; VEC
 // reads the natural runs as dwords (in, in_stride and L even).
 template <int NB, bool VEC>
-__global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in, size_t in_stride,
+__global__ __launch_bounds__(256) void k_load_nat(const TdGroup *__restrict__ groups, int ngroups,
+                                                  const int16_t *__restrict__ in, size_t in_stride,
                                                   const int16_t *const *__restrict__ rows,
-                                                  int K, int ncb, s4 *__restrict__ SP0,
-                                                  s2 *__restrict__ P1, s2 *__restrict__ T) {
+                                                  TdArrays arr) {
   constexpr int RUN = 3 * LOAD_KT; // int16 per (CB, sub-block) run of one tile
   __shared__ short lds[2][3][LOAD_KT * NB];
-  const int npairs = (ncb + 1) / 2;
+  const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs;
   const int L = K / NB;
   const int ktiles = (L + LOAD_KT - 1) / LOAD_KT;
-  const int pair = blockIdx.x / ktiles;
-  const int kt = blockIdx.x - pair * ktiles;
+  const int blk = blockIdx.x - G.blk_load;
+  const int pair = blk / ktiles;
+  const int kt = blk - pair * ktiles;
   if (pair >= npairs) return;
-  const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
   const int k0 = kt * LOAD_KT;
   const int kn = min(LOAD_KT, L - k0);
 #pragma unroll
   for (int h = 0; h < 2; h++) {
-    const int16_t *src = cb_row(in, in_stride, rows, h ? c1 : c0) + 3 * k0;
+    const gptr_t<int16_t> src = cb_row(in, in_stride, rows, h ? c1 : c0) + 3 * k0;
     if (VEC) {
-      const uint32_t *s32 = reinterpret_cast<const uint32_t *>(src);
+      const gptr_t<uint32_t> s32 = (gptr_t<uint32_t>)src;
       for (int w = threadIdx.x; w < NB * RUN / 2; w += 256) {
         const int dd = w / (RUN / 2), r = 2 * (w - dd * (RUN / 2));
         if (r < 3 * kn) {
@@ -1112,33 +881,39 @@ __global__ __launch_bounds__(256) void k_load_nat(const int16_t *__restrict__ in
     }
   }
   __syncthreads();
-  const size_t base = (size_t)pair * K + (size_t)k0 * NB;
+  const gmut_t<s4> SP0 = gmut<s4>(arr.SP0);
+  const gmut_t<s2> P1 = gmut<s2>(arr.XP1) + arr.plane;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * K + (size_t)k0 * NB;
   for (int e = threadIdx.x; e < kn * NB; e += 256) {
     SP0[base + e] = s4{lds[0][0][e], lds[1][0][e], lds[0][1][e], lds[1][1][e]};
     P1[base + e] = s2{lds[0][2][e], lds[1][2][e]};
   }
   if (kt == 0 && threadIdx.x < 12) {
     const int t = threadIdx.x;
-    T[(size_t)pair * 12 + t] = s2{cb_row(in, in_stride, rows, c0)[3 * K + t],
-                                  cb_row(in, in_stride, rows, c1)[3 * K + t]};
+    gmut<s2>(arr.T)[(size_t)(G.pair0 + pair) * 12 + t] = s2{cb_row(in, in_stride, rows, c0)[3 * K + t],
+                                                         cb_row(in, in_stride, rows, c1)[3 * K + t]};
   }
 }
 
 // SB input (rm_turbo's layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280):
 // already in SB index order, a straight pair-interleaving copy, two elements per thread.
-__global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in, size_t in_stride,
+__global__ __launch_bounds__(256) void k_load_sb(const TdGroup *__restrict__ groups, int ngroups,
+                                                 const int16_t *__restrict__ in, size_t in_stride,
                                                  const int16_t *const *__restrict__ rows,
-                                                 int K, int ncb, s4 *__restrict__ SP0,
-                                                 s2 *__restrict__ P1, s2 *__restrict__ T) {
-  const int npairs = (ncb + 1) / 2;
+                                                 TdArrays arr) {
+  const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs;
   const int per = K / 2;
-  const size_t gid = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t gid = (size_t)(blockIdx.x - G.blk_load) * 256 + threadIdx.x;
   const int pair = (int)(gid / per);
   if (pair >= npairs) return;
   const int i = 2 * (int)(gid - (size_t)pair * per);
-  const int c0 = 2 * pair, c1 = c0 + 1 < ncb ? c0 + 1 : c0;
-  const int16_t *a = cb_row(in, in_stride, rows, c0), *b = cb_row(in, in_stride, rows, c1);
-  const size_t o = (size_t)pair * K + i;
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
+  const gptr_t<int16_t> a = cb_row(in, in_stride, rows, c0), b = cb_row(in, in_stride, rows, c1);
+  const gmut_t<s4> SP0 = gmut<s4>(arr.SP0);
+  const gmut_t<s2> P1 = gmut<s2>(arr.XP1) + arr.plane;
+  const gmut_t<s2> T = gmut<s2>(arr.T);
+  const size_t o = (size_t)G.elem0 + (size_t)pair * K + i;
 #pragma unroll
   for (int u = 0; u < 2; u++) {
     SP0[o + u] = s4{a[i + u], b[i + u], a[K + 32 + i + u], b[K + 32 + i + u]};
@@ -1146,8 +921,9 @@ __global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in,
   }
   if (i < 12) {
     const int tb = 3 * (K + 32);
-    T[(size_t)pair * 12 + i] = s2{a[tb + i], b[tb + i]};
-    T[(size_t)pair * 12 + i + 1] = s2{a[tb + i + 1], b[tb + i + 1]};
+    const size_t t = (size_t)(G.pair0 + pair) * 12 + i;
+    T[t] = s2{a[tb + i], b[tb + i]};
+    T[t + 1] = s2{a[tb + i + 1], b[tb + i + 1]};
   }
 }
 
@@ -1161,25 +937,28 @@ __global__ __launch_bounds__(256) void k_load_sb(const int16_t *__restrict__ in,
 //      lanes 0-15 write the 8+8 output bytes, and the CRC (crc.c:144-155, MSB-first, zero
 //      init) is folded from coalesced reads of crc_pw (see below) and reduced.
 // With early stop the same workgroup updates the done flags (sch.c:361-391).
-__global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
-                                                const uint16_t *__restrict__ dmap,
-                                                const uint32_t *__restrict__ Darr,
-                                                uint8_t *__restrict__ outb,
-                                                size_t out_stride, uint8_t *__restrict__ cb_done,
+__global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict__ groups,
+                                                int ngroups, const uint32_t *__restrict__ Darr,
+                                                uint8_t *__restrict__ outb, size_t out_stride,
+                                                int early, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
-                                                int crc_bytes, const uint32_t *__restrict__ crc_pw,
-                                                int max_halfits) {
+                                                int max_halfits, uint8_t *__restrict__ pair_done) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ uint32_t red[2][4];
-  const int pair = blockIdx.x;
-  const int npairs = (ncb + 1) / 2;
-  if (pair >= npairs) return;
-  const int cbs[2] = {2 * pair, 2 * pair + 1 < ncb ? 2 * pair + 1 : -1};
-  const bool skip0 = cb_done && cb_done[cbs[0]];
-  const bool skip1 = cbs[1] < 0 || (cb_done && cb_done[cbs[1]]);
+  __shared__ int fin[2];
+  const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, NB = G.nb, ncb = G.ncb;
+  const int pair = blockIdx.x - G.pair0;
+  if (pair >= G.npairs) return;
+  const int cbs[2] = {G.cb0 + 2 * pair, 2 * pair + 1 < ncb ? G.cb0 + 2 * pair + 1 : -1};
+  const bool skip0 = early && cb_done[cbs[0]];
+  const bool skip1 = cbs[1] < 0 || (early && cb_done[cbs[1]]);
   if (skip0 && skip1) return;
+  const gptr_t<uint16_t> dmap = gptr(G.dmap);
+  const gptr_t<uint32_t> crc_pw = gptr(G.crc_pw);
+  const int crc_bytes = early ? G.crc_bytes : 0;
   const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
-  const uint32_t *src = Darr + (size_t)pair * nw;
+  const uint32_t *src = Darr + G.dw0 + (size_t)pair * nw;
   for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
   __syncthreads();
   const bool dec2 = n & 1;
@@ -1238,6 +1017,7 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
   __syncthreads();
   if (threadIdx.x < 2) {
     const int h = threadIdx.x;
+    int done = 1;
     if (!(h ? skip1 : skip0)) {
       uint32_t crc = 0;
       for (int w = 0; w < (int)(blockDim.x >> 6); w++) crc ^= red[h][w];
@@ -1248,19 +1028,25 @@ __global__ __launch_bounds__(256) void k_decide(int n, int K, int NB, int ncb,
         cb_done[cb] = 1;
       } else if (n + 1 >= max_halfits) {
         cb_done[cb] = 1;
+      } else {
+        done = 0;
       }
     }
+    fin[h] = done;
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && pair_done) pair_done[blockIdx.x] = (uint8_t)(fin[0] && fin[1]);
 }
 
-// pair_done = both code blocks finished
-__global__ void k_pair_done(int ncb, const uint8_t *__restrict__ cb_done,
-                            uint8_t *__restrict__ pair_done) {
+// pair_done = both code blocks finished (seeding after init_done)
+__global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
+                            const uint8_t *__restrict__ cb_done, uint8_t *__restrict__ pair_done) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int npairs = (ncb + 1) / 2;
-  if (p >= npairs) return;
-  const int c1 = 2 * p + 1 < ncb ? 2 * p + 1 : 2 * p;
-  pair_done[p] = cb_done[2 * p] && cb_done[c1];
+  if (p >= npairs_total) return;
+  const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, p)];
+  const int lp = p - G.pair0;
+  const int c0 = G.cb0 + 2 * lp, c1 = 2 * lp + 1 < G.ncb ? c0 + 1 : c0;
+  pair_done[p] = cb_done[c0] && cb_done[c1];
 }
 
 // ------------------------------------------------------------------ launchers ----
@@ -1272,126 +1058,105 @@ static void allow_big_lds(const void *f) {
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-hipError_t launch_load(const int16_t *in, size_t in_stride, const int16_t *const *rows,
-                       int rows_aligned, int sb_input, int K, int NB, int ncb, void *SP0, void *XP1,
-                       void *T, hipStream_t st) {
-  const int npairs = (ncb + 1) / 2;
-  s4 *sp0 = (s4 *)SP0;
-  s2 *p1 = (s2 *)XP1 + (size_t)npairs * K;
-  s2 *t = (s2 *)T;
+int load_blocks(int K, int nb, int npairs, int sb_input) {
+  if (sb_input) return (int)nblk((size_t)npairs * (K / 2), 256);
+  return npairs * ((K / nb + LOAD_KT - 1) / LOAD_KT);
+}
+
+int halfit_blocks(int nb, int npairs) { return nb > 1 ? (int)nblk((size_t)npairs * nb, 64) : (int)nblk(npairs, 64); }
+
+size_t seq_scratch_elems(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs; }
+
+size_t bidir_lds_bytes(int K, int nb) {
+  return (size_t)((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
+}
+
+int dec_words_host(int K, int nb) { return nb * ((K / nb + 15) / 16); }
+
+hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_input, bool vec,
+                       const int16_t *in, size_t in_stride, const int16_t *const *rows,
+                       const TdArrays &a, hipStream_t st) {
+  if (ng <= 0 || nblocks <= 0) return hipSuccess;
   if (sb_input) {
-    hipLaunchKernelGGL(k_load_sb, dim3(nblk((size_t)npairs * (K / 2), 256)), dim3(256), 0, st, in,
-                       in_stride, rows, K, ncb, sp0, p1, t);
+    hipLaunchKernelGGL(k_load_sb, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
     return hipGetLastError();
   }
-  const int L = K / NB;
-  const unsigned grid = (unsigned)(npairs * ((L + LOAD_KT - 1) / LOAD_KT));
-  const bool vec = (rows ? rows_aligned != 0 : ((uintptr_t)in % 4 == 0 && in_stride % 2 == 0)) &&
-                   (L % 2 == 0);
-#define LOADNAT(nb)                                                                                \
+#define LOADNAT(n)                                                                                 \
   do {                                                                                             \
     if (vec)                                                                                       \
-      hipLaunchKernelGGL((k_load_nat<nb, true>), dim3(grid), dim3(256), 0, st, in, in_stride, rows, K, \
-                         ncb, sp0, p1, t);                                                         \
+      hipLaunchKernelGGL((k_load_nat<n, true>), dim3(nblocks), dim3(256), 0, st, dg, ng, in,        \
+                         in_stride, rows, a);                                                      \
     else                                                                                           \
-      hipLaunchKernelGGL((k_load_nat<nb, false>), dim3(grid), dim3(256), 0, st, in, in_stride, rows, K, \
-                         ncb, sp0, p1, t);                                                         \
+      hipLaunchKernelGGL((k_load_nat<n, false>), dim3(nblocks), dim3(256), 0, st, dg, ng, in,       \
+                         in_stride, rows, a);                                                      \
   } while (0)
-  if (NB == 16) LOADNAT(16);
-  else if (NB == 8) LOADNAT(8);
-  else if (NB == 1) LOADNAT(1);
+  if (nb == 16) LOADNAT(16);
+  else if (nb == 8) LOADNAT(8);
+  else if (nb == 1) LOADNAT(1);
   else return hipErrorInvalidValue;
 #undef LOADNAT
   return hipGetLastError();
 }
 
-size_t win_ck_bytes(int K, int NB, int npairs) {
-  const int L = K / NB;
-  size_t slots = (size_t)(L + TD_W - 1) / TD_W + 1;
-  return slots * (size_t)npairs * NB * 8 * sizeof(s2);
-}
-
-size_t seq_scratch_bytes(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs * sizeof(s2); }
-
-hipError_t launch_halfit(int n, int NB, int impl_seq, void *SP0, void *XP1, void *A, void *D,
-                         const void *T,
-                         const uint16_t *fwd, const uint16_t *rev, void *scratch,
-                         const uint8_t *pair_done, int K, int npairs, hipStream_t st) {
-  const bool dec2 = n & 1;
-  const int mode = dec2 ? 1 : (n == 0 ? 2 : 0);
-  const uint16_t *tbl = dec2 ? fwd : rev;
-  const s4 *sp0 = (const s4 *)SP0;
-  s2 *xp1 = (s2 *)XP1;
-  s2 *a = (s2 *)A;
-  uint32_t *dp = (uint32_t *)D;
-  const s2 *t = (const s2 *)T;
-  if (NB > 1) {
-    dim3 grid(nblk((size_t)npairs * NB, 256)), blk(256);
-    s4 *ck = (s4 *)scratch;
-#define WIN(nb, div, d2)                                                                           \
-  hipLaunchKernelGGL((k_win_halfit<nb, div, d2>), grid, blk, 0, st, sp0, xp1, a, dp, t, tbl, ck,    \
-                     pair_done, K, npairs)
-#define BIDIR1(nb, div, d2, dout)                                                                  \
+hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
+                         bool dec, const TdArrays &arr, const uint8_t *pair_done, hipStream_t st) {
+  if (ng <= 0 || nblocks <= 0) return hipSuccess;
+  const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
+  TdArrays a = arr;
+  if (!dec) a.D = nullptr;
+#define BIDIR1(nb, div, m, dout)                                                                   \
   do {                                                                                             \
-    allow_big_lds((const void *)(k_win_bidir<nb, div, d2, TD_BIDIR_CW, dout>));                    \
-    hipLaunchKernelGGL((k_win_bidir<nb, div, d2, TD_BIDIR_CW, dout>),                              \
-                       dim3(nblk((size_t)npairs * NB, 64)), dim3(128), bidir_lds, st, sp0, xp1, a, \
-                       dp, t, tbl, pair_done, K, npairs);                                          \
+    allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout>));                     \
+    hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout>), dim3(nblocks), dim3(128),     \
+                       lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
+                       (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done);                                             \
   } while (0)
-#define BIDIR(nb, div, d2)                                                                         \
+#define BIDIR(nb, div, m)                                                                          \
   do {                                                                                             \
-    if (dp) BIDIR1(nb, div, d2, true); else BIDIR1(nb, div, d2, false);                            \
+    if (dec) BIDIR1(nb, div, m, true); else BIDIR1(nb, div, m, false);                             \
   } while (0)
-    static const bool unidir = getenv("SRSGPU_TDEC_UNIDIR") != nullptr;
-    const size_t bidir_lds = (size_t)((K / NB + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
-    if (NB == 16) {
-      if (unidir) {
-        if (mode == 1) WIN(16, 0, 1); else if (mode == 2) WIN(16, 0, 2); else WIN(16, 0, 0);
-      } else {
-        if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
-      }
-    } else if (NB == 8) {
-      if (unidir) {
-        if (mode == 1) WIN(8, 1, 1); else if (mode == 2) WIN(8, 1, 2); else WIN(8, 1, 0);
-      } else {
-        if (mode == 1) BIDIR(8, 1, 1); else if (mode == 2) BIDIR(8, 1, 2); else BIDIR(8, 1, 0);
-      }
-    } else {
-      return hipErrorInvalidValue;
-    }
-#undef WIN
+#define SEQ(kern, m)                                                                               \
+  hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
+                     (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
+                     (s2 *)a.scratch, pair_done)
+  switch (kind) {
+  case TD_KIND_W16:
+    if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
+    break;
+  case TD_KIND_W8:
+    if (mode == 1) BIDIR(8, 1, 1); else if (mode == 2) BIDIR(8, 1, 2); else BIDIR(8, 1, 0);
+    break;
+  case TD_KIND_SSE:
+    if (mode == 1) SEQ(k_sse_halfit, 1); else if (mode == 2) SEQ(k_sse_halfit, 2); else SEQ(k_sse_halfit, 0);
+    break;
+  case TD_KIND_GEN:
+    if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
+    break;
+  default:
+    return hipErrorInvalidValue;
+  }
+#undef SEQ
 #undef BIDIR
 #undef BIDIR1
-  } else {
-    dim3 grid(nblk(npairs, 64)), blk(64);
-    s2 *sc = (s2 *)scratch;
-    if (impl_seq == 0) { // SSE non-window
-#define SEQ(kern, m) hipLaunchKernelGGL(kern<m>, grid, blk, 0, st, sp0, xp1, a, dp, t, tbl, sc, pair_done, K, npairs)
-      if (mode == 1) SEQ(k_sse_halfit, 1); else if (mode == 2) SEQ(k_sse_halfit, 2); else SEQ(k_sse_halfit, 0);
-    } else {
-      if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
-#undef SEQ
-    }
-  }
   return hipGetLastError();
 }
 
-hipError_t launch_pair_done(int ncb, const uint8_t *cb_done, uint8_t *pair_done, hipStream_t st) {
-  const int npairs = (ncb + 1) / 2;
-  hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
+hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *cb_done,
+                            uint8_t *pair_done, hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, dg, ng, npairs, cb_done,
+                     pair_done);
   return hipGetLastError();
 }
 
-hipError_t launch_decide(int n, int K, int NB, int ncb, const uint16_t *dmap, const void *D,
-                         uint8_t *outb, size_t out_stride, uint8_t *cb_done,
-                         uint8_t *cb_ok, uint32_t *noi, int crc_bytes, const uint32_t *crc_pw,
-                         int max_halfits, uint8_t *pair_done, hipStream_t st) {
-  const int npairs = (ncb + 1) / 2;
-  hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, K, NB, ncb, dmap,
-                     (const uint32_t *)D, outb, out_stride, cb_done, cb_ok, noi, crc_bytes, crc_pw,
-                     max_halfits);
-  if (crc_bytes && pair_done)
-    hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, ncb, cb_done, pair_done);
+hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,
+                         uint8_t *outb, size_t out_stride, bool early, uint8_t *cb_done,
+                         uint8_t *cb_ok, uint32_t *noi, int max_halfits, uint8_t *pair_done,
+                         hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, dg, ng, (const uint32_t *)a.D, outb,
+                     out_stride, early ? 1 : 0, cb_done, cb_ok, noi, max_halfits,
+                     early ? pair_done : nullptr);
   return hipGetLastError();
 }
 

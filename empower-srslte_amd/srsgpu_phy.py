@@ -337,6 +337,10 @@ class Dlsch:
         if r != 0:
             raise RuntimeError("softbuffer reset failed")
 
+    def reset_range(self, first, count):
+        if _lib.srsgpu_dlsch_softbuffer_reset_range(self.q, first, count) != 0:
+            raise RuntimeError("softbuffer reset failed")
+
     def decode(self, tbs_list, e_bits, max_halfits=8):
         """tbs_list: dicts {tbs, rv, Qm, nof_e_bits, softbuffer}; e_bits: int16 arrays.
         Returns (ret[], data[], noi[])."""

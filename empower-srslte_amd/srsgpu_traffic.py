@@ -1,0 +1,152 @@
+"""Mixed-bandwidth multi-cell downlink traffic on one GPU (BASELINE configs[4]).
+
+Cells of {6, 25, 50, 100} PRB (1.4 / 5 / 10 / 20 MHz) each carry a share of the subframes,
+interleaved round-robin. Every subframe holds one SISO PDSCH transport block with a random
+allocation of 1..nof_prb PRB from PRB 0 and a random MCS 0..28 (TBS and modulation from the
+36.213 tables, passed in as `table`), so code block sizes range over K = 40 .. 6144.
+
+Transmit side (untimed, all on the GPU): DL-SCH + PDSCH encoding (srsgpu_pdsch_encode_dev), CRS
+(srsgpu_chest_put_crs_dev), OFDM TX, AWGN.
+
+Receive step (the hot path): per cell, the front end runs as one batch over that cell's
+subframes — OFDM FFT, CRS channel estimation, PDSCH LLRs (RE extraction, MMSE with the device
+noise estimate, demapping, descrambling) into one shared LLR buffer. Then ONE DL-SCH call decodes
+the transport blocks of all cells together (srsgpu_dlsch_decode_dev): the engine bins the code
+blocks by decoder variant and size on the device side, so mixed K costs no per-cell launches.
+Reference flow per subframe: srslte_ofdm_rx_sf -> srslte_chest_dl_estimate -> srslte_pdsch_decode
+(lib/src/phy/ue/ue_dl.c:379-433,580).
+"""
+import numpy as np
+
+import srsgpu_phy as s
+
+BITS_PER_SYMBOL = {1: 2, 2: 4, 3: 6}
+MAX_CODE_RATE = 0.93  # 36.213 7.1.7: a UE may skip TBs above this effective rate
+
+
+class MixedCells:
+    def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
+                 snr_db=30.0, max_halfits=8, mcs=None, full_band=False):
+        """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
+        the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
+        traffic)"""
+        self.torch, self.dev = torch, dev
+        self.max_halfits = max_halfits
+        rng = np.random.default_rng(seed)
+        mods, tbs_tab = table["mod_by_mcs"], table["tbs_by_prb_mcs"]
+        self.cells = []
+        self.sf_total = n_sf
+        e_off = d_off = 0
+        tb_list = []
+        for ci, prb in enumerate(prbs):
+            idx = [i for i in range(n_sf) if i % len(prbs) == ci]
+            n = len(idx)
+            if n == 0:
+                continue
+            N = s.symbol_sz(prb, True)
+            gsz = 14 * 12 * prb
+            c = {"prb": prb, "N": N, "gsz": gsz, "n": n, "id": 1 + ci,
+                 "lstart": 2 if prb <= 10 else 1}
+            c["ofdm"] = s.OfdmRx(prb, N, stream=stream)
+            c["chest"] = s.Chest(prb, c["id"], max_grids=n, stream=stream)
+            c["pd"] = s.Pdsch(prb, c["id"], nof_softbuffers=1, max_cb=13, max_sf=n, stream=stream)
+            sfs, e_offs, sf_idx = [], [], []
+            for j in range(n):
+                sfi = 1 + (j % 4)
+                while True:
+                    L = prb if full_band else int(rng.integers(1, prb + 1))
+                    m = mcs if mcs is not None else int(rng.integers(0, 29))
+                    mod, tbs = mods[m], tbs_tab[L - 1][m]
+                    mask = np.zeros((2, prb), np.uint8)
+                    mask[:, :L] = 1
+                    probe = s.make_sf(sf_idx=sfi, lstart=c["lstart"], prb=mask, nof_prb=prb, mod=mod)
+                    nre = c["pd"].nof_re(probe)
+                    qm = BITS_PER_SYMBOL[mod]
+                    if (tbs + 24) <= MAX_CODE_RATE * nre * qm or mcs is not None:
+                        break
+                sf = s.make_sf(sf_idx=sfi, lstart=c["lstart"], prb=mask, nof_prb=prb, mod=mod,
+                               nof_re=nre, rnti=1234, tbs=tbs, softbuffer=len(tb_list),
+                               grid_offset=j * gsz, data_offset=d_off)
+                sfs.append(sf)
+                e_offs.append(e_off)
+                sf_idx.append(sfi)
+                tb_list.append({"tbs": tbs, "rv": 0, "Qm": qm, "nof_e_bits": nre * qm,
+                                "softbuffer": len(tb_list), "e_offset": e_off, "data_offset": d_off})
+                e_off += (nre * qm + 63) // 64 * 64
+                d_off += s.dlsch_data_len(tbs) + 2
+            c.update(sfs=sfs, e_offs=e_offs, sf_idx=sf_idx)
+            self.cells.append(c)
+        self.tb_list = tb_list
+        self.ntb = len(tb_list)
+        self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
+        self.bits = sum(t["tbs"] for t in tb_list)
+        self.dlsch = s.Dlsch(self.ntb, max_cb=13, max_cbs_per_call=self.ncb, stream=stream)
+        z = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
+        self.d_e = z(max(e_off, 1), torch.int16)
+        self.d_data_tx = torch.randint(0, 256, (max(d_off, 1),), dtype=torch.uint8, device=dev,
+                                       generator=torch.Generator(device=dev).manual_seed(seed))
+        self.d_data = z(max(d_off, 1), torch.uint8)
+        self.d_ret = z(self.ntb, torch.int32)
+        self.d_noi = z(self.ntb, torch.int32)
+        for c in self.cells:
+            n, gsz, N = c["n"], c["gsz"], c["N"]
+            c["grid"] = z(n * gsz, torch.complex64)
+            c["ce"] = z(n * gsz, torch.complex64)
+            c["noise"] = z(n, torch.float32)
+            c["x"] = z(n * 15 * N, torch.complex64)
+            c["pd"].set_noise_dev(c["noise"].data_ptr())
+        self._transmit(snr_db, seed)
+
+    def _transmit(self, snr_db, seed):
+        torch = self.torch
+        g = torch.Generator(device=self.dev).manual_seed(seed + 1)
+        for c in self.cells:
+            n, gsz, N = c["n"], c["gsz"], c["N"]
+            grid = self.torch.zeros(n * gsz, dtype=torch.complex64, device=self.dev)
+            assert c["pd"].encode_dev(c["sfs"], self.d_data_tx.data_ptr(), grid.data_ptr()) == 0
+            assert c["chest"].put_crs_dev(c["sf_idx"], grid.data_ptr(), gsz) == 0
+            assert c["ofdm"].tx_dev(n, grid.data_ptr(), gsz, c["x"].data_ptr(), 15 * N) == 0
+            torch.cuda.synchronize(self.dev)
+            p = c["x"].abs().pow(2).mean().item()
+            sd = float(np.sqrt(p / 10 ** (snr_db / 10) / 2))
+            c["x"] += (sd * torch.randn(c["x"].shape, dtype=torch.complex64, device=self.dev,
+                                        generator=g)).to(torch.complex64)
+
+    def front_end(self):
+        """per cell: OFDM RX, channel estimation, PDSCH LLRs into the shared LLR buffer"""
+        for c in self.cells:
+            n, gsz, N = c["n"], c["gsz"], c["N"]
+            assert c["ofdm"].rx_dev(n, c["x"].data_ptr(), 15 * N, c["grid"].data_ptr(), gsz) == 0
+            assert c["chest"].estimate_dev(c["sf_idx"], c["grid"].data_ptr(), gsz, c["ce"].data_ptr(),
+                                           c["noise"].data_ptr()) == 0
+            assert c["pd"].llr_dev(c["sfs"], c["grid"].data_ptr(), c["ce"].data_ptr(), gsz,
+                                   self.d_e.data_ptr(), c["e_offs"]) == 0
+
+    def decode(self):
+        """one DL-SCH call over every cell's transport blocks (new TBs: softbuffers reset)"""
+        self.dlsch.reset_range(0, self.ntb)
+        assert self.dlsch.decode_dev(self.tb_list, self.d_e.data_ptr(), self.d_data.data_ptr(),
+                                     self.max_halfits, self.d_ret.data_ptr(),
+                                     self.d_noi.data_ptr()) == 0
+
+    def step(self):
+        self.front_end()
+        self.decode()
+
+    def check(self):
+        """(acked TBs, TBs whose bytes equal the transmitted ones, mean nof_iterations)"""
+        ret = self.d_ret.cpu().numpy()
+        tx = self.d_data_tx.cpu().numpy()
+        rx = self.d_data.cpu().numpy()
+        good = 0
+        for t, r in zip(self.tb_list, ret):
+            o, nb = t["data_offset"], t["tbs"] // 8
+            good += int(r == 0 and (tx[o:o + nb] == rx[o:o + nb]).all())
+        return int((ret == 0).sum()), good, float(self.d_noi.cpu().numpy().mean())
+
+    def close(self):
+        for c in self.cells:
+            for k in ("ofdm", "chest", "pd"):
+                c[k].close()
+        self.dlsch.close()
+

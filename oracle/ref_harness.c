@@ -405,3 +405,13 @@ int ref_crs_get_sf(uint32_t nof_prb, uint32_t cell_id, uint32_t port, const floa
   cell.cp = SRSLTE_CP_NORM;
   return srslte_refsignal_cs_get_sf(cell, port, (cf_t *)grid, (cf_t *)out);
 }
+
+#include "srslte/phy/phch/ra.h"
+/* ra.c:697-731: MCS -> I_TBS (table 7.1.7.1-1) and modulation, then the TBS table 7.1.7.2.1-1.
+ * Returns the TBS (or -1) and writes the srslte_mod_t value to *mod. */
+int ref_mcs_tbs(uint32_t mcs, uint32_t nof_prb, uint32_t *mod) {
+  int i = srslte_ra_tbs_idx_from_mcs(mcs);
+  if (i < 0) return -1;
+  *mod = (uint32_t)srslte_ra_mod_from_mcs(mcs);
+  return srslte_ra_tbs_from_idx((uint32_t)i, nof_prb);
+}
