@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libsrsgpu_phy.so")
+LIB_PATH = os.environ.get("SRSGPU_LIB") or os.path.join(_HERE, "lib", "libsrsgpu_phy.so")  # debug builds
 
 SRSLTE_TDEC_AUTO, SRSLTE_TDEC_GENERIC, SRSLTE_TDEC_SSE = 0, 1, 2
 SRSLTE_TDEC_SSE_WINDOW, SRSLTE_TDEC_AVX_WINDOW = 3, 4
