@@ -229,9 +229,14 @@ __device__ __forceinline__ void store_out(s2 *__restrict__ x2, s2 *__restrict__ 
 // bits 0-15 and CB y's in bits 16-31. llr > 0 is the reference's decision on ext1 / app1
 // (turbodecoder.c:353-360), since A + app2 reproduces llr exactly modulo 2^16. k_decide maps
 // natural positions onto it (directly after DEC1, through dmap after DEC2).
-// dec_bits: 1 at bit 0 (x) / bit 16 (y) where llr > 0 (two packed ops)
+// dec_bits: 1 at bit 0 (x) / bit 16 (y) where llr > 0. Two packed ops, written as asm: left to
+// itself the compiler turns the clamp into per-half compares, selects and a permute (6 ops).
 __device__ __forceinline__ uint32_t dec_bits(s2 llr) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(smax(llr, splat(0)), splat(1)));
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0\n\tv_pk_min_i16 %0, %0, 1 op_sel_hi:[1,0]"
+      : "=v"(r)
+      : "v"(__builtin_bit_cast(uint32_t, llr)));
+  return r;
 }
 __device__ __forceinline__ int dec_words(int K, int NB) { return NB * ((K / NB + 15) / 16); }
 
@@ -299,34 +304,60 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     o.s[6] = lo2(e);
     o.s[7] = hi2(e);
   };
-  auto load_x8 = [&](ChunkW<8> &c, int col, int k0) { // prepass chunks
+  auto load_x8 = [&](ChunkW<8> &c, int col, int k0) { // prepass chunks (0 <= k0, k0 + 7 < L)
+    const int i0 = k0 * NB + col;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      int k = min(max(k0 + j, 0), L - 1);
-      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + col);
+      StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
   };
+  // chunk loads: a full chunk addresses its 16 steps as one base + constant offsets (no
+  // per-step index arithmetic); the last, partial chunk and the backward wave's prefetch past
+  // the start (chunk -1, never used) clamp k to [0, L - 1]. Not for MODE 0 (DEC1 with A):
+  // there the compiler hoists the offset loads and runs out of registers (measured +30%).
   auto load_xy = [&](ChunkW<CW> &c, int q) {
+    if (MODE != 0 && q >= 0 && CW * q + CW <= L) { // (the backward wave prefetches chunk -1)
+      const int i0 = CW * q * NB + d;
 #pragma unroll
-    for (int j = 0; j < CW; j++) {
-      int k = min(max(CW * q + j, 0), L - 1);
-      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + d);
-      c.x[j] = s.x;
-      c.y[j] = s.y;
+      for (int j = 0; j < CW; j++) {
+        StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
+        c.x[j] = s.x;
+        c.y[j] = s.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < CW; j++) {
+        int k = min(max(CW * q + j, 0), L - 1);
+        StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + d);
+        c.x[j] = s.x;
+        c.y[j] = s.y;
+      }
     }
   };
   auto load_full = [&](ChunkW<CW> &c, int q) {
+    if (MODE != 0 && q >= 0 && CW * q + CW <= L) { // (the backward wave prefetches chunk -1)
+      const int i0 = CW * q * NB + d;
 #pragma unroll
-    for (int j = 0; j < CW; j++) {
-      int k = min(max(CW * q + j, 0), L - 1);
-      int i = k * NB + d;
-      StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
-      c.x[j] = s.x;
-      c.y[j] = s.y;
-      c.e[j] = s.e;
-      c.t[j] = tbl[i];
+      for (int j = 0; j < CW; j++) {
+        StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
+        c.x[j] = s.x;
+        c.y[j] = s.y;
+        c.e[j] = s.e;
+        c.t[j] = tbl[i0 + j * NB];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < CW; j++) {
+        int k = min(max(CW * q + j, 0), L - 1);
+        int i = k * NB + d;
+        StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
+        c.x[j] = s.x;
+        c.y[j] = s.y;
+        c.e[j] = s.e;
+        c.t[j] = tbl[i];
+      }
     }
   };
   auto norm_by = [&](St8 &o, s2 z) {

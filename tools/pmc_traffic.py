@@ -17,9 +17,12 @@ KERNEL = "k_win_bidir"
 
 
 def per_launch(path, counter):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    return sum(vals) / len(vals), len(vals)
+    """counter summed over its instance rows per dispatch, averaged over the kernel's dispatches"""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return sum(per.values()) / len(per), len(per)
 
 
 fetch_kib, nf = per_launch(sys.argv[1], "FETCH_SIZE")
