@@ -293,14 +293,15 @@ def decoded_mbps(nranks, ncb, k, steps, elapsed):
     return nranks * ncb * k * steps / elapsed / 1e6
 
 
-def load_pmc_traffic(workload):
-    """Per-launch HBM bytes of the dominant kernel from a committed rocprofv3 PMC summary
-    (profiles/*pmc_traffic*.json, written by tools/pmc_traffic.py), if one matches."""
+def load_profile_json(workload, tag="pmc_traffic"):
+    """Per-launch figures of the dominant kernel from a committed profile summary
+    (profiles/*<tag>*.json): HBM bytes from rocprofv3 FETCH/WRITE passes (tools/pmc_traffic.py),
+    or VALU instructions per launch and the measured packed-int16 issue peak (tag "valu")."""
     pdir = os.path.join(REPO, "profiles")
     best = None
     if os.path.isdir(pdir):
         for f in sorted(os.listdir(pdir)):
-            if "pmc_traffic" in f and f.endswith(".json"):
+            if tag in f and f.endswith(".json"):
                 try:
                     d = json.load(open(os.path.join(pdir, f)))
                 except Exception:
@@ -380,7 +381,8 @@ def main():
         avg_launch_ms = kern_ms / max(kern_n, 1)
         alg_bytes = ALG_BYTES_PER_BIT_HALFIT * NCB * K
         achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
-        pmc = load_pmc_traffic(workload)
+        pmc = load_profile_json(workload)
+        valu = load_profile_json(workload, "valu")
         roofline = {"bound": "hbm", "kernel": "k_win_halfit",
                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -399,6 +401,16 @@ def main():
                        "bit_errors": bit_errors},
             "roofline": roofline,
         }
+        if valu and kern_n:
+            # the decoder's actual bound: packed int16 VALU issue
+            rate = valu["valu_instr_per_launch"] / (avg_launch_ms / 1e3)
+            peak = valu["simds"] / (valu["peak_ns_per_packed_instr_per_simd"] * 1e-9)
+            result["valu_roofline"] = {
+                "bound": "valu (packed int16 issue)", "kernel": "k_win_bidir",
+                "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1),
+                "unit": "G wave-instructions/s", "frac": round(rate / peak, 4),
+                "int16_ops_per_s_T": round(rate * 128 / 1e12, 1),
+                "instr_per_launch": valu["valu_instr_per_launch"]}
     batch.close()
     pipe = None
     if not args.no_pipeline:
