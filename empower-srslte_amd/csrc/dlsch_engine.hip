@@ -130,7 +130,7 @@ struct DlschEngine {
   uint32_t *h_cbmap = nullptr;
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
   EncItem *h_enc = nullptr, *d_enc = nullptr;
@@ -196,8 +196,28 @@ struct DlschEngine {
       if (p) (void)hipHostFree(p);
     for (auto &kv : tables) (void)hipFree(kv.second);
     tables.clear();
+    for (auto &kv : inv_tables) (void)hipFree(kv.second);
+    inv_tables.clear();
     if (staged) (void)hipEventDestroy(staged);
     tdec.destroy();
+  }
+
+  // inverse of the receive table: decoder-input position -> table entry (0xFFFF: none), over the
+  // row length rounded up to 8 (k_derm gathers 8 entries per 16-byte access)
+  const uint16_t *inv_table(uint32_t K, uint32_t rv, uint32_t nsb) {
+    auto key = std::make_tuple(K, rv, nsb);
+    auto it = inv_tables.find(key);
+    if (it != inv_tables.end()) return it->second;
+    std::vector<uint16_t> t;
+    rm_rx_table(K, rv, nsb, t);
+    const uint32_t rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
+    std::vector<uint16_t> inv((rowlen + 7) / 8 * 8, 0xFFFF);
+    for (uint32_t m = 0; m < t.size(); m++) inv[t[m]] = (uint16_t)m;
+    uint16_t *d = nullptr;
+    if (hipMalloc(&d, inv.size() * 2) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    inv_tables.emplace(key, d);
+    return d;
   }
 
   const uint16_t *table(uint32_t K, uint32_t rv, uint32_t nsb) {
@@ -352,12 +372,14 @@ struct DlschEngine {
         }
         const uint32_t nsb = auto_subblocks(K);
         const uint16_t *tab = table(K, t.rv, nsb);
-        if (!tab) return -1;
+        const uint16_t *inv = inv_table(K, t.rv, nsb);
+        if (!tab || !inv) return -1;
         DermItem &it = h_items[ncb];
         it.e = e_ptr[b] + rp;
         it.ne = ne;
         it.N = 3 * K + 12;
         it.table = tab;
+        it.inv = inv;
         it.row = row(t.softbuffer, i);
         it.cb_crc = ti.cb_crc + i;
         it.rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
@@ -559,6 +581,7 @@ int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_ou
   it.ne = in_len;
   it.N = 3 * K + 12;
   it.table = tab;
+  it.inv = nullptr;
   it.row = d_out;
   it.cb_crc = nullptr;
   it.pos = 0;

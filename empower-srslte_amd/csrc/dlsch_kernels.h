@@ -13,6 +13,8 @@ struct DermItem {
   uint32_t ne;            // E
   uint32_t N;             // 3K + 12 (table length)
   const uint16_t *table;  // receive table for (K, rv), decoder layout
+  const uint16_t *inv;    // its inverse: row position -> table entry m, 0xFFFF if none (rowlen,
+                          // padded with 0xFFFF to a multiple of 8)
   int16_t *row;           // softbuffer row (SOFTBUFFER_SIZE int16)
   const uint8_t *cb_crc;  // softbuffer cb_crc[i]: already decoded -> skipped
   uint32_t pos;           // position in the decoder's (K-grouped) CB order

@@ -17,13 +17,17 @@
 
 namespace srsgpu {
 
-// One workgroup per code block: the softbuffer row is staged in LDS (or starts at zero when the
-// row was reset since its last use: lazy reset, no memset pass over the softbuffers), the
-// E LLRs are scatter-added there and the row is written back with coalesced stores.
-#define DERM_MAXROW (3 * (6144 + 32) + 12)
+// One workgroup per code block, gathering by row position: entry o of the softbuffer row becomes
+// old[o] (or 0 when the row was reset since its last use: lazy reset, no memset pass) plus the
+// sum of the E received LLRs e[i] with i = m (mod N), m = inv[o] the circular-buffer entry that
+// lands on o. Eight consecutive entries per thread: one 16-byte inverse-table load, one 16-byte
+// row load (unless fresh) and one 16-byte row store; the LLRs (≈14 KB per block) are gathered
+// from L1/L2. Wrapping int16 sums, as rm_turbo.c:394-430's `output[j] += input[i]`, so the order
+// of the additions does not matter.
+#define DERM_LDS 12288 // LLRs staged per code block (24 KB of LDS)
 __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
                                               uint8_t *__restrict__ init_done) {
-  __shared__ int16_t row[DERM_MAXROW];
+  __shared__ uint32_t es[DERM_LDS / 2];
   const int g = blockIdx.x;
   if (g >= nitems) return;
   const DermItem it = items[g];
@@ -31,18 +35,64 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
   if (threadIdx.x == 0) init_done[it.pos] = skip;
   if (skip) return; // sch.c:323: blocks whose CRC passed before are not combined again
   const bool fresh = it.fresh && *it.fresh;
-  for (uint32_t p = threadIdx.x; p < it.rowlen; p += blockDim.x) row[p] = fresh ? 0 : it.row[p];
-  __syncthreads();
-  const uint32_t N = it.N;
-  const uint32_t lim = it.ne < N ? it.ne : N;
-  for (uint32_t m = threadIdx.x; m < lim; m += blockDim.x) {
-    uint32_t acc = 0;
-    for (uint32_t i = m; i < it.ne; i += N) acc += (uint16_t)it.e[i];
-    const uint32_t o = it.table[m]; // a bijection: no two m share o
-    row[o] = (int16_t)(uint16_t)((uint16_t)row[o] + acc);
+  const uint32_t N = it.N, ne = it.ne, len = it.rowlen;
+  const uint16_t *__restrict__ e = reinterpret_cast<const uint16_t *>(it.e);
+  auto add = [&](uint32_t old, uint32_t m) -> uint32_t { // one int16 entry, wrapping
+    uint32_t acc = old;
+    for (uint32_t i = m; i < ne; i += N) acc += e[i];
+    return acc & 0xFFFFu;
+  };
+  const uint32_t nv = (len + 7) / 8; // the inverse table is padded: entries past len are 0xFFFF
+  const uint4 *__restrict__ inv = reinterpret_cast<const uint4 *>(it.inv);
+  uint4 *__restrict__ row = reinterpret_cast<uint4 *>(it.row);
+  // rows hold SOFTBUFFER_SIZE entries, so the padded tail of the last vector stays inside the
+  // row; entries past len keep their value (or become 0 on a fresh row)
+  if (ne <= N && ne <= DERM_LDS) {
+    // each circular-buffer entry received at most once (the usual case): the E LLRs are staged
+    // in LDS with 16-byte loads and gathered from there (scattered 2-byte global gathers cost
+    // one address-unit slot per lane)
+    const uint32_t nw = (ne + 1) / 2;
+    if (((uintptr_t)it.e & 3) == 0) { // E is even for every Qm; an odd tail is read alone
+      const uint32_t *__restrict__ e32 = reinterpret_cast<const uint32_t *>(it.e);
+      for (uint32_t w = threadIdx.x; w < ne / 2; w += blockDim.x) es[w] = e32[w];
+      if ((ne & 1) && threadIdx.x == 0) es[ne / 2] = e[ne - 1];
+    } else {
+      for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
+        es[w] = (uint32_t)e[2 * w] | (2 * w + 1 < ne ? (uint32_t)e[2 * w + 1] << 16 : 0u);
+    }
+    __syncthreads();
+    const uint16_t *el = reinterpret_cast<const uint16_t *>(es);
+#pragma unroll 4
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+      const uint4 iv = inv[v];
+      const uint4 ov = fresh ? make_uint4(0, 0, 0, 0) : row[v];
+      const uint32_t im[4] = {iv.x, iv.y, iv.z, iv.w}, om[4] = {ov.x, ov.y, ov.z, ov.w};
+      uint32_t r[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const uint32_t m0 = im[h] & 0xFFFFu, m1 = im[h] >> 16;
+        const uint32_t e0 = m0 < ne ? el[m0] : 0u, e1 = m1 < ne ? el[m1] : 0u; // 0xFFFF >= ne
+        r[h] = ((om[h] + e0) & 0xFFFFu) | (((om[h] >> 16) + e1) << 16);
+      }
+      row[v] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  } else {
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
+      const uint4 iv = inv[v];
+      const uint4 ov = fresh ? make_uint4(0, 0, 0, 0) : row[v];
+      const uint32_t im[4] = {iv.x, iv.y, iv.z, iv.w}, om[4] = {ov.x, ov.y, ov.z, ov.w};
+      uint32_t r[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const uint32_t m0 = im[h] & 0xFFFFu, m1 = im[h] >> 16;
+        const uint32_t lo = m0 == 0xFFFFu ? om[h] & 0xFFFFu : add(om[h] & 0xFFFFu, m0);
+        const uint32_t hi = m1 == 0xFFFFu ? om[h] >> 16 : add(om[h] >> 16, m1);
+        r[h] = lo | (hi << 16);
+      }
+      row[v] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
   }
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < it.rowlen; p += blockDim.x) it.row[p] = row[p];
   if (fresh && threadIdx.x == 0) *it.fresh = 0; // the row now holds real soft bits
 }
 
