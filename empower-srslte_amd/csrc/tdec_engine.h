@@ -31,6 +31,7 @@ namespace srsgpu {
 
 // live kernel timing (srsgpu_prof_*)
 bool prof_on();
+hipEvent_t prof_event(); // from a pool of drained events
 void prof_push(const char *name, hipEvent_t a, hipEvent_t b);
 struct ProfScope {
   hipEvent_t a = nullptr, b = nullptr;
@@ -38,8 +39,9 @@ struct ProfScope {
   hipStream_t st;
   ProfScope(const char *n, hipStream_t s) : name(n), st(s) {
     if (prof_on()) {
-      if (hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
-        (void)hipEventRecord(a, st);
+      a = prof_event();
+      b = prof_event();
+      if (a && b) (void)hipEventRecord(a, st);
     }
   }
   ~ProfScope() {
@@ -327,6 +329,7 @@ struct TdecEngine {
         vec = vec && (groups[g1].K / groups[g1].nb) % 2 == 0;
         g1++;
       }
+      ProfScope ps("k_load", st);
       HIPCHK(launch_load(d_groups + g0, (int)(g1 - g0), blocks, f.nb, f.sb_input, vec, d_in, in_stride,
                          rows, a, st));
       g0 = g1;
@@ -382,6 +385,7 @@ struct TdecEngine {
   }
 
   int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t maxh = 0) {
+    ProfScope ps("k_decide", st);
     HIPCHK(launch_decide(n, d_groups, (int)groups.size(), total_pairs, arrays(), d_out, out_stride,
                          early, cb_done, cb_ok, noi, (int)maxh, pair_done, st));
     return 0;

@@ -34,6 +34,7 @@ struct Prof {
   std::mutex mu;
   bool on = false;
   std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool; // drained events, reused (hipEventCreate is not free)
   std::map<std::string, std::pair<double, uint64_t>> acc;
   void drain() {
     for (auto &r : pending) {
@@ -43,14 +44,26 @@ struct Prof {
         e.first += ms;
         e.second += 1;
       }
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
+      pool.push_back(r.a);
+      pool.push_back(r.b);
     }
     pending.clear();
   }
 } g_prof;
 
 bool prof_on() { return g_prof.on; }
+hipEvent_t prof_event() {
+  {
+    std::lock_guard<std::mutex> g(g_prof.mu);
+    if (!g_prof.pool.empty()) {
+      hipEvent_t e = g_prof.pool.back();
+      g_prof.pool.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
 void prof_push(const char *name, hipEvent_t a, hipEvent_t b) {
   std::lock_guard<std::mutex> g(g_prof.mu);
   g_prof.pending.push_back({name, a, b});

@@ -1007,33 +1007,35 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
   const int crc_bits = 8 * crc_bytes;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t c0 = 0, c1 = 0;
-  // 4 groups of 64 positions per wave and round, loads issued before use (latency hiding)
-  for (int r0 = wv * 64; r0 < K; r0 += 4 * blockDim.x) {
-    uint32_t dd[4], ww[4];
+  // Every load of the thread (the DEC2 map and the CRC weights of its <= 24 positions) is issued
+  // before the first use: one memory latency per workgroup instead of one per round.
+  // Position of group u in wave wv: p = wv * 64 + u * 256 + lane (64 consecutive per ballot).
+  constexpr int UMAX = 6144 / 256;
+  int ci[UMAX];
+  uint32_t ww[UMAX];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int p = r0 + u * blockDim.x + lane;
-      if (p < K) {
-        const int c = chain_index(p);
-        const uint32_t w = dw[c >> 4] >> (c & 15);
-        dd[u] = (w & 1u) | ((w >> 15) & 2u);
-      } else {
-        dd[u] = 0u;
-      }
-      ww[u] = p < crc_bits ? crc_pw[crc_bits - 1 - p] : 0u;
+  for (int u = 0; u < UMAX; u++) {
+    const int p = wv * 64 + u * 256 + lane;
+    ci[u] = p < K ? chain_index(p) : 0;
+    ww[u] = p < crc_bits ? crc_pw[crc_bits - 1 - p] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < UMAX; u++) {
+    const int p0 = wv * 64 + u * 256;
+    if (p0 >= K) break;
+    const int p = p0 + lane;
+    uint32_t dd = 0u;
+    if (p < K) {
+      const uint32_t w = dw[ci[u] >> 4] >> (ci[u] & 15);
+      dd = (w & 1u) | ((w >> 15) & 2u);
     }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int p0 = r0 + u * blockDim.x;
-      if (p0 >= K) break;
-      const uint64_t m0 = __ballot(dd[u] & 1u), m1 = __ballot(dd[u] & 2u);
-      if (dd[u] & 1u) c0 ^= ww[u];
-      if (dd[u] & 2u) c1 ^= ww[u];
-      const int h = lane >> 3, b = lane & 7;
-      if (lane < 16 && p0 + 8 * b < K && !(h ? skip1 : skip0)) {
-        const uint32_t v = (uint32_t)(((h ? m1 : m0) >> (8 * b)) & 0xffu);
-        outb[(size_t)cbs[h] * out_stride + (p0 >> 3) + b] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
-      }
+    const uint64_t m0 = __ballot(dd & 1u), m1 = __ballot(dd & 2u);
+    if (dd & 1u) c0 ^= ww[u];
+    if (dd & 2u) c1 ^= ww[u];
+    const int h = lane >> 3, b = lane & 7;
+    if (lane < 16 && p0 + 8 * b < K && !(h ? skip1 : skip0)) {
+      const uint32_t v = (uint32_t)(((h ? m1 : m0) >> (8 * b)) & 0xffu);
+      outb[(size_t)cbs[h] * out_stride + (p0 >> 3) + b] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
     }
   }
   if (!crc_bytes) return;

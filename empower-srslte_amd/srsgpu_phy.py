@@ -325,6 +325,8 @@ class Dlsch:
 
     @staticmethod
     def _tbs(tbs_list):
+        if isinstance(tbs_list, ctypes.Array):  # prebuilt descriptors (make_tb_array)
+            return tbs_list
         arr = (srsgpu_dlsch_tb_t * len(tbs_list))()
         for i, t in enumerate(tbs_list):
             for k, v in t.items():
@@ -412,6 +414,16 @@ def make_sf(sf_idx=1, lstart=1, prb=None, nof_prb=100, mod=3, nof_re=0, rnti=123
     return s
 
 
+def make_tb_array(tbs_list):
+    """srsgpu_dlsch_tb_t[] from dicts, built once and reusable across calls"""
+    return Dlsch._tbs(tbs_list)
+
+
+def make_sf_array(sfs):
+    """srsgpu_pdsch_sf_t[] from make_sf() results, built once and reusable across calls"""
+    return sfs if isinstance(sfs, ctypes.Array) else (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+
+
 class Pdsch:
     """srsgpu_pdsch_t: batched PDSCH receive (RE extraction, SISO equalisation, demapping,
     descrambling, CSI, DL-SCH decoding) on device grids."""
@@ -443,18 +455,19 @@ class Pdsch:
         return _lib.srsgpu_pdsch_nof_re(ctypes.byref(self.cell), ctypes.byref(sf))
 
     def llr_dev(self, sfs, d_grid, d_ce, ant_stride, d_e, e_offsets):
-        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
-        offs = (ctypes.c_uint64 * len(e_offsets))(*e_offsets)  # one per TB
+        arr = make_sf_array(sfs)
+        offs = e_offsets if isinstance(e_offsets, ctypes.Array) else \
+            (ctypes.c_uint64 * len(e_offsets))(*e_offsets)  # one per TB
         return _lib.srsgpu_pdsch_llr_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                          _vp(d_e), offs)
 
     def encode_dev(self, sfs, d_data, d_grid):
         """srsgpu_pdsch_encode_dev: TB bytes (data_offset[0]) -> PDSCH REs of each grid"""
-        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+        arr = make_sf_array(sfs)
         return _lib.srsgpu_pdsch_encode_dev(self.q, arr, len(sfs), _vp(d_data), _vp(d_grid))
 
     def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_data, max_halfits, d_ret, d_noi):
-        arr = (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+        arr = make_sf_array(sfs)
         return _lib.srsgpu_pdsch_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                             _vp(d_data), max_halfits, _vp(d_ret), _vp(d_noi))
 
@@ -492,12 +505,12 @@ class Chest:
 
     def put_crs_dev(self, sf_idx, d_grid, stride):
         n = len(sf_idx)
-        arr = (ctypes.c_uint32 * n)(*sf_idx)
+        arr = sf_idx if isinstance(sf_idx, ctypes.Array) else (ctypes.c_uint32 * n)(*sf_idx)
         return _lib.srsgpu_chest_put_crs_dev(self.q, arr, n, _vp(d_grid), stride)
 
     def estimate_dev(self, sf_idx, d_grid, stride, d_ce, d_noise=None):
         n = len(sf_idx)
-        arr = (ctypes.c_uint32 * n)(*sf_idx)
+        arr = sf_idx if isinstance(sf_idx, ctypes.Array) else (ctypes.c_uint32 * n)(*sf_idx)
         return _lib.srsgpu_chest_estimate_dev(self.q, arr, n, _vp(d_grid), stride, _vp(d_ce),
                                               _vp(d_noise) if d_noise else None)
 

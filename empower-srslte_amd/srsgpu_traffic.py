@@ -16,6 +16,8 @@ blocks by decoder variant and size on the device side, so mixed K costs no per-c
 Reference flow per subframe: srslte_ofdm_rx_sf -> srslte_chest_dl_estimate -> srslte_pdsch_decode
 (lib/src/phy/ue/ue_dl.c:379-433,580).
 """
+import ctypes
+
 import numpy as np
 
 import srsgpu_phy as s
@@ -74,9 +76,12 @@ class MixedCells:
                                 "softbuffer": len(tb_list), "e_offset": e_off, "data_offset": d_off})
                 e_off += (nre * qm + 63) // 64 * 64
                 d_off += s.dlsch_data_len(tbs) + 2
-            c.update(sfs=sfs, e_offs=e_offs, sf_idx=sf_idx)
+            # descriptor arrays built once (the receive step reuses them every batch)
+            c.update(sfs=s.make_sf_array(sfs), e_offs=(ctypes.c_uint64 * n)(*e_offs),
+                     sf_idx=(ctypes.c_uint32 * n)(*sf_idx))
             self.cells.append(c)
         self.tb_list = tb_list
+        self.tb_array = s.make_tb_array(tb_list)
         self.ntb = len(tb_list)
         self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
         self.bits = sum(t["tbs"] for t in tb_list)
@@ -125,7 +130,7 @@ class MixedCells:
     def decode(self):
         """one DL-SCH call over every cell's transport blocks (new TBs: softbuffers reset)"""
         self.dlsch.reset_range(0, self.ntb)
-        assert self.dlsch.decode_dev(self.tb_list, self.d_e.data_ptr(), self.d_data.data_ptr(),
+        assert self.dlsch.decode_dev(self.tb_array, self.d_e.data_ptr(), self.d_data.data_ptr(),
                                      self.max_halfits, self.d_ret.data_ptr(),
                                      self.d_noi.data_ptr()) == 0
 
