@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <map>
+#include <tuple>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -84,6 +85,8 @@ struct TdecEngine {
   };
   std::map<std::pair<uint32_t, uint32_t>, Interl> interl;
   std::map<uint32_t, uint32_t *> crc_tables; // poly -> x^(d+24) mod P, d < 6144 (k_decide)
+  // (K, nb, poly, crc_len) -> chain-major CRC weights after DEC1 and DEC2 (TdGroup::wc)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t *, uint32_t *>> wc_tables;
   // current job (one pass)
   std::vector<TdGroup> groups; // kind order
   TdGroup *d_groups = nullptr, *h_groups = nullptr;
@@ -141,6 +144,11 @@ struct TdecEngine {
     if (gev) (void)hipEventDestroy(gev);
     for (auto &kv : crc_tables) (void)hipFree(kv.second);
     crc_tables.clear();
+    for (auto &kv : wc_tables) {
+      (void)hipFree(kv.second.first);
+      (void)hipFree(kv.second.second);
+    }
+    wc_tables.clear();
     for (auto &kv : interl)
       for (uint16_t *p : {kv.second.fwd, kv.second.rev, kv.second.dmap}) (void)hipFree(p);
     interl.clear();
@@ -190,6 +198,43 @@ struct TdecEngine {
     if (hipMemcpy(dt, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
     crc_tables.emplace(poly, dt);
     return dt;
+  }
+
+  // CRC weight per decision bit in chain-major order (k_decide folds the CRC over the decoder's
+  // decision words directly): after DEC1 natural position p = d L + k sits at d*16*G16 + k; after
+  // DEC2 at dmap[p]
+  int wc_table(uint32_t Kv, uint32_t nbv, uint32_t poly, uint32_t crc_len, const Interl *il,
+               const uint32_t *w[2]) {
+    const auto key = std::make_tuple(Kv, nbv, poly, crc_len);
+    auto it = wc_tables.find(key);
+    if (it == wc_tables.end()) {
+      std::vector<uint32_t> pw(6144);
+      uint32_t r = 1u << 23;
+      for (int d = 0; d < 6144; d++) {
+        const uint32_t top = r & 0x800000u;
+        r = (r << 1) & 0xFFFFFFu;
+        if (top) r ^= poly & 0xFFFFFFu;
+        pw[d] = r;
+      }
+      const uint32_t L = Kv / nbv, G16 = (L + 15) / 16, n = nbv * G16 * 16;
+      std::vector<uint16_t> dm(Kv);
+      if (hipMemcpy(dm.data(), il->dmap, Kv * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+      std::vector<uint32_t> w1(n, 0), w2(n, 0);
+      for (uint32_t p = 0; p < Kv && p < crc_len; p++) {
+        const uint32_t v = pw[crc_len - 1 - p];
+        w1[(p / L) * 16 * G16 + p % L] = v;
+        w2[dm[p]] = v;
+      }
+      uint32_t *d1 = nullptr, *d2 = nullptr;
+      if (hipMalloc(&d1, n * 4) != hipSuccess || hipMalloc(&d2, n * 4) != hipSuccess) return -1;
+      if (hipMemcpy(d1, w1.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d2, w2.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return -1;
+      it = wc_tables.emplace(key, std::make_pair(d1, d2)).first;
+    }
+    w[0] = it->second.first;
+    w[1] = it->second.second;
+    return 0;
   }
 
   static int kind_of(int r) {
@@ -264,9 +309,10 @@ struct TdecEngine {
       g.dmap = it->dmap;
       g.crc_bytes = (int)(sp.crc_len / 8);
       g.crc_pw = nullptr;
+      g.wc[0] = g.wc[1] = nullptr;
       if (g.crc_bytes) {
         g.crc_pw = crc_table(sp.poly);
-        if (!g.crc_pw) return -1;
+        if (!g.crc_pw || wc_table(sp.K, (uint32_t)nbv, sp.poly, sp.crc_len, it, g.wc)) return -1;
       }
       pairs += g.npairs;
       elems += (size_t)g.npairs * sp.K;

@@ -28,6 +28,9 @@ struct TdGroup {
   int64_t sc0;                // first short2 of the sequential decoders' scratch
   const uint16_t *fwd, *rev, *dmap;
   const uint32_t *crc_pw;     // x^(d+24) mod P of the group's CRC (early stop)
+  const uint32_t *wc[2];      // CRC weight of each decision bit in the decoder's chain-major order
+                              // after DEC1 / DEC2: crc_pw[crc_bits - 1 - p] for the natural
+                              // position p the bit carries, 0 for padding and p >= crc_bits
   int32_t crc_bytes;          // CRC-checked prefix in bytes (0: no CRC)
   int32_t sb_input;           // input rows in rm_turbo's sub-block layout
 };

@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
                                                 int max_halfits, uint8_t *__restrict__ pair_done) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ uint32_t red[2][4];
-  __shared__ int fin[2];
+  __shared__ int fin[4]; // [0..1] CB done, [2..3] CB finished at this half-iteration
   const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, blockIdx.x)];
   const int K = G.K, NB = G.nb, ncb = G.ncb;
   const int pair = blockIdx.x - G.pair0;
@@ -986,13 +986,74 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
   const bool skip1 = cbs[1] < 0 || (early && cb_done[cbs[1]]);
   if (skip0 && skip1) return;
   const gptr_t<uint16_t> dmap = gptr(G.dmap);
-  const gptr_t<uint32_t> crc_pw = gptr(G.crc_pw);
   const int crc_bytes = early ? G.crc_bytes : 0;
   const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
   const uint32_t *src = Darr + G.dw0 + (size_t)pair * nw;
   for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
   __syncthreads();
   const bool dec2 = n & 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int UMAX = (6144 + 256) / 256; // chain-major bits per thread (nw * 16 <= 6400)
+  bool out[2] = {!skip0, !skip1};          // natural-order bytes wanted for CB h
+  if (crc_bytes) {
+    // CRC straight from the decision words (crc.c:144-155 is linear): the XOR of the chain-major
+    // weights wc[c] over the set bits c (TdGroup::wc); all loads issued up front
+    const gptr_t<uint32_t> wc = gptr(G.wc[dec2 ? 1 : 0]);
+    uint32_t c0 = 0, c1 = 0, v[UMAX];
+#pragma unroll
+    for (int u = 0; u < UMAX; u++) {
+      const int c = u * 256 + threadIdx.x;
+      v[u] = c < nw * 16 ? wc[c] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < UMAX; u++) {
+      const int c = u * 256 + threadIdx.x;
+      if (c < nw * 16) {
+        const uint32_t w = dw[c >> 4] >> (c & 15);
+        if (w & 1u) c0 ^= v[u];
+        if (w & 0x10000u) c1 ^= v[u];
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 ^= __shfl_xor(c0, o);
+      c1 ^= __shfl_xor(c1, o);
+    }
+    if (lane == 0) {
+      red[0][wv] = c0;
+      red[1][wv] = c1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const int h = threadIdx.x;
+      int done = 1, now = 0;
+      if (!(h ? skip1 : skip0)) {
+        uint32_t crc = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) crc ^= red[h][w];
+        const int cb = cbs[h];
+        noi[cb] = (uint32_t)(n + 1);
+        if (crc == 0) {
+          cb_ok[cb] = 1;
+          cb_done[cb] = 1;
+          now = 1;
+        } else if (n + 1 >= max_halfits) {
+          cb_done[cb] = 1;
+          now = 1;
+        } else {
+          done = 0;
+        }
+      }
+      fin[h] = done;
+      fin[2 + h] = now;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && pair_done) pair_done[blockIdx.x] = (uint8_t)(fin[0] && fin[1]);
+    // the bytes of a block matter once, at the half-iteration that ends it (sch.c:361-391: the
+    // data of the last iteration run stays)
+    out[0] = fin[2] != 0;
+    out[1] = fin[3] != 0;
+    if (!out[0] && !out[1]) return;
+  }
+  // Hard decisions in natural order (turbodecoder.c:353-360 + decision_byte), MSB first.
   // DEC1: p = d L + k -> d * 16 G16 + k; d from a float reciprocal (exact: p < 6144, so the
   // fraction of (p + 0.5) / L stays >= 1 / (2 L) away from an integer)
   const float invL = 1.0f / (float)L;
@@ -1002,25 +1063,17 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
     const int d = (int)(((float)p + 0.5f) * invL);
     return p + d * gap;
   };
-  // CRC is linear: the checksum of the first crc_bits bits is the XOR over set bits p of
-  // x^(crc_bits - 1 - p + 24) mod P = crc_pw[crc_bits - 1 - p].
-  const int crc_bits = 8 * crc_bytes;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t c0 = 0, c1 = 0;
-  // Every load of the thread (the DEC2 map and the CRC weights of its <= 24 positions) is issued
-  // before the first use: one memory latency per workgroup instead of one per round.
-  // Position of group u in wave wv: p = wv * 64 + u * 256 + lane (64 consecutive per ballot).
-  constexpr int UMAX = 6144 / 256;
-  int ci[UMAX];
-  uint32_t ww[UMAX];
+  // Position of group u in wave wv: p = wv * 64 + u * 256 + lane (64 consecutive per ballot);
+  // every map load of the thread issued before the first use
+  constexpr int PMAX = 6144 / 256;
+  int ci[PMAX];
 #pragma unroll
-  for (int u = 0; u < UMAX; u++) {
+  for (int u = 0; u < PMAX; u++) {
     const int p = wv * 64 + u * 256 + lane;
     ci[u] = p < K ? chain_index(p) : 0;
-    ww[u] = p < crc_bits ? crc_pw[crc_bits - 1 - p] : 0u;
   }
 #pragma unroll
-  for (int u = 0; u < UMAX; u++) {
+  for (int u = 0; u < PMAX; u++) {
     const int p0 = wv * 64 + u * 256;
     if (p0 >= K) break;
     const int p = p0 + lane;
@@ -1030,45 +1083,12 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
       dd = (w & 1u) | ((w >> 15) & 2u);
     }
     const uint64_t m0 = __ballot(dd & 1u), m1 = __ballot(dd & 2u);
-    if (dd & 1u) c0 ^= ww[u];
-    if (dd & 2u) c1 ^= ww[u];
     const int h = lane >> 3, b = lane & 7;
-    if (lane < 16 && p0 + 8 * b < K && !(h ? skip1 : skip0)) {
+    if (lane < 16 && p0 + 8 * b < K && out[h]) {
       const uint32_t v = (uint32_t)(((h ? m1 : m0) >> (8 * b)) & 0xffu);
       outb[(size_t)cbs[h] * out_stride + (p0 >> 3) + b] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
     }
   }
-  if (!crc_bytes) return;
-  for (int o = 32; o > 0; o >>= 1) {
-    c0 ^= __shfl_xor(c0, o);
-    c1 ^= __shfl_xor(c1, o);
-  }
-  if (lane == 0) {
-    red[0][wv] = c0;
-    red[1][wv] = c1;
-  }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    const int h = threadIdx.x;
-    int done = 1;
-    if (!(h ? skip1 : skip0)) {
-      uint32_t crc = 0;
-      for (int w = 0; w < (int)(blockDim.x >> 6); w++) crc ^= red[h][w];
-      const int cb = cbs[h];
-      noi[cb] = (uint32_t)(n + 1);
-      if (crc == 0) {
-        cb_ok[cb] = 1;
-        cb_done[cb] = 1;
-      } else if (n + 1 >= max_halfits) {
-        cb_done[cb] = 1;
-      } else {
-        done = 0;
-      }
-    }
-    fin[h] = done;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && pair_done) pair_done[blockIdx.x] = (uint8_t)(fin[0] && fin[1]);
 }
 
 // pair_done = both code blocks finished (seeding after init_done)
