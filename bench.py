@@ -13,6 +13,7 @@ Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -226,11 +227,13 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    gc.disable()  # the host-bound legs must not pay a collector pause inside the timed loop
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    gc.enable()
     stages = stage_profile(s, torch, step, steps)
     noi = d_noi.cpu().numpy()
     for o in (ofdm, chest, pd):
@@ -263,11 +266,13 @@ def run_traffic(s, torch, dev, steps, warmup, kind):
     for _ in range(warmup):
         m.step()
     torch.cuda.synchronize()
+    gc.disable()
     t0 = time.perf_counter()
     for _ in range(steps):
         m.step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    gc.enable()
     stages = stage_profile(s, torch, m.step, steps)
     acks, good, noi = m.check()
     ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in m.tb_list})
@@ -369,6 +374,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    gc.disable()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -376,6 +382,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     # The decoder kernel's launch duration for the roofline: HIP events around every launch on the
     # batch stream (srsgpu_prof_*), over the same number of steps right after the timed loop.
     # Events inside the timed loop would cost ~9% of the step (event records between launches).
@@ -431,14 +438,14 @@ def main():
     pipe = None
     legs = set() if args.no_pipeline else set(args.legs.split(","))
     if "c3" in legs:
-        pipe = run_pipeline(s, torch, dev, max(1, args.steps // 2), 1)
+        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2)
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
             pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
     pipe3 = None
     if "tm3" in legs:
-        pipe3 = run_pipeline(s, torch, dev, max(1, args.steps // 2), 1, tm=3)
+        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3)
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
             pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
@@ -446,7 +453,8 @@ def main():
     extra = {}
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
-            r = run_traffic(s, torch, dev, max(1, args.steps // 2), 1, kind)
+            # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
+            r = run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind)
             if dist:
                 ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
                 r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)

@@ -195,12 +195,14 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   if (all_ok) {
     uint32_t acc = 0;
     const uint32_t nbytes = t.tbs / 8;
+    // the 8 weights of a byte are loaded unconditionally and masked, so a thread's loads do not
+    // wait behind data-dependent branches; two bytes per thread and round in flight
+#pragma unroll 2
     for (uint32_t j = threadIdx.x; j < nbytes; j += blockDim.x) {
       const uint32_t v = t.data[j];
       const uint32_t *w = crc_a + (t.tbs - 1 - 8 * j); // w[-b]: bit b (MSB first) of byte j
 #pragma unroll
-      for (int b = 0; b < 8; b++)
-        if ((v >> (7 - b)) & 1u) acc ^= *(w - b);
+      for (int b = 0; b < 8; b++) acc ^= w[-b] & (0u - ((v >> (7 - b)) & 1u));
     }
     crc = wg_xor(acc, red);
   }
