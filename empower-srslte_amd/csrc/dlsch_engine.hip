@@ -426,7 +426,7 @@ struct DlschEngine {
     }
     if (!specs.empty() &&
         tdec.decode_multi(SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
-                          (const int16_t *const *)d_rows, 1, d_init, maxh, d_dec, 768, d_ok, d_noi))
+                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi))
       return -1;
     {
       ProfScope ps("k_tb_finish", st);

@@ -320,17 +320,6 @@ struct TdecEngine {
       if (nbv == 1) sc += seq_scratch_elems(g.K, g.npairs);
     }
     for (int k = TD_NKIND - 1; k >= 0; k--) kind_g0[k] = std::min(kind_g0[k], kind_g0[k + 1]);
-    // load launches: runs of groups with the same loader (nb, sb_input)
-    for (size_t g0 = 0; g0 < ns;) {
-      size_t g1 = g0;
-      int blocks = 0;
-      while (g1 < ns && groups[g1].nb == groups[g0].nb && groups[g1].sb_input == groups[g0].sb_input) {
-        groups[g1].blk_load = blocks;
-        blocks += load_blocks(groups[g1].K, groups[g1].nb, groups[g1].npairs, groups[g1].sb_input);
-        g1++;
-      }
-      g0 = g1;
-    }
     if ((size_t)pairs > cap_pairs || elems > cap_elems || dw > cap_dw || sc > cap_sc) return 1;
     total_pairs = pairs;
     return 0;
@@ -362,23 +351,41 @@ struct TdecEngine {
   // (total_cbs code blocks; init_done seeds cb_done: blocks already decoded are skipped, noi 0)
   int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
                    int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs) {
-    if (upload_groups()) return -1;
-    const TdArrays a = arrays();
+    // load launches: runs of groups with the same loader (nb, sb_input); rows_aligned is the
+    // byte alignment every row is guaranteed to have (0: none)
     const size_t ng = groups.size();
+    struct Run {
+      size_t g0, g1;
+      int blocks;
+      bool vec;
+    };
+    std::vector<Run> runs;
     for (size_t g0 = 0; g0 < ng;) {
       const TdGroup &f = groups[g0];
+      bool vec = f.sb_input ? (rows ? rows_aligned >= 16
+                                    : ((uintptr_t)d_in % 16 == 0 && (in_stride * 2) % 16 == 0))
+                            : (rows ? rows_aligned >= 4 : ((uintptr_t)d_in % 4 == 0 && in_stride % 2 == 0));
       size_t g1 = g0;
-      int blocks = 0;
-      bool vec = rows ? rows_aligned != 0 : ((uintptr_t)d_in % 4 == 0 && in_stride % 2 == 0);
       while (g1 < ng && groups[g1].nb == f.nb && groups[g1].sb_input == f.sb_input) {
-        blocks += load_blocks(groups[g1].K, groups[g1].nb, groups[g1].npairs, groups[g1].sb_input);
-        vec = vec && (groups[g1].K / groups[g1].nb) % 2 == 0;
+        if (!f.sb_input) vec = vec && (groups[g1].K / groups[g1].nb) % 2 == 0;
         g1++;
       }
-      ProfScope ps("k_load", st);
-      HIPCHK(launch_load(d_groups + g0, (int)(g1 - g0), blocks, f.nb, f.sb_input, vec, d_in, in_stride,
-                         rows, a, st));
+      int blocks = 0;
+      for (size_t g = g0; g < g1; g++) {
+        groups[g].blk_load = blocks;
+        blocks += load_blocks(groups[g].K, groups[g].nb, groups[g].npairs, groups[g].sb_input,
+                              f.sb_input && vec);
+      }
+      runs.push_back(Run{g0, g1, blocks, vec});
       g0 = g1;
+    }
+    if (upload_groups()) return -1;
+    const TdArrays a = arrays();
+    for (const Run &r : runs) {
+      const TdGroup &f = groups[r.g0];
+      ProfScope ps("k_load", st);
+      HIPCHK(launch_load(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, f.nb, f.sb_input, r.vec, d_in,
+                         in_stride, rows, a, st));
     }
     if (first) {
       HIPCHK(hipMemsetAsync(cb_ok, 0, total_cbs, st));

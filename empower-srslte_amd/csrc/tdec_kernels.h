@@ -42,12 +42,13 @@ struct TdArrays {
 
 // user input -> SP0 / P1 / T for groups [0, ng) of dg (all with the same nb and sb_input).
 // rows != NULL: code block c's input starts at rows[c], else at in + c * in_stride.
-// vec: natural rows may be read as dwords.
+// vec: natural rows may be read as dwords; sub-block rows as 16-byte vectors.
 hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_input, bool vec,
                        const int16_t *in, size_t in_stride, const int16_t *const *rows,
                        const TdArrays &a, hipStream_t st);
 // workgroups a group needs in the load / half-iteration launch of its kind
-int load_blocks(int K, int nb, int npairs, int sb_input);
+// vec16: sub-block rows that are 16-byte aligned (8 elements per thread)
+int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16);
 int halfit_blocks(int nb, int npairs);
 size_t seq_scratch_elems(int K, int npairs); // short2 elements
 size_t bidir_lds_bytes(int K, int nb);

@@ -958,6 +958,48 @@ __global__ __launch_bounds__(256) void k_load_sb(const TdGroup *__restrict__ gro
   }
 }
 
+// The same copy, eight elements of a pair per thread with 16-byte accesses (rows 16-byte aligned,
+// as the DL-SCH softbuffer rows are; K is a multiple of 8 for every LTE code block size): six
+// 16-byte loads, four 16-byte SP0 stores and two 16-byte P1 stores per thread.
+__global__ __launch_bounds__(256) void k_load_sb8(const TdGroup *__restrict__ groups, int ngroups,
+                                                  const int16_t *__restrict__ in, size_t in_stride,
+                                                  const int16_t *const *__restrict__ rows,
+                                                  TdArrays arr) {
+  const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs;
+  const int per = K / 8;
+  const size_t gid = (size_t)(blockIdx.x - G.blk_load) * 256 + threadIdx.x;
+  const int pair = (int)(gid / per);
+  if (pair >= npairs) return;
+  const int i = 8 * (int)(gid - (size_t)pair * per);
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
+  const gptr_t<int16_t> a = cb_row(in, in_stride, rows, c0), b = cb_row(in, in_stride, rows, c1);
+  typedef short s8v __attribute__((ext_vector_type(8)));
+  auto ld8 = [](gptr_t<int16_t> p) { return *(const __attribute__((address_space(1))) s8v *)p; };
+  const s8v sa = ld8(a + i), sb = ld8(b + i);
+  const s8v pa = ld8(a + K + 32 + i), pb = ld8(b + K + 32 + i);
+  const s8v qa = ld8(a + 2 * (K + 32) + i), qb = ld8(b + 2 * (K + 32) + i);
+  const size_t o = (size_t)G.elem0 + (size_t)pair * K + i; // multiple of 8: 16-byte aligned
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const gmut_t<u4v> SP0 = gmut<u4v>((s4 *)arr.SP0 + o);
+  const gmut_t<u4v> P1 = gmut<u4v>((s2 *)arr.XP1 + arr.plane + o);
+  auto pk = [](short lo, short hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
+#pragma unroll
+  for (int u = 0; u < 4; u++) // two short4 (syst.a, syst.b, par0.a, par0.b) per 16-byte store
+    SP0[u] = u4v{pk(sa[2 * u], sb[2 * u]), pk(pa[2 * u], pb[2 * u]),
+                 pk(sa[2 * u + 1], sb[2 * u + 1]), pk(pa[2 * u + 1], pb[2 * u + 1])};
+#pragma unroll
+  for (int u = 0; u < 2; u++) // four short2 (par1.a, par1.b) per 16-byte store
+    P1[u] = u4v{pk(qa[4 * u], qb[4 * u]), pk(qa[4 * u + 1], qb[4 * u + 1]),
+                pk(qa[4 * u + 2], qb[4 * u + 2]), pk(qa[4 * u + 3], qb[4 * u + 3])};
+  if (i == 0) { // one thread per pair: the tails
+    const int tb = 3 * (K + 32);
+    const gmut_t<s2> T = gmut<s2>(arr.T);
+#pragma unroll
+    for (int t = 0; t < 12; t++) T[(size_t)(G.pair0 + pair) * 12 + t] = s2{a[tb + t], b[tb + t]};
+  }
+}
+
 // ------------------------------------------------------------------ decide (+ CRC) ----
 // Hard decision after half-iteration n (turbodecoder.c:353-360 + decision_byte), MSB first,
 // from the decoders' packed decision words D (see dec_bits). One workgroup per CB pair:
@@ -1111,8 +1153,8 @@ static void allow_big_lds(const void *f) {
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
-int load_blocks(int K, int nb, int npairs, int sb_input) {
-  if (sb_input) return (int)nblk((size_t)npairs * (K / 2), 256);
+int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16) {
+  if (sb_input) return (int)nblk((size_t)npairs * (K / (vec16 ? 8 : 2)), 256);
   return npairs * ((K / nb + LOAD_KT - 1) / LOAD_KT);
 }
 
@@ -1131,7 +1173,10 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
                        const TdArrays &a, hipStream_t st) {
   if (ng <= 0 || nblocks <= 0) return hipSuccess;
   if (sb_input) {
-    hipLaunchKernelGGL(k_load_sb, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
+    if (vec) // 16-byte aligned rows (load_blocks counted 8 elements per thread)
+      hipLaunchKernelGGL(k_load_sb8, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
+    else
+      hipLaunchKernelGGL(k_load_sb, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
     return hipGetLastError();
   }
 #define LOADNAT(n)                                                                                 \
