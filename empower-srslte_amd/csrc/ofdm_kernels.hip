@@ -102,12 +102,151 @@ __global__ __launch_bounds__(256) void k_ofdm_rx(const float2 *__restrict__ in, 
   }
 }
 
+// ---- fixed-size path: the LTE symbol sizes, with the whole stage plan known at compile time ----
+// Radix 8 first (then 4, 2, 3): 2048 = 8.8.8.4 is four LDS passes instead of six, and with N, R
+// and Ns constants every index division is a shift or a multiply. Small symbols share a
+// workgroup (256 / S threads per symbol) so every size launches full 256-thread workgroups.
+template <int R, int N, int Ns, int TPS>
+__device__ __forceinline__ void stage_c(const cf *__restrict__ d0, cf *__restrict__ d1,
+                                        const float2 *__restrict__ tw, int t) {
+  constexpr int nb = N / R;
+  for (int j = t; j < nb; j += TPS) {
+    const int k = j % Ns;
+    cf v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      cf a = d0[j + r * nb];
+      if (Ns > 1 && r) { // e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
+        const float2 w = tw[r * k * (N / (Ns * R))];
+        a = cmul(a, cf{w.x, w.y});
+      }
+      v[r] = a;
+    }
+    cf y[R];
+    if constexpr (R == 8) {
+      // two 4-point DFTs (even / odd inputs) joined with W8^k = e^{-i pi k / 4}
+      const float c = 0.70710678118654752f;
+      cf e[4], o[4];
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const cf a0 = v[h], a1 = v[h + 2], a2 = v[h + 4], a3 = v[h + 6];
+        const cf s02 = cadd(a0, a2), d02 = csub(a0, a2);
+        const cf s13 = cadd(a1, a3), d13 = mul_mi(csub(a1, a3));
+        cf *z = h ? o : e;
+        z[0] = cadd(s02, s13);
+        z[2] = csub(s02, s13);
+        z[1] = cadd(d02, d13);
+        z[3] = csub(d02, d13);
+      }
+      const cf o1 = {c * (o[1].x + o[1].y), c * (o[1].y - o[1].x)}; // * (c - ic)
+      const cf o2 = mul_mi(o[2]);                                    // * -i
+      const cf o3 = {c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)}; // * (-c - ic)
+      y[0] = cadd(e[0], o[0]);
+      y[4] = csub(e[0], o[0]);
+      y[1] = cadd(e[1], o1);
+      y[5] = csub(e[1], o1);
+      y[2] = cadd(e[2], o2);
+      y[6] = csub(e[2], o2);
+      y[3] = cadd(e[3], o3);
+      y[7] = csub(e[3], o3);
+    } else if constexpr (R == 4) {
+      const cf s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+      const cf s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+      y[0] = cadd(s02, s13);
+      y[2] = csub(s02, s13);
+      y[1] = cadd(d02, d13);
+      y[3] = csub(d02, d13);
+    } else if constexpr (R == 2) {
+      y[0] = cadd(v[0], v[1]);
+      y[1] = csub(v[0], v[1]);
+    } else {
+      const float cc = -0.5f, sn = -0.86602540378443865f;
+      const cf tt = cadd(v[1], v[2]), u = csub(v[1], v[2]);
+      y[0] = cadd(v[0], tt);
+      const cf m = {v[0].x + cc * tt.x, v[0].y + cc * tt.y};
+      const cf q = {-sn * u.y, sn * u.x};
+      y[1] = cadd(m, q);
+      y[2] = csub(m, q);
+    }
+    const int o = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; r++) d1[o + r * Ns] = y[r];
+  }
+}
+
+// stages Ns .. N; returns the buffer holding the result
+template <int N, int Ns, int TPS>
+__device__ __forceinline__ cf *fft_c(cf *b0, cf *b1, const float2 *__restrict__ tw, int t) {
+  if constexpr (Ns >= N) {
+    return b0;
+  } else {
+    constexpr int rem = N / Ns;
+    constexpr int R = rem % 8 == 0 ? 8 : rem % 4 == 0 ? 4 : rem % 2 == 0 ? 2 : 3;
+    stage_c<R, N, Ns, TPS>(b0, b1, tw, t);
+    __syncthreads();
+    return fft_c<N, Ns * R, TPS>(b1, b0, tw, t);
+  }
+}
+
+template <int N>
+constexpr int syms_per_wg() {
+  return N >= 1024 ? 1 : N >= 512 ? 2 : N >= 256 ? 4 : 8;
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in, size_t in_stride,
+                                                   float2 *__restrict__ out, size_t out_stride, int nsym,
+                                                   int nre, int cp0, int cp,
+                                                   const float2 *__restrict__ tw, float scale) {
+  constexpr int S = syms_per_wg<N>(), TPS = 256 / S;
+  __shared__ cf buf[S][2][N];
+  const int s = threadIdx.x / TPS, t = threadIdx.x % TPS;
+  const int g = blockIdx.x * S + s; // symbol of this thread group (past nsym: idle, but at barriers)
+  const bool live = g < nsym;
+  const int sym = g % 14, sf = g / 14;
+  const int slot = sym / 7, l = sym % 7;
+  const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
+  if (live) {
+    const cf *src = (const cf *)(in + (size_t)sf * in_stride + start);
+    for (int n = t; n < N; n += TPS) buf[s][0][n] = src[n];
+  }
+  __syncthreads();
+  const cf *res = fft_c<N, 1, TPS>(buf[s][0], buf[s][1], tw, t);
+  if (live) {
+    cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
+    const int h = nre / 2;
+    for (int k = t; k < nre; k += TPS) {
+      const cf v = res[k < h ? N - h + k : 1 + k - h];
+      dst[k] = cf{v.x * scale, v.y * scale};
+    }
+  }
+}
+
 hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
                           int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
                           hipStream_t st) {
   if (nsf <= 0) return hipSuccess;
   const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
-  hipLaunchKernelGGL(k_ofdm_rx, dim3((unsigned)nsf * 14), dim3(256), 0, st, in, in_stride, out, out_stride,
+  const int nsym = nsf * 14;
+#define OFDM_RX_C(n)                                                                               \
+  case n:                                                                                          \
+    hipLaunchKernelGGL(k_ofdm_rx_c<n>, dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \
+                       dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, tw, scale); \
+    return hipGetLastError();
+  switch (N) {
+    OFDM_RX_C(128)
+    OFDM_RX_C(256)
+    OFDM_RX_C(384)
+    OFDM_RX_C(512)
+    OFDM_RX_C(768)
+    OFDM_RX_C(1024)
+    OFDM_RX_C(1536)
+    OFDM_RX_C(2048)
+  default:
+    break;
+  }
+#undef OFDM_RX_C
+  hipLaunchKernelGGL(k_ofdm_rx, dim3((unsigned)nsym), dim3(256), 0, st, in, in_stride, out, out_stride,
                      N, nre, cp0, cp, tw, radices, nstages, scale);
   return hipGetLastError();
 }

@@ -51,3 +51,25 @@ def test_ofdm_rx_gpu_vs_numpy(nof_prb, standard):
         rms = np.sqrt(np.mean(np.abs(ref) ** 2))
         assert np.max(np.abs(got[i] - ref)) / rms < 1e-4, (i, np.max(np.abs(got[i] - ref)) / rms)
     o.close()
+
+
+@pytest.mark.gpu
+def test_ofdm_rx_gpu_generic_size():
+    """a 2^a 3^b size outside the LTE table (1152 = 2^7 3^2) takes the run-time-planned kernel"""
+    import torch
+    import srsgpu_phy as s
+    nof_prb, N, n = 75, 1152, 3
+    rng = np.random.default_rng(11)
+    x = (rng.standard_normal((n, 15 * N)) + 1j * rng.standard_normal((n, 15 * N))).astype(np.complex64)
+    o = s.OfdmRx(nof_prb, N)
+    d_x = torch.from_numpy(x.reshape(-1)).cuda()
+    gsz = 14 * 12 * nof_prb
+    d_g = torch.zeros(n * gsz, dtype=torch.complex64, device="cuda")
+    assert o.rx_dev(n, d_x.data_ptr(), 15 * N, d_g.data_ptr(), gsz) == 0
+    torch.cuda.synchronize()
+    got = d_g.cpu().numpy().reshape(n, -1)
+    for i in range(n):
+        ref = oo.rx_sf(x[i], nof_prb, N)
+        rms = np.sqrt(np.mean(np.abs(ref) ** 2))
+        assert np.max(np.abs(got[i] - ref)) / rms < 1e-4
+    o.close()
