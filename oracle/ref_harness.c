@@ -415,3 +415,51 @@ int ref_mcs_tbs(uint32_t mcs, uint32_t nof_prb, uint32_t *mod) {
   *mod = (uint32_t)srslte_ra_mod_from_mcs(mcs);
   return srslte_ra_tbs_from_idx((uint32_t)i, nof_prb);
 }
+
+/* 8-bit path: init_manual(impl) [+ force_not_sb] + new_cb + nof_halfits x
+ * srslte_tdec_iteration_8bit (turbodecoder.c:536-543), decisions after every half-iteration.
+ * in_len int8 values are copied into a private, padded input (the reference writes tail copies
+ * into it). */
+int ref_tdec8_run(int impl, int sb_layout, const int8_t *input, size_t in_len, uint32_t K,
+                  uint32_t nof_halfits, uint8_t *decisions) {
+  srslte_tdec_t h;
+  if (srslte_tdec_init_manual(&h, SRSLTE_TCOD_MAX_LEN_CB, (srslte_tdec_impl_type_t)impl)) return -1;
+  if (!sb_layout) srslte_tdec_force_not_sb(&h);
+  size_t n = 3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 64;
+  int8_t *buf = NULL;
+  if (posix_memalign((void **)&buf, 64, n)) return -1;
+  memset(buf, 0, n);
+  memcpy(buf, input, in_len);
+  if (srslte_tdec_new_cb(&h, K)) {
+    free(buf);
+    srslte_tdec_free(&h);
+    return -1;
+  }
+  for (uint32_t i = 0; i < nof_halfits; i++) srslte_tdec_iteration_8bit(&h, buf, decisions + (size_t)i * (K / 8));
+  free(buf);
+  srslte_tdec_free(&h);
+  return 0;
+}
+
+/* manual 8-bit window type through the 16-bit entry point (srslte_tdec_iteration), natural
+ * input (force_not_sb) */
+int ref_tdec8_run16(int impl, const int16_t *input, uint32_t K, uint32_t nof_halfits,
+                    uint8_t *decisions) {
+  srslte_tdec_t h;
+  if (srslte_tdec_init_manual(&h, SRSLTE_TCOD_MAX_LEN_CB, (srslte_tdec_impl_type_t)impl)) return -1;
+  srslte_tdec_force_not_sb(&h);
+  size_t n = 3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 64;
+  int16_t *buf = NULL;
+  if (posix_memalign((void **)&buf, 64, n * 2)) return -1;
+  memset(buf, 0, n * 2);
+  memcpy(buf, input, (3 * (size_t)K + 12) * 2);
+  if (srslte_tdec_new_cb(&h, K)) {
+    free(buf);
+    srslte_tdec_free(&h);
+    return -1;
+  }
+  for (uint32_t i = 0; i < nof_halfits; i++) srslte_tdec_iteration(&h, buf, decisions + (size_t)i * (K / 8));
+  free(buf);
+  srslte_tdec_free(&h);
+  return 0;
+}

@@ -13,10 +13,11 @@ ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
 REF_SO = os.path.join(REPO, "oracle", "_ref", "libsrsref.so")
 
 # srslte_tdec_impl_type_t (turbodecoder_impl.h:33-42)
-AUTO, GENERIC, SSE, SSE_WINDOW, AVX_WINDOW = 0, 1, 2, 3, 4
+AUTO, GENERIC, SSE, SSE_WINDOW, AVX_WINDOW, SSE8_WINDOW, AVX8_WINDOW = 0, 1, 2, 3, 4, 5, 6
 CRC24A, CRC24B = 0x1864CFB, 0x1800063
 
 _i16p = ctypes.POINTER(ctypes.c_int16)
+_i8p = ctypes.POINTER(ctypes.c_int8)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u16p = ctypes.POINTER(ctypes.c_uint16)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -74,6 +75,9 @@ class Oracle(_Lib):
     def __init__(self):
         super().__init__(ORACLE_SO, "orc_")
         L = self.lib
+        L.orc_tdec8_run.argtypes = [ctypes.c_int, ctypes.c_int, _i8p, ctypes.c_uint32,
+                                    ctypes.c_uint32, _u8p]
+        L.orc_tdec8_run16.argtypes = [ctypes.c_int, _i16p, ctypes.c_uint32, ctypes.c_uint32, _u8p]
         L.orc_tdec_input_len.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.orc_tdec_decode_cb.argtypes = [ctypes.c_int, ctypes.c_int, _i16p, ctypes.c_uint32,
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u8p,
@@ -82,6 +86,23 @@ class Oracle(_Lib):
 
     def input_len(self, impl, sb, K):
         return self.lib.orc_tdec_input_len(impl, sb, K)
+
+    def tdec8_run(self, impl, sb_layout, inp, K, nhalf):
+        """8-bit path (srslte_tdec_iteration_8bit); decisions per half-iteration, or None where
+        the reference has no defined result (orc_tdec8_run returns -2)"""
+        inp = np.ascontiguousarray(inp, dtype=np.int8)
+        dec = np.zeros((nhalf, K // 8), np.uint8)
+        r = self.lib.orc_tdec8_run(impl, sb_layout, _ptr(inp, _i8p), K, nhalf, _ptr(dec, _u8p))
+        if r == -2:
+            return None
+        assert r == 0, r
+        return dec
+
+    def tdec8_run16(self, impl, inp, K, nhalf):
+        inp = np.ascontiguousarray(inp, dtype=np.int16)
+        dec = np.zeros((nhalf, K // 8), np.uint8)
+        assert self.lib.orc_tdec8_run16(impl, _ptr(inp, _i16p), K, nhalf, _ptr(dec, _u8p)) == 0
+        return dec
 
     def decode_cb(self, impl, sb, inp, K, max_halfits, poly, crc_len):
         inp = np.ascontiguousarray(inp, dtype=np.int16)
@@ -183,6 +204,24 @@ class Ref(_Lib):
         assert self.lib.ref_cbsegm(tbs, _ptr(o, _u32p)) == 0
         return tuple(int(x) for x in o)
 
+    def tdec8_run(self, impl, sb_layout, inp, K, nhalf):
+        L = self.lib
+        L.ref_tdec8_run.argtypes = [ctypes.c_int, ctypes.c_int, _i8p, ctypes.c_size_t,
+                                    ctypes.c_uint32, ctypes.c_uint32, _u8p]
+        inp = np.ascontiguousarray(inp, dtype=np.int8)
+        dec = np.zeros((nhalf, K // 8), np.uint8)
+        assert L.ref_tdec8_run(impl, sb_layout, _ptr(inp, _i8p), inp.size, K, nhalf,
+                               _ptr(dec, _u8p)) == 0
+        return dec
+
+    def tdec8_run16(self, impl, inp, K, nhalf):
+        L = self.lib
+        L.ref_tdec8_run16.argtypes = [ctypes.c_int, _i16p, ctypes.c_uint32, ctypes.c_uint32, _u8p]
+        inp = np.ascontiguousarray(inp, dtype=np.int16)
+        dec = np.zeros((nhalf, K // 8), np.uint8)
+        assert L.ref_tdec8_run16(impl, _ptr(inp, _i16p), K, nhalf, _ptr(dec, _u8p)) == 0
+        return dec
+
     # ---- DL-SCH (sch.c through ref_harness.c) ----
     def _dl_sigs(self):
         L = self.lib
@@ -246,11 +285,27 @@ def awgn_llr(coded_bits, ebno_db, rng, scale=100.0):
     return (np.float32(scale) * y).astype(np.int16)
 
 
+def awgn_llr8(coded_bits, ebno_db, rng, scale=20.0):
+    """as awgn_llr, quantised to int8 with saturation (the 8-bit LLR path)"""
+    esno_db = ebno_db + 10.0 * np.log10(1.0 / 3.0)
+    sigma = np.float32(np.sqrt(1.0 / (10.0 ** (esno_db / 10.0))))
+    sym = np.where(coded_bits.astype(bool), np.float32(1.0), np.float32(-1.0))
+    y = sym + sigma * rng.standard_normal(coded_bits.size).astype(np.float32)
+    return np.clip(np.rint(np.float32(scale) * y), -128, 127).astype(np.int8)
+
+
+def make_cb8(K, ebno_db, seed, scale=20.0, oracle=None):
+    rng = np.random.default_rng(seed)
+    bits = rng.integers(0, 2, K, dtype=np.uint8)
+    coded = (oracle or Oracle()).tcod_encode(bits)
+    return bits, awgn_llr8(coded, ebno_db, rng, scale)
+
+
 def natural_to_sb(inp_nat, K, nsb):
     """[s,p0,p1]*K + 12 tail (natural) -> rm_turbo's sub-block layout: stream s at s*(K+32),
     SB index k*nsb+d = natural position d*(K/nsb)+k, tail at 3*(K+32) (rm_turbo.c:239-264)."""
     L = K // nsb
-    out = np.zeros(3 * (K + 32) + 12, np.int16)
+    out = np.zeros(3 * (K + 32) + 12, inp_nat.dtype)
     p = np.arange(K)
     sbidx = (p % L) * nsb + p // L
     for s in range(3):
