@@ -55,8 +55,10 @@ struct ProfScope {
 
 int cb_index(uint32_t K);
 uint32_t auto_subblocks(uint32_t K);
+uint32_t auto_subblocks_8bit(uint32_t K);
 int resolve_impl(int impl, uint32_t K);
 int impl_nb(int r);
+bool sb_input_for(int impl, int r); // does the decoder read rm_turbo's sub-block layout
 void gen_interleaver(uint32_t K, uint32_t nb, std::vector<uint16_t> &fwd, std::vector<uint16_t> &rev);
 
 // ------------------------------------------------------------------ engine ----
@@ -118,7 +120,7 @@ struct TdecEngine {
     cap_pairs = (max_cbs + 1) / 2 + EXTRA_PAIRS;
     cap_elems = (size_t)((max_cbs + 1) / 2) * max_K + EXTRA_PAIRS * std::min<uint32_t>(max_K, 1024);
     cap_dw = cap_elems / 16 + cap_pairs * 16;
-    cap_sc = (cap_elems + 4 * cap_pairs) * 8;
+    cap_sc = (cap_elems + 32 * cap_pairs) * 8; // int8 windows: (K + 32) * 8 per pair
     HIPCHK(hipMalloc(&SP0, cap_elems * 8));
     HIPCHK(hipMalloc(&XP1, cap_elems * 8));
     HIPCHK(hipMalloc(&A, cap_elems * 4));
@@ -238,6 +240,8 @@ struct TdecEngine {
   }
 
   static int kind_of(int r) {
+    if (r == SRSLTE_TDEC_SSE8_WINDOW) return TD_KIND_B16;
+    if (r == SRSLTE_TDEC_AVX8_WINDOW) return TD_KIND_B32;
     const int nbv = impl_nb(r);
     return nbv == 16 ? TD_KIND_W16 : nbv == 8 ? TD_KIND_W8 : r == SRSLTE_TDEC_SSE ? TD_KIND_SSE : TD_KIND_GEN;
   }
@@ -251,7 +255,7 @@ struct TdecEngine {
       fprintf(stderr, "srsgpu: batch of %u x K=%u exceeds capacity %u x %u\n", n, Kv, cap_cbs, cap_K);
       return -1;
     }
-    if (impl < SRSLTE_TDEC_AUTO || impl > SRSLTE_TDEC_AVX_WINDOW) {
+    if ((impl < SRSLTE_TDEC_AUTO || impl > SRSLTE_TDEC_AVX8_WINDOW) && impl != SRSGPU_TDEC_AUTO_8BIT) {
       fprintf(stderr, "srsgpu: decoder type %d not supported\n", impl);
       return -1;
     }
@@ -298,10 +302,17 @@ struct TdecEngine {
       g.elem0 = (int64_t)elems;
       g.dw0 = (int64_t)dw;
       g.sc0 = (int64_t)sc;
-      g.sb_input = sb_layout && impl == SRSLTE_TDEC_AUTO && nbv > 1;
+      g.sb_input = sb_layout && sb_input_for(impl, r);
+      if (sb_layout && impl == SRSGPU_TDEC_AUTO_8BIT && r == SRSLTE_TDEC_SSE_WINDOW) {
+        // turbodecoder.c:457-460 converts 3K+12 int8 values but the SSE16 window decoder then
+        // reads the sub-block layout's 3(K+32)+12: undefined in the reference
+        fprintf(stderr, "srsgpu: 8-bit input in sub-block layout at K=%u (400 < K <= 800) is not "
+                        "defined by the reference\n", sp.K);
+        return -1;
+      }
       g.blk_half = kind_blocks[kd];
       kind_blocks[kd] += halfit_blocks(nbv, g.npairs);
-      if (nbv > 1) kind_lds[kd] = std::max(kind_lds[kd], bidir_lds_bytes(g.K, nbv));
+      if (kd <= TD_KIND_W8) kind_lds[kd] = std::max(kind_lds[kd], bidir_lds_bytes(g.K, nbv));
       const Interl *it = get_interleaver(sp.K, (uint32_t)nbv);
       if (!it) return -1;
       g.fwd = it->fwd;
@@ -318,6 +329,7 @@ struct TdecEngine {
       elems += (size_t)g.npairs * sp.K;
       dw += (size_t)g.npairs * dec_words_host(g.K, nbv);
       if (nbv == 1) sc += seq_scratch_elems(g.K, g.npairs);
+      if (kd >= TD_KIND_B16) sc += win8_scratch_elems(g.K, nbv, g.npairs);
     }
     for (int k = TD_NKIND - 1; k >= 0; k--) kind_g0[k] = std::min(kind_g0[k], kind_g0[k + 1]);
     if ((size_t)pairs > cap_pairs || elems > cap_elems || dw > cap_dw || sc > cap_sc) return 1;
@@ -431,7 +443,9 @@ struct TdecEngine {
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      ProfScope ps(k <= TD_KIND_W8 ? "k_win_halfit" : (k == TD_KIND_SSE ? "k_sse_halfit" : "k_gen_halfit"), st);
+      static const char *const names[TD_NKIND] = {"k_win_halfit",  "k_win_halfit",  "k_sse_halfit",
+                                                   "k_gen_halfit",  "k_win8_halfit", "k_win8_halfit"};
+      ProfScope ps(names[k], st);
       HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
     }
     return 0;

@@ -84,14 +84,45 @@ uint32_t auto_subblocks(uint32_t K) {
 }
 
 // impl actually run for (impl, K): turbodecoder.c:153-291, 467-489
+// turbodecoder.c:392-423 (AVX2 build): the int8 window decoders where K allows them, else the
+// 16-bit AUTO choice on the sign-extended input (tdec_iteration_8, :439-464)
+uint32_t auto_subblocks_8bit(uint32_t K) {
+  if (!(K % 32) && K > 2048) return 32;
+  if (!(K % 16) && K > 800) return 16;
+  if (!(K % 8) && K > 400) return 8;
+  return 0;
+}
+
 int resolve_impl(int impl, uint32_t K) {
+  if (impl == SRSGPU_TDEC_AUTO_8BIT) {
+    const uint32_t s = auto_subblocks_8bit(K);
+    if (s == 32) return SRSLTE_TDEC_AVX8_WINDOW;
+    if (s == 16) return SRSLTE_TDEC_SSE8_WINDOW;
+    impl = SRSLTE_TDEC_AUTO;
+  }
   if (impl == SRSLTE_TDEC_AUTO) {
     uint32_t nsb = auto_subblocks(K);
     return nsb == 16 ? SRSLTE_TDEC_AVX_WINDOW : nsb == 8 ? SRSLTE_TDEC_SSE_WINDOW : SRSLTE_TDEC_SSE;
   }
   return impl;
 }
-int impl_nb(int r) { return r == SRSLTE_TDEC_AVX_WINDOW ? 16 : r == SRSLTE_TDEC_SSE_WINDOW ? 8 : 1; }
+int impl_nb(int r) {
+  switch (r) {
+  case SRSLTE_TDEC_AVX8_WINDOW: return 32;
+  case SRSLTE_TDEC_AVX_WINDOW:
+  case SRSLTE_TDEC_SSE8_WINDOW: return 16;
+  case SRSLTE_TDEC_SSE_WINDOW: return 8;
+  default: return 1;
+  }
+}
+
+// turbodecoder_iter.h:31-47,91-108: the 16-bit decoders read sub-block input only when chosen by
+// AUTO (input_is_interleaved = current_dec > 0); the int8 ones always (input_is_interleaved 1)
+bool sb_input_for(int impl, int r) {
+  if (impl_nb(r) <= 1) return false;
+  return impl == SRSLTE_TDEC_AUTO || impl == SRSGPU_TDEC_AUTO_8BIT || r == SRSLTE_TDEC_SSE8_WINDOW ||
+         r == SRSLTE_TDEC_AVX8_WINDOW;
+}
 
 // QPP interleaver (TS 36.212 5.1.3.2.3) in the decoder's index space: natural for nb == 1, the
 // sub-block index k*nb+d <-> natural d*(K/nb)+k otherwise (tc_interl_lte.c:78-119).
@@ -119,6 +150,7 @@ using srsgpu::auto_subblocks;
 using srsgpu::cb_index;
 using srsgpu::impl_nb;
 using srsgpu::resolve_impl;
+using srsgpu::sb_input_for;
 typedef TdecEngine Engine;
 
 struct srsgpu_tdec_batch {
@@ -128,8 +160,7 @@ struct srsgpu_tdec_batch {
 extern "C" {
 
 uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t K) {
-  int r = resolve_impl(impl, K);
-  int sb = sb_layout && impl == SRSLTE_TDEC_AUTO && impl_nb(r) > 1;
+  const int sb = sb_layout && sb_input_for(impl, resolve_impl(impl, K));
   return sb ? 3 * (K + 32) + 12 : 3 * K + 12;
 }
 
@@ -255,6 +286,7 @@ int srsgpu_prof_get(const char *name, double *total_ms, uint64_t *count) {
 
 struct TdecGpu {
   Engine e;
+  std::vector<int16_t> conv; // int8 <-> int16 input conversion (the 8-bit entry points)
   int16_t *d_in = nullptr;
   uint8_t *d_out = nullptr;
   size_t in_len = 0;
@@ -267,7 +299,7 @@ int srslte_tdec_init(srslte_tdec_t *h, uint32_t max_long_cb) {
 int srslte_tdec_init_manual(srslte_tdec_t *h, uint32_t max_long_cb, srslte_tdec_impl_type_t dec_type) {
   if (!h) return -1;
   memset(h, 0, sizeof(*h));
-  if (dec_type > SRSLTE_TDEC_AVX_WINDOW) {
+  if (dec_type > SRSLTE_TDEC_AVX8_WINDOW) {
     fprintf(stderr, "Error decoder %d not supported\n", (int)dec_type);
     return -1;
   }
@@ -327,23 +359,19 @@ int srslte_tdec_get_nof_iterations(srslte_tdec_t *h) { return h->n_iter; }
 
 uint32_t srslte_tdec_autoimp_get_subblocks(uint32_t long_cb) { return auto_subblocks(long_cb); }
 
-// turbodecoder.c:392-406 (AVX2 build); the int8 decoders themselves are not provided
-uint32_t srslte_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb) {
-  if (!(long_cb % 32) && long_cb > 2048) return 32;
-  if (!(long_cb % 16) && long_cb > 800) return 16;
-  if (!(long_cb % 8) && long_cb > 400) return 8;
-  return 0;
-}
+// turbodecoder.c:392-406 (AVX2 build)
+uint32_t srslte_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb) { return srsgpu::auto_subblocks_8bit(long_cb); }
 
-static int tdec_gpu_halfit(srslte_tdec_t *h, int16_t *input) {
+// one half-iteration; at the first one the (int16) input of decoder `impl` is uploaded and loaded
+static int tdec_gpu_halfit(srslte_tdec_t *h, const int16_t *input, int impl) {
   auto *g = (TdecGpu *)h->gpu;
   Engine &e = g->e;
   const uint32_t K = h->current_long_cb;
   const int sb = !h->force_not_sb;
   if (h->n_iter == 0) {
-    const size_t len = srsgpu_tdec_input_len(h->dec_type, sb, K);
+    const size_t len = srsgpu_tdec_input_len(impl, sb, K);
     HIPCHK(hipMemcpyAsync(g->d_in, input, len * 2, hipMemcpyHostToDevice, e.st));
-    if (e.load(h->dec_type, sb, g->d_in, len, K, 1)) return -1;
+    if (e.load(impl, sb, g->d_in, len, K, 1)) return -1;
   }
   if (e.halfit(h->n_iter, false)) return -1;
   h->n_iter++;
@@ -360,9 +388,41 @@ static int tdec_gpu_decide(srslte_tdec_t *h, uint8_t *output) {
   return 0;
 }
 
+static bool is_int8_type(int t) { return t == SRSLTE_TDEC_SSE8_WINDOW || t == SRSLTE_TDEC_AVX8_WINDOW; }
+
+// 16-bit entry with a manual int8 window type (tdec_iteration_16, turbodecoder.c:491-503): the
+// input is truncated to int8 (convert_16_to_8); natural layout only — with sub-block input the
+// reference converts 3K+12 values of a 3(K+32)+12 layout
+static const int16_t *tdec_input16(srslte_tdec_t *h, int16_t *input) {
+  if (!is_int8_type(h->dec_type)) return input;
+  auto *g = (TdecGpu *)h->gpu;
+  if (!h->force_not_sb) {
+    fprintf(stderr, "srsgpu: int8 decoder type %d with 16-bit sub-block input is not defined by the "
+                    "reference (use srslte_tdec_force_not_sb)\n", (int)h->dec_type);
+    return nullptr;
+  }
+  const size_t n = 3 * (size_t)h->current_long_cb + 12;
+  g->conv.resize(n);
+  for (size_t i = 0; i < n; i++) g->conv[i] = (int8_t)input[i];
+  return g->conv.data();
+}
+
+// 8-bit entry (tdec_iteration_8, turbodecoder.c:439-464): int8 values sign-extended into the
+// engine's int16 lanes; AUTO becomes the 8-bit AUTO choice
+static const int16_t *tdec_input8(srslte_tdec_t *h, const int8_t *input, int *impl) {
+  auto *g = (TdecGpu *)h->gpu;
+  *impl = h->dec_type == SRSLTE_TDEC_AUTO ? SRSGPU_TDEC_AUTO_8BIT : (int)h->dec_type;
+  const size_t n = srsgpu_tdec_input_len(*impl, !h->force_not_sb, h->current_long_cb);
+  g->conv.resize(n);
+  for (size_t i = 0; i < n; i++) g->conv[i] = input[i];
+  return g->conv.data();
+}
+
 void srslte_tdec_iteration(srslte_tdec_t *h, int16_t *input, uint8_t *output) {
   if (h && h->gpu && h->current_cbidx >= 0) {
-    if (tdec_gpu_halfit(h, input) == 0) (void)tdec_gpu_decide(h, output);
+    const int16_t *in = h->n_iter == 0 ? tdec_input16(h, input) : input;
+    if (!in) return;
+    if (tdec_gpu_halfit(h, in, h->dec_type) == 0) (void)tdec_gpu_decide(h, output);
   }
 }
 
@@ -370,28 +430,32 @@ int srslte_tdec_run_all(srslte_tdec_t *h, int16_t *input, uint8_t *output, uint3
                         uint32_t long_cb) {
   if (!h || !h->gpu) return -1;
   if (srslte_tdec_new_cb(h, long_cb)) return -1;
+  const int16_t *in = tdec_input16(h, input);
+  if (!in) return -1;
   do {
-    if (tdec_gpu_halfit(h, input)) return -1;
+    if (tdec_gpu_halfit(h, in, h->dec_type)) return -1;
   } while (h->n_iter < (int)nof_iterations);
   return tdec_gpu_decide(h, output);
 }
 
 void srslte_tdec_iteration_8bit(srslte_tdec_t *h, int8_t *input, uint8_t *output) {
-  (void)h;
-  (void)input;
-  (void)output;
-  fprintf(stderr, "srsgpu: 8-bit turbo decoders are not provided (DESIGN.md)\n");
+  if (h && h->gpu && h->current_cbidx >= 0) {
+    int impl = 0;
+    const int16_t *in = tdec_input8(h, input, &impl);
+    if (tdec_gpu_halfit(h, in, impl) == 0) (void)tdec_gpu_decide(h, output);
+  }
 }
 
 int srslte_tdec_run_all_8bit(srslte_tdec_t *h, int8_t *input, uint8_t *output, uint32_t nof_iterations,
                              uint32_t long_cb) {
-  (void)h;
-  (void)input;
-  (void)output;
-  (void)nof_iterations;
-  (void)long_cb;
-  fprintf(stderr, "srsgpu: 8-bit turbo decoders are not provided (DESIGN.md)\n");
-  return -1;
+  if (!h || !h->gpu) return -1;
+  if (srslte_tdec_new_cb(h, long_cb)) return -1;
+  int impl = 0;
+  const int16_t *in = tdec_input8(h, input, &impl);
+  do {
+    if (tdec_gpu_halfit(h, in, impl)) return -1;
+  } while (h->n_iter < (int)nof_iterations);
+  return tdec_gpu_decide(h, output);
 }
 
 } // extern "C"

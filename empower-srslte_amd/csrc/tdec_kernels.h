@@ -14,8 +14,17 @@
 
 namespace srsgpu {
 
-// decoder variants, in the order groups are laid out in a job
-enum { TD_KIND_W16 = 0, TD_KIND_W8 = 1, TD_KIND_SSE = 2, TD_KIND_GEN = 3, TD_NKIND = 4 };
+// decoder variants, in the order groups are laid out in a job (B16 / B32: the int8 window
+// decoders of srslte_tdec_iteration_8bit, 16 / 32 sub-blocks)
+enum {
+  TD_KIND_W16 = 0,
+  TD_KIND_W8 = 1,
+  TD_KIND_SSE = 2,
+  TD_KIND_GEN = 3,
+  TD_KIND_B16 = 4,
+  TD_KIND_B32 = 5,
+  TD_NKIND = 6
+};
 
 struct TdGroup {
   int32_t K, nb, ncb, npairs; // nb: 16 / 8 windowed sub-blocks, 1 sequential
@@ -51,6 +60,7 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
 int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16);
 int halfit_blocks(int nb, int npairs);
 size_t seq_scratch_elems(int K, int npairs); // short2 elements
+size_t win8_scratch_elems(int K, int nb, int npairs); // short2 elements (int8 window betas)
 size_t bidir_lds_bytes(int K, int nb);
 int dec_words_host(int K, int nb);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n) of every group of one kind

@@ -854,6 +854,191 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ g
   }
 }
 
+// ------------------------------------------------------------------ int8 windows ----
+// The 8-bit window decoders (turbodecoder_win.h WINIMP sse8: 16 sub-blocks, avx8: 32), driven
+// by srslte_tdec_iteration_8bit (turbodecoder.c:439-464, turbodecoder_iter.h with LLR_IS_8BIT).
+// int8 values live in the packed int16 lanes; saturating int8 arithmetic is an exact int16 add
+// clamped to [-128, 127]. Reference semantics: "-INF" = 0, so every start state (known or
+// estimated) is all-zero; normalisation subtracts the maximum state after every step k != 0;
+// output (m1 - m0) >> 1; the tail trellis adds with MAKE_FUNC(sadd) (:196-203: clamps upwards,
+// wraps downwards). The half-iteration subtractions (srslte_vec_sub_bbb) saturate below
+// K & ~31 and wrap above (AVX2 vector body + scalar tail, vector_simd.c:165-191); the index that
+// decides is the reference's array index: j for DEC1's ext1 - app1, fwd[j] for DEC2's.
+// One lane = one sub-block chain of one pair, sequential beta pass (betas to scratch, coalesced
+// [step][state][lane]) then alpha pass; an opt-in path (srsUE pdsch_8bit_decoder), kept simple.
+__device__ __forceinline__ s2 b8(s2 v) {
+  return __builtin_elementwise_min(__builtin_elementwise_max(v, splat(-128)), splat(127));
+}
+__device__ __forceinline__ s2 badd(s2 a, s2 b) { return b8(wadd(a, b)); }
+__device__ __forceinline__ s2 bsub(s2 a, s2 b) { return b8(wsub(a, b)); }
+__device__ __forceinline__ short wrap8(int v) { return (short)(signed char)(unsigned char)(v & 255); }
+__device__ __forceinline__ short tail8(short a, short b) {
+  const int z = a + b;
+  return z > 127 ? (short)127 : wrap8(z);
+}
+__device__ __forceinline__ s2 tadd8(s2 a, s2 b) { return s2{tail8(a.x, b.x), tail8(a.y, b.y)}; }
+// ext - app with the reference's choice of saturation (sat) or wrap-around
+__device__ __forceinline__ s2 sub8sel(s2 a, s2 b, bool sat) {
+  return sat ? bsub(a, b) : s2{wrap8(a.x - b.x), wrap8(a.y - b.y)};
+}
+__device__ __forceinline__ void b_norm(int k, St8 &o) {
+  if (k != 0) {
+    s2 m = smax(smax(smax(o.s[0], o.s[1]), smax(o.s[2], o.s[3])),
+                smax(smax(o.s[4], o.s[5]), smax(o.s[6], o.s[7])));
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = bsub(o.s[i], m);
+  }
+}
+__device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
+  s2 xy = badd(x, y);
+  s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
+  s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
+  o.s[0] = smax(badd(b4, xy), b0);
+  o.s[1] = smax(b4, badd(b0, xy));
+  o.s[2] = smax(badd(b5, y), badd(b1, x));
+  o.s[3] = smax(badd(b5, x), badd(b1, y));
+  o.s[4] = smax(badd(b6, x), badd(b2, y));
+  o.s[5] = smax(badd(b6, y), badd(b2, x));
+  o.s[6] = smax(b7, badd(b3, xy));
+  o.s[7] = smax(badd(b7, xy), b3);
+}
+__device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb[8], s2 nw[8]) {
+  s2 xy = badd(x, y);
+  mb[0] = o.s[0];
+  mb[1] = badd(o.s[3], y);
+  mb[2] = badd(o.s[4], y);
+  mb[3] = o.s[7];
+  mb[4] = o.s[1];
+  mb[5] = badd(o.s[2], y);
+  mb[6] = badd(o.s[5], y);
+  mb[7] = o.s[6];
+  nw[0] = badd(o.s[1], xy);
+  nw[1] = badd(o.s[2], x);
+  nw[2] = badd(o.s[5], x);
+  nw[3] = badd(o.s[6], xy);
+  nw[4] = badd(o.s[0], xy);
+  nw[5] = badd(o.s[3], x);
+  nw[6] = badd(o.s[4], x);
+  nw[7] = badd(o.s[7], xy);
+}
+
+template <int NB, int MODE>
+__global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ groups, int ngroups,
+                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                    const s2 *__restrict__ T, size_t plane,
+                                                    s2 *__restrict__ scratch_base,
+                                                    const uint8_t *__restrict__ pair_done) {
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, npairs = G.npairs;
+  const int L = K / NB, K32 = K & ~31, G16 = (L + 15) / 16;
+  const int nlanes = npairs * NB;
+  const int g = (blockIdx.x - G.blk_half) * 64 + threadIdx.x;
+  if (g >= nlanes) return;
+  const int pair = g / NB, d = g - pair * NB;
+  if (pair_done && pair_done[G.pair0 + pair]) return;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
+  const s4 *sp0 = SP0 + base;
+  s2 *xp1 = XP1 + base;
+  const s2 *p1 = XP1 + plane + base;
+  s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
+  s2 *scratch = scratch_base + G.sc0;
+  auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * nlanes + g]; };
+  auto in = [&](int i, s2 &x, s2 &y) {
+    if (MODE == 1) {
+      x = xp1[i];
+      y = p1[i];
+    } else {
+      const s4 v = sp0[i];
+      x = MODE == 2 ? lo2(v) : badd(A[i], lo2(v));
+      y = hi2(v);
+    }
+  };
+  St8 o;
+  // ---- beta (win.h:310-435) ----
+  if (d == NB - 1) { // tail trellis (:263-307), start states all "-INF" = 0
+    const int xoff = MODE == 1 ? 6 : 0;
+    st_fill(o, 0, 0);
+#pragma unroll
+    for (int j = 2; j >= 0; j--) {
+      s2 x = tl[xoff + 2 * j], y = tl[xoff + 2 * j + 1], xy = tadd8(x, y);
+      s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
+      s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
+      o.s[0] = smax(tadd8(b4, xy), b0);
+      o.s[1] = smax(b4, tadd8(b0, xy));
+      o.s[2] = smax(tadd8(b5, y), tadd8(b1, x));
+      o.s[3] = smax(tadd8(b5, x), tadd8(b1, y));
+      o.s[4] = smax(tadd8(b6, x), tadd8(b2, y));
+      o.s[5] = smax(tadd8(b6, y), tadd8(b2, x));
+      o.s[6] = smax(b7, tadd8(b3, xy));
+      o.s[7] = smax(tadd8(b7, xy), b3);
+    }
+  } else { // estimate from the first 40 steps of sub-block d+1 (move_right)
+    st_fill(o, 0, 0);
+    for (int k = TD_OVERLAP - 1; k >= 0; k--) {
+      s2 x, y;
+      in(k * NB + d + 1, x, y);
+      b_beta_step(o, x, y);
+      b_norm(k, o);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) BE(L, i) = o.s[i];
+  for (int k = L - 1; k >= 0; k--) {
+    s2 x, y;
+    in(k * NB + d, x, y);
+    b_beta_step(o, x, y);
+#pragma unroll
+    for (int i = 0; i < 8; i++) BE(k, i) = o.s[i]; // stored before normalisation
+    b_norm(k, o);
+  }
+  // ---- alpha + output (win.h:438-586) ----
+  st_fill(o, 0, 0);
+  if (d > 0) { // estimate from the last 40 steps of sub-block d-1 (move_left)
+    for (int k = 0; k < TD_OVERLAP; k++) {
+      s2 x, y, mb[8], nw[8];
+      in((L - TD_OVERLAP + k) * NB + d - 1, x, y);
+      b_alpha_branches(o, x, y, mb, nw);
+#pragma unroll
+      for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+      b_norm(k, o);
+    }
+  }
+  uint32_t dacc = 0;
+  for (int k = 0; k < L; k++) {
+    const int idx = k * NB + d;
+    s2 x, y, mb[8], nw[8];
+    in(idx, x, y);
+    b_alpha_branches(o, x, y, mb, nw);
+    s2 m0 = badd(BE(k + 1, 0), mb[0]), m1 = badd(BE(k + 1, 0), nw[0]);
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      const s2 be = BE(k + 1, i);
+      m0 = smax(m0, badd(be, mb[i]));
+      m1 = smax(m1, badd(be, nw[i]));
+    }
+    const s2 llr = bsub(m1, m0) >> 1;
+    const int t = tbl[idx];
+    if (MODE == 1)
+      A[t] = sub8sel(llr, x, t < K32); // app1[fwd] = ext2 then app1 -= ext1 (x = app2 = ext1[fwd])
+    else
+      xp1[t] = sub8sel(llr, MODE == 2 ? splat(0) : A[idx], idx < K32); // ext1 -= app1, interleave
+    if (D) {
+      dacc |= dec_bits(llr) << (k & 15);
+      if ((k & 15) == 15 || k == L - 1) {
+        D[d * G16 + (k >> 4)] = dacc;
+        dacc = 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+    b_norm(k, o);
+  }
+}
+
 // ------------------------------------------------------------------ load ----
 // User layout -> SP0 / P1 / T. Natural input ([s,p0,p1]*K + 12 tail;
 // turbodecoder_gen.c:240-259, win.h:634-674) is transposed through LDS: a workgroup takes 64
@@ -1162,6 +1347,8 @@ int halfit_blocks(int nb, int npairs) { return nb > 1 ? (int)nblk((size_t)npairs
 
 size_t seq_scratch_elems(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs; }
 
+size_t win8_scratch_elems(int K, int nb, int npairs) { return (size_t)(K + nb) * 8 * npairs; }
+
 size_t bidir_lds_bytes(int K, int nb) {
   return (size_t)((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
 }
@@ -1188,7 +1375,8 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
       hipLaunchKernelGGL((k_load_nat<n, false>), dim3(nblocks), dim3(256), 0, st, dg, ng, in,       \
                          in_stride, rows, a);                                                      \
   } while (0)
-  if (nb == 16) LOADNAT(16);
+  if (nb == 32) LOADNAT(32);
+  else if (nb == 16) LOADNAT(16);
   else if (nb == 8) LOADNAT(8);
   else if (nb == 1) LOADNAT(1);
   else return hipErrorInvalidValue;
@@ -1217,6 +1405,10 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
   hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
                      (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
                      (s2 *)a.scratch, pair_done)
+#define SEQ8(nb, m)                                                                                \
+  hipLaunchKernelGGL((k_win8_halfit<nb, m>), dim3(nblocks), dim3(64), 0, st, dg, ng,                \
+                     (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T,   \
+                     a.plane, (s2 *)a.scratch, pair_done)
   switch (kind) {
   case TD_KIND_W16:
     if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
@@ -1230,9 +1422,18 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
   case TD_KIND_GEN:
     if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
     break;
+  case TD_KIND_B16:
+  case TD_KIND_B32:
+    if (kind == TD_KIND_B16) {
+      if (mode == 1) SEQ8(16, 1); else if (mode == 2) SEQ8(16, 2); else SEQ8(16, 0);
+    } else {
+      if (mode == 1) SEQ8(32, 1); else if (mode == 2) SEQ8(32, 2); else SEQ8(32, 0);
+    }
+    break;
   default:
     return hipErrorInvalidValue;
   }
+#undef SEQ8
 #undef SEQ
 #undef BIDIR
 #undef BIDIR1

@@ -21,6 +21,8 @@ LIB_PATH = os.environ.get("SRSGPU_LIB") or os.path.join(_HERE, "lib", "libsrsgpu
 SRSLTE_TDEC_AUTO, SRSLTE_TDEC_GENERIC, SRSLTE_TDEC_SSE = 0, 1, 2
 SRSLTE_TDEC_SSE_WINDOW, SRSLTE_TDEC_AVX_WINDOW = 3, 4
 SRSLTE_TDEC_SSE8_WINDOW, SRSLTE_TDEC_AVX8_WINDOW = 5, 6
+SRSGPU_TDEC_AUTO_8BIT = 16  # include/srsgpu/tdec_batch.h: the reference's 8-bit AUTO path
+SRSLTE_TDEC_SSE8_WINDOW, SRSLTE_TDEC_AVX8_WINDOW = 5, 6
 SRSLTE_SUCCESS, SRSLTE_ERROR = 0, -1
 CRC24A, CRC24B = 0x1864CFB, 0x1800063
 
@@ -40,6 +42,7 @@ if not os.path.exists(LIB_PATH):
 _lib = ctypes.CDLL(LIB_PATH)
 _vp, _sz, _u32, _i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
 _i16p = ctypes.POINTER(ctypes.c_int16)
+_i8p = ctypes.POINTER(ctypes.c_int8)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -104,8 +107,8 @@ _sig = {
     "srslte_tdec_autoimp_get_subblocks_8bit": (_u32, [_u32]),
     "srslte_tdec_iteration": (None, [_P, _i16p, _u8p]),
     "srslte_tdec_run_all": (_i32, [_P, _i16p, _u8p, _u32, _u32]),
-    "srslte_tdec_iteration_8bit": (None, [_P, ctypes.POINTER(ctypes.c_int8), _u8p]),
-    "srslte_tdec_run_all_8bit": (_i32, [_P, ctypes.POINTER(ctypes.c_int8), _u8p, _u32, _u32]),
+    "srslte_tdec_iteration_8bit": (None, [_P, _i8p, _u8p]),
+    "srslte_tdec_run_all_8bit": (_i32, [_P, _i8p, _u8p, _u32, _u32]),
     "srslte_tcod_init": (_i32, [_PC, _u32]),
     "srslte_tcod_free": (None, [_PC]),
     "srslte_tcod_encode": (_i32, [_PC, _u8p, _u8p, _u32]),
@@ -210,6 +213,13 @@ class Tdec:
 
     def run_all(self, inp, out, nof_iterations, K):
         return _lib.srslte_tdec_run_all(ctypes.byref(self.h), _i16(inp), _u8(out), nof_iterations, K)
+
+    def iteration_8bit(self, inp, out):
+        _lib.srslte_tdec_iteration_8bit(ctypes.byref(self.h), inp.ctypes.data_as(_i8p), _u8(out))
+
+    def run_all_8bit(self, inp, out, nof_iterations, K):
+        return _lib.srslte_tdec_run_all_8bit(ctypes.byref(self.h), inp.ctypes.data_as(_i8p), _u8(out),
+                                             nof_iterations, K)
 
     def get_nof_iterations(self):
         return _lib.srslte_tdec_get_nof_iterations(ctypes.byref(self.h))

@@ -32,6 +32,13 @@ extern "C" {
 
 typedef struct srsgpu_tdec_batch srsgpu_tdec_batch_t;
 
+/* impl value for the reference's 8-bit path (srslte_tdec_iteration_8bit, turbodecoder.c:392-464):
+ * int8 LLRs held in the int16 inputs (values in [-128, 127]); the SSE8 (16 sub-blocks) and AVX8
+ * (32 sub-blocks) int8 window decoders where K allows them, otherwise the 16-bit AUTO decoder.
+ * SRSLTE_TDEC_SSE8_WINDOW / _AVX8_WINDOW force one int8 decoder. Sub-block input layout
+ * applies whenever an int8 decoder runs. */
+#define SRSGPU_TDEC_AUTO_8BIT 16
+
 /* Allocates device buffers for up to max_cbs code blocks of up to max_long_cb bits. */
 int srsgpu_tdec_batch_create(srsgpu_tdec_batch_t **q, uint32_t max_cbs, uint32_t max_long_cb);
 void srsgpu_tdec_batch_destroy(srsgpu_tdec_batch_t *q);

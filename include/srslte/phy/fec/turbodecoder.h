@@ -9,10 +9,13 @@
  * force_not_sb, current_long_cb, current_cbidx, n_iter); the decoder state itself lives in
  * GPU memory behind `gpu`.
  *
- * Differences, all documented in DESIGN.md: the int8 decoders (SSE8/AVX8 windows,
- * *_8bit entry points) are not provided and return -1; the input buffer is read once per
- * code block (at the first half-iteration) and never written (the reference copies tail
- * values into the caller's padding).
+ * The *_8bit entry points and the int8 SSE8 / AVX8 window decoders follow turbodecoder.c:392-563
+ * bit-exactly. Differences, all documented in DESIGN.md: the input buffer is read once per code
+ * block (at the first half-iteration) and never written (the reference copies tail values into
+ * the caller's padding); where the reference's result is undefined (8-bit sub-block input at
+ * 400 < K <= 800, 16-bit sub-block input to a manual int8 type) the call fails with a message;
+ * the manual window types through the *_8bit entry points, which fault in the reference (no
+ * interleaver selected, turbodecoder.c:451-453), decode with the type's own interleaver.
  */
 #ifndef SRSLTE_TURBODECODER_H
 #define SRSLTE_TURBODECODER_H
