@@ -331,7 +331,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,c5",
+    ap.add_argument("--legs", default="c3,tm3,coded,c5,d8",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -434,9 +434,40 @@ def main():
                 "unit": "G wave-instructions/s", "frac": round(rate / peak, 4),
                 "int16_ops_per_s_T": round(rate * 128 / 1e12, 1),
                 "instr_per_launch": valu["valu_instr_per_launch"]}
+    legs = set() if args.no_pipeline else set(args.legs.split(","))
+    dec8 = None
+    if "d8" in legs:
+        # the reference's 8-bit path (srslte_tdec_iteration_8bit: AUTO -> int8 AVX8 window, 32
+        # sub-blocks at K = 6144) on the same code blocks, LLRs requantised to int8
+        d_in8 = torch.clamp(torch.div(d_in, 6, rounding_mode="trunc"), -128, 127).contiguous()
+
+        def step8():
+            if batch.run_dev(s.SRSGPU_TDEC_AUTO_8BIT, 0, d_in8.data_ptr(), stride, K, NCB, NHALF,
+                             d_out.data_ptr(), K // 8) != 0:
+                raise RuntimeError("srsgpu_tdec_batch_run_dev (8-bit) failed")
+
+        for _ in range(args.warmup):
+            step8()
+        torch.cuda.synchronize()
+        err8 = int(np.unpackbits(d_out.cpu().numpy() ^ expect).sum())
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        gc.disable()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step8()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el8 = time.perf_counter() - t0
+        gc.enable()
+        el8, err8 = reduce_over_ranks(dist, dev, el8, err8)
+        dec8 = {"decoder": "AUTO 8-bit (int8 AVX8 window, 32 sub-blocks)",
+                "mbps": round(decoded_mbps(max(1, world), NCB, K, args.steps, el8), 1),
+                "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
     batch.close()
     pipe = None
-    legs = set() if args.no_pipeline else set(args.legs.split(","))
     if "c3" in legs:
         pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2)
         if dist:
@@ -460,6 +491,8 @@ def main():
                 r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)
                 r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             extra[kind] = r
+    if rank == 0 and dec8:
+        result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
         result["config"]["subframes_per_s"] = pipe["subframes_per_s"]
         result["pipeline"] = pipe
