@@ -857,36 +857,40 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ g
 // ------------------------------------------------------------------ int8 windows ----
 // The 8-bit window decoders (turbodecoder_win.h WINIMP sse8: 16 sub-blocks, avx8: 32), driven
 // by srslte_tdec_iteration_8bit (turbodecoder.c:439-464, turbodecoder_iter.h with LLR_IS_8BIT).
-// int8 values live in the packed int16 lanes; saturating int8 arithmetic is an exact int16 add
-// clamped to [-128, 127]. Reference semantics: "-INF" = 0, so every start state (known or
-// estimated) is all-zero; normalisation subtracts the maximum state after every step k != 0;
-// output (m1 - m0) >> 1; the tail trellis adds with MAKE_FUNC(sadd) (:196-203: clamps upwards,
-// wraps downwards). The half-iteration subtractions (srslte_vec_sub_bbb) saturate below
-// K & ~31 and wrap above (AVX2 vector body + scalar tail, vector_simd.c:165-191); the index that
-// decides is the reference's array index: j for DEC1's ext1 - app1, fwd[j] for DEC2's.
-// One lane = one sub-block chain of one pair, sequential beta pass (betas to scratch, coalesced
-// [step][state][lane]) then alpha pass; an opt-in path (srsUE pdsch_8bit_decoder), kept simple.
-__device__ __forceinline__ s2 b8(s2 v) {
-  return __builtin_elementwise_min(__builtin_elementwise_max(v, splat(-128)), splat(127));
+// Reference semantics: "-INF" = 0, so every start state (known or estimated) is all-zero;
+// normalisation subtracts the maximum state after every step k != 0; output (m1 - m0) >> 1 per
+// byte; the tail trellis adds with MAKE_FUNC(sadd) (:196-203: clamps upwards, wraps downwards).
+// The half-iteration subtractions (srslte_vec_sub_bbb) saturate below K & ~31 and wrap above
+// (AVX2 vector body + scalar tail, vector_simd.c:165-191); the index that decides is the
+// reference's array index: j for DEC1's ext1 - app1, fwd[j] for DEC2's.
+//
+// Representation: an int8 value v is held as v << 8 in a packed int16 lane (two CBs per lane as
+// everywhere). Then the int16 saturating add clamps exactly at the int8 limits: the sum is exact
+// in range, clamps to -128 << 8 below, and to 0x7FFF above, which one AND with 0xFF00 turns into
+// 127 << 8 — two packed ops per saturating int8 add, max is one, wrap-around subtraction is the
+// plain int16 one, and a subtraction whose result cannot be positive (normalisation) needs no
+// mask. SP0 / P1 / T come from the shared loaders unscaled (shifted on load); A and X2, private
+// to the int8 decoders between half-iterations, stay scaled.
+// One lane = one sub-block chain of one pair: sequential beta pass, betas to scratch as the int8
+// bytes of 8 states x 2 CBs (one 16-byte store per step, [step][lane] coalesced), then the alpha
+// pass. An opt-in path (srsUE pdsch_8bit_decoder), kept simple.
+__device__ __forceinline__ s2 bmask(s2 v) {
+  return __builtin_bit_cast(s2, __builtin_bit_cast(uint32_t, v) & 0xFF00FF00u);
 }
-__device__ __forceinline__ s2 badd(s2 a, s2 b) { return b8(wadd(a, b)); }
-__device__ __forceinline__ s2 bsub(s2 a, s2 b) { return b8(wsub(a, b)); }
-__device__ __forceinline__ short wrap8(int v) { return (short)(signed char)(unsigned char)(v & 255); }
-__device__ __forceinline__ short tail8(short a, short b) {
+__device__ __forceinline__ s2 badd(s2 a, s2 b) { return bmask(sadd(a, b)); }
+__device__ __forceinline__ s2 bsub(s2 a, s2 b) { return bmask(ssub(a, b)); }
+__device__ __forceinline__ s2 bscale(s2 v) { return v << 8; }
+__device__ __forceinline__ short tail8(short a, short b) { // unscaled operands
   const int z = a + b;
-  return z > 127 ? (short)127 : wrap8(z);
+  return z > 127 ? (short)127 : (short)(signed char)(unsigned char)(z & 255);
 }
 __device__ __forceinline__ s2 tadd8(s2 a, s2 b) { return s2{tail8(a.x, b.x), tail8(a.y, b.y)}; }
-// ext - app with the reference's choice of saturation (sat) or wrap-around
-__device__ __forceinline__ s2 sub8sel(s2 a, s2 b, bool sat) {
-  return sat ? bsub(a, b) : s2{wrap8(a.x - b.x), wrap8(a.y - b.y)};
-}
 __device__ __forceinline__ void b_norm(int k, St8 &o) {
   if (k != 0) {
     s2 m = smax(smax(smax(o.s[0], o.s[1]), smax(o.s[2], o.s[3])),
                 smax(smax(o.s[4], o.s[5]), smax(o.s[6], o.s[7])));
 #pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = bsub(o.s[i], m);
+    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], m); // <= 0: only the lower clamp can act
   }
 }
 __device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
@@ -921,6 +925,22 @@ __device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb
   nw[6] = badd(o.s[4], x);
   nw[7] = badd(o.s[7], xy);
 }
+// 8 scaled states <-> 4 dwords of int8 bytes (v_perm_b32)
+__device__ __forceinline__ uint4 b_pack(const St8 &o) {
+  auto u = [&](int i) { return __builtin_bit_cast(uint32_t, o.s[i]); };
+  return make_uint4(__builtin_amdgcn_perm(u(1), u(0), 0x07050301u),
+                    __builtin_amdgcn_perm(u(3), u(2), 0x07050301u),
+                    __builtin_amdgcn_perm(u(5), u(4), 0x07050301u),
+                    __builtin_amdgcn_perm(u(7), u(6), 0x07050301u));
+}
+__device__ __forceinline__ void b_unpack(uint4 w, s2 be[8]) {
+  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    be[2 * j] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, v[j], 0x010C000Cu));
+    be[2 * j + 1] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, v[j], 0x030C020Cu));
+  }
+}
 
 template <int NB, int MODE>
 __global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ groups, int ngroups,
@@ -945,21 +965,20 @@ __global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ 
   uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
   const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  s2 *scratch = scratch_base + G.sc0;
-  auto BE = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * nlanes + g]; };
+  uint4 *BE = (uint4 *)(scratch_base + G.sc0) + g; // step k at BE[k * nlanes]
   auto in = [&](int i, s2 &x, s2 &y) {
     if (MODE == 1) {
       x = xp1[i];
-      y = p1[i];
+      y = bscale(p1[i]);
     } else {
       const s4 v = sp0[i];
-      x = MODE == 2 ? lo2(v) : badd(A[i], lo2(v));
-      y = hi2(v);
+      x = MODE == 2 ? bscale(lo2(v)) : badd(A[i], bscale(lo2(v)));
+      y = bscale(hi2(v));
     }
   };
   St8 o;
   // ---- beta (win.h:310-435) ----
-  if (d == NB - 1) { // tail trellis (:263-307), start states all "-INF" = 0
+  if (d == NB - 1) { // tail trellis (:263-307) on unscaled values, start states all "-INF" = 0
     const int xoff = MODE == 1 ? 6 : 0;
     st_fill(o, 0, 0);
 #pragma unroll
@@ -976,6 +995,8 @@ __global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ 
       o.s[6] = smax(b7, tadd8(b3, xy));
       o.s[7] = smax(tadd8(b7, xy), b3);
     }
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = bscale(o.s[i]);
   } else { // estimate from the first 40 steps of sub-block d+1 (move_right)
     st_fill(o, 0, 0);
     for (int k = TD_OVERLAP - 1; k >= 0; k--) {
@@ -985,14 +1006,12 @@ __global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ 
       b_norm(k, o);
     }
   }
-#pragma unroll
-  for (int i = 0; i < 8; i++) BE(L, i) = o.s[i];
+  BE[(size_t)L * nlanes] = b_pack(o);
   for (int k = L - 1; k >= 0; k--) {
     s2 x, y;
     in(k * NB + d, x, y);
     b_beta_step(o, x, y);
-#pragma unroll
-    for (int i = 0; i < 8; i++) BE(k, i) = o.s[i]; // stored before normalisation
+    BE[(size_t)k * nlanes] = b_pack(o); // stored before normalisation
     b_norm(k, o);
   }
   // ---- alpha + output (win.h:438-586) ----
@@ -1010,22 +1029,26 @@ __global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ 
   uint32_t dacc = 0;
   for (int k = 0; k < L; k++) {
     const int idx = k * NB + d;
-    s2 x, y, mb[8], nw[8];
+    s2 x, y, mb[8], nw[8], be[8];
     in(idx, x, y);
+    b_unpack(BE[(size_t)(k + 1) * nlanes], be);
     b_alpha_branches(o, x, y, mb, nw);
-    s2 m0 = badd(BE(k + 1, 0), mb[0]), m1 = badd(BE(k + 1, 0), nw[0]);
+    s2 m0 = badd(be[0], mb[0]), m1 = badd(be[0], nw[0]);
 #pragma unroll
     for (int i = 1; i < 8; i++) {
-      const s2 be = BE(k + 1, i);
-      m0 = smax(m0, badd(be, mb[i]));
-      m1 = smax(m1, badd(be, nw[i]));
+      m0 = smax(m0, badd(be[i], mb[i]));
+      m1 = smax(m1, badd(be[i], nw[i]));
     }
-    const s2 llr = bsub(m1, m0) >> 1;
+    const s2 llr = bmask(bsub(m1, m0) >> 1); // per-byte srai 1 (simd_rb_shift)
     const int t = tbl[idx];
-    if (MODE == 1)
-      A[t] = sub8sel(llr, x, t < K32); // app1[fwd] = ext2 then app1 -= ext1 (x = app2 = ext1[fwd])
-    else
-      xp1[t] = sub8sel(llr, MODE == 2 ? splat(0) : A[idx], idx < K32); // ext1 -= app1, interleave
+    if (MODE == 1) // app1[fwd] = ext2, then app1 -= ext1 (x = app2 = ext1 at fwd)
+      A[t] = t < K32 ? bsub(llr, x) : wsub(llr, x);
+    else if (MODE == 2) // ext1 interleaved into app2
+      xp1[t] = llr;
+    else { // ext1 -= app1, interleaved into app2
+      const s2 a = A[idx];
+      xp1[t] = idx < K32 ? bsub(llr, a) : wsub(llr, a);
+    }
     if (D) {
       dacc |= dec_bits(llr) << (k & 15);
       if ((k & 15) == 15 || k == L - 1) {
@@ -1347,7 +1370,7 @@ int halfit_blocks(int nb, int npairs) { return nb > 1 ? (int)nblk((size_t)npairs
 
 size_t seq_scratch_elems(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs; }
 
-size_t win8_scratch_elems(int K, int nb, int npairs) { return (size_t)(K + nb) * 8 * npairs; }
+size_t win8_scratch_elems(int K, int nb, int npairs) { return (size_t)(K + nb) * 4 * npairs; } // 16 B / lane / step
 
 size_t bidir_lds_bytes(int K, int nb) {
   return (size_t)((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
