@@ -435,8 +435,32 @@ def main():
                 "int16_ops_per_s_T": round(rate * 128 / 1e12, 1),
                 "instr_per_launch": valu["valu_instr_per_launch"]}
     legs = set() if args.no_pipeline else set(args.legs.split(","))
+    pipe = None
+    if "c3" in legs:
+        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2)
+        if dist:
+            ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
+            pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
+    pipe3 = None
+    if "tm3" in legs:
+        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3)
+        if dist:
+            ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
+            pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            pipe3["tb_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
+    extra = {}
+    for kind in ("c3_coded", "c5"):
+        if kind.split("_")[-1] in legs:
+            # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
+            r = run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind)
+            if dist:
+                ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
+                r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)
+                r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            extra[kind] = r
     dec8 = None
-    if "d8" in legs:
+    if "d8" in legs:  # last: the subframe legs above are timed as before
         # the reference's 8-bit path (srslte_tdec_iteration_8bit: AUTO -> int8 AVX8 window, 32
         # sub-blocks at K = 6144) on the same code blocks, LLRs requantised to int8
         d_in8 = torch.clamp(torch.div(d_in, 6, rounding_mode="trunc"), -128, 127).contiguous()
@@ -467,30 +491,6 @@ def main():
                 "mbps": round(decoded_mbps(max(1, world), NCB, K, args.steps, el8), 1),
                 "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
     batch.close()
-    pipe = None
-    if "c3" in legs:
-        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2)
-        if dist:
-            ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
-            pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
-    pipe3 = None
-    if "tm3" in legs:
-        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3)
-        if dist:
-            ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
-            pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe3["tb_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
-    extra = {}
-    for kind in ("c3_coded", "c5"):
-        if kind.split("_")[-1] in legs:
-            # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
-            r = run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind)
-            if dist:
-                ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
-                r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)
-                r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            extra[kind] = r
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
