@@ -360,9 +360,11 @@ struct TdecEngine {
   }
 
   // load the inputs of the planned groups; first: reset the per-CB flags of the whole job
-  // (total_cbs code blocks; init_done seeds cb_done: blocks already decoded are skipped, noi 0)
+  // (total_cbs code blocks; init_done seeds cb_done: blocks already decoded are skipped, noi 0).
+  // flags = false: a fixed-half-iteration job, which never reads the early-stop flags
   int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
-                   int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs) {
+                   int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs,
+                   bool flags = true) {
     // load launches: runs of groups with the same loader (nb, sb_input); rows_aligned is the
     // byte alignment every row is guaranteed to have (0: none)
     const size_t ng = groups.size();
@@ -376,10 +378,10 @@ struct TdecEngine {
       const TdGroup &f = groups[g0];
       bool vec = f.sb_input ? (rows ? rows_aligned >= 16
                                     : ((uintptr_t)d_in % 16 == 0 && (in_stride * 2) % 16 == 0))
-                            : (rows ? rows_aligned >= 4 : ((uintptr_t)d_in % 4 == 0 && in_stride % 2 == 0));
+                            : (rows ? rows_aligned >= 8 : ((uintptr_t)d_in % 8 == 0 && in_stride % 4 == 0));
       size_t g1 = g0;
       while (g1 < ng && groups[g1].nb == f.nb && groups[g1].sb_input == f.sb_input) {
-        if (!f.sb_input) vec = vec && (groups[g1].K / groups[g1].nb) % 2 == 0;
+        if (!f.sb_input) vec = vec && (groups[g1].K / groups[g1].nb) % 4 == 0;
         g1++;
       }
       int blocks = 0;
@@ -399,6 +401,7 @@ struct TdecEngine {
       HIPCHK(launch_load(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, f.nb, f.sb_input, r.vec, d_in,
                          in_stride, rows, a, st));
     }
+    if (!flags) return 0;
     if (first) {
       HIPCHK(hipMemsetAsync(cb_ok, 0, total_cbs, st));
       HIPCHK(hipMemsetAsync(noi, 0, (size_t)total_cbs * 4, st));
@@ -417,7 +420,8 @@ struct TdecEngine {
   // single-size job (batch API and the drop-in srslte_tdec_* path)
   int load(int impl, int sb_layout, const int16_t *d_in, size_t in_stride, uint32_t Kv, uint32_t n,
            const int16_t *const *rows = nullptr, int rows_aligned = 0,
-           const uint8_t *init_done = nullptr, uint32_t poly = 0, uint32_t crc_len = 0) {
+           const uint8_t *init_done = nullptr, uint32_t poly = 0, uint32_t crc_len = 0,
+           bool early_flags = false) {
     if (check_spec(impl, Kv, n)) return -1;
     if (!rows && in_stride < srsgpu_tdec_input_len(impl, sb_layout, Kv)) {
       fprintf(stderr, "srsgpu: input stride %zu too small\n", in_stride);
@@ -433,7 +437,7 @@ struct TdecEngine {
     fwd = groups[0].fwd;
     rev = groups[0].rev;
     dmap = groups[0].dmap;
-    return load_planned(d_in, in_stride, rows, rows_aligned, init_done, true, n);
+    return load_planned(d_in, in_stride, rows, rows_aligned, init_done, true, n, early_flags);
   }
 
   // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)

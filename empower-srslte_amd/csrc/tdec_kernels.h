@@ -51,7 +51,7 @@ struct TdArrays {
 
 // user input -> SP0 / P1 / T for groups [0, ng) of dg (all with the same nb and sb_input).
 // rows != NULL: code block c's input starts at rows[c], else at in + c * in_stride.
-// vec: natural rows may be read as dwords; sub-block rows as 16-byte vectors.
+// vec: natural rows may be read as 8-byte words; sub-block rows as 16-byte vectors.
 hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_input, bool vec,
                        const int16_t *in, size_t in_stride, const int16_t *const *rows,
                        const TdArrays &a, hipStream_t st);

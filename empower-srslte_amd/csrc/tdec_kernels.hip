@@ -1075,14 +1075,19 @@ __device__ __forceinline__ gptr_t<int16_t> cb_row(const int16_t *in, size_t stri
   return gptr(rows ? rows[c] : in + (size_t)c * stride);
 }
 // NB and the tile are compile-time so the run/offset arithmetic is shifts and multiplies; VEC
-// reads the natural runs as dwords (in, in_stride and L even).
+// reads the natural runs as 8-byte words (rows 8-byte aligned, L a multiple of 4).
 template <int NB, bool VEC>
 __global__ __launch_bounds__(256) void k_load_nat(const TdGroup *__restrict__ groups, int ngroups,
                                                   const int16_t *__restrict__ in, size_t in_stride,
                                                   const int16_t *const *__restrict__ rows,
                                                   TdArrays arr) {
+  // phase 1 copies each (CB, sub-block) run of 3 * LOAD_KT int16 into LDS as it lies (natural
+  // order, 8-byte accesses when VEC), rows padded to RS shorts (98 dwords: the phase-2 reads of
+  // 16 sub-blocks fall in distinct banks); phase 2 reads the triplets back in sub-block order
+  // and writes SP0 / P1 coalesced
   constexpr int RUN = 3 * LOAD_KT; // int16 per (CB, sub-block) run of one tile
-  __shared__ short lds[2][3][LOAD_KT * NB];
+  constexpr int RS = RUN + 4;
+  __shared__ __attribute__((aligned(16))) short lds[2][NB][RS];
   const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
   const int K = G.K, ncb = G.ncb, npairs = G.npairs;
   const int L = K / NB;
@@ -1094,28 +1099,22 @@ __global__ __launch_bounds__(256) void k_load_nat(const TdGroup *__restrict__ gr
   const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
   const int k0 = kt * LOAD_KT;
   const int kn = min(LOAD_KT, L - k0);
+  const int n3 = 3 * kn;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const gptr_t<int16_t> src = cb_row(in, in_stride, rows, h ? c1 : c0) + 3 * k0;
-    if (VEC) {
-      const gptr_t<uint32_t> s32 = (gptr_t<uint32_t>)src;
-      for (int w = threadIdx.x; w < NB * RUN / 2; w += 256) {
-        const int dd = w / (RUN / 2), r = 2 * (w - dd * (RUN / 2));
-        if (r < 3 * kn) {
-          const uint32_t v = s32[(dd * 3 * L) / 2 + r / 2];
-          const int kk = r / 3, sidx = r - 3 * kk;
-          lds[h][sidx][kk * NB + dd] = (short)(v & 0xffff);
-          const int r1 = r + 1, kk1 = r1 / 3, s1 = r1 - 3 * kk1;
-          lds[h][s1][kk1 * NB + dd] = (short)(v >> 16);
-        }
+    if (VEC) { // src, 3L and 3 k0 all multiples of 4 int16 (the launcher checks)
+      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+      constexpr int Q = RUN / 4; // 8-byte words per run
+      for (int w = threadIdx.x; w < NB * Q; w += 256) {
+        const int dd = w / Q, q = w - dd * Q;
+        if (4 * q < n3)
+          *(u2v *)&lds[h][dd][4 * q] = *(const __attribute__((address_space(1))) u2v *)(src + dd * 3 * L + 4 * q);
       }
     } else {
       for (int e = threadIdx.x; e < NB * RUN; e += 256) {
         const int dd = e / RUN, r = e - dd * RUN;
-        if (r < 3 * kn) {
-          const int kk = r / 3, sidx = r - 3 * kk;
-          lds[h][sidx][kk * NB + dd] = src[dd * 3 * L + r];
-        }
+        if (r < n3) lds[h][dd][r] = src[dd * 3 * L + r];
       }
     }
   }
@@ -1124,8 +1123,10 @@ __global__ __launch_bounds__(256) void k_load_nat(const TdGroup *__restrict__ gr
   const gmut_t<s2> P1 = gmut<s2>(arr.XP1) + arr.plane;
   const size_t base = (size_t)G.elem0 + (size_t)pair * K + (size_t)k0 * NB;
   for (int e = threadIdx.x; e < kn * NB; e += 256) {
-    SP0[base + e] = s4{lds[0][0][e], lds[1][0][e], lds[0][1][e], lds[1][1][e]};
-    P1[base + e] = s2{lds[0][2][e], lds[1][2][e]};
+    const int kk = e / NB, dd = e - kk * NB;
+    const short *a = &lds[0][dd][3 * kk], *b = &lds[1][dd][3 * kk];
+    SP0[base + e] = s4{a[0], b[0], a[1], b[1]};
+    P1[base + e] = s2{a[2], b[2]};
   }
   if (kt == 0 && threadIdx.x < 12) {
     const int t = threadIdx.x;
