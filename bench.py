@@ -164,7 +164,8 @@ STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "
 def stage_profile(s, torch, step, steps):
     """Per-stage device time per batch, from HIP events around every launch (srsgpu_prof_*), in
     a separate pass after the timed loop: creating and recording the events costs host time that
-    would otherwise show in the host-bound legs' wall clock."""
+    would otherwise show in the host-bound legs' wall clock. With several streams the spans of
+    concurrent launches overlap, so the stage sums then exceed the wall time per batch."""
     s.prof_reset()
     s.prof_enable(True)
     for _ in range(steps):
@@ -179,50 +180,61 @@ def stage_profile(s, torch, step, steps):
     return out
 
 
-def run_pipeline(s, torch, dev, steps, warmup, tm=1):
+def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
     """tm 1 — BASELINE configs[2]: one step = 1024 subframes through OFDM FFT -> CRS channel
     estimation -> PDSCH (RE extraction, MMSE, 64QAM demap, descramble) -> DL-SCH (de-RM, turbo
     decoding with CRC early stop up to 8 half-iterations, TB CRC) for TBS 75376 (13 x K=5824).
     tm 3 — the per-GPU shard of BASELINE configs[3]: 1024 TM3 subframes (2 CRS ports, 2 rx
-    antennas, CDD 2x2 MMSE, two MCS-28 TBs per subframe) through the same stages."""
+    antennas, CDD 2x2 MMSE, two MCS-28 TBs per subframe) through the same stages.
+    lanes: the batch is split over that many HIP streams, each with its own OFDM / estimator /
+    PDSCH handles (a worker per stream, as srsUE runs one phch_worker per subframe): one lane's
+    front end and small kernels fill the SIMDs the other lane's decoder leaves idle."""
     nrx = nports = 2 if tm == 3 else 1
     ntb = 2 if tm == 3 else 1
     rng = np.random.default_rng(99)
     N, x = pipeline_inputs(s, C3_SF, rng, nrx, nports)
-    stream = torch.cuda.current_stream(dev).cuda_stream
     gsz = 14 * 12 * C3_PRB
-    ngrid = C3_SF * nrx
-    ofdm = s.OfdmRx(C3_PRB, N, stream=stream)
-    chest = s.Chest(C3_PRB, C3_CELL, max_grids=ngrid, stream=stream, nof_ports=nports)
-    pd = s.Pdsch(C3_PRB, C3_CELL, nof_ports=nports, nof_rx_ant=nrx, nof_softbuffers=C3_SF * ntb,
-                 max_cb=13, max_sf=C3_SF, stream=stream)
+    nsf = C3_SF // lanes
+    ngrid = nsf * nrx
     d_x = torch.from_numpy(x.reshape(-1)).to(dev)
     del x
-    d_grid = torch.zeros(ngrid * gsz, dtype=torch.complex64, device=dev)
-    d_ce = torch.zeros(ngrid * nports * gsz, dtype=torch.complex64, device=dev)
-    d_noise = torch.zeros(ngrid * nports, dtype=torch.float32, device=dev)
     dlen = C3_TBS // 8 + 6
-    d_data = torch.zeros(C3_SF * ntb * dlen, dtype=torch.uint8, device=dev)
-    d_ret = torch.zeros(C3_SF * ntb, dtype=torch.int32, device=dev)
-    d_noi = torch.zeros(C3_SF * ntb, dtype=torch.int32, device=dev)
-    pd.set_noise_dev(d_noise.data_ptr())
-    sf_idx = [1 + (i % 4) for i in range(C3_SF)]  # subframes without PSS/SSS/PBCH
+    sf_idx = [1 + (i % 4) for i in range(nsf)]  # subframes without PSS/SSS/PBCH
     mimo = s.MIMO_CDD if tm == 3 else s.MIMO_SINGLE_ANTENNA
-    nre = pd.nof_re(s.make_sf(sf_idx=1, lstart=1, nof_prb=C3_PRB, mod=3))
-    sfs = [s.make_sf(sf_idx=sf_idx[i], lstart=1, nof_prb=C3_PRB, mod=(3, 3), nof_re=nre, rnti=1234,
-                     tbs=(C3_TBS, C3_TBS), softbuffer=(ntb * i, ntb * i + 1), mimo=mimo,
-                     grid_offset=i * nrx * gsz, ce_offset=i * nrx * nports * gsz,
-                     data_offset=(ntb * i * dlen, (ntb * i + 1) * dlen))
-           for i in range(C3_SF)]
-    grid_sf = [v for v in sf_idx for _ in range(nrx)]
-    sfs, grid_sf = s.make_sf_array(sfs), (ctypes.c_uint32 * len(grid_sf))(*grid_sf)  # built once
+    L = []
+    for li in range(lanes):
+        st = torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)
+        o = {"st": st, "x": d_x[li * ngrid * 15 * N:(li + 1) * ngrid * 15 * N]}
+        o["ofdm"] = s.OfdmRx(C3_PRB, N, stream=st.cuda_stream)
+        o["chest"] = s.Chest(C3_PRB, C3_CELL, max_grids=ngrid, stream=st.cuda_stream, nof_ports=nports)
+        o["pd"] = s.Pdsch(C3_PRB, C3_CELL, nof_ports=nports, nof_rx_ant=nrx, nof_softbuffers=nsf * ntb,
+                          max_cb=13, max_sf=nsf, stream=st.cuda_stream)
+        o["grid"] = torch.zeros(ngrid * gsz, dtype=torch.complex64, device=dev)
+        o["ce"] = torch.zeros(ngrid * nports * gsz, dtype=torch.complex64, device=dev)
+        o["noise"] = torch.zeros(ngrid * nports, dtype=torch.float32, device=dev)
+        o["data"] = torch.zeros(nsf * ntb * dlen, dtype=torch.uint8, device=dev)
+        o["ret"] = torch.zeros(nsf * ntb, dtype=torch.int32, device=dev)
+        o["noi"] = torch.zeros(nsf * ntb, dtype=torch.int32, device=dev)
+        o["pd"].set_noise_dev(o["noise"].data_ptr())
+        nre = o["pd"].nof_re(s.make_sf(sf_idx=1, lstart=1, nof_prb=C3_PRB, mod=3))
+        sfs = [s.make_sf(sf_idx=sf_idx[i], lstart=1, nof_prb=C3_PRB, mod=(3, 3), nof_re=nre, rnti=1234,
+                         tbs=(C3_TBS, C3_TBS), softbuffer=(ntb * i, ntb * i + 1), mimo=mimo,
+                         grid_offset=i * nrx * gsz, ce_offset=i * nrx * nports * gsz,
+                         data_offset=(ntb * i * dlen, (ntb * i + 1) * dlen))
+               for i in range(nsf)]
+        grid_sf = [v for v in sf_idx for _ in range(nrx)]
+        o["sfs"], o["grid_sf"] = s.make_sf_array(sfs), (ctypes.c_uint32 * len(grid_sf))(*grid_sf)  # built once
+        L.append(o)
+    torch.cuda.synchronize()
 
     def step():
-        pd.reset_softbuffer(0, C3_SF * ntb)  # new TBs: one softbuffer reset pass
-        assert ofdm.rx_dev(ngrid, d_x.data_ptr(), 15 * N, d_grid.data_ptr(), gsz) == 0
-        assert chest.estimate_dev(grid_sf, d_grid.data_ptr(), gsz, d_ce.data_ptr(), d_noise.data_ptr()) == 0
-        assert pd.decode_dev(sfs, d_grid.data_ptr(), d_ce.data_ptr(), gsz, d_data.data_ptr(), 8,
-                             d_ret.data_ptr(), d_noi.data_ptr()) == 0
+        for o in L:
+            o["pd"].reset_softbuffer(0, nsf * ntb)  # new TBs: one softbuffer reset pass
+            assert o["ofdm"].rx_dev(ngrid, o["x"].data_ptr(), 15 * N, o["grid"].data_ptr(), gsz) == 0
+            assert o["chest"].estimate_dev(o["grid_sf"], o["grid"].data_ptr(), gsz, o["ce"].data_ptr(),
+                                           o["noise"].data_ptr()) == 0
+            assert o["pd"].decode_dev(o["sfs"], o["grid"].data_ptr(), o["ce"].data_ptr(), gsz,
+                                      o["data"].data_ptr(), 8, o["ret"].data_ptr(), o["noi"].data_ptr()) == 0
 
     for _ in range(warmup):
         step()
@@ -235,56 +247,72 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1):
     el = time.perf_counter() - t0
     gc.enable()
     stages = stage_profile(s, torch, step, steps)
-    noi = d_noi.cpu().numpy()
-    for o in (ofdm, chest, pd):
-        o.close()
+    noi = np.concatenate([o["noi"].cpu().numpy() for o in L])
+    for o in L:
+        for k in ("ofdm", "chest", "pd"):
+            o[k].close()
     name = "c3_pdsch_pipeline" if tm == 1 else "c4_tm3_cdd2x2_pipeline"
     return {"workload": "%s_%dsf_20MHz_64QAM_%dx_tbs%d" % (name, C3_SF, ntb, C3_TBS),
             "subframes_per_s": round(C3_SF * steps / el, 1),
             "tb_mbps": round(C3_SF * ntb * steps * C3_TBS / el / 1e6, 1),
             "ms_per_batch": round(el / steps * 1e3, 3), "symbol_size": N, "rx_antennas": nrx,
-            "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
+            "streams": lanes, "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
             "data": "synthetic 64QAM symbols (not codewords: every CB runs 8 half-iterations)"}
 
 
-def run_traffic(s, torch, dev, steps, warmup, kind):
+def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes interleaved over cells of
       6/25/50/100 PRB, random allocation and MCS 0..28 (K 40..6144), all cells' TBs in one
-      DL-SCH call; AWGN at 20 dB.
+      DL-SCH call per stream; AWGN at 20 dB.
     kind "c3_coded" — the C3 subframe (100 PRB, MCS 28, TBS 75376) as real codewords at 30 dB
-      (the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst case."""
+      (the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst case.
+    lanes: the 1024 subframes are split over that many HIP streams (run_pipeline)."""
     import srsgpu_traffic as tr
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    if kind == "c5":
-        m = tr.MixedCells(table, C3_SF, torch, dev, seed=21, stream=stream, snr_db=20.0)
-    else:
-        m = tr.MixedCells(table, C3_SF, torch, dev, prbs=(100,), seed=22, stream=stream,
-                          snr_db=30.0, mcs=28, full_band=True)
+    ms = []
+    for li in range(lanes):
+        st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
+        n = C3_SF // lanes
+        if kind == "c5":
+            ms.append(tr.MixedCells(table, n, torch, dev, seed=21 + 100 * li, stream=st, snr_db=20.0))
+        else:
+            ms.append(tr.MixedCells(table, n, torch, dev, prbs=(100,), seed=22 + 100 * li, stream=st,
+                                    snr_db=30.0, mcs=28, full_band=True))
+    torch.cuda.synchronize()
+
+    def step():
+        for m in ms:
+            m.step()
+
     for _ in range(warmup):
-        m.step()
+        step()
     torch.cuda.synchronize()
     gc.disable()
     t0 = time.perf_counter()
     for _ in range(steps):
-        m.step()
+        step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     gc.enable()
-    stages = stage_profile(s, torch, m.step, steps)
-    acks, good, noi = m.check()
-    ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in m.tb_list})
+    stages = stage_profile(s, torch, step, steps)
+    chk = [m.check() for m in ms]
+    acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
+    noi = float(np.mean([c[2] for c in chk]))
+    tbl = [t for m in ms for t in m.tb_list]
+    ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in tbl})
+    bits = sum(m.bits for m in ms)
     out = {"workload": ("c5_mixed_bw_%dsf_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
                         "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS)),
            "subframes_per_s": round(C3_SF * steps / el, 1),
-           "tb_mbps": round(m.bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
-           "code_blocks": m.ncb, "distinct_K": len(ks), "K_range": [ks[0], ks[-1]],
-           "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": m.ntb, "nof_iterations_mean": noi,
-           "stage_ms_per_batch": stages,
+           "tb_mbps": round(bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+           "streams": lanes, "code_blocks": sum(m.ncb for m in ms), "distinct_K": len(ks),
+           "K_range": [ks[0], ks[-1]], "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": len(tbl),
+           "nof_iterations_mean": noi, "stage_ms_per_batch": stages,
            "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % ("20" if kind == "c5" else "30")}
-    m.close()
+    for m in ms:
+        m.close()
     return out
 
 
