@@ -309,9 +309,15 @@ int srslte_tdec_init_manual(srslte_tdec_t *h, uint32_t max_long_cb, srslte_tdec_
     delete g;
     return -1;
   }
+  // a stream of its own (non-blocking): null-stream launches carry HIP's implicit cross-stream
+  // synchronisation
   if (hipMalloc(&g->d_in, (3 * (max_long_cb + 32) + 12) * 2) != hipSuccess ||
-      hipMalloc(&g->d_out, max_long_cb / 8 + 1) != hipSuccess) {
+      hipMalloc(&g->d_out, max_long_cb / 8 + 1) != hipSuccess ||
+      hipStreamCreateWithFlags(&g->e.st, hipStreamNonBlocking) != hipSuccess) {
     fprintf(stderr, "srsgpu: device allocation failed\n");
+    if (g->d_in) (void)hipFree(g->d_in);
+    if (g->d_out) (void)hipFree(g->d_out);
+    g->e.st = nullptr;
     g->e.destroy();
     delete g;
     return -1;
@@ -331,6 +337,7 @@ void srslte_tdec_free(srslte_tdec_t *h) {
     if (g->d_in) (void)hipFree(g->d_in);
     if (g->d_out) (void)hipFree(g->d_out);
     g->e.destroy();
+    if (g->e.st) (void)hipStreamDestroy(g->e.st);
     delete g;
   }
   memset(h, 0, sizeof(*h));
