@@ -12,6 +12,8 @@ timeout -k 10 500 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 
 echo bench done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -T -d $O/trace -o kt -- python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1
 echo trace done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -T -d $O/trace_headline -o kt -- python3 bench.py --no-cpu-baseline --no-pipeline > $O/trace_headline.log 2>&1
+echo headline trace done
 bash tools/pmc_traffic.sh $TAG > $O/traffic.log 2>&1
 echo traffic done
 bash tools/pmc_dec.sh ${TAG}_sq > $O/sq.log 2>&1
