@@ -373,8 +373,9 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one rank per GPU over RCCL; SRSGPU_DIST_BACKEND=gloo rehearses several ranks on one card
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(os.environ.get("SRSGPU_DIST_BACKEND", "nccl"))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
