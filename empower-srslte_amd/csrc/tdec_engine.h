@@ -120,7 +120,7 @@ struct TdecEngine {
     cap_pairs = (max_cbs + 1) / 2 + EXTRA_PAIRS;
     cap_elems = (size_t)((max_cbs + 1) / 2) * max_K + EXTRA_PAIRS * std::min<uint32_t>(max_K, 1024);
     cap_dw = cap_elems / 16 + cap_pairs * 16;
-    cap_sc = (cap_elems + 32 * cap_pairs) * 8; // int8 windows: (K + 32) * 8 per pair
+    cap_sc = (cap_elems + 4 * cap_pairs) * 8;
     HIPCHK(hipMalloc(&SP0, cap_elems * 8));
     HIPCHK(hipMalloc(&XP1, cap_elems * 8));
     HIPCHK(hipMalloc(&A, cap_elems * 4));
@@ -312,7 +312,7 @@ struct TdecEngine {
       }
       g.blk_half = kind_blocks[kd];
       kind_blocks[kd] += halfit_blocks(nbv, g.npairs);
-      if (kd <= TD_KIND_W8) kind_lds[kd] = std::max(kind_lds[kd], bidir_lds_bytes(g.K, nbv));
+      if (nbv > 1) kind_lds[kd] = std::max(kind_lds[kd], bidir_lds_bytes(g.K, nbv));
       const Interl *it = get_interleaver(sp.K, (uint32_t)nbv);
       if (!it) return -1;
       g.fwd = it->fwd;
@@ -329,7 +329,6 @@ struct TdecEngine {
       elems += (size_t)g.npairs * sp.K;
       dw += (size_t)g.npairs * dec_words_host(g.K, nbv);
       if (nbv == 1) sc += seq_scratch_elems(g.K, g.npairs);
-      if (kd >= TD_KIND_B16) sc += win8_scratch_elems(g.K, nbv, g.npairs);
     }
     for (int k = TD_NKIND - 1; k >= 0; k--) kind_g0[k] = std::min(kind_g0[k], kind_g0[k + 1]);
     if ((size_t)pairs > cap_pairs || elems > cap_elems || dw > cap_dw || sc > cap_sc) return 1;
@@ -447,8 +446,8 @@ struct TdecEngine {
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      static const char *const names[TD_NKIND] = {"k_win_halfit",  "k_win_halfit",  "k_sse_halfit",
-                                                   "k_gen_halfit",  "k_win8_halfit", "k_win8_halfit"};
+      static const char *const names[TD_NKIND] = {"k_win_halfit", "k_win_halfit", "k_sse_halfit",
+                                                   "k_gen_halfit", "k_win8_halfit", "k_win8_halfit"};
       ProfScope ps(names[k], st);
       HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
     }

@@ -60,7 +60,6 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
 int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16);
 int halfit_blocks(int nb, int npairs);
 size_t seq_scratch_elems(int K, int npairs); // short2 elements
-size_t win8_scratch_elems(int K, int nb, int npairs); // short2 elements (int8 window betas)
 size_t bidir_lds_bytes(int K, int nb);
 int dec_words_host(int K, int nb);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n) of every group of one kind

@@ -182,6 +182,102 @@ __device__ __forceinline__ void st_fill(St8 &o, short v0, short v) {
   for (int i = 1; i < 8; i++) o.s[i] = splat(v);
 }
 
+// ------------------------------------------------------------------ int8 arithmetic ----
+// The 8-bit window decoders (turbodecoder_win.h WINIMP sse8: 16 sub-blocks, avx8: 32), driven
+// by srslte_tdec_iteration_8bit (turbodecoder.c:439-464, turbodecoder_iter.h with LLR_IS_8BIT),
+// run as k_win_bidir<..., B8 = true>. Reference semantics: "-INF" = 0, so every start state
+// (known or estimated) is all-zero; normalisation subtracts the maximum state after every step
+// k != 0; output (m1 - m0) >> 1 per byte; the tail trellis adds with MAKE_FUNC(sadd)
+// (:196-203: clamps upwards, wraps downwards). The half-iteration subtractions
+// (srslte_vec_sub_bbb) saturate below K & ~31 and wrap above (AVX2 vector body + scalar tail,
+// vector_simd.c:165-191); the index that decides is the reference's array index: j for DEC1's
+// ext1 - app1, fwd[j] for DEC2's.
+// Representation: an int8 value v is held as v << 8 in a packed int16 lane (two CBs per lane as
+// everywhere). Then the int16 saturating add clamps exactly at the int8 limits: the sum is exact
+// in range, clamps to -128 << 8 below, and to 0x7FFF above, which one AND with 0xFF00 turns into
+// 127 << 8 — two packed ops per saturating int8 add, max is one, wrap-around subtraction is the
+// plain int16 one, and a subtraction whose result cannot be positive (normalisation) needs no
+// mask. SP0 / P1 / T come from the shared loaders unscaled (shifted on load); A and X2, private
+// to the int8 decoders between half-iterations, stay scaled.
+__device__ __forceinline__ s2 bmask(s2 v) {
+  return __builtin_bit_cast(s2, __builtin_bit_cast(uint32_t, v) & 0xFF00FF00u);
+}
+__device__ __forceinline__ s2 badd(s2 a, s2 b) { return bmask(sadd(a, b)); }
+__device__ __forceinline__ s2 bsub(s2 a, s2 b) { return bmask(ssub(a, b)); }
+__device__ __forceinline__ s2 bscale(s2 v) { return v << 8; }
+__device__ __forceinline__ short tail8(short a, short b) { // unscaled operands
+  const int z = a + b;
+  return z > 127 ? (short)127 : (short)(signed char)(unsigned char)(z & 255);
+}
+__device__ __forceinline__ s2 tadd8(s2 a, s2 b) { return s2{tail8(a.x, b.x), tail8(a.y, b.y)}; }
+__device__ __forceinline__ void b_norm(int k, St8 &o) {
+  if (k != 0) {
+    s2 m = smax(smax(smax(o.s[0], o.s[1]), smax(o.s[2], o.s[3])),
+                smax(smax(o.s[4], o.s[5]), smax(o.s[6], o.s[7])));
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], m); // <= 0: only the lower clamp can act
+  }
+}
+__device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
+  s2 xy = badd(x, y);
+  s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
+  s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
+  o.s[0] = smax(badd(b4, xy), b0);
+  o.s[1] = smax(b4, badd(b0, xy));
+  o.s[2] = smax(badd(b5, y), badd(b1, x));
+  o.s[3] = smax(badd(b5, x), badd(b1, y));
+  o.s[4] = smax(badd(b6, x), badd(b2, y));
+  o.s[5] = smax(badd(b6, y), badd(b2, x));
+  o.s[6] = smax(b7, badd(b3, xy));
+  o.s[7] = smax(badd(b7, xy), b3);
+}
+__device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb[8], s2 nw[8]) {
+  s2 xy = badd(x, y);
+  mb[0] = o.s[0];
+  mb[1] = badd(o.s[3], y);
+  mb[2] = badd(o.s[4], y);
+  mb[3] = o.s[7];
+  mb[4] = o.s[1];
+  mb[5] = badd(o.s[2], y);
+  mb[6] = badd(o.s[5], y);
+  mb[7] = o.s[6];
+  nw[0] = badd(o.s[1], xy);
+  nw[1] = badd(o.s[2], x);
+  nw[2] = badd(o.s[5], x);
+  nw[3] = badd(o.s[6], xy);
+  nw[4] = badd(o.s[0], xy);
+  nw[5] = badd(o.s[3], x);
+  nw[6] = badd(o.s[4], x);
+  nw[7] = badd(o.s[7], xy);
+}
+// turbodecoder_win.h:263-307 with int8 sadd (unscaled tail values), states returned scaled
+__device__ __forceinline__ void b_tail_trellis(const s2 *tail, int xoff, St8 &o) {
+  st_fill(o, 0, 0);
+#pragma unroll
+  for (int j = 2; j >= 0; j--) {
+    s2 x = tail[xoff + 2 * j], y = tail[xoff + 2 * j + 1], xy = tadd8(x, y);
+    s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
+    s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
+    o.s[0] = smax(tadd8(b4, xy), b0);
+    o.s[1] = smax(b4, tadd8(b0, xy));
+    o.s[2] = smax(tadd8(b5, y), tadd8(b1, x));
+    o.s[3] = smax(tadd8(b5, x), tadd8(b1, y));
+    o.s[4] = smax(tadd8(b6, x), tadd8(b2, y));
+    o.s[5] = smax(tadd8(b6, y), tadd8(b2, x));
+    o.s[6] = smax(b7, tadd8(b3, xy));
+    o.s[7] = smax(tadd8(b7, xy), b3);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.s[i] = o.s[i] << 8;
+}
+// normalisation by the maximum state (int8 windows, every step k != 0)
+__device__ __forceinline__ void b_norm_max(St8 &o) {
+  s2 m = smax(smax(smax(o.s[0], o.s[1]), smax(o.s[2], o.s[3])),
+              smax(smax(o.s[4], o.s[5]), smax(o.s[6], o.s[7])));
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], m);
+}
+
 // ------------------------------------------------------------------ input policy ----
 // Per-step inputs of one constituent decoder run. DEC1: x = syst (+) A, y = par0, operand of
 // the output stage = A, scatter table = rev. DEC2: x = app2, y = par1, operand = app2, table =
@@ -207,6 +303,27 @@ __device__ __forceinline__ StepIn load_step(const s4 *__restrict__ sp0, const s2
     s2 a = MODE == 2 ? splat(0) : A[i];
     r.x = WRAP ? wadd(lo2(v), a) : sadd(a, lo2(v));
     r.y = hi2(v);
+    r.e = a;
+  }
+  return r;
+}
+
+// the same inputs for the int8 windows (B8): values scaled by 256, the a priori added with int8
+// saturation; X2 already holds scaled values
+template <int MODE, bool B8>
+__device__ __forceinline__ StepIn load_w(const s4 *__restrict__ sp0, const s2 *__restrict__ x2,
+                                         const s2 *__restrict__ p1, const s2 *__restrict__ A, int i) {
+  if (!B8) return load_step<MODE, false>(sp0, x2, p1, A, i);
+  StepIn r;
+  if (MODE == 1) {
+    r.x = x2[i];
+    r.y = bscale(p1[i]);
+    r.e = r.x;
+  } else {
+    s4 v = sp0[i];
+    s2 a = MODE == 2 ? splat(0) : A[i];
+    r.x = MODE == 2 ? bscale(lo2(v)) : badd(a, bscale(lo2(v)));
+    r.y = bscale(hi2(v));
     r.e = a;
   }
   return r;
@@ -272,7 +389,7 @@ __device__ unsigned long long td_times[2048 * 8];
 
 // The body of k_win_bidir: every pointer a __restrict__ parameter, so the scoped no-alias
 // facts survive inlining (the group tables would otherwise hide them from the scheduler).
-template <int NB, int DIV, int MODE, int CW, bool DOUT>
+template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
 __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *__restrict__ xp1,
                                                const s2 *__restrict__ p1, s2 *__restrict__ A,
                                                uint32_t *__restrict__ D, const s2 *__restrict__ tl,
@@ -282,6 +399,32 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
   const int nc = (L + CW - 1) / CW;
   const int qm = nc / 2; // meeting chunk: M = CW*qm
   const int tail_xoff = MODE == 1 ? 6 : 0;
+  const int K32 = K & ~31; // B8: srslte_vec_sub_bbb saturates below, wraps above (AVX2 body)
+  // arithmetic of the variant: 16-bit windows (saturating int16, state-0 normalisation every
+  // second step) or B8, the int8 windows (int8 saturation on scaled lanes, maximum-state
+  // normalisation after every step)
+  auto astep = [&](St8 &o, s2 x, s2 y) {
+    if (B8) {
+      s2 mb[8], nw[8];
+      b_alpha_branches(o, x, y, mb, nw);
+#pragma unroll
+      for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+    } else {
+      win_alpha_step(o, x, y);
+    }
+  };
+  auto bstep = [&](St8 &o, s2 x, s2 y) {
+    if (B8)
+      b_beta_step(o, x, y);
+    else
+      win_beta_step(o, x, y);
+  };
+  auto pnorm = [&](int k, St8 &o) { // prepass normalisation at step k
+    if (B8)
+      b_norm(k, o);
+    else
+      win_norm(k, o);
+  };
 
   auto ck_put = [&](int slot, const St8 &o) {
     s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
@@ -308,7 +451,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     const int i0 = k0 * NB + col;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
+      StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
       c.x[j] = s.x;
       c.y[j] = s.y;
     }
@@ -322,7 +465,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       const int i0 = CW * q * NB + d;
 #pragma unroll
       for (int j = 0; j < CW; j++) {
-        StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
+        StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
         c.x[j] = s.x;
         c.y[j] = s.y;
       }
@@ -330,7 +473,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
 #pragma unroll
       for (int j = 0; j < CW; j++) {
         int k = min(max(CW * q + j, 0), L - 1);
-        StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, k * NB + d);
+        StepIn s = load_w<MODE, B8>(sp0, xp1, p1, A, k * NB + d);
         c.x[j] = s.x;
         c.y[j] = s.y;
       }
@@ -341,7 +484,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       const int i0 = CW * q * NB + d;
 #pragma unroll
       for (int j = 0; j < CW; j++) {
-        StepIn s = load_step<MODE, false>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
+        StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
         c.x[j] = s.x;
         c.y[j] = s.y;
         c.e[j] = s.e;
@@ -352,7 +495,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       for (int j = 0; j < CW; j++) {
         int k = min(max(CW * q + j, 0), L - 1);
         int i = k * NB + d;
-        StepIn s = load_step<MODE, false>(sp0, xp1, p1, A, i);
+        StepIn s = load_w<MODE, B8>(sp0, xp1, p1, A, i);
         c.x[j] = s.x;
         c.y[j] = s.y;
         c.e[j] = s.e;
@@ -368,18 +511,36 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
   auto norm_op = [&](const St8 &o, int q, int j) -> s2 {
     return (j == 0 && q == 0) ? splat(0) : o.s[0];
   };
+  // alpha after step k = CW q + j
+  auto nrm_fwd = [&](St8 &o, int q, int j) {
+    if (B8) {
+      if (!(q == 0 && j == 0)) b_norm_max(o);
+    } else if ((j & 1) == 0) {
+      norm_by(o, norm_op(o, q, j));
+    }
+  };
+  // after a step k != 0 that is even when `even`
+  auto nrm_k = [&](St8 &o, bool even) {
+    if (B8)
+      b_norm_max(o);
+    else if (even)
+      norm_by(o, o.s[0]);
+  };
   // LLR at position k from alpha_k (al), the chunk's inputs and stored beta[k+1] (be)
   static_assert(CW == 16, "decision words hold 16 steps");
   const int G16 = (L + 15) / 16;
   auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, uint32_t &dacc,
-                     s2 mb[8], s2 nw[8]) {
-    win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
+                     s2 mb[8], s2 nw[8], int idx) {
+    if (B8)
+      b_alpha_branches(al, c.x[j], c.y[j], mb, nw);
+    else
+      win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
     // max over the 8 branches as a tree (max is exact, so any order is the reference's)
     s2 t0[8], t1[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      t0[i] = sadd(be.s[i], mb[i]);
-      t1[i] = sadd(be.s[i], nw[i]);
+      t0[i] = B8 ? badd(be.s[i], mb[i]) : sadd(be.s[i], mb[i]);
+      t1[i] = B8 ? badd(be.s[i], nw[i]) : sadd(be.s[i], nw[i]);
     }
 #pragma unroll
     for (int w = 4; w >= 1; w >>= 1)
@@ -388,9 +549,24 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         t0[i] = smax(t0[i], t0[i + w]);
         t1[i] = smax(t1[i], t1[i + w]);
       }
-    s2 v = ssub(t1[0], t0[0]);
-    if (DIV) v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
-    if (wr) store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
+    s2 v = B8 ? bsub(t1[0], t0[0]) : ssub(t1[0], t0[0]);
+    if (B8)
+      v = bmask(v >> 1); // per-byte srai 1 (simd_rb_shift)
+    else if (DIV)
+      v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
+    if (wr) {
+      if (B8) { // ext - app with the reference's saturate / wrap split (K32, see above)
+        const int t = c.t[j];
+        const bool sat = (MODE == 1 ? t : idx) < K32;
+        const s2 out = MODE == 2 ? v : (sat ? bsub(v, c.e[j]) : wsub(v, c.e[j]));
+        if (MODE == 1)
+          A[t] = out;
+        else
+          xp1[t] = out;
+      } else {
+        store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
+      }
+    }
     if (DOUT) dacc |= dec_bits(v) << j;
   };
 
@@ -401,7 +577,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       // win.h:501-506,512-584 (loop_len = 40) over the last 40 steps of sub-block d-1;
       // move_left (:469-495); sub-block 0 starts in state 0 (:496-500)
       const int dp = d > 0 ? d - 1 : 0;
-      st_fill(o, -TD_INF, -TD_INF);
+      st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
       ChunkW<8> c0, c1;
       load_x8(c0, dp, L - TD_OVERLAP);
 #pragma unroll
@@ -409,19 +585,19 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         if (q < 4) load_x8(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-          win_alpha_step(o, c0.x[j], c0.y[j]);
-          win_norm(8 * q + j, o);
+          astep(o, c0.x[j], c0.y[j]);
+          pnorm(8 * q + j, o);
         }
         if (q < 4) {
           if (q < 3) load_x8(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
 #pragma unroll
           for (int j = 0; j < 8; j++) {
-            win_alpha_step(o, c1.x[j], c1.y[j]);
-            win_norm(8 * (q + 1) + j, o);
+            astep(o, c1.x[j], c1.y[j]);
+            pnorm(8 * (q + 1) + j, o);
           }
         }
       }
-      if (d == 0) st_fill(o, 0, -TD_INF);
+      if (d == 0) st_fill(o, 0, B8 ? 0 : -TD_INF);
     }
     TD_T(1);
     // first half: chunks 0 .. qm-1, checkpoint the entering state of each
@@ -430,8 +606,8 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         ck_put(q, o);
 #pragma unroll
         for (int j = 0; j < CW; j++) {
-          win_alpha_step(o, c.x[j], c.y[j]);
-          if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+          astep(o, c.x[j], c.y[j]);
+          nrm_fwd(o, q, j);
         }
       };
       ChunkW<CW> c0, c1;
@@ -460,23 +636,23 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--)
           if (j == n - 1) bst[j] = run;
-        if (!last) norm_by(run, run.s[0]); // s1 = s0+CW < L: even, non-zero
+        if (!last) nrm_k(run, true); // s1 = s0+CW < L: even, non-zero
 #pragma unroll
         for (int j = CW - 2; j >= 0; j--) {
           if (j <= n - 2) {
-            win_beta_step(run, c.x[j + 1], c.y[j + 1]);
+            bstep(run, c.x[j + 1], c.y[j + 1]);
             bst[j] = run;
-            if (((j + 1) & 1) == 0) norm_by(run, run.s[0]); // k = s0+1+j >= 1
+            nrm_k(run, ((j + 1) & 1) == 0); // k = s0+1+j >= 1
           }
         }
 #pragma unroll
         for (int j = 0; j < CW; j++) {
           if (j < n) {
             s2 mb[8], nw[8];
-            llr_out(c, o, bst[j], j, dacc, mb, nw);
+            llr_out(c, o, bst[j], j, dacc, mb, nw, (s0 + j) * NB + d);
 #pragma unroll
             for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
-            if ((j & 1) == 0) norm_by(o, norm_op(o, q, j));
+            nrm_fwd(o, q, j);
           }
         }
         if (DOUT && wr) D[d * G16 + q] = dacc;
@@ -504,7 +680,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       // win.h:376-384,386-433 (loop_len = 40) over the first 40 steps of sub-block d+1;
       // move_right (:333-366); the last sub-block starts from the tail trellis (:350-355)
       const int dn = d + 1 < NB ? d + 1 : d;
-      st_fill(o, -TD_INF, -TD_INF);
+      st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
       ChunkW<8> c0, c1;
       load_x8(c0, dn, 32);
 #pragma unroll
@@ -512,20 +688,23 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         if (q > 0) load_x8(c1, dn, 8 * (q - 1));
 #pragma unroll
         for (int j = 7; j >= 0; j--) {
-          win_beta_step(o, c0.x[j], c0.y[j]);
-          win_norm(8 * q + j, o);
+          bstep(o, c0.x[j], c0.y[j]);
+          pnorm(8 * q + j, o);
         }
         if (q > 0) {
           if (q > 1) load_x8(c0, dn, 8 * (q - 2));
 #pragma unroll
           for (int j = 7; j >= 0; j--) {
-            win_beta_step(o, c1.x[j], c1.y[j]);
-            win_norm(8 * (q - 1) + j, o);
+            bstep(o, c1.x[j], c1.y[j]);
+            pnorm(8 * (q - 1) + j, o);
           }
         }
       }
       St8 t;
-      win_tail_trellis(tl, tail_xoff, t);
+      if (B8)
+        b_tail_trellis(tl, tail_xoff, t);
+      else
+        win_tail_trellis(tl, tail_xoff, t);
       if (d == NB - 1) o = t;
     }
     ck_put(nc, o); // beta[L] (win.h:372-374)
@@ -537,14 +716,14 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--) {
           if (j < n) {
-            win_beta_step(o, c.x[j], c.y[j]);
+            bstep(o, c.x[j], c.y[j]);
             if (j == 0) {
               if (keep)
                 bpre = o;
               else
                 ck_put(q, o);
             }
-            if ((j & 1) == 0) norm_by(o, o.s[0]);
+            nrm_k(o, (j & 1) == 0);
           }
         }
       };
@@ -580,17 +759,17 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
 #pragma unroll
         for (int j = 0; j < CW - 1; j++) {
           ast[j + 1] = ast[j];
-          win_alpha_step(ast[j + 1], c.x[j], c.y[j]);
-          if ((j & 1) == 0) norm_by(ast[j + 1], norm_op(ast[j + 1], q, j));
+          astep(ast[j + 1], c.x[j], c.y[j]);
+          nrm_fwd(ast[j + 1], q, j);
         }
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--) {
           s2 mb[8], nw[8];
-          llr_out(c, ast[j], bpre, j, dacc, mb, nw); // bpre = stored beta[k+1]
+          llr_out(c, ast[j], bpre, j, dacc, mb, nw, (CW * q + j) * NB + d); // bpre = stored beta[k+1]
           // running beta at k+1 (normalised when k+1 is even; k+1 >= 1), then beta[k]
           St8 run = bpre;
-          if (((j + 1) & 1) == 0) norm_by(run, run.s[0]);
-          win_beta_step(run, c.x[j], c.y[j]);
+          nrm_k(run, ((j + 1) & 1) == 0);
+          bstep(run, c.x[j], c.y[j]);
           bpre = run;
         }
         if (DOUT && wr) D[d * G16 + q] = dacc;
@@ -609,7 +788,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
   }
 }
 
-template <int NB, int DIV, int MODE, int CW, bool DOUT>
+template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
 __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
@@ -649,7 +828,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
   uint32_t *D = DOUT ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
   const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  win_bidir_body<NB, DIV, MODE, CW, DOUT>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, wr, role, lane);
+  win_bidir_body<NB, DIV, MODE, CW, DOUT, B8>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, wr, role, lane);
   TD_T(4);
 }
 
@@ -851,214 +1030,6 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ g
         dacc = 0;
       }
     }
-  }
-}
-
-// ------------------------------------------------------------------ int8 windows ----
-// The 8-bit window decoders (turbodecoder_win.h WINIMP sse8: 16 sub-blocks, avx8: 32), driven
-// by srslte_tdec_iteration_8bit (turbodecoder.c:439-464, turbodecoder_iter.h with LLR_IS_8BIT).
-// Reference semantics: "-INF" = 0, so every start state (known or estimated) is all-zero;
-// normalisation subtracts the maximum state after every step k != 0; output (m1 - m0) >> 1 per
-// byte; the tail trellis adds with MAKE_FUNC(sadd) (:196-203: clamps upwards, wraps downwards).
-// The half-iteration subtractions (srslte_vec_sub_bbb) saturate below K & ~31 and wrap above
-// (AVX2 vector body + scalar tail, vector_simd.c:165-191); the index that decides is the
-// reference's array index: j for DEC1's ext1 - app1, fwd[j] for DEC2's.
-//
-// Representation: an int8 value v is held as v << 8 in a packed int16 lane (two CBs per lane as
-// everywhere). Then the int16 saturating add clamps exactly at the int8 limits: the sum is exact
-// in range, clamps to -128 << 8 below, and to 0x7FFF above, which one AND with 0xFF00 turns into
-// 127 << 8 — two packed ops per saturating int8 add, max is one, wrap-around subtraction is the
-// plain int16 one, and a subtraction whose result cannot be positive (normalisation) needs no
-// mask. SP0 / P1 / T come from the shared loaders unscaled (shifted on load); A and X2, private
-// to the int8 decoders between half-iterations, stay scaled.
-// One lane = one sub-block chain of one pair: sequential beta pass, betas to scratch as the int8
-// bytes of 8 states x 2 CBs (one 16-byte store per step, [step][lane] coalesced), then the alpha
-// pass. An opt-in path (srsUE pdsch_8bit_decoder), kept simple.
-__device__ __forceinline__ s2 bmask(s2 v) {
-  return __builtin_bit_cast(s2, __builtin_bit_cast(uint32_t, v) & 0xFF00FF00u);
-}
-__device__ __forceinline__ s2 badd(s2 a, s2 b) { return bmask(sadd(a, b)); }
-__device__ __forceinline__ s2 bsub(s2 a, s2 b) { return bmask(ssub(a, b)); }
-__device__ __forceinline__ s2 bscale(s2 v) { return v << 8; }
-__device__ __forceinline__ short tail8(short a, short b) { // unscaled operands
-  const int z = a + b;
-  return z > 127 ? (short)127 : (short)(signed char)(unsigned char)(z & 255);
-}
-__device__ __forceinline__ s2 tadd8(s2 a, s2 b) { return s2{tail8(a.x, b.x), tail8(a.y, b.y)}; }
-__device__ __forceinline__ void b_norm(int k, St8 &o) {
-  if (k != 0) {
-    s2 m = smax(smax(smax(o.s[0], o.s[1]), smax(o.s[2], o.s[3])),
-                smax(smax(o.s[4], o.s[5]), smax(o.s[6], o.s[7])));
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], m); // <= 0: only the lower clamp can act
-  }
-}
-__device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
-  s2 xy = badd(x, y);
-  s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
-  s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
-  o.s[0] = smax(badd(b4, xy), b0);
-  o.s[1] = smax(b4, badd(b0, xy));
-  o.s[2] = smax(badd(b5, y), badd(b1, x));
-  o.s[3] = smax(badd(b5, x), badd(b1, y));
-  o.s[4] = smax(badd(b6, x), badd(b2, y));
-  o.s[5] = smax(badd(b6, y), badd(b2, x));
-  o.s[6] = smax(b7, badd(b3, xy));
-  o.s[7] = smax(badd(b7, xy), b3);
-}
-__device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb[8], s2 nw[8]) {
-  s2 xy = badd(x, y);
-  mb[0] = o.s[0];
-  mb[1] = badd(o.s[3], y);
-  mb[2] = badd(o.s[4], y);
-  mb[3] = o.s[7];
-  mb[4] = o.s[1];
-  mb[5] = badd(o.s[2], y);
-  mb[6] = badd(o.s[5], y);
-  mb[7] = o.s[6];
-  nw[0] = badd(o.s[1], xy);
-  nw[1] = badd(o.s[2], x);
-  nw[2] = badd(o.s[5], x);
-  nw[3] = badd(o.s[6], xy);
-  nw[4] = badd(o.s[0], xy);
-  nw[5] = badd(o.s[3], x);
-  nw[6] = badd(o.s[4], x);
-  nw[7] = badd(o.s[7], xy);
-}
-// 8 scaled states <-> 4 dwords of int8 bytes (v_perm_b32)
-__device__ __forceinline__ uint4 b_pack(const St8 &o) {
-  auto u = [&](int i) { return __builtin_bit_cast(uint32_t, o.s[i]); };
-  return make_uint4(__builtin_amdgcn_perm(u(1), u(0), 0x07050301u),
-                    __builtin_amdgcn_perm(u(3), u(2), 0x07050301u),
-                    __builtin_amdgcn_perm(u(5), u(4), 0x07050301u),
-                    __builtin_amdgcn_perm(u(7), u(6), 0x07050301u));
-}
-__device__ __forceinline__ void b_unpack(uint4 w, s2 be[8]) {
-  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int j = 0; j < 4; j++) {
-    be[2 * j] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, v[j], 0x010C000Cu));
-    be[2 * j + 1] = __builtin_bit_cast(s2, __builtin_amdgcn_perm(0u, v[j], 0x030C020Cu));
-  }
-}
-
-template <int NB, int MODE>
-__global__ __launch_bounds__(64) void k_win8_halfit(const TdGroup *__restrict__ groups, int ngroups,
-                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
-                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
-                                                    const s2 *__restrict__ T, size_t plane,
-                                                    s2 *__restrict__ scratch_base,
-                                                    const uint8_t *__restrict__ pair_done) {
-  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
-  const int K = G.K, npairs = G.npairs;
-  const int L = K / NB, K32 = K & ~31, G16 = (L + 15) / 16;
-  const int nlanes = npairs * NB;
-  const int g = (blockIdx.x - G.blk_half) * 64 + threadIdx.x;
-  if (g >= nlanes) return;
-  const int pair = g / NB, d = g - pair * NB;
-  if (pair_done && pair_done[G.pair0 + pair]) return;
-  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
-  const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;
-  const s2 *p1 = XP1 + plane + base;
-  s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
-  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
-  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  uint4 *BE = (uint4 *)(scratch_base + G.sc0) + g; // step k at BE[k * nlanes]
-  auto in = [&](int i, s2 &x, s2 &y) {
-    if (MODE == 1) {
-      x = xp1[i];
-      y = bscale(p1[i]);
-    } else {
-      const s4 v = sp0[i];
-      x = MODE == 2 ? bscale(lo2(v)) : badd(A[i], bscale(lo2(v)));
-      y = bscale(hi2(v));
-    }
-  };
-  St8 o;
-  // ---- beta (win.h:310-435) ----
-  if (d == NB - 1) { // tail trellis (:263-307) on unscaled values, start states all "-INF" = 0
-    const int xoff = MODE == 1 ? 6 : 0;
-    st_fill(o, 0, 0);
-#pragma unroll
-    for (int j = 2; j >= 0; j--) {
-      s2 x = tl[xoff + 2 * j], y = tl[xoff + 2 * j + 1], xy = tadd8(x, y);
-      s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
-      s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
-      o.s[0] = smax(tadd8(b4, xy), b0);
-      o.s[1] = smax(b4, tadd8(b0, xy));
-      o.s[2] = smax(tadd8(b5, y), tadd8(b1, x));
-      o.s[3] = smax(tadd8(b5, x), tadd8(b1, y));
-      o.s[4] = smax(tadd8(b6, x), tadd8(b2, y));
-      o.s[5] = smax(tadd8(b6, y), tadd8(b2, x));
-      o.s[6] = smax(b7, tadd8(b3, xy));
-      o.s[7] = smax(tadd8(b7, xy), b3);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = bscale(o.s[i]);
-  } else { // estimate from the first 40 steps of sub-block d+1 (move_right)
-    st_fill(o, 0, 0);
-    for (int k = TD_OVERLAP - 1; k >= 0; k--) {
-      s2 x, y;
-      in(k * NB + d + 1, x, y);
-      b_beta_step(o, x, y);
-      b_norm(k, o);
-    }
-  }
-  BE[(size_t)L * nlanes] = b_pack(o);
-  for (int k = L - 1; k >= 0; k--) {
-    s2 x, y;
-    in(k * NB + d, x, y);
-    b_beta_step(o, x, y);
-    BE[(size_t)k * nlanes] = b_pack(o); // stored before normalisation
-    b_norm(k, o);
-  }
-  // ---- alpha + output (win.h:438-586) ----
-  st_fill(o, 0, 0);
-  if (d > 0) { // estimate from the last 40 steps of sub-block d-1 (move_left)
-    for (int k = 0; k < TD_OVERLAP; k++) {
-      s2 x, y, mb[8], nw[8];
-      in((L - TD_OVERLAP + k) * NB + d - 1, x, y);
-      b_alpha_branches(o, x, y, mb, nw);
-#pragma unroll
-      for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
-      b_norm(k, o);
-    }
-  }
-  uint32_t dacc = 0;
-  for (int k = 0; k < L; k++) {
-    const int idx = k * NB + d;
-    s2 x, y, mb[8], nw[8], be[8];
-    in(idx, x, y);
-    b_unpack(BE[(size_t)(k + 1) * nlanes], be);
-    b_alpha_branches(o, x, y, mb, nw);
-    s2 m0 = badd(be[0], mb[0]), m1 = badd(be[0], nw[0]);
-#pragma unroll
-    for (int i = 1; i < 8; i++) {
-      m0 = smax(m0, badd(be[i], mb[i]));
-      m1 = smax(m1, badd(be[i], nw[i]));
-    }
-    const s2 llr = bmask(bsub(m1, m0) >> 1); // per-byte srai 1 (simd_rb_shift)
-    const int t = tbl[idx];
-    if (MODE == 1) // app1[fwd] = ext2, then app1 -= ext1 (x = app2 = ext1 at fwd)
-      A[t] = t < K32 ? bsub(llr, x) : wsub(llr, x);
-    else if (MODE == 2) // ext1 interleaved into app2
-      xp1[t] = llr;
-    else { // ext1 -= app1, interleaved into app2
-      const s2 a = A[idx];
-      xp1[t] = idx < K32 ? bsub(llr, a) : wsub(llr, a);
-    }
-    if (D) {
-      dacc |= dec_bits(llr) << (k & 15);
-      if ((k & 15) == 15 || k == L - 1) {
-        D[d * G16 + (k >> 4)] = dacc;
-        dacc = 0;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
-    b_norm(k, o);
   }
 }
 
@@ -1371,7 +1342,6 @@ int halfit_blocks(int nb, int npairs) { return nb > 1 ? (int)nblk((size_t)npairs
 
 size_t seq_scratch_elems(int K, int npairs) { return (size_t)(K + 4) * 8 * npairs; }
 
-size_t win8_scratch_elems(int K, int nb, int npairs) { return (size_t)(K + nb) * 4 * npairs; } // 16 B / lane / step
 
 size_t bidir_lds_bytes(int K, int nb) {
   return (size_t)((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
@@ -1414,25 +1384,25 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
   const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
   TdArrays a = arr;
   if (!dec) a.D = nullptr;
-#define BIDIR1(nb, div, m, dout)                                                                   \
+#define BIDIR1(nb, div, m, dout, b8)                                                               \
   do {                                                                                             \
-    allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout>));                     \
-    hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout>), dim3(nblocks), dim3(128),     \
+    allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>));                 \
+    hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>), dim3(nblocks), dim3(128), \
                        lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
                        (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done);                                             \
   } while (0)
 #define BIDIR(nb, div, m)                                                                          \
   do {                                                                                             \
-    if (dec) BIDIR1(nb, div, m, true); else BIDIR1(nb, div, m, false);                             \
+    if (dec) BIDIR1(nb, div, m, true, false); else BIDIR1(nb, div, m, false, false);               \
+  } while (0)
+#define BIDIR8(nb, m)                                                                              \
+  do {                                                                                             \
+    if (dec) BIDIR1(nb, 1, m, true, true); else BIDIR1(nb, 1, m, false, true);                     \
   } while (0)
 #define SEQ(kern, m)                                                                               \
   hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
                      (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
                      (s2 *)a.scratch, pair_done)
-#define SEQ8(nb, m)                                                                                \
-  hipLaunchKernelGGL((k_win8_halfit<nb, m>), dim3(nblocks), dim3(64), 0, st, dg, ng,                \
-                     (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T,   \
-                     a.plane, (s2 *)a.scratch, pair_done)
   switch (kind) {
   case TD_KIND_W16:
     if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
@@ -1449,16 +1419,16 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
   case TD_KIND_B16:
   case TD_KIND_B32:
     if (kind == TD_KIND_B16) {
-      if (mode == 1) SEQ8(16, 1); else if (mode == 2) SEQ8(16, 2); else SEQ8(16, 0);
+      if (mode == 1) BIDIR8(16, 1); else if (mode == 2) BIDIR8(16, 2); else BIDIR8(16, 0);
     } else {
-      if (mode == 1) SEQ8(32, 1); else if (mode == 2) SEQ8(32, 2); else SEQ8(32, 0);
+      if (mode == 1) BIDIR8(32, 1); else if (mode == 2) BIDIR8(32, 2); else BIDIR8(32, 0);
     }
     break;
   default:
     return hipErrorInvalidValue;
   }
-#undef SEQ8
 #undef SEQ
+#undef BIDIR8
 #undef BIDIR
 #undef BIDIR1
   return hipGetLastError();
