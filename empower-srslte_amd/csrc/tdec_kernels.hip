@@ -218,18 +218,20 @@ __device__ __forceinline__ void b_norm(int k, St8 &o) {
     for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], m); // <= 0: only the lower clamp can act
   }
 }
+// max(badd(a, b), badd(c, d)) == bmask(max(sadd(a, b), sadd(c, d))) for masked operands (bmask
+// is monotone and equals badd on each sum), so each new state is masked once
 __device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
   s2 xy = badd(x, y);
   s2 b0 = o.s[0], b1 = o.s[1], b2 = o.s[2], b3 = o.s[3];
   s2 b4 = o.s[4], b5 = o.s[5], b6 = o.s[6], b7 = o.s[7];
-  o.s[0] = smax(badd(b4, xy), b0);
-  o.s[1] = smax(b4, badd(b0, xy));
-  o.s[2] = smax(badd(b5, y), badd(b1, x));
-  o.s[3] = smax(badd(b5, x), badd(b1, y));
-  o.s[4] = smax(badd(b6, x), badd(b2, y));
-  o.s[5] = smax(badd(b6, y), badd(b2, x));
-  o.s[6] = smax(b7, badd(b3, xy));
-  o.s[7] = smax(badd(b7, xy), b3);
+  o.s[0] = bmask(smax(sadd(b4, xy), b0));
+  o.s[1] = bmask(smax(b4, sadd(b0, xy)));
+  o.s[2] = bmask(smax(sadd(b5, y), sadd(b1, x)));
+  o.s[3] = bmask(smax(sadd(b5, x), sadd(b1, y)));
+  o.s[4] = bmask(smax(sadd(b6, x), sadd(b2, y)));
+  o.s[5] = bmask(smax(sadd(b6, y), sadd(b2, x)));
+  o.s[6] = bmask(smax(b7, sadd(b3, xy)));
+  o.s[7] = bmask(smax(sadd(b7, xy), b3));
 }
 __device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb[8], s2 nw[8]) {
   s2 xy = badd(x, y);
@@ -539,8 +541,8 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     s2 t0[8], t1[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      t0[i] = B8 ? badd(be.s[i], mb[i]) : sadd(be.s[i], mb[i]);
-      t1[i] = B8 ? badd(be.s[i], nw[i]) : sadd(be.s[i], nw[i]);
+      t0[i] = sadd(be.s[i], mb[i]); // B8: masked once after the tree (bmask is monotone)
+      t1[i] = sadd(be.s[i], nw[i]);
     }
 #pragma unroll
     for (int w = 4; w >= 1; w >>= 1)
@@ -549,7 +551,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         t0[i] = smax(t0[i], t0[i + w]);
         t1[i] = smax(t1[i], t1[i + w]);
       }
-    s2 v = B8 ? bsub(t1[0], t0[0]) : ssub(t1[0], t0[0]);
+    s2 v = B8 ? bsub(bmask(t1[0]), bmask(t0[0])) : ssub(t1[0], t0[0]);
     if (B8)
       v = bmask(v >> 1); // per-byte srai 1 (simd_rb_shift)
     else if (DIV)
