@@ -233,24 +233,27 @@ __device__ __forceinline__ void b_beta_step(St8 &o, s2 x, s2 y) {
   o.s[6] = bmask(smax(b7, sadd(b3, xy)));
   o.s[7] = bmask(smax(sadd(b7, xy), b3));
 }
+// branch sums left unmasked: each is exact or saturated at 0x7FFF / -32768, and is only combined
+// with masked values (stored betas) before a max and one final mask (see b_beta_step), so every
+// result equals the all-masked computation
 __device__ __forceinline__ void b_alpha_branches(const St8 &o, s2 x, s2 y, s2 mb[8], s2 nw[8]) {
   s2 xy = badd(x, y);
   mb[0] = o.s[0];
-  mb[1] = badd(o.s[3], y);
-  mb[2] = badd(o.s[4], y);
+  mb[1] = sadd(o.s[3], y);
+  mb[2] = sadd(o.s[4], y);
   mb[3] = o.s[7];
   mb[4] = o.s[1];
-  mb[5] = badd(o.s[2], y);
-  mb[6] = badd(o.s[5], y);
+  mb[5] = sadd(o.s[2], y);
+  mb[6] = sadd(o.s[5], y);
   mb[7] = o.s[6];
-  nw[0] = badd(o.s[1], xy);
-  nw[1] = badd(o.s[2], x);
-  nw[2] = badd(o.s[5], x);
-  nw[3] = badd(o.s[6], xy);
-  nw[4] = badd(o.s[0], xy);
-  nw[5] = badd(o.s[3], x);
-  nw[6] = badd(o.s[4], x);
-  nw[7] = badd(o.s[7], xy);
+  nw[0] = sadd(o.s[1], xy);
+  nw[1] = sadd(o.s[2], x);
+  nw[2] = sadd(o.s[5], x);
+  nw[3] = sadd(o.s[6], xy);
+  nw[4] = sadd(o.s[0], xy);
+  nw[5] = sadd(o.s[3], x);
+  nw[6] = sadd(o.s[4], x);
+  nw[7] = sadd(o.s[7], xy);
 }
 // turbodecoder_win.h:263-307 with int8 sadd (unscaled tail values), states returned scaled
 __device__ __forceinline__ void b_tail_trellis(const s2 *tail, int xoff, St8 &o) {
@@ -410,7 +413,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       s2 mb[8], nw[8];
       b_alpha_branches(o, x, y, mb, nw);
 #pragma unroll
-      for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+      for (int i = 0; i < 8; i++) o.s[i] = bmask(smax(mb[i], nw[i]));
     } else {
       win_alpha_step(o, x, y);
     }
@@ -653,7 +656,7 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
             s2 mb[8], nw[8];
             llr_out(c, o, bst[j], j, dacc, mb, nw, (s0 + j) * NB + d);
 #pragma unroll
-            for (int i = 0; i < 8; i++) o.s[i] = smax(mb[i], nw[i]);
+            for (int i = 0; i < 8; i++) o.s[i] = B8 ? bmask(smax(mb[i], nw[i])) : smax(mb[i], nw[i]);
             nrm_fwd(o, q, j);
           }
         }
