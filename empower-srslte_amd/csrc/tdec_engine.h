@@ -118,7 +118,8 @@ struct TdecEngine {
     cap_cbs = max_cbs;
     cap_K = max_K;
     cap_pairs = (max_cbs + 1) / 2 + EXTRA_PAIRS;
-    cap_elems = (size_t)((max_cbs + 1) / 2) * max_K + EXTRA_PAIRS * std::min<uint32_t>(max_K, 1024);
+    // T4 regions pad a pair's K elements by at most 3 * 32 (t4_pair_elems)
+    cap_elems = (size_t)((max_cbs + 1) / 2) * (max_K + 96) + EXTRA_PAIRS * (std::min<uint32_t>(max_K, 1024) + 96);
     cap_dw = cap_elems / 16 + cap_pairs * 16;
     cap_sc = (cap_elems + 4 * cap_pairs) * 8;
     HIPCHK(hipMalloc(&SP0, cap_elems * 8));
@@ -172,11 +173,21 @@ struct TdecEngine {
         const uint32_t i = r[j];
         m[p] = (uint16_t)((i % nbv) * 16 * G16 + i / nbv);
       }
+      // device scatter tables: T16 layout, sub-block-index valued (tdec_kernels.h)
+      const uint32_t nt = (uint32_t)t16_table_elems((int)Kv, (int)nbv);
+      std::vector<uint16_t> f16(nt, 0), r16(nt, 0);
+      for (uint32_t d = 0; d < nbv; d++)
+        for (uint32_t k = 0; k < L; k++) {
+          const uint32_t e = ((k / 16) * nbv + d) * 16 + k % 16, i = k * nbv + d;
+          f16[e] = f[i];
+          r16[e] = r[i];
+        }
       Interl t{};
-      for (uint16_t **pp : {&t.fwd, &t.rev, &t.dmap})
-        if (hipMalloc(pp, Kv * 2) != hipSuccess) return nullptr;
-      if (hipMemcpy(t.fwd, f.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(t.rev, r.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      if (hipMalloc(&t.fwd, nt * 2) != hipSuccess || hipMalloc(&t.rev, nt * 2) != hipSuccess ||
+          hipMalloc(&t.dmap, Kv * 2) != hipSuccess)
+        return nullptr;
+      if (hipMemcpy(t.fwd, f16.data(), nt * 2, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(t.rev, r16.data(), nt * 2, hipMemcpyHostToDevice) != hipSuccess ||
           hipMemcpy(t.dmap, m.data(), Kv * 2, hipMemcpyHostToDevice) != hipSuccess)
         return nullptr;
       it = interl.emplace(key, t).first;
@@ -326,7 +337,7 @@ struct TdecEngine {
         if (!g.crc_pw || wc_table(sp.K, (uint32_t)nbv, sp.poly, sp.crc_len, it, g.wc)) return -1;
       }
       pairs += g.npairs;
-      elems += (size_t)g.npairs * sp.K;
+      elems += (size_t)g.npairs * t4_pair_elems(g.K, nbv);
       dw += (size_t)g.npairs * dec_words_host(g.K, nbv);
       if (nbv == 1) sc += seq_scratch_elems(g.K, g.npairs);
     }

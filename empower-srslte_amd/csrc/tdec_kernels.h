@@ -32,7 +32,7 @@ struct TdGroup {
                               // outputs, cb_done / cb_ok / noi)
   int32_t pair0;              // first pair (T, pair_done; monotonic over the group list)
   int32_t blk_load, blk_half; // first workgroup of the group in its load / half-iteration launch
-  int64_t elem0;              // first element of the group's [pair][K] arrays (SP0, X2, P1, A)
+  int64_t elem0;              // first element of the group's per-pair T4 regions (SP0, X2, P1, A)
   int64_t dw0;                // first packed decision word (D)
   int64_t sc0;                // first short2 of the sequential decoders' scratch
   const uint16_t *fwd, *rev, *dmap;
@@ -43,6 +43,21 @@ struct TdGroup {
   int32_t crc_bytes;          // CRC-checked prefix in bytes (0: no CRC)
   int32_t sb_input;           // input rows in rm_turbo's sub-block layout
 };
+
+// Decoder inputs SP0 and P1 (written by the loaders, read by every half-iteration) use the T4
+// layout: within a pair's region, step k of sub-block chain d sits at
+// ((k >> 2) * nb + d) * 4 + (k & 3). A chain's steps come in runs of 4 (16 bytes of short2, 32 of
+// short4), so one 16-byte load per lane covers 4 trellis steps. X2 and A, the targets of the
+// interleaver scatter, stay in sub-block order k * nb + d: one step's scatter from the nb chains
+// of a pair then lands on nb consecutive elements (QPP interleavers are contention-free), a
+// 64-byte store. For nb = 1 (sequential decoders) both are the natural index. Region size of a
+// pair (every array):
+__host__ __device__ inline int t4_pair_elems(int K, int nb) { return nb * 4 * ((K / nb + 3) / 4); }
+__host__ __device__ inline int t4_pos(int k, int d, int nb) { return ((k >> 2) * nb + d) * 4 + (k & 3); }
+// Interleaver tables (TdGroup::fwd / rev) are in T16 layout: entry (q * nb + d) * 16 + j holds,
+// for step k = 16 q + j of chain d (k < K / nb; padding 0), the sub-block index of its scatter
+// target; nb * 16 * ceil(K / nb / 16) entries.
+__host__ __device__ inline int t16_table_elems(int K, int nb) { return nb * 16 * ((K / nb + 15) / 16); }
 
 struct TdArrays {
   void *SP0, *XP1, *A, *D, *T, *scratch;

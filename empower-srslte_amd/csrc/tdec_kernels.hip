@@ -103,11 +103,13 @@ __device__ __forceinline__ int grp_find(const TdGroup *__restrict__ g, int ng, i
 // ------------------------------------------------------------------ windowed steps ----
 
 // turbodecoder_win.h:244-261 (16-bit): subtract state 0 every 2 steps, never at k == 0
+// (states 1..7 minus state 0, then state 0 = 0: a literal the next step folds away)
 __device__ __forceinline__ void win_norm(int k, St8 &o) {
   if ((k & 1) == 0 && k != 0) {
     s2 z = o.s[0];
 #pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], z);
+    for (int i = 1; i < 8; i++) o.s[i] = ssub(o.s[i], z);
+    o.s[0] = splat(0);
   }
 }
 
@@ -363,20 +365,67 @@ __device__ __forceinline__ uint32_t dec_bits(s2 llr) {
 __device__ __forceinline__ int dec_words(int K, int NB) { return NB * ((K / NB + 15) / 16); }
 
 // ------------------------------------------------------------------ windowed, bidirectional ----
-// Windowed decoder (turbodecoder_win.h), two waves per 64 sub-block chains: wave 0 runs the forward
-// (alpha) recursion, wave 1 the backward (beta) recursion, both starting at their end of the
-// sub-block and meeting at M (a multiple of CW near L/2). In its first half each wave only
-// recurses and checkpoints its metric every CW steps into LDS (alpha: entering state; beta: the
-// value the reference stores, before normalisation); after a workgroup barrier each wave emits
-// the LLRs of the other wave's first half, recomputing the other metric CW steps at a time from
-// those checkpoints. Every position is visited once per direction with the reference's
-// normalisation schedule, so all metrics are the reference's; the serial chain is half as long
-// and the checkpoints never touch HBM.
-template <int CW>
-struct ChunkW {
-  s2 x[CW], y[CW], e[CW];
-  int t[CW];
+// Windowed decoder (turbodecoder_win.h), two waves per 64 sub-block chains, both starting at
+// their end of the sub-block and meeting at M = 16*qm (qm = nc/2 of the nc 16-step chunks):
+//   phase 1  wave 0 runs the alpha recursion over chunks 0..qm-1, wave 1 the beta recursion over
+//            chunks nc-1..qm; each checkpoints its metric every 16 steps into LDS (alpha: the
+//            state entering the chunk; beta: the value the reference stores, before
+//            normalisation). One workgroup barrier.
+//   phase 2  both waves emit LLRs chunk by chunk, the same way: first the 16 betas of the chunk
+//            into registers (wave 0 recomputes them from wave 1's checkpoints, wave 1 continues
+//            its own recursion), then the alpha recursion over the chunk with the LLR of every
+//            step (wave 0 continues its alpha, wave 1 restarts it from wave 0's checkpoint). The
+//            LLR reuses the alpha step's branch sums, so a step of phase 2 costs one beta step and
+//            one alpha step plus the LLR, whichever wave runs it.
+// Every position is visited with the reference's normalisation schedule, and the integer
+// recursions are exact, so every metric equals the reference's. The serial chain is half as
+// long as the reference's, and the checkpoints never touch HBM.
+static_assert(TD_BIDIR_CW == 16, "phase-2 chunks and decision words hold 16 steps");
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s2 as_s2(uint32_t v) { return __builtin_bit_cast(s2, v); }
+
+// Raw inputs of one group (4 steps of one chain): MODE 1: s0 = X2 (app2), s1 = P1; MODE 0/2:
+// s0, s1 = SP0 of steps 0-1 / 2-3 (syst, par0 per step); MODE 0: a = A
+template <int MODE> struct Grp {
+  u4 s0, s1, a;
 };
+
+// x, y and the output operand e of step jj of a group (the input policy of turbodecoder_iter.h
+// and win.h:386-393,512-519: DEC1 x = syst (+) app1 saturating, DEC2 x = app2; B8: scaled lanes)
+template <int MODE, bool B8>
+__device__ __forceinline__ void grp_step(const Grp<MODE> &g, int jj, s2 &x, s2 &y, s2 &e) {
+  if (MODE == 1) {
+    x = as_s2(g.s0[jj]);
+    const s2 p = as_s2(g.s1[jj]);
+    y = B8 ? bscale(p) : p;
+    e = x;
+  } else {
+    const u4 &v = jj < 2 ? g.s0 : g.s1;
+    const s2 sy = as_s2(v[(jj & 1) * 2]), pa = as_s2(v[(jj & 1) * 2 + 1]);
+    const s2 a = MODE == 2 ? splat(0) : as_s2(g.a[jj]);
+    if (B8)
+      x = MODE == 2 ? bscale(sy) : badd(a, bscale(sy));
+    else
+      x = MODE == 2 ? sy : sadd(a, sy);
+    y = B8 ? bscale(pa) : pa;
+    e = a;
+  }
+}
+
+// a 16-step chunk: 4 groups and, in phase 2, the 16 scatter targets (T16 table words)
+template <int MODE> struct Chunk {
+  Grp<MODE> g[4];
+  u4 t[2];
+};
+// s_waitcnt vmcnt(0) as a builtin, which the compiler's wait insertion takes into account: a loop
+// entered with loads of its first operands still pending gets, at the loop-header merge, waits
+// sized for the first iteration in every iteration (there they wait for the previous chunk's
+// stores too)
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+template <int MODE> __device__ __forceinline__ int chunk_t(const Chunk<MODE> &c, int j) {
+  return (int)((c.t[j >> 3][(j & 7) >> 1] >> (16 * (j & 1))) & 0xffffu);
+}
 
 #ifdef TD_TIMING
 // debug build only (make timing): shader-clock stamps per wave of the bidirectional decoder
@@ -388,24 +437,41 @@ __device__ unsigned long long td_times[2048 * 8];
       if ((k) == 0 || (k) == 4) td_times[(blockIdx.x * 2 + role) * 8 + 5 + (k) / 4] = wall_clock64(); \
     }                                                                                              \
   } while (0)
+// finer stamps: per chunk of phase 1 (slot q) and per phase-2 chunk (start / betas done / LLRs
+// done at 32 + 3 i, i = the i-th chunk the wave emits)
+__device__ unsigned long long td_chunk[2048 * 80];
+#define TD_C(k)                                                                                    \
+  do {                                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024 && (k) < 80)                                  \
+      td_chunk[(blockIdx.x * 2 + role) * 80 + (k)] = clock64();                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                             \
+  } while (0)
 #else
 #define TD_T(k)
+#define TD_C(k)
 #endif
 
 // The body of k_win_bidir: every pointer a __restrict__ parameter, so the scoped no-alias
 // facts survive inlining (the group tables would otherwise hide them from the scheduler).
-template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
-__device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *__restrict__ xp1,
+// sp0 / p1 point at the pair's T4 regions, x2 / A at its sub-block-order ones, tbl at the group's
+// T16 table.
+template <int NB, int DIV, int MODE, bool DOUT, bool B8>
+__device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *__restrict__ x2,
                                                const s2 *__restrict__ p1, s2 *__restrict__ A,
                                                uint32_t *__restrict__ D, const s2 *__restrict__ tl,
                                                gptr_t<uint16_t> __restrict__ tbl, s4 *__restrict__ cks,
-                                               int K, int d, bool wr, int role, int lane) {
+                                               int K, int d, int role, int lane) {
+  constexpr int CW = 16;
   const int L = K / NB;
+  const int G4 = (L + 3) >> 2; // T4 groups per chain
   const int nc = (L + CW - 1) / CW;
   const int qm = nc / 2; // meeting chunk: M = CW*qm
   const int tail_xoff = MODE == 1 ? 6 : 0;
   const int K32 = K & ~31; // B8: srslte_vec_sub_bbb saturates below, wraps above (AVX2 body)
-  // arithmetic of the variant: 16-bit windows (saturating int16, state-0 normalisation every
+  const int G16 = (L + 15) / 16;
+
+  // ---- arithmetic of the variant: 16-bit windows (saturating int16, state-0 normalisation every
   // second step) or B8, the int8 windows (int8 saturation on scaled lanes, maximum-state
   // normalisation after every step)
   auto astep = [&](St8 &o, s2 x, s2 y) {
@@ -430,7 +496,34 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     else
       win_norm(k, o);
   };
+  // win.h:255-258: states 1..7 minus state 0, state 0 set to 0 (a literal, so the next step's
+  // operations on it fold away)
+  auto norm0 = [&](St8 &o) {
+    const s2 z = o.s[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++) o.s[i] = ssub(o.s[i], z);
+    o.s[0] = splat(0);
+  };
+  // alpha after step k = CW q + j (win.h:579: k even and k != 0; B8: every k != 0)
+  auto nrm_fwd = [&](St8 &o, int q, int j) {
+    if (B8) {
+      if (!(q == 0 && j == 0)) b_norm_max(o);
+    } else if ((j & 1) == 0) {
+      if (j != 0)
+        norm0(o);
+      else if (q != 0)
+        norm0(o);
+    }
+  };
+  // beta after a step k != 0 that is even when `even` (win.h:432)
+  auto nrm_k = [&](St8 &o, bool even) {
+    if (B8)
+      b_norm_max(o);
+    else if (even)
+      norm0(o);
+  };
 
+  // ---- checkpoints in LDS: [slot][half][lane] x 16 B (conflict-free b128 accesses)
   auto ck_put = [&](int slot, const St8 &o) {
     s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
     p[0] = s4{o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
@@ -452,276 +545,313 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     o.s[6] = lo2(e);
     o.s[7] = hi2(e);
   };
-  auto load_x8 = [&](ChunkW<8> &c, int col, int k0) { // prepass chunks (0 <= k0, k0 + 7 < L)
-    const int i0 = k0 * NB + col;
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
-      c.x[j] = s.x;
-      c.y[j] = s.y;
+
+  // ---- group loads: group g (steps 4g..4g+3) of chain dd. SP0 (T4) groups are 32 B (two u4),
+  // P1 (T4) 16 B; X2 and A in sub-block order.
+  const u4 *uS = reinterpret_cast<const u4 *>(sp0);
+  const uint32_t *wX = reinterpret_cast<const uint32_t *>(x2);
+  const u4 *uP = reinterpret_cast<const u4 *>(p1);
+  const uint32_t *wA = reinterpret_cast<const uint32_t *>(A);
+  // X2 / A (the scatter targets) are in sub-block order: 4 element loads per group
+  auto ld_sb4 = [&](const uint32_t *w, int g, int dd) {
+    const int i0 = 4 * g * NB + dd;
+    return u4{w[i0], w[i0 + NB], w[i0 + 2 * NB], w[i0 + 3 * NB]};
+  };
+  auto ld_grp = [&](Grp<MODE> &r, int g, int dd) {
+    const int o = g * NB + dd;
+    if (MODE == 1) {
+      r.s0 = ld_sb4(wX, g, dd);
+      r.s1 = uP[o];
+    } else {
+      r.s0 = uS[2 * o];
+      r.s1 = uS[2 * o + 1];
+      if (MODE == 0) r.a = ld_sb4(wA, g, dd);
     }
   };
-  // chunk loads: a full chunk addresses its 16 steps as one base + constant offsets (no
-  // per-step index arithmetic); the last, partial chunk and the backward wave's prefetch past
-  // the start (chunk -1, never used) clamp k to [0, L - 1]. Not for MODE 0 (DEC1 with A):
-  // there the compiler hoists the offset loads and runs out of registers (measured +30%).
-  auto load_xy = [&](ChunkW<CW> &c, int q) {
-    if (MODE != 0 && q >= 0 && CW * q + CW <= L) { // (the backward wave prefetches chunk -1)
-      const int i0 = CW * q * NB + d;
+  // chunk q of this lane's chain: groups 4q..4q+3 (clamped into the chain for the last, partial
+  // chunk: the recursion never reads its steps past L); tables only where phase 2 needs them
+  auto ld_chunk = [&](Chunk<MODE> &c, int q, bool with_t) {
+    const int g0 = 4 * q;
+    if (g0 + 4 <= G4) {
 #pragma unroll
-      for (int j = 0; j < CW; j++) {
-        StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
-        c.x[j] = s.x;
-        c.y[j] = s.y;
-      }
+      for (int u = 0; u < 4; u++) ld_grp(c.g[u], g0 + u, d);
     } else {
 #pragma unroll
-      for (int j = 0; j < CW; j++) {
-        int k = min(max(CW * q + j, 0), L - 1);
-        StepIn s = load_w<MODE, B8>(sp0, xp1, p1, A, k * NB + d);
-        c.x[j] = s.x;
-        c.y[j] = s.y;
+      for (int u = 0; u < 4; u++) ld_grp(c.g[u], min(g0 + u, G4 - 1), d);
+    }
+    if (with_t) {
+      const gptr_t<u4> ut = (gptr_t<u4>)tbl + (q * NB + d) * 2;
+      c.t[0] = ut[0];
+      c.t[1] = ut[1];
+    }
+    // keep the loads here, a chunk ahead of their use: left alone, the scheduler sinks them
+    // towards the first use to save registers, and the waves then wait on memory every chunk
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto cstep = [&](const Chunk<MODE> &c, int j, s2 &x, s2 &y, s2 &e) {
+    grp_step<MODE, B8>(c.g[j >> 2], j & 3, x, y, e);
+  };
+
+  // ---- phase 2 pieces, shared by both waves
+  // bst[j] = beta[s0+1+j] for j < n, from `top` = beta[s0+n] before normalisation (normalised
+  // first unless it is beta[L]); returns the running beta ready for step s0 (normalised when
+  // s0+1 is even... i.e. as the reference leaves it after beta[s0+1])
+  auto betas = [&](const Chunk<MODE> &c, St8 top, bool top_is_L, int n, St8 bst[CW]) -> St8 {
+    St8 run = top;
+#pragma unroll
+    for (int j = CW - 1; j >= 0; j--)
+      if (j == n - 1) bst[j] = run;
+    if (!top_is_L) nrm_k(run, true); // s0 + CW: even, non-zero
+#pragma unroll
+    for (int j = CW - 2; j >= 0; j--) {
+      if (j <= n - 2) {
+        s2 x, y, e;
+        cstep(c, j + 1, x, y, e);
+        bstep(run, x, y);
+        bst[j] = run;
+        nrm_k(run, ((j + 1) & 1) == 0); // k = s0+1+j >= 1
       }
     }
+    return run;
   };
-  auto load_full = [&](ChunkW<CW> &c, int q) {
-    if (MODE != 0 && q >= 0 && CW * q + CW <= L) { // (the backward wave prefetches chunk -1)
-      const int i0 = CW * q * NB + d;
+  // alpha recursion over the chunk's n steps from `o` = alpha[s0], with the LLR of every step
+  auto alpha_llr = [&](const Chunk<MODE> &c, St8 &o, const St8 bst[CW], int q, int n) {
+    const int s0 = CW * q;
+    uint32_t dacc = 0;
 #pragma unroll
-      for (int j = 0; j < CW; j++) {
-        StepIn s = load_w<MODE, B8>(sp0 + i0, xp1 + i0, p1 + i0, A + i0, j * NB);
-        c.x[j] = s.x;
-        c.y[j] = s.y;
-        c.e[j] = s.e;
-        c.t[j] = tbl[i0 + j * NB];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < CW; j++) {
-        int k = min(max(CW * q + j, 0), L - 1);
-        int i = k * NB + d;
-        StepIn s = load_w<MODE, B8>(sp0, xp1, p1, A, i);
-        c.x[j] = s.x;
-        c.y[j] = s.y;
-        c.e[j] = s.e;
-        c.t[j] = tbl[i];
-      }
-    }
-  };
-  auto norm_by = [&](St8 &o, s2 z) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) o.s[i] = ssub(o.s[i], z);
-  };
-  // normalisation operand at step k = CW*q + j, k even (win.h:244-261: never at k == 0)
-  auto norm_op = [&](const St8 &o, int q, int j) -> s2 {
-    return (j == 0 && q == 0) ? splat(0) : o.s[0];
-  };
-  // alpha after step k = CW q + j
-  auto nrm_fwd = [&](St8 &o, int q, int j) {
-    if (B8) {
-      if (!(q == 0 && j == 0)) b_norm_max(o);
-    } else if ((j & 1) == 0) {
-      norm_by(o, norm_op(o, q, j));
-    }
-  };
-  // after a step k != 0 that is even when `even`
-  auto nrm_k = [&](St8 &o, bool even) {
-    if (B8)
-      b_norm_max(o);
-    else if (even)
-      norm_by(o, o.s[0]);
-  };
-  // LLR at position k from alpha_k (al), the chunk's inputs and stored beta[k+1] (be)
-  static_assert(CW == 16, "decision words hold 16 steps");
-  const int G16 = (L + 15) / 16;
-  auto llr_out = [&](const ChunkW<CW> &c, const St8 &al, const St8 &be, int j, uint32_t &dacc,
-                     s2 mb[8], s2 nw[8], int idx) {
-    if (B8)
-      b_alpha_branches(al, c.x[j], c.y[j], mb, nw);
-    else
-      win_alpha_branches(al, c.x[j], c.y[j], mb, nw);
-    // max over the 8 branches as a tree (max is exact, so any order is the reference's)
-    s2 t0[8], t1[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      t0[i] = sadd(be.s[i], mb[i]); // B8: masked once after the tree (bmask is monotone)
-      t1[i] = sadd(be.s[i], nw[i]);
-    }
-#pragma unroll
-    for (int w = 4; w >= 1; w >>= 1)
-#pragma unroll
-      for (int i = 0; i < w; i++) {
-        t0[i] = smax(t0[i], t0[i + w]);
-        t1[i] = smax(t1[i], t1[i + w]);
-      }
-    s2 v = B8 ? bsub(bmask(t1[0]), bmask(t0[0])) : ssub(t1[0], t0[0]);
-    if (B8)
-      v = bmask(v >> 1); // per-byte srai 1 (simd_rb_shift)
-    else if (DIV)
-      v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
-    if (wr) {
-      if (B8) { // ext - app with the reference's saturate / wrap split (K32, see above)
-        const int t = c.t[j];
-        const bool sat = (MODE == 1 ? t : idx) < K32;
-        const s2 out = MODE == 2 ? v : (sat ? bsub(v, c.e[j]) : wsub(v, c.e[j]));
-        if (MODE == 1)
-          A[t] = out;
+    for (int j = 0; j < CW; j++) {
+      if (j < n) {
+        s2 x, y, e;
+        cstep(c, j, x, y, e);
+        s2 mb[8], nw[8];
+        if (B8)
+          b_alpha_branches(o, x, y, mb, nw);
         else
-          xp1[t] = out;
-      } else {
-        store_out<MODE == 1>(xp1, A, c.t[j], v, c.e[j]);
+          win_alpha_branches(o, x, y, mb, nw);
+        // max over the 8 branches as a tree (max is exact, so any order is the reference's)
+        const St8 &be = bst[j];
+        s2 t0[8], t1[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          t0[i] = sadd(be.s[i], mb[i]); // B8: masked once after the tree (bmask is monotone)
+          t1[i] = sadd(be.s[i], nw[i]);
+        }
+#pragma unroll
+        for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+          for (int i = 0; i < w; i++) {
+            t0[i] = smax(t0[i], t0[i + w]);
+            t1[i] = smax(t1[i], t1[i + w]);
+          }
+        s2 v = B8 ? bsub(bmask(t1[0]), bmask(t0[0])) : ssub(t1[0], t0[0]);
+        if (B8)
+          v = bmask(v >> 1); // per-byte srai 1 (simd_rb_shift)
+        else if (DIV)
+          v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
+        {
+          const int t = chunk_t(c, j); // sub-block index of the scatter target
+          if (B8) { // ext - app with the reference's saturate / wrap split (K32, see above)
+            // the reference's array index decides: j for DEC1, fwd[j] for DEC2
+            const bool sat = (MODE == 1 ? t : (s0 + j) * NB + d) < K32;
+            const s2 out = MODE == 2 ? v : (sat ? bsub(v, e) : wsub(v, e));
+            if (MODE == 1)
+              A[t] = out;
+            else
+              x2[t] = out;
+          } else {
+            store_out<MODE == 1>(x2, A, t, v, e);
+          }
+        }
+        if (DOUT) dacc |= dec_bits(v) << j;
+#pragma unroll
+        for (int i = 0; i < 8; i++) o.s[i] = B8 ? bmask(smax(mb[i], nw[i])) : smax(mb[i], nw[i]);
+        nrm_fwd(o, q, j);
       }
     }
-    if (DOUT) dacc |= dec_bits(v) << j;
+    if (DOUT) D[d * G16 + q] = dacc;
   };
 
   St8 o;
   if (role == 0) {
     // ================= forward wave =================
+    Chunk<MODE> c0, c1, c2; // phase 1's chunk buffers, the first two loading during the prepass
     {
       // win.h:501-506,512-584 (loop_len = 40) over the last 40 steps of sub-block d-1;
       // move_left (:469-495); sub-block 0 starts in state 0 (:496-500)
       const int dp = d > 0 ? d - 1 : 0;
       st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
-      ChunkW<8> c0, c1;
-      load_x8(c0, dp, L - TD_OVERLAP);
+      if ((L & 3) == 0) {
+        // ten T4 groups, all loads issued up front
+        Grp<MODE> pg[10];
+        const int gp = (L - TD_OVERLAP) >> 2;
 #pragma unroll
-      for (int q = 0; q < 5; q += 2) {
-        if (q < 4) load_x8(c1, dp, L - TD_OVERLAP + 8 * (q + 1));
+        for (int u = 0; u < 10; u++) ld_grp(pg[u], gp + u, dp);
+        ld_chunk(c0, 0, false);
+        ld_chunk(c1, min(1, qm - 1), false);
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-          astep(o, c0.x[j], c0.y[j]);
-          pnorm(8 * q + j, o);
+        for (int k = 0; k < TD_OVERLAP; k++) {
+          s2 x, y, e;
+          grp_step<MODE, B8>(pg[k >> 2], k & 3, x, y, e);
+          astep(o, x, y);
+          pnorm(k, o);
         }
-        if (q < 4) {
-          if (q < 3) load_x8(c0, dp, L - TD_OVERLAP + 8 * (q + 2));
+      } else {
+        // steps of one chain do not fill T4 groups evenly: element loads, 8 steps at a time
+        ld_chunk(c0, 0, false);
+        ld_chunk(c1, min(1, qm - 1), false);
+        for (int k0 = 0; k0 < TD_OVERLAP; k0 += 8) {
+          s2 xs[8], ys[8];
 #pragma unroll
-          for (int j = 0; j < 8; j++) {
-            astep(o, c1.x[j], c1.y[j]);
-            pnorm(8 * (q + 1) + j, o);
+          for (int u = 0; u < 8; u++) {
+            const int k = L - TD_OVERLAP + k0 + u;
+            const int pos = ((k >> 2) * NB + dp) * 4 + (k & 3), sb = k * NB + dp;
+            if (MODE == 1) {
+              xs[u] = x2[sb];
+              const s2 p = p1[pos];
+              ys[u] = B8 ? bscale(p) : p;
+            } else {
+              const s4 v = sp0[pos];
+              const s2 a = MODE == 2 ? splat(0) : A[sb];
+              if (B8)
+                xs[u] = MODE == 2 ? bscale(lo2(v)) : badd(a, bscale(lo2(v)));
+              else
+                xs[u] = MODE == 2 ? lo2(v) : sadd(a, lo2(v));
+              ys[u] = B8 ? bscale(hi2(v)) : hi2(v);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            astep(o, xs[u], ys[u]);
+            pnorm(k0 + u, o);
           }
         }
       }
       if (d == 0) st_fill(o, 0, B8 ? 0 : -TD_INF);
     }
     TD_T(1);
-    // first half: chunks 0 .. qm-1, checkpoint the entering state of each
+    // phase 1: chunks 0 .. qm-1, checkpoint the entering state of each; loads two chunks ahead
     {
-      auto fwd_chunk = [&](ChunkW<CW> &c, int q) {
+      auto fwd_chunk = [&](const Chunk<MODE> &c, int q) {
+        TD_C(q);
         ck_put(q, o);
 #pragma unroll
         for (int j = 0; j < CW; j++) {
-          astep(o, c.x[j], c.y[j]);
+          s2 x, y, e;
+          cstep(c, j, x, y, e);
+          astep(o, x, y);
           nrm_fwd(o, q, j);
         }
       };
-      ChunkW<CW> c0, c1;
       int q = 0;
-      load_xy(c0, 0);
-      for (; q + 1 < qm; q += 2) {
-        load_xy(c1, q + 1);
+      for (; q + 2 < qm; q += 3) {
+        ld_chunk(c2, q + 2, false);
         fwd_chunk(c0, q);
-        load_xy(c0, q + 2);
-        fwd_chunk(c1, q + 1);
+        ld_chunk(c0, min(q + 3, qm - 1), false); // unconditional: a load under a branch makes
+        fwd_chunk(c1, q + 1);                    // the vmcnt merge wait for the fresh loads
+        ld_chunk(c1, min(q + 4, qm - 1), false);
+        fwd_chunk(c2, q + 2);
       }
       if (q < qm) fwd_chunk(c0, q);
+      if (q + 1 < qm) fwd_chunk(c1, q + 1);
     }
+    Chunk<MODE> cur, cnx;
+    ld_chunk(cur, qm, true); // phase 2's first chunk, loading across the barrier
     TD_T(2);
     __syncthreads();
+    vm_drain();
     TD_T(3);
-    // second half: segments qm .. nc-1 with betas recomputed from the backward checkpoints
+    // phase 2: chunks qm .. nc-1, betas recomputed from the backward wave's checkpoints. One
+    // chunk per loop iteration (the next one loading meanwhile); the last chunk, when L is not a
+    // multiple of 16, after the loop.
     {
-      auto seg = [&](ChunkW<CW> &c, int q, bool last) {
-        const int s0 = CW * q;
-        const int n = last ? L - s0 : CW;
-        St8 bst[CW]; // bst[j] = stored beta[s0+1+j]
-        uint32_t dacc = 0;
-        St8 run;
-        ck_get(min(q + 1, nc), run);
-#pragma unroll
-        for (int j = CW - 1; j >= 0; j--)
-          if (j == n - 1) bst[j] = run;
-        if (!last) nrm_k(run, true); // s1 = s0+CW < L: even, non-zero
+      auto seg = [&](const Chunk<MODE> &c, int q) {
+        St8 top, bst[CW];
+        TD_C(32 + 3 * (q - qm));
+        ck_get(q + 1, top); // beta[CW(q+1)] (beta[L] when q + 1 == nc)
+        (void)betas(c, top, q == nc - 1, CW, bst);
+        TD_C(33 + 3 * (q - qm));
+        alpha_llr(c, o, bst, q, CW);
+        TD_C(34 + 3 * (q - qm));
+      };
+      const int qf = L / CW; // full chunks
+      for (int q = qm; q < qf; q++) {
+        ld_chunk(cnx, min(q + 1, nc - 1), true);
+        seg(cur, q);
+        cur = cnx;
+      }
+      if (qf < nc) {
+        // the partial chunk, n = L - CW qf steps (cur holds it): betas by selects, so every
+        // metric stays in a register whatever n is; the alpha / LLR steps under uniform guards
+        const int q = qf, n = L - CW * qf;
+        St8 top, bst[CW];
+        ck_get(nc, top); // beta[L], never normalised
+        St8 run = top;
+        bst[CW - 1] = top;
 #pragma unroll
         for (int j = CW - 2; j >= 0; j--) {
-          if (j <= n - 2) {
-            bstep(run, c.x[j + 1], c.y[j + 1]);
-            bst[j] = run;
-            nrm_k(run, ((j + 1) & 1) == 0); // k = s0+1+j >= 1
-          }
-        }
+          St8 nx = run; // beta[s0+2+j] once j + 1 <= n - 1
+          if (B8 || (j & 1) == 0) { // k = s0+2+j even (16-bit) / any (B8); not beta[L]
+            St8 nn = nx;
+            nrm_k(nn, true);
+            const bool is_top = j + 1 == n - 1;
 #pragma unroll
-        for (int j = 0; j < CW; j++) {
-          if (j < n) {
-            s2 mb[8], nw[8];
-            llr_out(c, o, bst[j], j, dacc, mb, nw, (s0 + j) * NB + d);
-#pragma unroll
-            for (int i = 0; i < 8; i++) o.s[i] = B8 ? bmask(smax(mb[i], nw[i])) : smax(mb[i], nw[i]);
-            nrm_fwd(o, q, j);
+            for (int i = 0; i < 8; i++) nx.s[i] = is_top ? nx.s[i] : nn.s[i];
           }
+          s2 x, y, e;
+          cstep(cur, j + 1, x, y, e);
+          bstep(nx, x, y);
+          const bool above = j >= n - 1;
+#pragma unroll
+          for (int i = 0; i < 8; i++) run.s[i] = above ? top.s[i] : nx.s[i];
+          bst[j] = run;
         }
-        if (DOUT && wr) D[d * G16 + q] = dacc;
-      };
-      ChunkW<CW> c0, c1;
-      int q = qm;
-      load_full(c0, q);
-      for (; q + 2 < nc; q += 2) {
-        load_full(c1, q + 1);
-        seg(c0, q, false);
-        load_full(c0, q + 2);
-        seg(c1, q + 1, false);
-      }
-      if (q == nc - 2) {
-        load_full(c1, q + 1);
-        seg(c0, q, false);
-        seg(c1, q + 1, true);
-      } else {
-        seg(c0, q, true);
+        alpha_llr(cur, o, bst, q, n);
       }
     }
   } else {
     // ================= backward wave =================
+    Chunk<MODE> c0, c1, c2; // phase 1's chunk buffers, the first two loading during the prepass
+    const int qt = nc - 1;  // top chunk, possibly partial; qm < qt (L > 40: nc >= 3)
     {
       // win.h:376-384,386-433 (loop_len = 40) over the first 40 steps of sub-block d+1;
       // move_right (:333-366); the last sub-block starts from the tail trellis (:350-355)
       const int dn = d + 1 < NB ? d + 1 : d;
       st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
-      ChunkW<8> c0, c1;
-      load_x8(c0, dn, 32);
+      Grp<MODE> pg[10];
 #pragma unroll
-      for (int q = 4; q >= 0; q -= 2) {
-        if (q > 0) load_x8(c1, dn, 8 * (q - 1));
+      for (int u = 0; u < 10; u++) ld_grp(pg[u], u, dn);
+      s2 tv[6]; // this decoder's tail values (x, y) x 3
 #pragma unroll
-        for (int j = 7; j >= 0; j--) {
-          bstep(o, c0.x[j], c0.y[j]);
-          pnorm(8 * q + j, o);
-        }
-        if (q > 0) {
-          if (q > 1) load_x8(c0, dn, 8 * (q - 2));
+      for (int u = 0; u < 6; u++) tv[u] = tl[tail_xoff + u];
+      ld_chunk(c0, qt, false);
+      ld_chunk(c1, qt - 1, false); // qt - 1 >= qm
 #pragma unroll
-          for (int j = 7; j >= 0; j--) {
-            bstep(o, c1.x[j], c1.y[j]);
-            pnorm(8 * (q - 1) + j, o);
-          }
-        }
+      for (int k = TD_OVERLAP - 1; k >= 0; k--) {
+        s2 x, y, e;
+        grp_step<MODE, B8>(pg[k >> 2], k & 3, x, y, e);
+        bstep(o, x, y);
+        pnorm(k, o);
       }
       St8 t;
       if (B8)
-        b_tail_trellis(tl, tail_xoff, t);
+        b_tail_trellis(tv, 0, t);
       else
-        win_tail_trellis(tl, tail_xoff, t);
+        win_tail_trellis(tv, 0, t);
       if (d == NB - 1) o = t;
     }
     ck_put(nc, o); // beta[L] (win.h:372-374)
     TD_T(1);
-    // first half: chunks nc-1 .. qm (steps L-1 .. M); bpre ends as beta[M] before normalisation
+    // phase 1: chunks nc-1 .. qm (steps L-1 .. M); bpre ends as beta[M] before normalisation
     St8 bpre;
     {
-      auto bwd_chunk = [&](ChunkW<CW> &c, int q, int n, bool keep) { // q > 0: norm never at 0
+      auto bwd_chunk = [&](const Chunk<MODE> &c, int q, int n, bool keep) { // q > 0: norm never at 0
+        TD_C(nc - 1 - q);
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--) {
           if (j < n) {
-            bstep(o, c.x[j], c.y[j]);
+            s2 x, y, e;
+            cstep(c, j, x, y, e);
+            bstep(o, x, y);
             if (j == 0) {
               if (keep)
                 bpre = o;
@@ -732,63 +862,51 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
           }
         }
       };
-      ChunkW<CW> c0, c1;
-      const int qt = nc - 1; // top chunk, possibly partial; qt > qm
-      load_xy(c0, qt);
-      load_xy(c1, qt - 1);
+      ld_chunk(c2, max(qt - 2, qm), false);
       bwd_chunk(c0, qt, L - CW * qt, false);
-      int q = qt - 1; // in c1
-      for (; q - 1 > qm; q -= 2) {
-        load_xy(c0, q - 1);
+      // then full chunks q, q-1, q-2 in c1, c2, c0 (rotating), down to qm; loads two ahead
+      int q = qt - 1;
+      for (; q - 2 >= qm; q -= 3) {
+        ld_chunk(c0, q - 2, false);
         bwd_chunk(c1, q, CW, false);
-        load_xy(c1, q - 2);
-        bwd_chunk(c0, q - 1, CW, false);
+        ld_chunk(c1, max(q - 3, qm), false);
+        bwd_chunk(c2, q - 1, CW, false);
+        ld_chunk(c2, max(q - 4, qm), false);
+        bwd_chunk(c0, q - 2, CW, q - 2 == qm);
       }
-      if (q > qm) {
-        load_xy(c0, q - 1);
-        bwd_chunk(c1, q, CW, false);
-        bwd_chunk(c0, qm, CW, true);
-      } else {
-        bwd_chunk(c1, qm, CW, true);
-      }
+      if (q >= qm) bwd_chunk(c1, q, CW, q == qm);
+      if (q - 1 >= qm) bwd_chunk(c2, q - 1, CW, q - 1 == qm);
     }
+    Chunk<MODE> cur, cnx;
+    ld_chunk(cur, qm - 1, true); // phase 2's first chunk, loading across the barrier
     TD_T(2);
     __syncthreads();
+    vm_drain();
     TD_T(3);
-    // second half: segments qm-1 .. 0 (full), alphas recomputed from the forward checkpoints
+    // phase 2: chunks qm-1 .. 0 (full), one per loop iteration: the beta recursion continues,
+    // alphas restart from the forward wave's checkpoints
     {
-      auto seg = [&](ChunkW<CW> &c, int q) {
-        St8 ast[CW]; // ast[j] = alpha entering step CW*q+j
-        uint32_t dacc = 0;
-        ck_get(q, ast[0]);
-#pragma unroll
-        for (int j = 0; j < CW - 1; j++) {
-          ast[j + 1] = ast[j];
-          astep(ast[j + 1], c.x[j], c.y[j]);
-          nrm_fwd(ast[j + 1], q, j);
-        }
-#pragma unroll
-        for (int j = CW - 1; j >= 0; j--) {
-          s2 mb[8], nw[8];
-          llr_out(c, ast[j], bpre, j, dacc, mb, nw, (CW * q + j) * NB + d); // bpre = stored beta[k+1]
-          // running beta at k+1 (normalised when k+1 is even; k+1 >= 1), then beta[k]
-          St8 run = bpre;
-          nrm_k(run, ((j + 1) & 1) == 0);
-          bstep(run, c.x[j], c.y[j]);
+      auto seg = [&](const Chunk<MODE> &c, int q) {
+        St8 bst[CW];
+        TD_C(32 + 3 * (qm - 1 - q));
+        St8 run = betas(c, bpre, false, CW, bst);
+        if (q > 0) { // beta[s0] before normalisation, the next chunk's top
+          s2 x, y, e;
+          cstep(c, 0, x, y, e);
+          bstep(run, x, y);
           bpre = run;
         }
-        if (DOUT && wr) D[d * G16 + q] = dacc;
+        St8 a;
+        ck_get(q, a);
+        TD_C(33 + 3 * (qm - 1 - q));
+        alpha_llr(c, a, bst, q, CW);
+        TD_C(34 + 3 * (qm - 1 - q));
       };
-      ChunkW<CW> c0, c1;
-      int q = qm - 1;
-      load_full(c0, q);
-      for (; q - 1 >= 0; q -= 2) {
-        load_full(c1, q - 1);
-        seg(c0, q);
-        load_full(c0, q - 2);
-        seg(c1, q - 1);
+      for (int q = qm - 1; q >= 0; q--) {
+        ld_chunk(cnx, max(q - 1, 0), true);
+        seg(cur, q);
+        cur = cnx;
       }
-      if (q == 0) seg(c0, 0);
     }
   }
 }
@@ -810,8 +928,9 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
   const int lane = threadIdx.x & 63;
   const int gl = blk * 64 + lane;
   const int nlanes = npairs * NB;
-  const bool live = gl < nlanes;
-  const int g = live ? gl : nlanes - 1; // dead lanes compute on valid data, store nothing
+  // lanes past the group's chains repeat the last chain: same inputs, same results, stored to
+  // the same addresses (stores are unconditional: a per-lane guard costs a branch per step)
+  const int g = gl < nlanes ? gl : nlanes - 1;
   const int pair = g / NB;              // within the group
   const int d = g % NB;
   const uint8_t *pdone = pair_done ? pair_done + G.pair0 : nullptr;
@@ -824,16 +943,17 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
       for (int p = p0; p <= p1; p++) all_done = all_done && pdone[p];
     if (all_done) return;
   }
-  const bool wr = live && !(pdone && pdone[pair]);
-  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
+  // pairs already finished (early stop) in a partly finished workgroup decode on: their arrays
+  // and decision words are never read again (k_decide skips them)
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, NB);
   const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
-  const s2 *p1 = XP1 + plane + base;     // par1
+  s2 *xp1 = XP1 + base;              // app2 (DEC1 output)
+  const s2 *p1 = XP1 + plane + base; // par1
   s2 *A = Aarr + base;
   uint32_t *D = DOUT ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
   const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  win_bidir_body<NB, DIV, MODE, CW, DOUT, B8>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, wr, role, lane);
+  win_bidir_body<NB, DIV, MODE, DOUT, B8>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, role, lane);
   TD_T(4);
 }
 
@@ -853,7 +973,7 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ g
   const int pair = (blockIdx.x - G.blk_half) * blockDim.x + threadIdx.x; // within the group
   if (pair >= npairs) return;
   if (pair_done && pair_done[G.pair0 + pair]) return;
-  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, 1);
   const s4 *sp0 = SP0 + base;
   s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
   const s2 *p1 = XP1 + plane + base;     // par1
@@ -959,7 +1079,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ g
   const int pair = (blockIdx.x - G.blk_half) * blockDim.x + threadIdx.x; // within the group
   if (pair >= npairs) return;
   if (pair_done && pair_done[G.pair0 + pair]) return;
-  const size_t base = (size_t)G.elem0 + (size_t)pair * K;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, 1);
   const s4 *sp0 = SP0 + base;
   s2 *xp1 = XP1 + base;                  // app2 (DEC1 output)
   const s2 *p1 = XP1 + plane + base;     // par1
@@ -1097,9 +1217,13 @@ __global__ __launch_bounds__(256) void k_load_nat(const TdGroup *__restrict__ gr
   __syncthreads();
   const gmut_t<s4> SP0 = gmut<s4>(arr.SP0);
   const gmut_t<s2> P1 = gmut<s2>(arr.XP1) + arr.plane;
-  const size_t base = (size_t)G.elem0 + (size_t)pair * K + (size_t)k0 * NB;
-  for (int e = threadIdx.x; e < kn * NB; e += 256) {
-    const int kk = e / NB, dd = e - kk * NB;
+  // the tile's steps k0 .. k0+kn-1 of all NB chains are one contiguous T4 run from k0 * NB
+  // (k0 is a multiple of 4), written in order: e -> step (e / 4 / NB) * 4 + e % 4, chain e / 4 % NB
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, NB) + (size_t)k0 * NB;
+  const int ne = ((kn + 3) >> 2) * NB * 4;
+  for (int e = threadIdx.x; e < ne; e += 256) {
+    const int gq = e >> 2, kk = (gq / NB) * 4 + (e & 3), dd = gq - (gq / NB) * NB;
+    if (kk >= kn) continue;
     const short *a = &lds[0][dd][3 * kk], *b = &lds[1][dd][3 * kk];
     SP0[base + e] = s4{a[0], b[0], a[1], b[1]};
     P1[base + e] = s2{a[2], b[2]};
@@ -1129,11 +1253,14 @@ __global__ __launch_bounds__(256) void k_load_sb(const TdGroup *__restrict__ gro
   const gmut_t<s4> SP0 = gmut<s4>(arr.SP0);
   const gmut_t<s2> P1 = gmut<s2>(arr.XP1) + arr.plane;
   const gmut_t<s2> T = gmut<s2>(arr.T);
-  const size_t o = (size_t)G.elem0 + (size_t)pair * K + i;
+  const int nb = G.nb;
+  const size_t o0 = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    SP0[o + u] = s4{a[i + u], b[i + u], a[K + 32 + i + u], b[K + 32 + i + u]};
-    P1[o + u] = s2{a[2 * (K + 32) + i + u], b[2 * (K + 32) + i + u]};
+  for (int u = 0; u < 2; u++) { // SB index i + u = step k, chain d -> T4 position
+    const int k = (i + u) / nb, dd = (i + u) - k * nb;
+    const size_t o = o0 + t4_pos(k, dd, nb);
+    SP0[o] = s4{a[i + u], b[i + u], a[K + 32 + i + u], b[K + 32 + i + u]};
+    P1[o] = s2{a[2 * (K + 32) + i + u], b[2 * (K + 32) + i + u]};
   }
   if (i < 12) {
     const int tb = 3 * (K + 32);
@@ -1143,41 +1270,54 @@ __global__ __launch_bounds__(256) void k_load_sb(const TdGroup *__restrict__ gro
   }
 }
 
-// The same copy, eight elements of a pair per thread with 16-byte accesses (rows 16-byte aligned,
-// as the DL-SCH softbuffer rows are; K is a multiple of 8 for every LTE code block size): six
-// 16-byte loads, four 16-byte SP0 stores and two 16-byte P1 stores per thread.
+// The same copy for 16-byte aligned rows (the DL-SCH softbuffer rows; K a multiple of 8, so
+// chains pair up), one T4 group (4 steps) of two adjacent chains d, d+1 of a pair per thread:
+// 4-byte loads of the two chains' values per step and stream (consecutive threads read
+// consecutive chain pairs), then the two chains' 32-byte SP0 groups and 16-byte P1 groups, which
+// are adjacent in T4, as 16-byte stores.
 __global__ __launch_bounds__(256) void k_load_sb8(const TdGroup *__restrict__ groups, int ngroups,
                                                   const int16_t *__restrict__ in, size_t in_stride,
                                                   const int16_t *const *__restrict__ rows,
                                                   TdArrays arr) {
   const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
-  const int K = G.K, ncb = G.ncb, npairs = G.npairs;
-  const int per = K / 8;
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
+  const int L = K / nb, G4 = (L + 3) >> 2, hp = nb >> 1;
+  const int per = G4 * hp;
   const size_t gid = (size_t)(blockIdx.x - G.blk_load) * 256 + threadIdx.x;
   const int pair = (int)(gid / per);
   if (pair >= npairs) return;
-  const int i = 8 * (int)(gid - (size_t)pair * per);
+  const int r = (int)(gid - (size_t)pair * per);
+  const int g4 = r / hp, d = 2 * (r - g4 * hp);
   const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
   const gptr_t<int16_t> a = cb_row(in, in_stride, rows, c0), b = cb_row(in, in_stride, rows, c1);
-  typedef short s8v __attribute__((ext_vector_type(8)));
-  auto ld8 = [](gptr_t<int16_t> p) { return *(const __attribute__((address_space(1))) s8v *)p; };
-  const s8v sa = ld8(a + i), sb = ld8(b + i);
-  const s8v pa = ld8(a + K + 32 + i), pb = ld8(b + K + 32 + i);
-  const s8v qa = ld8(a + 2 * (K + 32) + i), qb = ld8(b + 2 * (K + 32) + i);
-  const size_t o = (size_t)G.elem0 + (size_t)pair * K + i; // multiple of 8: 16-byte aligned
+  auto ld2 = [](gptr_t<int16_t> p) { return *(const __attribute__((address_space(1))) uint32_t *)p; };
+  uint32_t sa[4], sb[4], pa[4], pb[4], qa[4], qb[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int k = min(4 * g4 + u, L - 1); // the last group may run past L: values unused
+    const int i = k * nb + d;             // even: 4-byte aligned
+    sa[u] = ld2(a + i);
+    sb[u] = ld2(b + i);
+    pa[u] = ld2(a + K + 32 + i);
+    pb[u] = ld2(b + K + 32 + i);
+    qa[u] = ld2(a + 2 * (K + 32) + i);
+    qb[u] = ld2(b + 2 * (K + 32) + i);
+  }
+  // chain h (0: d, 1: d + 1) of CB x / y: low / high half of the loaded words
+  auto lo = [](uint32_t x, uint32_t y) { return (x & 0xffffu) | (y << 16); };
+  auto hi = [](uint32_t x, uint32_t y) { return (x >> 16) | (y & 0xffff0000u); };
+  const size_t o = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb) + (size_t)(g4 * nb + d) * 4;
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-  const gmut_t<u4v> SP0 = gmut<u4v>((s4 *)arr.SP0 + o);
-  const gmut_t<u4v> P1 = gmut<u4v>((s2 *)arr.XP1 + arr.plane + o);
-  auto pk = [](short lo, short hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); };
+  const gmut_t<u4v> SP0 = gmut<u4v>((s4 *)arr.SP0 + o); // 2 chains x 4 steps x 8 B: four u4v
+  const gmut_t<u4v> P1 = gmut<u4v>((s2 *)arr.XP1 + arr.plane + o); // 2 x 4 x 4 B: two u4v
 #pragma unroll
-  for (int u = 0; u < 4; u++) // two short4 (syst.a, syst.b, par0.a, par0.b) per 16-byte store
-    SP0[u] = u4v{pk(sa[2 * u], sb[2 * u]), pk(pa[2 * u], pb[2 * u]),
-                 pk(sa[2 * u + 1], sb[2 * u + 1]), pk(pa[2 * u + 1], pb[2 * u + 1])};
-#pragma unroll
-  for (int u = 0; u < 2; u++) // four short2 (par1.a, par1.b) per 16-byte store
-    P1[u] = u4v{pk(qa[4 * u], qb[4 * u]), pk(qa[4 * u + 1], qb[4 * u + 1]),
-                pk(qa[4 * u + 2], qb[4 * u + 2]), pk(qa[4 * u + 3], qb[4 * u + 3])};
-  if (i == 0) { // one thread per pair: the tails
+  for (int h = 0; h < 2; h++) {
+    auto f = [&](uint32_t x, uint32_t y) { return h ? hi(x, y) : lo(x, y); };
+    SP0[2 * h] = u4v{f(sa[0], sb[0]), f(pa[0], pb[0]), f(sa[1], sb[1]), f(pa[1], pb[1])};
+    SP0[2 * h + 1] = u4v{f(sa[2], sb[2]), f(pa[2], pb[2]), f(sa[3], sb[3]), f(pa[3], pb[3])};
+    P1[h] = u4v{f(qa[0], qb[0]), f(qa[1], qb[1]), f(qa[2], qb[2]), f(qa[3], qb[3])};
+  }
+  if (r == 0) { // one thread per pair: the tails
     const int tb = 3 * (K + 32);
     const gmut_t<s2> T = gmut<s2>(arr.T);
 #pragma unroll
@@ -1339,7 +1479,8 @@ static void allow_big_lds(const void *f) {
 }
 
 int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16) {
-  if (sb_input) return (int)nblk((size_t)npairs * (K / (vec16 ? 8 : 2)), 256);
+  if (sb_input && vec16) return (int)nblk((size_t)npairs * ((K / nb + 3) / 4) * (nb / 2), 256);
+  if (sb_input) return (int)nblk((size_t)npairs * (K / 2), 256);
   return npairs * ((K / nb + LOAD_KT - 1) / LOAD_KT);
 }
 
@@ -1461,6 +1602,12 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
 } // namespace srsgpu
 
 #ifdef TD_TIMING
+extern "C" int srsgpu_debug_td_chunk(unsigned long long *out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(srsgpu::td_chunk), sizeof(unsigned long long) * n) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
 extern "C" int srsgpu_debug_td_times(unsigned long long *out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(srsgpu::td_times), sizeof(unsigned long long) * n) ==
                  hipSuccess

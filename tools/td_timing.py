@@ -55,3 +55,20 @@ assert lib.srsgpu_tdec_batch_run_dev(q, 0, 0, vp(llr.data_ptr()), ctypes.c_size_
 ev1.record()
 torch.cuda.synchronize()
 print("one batch (load + %d half-its + decide): %.1f us" % (NH, ev0.elapsed_time(ev1) * 1e3))
+
+# per-chunk stamps (td_chunk): phase-1 chunk starts, phase-2 chunk start / betas done / LLRs done
+c = (ctypes.c_ulonglong * (2048 * 80))()
+if hasattr(lib, "srsgpu_debug_td_chunk") and lib.srsgpu_debug_td_chunk(c, 2048 * 80) == 0:
+    ch = np.frombuffer(c, dtype=np.uint64).reshape(2048, 80)[:nw].astype(np.int64)
+    for role in (0, 1):
+        r = ch[role::2]
+        t0 = a[role::2, 0]
+        p1 = r[:, :12] - t0[:, None]
+        print("wave %d phase-1 chunk starts (cycles from wave start):" % role, p1.mean(0).round(0).tolist())
+        p2 = r[:, 32:32 + 36].reshape(-1, 12, 3)
+        betas = (p2[:, :, 1] - p2[:, :, 0]).mean(0)
+        llrs = (p2[:, :, 2] - p2[:, :, 1]).mean(0)
+        gaps = (p2[:, 1:, 0] - p2[:, :-1, 2]).mean(0)
+        print("wave %d phase-2 betas per chunk:" % role, betas.round(0).tolist())
+        print("wave %d phase-2 LLRs per chunk: " % role, llrs.round(0).tolist())
+        print("wave %d phase-2 gaps between chunks:" % role, gaps.round(0).tolist())
