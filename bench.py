@@ -33,9 +33,19 @@ NSTREAMS = 3  # batches in flight in the streaming measurement
 EBNO_DB = 4.5            # reference convention (noise std sqrt(1/(Es/N0))), error-free region
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SF_BITS = 75376          # 20 MHz, MCS 28 transport block (13 x K=5824): subframe equivalent
-# Algorithmic bytes of one constituent-decoder launch (one half-iteration) per info bit:
-# read x (systematic/app, int16) + y (parity, int16), write the LLR (int16) = 6 B/bit.
-ALG_BYTES_PER_BIT_HALFIT = 6
+# SURVEY §8(d) compulsory HBM bytes of one code block's whole decode: the int16 input in the
+# reference's sub-block layout, (3(K+32)+12) * 2 B, plus K/8 decision bytes = 37,848 B at K=6144.
+# One half-iteration launch is charged 1/NHALF of it (roofline.achieved).
+COMPULSORY_BYTES_PER_CB = (3 * (K + 32) + 12) * 2 + K // 8
+# SURVEY §8(d) algorithmic work: ~90 int16 operations per info bit per half-iteration (beta ~25.5,
+# alpha ~56.5, estimation pre-passes ~4.8, extrinsic subtraction + scatter ~3)
+ALG_OPS_PER_BIT_HALFIT = 90
+# SURVEY §8(d) VALU peak for packed int16: 256 CUs x 64 lanes x 2 packed halves x 2.4 GHz
+# = 78.6 T int16-ops/s. The issue rate measured on the MI355X (tools/dbg/vrate16.hip,
+# profiles/r02_vrate16.txt) is lower: 1024 SIMDs x 128 ops / 1.96 ns = 66.9 T at 4 waves per
+# SIMD, 51.4 T (2.55 ns) at the decoder's one wave per SIMD with 8 independent chains.
+VALU_INT16_PEAK_T = 78.6
+VALU_INT16_MEASURED_T = {"4_waves_per_simd": 66.9, "1_wave_per_simd_ilp8": 51.4}
 
 
 def make_inputs(n, seed, tcod):
@@ -56,10 +66,33 @@ def make_inputs(n, seed, tcod):
     return bits, idx, llr
 
 
-def cpu_baseline(llr, nthreads):
+def physical_cpus():
+    """One logical CPU per physical core among the CPUs this process may run on (SMT siblings
+    from /sys/devices/system/cpu/cpu*/topology/thread_siblings_list)."""
+    out, seen = [], set()
+    for c in sorted(os.sched_getaffinity(0)):
+        try:
+            sib = open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c).read().strip()
+        except OSError:
+            sib = str(c)
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+    return out
+
+
+def cpu_baseline(llr, nthreads=None):
     """Reference AVX2 AUTO decoder (oracle/_ref, compiled from the reference's own sources) on
-    the host cores: one srslte_tdec_t per thread, srslte_tdec_run_all over a bounded sample of
-    the same code blocks. Falls back to the scalar oracle port if _ref is absent."""
+    the host cores: one srslte_tdec_t per thread, each thread pinned to its own physical core
+    (SURVEY §8(d)), srslte_tdec_run_all over a bounded sample of the same code blocks. Threads =
+    every physical core this process may use, capped by the host's CPU share for this job
+    (OMP_NUM_THREADS, 16 per GPU on the GPU box) or SRSGPU_CPU_THREADS. Falls back to the scalar
+    oracle port if _ref is absent."""
+    cores = physical_cpus()
+    cap = int(os.environ.get("SRSGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", len(cores))))
+    if nthreads is None:
+        nthreads = max(1, min(len(cores), cap))
+    pin = cores[:nthreads]
     ref = os.path.join(REPO, "oracle", "_ref", "libsrsref.so")
     port = os.path.join(REPO, "oracle", "liboracle.so")
     kind = "reference" if os.path.exists(ref) else "port"
@@ -92,6 +125,8 @@ def cpu_baseline(llr, nthreads):
 
     def threaded(reps):
         def thread_fn(i):
+            if i < len(pin):
+                os.sched_setaffinity(0, {pin[i]})  # Linux: pins the calling thread
             rows = llr[i * per_thread:(i + 1) * per_thread]
             for _ in range(reps):
                 work(rows, outs[i])
@@ -111,11 +146,13 @@ def cpu_baseline(llr, nthreads):
         reps = int(min(400, max(reps + 1, np.ceil(reps * 20.0 / (wall * nthreads)))))
     ncb = per_thread * nthreads * reps
     return {"value": round(ncb * K / wall / 1e6, 2), "unit": "Mbps", "cores": nthreads,
-            "kind": kind,
+            "kind": kind, "pinned_cpus": pin, "physical_cores_available": len(cores),
             "sample": "%d CB decodes of K=%d (%d threads x %d CBs x %d passes), %d half-iterations, "
-                      "AUTO (AVX2) decoder, natural layout, one srslte_tdec_t per thread, %.1f s wall "
-                      "(%.0f thread-seconds)" % (ncb, K, nthreads, per_thread, reps, NHALF, wall,
-                                                 wall * nthreads)}
+                      "AUTO (AVX2) decoder, natural layout, one srslte_tdec_t per thread, each thread "
+                      "pinned to its own physical core (%d physical cores in the affinity set, CPU "
+                      "share cap %d), %.1f s wall (%.0f thread-seconds)"
+                      % (ncb, K, nthreads, per_thread, reps, NHALF, len(cores), cap, wall,
+                         wall * nthreads)}
 
 
 # ---------------------------------------------------------------- C3 subframe pipeline ----
@@ -158,7 +195,7 @@ def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1):
     return N, x
 
 
-STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_halfit",
+STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_bidir",
           "k_sse_halfit", "k_decide", "k_tb_finish")
 
 
@@ -255,21 +292,25 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
     name = "c3_pdsch_pipeline" if tm == 1 else "c4_tm3_cdd2x2_pipeline"
     return {"workload": "%s_%dsf_20MHz_64QAM_%dx_tbs%d" % (name, C3_SF, ntb, C3_TBS),
             "subframes_per_s": round(C3_SF * steps / el, 1),
-            "tb_mbps": round(C3_SF * ntb * steps * C3_TBS / el / 1e6, 1),
+            "processing_mbps": round(C3_SF * ntb * steps * C3_TBS / el / 1e6, 1),
             "ms_per_batch": round(el / steps * 1e3, 3), "symbol_size": N, "rx_antennas": nrx,
             "streams": lanes, "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
-            "data": "synthetic 64QAM symbols (not codewords: every CB runs 8 half-iterations)"}
+            "data": "synthetic 64QAM symbols (not codewords: every CB runs the full 8 half-iterations "
+                    "and fails its CRC, so this is the fixed-8 processing rate in TB bits per second, "
+                    "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
 
 
-def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2):
+def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes interleaved over cells of
       6/25/50/100 PRB, random allocation and MCS 0..28 (K 40..6144), all cells' TBs in one
       DL-SCH call per stream; AWGN at 20 dB.
-    kind "c3_coded" — the C3 subframe (100 PRB, MCS 28, TBS 75376) as real codewords at 30 dB
-      (the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst case.
-    lanes: the 1024 subframes are split over that many HIP streams (run_pipeline)."""
+    kind "c3_coded" — the C3 subframe (100 PRB, MCS 28, TBS 75376) as real codewords at snr_db
+      (default 30 dB, the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst
+      case.
+    lanes: the 1024 subframes are split over that many HIP streams (run_pipeline).
+    decoded_mbps is SURVEY §8(d)'s metric: the sum of K over CRC-passing code blocks per second."""
     import srsgpu_traffic as tr
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
     ms = []
@@ -277,10 +318,12 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2):
         st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
         n = C3_SF // lanes
         if kind == "c5":
-            ms.append(tr.MixedCells(table, n, torch, dev, seed=21 + 100 * li, stream=st, snr_db=20.0))
+            snr = 20.0 if snr_db is None else snr_db
+            ms.append(tr.MixedCells(table, n, torch, dev, seed=21 + 100 * li, stream=st, snr_db=snr))
         else:
+            snr = 30.0 if snr_db is None else snr_db
             ms.append(tr.MixedCells(table, n, torch, dev, prbs=(100,), seed=22 + 100 * li, stream=st,
-                                    snr_db=30.0, mcs=28, full_band=True))
+                                    snr_db=snr, mcs=28, full_band=True))
     torch.cuda.synchronize()
 
     def step():
@@ -304,14 +347,18 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2):
     tbl = [t for m in ms for t in m.tb_list]
     ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in tbl})
     bits = sum(m.bits for m in ms)
+    cb_bits = sum(m.decoded_bits(table) for m in ms)
     out = {"workload": ("c5_mixed_bw_%dsf_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
                         "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS)),
-           "subframes_per_s": round(C3_SF * steps / el, 1),
-           "tb_mbps": round(bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
+           "snr_db": snr, "subframes_per_s": round(C3_SF * steps / el, 1),
+           "decoded_mbps": round(cb_bits * steps / el / 1e6, 1),
+           "acked_tb_mbps": round(sum(t["tbs"] for m in ms for t, r in zip(m.tb_list, m.d_ret.cpu().numpy())
+                                      if r == 0) * steps / el / 1e6, 1),
+           "offered_tb_mbps": round(bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
            "streams": lanes, "code_blocks": sum(m.ncb for m in ms), "distinct_K": len(ks),
            "K_range": [ks[0], ks[-1]], "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": len(tbl),
            "nof_iterations_mean": noi, "stage_ms_per_batch": stages,
-           "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % ("20" if kind == "c5" else "30")}
+           "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % snr}
     for m in ms:
         m.close()
     return out
@@ -360,7 +407,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,c5,d8",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -432,12 +479,13 @@ def main():
         step()
     torch.cuda.synchronize()
     s.prof_enable(False)
-    kern_ms, kern_n = s.prof_get("k_win_halfit")
+    kern_ms, kern_n = s.prof_get("k_win_bidir")
     # streaming: NSTREAMS batches in flight on their own streams (a receiver double/triple
     # buffering its batches); every batch is the full 4096-CB step
     ms_batches = [batch] + [s.TdecBatch(NCB, K, stream=torch.cuda.Stream(dev).cuda_stream)
                             for _ in range(NSTREAMS - 1)]
     ms_outs = [d_out] + [torch.zeros_like(d_out) for _ in range(NSTREAMS - 1)]
+    torch.cuda.synchronize()  # the fills ran on the current stream; the batches use their own
 
     def step_ms(i):
         j = i % NSTREAMS
@@ -473,16 +521,21 @@ def main():
     if rank == 0:
         workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
         avg_launch_ms = kern_ms / max(kern_n, 1)
-        alg_bytes = ALG_BYTES_PER_BIT_HALFIT * NCB * K
+        # compulsory bytes of the whole decode, one NHALF-th per half-iteration launch
+        alg_bytes = COMPULSORY_BYTES_PER_CB * NCB / NHALF
         achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
         pmc = load_profile_json(workload)
-        valu = load_profile_json(workload, "valu")
-        roofline = {"bound": "hbm", "kernel": "k_win_halfit",
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        roofline = {"bound": "hbm", "kernel": "k_win_bidir",
                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
-                    "alg_bytes_per_launch": alg_bytes, "avg_launch_ms": round(avg_launch_ms, 4),
-                    "launches": kern_n}
+                    "traffic": traffic, "layout_traffic": traffic,
+                    "traffic_over_compulsory": round(traffic / alg_bytes, 2) if traffic else None,
+                    "traffic_source": pmc.get("source") if pmc else None,
+                    "alg_bytes_per_launch": int(alg_bytes),
+                    "alg_bytes_def": "SURVEY 8(d): (3(K+32)+12)*2 + K/8 = %d B per CB per decode, / %d "
+                                     "half-iterations" % (COMPULSORY_BYTES_PER_CB, NHALF),
+                    "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n}
         result = {
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": nranks,
             "steps": args.steps, "warmup": args.warmup,
@@ -500,16 +553,18 @@ def main():
             "ms_per_step": round(el_ms / args.steps * 1e3, 3), "bit_errors": ms_err,
             "note": "the same steps with %d batches in flight on separate streams; value above is "
                     "one stream, one batch at a time" % NSTREAMS}
-        if valu and kern_n:
-            # the decoder's actual bound: packed int16 VALU issue
-            rate = valu["valu_instr_per_launch"] / (avg_launch_ms / 1e3)
-            peak = valu["simds"] / (valu["peak_ns_per_packed_instr_per_simd"] * 1e-9)
+        if kern_n:
+            # the decoder's actual bound: int16 VALU work, SURVEY §8(d)'s algorithmic 90 ops per
+            # info bit per half-iteration over the live launch time, against §8(d)'s peak
+            ops = ALG_OPS_PER_BIT_HALFIT * NCB * K
+            rate_t = ops / (avg_launch_ms / 1e3) / 1e12
             result["valu_roofline"] = {
-                "bound": "valu (packed int16 issue)", "kernel": "k_win_bidir",
-                "achieved": round(rate / 1e9, 1), "peak": round(peak / 1e9, 1),
-                "unit": "G wave-instructions/s", "frac": round(rate / peak, 4),
-                "int16_ops_per_s_T": round(rate * 128 / 1e12, 1),
-                "instr_per_launch": valu["valu_instr_per_launch"]}
+                "bound": "valu (packed int16)", "kernel": "k_win_bidir",
+                "achieved": round(rate_t, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
+                "frac": round(rate_t / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": ops,
+                "alg_ops_def": "SURVEY 8(d): %d int16 ops per info bit per half-iteration" % ALG_OPS_PER_BIT_HALFIT,
+                "measured_issue_peaks_T": VALU_INT16_MEASURED_T,
+                "frac_of_1wave_issue_peak": round(rate_t / VALU_INT16_MEASURED_T["1_wave_per_simd_ilp8"], 4)}
     legs = set() if args.no_pipeline else set(args.legs.split(","))
     pipe = None
     if "c3" in legs:
@@ -517,29 +572,45 @@ def main():
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
             pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe["tb_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
+            pipe["processing_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
     pipe3 = None
     if "tm3" in legs:
         pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3)
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
             pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe3["tb_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
+            pipe3["processing_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
     extra = {}
+    def scale_ranks(r):
+        if dist:  # whole job: the slowest rank's batch time, every rank's subframes
+            ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
+            for key in ("decoded_mbps", "acked_tb_mbps", "offered_tb_mbps"):
+                r[key] = round(r[key] * r["ms_per_batch"] / ms * nranks, 1)
+            r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+        return r
+
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
             # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
-            r = run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind)
-            if dist:
-                ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
-                r["tb_mbps"] = round(r["tb_mbps"] * r["ms_per_batch"] / ms * nranks, 1)
-                r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            extra[kind] = r
+            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind))
+    sweep = None
+    if "sweep" in legs:
+        # SURVEY §8(d) C3 points: coded subframes at 20 / 25 / 30 dB, CRC early stop (max 8
+        # half-iterations); decoded Mbps = sum of K over CRC-passing code blocks per second
+        sweep = []
+        # (16 and 18 dB added: with this channel the 20 dB point already decodes every TB at the
+        # first half-iteration; below it the early stop runs 2..8 half-iterations)
+        for snr in (16.0, 18.0, 20.0, 25.0, 30.0):
+            r = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, "c3_coded", snr_db=snr))
+            sweep.append({k: r[k] for k in ("snr_db", "decoded_mbps", "acked_tb_mbps", "offered_tb_mbps",
+                                             "subframes_per_s", "ms_per_batch", "nof_iterations_mean",
+                                             "acked_tbs", "tbs")})
     dec8 = None
     if "d8" in legs:  # last: the subframe legs above are timed as before
         # the reference's 8-bit path (srslte_tdec_iteration_8bit: AUTO -> int8 AVX8 window, 32
         # sub-blocks at K = 6144) on the same code blocks, LLRs requantised to int8
         d_in8 = torch.clamp(torch.div(d_in, 6, rounding_mode="trunc"), -128, 127).contiguous()
+        torch.cuda.synchronize()  # built on the current stream, read on the batch stream
 
         def step8():
             if batch.run_dev(s.SRSGPU_TDEC_AUTO_8BIT, 0, d_in8.data_ptr(), stride, K, NCB, NHALF,
@@ -575,14 +646,16 @@ def main():
     if rank == 0 and pipe3:
         result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
         result["pipeline_tm3"] = pipe3
+    if rank == 0 and sweep:
+        result["c3_coded_sweep"] = {"workload": "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS),
+                                    "early_stop_max_halfits": 8, "points": sweep}
     if rank == 0:
         for kind, key in (("c3_coded", "coded"), ("c5", "c5")):
             if kind in extra:
                 result["config"]["subframes_per_s_" + key] = extra[kind]["subframes_per_s"]
                 result["pipeline_" + key] = extra[kind]
     if rank == 0 and not args.no_cpu_baseline and nranks == 1:
-        result["cpu_baseline"] = cpu_baseline(llr, int(os.environ.get("SRSGPU_CPU_THREADS",
-                                                                       min(16, os.cpu_count() or 1))))
+        result["cpu_baseline"] = cpu_baseline(llr)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -457,8 +457,8 @@ struct TdecEngine {
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      static const char *const names[TD_NKIND] = {"k_win_halfit", "k_win_halfit", "k_sse_halfit",
-                                                   "k_gen_halfit", "k_win8_halfit", "k_win8_halfit"};
+      static const char *const names[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
+                                                   "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
       ProfScope ps(names[k], st);
       HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
     }

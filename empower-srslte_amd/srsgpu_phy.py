@@ -374,6 +374,13 @@ class Dlsch:
         return _lib.srsgpu_dlsch_decode_dev(self.q, arr, len(tbs_list), _vp(d_e), _vp(d_data),
                                             max_halfits, _vp(d_ret), _vp(d_noi))
 
+    def read_cb_crc(self, slot):
+        """cb_crc flags of softbuffer `slot` (the soft bits are not copied)"""
+        crc = np.zeros(self.max_cb, np.uint8)
+        if _lib.srsgpu_dlsch_softbuffer_read(self.q, slot, None, _u8(crc)) != 0:
+            raise RuntimeError("softbuffer read failed")
+        return crc
+
     def read_softbuffer(self, slot):
         rows = np.zeros((self.max_cb, SOFTBUFFER_SIZE), np.int16)
         crc = np.zeros(self.max_cb, np.uint8)

@@ -149,6 +149,23 @@ class MixedCells:
             good += int(r == 0 and (tx[o:o + nb] == rx[o:o + nb]).all())
         return int((ret == 0).sum()), good, float(self.d_noi.cpu().numpy().mean())
 
+    def decoded_bits(self, table):
+        """SURVEY §8(d)'s decoded bits of the last decode: the sum of K over the code blocks whose
+        CRC passed. A TB that acks passed every code block; a failed TB contributes the code
+        blocks its softbuffer marks in cb_crc (sch.c:394-401)."""
+        ret = self.d_ret.cpu().numpy()
+        seg = table["cbsegm_C_C1_K1_C2_K2_F"]
+        total = 0
+        for t, r in zip(self.tb_list, ret):
+            C, _c1, K1, C2, K2, _f = seg[str(t["tbs"])]
+            ks = [K2 if i < C2 else K1 for i in range(C)]
+            if r == 0:
+                total += sum(ks)
+            else:
+                crc = self.dlsch.read_cb_crc(t["softbuffer"])
+                total += sum(k for k, c in zip(ks, crc) if c)
+        return total
+
     def close(self):
         for c in self.cells:
             for k in ("ofdm", "chest", "pd"):

@@ -3,9 +3,9 @@ WRITE_SIZE, collected separately as MI355X_MICROARCH.md's HBM section prescribes
 `bench.py --no-pipeline`. Writes the profiles/*pmc_traffic*.json that bench.py reads into
 roofline.traffic.
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. The guide's x2 correction applies to 16-B/lane
-streaming reads only; the decoder reads 8-B (short4) and 4-B lanes, which the guide lists as
-uncalibrated, so the raw counter is reported and the correction is recorded as not applied.
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. The guide's x2 FETCH_SIZE correction (16-B/lane
+streaming reads) is applied: the decoder's dominant reads (SP0 / P1 in T4 layout) are 16 B per
+lane; the raw counter is recorded beside it.
 
 usage: python3 tools/pmc_traffic.py <fetch_csv> <write_csv> <out_json>
 """
@@ -27,17 +27,24 @@ def per_launch(path, counter):
 
 fetch_kib, nf = per_launch(sys.argv[1], "FETCH_SIZE")
 write_kib, nw = per_launch(sys.argv[2], "WRITE_SIZE")
-alg = 6 * 4096 * 6144
+# SURVEY 8(d) compulsory bytes per launch: (3(K+32)+12)*2 + K/8 per CB per decode, / 8 half-its
+alg = ((3 * (6144 + 32) + 12) * 2 + 6144 // 8) * 4096 / 8
+fetch = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts half the bytes of 16-B/lane reads
+write = write_kib * 1024
 out = {
     "workload": "batched_turbo_decode_4096xK6144_8halfits",
     "kernel": KERNEL,
     "launches": [nf, nw],
-    "fetch_bytes_per_launch": round(fetch_kib * 1024),
-    "write_bytes_per_launch": round(write_kib * 1024),
-    "hbm_bytes_per_launch": round((fetch_kib + write_kib) * 1024),
-    "alg_bytes_per_launch": alg,
-    "traffic_over_alg": round((fetch_kib + write_kib) * 1024 / alg, 3),
-    "fetch_x2_correction": "not applied (8-B and 4-B lane accesses are uncalibrated on gfx950)",
+    "fetch_size_raw_bytes_per_launch": round(fetch_kib * 1024),
+    "fetch_bytes_per_launch": round(fetch),
+    "write_bytes_per_launch": round(write),
+    "hbm_bytes_per_launch": round(fetch + write),
+    "alg_bytes_per_launch": round(alg),
+    "traffic_over_alg": round((fetch + write) / alg, 3),
+    "fetch_x2_correction": "applied (MI355X_MICROARCH.md HBM: FETCH_SIZE reports half the bytes of "
+                           "16-B/lane reads; the decoder's SP0/P1 reads are 16 B/lane, its X2/A reads "
+                           "4 B/lane, uncalibrated)",
+    "source": sys.argv[3].split("/")[-1],
 }
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 print(json.dumps(out))
