@@ -48,13 +48,16 @@ VALU_INT16_PEAK_T = 78.6
 VALU_INT16_MEASURED_T = {"4_waves_per_simd": 66.9, "1_wave_per_simd_ilp8": 51.4}
 
 
-def make_inputs(n, seed, tcod):
-    """n code blocks: random bits, srslte_tcod_encode (product encoder), AWGN, int16 LLRs."""
+def make_inputs(n, seed, tcod, first=0):
+    """Code blocks first .. first+n-1 of the global job (a rank's contiguous shard): random bits
+    (256 templates, the same on every rank), srslte_tcod_encode (product encoder), AWGN (noise
+    seeded by the shard), int16 LLRs."""
     rng = np.random.default_rng(seed)
-    ntmpl = min(n, 256)
+    ntmpl = 256
     bits = rng.integers(0, 2, (ntmpl, K), dtype=np.uint8)
     coded = np.stack([tcod.encode(b) for b in bits])
-    idx = np.arange(n) % ntmpl
+    rng = np.random.default_rng(seed + 1 + first)
+    idx = (first + np.arange(n)) % ntmpl
     esno = EBNO_DB + 10 * np.log10(1.0 / 3.0)
     sigma = np.float32(np.sqrt(1.0 / 10 ** (esno / 10)))
     llr = np.empty((n, 3 * K + 12), np.int16)
@@ -300,30 +303,45 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
                     "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
 
 
-def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None):
+def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
-    kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes interleaved over cells of
+    kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
       6/25/50/100 PRB, random allocation and MCS 0..28 (K 40..6144), all cells' TBs in one
       DL-SCH call per stream; AWGN at 20 dB.
     kind "c3_coded" — the C3 subframe (100 PRB, MCS 28, TBS 75376) as real codewords at snr_db
       (default 30 dB, the operating point of a loaded 20 MHz cell) rather than the fixed-8 worst
       case.
-    lanes: the 1024 subframes are split over that many HIP streams (run_pipeline).
+    Multi-GPU: the job is nranks x 1024 subframes, planned identically on every
+    rank (srsgpu_traffic.plan) and split by the native partitioner: C5 by decoding cost from one
+    global longest-first queue, C3 in contiguous ranges. After the timed loop the results of every
+    rank (TB bytes, return code, nof_iterations, cb_crc) go to rank 0 in one grouped send/recv
+    batch (srsgpu_shard.gather_records), timed separately as gather_ms.
+    lanes: a rank's subframes are split over that many HIP streams (run_pipeline).
     decoded_mbps is SURVEY §8(d)'s metric: the sum of K over CRC-passing code blocks per second."""
+    import srsgpu_shard as sh
     import srsgpu_traffic as tr
+    rank = dist.get_rank() if dist else 0
+    nranks = dist.get_world_size() if dist else 1
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
+    n_global = C3_SF * nranks
+    if kind == "c5":
+        snr, seed, kw = (20.0 if snr_db is None else snr_db), 21, {}
+        sf_plan = tr.plan(table, n_global, seed=seed)
+        owner, load = sh.weighted(tr.tb_weights(table, sf_plan), nranks)
+        part = {"kind": "weighted (global longest-first queue over sum K x 8)", "balance": sh.balance(load)}
+    else:
+        snr, seed, kw = (30.0 if snr_db is None else snr_db), 22, dict(prbs=(100,), mcs=28, full_band=True)
+        sf_plan = tr.plan(table, n_global, seed=seed, **kw)
+        f = sh.contiguous(n_global, nranks)
+        owner = np.repeat(np.arange(nranks), np.diff(f))
+        part = {"kind": "contiguous", "balance": 1.0}
+    mine = [i for i in range(n_global) if owner[i] == rank]
     ms = []
     for li in range(lanes):
         st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
-        n = C3_SF // lanes
-        if kind == "c5":
-            snr = 20.0 if snr_db is None else snr_db
-            ms.append(tr.MixedCells(table, n, torch, dev, seed=21 + 100 * li, stream=st, snr_db=snr))
-        else:
-            snr = 30.0 if snr_db is None else snr_db
-            ms.append(tr.MixedCells(table, n, torch, dev, prbs=(100,), seed=22 + 100 * li, stream=st,
-                                    snr_db=snr, mcs=28, full_band=True))
+        ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
+                                keep=mine[li::lanes], **kw))  # one plan: the same seed everywhere
     torch.cuda.synchronize()
 
     def step():
@@ -333,11 +351,15 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     gc.disable()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     el = time.perf_counter() - t0
     gc.enable()
     stages = stage_profile(s, torch, step, steps)
@@ -348,30 +370,50 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None):
     ks = sorted({int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][2]) for t in tbl})
     bits = sum(m.bits for m in ms)
     cb_bits = sum(m.decoded_bits(table) for m in ms)
-    out = {"workload": ("c5_mixed_bw_%dsf_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
-                        "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS)),
-           "snr_db": snr, "subframes_per_s": round(C3_SF * steps / el, 1),
+    acked_bits = sum(t["tbs"] for m in ms for t, r in zip(m.tb_list, m.d_ret.cpu().numpy()) if r == 0)
+    # gather of the results to rank 0 (RCCL grouped send/recv on the GPU box)
+    recs = {}
+    for m in ms:
+        ret, noiv, data = m.d_ret.cpu().numpy(), m.d_noi.cpu().numpy(), m.d_data.cpu().numpy()
+        for t, r, n in zip(m.tb_list, ret, noiv):
+            o = t["data_offset"]
+            recs[t["sf"]] = sh.pack_tb_record(r, n, data[o:o + t["tbs"] // 8], m.dlsch.read_cb_crc(t["softbuffer"]),
+                                              t["tbs"])
+    local = torch.from_numpy(np.concatenate([recs[i] for i in mine])).to(dev)
+    sizes = [sh.tb_record_len(p["tbs"]) for p in sf_plan]
+    gather_ms = None
+    if dist:
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        sh.gather_records(dist, torch, dev, owner, sizes, local)
+        torch.cuda.synchronize()
+        gather_ms = round((time.perf_counter() - tg) * 1e3, 3)
+    out = {"workload": ("c5_mixed_bw_%dsf_per_gpu_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
+                        "c3_coded_%dsf_per_gpu_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS)),
+           "snr_db": snr, "subframes_per_s": round(len(mine) * steps / el, 1),
            "decoded_mbps": round(cb_bits * steps / el / 1e6, 1),
-           "acked_tb_mbps": round(sum(t["tbs"] for m in ms for t, r in zip(m.tb_list, m.d_ret.cpu().numpy())
-                                      if r == 0) * steps / el / 1e6, 1),
+           "acked_tb_mbps": round(acked_bits * steps / el / 1e6, 1),
            "offered_tb_mbps": round(bits * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 3),
            "streams": lanes, "code_blocks": sum(m.ncb for m in ms), "distinct_K": len(ks),
            "K_range": [ks[0], ks[-1]], "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": len(tbl),
-           "nof_iterations_mean": noi, "stage_ms_per_batch": stages,
+           "nof_iterations_mean": noi, "stage_ms_per_batch": stages, "partition": part,
+           "subframes_this_rank": len(mine), "gather_ms": gather_ms,
+           "result_bytes_per_rank": int(local.numel()),
            "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % snr}
     for m in ms:
         m.close()
     return out
 
 
-def reduce_over_ranks(dist, dev, elapsed, bit_errors):
+def reduce_over_ranks(dist, dev, elapsed, bit_errors, op="max"):
     """Job time = the slowest rank's timed region (it is bracketed by barriers); bit errors are
-    summed. Identity on a single process."""
+    summed (op="sum" sums the first value too). Identity on a single process."""
     if not dist:
         return elapsed, bit_errors
     import torch
     t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     e = torch.tensor([bit_errors], device=dev, dtype=torch.int64)
     dist.all_reduce(e)
     return float(t.item()), int(e.item())
@@ -428,7 +470,13 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     tcod = s.Tcod(K)
-    bits, idx, llr = make_inputs(NCB, 1234 + rank, tcod)
+    nranks = max(1, world)
+    # the global job is nranks x NCB code blocks, split in contiguous ranges by the
+    # native partitioner (include/srsgpu/shard.h); every rank decodes its own range
+    import srsgpu_shard as sh
+    first = sh.contiguous(nranks * NCB, nranks)
+    assert first[rank + 1] - first[rank] == NCB
+    bits, idx, llr = make_inputs(NCB, 1234, tcod, first=first[rank])
     d_in = torch.from_numpy(llr).to(dev)
     d_out = torch.zeros((NCB, K // 8), dtype=torch.uint8, device=dev)
     # a dedicated stream: launches on the null stream carry HIP's implicit cross-stream
@@ -514,7 +562,6 @@ def main():
     el_ms, ms_err = reduce_over_ranks(dist, dev, el_ms, ms_err)
     elapsed, bit_errors = reduce_over_ranks(dist, dev, elapsed, bit_errors)
 
-    nranks = max(1, world)
     bits_total = nranks * NCB * K * args.steps
     mbps = decoded_mbps(nranks, NCB, K, args.steps, elapsed)
     result = None
@@ -582,17 +629,18 @@ def main():
             pipe3["processing_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
     extra = {}
     def scale_ranks(r):
-        if dist:  # whole job: the slowest rank's batch time, every rank's subframes
+        if dist:  # whole job: every rank's bits and subframes over the slowest rank's batch time
             ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
             for key in ("decoded_mbps", "acked_tb_mbps", "offered_tb_mbps"):
-                r[key] = round(r[key] * r["ms_per_batch"] / ms * nranks, 1)
+                tot, _ = reduce_over_ranks(dist, dev, r[key] * r["ms_per_batch"], 0, op="sum")
+                r[key] = round(tot / ms, 1)
             r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
         return r
 
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
             # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
-            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind))
+            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind, dist=dist))
     sweep = None
     if "sweep" in legs:
         # SURVEY §8(d) C3 points: coded subframes at 20 / 25 / 30 dB, CRC early stop (max 8
@@ -601,7 +649,8 @@ def main():
         # (16 and 18 dB added: with this channel the 20 dB point already decodes every TB at the
         # first half-iteration; below it the early stop runs 2..8 half-iterations)
         for snr in (16.0, 18.0, 20.0, 25.0, 30.0):
-            r = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, "c3_coded", snr_db=snr))
+            r = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, "c3_coded", snr_db=snr,
+                                        dist=dist))
             sweep.append({k: r[k] for k in ("snr_db", "decoded_mbps", "acked_tb_mbps", "offered_tb_mbps",
                                              "subframes_per_s", "ms_per_batch", "nof_iterations_mean",
                                              "acked_tbs", "tbs")})

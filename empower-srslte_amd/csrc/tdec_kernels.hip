@@ -558,6 +558,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     return u4{w[i0], w[i0 + NB], w[i0 + 2 * NB], w[i0 + 3 * NB]};
   };
   auto ld_grp = [&](Grp<MODE> &r, int g, int dd) {
+#ifdef TD_EXP_L2
+    g &= 3; // timing experiment only: every load from the pair's first 4 groups (cache resident)
+#endif
     const int o = g * NB + dd;
     if (MODE == 1) {
       r.s0 = ld_sb4(wX, g, dd);
@@ -774,10 +777,20 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         TD_C(34 + 3 * (q - qm));
       };
       const int qf = L / CW; // full chunks
-      for (int q = qm; q < qf; q++) {
+      // two chunks per iteration, the buffers alternating (no copies); an odd count first takes
+      // one chunk and a single copy, so the loop is entered as it loops
+      int q = qm;
+      if ((qf - qm) & 1) {
         ld_chunk(cnx, min(q + 1, nc - 1), true);
         seg(cur, q);
         cur = cnx;
+        q++;
+      }
+      for (; q + 1 < qf; q += 2) {
+        ld_chunk(cnx, q + 1, true);
+        seg(cur, q);
+        ld_chunk(cur, min(q + 2, nc - 1), true);
+        seg(cnx, q + 1);
       }
       if (qf < nc) {
         // the partial chunk, n = L - CW qf steps (cur holds it): betas by selects, so every
@@ -902,10 +915,18 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         alpha_llr(c, a, bst, q, CW);
         TD_C(34 + 3 * (qm - 1 - q));
       };
-      for (int q = qm - 1; q >= 0; q--) {
+      int q = qm - 1; // two chunks per iteration, as in the forward wave
+      if (qm & 1) {
         ld_chunk(cnx, max(q - 1, 0), true);
         seg(cur, q);
         cur = cnx;
+        q--;
+      }
+      for (; q >= 1; q -= 2) {
+        ld_chunk(cnx, q - 1, true);
+        seg(cur, q);
+        ld_chunk(cur, max(q - 2, 0), true);
+        seg(cnx, q - 1);
       }
     }
   }

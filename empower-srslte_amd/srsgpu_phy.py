@@ -135,6 +135,9 @@ _sig = {
                                    ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u32,
                                    ctypes.POINTER(ctypes.c_int32), _u32p]),
     "srsgpu_dlsch_softbuffer_read": (_i32, [_vp, _u32, _i16p, _u8p]),
+    "srsgpu_shard_contiguous": (_i32, [_u32, _u32, _u32p]),
+    "srsgpu_shard_weighted": (_i32, [ctypes.POINTER(ctypes.c_uint64), _u32, _u32,
+                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64)]),
     "srsgpu_rm_turbo_rx_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
     "srsgpu_dlsch_encode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp]),
     "srsgpu_pdsch_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32, _u32,
@@ -590,3 +593,23 @@ def prof_get(name):
     c = ctypes.c_uint64(0)
     _lib.srsgpu_prof_get(name.encode() if name else None, ctypes.byref(t), ctypes.byref(c))
     return t.value, c.value
+
+
+def shard_contiguous(n, world):
+    """srsgpu_shard_contiguous: rank r owns units [first[r], first[r + 1])"""
+    first = (ctypes.c_uint32 * (world + 1))()
+    if _lib.srsgpu_shard_contiguous(n, world, first) != 0:
+        raise ValueError("invalid partition request (n=%d, world=%d)" % (n, world))
+    return list(first)
+
+
+def shard_weighted(weights, world):
+    """srsgpu_shard_weighted: (owner per unit, summed weight per rank), global LPT queue"""
+    w = np.ascontiguousarray(weights, np.uint64)
+    owner = np.zeros(w.size, np.int32)
+    load = np.zeros(world, np.uint64)
+    if _lib.srsgpu_shard_weighted(w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), w.size, world,
+                                  owner.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                  load.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) != 0:
+        raise ValueError("invalid partition request (n=%d, world=%d)" % (w.size, world))
+    return owner, load

@@ -26,23 +26,61 @@ BITS_PER_SYMBOL = {1: 2, 2: 4, 3: 6}
 MAX_CODE_RATE = 0.93  # 36.213 7.1.7: a UE may skip TBs above this effective rate
 
 
+def plan(table, n_sf, prbs=(6, 25, 50, 100), seed=5, mcs=None, full_band=False):
+    """The subframes of one traffic job, deterministic in its arguments (every rank of a sharded
+    job draws the same plan): subframe i belongs to the cell of prbs[i % len(prbs)] and carries one
+    TB with a random allocation of L PRB from PRB 0 and a random MCS (or the pinned ones), redrawn
+    while the code rate exceeds MAX_CODE_RATE. Returns dicts {sf, prb, cell, L, mcs, mod, tbs, nre,
+    sf_idx, lstart} in subframe order."""
+    rng = np.random.default_rng(seed)
+    mods, tbs_tab = table["mod_by_mcs"], table["tbs_by_prb_mcs"]
+    out = [None] * n_sf
+    for ci, prb in enumerate(prbs):
+        cell = s.srsgpu_cell_t(prb, 1 + ci, 1, 1)
+        lstart = 2 if prb <= 10 else 1
+        for j, i in enumerate(i for i in range(n_sf) if i % len(prbs) == ci):
+            sfi = 1 + (j % 4)
+            while True:
+                L = prb if full_band else int(rng.integers(1, prb + 1))
+                m = mcs if mcs is not None else int(rng.integers(0, 29))
+                mod, tbs = mods[m], tbs_tab[L - 1][m]
+                mask = np.zeros((2, prb), np.uint8)
+                mask[:, :L] = 1
+                probe = s.make_sf(sf_idx=sfi, lstart=lstart, prb=mask, nof_prb=prb, mod=mod)
+                nre = s._lib.srsgpu_pdsch_nof_re(ctypes.byref(cell), ctypes.byref(probe))
+                if (tbs + 24) <= MAX_CODE_RATE * nre * BITS_PER_SYMBOL[mod] or mcs is not None:
+                    break
+            out[i] = {"sf": i, "prb": prb, "cell": ci, "L": L, "mcs": m, "mod": mod, "tbs": tbs,
+                      "nre": nre, "sf_idx": sfi, "lstart": lstart}
+    return out
+
+
+def tb_weights(table, sf_plan, max_halfits=8):
+    """decoding cost per planned subframe (sum of K of its TB's code blocks x the budget), the
+    weights of the multi-GPU partition (srsgpu_shard.weighted)"""
+    import srsgpu_shard as sh
+    return [sh.tb_weight(table["cbsegm_C_C1_K1_C2_K2_F"][str(p["tbs"])], max_halfits) for p in sf_plan]
+
+
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
-                 snr_db=30.0, max_halfits=8, mcs=None, full_band=False):
+                 snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
-        traffic)"""
+        traffic). keep: the subframe indices this instance builds and receives (a rank's shard
+        of one planned job, srsgpu_shard); default all."""
         self.torch, self.dev = torch, dev
         self.max_halfits = max_halfits
-        rng = np.random.default_rng(seed)
-        mods, tbs_tab = table["mod_by_mcs"], table["tbs_by_prb_mcs"]
+        sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
+        keep = set(range(n_sf)) if keep is None else set(int(k) for k in keep)
+        self.kept = sorted(keep)
         self.cells = []
-        self.sf_total = n_sf
+        self.sf_total = len(self.kept)
         e_off = d_off = 0
         tb_list = []
         for ci, prb in enumerate(prbs):
-            idx = [i for i in range(n_sf) if i % len(prbs) == ci]
-            n = len(idx)
+            mine = [p for p in sf_plan if p["cell"] == ci and p["sf"] in keep]
+            n = len(mine)
             if n == 0:
                 continue
             N = s.symbol_sz(prb, True)
@@ -53,29 +91,21 @@ class MixedCells:
             c["chest"] = s.Chest(prb, c["id"], max_grids=n, stream=stream)
             c["pd"] = s.Pdsch(prb, c["id"], nof_softbuffers=1, max_cb=13, max_sf=n, stream=stream)
             sfs, e_offs, sf_idx = [], [], []
-            for j in range(n):
-                sfi = 1 + (j % 4)
-                while True:
-                    L = prb if full_band else int(rng.integers(1, prb + 1))
-                    m = mcs if mcs is not None else int(rng.integers(0, 29))
-                    mod, tbs = mods[m], tbs_tab[L - 1][m]
-                    mask = np.zeros((2, prb), np.uint8)
-                    mask[:, :L] = 1
-                    probe = s.make_sf(sf_idx=sfi, lstart=c["lstart"], prb=mask, nof_prb=prb, mod=mod)
-                    nre = c["pd"].nof_re(probe)
-                    qm = BITS_PER_SYMBOL[mod]
-                    if (tbs + 24) <= MAX_CODE_RATE * nre * qm or mcs is not None:
-                        break
-                sf = s.make_sf(sf_idx=sfi, lstart=c["lstart"], prb=mask, nof_prb=prb, mod=mod,
-                               nof_re=nre, rnti=1234, tbs=tbs, softbuffer=len(tb_list),
+            for j, p in enumerate(mine):
+                mask = np.zeros((2, prb), np.uint8)
+                mask[:, :p["L"]] = 1
+                qm = BITS_PER_SYMBOL[p["mod"]]
+                sf = s.make_sf(sf_idx=p["sf_idx"], lstart=p["lstart"], prb=mask, nof_prb=prb, mod=p["mod"],
+                               nof_re=p["nre"], rnti=1234, tbs=p["tbs"], softbuffer=len(tb_list),
                                grid_offset=j * gsz, data_offset=d_off)
                 sfs.append(sf)
                 e_offs.append(e_off)
-                sf_idx.append(sfi)
-                tb_list.append({"tbs": tbs, "rv": 0, "Qm": qm, "nof_e_bits": nre * qm,
-                                "softbuffer": len(tb_list), "e_offset": e_off, "data_offset": d_off})
-                e_off += (nre * qm + 63) // 64 * 64
-                d_off += s.dlsch_data_len(tbs) + 2
+                sf_idx.append(p["sf_idx"])
+                tb_list.append({"tbs": p["tbs"], "rv": 0, "Qm": qm, "nof_e_bits": p["nre"] * qm,
+                                "softbuffer": len(tb_list), "e_offset": e_off, "data_offset": d_off,
+                                "sf": p["sf"]})
+                e_off += (p["nre"] * qm + 63) // 64 * 64
+                d_off += s.dlsch_data_len(p["tbs"]) + 2
             # descriptor arrays built once (the receive step reuses them every batch)
             c.update(sfs=s.make_sf_array(sfs), e_offs=(ctypes.c_uint64 * n)(*e_offs),
                      sf_idx=(ctypes.c_uint32 * n)(*sf_idx))
@@ -85,7 +115,7 @@ class MixedCells:
         self.ntb = len(tb_list)
         self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
         self.bits = sum(t["tbs"] for t in tb_list)
-        self.dlsch = s.Dlsch(self.ntb, max_cb=13, max_cbs_per_call=self.ncb, stream=stream)
+        self.dlsch = s.Dlsch(max(self.ntb, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
         z = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         self.d_e = z(max(e_off, 1), torch.int16)
         self.d_data_tx = torch.randint(0, 256, (max(d_off, 1),), dtype=torch.uint8, device=dev,
