@@ -379,14 +379,15 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
             o = t["data_offset"]
             recs[t["sf"]] = sh.pack_tb_record(r, n, data[o:o + t["tbs"] // 8], m.dlsch.read_cb_crc(t["softbuffer"]),
                                               t["tbs"])
-    local = torch.from_numpy(np.concatenate([recs[i] for i in mine])).to(dev)
+    gdev = dev if (dist and dist.get_backend() == "nccl") else torch.device("cpu")  # gloo: host tensors
+    local = torch.from_numpy(np.concatenate([recs[i] for i in mine])).to(gdev)
     sizes = [sh.tb_record_len(p["tbs"]) for p in sf_plan]
     gather_ms = None
     if dist:
         dist.barrier()
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        sh.gather_records(dist, torch, dev, owner, sizes, local)
+        sh.gather_records(dist, torch, gdev, owner, sizes, local)
         torch.cuda.synchronize()
         gather_ms = round((time.perf_counter() - tg) * 1e3, 3)
     out = {"workload": ("c5_mixed_bw_%dsf_per_gpu_6-25-50-100prb_mcs0-28" % C3_SF if kind == "c5" else
