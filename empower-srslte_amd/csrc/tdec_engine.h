@@ -451,7 +451,10 @@ struct TdecEngine {
   }
 
   // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)
+  int last_n = -1; // the last half-iteration launched (read_state)
+
   int halfit(int n, bool early, bool dec = true) {
+    last_n = n;
     const uint8_t *pd = early ? pair_done : nullptr;
     const TdArrays a = arrays();
     for (int k = 0; k < TD_NKIND; k++) {
@@ -461,6 +464,41 @@ struct TdecEngine {
                                                    "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
       ProfScope ps(names[k], st);
       HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
+    }
+    return 0;
+  }
+
+  // app1 / ext1 of caller CB `cb` as the reference holds them after half-iteration last_n
+  // (turbodecoder_iter.h:283-357): after DEC1 app1 = A and ext1 = DEC1's LLR = E' + A, with
+  // E'[j] = X2[rev[j]]; after DEC2 ext1 = X2[rev[j]] (the subtracted ext1 that was interleaved)
+  // and app1 = A + ext1. All int16 wrapping.
+  int read_state(uint32_t cb, int16_t *app1, int16_t *ext1) {
+    if (last_n < 0) return -1;
+    const TdGroup *g = nullptr;
+    for (const TdGroup &x : groups)
+      if (cb >= (uint32_t)x.cb0 && cb < (uint32_t)(x.cb0 + x.ncb)) g = &x;
+    // groups are in kind order: from kind_g0[TD_KIND_B16] on, the int8 decoders (scaled values)
+    if (!g || (int)(g - groups.data()) >= kind_g0[TD_KIND_B16]) return -1;
+    const uint32_t K = (uint32_t)g->K, nb = (uint32_t)g->nb, c = cb - (uint32_t)g->cb0;
+    const size_t base = (size_t)g->elem0 + (size_t)(c / 2) * t4_pair_elems((int)K, (int)nb);
+    std::vector<uint32_t> a(K), x(K);
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(a.data(), (uint32_t *)A + base, K * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(x.data(), (uint32_t *)XP1 + base, K * 4, hipMemcpyDeviceToHost));
+    std::vector<uint16_t> f, r;
+    gen_interleaver(K, nb, f, r);
+    const int sh = (c & 1) ? 16 : 0;
+    for (uint32_t j = 0; j < K; j++) {
+      // the first DEC1 runs without a priori (app1 still all zero, turbodecoder_iter.h:318-323)
+      // and leaves A unwritten
+      const uint16_t av = last_n == 0 ? 0 : (uint16_t)(a[j] >> sh), ev = (uint16_t)(x[r[j]] >> sh);
+      if (last_n & 1) {
+        ext1[j] = (int16_t)ev;
+        app1[j] = (int16_t)(uint16_t)(av + ev);
+      } else {
+        app1[j] = (int16_t)av;
+        ext1[j] = (int16_t)(uint16_t)(ev + av);
+      }
     }
     return 0;
   }

@@ -206,6 +206,11 @@ int srsgpu_tdec_batch_decode_dev(srsgpu_tdec_batch_t *q, int impl, int sb_layout
                      d_noi);
 }
 
+int srsgpu_tdec_batch_read_state(srsgpu_tdec_batch_t *q, uint32_t cb, int16_t *app1, int16_t *ext1) {
+  if (!q || !app1 || !ext1) return -1;
+  return q->e.read_state(cb, app1, ext1);
+}
+
 static int host_stage_in(Engine &e, int impl, int sb_layout, const int16_t *const *input, uint32_t K,
                          uint32_t n, size_t *stride) {
   if (n > e.cap_cbs || K > e.cap_K || cb_index(K) < 0) {

@@ -123,6 +123,7 @@ _sig = {
     "srsgpu_tdec_batch_decode": (_i32, [_vp, _i32, _i32, ctypes.POINTER(_vp), _u32, _u32, _u32,
                                         _u32, _u32, ctypes.POINTER(_vp), _u8p, _u32p]),
     "srsgpu_tdec_input_len": (_u32, [_i32, _i32, _u32]),
+    "srsgpu_tdec_batch_read_state": (_i32, [_vp, _u32, _i16p, _i16p]),
     "srsgpu_dlsch_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32, _u32]),
     "srsgpu_dlsch_destroy": (None, [_vp]),
     "srsgpu_dlsch_set_stream": (None, [_vp, _vp]),
@@ -262,6 +263,13 @@ class TdecBatch:
         return _lib.srsgpu_tdec_batch_decode_dev(self.q, impl, sb, _vp(d_in), in_stride, K, n,
                                                  maxh, poly, crc_len, _vp(d_out), out_stride,
                                                  _vp(d_ok), _vp(d_noi))
+
+    def read_state(self, cb, K):
+        """(app1, ext1) of code block cb after the last half-iteration, reference index space"""
+        app1, ext1 = np.zeros(K, np.int16), np.zeros(K, np.int16)
+        if _lib.srsgpu_tdec_batch_read_state(self.q, cb, _i16(app1), _i16(ext1)) != 0:
+            raise RuntimeError("srsgpu_tdec_batch_read_state failed")
+        return app1, ext1
 
     # ---- host numpy arrays ----
     def run(self, impl, sb, inputs, K, nhalf):

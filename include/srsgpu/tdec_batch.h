@@ -71,6 +71,15 @@ int srsgpu_tdec_batch_decode(srsgpu_tdec_batch_t *q, int impl, int sb_layout,
                              uint32_t max_halfits, uint32_t crc_poly, uint32_t crc_len_bits,
                              uint8_t *const *output, uint8_t *crc_ok, uint32_t *noi);
 
+/* Decoder state of code block `cb` after the last half-iteration of the last job (run or
+ * decode, the 16-bit decoders), as the reference holds it in srslte_tdec_t: app1 and ext1, K int16
+ * each, in the decoder's own index space (sub-block order for the windowed decoders, natural for
+ * SSE / generic), turbodecoder_iter.h:283-357. The device keeps A = app1 - ext1 and app2 =
+ * interleave(ext1 ...); this reconstructs both arrays exactly (the subtractions wrap, so they
+ * invert modulo 2^16). Synchronises the batch stream. Returns 0, or -1 if there is no such CB or
+ * the last job ran an 8-bit decoder. */
+int srsgpu_tdec_batch_read_state(srsgpu_tdec_batch_t *q, uint32_t cb, int16_t *app1, int16_t *ext1);
+
 /* Input length (int16 elements) one CB needs for (impl, sb_layout, K). */
 uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t long_cb);
 

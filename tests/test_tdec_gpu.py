@@ -67,6 +67,64 @@ def test_golden_run_all_batch(batch, golden):
         assert (out[0] == z[c["key"] + "_dec"][-1]).all(), c["key"]
 
 
+def test_golden_extrinsics_batch(batch, golden):
+    """SURVEY §8(a)'s int16 parity: the decoder state app1 / ext1 (srslte_tdec_t, reference
+    index space) after the last half-iteration equals the reference's recorded arrays, for every
+    golden run case; three copies per case put the block in both halves of a pair."""
+    z, manifest = golden
+    n = 0
+    for c in manifest:
+        if c["kind"] != "run":
+            continue
+        K, inp = c["K"], z[c["key"] + "_in"]
+        out = batch.run(c["impl"], c["sb"], [inp, inp, inp], K, c["halfits"])
+        assert (out[0] == z[c["key"] + "_dec"][-1]).all(), c["key"]
+        for cb in range(3):
+            app1, ext1 = batch.read_state(cb, K)
+            assert (app1 == z[c["key"] + "_app1"]).all(), (c["key"], cb)
+            assert (ext1 == z[c["key"] + "_ext1"]).all(), (c["key"], cb)
+        n += 1
+    assert n >= 30
+
+
+@pytest.mark.parametrize("impl,K,sb", [(AUTO, 6144, 1), (AUTO, 5824, 0), (AUTO, 800, 1), (AUTO, 408, 0),
+                                       (AUTO, 400, 0), (GENERIC, 1024, 0), (SSE_WINDOW, 1024, 0)])
+def test_extrinsics_every_halfiteration_vs_oracle(batch, oracle, impl, K, sb):
+    """app1 / ext1 after every half-iteration count 1..8 equal the oracle's (the restatement
+    pinned to the reference by test_oracle.py), odd batch: both pair halves and a padded pair"""
+    rng = np.random.default_rng(K + impl)
+    ins = []
+    for i in range(5):
+        _, llr = make_cb(K, float(rng.uniform(0.5, 3.0)), int(rng.integers(1 << 30)), oracle)
+        ins.append(_sb_input(oracle, llr, K, sb) if impl == AUTO else llr)
+    for nh in range(1, 9):
+        batch.run(impl, sb, ins, K, nh)
+        for i in range(len(ins)):
+            _, app1, ext1 = oracle.tdec_run(impl, sb, ins[i], K, nh)
+            g1, g2 = batch.read_state(i, K)
+            assert (g1 == app1).all() and (g2 == ext1).all(), (impl, K, sb, nh, i)
+
+
+def test_kat_decode(batch, oracle):
+    """the reference's 504-bit known-answer vectors (tests/golden/tdec_kat.npz, see test_kat.py):
+    the KAT's coded bits as +-100 LLRs decode to known_data with every decoder; with AWGN at the
+    KAT's 0.5 dB (our own PRNG) the GPU equals the oracle bit for bit"""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tdec_kat.npz"))
+    data, enc = z["known_data"], z["known_data_encoded"]
+    clean = np.where(enc == 1, 100, -100).astype(np.int16)
+    rng = np.random.default_rng(504)
+    esno = 0.5 + 10 * np.log10(1 / 3)
+    noisy = (100 * (np.where(enc == 1, 1.0, -1.0) + np.sqrt(1 / 10 ** (esno / 10)) *
+                    rng.standard_normal(enc.size))).astype(np.float32).astype(np.int16)
+    for impl in (AUTO, GENERIC, SSE, SSE_WINDOW):
+        out = batch.run(impl, 0, [clean], 504, 8)
+        assert (out[0] == pack_bits(data)).all(), impl
+        for nh in (2, 4, 8):
+            got = batch.run(impl, 0, [noisy], 504, nh)[0]
+            assert (got == oracle.tdec_run(impl, 0, noisy, 504, nh)[0][-1]).all(), (impl, nh)
+
+
 def test_golden_early_stop_batch(batch, golden):
     z, manifest = golden
     for c in manifest:
