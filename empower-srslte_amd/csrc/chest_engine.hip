@@ -48,10 +48,11 @@ struct ChestEngine {
   hipStream_t st = nullptr;
   srsgpu_cell_t cell{};
   uint32_t cap = 0;
-  float2 *d_crs = nullptr;
+  float2 *d_crs = nullptr, *d_pss = nullptr;
   float *d_filt = nullptr;
+  srsgpu_chest_cfg_t cfg{};
   int flen = 3;
-  float filt[16] = {0.1f, 1 - 2 * 0.1f, 0.1f};
+  float filt[64] = {0.1f, 1 - 2 * 0.1f, 0.1f};
   bool filt_dirty = true;
   ChestItem *h_items = nullptr, *d_items = nullptr;
   hipEvent_t staged = nullptr;
@@ -69,7 +70,21 @@ struct ChestEngine {
     crs_table(c.nof_prb, c.id, t);
     HIPCHK(hipMalloc(&d_crs, t.size() * 4));
     HIPCHK(hipMemcpy(d_crs, t.data(), t.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&d_filt, 16 * 4));
+    HIPCHK(hipMalloc(&d_filt, 64 * 4));
+    // PSS of N_id_2 = id % 3 for the PSS noise estimate (sync/pss.c:354-382)
+    float pss[2 * 62];
+    const float root[3] = {25.0f, 29.0f, 34.0f};
+    for (int i = 0; i < 62; i++) { // the argument in double precision, rounded to float (pss.c:370-377)
+      const float fi = (float)i;
+      const float arg = i < 31 ? (float)((float)-1 * M_PI * root[c.id % 3] * (fi * (fi + 1.0)) / 63.0)
+                               : (float)((float)-1 * M_PI * root[c.id % 3] * ((fi + 2.0) * (fi + 1.0)) / 63.0);
+      pss[2 * i] = cosf(arg);
+      pss[2 * i + 1] = sinf(arg);
+    }
+    HIPCHK(hipMalloc(&d_pss, sizeof(pss)));
+    HIPCHK(hipMemcpy(d_pss, pss, sizeof(pss), hipMemcpyHostToDevice));
+    cfg.symbol_sz = c.nof_prb <= 6 ? 128 : c.nof_prb <= 15 ? 256 : c.nof_prb <= 25 ? 384
+                  : c.nof_prb <= 50 ? 768 : c.nof_prb <= 75 ? 1024 : 1536;
     HIPCHK(hipHostMalloc(&h_items, sizeof(ChestItem) * n));
     HIPCHK(hipMalloc(&d_items, sizeof(ChestItem) * n));
     HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
@@ -78,14 +93,14 @@ struct ChestEngine {
 
   void destroy() {
     if (st) (void)hipStreamSynchronize(st);
-    for (void *p : {(void *)d_crs, (void *)d_filt, (void *)d_items})
+    for (void *p : {(void *)d_crs, (void *)d_pss, (void *)d_filt, (void *)d_items})
       if (p) (void)hipFree(p);
     if (h_items) (void)hipHostFree(h_items);
     if (staged) (void)hipEventDestroy(staged);
   }
 
   int estimate(const uint32_t *sf_idx, uint32_t n, const float *d_grid, size_t stride, float *d_ce,
-               float *d_noise) {
+               float *d_noise, float *d_meas) {
     if (n > cap) {
       fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
       return -1;
@@ -103,17 +118,30 @@ struct ChestEngine {
         t.grid = (const float2 *)d_grid + i * stride;
         t.ce = (float2 *)d_ce + (i * np + p) * stride;
         t.noise = d_noise ? d_noise + i * np + p : nullptr;
+        t.meas = d_meas ? d_meas + (size_t)(i * np + p) * 4 : nullptr;
         t.sf_idx = sf_idx[i];
         t.port = p;
+        t.cfo = cfg.cfo_estimate_enable && ((1u << sf_idx[i]) & cfg.cfo_estimate_sf_mask); // chest_dl.c:607
+        t.pad = 0;
       }
     }
     HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
     // chest_dl.c:620-621: no smoothing for an empty filter or a 3-tap one with w == 0
-    const int fl = (flen == 3 && filt[0] == 0.f) ? 0 : flen;
+    ChestCfg kc;
+    kc.nprb = (int)cell.nof_prb;
+    kc.cell_id = (int)cell.id;
+    kc.nof_ports = (int)np;
+    kc.flen = (flen == 3 && filt[0] == 0.f) ? 0 : flen;
+    kc.average = cfg.average_subframe ? 1 : 0;
+    kc.noise_alg = (int)cfg.noise_alg;
+    kc.filt_auto = cfg.smooth_filter_auto ? 1 : 0;
+    kc.rsrp_neighbour = cfg.rsrp_neighbour ? 1 : 0;
+    kc.cfo_n = (float)cfg.symbol_sz;
+    kc.cfo_ng = ceilf((144.0f * (float)cfg.symbol_sz) / 2048.0f); // SRSLTE_CP_LEN_NORM(1, n)
     ProfScope ps("k_chest", st);
-    HIPCHK(launch_chest(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, d_crs, d_filt, fl, st));
+    HIPCHK(launch_chest(d_items, (int)(n * np), kc, d_crs, d_filt, d_pss, st));
     return 0;
   }
 
@@ -131,6 +159,8 @@ struct ChestEngine {
         t.grid = nullptr;
         t.ce = (float2 *)d_grid + (i * np + p) * stride;
         t.noise = nullptr;
+        t.meas = nullptr;
+        t.cfo = 0;
         t.sf_idx = sf_idx[i];
         t.port = p;
       }
@@ -175,8 +205,8 @@ void srsgpu_chest_set_stream(srsgpu_chest_t *q, void *s) {
 }
 
 int srsgpu_chest_set_smooth_filter(srsgpu_chest_t *q, const float *f, uint32_t len) {
-  if (!q || len >= 16 || (len && !(len % 2)) || (len && !f)) {
-    fprintf(stderr, "srsgpu: smoothing filter must have an odd length below 16\n");
+  if (!q || len >= 65 || (len && !f)) { // chest_dl.c:427: below SRSLTE_CHEST_MAX_SMOOTH_FIL_LEN
+    fprintf(stderr, "srsgpu: smoothing filter must be shorter than 65 taps\n");
     return -1;
   }
   q->e.flen = (int)len;
@@ -194,10 +224,25 @@ void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w) { // ches
   q->e.filt_dirty = true;
 }
 
+int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg) {
+  if (!q || !cfg || cfg->noise_alg > 2 || !cfg->symbol_sz) return -1;
+  q->e.cfg = *cfg;
+  return 0;
+}
+
+int srsgpu_chest_estimate_meas_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, const float *d_grid,
+                                   size_t stride, float *d_ce, float *d_noise, float *d_meas) {
+  if (!q || (!sf_idx && n) || !d_grid || !d_ce) return -1;
+  if (q->e.cfg.smooth_filter_auto && !d_noise) {
+    fprintf(stderr, "srsgpu: smooth_filter_auto needs the noise estimate array\n");
+    return -1;
+  }
+  return q->e.estimate(sf_idx, n, d_grid, stride, d_ce, d_noise, d_meas);
+}
+
 int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, const float *d_grid,
                               size_t stride, float *d_ce, float *d_noise) {
-  if (!q || (!sf_idx && n) || !d_grid || !d_ce) return -1;
-  return q->e.estimate(sf_idx, n, d_grid, stride, d_ce, d_noise);
+  return srsgpu_chest_estimate_meas_dev(q, sf_idx, n, d_grid, stride, d_ce, d_noise, nullptr);
 }
 
 int srsgpu_chest_put_crs_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, float *d_grid,

@@ -1,20 +1,28 @@
-// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0 and 1) for the
-// normal-CP, non-MBSFN, per-symbol (average_subframe off) configuration
-// (reference: lib/src/phy/ch_estimation/chest_dl.c:641-694 and the helpers it calls):
+// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0 and 1) for
+// normal-CP, non-MBSFN subframes, in every configuration srsUE's phch_worker sets
+// (srsue/src/phy/phch_worker.cc:149,553-565; reference: lib/src/phy/ch_estimation/chest_dl.c:641-694
+// and the helpers it calls):
 //   1. least squares   pilots received at the CRS REs of symbols 0/4/7/11 (refsignal_cs_get_sf,
 //                      refsignal_dl.c:404-430) times conj(CRS) (refsignal_dl.c:265-318)
-//   2. noise           estimate_noise_pilots (chest_dl.c:268-329), REFS algorithm, including its
-//                      reference behaviour of keeping only the last symbol's residual power
-//   3. smoothing       srslte_conv_same_cf with extrapolated extremes (convolution.c:172-211),
-//                      default 3-tap [w, 1-2w, w] (chest_dl.c:155-160, 464-469)
-//   4. frequency       srslte_interp_linear_offset per CRS symbol (interp.c:245-272), M = 6
-//   5. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:392-397,
-//                      interp.c:150-173): running sums of (ce_b - ce_a) / d
+//   2. measurements    RSRP, RSSI (chest_dl.c:500-511), RSRP correlation (:652-656), CFO (:562-587)
+//   3. noise (REFS)    estimate_noise_pilots (chest_dl.c:268-329), including its reference behaviour
+//                      of keeping only the last symbol's residual power
+//   4. filter          fixed taps, or smooth_filter_auto's order-4 Gaussian with std dev = noise x 200
+//                      (chest_dl.c:471-490, 616-618)
+//   5. average/smooth  average_subframe: the 4 CRS symbols folded into one row at spacing 3
+//                      (chest_dl.c:528-548); srslte_conv_same_cf with extrapolated extremes
+//                      (convolution.c:172-211)
+//   6. frequency       srslte_interp_linear_offset (interp.c:245-272): per CRS symbol with M = 6, or
+//                      the averaged row with M = 3 and offset cell_id % 3 (chest_dl.c:393-399)
+//   7. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:416-421,
+//                      interp.c:150-173), or the averaged row copied to all 14 symbols (:410-414)
+//   8. noise (PSS/EMPTY) in subframes 0 and 5 only (chest_dl.c:628-637, 332-361)
 // One workgroup per (subframe, rx antenna, port): pilots and their smoothed copy stay in LDS, each
 // thread then produces whole subcarrier columns (14 symbols) in registers and streams them out.
 // Float arithmetic in the reference's operation order; the stage is checked with a tolerance
 // (float stages 1e-4 relative).
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "chest_kernels.h"
@@ -29,139 +37,243 @@ struct c32 {
 __device__ __forceinline__ c32 cadd(c32 a, c32 b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ c32 csub(c32 a, c32 b) { return {a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ c32 cscale(c32 a, float s) { return {a.x * s, a.y * s}; }
+__device__ __forceinline__ c32 cmul(c32 a, c32 b) { return {a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
 __device__ __forceinline__ c32 cmulconj(c32 a, c32 b) { // a * conj(b)
   return {a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y};
 }
+__device__ __forceinline__ float cpow(c32 a) { return a.x * a.x + a.y * a.y; }
 
 #define CH_MAXP (2 * 110) // pilots per CRS symbol
+#define CH_NRED 7
 
-__global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ items, int nitems,
-                                               int nprb, int cell_id, const float2 *__restrict__ crs,
-                                               const float *__restrict__ filt, int flen) {
-  __shared__ c32 ls[4][CH_MAXP];
-  __shared__ c32 sm[4][CH_MAXP];
-  __shared__ float red[256];
+// block-wide sums of nv per-thread values (block-uniform call); results in red[j][0]
+__device__ __forceinline__ void block_sum(float (*red)[256], const float *v, int nv) {
+  for (int j = 0; j < nv; j++) red[j][threadIdx.x] = v[j];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int j = 0; j < nv; j++) red[j][threadIdx.x] += red[j][threadIdx.x + s];
+    __syncthreads();
+  }
+}
+
+// srslte_conv_same_cf output i (convolution.c:172-211), any filter length M: outputs i < M/2 read
+// first[], outputs i >= N - M/2 read last[], both with extrapolated extremes
+__device__ __forceinline__ c32 conv_same_at(const c32 *in, int N, int i, const float *f, int M) {
+  const int h = M / 2;
+  c32 acc = {0.f, 0.f};
+  for (int k = 0; k < M; k++) {
+    c32 v;
+    if (i < h) { // first[q] = (2 + h - q) in[1] - (1 + h - q) in[0] for q < h, else in[q - h]
+      const int q = i + k;
+      v = q < h ? csub(cscale(in[1], (float)(2 + h - q)), cscale(in[0], (float)(1 + h - q))) : in[q - h];
+    } else if (i < N - h) {
+      v = in[i - h + k];
+    } else { // last[q] = (2 + q - h) in[N-1] - (1 + q - h) in[N-2] for q >= M - 1, else in[N-M+q+1]
+      const int q = i - (N - h) + k;
+      v = q >= M - 1 ? csub(cscale(in[N - 1], (float)(2 + q - h)), cscale(in[N - 2], (float)(1 + q - h)))
+                     : in[N - M + q + 1];
+    }
+    acc = cadd(acc, cscale(v, f[k]));
+  }
+  return acc;
+}
+
+// srslte_interp_linear_offset output k (interp.c:245-272): n inputs, M outputs per input, off_st
+// extrapolated ahead, diff_vec = (in[i+1] - in[i]) * (1/M) times the ramp j
+__device__ __forceinline__ c32 interp_at(const c32 *in, int n, int k, int off, int M, float invM) {
+  if (k < off) { // output[off-j-1] = in[0] - (j+1) (in[1]-in[0]) / M
+    const c32 v = cscale(csub(in[1], in[0]), (float)(off - k)); // complex / (M + 0i)
+    return csub(in[0], c32{v.x / (float)M, v.y / (float)M});
+  }
+  const int tt = k - off, i = tt / M, j = tt % M;
+  if (i < n - 1) return cadd(in[i], cscale(cscale(csub(in[i + 1], in[i]), invM), (float)j));
+  const c32 v = cscale(csub(in[n - 1], in[n - 2]), (float)j);
+  return cadd(in[n - 1], c32{v.x / (float)M, v.y / (float)M});
+}
+
+__global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ items, int nitems, ChestCfg cfg,
+                                               const float2 *__restrict__ crs, const float *__restrict__ filt,
+                                               const float2 *__restrict__ pss) {
+  __shared__ c32 ls[4 * CH_MAXP]; // LS estimates, row l at l * np (the reference's pilot_estimates)
+  __shared__ c32 sm[4 * CH_MAXP];
+  __shared__ float red[CH_NRED][256];
+  __shared__ float fs[64];
+  __shared__ float s_noise;
   const int it = blockIdx.x;
   if (it >= nitems) return;
   const ChestItem t = items[it];
-  const int np = 2 * nprb, nsc = 12 * nprb;
+  const int nprb = cfg.nprb, cell_id = cfg.cell_id, np = 2 * nprb, nsc = 12 * nprb;
   const c32 *grid = (const c32 *)t.grid;
   const c32 *pil = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);
   const int sym[4] = {0, 4, 7, 11};
   const int port = (int)t.port;
+  const int tid = threadIdx.x;
+  auto fidx = [&](int l) { return (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6; };
   // 1. LS: v = 0 / 3 alternating over the CRS symbols (port 1: 3 / 0), fidx = (v + id % 6) % 6;
   //    ports 0 and 1 share the pilot sequence (csr_refs.pilots[port / 2])
-  for (int e = threadIdx.x; e < 4 * np; e += blockDim.x) {
+  for (int e = tid; e < 4 * np; e += blockDim.x) {
     const int l = e / np, m = e % np;
-    const int f = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
-    ls[l][m] = cmulconj(grid[sym[l] * nsc + f + 6 * m], pil[l * np + m]);
+    ls[e] = cmulconj(grid[sym[l] * nsc + fidx(l) + 6 * m], pil[e]);
   }
   __syncthreads();
-  // 2. noise (REFS): residual of the last CRS symbol against its 4 staggered neighbours in the
-  //    symbols around it (bottom one extrapolated as 2 ls[2] - ls[0]), power / 4 * sqrt(5)
-  if (t.noise) {
-    const int f0 = ((port ? 3 : 0) + cell_id % 6) % 6; // srslte_refsignal_cs_fidx(cell, 0, port, 0)
-    const int off = f0 < 3 ? 0 : 1; // ((fidx < 3) ^ (4 & 1)) ? 0 : 1
-    float acc = 0.f;
-    for (int k = threadIdx.x; k < np; k += blockDim.x) {
-      c32 tmp = ls[3][k];
-      for (int nb = 0; nb < 2; nb++) {
-        auto row = [&](int q) -> c32 {
-          return nb == 0 ? ls[2][q] : csub(cscale(ls[2][q], 2.0f), ls[0][q]);
-        };
-        if (k >= off) tmp = cadd(tmp, row(k - off));            // tmp[off + t] += prev[t]
-        if (k < np + off - 1) tmp = cadd(tmp, row(1 - off + k)); // tmp[t] += prev[1 - off + t]
-        if (off && k == 0) tmp = cadd(tmp, csub(cscale(row(0), 2.0f), row(1)));
-        if (!off && k == np - 1) tmp = cadd(tmp, csub(cscale(row(np - 2), 2.0f), row(np - 1)));
+  // 2 + 3. block sums: REFS residual power, RSRP, RSSI, sum of estimates, CFO correlation
+  const bool refs = cfg.noise_alg == 0 && (t.noise || cfg.filt_auto);
+  if (refs || t.meas) {
+    float v[CH_NRED] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (refs) { // residual of the last CRS symbol against its staggered neighbours (bottom one
+                // extrapolated as 2 ls[2] - ls[0]), power / 4 * sqrt(5)
+      const int off = fidx(0) < 3 ? 0 : 1; // ((fidx < 3) ^ (4 & 1)) ? 0 : 1
+      const c32 *r0 = ls, *r2 = ls + 2 * np, *r3 = ls + 3 * np;
+      for (int k = tid; k < np; k += blockDim.x) {
+        c32 tmp = r3[k];
+        for (int nb = 0; nb < 2; nb++) {
+          auto row = [&](int q) -> c32 { return nb == 0 ? r2[q] : csub(cscale(r2[q], 2.0f), r0[q]); };
+          if (k >= off) tmp = cadd(tmp, row(k - off));            // tmp[off + t] += prev[t]
+          if (k < np + off - 1) tmp = cadd(tmp, row(1 - off + k)); // tmp[t] += prev[1 - off + t]
+          if (off && k == 0) tmp = cadd(tmp, csub(cscale(row(0), 2.0f), row(1)));
+          if (!off && k == np - 1) tmp = cadd(tmp, csub(cscale(row(np - 2), 2.0f), row(np - 1)));
+        }
+        tmp = cscale(tmp, 1.0f / 5.0f);
+        v[0] += cpow(csub(r3[k], tmp));
       }
-      tmp = cscale(tmp, 1.0f / 5.0f);
-      const c32 r = csub(ls[3][k], tmp);
-      acc += r.x * r.x + r.y * r.y;
     }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) *t.noise = red[0] / (float)np / 4.0f * sqrtf(5.0f);
-  }
-  // 3. smoothing (conv_same with extrapolated extremes); flen == 0: none
-  for (int e = threadIdx.x; e < 4 * np; e += blockDim.x) {
-    const int l = e / np, i = e % np;
-    if (flen == 0) {
-      sm[l][i] = ls[l][i];
-      continue;
-    }
-    const int M = flen, h = M / 2;
-    c32 acc = {0.f, 0.f};
-    for (int k = 0; k < M; k++) {
-      const int src = i - h + k;
-      c32 v;
-      if (src < 0) { // first[i] = (2 + h - q) in[1] - (1 + h - q) in[0], q = i + k
-        const float q = (float)(i + k);
-        v = csub(cscale(ls[l][1], 2.0f + h - q), cscale(ls[l][0], 1.0f + h - q));
-      } else if (src >= np) { // last[q] = (2 + q - h) in[N-1] - (1 + q - h) in[N-2]
-        const float q = (float)(src - (np - M + 1) + 0);
-        v = csub(cscale(ls[l][np - 1], 2.0f + q - h), cscale(ls[l][np - 2], 1.0f + q - h));
-      } else {
-        v = ls[l][src];
+    if (t.meas) {
+      for (int e = tid; e < 4 * np; e += blockDim.x) {
+        const int l = e / np, m = e % np;
+        v[1] += cpow(grid[sym[l] * nsc + fidx(l) + 6 * m]); // pilot_recv_signal power
+        v[3] += ls[e].x;
+        v[4] += ls[e].y;
       }
-      acc = cadd(acc, cscale(v, filt[k]));
+      for (int e = tid; e < 4 * nsc; e += blockDim.x) v[2] += cpow(grid[sym[e / nsc] * nsc + e % nsc]);
+      for (int e = tid; e < 2 * np; e += blockDim.x) { // slot 0 against slot 1, per CRS symbol
+        const c32 p = cmulconj(ls[e], ls[e + 2 * np]);
+        v[5] += p.x;
+        v[6] += p.y;
+      }
     }
-    sm[l][i] = acc;
-  }
-  __syncthreads();
-  // 4 + 5. per subcarrier column: frequency interpolation of the 4 CRS symbols, then time
-  c32 *ce = (c32 *)t.ce;
-  const float inv6 = 1.0f / 6.0f;
-  for (int k = threadIdx.x; k < nsc; k += blockDim.x) {
-    c32 f[4];
-    for (int l = 0; l < 4; l++) {
-      const int fo = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
-      const c32 *in = sm[l];
-      if (k < fo) { // output[fo-j-1] = in[0] - (j+1) (in[1]-in[0]) / M
-        const int j = fo - 1 - k;
-        const c32 v = cscale(csub(in[1], in[0]), (float)(j + 1)); // complex / (6 + 0i)
-        f[l] = csub(in[0], c32{v.x / 6.0f, v.y / 6.0f});
-      } else {
-        const int tt = k - fo, i = tt / 6, j = tt % 6;
-        if (i < np - 1)
-          f[l] = cadd(in[i], cscale(cscale(csub(in[i + 1], in[i]), inv6), (float)j));
-        else
-        {
-          const c32 v = cscale(csub(in[np - 1], in[np - 2]), (float)j);
-          f[l] = cadd(in[np - 1], c32{v.x / 6.0f, v.y / 6.0f});
+    block_sum(red, v, CH_NRED);
+    if (tid == 0) {
+      if (refs) {
+        s_noise = red[0][0] / (float)np / 4.0f * sqrtf(5.0f);
+        if (t.noise) *t.noise = s_noise;
+      }
+      if (t.meas) {
+        const float npil = (float)(4 * np);
+        t.meas[0] = red[1][0] / npil;
+        t.meas[1] = red[2][0] / 4.0f;
+        if (cfg.rsrp_neighbour) {
+          const double e = hypot((double)(red[3][0] / npil), (double)(red[4][0] / npil));
+          t.meas[2] = (float)(e * e);
+        }
+        if (t.cfo) {
+          const float a = -atan2f(red[6][0], red[5][0]) * cfg.cfo_n / (7.0f * (cfg.cfo_n + cfg.cfo_ng)) / 2;
+          t.meas[3] = (float)((double)a / M_PI);
         }
       }
     }
-    c32 col[14];
-    col[0] = f[0];
-    col[4] = f[1];
-    col[7] = f[2];
-    col[11] = f[3];
-    c32 d = cscale(csub(f[1], f[0]), 0.25f); // symbols 1-3: d = 4
-    col[1] = cadd(f[0], d);
-    col[2] = cadd(col[1], d);
-    col[3] = cadd(col[2], d);
-    d = cscale(csub(f[2], f[1]), 1.0f / 3.0f); // symbols 5-6: d = 3
-    col[5] = cadd(f[1], d);
-    col[6] = cadd(col[5], d);
-    d = cscale(csub(f[3], f[2]), 0.25f); // symbols 8-10, then 12-13 extrapolated from 11
-    col[8] = cadd(f[2], d);
-    col[9] = cadd(col[8], d);
-    col[10] = cadd(col[9], d);
-    col[12] = cadd(f[3], d);
-    col[13] = cadd(col[12], d);
-    for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
+  }
+  // 4. filter taps
+  if (tid == 0) {
+    if (cfg.noise_alg != 0) s_noise = t.noise ? *t.noise : 0.f;
+    if (cfg.filt_auto) { // srslte_chest_dl_set_smooth_filter_gauss(q, 4, noise * 200)
+      const float sd = s_noise * 200.0f;
+      float norm = 0.f;
+      for (int i = 0; i < 5; i++) {
+        fs[i] = expf(-powf((float)(i - 2), 2) / (2.0f * powf(sd, 2)));
+        norm += fs[i];
+      }
+      const float inv = 1.0f / norm;
+      for (int i = 0; i < 5; i++) fs[i] *= inv;
+    } else {
+      for (int i = 0; i < cfg.flen; i++) fs[i] = filt[i];
+    }
+  }
+  __syncthreads();
+  const int fl = cfg.filt_auto ? 5 : cfg.flen;
+  // 5. averaging / smoothing; rows: what the frequency interpolation reads
+  const c32 *rows = ls;
+  if (cfg.average) {
+    if (fl) { // average_pilots: interleave the slot pairs, scale 2 / 4, then smooth the 2np row
+      const int a = fidx(0) < 3 ? 0 : 1, b = 1 - a;
+      for (int m = tid; m < np; m += blockDim.x) {
+        sm[2 * m] = cscale(cadd(ls[a * np + m], ls[(a + 2) * np + m]), 0.5f);
+        sm[2 * m + 1] = cscale(cadd(ls[b * np + m], ls[(b + 2) * np + m]), 0.5f);
+      }
+      __syncthreads();
+      for (int i = tid; i < 2 * np; i += blockDim.x) ls[i] = conv_same_at(sm, 2 * np, i, fs, fl);
+      __syncthreads();
+    } // no smoothing: the raw buffer (symbols 0 and 4 back to back) is interpolated as the row
+  } else if (fl) {
+    for (int e = tid; e < 4 * np; e += blockDim.x) {
+      const int l = e / np;
+      sm[e] = conv_same_at(ls + l * np, np, e - l * np, fs, fl);
+    }
+    __syncthreads();
+    rows = sm;
+  }
+  // 6 + 7. per subcarrier column: frequency interpolation, then time
+  c32 *ce = (c32 *)t.ce;
+  const bool nz05 = t.noise && cfg.noise_alg != 0 && (t.sf_idx == 0 || t.sf_idx == 5);
+  const bool pss_on = nz05 && cfg.noise_alg == 1;
+  const int k0 = nsc / 2 - 31; // srslte_pss_get_slot position within symbol 6
+  float pacc = 0.f;
+  for (int k = tid; k < nsc; k += blockDim.x) {
+    c32 c6;
+    if (cfg.average) {
+      const c32 v = interp_at(rows, 2 * np, k, cell_id % 3, 3, 1.0f / 3);
+      for (int s = 0; s < 14; s++) ce[s * nsc + k] = v;
+      c6 = v;
+    } else {
+      c32 f[4];
+      for (int l = 0; l < 4; l++) f[l] = interp_at(rows + l * np, np, k, fidx(l), 6, 1.0f / 6);
+      c32 col[14];
+      col[0] = f[0];
+      col[4] = f[1];
+      col[7] = f[2];
+      col[11] = f[3];
+      c32 d = cscale(csub(f[1], f[0]), 0.25f); // symbols 1-3: d = 4
+      col[1] = cadd(f[0], d);
+      col[2] = cadd(col[1], d);
+      col[3] = cadd(col[2], d);
+      d = cscale(csub(f[2], f[1]), 1.0f / 3.0f); // symbols 5-6: d = 3
+      col[5] = cadd(f[1], d);
+      col[6] = cadd(col[5], d);
+      d = cscale(csub(f[3], f[2]), 0.25f); // symbols 8-10, then 12-13 extrapolated from 11
+      col[8] = cadd(f[2], d);
+      col[9] = cadd(col[8], d);
+      col[10] = cadd(col[9], d);
+      col[12] = cadd(f[3], d);
+      col[13] = cadd(col[12], d);
+      for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
+      c6 = col[6];
+    }
+    if (pss_on && k >= k0 && k < k0 + 62) // estimate_noise_pss: ce * PSS - received
+      pacc += cpow(csub(cmul(c6, ((const c32 *)pss)[k - k0]), grid[6 * nsc + k]));
+  }
+  // 8. PSS / EMPTY noise, subframes 0 and 5 only (otherwise the value is left as it was)
+  if (pss_on) {
+    block_sum(red, &pacc, 1);
+    if (tid == 0) *t.noise = (float)((double)((float)cfg.nof_ports * (red[0][0] / 62.0f)) / sqrt(2.0));
+  } else if (nz05 && tid == 0) { // estimate_noise_empty_sc: 5 empty subcarriers either side of SSS / PSS
+    float np_ = 0.f;
+    for (int s = 5; s <= 6; s++) {
+      const int kk = s * nsc + k0;
+      for (int side = 0; side < 2; side++) {
+        const c32 *x = grid + (side ? kk + 62 : kk - 5);
+        float acc = 0.f;
+        for (int i = 0; i < 5; i++) acc += cpow(x[i]);
+        np_ += acc / 5.0f;
+      }
+    }
+    *t.noise = np_;
   }
 }
 
-hipError_t launch_chest(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
-                        const float *filt, int flen, hipStream_t st) {
+hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, const float2 *crs,
+                        const float *filt, const float2 *pss, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chest, dim3((unsigned)n), dim3(256), 0, st, d_items, n, nprb, cell_id, crs, filt,
-                     flen);
+  hipLaunchKernelGGL(k_chest, dim3((unsigned)n), dim3(256), 0, st, d_items, n, cfg, crs, filt, pss);
   return hipGetLastError();
 }
 

@@ -159,6 +159,8 @@ _sig = {
     "srsgpu_chest_set_smooth_filter": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _u32]),
     "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
+    "srsgpu_chest_estimate_meas_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp, _vp]),
+    "srsgpu_chest_set_cfg": (_i32, [_vp, _vp]),
     "srsgpu_symbol_sz": (_i32, [_u32, _i32]),
     "srsgpu_ofdm_rx_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32]),
     "srsgpu_ofdm_rx_destroy": (None, [_vp]),
@@ -511,6 +513,12 @@ class Pdsch:
             pass
 
 
+class srsgpu_chest_cfg_t(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("average_subframe", "noise_alg", "smooth_filter_auto",
+                                               "rsrp_neighbour", "cfo_estimate_enable",
+                                               "cfo_estimate_sf_mask", "symbol_sz")]
+
+
 class Chest:
     """srsgpu_chest_t: batched CRS channel estimation (ports 0/1, normal CP) on device grids.
     With nof_ports = 2 grid i yields estimates i*2 (port 0) and i*2 + 1 (port 1)."""
@@ -536,6 +544,21 @@ class Chest:
         arr = sf_idx if isinstance(sf_idx, ctypes.Array) else (ctypes.c_uint32 * n)(*sf_idx)
         return _lib.srsgpu_chest_put_crs_dev(self.q, arr, n, _vp(d_grid), stride)
 
+    def set_cfg(self, average_subframe=False, noise_alg=0, smooth_filter_auto=False,
+                rsrp_neighbour=False, cfo_enable=False, cfo_mask=0, symbol_sz=None):
+        """srsgpu_chest_cfg_t; noise_alg 0 REFS, 1 PSS, 2 EMPTY"""
+        c = srsgpu_chest_cfg_t(int(average_subframe), noise_alg, int(smooth_filter_auto), int(rsrp_neighbour),
+                               int(cfo_enable), cfo_mask, symbol_sz or symbol_sz_of(self.cell.nof_prb))
+        if _lib.srsgpu_chest_set_cfg(self.q, ctypes.byref(c)) != 0:
+            raise RuntimeError("invalid chest configuration")
+
+    def estimate_meas_dev(self, sf_idx, d_grid, stride, d_ce, d_noise=None, d_meas=None):
+        n = len(sf_idx)
+        arr = sf_idx if isinstance(sf_idx, ctypes.Array) else (ctypes.c_uint32 * n)(*sf_idx)
+        return _lib.srsgpu_chest_estimate_meas_dev(self.q, arr, n, _vp(d_grid), stride, _vp(d_ce),
+                                                   _vp(d_noise) if d_noise else None,
+                                                   _vp(d_meas) if d_meas else None)
+
     def estimate_dev(self, sf_idx, d_grid, stride, d_ce, d_noise=None):
         n = len(sf_idx)
         arr = sf_idx if isinstance(sf_idx, ctypes.Array) else (ctypes.c_uint32 * n)(*sf_idx)
@@ -552,6 +575,12 @@ class Chest:
             self.close()
         except Exception:
             pass
+
+
+def symbol_sz_of(nof_prb):
+    """srslte_symbol_sz without standard rates (phy_common.c:245-264)"""
+    return next(sz for lim, sz in ((6, 128), (15, 256), (25, 384), (50, 768), (75, 1024), (110, 1536))
+                if nof_prb <= lim)
 
 
 def symbol_sz(nof_prb, standard_rates=False):

@@ -3,13 +3,14 @@
  * estimation (reference: lib/src/phy/ch_estimation/chest_dl.c, srslte_chest_dl_estimate_port
  * :641-664 and the helpers it calls).
  *
- * Supported: CRS ports 0 and 1 (cell.nof_ports 1 or 2), normal cyclic prefix, per-symbol estimation
- * (average_subframe off), REFS noise estimation. Processing per grid:
- *   - least-squares pilot estimates;
- *   - optional frequency smoothing (srslte_chest_dl_set_smooth_filter /
- *     _set_smooth_filter3_coeff; default [0.1, 0.8, 0.1]);
- *   - linear interpolation in frequency, then in time;
- *   - noise estimate as estimate_noise_pilots computes it.
+ * Supported: CRS ports 0 and 1 (cell.nof_ports 1 or 2), normal cyclic prefix, non-MBSFN subframes,
+ * every estimator setting srsUE's phch_worker uses (phch_worker.cc:149,553-565). Processing per grid:
+ *   - least-squares pilot estimates; RSRP / RSSI / RSRP correlation / CFO measurements;
+ *   - noise estimate: REFS (estimate_noise_pilots), PSS or EMPTY (subframes 0 and 5 only);
+ *   - frequency smoothing (srslte_chest_dl_set_smooth_filter / _set_smooth_filter3_coeff, default
+ *     [0.1, 0.8, 0.1]; or smooth_filter_auto's Gaussian from the noise estimate);
+ *   - per-symbol interpolation in frequency then time, or with average_subframe (srsUE's default)
+ *     the subframe average interpolated in frequency and copied to all 14 symbols.
  * Grid and estimate layout: 14 OFDM symbols x nof_prb*12 subcarriers of complex float per
  * (subframe, rx antenna), the layout srslte_ofdm_rx_sf produces.
  */
@@ -30,10 +31,22 @@ typedef struct srsgpu_chest srsgpu_chest_t;
 int srsgpu_chest_create(srsgpu_chest_t **q, const srsgpu_cell_t *cell, uint32_t max_grids);
 void srsgpu_chest_destroy(srsgpu_chest_t *q);
 void srsgpu_chest_set_stream(srsgpu_chest_t *q, void *hip_stream);
-/* srslte_chest_dl_set_smooth_filter: filter_len 0 disables smoothing (max 16 taps, odd) */
+/* srslte_chest_dl_set_smooth_filter: filter_len 0 disables smoothing (at most 64 taps) */
 int srsgpu_chest_set_smooth_filter(srsgpu_chest_t *q, const float *filter, uint32_t filter_len);
 /* srslte_chest_dl_set_smooth_filter3_coeff: [w, 1-2w, w] */
 void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w);
+
+/* the srslte_chest_dl_t settings chest_dl.c reads (defaults as srslte_chest_dl_init leaves them:
+ * all zero = per-symbol, REFS, fixed filter, no neighbour RSRP, no CFO) */
+typedef struct {
+  uint32_t average_subframe;   /* srslte_chest_dl_average_subframe */
+  uint32_t noise_alg;          /* 0 REFS, 1 PSS, 2 EMPTY: srslte_chest_dl_noise_alg_t order */
+  uint32_t smooth_filter_auto; /* srslte_chest_dl_set_smooth_filter_auto (needs d_noise) */
+  uint32_t rsrp_neighbour;     /* srslte_chest_dl_set_rsrp_neighbour: meas[2] computed */
+  uint32_t cfo_estimate_enable, cfo_estimate_sf_mask; /* srslte_chest_dl_cfo_estimate_enable */
+  uint32_t symbol_sz;          /* FFT size for the CFO formula (srslte_symbol_sz(nof_prb)) */
+} srsgpu_chest_cfg_t;
+int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg);
 
 /* Estimate nof_grids grids: grid i (subframe index sf_idx[i], host array) at d_grid + i*stride
  * complex elements. For every CRS port p of the cell (srslte_chest_dl_estimate_multi order), the
@@ -42,6 +55,15 @@ void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w);
  * separate grids, so a subframe's estimates come out as [rx antenna][port] planes. */
 int srsgpu_chest_estimate_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t nof_grids,
                               const float *d_grid, size_t stride, float *d_ce, float *d_noise);
+/* As above, plus measurements. d_noise is in/out: with PSS / EMPTY noise it is written only for
+ * grids of subframes 0 and 5 and otherwise keeps (and, for smooth_filter_auto, supplies) the
+ * caller's value, as q->noise_estimate does in the reference. d_meas (may be NULL) receives per
+ * (grid, port) 4 floats [rsrp, rssi, rsrp_corr, cfo]: q->rsrp / q->rssi / q->rsrp_corr / q->cfo of
+ * srslte_chest_dl_estimate_port; rsrp_corr only with rsrp_neighbour and cfo only where enabled
+ * for the grid's subframe, else left untouched. */
+int srsgpu_chest_estimate_meas_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t nof_grids,
+                                   const float *d_grid, size_t stride, float *d_ce, float *d_noise,
+                                   float *d_meas);
 
 /* Transmit side (srslte_refsignal_cs_put_sf, refsignal_dl.c:380-402): the CRS of every port of
  * the cell into nof_grids grids; port p of grid i is the plane d_grid + (i*nof_ports + p)*stride.

@@ -7,19 +7,26 @@
  * defines the receive entry points that srsLTE's ue_dl.c / pdsch_test.c call:
  *
  *   srslte_ofdm_rx_sf(q)                 (replaces dft/ofdm.c:460-470 for normal-CP subframes)
- *   srslte_chest_dl_estimate(_multi)(q, in, ce, sf_idx[, nof_rx])  (chest_dl.c:681-715, ports 0-1)
+ *   srslte_chest_dl_estimate(_multi)(q, in, ce, sf_idx[, nof_rx])  (chest_dl.c:681-715, ports 0-1,
+ *                                        every estimator setting of srsUE's phch_worker)
  *   srslte_pdsch_decode(q, cfg, sb, sf_symbols, ce, noise, rnti, data, acks)
  *                                        (pdsch.c:868-1007, TM1 single antenna port and TM3 CDD)
+ *   srsgpu_shim_release(q)               called from srslte_ofdm_rx_free / srslte_chest_dl_free /
+ *                                        srslte_pdsch_free (one added line each)
  *
- * Build it with -DSRSGPU_SHIM and drop the three replaced functions from their reference
- * translation units. The reference objects keep their own state. This file keeps one GPU handle
- * per object in a small registry keyed by the object's address, because the reference structs
- * have no spare field. Calls that are out of the GPU path's scope (MBSFN, extended CP, transmit
- * diversity, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a message. There is no hidden CPU path
- * behind them.
+ * Build it with -DSRSGPU_SHIM and drop the replaced functions from their reference translation
+ * units. The reference objects keep their own state. This file keeps one GPU handle per object in
+ * a small registry keyed by the object's address, because the reference structs have no spare
+ * field. The registry is shared by srsUE's PHY worker threads (phch_worker.cc, one ue_dl per
+ * worker): lookups and claims hold a mutex; a registered object is only used by the thread that
+ * owns the object, as in the reference. Calls that are out of the GPU path's scope (MBSFN,
+ * extended CP, transmit diversity, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a
+ * message. There is no hidden CPU path behind them.
  * Each call moves one subframe host -> device -> host, as the reference API is per subframe.
  * Batch users call include/srsgpu/ headers directly and keep the data in HBM.
  */
+#include <math.h>
+#include <pthread.h>
 #include <stdbool.h>
 #include <stdio.h>
 #include <string.h>
@@ -45,34 +52,77 @@ extern hipError_t hipDeviceSynchronize(void);
 
 /* ---- object registry ---- */
 #define SHIM_MAX 64
+typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH } shim_kind_t;
 typedef struct {
   const void *owner;
+  shim_kind_t kind;
   void *gpu;          /* srsgpu_ofdm_t / srsgpu_chest_t / srsgpu_pdsch_t */
   float *d_a, *d_b, *d_c, *d_d;
   uint32_t nof_prb, cell_id, aux; /* aux: FFT size (OFDM) or CRS port count (chest, PDSCH) */
   const void *sb[SHIM_MAX]; /* pdsch: softbuffer object -> GPU softbuffer index */
 } shim_entry_t;
 static shim_entry_t shim[SHIM_MAX];
+static pthread_mutex_t shim_mutex = PTHREAD_MUTEX_INITIALIZER;
 
-static shim_entry_t *shim_get(const void *owner, bool create) {
-  for (int i = 0; i < SHIM_MAX; i++)
-    if (shim[i].owner == owner) return &shim[i];
-  if (!create) return NULL;
-  for (int i = 0; i < SHIM_MAX; i++)
+/* the entry of `owner`, claiming a free one if there is none */
+static shim_entry_t *shim_get(const void *owner, shim_kind_t kind) {
+  shim_entry_t *e = NULL;
+  pthread_mutex_lock(&shim_mutex);
+  for (int i = 0; i < SHIM_MAX && !e; i++)
+    if (shim[i].owner == owner) e = &shim[i];
+  for (int i = 0; i < SHIM_MAX && !e; i++)
     if (!shim[i].owner) {
       memset(&shim[i], 0, sizeof(shim[i]));
       shim[i].owner = owner;
-      return &shim[i];
+      shim[i].kind = kind;
+      e = &shim[i];
     }
-  return NULL;
+  pthread_mutex_unlock(&shim_mutex);
+  if (!e) fprintf(stderr, "srsgpu shim: more than %d live objects\n", SHIM_MAX);
+  return e;
 }
 
-static void shim_drop(shim_entry_t *e) {
+/* frees the entry's GPU handle and staging buffers; the entry stays claimed by its owner */
+static void shim_reset(shim_entry_t *e) {
+  if (e->gpu) {
+    if (e->kind == SHIM_OFDM) srsgpu_ofdm_rx_destroy((srsgpu_ofdm_t *)e->gpu);
+    if (e->kind == SHIM_CHEST) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
+    if (e->kind == SHIM_PDSCH) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
+  }
   if (e->d_a) hipFree(e->d_a);
   if (e->d_b) hipFree(e->d_b);
   if (e->d_c) hipFree(e->d_c);
   if (e->d_d) hipFree(e->d_d);
+  const void *owner = e->owner;
+  const shim_kind_t kind = e->kind;
   memset(e, 0, sizeof(*e));
+  e->owner = owner;
+  e->kind = kind;
+}
+
+/* Releases the GPU state of a reference object: srslte_ofdm_rx_free (ofdm.c:138),
+ * srslte_chest_dl_free (chest_dl.c:171) and srslte_pdsch_free (pdsch.c:369) call it before they
+ * clear the object. Returns 1 if the object had GPU state, 0 if not. */
+int srsgpu_shim_release(const void *owner) {
+  shim_entry_t *e = NULL;
+  pthread_mutex_lock(&shim_mutex);
+  for (int i = 0; i < SHIM_MAX && !e; i++)
+    if (owner && shim[i].owner == owner) e = &shim[i];
+  if (e) {
+    shim_reset(e);
+    memset(e, 0, sizeof(*e)); /* free for the next object */
+  }
+  pthread_mutex_unlock(&shim_mutex);
+  return e != NULL;
+}
+
+/* number of objects with GPU state (for tests) */
+int srsgpu_shim_live(void) {
+  int n = 0;
+  pthread_mutex_lock(&shim_mutex);
+  for (int i = 0; i < SHIM_MAX; i++) n += shim[i].owner != NULL;
+  pthread_mutex_unlock(&shim_mutex);
+  return n;
 }
 
 /* ------------------------------------------------------------------ OFDM ---- */
@@ -82,12 +132,10 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
     return;
   }
   const uint32_t nof_prb = q->nof_re / SRSLTE_NRE;
-  shim_entry_t *e = shim_get(q, true);
+  shim_entry_t *e = shim_get(q, SHIM_OFDM);
   if (!e) return;
-  if (e->aux != q->symbol_sz || e->nof_prb != nof_prb) {
-    if (e->gpu) srsgpu_ofdm_rx_destroy((srsgpu_ofdm_t *)e->gpu);
-    shim_drop(e);
-    e->owner = q;
+  if (e->aux != q->symbol_sz || e->nof_prb != nof_prb || !e->gpu) {
+    shim_reset(e);
     if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz)) return;
     hipMalloc((void **)&e->d_a, sizeof(cf_t) * q->sf_sz);
     hipMalloc((void **)&e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp));
@@ -102,44 +150,80 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
 }
 
 /* ------------------------------------------------------------------ channel estimation ---- */
-/* srslte_chest_dl_estimate_multi (chest_dl.c:681-694): every rx antenna x every CRS port */
+/* srslte_chest_dl_set_smooth_filter_gauss (chest_dl.c:471-490): what smooth_filter_auto leaves in q */
+static void shim_gauss(srslte_chest_dl_t *q, uint32_t order, float std_dev) {
+  const uint32_t len = order + 1;
+  const int center = (int)(len - 1) / 2;
+  float norm = 0.0f;
+  for (int i = 0; i < (int)len; i++) {
+    q->smooth_filter[i] = expf(-powf(i - center, 2) / (2.0f * powf(std_dev, 2)));
+    norm += q->smooth_filter[i];
+  }
+  for (uint32_t i = 0; i < len; i++) q->smooth_filter[i] *= 1.0f / norm;
+  q->smooth_filter_len = len;
+}
+
+/* srslte_chest_dl_estimate_multi (chest_dl.c:681-694): every rx antenna x every CRS port, with
+ * the reference object's settings (average_subframe, noise algorithm, smoothing filter or
+ * smooth_filter_auto, neighbour RSRP, CFO mask); writes back what the reference writes into q:
+ * noise_estimate, rsrp, rssi, rsrp_corr, cfo, last_nof_antennas (and the auto filter) */
 int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_PORTS],
                                    cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], uint32_t sf_idx,
                                    uint32_t nof_rx_antennas) {
-  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->average_subframe ||
-      q->noise_alg != SRSLTE_NOISE_ALG_REFS || q->smooth_filter_auto || nof_rx_antennas > 2) {
-    fprintf(stderr, "srsgpu shim: GPU channel estimation covers ports 0-1, normal CP, REFS noise\n");
+  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || nof_rx_antennas > 2) {
+    fprintf(stderr, "srsgpu shim: GPU channel estimation covers CRS ports 0-1, normal CP, 2 rx\n");
     return SRSLTE_ERROR;
   }
-  shim_entry_t *e = shim_get(q, true);
+  shim_entry_t *e = shim_get(q, SHIM_CHEST);
   if (!e) return SRSLTE_ERROR;
   const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
   if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
-    if (e->gpu) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
-    shim_drop(e);
-    e->owner = q;
+    shim_reset(e);
     srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, 1};
     if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 2)) return SRSLTE_ERROR;
     hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
     hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
-    hipMalloc((void **)&e->d_c, sizeof(float) * 4);
+    hipMalloc((void **)&e->d_c, sizeof(float) * 4 * 5); /* noise [4] + measurements [4][4] */
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
     e->aux = np;
   }
-  if (srsgpu_chest_set_smooth_filter((srsgpu_chest_t *)e->gpu, q->smooth_filter, q->smooth_filter_len))
+  srsgpu_chest_t *g = (srsgpu_chest_t *)e->gpu;
+  const srsgpu_chest_cfg_t cfg = {q->average_subframe, (uint32_t)q->noise_alg, q->smooth_filter_auto,
+                                  q->rsrp_neighbour, q->cfo_estimate_enable, q->cfo_estimate_sf_mask,
+                                  (uint32_t)srslte_symbol_sz(q->cell.nof_prb)};
+  if (srsgpu_chest_set_cfg(g, &cfg) ||
+      srsgpu_chest_set_smooth_filter(g, q->smooth_filter, q->smooth_filter_len))
     return SRSLTE_ERROR;
+  /* in/out state: the noise estimate (kept by PSS / EMPTY outside subframes 0 and 5) and the
+   * measurements left untouched when disabled */
+  float st[4 + 16];
+  for (uint32_t a = 0; a < nof_rx_antennas; a++)
+    for (uint32_t p = 0; p < np; p++) {
+      float *m = &st[4 + 4 * (a * np + p)];
+      st[a * np + p] = q->noise_estimate[a][p];
+      m[0] = q->rsrp[a][p];
+      m[1] = q->rssi[a][p];
+      m[2] = q->rsrp_corr[a][p];
+      m[3] = q->cfo;
+    }
+  hipMemcpy(e->d_c, st, sizeof(st), H2D);
   uint32_t sfs[2] = {sf_idx, sf_idx};
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
     hipMemcpy(e->d_a + 2 * (size_t)a * n, input[a], sizeof(cf_t) * n, H2D);
-  if (srsgpu_chest_estimate_dev((srsgpu_chest_t *)e->gpu, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c))
+  if (srsgpu_chest_estimate_meas_dev(g, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c, e->d_c + 4))
     return SRSLTE_ERROR;
-  float noise[4];
-  hipMemcpy(noise, e->d_c, sizeof(float) * nof_rx_antennas * np, D2H);
+  hipMemcpy(st, e->d_c, sizeof(st), D2H);
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
     for (uint32_t p = 0; p < np; p++) { /* GPU order [rx][port]; reference ce[port][rx] */
+      const float *m = &st[4 + 4 * (a * np + p)];
       hipMemcpy(ce[p][a], e->d_b + 2 * (size_t)(a * np + p) * n, sizeof(cf_t) * n, D2H);
-      q->noise_estimate[a][p] = noise[a * np + p];
+      q->noise_estimate[a][p] = st[a * np + p];
+      q->rsrp[a][p] = m[0];
+      q->rssi[a][p] = m[1];
+      q->rsrp_corr[a][p] = m[2];
+      q->cfo = m[3]; /* the reference overwrites it per (rx, port): the last one stays */
+      if (q->smooth_filter_auto) shim_gauss(q, 4, q->noise_estimate[a][p] * 200.0f);
     }
   q->last_nof_antennas = (int)nof_rx_antennas;
   return SRSLTE_SUCCESS;
@@ -201,15 +285,13 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   }
   if (siso && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
   if (cdd && acks[0] && acks[1]) return SRSLTE_SUCCESS;
-  shim_entry_t *e = shim_get(q, true);
+  shim_entry_t *e = shim_get(q, SHIM_PDSCH);
   if (!e) return SRSLTE_ERROR;
   const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
   const uint32_t max_tbs = (uint32_t)srslte_ra_tbs_from_idx(26, q->cell.nof_prb);
   const size_t dlen = SRSGPU_DLSCH_DATA_LEN(max_tbs) + 16;
   if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
-    if (e->gpu) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
-    shim_drop(e);
-    e->owner = q;
+    shim_reset(e);
     srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, q->nof_rx_antennas};
     const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
     if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1)) return SRSLTE_ERROR;

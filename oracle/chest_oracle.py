@@ -1,5 +1,5 @@
 """CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's downlink CRS
-channel estimation for CRS ports 0 and 1, normal CP, per-symbol mode (paths relative to
+channel estimation for CRS ports 0 and 1, normal CP (paths relative to
 /root/reference/lib/src/phy):
 
   crs_pilots        ch_estimation/refsignal_dl.c:265-318 (Gold sequence per slot/symbol)
@@ -9,6 +9,15 @@ channel estimation for CRS ports 0 and 1, normal CP, per-symbol mode (paths rela
   smooth            utils/convolution.c:172-211 srslte_conv_same_cf with extrapolated extremes
   interp_freq       resampling/interp.c:245-272 srslte_interp_linear_offset (M = 6)
   interp_time       chest_dl.c:392-397 + interp.c:150-173 (running sums of (b - a) / d)
+  average_row       chest_dl.c:528-548 average_pilots with average_subframe (srsUE's default,
+                    srsue/src/main.cc:287-289): the 4 CRS symbols folded into one row of 4*nof_prb
+                    pilots at spacing 3, interpolated with M = 3 (chest_dl.c:393-399) and copied to
+                    all 14 symbols (chest_dl.c:410-414)
+  gauss_filter      chest_dl.c:471-490 srslte_chest_dl_set_smooth_filter_gauss (smooth_filter_auto,
+                    chest_dl.c:616-618: order 4, std dev = noise estimate x 200)
+  noise_pss         chest_dl.c:332-348 estimate_noise_pss (sync/pss.c:354-398 sequence / slot)
+  noise_empty       chest_dl.c:351-361 estimate_noise_empty_sc; both only in subframes 0 and 5
+  measurements      chest_dl.c:500-515 rssi, :562-587 CFO, :652-657 RSRP / RSRP correlation
 
 The reference chest (chest_dl.c) cannot be compiled here: through sync/pss.c and
 utils/convolution.c it needs the FFTW-backed DFT, which the image lacks. Its CRS generation and
@@ -127,3 +136,98 @@ def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0):
             prev = prev + diff
             ce[first + k] = prev
     return ce.reshape(-1), noise
+
+
+def average_row(est, cell_id, port=0):
+    """chest_dl.c:528-548: slot-pair interleave of the 4 CRS symbols, scaled by 2 / 4"""
+    n = est.shape[1]
+    a, b = (0, 1) if fidx(cell_id, 0, port) < 3 else (1, 0)
+    t = np.zeros(2 * n, np.complex128)
+    t[0::2] = est[a] + est[a + 2]
+    t[1::2] = est[b] + est[b + 2]
+    return t * 0.5
+
+
+def gauss_filter(order, std_dev):
+    """chest_dl.c:471-490 (float32 as the reference computes it)"""
+    L, c = order + 1, order // 2
+    f = np.array([np.exp(np.float32(-float((i - c) ** 2)) / np.float32(2.0 * np.float32(std_dev) ** 2))
+                  for i in range(L)], np.float32)
+    norm = np.float32(0)
+    for v in f:
+        norm = np.float32(norm + v)
+    return (f * np.float32(1.0 / norm)).astype(np.float64)
+
+
+def pss_sequence(n_id_2):
+    """sync/pss.c:354-382: length-62 Zadoff-Chu, roots 25 / 29 / 34"""
+    u = (25.0, 29.0, 34.0)[n_id_2]
+    i = np.arange(62, dtype=np.float64)
+    arg = np.where(i < 31, -np.pi * u * i * (i + 1) / 63.0, -np.pi * u * (i + 2) * (i + 1) / 63.0)
+    return np.exp(1j * arg.astype(np.float32).astype(np.float64))  # pss.c stores the argument as float
+
+
+def _avg_power(x):
+    return float(np.mean(np.abs(x) ** 2))
+
+
+def noise_pss(grid, ce, nof_prb, cell_id, nof_ports):
+    nsc = 12 * nof_prb
+    k = 6 * nsc + nsc // 2 - 31  # srslte_pss_get_slot: last symbol of slot 0
+    r = ce[k:k + 62] * pss_sequence(cell_id % 3) - grid[k:k + 62]
+    return nof_ports * _avg_power(r) / np.sqrt(2)
+
+
+def noise_empty(grid, nof_prb):
+    nsc = 12 * nof_prb
+    ks = 5 * nsc + nsc // 2 - 31
+    kp = 6 * nsc + nsc // 2 - 31
+    return (_avg_power(grid[ks - 5:ks]) + _avg_power(grid[ks + 62:ks + 67]) +
+            _avg_power(grid[kp - 5:kp]) + _avg_power(grid[kp + 62:kp + 67]))
+
+
+def measurements(grid, nof_prb, cell_id, sf_idx, port=0, symbol_sz=1536):
+    """(rsrp, rssi, rsrp_corr, cfo) as srslte_chest_dl_estimate_port leaves them in q"""
+    g = grid.reshape(14, 12 * nof_prb)
+    recv = np.stack([g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] for l, s in enumerate(SYMS)])
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+    rsrp = _avg_power(recv)
+    rssi = float(sum(np.sum(np.abs(g[s]) ** 2) for s in SYMS) / 4)
+    corr = abs(est.sum() / est.size) ** 2
+    acc = np.sum(est[0] * np.conj(est[2])) + np.sum(est[1] * np.conj(est[3]))
+    n = float(symbol_sz)
+    ng = float(np.ceil(144 * n / 2048))
+    cfo = -np.angle(acc) * n / (7 * (n + ng)) / 2 / np.pi
+    return rsrp, rssi, corr, cfo
+
+
+def estimate_full(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0, average=False,
+                  noise_alg="refs", filt_auto=False, noise_in=0.0, nof_ports=1):
+    """chest_interpolate_noise_est (chest_dl.c:606-639) in any of srsUE's configurations.
+    -> (ce, noise): noise is the value q->noise_estimate[rx][port] holds afterwards (noise_in when
+    the algorithm leaves it alone: PSS / EMPTY outside subframes 0 and 5)"""
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+    noise = noise_refs(est, cell_id, port) if noise_alg == "refs" else noise_in
+    f = gauss_filter(4, noise * 200.0) if filt_auto else np.asarray(filt, np.float64)
+    smoothing = not (len(f) == 0 or (len(f) == 3 and f[0] == 0))
+    nsc = 12 * nof_prb
+    ce = np.zeros((14, nsc), np.complex128)
+    if average:
+        # without smoothing the reference interpolates the raw pilot buffer (symbols 0 and 4
+        # back to back) as if it were the averaged row (chest_dl.c:619-621 + 393-399)
+        row = smooth(average_row(est, cell_id, port), f) if smoothing else est[:2].reshape(-1)
+        ce[:] = interp_freq(row, cell_id % 3, M=3)[None, :]
+    else:
+        sm = np.stack([smooth(r, f) for r in est]) if smoothing else est
+        for l, s in enumerate(SYMS):
+            ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
+        for a, b, d, first, cnt in ((0, 4, 4, 1, 3), (4, 7, 3, 5, 2), (7, 11, 4, 8, 3), (7, 11, 4, 12, 2)):
+            diff = (ce[b] - ce[a]) / d
+            prev = ce[b] if first == 12 else ce[a]
+            for k in range(cnt):
+                prev = prev + diff
+                ce[first + k] = prev
+    ce = ce.reshape(-1)
+    if noise_alg != "refs" and sf_idx in (0, 5):
+        noise = noise_pss(grid, ce, nof_prb, cell_id, nof_ports) if noise_alg == "pss" else noise_empty(grid, nof_prb)
+    return ce, noise

@@ -56,3 +56,32 @@ def test_shim_pdsch_decode_matches_reference(case):
     assert int(stats["mismatches"]) == 0 and int(stats["tx"]) >= case[6]
     assert int(stats["soft"]) <= max(1, int(stats["tx"]) // 10), r.stdout + r.stderr
     assert int(stats["acks"]) > 0
+
+
+FRONT = os.path.join(REPO, "oracle", "_ref", "shim_front")
+# nof_prb_a, nof_prb_b, cell_id, mcs, nof_rx, nof_sf, snr_db, seed
+FRONT_CASES = [
+    (25, 6, 33, 16, 2, 10, 24.0, 1),   # 5 MHz -> 1.4 MHz, 2 rx
+    (100, 50, 400, 22, 1, 10, 26.0, 2),  # 20 MHz -> 10 MHz
+    (6, 15, 502, 9, 2, 10, 20.0, 3),   # 1.4 MHz -> 3 MHz (odd PRB count), cell id 502 -> 503
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FRONT_CASES, ids=[f"prb{c[0]}to{c[1]}_rx{c[4]}" for c in FRONT_CASES])
+def test_shim_front_end_time_domain(case):
+    """shim srslte_ofdm_rx_sf -> srslte_chest_dl_estimate_multi -> srslte_pdsch_decode on a time
+    signal (oracle/shim_front.c): OFDM grid within 1e-4 of the transmitted one, channel estimate
+    close to the true channel, noise / RSRP / RSSI / CFO written back into the reference object
+    (EMPTY noise only in subframes 0 and 5), the PDSCH decode bit-exact with the reference CPU
+    decoder on the same grids and estimates, GPU handles recreated after the cell change and all
+    released through srsgpu_shim_release"""
+    if not os.path.exists(FRONT):
+        pytest.skip("oracle/_ref/shim_front not built (needs /root/reference at build time)")
+    r = subprocess.run([FRONT] + [str(v) for v in case], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    stats = dict(kv.split("=") for kv in r.stdout.split())
+    assert int(stats["mismatches"]) == 0 and int(stats["sf"]) == 2 * case[5]
+    assert float(stats["ofdm_err"]) < 1e-4 and float(stats["ce_err"]) < 0.2, r.stdout
+    assert int(stats["recreated"]) == 1 and int(stats["live"]) == 0
+    assert int(stats["acks"]) >= case[5]  # at least the high-SNR phase decodes
