@@ -11,8 +11,13 @@
  *                                        every estimator setting of srsUE's phch_worker)
  *   srslte_pdsch_decode(q, cfg, sb, sf_symbols, ce, noise, rnti, data, acks)
  *                                        (pdsch.c:868-1007, TM1 single antenna port and TM3 CDD)
+ *   srslte_dlsch_decode2(q, cfg, sb, e_bits, data, tb_idx)  (sch.c:506-517, 16-bit LLRs)
+ *   srslte_rm_turbo_rx_lut(in, out, in_len, cb_idx, rv)      (rm_turbo.c:378-381)
+ *   srslte_softbuffer_rx_init / _free / _reset / _reset_tbs / _reset_cb  (softbuffer.c:46-153):
+ *                                        the reference's host work, plus the GPU softbuffer state
  *   srsgpu_shim_release(q)               called from srslte_ofdm_rx_free / srslte_chest_dl_free /
- *                                        srslte_pdsch_free (one added line each)
+ *                                        srslte_pdsch_free / srslte_sch_free (one added line each,
+ *                                        INTEGRATION.md)
  *
  * Build it with -DSRSGPU_SHIM and drop the replaced functions from their reference translation
  * units. The reference objects keep their own state. This file keeps one GPU handle per object in
@@ -33,7 +38,11 @@
 
 #include "srslte/phy/ch_estimation/chest_dl.h"
 #include "srslte/phy/dft/ofdm.h"
+#include "srslte/phy/fec/cbsegm.h"
+#include "srslte/phy/fec/rm_turbo.h"
+#include "srslte/phy/fec/softbuffer.h"
 #include "srslte/phy/phch/pdsch.h"
+#include "srslte/phy/phch/sch.h"
 
 #include "srsgpu/chest_batch.h"
 #include "srsgpu/dlsch_batch.h"
@@ -46,20 +55,20 @@ extern hipError_t hipMalloc(void **ptr, size_t size);
 extern hipError_t hipFree(void *ptr);
 extern hipError_t hipMemcpy(void *dst, const void *src, size_t n, int kind);
 extern hipError_t hipDeviceSynchronize(void);
-#define SHIM_MARK 0x5a5a
 #define H2D 1
 #define D2H 2
 
 /* ---- object registry ---- */
 #define SHIM_MAX 64
-typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH } shim_kind_t;
+typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH, SHIM_SCH } shim_kind_t;
 typedef struct {
   const void *owner;
   shim_kind_t kind;
   void *gpu;          /* srsgpu_ofdm_t / srsgpu_chest_t / srsgpu_pdsch_t */
   float *d_a, *d_b, *d_c, *d_d;
-  uint32_t nof_prb, cell_id, aux; /* aux: FFT size (OFDM) or CRS port count (chest, PDSCH) */
-  const void *sb[SHIM_MAX]; /* pdsch: softbuffer object -> GPU softbuffer index */
+  uint32_t nof_prb, cell_id, aux; /* aux: FFT size (OFDM), CRS port count (chest, PDSCH), or
+                                     e-bits capacity (SCH) */
+  const void *sb[SHIM_MAX]; /* pdsch / sch: softbuffer object -> GPU softbuffer index */
 } shim_entry_t;
 static shim_entry_t shim[SHIM_MAX];
 static pthread_mutex_t shim_mutex = PTHREAD_MUTEX_INITIALIZER;
@@ -88,6 +97,7 @@ static void shim_reset(shim_entry_t *e) {
     if (e->kind == SHIM_OFDM) srsgpu_ofdm_rx_destroy((srsgpu_ofdm_t *)e->gpu);
     if (e->kind == SHIM_CHEST) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
     if (e->kind == SHIM_PDSCH) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
+    if (e->kind == SHIM_SCH) srsgpu_dlsch_destroy((srsgpu_dlsch_t *)e->gpu);
   }
   if (e->d_a) hipFree(e->d_a);
   if (e->d_b) hipFree(e->d_b);
@@ -240,31 +250,194 @@ int srslte_chest_dl_estimate(srslte_chest_dl_t *q, cf_t *input, cf_t *ce[SRSLTE_
 }
 
 /* ------------------------------------------------------------------ PDSCH ---- */
-/* GPU softbuffer index of a reference softbuffer; the last index is a scratch buffer for TBs the
- * caller already acked (the reference skips them, pdsch.c:963-965) */
+/* ------------------------------------------------------------------ softbuffers ---- */
+/* The soft bits of a reference softbuffer live in HBM, in a slot of the decoding object's GPU
+ * softbuffer pool. The srslte_softbuffer_rx_* drop-ins below do the reference's host work
+ * (SHIM_CPU: softbuffer.c compiled with its rx functions renamed *_cpu) and record
+ * how many leading code-block rows the caller reset; the next decode applies that to the slot. */
+#ifndef SHIM_CPU
+#define SHIM_CPU(f) f##_cpu
+#endif
+int SHIM_CPU(srslte_softbuffer_rx_init)(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
+void SHIM_CPU(srslte_softbuffer_rx_free)(srslte_softbuffer_rx_t *q);
+void SHIM_CPU(srslte_softbuffer_rx_reset)(srslte_softbuffer_rx_t *q);
+void SHIM_CPU(srslte_softbuffer_rx_reset_tbs)(srslte_softbuffer_rx_t *q, uint32_t tbs);
+void SHIM_CPU(srslte_softbuffer_rx_reset_cb)(srslte_softbuffer_rx_t *q, uint32_t nof_cb);
+
+#define SHIM_SB_MAX 1024
+static struct {
+  const void *sb;
+  uint32_t reset_cb; /* leading rows reset since the last decode */
+} shim_sbs[SHIM_SB_MAX];
+
+static void shim_sb_mark(const srslte_softbuffer_rx_t *sb, uint32_t nof_cb) {
+  pthread_mutex_lock(&shim_mutex);
+  int slot = -1;
+  for (int i = 0; i < SHIM_SB_MAX && slot < 0; i++)
+    if (shim_sbs[i].sb == sb) slot = i;
+  for (int i = 0; i < SHIM_SB_MAX && slot < 0; i++)
+    if (!shim_sbs[i].sb) {
+      shim_sbs[i].sb = sb;
+      shim_sbs[i].reset_cb = 0;
+      slot = i;
+    }
+  if (slot >= 0 && nof_cb > shim_sbs[slot].reset_cb) shim_sbs[slot].reset_cb = nof_cb;
+  pthread_mutex_unlock(&shim_mutex);
+  if (slot < 0) fprintf(stderr, "srsgpu shim: more than %d live softbuffers\n", SHIM_SB_MAX);
+}
+
+int srslte_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb) {
+  const int ret = SHIM_CPU(srslte_softbuffer_rx_init)(q, nof_prb);
+  if (ret == SRSLTE_SUCCESS) shim_sb_mark(q, q->max_cb);
+  return ret;
+}
+
+void srslte_softbuffer_rx_free(srslte_softbuffer_rx_t *q) {
+  pthread_mutex_lock(&shim_mutex);
+  for (int i = 0; i < SHIM_SB_MAX; i++)
+    if (shim_sbs[i].sb == q) shim_sbs[i].sb = NULL;
+  for (int i = 0; i < SHIM_MAX; i++) /* its slots in every decoding object become free */
+    for (int j = 0; j < SHIM_MAX; j++)
+      if (shim[i].sb[j] == q) shim[i].sb[j] = NULL;
+  pthread_mutex_unlock(&shim_mutex);
+  SHIM_CPU(srslte_softbuffer_rx_free)(q);
+}
+
+void srslte_softbuffer_rx_reset(srslte_softbuffer_rx_t *q) {
+  SHIM_CPU(srslte_softbuffer_rx_reset)(q);
+  shim_sb_mark(q, q->max_cb);
+}
+
+void srslte_softbuffer_rx_reset_tbs(srslte_softbuffer_rx_t *q, uint32_t tbs) {
+  SHIM_CPU(srslte_softbuffer_rx_reset_tbs)(q, tbs);
+  shim_sb_mark(q, (tbs + 24) / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1); /* softbuffer.c:120-121 */
+}
+
+void srslte_softbuffer_rx_reset_cb(srslte_softbuffer_rx_t *q, uint32_t nof_cb) {
+  SHIM_CPU(srslte_softbuffer_rx_reset_cb)(q, nof_cb);
+  shim_sb_mark(q, nof_cb);
+}
+
+/* GPU softbuffer index of a reference softbuffer in the object's pool, with the resets recorded
+ * since its last decode applied; the last index is a scratch buffer for TBs the caller already
+ * acked (the reference skips them, pdsch.c:963-965) */
 #define SHIM_SCRATCH (SHIM_MAX - 1)
 static int shim_softbuffer(shim_entry_t *e, srsgpu_dlsch_t *dl, srslte_softbuffer_rx_t *sb) {
-  int slot = -1;
+  int slot = -1, fresh = 0;
+  uint32_t nreset = 0;
+  pthread_mutex_lock(&shim_mutex);
   for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
     if (e->sb[i] == sb) slot = i;
   for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
-    if (!e->sb[i]) { /* a new object starts reset (softbuffer_rx_init) */
+    if (!e->sb[i]) {
       e->sb[i] = sb;
       slot = i;
-      srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)i);
+      fresh = 1;
     }
+  for (int i = 0; i < SHIM_SB_MAX; i++)
+    if (shim_sbs[i].sb == sb) {
+      nreset = shim_sbs[i].reset_cb;
+      shim_sbs[i].reset_cb = 0;
+    }
+  pthread_mutex_unlock(&shim_mutex);
   if (slot < 0) return -1;
-  /* The soft bits live in HBM; the host rows only carry a marker in element 0 of each code block
-   * row, written after every decode. srslte_softbuffer_rx_reset / _reset_tbs / _reset_cb
-   * (softbuffer.c:127-150) zero a prefix of the rows, so the zeroed prefix length is exactly the
-   * number of rows the caller reset since the last decode. */
-  uint32_t nreset = 0;
-  while (nreset < sb->max_cb && sb->buffer_f[nreset] && sb->buffer_f[nreset][0] != SHIM_MARK) nreset++;
-  if (nreset == sb->max_cb)
+  if (fresh || nreset >= sb->max_cb) /* a new slot starts reset (softbuffer_rx_init) */
     srsgpu_dlsch_softbuffer_reset(dl, (uint32_t)slot);
-  else if (nreset > 0)
+  else if (nreset > 0) /* softbuffer.c:127-150 zero the first nreset rows and every cb_crc flag */
     srsgpu_dlsch_softbuffer_reset_tbs(dl, (uint32_t)slot, (nreset - 1) * (SRSLTE_TCOD_MAX_LEN_CB - 24));
   return slot;
+}
+
+/* the code block CRC flags and tb_crc the reference leaves in the softbuffer (sch.c:404-408) */
+static void shim_mirror_crc(srsgpu_dlsch_t *dl, uint32_t slot, srslte_softbuffer_rx_t *sb, uint32_t C) {
+  uint8_t crc[SHIM_MAX];
+  if (srsgpu_dlsch_softbuffer_read(dl, slot, NULL, crc) == 0) {
+    for (uint32_t i = 0; i < sb->max_cb && i < SHIM_MAX; i++) sb->cb_crc[i] = crc[i] != 0;
+    sb->tb_crc = true;
+    for (uint32_t i = 0; i < C && sb->tb_crc; i++) sb->tb_crc = sb->cb_crc[i];
+  }
+}
+
+/* ------------------------------------------------------------------ DL-SCH ---- */
+/* srslte_dlsch_decode2 (sch.c:506-517 -> decode_tb :430-497): one transport block from host
+ * LLRs; sets q->nof_iterations (srslte_sch_last_noi) and the softbuffer's cb_crc / tb_crc */
+int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
+                         int16_t *e_bits, uint8_t *data, int tb_idx) {
+  if (!q || !cfg || !softbuffer || !e_bits || !data || tb_idx < 0 || tb_idx >= SRSLTE_MAX_CODEWORDS)
+    return SRSLTE_ERROR_INVALID_INPUTS;
+  if (q->llr_is_8bit) {
+    fprintf(stderr, "srsgpu shim: GPU DL-SCH decode takes 16-bit LLRs\n");
+    return SRSLTE_ERROR;
+  }
+  const uint32_t Nl = cfg->nof_layers != (uint32_t)SRSLTE_RA_DL_GRANT_NOF_TB(&cfg->grant) ? 2 : 1;
+  const uint32_t tbs = cfg->cb_segm[tb_idx].tbs, nof_e = cfg->nbits[tb_idx].nof_bits;
+  shim_entry_t *e = shim_get(q, SHIM_SCH);
+  if (!e) return SRSLTE_ERROR;
+  const size_t dlen = SRSGPU_DLSCH_DATA_LEN(75376) + 16;
+  if (!e->gpu || e->nof_prb < softbuffer->max_cb || e->aux < nof_e) {
+    const uint32_t max_cb = e->nof_prb > softbuffer->max_cb ? e->nof_prb : softbuffer->max_cb;
+    const uint32_t cap = e->aux > nof_e ? e->aux : nof_e;
+    shim_reset(e);
+    if (srsgpu_dlsch_create((srsgpu_dlsch_t **)&e->gpu, SHIM_MAX, max_cb, max_cb)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(int16_t) * (cap ? cap : 1));
+    hipMalloc((void **)&e->d_b, dlen);
+    hipMalloc((void **)&e->d_c, 2 * sizeof(int32_t));
+    e->nof_prb = max_cb; /* SCH entries: the pool's code blocks per softbuffer */
+    e->aux = cap;
+  }
+  srsgpu_dlsch_t *dl = (srsgpu_dlsch_t *)e->gpu;
+  const int slot = shim_softbuffer(e, dl, softbuffer);
+  if (slot < 0) return SRSLTE_ERROR;
+  srsgpu_dlsch_tb_t tb = {tbs, cfg->rv[tb_idx], cfg->grant.Qm[tb_idx] * Nl, nof_e, (uint32_t)slot, 0, 0};
+  hipMemcpy(e->d_a, e_bits, sizeof(int16_t) * nof_e, H2D);
+  int32_t *d_ret = (int32_t *)e->d_c;
+  uint32_t *d_noi = (uint32_t *)e->d_c + 1;
+  if (srsgpu_dlsch_decode_dev(dl, &tb, 1, (const int16_t *)e->d_a, (uint8_t *)e->d_b, q->max_iterations,
+                              d_ret, d_noi))
+    return SRSLTE_ERROR;
+  int32_t rn[2];
+  hipMemcpy(rn, e->d_c, sizeof(rn), D2H);
+  if (rn[0] != SRSLTE_ERROR_INVALID_INPUTS) {
+    hipMemcpy(data, e->d_b, tbs / 8 + 3, D2H); /* the TB and its CRC bytes (sch.c:466-468) */
+    q->nof_iterations = (uint32_t)rn[1];
+    shim_mirror_crc(dl, (uint32_t)slot, softbuffer, cfg->cb_segm[tb_idx].C);
+  }
+  return rn[0];
+}
+
+/* srslte_rm_turbo_rx_lut (rm_turbo.c:378-381, :394-430): output[deinter[i % (3K+12)]] += input[i]
+ * on host buffers, with the sub-block layout the AUTO decoder expects. One process-wide GPU
+ * context; latency-bound by nature (one code block per call). */
+static struct {
+  srsgpu_dlsch_t *dl;
+  int16_t *d_in, *d_out;
+  uint32_t cap;
+} shim_rm;
+
+int srslte_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx) {
+  if (rv_idx >= 4 || cb_idx >= SRSLTE_NOF_TC_CB_SIZES || !input || !output) {
+    printf("Invalid inputs rv_idx=%d, cb_idx=%d\n", rv_idx, cb_idx);
+    return SRSLTE_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cb_idx), out_len = 3 * K + 12;
+  int ret = SRSLTE_ERROR;
+  pthread_mutex_lock(&shim_mutex);
+  if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
+  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * 3 * (SRSLTE_TCOD_MAX_LEN_CB + 4));
+  if (in_len > shim_rm.cap) {
+    if (shim_rm.d_in) hipFree(shim_rm.d_in);
+    hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
+    shim_rm.cap = in_len;
+  }
+  hipMemcpy(shim_rm.d_in, input, sizeof(int16_t) * in_len, H2D);
+  hipMemcpy(shim_rm.d_out, output, sizeof(int16_t) * out_len, H2D);
+  if (srsgpu_rm_turbo_rx_dev(shim_rm.dl, shim_rm.d_in, shim_rm.d_out, in_len, K, rv_idx, 1) == 0) {
+    hipMemcpy(output, shim_rm.d_out, sizeof(int16_t) * out_len, D2H);
+    ret = SRSLTE_SUCCESS;
+  }
+out:
+  pthread_mutex_unlock(&shim_mutex);
+  return ret;
 }
 
 int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
@@ -355,17 +528,7 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     /* srslte_pdsch_codeword_decode (pdsch.c:811-822): ack on a good TB CRC; srslte_pdsch_decode
      * returns SRSLTE_SUCCESS whatever the codeword result (pdsch.c:966-985) */
     acks[t] = ret[t] == SRSLTE_SUCCESS;
-    if (ret[t] != SRSLTE_ERROR_INVALID_INPUTS) {
-      /* mirror the code block CRC flags and tb_crc (sch.c:404-408) into the reference object */
-      uint8_t crc[SHIM_MAX];
-      if (srsgpu_dlsch_softbuffer_read(dl, sf.softbuffer[t], NULL, crc) == 0) {
-        for (uint32_t i = 0; i < sb->max_cb && i < SHIM_MAX; i++) sb->cb_crc[i] = crc[i] != 0;
-        sb->tb_crc = true;
-        for (uint32_t i = 0; i < cfg->cb_segm[t].C && sb->tb_crc; i++) sb->tb_crc = sb->cb_crc[i];
-      }
-    }
-    for (uint32_t i = 0; i < sb->max_cb; i++)
-      if (sb->buffer_f[i]) sb->buffer_f[i][0] = SHIM_MARK;
+    if (ret[t] != SRSLTE_ERROR_INVALID_INPUTS) shim_mirror_crc(dl, sf.softbuffer[t], sb, cfg->cb_segm[t].C);
   }
   return SRSLTE_SUCCESS;
 }

@@ -14,10 +14,18 @@
  * empower-srslte_amd/lib/libsrsgpu_phy.so); tests/test_integration.py runs it on the GPU.
  * Usage: shim_check nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm
  *   tm 1: single antenna port (TM1); tm 3: 2 CRS ports, CDD with 2 layers and 2 TBs (nof_rx 2).
- * Prints "tx=<n> acks=<n> mismatches=<n> soft=<n> tbs=<n>". In the exact configurations (TM1
- * without CSI) every compared field must agree (mismatches). Where the reference equaliser uses
- * rcpps (CSI, TM3 MMSE) LLRs agree only to its tolerance: data bytes are compared on acks, and
- * ack / iteration-count differences near the decoding threshold are counted as "soft".
+ * Prints "tx=<n> acks=<n> mismatches=<n> soft=<n> tbs=<n> dlsch=<n> dlsch_mismatches=<n>
+ * rm_mismatches=<n>". In the exact configurations (TM1 without CSI) every compared field must agree
+ * (mismatches). Where the reference equaliser uses rcpps (CSI, TM3 MMSE) LLRs agree only to its
+ * tolerance: data bytes are compared on acks, and ack / iteration-count differences near the
+ * decoding threshold are counted as "soft".
+ *
+ * The DL-SCH drop-ins are checked on the same HARQ sequence: the codeword LLRs the reference PDSCH
+ * leaves in q->e (pdsch.c:796-816) go through the reference srslte_dlsch_decode2 (sch.c:506) and
+ * the shim's, each with its own srslte_sch_t and softbuffer (the shim's reset through the shim's
+ * srslte_softbuffer_rx_reset): return value, data and CRC bytes, nof_iterations, cb_crc and tb_crc
+ * must agree exactly in every configuration. srslte_rm_turbo_rx_lut (rm_turbo.c:378) is compared
+ * with the reference on random LLRs accumulated into random rows for every rv and a K sweep.
  */
 #include <complex.h>
 #include <math.h>
@@ -25,7 +33,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "srslte/phy/fec/cbsegm.h"
+#include "srslte/phy/fec/rm_turbo.h"
 #include "srslte/phy/fec/softbuffer.h"
+#include "srslte/phy/phch/sch.h"
 #include "srslte/phy/phch/pdsch.h"
 #include "srslte/phy/phch/ra.h"
 #include "srslte/phy/utils/vector.h"
@@ -36,6 +47,14 @@ int srsgpu_shim_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
                              cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
                              uint16_t rnti, uint8_t *data[SRSLTE_MAX_CODEWORDS],
                              bool acks[SRSLTE_MAX_CODEWORDS]);
+
+int srsgpu_shim_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
+                              int16_t *e_bits, uint8_t *data, int tb_idx);
+int srsgpu_shim_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uint32_t cb_idx,
+                                uint32_t rv_idx);
+int srsgpu_shim_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
+void srsgpu_shim_softbuffer_rx_reset(srslte_softbuffer_rx_t *q);
+void srsgpu_shim_softbuffer_rx_free(srslte_softbuffer_rx_t *q);
 
 static uint64_t rng = 1;
 static double urand(void) {
@@ -98,7 +117,7 @@ int main(int argc, char **argv) {
   uint8_t *db_p[SRSLTE_MAX_CODEWORDS] = {NULL};
   for (uint32_t t = 0; t < ntb; t++) {
     if (srslte_softbuffer_tx_init(&sbt[t], nof_prb) || srslte_softbuffer_rx_init(&sra[t], nof_prb) ||
-        srslte_softbuffer_rx_init(&srb[t], nof_prb))
+        srsgpu_shim_softbuffer_rx_init(&srb[t], nof_prb))
       return 2;
     sbt_p[t] = &sbt[t];
     sra_p[t] = &sra[t];
@@ -109,6 +128,40 @@ int main(int argc, char **argv) {
   }
   const int exact = tm == 1 && !csi;
 
+  /* srslte_rm_turbo_rx_lut: reference vs shim over rv 0-3 and a K sweep */
+  uint32_t nrm_bad = 0;
+  {
+    const uint32_t cbs[] = {0, 1, 40, 60, 100, 150, 187};
+    int16_t *in = malloc(sizeof(int16_t) * 3 * 3 * 6200), *oa = malloc(sizeof(int16_t) * 3 * 6200);
+    int16_t *ob = malloc(sizeof(int16_t) * 3 * 6200);
+    for (uint32_t c = 0; c < sizeof(cbs) / sizeof(cbs[0]); c++)
+      for (uint32_t rv = 0; rv < 4; rv++) {
+        const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cbs[c]), out_len = 3 * K + 12;
+        const uint32_t in_len = (uint32_t)(out_len * (0.3 + 2.0 * urand()));
+        for (uint32_t i = 0; i < in_len; i++) in[i] = (int16_t)(urand() * 400 - 200);
+        for (uint32_t i = 0; i < out_len; i++) oa[i] = ob[i] = (int16_t)(urand() * 400 - 200);
+        const int r1 = srslte_rm_turbo_rx_lut(in, oa, in_len, cbs[c], rv);
+        const int r2 = srsgpu_shim_rm_turbo_rx_lut(in, ob, in_len, cbs[c], rv);
+        if (r1 != r2 || memcmp(oa, ob, sizeof(int16_t) * out_len)) {
+          fprintf(stderr, "rm_turbo_rx_lut mismatch K %u rv %u in_len %u\n", K, rv, in_len);
+          nrm_bad++;
+        }
+      }
+    free(in);
+    free(oa);
+    free(ob);
+  }
+  /* DL-SCH drop-in state: one srslte_sch_t and one softbuffer per TB on each side */
+  srslte_sch_t scha, schb;
+  if (srslte_sch_init(&scha) || srslte_sch_init(&schb)) return 2;
+  srslte_softbuffer_rx_t sra2[2], srb2[2];
+  for (uint32_t t = 0; t < ntb; t++)
+    if (srslte_softbuffer_rx_init(&sra2[t], nof_prb) || srsgpu_shim_softbuffer_rx_init(&srb2[t], nof_prb))
+      return 2;
+  int16_t *ebuf = malloc(sizeof(int16_t) * n * 6 * 2);
+  uint8_t *d2a = calloc(dl, 1), *d2b = calloc(dl, 1);
+  uint32_t ndl = 0, ndl_bad = 0;
+
   const uint32_t rvs[4] = {0, 2, 3, 1};
   uint32_t ntx = 0, nacks = 0, nbad = 0, nsoft = 0;
   for (uint32_t k = 0; k < nof_tb; k++) {
@@ -117,7 +170,9 @@ int main(int argc, char **argv) {
       for (uint32_t i = 0; i < (uint32_t)grant.mcs[t].tbs / 8; i++) dtx_p[t][i] = (uint8_t)(urand() * 256);
       srslte_softbuffer_tx_reset(&sbt[t]);
       srslte_softbuffer_rx_reset(&sra[t]);
-      srslte_softbuffer_rx_reset(&srb[t]);
+      srsgpu_shim_softbuffer_rx_reset(&srb[t]);
+      srslte_softbuffer_rx_reset(&sra2[t]);
+      srsgpu_shim_softbuffer_rx_reset(&srb2[t]);
     }
     /* the SNR steps down every third TB so that some need retransmissions */
     const float snr = snr_db - 3.0f * (float)(k % 3);
@@ -154,6 +209,26 @@ int main(int argc, char **argv) {
       }
       const int ra = srslte_pdsch_decode(&rx, &cfg, sra_p, y, h, sigma2, rnti, da_p, acka);
       uint32_t noia[2] = {rx.last_nof_iterations[0], rx.last_nof_iterations[1]};
+      /* DL-SCH drop-in on the reference's codeword LLRs */
+      for (uint32_t t = 0; t < ntb; t++) {
+        if (acka0[t]) continue;
+        const uint32_t cw = tm == 3 ? (t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
+        const uint32_t nb = cfg.nbits[t].nof_bits, nbytes = (uint32_t)grant.mcs[t].tbs / 8 + 3;
+        memcpy(ebuf, rx.e[cw], sizeof(int16_t) * nb);
+        memset(d2a, 0, dl);
+        memset(d2b, 0, dl);
+        const int r1 = srslte_dlsch_decode2(&scha, &cfg, &sra2[t], ebuf, d2a, (int)t);
+        memcpy(ebuf, rx.e[cw], sizeof(int16_t) * nb);
+        const int r2 = srsgpu_shim_dlsch_decode2(&schb, &cfg, &srb2[t], ebuf, d2b, (int)t);
+        int b = r1 != r2 || scha.nof_iterations != schb.nof_iterations || sra2[t].tb_crc != srb2[t].tb_crc ||
+                (r1 != SRSLTE_ERROR_INVALID_INPUTS && memcmp(d2a, d2b, nbytes));
+        for (uint32_t i = 0; i < cfg.cb_segm[t].C; i++) b |= sra2[t].cb_crc[i] != srb2[t].cb_crc[i];
+        if (b)
+          fprintf(stderr, "dlsch_decode2 mismatch tb %u/%u rv %u: ret %d/%d noi %u/%u\n", k, t, rvs[r], r1, r2,
+                  scha.nof_iterations, schb.nof_iterations);
+        ndl++;
+        ndl_bad += b;
+      }
       const int rb = srsgpu_shim_pdsch_decode(&rx, &cfg, srb_p, y, h, sigma2, rnti, db_p, ackb);
       uint32_t noib[2] = {rx.last_nof_iterations[0], rx.last_nof_iterations[1]};
       int bad = ra != rb, soft = 0;
@@ -188,6 +263,11 @@ int main(int argc, char **argv) {
       ntx++;
     }
   }
-  printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u\n", ntx, nacks, nbad, nsoft, tbs);
-  return nbad ? 1 : 0;
+  for (uint32_t t = 0; t < ntb; t++) {
+    srslte_softbuffer_rx_free(&sra2[t]);
+    srsgpu_shim_softbuffer_rx_free(&srb2[t]);
+  }
+  printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u dlsch=%u dlsch_mismatches=%u rm_mismatches=%u\n", ntx,
+         nacks, nbad, nsoft, tbs, ndl, ndl_bad, nrm_bad);
+  return nbad || ndl_bad || nrm_bad ? 1 : 0;
 }

@@ -51,6 +51,9 @@ int srsgpu_shim_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE
                                         uint32_t nof_rx_antennas);
 void srsgpu_shim_ofdm_rx_sf(srslte_ofdm_t *q);
 int srsgpu_shim_release(const void *owner);
+int srsgpu_shim_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
+void srsgpu_shim_softbuffer_rx_reset(srslte_softbuffer_rx_t *q);
+void srsgpu_shim_softbuffer_rx_free(srslte_softbuffer_rx_t *q);
 int srsgpu_shim_live(void);
 
 static uint64_t rng = 1;
@@ -161,7 +164,7 @@ int main(int argc, char **argv) {
   srslte_softbuffer_tx_t sbt;
   srslte_softbuffer_rx_t sra, srb;
   if (srslte_softbuffer_tx_init(&sbt, max_prb) || srslte_softbuffer_rx_init(&sra, max_prb) ||
-      srslte_softbuffer_rx_init(&srb, max_prb))
+      srsgpu_shim_softbuffer_rx_init(&srb, max_prb))
     return 2;
   srslte_softbuffer_tx_t *sbt_p[SRSLTE_MAX_CODEWORDS] = {&sbt};
   srslte_softbuffer_rx_t *sra_p[SRSLTE_MAX_CODEWORDS] = {&sra}, *srb_p[SRSLTE_MAX_CODEWORDS] = {&srb};
@@ -211,7 +214,7 @@ int main(int argc, char **argv) {
       for (uint32_t i = 0; i < tbs / 8; i++) dtx[i] = (uint8_t)(urand() * 256);
       srslte_softbuffer_tx_reset(&sbt);
       srslte_softbuffer_rx_reset(&sra);
-      srslte_softbuffer_rx_reset(&srb);
+      srsgpu_shim_softbuffer_rx_reset(&srb);
       srslte_pdsch_cfg_t cfg;
       memset(&cfg, 0, sizeof(cfg));
       int rv[SRSLTE_MAX_CODEWORDS] = {0, 0};
@@ -291,6 +294,7 @@ int main(int argc, char **argv) {
   for (uint32_t a = 0; a < nof_rx; a++) released += srsgpu_shim_release(&ofdm[a]);
   released += srsgpu_shim_release(&chest);
   released += srsgpu_shim_release(&rx);
+  srsgpu_shim_softbuffer_rx_free(&srb);
   const int live = srsgpu_shim_live();
   if (released != (int)nof_rx + 2 || live != 0 || srsgpu_shim_release(&chest) != 0) nbad++;
   printf("sf=%u acks=%u mismatches=%u ofdm_err=%.3g ce_err=%.3g recreated=%d live=%d\n", nsf, nacks, nbad,

@@ -56,6 +56,10 @@ def test_shim_pdsch_decode_matches_reference(case):
     assert int(stats["mismatches"]) == 0 and int(stats["tx"]) >= case[6]
     assert int(stats["soft"]) <= max(1, int(stats["tx"]) // 10), r.stdout + r.stderr
     assert int(stats["acks"]) > 0
+    # reference-named DL-SCH drop-ins (srslte_dlsch_decode2, srslte_softbuffer_rx_*,
+    # srslte_rm_turbo_rx_lut) on the same LLRs: exact in every configuration
+    assert int(stats["dlsch"]) >= case[6] and int(stats["dlsch_mismatches"]) == 0, r.stdout + r.stderr
+    assert int(stats["rm_mismatches"]) == 0, r.stdout + r.stderr
 
 
 FRONT = os.path.join(REPO, "oracle", "_ref", "shim_front")
