@@ -110,9 +110,9 @@ static void shim_reset(shim_entry_t *e) {
   e->kind = kind;
 }
 
-/* Releases the GPU state of a reference object: srslte_ofdm_rx_free (ofdm.c:138),
- * srslte_chest_dl_free (chest_dl.c:171) and srslte_pdsch_free (pdsch.c:369) call it before they
- * clear the object. Returns 1 if the object had GPU state, 0 if not. */
+/* Releases the GPU state of a reference object: srslte_ofdm_rx_free (ofdm.c:356),
+ * srslte_chest_dl_free (chest_dl.c:173), srslte_pdsch_free (pdsch.c:344) and srslte_sch_free
+ * (sch.c:156) call it before they clear the object. Returns 1 if the object had GPU state. */
 int srsgpu_shim_release(const void *owner) {
   shim_entry_t *e = NULL;
   pthread_mutex_lock(&shim_mutex);
