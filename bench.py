@@ -528,7 +528,13 @@ def main():
         step()
     torch.cuda.synchronize()
     s.prof_enable(False)
-    kern_ms, kern_n = s.prof_get("k_win_bidir")
+    # the decoder kernel: k_win_bidir_run (all NHALF half-iterations in one launch) unless
+    # SRSGPU_TDEC_FUSED=0 selects one k_win_bidir launch per half-iteration
+    kern_name, halfits_per_launch = "k_win_bidir_run", NHALF
+    kern_ms, kern_n = s.prof_get(kern_name)
+    if not kern_n:
+        kern_name, halfits_per_launch = "k_win_bidir", 1
+        kern_ms, kern_n = s.prof_get(kern_name)
     # streaming: NSTREAMS batches in flight on their own streams (a receiver double/triple
     # buffering its batches); every batch is the full 4096-CB step
     ms_batches = [batch] + [s.TdecBatch(NCB, K, stream=torch.cuda.Stream(dev).cuda_stream)
@@ -569,12 +575,13 @@ def main():
     if rank == 0:
         workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
         avg_launch_ms = kern_ms / max(kern_n, 1)
-        # compulsory bytes of the whole decode, one NHALF-th per half-iteration launch
-        alg_bytes = COMPULSORY_BYTES_PER_CB * NCB / NHALF
+        # compulsory bytes of the whole decode, one NHALF-th per half-iteration
+        alg_bytes = COMPULSORY_BYTES_PER_CB * NCB / NHALF * halfits_per_launch
         achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
         pmc = load_profile_json(workload)
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-        roofline = {"bound": "hbm", "kernel": "k_win_bidir",
+        # PMC bytes only from a profile of this same kernel (per launch)
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc and pmc.get("kernel") == kern_name else None
+        roofline = {"bound": "hbm", "kernel": kern_name,
                     "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                     "traffic": traffic, "layout_traffic": traffic,
@@ -583,7 +590,9 @@ def main():
                     "alg_bytes_per_launch": int(alg_bytes),
                     "alg_bytes_def": "SURVEY 8(d): (3(K+32)+12)*2 + K/8 = %d B per CB per decode, / %d "
                                      "half-iterations" % (COMPULSORY_BYTES_PER_CB, NHALF),
-                    "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n}
+                    "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n,
+                    "halfits_per_launch": halfits_per_launch,
+                    "avg_halfit_ms": round(avg_launch_ms / halfits_per_launch, 4)}
         result = {
             "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": nranks,
             "steps": args.steps, "warmup": args.warmup,
@@ -604,10 +613,10 @@ def main():
         if kern_n:
             # the decoder's actual bound: int16 VALU work, SURVEY §8(d)'s algorithmic 90 ops per
             # info bit per half-iteration over the live launch time, against §8(d)'s peak
-            ops = ALG_OPS_PER_BIT_HALFIT * NCB * K
+            ops = ALG_OPS_PER_BIT_HALFIT * NCB * K * halfits_per_launch
             rate_t = ops / (avg_launch_ms / 1e3) / 1e12
             result["valu_roofline"] = {
-                "bound": "valu (packed int16)", "kernel": "k_win_bidir",
+                "bound": "valu (packed int16)", "kernel": kern_name,
                 "achieved": round(rate_t, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
                 "frac": round(rate_t / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": ops,
                 "alg_ops_def": "SURVEY 8(d): %d int16 ops per info bit per half-iteration" % ALG_OPS_PER_BIT_HALFIT,

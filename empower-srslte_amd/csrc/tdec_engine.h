@@ -517,9 +517,40 @@ struct TdecEngine {
       return -1;
     }
     if (load(impl, sb_layout, d_in, in_stride, Kv, n)) return -1;
-    for (uint32_t h = 0; h < nhalf; h++)
-      if (halfit((int)h, false, h + 1 == nhalf)) return -1;
+    if (halfits_fixed((int)nhalf)) return -1;
     return decide((int)nhalf - 1, d_out, out_stride, false);
+  }
+
+  // all nh half-iterations of a fixed-iteration job, decisions after the last: windowed kinds in
+  // one launch each (k_win_bidir_run), the sequential decoders one launch per half-iteration.
+  // SRSGPU_TDEC_FUSED=0 selects the per-half-iteration launches everywhere (A/B measurements).
+  int halfits_fixed(int nh) {
+    static const bool fused = [] {
+      const char *e = getenv("SRSGPU_TDEC_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    if (!fused || nh < 2) {
+      for (int h = 0; h < nh; h++)
+        if (halfit(h, false, h + 1 == nh)) return -1;
+      return 0;
+    }
+    last_n = nh - 1;
+    const TdArrays a = arrays();
+    for (int k = 0; k < TD_NKIND; k++) {
+      const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+      if (g1 <= g0) continue;
+      if (halfits_fusable(k)) {
+        ProfScope ps("k_win_bidir_run", st);
+        HIPCHK(launch_halfits(0, nh, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, st));
+      } else {
+        for (int h = 0; h < nh; h++) {
+          ProfScope ps(k == TD_KIND_SSE ? "k_sse_halfit" : "k_gen_halfit", st);
+          HIPCHK(launch_halfit(h, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], h + 1 == nh,
+                               a, nullptr, st));
+        }
+      }
+    }
+    return 0;
   }
 
   // early-stop decoding of one pass (planned groups) — maxh half-iterations at most

@@ -421,9 +421,12 @@ static const int16_t *tdec_input16(srslte_tdec_t *h, int16_t *input) {
 
 // 8-bit entry (tdec_iteration_8, turbodecoder.c:439-464): int8 values sign-extended into the
 // engine's int16 lanes; AUTO becomes the 8-bit AUTO choice
+// Converted once per code block, like the reference (turbodecoder.c:458): the input is only
+// uploaded by the first half-iteration, later calls just resolve the implementation.
 static const int16_t *tdec_input8(srslte_tdec_t *h, const int8_t *input, int *impl) {
   auto *g = (TdecGpu *)h->gpu;
   *impl = h->dec_type == SRSLTE_TDEC_AUTO ? SRSGPU_TDEC_AUTO_8BIT : (int)h->dec_type;
+  if (h->n_iter != 0) return g->conv.data();
   const size_t n = srsgpu_tdec_input_len(*impl, !h->force_not_sb, h->current_long_cb);
   g->conv.resize(n);
   for (size_t i = 0; i < n; i++) g->conv[i] = input[i];

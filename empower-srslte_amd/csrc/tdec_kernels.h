@@ -80,6 +80,11 @@ int dec_words_host(int K, int nb);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n) of every group of one kind
 hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
                          bool dec, const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
+// half-iterations n0 .. n0+nh-1 of every group of one windowed kind in one launch (fixed-iteration
+// jobs: no early stop in between); dec: decisions after the last one
+bool halfits_fusable(int kind);
+hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, int nblocks,
+                          size_t lds, bool dec, const TdArrays &a, hipStream_t st);
 // hard decision after half-iteration n for every pair of the job (npairs in total); early: also
 // the CRC, cb_done / cb_ok / noi and pair_done (turbodecoder.c:353-360, sch.c:361-391)
 hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,

@@ -43,6 +43,11 @@
 
 #include "tdec_kernels.h"
 
+// translation-unit part (see the launchers at the end); the file alone is part 0
+#ifndef TD_PART
+#define TD_PART 0
+#endif
+
 namespace srsgpu {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
@@ -429,7 +434,7 @@ template <int MODE> __device__ __forceinline__ int chunk_t(const Chunk<MODE> &c,
 
 #ifdef TD_TIMING
 // debug build only (make timing): shader-clock stamps per wave of the bidirectional decoder
-__device__ unsigned long long td_times[2048 * 8];
+static __device__ unsigned long long td_times[2048 * 8];
 #define TD_T(k)                                                                                    \
   do {                                                                                             \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {                                           \
@@ -439,7 +444,7 @@ __device__ unsigned long long td_times[2048 * 8];
   } while (0)
 // finer stamps: per chunk of phase 1 (slot q) and per phase-2 chunk (start / betas done / LLRs
 // done at 32 + 3 i, i = the i-th chunk the wave emits)
-__device__ unsigned long long td_chunk[2048 * 80];
+static __device__ unsigned long long td_chunk[2048 * 80];
 #define TD_C(k)                                                                                    \
   do {                                                                                             \
     __builtin_amdgcn_sched_barrier(0);                                                             \
@@ -978,6 +983,72 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
   TD_T(4);
 }
 
+// Half-iterations n0 .. n0+nh-1 of a fixed-iteration job in ONE launch (turbodecoder.c:510-533,
+// srslte_tdec_run_all's loop). A pair's 16 / 8 / 32 chains all sit in one workgroup, and the
+// interleaver permutes within a code block, so half-iteration n+1 of a pair reads only what this
+// workgroup wrote in half-iteration n: a workgroup barrier orders them (the waves of a workgroup
+// share the CU's L1, so workgroup-scope ordering is enough). Compared with one launch per
+// half-iteration, the waves never restart together: the start-up burst of every wave's prepass
+// loads (all 1024 waves at once, ~10 % of a half-iteration) happens once, and the launch gaps and
+// end-of-kernel skew go. Decisions only after the last half-iteration (early stop keeps the
+// per-half-iteration launches and k_decide between them). Arithmetic identical to k_win_bidir.
+template <int NB, int DIV, bool B8>
+__global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict__ groups, int ngroups,
+                                                       const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                       s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                       const s2 *__restrict__ T, size_t plane, int n0,
+                                                       int nh, int dout) {
+  extern __shared__ s4 cks[];
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K_ = G.K, npairs = G.npairs;
+  const int blk = blockIdx.x - G.blk_half;
+  const int lane_ = threadIdx.x & 63;
+  const int gl = blk * 64 + lane_;
+  const int nlanes = npairs * NB;
+  const int g = gl < nlanes ? gl : nlanes - 1;
+  const int pair = g / NB;
+  const int d_ = g % NB;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K_, NB);
+  const s4 *sp0_ = SP0 + base;
+  s2 *xp1_ = XP1 + base;
+  const s2 *p1_ = XP1 + plane + base;
+  s2 *A_ = Aarr + base;
+  uint32_t *D_ = Darr + G.dw0 + (size_t)pair * dec_words(K_, NB);
+  const s2 *tl_ = T + (size_t)(G.pair0 + pair) * 12;
+  const uint16_t *fwd0 = G.fwd, *rev0 = G.rev;
+  for (int n = n0; n < n0 + nh; n++) {
+    const bool dec = dout && n + 1 == n0 + nh;
+    if (n > n0) __syncthreads(); // the previous half-iteration's stores and LDS reads are done
+    // opaque copies of the loop invariants: without them the compiler hoists every body's
+    // address arithmetic out of the half-iteration loop, and the five bodies' hoisted values
+    // together no longer fit the register file (scratch spills)
+    const s4 *sp0 = sp0_;
+    s2 *xp1 = xp1_, *A = A_, *D_unused = nullptr;
+    const s2 *p1 = p1_, *tl = tl_;
+    uint32_t *D = D_;
+    const uint16_t *fw = fwd0, *rv = rev0;
+    int K = K_, d = d_, lane = lane_;
+    asm volatile("" : "+v"(sp0), "+v"(xp1), "+v"(A), "+v"(p1), "+v"(tl), "+v"(D), "+v"(d), "+v"(lane));
+    asm volatile("" : "+s"(fw), "+s"(rv), "+s"(K));
+    (void)D_unused;
+    const gptr_t<uint16_t> fwd = gptr(fw), rev = gptr(rv);
+    if (n & 1) {
+      if (dec)
+        win_bidir_body<NB, DIV, 1, true, B8>(sp0, xp1, p1, A, D, tl, fwd, cks, K, d, role, lane);
+      else
+        win_bidir_body<NB, DIV, 1, false, B8>(sp0, xp1, p1, A, D, tl, fwd, cks, K, d, role, lane);
+    } else if (n == 0) {
+      win_bidir_body<NB, DIV, 2, false, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+    } else {
+      if (dec)
+        win_bidir_body<NB, DIV, 0, true, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+      else
+        win_bidir_body<NB, DIV, 0, false, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ SSE non-window ----
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
@@ -1185,6 +1256,7 @@ __global__ __launch_bounds__(64) void k_gen_halfit(const TdGroup *__restrict__ g
 // consecutive steps k of all NB sub-blocks of one pair, reads NB runs of 64 natural positions
 // (coalesced), and writes the 64*NB SB-ordered elements contiguously. SB input (rm_turbo's
 // layout, streams at s*(K+32), tails at 3*(K+32); turbodecoder_iter.h:271-280) is a straight copy.
+#if TD_PART == 0 // loaders, decide: part 0 only
 #define LOAD_KT 64
 // input row of code block c: strided rows, or a per-CB pointer table (DL-SCH softbuffer rows)
 __device__ __forceinline__ gptr_t<int16_t> cb_row(const int16_t *in, size_t stride,
@@ -1490,15 +1562,18 @@ __global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int
   pair_done[p] = cb_done[c0] && cb_done[c1];
 }
 
+#endif // TD_PART == 0
+
 // ------------------------------------------------------------------ launchers ----
 
 static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 // dynamic LDS above 64 KiB (the 8-sub-block decoder at large K) needs the per-kernel opt-in
-static void allow_big_lds(const void *f) {
+[[maybe_unused]] static void allow_big_lds(const void *f) {
   (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+#if TD_PART == 0
 int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16) {
   if (sb_input && vec16) return (int)nblk((size_t)npairs * ((K / nb + 3) / 4) * (nb / 2), 256);
   if (sb_input) return (int)nblk((size_t)npairs * (K / 2), 256);
@@ -1545,60 +1620,120 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
   return hipGetLastError();
 }
 
+#endif // TD_PART == 0
+
+// Kernel instances by part, so the library builds in parallel translation units (each part
+// file defines TD_PART and includes this file): part 0 = loaders, decide and the dispatchers
+// below; parts 1-4 = the window decoders of one kind each (per-half-iteration and fused), part 2
+// also the sequential decoders.
+// one decoder kind's per-half-iteration (halfit_part) and fused (halfits_part) launchers,
+// specialised in the part that instantiates the kind
+template <int KIND>
+hipError_t halfit_part(int mode, const TdGroup *dg, int ng, int nblocks, size_t lds, bool dec,
+                       const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
+template <int KIND>
+hipError_t halfits_part(int n0, int nh, const TdGroup *dg, int ng, int nblocks, size_t lds, bool dec,
+                        const TdArrays &a, hipStream_t st);
+
+#define BIDIR1(nb, div, m, dout, b8)                                                               \
+  do {                                                                                             \
+    allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>));                 \
+    hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>), dim3(nblocks), dim3(128), \
+                       lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
+                       (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done);                     \
+  } while (0)
+#define BIDIR(nb, div, b8)                                                                         \
+  do {                                                                                             \
+    if (mode == 1) {                                                                               \
+      if (dec) BIDIR1(nb, div, 1, true, b8); else BIDIR1(nb, div, 1, false, b8);                   \
+    } else if (mode == 2) {                                                                        \
+      if (dec) BIDIR1(nb, div, 2, true, b8); else BIDIR1(nb, div, 2, false, b8);                   \
+    } else {                                                                                       \
+      if (dec) BIDIR1(nb, div, 0, true, b8); else BIDIR1(nb, div, 0, false, b8);                   \
+    }                                                                                              \
+  } while (0)
+#define SEQ(kern)                                                                                  \
+  do {                                                                                             \
+    if (mode == 1) SEQ1(kern, 1); else if (mode == 2) SEQ1(kern, 2); else SEQ1(kern, 0);           \
+  } while (0)
+#define SEQ1(kern, m)                                                                              \
+  hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
+                     (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
+                     (s2 *)a.scratch, pair_done)
+#define RUN1(nb, div, b8)                                                                          \
+  do {                                                                                             \
+    allow_big_lds((const void *)(k_win_bidir_run<nb, div, b8>));                                   \
+    hipLaunchKernelGGL((k_win_bidir_run<nb, div, b8>), dim3(nblocks), dim3(128), lds, st, dg, ng,  \
+                       (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,                 \
+                       (const s2 *)a.T, a.plane, n0, nh, dec ? 1 : 0);                             \
+  } while (0)
+#define PART_FUNCS(KIND, HALFIT_BODY, RUN_BODY)                                                    \
+  template <>                                                                                      \
+  hipError_t halfit_part<KIND>(int mode, const TdGroup *dg, int ng, int nblocks, size_t lds,       \
+                               bool dec, const TdArrays &a, const uint8_t *pair_done,              \
+                               hipStream_t st) {                                                   \
+    HALFIT_BODY;                                                                                   \
+    return hipGetLastError();                                                                      \
+  }                                                                                                \
+  template <>                                                                                      \
+  hipError_t halfits_part<KIND>(int n0, int nh, const TdGroup *dg, int ng, int nblocks, size_t lds, \
+                                bool dec, const TdArrays &a, hipStream_t st) {                     \
+    RUN_BODY;                                                                                      \
+    return hipGetLastError();                                                                      \
+  }
+
+#if TD_PART == 1
+PART_FUNCS(TD_KIND_W16, BIDIR(16, 0, false), RUN1(16, 0, false))
+#elif TD_PART == 2
+PART_FUNCS(TD_KIND_W8, BIDIR(8, 1, false), RUN1(8, 1, false))
+PART_FUNCS(TD_KIND_SSE, SEQ(k_sse_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
+           return hipErrorInvalidValue)
+PART_FUNCS(TD_KIND_GEN, SEQ(k_gen_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
+           return hipErrorInvalidValue)
+#elif TD_PART == 3
+PART_FUNCS(TD_KIND_B16, BIDIR(16, 1, true), RUN1(16, 1, true))
+#elif TD_PART == 4
+PART_FUNCS(TD_KIND_B32, BIDIR(32, 1, true), RUN1(32, 1, true))
+#endif
+#undef PART_FUNCS
+#undef RUN1
+#undef SEQ1
+#undef SEQ
+#undef BIDIR
+#undef BIDIR1
+
+#if TD_PART == 0
 hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
                          bool dec, const TdArrays &arr, const uint8_t *pair_done, hipStream_t st) {
   if (ng <= 0 || nblocks <= 0) return hipSuccess;
   const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
   TdArrays a = arr;
   if (!dec) a.D = nullptr;
-#define BIDIR1(nb, div, m, dout, b8)                                                               \
-  do {                                                                                             \
-    allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>));                 \
-    hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>), dim3(nblocks), dim3(128), \
-                       lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
-                       (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done);                                             \
-  } while (0)
-#define BIDIR(nb, div, m)                                                                          \
-  do {                                                                                             \
-    if (dec) BIDIR1(nb, div, m, true, false); else BIDIR1(nb, div, m, false, false);               \
-  } while (0)
-#define BIDIR8(nb, m)                                                                              \
-  do {                                                                                             \
-    if (dec) BIDIR1(nb, 1, m, true, true); else BIDIR1(nb, 1, m, false, true);                     \
-  } while (0)
-#define SEQ(kern, m)                                                                               \
-  hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
-                     (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
-                     (s2 *)a.scratch, pair_done)
   switch (kind) {
-  case TD_KIND_W16:
-    if (mode == 1) BIDIR(16, 0, 1); else if (mode == 2) BIDIR(16, 0, 2); else BIDIR(16, 0, 0);
-    break;
-  case TD_KIND_W8:
-    if (mode == 1) BIDIR(8, 1, 1); else if (mode == 2) BIDIR(8, 1, 2); else BIDIR(8, 1, 0);
-    break;
-  case TD_KIND_SSE:
-    if (mode == 1) SEQ(k_sse_halfit, 1); else if (mode == 2) SEQ(k_sse_halfit, 2); else SEQ(k_sse_halfit, 0);
-    break;
-  case TD_KIND_GEN:
-    if (mode == 1) SEQ(k_gen_halfit, 1); else if (mode == 2) SEQ(k_gen_halfit, 2); else SEQ(k_gen_halfit, 0);
-    break;
-  case TD_KIND_B16:
-  case TD_KIND_B32:
-    if (kind == TD_KIND_B16) {
-      if (mode == 1) BIDIR8(16, 1); else if (mode == 2) BIDIR8(16, 2); else BIDIR8(16, 0);
-    } else {
-      if (mode == 1) BIDIR8(32, 1); else if (mode == 2) BIDIR8(32, 2); else BIDIR8(32, 0);
-    }
-    break;
-  default:
-    return hipErrorInvalidValue;
+  case TD_KIND_W16: return halfit_part<TD_KIND_W16>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  case TD_KIND_W8: return halfit_part<TD_KIND_W8>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  case TD_KIND_SSE: return halfit_part<TD_KIND_SSE>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  case TD_KIND_GEN: return halfit_part<TD_KIND_GEN>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  case TD_KIND_B16: return halfit_part<TD_KIND_B16>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  case TD_KIND_B32: return halfit_part<TD_KIND_B32>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  default: return hipErrorInvalidValue;
   }
-#undef SEQ
-#undef BIDIR8
-#undef BIDIR
-#undef BIDIR1
-  return hipGetLastError();
+}
+
+bool halfits_fusable(int kind) {
+  return kind == TD_KIND_W16 || kind == TD_KIND_W8 || kind == TD_KIND_B16 || kind == TD_KIND_B32;
+}
+
+hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, int nblocks,
+                          size_t lds, bool dec, const TdArrays &a, hipStream_t st) {
+  if (ng <= 0 || nblocks <= 0 || nh <= 0) return hipSuccess;
+  switch (kind) {
+  case TD_KIND_W16: return halfits_part<TD_KIND_W16>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
+  case TD_KIND_W8: return halfits_part<TD_KIND_W8>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
+  case TD_KIND_B16: return halfits_part<TD_KIND_B16>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
+  case TD_KIND_B32: return halfits_part<TD_KIND_B32>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
+  default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *cb_done,
@@ -1619,10 +1754,11 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
                      early ? pair_done : nullptr);
   return hipGetLastError();
 }
+#endif // TD_PART == 0
 
 } // namespace srsgpu
 
-#ifdef TD_TIMING
+#if defined(TD_TIMING) && TD_PART == 1
 extern "C" int srsgpu_debug_td_chunk(unsigned long long *out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(srsgpu::td_chunk), sizeof(unsigned long long) * n) ==
                  hipSuccess

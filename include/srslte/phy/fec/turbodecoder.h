@@ -73,7 +73,8 @@ uint32_t srslte_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb);
 void srslte_tdec_iteration(srslte_tdec_t *h, int16_t *input, uint8_t *output);
 int srslte_tdec_run_all(srslte_tdec_t *h, int16_t *input, uint8_t *output,
                         uint32_t nof_iterations, uint32_t long_cb);
-/* turbodecoder.h:132-140 (int8 decoders: not provided, return -1 / no-op) */
+/* turbodecoder.h:132-140: the int8 decoders (turbodecoder.c:536-559), AUTO resolving to the
+   8-bit AUTO choice (SSE8 / AVX8 windows, 16-bit fallbacks, turbodecoder.c:392-464) */
 void srslte_tdec_iteration_8bit(srslte_tdec_t *h, int8_t *input, uint8_t *output);
 int srslte_tdec_run_all_8bit(srslte_tdec_t *h, int8_t *input, uint8_t *output,
                              uint32_t nof_iterations, uint32_t long_cb);
