@@ -1023,16 +1023,23 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
     // opaque copies of the loop invariants: without them the compiler hoists every body's
     // address arithmetic out of the half-iteration loop, and the five bodies' hoisted values
     // together no longer fit the register file (scratch spills)
-    const s4 *sp0 = sp0_;
-    s2 *xp1 = xp1_, *A = A_, *D_unused = nullptr;
-    const s2 *p1 = p1_, *tl = tl_;
-    uint32_t *D = D_;
-    const uint16_t *fw = fwd0, *rv = rev0;
+    // The copies go through the asm as global (address space 1) pointers: a generic pointer that
+    // leaves an asm is of unknown space to the compiler, and every access through it would be a
+    // flat instruction, which counts against lgkmcnt too (the checkpoint LDS waits would then wait
+    // for the chunk prefetches). The casts back to generic are address-space casts from global,
+    // which the address-space inference folds into global loads and stores.
+    gptr_t<s4> gsp0 = gptr(sp0_);
+    gmut_t<s2> gxp1 = gmut<s2>(xp1_), gA = gmut<s2>(A_);
+    gptr_t<s2> gp1 = gptr(p1_), gtl = gptr(tl_);
+    gmut_t<uint32_t> gD = gmut<uint32_t>(D_);
+    gptr_t<uint16_t> fwd = gptr(fwd0), rev = gptr(rev0);
     int K = K_, d = d_, lane = lane_;
-    asm volatile("" : "+v"(sp0), "+v"(xp1), "+v"(A), "+v"(p1), "+v"(tl), "+v"(D), "+v"(d), "+v"(lane));
-    asm volatile("" : "+s"(fw), "+s"(rv), "+s"(K));
-    (void)D_unused;
-    const gptr_t<uint16_t> fwd = gptr(fw), rev = gptr(rv);
+    asm volatile("" : "+v"(gsp0), "+v"(gxp1), "+v"(gA), "+v"(gp1), "+v"(gtl), "+v"(gD), "+v"(d), "+v"(lane));
+    asm volatile("" : "+s"(fwd), "+s"(rev), "+s"(K));
+    const s4 *sp0 = (const s4 *)gsp0;
+    s2 *xp1 = (s2 *)gxp1, *A = (s2 *)gA;
+    const s2 *p1 = (const s2 *)gp1, *tl = (const s2 *)gtl;
+    uint32_t *D = (uint32_t *)gD;
     if (n & 1) {
       if (dec)
         win_bidir_body<NB, DIV, 1, true, B8>(sp0, xp1, p1, A, D, tl, fwd, cks, K, d, role, lane);

@@ -242,3 +242,85 @@ int orc_dlsch_decode(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm
                           data[tbs / 8 + 2];
   return (par_rx == par_tx && par_rx) ? 0 : -1;
 }
+
+/* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469 -> srslte_rm_turbo_rx_lut_sse_8bit :543-):
+ * out[deinter[i % N]] += in[i] in int8 (wrapping; the order of the adds does not matter modulo
+ * 256), with the sub-block table of the 8-bit decoder (srslte_tdec_autoimp_get_subblocks_8bit) */
+int orc_rm_turbo_rx_8bit(const int8_t *in, int8_t *out, uint32_t in_len, uint32_t K, uint32_t rv) {
+  const uint32_t N = 3 * K + 12;
+  uint16_t *t = malloc(sizeof(uint16_t) * N);
+  if (!t || orc_rm_turbo_rx_table(K, rv, orc_autoimp_subblocks_8bit(K), t)) {
+    free(t);
+    return -1;
+  }
+  for (uint32_t i = 0; i < in_len; i++) {
+    const uint32_t o = t[i % N];
+    out[o] = (int8_t)(uint8_t)((uint32_t)(uint8_t)out[o] + (uint32_t)(uint8_t)in[i]);
+  }
+  free(t);
+  return 0;
+}
+
+/* decode_tb_cb with llr_is_8bit (sch.c:344-364): the softbuffer row holds int8 values
+ * ((int8_t *) buffer_f) and srslte_tdec_iteration_8bit decodes it; early stop on the CB / TB CRC
+ * after every half-iteration. The 8-bit AUTO choice at 400 < K <= 800 (8 sub-blocks) feeds the
+ * SSE16 window 3K+12 converted values of a 3(K+32)+12 sub-block row, the remaining inputs being
+ * whatever the decoder's conversion buffer last held (turbodecoder.c:439-459): no defined result,
+ * so such a TB is refused (-3). */
+int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm,
+                      uint32_t nof_e_bits, const int8_t *e_bits, uint8_t *data,
+                      uint32_t max_halfits, uint32_t *nof_iterations) {
+  orc_cbsegm_t s;
+  if (orc_segm(tbs, &s)) return -1;
+  if (s.tbs == 0 || s.C == 0) return 0;
+  if (s.F) return -2;
+  if (s.C > q->max_cb) return -2;
+  for (uint32_t i = 0; i < s.C; i++) {
+    const uint32_t K = i < s.C1 ? s.K1 : s.K2;
+    if (orc_autoimp_subblocks_8bit(K) == 8) return -3;
+  }
+  data[tbs / 8 + 0] = data[tbs / 8 + 1] = data[tbs / 8 + 2] = 0;
+  uint32_t iters = 0;
+  uint8_t *dec = malloc((size_t)max_halfits * (6144 / 8) + 64);
+  if (!dec) return -1;
+  for (uint32_t i = 0; i < s.C; i++) {
+    uint32_t K, rlen, rp, ne;
+    rx_cb_params(&s, Qm, nof_e_bits, i, &K, &rlen, &rp, &ne);
+    if (!q->cb_crc[i]) {
+      int8_t *sb = (int8_t *)(q->buffer + (size_t)i * ORC_SOFTBUFFER_SIZE);
+      if (orc_rm_turbo_rx_8bit(e_bits + rp, sb, ne, K, rv)) return -1;
+      const uint32_t poly = s.C > 1 ? ORC_CRC24B : ORC_CRC24A;
+      const uint32_t len = s.C > 1 ? K : tbs + 24;
+      uint8_t *out = data + i * rlen / 8;
+      /* decisions (packed bytes) after every half-iteration; the CRC decides where it stops */
+      if (orc_tdec8_run(ORC_TDEC_AUTO, 1, sb, K, max_halfits, dec) < 0) return -1;
+      uint32_t noi = 0;
+      int ok = 0;
+      while (noi < max_halfits && !ok) {
+        memcpy(out, dec + (size_t)noi * (K / 8), K / 8);
+        noi++;
+        ok = orc_crc_checksum_byte(poly, 24, out, len) == 0;
+      }
+      if (ok) q->cb_crc[i] = 1;
+      iters += noi;
+    } else {
+      memcpy(data + i * rlen / 8, q->data + (size_t)i * 768, rlen / 8);
+    }
+  }
+  free(dec);
+  q->tb_crc = 1;
+  for (uint32_t i = 0; i < s.C && q->tb_crc; i++) q->tb_crc = q->cb_crc[i];
+  if (!q->tb_crc) {
+    for (uint32_t i = 0; i < s.C; i++) {
+      uint32_t K, rlen, rp, ne;
+      rx_cb_params(&s, Qm, nof_e_bits, i, &K, &rlen, &rp, &ne);
+      if (q->cb_crc[i]) memcpy(q->data + (size_t)i * 768, data + i * rlen / 8, rlen / 8);
+    }
+  }
+  *nof_iterations = iters / s.C;
+  if (!q->tb_crc) return -1;
+  const uint32_t par_rx = orc_crc_checksum_byte(ORC_CRC24A, 24, data, tbs);
+  const uint32_t par_tx = ((uint32_t)data[tbs / 8] << 16) | ((uint32_t)data[tbs / 8 + 1] << 8) |
+                          data[tbs / 8 + 2];
+  return (par_rx == par_tx && par_rx) ? 0 : -1;
+}

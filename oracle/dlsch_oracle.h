@@ -29,6 +29,10 @@ int orc_dlsch_encode(uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_e_bits
 int orc_softbuffer_init(orc_softbuffer_t *q, uint32_t max_cb);
 void orc_softbuffer_reset(orc_softbuffer_t *q);
 void orc_softbuffer_free(orc_softbuffer_t *q);
+int orc_rm_turbo_rx_8bit(const int8_t *in, int8_t *out, uint32_t in_len, uint32_t K, uint32_t rv);
+int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm,
+                      uint32_t nof_e_bits, const int8_t *e_bits, uint8_t *data,
+                      uint32_t max_halfits, uint32_t *nof_iterations);
 int orc_dlsch_decode(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm,
                      uint32_t nof_e_bits, const int16_t *e_bits, uint8_t *data,
                      uint32_t max_halfits, uint32_t *nof_iterations);

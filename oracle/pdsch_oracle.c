@@ -358,3 +358,102 @@ int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e) {
   }
   return 0;
 }
+
+/* ---------------------------------------------------------------- 8-bit LLR chain ---------- */
+/* The reference's llr_is_8bit receive path (pdsch.c:795-806, sch.c:344-364): int8 soft demapping,
+ * int8 scrambling, the 8-bit CSI weighting and (dlsch_oracle.c) the 8-bit de-rate-matching. */
+static int8_t sat8(int32_t v) { return (int8_t)(v > 127 ? 127 : v < -128 ? -128 : v); }
+static int8_t wrap8(int32_t v) { return (int8_t)(uint8_t)(uint32_t)v; }
+static int8_t abs8(int8_t v) { return wrap8(v < 0 ? -(int32_t)v : v); } /* _mm_abs_epi8 */
+
+/* srslte_demod_soft_demodulate_b (demod_soft.c:458-477). SIMD blocks of 8 symbols (16 floats for
+ * QPSK's srslte_vec_convert_fb, vector_simd.c:433-462: cvttps + packs_epi32 + packs_epi16, i.e.
+ * truncate and saturate; the 16/64QAM SSE loops :153-178, :329-359: cvtps (nearest even), both
+ * packs, abs_epi8 / sub_epi8 wrap with offsets (int8)(2*30/sqrt 10) = 18, (int8)(4*40/sqrt 42) =
+ * 24, (int8)(2*40/sqrt 42) = 12). C tails: (int8_t) conversions (truncate, then the low byte), the
+ * offsets subtracted in double. */
+int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr) {
+  switch (mod) {
+  case 1: { /* demod_qpsk_lte_b :67-69 */
+    const float scale = (float)(-20 * sqrt(2));
+    const int len = 2 * nsym, simd = 16 * (len / 16);
+    for (int i = 0; i < simd; i++) llr[i] = sat8(sat16(cvt_rz(sym[i] * scale)));
+    for (int i = simd; i < len; i++) llr[i] = wrap8(cvt_rz(sym[i] * scale));
+    return 0;
+  }
+  case 2: { /* demod_16qam_lte_b_sse */
+    const int8_t off = (int8_t)(2 * 30 / sqrt(10));
+    const int simd = 8 * (nsym / 8);
+    for (int i = 0; i < simd; i++) {
+      const int8_t re = sat8(sat16(cvt_rn(sym[2 * i] * -30.0f)));
+      const int8_t im = sat8(sat16(cvt_rn(sym[2 * i + 1] * -30.0f)));
+      llr[4 * i + 0] = re;
+      llr[4 * i + 1] = im;
+      llr[4 * i + 2] = wrap8(abs8(re) - off);
+      llr[4 * i + 3] = wrap8(abs8(im) - off);
+    }
+    for (int i = simd; i < nsym; i++) { /* :180-191 */
+      const int16_t yre = (int8_t)wrap8(cvt_rz(30 * sym[2 * i]));
+      const int16_t yim = (int8_t)wrap8(cvt_rz(30 * sym[2 * i + 1]));
+      llr[4 * i + 0] = wrap8(-yre);
+      llr[4 * i + 1] = wrap8(-yim);
+      llr[4 * i + 2] = wrap8((int32_t)(abs(yre) - 2 * 30 / sqrt(10)));
+      llr[4 * i + 3] = wrap8((int32_t)(abs(yim) - 2 * 30 / sqrt(10)));
+    }
+    return 0;
+  }
+  case 3: { /* demod_64qam_lte_b_sse */
+    const int8_t off1 = (int8_t)(4 * 40 / sqrt(42)), off2 = (int8_t)(2 * 40 / sqrt(42));
+    const int simd = 8 * (nsym / 8);
+    for (int i = 0; i < simd; i++) {
+      const int8_t re = sat8(sat16(cvt_rn(sym[2 * i] * -40.0f)));
+      const int8_t im = sat8(sat16(cvt_rn(sym[2 * i + 1] * -40.0f)));
+      const int8_t a1r = wrap8(abs8(re) - off1), a1i = wrap8(abs8(im) - off1);
+      llr[6 * i + 0] = re;
+      llr[6 * i + 1] = im;
+      llr[6 * i + 2] = a1r;
+      llr[6 * i + 3] = a1i;
+      llr[6 * i + 4] = wrap8(abs8(a1r) - off2);
+      llr[6 * i + 5] = wrap8(abs8(a1i) - off2);
+    }
+    for (int i = simd; i < nsym; i++) { /* :360-371 */
+      const float yre = (int8_t)wrap8(cvt_rz(40 * sym[2 * i]));
+      const float yim = (int8_t)wrap8(cvt_rz(40 * sym[2 * i + 1]));
+      llr[6 * i + 0] = wrap8((int32_t)-yre);
+      llr[6 * i + 1] = wrap8((int32_t)-yim);
+      llr[6 * i + 2] = wrap8((int32_t)(abs((int)yre) - 4 * 40 / sqrt(42)));
+      llr[6 * i + 3] = wrap8((int32_t)(abs((int)yim) - 4 * 40 / sqrt(42)));
+      llr[6 * i + 4] = wrap8((int32_t)(abs(llr[6 * i + 2]) - 2 * 40 / sqrt(42)));
+      llr[6 * i + 5] = wrap8((int32_t)(abs(llr[6 * i + 3]) - 2 * 40 / sqrt(42)));
+    }
+    return 0;
+  }
+  default: /* BPSK is not a PDSCH modulation */
+    return -1;
+  }
+}
+
+/* srslte_scrambling_sb_offset (scrambling.c:53-56): srslte_vec_neg_bbb with c_char = 1 - 2c
+ * (_mm256_sign_epi8 / the C tail y < 0 ? -x : x, both wrapping at -128) */
+int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len) {
+  uint8_t *c = malloc(len + 1);
+  if (!c || orc_sequence(seed, len, c)) return -1;
+  for (uint32_t i = 0; i < len; i++)
+    if (c[i]) llr[i] = wrap8(-(int32_t)llr[i]);
+  free(c);
+  return 0;
+}
+
+/* csi_correction, 8-bit path (pdsch.c:707-713): e = (int8_t)((float)e * (csi / csi_max)) */
+int orc_csi_correction_b(int mod, const float *csi, int nsym, int8_t *e) {
+  const int qm = mod == 0 ? 1 : mod == 1 ? 2 : mod == 2 ? 4 : 6;
+  float cmax = -INFINITY;
+  for (int i = 0; i < nsym; i++)
+    if (csi[i] > cmax) cmax = csi[i];
+  if (nsym == 0) cmax = 1.0f;
+  for (int sy = 0; sy < nsym; sy++) {
+    const float c = csi[sy] / cmax;
+    for (int k = 0; k < qm; k++) e[qm * sy + k] = wrap8(cvt_rz((float)e[qm * sy + k] * c));
+  }
+  return 0;
+}

@@ -15,4 +15,8 @@ int orc_sequence(uint32_t seed, uint32_t len, uint8_t *c);
 uint32_t orc_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
 int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len);
 int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e);
+/* 8-bit LLR chain (llr_is_8bit) */
+int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
+int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);
+int orc_csi_correction_b(int mod, const float *csi, int nsym, int8_t *e);
 #endif

@@ -463,3 +463,69 @@ int ref_tdec8_run16(int impl, const int16_t *input, uint32_t K, uint32_t nof_hal
   srslte_tdec_free(&h);
   return 0;
 }
+
+/* ---------------------------------------------------------------- 8-bit LLR chain ---------- */
+/* srslte_demod_soft_demodulate_b (demod_soft.c:458-477) */
+int ref_demod_b(int mod, const float *sym, int nsym, int8_t *llr) {
+  cf_t *s = NULL;
+  int8_t *l = NULL;
+  if (posix_memalign((void **)&s, 64, (nsym + 16) * sizeof(cf_t))) return -1;
+  if (posix_memalign((void **)&l, 64, 6 * nsym + 64)) return -1;
+  memcpy(s, sym, nsym * sizeof(cf_t));
+  int r = srslte_demod_soft_demodulate_b((srslte_mod_t)mod, s, l, nsym);
+  const int bps = mod == SRSLTE_MOD_BPSK ? 1 : mod == SRSLTE_MOD_QPSK ? 2 : mod == SRSLTE_MOD_16QAM ? 4 : 6;
+  memcpy(llr, l, (size_t)bps * nsym);
+  free(s);
+  free(l);
+  return r;
+}
+
+/* srslte_scrambling_sb_offset (scrambling.c:53-56) with the PDSCH sequence */
+int ref_scramble_pdsch_sb(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id, int8_t *llr, uint32_t len) {
+  srslte_sequence_t seq;
+  memset(&seq, 0, sizeof(seq));
+  if (srslte_sequence_pdsch(&seq, rnti, q, nslot, cell_id, len)) return -1;
+  int8_t *l = NULL;
+  if (posix_memalign((void **)&l, 64, len + 64)) return -1;
+  memcpy(l, llr, len);
+  srslte_scrambling_sb_offset(&seq, l, 0, len);
+  memcpy(llr, l, len);
+  free(l);
+  srslte_sequence_free(&seq);
+  return 0;
+}
+
+/* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469): out += de-rate-matched in (int8) */
+int ref_rm_turbo_rx_8bit(const int8_t *input, int8_t *output, uint32_t in_len, uint32_t K, uint32_t rv) {
+  srslte_rm_turbo_gentables();
+  int idx = srslte_cbsegm_cbindex(K);
+  if (idx < 0) return -1;
+  int8_t *in = NULL;
+  if (posix_memalign((void **)&in, 64, in_len + 64)) return -1;
+  memcpy(in, input, in_len);
+  int r = srslte_rm_turbo_rx_lut_8bit(in, output, in_len, (uint32_t)idx, rv);
+  free(in);
+  return r;
+}
+
+/* srslte_dlsch_decode2 with llr_is_8bit (sch.c:344-364): int8 e bits -> data, on the same
+ * persistent softbuffers as ref_dlsch_decode */
+int ref_dlsch_decode8(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_e_bits,
+                      const int8_t *e_bits, uint8_t *data, uint32_t max_halfits, uint32_t *noi,
+                      uint8_t *cb_crc) {
+  if (ref_sch_get()) return -100;
+  if (slot < 0 || slot >= REF_NSLOT || !ref_sbrx_ready[slot]) return -100;
+  srslte_pdsch_cfg_t cfg;
+  ref_cfg(&cfg, tbs, rv, Qm, nof_e_bits);
+  srslte_sch_set_max_noi(&ref_sch, max_halfits);
+  int8_t *e = NULL;
+  if (posix_memalign((void **)&e, 64, nof_e_bits + 64)) return -100;
+  memcpy(e, e_bits, nof_e_bits);
+  ref_sch.llr_is_8bit = true;
+  int r = srslte_dlsch_decode2(&ref_sch, &cfg, &ref_sbrx[slot], e, data, 0);
+  ref_sch.llr_is_8bit = false;
+  free(e);
+  *noi = srslte_sch_last_noi(&ref_sch);
+  for (uint32_t i = 0; i < cfg.cb_segm[0].C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
+  return r;
+}

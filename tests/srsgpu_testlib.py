@@ -441,3 +441,86 @@ def ref_predecode_ccd(L, y, h, scaling=1.0, noise=0.0, csi=False):
     assert L.ref_predecode_ccd(*[v.ctypes.data_as(_f32p) for v in y + hh + x],
                                _ptr(c[0], _f32p), _ptr(c[1], _f32p), n, scaling, noise) == 0
     return (x, c) if csi else x
+
+
+# ------------------------------------------------------------------ 8-bit LLR chain ----
+class Llr8:
+    """The llr_is_8bit receive chain (pdsch.c:795-806, sch.c:344-364): int8 soft demapping,
+    int8 scrambling, the 8-bit CSI weighting, 8-bit de-rate-matching and the DL-SCH decode on int8
+    softbuffer rows. `lib` is the oracle (prefix orc_) or the reference harness (prefix ref_)."""
+
+    def __init__(self, lib, ref=False):
+        L = self.lib = lib.lib if hasattr(lib, "lib") else lib
+        self.ref = ref
+        u32 = ctypes.c_uint32
+        if ref:
+            L.ref_demod_b.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i8p]
+            L.ref_scramble_pdsch_sb.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32, _i8p, u32]
+            L.ref_rm_turbo_rx_8bit.argtypes = [_i8p, _i8p, u32, u32, u32]
+            L.ref_dlsch_decode8.argtypes = [ctypes.c_int, u32, u32, u32, u32, _i8p, _u8p, u32, _u32p,
+                                            _u8p]
+            L.ref_softbuffer_reset.argtypes = [ctypes.c_int, u32]
+            L.ref_cbsegm.argtypes = [u32, _u32p]
+        else:
+            L.orc_demod_b.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i8p]
+            L.orc_scramble_sb.argtypes = [u32, _i8p, u32]
+            L.orc_pdsch_seed.argtypes = [ctypes.c_uint16, ctypes.c_int, u32, u32]
+            L.orc_pdsch_seed.restype = u32
+            L.orc_csi_correction_b.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i8p]
+            L.orc_rm_turbo_rx_8bit.argtypes = [_i8p, _i8p, u32, u32, u32]
+            L.orc_dlsch_decode8.argtypes = [ctypes.POINTER(OrcSoftbuffer), u32, u32, u32, u32, _i8p,
+                                            _u8p, u32, _u32p]
+            L.orc_cbsegm.argtypes = [u32] + [_u32p] * 6
+
+    def demod(self, mod, sym):
+        sym = np.ascontiguousarray(sym, np.complex64)
+        llr = np.zeros(sym.size * BITS_PER_SYMBOL[mod], np.int8)
+        f = self.lib.ref_demod_b if self.ref else self.lib.orc_demod_b
+        assert f(mod, sym.ctypes.data_as(_f32p), sym.size, _ptr(llr, _i8p)) == 0
+        return llr
+
+    def scramble(self, rnti, q, nslot, cell_id, llr):
+        llr = np.array(llr, np.int8)
+        if self.ref:
+            assert self.lib.ref_scramble_pdsch_sb(rnti, q, nslot, cell_id, _ptr(llr, _i8p), llr.size) == 0
+        else:
+            seed = self.lib.orc_pdsch_seed(rnti, q, nslot, cell_id)
+            assert self.lib.orc_scramble_sb(seed, _ptr(llr, _i8p), llr.size) == 0
+        return llr
+
+    def csi_correction(self, mod, csi, llr):
+        csi = np.ascontiguousarray(csi, np.float32)
+        llr = np.array(llr, np.int8)
+        assert self.lib.orc_csi_correction_b(mod, csi.ctypes.data_as(_f32p), csi.size, _ptr(llr, _i8p)) == 0
+        return llr
+
+    def rm_rx(self, e, out, K, rv):
+        e = np.ascontiguousarray(e, np.int8)
+        f = self.lib.ref_rm_turbo_rx_8bit if self.ref else self.lib.orc_rm_turbo_rx_8bit
+        assert f(_ptr(e, _i8p), _ptr(out, _i8p), e.size, K, rv) == 0
+        return out
+
+    def segm_C(self, tbs):
+        o = np.zeros(6, np.uint32)
+        if self.ref:
+            self.lib.ref_cbsegm(tbs, _ptr(o, _u32p))
+            return int(o[0])
+        v = [ctypes.c_uint32(0) for _ in range(6)]
+        self.lib.orc_cbsegm(tbs, *[ctypes.byref(x) for x in v])
+        return v[0].value
+
+    def decode(self, sb, tbs, rv, Qm, e, max_halfits):
+        """sb: an OrcSoftbuffer (oracle) or a reference HARQ slot number"""
+        e = np.ascontiguousarray(e, np.int8)
+        data = np.zeros(tbs // 8 + 8, np.uint8)
+        noi = ctypes.c_uint32(0)
+        C = self.segm_C(tbs)
+        if self.ref:
+            crc = np.zeros(64, np.uint8)
+            r = self.lib.ref_dlsch_decode8(sb, tbs, rv, Qm, e.size, _ptr(e, _i8p), _ptr(data, _u8p),
+                                           max_halfits, ctypes.byref(noi), _ptr(crc, _u8p))
+            return r, data, noi.value, crc[:C]
+        r = self.lib.orc_dlsch_decode8(ctypes.byref(sb), tbs, rv, Qm, e.size, _ptr(e, _i8p),
+                                       _ptr(data, _u8p), max_halfits, ctypes.byref(noi))
+        cb_crc = np.ctypeslib.as_array(sb.cb_crc, shape=(sb.max_cb,))[:C].copy()
+        return r, data, noi.value, cb_crc

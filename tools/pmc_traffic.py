@@ -13,14 +13,28 @@ import csv
 import json
 import sys
 
-KERNEL = "k_win_bidir"
+# the fused fixed-iteration decoder (all 8 half-iterations per launch) when the run has it,
+# otherwise the per-half-iteration kernel; names matched up to the template argument list
+KERNELS = (("k_win_bidir_run", 8), ("k_win_bidir", 1))
+
+
+def kernel_of(path):
+    names = {r["Kernel_Name"] for r in csv.DictReader(open(path))}
+    for k, h in KERNELS:
+        if any(k + "<" in n or n.endswith(k) for n in names):
+            return k, h
+    raise SystemExit("no decoder kernel in " + path)
+
+
+KERNEL, HALFITS = kernel_of(sys.argv[1])
 
 
 def per_launch(path, counter):
     """counter summed over its instance rows per dispatch, averaged over the kernel's dispatches"""
     per = {}
     for r in csv.DictReader(open(path)):
-        if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        n = r["Kernel_Name"]
+        if (KERNEL + "<" in n or n.endswith(KERNEL)) and r["Counter_Name"] == counter:
             per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return sum(per.values()) / len(per), len(per)
 
@@ -28,12 +42,13 @@ def per_launch(path, counter):
 fetch_kib, nf = per_launch(sys.argv[1], "FETCH_SIZE")
 write_kib, nw = per_launch(sys.argv[2], "WRITE_SIZE")
 # SURVEY 8(d) compulsory bytes per launch: (3(K+32)+12)*2 + K/8 per CB per decode, / 8 half-its
-alg = ((3 * (6144 + 32) + 12) * 2 + 6144 // 8) * 4096 / 8
+alg = ((3 * (6144 + 32) + 12) * 2 + 6144 // 8) * 4096 / 8 * HALFITS
 fetch = fetch_kib * 1024 * 2  # gfx950: FETCH_SIZE counts half the bytes of 16-B/lane reads
 write = write_kib * 1024
 out = {
     "workload": "batched_turbo_decode_4096xK6144_8halfits",
     "kernel": KERNEL,
+    "halfits_per_launch": HALFITS,
     "launches": [nf, nw],
     "fetch_size_raw_bytes_per_launch": round(fetch_kib * 1024),
     "fetch_bytes_per_launch": round(fetch),
