@@ -130,6 +130,7 @@ struct DlschEngine {
   uint32_t *h_cbmap = nullptr;
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
+  bool llr8 = false; // srslte_sch_t.llr_is_8bit: int8 LLRs, 8-bit de-RM and decoders
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
@@ -352,6 +353,15 @@ struct DlschEngine {
         fprintf(stderr, "srsgpu: code blocks of this call exceed the capacity %u\n", cap);
         return -1;
       }
+      if (llr8 && (auto_subblocks_8bit(s.K1) == 8 || (s.C2 && auto_subblocks_8bit(s.K2) == 8))) {
+        // 400 < K <= 800: the reference's 8-bit AUTO choice feeds a 16-bit window 3K+12 converted
+        // values of a 3(K+32)+12 sub-block row (turbodecoder.c:439-459), the rest being whatever
+        // its conversion buffer last held: no defined result to reproduce
+        fprintf(stderr, "srsgpu: 8-bit LLRs with code block size %u have no defined decode "
+                        "(turbodecoder.c:439-459)\n", auto_subblocks_8bit(s.K1) == 8 ? s.K1 : s.K2);
+        ti.preset_ret = -2;
+        continue;
+      }
       ti.tbs = s.tbs;
       ti.C = s.C;
       ti.C1 = s.C1;
@@ -370,7 +380,7 @@ struct DlschEngine {
           ne = n_e + t.Qm;
           rp = (s.C - gamma) * n_e + (i - (s.C - gamma)) * ne;
         }
-        const uint32_t nsb = auto_subblocks(K);
+        const uint32_t nsb = llr8 ? auto_subblocks_8bit(K) : auto_subblocks(K);
         const uint16_t *tab = table(K, t.rv, nsb);
         const uint16_t *inv = inv_table(K, t.rv, nsb);
         if (!tab || !inv) return -1;
@@ -384,6 +394,7 @@ struct DlschEngine {
         it.cb_crc = ti.cb_crc + i;
         it.rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
         it.fresh = fresh + (size_t)t.softbuffer * max_cb + i;
+        it.w8 = llr8;
         max_n = std::max(max_n, std::min(ne, it.N));
         cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
       }
@@ -425,7 +436,7 @@ struct DlschEngine {
       p0 = p1;
     }
     if (!specs.empty() &&
-        tdec.decode_multi(SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
+        tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
                           (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi))
       return -1;
     {
@@ -569,12 +580,12 @@ int srsgpu_dlsch_encode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
   return q->e.encode(tb, nof_tb, d_data, d_e_bits);
 }
 
-int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
-                           uint32_t K, uint32_t rv, int sb_layout) {
+static int rm_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
+                     uint32_t K, uint32_t rv, uint32_t nsb, bool w8) {
   if (!q || !d_in || !d_out || rv > 3 || srsgpu::cb_index(K) < 0) return -1;
   DlschEngine &E = q->e;
   if (E.staged_pending) HIPCHK(hipEventSynchronize(E.staged));
-  const uint16_t *tab = E.table(K, rv, sb_layout ? srsgpu::auto_subblocks(K) : 0);
+  const uint16_t *tab = E.table(K, rv, nsb);
   if (!tab) return -1;
   srsgpu::DermItem &it = E.h_items[0];
   it.e = d_in;
@@ -586,11 +597,26 @@ int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_ou
   it.cb_crc = nullptr;
   it.pos = 0;
   it.fresh = nullptr;
+  it.w8 = w8;
   HIPCHK(hipMemcpyAsync(E.d_items, E.h_items, sizeof(srsgpu::DermItem), hipMemcpyHostToDevice, E.st));
   HIPCHK(hipEventRecord(E.staged, E.st));
   E.staged_pending = true;
   HIPCHK(srsgpu::launch_derm_rmw(E.d_items, std::min(in_len, 3 * K + 12), E.st));
   return 0;
+}
+
+int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
+                           uint32_t K, uint32_t rv, int sb_layout) {
+  return rm_rx_dev(q, d_in, d_out, in_len, K, rv, sb_layout ? srsgpu::auto_subblocks(K) : 0, false);
+}
+
+int srsgpu_rm_turbo_rx_8bit_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out,
+                                uint32_t in_len, uint32_t K, uint32_t rv) {
+  return rm_rx_dev(q, d_in, d_out, in_len, K, rv, srsgpu::auto_subblocks_8bit(K), true);
+}
+
+void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable) {
+  if (q) q->e.llr8 = enable != 0;
 }
 
 } // extern "C"

@@ -20,6 +20,8 @@ struct DermItem {
   uint32_t pos;           // position in the decoder's (K-grouped) CB order
   uint32_t rowlen;        // decoder-input length of the row: 3(K+32)+12 (SB) or 3K+12
   uint8_t *fresh;         // row reset since its last use: content counts as zero (cleared here)
+  uint32_t w8;            // 8-bit LLR chain (llr_is_8bit, rm_turbo.c:432-469): int8 values held
+                          // sign-extended in the int16 row, sums wrapping at 8 bits
 };
 
 // one transport block's epilogue

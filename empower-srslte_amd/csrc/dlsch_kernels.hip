@@ -17,6 +17,19 @@
 
 namespace srsgpu {
 
+// Pointers read from an item descriptor are generic to the compiler, and accesses through them
+// become flat instructions, which count against lgkmcnt too (the LDS waits then wait for global
+// loads in flight). The descriptors only ever point at global memory: say so.
+template <typename T> using gp_t = T __attribute__((address_space(1))) *;
+template <typename T> __device__ __forceinline__ gp_t<T> glob(T *p) {
+  return (gp_t<T>)(__attribute__((address_space(1))) void *)(uintptr_t)p;
+}
+typedef uint32_t u4v __attribute__((ext_vector_type(4))); // HIP's uint4 class has no AS-1 methods
+// one softbuffer entry: int16 wrap, or (w8) int8 wrap sign-extended into the int16 entry
+__device__ __forceinline__ uint32_t derm_fold(uint32_t v, bool w8) {
+  return w8 ? (uint32_t)(uint16_t)(int16_t)(int8_t)(uint8_t)v : v & 0xFFFFu;
+}
+
 // One workgroup per code block, gathering by row position: entry o of the softbuffer row becomes
 // old[o] (or 0 when the row was reset since its last use: lazy reset, no memset pass) plus the
 // sum of the E received LLRs e[i] with i = m (mod N), m = inv[o] the circular-buffer entry that
@@ -31,20 +44,21 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
   const int g = blockIdx.x;
   if (g >= nitems) return;
   const DermItem it = items[g];
-  const uint8_t skip = it.cb_crc ? *it.cb_crc : 0;
+  const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
   if (threadIdx.x == 0) init_done[it.pos] = skip;
   if (skip) return; // sch.c:323: blocks whose CRC passed before are not combined again
-  const bool fresh = it.fresh && *it.fresh;
+  const bool fresh = it.fresh && *glob(it.fresh);
+  const bool w8 = it.w8 != 0;
   const uint32_t N = it.N, ne = it.ne, len = it.rowlen;
-  const uint16_t *__restrict__ e = reinterpret_cast<const uint16_t *>(it.e);
-  auto add = [&](uint32_t old, uint32_t m) -> uint32_t { // one int16 entry, wrapping
+  const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(it.e));
+  auto add = [&](uint32_t old, uint32_t m) -> uint32_t { // one entry, wrapping
     uint32_t acc = old;
     for (uint32_t i = m; i < ne; i += N) acc += e[i];
-    return acc & 0xFFFFu;
+    return derm_fold(acc, w8);
   };
   const uint32_t nv = (len + 7) / 8; // the inverse table is padded: entries past len are 0xFFFF
-  const uint4 *__restrict__ inv = reinterpret_cast<const uint4 *>(it.inv);
-  uint4 *__restrict__ row = reinterpret_cast<uint4 *>(it.row);
+  const gp_t<const u4v> inv = glob(reinterpret_cast<const u4v *>(it.inv));
+  const gp_t<u4v> row = glob(reinterpret_cast<u4v *>(it.row));
   // rows hold SOFTBUFFER_SIZE entries, so the padded tail of the last vector stays inside the
   // row; entries past len keep their value (or become 0 on a fresh row)
   if (ne <= N && ne <= DERM_LDS) {
@@ -53,7 +67,7 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
     // one address-unit slot per lane)
     const uint32_t nw = (ne + 1) / 2;
     if (((uintptr_t)it.e & 3) == 0) { // E is even for every Qm; an odd tail is read alone
-      const uint32_t *__restrict__ e32 = reinterpret_cast<const uint32_t *>(it.e);
+      const gp_t<const uint32_t> e32 = glob(reinterpret_cast<const uint32_t *>(it.e));
       for (uint32_t w = threadIdx.x; w < ne / 2; w += blockDim.x) es[w] = e32[w];
       if ((ne & 1) && threadIdx.x == 0) es[ne / 2] = e[ne - 1];
     } else {
@@ -64,22 +78,25 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
     const uint16_t *el = reinterpret_cast<const uint16_t *>(es);
 #pragma unroll 4
     for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
-      const uint4 iv = inv[v];
-      const uint4 ov = fresh ? make_uint4(0, 0, 0, 0) : row[v];
+      const u4v iv = inv[v];
+      const u4v ov = fresh ? u4v{0, 0, 0, 0} : row[v];
       const uint32_t im[4] = {iv.x, iv.y, iv.z, iv.w}, om[4] = {ov.x, ov.y, ov.z, ov.w};
       uint32_t r[4];
 #pragma unroll
       for (int h = 0; h < 4; h++) {
         const uint32_t m0 = im[h] & 0xFFFFu, m1 = im[h] >> 16;
         const uint32_t e0 = m0 < ne ? el[m0] : 0u, e1 = m1 < ne ? el[m1] : 0u; // 0xFFFF >= ne
-        r[h] = ((om[h] + e0) & 0xFFFFu) | (((om[h] >> 16) + e1) << 16);
+        if (w8)
+          r[h] = derm_fold(om[h] + e0, true) | (derm_fold((om[h] >> 16) + e1, true) << 16);
+        else
+          r[h] = ((om[h] + e0) & 0xFFFFu) | (((om[h] >> 16) + e1) << 16);
       }
-      row[v] = make_uint4(r[0], r[1], r[2], r[3]);
+      row[v] = u4v{r[0], r[1], r[2], r[3]};
     }
   } else {
     for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) {
-      const uint4 iv = inv[v];
-      const uint4 ov = fresh ? make_uint4(0, 0, 0, 0) : row[v];
+      const u4v iv = inv[v];
+      const u4v ov = fresh ? u4v{0, 0, 0, 0} : row[v];
       const uint32_t im[4] = {iv.x, iv.y, iv.z, iv.w}, om[4] = {ov.x, ov.y, ov.z, ov.w};
       uint32_t r[4];
 #pragma unroll
@@ -89,11 +106,11 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
         const uint32_t hi = m1 == 0xFFFFu ? om[h] >> 16 : add(om[h] >> 16, m1);
         r[h] = lo | (hi << 16);
       }
-      row[v] = make_uint4(r[0], r[1], r[2], r[3]);
+      row[v] = u4v{r[0], r[1], r[2], r[3]};
     }
   }
   __syncthreads();
-  if (fresh && threadIdx.x == 0) *it.fresh = 0; // the row now holds real soft bits
+  if (fresh && threadIdx.x == 0) *glob(it.fresh) = 0; // the row now holds real soft bits
 }
 
 // srsgpu_rm_turbo_rx_dev: arbitrary output buffers, read-modify-write in place (one block)
@@ -105,7 +122,7 @@ __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ i
     uint32_t acc = 0;
     for (uint32_t i = m; i < it.ne; i += N) acc += (uint16_t)it.e[i];
     const uint32_t o = it.table[m];
-    it.row[o] = (int16_t)(uint16_t)((uint16_t)it.row[o] + acc);
+    it.row[o] = (int16_t)(uint16_t)derm_fold((uint16_t)it.row[o] + acc, it.w8 != 0);
   }
 }
 

@@ -77,6 +77,7 @@ struct PdschEngine {
   srsgpu_cell_t cell{};
   uint32_t max_sf = 0;
   bool csi = false;
+  bool llr8 = false; // srslte_pdsch_t.llr_is_8bit
   const float *noise_dev = nullptr; // per-subframe chest noise estimates (nof_rx_ant each)
   srsgpu_dlsch_t *dl = nullptr;
   // Gold tables: x1 and the 31 x2 basis sequences, bits 0 .. 32*words-1
@@ -258,6 +259,7 @@ struct PdschEngine {
         t.cdd = s.mimo_type == SRSGPU_MIMO_CDD;
         t.layer = (int)cw;
         t.csi_mode = csi ? 1 : 0;
+        t.llr8 = llr8 ? 1 : 0;
         t.aligned = ((uintptr_t)t.e % 4) == 0;
         t.noise = s.noise_estimate;
         t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant * cell.nof_ports : nullptr;
@@ -412,6 +414,12 @@ void srsgpu_pdsch_set_noise_dev(srsgpu_pdsch_t *q, const float *d_noise) {
 
 void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {
   if (q) q->e.csi = enable != 0;
+}
+
+void srsgpu_pdsch_set_llr_8bit(srsgpu_pdsch_t *q, int enable) {
+  if (!q) return;
+  q->e.llr8 = enable != 0;
+  srsgpu_dlsch_set_llr_8bit(q->e.dl, enable);
 }
 
 srsgpu_dlsch_t *srsgpu_pdsch_get_dlsch(srsgpu_pdsch_t *q) { return q ? q->e.dl : nullptr; }

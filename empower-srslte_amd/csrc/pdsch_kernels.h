@@ -31,6 +31,7 @@ struct LlrItem {
   float noise, inv_scaling, scaling;
   const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does
   int nports;              // ports in noise_dev
+  int llr8;                // llr_is_8bit: int8 demapping / scrambling / CSI, values sign-extended in e
 };
 
 // one codeword to transmit: scramble + modulate + map

@@ -246,6 +246,71 @@ __device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr,
   }
 }
 
+// int8 LLRs of symbol j: srslte_demod_soft_demodulate_b (demod_soft.c:458-477). SIMD blocks of 8
+// symbols: QPSK srslte_vec_convert_fb (vector_simd.c:433-462: cvttps, packs_epi32, packs_epi16 =
+// truncate and saturate), 16/64QAM demod_*_lte_b_sse (:138-191, :306-372: cvtps nearest-even, both
+// packs, abs_epi8 and sub_epi8 wrapping with the int8 offsets 18 / 24, 12); C tails: (int8_t)
+// conversions (truncate, low byte) and the offsets subtracted in double.
+__device__ __forceinline__ int16_t sat8(int32_t v) { return (int16_t)(v > 127 ? 127 : v < -128 ? -128 : v); }
+__device__ __forceinline__ int16_t wrap8(int32_t v) { return (int16_t)(int8_t)(uint8_t)(uint32_t)v; }
+__device__ __forceinline__ int16_t abs8(int16_t v) { return wrap8(v < 0 ? -(int32_t)v : v); }
+__device__ __forceinline__ void demap8(int mod, uint32_t j, uint32_t n, float xr, float xi,
+                                       int16_t *o) {
+  switch (mod) {
+  case 0: // BPSK demod_bpsk_lte_b (:49-53)
+    o[0] = wrap8((int32_t)((double)(-20.0f * (xr + xi)) / 1.4142135623730951));
+    break;
+  case 1: { // QPSK srslte_vec_convert_fb(-20 sqrt 2): 16-float SIMD blocks, C tail
+    const float sc = -28.284271247461902f;
+    const bool simd = 2 * j + 1 < 16 * ((2 * n) / 16);
+    const float a = __fmul_rn(xr, sc), b = __fmul_rn(xi, sc);
+    o[0] = simd ? sat8(sat16(cvt_rz(a))) : wrap8(cvt_rz(a));
+    o[1] = simd ? sat8(sat16(cvt_rz(b))) : wrap8(cvt_rz(b));
+    break;
+  }
+  case 2: { // 16QAM
+    if (j < 8 * (n / 8)) {
+      const int16_t re = sat8(sat16(cvt_rn(__fmul_rn(xr, -30.f))));
+      const int16_t im = sat8(sat16(cvt_rn(__fmul_rn(xi, -30.f))));
+      o[0] = re;
+      o[1] = im;
+      o[2] = wrap8(abs8(re) - 18);
+      o[3] = wrap8(abs8(im) - 18);
+    } else {
+      const int16_t yre = wrap8(cvt_rz(__fmul_rn(30.f, xr)));
+      const int16_t yim = wrap8(cvt_rz(__fmul_rn(30.f, xi)));
+      o[0] = wrap8(-(int32_t)yre);
+      o[1] = wrap8(-(int32_t)yim);
+      o[2] = wrap8((int32_t)((double)abs(yre) - 18.973665961010276));
+      o[3] = wrap8((int32_t)((double)abs(yim) - 18.973665961010276));
+    }
+    break;
+  }
+  default: { // 64QAM
+    if (j < 8 * (n / 8)) {
+      const int16_t re = sat8(sat16(cvt_rn(__fmul_rn(xr, -40.f))));
+      const int16_t im = sat8(sat16(cvt_rn(__fmul_rn(xi, -40.f))));
+      const int16_t a1r = wrap8(abs8(re) - 24), a1i = wrap8(abs8(im) - 24);
+      o[0] = re;
+      o[1] = im;
+      o[2] = a1r;
+      o[3] = a1i;
+      o[4] = wrap8(abs8(a1r) - 12);
+      o[5] = wrap8(abs8(a1i) - 12);
+    } else {
+      const float yre = (float)wrap8(cvt_rz(__fmul_rn(40.f, xr)));
+      const float yim = (float)wrap8(cvt_rz(__fmul_rn(40.f, xi)));
+      o[0] = wrap8((int32_t)-yre);
+      o[1] = wrap8((int32_t)-yim);
+      o[2] = wrap8((int32_t)((double)abs((int)yre) - 24.688535993934706));
+      o[3] = wrap8((int32_t)((double)abs((int)yim) - 24.688535993934706));
+      o[4] = wrap8((int32_t)((double)abs((int)o[2]) - 12.344267996967353));
+      o[5] = wrap8((int32_t)((double)abs((int)o[3]) - 12.344267996967353));
+    }
+  }
+  }
+}
+
 template <int MOD>
 __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
@@ -253,14 +318,18 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     const uint32_t pos = t.map[j];
     const Eq e = t.cdd ? equalise_cdd(t, pos, j) : equalise(t, pos, j);
     int16_t o[Q];
-    demap(MOD, j, t.nof_re, e.xr, e.xi, o);
+    if (t.llr8)
+      demap8(MOD, j, t.nof_re, e.xr, e.xi, o);
+    else
+      demap(MOD, j, t.nof_re, e.xr, e.xi, o);
     // scrambling bits b0 .. b0+Q-1 (may straddle two words)
     const uint32_t b0 = j * Q, w = b0 >> 5, sh = b0 & 31;
     const uint64_t cw = (uint64_t)t.c[w] | ((uint64_t)t.c[w + 1] << 32);
     const uint32_t cb = (uint32_t)(cw >> sh);
 #pragma unroll
     for (int k = 0; k < Q; k++)
-      if ((cb >> k) & 1) o[k] = wrap16(-(int32_t)o[k]); // _mm256_sign_epi16 by c_short = 1 - 2c
+      if ((cb >> k) & 1) // _mm256_sign_epi16 / _epi8 (scrambling_sb_offset) by c = 1 - 2c
+        o[k] = t.llr8 ? wrap8(-(int32_t)o[k]) : wrap16(-(int32_t)o[k]);
     if (Q % 2 == 0 && t.aligned) {
       uint32_t *dst = reinterpret_cast<uint32_t *>(t.e + b0);
 #pragma unroll
@@ -315,6 +384,11 @@ __global__ __launch_bounds__(256) void k_csi_correct(const LlrItem *__restrict__
     simd_bits = nbits >= 12 ? ((nbits - 12) / 12 + 1) * 12 : 0;
   for (uint32_t n = blockIdx.x * 256 + threadIdx.x; n < nbits; n += gridDim.x * 256) {
     int16_t v = t.e[n];
+    if (t.llr8) { // pdsch.c:707-713: (int8_t)((float)e * (csi / csi_max)), no SIMD part
+      const float c = __fdiv_rn(t.csi[n / t.qm], cmax);
+      t.e[n] = wrap8(cvt_rz(__fmul_rn((float)v, c)));
+      continue;
+    }
     if (n < simd_bits) {
       uint32_t sym;
       if (t.mod == 1) { // 4 LLRs = symbols 2g, 2g+1; lanes 0,1 take csi[2g+1], lanes 2,3 csi[2g]

@@ -146,6 +146,9 @@ _sig = {
     "srsgpu_pdsch_destroy": (None, [_vp]),
     "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
+    "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
     "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
     "srsgpu_pdsch_get_dlsch": (_vp, [_vp]),
     "srsgpu_pdsch_llr_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz, _vp,
@@ -410,6 +413,13 @@ class Dlsch:
     def rm_rx_dev(self, d_in, d_out, in_len, K, rv, sb_layout):
         return _lib.srsgpu_rm_turbo_rx_dev(self.q, _vp(d_in), _vp(d_out), in_len, K, rv, sb_layout)
 
+    def set_llr_8bit(self, on):
+        """srslte_sch_t.llr_is_8bit: e_bits hold int8 values (int16 elements)"""
+        _lib.srsgpu_dlsch_set_llr_8bit(self.q, 1 if on else 0)
+
+    def rm_rx_8bit_dev(self, d_in, d_out, in_len, K, rv):
+        return _lib.srsgpu_rm_turbo_rx_8bit_dev(self.q, _vp(d_in), _vp(d_out), in_len, K, rv)
+
     def close(self):
         if self.q:
             _lib.srsgpu_dlsch_destroy(self.q)
@@ -471,6 +481,10 @@ class Pdsch:
 
     def set_csi(self, on):
         _lib.srsgpu_pdsch_set_csi(self.q, 1 if on else 0)
+
+    def set_llr_8bit(self, on):
+        """srslte_pdsch_t.llr_is_8bit: int8 LLR chain (values held in the int16 LLR elements)"""
+        _lib.srsgpu_pdsch_set_llr_8bit(self.q, 1 if on else 0)
 
     def set_noise_dev(self, d_noise):
         _lib.srsgpu_pdsch_set_noise_dev(self.q, _vp(d_noise) if d_noise else None)

@@ -91,6 +91,19 @@ int srsgpu_dlsch_encode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
 int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out, uint32_t in_len,
                            uint32_t K, uint32_t rv, int sb_layout);
 
+/* 8-bit LLR chain (srslte_sch_t.llr_is_8bit; sch.c:344-364). Enabled, srsgpu_dlsch_decode(_dev)
+ * takes int8 LLRs held in the int16 e-bits elements (values in [-128, 127]), de-rate-matches them
+ * as srslte_rm_turbo_rx_lut_8bit (int8 sums wrapping at 8 bits, held sign-extended in the int16
+ * softbuffer rows, the 8-bit decoder's sub-block table) and decodes with
+ * srslte_tdec_iteration_8bit's decoders (SRSGPU_TDEC_AUTO_8BIT). A TB with a code block of
+ * 400 < K <= 800 returns -2: the reference's 8-bit AUTO choice has no defined result there
+ * (turbodecoder.c:439-459). Softbuffers must not change mode between transmissions of a TB. */
+void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable);
+/* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469) on device buffers, int8 values held in int16
+ * elements: d_out[t[i % (3K+12)]] += d_in[i], wrapping at 8 bits, 8-bit decoder sub-block table. */
+int srsgpu_rm_turbo_rx_8bit_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out,
+                                uint32_t in_len, uint32_t K, uint32_t rv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,6 +75,11 @@ int srsgpu_pdsch_create(srsgpu_pdsch_t **q, const srsgpu_cell_t *cell, uint32_t 
 void srsgpu_pdsch_destroy(srsgpu_pdsch_t *q);
 void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *hip_stream);
 void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable); /* srslte_pdsch_enable_csi */
+/* srslte_pdsch_t.llr_is_8bit (+ srslte_sch_t.llr_is_8bit of its DL-SCH): int8 soft demapping
+ * (srslte_demod_soft_demodulate_b), int8 scrambling (srslte_scrambling_sb_offset), the 8-bit CSI
+ * weighting (pdsch.c:707-713), 8-bit de-rate-matching and decoders (pdsch.c:795-806,
+ * sch.c:344-364). The LLRs stay int16 elements holding int8 values. */
+void srsgpu_pdsch_set_llr_8bit(srsgpu_pdsch_t *q, int enable);
 /* Take the MMSE noise term from device memory instead of sf[i].noise_estimate: subframe i of a
  * call uses the mean of d_noise[i*nof_rx_ant + a] (the channel estimator's per-antenna outputs,
  * as srslte_chest_dl_get_noise_estimate averages them). NULL restores sf[i].noise_estimate. */

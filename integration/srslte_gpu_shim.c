@@ -34,6 +34,7 @@
 #include <pthread.h>
 #include <stdbool.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "srslte/phy/ch_estimation/chest_dl.h"
@@ -365,10 +366,6 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
                          int16_t *e_bits, uint8_t *data, int tb_idx) {
   if (!q || !cfg || !softbuffer || !e_bits || !data || tb_idx < 0 || tb_idx >= SRSLTE_MAX_CODEWORDS)
     return SRSLTE_ERROR_INVALID_INPUTS;
-  if (q->llr_is_8bit) {
-    fprintf(stderr, "srsgpu shim: GPU DL-SCH decode takes 16-bit LLRs\n");
-    return SRSLTE_ERROR;
-  }
   const uint32_t Nl = cfg->nof_layers != (uint32_t)SRSLTE_RA_DL_GRANT_NOF_TB(&cfg->grant) ? 2 : 1;
   const uint32_t tbs = cfg->cb_segm[tb_idx].tbs, nof_e = cfg->nbits[tb_idx].nof_bits;
   shim_entry_t *e = shim_get(q, SHIM_SCH);
@@ -389,7 +386,17 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
   const int slot = shim_softbuffer(e, dl, softbuffer);
   if (slot < 0) return SRSLTE_ERROR;
   srsgpu_dlsch_tb_t tb = {tbs, cfg->rv[tb_idx], cfg->grant.Qm[tb_idx] * Nl, nof_e, (uint32_t)slot, 0, 0};
-  hipMemcpy(e->d_a, e_bits, sizeof(int16_t) * nof_e, H2D);
+  /* llr_is_8bit (sch.c:344-364): e_bits holds int8 LLRs; the GPU takes them as int16 elements */
+  srsgpu_dlsch_set_llr_8bit(dl, q->llr_is_8bit);
+  if (q->llr_is_8bit) {
+    int16_t *w = malloc(sizeof(int16_t) * (nof_e ? nof_e : 1));
+    if (!w) return SRSLTE_ERROR;
+    for (uint32_t i = 0; i < nof_e; i++) w[i] = ((const int8_t *)e_bits)[i];
+    hipMemcpy(e->d_a, w, sizeof(int16_t) * nof_e, H2D);
+    free(w);
+  } else {
+    hipMemcpy(e->d_a, e_bits, sizeof(int16_t) * nof_e, H2D);
+  }
   int32_t *d_ret = (int32_t *)e->d_c;
   uint32_t *d_noi = (uint32_t *)e->d_c + 1;
   if (srsgpu_dlsch_decode_dev(dl, &tb, 1, (const int16_t *)e->d_a, (uint8_t *)e->d_b, q->max_iterations,
@@ -440,6 +447,41 @@ out:
   return ret;
 }
 
+/* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469): the same on int8 buffers (sums wrapping at 8
+ * bits, the 8-bit decoder's sub-block table), through int16 device elements */
+int srslte_rm_turbo_rx_lut_8bit(int8_t *input, int8_t *output, uint32_t in_len, uint32_t cb_idx,
+                                uint32_t rv_idx) {
+  if (rv_idx >= 4 || cb_idx >= SRSLTE_NOF_TC_CB_SIZES || !input || !output) {
+    printf("Invalid inputs rv_idx=%d, cb_idx=%d\n", rv_idx, cb_idx);
+    return SRSLTE_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cb_idx), out_len = 3 * (K + 32) + 12;
+  int16_t *w = malloc(sizeof(int16_t) * (in_len > out_len ? in_len : out_len));
+  if (!w) return SRSLTE_ERROR;
+  int ret = SRSLTE_ERROR;
+  pthread_mutex_lock(&shim_mutex);
+  if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
+  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * 3 * (SRSLTE_TCOD_MAX_LEN_CB + 4));
+  if (in_len > shim_rm.cap) {
+    if (shim_rm.d_in) hipFree(shim_rm.d_in);
+    hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
+    shim_rm.cap = in_len;
+  }
+  for (uint32_t i = 0; i < in_len; i++) w[i] = input[i];
+  hipMemcpy(shim_rm.d_in, w, sizeof(int16_t) * in_len, H2D);
+  for (uint32_t i = 0; i < out_len; i++) w[i] = output[i];
+  hipMemcpy(shim_rm.d_out, w, sizeof(int16_t) * out_len, H2D);
+  if (srsgpu_rm_turbo_rx_8bit_dev(shim_rm.dl, shim_rm.d_in, shim_rm.d_out, in_len, K, rv_idx) == 0) {
+    hipMemcpy(w, shim_rm.d_out, sizeof(int16_t) * out_len, D2H);
+    for (uint32_t i = 0; i < out_len; i++) output[i] = (int8_t)w[i];
+    ret = SRSLTE_SUCCESS;
+  }
+out:
+  pthread_mutex_unlock(&shim_mutex);
+  free(w);
+  return ret;
+}
+
 int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
                         srslte_softbuffer_rx_t *softbuffers[SRSLTE_MAX_CODEWORDS],
                         cf_t *sf_symbols[SRSLTE_MAX_PORTS], cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS],
@@ -451,9 +493,9 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
                     nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
   const bool cdd = cfg->mimo_type == SRSLTE_MIMO_TYPE_CDD && q->cell.nof_ports == 2 && nof_tb == 2 &&
                    cfg->nof_layers == 2 && q->nof_rx_antennas == 2;
-  if ((!siso && !cdd) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit) {
+  if ((!siso && !cdd) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
     fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port) and TM3 CDD (2 ports, 2 layers, "
-                    "2 rx), normal CP, 16-bit LLRs\n");
+                    "2 rx), normal CP, 16-bit or 8-bit LLRs (the same in the PDSCH and its DL-SCH)\n");
     return SRSLTE_ERROR;
   }
   if (siso && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
@@ -509,6 +551,7 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
       hipMemcpy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D);
   }
   srsgpu_pdsch_set_csi(g, q->csi_enabled);
+  srsgpu_pdsch_set_llr_8bit(g, q->llr_is_8bit); /* pdsch.c:795-806 */
   int32_t *d_ret = (int32_t *)e->d_d;
   uint32_t *d_noi = (uint32_t *)e->d_d + 2;
   if (srsgpu_pdsch_decode_dev(g, &sf, 1, e->d_a, e->d_b, (size_t)n, (uint8_t *)e->d_c,

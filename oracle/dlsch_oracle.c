@@ -266,7 +266,7 @@ int orc_rm_turbo_rx_8bit(const int8_t *in, int8_t *out, uint32_t in_len, uint32_
  * after every half-iteration. The 8-bit AUTO choice at 400 < K <= 800 (8 sub-blocks) feeds the
  * SSE16 window 3K+12 converted values of a 3(K+32)+12 sub-block row, the remaining inputs being
  * whatever the decoder's conversion buffer last held (turbodecoder.c:439-459): no defined result,
- * so such a TB is refused (-3). */
+ * so such a TB is refused (-2, as the GPU path). */
 int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm,
                       uint32_t nof_e_bits, const int8_t *e_bits, uint8_t *data,
                       uint32_t max_halfits, uint32_t *nof_iterations) {
@@ -277,7 +277,7 @@ int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Q
   if (s.C > q->max_cb) return -2;
   for (uint32_t i = 0; i < s.C; i++) {
     const uint32_t K = i < s.C1 ? s.K1 : s.K2;
-    if (orc_autoimp_subblocks_8bit(K) == 8) return -3;
+    if (orc_autoimp_subblocks_8bit(K) == 8) return -2;
   }
   data[tbs / 8 + 0] = data[tbs / 8 + 1] = data[tbs / 8 + 2] = 0;
   uint32_t iters = 0;

@@ -50,6 +50,8 @@ int srsgpu_shim_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
 
 int srsgpu_shim_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
                               int16_t *e_bits, uint8_t *data, int tb_idx);
+int srsgpu_shim_rm_turbo_rx_lut_8bit(int8_t *input, int8_t *output, uint32_t in_len, uint32_t cb_idx,
+                                     uint32_t rv_idx);
 int srsgpu_shim_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uint32_t cb_idx,
                                 uint32_t rv_idx);
 int srsgpu_shim_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
@@ -64,10 +66,12 @@ static double urand(void) {
 static float gauss(void) { return (float)(sqrt(-2.0 * log(urand())) * cos(2.0 * M_PI * urand())); }
 
 int main(int argc, char **argv) {
-  if (argc != 11) {
-    fprintf(stderr, "usage: %s nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm\n", argv[0]);
+  if (argc != 11 && argc != 12) {
+    fprintf(stderr, "usage: %s nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm [llr8]\n", argv[0]);
     return 2;
   }
+  /* llr8: the 8-bit LLR chain (llr_is_8bit, pdsch.c:795-806, sch.c:344-364) on both sides */
+  const bool llr8 = argc == 12 && atoi(argv[11]) != 0;
   const int tm = atoi(argv[10]);
   const uint32_t nports = tm == 3 ? 2 : 1, ntb = tm == 3 ? 2 : 1;
   const uint32_t nof_prb = atoi(argv[1]), cell_id = atoi(argv[2]), mcs = atoi(argv[3]);
@@ -84,6 +88,7 @@ int main(int argc, char **argv) {
       srslte_pdsch_set_cell(&rx, cell) || srslte_pdsch_set_rnti(&rx, rnti) ||
       srslte_pdsch_enable_csi(&rx, csi != 0))
     return 2;
+  rx.llr_is_8bit = rx.dl_sch.llr_is_8bit = llr8;
 
   srslte_ra_dl_grant_t grant;
   memset(&grant, 0, sizeof(grant));
@@ -150,10 +155,29 @@ int main(int argc, char **argv) {
     free(in);
     free(oa);
     free(ob);
+    /* srslte_rm_turbo_rx_lut_8bit: int8, 3(K+32)+12 row (sub-block layout of the 8-bit decoder) */
+    int8_t *in8 = malloc(3 * 3 * 6200), *oa8 = malloc(3 * 6200), *ob8 = malloc(3 * 6200);
+    for (uint32_t c = 0; c < sizeof(cbs) / sizeof(cbs[0]); c++)
+      for (uint32_t rv = 0; rv < 4; rv++) {
+        const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cbs[c]), row = 3 * (K + 32) + 12;
+        const uint32_t in_len = (uint32_t)((3 * K + 12) * (0.3 + 2.0 * urand()));
+        for (uint32_t i = 0; i < in_len; i++) in8[i] = (int8_t)(urand() * 256 - 128);
+        for (uint32_t i = 0; i < row; i++) oa8[i] = ob8[i] = (int8_t)(urand() * 256 - 128);
+        const int r1 = srslte_rm_turbo_rx_lut_8bit(in8, oa8, in_len, cbs[c], rv);
+        const int r2 = srsgpu_shim_rm_turbo_rx_lut_8bit(in8, ob8, in_len, cbs[c], rv);
+        if (r1 != r2 || memcmp(oa8, ob8, row)) {
+          fprintf(stderr, "rm_turbo_rx_lut_8bit mismatch K %u rv %u in_len %u\n", K, rv, in_len);
+          nrm_bad++;
+        }
+      }
+    free(in8);
+    free(oa8);
+    free(ob8);
   }
   /* DL-SCH drop-in state: one srslte_sch_t and one softbuffer per TB on each side */
   srslte_sch_t scha, schb;
   if (srslte_sch_init(&scha) || srslte_sch_init(&schb)) return 2;
+  scha.llr_is_8bit = schb.llr_is_8bit = llr8;
   srslte_softbuffer_rx_t sra2[2], srb2[2];
   for (uint32_t t = 0; t < ntb; t++)
     if (srslte_softbuffer_rx_init(&sra2[t], nof_prb) || srsgpu_shim_softbuffer_rx_init(&srb2[t], nof_prb))

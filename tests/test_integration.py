@@ -62,6 +62,31 @@ def test_shim_pdsch_decode_matches_reference(case):
     assert int(stats["rm_mismatches"]) == 0, r.stdout + r.stderr
 
 
+# the 8-bit LLR chain (llr_is_8bit on the PDSCH and its DL-SCH, pdsch.c:795-806, sch.c:344-364):
+# same arguments plus llr8 = 1. The 8-bit HARQ combining wraps at 8 bits, as the reference's does.
+CASES8 = [
+    (25, 301, 16, 1, 1, 0, 6, 12.0, 11, 1),  # 16QAM, 25 PRB (AVX8 window at K = 6144 / 3136...)
+    (50, 503, 27, 2, 2, 1, 4, 18.0, 12, 1),  # 64QAM, 2 rx, CSI (8-bit weighting)
+    (100, 12, 28, 2, 1, 0, 3, 21.0, 13, 1),  # 20 MHz, 13 code blocks
+    (25, 7, 16, 2, 2, 0, 6, 16.0, 14, 3),    # TM3 CDD 2x2, two 16QAM TBs
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES8,
+                         ids=[f"llr8_tm{c[9]}_prb{c[0]}_mcs{c[2]}_rx{c[4]}_csi{c[5]}" for c in CASES8])
+def test_shim_pdsch_decode_8bit_matches_reference(case):
+    if not os.path.exists(CHECK):
+        pytest.skip("oracle/_ref/shim_check not built (needs /root/reference at build time)")
+    r = subprocess.run([CHECK] + [str(v) for v in case] + ["1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    stats = dict(kv.split("=") for kv in r.stdout.split())
+    assert int(stats["mismatches"]) == 0 and int(stats["tx"]) >= case[6], r.stdout + r.stderr
+    assert int(stats["soft"]) <= max(1, int(stats["tx"]) // 10), r.stdout + r.stderr
+    assert int(stats["dlsch_mismatches"]) == 0 and int(stats["rm_mismatches"]) == 0, r.stdout + r.stderr
+
+
 FRONT = os.path.join(REPO, "oracle", "_ref", "shim_front")
 # nof_prb_a, nof_prb_b, cell_id, mcs, nof_rx, nof_sf, snr_db, seed
 FRONT_CASES = [

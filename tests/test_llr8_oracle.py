@@ -76,7 +76,7 @@ def test_refuses_undefined_8bit_sizes(oracle, l8):
     sb = dl.softbuffer(4)
     r, _, _, _ = l8.decode(sb, 456, 0, 2, np.ones(1200, np.int8), 8)
     dl.free(sb)
-    assert r == -3
+    assert r == -2
 
 
 def test_csi_8bit_weights():
