@@ -200,6 +200,11 @@ struct PdschEngine {
         fprintf(stderr, "srsgpu: single-antenna PDSCH needs a 1-port cell\n");
         return -1;
       }
+    } else if (s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY) { // precoding.c:1811-1818, 2 ports
+      if (cell.nof_ports != 2) {
+        fprintf(stderr, "srsgpu: transmit diversity on the GPU needs a 2-port cell\n");
+        return -1;
+      }
     } else if (s.mimo_type == SRSGPU_MIMO_CDD) { // precoding.c:1085-1097
       if (cell.nof_ports != 2 || cell.nof_rx_ant != 2) {
         fprintf(stderr, "Error predecoding CCD: Invalid combination of ports %u and rx antennax %u\n",
@@ -257,6 +262,7 @@ struct PdschEngine {
         t.nrx = (int)cell.nof_rx_ant;
         t.nports = (int)cell.nof_ports;
         t.cdd = s.mimo_type == SRSGPU_MIMO_CDD;
+        t.txdiv = s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY;
         t.layer = (int)cw;
         t.csi_mode = csi ? 1 : 0;
         t.llr8 = llr8 ? 1 : 0;

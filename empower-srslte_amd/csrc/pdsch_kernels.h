@@ -27,6 +27,7 @@ struct LlrItem {
   uint32_t nof_re;
   int qm, mod, nrx, csi_mode;
   int cdd, layer;          // TM3 CDD 2x2 MMSE: this TB's codeword / layer (0 or 1)
+  int txdiv;               // TM2 transmit diversity, 2 ports (SFBC over RE pairs), 1-2 rx
   int aligned;             // e is 4-byte aligned: LLR pairs stored as 32-bit words
   float noise, inv_scaling, scaling;
   const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does

@@ -188,6 +188,72 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint3
   return e;
 }
 
+// TM2 transmit diversity, 2 ports (srslte_predecoding_diversity_multi, precoding.c:670-685, then
+// srslte_layerdemap_diversity, layermap.c:143-151): symbol j is x0 (j even) or x1 (j odd) of RE
+// pair i = j / 2. Without CSI and above 32 REs the first 4*(n/4) REs take the SSE arithmetic
+// (srslte_predecoding_diversity2_sse, :438-543: PROD products, |h|^2 by hadd, x / hh *
+// (sqrtf(2) / scaling)); the rest, and every pair with CSI (srslte_predecoding_diversity_csi,
+// :569-602), take gcc's evaluation of the C code (:356-428): float complex products, x1's
+// terms in double (the double conj()), hh = 1e-4 when 0, x / (hh * scaling) * sqrt(2) in double;
+// csi = hh before scaling.
+__device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
+  const uint32_t i = j >> 1, p0 = t.map[2 * i], p1 = t.map[2 * i + 1];
+  const bool odd = j & 1;
+  Eq e;
+  if (!t.csi_mode && t.nof_re > 32 && i < 2 * (t.nof_re / 4)) {
+    float hh = 0.f;
+    cf x0 = {0.f, 0.f}, x1 = {0.f, 0.f};
+    for (int a = 0; a < 2; a++) {
+      if (a == 1 && t.nrx < 2) break;
+      const cf h00 = c_ld(t.h[0][a], p0), h01 = c_ld(t.h[0][a], p1);
+      const cf h10 = c_ld(t.h[1][a], p0), h11 = c_ld(t.h[1][a], p1);
+      const cf r0 = c_ld(t.y[a], p0), r1 = c_ld(t.y[a], p1);
+      const float g = __fadd_rn(__fadd_rn(__fmul_rn(h00.r, h00.r), __fmul_rn(h00.i, h00.i)),
+                                __fadd_rn(__fmul_rn(h11.r, h11.r), __fmul_rn(h11.i, h11.i)));
+      hh = a ? __fadd_rn(hh, g) : g;
+      const cf u0 = c_add(c_mul(c_conj(h00), r0), c_mul(h11, c_conj(r1)));
+      const cf u1 = c_sub(c_mul(c_conj(h01), r1), c_mul(h10, c_conj(r0)));
+      x0 = a ? c_add(x0, u0) : u0;
+      x1 = a ? c_add(x1, u1) : u1;
+    }
+    const float s2 = __fdiv_rn(1.41421354f, t.scaling); // sqrtf(2) / scaling
+    const cf x = odd ? x1 : x0;
+    e.xr = __fmul_rn(__fdiv_rn(x.r, hh), s2);
+    e.xi = __fmul_rn(__fdiv_rn(x.i, hh), s2);
+    e.csi = hh;
+    return e;
+  }
+  float hh = 0.f;
+  cf x0 = {0.f, 0.f}, x1 = {0.f, 0.f};
+  for (int a = 0; a < 2; a++) {
+    if (a == 1 && t.nrx < 2) break;
+    const cf h00 = c_ld(t.h[0][a], p0), h01 = c_ld(t.h[0][a], p1);
+    const cf h10 = c_ld(t.h[1][a], p0), h11 = c_ld(t.h[1][a], p1);
+    hh = __fadd_rn(hh, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h00.r, h00.r), __fmul_rn(h00.i, h00.i)),
+                                           __fmul_rn(h11.r, h11.r)),
+                                 __fmul_rn(h11.i, h11.i)));
+    const cf r0 = c_ld(t.y[a], p0), r1 = c_ld(t.y[a], p1);
+    if (hh == 0.f) hh = 1e-4f;
+    const cf u0 = c_add(c_mul(c_conj(h00), r0), c_mul(h11, c_conj(r1)));
+    x0 = c_add(x0, u0);
+    // -h10 * conj(r0) + conj(h01) * r1 in double complex
+    const double nr = -(double)h10.r, ni = -(double)h10.i, cr = r0.r, ci = -(double)r0.i;
+    const double pr = __dsub_rn(__dmul_rn(nr, cr), __dmul_rn(ni, ci));
+    const double pi = __dadd_rn(__dmul_rn(nr, ci), __dmul_rn(ni, cr));
+    const double gr = h01.r, gi = -(double)h01.i, sr = r1.r, si = r1.i;
+    const double qr = __dsub_rn(__dmul_rn(gr, sr), __dmul_rn(gi, si));
+    const double qi = __dadd_rn(__dmul_rn(gr, si), __dmul_rn(gi, sr));
+    x1.r = (float)__dadd_rn((double)x1.r, __dadd_rn(pr, qr));
+    x1.i = (float)__dadd_rn((double)x1.i, __dadd_rn(pi, qi));
+  }
+  e.csi = hh;
+  const float hs = __fmul_rn(hh, t.scaling);
+  const cf x = odd ? x1 : x0;
+  e.xr = (float)__dmul_rn((double)__fdiv_rn(x.r, hs), 1.4142135623730951);
+  e.xi = (float)__dmul_rn((double)__fdiv_rn(x.i, hs), 1.4142135623730951);
+  return e;
+}
+
 // LLRs of symbol j (q per symbol) into out[0..q)
 __device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr, float xi,
                                       int16_t *o) {
@@ -316,7 +382,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
     const uint32_t pos = t.map[j];
-    const Eq e = t.cdd ? equalise_cdd(t, pos, j) : equalise(t, pos, j);
+    const Eq e = t.txdiv ? equalise_txdiv(t, j) : t.cdd ? equalise_cdd(t, pos, j) : equalise(t, pos, j);
     int16_t o[Q];
     if (t.llr8)
       demap8(MOD, j, t.nof_re, e.xr, e.xi, o);

@@ -75,7 +75,7 @@ class srsgpu_cell_t(ctypes.Structure):
                 ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32)]
 
 
-MIMO_SINGLE_ANTENNA, MIMO_CDD = 0, 3
+MIMO_SINGLE_ANTENNA, MIMO_TX_DIVERSITY, MIMO_CDD = 0, 1, 3
 
 
 class srsgpu_pdsch_sf_t(ctypes.Structure):

@@ -7,7 +7,9 @@
  *   - RE extraction of the grant (srslte_pdsch_get, pdsch.c:95-234);
  *   - SISO ZF/MMSE equalisation over 1-2 rx antennas (srslte_predecoding_single_multi,
  *     mimo/precoding.c:243-352), or TM3 large-delay CDD 2x2 MMSE over 2 ports and 2 rx antennas
- *     (srslte_predecoding_ccd_mmse, precoding.c:930-1097), optionally with CSI;
+ *     (srslte_predecoding_ccd_mmse, precoding.c:930-1097), or TM2 transmit diversity over 2 ports
+ *     and 1-2 rx antennas (srslte_predecoding_diversity_multi + srslte_layerdemap_diversity,
+ *     precoding.c:356-685, layermap.c:143-151), optionally with CSI;
  *   - soft demapping to int16 LLRs (srslte_demod_soft_demodulate_s, modem/demod_soft.c);
  *   - descrambling with the PDSCH Gold sequence (scrambling.c:48-51, sequences.c:64-66);
  *   - optional CSI weighting (csi_correction, pdsch.c:676-776);
@@ -49,6 +51,7 @@ typedef struct {
 
 /* srslte_mimo_type_t values accepted by the GPU receiver */
 #define SRSGPU_MIMO_SINGLE_ANTENNA 0 /* 1 CRS port, 1 layer, 1 TB (TM1), 1-2 rx antennas */
+#define SRSGPU_MIMO_TX_DIVERSITY 1   /* TM2 / DCI 1A on 2-port cells: SFBC over RE pairs, 1 TB, 1-2 rx */
 #define SRSGPU_MIMO_CDD 3            /* TM3 large-delay CDD: 2 ports, 2 layers, 2 TBs, 2 rx antennas */
 
 typedef struct {
@@ -59,7 +62,7 @@ typedef struct {
   uint16_t rnti;
   float noise_estimate;     /* MMSE term (0 = ZF) */
   float scaling;            /* pdsch_scaling (rho_a, 1.0 by default) */
-  uint32_t mimo_type;       /* SRSGPU_MIMO_SINGLE_ANTENNA or SRSGPU_MIMO_CDD */
+  uint32_t mimo_type;       /* SRSGPU_MIMO_SINGLE_ANTENNA, SRSGPU_MIMO_TX_DIVERSITY or SRSGPU_MIMO_CDD */
   uint32_t tb_cw_swap;      /* srslte_pdsch_cfg_t.tb_cw_swap (CDD): TB 0 on codeword 1 */
   /* per transport block (index 1 only with CDD) */
   uint32_t mod[2];          /* srslte_mod_t: 0 BPSK, 1 QPSK, 2 16QAM, 3 64QAM */

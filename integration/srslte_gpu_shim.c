@@ -430,7 +430,7 @@ int srslte_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uin
   int ret = SRSLTE_ERROR;
   pthread_mutex_lock(&shim_mutex);
   if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
-  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * 3 * (SRSLTE_TCOD_MAX_LEN_CB + 4));
+  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * (3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 12));
   if (in_len > shim_rm.cap) {
     if (shim_rm.d_in) hipFree(shim_rm.d_in);
     hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
@@ -461,7 +461,7 @@ int srslte_rm_turbo_rx_lut_8bit(int8_t *input, int8_t *output, uint32_t in_len, 
   int ret = SRSLTE_ERROR;
   pthread_mutex_lock(&shim_mutex);
   if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
-  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * 3 * (SRSLTE_TCOD_MAX_LEN_CB + 4));
+  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * (3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 12));
   if (in_len > shim_rm.cap) {
     if (shim_rm.d_in) hipFree(shim_rm.d_in);
     hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
@@ -493,12 +493,16 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
                     nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
   const bool cdd = cfg->mimo_type == SRSLTE_MIMO_TYPE_CDD && q->cell.nof_ports == 2 && nof_tb == 2 &&
                    cfg->nof_layers == 2 && q->nof_rx_antennas == 2;
-  if ((!siso && !cdd) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
-    fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port) and TM3 CDD (2 ports, 2 layers, "
-                    "2 rx), normal CP, 16-bit or 8-bit LLRs (the same in the PDSCH and its DL-SCH)\n");
+  /* TM2 / DCI 1A on a 2-port cell: SFBC transmit diversity, one TB (precoding.c:1811-1818) */
+  const bool txdiv = cfg->mimo_type == SRSLTE_MIMO_TYPE_TX_DIVERSITY && q->cell.nof_ports == 2 &&
+                     nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
+  if ((!siso && !cdd && !txdiv) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
+    fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port), TM2 transmit diversity (2 ports, 1-2 "
+                    "rx) and TM3 CDD (2 ports, 2 layers, 2 rx), normal CP, 16-bit or 8-bit LLRs (the "
+                    "same in the PDSCH and its DL-SCH)\n");
     return SRSLTE_ERROR;
   }
-  if (siso && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
+  if ((siso || txdiv) && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
   if (cdd && acks[0] && acks[1]) return SRSLTE_SUCCESS;
   shim_entry_t *e = shim_get(q, SHIM_PDSCH);
   if (!e) return SRSLTE_ERROR;
@@ -531,7 +535,7 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   sf.rnti = rnti;
   sf.noise_estimate = noise_estimate;
   sf.scaling = q->rho_a != 0.0f ? q->rho_a : 1.0f; /* pdsch.c:924-927 */
-  sf.mimo_type = cdd ? SRSGPU_MIMO_CDD : SRSGPU_MIMO_SINGLE_ANTENNA;
+  sf.mimo_type = cdd ? SRSGPU_MIMO_CDD : txdiv ? SRSGPU_MIMO_TX_DIVERSITY : SRSGPU_MIMO_SINGLE_ANTENNA;
   sf.tb_cw_swap = cfg->tb_cw_swap ? 1 : 0;
   sf.grid_offset = 0;
   sf.ce_offset = 0;

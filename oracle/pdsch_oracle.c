@@ -457,3 +457,87 @@ int orc_csi_correction_b(int mod, const float *csi, int nsym, int8_t *e) {
   }
   return 0;
 }
+
+/* ---------------------------------------------------------------- TM2 transmit diversity ---------- */
+/* srslte_predecoding_diversity_multi for 2 ports (precoding.c:670-685) + srslte_layerdemap_diversity
+ * (layermap.c:143-151): d[2i] = x0[i], d[2i+1] = x1[i] for RE pairs (2i, 2i+1).
+ * - CSI on: srslte_predecoding_diversity_csi (:569-602), generic arithmetic for every pair,
+ *   csi[2i] = csi[2i+1] = hh before scaling;
+ * - CSI off, n > 32: srslte_predecoding_diversity2_sse (:438-543) for the first 4*(n/4) REs, then
+ *   the generic srslte_predecoding_diversity_gen_ (:356-428) from there;
+ * - CSI off, n <= 32: generic for every pair.
+ * Generic: float complex arithmetic as gcc evaluates it (no FMA), with the double conj() of
+ * x1's terms (products and sums in double, rounded into the float accumulator) and the double
+ * sqrt(2) factor; hh = 1e-4 when it is exactly 0. SSE: PROD = addsub(a*ldup(b), swap(a)*hdup(b)),
+ * |h|^2 by hadd (re^2 + im^2, then h00 + h11), rx antennas added in order, x = x / hh * (sqrtf(2) /
+ * scaling). y: [rx][2n floats], h: [port][rx][2n floats] (n REs of this grant, extraction order). */
+typedef struct {
+  float r, i;
+} txd_cf;
+static txd_cf txd_ld(const float *p, int k) { return (txd_cf){p[2 * k], p[2 * k + 1]}; }
+static txd_cf txd_mul(txd_cf a, txd_cf b) { return (txd_cf){a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+
+static void txd_gen_pair(const float *const *y, const float *const h[2][2], int nrx, int i, float scaling,
+                         float *d, float *csi) {
+  float hh = 0;
+  txd_cf x0 = {0, 0}, x1 = {0, 0};
+  for (int p = 0; p < nrx; p++) {
+    const txd_cf h00 = txd_ld(h[0][p], 2 * i), h01 = txd_ld(h[0][p], 2 * i + 1);
+    const txd_cf h10 = txd_ld(h[1][p], 2 * i), h11 = txd_ld(h[1][p], 2 * i + 1);
+    hh += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+    const txd_cf r0 = txd_ld(y[p], 2 * i), r1 = txd_ld(y[p], 2 * i + 1);
+    if (hh == 0) hh = 1e-4;
+    const txd_cf a = txd_mul((txd_cf){h00.r, -h00.i}, r0), b = txd_mul(h11, (txd_cf){r1.r, -r1.i});
+    x0.r = x0.r + (a.r + b.r);
+    x0.i = x0.i + (a.i + b.i);
+    /* -h10 * conj(r0) + conj(h01) * r1 in double complex */
+    const double nr = -(double)h10.r, ni = -(double)h10.i, cr = r0.r, ci = -(double)r0.i;
+    const double pr = nr * cr - ni * ci, pi = nr * ci + ni * cr;
+    const double gr = h01.r, gi = -(double)h01.i, s1r = r1.r, s1i = r1.i;
+    const double qr = gr * s1r - gi * s1i, qi = gr * s1i + gi * s1r;
+    x1.r = (float)((double)x1.r + (pr + qr));
+    x1.i = (float)((double)x1.i + (pi + qi));
+  }
+  if (csi) csi[2 * i] = csi[2 * i + 1] = hh;
+  hh *= scaling;
+  d[4 * i + 0] = (float)((double)(x0.r / hh) * sqrt(2));
+  d[4 * i + 1] = (float)((double)(x0.i / hh) * sqrt(2));
+  d[4 * i + 2] = (float)((double)(x1.r / hh) * sqrt(2));
+  d[4 * i + 3] = (float)((double)(x1.i / hh) * sqrt(2));
+}
+
+static void txd_sse_pair(const float *const *y, const float *const h[2][2], int nrx, int i, float scaling,
+                         float *d) {
+  const float s2 = sqrtf(2) / scaling;
+  float hh = 0;
+  txd_cf x0 = {0, 0}, x1 = {0, 0};
+  for (int p = 0; p < nrx; p++) {
+    const txd_cf h00 = txd_ld(h[0][p], 2 * i), h01 = txd_ld(h[0][p], 2 * i + 1);
+    const txd_cf h10 = txd_ld(h[1][p], 2 * i), h11 = txd_ld(h[1][p], 2 * i + 1);
+    const txd_cf r0 = txd_ld(y[p], 2 * i), r1 = txd_ld(y[p], 2 * i + 1);
+    const float g = (h00.r * h00.r + h00.i * h00.i) + (h11.r * h11.r + h11.i * h11.i);
+    hh = p ? hh + g : g;
+    const txd_cf a = txd_mul((txd_cf){h00.r, -h00.i}, r0), b = txd_mul(h11, (txd_cf){r1.r, -r1.i});
+    const txd_cf c = txd_mul((txd_cf){h01.r, -h01.i}, r1), e = txd_mul(h10, (txd_cf){r0.r, -r0.i});
+    const txd_cf u0 = {a.r + b.r, a.i + b.i}, u1 = {c.r - e.r, c.i - e.i};
+    x0 = p ? (txd_cf){x0.r + u0.r, x0.i + u0.i} : u0;
+    x1 = p ? (txd_cf){x1.r + u1.r, x1.i + u1.i} : u1;
+  }
+  d[4 * i + 0] = (x0.r / hh) * s2;
+  d[4 * i + 1] = (x0.i / hh) * s2;
+  d[4 * i + 2] = (x1.r / hh) * s2;
+  d[4 * i + 3] = (x1.i / hh) * s2;
+}
+
+int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, const float *h01,
+                        const float *h10, const float *h11, int nrx, int n, float scaling, float *d,
+                        float *csi) {
+  const float *y[2] = {y0, y1};
+  const float *const h[2][2] = {{h00, h01}, {h10, h11}}; /* [port][rx] */
+  int i0 = 0;
+  if (!csi && n > 32) {
+    for (; i0 < 2 * (n / 4); i0++) txd_sse_pair(y, h, nrx, i0, scaling, d);
+  }
+  for (int i = i0; i < n / 2; i++) txd_gen_pair(y, h, nrx, i, scaling, d, csi);
+  return 0;
+}

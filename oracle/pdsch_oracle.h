@@ -15,6 +15,10 @@ int orc_sequence(uint32_t seed, uint32_t len, uint8_t *c);
 uint32_t orc_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
 int orc_scramble_s(uint32_t seed, int16_t *llr, uint32_t len);
 int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e);
+/* TM2 transmit diversity, 2 ports: predecoding + layer demapping -> d (interleaved complex) */
+int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, const float *h01,
+                        const float *h10, const float *h11, int nrx, int n, float scaling, float *d,
+                        float *csi);
 /* 8-bit LLR chain (llr_is_8bit) */
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);

@@ -529,3 +529,42 @@ int ref_dlsch_decode8(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t
   for (uint32_t i = 0; i < cfg.cb_segm[0].C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
   return r;
 }
+
+/* ---------------------------------------------------------------- TM2 transmit diversity ---------- */
+/* srslte_predecoding_type(..., SRSLTE_MIMO_TYPE_TX_DIVERSITY) (precoding.c:1811-1818) with 2 ports
+ * and srslte_layerdemap_type (layermap.c:175-) -> d; csi may be NULL (CSI off) */
+int ref_predecode_txdiv(const float *y0, const float *y1, const float *h00, const float *h01,
+                        const float *h10, const float *h11, int nrx, int n, float scaling, float *d,
+                        float *csi) {
+  cf_t *y[SRSLTE_MAX_PORTS] = {NULL}, *h[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  cf_t *x[SRSLTE_MAX_LAYERS] = {NULL}, *dd = NULL;
+  float *c[SRSLTE_MAX_CODEWORDS] = {NULL};
+  const float *ys[2] = {y0, y1}, *hs[2][2] = {{h00, h01}, {h10, h11}};
+  for (int a = 0; a < nrx; a++) {
+    if (posix_memalign((void **)&y[a], 64, (n + 16) * sizeof(cf_t))) return -1;
+    memcpy(y[a], ys[a], n * sizeof(cf_t));
+    for (int p = 0; p < 2; p++) {
+      if (posix_memalign((void **)&h[p][a], 64, (n + 16) * sizeof(cf_t))) return -1;
+      memcpy(h[p][a], hs[p][a], n * sizeof(cf_t));
+    }
+  }
+  for (int l = 0; l < 2; l++)
+    if (posix_memalign((void **)&x[l], 64, (n + 16) * sizeof(cf_t))) return -1;
+  if (posix_memalign((void **)&dd, 64, (n + 16) * sizeof(cf_t))) return -1;
+  if (csi && posix_memalign((void **)&c[0], 64, (n + 16) * sizeof(float))) return -1;
+  int r = srslte_predecoding_type(y, h, x, c, nrx, 2, 2, 0, n, SRSLTE_MIMO_TYPE_TX_DIVERSITY, scaling, 0.0f);
+  int nsym[SRSLTE_MAX_CODEWORDS] = {0};
+  cf_t *dp[SRSLTE_MAX_CODEWORDS] = {dd, NULL};
+  if (r >= 0) r = srslte_layerdemap_type(x, dp, 2, 1, n / 2, nsym, SRSLTE_MIMO_TYPE_TX_DIVERSITY);
+  memcpy(d, dd, n * sizeof(cf_t));
+  if (csi) memcpy(csi, c[0], n * sizeof(float));
+  for (int a = 0; a < nrx; a++) {
+    free(y[a]);
+    for (int p = 0; p < 2; p++) free(h[p][a]);
+  }
+  free(x[0]);
+  free(x[1]);
+  free(dd);
+  free(c[0]);
+  return r < 0 ? -1 : 0;
+}

@@ -15,7 +15,7 @@
  * Usage: shim_check nof_prb cell_id mcs cfi nof_rx csi nof_tb snr_db seed tm
  *   tm 1: single antenna port (TM1); tm 3: 2 CRS ports, CDD with 2 layers and 2 TBs (nof_rx 2).
  * Prints "tx=<n> acks=<n> mismatches=<n> soft=<n> tbs=<n> dlsch=<n> dlsch_mismatches=<n>
- * rm_mismatches=<n>". In the exact configurations (TM1 without CSI) every compared field must agree
+ * rm_mismatches=<n>". In the exact configurations (TM1 without CSI, TM2) every compared field must agree
  * (mismatches). Where the reference equaliser uses rcpps (CSI, TM3 MMSE) LLRs agree only to its
  * tolerance: data bytes are compared on acks, and ack / iteration-count differences near the
  * decoding threshold are counted as "soft".
@@ -73,7 +73,8 @@ int main(int argc, char **argv) {
   /* llr8: the 8-bit LLR chain (llr_is_8bit, pdsch.c:795-806, sch.c:344-364) on both sides */
   const bool llr8 = argc == 12 && atoi(argv[11]) != 0;
   const int tm = atoi(argv[10]);
-  const uint32_t nports = tm == 3 ? 2 : 1, ntb = tm == 3 ? 2 : 1;
+  /* tm 1: one port; tm 2: transmit diversity on a 2-port cell (one TB); tm 3: CDD, two TBs */
+  const uint32_t nports = tm >= 2 ? 2 : 1, ntb = tm == 3 ? 2 : 1;
   const uint32_t nof_prb = atoi(argv[1]), cell_id = atoi(argv[2]), mcs = atoi(argv[3]);
   const uint32_t cfi = atoi(argv[4]), nof_rx = atoi(argv[5]), nof_tb = atoi(argv[7]);
   const int csi = atoi(argv[6]);
@@ -131,7 +132,8 @@ int main(int argc, char **argv) {
     da_p[t] = calloc(dl, 1);
     db_p[t] = calloc(dl, 1);
   }
-  const int exact = tm == 1 && !csi;
+  /* TM2's predecoding has no rcpps (exact divisions, CSI or not): exact like TM1 without CSI */
+  const int exact = (tm == 1 && !csi) || tm == 2;
 
   /* srslte_rm_turbo_rx_lut: reference vs shim over rv 0-3 and a K sweep */
   uint32_t nrm_bad = 0;
@@ -155,7 +157,10 @@ int main(int argc, char **argv) {
     free(in);
     free(oa);
     free(ob);
-    /* srslte_rm_turbo_rx_lut_8bit: int8, 3(K+32)+12 row (sub-block layout of the 8-bit decoder) */
+    /* srslte_rm_turbo_rx_lut_8bit: int8, 3(K+32)+12 row (sub-block layout of the 8-bit decoder);
+     * on a random stream of its own, so the PDSCH cases below see the same data as without it */
+    const uint64_t rng_saved = rng;
+    rng ^= 0x8b8b8b8bULL;
     int8_t *in8 = malloc(3 * 3 * 6200), *oa8 = malloc(3 * 6200), *ob8 = malloc(3 * 6200);
     for (uint32_t c = 0; c < sizeof(cbs) / sizeof(cbs[0]); c++)
       for (uint32_t rv = 0; rv < 4; rv++) {
@@ -173,6 +178,7 @@ int main(int argc, char **argv) {
     free(in8);
     free(oa8);
     free(ob8);
+    rng = rng_saved;
   }
   /* DL-SCH drop-in state: one srslte_sch_t and one softbuffer per TB on each side */
   srslte_sch_t scha, schb;
@@ -207,7 +213,9 @@ int main(int argc, char **argv) {
       memset(&cfg, 0, sizeof(cfg));
       int rv2[SRSLTE_MAX_CODEWORDS] = {(int)rvs[r], (int)rvs[r]};
       if (srslte_pdsch_cfg_mimo(&cfg, cell, &grant, cfi, sf_idx, rv2,
-                                tm == 3 ? SRSLTE_MIMO_TYPE_CDD : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA, 0))
+                                tm == 3 ? SRSLTE_MIMO_TYPE_CDD
+                                        : tm == 2 ? SRSLTE_MIMO_TYPE_TX_DIVERSITY : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA,
+                                0))
         return 2;
       for (uint32_t p = 0; p < nports; p++) memset(txg[p], 0, sizeof(cf_t) * n);
       if (srslte_pdsch_encode(&tx, &cfg, sbt_p, dtx_p, rnti, txg)) return 2;

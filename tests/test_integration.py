@@ -40,6 +40,9 @@ CASES = [
     (25, 7, 16, 2, 2, 0, 8, 16.0, 7, 3),   # TM3 CDD 2x2, two 16QAM TBs
     (50, 150, 26, 1, 2, 1, 6, 25.0, 8, 3),  # TM3, 64QAM, CSI
     (100, 1, 28, 1, 2, 0, 4, 27.0, 9, 3),  # TM3 20 MHz, two 64QAM TBs (BASELINE configs[3] shape)
+    (6, 3, 9, 3, 2, 0, 8, 4.0, 21, 2),     # TM2 transmit diversity, QPSK, 2 rx (SIB-like)
+    (25, 33, 16, 2, 1, 0, 6, 12.0, 22, 2),  # TM2, 16QAM, 1 rx
+    (50, 211, 27, 1, 2, 1, 4, 20.0, 23, 2),  # TM2, 64QAM, 2 rx, CSI
 ]
 
 
@@ -69,6 +72,7 @@ CASES8 = [
     (50, 503, 27, 2, 2, 1, 4, 18.0, 12, 1),  # 64QAM, 2 rx, CSI (8-bit weighting)
     (100, 12, 28, 2, 1, 0, 3, 21.0, 13, 1),  # 20 MHz, 13 code blocks
     (25, 7, 16, 2, 2, 0, 6, 16.0, 14, 3),    # TM3 CDD 2x2, two 16QAM TBs
+    (15, 41, 22, 2, 2, 1, 6, 16.0, 15, 2),   # TM2 transmit diversity, CSI
 ]
 
 
