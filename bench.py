@@ -443,6 +443,34 @@ def load_profile_json(workload, tag="pmc_traffic"):
     return best
 
 
+def dropin_latency(s, llr, ncb=16):
+    """The drop-in srslte_tdec_iteration path (include/srslte/phy/fec/turbodecoder.h) as an
+    unmodified decode_tb_cb loop drives it (sch.c:356-391): per code block srslte_tdec_new_cb, then
+    one call per half-iteration, each a GPU launch for ONE code block, a stream synchronisation and
+    the decision bytes copied back. Latency-bound by construction; reported so the cost of the
+    compatibility path is on record (host-pointer rate, never `value`)."""
+    d = s.Tdec(K)
+    d.force_not_sb()  # the bench's LLRs are in natural [s, p0, p1] order
+    out = np.zeros(K // 8, np.uint8)
+    rows = [np.ascontiguousarray(llr[i]) for i in range(ncb)]
+    for r in rows[:2]:  # warm-up: tables, first launches
+        d.new_cb(K)
+        for _ in range(NHALF):
+            d.iteration(r, out)
+    t0 = time.perf_counter()
+    for r in rows:
+        d.new_cb(K)
+        for _ in range(NHALF):
+            d.iteration(r, out)
+    el = time.perf_counter() - t0
+    d.free()
+    return {"K": K, "code_blocks": ncb, "half_iterations": NHALF,
+            "us_per_halfit_call": round(el / (ncb * NHALF) * 1e6, 2),
+            "mbps": round(ncb * K / el / 1e6, 2),
+            "note": "one code block per srslte_tdec_iteration call (host buffers, synchronous); the "
+                    "batch APIs carry the throughput"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -450,7 +478,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -696,7 +724,12 @@ def main():
         dec8 = {"decoder": "AUTO 8-bit (int8 AVX8 window, 32 sub-blocks)",
                 "mbps": round(decoded_mbps(max(1, world), NCB, K, args.steps, el8), 1),
                 "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
+    dropin = None
+    if "dropin" in legs and rank == 0:
+        dropin = dropin_latency(s, llr)
     batch.close()
+    if rank == 0 and dropin:
+        result["dropin_latency"] = dropin
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
@@ -715,6 +748,10 @@ def main():
                 result["pipeline_" + key] = extra[kind]
     if rank == 0 and not args.no_cpu_baseline and nranks == 1:
         result["cpu_baseline"] = cpu_baseline(llr)
+        if dropin:  # the reference's own per-call cost on one pinned thread, for comparison
+            cb = result["cpu_baseline"]
+            per_thread_mbps = cb["value"] / max(cb["cores"], 1)
+            dropin["cpu_reference_us_per_halfit_one_thread"] = round(K / per_thread_mbps / NHALF, 2)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
