@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "chest_kernels.h"
+#include "gmem.h"
 
 #pragma clang fp contract(off)
 
@@ -102,7 +103,11 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   __shared__ float s_noise;
   const int it = blockIdx.x;
   if (it >= nitems) return;
-  const ChestItem t = items[it];
+  ChestItem t = items[it];
+  t.grid = gmem(t.grid);
+  t.ce = gmem(t.ce);
+  t.noise = gmem(t.noise);
+  t.meas = gmem(t.meas);
   const int nprb = cfg.nprb, cell_id = cfg.cell_id, np = 2 * nprb, nsc = 12 * nprb;
   const c32 *grid = (const c32 *)t.grid;
   const c32 *pil = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);

@@ -25,6 +25,8 @@ template <typename T> __device__ __forceinline__ gp_t<T> glob(T *p) {
   return (gp_t<T>)(__attribute__((address_space(1))) void *)(uintptr_t)p;
 }
 typedef uint32_t u4v __attribute__((ext_vector_type(4))); // HIP's uint4 class has no AS-1 methods
+// generic pointer known to be global (the address-space inference turns its accesses into global_*)
+template <typename T> __device__ __forceinline__ T *glob_g(T *p) { return (T *)glob(p); }
 // one softbuffer entry: int16 wrap, or (w8) int8 wrap sign-extended into the int16 entry
 __device__ __forceinline__ uint32_t derm_fold(uint32_t v, bool w8) {
   return w8 ? (uint32_t)(uint16_t)(int16_t)(int8_t)(uint8_t)v : v & 0xFFFFu;
@@ -149,7 +151,12 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   __shared__ uint32_t noi_sum;
   const int b = blockIdx.x;
   if (b >= ntb) return;
-  const TbItem t = tbs_[b];
+  TbItem t = tbs_[b];
+  t.data = glob_g(t.data);
+  t.cb_crc = glob_g(t.cb_crc);
+  t.saved = glob_g(t.saved);
+  t.ret = glob_g(t.ret);
+  t.noi = glob_g(t.noi);
   if (t.C == 0) { // tbs == 0 (sch.c:451-453) or invalid inputs: result set on the host
     if (threadIdx.x == 0) {
       *t.ret = t.preset_ret;

@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "pdsch_kernels.h"
+#include "gmem.h"
 
 // The equaliser must round like the reference's separate SSE/AVX multiplies and adds: no FMA
 // contraction anywhere in this file (HIP's __fmul_rn is a plain '*').
@@ -415,6 +416,17 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
   const int it = blockIdx.y;
   if (it >= nitems) return;
   LlrItem t = items[it];
+  for (int a = 0; a < 2; a++) {
+    t.y[a] = gmem(t.y[a]);
+    t.h[0][a] = gmem(t.h[0][a]);
+    t.h[1][a] = gmem(t.h[1][a]);
+  }
+  t.map = gmem(t.map);
+  t.c = gmem(t.c);
+  t.e = gmem(t.e);
+  t.csi = gmem(t.csi);
+  t.csi_max = gmem(t.csi_max);
+  t.noise_dev = gmem(t.noise_dev);
   if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
                      // the mean over ports, then the mean over antennas
     float n = 0.f;
@@ -439,7 +451,10 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
 __global__ __launch_bounds__(256) void k_csi_correct(const LlrItem *__restrict__ items, int nitems) {
   const int it = blockIdx.y;
   if (it >= nitems) return;
-  const LlrItem t = items[it];
+  LlrItem t = items[it];
+  t.e = gmem(t.e);
+  t.csi = gmem(t.csi);
+  t.csi_max = gmem(t.csi_max);
   const uint32_t nbits = t.nof_re * t.qm;
   const float cmax = __uint_as_float(*t.csi_max);
   const float scale = __fdiv_rn(32767.f, cmax);
