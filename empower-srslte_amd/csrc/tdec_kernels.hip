@@ -1057,6 +1057,7 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
 }
 
 // ------------------------------------------------------------------ SSE non-window ----
+#define TD_SP 8 // steps per prefetch group of the sequential decoders (every LTE K is a multiple)
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
 // scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
@@ -1089,27 +1090,44 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ g
   for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
 #pragma unroll
   for (int i = 0; i < 8; i++) AL(0, i) = a[i];
-  for (int k = 0; k < K; k++) { // :211-297
-    StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k);
-    s2 g1 = wadd(s.x, s.y) >> 1, g0 = wsub(s.x, s.y) >> 1;
-    s2 n[8];
-    n[0] = smax(wadd(a[1], g1), wsub(a[0], g1));
-    n[1] = smax(wadd(a[2], g0), wsub(a[3], g0));
-    n[2] = smax(wadd(a[5], g0), wsub(a[4], g0));
-    n[3] = smax(wadd(a[6], g1), wsub(a[7], g1));
-    n[4] = smax(wadd(a[0], g1), wsub(a[1], g1));
-    n[5] = smax(wadd(a[3], g0), wsub(a[2], g0));
-    n[6] = smax(wadd(a[4], g0), wsub(a[5], g0));
-    n[7] = smax(wadd(a[7], g1), wsub(a[6], g1));
+  // every LTE K is a multiple of 8: the recursion runs in groups of TD_SP steps whose inputs were
+  // loaded one group ahead (the loads do not depend on the recursion; one serial chain per lane
+  // leaves nothing else to hide their latency)
+  constexpr int P = TD_SP;
+  StepIn nx[P];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      a[i] = n[i];
-      AL(k + 1, i) = a[i];
-    }
-    if ((k & 3) == 3) {
-      s2 z = a[0];
+  for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, u);
+  for (int k0 = 0; k0 < K; k0 += P) { // :211-297
+    StepIn cu[P];
 #pragma unroll
-      for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
+    for (int u = 0; u < P; u++) cu[u] = nx[u];
+    const int kn = min(k0 + P, K - P);
+#pragma unroll
+    for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, kn + u);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int k = k0 + u;
+      const StepIn &s = cu[u];
+      s2 g1 = wadd(s.x, s.y) >> 1, g0 = wsub(s.x, s.y) >> 1;
+      s2 n[8];
+      n[0] = smax(wadd(a[1], g1), wsub(a[0], g1));
+      n[1] = smax(wadd(a[2], g0), wsub(a[3], g0));
+      n[2] = smax(wadd(a[5], g0), wsub(a[4], g0));
+      n[3] = smax(wadd(a[6], g1), wsub(a[7], g1));
+      n[4] = smax(wadd(a[0], g1), wsub(a[1], g1));
+      n[5] = smax(wadd(a[3], g0), wsub(a[2], g0));
+      n[6] = smax(wadd(a[4], g0), wsub(a[5], g0));
+      n[7] = smax(wadd(a[7], g1), wsub(a[6], g1));
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        a[i] = n[i];
+        AL(k + 1, i) = a[i];
+      }
+      if ((k & 3) == 3) {
+        s2 z = a[0];
+#pragma unroll
+        for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
+      }
     }
   }
   s2 b[8];
@@ -1117,35 +1135,65 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ g
 #pragma unroll
   for (int i = 1; i < 8; i++) b[i] = splat(-TD_INF);
   uint32_t dacc = 0;
-  for (int k = K + 2; k >= 0; k--) { // :105-206
-    s2 g0, g1, e = splat(0);
-    if (k >= K) {
-      s2 x = tl[tail_xoff + 2 * (k - K)], y = tl[tail_xoff + 2 * (k - K) + 1];
-      g0 = s2{(short)(((int)x.x - y.x) / 2), (short)(((int)x.y - y.y) / 2)};
-      g1 = s2{(short)(((int)x.x + y.x) / 2), (short)(((int)x.y + y.y) / 2)};
-    } else {
-      StepIn s = load_step<MODE, true>(sp0, xp1, p1, A, k);
-      g1 = wadd(s.x, s.y) >> 1;
-      g0 = wsub(s.x, s.y) >> 1;
-      e = s.e;
-    }
-    s2 bp[8] = {wadd(b[4], g1), wadd(b[0], g1), wadd(b[1], g0), wadd(b[5], g0),
-                wadd(b[6], g0), wadd(b[2], g0), wadd(b[3], g1), wadd(b[7], g1)};
-    s2 bn[8] = {wsub(b[0], g1), wsub(b[4], g1), wsub(b[5], g0), wsub(b[1], g0),
-                wsub(b[2], g0), wsub(b[6], g0), wsub(b[7], g1), wsub(b[3], g1)};
+  // :105-206. Tail steps K+2 .. K (no LLR), then steps K-1 .. 0 in groups of TD_SP whose inputs,
+  // stored alphas and scatter targets were loaded one group ahead.
+  auto bsteps = [&](s2 g0, s2 g1, s2 bp[8], s2 bn[8]) {
+    bp[0] = wadd(b[4], g1); bp[1] = wadd(b[0], g1); bp[2] = wadd(b[1], g0); bp[3] = wadd(b[5], g0);
+    bp[4] = wadd(b[6], g0); bp[5] = wadd(b[2], g0); bp[6] = wadd(b[3], g1); bp[7] = wadd(b[7], g1);
+    bn[0] = wsub(b[0], g1); bn[1] = wsub(b[4], g1); bn[2] = wsub(b[5], g0); bn[3] = wsub(b[1], g0);
+    bn[4] = wsub(b[2], g0); bn[5] = wsub(b[6], g0); bn[6] = wsub(b[7], g1); bn[7] = wsub(b[3], g1);
 #pragma unroll
     for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
-    if (k < K) {
+  };
+  for (int k = K + 2; k >= K; k--) {
+    const s2 x = tl[tail_xoff + 2 * (k - K)], y = tl[tail_xoff + 2 * (k - K) + 1];
+    const s2 g0 = s2{(short)(((int)x.x - y.x) / 2), (short)(((int)x.y - y.y) / 2)};
+    const s2 g1 = s2{(short)(((int)x.x + y.x) / 2), (short)(((int)x.y + y.y) / 2)};
+    s2 bp[8], bn[8];
+    bsteps(g0, g1, bp, bn);
+  }
+  StepIn ns[P];
+  s2 na[P][8];
+  int nt[P];
+  auto fetch = [&](int k1, StepIn *fs, s2 (*fa)[8], int *ft) {
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int k = k1 - u;
+      fs[u] = load_step<MODE, true>(sp0, xp1, p1, A, k);
+#pragma unroll
+      for (int i = 0; i < 8; i++) fa[u][i] = AL(k, i);
+      ft[u] = tbl[k];
+    }
+  };
+  fetch(K - 1, ns, na, nt);
+  for (int k1 = K - 1; k1 >= 0; k1 -= P) {
+    StepIn cs[P];
+    s2 ca[P][8];
+    int ct[P];
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      cs[u] = ns[u];
+      ct[u] = nt[u];
+#pragma unroll
+      for (int i = 0; i < 8; i++) ca[u][i] = na[u][i];
+    }
+    fetch(max(k1 - P, P - 1), ns, na, nt);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int k = k1 - u;
+      const StepIn &st = cs[u];
+      const s2 g1 = wadd(st.x, st.y) >> 1, g0 = wsub(st.x, st.y) >> 1;
+      s2 bp[8], bn[8];
+      bsteps(g0, g1, bp, bn);
       s2 mp = splat(-32768), mn = splat(-32768);
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        s2 al = AL(k, i);
-        mp = smax(mp, wadd(bp[i], al));
-        mn = smax(mn, wadd(bn[i], al));
+        mp = smax(mp, wadd(bp[i], ca[u][i]));
+        mn = smax(mn, wadd(bn[i], ca[u][i]));
       }
       // hMax(bn) - hMax(bp) with hMax(v) = 0x7FFF - max(v) (minpos_epu16 trick, :97-102)
-      s2 llr = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
-      store_out<MODE == 1>(xp1, A, tbl[k], llr, e);
+      const s2 llr = wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp));
+      store_out<MODE == 1>(xp1, A, ct[u], llr, st.e);
       if (D) { // k descends: flush each 16-step group at its first step
         dacc |= dec_bits(llr) << (k & 15);
         if ((k & 15) == 0) {
