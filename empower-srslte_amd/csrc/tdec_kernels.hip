@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
 }
 
 // ------------------------------------------------------------------ SSE non-window ----
-#define TD_SP 8 // steps per prefetch group of the sequential decoders (every LTE K is a multiple)
+#define TD_SP 8 // steps per prefetch group of the sequential decoders: must divide 8 (every LTE K is a multiple of 8, not of 16)
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
 // x (wrapping app add, tdec_sse_gamma :321-325) and y; tail gammas use C division (:349-352).
 // scratch: alpha (K+1)*8 short2 per pair, lane-interleaved.
