@@ -90,6 +90,13 @@ class srsgpu_pdsch_sf_t(ctypes.Structure):
                 ("ce_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64 * 2)]
 
 
+class srsgpu_rxq_item_t(ctypes.Structure):
+    """include/srsgpu/rx_queue.h"""
+    _fields_ = [("td", ctypes.c_void_p * 2), ("sf", srsgpu_pdsch_sf_t),
+                ("reset_softbuffer", ctypes.c_uint32 * 2), ("data", ctypes.c_void_p * 2),
+                ("ret", ctypes.c_int32 * 2), ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float)]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -147,6 +154,15 @@ _sig = {
     "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
     "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_rxq_create": (_i32, [ctypes.POINTER(_vp), _vp, _u32, _u32, _u32, _u32, _u32]),
+    "srsgpu_rxq_destroy": (None, [_vp]),
+    "srsgpu_rxq_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_rxq_wait": (_i32, [_vp, ctypes.c_uint64]),
+    "srsgpu_rxq_decode": (_i32, [_vp, _vp]),
+    "srsgpu_rxq_flush": (None, [_vp]),
+    "srsgpu_rxq_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_rxq_get_chest": (_vp, [_vp]),
+    "srsgpu_rxq_get_pdsch": (_vp, [_vp]),
     "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
     "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
@@ -664,3 +680,60 @@ def shard_weighted(weights, world):
                                   load.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))) != 0:
         raise ValueError("invalid partition request (n=%d, world=%d)" % (w.size, world))
     return owner, load
+
+
+class RxQueue:
+    """srsgpu_rxq_t (include/srsgpu/rx_queue.h): PHY-worker threads hand over single time-domain
+    subframes; one dispatcher thread decodes them in batches (OFDM -> chest -> PDSCH / DL-SCH)."""
+
+    def __init__(self, nof_prb, cell_id, symbol_sz, nof_ports=1, nof_rx_ant=1, nof_softbuffers=16,
+                 max_batch=32, max_wait_us=500, max_halfits=8):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+        self.q = _vp()
+        if _lib.srsgpu_rxq_create(ctypes.byref(self.q), ctypes.byref(self.cell), symbol_sz,
+                                  nof_softbuffers, max_batch, max_wait_us, max_halfits) != 0:
+            raise RuntimeError("srsgpu_rxq_create failed")
+
+    @staticmethod
+    def item(td, sf, data, reset=(1, 0)):
+        """td: complex64 arrays per rx antenna (kept alive by the caller); data: uint8 output arrays
+        per TB; sf: make_sf(...)"""
+        it = srsgpu_rxq_item_t()
+        for a, x in enumerate(td):
+            it.td[a] = x.ctypes.data
+        it.sf = sf
+        for t, d in enumerate(data):
+            it.data[t] = d.ctypes.data
+        it.reset_softbuffer[0], it.reset_softbuffer[1] = reset
+        return it
+
+    def decode(self, it):
+        return _lib.srsgpu_rxq_decode(self.q, ctypes.byref(it))
+
+    def submit(self, it):
+        t = ctypes.c_uint64(0)
+        if _lib.srsgpu_rxq_submit(self.q, ctypes.byref(it), ctypes.byref(t)) != 0:
+            raise RuntimeError("srsgpu_rxq_submit failed")
+        return t.value
+
+    def wait(self, ticket):
+        return _lib.srsgpu_rxq_wait(self.q, ticket)
+
+    def flush(self):
+        _lib.srsgpu_rxq_flush(self.q)
+
+    def stats(self):
+        b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _lib.srsgpu_rxq_stats(self.q, ctypes.byref(b), ctypes.byref(n))
+        return b.value, n.value
+
+    def close(self):
+        if self.q:
+            _lib.srsgpu_rxq_destroy(self.q)
+            self.q = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,104 @@
+"""The subframe batch queue (include/srsgpu/rx_queue.h), driven the way srsUE's PHY workers would
+drive it (srsue/src/phy/phch_worker.cc:548-806, one subframe per worker call, several workers):
+four threads each decode their own time-domain subframes through srsgpu_rxq_decode, the queue's
+dispatcher batches them, and every TB must equal what the direct batch API (ofdm -> chest ->
+pdsch_decode_dev in one call, tests/test_pipeline_gpu.py's chain) returns for the same subframes:
+return codes, nof_iterations, data bytes — and the transmitted bytes at high SNR."""
+import threading
+
+import numpy as np
+import pytest
+
+from srsgpu_testlib import DlschOracle, PdschOracle
+from test_pipeline_gpu import build_subframe
+
+pytestmark = pytest.mark.gpu
+
+
+def _direct(s, torch, xs, sfs, nof_prb, cell_id, N, tbs):
+    n, gsz = len(xs), 14 * 12 * nof_prb
+    ofdm = s.OfdmRx(nof_prb, N)
+    chest = s.Chest(nof_prb, cell_id, max_grids=n)
+    pd = s.Pdsch(nof_prb, cell_id, nof_softbuffers=n, max_sf=n)
+    d_x = torch.from_numpy(np.stack(xs).reshape(-1)).cuda()
+    d_grid = torch.zeros(n * gsz, dtype=torch.complex64, device="cuda")
+    d_ce = torch.zeros_like(d_grid)
+    d_noise = torch.zeros(n, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    assert ofdm.rx_dev(n, d_x.data_ptr(), 15 * N, d_grid.data_ptr(), gsz) == 0
+    assert chest.estimate_dev([sf for sf, _ in sfs], d_grid.data_ptr(), gsz, d_ce.data_ptr(),
+                              d_noise.data_ptr()) == 0
+    pd.set_noise_dev(d_noise.data_ptr())
+    dlen = tbs // 8 + 6
+    sfl = []
+    for i, (sf_idx, nre) in enumerate(sfs):
+        pd.reset_softbuffer(i)
+        sfl.append(s.make_sf(sf_idx=sf_idx, lstart=1, nof_prb=nof_prb, mod=3, nof_re=nre, rnti=1234,
+                             tbs=tbs, softbuffer=i, grid_offset=i * gsz, data_offset=i * dlen))
+    d_data = torch.zeros(n * dlen, dtype=torch.uint8, device="cuda")
+    d_ret = torch.full((n,), 9, dtype=torch.int32, device="cuda")
+    d_noi = torch.zeros(n, dtype=torch.int32, device="cuda")
+    assert pd.decode_dev(sfl, d_grid.data_ptr(), d_ce.data_ptr(), gsz, d_data.data_ptr(), 8,
+                         d_ret.data_ptr(), d_noi.data_ptr()) == 0
+    torch.cuda.synchronize()
+    out = (d_ret.cpu().numpy(), d_noi.cpu().numpy(), d_data.cpu().numpy().reshape(n, dlen),
+           d_noise.cpu().numpy())
+    for h in (pd, chest, ofdm):
+        h.close()
+    return out
+
+
+def test_worker_threads_through_the_queue(oracle):
+    import torch
+    import srsgpu_phy as s
+    po, dl = PdschOracle(oracle), DlschOracle(oracle)
+    rng = np.random.default_rng(77)
+    nof_prb, cell_id, tbs = 50, 3, 36696  # 10 MHz, MCS 28
+    N = s.symbol_sz(nof_prb, True)
+    n, nthreads = 24, 4
+    xs, datas, sfs = [], [], []
+    for i in range(n):
+        sf_idx = [1, 2, 3, 4, 6, 7, 8, 9][i % 8]
+        snr = 30.0 if i % 3 else 14.0  # some TBs fail, some need more half-iterations
+        x, data, idx = build_subframe(po, dl, rng, nof_prb, cell_id, N, sf_idx, tbs, 1234, snr,
+                                      rng.uniform(0, 6.28))
+        xs.append(x)
+        datas.append(data)
+        sfs.append((sf_idx, idx.size))
+    ret_d, noi_d, data_d, noise_d = _direct(s, torch, xs, sfs, nof_prb, cell_id, N, tbs)
+
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=n, max_batch=8, max_wait_us=3000)
+    dlen = tbs // 8 + 6
+    outs = [np.zeros(dlen, np.uint8) for _ in range(n)]
+    items = [q.item([xs[i]], s.make_sf(sf_idx=sfs[i][0], lstart=1, nof_prb=nof_prb, mod=3,
+                                        nof_re=sfs[i][1], rnti=1234, tbs=tbs, softbuffer=i),
+                    [outs[i]]) for i in range(n)]
+    rcs = [None] * n
+
+    def worker(w):
+        for i in range(w, n, nthreads):
+            rcs[i] = q.decode(items[i])
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(nthreads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    batches, done = q.stats()
+    assert rcs == [0] * n and done == n
+    assert batches < n  # the dispatcher batched the workers' subframes
+    nb = (tbs + 24) // 8
+    for i in range(n):
+        assert items[i].ret[0] == ret_d[i] and items[i].noi[0] == noi_d[i], i
+        assert (outs[i][:nb] == data_d[i][:nb]).all(), i
+        assert abs(items[i].noise - noise_d[i]) <= 1e-6 * max(1.0, abs(noise_d[i])), i
+        if i % 3:
+            assert items[i].ret[0] == 0 and (outs[i][:tbs // 8] == datas[i]).all(), i
+    # asynchronous form: submit everything, flush, then wait
+    for i in range(n):
+        items[i].reset_softbuffer[0] = 1
+    tickets = [q.submit(items[i]) for i in range(n)]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in tickets)
+    assert all(items[i].ret[0] == ret_d[i] for i in range(n))
+    q.close()
