@@ -1,0 +1,98 @@
+// Batched tail-biting Viterbi decoder (include/srsgpu/viterbi_batch.h): one wavefront per frame,
+// lane s = trellis state s. The reference's srslte_viterbi_decode_f on an AVX2 build
+// (lib/src/phy/fec/viterbi.c:520-546 with VITERBI_16 -> decode37_avx2_16bit :133-160 ->
+// viterbi37_avx2_16bit.c), restated per state:
+//   quantisation  q = clamp((long)(32767.5f + (1000 / max|x|) * x), 0, 65535) (vector.c:408-420)
+//   per bit t     (the frame repeated 3 times) butterfly b = s >> 1 joins old states b and b + 32;
+//                 metric = avg(B2 ^ q2, avg(B0 ^ q0, B1 ^ q1)) >> 3 with B = 0 / 65535 from the
+//                 polynomial parities, complement 8191 - metric; uint16 wrapping sums; decision =
+//                 signed 16-bit difference > 0 ("modulo" compare); no normalisation (the
+//                 reference's is a no-op: its in-lane byte shift by 16 zeroes the minimum)
+//   end           best state = the last index of the minimum metric; chainback from it reading
+//                 the decisions 6 positions past the bit it decides (zero beyond the frame); the
+//                 middle copy of the frame is the output.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gmem.h"
+#include "srsgpu/viterbi_batch.h"
+
+namespace srsgpu {
+
+__device__ __forceinline__ int vparity(int x) { return __popc((unsigned)x) & 1; }
+
+__global__ __launch_bounds__(64) void k_viterbi37_tb(const srsgpu_viterbi_frame_t *__restrict__ frames,
+                                                     int nframes, const float *__restrict__ sym_base,
+                                                     uint8_t *__restrict__ out_base) {
+  __shared__ uint16_t q[3 * SRSGPU_VITERBI_MAX_FRAME];
+  __shared__ uint64_t dec[3 * SRSGPU_VITERBI_MAX_FRAME + 8];
+  const int f = blockIdx.x;
+  if (f >= nframes) return;
+  const srsgpu_viterbi_frame_t fr = frames[f];
+  const int F = (int)fr.frame_length;
+  if (F < 1 || F > SRSGPU_VITERBI_MAX_FRAME) return; // checked on the host too
+  const float *sym = gmem(sym_base + fr.sym_offset);
+  uint8_t *out = gmem(out_base + fr.out_offset);
+  const int lane = threadIdx.x, len = 3 * F, nb = 3 * F;
+  // max |x| (viterbi.c:531-536: float max starting at -9e9, fabs compared in double)
+  float mx = -9e9f;
+  for (int i = lane; i < len; i += 64) mx = fmaxf(mx, fabsf(sym[i]));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  const float gain = __fdiv_rn(1000.0f, mx);
+  for (int i = lane; i < len; i += 64) {
+    const float v = __fadd_rn(32767.5f, __fmul_rn(gain, sym[i]));
+    long t = (v == v && v >= -9.2e18f && v < 9.2e18f) ? (long)v : (long)INT64_MIN; // cvttss2si
+    t = t < 0 ? 0 : t > 65535 ? 65535 : t;
+    q[i] = (uint16_t)t;
+  }
+  for (int i = lane; i < 8; i += 64) dec[nb + i] = 0; // chainback reads up to 6 past the end
+  __syncthreads();
+  const int b = lane >> 1, h = lane & 1;
+  const uint32_t B0 = vparity((2 * b) & 0x6D) ? 65535u : 0u;
+  const uint32_t B1 = vparity((2 * b) & 0x4F) ? 65535u : 0u;
+  const uint32_t B2 = vparity((2 * b) & 0x57) ? 65535u : 0u;
+  uint32_t m = 63; // this lane's state metric (uint16 held in 32 bits)
+  int k = 0;       // t mod F
+  for (int t = 0; t < nb; t++) {
+    const uint32_t s0 = q[3 * k], s1 = q[3 * k + 1], s2 = q[3 * k + 2];
+    if (++k == F) k = 0;
+    const uint32_t m0a = ((B0 ^ s0) + (B1 ^ s1) + 1) >> 1;
+    const uint32_t metric = (((B2 ^ s2) + m0a + 1) >> 1) >> 3;
+    const uint32_t mm = (8191u - metric) & 0xFFFFu;
+    const uint32_t ob = (uint32_t)__shfl((int)m, b), ob32 = (uint32_t)__shfl((int)m, b + 32);
+    // h = 0: m0 = ob + metric vs m1 = ob32 + mm; h = 1: m2 = ob + mm vs m3 = ob32 + metric
+    const uint32_t a = (ob + (h ? mm : metric)) & 0xFFFFu;
+    const uint32_t c = (ob32 + (h ? metric : mm)) & 0xFFFFu;
+    const bool d = (int16_t)(uint16_t)(a - c) > 0;
+    m = d ? c : a;
+    const uint64_t w = __ballot(d);
+    if (lane == 0) dec[t] = w;
+  }
+  // best end state: the last index holding the minimum metric
+  uint32_t mn = m;
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+  int best = m == mn ? lane : -1;
+  for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o));
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t es = (uint32_t)best << 2;
+    for (int t = nb - 1; t >= 0; t--) {
+      const uint32_t bit = (uint32_t)((dec[t + 6] >> (es >> 2)) & 1u);
+      es = (es >> 1) | (bit << 7);
+      if (t >= F && t < 2 * F) out[t - F] = (uint8_t)bit;
+    }
+  }
+}
+
+} // namespace srsgpu
+
+extern "C" int srsgpu_viterbi37_tb_decode_f_dev(const srsgpu_viterbi_frame_t *d_frames,
+                                                uint32_t nof_frames, const float *d_sym,
+                                                uint8_t *d_out, void *hip_stream) {
+  if (!d_frames || !d_sym || !d_out) return -1;
+  if (!nof_frames) return 0;
+  hipLaunchKernelGGL(srsgpu::k_viterbi37_tb, dim3(nof_frames), dim3(64), 0, (hipStream_t)hip_stream,
+                     d_frames, (int)nof_frames, d_sym, d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -97,6 +97,12 @@ class srsgpu_rxq_item_t(ctypes.Structure):
                 ("ret", ctypes.c_int32 * 2), ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float)]
 
 
+class srsgpu_viterbi_frame_t(ctypes.Structure):
+    """include/srsgpu/viterbi_batch.h"""
+    _fields_ = [("sym_offset", ctypes.c_uint64), ("out_offset", ctypes.c_uint64),
+                ("frame_length", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -154,6 +160,7 @@ _sig = {
     "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
     "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_viterbi37_tb_decode_f_dev": (_i32, [_vp, _u32, _vp, _vp, _vp]),
     "srsgpu_rxq_create": (_i32, [ctypes.POINTER(_vp), _vp, _u32, _u32, _u32, _u32, _u32]),
     "srsgpu_rxq_destroy": (None, [_vp]),
     "srsgpu_rxq_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -737,3 +744,27 @@ class RxQueue:
             self.close()
         except Exception:
             pass
+
+
+def viterbi37_tb_decode_f_batch(torch, frames_sym, stream=None):
+    """srsgpu_viterbi37_tb_decode_f_dev on a list of float32 symbol arrays (3F each): one launch,
+    returns the decoded bits (one per byte) per frame"""
+    offs, outs, so, oo = [], [], 0, 0
+    for x in frames_sym:
+        F = x.size // 3
+        offs.append((so, oo, F))
+        so += x.size
+        oo += F
+    arr = (srsgpu_viterbi_frame_t * len(offs))()
+    for i, (a, b, F) in enumerate(offs):
+        arr[i].sym_offset, arr[i].out_offset, arr[i].frame_length = a, b, F
+    d_frames = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
+    d_sym = torch.from_numpy(np.concatenate(frames_sym).astype(np.float32)).cuda()
+    d_out = torch.zeros(max(oo, 1), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    if _lib.srsgpu_viterbi37_tb_decode_f_dev(_vp(d_frames.data_ptr()), len(offs), _vp(d_sym.data_ptr()),
+                                             _vp(d_out.data_ptr()), _vp(stream)) != 0:
+        raise RuntimeError("srsgpu_viterbi37_tb_decode_f_dev failed")
+    torch.cuda.synchronize()
+    o = d_out.cpu().numpy()
+    return [o[b:b + F].copy() for (_, b, F) in offs]

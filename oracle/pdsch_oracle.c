@@ -12,6 +12,7 @@
  *     and srslte_scrambling_s_offset (src/phy/scrambling/scrambling.c:48-51).
  * Only tests/, __graft_entry__.smoke() and bench.py's CPU baseline may use this code.
  */
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -539,5 +540,86 @@ int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
     for (; i0 < 2 * (n / 4); i0++) txd_sse_pair(y, h, nrx, i0, scaling, d);
   }
   for (int i = i0; i < n / 2; i++) txd_gen_pair(y, h, nrx, i, scaling, d, csi);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- Viterbi (PDCCH) ---------- */
+/* srslte_viterbi_decode_f with the tail-biting K=7 r=1/3 decoder srsLTE builds for the PDCCH
+ * (pdcch.c:79,341). With AVX2 viterbi.c defines VITERBI_16 (:46-50), so decode_f quantises to
+ * uint16 (gain 1000 / max|x|, srslte_vec_quant_fus offset 32767.5 clip 65535, vector.c:408-420)
+ * and runs decode37_avx2_16bit (:133-160: TB_ITER = 3 copies of the frame, the middle third out)
+ * over viterbi37_avx2_16bit.c: all 64 metrics start at 63, branch metric
+ * avg(B2^s2, avg(B0^s0, B1^s1)) >> 3 with B = 0 / 65535, complement 8191 - metric, uint16
+ * wrapping adds, "modulo" compare (signed 16-bit difference > 0), new state 2b / 2b+1 from old b
+ * and b+32. The normalisation (:304-328) subtracts 0: its _mm256_srli_si256(v, 16) shifts each
+ * 128-bit lane out entirely, so the minimum it takes is always 0 and the metrics just wrap. Best
+ * end state = the last index of the minimum; chainback reads the decisions 6 positions past the
+ * bit it decides (zero beyond the frame). */
+static int orc_parity(int x) {
+  x ^= x >> 16;
+  x ^= x >> 8;
+  x ^= x >> 4;
+  x ^= x >> 2;
+  x ^= x >> 1;
+  return x & 1;
+}
+
+int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
+  const int poly[3] = {0x6D, 0x4F, 0x57};
+  const uint32_t len = 3 * F, nb = 3 * F;
+  float mx = -9e9f;
+  for (uint32_t i = 0; i < len; i++)
+    if (fabs(sym[i]) > mx) mx = (float)fabs(sym[i]);
+  const float gain = 1000.0f / mx;
+  uint16_t *q = malloc(len * sizeof(uint16_t));
+  uint64_t *dec = calloc(nb + 6, sizeof(uint64_t));
+  uint8_t *tmp = malloc(nb);
+  if (!q || !dec || !tmp) return -1;
+  for (uint32_t i = 0; i < len; i++) {
+    const float v = 32767.5f + gain * sym[i];
+    long t = (v == v && v >= -9.2e18f && v < 9.2e18f) ? (long)v : LONG_MIN; /* cvttss2si 64 */
+    if (t < 0) t = 0;
+    if (t > 65535) t = 65535;
+    q[i] = (uint16_t)t;
+  }
+  uint16_t B[3][32];
+  for (int st = 0; st < 32; st++)
+    for (int j = 0; j < 3; j++) B[j][st] = orc_parity((2 * st) & poly[j]) ? 65535 : 0;
+  uint16_t old[64], nw[64];
+  for (int st = 0; st < 64; st++) old[st] = 63;
+  for (uint32_t t = 0; t < nb; t++) {
+    const uint16_t *s = q + 3 * (t % F); /* the frame repeated TB_ITER times */
+    uint64_t d = 0;
+    for (int b = 0; b < 32; b++) {
+      const uint32_t m0a = ((uint32_t)(B[0][b] ^ s[0]) + (uint32_t)(B[1][b] ^ s[1]) + 1) >> 1;
+      const uint32_t metric = (((uint32_t)(B[2][b] ^ s[2]) + m0a + 1) >> 1) >> 3;
+      const uint32_t mm = (uint16_t)(8191 - metric);
+      const uint16_t m0 = (uint16_t)(old[b] + metric), m2 = (uint16_t)(old[b] + mm);
+      const uint16_t m3 = (uint16_t)(old[b + 32] + metric), m1 = (uint16_t)(old[b + 32] + mm);
+      const int d0 = (int16_t)(uint16_t)(m0 - m1) > 0, d1 = (int16_t)(uint16_t)(m2 - m3) > 0;
+      nw[2 * b] = d0 ? m1 : m0;
+      nw[2 * b + 1] = d1 ? m3 : m2;
+      d |= (uint64_t)d0 << (2 * b) | (uint64_t)d1 << (2 * b + 1);
+    }
+    dec[t] = d;
+    memcpy(old, nw, sizeof(old));
+  }
+  uint32_t best = 0;
+  uint16_t mn = 65535;
+  for (uint32_t st = 0; st < 64; st++)
+    if (old[st] <= mn) {
+      best = st;
+      mn = old[st];
+    }
+  uint32_t es = (best % 64) << 2;
+  for (int32_t b = (int32_t)nb - 1; b >= 0; b--) {
+    const uint32_t k = (uint32_t)((dec[b + 6] >> (es >> 2)) & 1);
+    es = (es >> 1) | (k << 7);
+    tmp[b] = (uint8_t)k;
+  }
+  memcpy(out, tmp + F, F);
+  free(q);
+  free(dec);
+  free(tmp);
   return 0;
 }

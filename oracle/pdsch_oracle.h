@@ -19,6 +19,8 @@ int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e);
 int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, const float *h01,
                         const float *h10, const float *h11, int nrx, int n, float scaling, float *d,
                         float *csi);
+/* PDCCH Viterbi: srslte_viterbi_decode_f, tail-biting K=7 r=1/3, F bits out (one per byte) */
+int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out);
 /* 8-bit LLR chain (llr_is_8bit) */
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);

@@ -568,3 +568,20 @@ int ref_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
   free(c[0]);
   return r < 0 ? -1 : 0;
 }
+
+/* ---------------------------------------------------------------- Viterbi (PDCCH) ---------- */
+#include "srslte/phy/fec/viterbi.h"
+/* srslte_viterbi_decode_f on a tail-biting K=7 r=1/3 decoder (pdcch.c:79,341: poly {0x6D, 0x4F,
+ * 0x57}, frame = DCI bits + 16): 3*F float symbols -> F bits (one per byte) */
+int ref_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
+  int poly[3] = {0x6D, 0x4F, 0x57};
+  srslte_viterbi_t v;
+  if (srslte_viterbi_init(&v, SRSLTE_VITERBI_37, poly, F, true)) return -1;
+  float *s = NULL;
+  if (posix_memalign((void **)&s, 64, (3 * F + 64) * sizeof(float))) return -1;
+  memcpy(s, sym, 3 * F * sizeof(float));
+  int r = srslte_viterbi_decode_f(&v, s, out, F);
+  free(s);
+  srslte_viterbi_free(&v);
+  return r < 0 ? -1 : 0;
+}

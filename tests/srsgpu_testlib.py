@@ -542,3 +542,15 @@ def predecode_txdiv(lib, y, h, scaling=1.0, csi=False, ref=False):
     P = lambda a: a.ctypes.data_as(_f32p) if a is not None else None
     assert f(P(ys[0]), P(ys[1]), *[P(v) for v in hs], nrx, n, scaling, P(d), P(c)) == 0
     return (d, c) if csi else d
+
+
+# ------------------------------------------------------------------ PDCCH Viterbi ----
+def viterbi_tb_decode_f(lib, sym, F, ref=False):
+    """srslte_viterbi_decode_f (tail-biting K=7 r=1/3, PDCCH polynomials): 3F floats -> F bits"""
+    L = lib.lib if hasattr(lib, "lib") else lib
+    f = getattr(L, "ref_viterbi37_tb_decode_f" if ref else "orc_viterbi37_tb_decode_f")
+    f.argtypes = [_f32p, ctypes.c_uint32, _u8p]
+    sym = np.ascontiguousarray(sym, np.float32)
+    out = np.zeros(F, np.uint8)
+    assert f(sym.ctypes.data_as(_f32p), F, _ptr(out, _u8p)) == 0
+    return out
