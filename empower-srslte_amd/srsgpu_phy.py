@@ -103,6 +103,12 @@ class srsgpu_viterbi_frame_t(ctypes.Structure):
                 ("frame_length", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
+class srsgpu_dci_cand_t(ctypes.Structure):
+    """include/srsgpu/viterbi_batch.h"""
+    _fields_ = [("llr_offset", ctypes.c_uint64), ("out_offset", ctypes.c_uint64),
+                ("E", ctypes.c_uint32), ("nof_bits", ctypes.c_uint32)]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -161,6 +167,7 @@ _sig = {
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
     "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_viterbi37_tb_decode_f_dev": (_i32, [_vp, _u32, _vp, _vp, _vp]),
+    "srsgpu_dci_decode_dev": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "srsgpu_rxq_create": (_i32, [ctypes.POINTER(_vp), _vp, _u32, _u32, _u32, _u32, _u32]),
     "srsgpu_rxq_destroy": (None, [_vp]),
     "srsgpu_rxq_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -768,3 +775,31 @@ def viterbi37_tb_decode_f_batch(torch, frames_sym, stream=None):
     torch.cuda.synchronize()
     o = d_out.cpu().numpy()
     return [o[b:b + F].copy() for (_, b, F) in offs]
+
+
+def dci_decode_batch(torch, cands, stream=None):
+    """srsgpu_dci_decode_dev on a list of (float32 LLRs, nof_bits): one launch; returns per
+    candidate (decoded, bits, crc_rem)"""
+    arr = (srsgpu_dci_cand_t * len(cands))()
+    lo, oo = 0, 0
+    for i, (e, nb) in enumerate(cands):
+        arr[i].llr_offset, arr[i].out_offset, arr[i].E, arr[i].nof_bits = lo, oo, e.size, nb
+        lo += e.size
+        oo += nb + 16
+    d_c = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
+    d_llr = torch.from_numpy(np.concatenate([e for e, _ in cands]).astype(np.float32)).cuda()
+    d_out = torch.zeros(oo, dtype=torch.uint8, device="cuda")
+    d_crc = torch.zeros(len(cands), dtype=torch.int16, device="cuda")
+    d_dec = torch.full((len(cands),), 7, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    if _lib.srsgpu_dci_decode_dev(_vp(d_c.data_ptr()), len(cands), _vp(d_llr.data_ptr()),
+                                  _vp(d_out.data_ptr()), _vp(d_crc.data_ptr()), _vp(d_dec.data_ptr()),
+                                  _vp(stream)) != 0:
+        raise RuntimeError("srsgpu_dci_decode_dev failed")
+    torch.cuda.synchronize()
+    out, crc, dec = d_out.cpu().numpy(), d_crc.cpu().numpy().view(np.uint16), d_dec.cpu().numpy()
+    res, oo = [], 0
+    for i, (e, nb) in enumerate(cands):
+        res.append((int(dec[i]), out[oo:oo + nb + 16].copy(), int(crc[i])))
+        oo += nb + 16
+    return res

@@ -32,6 +32,24 @@ typedef struct {
 int srsgpu_viterbi37_tb_decode_f_dev(const srsgpu_viterbi_frame_t *d_frames, uint32_t nof_frames,
                                      const float *d_sym, uint8_t *d_out, void *hip_stream);
 
+/* DCI candidates of the PDCCH blind search, decoded as srslte_pdcch_decode_msg does
+ * (lib/src/phy/phch/pdcch.c:380-396, srslte_pdcch_dci_decode :322-360): skipped unless the mean
+ * |llr| over the candidate's E bits exceeds 0.5; srslte_rm_conv_rx to 3 (nof_bits + 16) soft
+ * bits; the Viterbi decoder above; the 16-bit CRC remainder (CRC16 0x11021 of the nof_bits
+ * payload bits XOR the 16 received parity bits), which the caller compares with its RNTI. */
+#define SRSGPU_DCI_MAX_BITS 128 /* SRSLTE_DCI_MAX_BITS */
+#define SRSGPU_DCI_MAX_E 576    /* PDCCH_FORMAT_NOF_BITS(3): 8 CCEs x 72 bits */
+typedef struct {
+  uint64_t llr_offset; /* first of the candidate's E float LLRs (q->llr[ncce * 72 ..]) in d_llr */
+  uint64_t out_offset; /* first of its nof_bits + 16 decoded bits (one per byte) in d_data */
+  uint32_t E;          /* PDCCH_FORMAT_NOF_BITS(L) */
+  uint32_t nof_bits;   /* srslte_dci_format_sizeof */
+} srsgpu_dci_cand_t;
+/* d_decoded[i] = 1 decoded (d_crc_rem[i] valid), 0 skipped by the mean check. Device arrays;
+ * asynchronous on hip_stream. */
+int srsgpu_dci_decode_dev(const srsgpu_dci_cand_t *d_cands, uint32_t nof_cands, const float *d_llr,
+                          uint8_t *d_data, uint16_t *d_crc_rem, uint8_t *d_decoded, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -623,3 +623,58 @@ int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
   free(tmp);
   return 0;
 }
+
+/* DCI candidate decode as srslte_pdcch_decode_msg does it (pdcch.c:380-396: skipped unless the
+ * mean |llr| over the E bits, summed in double, exceeds 0.5; then srslte_pdcch_dci_decode
+ * :322-360): srslte_rm_conv_rx (rm_conv.c:99-157: 32-column sub-block interleaver over the three
+ * streams, dummy positions skipped, repetitions soft-combined in input order with 10000 as the
+ * empty marker, empty outputs 0), the Viterbi decoder above over nof_bits + 16 bits, and the CRC16
+ * (0x11021, init 0) of the first nof_bits XOR the 16 received parity bits. Returns 1 decoded,
+ * 0 skipped. */
+static const uint8_t RM_PERM_CC[32] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
+                                       0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
+static const uint8_t RM_PERM_CC_INV[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 10, 22, 6, 30, 14,
+                                           17, 1, 25, 9, 21, 5, 29, 13, 19, 3, 27, 11, 23, 7, 31, 15};
+int orc_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data, uint16_t *crc_rem) {
+  double mean = 0;
+  for (uint32_t i = 0; i < E; i++) mean += fabsf(e[i]);
+  mean /= E;
+  if (!(mean > 0.5)) return 0;
+  const uint32_t out_len = 3 * (nof_bits + 16);
+  const int nrows = (int)((out_len / 3 - 1) / 32 + 1), K_p = nrows * 32;
+  int ndummy = K_p - (int)(out_len / 3);
+  if (ndummy < 0) ndummy = 0;
+  float tmp[3 * 32 * 32], rm[3 * 144];
+  for (int i = 0; i < 3 * K_p; i++) tmp[i] = 10000.0f;
+  uint32_t k = 0;
+  int j = 0;
+  while (k < E) {
+    const int d_i = (j % K_p) / nrows, d_j = (j % K_p) % nrows;
+    if (d_j * 32 + RM_PERM_CC[d_i] >= ndummy) {
+      if (tmp[j] == 10000.0f)
+        tmp[j] = e[k];
+      else if (e[k] != 10000.0f)
+        tmp[j] += e[k];
+      k++;
+    }
+    if (++j == 3 * K_p) j = 0;
+  }
+  for (uint32_t i = 0; i < out_len / 3; i++) {
+    const int d_i = (int)(i + ndummy) / 32, d_j = (int)(i + ndummy) % 32;
+    for (int s = 0; s < 3; s++) {
+      const float o = tmp[K_p * s + RM_PERM_CC_INV[d_j] * nrows + d_i];
+      rm[i * 3 + s] = o != 10000.0f ? o : 0;
+    }
+  }
+  if (orc_viterbi37_tb_decode_f(rm, nof_bits + 16, data)) return -1;
+  uint32_t crc = 0;
+  for (uint32_t i = 0; i < nof_bits; i++) {
+    const uint32_t fb = ((crc >> 15) & 1) ^ (data[i] & 1);
+    crc = (crc << 1) & 0xFFFF;
+    if (fb) crc ^= 0x1021;
+  }
+  uint32_t p = 0;
+  for (int i = 0; i < 16; i++) p = (p << 1) | (data[nof_bits + i] & 1);
+  *crc_rem = (uint16_t)(p ^ crc);
+  return 1;
+}

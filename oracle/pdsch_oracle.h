@@ -21,6 +21,8 @@ int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
                         float *csi);
 /* PDCCH Viterbi: srslte_viterbi_decode_f, tail-biting K=7 r=1/3, F bits out (one per byte) */
 int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out);
+/* one DCI candidate as srslte_pdcch_decode_msg: 1 decoded (data: nof_bits + 16 bits), 0 skipped */
+int orc_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data, uint16_t *crc_rem);
 /* 8-bit LLR chain (llr_is_8bit) */
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);

@@ -585,3 +585,40 @@ int ref_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
   srslte_viterbi_free(&v);
   return r < 0 ? -1 : 0;
 }
+
+/* srslte_pdcch_decode_msg's decode of one DCI candidate (pdcch.c:380-396 mean check, then
+ * srslte_pdcch_dci_decode :322-360: srslte_rm_conv_rx, srslte_viterbi_decode_f, CRC16 remainder),
+ * composed from the reference's own functions as pdcch.c calls them. Returns 1 when decoded, 0
+ * when skipped (mean |llr| <= 0.5), -1 on error. */
+#include <math.h>
+#include <strings.h>
+#include "srslte/phy/fec/rm_conv.h"
+#include "srslte/phy/phch/dci.h"
+#include "srslte/phy/utils/bit.h"
+int ref_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data, uint16_t *crc_rem) {
+  double mean = 0;
+  for (uint32_t i = 0; i < E; i++) mean += fabsf(e[i]);
+  mean /= E;
+  if (!(mean > 0.5)) return 0;
+  int poly[3] = {0x6D, 0x4F, 0x57};
+  srslte_viterbi_t v;
+  srslte_crc_t crc;
+  if (srslte_viterbi_init(&v, SRSLTE_VITERBI_37, poly, SRSLTE_DCI_MAX_BITS + 16, true)) return -1;
+  if (srslte_crc_init(&crc, SRSLTE_LTE_CRC16, 16)) return -1;
+  float *rm = NULL, *in = NULL;
+  if (posix_memalign((void **)&rm, 64, sizeof(float) * 3 * (SRSLTE_DCI_MAX_BITS + 16) + 64)) return -1;
+  if (posix_memalign((void **)&in, 64, sizeof(float) * E + 64)) return -1;
+  memcpy(in, e, sizeof(float) * E);
+  bzero(rm, sizeof(float) * 3 * (SRSLTE_DCI_MAX_BITS + 16));
+  const uint32_t coded_len = 3 * (nof_bits + 16);
+  srslte_rm_conv_rx(in, E, rm, coded_len);
+  srslte_viterbi_decode_f(&v, rm, data, nof_bits + 16);
+  uint8_t *x = &data[nof_bits];
+  const uint16_t p_bits = (uint16_t)srslte_bit_pack(&x, 16);
+  const uint16_t crc_res = (uint16_t)(srslte_crc_checksum(&crc, data, nof_bits) & 0xffff);
+  *crc_rem = p_bits ^ crc_res;
+  srslte_viterbi_free(&v);
+  free(rm);
+  free(in);
+  return 1;
+}

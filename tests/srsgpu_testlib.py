@@ -554,3 +554,16 @@ def viterbi_tb_decode_f(lib, sym, F, ref=False):
     out = np.zeros(F, np.uint8)
     assert f(sym.ctypes.data_as(_f32p), F, _ptr(out, _u8p)) == 0
     return out
+
+
+def dci_decode(lib, e, nof_bits, ref=False):
+    """srslte_pdcch_decode_msg's decode of one candidate: (decoded 0/1, bits[nof_bits+16], crc_rem)"""
+    L = lib.lib if hasattr(lib, "lib") else lib
+    f = getattr(L, "ref_dci_decode" if ref else "orc_dci_decode")
+    f.argtypes = [_f32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint16)]
+    e = np.ascontiguousarray(e, np.float32)
+    d = np.zeros(nof_bits + 16, np.uint8)
+    c = ctypes.c_uint16(0)
+    r = f(e.ctypes.data_as(_f32p), e.size, nof_bits, _ptr(d, _u8p), ctypes.byref(c))
+    assert r in (0, 1)
+    return r, d, c.value

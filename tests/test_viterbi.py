@@ -56,3 +56,46 @@ def test_gpu_batch_vs_golden_and_oracle(oracle, gold):
     got = s.viterbi37_tb_decode_f_batch(torch, frames)
     for i, (g, w) in enumerate(zip(got, want)):
         assert (g == w).all(), i
+
+
+@pytest.fixture(scope="module")
+def dgold():
+    z = np.load(os.path.join(HERE, "golden", "dci_golden.npz"))
+    return z, json.loads(bytes(z["manifest"]))
+
+
+def test_golden_dci_oracle(oracle, dgold):
+    """srslte_pdcch_decode_msg's candidate decode (mean check, rm_conv_rx, Viterbi, CRC16)"""
+    from srsgpu_testlib import dci_decode
+    z, man = dgold
+    assert len(man) == 84 and 0 < sum(c["decoded"] for c in man) < 84
+    for c in man:
+        r, d, crc = dci_decode(oracle, z[c["key"] + "_e"], c["nof_bits"])
+        assert r == c["decoded"], c["key"]
+        if r:
+            assert (d == z[c["key"] + "_bits"]).all() and crc == c["crc_rem"], c["key"]
+
+
+@pytest.mark.gpu
+def test_gpu_dci_batch_vs_golden_and_oracle(oracle, dgold):
+    """every golden candidate plus 500 random ones (all PDCCH formats, DCI sizes 19..57) in one
+    launch: skip decision, bits and CRC remainder equal"""
+    import torch
+    import srsgpu_phy as s
+    from srsgpu_testlib import dci_decode
+    z, man = dgold
+    cands = [(z[c["key"] + "_e"], c["nof_bits"]) for c in man]
+    want = [(c["decoded"], z[c["key"] + "_bits"], c["crc_rem"]) for c in man]
+    rng = np.random.default_rng(5)
+    for i in range(500):
+        E = int(rng.choice([72, 144, 288, 576]))
+        nb = int(rng.choice([19, 21, 25, 27, 31, 43, 57]))
+        amp = float(rng.uniform(0.2, 3))
+        e = (amp * (rng.standard_normal(E) + np.where(rng.random(E) < 0.5, 1, -1))).astype(np.float32)
+        cands.append((e, nb))
+        want.append(dci_decode(oracle, e, nb))
+    got = s.dci_decode_batch(torch, cands)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g[0] == w[0], i
+        if w[0]:
+            assert (g[1] == w[1]).all() and g[2] == w[2], i
