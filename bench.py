@@ -443,6 +443,52 @@ def load_profile_json(workload, tag="pmc_traffic"):
     return best
 
 
+def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
+    """PDCCH blind decoding: per subframe srsUE tries up to 44 candidates
+    (common + UE-specific search spaces over the aggregation levels, two DCI sizes); each is
+    srslte_pdcch_decode_msg's candidate decode (mean check, srslte_rm_conv_rx, tail-biting Viterbi
+    of nof_bits + 16, CRC16 remainder). nsf subframes' candidates per launch (srsgpu_dci_decode_dev),
+    random LLRs of the PDCCH formats, 20 MHz DCI sizes (1A / 1: 27 / 31 bits)."""
+    rng = np.random.default_rng(3)
+    n = nsf * per_sf
+    Ls = rng.choice([72, 144, 288, 576], n)
+    nbs = rng.choice([27, 31], n)
+    arr = (s.srsgpu_dci_cand_t * n)()
+    lo = oo = 0
+    for i in range(n):
+        arr[i].llr_offset, arr[i].out_offset, arr[i].E, arr[i].nof_bits = lo, oo, int(Ls[i]), int(nbs[i])
+        lo += int(Ls[i])
+        oo += int(nbs[i]) + 16
+    llr = (rng.standard_normal(lo) + np.where(rng.random(lo) < 0.5, 1.0, -1.0)).astype(np.float32)
+    d_c = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
+    d_llr = torch.from_numpy(llr).cuda()
+    d_out = torch.zeros(oo, dtype=torch.uint8, device="cuda")
+    d_crc = torch.zeros(n, dtype=torch.int16, device="cuda")
+    d_dec = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+
+    def step():
+        if s._lib.srsgpu_dci_decode_dev(s._vp(d_c.data_ptr()), n, s._vp(d_llr.data_ptr()),
+                                        s._vp(d_out.data_ptr()), s._vp(d_crc.data_ptr()),
+                                        s._vp(d_dec.data_ptr()), s._vp(st)) != 0:
+            raise RuntimeError("srsgpu_dci_decode_dev failed")
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": "pdcch_dci_blind_decode_%dsf_x%d_candidates" % (nsf, per_sf),
+            "candidates_per_launch": n, "ms_per_launch": round(el / steps * 1e3, 3),
+            "candidates_per_s": round(n * steps / el, 1),
+            "subframes_per_s": round(nsf * steps / el, 1),
+            "decoded_fraction": round(float(d_dec.float().mean().item()), 3)}
+
+
 def dropin_latency(s, llr, ncb=16):
     """The drop-in srslte_tdec_iteration path (include/srslte/phy/fec/turbodecoder.h) as an
     unmodified decode_tb_cb loop drives it (sch.c:356-391): per code block srslte_tdec_new_cb, then
@@ -478,7 +524,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -724,12 +770,17 @@ def main():
         dec8 = {"decoder": "AUTO 8-bit (int8 AVX8 window, 32 sub-blocks)",
                 "mbps": round(decoded_mbps(max(1, world), NCB, K, args.steps, el8), 1),
                 "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
+    dci = None
+    if "dci" in legs and rank == 0:
+        dci = dci_blind_decode(s, torch, max(4, args.steps // 2))
     dropin = None
     if "dropin" in legs and rank == 0:
         dropin = dropin_latency(s, llr)
     batch.close()
     if rank == 0 and dropin:
         result["dropin_latency"] = dropin
+    if rank == 0 and dci:
+        result["pdcch_dci"] = dci
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
