@@ -124,26 +124,43 @@ __global__ __launch_bounds__(64) void k_dci_decode(const srsgpu_dci_cand_t *__re
   const int F = nbits + 16, out_len = 3 * F;
   const int nrows = (out_len / 3 - 1) / 32 + 1, K_p = nrows * 32;
   const int ndummy = max(K_p - out_len / 3, 0);
+  __shared__ float es[SRSGPU_DCI_MAX_E];
+  for (int i = lane; i < E; i += 64) es[i] = e[i];
   for (int i = lane; i < 3 * K_p; i += 64) tmp[i] = 10000.0f;
   __syncthreads();
-  if (lane == 0) {
+  if (lane == 0) { // the mean in the reference's order (double sum, pdcch.c:386-390)
     double mean = 0;
-    for (int i = 0; i < E; i++) mean = __dadd_rn(mean, (double)fabsf(e[i]));
+    for (int i = 0; i < E; i++) mean = __dadd_rn(mean, (double)fabsf(es[i]));
     mean = __ddiv_rn(mean, (double)E);
     go = mean > 0.5;
-    if (go) {
-      int k = 0, j = 0;
-      while (k < E) {
+  }
+  __syncthreads();
+  if (go) {
+    // bit collection (rm_conv_rx.c:124-143) in parallel: input k lands on the valid position of
+    // rank k mod V (V = out_len valid positions per pass), so position j of rank r receives
+    // inputs r, r + V, r + 2V, ... in that order, which is the reference's soft-combining order
+    const int V = out_len;
+    int base = 0;
+    for (int c0 = 0; c0 < 3 * K_p; c0 += 64) {
+      const int j = c0 + lane;
+      bool valid = false;
+      if (j < 3 * K_p) {
         const int d_i = (j % K_p) / nrows, d_j = (j % K_p) % nrows;
-        if (d_j * 32 + kPermCC[d_i] >= ndummy) {
-          const float x = e[k];
-          if (tmp[j] == 10000.0f)
-            tmp[j] = x;
+        valid = d_j * 32 + kPermCC[d_i] >= ndummy;
+      }
+      const uint64_t mask = __ballot(valid);
+      const int r = base + __popcll(mask & ((1ull << lane) - 1ull));
+      base += __popcll(mask);
+      if (valid) {
+        float acc = 10000.0f;
+        for (int k = r; k < E; k += V) {
+          const float x = es[k];
+          if (acc == 10000.0f)
+            acc = x;
           else if (x != 10000.0f)
-            tmp[j] = __fadd_rn(tmp[j], x);
-          k++;
+            acc = __fadd_rn(acc, x);
         }
-        if (++j == 3 * K_p) j = 0;
+        tmp[j] = acc;
       }
     }
   }
