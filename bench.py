@@ -15,6 +15,7 @@ import argparse
 import ctypes
 import gc
 import json
+import re
 import os
 import sys
 import threading
@@ -432,7 +433,9 @@ def load_profile_json(workload, tag="pmc_traffic"):
     pdir = os.path.join(REPO, "profiles")
     best = None
     if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
+        # natural order (r02_s13 after r02_s7): the newest matching record wins
+        natural = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]
+        for f in sorted(os.listdir(pdir), key=natural):
             if tag in f and f.endswith(".json"):
                 try:
                     d = json.load(open(os.path.join(pdir, f)))
