@@ -52,5 +52,15 @@ hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool
 // tables: 2 BPSK + 4 QPSK + 16 16QAM + 64 64QAM constellation points (lte_tables.c order)
 hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const float2 *tables,
                            hipStream_t st);
+// PCFICH of one subframe (srslte_pcfich_decode_multi)
+struct PcfichItem {
+  uint64_t grid_off, ce_off; // this subframe's [rx] grid planes / [rx][port] estimate planes
+  uint32_t sf_idx;
+  float noise;
+};
+// idx: the 16 RE indices of symbol 0; seq[sf]: the 32 scrambling bits of subframe sf
+hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, const float2 *ce,
+                         size_t ant_stride, int nof_prb, int nports, int nrx, const uint32_t *idx,
+                         const uint32_t *seq, uint32_t *cfi, float *corr, hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -544,4 +544,74 @@ hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ PCFICH ----
+// srslte_pcfich_decode_multi (pcfich.c:178-241) per subframe, one wavefront: lane j < 16
+// equalises RE j of the 16 PCFICH REs (regs.c:477-512 + :622-665: four REGs of symbol 0) with the
+// PDSCH equalisers above on the reference's paths for 16 <= 32 symbols (SISO: the C path with the
+// noise estimate, scaling 1; 2 ports: generic transmit diversity + layer demapping), demaps QPSK
+// (x times (float) -sqrt 2, demod_soft.c:71-73) and descrambles (+-1, sequences.c:42-44); lane 0
+// correlates with the three CFI codewords as +-1 in order (pcfich.c:129-147, vector.c:359-366).
+__device__ __forceinline__ int cfi_bit(int c, int i) { // 36.212 Table 5.3.4-1: 011 / 101 / 110 repeated
+  const int r = i % 3;
+  return c == 0 ? (r != 0) : c == 1 ? (r != 1) : (r != 2);
+}
+__global__ __launch_bounds__(64) void k_pcfich(const PcfichItem *__restrict__ items, int n,
+                                               const float2 *__restrict__ grid,
+                                               const float2 *__restrict__ ce, size_t ant_stride,
+                                               int nof_prb, int nports, int nrx,
+                                               const uint32_t *__restrict__ idx,
+                                               const uint32_t *__restrict__ seq,
+                                               uint32_t *__restrict__ cfi, float *__restrict__ corr) {
+  __shared__ float l[32];
+  const int s = blockIdx.x, j = threadIdx.x;
+  if (s >= n) return;
+  const PcfichItem it = items[s];
+  LlrItem t;
+  memset(&t, 0, sizeof(t));
+  for (int a = 0; a < nrx; a++) {
+    t.y[a] = grid + it.grid_off + (size_t)a * ant_stride;
+    for (int p = 0; p < nports; p++) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
+  }
+  t.map = idx;
+  t.nof_re = 16;
+  t.nrx = nrx;
+  t.noise = it.noise;
+  t.scaling = 1.0f;
+  t.inv_scaling = 1.0f;
+  if (j < 16) {
+    const Eq e = nports == 2 ? equalise_txdiv(t, (uint32_t)j) : equalise(t, idx[j], (uint32_t)j);
+    const float s2 = -1.41421354f; // (float) -sqrt(2)
+    const uint32_t c = seq[it.sf_idx];
+    float a0 = __fmul_rn(e.xr, s2), a1 = __fmul_rn(e.xi, s2);
+    if ((c >> (2 * j)) & 1u) a0 = -a0;
+    if ((c >> (2 * j + 1)) & 1u) a1 = -a1;
+    l[2 * j] = a0;
+    l[2 * j + 1] = a1;
+  }
+  __syncthreads();
+  if (j == 0) {
+    float mx = 0.f;
+    int index = 0;
+    for (int k = 0; k < 3; k++) {
+      float r = 0.f;
+      for (int i = 0; i < 32; i++) r = __fadd_rn(r, cfi_bit(k, i) ? l[i] : -l[i]);
+      if (r > mx) {
+        mx = r;
+        index = k;
+      }
+    }
+    cfi[s] = (uint32_t)index + 1;
+    corr[s] = mx;
+  }
+}
+
+hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, const float2 *ce,
+                         size_t ant_stride, int nof_prb, int nports, int nrx, const uint32_t *idx,
+                         const uint32_t *seq, uint32_t *cfi, float *corr, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pcfich, dim3(n), dim3(64), 0, st, d_items, n, grid, ce, ant_stride, nof_prb,
+                     nports, nrx, idx, seq, cfi, corr);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

@@ -109,6 +109,12 @@ class srsgpu_dci_cand_t(ctypes.Structure):
                 ("E", ctypes.c_uint32), ("nof_bits", ctypes.c_uint32)]
 
 
+class srsgpu_pcfich_sf_t(ctypes.Structure):
+    """include/srsgpu/pcfich_batch.h"""
+    _fields_ = [("grid_offset", ctypes.c_uint64), ("ce_offset", ctypes.c_uint64),
+                ("sf_idx", ctypes.c_uint32), ("noise_estimate", ctypes.c_float)]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -168,6 +174,11 @@ _sig = {
     "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_viterbi37_tb_decode_f_dev": (_i32, [_vp, _u32, _vp, _vp, _vp]),
     "srsgpu_dci_decode_dev": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "srsgpu_pcfich_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t)]),
+    "srsgpu_pcfich_destroy": (None, [_vp]),
+    "srsgpu_pcfich_re_map": (_i32, [_vp, _u32p]),
+    "srsgpu_pcfich_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pcfich_sf_t), _u32, _vp, _vp, _sz,
+                                        _vp, _vp, _vp]),
     "srsgpu_rxq_create": (_i32, [ctypes.POINTER(_vp), _vp, _u32, _u32, _u32, _u32, _u32]),
     "srsgpu_rxq_destroy": (None, [_vp]),
     "srsgpu_rxq_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -492,6 +503,35 @@ def make_tb_array(tbs_list):
 def make_sf_array(sfs):
     """srsgpu_pdsch_sf_t[] from make_sf() results, built once and reusable across calls"""
     return sfs if isinstance(sfs, ctypes.Array) else (srsgpu_pdsch_sf_t * len(sfs))(*sfs)
+
+
+class Pcfich:
+    """srsgpu_pcfich_t: batched srslte_pcfich_decode_multi (CFI detection) on device grids laid
+    out as Pdsch's (include/srsgpu/pcfich_batch.h)."""
+
+    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+        self.q = _vp()
+        if _lib.srsgpu_pcfich_create(ctypes.byref(self.q), ctypes.byref(self.cell)) != 0:
+            raise RuntimeError("srsgpu_pcfich_create failed")
+
+    def re_map(self):
+        idx = (ctypes.c_uint32 * 16)()
+        assert _lib.srsgpu_pcfich_re_map(self.q, idx) == 16
+        return list(idx)
+
+    def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_cfi, d_corr, stream=None):
+        """sfs: list of (grid_offset, ce_offset, sf_idx, noise_estimate)"""
+        arr = (srsgpu_pcfich_sf_t * max(len(sfs), 1))()
+        for i, (g, c, sf, n) in enumerate(sfs):
+            arr[i].grid_offset, arr[i].ce_offset, arr[i].sf_idx, arr[i].noise_estimate = g, c, sf, n
+        return _lib.srsgpu_pcfich_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
+                                             _vp(d_cfi), _vp(d_corr), _vp(stream))
+
+    def __del__(self):
+        if getattr(self, "q", None):
+            _lib.srsgpu_pcfich_destroy(self.q)
+            self.q = None
 
 
 class Pdsch:

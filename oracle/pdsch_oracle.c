@@ -678,3 +678,85 @@ int orc_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data,
   *crc_rem = (uint16_t)(p ^ crc);
   return 1;
 }
+
+/* ---------------------------------------------------------------- PCFICH ---------- */
+/* srslte_regs_pcfich_get's 16 REs (regs.c:477-512 regs_pcfich_init, :622-665 regs_reg_init):
+ * REG i at k = (6 (N_ID mod 2 N_RB) + floor(i N_RB / 2) 6) mod 12 N_RB in OFDM symbol 0, its four
+ * REs the six subcarriers k.. minus the reference signals at v_o = N_ID mod 3 and v_o + 3 */
+int orc_pcfich_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t *idx) {
+  const uint32_t k_hat = 6 * (cell_id % (2 * nof_prb)), vo = cell_id % 3;
+  int n = 0;
+  for (uint32_t i = 0; i < 4; i++) {
+    const uint32_t k0 = (k_hat + (i * nof_prb / 2) * 6) % (nof_prb * 12);
+    for (uint32_t s = 0; s < 6; s++)
+      if (s != vo && s != vo + 3) idx[n++] = k0 + s;
+  }
+  return n;
+}
+
+/* srslte_pcfich_decode_multi (pcfich.c:178-241): the 16 REs, SISO predecoding with the noise
+ * estimate (one port: the C path, 16 <= 32 symbols) or 2-port transmit diversity (generic path) +
+ * layer demapping, QPSK soft demapping x (-sqrt 2) (demod_soft.c:71-73, vector product, exact),
+ * scrambling by +-1 (sequences.c:42-44: c_init = (ns/2 + 1)(2 N_ID + 1) 2^9 + N_ID with ns =
+ * 2 sf), and the sequential float correlation with the three codewords as +-1 (pcfich.c:129-147,
+ * vector.c:359-366): cfi = 1 + the first index of the strict maximum over 0. y [rx][n], h
+ * [port][rx][n] full subframe grids (complex float). */
+int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx,
+                      const float *const *y, const float *const *h, float noise, uint32_t sf_idx,
+                      uint32_t *cfi, float *corr) {
+  static const uint8_t tab[3][32] = {
+      {0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1},
+      {1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0},
+      {1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1}};
+  uint32_t idx[16];
+  orc_pcfich_re_map(nof_prb, cell_id, idx);
+  float ys[2][32], hs[2][2][32], d[32];
+  for (uint32_t a = 0; a < nrx; a++)
+    for (int i = 0; i < 16; i++) {
+      ys[a][2 * i] = y[a][2 * idx[i]];
+      ys[a][2 * i + 1] = y[a][2 * idx[i] + 1];
+      for (uint32_t p = 0; p < nof_ports; p++) {
+        hs[p][a][2 * i] = h[p * nrx + a][2 * idx[i]];
+        hs[p][a][2 * i + 1] = h[p * nrx + a][2 * idx[i] + 1];
+      }
+    }
+  if (nof_ports == 1) {
+    /* srslte_predecoding_single_multi, C path (precoding.c:330-352 with n <= 32) */
+    for (int i = 0; i < 16; i++) {
+      float hh = 0, rr = 0, ri = 0;
+      for (uint32_t a = 0; a < nrx; a++) {
+        const double yr = ys[a][2 * i], yi = ys[a][2 * i + 1], hr = hs[0][a][2 * i], hi = hs[0][a][2 * i + 1];
+        rr = (float)((double)rr + (yr * hr - yi * -hi));
+        ri = (float)((double)ri + (yr * -hi + yi * hr));
+        hh = (float)((double)hh + (hr * hr + hi * hi));
+      }
+      const float den = (hh + noise) * 1.0f;
+      d[2 * i] = rr / den;
+      d[2 * i + 1] = ri / den;
+    }
+  } else {
+    orc_predecode_txdiv(ys[0], nrx > 1 ? ys[1] : NULL, hs[0][0], nrx > 1 ? hs[0][1] : NULL, hs[1][0],
+                        nrx > 1 ? hs[1][1] : NULL, (int)nrx, 16, 1.0f, d, NULL);
+  }
+  uint8_t c[32];
+  orc_sequence(((2 * sf_idx) / 2 + 1) * (2 * cell_id + 1) * 512 + cell_id, 32, c);
+  const float s2 = (float)(-sqrt(2));
+  float l[32];
+  for (int i = 0; i < 32; i++) {
+    l[i] = d[i] * s2;
+    if (c[i]) l[i] = -l[i];
+  }
+  float mx = 0;
+  int index = 0;
+  for (int k = 0; k < 3; k++) {
+    float r = 0;
+    for (int i = 0; i < 32; i++) r += (float)(2.0 * tab[k][i] - 1.0) * l[i];
+    if (r > mx) {
+      mx = r;
+      index = k;
+    }
+  }
+  *cfi = (uint32_t)index + 1;
+  *corr = mx;
+  return 0;
+}

@@ -23,6 +23,11 @@ int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
 int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out);
 /* one DCI candidate as srslte_pdcch_decode_msg: 1 decoded (data: nof_bits + 16 bits), 0 skipped */
 int orc_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data, uint16_t *crc_rem);
+/* PCFICH: RE map (16 indices into symbol 0) and srslte_pcfich_decode_multi; y [rx], h [port*nrx+rx] */
+int orc_pcfich_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t *idx);
+int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx,
+                      const float *const *y, const float *const *h, float noise, uint32_t sf_idx,
+                      uint32_t *cfi, float *corr);
 /* 8-bit LLR chain (llr_is_8bit) */
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);

@@ -622,3 +622,48 @@ int ref_dci_decode(const float *e, uint32_t E, uint32_t nof_bits, uint8_t *data,
   free(in);
   return 1;
 }
+
+/* ---------------------------------------------------------------- PCFICH ---------- */
+#include "srslte/phy/phch/pcfich.h"
+#include "srslte/phy/phch/regs.h"
+#include "srslte/phy/utils/vector.h"
+/* srslte_pcfich_decode_multi (pcfich.c:178-241) on one subframe: grids [nrx] and estimates
+ * [port][rx] (14 x 12 nof_prb complex each), noise_estimate -> cfi, corr; and, with grids = NULL,
+ * the 16 RE indices of srslte_regs_pcfich_get (index-valued grid) into idx */
+int ref_pcfich(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx, const float *g0,
+               const float *g1, const float *h00, const float *h01, const float *h10, const float *h11,
+               float noise, uint32_t sf_idx, uint32_t *cfi, float *corr, uint32_t *idx) {
+  srslte_cell_t cell = {nof_prb, nof_ports, cell_id, SRSLTE_CP_NORM, SRSLTE_PHICH_NORM, SRSLTE_PHICH_R_1};
+  srslte_regs_t regs;
+  srslte_pcfich_t q;
+  if (srslte_regs_init(&regs, cell)) return -1;
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  if (!g0) {
+    cf_t *g = srslte_vec_malloc(sizeof(cf_t) * n), out[REGS_PCFICH_NSYM];
+    for (uint32_t i = 0; i < n; i++) g[i] = (float)i;
+    const int r = srslte_regs_pcfich_get(&regs, g, out);
+    for (int i = 0; i < r; i++) idx[i] = (uint32_t)crealf(out[i]);
+    free(g);
+    srslte_regs_free(&regs);
+    return r;
+  }
+  if (srslte_pcfich_init(&q, nrx) || srslte_pcfich_set_cell(&q, &regs, cell)) return -1;
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL}, *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  const float *gs[2] = {g0, g1}, *hs[2][2] = {{h00, h01}, {h10, h11}};
+  for (uint32_t a = 0; a < nrx; a++) {
+    sf[a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    memcpy(sf[a], gs[a], sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nof_ports; p++) {
+      ce[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+      memcpy(ce[p][a], hs[p][a], sizeof(cf_t) * n);
+    }
+  }
+  const int r = srslte_pcfich_decode_multi(&q, sf, ce, noise, sf_idx, cfi, corr);
+  for (uint32_t a = 0; a < nrx; a++) {
+    free(sf[a]);
+    for (uint32_t p = 0; p < nof_ports; p++) free(ce[p][a]);
+  }
+  srslte_pcfich_free(&q);
+  srslte_regs_free(&regs);
+  return r < 0 ? -1 : 0;
+}

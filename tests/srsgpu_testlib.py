@@ -567,3 +567,51 @@ def dci_decode(lib, e, nof_bits, ref=False):
     r = f(e.ctypes.data_as(_f32p), e.size, nof_bits, _ptr(d, _u8p), ctypes.byref(c))
     assert r in (0, 1)
     return r, d, c.value
+
+
+# ------------------------------------------------------------------ PCFICH ----
+def pcfich_re_map(lib, nof_prb, cell_id, ref=False):
+    """the 16 RE indices of symbol 0 (srslte_regs_pcfich_get order)"""
+    L = lib.lib if hasattr(lib, "lib") else lib
+    idx = np.zeros(16, np.uint32)
+    if ref:
+        f = L.ref_pcfich
+        f.argtypes = [ctypes.c_uint32] * 4 + [_f32p] * 6 + [ctypes.c_float, ctypes.c_uint32, _u32p,
+                                                            _f32p, _u32p]
+        assert f(nof_prb, cell_id, 1, 1, None, None, None, None, None, None, 0.0, 0, None, None,
+                 _ptr(idx, _u32p)) == 16
+    else:
+        f = L.orc_pcfich_re_map
+        f.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _u32p]
+        assert f(nof_prb, cell_id, _ptr(idx, _u32p)) == 16
+    return idx
+
+
+def pcfich_decode(lib, nof_prb, cell_id, nports, nrx, y, h, noise, sf_idx, ref=False):
+    """srslte_pcfich_decode_multi: y[a] complex64 subframe grids, h[p][a] estimates -> (cfi, corr)"""
+    L = lib.lib if hasattr(lib, "lib") else lib
+    n = nof_prb * 12 * 14
+    pad = lambda a: np.ascontiguousarray(np.concatenate([a, np.zeros(n - a.size, np.complex64)])
+                                         if a.size < n else a, np.complex64)
+    ys = [pad(y[a]) for a in range(nrx)]
+    hs = [[pad(h[p][a]) for a in range(nrx)] for p in range(nports)]
+    P = lambda a: a.ctypes.data_as(_f32p) if a is not None else None
+    cfi, corr = ctypes.c_uint32(0), ctypes.c_float(0)
+    if ref:
+        f = L.ref_pcfich
+        f.argtypes = [ctypes.c_uint32] * 4 + [_f32p] * 6 + [ctypes.c_float, ctypes.c_uint32, _u32p,
+                                                            _f32p, _u32p]
+        g = lambda p, a: hs[p][a] if p < nports and a < nrx else None
+        r = f(nof_prb, cell_id, nports, nrx, P(ys[0]), P(ys[1]) if nrx > 1 else None,
+              P(g(0, 0)), P(g(0, 1)), P(g(1, 0)), P(g(1, 1)), noise, sf_idx, ctypes.byref(cfi),
+              ctypes.byref(corr), None)
+    else:
+        f = L.orc_pcfich_decode
+        f.argtypes = [ctypes.c_uint32] * 4 + [ctypes.POINTER(_f32p), ctypes.POINTER(_f32p),
+                                              ctypes.c_float, ctypes.c_uint32, _u32p, _f32p]
+        ya = (_f32p * 2)(*[P(v) for v in ys] + [None] * (2 - nrx))
+        ha = (_f32p * 4)(*[P(hs[p][a]) for p in range(nports) for a in range(nrx)] +
+                         [None] * (4 - nports * nrx))
+        r = f(nof_prb, cell_id, nports, nrx, ya, ha, noise, sf_idx, ctypes.byref(cfi), ctypes.byref(corr))
+    assert r == 0, r
+    return cfi.value, corr.value
