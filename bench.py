@@ -492,6 +492,41 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
             "decoded_fraction": round(float(d_dec.float().mean().item()), 3)}
 
 
+def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
+    """PCFICH CFI detection: srslte_pcfich_decode_multi for nsf subframes of
+    a 20 MHz 2-port cell with 2 rx antennas (transmit diversity) per launch (srsgpu_pcfich_decode_dev),
+    random grids and estimates laid out as the receiver's full subframe planes."""
+    rng = np.random.default_rng(4)
+    stride, nrx, nports = nof_prb * 12 * 14, 2, 2
+    n0 = nof_prb * 12
+    grid = torch.zeros((nsf, nrx, stride, 2), dtype=torch.float32, device="cuda")
+    ce = torch.zeros((nsf, nrx * nports, stride, 2), dtype=torch.float32, device="cuda")
+    grid[:, :, :n0] = torch.from_numpy(rng.standard_normal((nsf, nrx, n0, 2)).astype(np.float32)).cuda()
+    ce[:, :, :n0] = torch.from_numpy(rng.standard_normal((nsf, nrx * nports, n0, 2)).astype(np.float32)).cuda()
+    d_cfi = torch.zeros(nsf, dtype=torch.int32, device="cuda")
+    d_corr = torch.zeros(nsf, dtype=torch.float32, device="cuda")
+    q = s.Pcfich(nof_prb, 1, nports, nrx)
+    sfs = [(i * nrx * stride, i * nrx * nports * stride, i % 10, 0.01) for i in range(nsf)]
+    st = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+
+    def step():
+        if q.decode_dev(sfs, grid.data_ptr(), ce.data_ptr(), stride, d_cfi.data_ptr(), d_corr.data_ptr(), st) != 0:
+            raise RuntimeError("srsgpu_pcfich_decode_dev failed")
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del grid, ce
+    return {"workload": "pcfich_cfi_%dsf_%dprb_2ports_2rx" % (nsf, nof_prb),
+            "ms_per_launch": round(el / steps * 1e3, 3), "subframes_per_s": round(nsf * steps / el, 1)}
+
+
 def dropin_latency(s, llr, ncb=16):
     """The drop-in srslte_tdec_iteration path (include/srslte/phy/fec/turbodecoder.h) as an
     unmodified decode_tb_cb loop drives it (sch.c:356-391): per code block srslte_tdec_new_cb, then
@@ -527,7 +562,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -776,6 +811,9 @@ def main():
     dci = None
     if "dci" in legs and rank == 0:
         dci = dci_blind_decode(s, torch, max(4, args.steps // 2))
+    pcf = None
+    if "pcfich" in legs and rank == 0:
+        pcf = pcfich_cfi(s, torch, max(4, args.steps // 2))
     dropin = None
     if "dropin" in legs and rank == 0:
         dropin = dropin_latency(s, llr)
@@ -784,6 +822,8 @@ def main():
         result["dropin_latency"] = dropin
     if rank == 0 and dci:
         result["pdcch_dci"] = dci
+    if rank == 0 and pcf:
+        result["pcfich"] = pcf
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
