@@ -13,6 +13,7 @@
  *                                        (pdsch.c:868-1007, TM1 single antenna port and TM3 CDD)
  *   srslte_dlsch_decode2(q, cfg, sb, e_bits, data, tb_idx)  (sch.c:506-517, 16-bit LLRs)
  *   srslte_rm_turbo_rx_lut(in, out, in_len, cb_idx, rv)      (rm_turbo.c:378-381)
+ *   srslte_pcfich_decode_multi(q, sf, ce, noise, sf_idx, cfi, corr)  (pcfich.c:178-241)
  *   srslte_softbuffer_rx_init / _free / _reset / _reset_tbs / _reset_cb  (softbuffer.c:46-153):
  *                                        the reference's host work, plus the GPU softbuffer state
  *   srsgpu_shim_release(q)               called from srslte_ofdm_rx_free / srslte_chest_dl_free /
@@ -42,12 +43,14 @@
 #include "srslte/phy/fec/cbsegm.h"
 #include "srslte/phy/fec/rm_turbo.h"
 #include "srslte/phy/fec/softbuffer.h"
+#include "srslte/phy/phch/pcfich.h"
 #include "srslte/phy/phch/pdsch.h"
 #include "srslte/phy/phch/sch.h"
 
 #include "srsgpu/chest_batch.h"
 #include "srsgpu/dlsch_batch.h"
 #include "srsgpu/ofdm_batch.h"
+#include "srsgpu/pcfich_batch.h"
 #include "srsgpu/pdsch_batch.h"
 
 /* ---- HIP runtime entry points used for the host <-> device staging (libamdhip64) ---- */
@@ -61,7 +64,7 @@ extern hipError_t hipDeviceSynchronize(void);
 
 /* ---- object registry ---- */
 #define SHIM_MAX 64
-typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH, SHIM_SCH } shim_kind_t;
+typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH, SHIM_SCH, SHIM_PCFICH } shim_kind_t;
 typedef struct {
   const void *owner;
   shim_kind_t kind;
@@ -99,6 +102,7 @@ static void shim_reset(shim_entry_t *e) {
     if (e->kind == SHIM_CHEST) srsgpu_chest_destroy((srsgpu_chest_t *)e->gpu);
     if (e->kind == SHIM_PDSCH) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
     if (e->kind == SHIM_SCH) srsgpu_dlsch_destroy((srsgpu_dlsch_t *)e->gpu);
+    if (e->kind == SHIM_PCFICH) srsgpu_pcfich_destroy((srsgpu_pcfich_t *)e->gpu);
   }
   if (e->d_a) hipFree(e->d_a);
   if (e->d_b) hipFree(e->d_b);
@@ -158,6 +162,48 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
   srsgpu_ofdm_rx_sf_dev((srsgpu_ofdm_t *)e->gpu, 1, e->d_a, q->sf_sz, e->d_b,
                         SRSLTE_SF_LEN_RE(nof_prb, q->cp));
   hipMemcpy(q->out_buffer, e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp), D2H);
+}
+
+/* ------------------------------------------------------------------ PCFICH ---- */
+/* srslte_pcfich_decode_multi (pcfich.c:178-241): *cfi and *corr_result from the GPU
+ * (srsgpu_pcfich_decode_dev), bit-exact; returns 1 as the reference. Only OFDM symbol 0 of the grids
+ * is staged. The reference's scratch buffers in q (symbols, ce, d, data_f) are not filled. */
+int srslte_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_PORTS],
+                               cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
+                               uint32_t nsubframe, uint32_t *cfi, float *corr_result) {
+  if (!q || !sf_symbols || nsubframe >= SRSLTE_NSUBFRAMES_X_FRAME) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->nof_rx_antennas > 2 || !ce) {
+    fprintf(stderr, "srsgpu shim: GPU PCFICH covers 1-2 ports, normal CP, 1-2 rx antennas\n");
+    return SRSLTE_ERROR;
+  }
+  shim_entry_t *e = shim_get(q, SHIM_PCFICH);
+  if (!e) return SRSLTE_ERROR;
+  const uint32_t np = q->cell.nof_ports, nrx = q->nof_rx_antennas, n = q->cell.nof_prb * SRSLTE_NRE;
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np * 4 + nrx || !e->gpu) {
+    shim_reset(e);
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, nrx};
+    if (srsgpu_pcfich_create((srsgpu_pcfich_t **)&e->gpu, &c)) return SRSLTE_ERROR;
+    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
+    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
+    hipMalloc((void **)&e->d_c, sizeof(float) * 2); /* cfi, correlation */
+    e->nof_prb = q->cell.nof_prb;
+    e->cell_id = q->cell.id;
+    e->aux = np * 4 + nrx;
+  }
+  for (uint32_t a = 0; a < nrx; a++) {
+    hipMemcpy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D);
+    for (uint32_t p = 0; p < np; p++) /* reference ce[port][rx]; GPU planes [rx][port] */
+      hipMemcpy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D);
+  }
+  const srsgpu_pcfich_sf_t sf = {0, 0, nsubframe, noise_estimate};
+  if (srsgpu_pcfich_decode_dev((srsgpu_pcfich_t *)e->gpu, &sf, 1, e->d_a, e->d_b, n,
+                               (uint32_t *)e->d_c, e->d_c + 1, NULL))
+    return SRSLTE_ERROR;
+  uint32_t out[2];
+  hipMemcpy(out, e->d_c, sizeof(out), D2H);
+  if (cfi) *cfi = out[0];
+  if (corr_result) memcpy(corr_result, &out[1], sizeof(float));
+  return 1;
 }
 
 /* ------------------------------------------------------------------ channel estimation ---- */

@@ -37,6 +37,7 @@
 #include "srslte/phy/fec/rm_turbo.h"
 #include "srslte/phy/fec/softbuffer.h"
 #include "srslte/phy/phch/sch.h"
+#include "srslte/phy/phch/pcfich.h"
 #include "srslte/phy/phch/pdsch.h"
 #include "srslte/phy/phch/ra.h"
 #include "srslte/phy/utils/vector.h"
@@ -57,6 +58,10 @@ int srsgpu_shim_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len
 int srsgpu_shim_softbuffer_rx_init(srslte_softbuffer_rx_t *q, uint32_t nof_prb);
 void srsgpu_shim_softbuffer_rx_reset(srslte_softbuffer_rx_t *q);
 void srsgpu_shim_softbuffer_rx_free(srslte_softbuffer_rx_t *q);
+int srsgpu_shim_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_PORTS],
+                                    cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
+                                    uint32_t nsubframe, uint32_t *cfi, float *corr_result);
+int srsgpu_shim_release(const void *owner);
 
 static uint64_t rng = 1;
 static double urand(void) {
@@ -299,7 +304,37 @@ int main(int argc, char **argv) {
     srslte_softbuffer_rx_free(&sra2[t]);
     srsgpu_shim_softbuffer_rx_free(&srb2[t]);
   }
-  printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u dlsch=%u dlsch_mismatches=%u rm_mismatches=%u\n", ntx,
-         nacks, nbad, nsoft, tbs, ndl, ndl_bad, nrm_bad);
-  return nbad || ndl_bad || nrm_bad ? 1 : 0;
+  /* PCFICH: the reference srslte_pcfich_decode_multi and the shim on the same random symbol-0
+   * grids of this cell, every subframe index, with and without a noise estimate (own rng stream) */
+  uint32_t npc_bad = 0;
+  {
+    const uint64_t rng_saved = rng;
+    srslte_regs_t regs;
+    static srslte_pcfich_t pa, pb;
+    if (srslte_regs_init(&regs, cell) || srslte_pcfich_init(&pa, nof_rx) ||
+        srslte_pcfich_set_cell(&pa, &regs, cell) || srslte_pcfich_init(&pb, nof_rx) ||
+        srslte_pcfich_set_cell(&pb, &regs, cell))
+      return 2;
+    for (uint32_t it = 0; it < 20; it++) {
+      for (uint32_t a = 0; a < nof_rx; a++)
+        for (uint32_t i = 0; i < nof_prb * SRSLTE_NRE; i++) {
+          y[a][i] = gauss() + gauss() * _Complex_I;
+          for (uint32_t p = 0; p < nports; p++) h[p][a][i] = gauss() + gauss() * _Complex_I;
+        }
+      uint32_t c1 = 0, c2 = 0;
+      float r1 = 0, r2 = 0;
+      const float nz = (it & 1) ? 0.1f : 0.0f;
+      const int e1 = srslte_pcfich_decode_multi(&pa, y, h, nz, it % 10, &c1, &r1);
+      const int e2 = srsgpu_shim_pcfich_decode_multi(&pb, y, h, nz, it % 10, &c2, &r2);
+      if (e1 != e2 || c1 != c2 || memcmp(&r1, &r2, sizeof(float))) npc_bad++;
+    }
+    srsgpu_shim_release(&pb);
+    srslte_pcfich_free(&pa);
+    srslte_pcfich_free(&pb);
+    srslte_regs_free(&regs);
+    rng = rng_saved;
+  }
+  printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u dlsch=%u dlsch_mismatches=%u rm_mismatches=%u "
+         "pcfich_mismatches=%u\n", ntx, nacks, nbad, nsoft, tbs, ndl, ndl_bad, nrm_bad, npc_bad);
+  return nbad || ndl_bad || nrm_bad || npc_bad ? 1 : 0;
 }

@@ -63,6 +63,8 @@ def test_shim_pdsch_decode_matches_reference(case):
     # srslte_rm_turbo_rx_lut) on the same LLRs: exact in every configuration
     assert int(stats["dlsch"]) >= case[6] and int(stats["dlsch_mismatches"]) == 0, r.stdout + r.stderr
     assert int(stats["rm_mismatches"]) == 0, r.stdout + r.stderr
+    # srslte_pcfich_decode_multi drop-in on this cell's ports / rx antennas: CFI and correlation exact
+    assert int(stats["pcfich_mismatches"]) == 0, r.stdout + r.stderr
 
 
 # the 8-bit LLR chain (llr_is_8bit on the PDSCH and its DL-SCH, pdsch.c:795-806, sch.c:344-364):
