@@ -495,7 +495,9 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
 def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
     """PCFICH CFI detection: srslte_pcfich_decode_multi for nsf subframes of
     a 20 MHz 2-port cell with 2 rx antennas (transmit diversity) per launch (srsgpu_pcfich_decode_dev),
-    random grids and estimates laid out as the receiver's full subframe planes."""
+    random grids and estimates laid out as the receiver's full subframe planes. Per call: the
+    descriptor copy, the launch and the API's stream synchronisation (it reuses its pinned
+    descriptor buffer)."""
     rng = np.random.default_rng(4)
     stride, nrx, nports = nof_prb * 12 * 14, 2, 2
     n0 = nof_prb * 12
@@ -507,6 +509,7 @@ def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
     d_corr = torch.zeros(nsf, dtype=torch.float32, device="cuda")
     q = s.Pcfich(nof_prb, 1, nports, nrx)
     sfs = [(i * nrx * stride, i * nrx * nports * stride, i % 10, 0.01) for i in range(nsf)]
+    sfs = (q.make_sf_array(sfs), nsf)  # the host descriptor array a caller keeps between subframes
     st = torch.cuda.current_stream().cuda_stream
     torch.cuda.synchronize()
 

@@ -520,12 +520,19 @@ class Pcfich:
         assert _lib.srsgpu_pcfich_re_map(self.q, idx) == 16
         return list(idx)
 
-    def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_cfi, d_corr, stream=None):
-        """sfs: list of (grid_offset, ce_offset, sf_idx, noise_estimate)"""
+    @staticmethod
+    def make_sf_array(sfs):
+        """list of (grid_offset, ce_offset, sf_idx, noise_estimate) -> srsgpu_pcfich_sf_t array"""
         arr = (srsgpu_pcfich_sf_t * max(len(sfs), 1))()
         for i, (g, c, sf, n) in enumerate(sfs):
             arr[i].grid_offset, arr[i].ce_offset, arr[i].sf_idx, arr[i].noise_estimate = g, c, sf, n
-        return _lib.srsgpu_pcfich_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
+        return arr
+
+    def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_cfi, d_corr, stream=None):
+        """sfs: list of (grid_offset, ce_offset, sf_idx, noise_estimate), or (array, count) from
+        make_sf_array"""
+        arr, n = sfs if isinstance(sfs, tuple) else (self.make_sf_array(sfs), len(sfs))
+        return _lib.srsgpu_pcfich_decode_dev(self.q, arr, n, _vp(d_grid), _vp(d_ce), ant_stride,
                                              _vp(d_cfi), _vp(d_corr), _vp(stream))
 
     def __del__(self):
