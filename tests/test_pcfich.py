@@ -122,3 +122,14 @@ def test_gpu_batch_vs_oracle(oracle, nof_prb, cell_id, nports, nrx):
             assert not np.isfinite(corr[i]) or corr[i] == np.float32(w[1]), i
             continue
         assert cfi[i] == w[0] and corr[i] == np.float32(w[1]), (i, cfi[i], corr[i], w)
+
+
+@pytest.mark.parametrize("nof_prb,cell_id,nports,nrx", [(5, 0, 1, 1), (111, 0, 1, 1), (6, 504, 1, 1),
+                                                        (6, 0, 4, 1), (6, 0, 0, 1), (6, 0, 1, 3)])
+def test_create_rejects_invalid_cells(nof_prb, cell_id, nports, nrx):
+    """srsgpu_pcfich_create validates the cell before touching the device (runs without a GPU):
+    the GPU path covers 6-110 PRB, N_ID 0-503, 1-2 ports, 1-2 rx antennas, and refuses the rest
+    loudly instead of falling back"""
+    import srsgpu_phy as s
+    with pytest.raises(RuntimeError):
+        s.Pcfich(nof_prb, cell_id, nports, nrx)
