@@ -496,8 +496,8 @@ def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
     """PCFICH CFI detection: srslte_pcfich_decode_multi for nsf subframes of
     a 20 MHz 2-port cell with 2 rx antennas (transmit diversity) per launch (srsgpu_pcfich_decode_dev),
     random grids and estimates laid out as the receiver's full subframe planes. Per call: the
-    descriptor copy, the launch and the API's stream synchronisation (it reuses its pinned
-    descriptor buffer)."""
+    descriptor fill and upload and the launch; the API waits only for the previous call's
+    descriptor upload (it reuses its pinned descriptor buffer)."""
     rng = np.random.default_rng(4)
     stride, nrx, nports = nof_prb * 12 * 14, 2, 2
     n0 = nof_prb * 12

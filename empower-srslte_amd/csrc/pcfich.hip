@@ -15,6 +15,9 @@ struct srsgpu_pcfich {
   uint32_t *d_idx = nullptr, *d_seq = nullptr;
   srsgpu::PcfichItem *h_it = nullptr, *d_it = nullptr;
   uint32_t cap = 0;
+  hipEvent_t copied = nullptr; // the last descriptor upload out of h_it has finished
+  bool recorded = false;
+  hipStream_t last = nullptr; // stream of the last call (its kernel may still read d_it)
 };
 
 // 36.211 7.2 Gold sequence, first 32 bits packed LSB first: x1 starts at 1, x2 at c_init, N_c = 1600
@@ -39,6 +42,11 @@ int srsgpu_pcfich_create(srsgpu_pcfich_t **q, const srsgpu_cell_t *cell) {
     return -1;
   srsgpu_pcfich *p = new srsgpu_pcfich;
   p->cell = *cell;
+  if (hipEventCreateWithFlags(&p->copied, hipEventDisableTiming)) {
+    p->copied = nullptr;
+    srsgpu_pcfich_destroy(p);
+    return -1;
+  }
   const uint32_t N = cell->nof_prb, k_hat = 6 * (cell->id % (2 * N)), vo = cell->id % 3;
   int n = 0;
   for (uint32_t i = 0; i < 4; i++) { // REG i, its subcarriers minus the CRS at vo, vo + 3
@@ -64,6 +72,7 @@ void srsgpu_pcfich_destroy(srsgpu_pcfich_t *q) {
   (void)hipFree(q->d_seq);
   (void)hipFree(q->d_it);
   (void)hipHostFree(q->h_it);
+  if (q->copied) (void)hipEventDestroy(q->copied);
   delete q;
 }
 
@@ -80,8 +89,13 @@ int srsgpu_pcfich_decode_dev(srsgpu_pcfich_t *q, const srsgpu_pcfich_sf_t *sf, u
   if (nof_sf == 0) return 0;
   if (ant_stride < (size_t)q->cell.nof_prb * 12) return -1;
   hipStream_t st = (hipStream_t)hip_stream;
+  // h_it is reused: wait until the previous call's upload out of it is done (not its kernel); on
+  // the same stream the previous kernel's reads of d_it are ordered before the next upload, on
+  // another stream wait for them
+  if (q->recorded && (st == q->last ? hipEventSynchronize(q->copied) : hipStreamSynchronize(q->last)))
+    return -1;
   if (nof_sf > q->cap) {
-    if (hipStreamSynchronize(st)) return -1; // the previous call may still read h_it
+    if (q->recorded && hipStreamSynchronize(q->last)) return -1; // the last kernel reads d_it
     (void)hipFree(q->d_it);
     (void)hipHostFree(q->h_it);
     q->d_it = nullptr;
@@ -91,15 +105,16 @@ int srsgpu_pcfich_decode_dev(srsgpu_pcfich_t *q, const srsgpu_pcfich_sf_t *sf, u
         hipMalloc(&q->d_it, sizeof(srsgpu::PcfichItem) * nof_sf))
       return -1;
     q->cap = nof_sf;
-  } else if (hipStreamSynchronize(st)) {
-    return -1;
   }
   for (uint32_t i = 0; i < nof_sf; i++) {
     if (sf[i].sf_idx > 9) return -1;
     q->h_it[i] = {sf[i].grid_offset, sf[i].ce_offset, sf[i].sf_idx, sf[i].noise_estimate};
   }
-  if (hipMemcpyAsync(q->d_it, q->h_it, sizeof(srsgpu::PcfichItem) * nof_sf, hipMemcpyHostToDevice, st))
+  if (hipMemcpyAsync(q->d_it, q->h_it, sizeof(srsgpu::PcfichItem) * nof_sf, hipMemcpyHostToDevice, st) ||
+      hipEventRecord(q->copied, st))
     return -1;
+  q->recorded = true;
+  q->last = st;
   return srsgpu::launch_pcfich(q->d_it, (int)nof_sf, (const float2 *)d_grid, (const float2 *)d_ce,
                                ant_stride, (int)q->cell.nof_prb, (int)q->cell.nof_ports,
                                (int)q->cell.nof_rx_ant, q->d_idx, q->d_seq, d_cfi, d_corr, st)
