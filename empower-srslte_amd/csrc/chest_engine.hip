@@ -230,6 +230,12 @@ int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg) {
   return 0;
 }
 
+int srsgpu_chest_get_cfg(const srsgpu_chest_t *q, srsgpu_chest_cfg_t *cfg) {
+  if (!q || !cfg) return -1;
+  *cfg = q->e.cfg;
+  return 0;
+}
+
 int srsgpu_chest_estimate_meas_dev(srsgpu_chest_t *q, const uint32_t *sf_idx, uint32_t n, const float *d_grid,
                                    size_t stride, float *d_ce, float *d_noise, float *d_meas) {
   if (!q || (!sf_idx && n) || !d_grid || !d_ce) return -1;

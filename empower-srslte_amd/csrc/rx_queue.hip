@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -36,6 +37,24 @@ struct Pending {
   std::chrono::steady_clock::time_point t;
 };
 
+// PSS / EMPTY noise (chest_dl.c:628-637): only subframes 0 and 5 estimate the noise; every other
+// subframe keeps the estimate the object holds, i.e. the latest one of an earlier subframe. One
+// thread per (rx antenna, port) column walks the batch in submission order from the value the
+// previous batch left (last[c]).
+__global__ void k_noise_carry(float *__restrict__ noise, const uint8_t *__restrict__ est, int n, int cols,
+                              float *__restrict__ last) {
+  const int c = threadIdx.x;
+  if (c >= cols) return;
+  float v = last[c];
+  for (int i = 0; i < n; i++) {
+    if (est[i])
+      v = noise[i * cols + c];
+    else
+      noise[i * cols + c] = v;
+  }
+  last[c] = v;
+}
+
 } // namespace
 
 struct srsgpu_rxq {
@@ -47,6 +66,8 @@ struct srsgpu_rxq {
   srsgpu_chest_t *chest = nullptr;
   srsgpu_pdsch_t *pdsch = nullptr;
   float *d_td = nullptr, *d_grid = nullptr, *d_ce = nullptr, *d_noise = nullptr;
+  float *d_noise_last = nullptr; // PSS / EMPTY: the estimate carried between batches
+  uint8_t *d_est = nullptr, *h_est = nullptr; // per subframe: 1 if it estimates the noise
   uint8_t *d_data = nullptr;
   int32_t *d_ret = nullptr;
   uint32_t *d_noi = nullptr;
@@ -59,7 +80,7 @@ struct srsgpu_rxq {
   std::condition_variable cv_work, cv_done;
   std::deque<Pending> queue;
   uint64_t next_ticket = 1, done_upto = 0; // tickets are completed in order
-  std::vector<uint64_t> failed;            // tickets whose batch failed
+  std::set<uint64_t> failed;               // tickets whose batch failed, until waited for
   bool stop = false, flush = false;
   uint64_t nbatches = 0, nsf = 0;
   std::thread worker;
@@ -92,6 +113,10 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMalloc(&d_data, dlen * 2 * mb));
     RXQ_CHK(hipMalloc(&d_ret, sizeof(int32_t) * 2 * mb));
     RXQ_CHK(hipMalloc(&d_noi, sizeof(uint32_t) * 2 * mb));
+    RXQ_CHK(hipMalloc(&d_noise_last, sizeof(float) * nrx * nports));
+    RXQ_CHK(hipMemset(d_noise_last, 0, sizeof(float) * nrx * nports)); // srslte_chest_dl_init: 0
+    RXQ_CHK(hipMalloc(&d_est, mb));
+    RXQ_CHK(hipHostMalloc(&h_est, mb));
     RXQ_CHK(hipHostMalloc(&h_td, sizeof(float) * 2 * td_len * mb * nrx));
     RXQ_CHK(hipHostMalloc(&h_noise, sizeof(float) * mb * nrx * nports));
     RXQ_CHK(hipHostMalloc(&h_data, dlen * 2 * mb));
@@ -112,9 +137,9 @@ struct srsgpu_rxq {
     if (chest) srsgpu_chest_destroy(chest);
     if (pdsch) srsgpu_pdsch_destroy(pdsch);
     for (void *p : {(void *)d_td, (void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data,
-                    (void *)d_ret, (void *)d_noi})
+                    (void *)d_ret, (void *)d_noi, (void *)d_noise_last, (void *)d_est})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_td, (void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi})
+    for (void *p : {(void *)h_td, (void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -131,7 +156,22 @@ struct srsgpu_rxq {
     std::vector<uint32_t> sfi(n * nrx);
     for (uint32_t i = 0; i < n; i++)
       for (uint32_t a = 0; a < nrx; a++) sfi[i * nrx + a] = b[i].it->sf.sf_idx;
+    srsgpu_chest_cfg_t ccfg;
+    if (srsgpu_chest_get_cfg(chest, &ccfg)) return -1;
+    if (ccfg.noise_alg != 0 && ccfg.smooth_filter_auto) {
+      // each subframe's filter would come from the previous subframe's noise: no batch order
+      fprintf(stderr, "srsgpu rxq: smooth_filter_auto with PSS / EMPTY noise is not batched\n");
+      return -1;
+    }
     if (srsgpu_chest_estimate_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise)) return -1;
+    if (ccfg.noise_alg != 0) { // PSS / EMPTY: carry the estimate across subframes in order
+      for (uint32_t i = 0; i < n; i++) h_est[i] = (uint8_t)(b[i].it->sf.sf_idx == 0 || b[i].it->sf.sf_idx == 5);
+      RXQ_CHK(hipMemcpyAsync(d_est, h_est, n, hipMemcpyHostToDevice, st));
+      // grids of one subframe's rx antennas are consecutive: n rows of nrx * nports columns
+      hipLaunchKernelGGL(k_noise_carry, dim3(1), dim3(64), 0, st, d_noise, d_est, (int)n, (int)(nrx * nports),
+                         d_noise_last);
+      RXQ_CHK(hipGetLastError());
+    }
     srsgpu_pdsch_set_noise_dev(pdsch, d_noise);
     srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(pdsch);
     std::vector<srsgpu_pdsch_sf_t> sfs(n);
@@ -196,10 +236,13 @@ struct srsgpu_rxq {
       }
       l.unlock();
       const int r = run(b);
+      // a failed batch may have left copies in flight that still read the pinned staging
+      // buffers: drain the stream before they are reused
+      if (r) (void)hipStreamSynchronize(st);
       l.lock();
       if (r) {
         fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", b.size());
-        for (const Pending &p : b) failed.push_back(p.ticket);
+        for (const Pending &p : b) failed.insert(p.ticket);
       }
       done_upto = b.back().ticket;
       nbatches++;
@@ -251,9 +294,8 @@ int srsgpu_rxq_wait(srsgpu_rxq_t *q, uint64_t ticket) {
   std::unique_lock<std::mutex> l(q->m);
   if (ticket >= q->next_ticket) return -1;
   q->cv_done.wait(l, [&] { return q->done_upto >= ticket; });
-  for (uint64_t f : q->failed)
-    if (f == ticket) return -1;
-  return 0;
+  // a failure is reported once, to the ticket's waiter, and then forgotten
+  return q->failed.erase(ticket) ? -1 : 0;
 }
 
 int srsgpu_rxq_decode(srsgpu_rxq_t *q, srsgpu_rxq_item_t *it) {
@@ -266,6 +308,7 @@ void srsgpu_rxq_flush(srsgpu_rxq_t *q) {
   if (!q) return;
   {
     std::lock_guard<std::mutex> l(q->m);
+    if (q->queue.empty()) return; // nothing to close: the next submission waits as usual
     q->flush = true;
   }
   q->cv_work.notify_one();

@@ -89,6 +89,26 @@ template <typename T> __device__ __forceinline__ gmut_t<T> gmut(void *p) {
   return (gmut_t<T>)(__attribute__((address_space(1))) void *)(uintptr_t)p;
 }
 
+// Buffer resources for the windowed decoders' chunk loads and scatter stores. A wave's arrays are
+// addressed as (wave base in SGPRs) + (lane's byte offset, loop invariant, VGPR) + (step offset,
+// wave-uniform, SGPR): every load and store is one buffer instruction with no per-access VGPR
+// address arithmetic, and no VGPR temporaries whose reuse would make the compiler wait for loads
+// still in flight (the chunk prefetch of the recursions depends on that).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t mk_rsrc(const void *p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+typedef uint32_t u4b __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4b bld128(rsrc_t r, uint32_t vo, uint32_t so) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0);
+}
+__device__ __forceinline__ uint32_t bld32(rsrc_t r, uint32_t vo, uint32_t so) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+}
+__device__ __forceinline__ void bst32(uint32_t v, rsrc_t r, uint32_t vo) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, vo, 0, 0);
+}
+
 // group of workgroup b in a launch: the last group whose first workgroup (field F) is <= b
 enum { GF_LOAD, GF_HALF, GF_PAIR };
 template <int F>
@@ -461,12 +481,20 @@ static __device__ unsigned long long td_chunk[2048 * 80];
 // facts survive inlining (the group tables would otherwise hide them from the scheduler).
 // sp0 / p1 point at the pair's T4 regions, x2 / A at its sub-block-order ones, tbl at the group's
 // T16 table.
+// Wave-level buffer resources of the windowed decoders: SP0, X2, P1 and A from the wave's first
+// pair, the scatter table of the half-iteration; po = byte offset of the lane's pair from the
+// wave's first pair in the 4-byte arrays (2 po in SP0).
+struct WinRes {
+  rsrc_t sp0, x2, p1, a, tb;
+  uint32_t po;
+};
+
 template <int NB, int DIV, int MODE, bool DOUT, bool B8>
 __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *__restrict__ x2,
                                                const s2 *__restrict__ p1, s2 *__restrict__ A,
                                                uint32_t *__restrict__ D, const s2 *__restrict__ tl,
-                                               gptr_t<uint16_t> __restrict__ tbl, s4 *__restrict__ cks,
-                                               int K, int d, int role, int lane) {
+                                               const WinRes &R, s4 *__restrict__ cks, int K, int d,
+                                               int role, int lane) {
   constexpr int CW = 16;
   const int L = K / NB;
   const int G4 = (L + 3) >> 2; // T4 groups per chain
@@ -551,46 +579,38 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     o.s[7] = hi2(e);
   };
 
-  // ---- group loads: group g (steps 4g..4g+3) of chain dd. SP0 (T4) groups are 32 B (two u4),
-  // P1 (T4) 16 B; X2 and A in sub-block order.
-  const u4 *uS = reinterpret_cast<const u4 *>(sp0);
-  const uint32_t *wX = reinterpret_cast<const uint32_t *>(x2);
-  const u4 *uP = reinterpret_cast<const u4 *>(p1);
-  const uint32_t *wA = reinterpret_cast<const uint32_t *>(A);
-  // X2 / A (the scatter targets) are in sub-block order: 4 element loads per group
-  auto ld_sb4 = [&](const uint32_t *w, int g, int dd) {
-    const int i0 = 4 * g * NB + dd;
-    return u4{w[i0], w[i0 + NB], w[i0 + 2 * NB], w[i0 + 3 * NB]};
+  // ---- group loads: group g (steps 4g..4g+3) of chain dd, as buffer loads: lane offset (pair,
+  // chain) in a VGPR, step offset wave-uniform. SP0 (T4) groups are 32 B (two 16-byte loads), P1
+  // (T4) 16 B; X2 and A in sub-block order (4 element loads, one per step).
+  auto ld_sb4 = [&](rsrc_t r, int g, int dd) {
+    const uint32_t vo = R.po + 4u * (uint32_t)dd, so = 16u * NB * (uint32_t)g;
+    return u4{bld32(r, vo, so), bld32(r, vo, so + 4 * NB), bld32(r, vo, so + 8 * NB),
+              bld32(r, vo, so + 12 * NB)};
   };
   auto ld_grp = [&](Grp<MODE> &r, int g, int dd) {
 #ifdef TD_EXP_L2
     g &= 3; // timing experiment only: every load from the pair's first 4 groups (cache resident)
 #endif
-    const int o = g * NB + dd;
     if (MODE == 1) {
-      r.s0 = ld_sb4(wX, g, dd);
-      r.s1 = uP[o];
+      r.s0 = ld_sb4(R.x2, g, dd);
+      r.s1 = bld128(R.p1, R.po + 16u * (uint32_t)dd, 16u * NB * (uint32_t)g);
     } else {
-      r.s0 = uS[2 * o];
-      r.s1 = uS[2 * o + 1];
-      if (MODE == 0) r.a = ld_sb4(wA, g, dd);
+      const uint32_t vo = 2u * R.po + 32u * (uint32_t)dd, so = 32u * NB * (uint32_t)g;
+      r.s0 = bld128(R.sp0, vo, so);
+      r.s1 = bld128(R.sp0, vo, so + 16);
+      if (MODE == 0) r.a = ld_sb4(R.a, g, dd);
     }
   };
   // chunk q of this lane's chain: groups 4q..4q+3 (clamped into the chain for the last, partial
   // chunk: the recursion never reads its steps past L); tables only where phase 2 needs them
   auto ld_chunk = [&](Chunk<MODE> &c, int q, bool with_t) {
     const int g0 = 4 * q;
-    if (g0 + 4 <= G4) {
 #pragma unroll
-      for (int u = 0; u < 4; u++) ld_grp(c.g[u], g0 + u, d);
-    } else {
-#pragma unroll
-      for (int u = 0; u < 4; u++) ld_grp(c.g[u], min(g0 + u, G4 - 1), d);
-    }
+    for (int u = 0; u < 4; u++) ld_grp(c.g[u], min(g0 + u, G4 - 1), d); // uniform (SALU) clamp
     if (with_t) {
-      const gptr_t<u4> ut = (gptr_t<u4>)tbl + (q * NB + d) * 2;
-      c.t[0] = ut[0];
-      c.t[1] = ut[1];
+      const uint32_t vo = 32u * (uint32_t)d, so = 32u * NB * (uint32_t)q;
+      c.t[0] = bld128(R.tb, vo, so);
+      c.t[1] = bld128(R.tb, vo, so + 16);
     }
     // keep the loads here, a chunk ahead of their use: left alone, the scheduler sinks them
     // towards the first use to save registers, and the waves then wait on memory every chunk
@@ -657,18 +677,20 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
         else if (DIV)
           v = v >> 1; // win.h:565-567 srai 1 (SSE16 window)
         {
+#ifdef TD_EXP_FIXST
+          const int t = chunk_t(c, j) & 15; // timing experiment only: stores stay in one segment
+#else
           const int t = chunk_t(c, j); // sub-block index of the scatter target
+#endif
+          s2 out;
           if (B8) { // ext - app with the reference's saturate / wrap split (K32, see above)
             // the reference's array index decides: j for DEC1, fwd[j] for DEC2
             const bool sat = (MODE == 1 ? t : (s0 + j) * NB + d) < K32;
-            const s2 out = MODE == 2 ? v : (sat ? bsub(v, e) : wsub(v, e));
-            if (MODE == 1)
-              A[t] = out;
-            else
-              x2[t] = out;
+            out = MODE == 2 ? v : (sat ? bsub(v, e) : wsub(v, e));
           } else {
-            store_out<MODE == 1>(x2, A, t, v, e);
+            out = wsub(v, e); // store_out: DEC1 E' = L - A into app2, DEC2 L - app2 into A
           }
+          bst32(__builtin_bit_cast(uint32_t, out), MODE == 1 ? R.a : R.x2, R.po + 4u * (uint32_t)t);
         }
         if (DOUT) dacc |= dec_bits(v) << j;
 #pragma unroll
@@ -768,6 +790,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     __syncthreads();
     vm_drain();
     TD_T(3);
+#ifdef TD_EXP_P1ONLY
+    if (K > 0) return; // timing experiment only: prepass and phase 1
+#endif
     // phase 2: chunks qm .. nc-1, betas recomputed from the backward wave's checkpoints. One
     // chunk per loop iteration (the next one loading meanwhile); the last chunk, when L is not a
     // multiple of 16, after the loop.
@@ -862,7 +887,10 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     // phase 1: chunks nc-1 .. qm (steps L-1 .. M); bpre ends as beta[M] before normalisation
     St8 bpre;
     {
-      auto bwd_chunk = [&](const Chunk<MODE> &c, int q, int n, bool keep) { // q > 0: norm never at 0
+      // the state before normalisation at step CW q goes to slot q: a beta checkpoint for q > qm,
+      // bpre for q == qm (slot qm is free: alpha checkpoints fill 0..qm-1, beta ones qm+1..nc),
+      // read back after the loop, so the loop body has no branch on q
+      auto bwd_chunk = [&](const Chunk<MODE> &c, int q, int n) { // q > 0: norm never at 0
         TD_C(nc - 1 - q);
 #pragma unroll
         for (int j = CW - 1; j >= 0; j--) {
@@ -870,30 +898,26 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
             s2 x, y, e;
             cstep(c, j, x, y, e);
             bstep(o, x, y);
-            if (j == 0) {
-              if (keep)
-                bpre = o;
-              else
-                ck_put(q, o);
-            }
+            if (j == 0) ck_put(q, o);
             nrm_k(o, (j & 1) == 0);
           }
         }
       };
       ld_chunk(c2, max(qt - 2, qm), false);
-      bwd_chunk(c0, qt, L - CW * qt, false);
+      bwd_chunk(c0, qt, L - CW * qt);
       // then full chunks q, q-1, q-2 in c1, c2, c0 (rotating), down to qm; loads two ahead
       int q = qt - 1;
       for (; q - 2 >= qm; q -= 3) {
         ld_chunk(c0, q - 2, false);
-        bwd_chunk(c1, q, CW, false);
+        bwd_chunk(c1, q, CW);
         ld_chunk(c1, max(q - 3, qm), false);
-        bwd_chunk(c2, q - 1, CW, false);
+        bwd_chunk(c2, q - 1, CW);
         ld_chunk(c2, max(q - 4, qm), false);
-        bwd_chunk(c0, q - 2, CW, q - 2 == qm);
+        bwd_chunk(c0, q - 2, CW);
       }
-      if (q >= qm) bwd_chunk(c1, q, CW, q == qm);
-      if (q - 1 >= qm) bwd_chunk(c2, q - 1, CW, q - 1 == qm);
+      if (q >= qm) bwd_chunk(c1, q, CW);
+      if (q - 1 >= qm) bwd_chunk(c2, q - 1, CW);
+      ck_get(qm, bpre); // beta[M] before normalisation
     }
     Chunk<MODE> cur, cnx;
     ld_chunk(cur, qm - 1, true); // phase 2's first chunk, loading across the barrier
@@ -901,6 +925,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     __syncthreads();
     vm_drain();
     TD_T(3);
+#ifdef TD_EXP_P1ONLY
+    if (K > 0) return; // timing experiment only: prepass and phase 1
+#endif
     // phase 2: chunks qm-1 .. 0 (full), one per loop iteration: the beta recursion continues,
     // alphas restart from the forward wave's checkpoints
     {
@@ -935,6 +962,23 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
       }
     }
   }
+}
+
+// the wave's buffer resources (WinRes): bases at the wave's first pair pw, lane offset of `pair`
+template <int NB>
+__device__ __forceinline__ WinRes win_res(const TdGroup &G, int K, int blk, int pair, const s4 *SP0,
+                                          s2 *XP1, s2 *Aarr, size_t plane, const uint16_t *tb) {
+  const int pe = t4_pair_elems(K, NB);
+  const int pw = (blk * 64) / NB;
+  const size_t wb = (size_t)G.elem0 + (size_t)pw * pe;
+  WinRes R;
+  R.sp0 = mk_rsrc(SP0 + wb);
+  R.x2 = mk_rsrc(XP1 + wb);
+  R.p1 = mk_rsrc(XP1 + plane + wb);
+  R.a = mk_rsrc(Aarr + wb);
+  R.tb = mk_rsrc(tb);
+  R.po = (uint32_t)((pair - pw) * pe) * 4u;
+  return R;
 }
 
 template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
@@ -978,8 +1022,8 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
   s2 *A = Aarr + base;
   uint32_t *D = DOUT ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
   const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
-  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  win_bidir_body<NB, DIV, MODE, DOUT, B8>(sp0, xp1, p1, A, D, tl, tbl, cks, K, d, role, lane);
+  const WinRes R = win_res<NB>(G, K, blk, pair, SP0, XP1, Aarr, plane, MODE == 1 ? G.fwd : G.rev);
+  win_bidir_body<NB, DIV, MODE, DOUT, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
   TD_T(4);
 }
 
@@ -1016,6 +1060,12 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
   s2 *A_ = Aarr + base;
   uint32_t *D_ = Darr + G.dw0 + (size_t)pair * dec_words(K_, NB);
   const s2 *tl_ = T + (size_t)(G.pair0 + pair) * 12;
+  const int pe = t4_pair_elems(K_, NB), pw = (blk * 64) / NB;
+  const size_t wb = (size_t)G.elem0 + (size_t)pw * pe;
+  const s4 *wsp0_ = SP0 + wb;
+  s2 *wx2_ = XP1 + wb, *wa_ = Aarr + wb;
+  const s2 *wp1_ = XP1 + plane + wb;
+  const uint32_t po_ = (uint32_t)((pair - pw) * pe) * 4u;
   const uint16_t *fwd0 = G.fwd, *rev0 = G.rev;
   for (int n = n0; n < n0 + nh; n++) {
     const bool dec = dout && n + 1 == n0 + nh;
@@ -1034,24 +1084,35 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
     gmut_t<uint32_t> gD = gmut<uint32_t>(D_);
     gptr_t<uint16_t> fwd = gptr(fwd0), rev = gptr(rev0);
     int K = K_, d = d_, lane = lane_;
-    asm volatile("" : "+v"(gsp0), "+v"(gxp1), "+v"(gA), "+v"(gp1), "+v"(gtl), "+v"(gD), "+v"(d), "+v"(lane));
-    asm volatile("" : "+s"(fwd), "+s"(rev), "+s"(K));
+    uint32_t po = po_;
+    gptr_t<s4> wsp0 = gptr(wsp0_);
+    gptr_t<s2> wp1 = gptr(wp1_);
+    gmut_t<s2> wx2 = gmut<s2>(wx2_), wa = gmut<s2>(wa_);
+    asm volatile("" : "+v"(gsp0), "+v"(gxp1), "+v"(gA), "+v"(gp1), "+v"(gtl), "+v"(gD), "+v"(d), "+v"(lane), "+v"(po));
+    asm volatile("" : "+s"(fwd), "+s"(rev), "+s"(K), "+s"(wsp0), "+s"(wp1), "+s"(wx2), "+s"(wa));
+    WinRes R;
+    R.sp0 = mk_rsrc((const void *)wsp0);
+    R.x2 = mk_rsrc((const void *)wx2);
+    R.p1 = mk_rsrc((const void *)wp1);
+    R.a = mk_rsrc((const void *)wa);
+    R.tb = mk_rsrc((const void *)((n & 1) ? fwd : rev));
+    R.po = po;
     const s4 *sp0 = (const s4 *)gsp0;
     s2 *xp1 = (s2 *)gxp1, *A = (s2 *)gA;
     const s2 *p1 = (const s2 *)gp1, *tl = (const s2 *)gtl;
     uint32_t *D = (uint32_t *)gD;
     if (n & 1) {
       if (dec)
-        win_bidir_body<NB, DIV, 1, true, B8>(sp0, xp1, p1, A, D, tl, fwd, cks, K, d, role, lane);
+        win_bidir_body<NB, DIV, 1, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
       else
-        win_bidir_body<NB, DIV, 1, false, B8>(sp0, xp1, p1, A, D, tl, fwd, cks, K, d, role, lane);
+        win_bidir_body<NB, DIV, 1, false, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
     } else if (n == 0) {
-      win_bidir_body<NB, DIV, 2, false, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+      win_bidir_body<NB, DIV, 2, false, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
     } else {
       if (dec)
-        win_bidir_body<NB, DIV, 0, true, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+        win_bidir_body<NB, DIV, 0, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
       else
-        win_bidir_body<NB, DIV, 0, false, B8>(sp0, xp1, p1, A, D, tl, rev, cks, K, d, role, lane);
+        win_bidir_body<NB, DIV, 0, false, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
     }
   }
 }

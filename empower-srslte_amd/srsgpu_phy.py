@@ -205,6 +205,7 @@ _sig = {
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
     "srsgpu_chest_estimate_meas_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp, _vp]),
     "srsgpu_chest_set_cfg": (_i32, [_vp, _vp]),
+    "srsgpu_chest_get_cfg": (_i32, [_vp, _vp]),
     "srsgpu_symbol_sz": (_i32, [_u32, _i32]),
     "srsgpu_ofdm_rx_create": (_i32, [ctypes.POINTER(_vp), _u32, _u32]),
     "srsgpu_ofdm_rx_destroy": (None, [_vp]),
@@ -767,6 +768,14 @@ class RxQueue:
             it.data[t] = d.ctypes.data
         it.reset_softbuffer[0], it.reset_softbuffer[1] = reset
         return it
+
+    def set_chest_cfg(self, average_subframe=False, noise_alg=0, smooth_filter_auto=False,
+                      symbol_sz=None):
+        """the queue estimator's settings (srsgpu_chest_set_cfg on srsgpu_rxq_get_chest)"""
+        c = srsgpu_chest_cfg_t(int(average_subframe), noise_alg, int(smooth_filter_auto), 0, 0, 0,
+                               symbol_sz or symbol_sz_of(self.cell.nof_prb))
+        if _lib.srsgpu_chest_set_cfg(_lib.srsgpu_rxq_get_chest(self.q), ctypes.byref(c)) != 0:
+            raise RuntimeError("invalid chest configuration")
 
     def decode(self, it):
         return _lib.srsgpu_rxq_decode(self.q, ctypes.byref(it))

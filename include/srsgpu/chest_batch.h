@@ -47,6 +47,8 @@ typedef struct {
   uint32_t symbol_sz;          /* FFT size for the CFO formula (srslte_symbol_sz(nof_prb)) */
 } srsgpu_chest_cfg_t;
 int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg);
+/* the current settings (as set_cfg left them) */
+int srsgpu_chest_get_cfg(const srsgpu_chest_t *q, srsgpu_chest_cfg_t *cfg);
 
 /* Estimate nof_grids grids: grid i (subframe index sf_idx[i], host array) at d_grid + i*stride
  * complex elements. For every CRS port p of the cell (srslte_chest_dl_estimate_multi order), the

@@ -47,6 +47,13 @@ typedef enum {
 } srslte_tdec_impl_type_t;
 #endif
 
+/* sizeof(srslte_tdec_t) in the reference (turbodecoder.h:68-100, LP64: 4 x 188 interleaver
+ * structs plus pointers). srslte_sch_t embeds the decoder by value (sch.h:74), so objects built
+ * against the reference's sch.h stay layout-compatible only if this struct has the same size and
+ * alignment: the bookkeeping fields and the engine handle come first, the rest is padding.
+ * tests/test_capi.py compares both sizes with the reference header. */
+#define SRSLTE_TDEC_REF_SIZEOF 18264
+
 typedef struct {
   uint32_t max_long_cb;
   srslte_tdec_impl_type_t dec_type;
@@ -55,7 +62,11 @@ typedef struct {
   int current_cbidx;
   int n_iter;
   void *gpu; /* engine state (device buffers, stream), owned by the library */
+  uint8_t reserved[SRSLTE_TDEC_REF_SIZEOF - 4 * sizeof(uint32_t) - 2 * sizeof(int) - sizeof(void *)];
 } srslte_tdec_t;
+
+/* compile-time size check (C99 and C++): a negative array size if the layout drifts */
+typedef char srslte_tdec_size_check_t[(sizeof(void *) != 8 || sizeof(srslte_tdec_t) == SRSLTE_TDEC_REF_SIZEOF) ? 1 : -1];
 
 /* turbodecoder.h:102-107 */
 int srslte_tdec_init(srslte_tdec_t *h, uint32_t max_long_cb);

@@ -17,8 +17,8 @@
  *   srslte_softbuffer_rx_init / _free / _reset / _reset_tbs / _reset_cb  (softbuffer.c:46-153):
  *                                        the reference's host work, plus the GPU softbuffer state
  *   srsgpu_shim_release(q)               called from srslte_ofdm_rx_free / srslte_chest_dl_free /
- *                                        srslte_pdsch_free / srslte_sch_free (one added line each,
- *                                        INTEGRATION.md)
+ *                                        srslte_pdsch_free / srslte_sch_free / srslte_pcfich_free
+ *                                        (one added line each)
  *
  * Build it with -DSRSGPU_SHIM and drop the replaced functions from their reference translation
  * units. The reference objects keep their own state. This file keeps one GPU handle per object in
@@ -26,8 +26,10 @@
  * field. The registry is shared by srsUE's PHY worker threads (phch_worker.cc, one ue_dl per
  * worker): lookups and claims hold a mutex; a registered object is only used by the thread that
  * owns the object, as in the reference. Calls that are out of the GPU path's scope (MBSFN,
- * extended CP, transmit diversity, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a
- * message. There is no hidden CPU path behind them.
+ * extended CP, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a message. There is no
+ * hidden CPU path behind them. Every device allocation and copy is checked: a failure returns
+ * SRSLTE_ERROR (srslte_ofdm_rx_sf, void in the reference, prints and returns) and leaves the
+ * object's GPU state released, so the next call starts afresh.
  * Each call moves one subframe host -> device -> host, as the reference API is per subframe.
  * Batch users call include/srsgpu/ headers directly and keep the data in HBM.
  */
@@ -55,12 +57,34 @@
 
 /* ---- HIP runtime entry points used for the host <-> device staging (libamdhip64) ---- */
 typedef int hipError_t;
+typedef void *hipStream_t;
 extern hipError_t hipMalloc(void **ptr, size_t size);
 extern hipError_t hipFree(void *ptr);
 extern hipError_t hipMemcpy(void *dst, const void *src, size_t n, int kind);
-extern hipError_t hipDeviceSynchronize(void);
+extern hipError_t hipMemcpyAsync(void *dst, const void *src, size_t n, int kind, hipStream_t st);
+extern hipError_t hipStreamCreate(hipStream_t *st);
+extern hipError_t hipStreamDestroy(hipStream_t st);
+extern hipError_t hipStreamSynchronize(hipStream_t st);
 #define H2D 1
 #define D2H 2
+
+/* checked device allocation and copies: a failure prints and returns nonzero */
+static int shim_alloc(void *p, size_t n) {
+  void **pp = (void **)p;
+  if (hipMalloc(pp, n ? n : 1) != 0) {
+    *pp = NULL;
+    fprintf(stderr, "srsgpu shim: hipMalloc of %zu bytes failed\n", n);
+    return -1;
+  }
+  return 0;
+}
+static int shim_copy(void *dst, const void *src, size_t n, int kind) {
+  if (n && hipMemcpy(dst, src, n, kind) != 0) {
+    fprintf(stderr, "srsgpu shim: hipMemcpy of %zu bytes failed\n", n);
+    return -1;
+  }
+  return 0;
+}
 
 /* ---- object registry ---- */
 #define SHIM_MAX 64
@@ -77,12 +101,20 @@ typedef struct {
 static shim_entry_t shim[SHIM_MAX];
 static pthread_mutex_t shim_mutex = PTHREAD_MUTEX_INITIALIZER;
 
+static void shim_reset(shim_entry_t *e);
+
 /* the entry of `owner`, claiming a free one if there is none */
 static shim_entry_t *shim_get(const void *owner, shim_kind_t kind) {
   shim_entry_t *e = NULL;
   pthread_mutex_lock(&shim_mutex);
   for (int i = 0; i < SHIM_MAX && !e; i++)
     if (shim[i].owner == owner) e = &shim[i];
+  if (e && e->kind != kind) {
+    /* a freed object of another type whose free function has no release hook, and a new one at
+     * the same address: drop the old type's GPU state with the old type's destructor */
+    shim_reset(e);
+    e->kind = kind;
+  }
   for (int i = 0; i < SHIM_MAX && !e; i++)
     if (!shim[i].owner) {
       memset(&shim[i], 0, sizeof(shim[i]));
@@ -149,19 +181,23 @@ void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
   const uint32_t nof_prb = q->nof_re / SRSLTE_NRE;
   shim_entry_t *e = shim_get(q, SHIM_OFDM);
   if (!e) return;
+  const size_t nout = SRSLTE_SF_LEN_RE(nof_prb, q->cp);
   if (e->aux != q->symbol_sz || e->nof_prb != nof_prb || !e->gpu) {
     shim_reset(e);
-    if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz)) return;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * q->sf_sz);
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp));
+    if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz) ||
+        shim_alloc(&e->d_a, sizeof(cf_t) * q->sf_sz) || shim_alloc(&e->d_b, sizeof(cf_t) * nout)) {
+      shim_reset(e);
+      fprintf(stderr, "srsgpu shim: srslte_ofdm_rx_sf: GPU setup failed\n");
+      return;
+    }
     e->aux = q->symbol_sz;
     e->nof_prb = nof_prb;
   }
   srsgpu_ofdm_rx_set_normalize((srsgpu_ofdm_t *)e->gpu, q->fft_plan.norm);
-  hipMemcpy(e->d_a, q->in_buffer, sizeof(cf_t) * q->sf_sz, H2D);
-  srsgpu_ofdm_rx_sf_dev((srsgpu_ofdm_t *)e->gpu, 1, e->d_a, q->sf_sz, e->d_b,
-                        SRSLTE_SF_LEN_RE(nof_prb, q->cp));
-  hipMemcpy(q->out_buffer, e->d_b, sizeof(cf_t) * SRSLTE_SF_LEN_RE(nof_prb, q->cp), D2H);
+  if (shim_copy(e->d_a, q->in_buffer, sizeof(cf_t) * q->sf_sz, H2D) ||
+      srsgpu_ofdm_rx_sf_dev((srsgpu_ofdm_t *)e->gpu, 1, e->d_a, q->sf_sz, e->d_b, nout) ||
+      shim_copy(q->out_buffer, e->d_b, sizeof(cf_t) * nout, D2H))
+    fprintf(stderr, "srsgpu shim: srslte_ofdm_rx_sf failed\n");
 }
 
 /* ------------------------------------------------------------------ PCFICH ---- */
@@ -182,25 +218,26 @@ int srslte_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_P
   if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np * 4 + nrx || !e->gpu) {
     shim_reset(e);
     srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, nrx};
-    if (srsgpu_pcfich_create((srsgpu_pcfich_t **)&e->gpu, &c)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
-    hipMalloc((void **)&e->d_c, sizeof(float) * 2); /* cfi, correlation */
+    if (srsgpu_pcfich_create((srsgpu_pcfich_t **)&e->gpu, &c) || shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) ||
+        shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) || shim_alloc(&e->d_c, sizeof(float) * 2)) { /* cfi, corr */
+      shim_reset(e);
+      return SRSLTE_ERROR;
+    }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
     e->aux = np * 4 + nrx;
   }
   for (uint32_t a = 0; a < nrx; a++) {
-    hipMemcpy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D);
+    if (shim_copy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
     for (uint32_t p = 0; p < np; p++) /* reference ce[port][rx]; GPU planes [rx][port] */
-      hipMemcpy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D);
+      if (shim_copy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
   }
   const srsgpu_pcfich_sf_t sf = {0, 0, nsubframe, noise_estimate};
   if (srsgpu_pcfich_decode_dev((srsgpu_pcfich_t *)e->gpu, &sf, 1, e->d_a, e->d_b, n,
                                (uint32_t *)e->d_c, e->d_c + 1, NULL))
     return SRSLTE_ERROR;
   uint32_t out[2];
-  hipMemcpy(out, e->d_c, sizeof(out), D2H);
+  if (shim_copy(out, e->d_c, sizeof(out), D2H)) return SRSLTE_ERROR;
   if (cfi) *cfi = out[0];
   if (corr_result) memcpy(corr_result, &out[1], sizeof(float));
   return 1;
@@ -237,10 +274,12 @@ int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_
   if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
     shim_reset(e);
     srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, 1};
-    if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 2)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
-    hipMalloc((void **)&e->d_c, sizeof(float) * 4 * 5); /* noise [4] + measurements [4][4] */
+    if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 2) || shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) ||
+        shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) ||
+        shim_alloc(&e->d_c, sizeof(float) * 4 * 5)) { /* noise [4] + measurements [4][4] */
+      shim_reset(e);
+      return SRSLTE_ERROR;
+    }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
     e->aux = np;
@@ -264,17 +303,20 @@ int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_
       m[2] = q->rsrp_corr[a][p];
       m[3] = q->cfo;
     }
-  hipMemcpy(e->d_c, st, sizeof(st), H2D);
+  if (shim_copy(e->d_c, st, sizeof(st), H2D)) return SRSLTE_ERROR;
   uint32_t sfs[2] = {sf_idx, sf_idx};
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
-    hipMemcpy(e->d_a + 2 * (size_t)a * n, input[a], sizeof(cf_t) * n, H2D);
+    if (shim_copy(e->d_a + 2 * (size_t)a * n, input[a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
   if (srsgpu_chest_estimate_meas_dev(g, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c, e->d_c + 4))
     return SRSLTE_ERROR;
-  hipMemcpy(st, e->d_c, sizeof(st), D2H);
+  if (shim_copy(st, e->d_c, sizeof(st), D2H)) return SRSLTE_ERROR;
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
-    for (uint32_t p = 0; p < np; p++) { /* GPU order [rx][port]; reference ce[port][rx] */
+    for (uint32_t p = 0; p < np; p++) /* GPU order [rx][port]; reference ce[port][rx] */
+      if (shim_copy(ce[p][a], e->d_b + 2 * (size_t)(a * np + p) * n, sizeof(cf_t) * n, D2H))
+        return SRSLTE_ERROR;
+  for (uint32_t a = 0; a < nof_rx_antennas; a++)
+    for (uint32_t p = 0; p < np; p++) {
       const float *m = &st[4 + 4 * (a * np + p)];
-      hipMemcpy(ce[p][a], e->d_b + 2 * (size_t)(a * np + p) * n, sizeof(cf_t) * n, D2H);
       q->noise_estimate[a][p] = st[a * np + p];
       q->rsrp[a][p] = m[0];
       q->rssi[a][p] = m[1];
@@ -406,6 +448,13 @@ static void shim_mirror_crc(srsgpu_dlsch_t *dl, uint32_t slot, srslte_softbuffer
 }
 
 /* ------------------------------------------------------------------ DL-SCH ---- */
+/* The GPU DL-SCH object of a srslte_sch_t is created once, with a softbuffer pool sized for the
+ * largest cell (every softbuffer's max_cb fits: softbuffer.c:56 sizes it from the cell's PRBs), so
+ * the soft bits of every HARQ process survive any grant. Only the staging buffers grow. */
+static uint32_t shim_sch_max_cb(void) {
+  return (uint32_t)srslte_ra_tbs_from_idx(26, SRSLTE_MAX_PRB) / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1;
+}
+
 /* srslte_dlsch_decode2 (sch.c:506-517 -> decode_tb :430-497): one transport block from host
  * LLRs; sets q->nof_iterations (srslte_sch_last_noi) and the softbuffer's cb_crc / tb_crc */
 int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
@@ -416,17 +465,35 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
   const uint32_t tbs = cfg->cb_segm[tb_idx].tbs, nof_e = cfg->nbits[tb_idx].nof_bits;
   shim_entry_t *e = shim_get(q, SHIM_SCH);
   if (!e) return SRSLTE_ERROR;
-  const size_t dlen = SRSGPU_DLSCH_DATA_LEN(75376) + 16;
-  if (!e->gpu || e->nof_prb < softbuffer->max_cb || e->aux < nof_e) {
-    const uint32_t max_cb = e->nof_prb > softbuffer->max_cb ? e->nof_prb : softbuffer->max_cb;
-    const uint32_t cap = e->aux > nof_e ? e->aux : nof_e;
-    shim_reset(e);
-    if (srsgpu_dlsch_create((srsgpu_dlsch_t **)&e->gpu, SHIM_MAX, max_cb, max_cb)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(int16_t) * (cap ? cap : 1));
-    hipMalloc((void **)&e->d_b, dlen);
-    hipMalloc((void **)&e->d_c, 2 * sizeof(int32_t));
+  if (!e->gpu) {
+    const uint32_t max_cb = shim_sch_max_cb();
+    if (srsgpu_dlsch_create((srsgpu_dlsch_t **)&e->gpu, SHIM_MAX, max_cb, max_cb) ||
+        shim_alloc(&e->d_c, 2 * sizeof(int32_t))) {
+      shim_reset(e);
+      return SRSLTE_ERROR;
+    }
     e->nof_prb = max_cb; /* SCH entries: the pool's code blocks per softbuffer */
-    e->aux = cap;
+  }
+  if (softbuffer->max_cb > e->nof_prb) {
+    fprintf(stderr, "srsgpu shim: softbuffer with %u code blocks, the GPU pool holds %u\n",
+            softbuffer->max_cb, e->nof_prb);
+    return SRSLTE_ERROR;
+  }
+  /* staging: e-bits (d_a, capacity aux) and TB bytes (d_b, capacity cell_id) grow on demand */
+  if (e->aux < nof_e || !e->d_a) {
+    if (e->d_a) hipFree(e->d_a);
+    e->d_a = NULL;
+    e->aux = 0;
+    if (shim_alloc(&e->d_a, sizeof(int16_t) * nof_e)) return SRSLTE_ERROR;
+    e->aux = nof_e;
+  }
+  const uint32_t dlen = SRSGPU_DLSCH_DATA_LEN(tbs) + 16;
+  if (e->cell_id < dlen || !e->d_b) {
+    if (e->d_b) hipFree(e->d_b);
+    e->d_b = NULL;
+    e->cell_id = 0;
+    if (shim_alloc(&e->d_b, dlen)) return SRSLTE_ERROR;
+    e->cell_id = dlen;
   }
   srsgpu_dlsch_t *dl = (srsgpu_dlsch_t *)e->gpu;
   const int slot = shim_softbuffer(e, dl, softbuffer);
@@ -438,10 +505,11 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
     int16_t *w = malloc(sizeof(int16_t) * (nof_e ? nof_e : 1));
     if (!w) return SRSLTE_ERROR;
     for (uint32_t i = 0; i < nof_e; i++) w[i] = ((const int8_t *)e_bits)[i];
-    hipMemcpy(e->d_a, w, sizeof(int16_t) * nof_e, H2D);
+    const int r = shim_copy(e->d_a, w, sizeof(int16_t) * nof_e, H2D);
     free(w);
-  } else {
-    hipMemcpy(e->d_a, e_bits, sizeof(int16_t) * nof_e, H2D);
+    if (r) return SRSLTE_ERROR;
+  } else if (shim_copy(e->d_a, e_bits, sizeof(int16_t) * nof_e, H2D)) {
+    return SRSLTE_ERROR;
   }
   int32_t *d_ret = (int32_t *)e->d_c;
   uint32_t *d_noi = (uint32_t *)e->d_c + 1;
@@ -449,9 +517,10 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
                               d_ret, d_noi))
     return SRSLTE_ERROR;
   int32_t rn[2];
-  hipMemcpy(rn, e->d_c, sizeof(rn), D2H);
+  if (shim_copy(rn, e->d_c, sizeof(rn), D2H)) return SRSLTE_ERROR;
   if (rn[0] != SRSLTE_ERROR_INVALID_INPUTS) {
-    hipMemcpy(data, e->d_b, tbs / 8 + 3, D2H); /* the TB and its CRC bytes (sch.c:466-468) */
+    /* the TB and its CRC bytes (sch.c:466-468) */
+    if (shim_copy(data, e->d_b, tbs / 8 + 3, D2H)) return SRSLTE_ERROR;
     q->nof_iterations = (uint32_t)rn[1];
     shim_mirror_crc(dl, (uint32_t)slot, softbuffer, cfg->cb_segm[tb_idx].C);
   }
@@ -459,13 +528,61 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
 }
 
 /* srslte_rm_turbo_rx_lut (rm_turbo.c:378-381, :394-430): output[deinter[i % (3K+12)]] += input[i]
- * on host buffers, with the sub-block layout the AUTO decoder expects. One process-wide GPU
- * context; latency-bound by nature (one code block per call). */
-static struct {
+ * on host buffers, with the sub-block layout the AUTO decoder expects. Latency-bound by nature
+ * (one code block per call). Every calling thread (srsUE's PHY workers) has a context of its own:
+ * a GPU DL-SCH object, staging buffers and a stream, so workers do not serialise on one another;
+ * the context is freed when the thread exits. */
+typedef struct {
   srsgpu_dlsch_t *dl;
   int16_t *d_in, *d_out;
   uint32_t cap;
-} shim_rm;
+  hipStream_t st;
+} shim_rm_t;
+static pthread_key_t shim_rm_key;
+static pthread_once_t shim_rm_once = PTHREAD_ONCE_INIT;
+static void shim_rm_free(void *p) {
+  shim_rm_t *c = (shim_rm_t *)p;
+  if (!c) return;
+  if (c->dl) srsgpu_dlsch_destroy(c->dl);
+  if (c->d_in) hipFree(c->d_in);
+  if (c->d_out) hipFree(c->d_out);
+  if (c->st) hipStreamDestroy(c->st);
+  free(c);
+}
+static void shim_rm_key_init(void) { (void)pthread_key_create(&shim_rm_key, shim_rm_free); }
+
+/* this thread's context with room for in_len input elements, or NULL */
+static shim_rm_t *shim_rm_ctx(uint32_t in_len) {
+  (void)pthread_once(&shim_rm_once, shim_rm_key_init);
+  shim_rm_t *c = (shim_rm_t *)pthread_getspecific(shim_rm_key);
+  if (!c) {
+    c = (shim_rm_t *)calloc(1, sizeof(*c));
+    if (!c) return NULL;
+    if (hipStreamCreate(&c->st) != 0 || srsgpu_dlsch_create(&c->dl, 1, 1, 1) ||
+        shim_alloc(&c->d_out, sizeof(int16_t) * (3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 12)) ||
+        pthread_setspecific(shim_rm_key, c) != 0) {
+      shim_rm_free(c);
+      fprintf(stderr, "srsgpu shim: rate-dematching context setup failed\n");
+      return NULL;
+    }
+    srsgpu_dlsch_set_stream(c->dl, c->st);
+  }
+  if (in_len > c->cap) {
+    if (c->d_in) hipFree(c->d_in);
+    c->d_in = NULL;
+    c->cap = 0;
+    if (shim_alloc(&c->d_in, sizeof(int16_t) * in_len)) return NULL;
+    c->cap = in_len;
+  }
+  return c;
+}
+static int shim_copy_on(shim_rm_t *c, void *dst, const void *src, size_t n, int kind) {
+  if (n && hipMemcpyAsync(dst, src, n, kind, c->st) != 0) {
+    fprintf(stderr, "srsgpu shim: hipMemcpyAsync of %zu bytes failed\n", n);
+    return -1;
+  }
+  return 0;
+}
 
 int srslte_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx) {
   if (rv_idx >= 4 || cb_idx >= SRSLTE_NOF_TC_CB_SIZES || !input || !output) {
@@ -473,24 +590,13 @@ int srslte_rm_turbo_rx_lut(int16_t *input, int16_t *output, uint32_t in_len, uin
     return SRSLTE_ERROR_INVALID_INPUTS;
   }
   const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cb_idx), out_len = 3 * K + 12;
-  int ret = SRSLTE_ERROR;
-  pthread_mutex_lock(&shim_mutex);
-  if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
-  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * (3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 12));
-  if (in_len > shim_rm.cap) {
-    if (shim_rm.d_in) hipFree(shim_rm.d_in);
-    hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
-    shim_rm.cap = in_len;
-  }
-  hipMemcpy(shim_rm.d_in, input, sizeof(int16_t) * in_len, H2D);
-  hipMemcpy(shim_rm.d_out, output, sizeof(int16_t) * out_len, H2D);
-  if (srsgpu_rm_turbo_rx_dev(shim_rm.dl, shim_rm.d_in, shim_rm.d_out, in_len, K, rv_idx, 1) == 0) {
-    hipMemcpy(output, shim_rm.d_out, sizeof(int16_t) * out_len, D2H);
-    ret = SRSLTE_SUCCESS;
-  }
-out:
-  pthread_mutex_unlock(&shim_mutex);
-  return ret;
+  shim_rm_t *c = shim_rm_ctx(in_len);
+  if (!c || shim_copy_on(c, c->d_in, input, sizeof(int16_t) * in_len, H2D) ||
+      shim_copy_on(c, c->d_out, output, sizeof(int16_t) * out_len, H2D) ||
+      srsgpu_rm_turbo_rx_dev(c->dl, c->d_in, c->d_out, in_len, K, rv_idx, 1) ||
+      shim_copy_on(c, output, c->d_out, sizeof(int16_t) * out_len, D2H) || hipStreamSynchronize(c->st) != 0)
+    return SRSLTE_ERROR;
+  return SRSLTE_SUCCESS;
 }
 
 /* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469): the same on int8 buffers (sums wrapping at 8
@@ -502,28 +608,21 @@ int srslte_rm_turbo_rx_lut_8bit(int8_t *input, int8_t *output, uint32_t in_len, 
     return SRSLTE_ERROR_INVALID_INPUTS;
   }
   const uint32_t K = (uint32_t)srslte_cbsegm_cbsize(cb_idx), out_len = 3 * (K + 32) + 12;
-  int16_t *w = malloc(sizeof(int16_t) * (in_len > out_len ? in_len : out_len));
+  shim_rm_t *c = shim_rm_ctx(in_len);
+  if (!c) return SRSLTE_ERROR;
+  int16_t *w = malloc(sizeof(int16_t) * (in_len + out_len));
   if (!w) return SRSLTE_ERROR;
-  int ret = SRSLTE_ERROR;
-  pthread_mutex_lock(&shim_mutex);
-  if (!shim_rm.dl && srsgpu_dlsch_create(&shim_rm.dl, 1, 1, 1)) goto out;
-  if (!shim_rm.d_out) hipMalloc((void **)&shim_rm.d_out, sizeof(int16_t) * (3 * (SRSLTE_TCOD_MAX_LEN_CB + 32) + 12));
-  if (in_len > shim_rm.cap) {
-    if (shim_rm.d_in) hipFree(shim_rm.d_in);
-    hipMalloc((void **)&shim_rm.d_in, sizeof(int16_t) * in_len);
-    shim_rm.cap = in_len;
-  }
+  int16_t *wo = w + in_len;
   for (uint32_t i = 0; i < in_len; i++) w[i] = input[i];
-  hipMemcpy(shim_rm.d_in, w, sizeof(int16_t) * in_len, H2D);
-  for (uint32_t i = 0; i < out_len; i++) w[i] = output[i];
-  hipMemcpy(shim_rm.d_out, w, sizeof(int16_t) * out_len, H2D);
-  if (srsgpu_rm_turbo_rx_8bit_dev(shim_rm.dl, shim_rm.d_in, shim_rm.d_out, in_len, K, rv_idx) == 0) {
-    hipMemcpy(w, shim_rm.d_out, sizeof(int16_t) * out_len, D2H);
-    for (uint32_t i = 0; i < out_len; i++) output[i] = (int8_t)w[i];
+  for (uint32_t i = 0; i < out_len; i++) wo[i] = output[i];
+  int ret = SRSLTE_ERROR;
+  if (!shim_copy_on(c, c->d_in, w, sizeof(int16_t) * in_len, H2D) &&
+      !shim_copy_on(c, c->d_out, wo, sizeof(int16_t) * out_len, H2D) &&
+      !srsgpu_rm_turbo_rx_8bit_dev(c->dl, c->d_in, c->d_out, in_len, K, rv_idx) &&
+      !shim_copy_on(c, wo, c->d_out, sizeof(int16_t) * out_len, D2H) && hipStreamSynchronize(c->st) == 0) {
+    for (uint32_t i = 0; i < out_len; i++) output[i] = (int8_t)wo[i];
     ret = SRSLTE_SUCCESS;
   }
-out:
-  pthread_mutex_unlock(&shim_mutex);
   free(w);
   return ret;
 }
@@ -559,11 +658,12 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     shim_reset(e);
     srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, q->nof_rx_antennas};
     const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
-    if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1)) return SRSLTE_ERROR;
-    hipMalloc((void **)&e->d_a, sizeof(cf_t) * n * 2);
-    hipMalloc((void **)&e->d_b, sizeof(cf_t) * n * 4);
-    hipMalloc((void **)&e->d_c, 2 * dlen);
-    hipMalloc((void **)&e->d_d, 4 * sizeof(int32_t));
+    if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1) ||
+        shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) || shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) ||
+        shim_alloc(&e->d_c, 2 * dlen) || shim_alloc(&e->d_d, 4 * sizeof(int32_t))) {
+      shim_reset(e);
+      return SRSLTE_ERROR;
+    }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
     e->aux = np;
@@ -596,9 +696,10 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     sf.data_offset[t] = t * dlen;
   }
   for (uint32_t a = 0; a < q->nof_rx_antennas; a++) {
-    hipMemcpy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D);
+    if (shim_copy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
     for (uint32_t p = 0; p < np; p++) /* reference ce[port][rx] -> GPU [rx][port] planes */
-      hipMemcpy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D);
+      if (shim_copy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * n, H2D))
+        return SRSLTE_ERROR;
   }
   srsgpu_pdsch_set_csi(g, q->csi_enabled);
   srsgpu_pdsch_set_llr_8bit(g, q->llr_is_8bit); /* pdsch.c:795-806 */
@@ -609,12 +710,12 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     return SRSLTE_ERROR; /* RE count mismatch: pdsch.c:886-890 */
   int32_t ret[2] = {-1, -1};
   uint32_t noi[2] = {0, 0};
-  hipMemcpy(ret, d_ret, sizeof(int32_t) * nof_tb, D2H);
-  hipMemcpy(noi, d_noi, sizeof(uint32_t) * nof_tb, D2H);
+  if (shim_copy(ret, d_ret, sizeof(int32_t) * nof_tb, D2H) || shim_copy(noi, d_noi, sizeof(uint32_t) * nof_tb, D2H))
+    return SRSLTE_ERROR;
   for (uint32_t t = 0; t < nof_tb; t++) {
     if (acks[t]) continue; /* already acked: the reference does not touch it */
     srslte_softbuffer_rx_t *sb = softbuffers[t];
-    hipMemcpy(data[t], (uint8_t *)e->d_c + t * dlen, (size_t)sf.tbs[t] / 8, D2H);
+    if (shim_copy(data[t], (uint8_t *)e->d_c + t * dlen, (size_t)sf.tbs[t] / 8, D2H)) return SRSLTE_ERROR;
     /* last_nof_iterations is indexed by codeword (pdsch.c:815) */
     const uint32_t cw = cdd ? (t ^ sf.tb_cw_swap) : 0;
     q->last_nof_iterations[cw] = noi[t];

@@ -62,3 +62,31 @@ def test_product_encoder_matches_oracle(oracle):
     bits = rng.integers(0, 2, 104, dtype=np.uint8)
     bits[:8] = s.SRSLTE_TX_NULL if hasattr(s, "SRSLTE_TX_NULL") else 100
     assert enc.encode(bits)[1] == 100  # filler bits propagate to systematic and parity 0
+
+
+def _sizeof(include_dirs, extra=""):
+    import subprocess
+    import tempfile
+    src = ("#include <stdio.h>\n#include <stddef.h>\n%s#include \"srslte/phy/fec/turbodecoder.h\"\n"
+           "int main(void){printf(\"%%zu %%zu\", sizeof(srslte_tdec_t), _Alignof(srslte_tdec_t));return 0;}\n"
+           % extra)
+    with tempfile.TemporaryDirectory() as t:
+        c, exe = os.path.join(t, "s.c"), os.path.join(t, "s")
+        open(c, "w").write(src)
+        args = ["gcc", "-std=gnu11", "-D_GNU_SOURCE"] + ["-I" + d for d in include_dirs] + [c, "-o", exe]
+        subprocess.run(args, check=True, capture_output=True)
+        return tuple(int(x) for x in subprocess.run([exe], check=True, capture_output=True,
+                                                    text=True).stdout.split())
+
+
+def test_tdec_struct_layout_matches_reference(tmp_path):
+    """srslte_tdec_t is embedded by value in srslte_sch_t (reference sch.h:74): the drop-in
+    header's struct must have the reference's size and alignment (turbodecoder.h:68-100)."""
+    import pytest
+    ref_inc = "/root/reference/lib/include"
+    if not os.path.isdir(ref_inc):
+        pytest.skip("reference headers absent (GPU box)")
+    # the reference header needs srslte/config.h only; its umbrella version.h is CMake-generated
+    ref = _sizeof([ref_inc])
+    ours = _sizeof([os.path.join(REPO, "include")])
+    assert ours == ref, (ours, ref)

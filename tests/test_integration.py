@@ -120,3 +120,21 @@ def test_shim_front_end_time_domain(case):
     assert float(stats["ofdm_err"]) < 1e-4 and float(stats["ce_err"]) < 0.2, r.stdout
     assert int(stats["recreated"]) == 1 and int(stats["live"]) == 0
     assert int(stats["acks"]) >= case[5]  # at least the high-SNR phase decodes
+
+
+FAULT = os.path.join(REPO, "oracle", "_ref", "shim_fault")
+
+
+@pytest.mark.gpu
+def test_shim_error_paths_and_harq_growth():
+    """oracle/_ref/shim_fault: every device allocation the shim makes is failed once in turn (the
+    drop-in must return SRSLTE_ERROR and work again on the next call), and one srslte_sch_t decodes
+    two HARQ processes whose grants differ in size, interleaved, exactly as the reference does
+    (the larger grant must not drop the other process's combined soft bits)."""
+    if not os.path.exists(FAULT):
+        pytest.skip("oracle/_ref/shim_fault not built (needs /root/reference at build time)")
+    r = subprocess.run([FAULT], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    stats = dict(kv.split("=") for kv in r.stdout.split())
+    assert int(stats["fault_cases"]) >= 8 and int(stats["fault_failures"]) == 0, r.stdout + r.stderr
+    assert int(stats["harq_tx"]) == 36 and int(stats["harq_mismatches"]) == 0, r.stdout + r.stderr

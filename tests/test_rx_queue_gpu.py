@@ -102,3 +102,56 @@ def test_worker_threads_through_the_queue(oracle):
     assert all(q.wait(t) == 0 for t in tickets)
     assert all(items[i].ret[0] == ret_d[i] for i in range(n))
     q.close()
+
+
+def test_empty_noise_carried_across_batches(oracle):
+    """EMPTY noise (srsUE's snr_estim_alg=empty, phch_worker.cc:557-564): only subframes 0 and 5
+    estimate the noise (chest_dl.c:628-637); every other subframe keeps the latest estimate of an
+    earlier subframe — across the queue's batch boundaries too, and 0 before any estimate
+    (srslte_chest_dl_init). The queue's per-subframe noise must follow that order exactly."""
+    import torch
+    import srsgpu_phy as s
+    po, dl = PdschOracle(oracle), DlschOracle(oracle)
+    rng = np.random.default_rng(5)
+    nof_prb, cell_id, tbs = 25, 11, 2216
+    N = s.symbol_sz(nof_prb, True)
+    order = [1, 2, 3, 0, 1, 4, 6, 5, 7, 8, 9, 1, 2, 0, 3]  # batches of 4 split the carries
+    xs, sfs = [], []
+    for sf_idx in order:
+        x, _, idx = build_subframe(po, dl, rng, nof_prb, cell_id, N, sf_idx, tbs, 1234, 12.0,
+                                   rng.uniform(0, 6.28))
+        xs.append(x)
+        sfs.append((sf_idx, idx.size))
+    # the estimates of the 0 / 5 subframes, from the direct chest with the same settings
+    n, gsz = len(xs), 14 * 12 * nof_prb
+    ofdm = s.OfdmRx(nof_prb, N)
+    chest = s.Chest(nof_prb, cell_id, max_grids=n)
+    chest.set_cfg(noise_alg=2)
+    d_x = torch.from_numpy(np.stack(xs).reshape(-1)).cuda()
+    d_grid = torch.zeros(n * gsz, dtype=torch.complex64, device="cuda")
+    d_ce = torch.zeros_like(d_grid)
+    d_noise = torch.full((n,), -1.0, dtype=torch.float32, device="cuda")
+    assert ofdm.rx_dev(n, d_x.data_ptr(), 15 * N, d_grid.data_ptr(), gsz) == 0
+    assert chest.estimate_dev(order, d_grid.data_ptr(), gsz, d_ce.data_ptr(), d_noise.data_ptr()) == 0
+    est = d_noise.cpu().numpy()
+    expect, last = [], 0.0
+    for i, sf_idx in enumerate(order):
+        if sf_idx in (0, 5):
+            assert est[i] > 0
+            last = float(est[i])
+        expect.append(last)
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=n, max_batch=4, max_wait_us=200000)
+    q.set_chest_cfg(noise_alg=2)
+    outs = [np.zeros(tbs // 8 + 6, np.uint8) for _ in range(n)]
+    items = [q.item([xs[i]], s.make_sf(sf_idx=sfs[i][0], lstart=1, nof_prb=nof_prb, mod=3,
+                                        nof_re=sfs[i][1], rnti=1234, tbs=tbs, softbuffer=i),
+                    [outs[i]]) for i in range(n)]
+    tickets = [q.submit(it) for it in items]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in tickets)
+    got = [it.noise for it in items]
+    assert np.allclose(got, expect, rtol=1e-6, atol=0), (got, expect)
+    batches, done = q.stats()
+    assert done == n and batches >= 4
+    for h in (q, chest, ofdm):
+        h.close()
