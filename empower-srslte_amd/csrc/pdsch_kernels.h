@@ -62,5 +62,16 @@ struct PcfichItem {
 hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, const float2 *ce,
                          size_t ant_stride, int nof_prb, int nports, int nrx, const uint32_t *idx,
                          const uint32_t *seq, uint32_t *cfi, float *corr, hipStream_t st);
+// PDCCH of one subframe (srslte_pdcch_extract_llr_multi)
+struct PdcchItem {
+  uint64_t grid_off, ce_off, llr_off; // [rx] grid planes / [rx][port] estimate planes / LLR out
+  const uint32_t *map;                // the CFI's REG symbols (srslte_regs_pdcch_get order)
+  const uint32_t *c;                  // the subframe's scrambling bits, packed LSB first
+  uint32_t nof_symbols;               // 36 NOF_CCE(cfi)
+  float noise;                        // the noise_estimate argument
+};
+hipError_t launch_pdcch_llr(const PdcchItem *d_items, int n, uint32_t max_symbols, const float2 *grid,
+                            const float2 *ce, size_t ant_stride, int nports, int nrx, float *llr,
+                            hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -614,4 +614,52 @@ hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, c
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ PDCCH LLRs ----
+// srslte_pdcch_extract_llr_multi (pdcch.c:424-506) for many subframes, one thread per PDCCH
+// symbol j (blockIdx.y = subframe): the symbol is gathered at map[j] from every rx antenna's grid
+// and estimate (srslte_regs_pdcch_get), equalised on the reference's path for nof_symbols symbols
+// (1 port: srslte_predecoding_single_multi with noise_estimate / 2 and scaling 1; 2 ports:
+// srslte_predecoding_diversity_multi + srslte_layerdemap_diversity), QPSK soft-demapped as float
+// (demod_qpsk_lte: x (float) -sqrt(2), demod_soft.c:75-77) and descrambled
+// (srslte_scrambling_f_offset: a product with +-1, scrambling.c:39-42).
+__global__ __launch_bounds__(256) void k_pdcch_llr(const PdcchItem *__restrict__ items, int n,
+                                                   const float2 *__restrict__ grid,
+                                                   const float2 *__restrict__ ce, size_t ant_stride,
+                                                   int nports, int nrx, float *__restrict__ llr) {
+  const int s = blockIdx.y;
+  if (s >= n) return;
+  const PdcchItem it = items[s];
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= it.nof_symbols) return;
+  LlrItem t;
+  memset(&t, 0, sizeof(t));
+  for (int a = 0; a < nrx; a++) {
+    t.y[a] = grid + it.grid_off + (size_t)a * ant_stride;
+    for (int p = 0; p < nports; p++) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
+  }
+  t.map = it.map;
+  t.nof_re = it.nof_symbols;
+  t.nrx = nrx;
+  t.noise = nports == 2 ? 0.f : it.noise / 2;
+  t.scaling = 1.0f;
+  t.inv_scaling = 1.0f;
+  const Eq e = nports == 2 ? equalise_txdiv(t, j) : equalise(t, it.map[j], j);
+  const float s2 = -1.41421354f; // (float) -sqrt(2)
+  float a0 = __fmul_rn(e.xr, s2), a1 = __fmul_rn(e.xi, s2);
+  const uint32_t b = 2 * j, w = it.c[b >> 5] >> (b & 31);
+  if (w & 1u) a0 = -a0;
+  if (w & 2u) a1 = -a1;
+  float2 *o = reinterpret_cast<float2 *>(llr + it.llr_off);
+  o[j] = make_float2(a0, a1);
+}
+
+hipError_t launch_pdcch_llr(const PdcchItem *d_items, int n, uint32_t max_symbols, const float2 *grid,
+                            const float2 *ce, size_t ant_stride, int nports, int nrx, float *llr,
+                            hipStream_t st) {
+  if (n <= 0 || max_symbols == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pdcch_llr, dim3((max_symbols + 255) / 256, n), dim3(256), 0, st, d_items, n, grid,
+                     ce, ant_stride, nports, nrx, llr);
+  return hipGetLastError();
+}
+
 } // namespace srsgpu

@@ -115,6 +115,68 @@ class srsgpu_pcfich_sf_t(ctypes.Structure):
                 ("sf_idx", ctypes.c_uint32), ("noise_estimate", ctypes.c_float)]
 
 
+class srsgpu_pdcch_sf_t(ctypes.Structure):
+    """include/srsgpu/pdcch_batch.h"""
+    _fields_ = [("grid_offset", ctypes.c_uint64), ("ce_offset", ctypes.c_uint64),
+                ("llr_offset", ctypes.c_uint64), ("sf_idx", ctypes.c_uint32), ("cfi", ctypes.c_uint32),
+                ("noise_estimate", ctypes.c_float), ("reserved", ctypes.c_uint32)]
+
+
+class srsgpu_dci_location_t(ctypes.Structure):
+    """include/srsgpu/pdcch_batch.h"""
+    _fields_ = [("L", ctypes.c_uint32), ("ncce", ctypes.c_uint32)]
+
+
+class srsgpu_dci_search_t(ctypes.Structure):
+    """include/srsgpu/pdcch_batch.h"""
+    _fields_ = [("llr_offset", ctypes.c_uint64), ("sf_idx", ctypes.c_uint32), ("cfi", ctypes.c_uint32),
+                ("rnti", ctypes.c_uint32), ("tm", ctypes.c_uint32), ("rnti_type", ctypes.c_int32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class srsgpu_dci_result_t(ctypes.Structure):
+    """include/srsgpu/pdcch_batch.h"""
+    _fields_ = [("found", ctypes.c_int32), ("format", ctypes.c_uint32), ("L", ctypes.c_uint32),
+                ("ncce", ctypes.c_uint32), ("nof_bits", ctypes.c_uint32), ("data", ctypes.c_uint8 * 128)]
+
+
+DCI_FORMAT0, DCI_FORMAT1, DCI_FORMAT1A, DCI_FORMAT1C, DCI_FORMAT1B, DCI_FORMAT1D = range(6)
+DCI_FORMAT2, DCI_FORMAT2A, DCI_FORMAT2B = 6, 7, 8
+
+
+class srsgpu_ra_dl_dci_t(ctypes.Structure):
+    """include/srsgpu/dci.h"""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("alloc_type", "rbg_bitmask", "vrb_bitmask", "rbg_subset",
+                                               "shift", "riv", "L_crb", "RB_start", "n_prb1a", "n_gap",
+                                               "mode", "harq_process", "mcs_idx")] + \
+        [("rv_idx", ctypes.c_int32), ("ndi", ctypes.c_uint32), ("mcs_idx_1", ctypes.c_uint32),
+         ("rv_idx_1", ctypes.c_int32)] + \
+        [(n, ctypes.c_uint32) for n in ("ndi_1", "tb_cw_swap", "sram_id", "pinfo", "pconf", "power_offset")] + \
+        [("tb_en", ctypes.c_uint32 * 2)] + \
+        [(n, ctypes.c_uint32) for n in ("is_ra_order", "ra_preamble", "ra_mask_idx", "dci_is_1a", "dci_is_1c")]
+    # the reference harness's 30-field order (oracle/ref_harness.c ref_dci_out)
+    ORDER = ("alloc_type", "rbg_bitmask", "vrb_bitmask", "rbg_subset", "shift", "riv", "L_crb", "RB_start",
+             "n_prb1a", "n_gap", "mode", "harq_process", "mcs_idx", "rv_idx", "ndi", "mcs_idx_1", "rv_idx_1",
+             "ndi_1", "tb_cw_swap", "sram_id", "pinfo", "pconf", "power_offset", "tb_en0", "tb_en1",
+             "is_ra_order", "ra_preamble", "ra_mask_idx", "dci_is_1a", "dci_is_1c")
+
+    def fields30(self):
+        return [self.tb_en[int(n[-1])] if n.startswith("tb_en") else getattr(self, n) for n in self.ORDER]
+
+
+class srsgpu_ra_dl_grant_t(ctypes.Structure):
+    """include/srsgpu/dci.h"""
+    _fields_ = [("prb_idx", (ctypes.c_uint8 * 110) * 2), ("nof_prb", ctypes.c_uint32),
+                ("Qm", ctypes.c_uint32 * 2), ("mod", ctypes.c_uint32 * 2), ("tbs", ctypes.c_int32 * 2),
+                ("mcs_idx", ctypes.c_uint32 * 2), ("tb_en", ctypes.c_uint32 * 2), ("pinfo", ctypes.c_uint32),
+                ("tb_cw_swap", ctypes.c_uint32)]
+
+    def fields13(self):
+        """the reference harness's 13-field order (oracle/ref_harness.c ref_dci_to_dl_grant)"""
+        return [self.nof_prb, self.Qm[0], self.Qm[1], self.mod[0], self.tbs[0], self.mcs_idx[0], self.mod[1],
+                self.tbs[1], self.mcs_idx[1], self.tb_en[0], self.tb_en[1], self.pinfo, self.tb_cw_swap]
+
+
 def dlsch_data_len(tbs):
     return tbs // 8 + 6
 
@@ -179,6 +241,25 @@ _sig = {
     "srsgpu_pcfich_re_map": (_i32, [_vp, _u32p]),
     "srsgpu_pcfich_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pcfich_sf_t), _u32, _vp, _vp, _sz,
                                         _vp, _vp, _vp]),
+    "srsgpu_pdcch_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32, _u32]),
+    "srsgpu_pdcch_destroy": (None, [_vp]),
+    "srsgpu_pdcch_cell_map": (_i32, [ctypes.POINTER(srsgpu_cell_t), _u32, _u32, _u32, _u32p, _u32, _u32p]),
+    "srsgpu_pdcch_nof_cce": (_u32, [_vp, _u32]),
+    "srsgpu_pdcch_re_map": (_i32, [_vp, _u32, _u32p, _u32]),
+    "srsgpu_pdcch_extract_llr_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdcch_sf_t), _u32, _vp, _vp, _sz, _vp,
+                                            _vp]),
+    "srsgpu_pdcch_ue_locations": (_u32, [_u32, _u32, ctypes.c_uint16, ctypes.POINTER(srsgpu_dci_location_t),
+                                         _u32]),
+    "srsgpu_pdcch_common_locations": (_u32, [_u32, ctypes.POINTER(srsgpu_dci_location_t), _u32]),
+    "srsgpu_pdcch_find_dl_dci_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dci_search_t), _u32, _vp, _vp, _vp]),
+    "srsgpu_dci_format_sizeof": (_u32, [_u32, _u32, _u32]),
+    "srsgpu_dci_msg_to_dl_grant": (_i32, [_u8p, _u32, _u32, ctypes.c_uint16, _u32, _u32,
+                                          ctypes.POINTER(srsgpu_ra_dl_dci_t),
+                                          ctypes.POINTER(srsgpu_ra_dl_grant_t)]),
+    "srsgpu_ra_dl_dci_to_grant": (_i32, [ctypes.POINTER(srsgpu_ra_dl_dci_t), _u32, ctypes.c_uint16,
+                                         ctypes.POINTER(srsgpu_ra_dl_grant_t)]),
+    "srsgpu_ra_tbs_from_idx": (_i32, [_u32, _u32]),
+    "srsgpu_ra_tbs_idx_from_mcs": (_i32, [_u32]),
     "srsgpu_rxq_create": (_i32, [ctypes.POINTER(_vp), _vp, _u32, _u32, _u32, _u32, _u32]),
     "srsgpu_rxq_destroy": (None, [_vp]),
     "srsgpu_rxq_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -539,6 +620,115 @@ class Pcfich:
     def __del__(self):
         if getattr(self, "q", None):
             _lib.srsgpu_pcfich_destroy(self.q)
+            self.q = None
+
+
+def pdcch_cell_map(nof_prb, cell_id, nof_ports, phich_length, phich_resources, cfi):
+    """srsgpu_pdcch_cell_map (host only): (grid indices of the PDCCH symbols in srslte_regs_pdcch_get
+    order, NOF_CCE(cfi)); None for an invalid cell"""
+    cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1)
+    ncce = ctypes.c_uint32(0)
+    n = _lib.srsgpu_pdcch_cell_map(ctypes.byref(cell), phich_length, phich_resources, cfi, None, 0,
+                                   ctypes.byref(ncce))
+    if n < 0:
+        return None
+    idx = np.zeros(max(n, 1), np.uint32)
+    assert _lib.srsgpu_pdcch_cell_map(ctypes.byref(cell), phich_length, phich_resources, cfi,
+                                      idx.ctypes.data_as(_u32p), n, None) == n
+    return idx[:n], ncce.value
+
+
+def pdcch_locations(nof_cce, sf_idx=0, rnti=0, common=False):
+    """srsgpu_pdcch_ue_locations / _common_locations: [(L, ncce)] in the reference's order"""
+    c = (srsgpu_dci_location_t * 64)()
+    n = (_lib.srsgpu_pdcch_common_locations(nof_cce, c, 64) if common
+         else _lib.srsgpu_pdcch_ue_locations(nof_cce, sf_idx, rnti, c, 64))
+    return [(c[i].L, c[i].ncce) for i in range(n)]
+
+
+def dci_format_sizeof(fmt, nof_prb, nof_ports):
+    return _lib.srsgpu_dci_format_sizeof(fmt, nof_prb, nof_ports)
+
+
+def dci_msg_to_dl_grant(bits, fmt, rnti, nof_prb, nof_ports, nof_bits=None):
+    """srsgpu_dci_msg_to_dl_grant of bits[:nof_bits] (default: all of bits), read from a zero-padded
+    128-byte message buffer: (ret, srsgpu_ra_dl_dci_t, srsgpu_ra_dl_grant_t)"""
+    b = np.zeros(128, np.uint8)
+    b[:len(bits)] = bits
+    nof_bits = len(bits) if nof_bits is None else nof_bits
+    d, g = srsgpu_ra_dl_dci_t(), srsgpu_ra_dl_grant_t()
+    r = _lib.srsgpu_dci_msg_to_dl_grant(b.ctypes.data_as(_u8p), nof_bits, fmt, rnti, nof_prb, nof_ports,
+                                        ctypes.byref(d), ctypes.byref(g))
+    return r, d, g
+
+
+class Pdcch:
+    """srsgpu_pdcch_t: batched srslte_pdcch_extract_llr_multi and the srslte_ue_dl_find_dl_dci blind
+    search on device grids laid out as Pdsch's (include/srsgpu/pdcch_batch.h)."""
+
+    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, phich_length=0, phich_resources=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+        self.q = _vp()
+        if _lib.srsgpu_pdcch_create(ctypes.byref(self.q), ctypes.byref(self.cell), phich_length,
+                                    phich_resources) != 0:
+            raise RuntimeError("srsgpu_pdcch_create failed")
+
+    def nof_cce(self, cfi):
+        return _lib.srsgpu_pdcch_nof_cce(self.q, cfi)
+
+    def re_map(self, cfi):
+        idx = np.zeros(36 * max(self.nof_cce(cfi), 1), np.uint32)
+        n = _lib.srsgpu_pdcch_re_map(self.q, cfi, idx.ctypes.data_as(_u32p), idx.size)
+        assert n >= 0
+        return idx[:n]
+
+    @staticmethod
+    def make_sf_array(sfs):
+        """list of (grid_offset, ce_offset, llr_offset, sf_idx, cfi, noise) -> srsgpu_pdcch_sf_t array"""
+        arr = (srsgpu_pdcch_sf_t * max(len(sfs), 1))()
+        for i, (g, c, l, sf, cfi, n) in enumerate(sfs):
+            arr[i].grid_offset, arr[i].ce_offset, arr[i].llr_offset = g, c, l
+            arr[i].sf_idx, arr[i].cfi, arr[i].noise_estimate = sf, cfi, n
+        return arr
+
+    def extract_llr_dev(self, sfs, d_grid, d_ce, ant_stride, d_llr, stream=None):
+        arr, n = sfs if isinstance(sfs, tuple) else (self.make_sf_array(sfs), len(sfs))
+        return _lib.srsgpu_pdcch_extract_llr_dev(self.q, arr, n, _vp(d_grid), _vp(d_ce), ant_stride,
+                                                 _vp(d_llr), _vp(stream))
+
+    @staticmethod
+    def make_search_array(searches):
+        """list of (llr_offset, sf_idx, cfi, rnti, tm[, rnti_type]) -> srsgpu_dci_search_t array"""
+        arr = (srsgpu_dci_search_t * max(len(searches), 1))()
+        for i, s in enumerate(searches):
+            arr[i].llr_offset, arr[i].sf_idx, arr[i].cfi, arr[i].rnti, arr[i].tm = s[:5]
+            arr[i].rnti_type = s[5] if len(s) > 5 else -1
+        return arr
+
+    def find_dl_dci_dev(self, searches, d_llr, d_res, stream=None):
+        """d_res: device buffer of len(searches) srsgpu_dci_result_t (RESULT_SIZE bytes each)"""
+        arr = self.make_search_array(searches)
+        return _lib.srsgpu_pdcch_find_dl_dci_dev(self.q, arr, len(searches), _vp(d_llr), _vp(d_res),
+                                                 _vp(stream))
+
+    RESULT_SIZE = ctypes.sizeof(srsgpu_dci_result_t)
+
+    @staticmethod
+    def parse_results(raw):
+        """bytes of n srsgpu_dci_result_t -> [(found 1 / 0 / -1, format, L, ncce, the 128-byte message
+        buffer)]"""
+        raw = bytes(raw)
+        n = len(raw) // ctypes.sizeof(srsgpu_dci_result_t)
+        out = []
+        for i in range(n):
+            r = srsgpu_dci_result_t.from_buffer_copy(raw, i * ctypes.sizeof(srsgpu_dci_result_t))
+            out.append((r.found, r.format, r.L, r.ncce, np.array(r.data[:], np.uint8) if r.found > 0
+                        else np.zeros(0, np.uint8)))
+        return out
+
+    def __del__(self):
+        if getattr(self, "q", None):
+            _lib.srsgpu_pdcch_destroy(self.q)
             self.q = None
 
 

@@ -667,3 +667,280 @@ int ref_pcfich(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t 
   srslte_regs_free(&regs);
   return r < 0 ? -1 : 0;
 }
+
+/* ---------------------------------------------------------------- PDCCH / DCI ---------- */
+#include "srslte/phy/phch/pdcch.h"
+#include "srslte/phy/phch/ra.h"
+
+/* 36.213 tables as the reference's ra.c serves them */
+int ref_tbs_from_idx(uint32_t idx, uint32_t nprb) { return srslte_ra_tbs_from_idx(idx, nprb); }
+int ref_tbs_idx_from_mcs(uint32_t mcs) { return srslte_ra_tbs_idx_from_mcs(mcs); }
+/* tbs_format1c_table[mcs] through srslte_ra_dl_dci_to_grant (ra.c:517-522) for an SI-RNTI 1C */
+int ref_tbs_1c(uint32_t mcs) {
+  srslte_ra_dl_dci_t d;
+  srslte_ra_dl_grant_t g;
+  memset(&d, 0, sizeof(d));
+  d.alloc_type = SRSLTE_RA_ALLOC_TYPE2;
+  d.type2_alloc.mode = SRSLTE_RA_TYPE2_LOC;
+  d.type2_alloc.L_crb = 4;
+  d.dci_is_1c = true;
+  d.mcs_idx = mcs;
+  d.tb_en[0] = true;
+  if (srslte_ra_dl_dci_to_grant(&d, 25, SRSLTE_SIRNTI, &g)) return -1;
+  return g.mcs[0].tbs;
+}
+uint32_t ref_dci_sizeof(uint32_t format, uint32_t nof_prb, uint32_t nof_ports) {
+  return srslte_dci_format_sizeof((srslte_dci_format_t)format, nof_prb, nof_ports);
+}
+
+static int ref_regs_cell(srslte_regs_t *regs, srslte_cell_t *cell, uint32_t nof_prb, uint32_t cell_id,
+                         uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res) {
+  srslte_cell_t c = {nof_prb, nof_ports, cell_id, SRSLTE_CP_NORM, (srslte_phich_length_t)phich_len,
+                     (srslte_phich_resources_t)phich_res};
+  *cell = c;
+  return srslte_regs_init(regs, c);
+}
+
+/* srslte_regs_pdcch_get's symbol order for this cell and CFI as grid indices (an index-valued
+ * grid), and NOF_CCE(cfi); returns the symbol count */
+int ref_pdcch_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                  uint32_t phich_res, uint32_t cfi, uint32_t *idx, uint32_t *nof_cce) {
+  srslte_regs_t regs;
+  srslte_cell_t cell;
+  srslte_pdcch_t q;
+  if (ref_regs_cell(&regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
+  if (srslte_pdcch_init_ue(&q, nof_prb, 1) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  cf_t *g = srslte_vec_malloc(sizeof(cf_t) * n), *out = srslte_vec_malloc(sizeof(cf_t) * n);
+  for (uint32_t i = 0; i < n; i++) g[i] = (float)i;
+  const int r = srslte_regs_pdcch_get(&regs, cfi, g, out);
+  for (int i = 0; i < r; i++) idx[i] = (uint32_t)crealf(out[i]);
+  *nof_cce = q.nof_cce[cfi - 1];
+  free(g);
+  free(out);
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return r;
+}
+
+/* srslte_pdcch_encode (pdcch.c:568-643) of n DCI messages (bits[i * 128 ..], nof_bits[i], at
+ * aggregation level L[i] and first CCE ncce[i], CRC masked with rnti[i]) into the port grids
+ * (14 x 12 nof_prb complex each, added to what they hold) */
+int ref_pdcch_encode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                     uint32_t phich_res, uint32_t cfi, uint32_t sf_idx, uint32_t n, const uint8_t *bits,
+                     const uint32_t *nof_bits, const uint32_t *L, const uint32_t *ncce,
+                     const uint16_t *rnti, float *grid0, float *grid1) {
+  srslte_regs_t regs;
+  srslte_cell_t cell;
+  srslte_pdcch_t q;
+  if (ref_regs_cell(&regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
+  if (srslte_pdcch_init_enb(&q, nof_prb) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
+  cf_t *sf[SRSLTE_MAX_PORTS] = {(cf_t *)grid0, (cf_t *)grid1, NULL, NULL};
+  int ret = 0;
+  for (uint32_t i = 0; i < n && !ret; i++) {
+    srslte_dci_msg_t msg;
+    memset(&msg, 0, sizeof(msg));
+    memcpy(msg.data, bits + 128 * i, nof_bits[i]);
+    msg.nof_bits = nof_bits[i];
+    srslte_dci_location_t loc = {L[i], ncce[i]};
+    ret = srslte_pdcch_encode(&q, &msg, loc, rnti[i], sf, sf_idx, cfi) ? -1 : 0;
+  }
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return ret;
+}
+
+static int ref_pdcch_rx(srslte_regs_t *regs, srslte_pdcch_t *q, uint32_t nof_prb, uint32_t cell_id,
+                        uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res, uint32_t nrx) {
+  srslte_cell_t cell;
+  if (ref_regs_cell(regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
+  if (srslte_pdcch_init_ue(q, nof_prb, nrx) || srslte_pdcch_set_cell(q, regs, cell)) return -1;
+  return 0;
+}
+
+/* srslte_pdcch_extract_llr_multi (pdcch.c:424-506): grids [nrx], estimates [port][rx] -> the
+ * 72 NOF_CCE(cfi) float LLRs of q->llr; returns that count */
+int ref_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                  uint32_t phich_res, uint32_t nrx, uint32_t cfi, uint32_t sf_idx, float noise,
+                  const float *g0, const float *g1, const float *h00, const float *h01, const float *h10,
+                  const float *h11, float *llr) {
+  srslte_regs_t regs;
+  srslte_pdcch_t q;
+  if (ref_pdcch_rx(&regs, &q, nof_prb, cell_id, nof_ports, phich_len, phich_res, nrx)) return -1;
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL}, *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  const float *gs[2] = {g0, g1}, *hs[2][2] = {{h00, h01}, {h10, h11}};
+  for (uint32_t a = 0; a < nrx; a++) {
+    sf[a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    memcpy(sf[a], gs[a], sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nof_ports; p++) {
+      ce[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+      memcpy(ce[p][a], hs[p][a], sizeof(cf_t) * n);
+    }
+  }
+  int r = srslte_pdcch_extract_llr_multi(&q, sf, ce, noise, sf_idx, cfi);
+  const int e = 72 * (int)q.nof_cce[cfi - 1];
+  if (r == 0) memcpy(llr, q.llr, sizeof(float) * e);
+  for (uint32_t a = 0; a < nrx; a++) {
+    free(sf[a]);
+    for (uint32_t p = 0; p < nof_ports; p++) free(ce[p][a]);
+  }
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return r ? -1 : e;
+}
+
+/* ue_dl.c:768-923 (dci_blind_search, find_dl_dci_type_siprarnti / _crnti, the formats of
+ * ue_dci_formats[tm] (tm 0..7) and common_formats; rnti_type < 0: from the RNTI value as
+ * srslte_ue_dl_find_dl_dci, else srslte_ue_dl_find_dl_dci_type's), restated over the reference's
+ * srslte_pdcch_decode_msg and location functions, on LLRs the caller puts in q->llr.
+ * out5 = {found (1, 0, or -1 where the reference's search returns SRSLTE_ERROR: decode_msg refuses
+ * a location past nCCE 87, dci.c:215-221), format, L, ncce, nof_bits}, data = the message buffer.
+ * Returns 0, or -1 on a harness error. */
+static const srslte_dci_format_t ref_ue_formats[8][2] = {
+    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},  {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},
+    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2A}, {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2},
+    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1D}, {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1B},
+    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},  {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2B}};
+static int ref_blind(srslte_pdcch_t *q, srslte_dci_location_t *loc, uint32_t nloc, srslte_dci_format_t f,
+                     uint16_t rnti, uint32_t cfi, srslte_dci_msg_t *msg, srslte_dci_location_t *found) {
+  uint16_t crc_rem = 0;
+  for (uint32_t i = 0; i < nloc; i++) {
+    if (srslte_pdcch_decode_msg(q, msg, &loc[i], f, cfi, &crc_rem)) return -1;
+    if (crc_rem == rnti) {
+      if (msg->format == SRSLTE_DCI_FORMAT0 && f == SRSLTE_DCI_FORMAT1A) continue; /* UL: pending */
+      if (msg->format == f) {
+        *found = loc[i];
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+int ref_find_dl_dci(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                    uint32_t phich_res, uint32_t cfi, uint32_t sf_idx, const float *llr, uint16_t rnti,
+                    uint32_t tm, int rnti_type, int32_t *out5, uint8_t *data) {
+  srslte_regs_t regs;
+  srslte_pdcch_t q;
+  if (ref_pdcch_rx(&regs, &q, nof_prb, cell_id, nof_ports, phich_len, phich_res, 1)) return -1;
+  memcpy(q.llr, llr, sizeof(float) * 72 * q.nof_cce[cfi - 1]);
+  srslte_dci_msg_t msg;
+  memset(&msg, 0, sizeof(msg));
+  srslte_dci_location_t loc[64], found = {0, 0};
+  int r = 0;
+  const int common = rnti_type < 0 ? (rnti == SRSLTE_SIRNTI || rnti == SRSLTE_PRNTI || rnti <= SRSLTE_RARNTI_END)
+                                   : (rnti_type == SRSLTE_RNTI_SI || rnti_type == SRSLTE_RNTI_PCH ||
+                                      rnti_type == SRSLTE_RNTI_RAR);
+  if (common) {
+    const uint32_t n = srslte_pdcch_common_locations(&q, loc, 64, cfi);
+    const srslte_dci_format_t cf[2] = {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1C};
+    for (int f = 0; f < 2 && n > 0 && r == 0; f++) r = ref_blind(&q, loc, n, cf[f], rnti, cfi, &msg, &found);
+  } else {
+    uint32_t n = srslte_pdcch_ue_locations(&q, loc, 64, sf_idx, cfi, rnti);
+    for (int f = 0; f < 2 && r == 0; f++)
+      r = ref_blind(&q, loc, n, ref_ue_formats[tm][f], rnti, cfi, &msg, &found);
+    if (r == 0) {
+      n = srslte_pdcch_common_locations(&q, loc, 64, cfi);
+      if (n > 0) r = ref_blind(&q, loc, n, SRSLTE_DCI_FORMAT1A, rnti, cfi, &msg, &found);
+    }
+  }
+  out5[0] = r < 0 ? -1 : r > 0; /* -1: the search fails (srslte_pdcch_decode_msg refuses a location) */
+  out5[1] = r > 0 ? (int32_t)msg.format : -1;
+  out5[2] = (int32_t)found.L;
+  out5[3] = (int32_t)found.ncce;
+  out5[4] = r > 0 ? (int32_t)msg.nof_bits : 0;
+  if (r > 0) memcpy(data, msg.data, SRSLTE_DCI_MAX_BITS); /* the payload and, after it, the CRC bits */
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return 0;
+}
+
+/* bits: SRSLTE_DCI_MAX_BITS bytes as srslte_dci_msg_t.data holds them */
+/* srslte_ra_dl_dci_t <-> 30 int32 fields (ref order of srsgpu_ra_dl_dci_t; the union's members
+ * are read per allocation type) and srslte_ra_dl_grant_t -> 13 int32 fields + prb bytes */
+static void ref_dci_out(const srslte_ra_dl_dci_t *d, int32_t *o) {
+  memset(o, 0, sizeof(int32_t) * 30);
+  o[0] = d->alloc_type;
+  if (d->alloc_type == SRSLTE_RA_ALLOC_TYPE0) o[1] = d->type0_alloc.rbg_bitmask;
+  if (d->alloc_type == SRSLTE_RA_ALLOC_TYPE1) {
+    o[2] = d->type1_alloc.vrb_bitmask;
+    o[3] = d->type1_alloc.rbg_subset;
+    o[4] = d->type1_alloc.shift;
+  }
+  if (d->alloc_type == SRSLTE_RA_ALLOC_TYPE2) {
+    o[5] = d->type2_alloc.riv;
+    o[6] = d->type2_alloc.L_crb;
+    o[7] = d->type2_alloc.RB_start;
+    o[8] = d->type2_alloc.n_prb1a;
+    o[9] = d->type2_alloc.n_gap;
+    o[10] = d->type2_alloc.mode;
+  }
+  o[11] = d->harq_process; o[12] = d->mcs_idx; o[13] = d->rv_idx; o[14] = d->ndi;
+  o[15] = d->mcs_idx_1; o[16] = d->rv_idx_1; o[17] = d->ndi_1; o[18] = d->tb_cw_swap;
+  o[19] = d->sram_id; o[20] = d->pinfo; o[21] = d->pconf; o[22] = d->power_offset;
+  o[23] = d->tb_en[0]; o[24] = d->tb_en[1]; o[25] = d->is_ra_order; o[26] = d->ra_preamble;
+  o[27] = d->ra_mask_idx; o[28] = d->dci_is_1a; o[29] = d->dci_is_1c;
+}
+int ref_dci_to_dl_grant(const uint8_t *bits, uint32_t nof_bits, uint32_t format, uint16_t rnti,
+                        uint32_t nof_prb, uint32_t nof_ports, int32_t *dci30, int32_t *grant13,
+                        uint8_t *prb220) {
+  srslte_dci_msg_t msg;
+  memset(&msg, 0, sizeof(msg));
+  memcpy(msg.data, bits, SRSLTE_DCI_MAX_BITS); /* the unpackers may read past nof_bits (1C, N_gap 2) */
+  msg.nof_bits = nof_bits;
+  msg.format = (srslte_dci_format_t)format;
+  srslte_ra_dl_dci_t d;
+  srslte_ra_dl_grant_t g;
+  const int r = srslte_dci_msg_to_dl_grant(&msg, rnti, nof_prb, nof_ports, &d, &g);
+  ref_dci_out(&d, dci30);
+  grant13[0] = g.nof_prb; grant13[1] = g.Qm[0]; grant13[2] = g.Qm[1];
+  grant13[3] = g.mcs[0].mod; grant13[4] = g.mcs[0].tbs; grant13[5] = g.mcs[0].idx;
+  grant13[6] = g.mcs[1].mod; grant13[7] = g.mcs[1].tbs; grant13[8] = g.mcs[1].idx;
+  grant13[9] = g.tb_en[0]; grant13[10] = g.tb_en[1]; grant13[11] = g.pinfo; grant13[12] = g.tb_cw_swap;
+  for (int s = 0; s < 2; s++)
+    for (int p = 0; p < 110; p++) prb220[s * 110 + p] = g.prb_idx[s][p];
+  return r;
+}
+/* srslte_dci_msg_pack_pdsch (dci.c:1305) from 30 fields in the order above; returns nof_bits */
+int ref_dci_pack_dl(uint32_t format, uint32_t nof_prb, uint32_t nof_ports, int crc_is_crnti,
+                    const int32_t *f, uint8_t *bits) {
+  srslte_ra_dl_dci_t d;
+  memset(&d, 0, sizeof(d));
+  d.alloc_type = (srslte_ra_type_t)f[0];
+  if (f[0] == 0) d.type0_alloc.rbg_bitmask = f[1];
+  if (f[0] == 1) {
+    d.type1_alloc.vrb_bitmask = f[2];
+    d.type1_alloc.rbg_subset = f[3];
+    d.type1_alloc.shift = f[4];
+  }
+  if (f[0] == 2) {
+    d.type2_alloc.riv = f[5];
+    d.type2_alloc.L_crb = f[6];
+    d.type2_alloc.RB_start = f[7];
+    d.type2_alloc.n_prb1a = f[8];
+    d.type2_alloc.n_gap = f[9];
+    d.type2_alloc.mode = f[10];
+  }
+  d.harq_process = f[11]; d.mcs_idx = f[12]; d.rv_idx = f[13]; d.ndi = f[14];
+  d.mcs_idx_1 = f[15]; d.rv_idx_1 = f[16]; d.ndi_1 = f[17]; d.tb_cw_swap = f[18];
+  d.sram_id = f[19]; d.pinfo = f[20]; d.pconf = f[21]; d.power_offset = f[22];
+  d.tb_en[0] = f[23]; d.tb_en[1] = f[24];
+  srslte_dci_msg_t msg;
+  memset(&msg, 0, sizeof(msg));
+  if (srslte_dci_msg_pack_pdsch(&d, (srslte_dci_format_t)format, &msg, nof_prb, nof_ports, crc_is_crnti))
+    return -1;
+  memcpy(bits, msg.data, msg.nof_bits);
+  return (int)msg.nof_bits;
+}
+/* srslte_pdcch_ue_locations_ncce / srslte_pdcch_common_locations_ncce (pdcch.c:227-300):
+ * 2 uint32 (L, ncce) per candidate */
+int ref_pdcch_locations(uint32_t nof_cce, uint32_t sf_idx, uint16_t rnti, int common, uint32_t *out) {
+  srslte_dci_location_t c[64];
+  const uint32_t n = common ? srslte_pdcch_common_locations_ncce(nof_cce, c, 64)
+                            : srslte_pdcch_ue_locations_ncce(nof_cce, c, 64, sf_idx, rnti);
+  for (uint32_t i = 0; i < n; i++) {
+    out[2 * i] = c[i].L;
+    out[2 * i + 1] = c[i].ncce;
+  }
+  return (int)n;
+}

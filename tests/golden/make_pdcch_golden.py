@@ -1,0 +1,113 @@
+"""Record golden PDCCH receptions and DCI unpackings from the reference build (`make -C oracle ref`):
+
+  - the PDCCH symbol order (srslte_regs_init + srslte_regs_pdcch_get, regs.c) and NOF_CCE for each
+    cell and CFI;
+  - control regions built with srslte_pdcch_encode (pdcch.c:568-643) through a synthetic channel
+    (tests/srsgpu_testlib.py pdcch_subframe), their srslte_pdcch_extract_llr_multi LLRs
+    (pdcch.c:424-506) and the srslte_ue_dl_find_dl_dci blind search (ue_dl.c:768-923, restated in
+    oracle/ref_harness.c over the reference's srslte_pdcch_decode_msg) for C-, SI- and RA-RNTIs;
+  - srslte_dci_msg_to_dl_grant (dci.c:49-90 with ra.c) of the found messages and of random
+    messages of every DL format.
+
+    python tests/golden/make_pdcch_golden.py   -> tests/golden/pdcch_golden.npz
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from srsgpu_testlib import (F1, F1A, F1B, F1C, F1D, F2, F2A, F2B, Ref, dci_sizeof_ref,  # noqa: E402
+                            dci_to_dl_grant_ref, find_dl_dci, pdcch_llr, pdcch_locations, pdcch_map,
+                            pdcch_subframe,
+                            random_dl_msg)
+
+
+def main():
+    ref = Ref()
+    rng = np.random.default_rng(2018)
+    arrays, cases, maps, grants = {}, [], [], []
+    # symbol orders
+    for nof_prb in (6, 15, 25, 50, 75, 100):
+        for cell_id in (0, 7, 301):
+            for nports in (1, 2):
+                pl, pr = int(rng.integers(0, 2)), int(rng.integers(0, 4))
+                for cfi in (1, 2, 3):
+                    idx, ncce = pdcch_map(ref, nof_prb, cell_id, nports, pl, pr, cfi, ref=True)
+                    key = "m%d" % len(maps)
+                    arrays[key] = idx
+                    maps.append(dict(key=key, nof_prb=nof_prb, cell_id=cell_id, nports=nports, phich_len=pl,
+                                     phich_res=pr, cfi=cfi, nof_cce=ncce))
+    # received subframes; the "batch" group shares one cell for the multi-subframe launches
+    cells = [(p, c, np_, nr) for p in (6, 15, 25, 50, 100) for c in (int(rng.integers(0, 504)),)
+             for np_ in (1, 2) for nr in (1, 2)]
+    groups = [("single", cell, 1 if cell[0] >= 50 else 2) for cell in cells] + [("batch", (25, 77, 2, 2), 6)]
+    groups += [("refused", (110, 5, 2, 1), 2)]  # 96 CCEs: UE spaces reaching nCCE 88 end in an error
+    for group, (nof_prb, cell_id, nports, nrx), reps in groups:
+        pl, pr = (int(rng.integers(0, 2)), int(rng.integers(0, 4))) if group != "refused" else (0, 0)
+        for r in range(reps):
+            cfi, sf_idx, tm = int(rng.integers(1, 4)), int(rng.integers(0, 10)), int(rng.integers(0, 8))
+            if group == "refused":
+                cfi = 3
+            y, h, searches, noise = pdcch_subframe(ref, rng, nof_prb, cell_id, nports, nrx, pl, pr, cfi,
+                                                   sf_idx, tm, snr_db=float(rng.choice([6.0, 12.0, 30.0])))
+            if group == "refused":  # C-RNTIs whose UE-specific space holds a location past nCCE 87
+                ncce = pdcch_map(ref, nof_prb, cell_id, nports, pl, pr, cfi, ref=True)[1]
+                hits = [x for x in range(0x100, 0x2000)
+                        if any(c > 87 for _, c in pdcch_locations(ref, ncce, sf_idx, x, False))]
+                searches += [(x, tm, -1) for x in hits[:4]] + [(x, tm, 0) for x in hits[4:6]]
+            nre = (cfi + (1 if nof_prb <= 10 else 0)) * 12 * nof_prb  # store the control symbols only
+            y = [v[:nre] for v in y]
+            h = [[v[:nre] for v in hp] for hp in h]
+            llr = pdcch_llr(ref, nof_prb, cell_id, nports, pl, pr, nrx, cfi, sf_idx, noise, y, h, ref=True)
+            key = "c%d" % len(cases)
+            for a in range(nrx):
+                arrays["%s_y%d" % (key, a)] = y[a]
+                for p in range(nports):
+                    arrays["%s_h%d%d" % (key, p, a)] = h[p][a]
+            arrays[key + "_llr"] = llr
+            res = []
+            for j, (rnti, stm, rtype) in enumerate(searches):
+                found, fmt, L, ncce, nb, bits = find_dl_dci(ref, nof_prb, cell_id, nports, pl, pr, cfi, sf_idx, llr,
+                                                        rnti, stm, rtype, ref=True)
+                arrays["%s_s%d_bits" % (key, j)] = bits
+                res.append(dict(rnti=rnti, tm=stm, rnti_type=rtype, found=found, format=fmt, L=L, ncce=ncce,
+                                nof_bits=nb))
+                if found > 0:
+                    grants.append((bits, fmt, rnti, nof_prb, nports, nb))
+            cases.append(dict(key=key, group=group, nof_prb=nof_prb, cell_id=cell_id, nports=nports, nrx=nrx,
+                              phich_len=pl, phich_res=pr, cfi=cfi, sf_idx=sf_idx, noise=noise,
+                              searches=res))
+    # DCI unpacking: the found messages and random ones of every DL format / RNTI kind
+    for nof_prb in (6, 15, 25, 50, 75, 100):
+        for nports in (1, 2):
+            for fmt in (F1, F1A, F1C, F1B, F1D, F2, F2A, F2B):
+                for k in range(4):
+                    rnti = [0x4601, 0xFFFF, 0x0003, 0xFFFE][k]
+                    if k < 2:
+                        b = random_dl_msg(ref, rng, fmt, nof_prb, nports, crc_is_crnti=(k == 0))
+                    else:
+                        b = rng.integers(0, 2, dci_sizeof_ref(ref, fmt, nof_prb, nports)).astype(np.uint8)
+                    grants.append((b, fmt, rnti, nof_prb, nports, len(b)))
+    gman = []
+    for i, (b, fmt, rnti, nof_prb, nports, nb) in enumerate(grants):
+        r, d, g, p = dci_to_dl_grant_ref(ref, b, fmt, rnti, nof_prb, nports, nof_bits=nb)
+        key = "g%d" % i
+        arrays[key + "_bits"] = np.asarray(b, np.uint8)
+        arrays[key + "_prb"] = p
+        gman.append(dict(key=key, format=fmt, rnti=rnti, nof_prb=nof_prb, nports=nports, nof_bits=nb, ret=r,
+                         dci=[int(v) for v in d], grant=[int(v) for v in g]))
+    man = dict(maps=maps, cases=cases, grants=gman)
+    arrays["manifest"] = np.frombuffer(json.dumps(man).encode(), np.uint8)
+    np.savez_compressed(os.path.join(HERE, "pdcch_golden.npz"), **arrays)
+    nf = sum(s["found"] > 0 for c in cases for s in c["searches"])
+    ne = sum(s["found"] < 0 for c in cases for s in c["searches"])
+    print("maps %d, subframes %d, searches found %d (refused %d) of %d, grants %d (ok %d)" % (
+        len(maps), len(cases), nf, ne, sum(len(c["searches"]) for c in cases), len(gman),
+        sum(g["ret"] == 0 for g in gman)))
+
+
+if __name__ == "__main__":
+    main()

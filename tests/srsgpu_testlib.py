@@ -615,3 +615,234 @@ def pcfich_decode(lib, nof_prb, cell_id, nports, nrx, y, h, noise, sf_idx, ref=F
         r = f(nof_prb, cell_id, nports, nrx, ya, ha, noise, sf_idx, ctypes.byref(cfi), ctypes.byref(corr))
     assert r == 0, r
     return cfi.value, corr.value
+
+
+# ------------------------------------------------------------------ PDCCH / DCI ----
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def _L(lib):
+    return lib.lib if hasattr(lib, "lib") else lib
+
+
+def _pf(a):
+    return a.ctypes.data_as(_f32p) if a is not None else None
+
+
+def pdcch_map(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, ref=False):
+    """srslte_regs_pdcch_get's symbol order as grid indices and NOF_CCE(cfi)"""
+    f = getattr(_L(lib), "ref_pdcch_map" if ref else "orc_pdcch_map")
+    f.argtypes = [ctypes.c_uint32] * 6 + [_u32p, _u32p]
+    idx = np.zeros(4 * 3 * 110 * 4, np.uint32)
+    ncce = ctypes.c_uint32(0)
+    n = f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, _ptr(idx, _u32p), ctypes.byref(ncce))
+    assert n >= 0, n
+    return idx[:n].copy(), ncce.value
+
+
+def pdcch_encode(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, msgs):
+    """srslte_pdcch_encode of msgs [(bits, L, ncce, rnti)] -> port grids complex64 [nports][14 * 12 nof_prb]
+    (reference build only)"""
+    f = _L(lib).ref_pdcch_encode
+    f.argtypes = [ctypes.c_uint32] * 8 + [_u8p, _u32p, _u32p, _u32p, _u16p, _f32p, _f32p]
+    n = 14 * 12 * nof_prb
+    grids = [np.zeros(n, np.complex64) for _ in range(2)]
+    bits = np.zeros(128 * max(len(msgs), 1), np.uint8)
+    nb = np.zeros(max(len(msgs), 1), np.uint32)
+    Ls, nc = nb.copy(), nb.copy()
+    rn = np.zeros(max(len(msgs), 1), np.uint16)
+    for i, (b, L, c, r) in enumerate(msgs):
+        bits[128 * i:128 * i + len(b)] = b
+        nb[i], Ls[i], nc[i], rn[i] = len(b), L, c, r
+    assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, len(msgs), _ptr(bits, _u8p),
+             _ptr(nb, _u32p), _ptr(Ls, _u32p), _ptr(nc, _u32p), _ptr(rn, _u16p), _pf(grids[0]),
+             _pf(grids[1])) == 0
+    return grids[:nports]
+
+
+def pdcch_llr(lib, nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_idx, noise, y, h, ref=False):
+    """srslte_pdcch_extract_llr_multi: y[a] grids, h[p][a] estimates (complex64, 14 * 12 nof_prb or the
+    leading control symbols, zero-padded) -> the 72 NOF_CCE(cfi) float LLRs"""
+    f = getattr(_L(lib), "ref_pdcch_llr" if ref else "orc_pdcch_llr")
+    f.argtypes = [ctypes.c_uint32] * 8 + [ctypes.c_float] + [_f32p] * 7
+    n = 14 * 12 * nof_prb
+    pad = lambda a: np.ascontiguousarray(np.concatenate([a, np.zeros(n - a.size, np.complex64)])
+                                         if a.size < n else a, np.complex64)
+    ys = [pad(y[a]) if a < nrx else None for a in range(2)]
+    hs = [[pad(h[p][a]) if p < nports and a < nrx else None for a in range(2)] for p in range(2)]
+    llr = np.zeros(72 * 128, np.float32)  # NOF_CCE reaches 96 at 110 PRB
+    e = f(nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_idx, noise, _pf(ys[0]), _pf(ys[1]),
+          _pf(hs[0][0]), _pf(hs[0][1]), _pf(hs[1][0]), _pf(hs[1][1]), _pf(llr))
+    assert e > 0, e
+    return llr[:e].copy()
+
+
+def find_dl_dci(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, llr, rnti, tm,
+                rnti_type=-1, ref=False):
+    """the srslte_ue_dl_find_dl_dci blind search on LLRs -> (found, format, L, ncce, nof_bits, buf): buf is
+    the message buffer (128 bytes: the payload, then the 16 CRC bits) when found, else empty"""
+    f = getattr(_L(lib), "ref_find_dl_dci" if ref else "orc_find_dl_dci")
+    f.argtypes = [ctypes.c_uint32] * 7 + [_f32p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_int, _i32p, _u8p]
+    llr = np.ascontiguousarray(llr, np.float32)
+    out = np.zeros(5, np.int32)
+    data = np.zeros(128, np.uint8)
+    assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, _pf(llr), rnti, tm, rnti_type,
+             _ptr(out, _i32p), _ptr(data, _u8p)) == 0
+    return (int(out[0]), int(out[1]), int(out[2]), int(out[3]), int(out[4]),
+            data.copy() if out[0] > 0 else data[:0].copy())
+
+
+def pdcch_locations(lib, nof_cce, sf_idx, rnti, common, ref=True):
+    f = getattr(_L(lib), "ref_pdcch_locations" if ref else "orc_pdcch_locations")
+    f.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int, _u32p]
+    out = np.zeros(128, np.uint32)
+    n = f(nof_cce, sf_idx, rnti, int(common), _ptr(out, _u32p))
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
+
+
+def dci_sizeof_ref(lib, fmt, nof_prb, nports):
+    f = _L(lib).ref_dci_sizeof
+    f.argtypes = [ctypes.c_uint32] * 3
+    f.restype = ctypes.c_uint32
+    return f(fmt, nof_prb, nports)
+
+
+def dci_to_dl_grant_ref(lib, bits, fmt, rnti, nof_prb, nports, nof_bits=None):
+    """srslte_dci_msg_to_dl_grant of the message bits[:nof_bits] (bits: the payload, or a 128-byte message
+    buffer; zero-padded) -> (ret, dci 30 fields, grant 13 fields, prb_idx [2][110])"""
+    f = _L(lib).ref_dci_to_dl_grant
+    f.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32,
+                  _i32p, _i32p, _u8p]
+    b = np.zeros(128, np.uint8)
+    b[:len(bits)] = bits
+    nof_bits = len(bits) if nof_bits is None else nof_bits
+    d, g, p = np.zeros(30, np.int32), np.zeros(13, np.int32), np.zeros(220, np.uint8)
+    r = f(_ptr(b, _u8p), nof_bits, fmt, rnti, nof_prb, nports, _ptr(d, _i32p), _ptr(g, _i32p), _ptr(p, _u8p))
+    return r, d, g, p.reshape(2, 110)
+
+
+def dci_pack_dl_ref(lib, fmt, nof_prb, nports, crc_is_crnti, fields):
+    """srslte_dci_msg_pack_pdsch from 30 fields -> bits, or None if the reference refuses them"""
+    f = _L(lib).ref_dci_pack_dl
+    f.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, _i32p, _u8p]
+    fl = np.asarray(fields, np.int32)
+    b = np.zeros(128, np.uint8)
+    n = f(fmt, nof_prb, nports, int(crc_is_crnti), _ptr(fl, _i32p), _ptr(b, _u8p))
+    return None if n < 0 else b[:n].copy()
+
+
+# srslte_dci_format_t
+F0, F1, F1A, F1C, F1B, F1D, F2, F2A, F2B = range(9)
+UE_FORMATS = [(F1A, F1), (F1A, F1), (F1A, F2A), (F1A, F2), (F1A, F1D), (F1A, F1B), (F1A, F1), (F1A, F2B)]
+
+
+def random_dl_fields(rng, fmt, nof_prb):
+    """random srslte_ra_dl_dci_t fields (30, ref_harness order) that dci.c's packers mostly accept"""
+    f = [0] * 30
+    P = 1 if nof_prb <= 10 else 2 if nof_prb <= 26 else 3 if nof_prb <= 63 else 4
+    asz = -(-nof_prb // P)
+    if fmt in (F1, F2, F2A, F2B):
+        f[0] = int(rng.integers(0, 2)) if nof_prb > 10 else 0
+        if f[0] == 0:
+            f[1] = int(rng.integers(0, 1 << asz))
+        else:
+            lp = int(np.ceil(np.log2(P)))
+            f[3], f[4] = int(rng.integers(0, P)), int(rng.integers(0, 2))
+            f[2] = int(rng.integers(0, 1 << max(asz - lp - 1, 0)))
+    else:
+        f[0] = 2
+        f[10] = 1 if fmt == F1C else int(rng.integers(0, 2))
+        f[9] = int(rng.integers(0, 2)) if nof_prb >= 50 else 0
+        step = 2 if nof_prb < 50 else 4
+        lim = nof_prb if f[10] == 0 else min(nof_prb, 16 if nof_prb > 50 else nof_prb)
+        if fmt == F1C:
+            L = step * int(rng.integers(1, max(lim // step, 1) + 1))
+            f[6], f[7] = L, step * int(rng.integers(0, max((lim - L) // step, 0) + 1))
+        else:
+            L = int(rng.integers(1, lim + 1))
+            f[6], f[7] = L, int(rng.integers(0, lim - L + 1))
+        f[8] = int(rng.integers(0, 2))
+    f[11] = int(rng.integers(0, 8))
+    f[12] = int(rng.integers(0, 32)) if rng.random() < 0.15 else int(rng.integers(0, 29))
+    f[13], f[14] = int(rng.integers(0, 4)), int(rng.integers(0, 2))
+    f[15], f[16], f[17] = int(rng.integers(0, 29)), int(rng.integers(0, 4)), int(rng.integers(0, 2))
+    f[18], f[19] = int(rng.integers(0, 2)), int(rng.integers(0, 2))
+    f[20] = int(rng.integers(0, 8))
+    f[23] = 1
+    f[24] = int(rng.integers(0, 2)) if fmt in (F2, F2A, F2B) else 0
+    return f
+
+
+def random_dl_msg(ref, rng, fmt, nof_prb, nports, crc_is_crnti=True, tries=40):
+    """a DCI message of format fmt: packed by the reference from random fields where dci.c packs the
+    format (1, 1A, 1C, 2, 2A, 2B), else (or if every try is refused) random bits of the format's size"""
+    if fmt in (F1, F1A, F1C, F2, F2A, F2B):
+        for _ in range(tries):
+            b = dci_pack_dl_ref(ref, fmt, nof_prb, nports, crc_is_crnti, random_dl_fields(rng, fmt, nof_prb))
+            if b is not None:
+                return b
+    n = dci_sizeof_ref(ref, fmt, nof_prb, nports)
+    b = rng.integers(0, 2, n).astype(np.uint8)
+    if fmt == F1A:
+        b[0] = 1
+    return b
+
+
+def pdcch_subframe(ref, rng, nof_prb, cell_id, nports, nrx, phich_len, phich_res, cfi, sf_idx, tm,
+                   snr_db=12.0):
+    """A synthetic received control region built with the reference's srslte_pdcch_encode: DCIs for a
+    C-RNTI in its UE-specific space (the tm's formats, sometimes a format 0 look-alike before it) and
+    for SI- / RA-RNTIs in the common space, through a flat per-(port, antenna) channel with small
+    per-RE ripple and AWGN. Returns (y[nrx], h[nports][nrx] over the 4 leading symbols, searches
+    [(rnti, tm, rnti_type)], noise estimate)."""
+    idx, ncce = pdcch_map(ref, nof_prb, cell_id, nports, phich_len, phich_res, cfi, ref=True)
+    used = np.zeros(max(ncce, 1), bool)
+    msgs = []
+
+    def place(locs, bits, rnti):
+        rng.shuffle(locs)
+        for L, c in locs:
+            if c <= 87 and not used[c:c + (1 << L)].any():  # srslte_dci_location_isvalid
+                used[c:c + (1 << L)] = True
+                msgs.append((bits, L, c, rnti))
+                return True
+        return False
+
+    crnti = int(rng.integers(0x000B, 0xFFF4))
+    ue = pdcch_locations(ref, ncce, sf_idx, crnti, False)
+    com = pdcch_locations(ref, ncce, sf_idx, 0, True)
+    if ue and rng.random() < 0.3:  # a UL grant (format 0 shares 1A's size) the DL search passes over
+        b = rng.integers(0, 2, dci_sizeof_ref(ref, F0, nof_prb, nports)).astype(np.uint8)
+        b[0] = 0
+        place(list(ue), b, crnti)
+    if ue and rng.random() < 0.9:
+        fmt = UE_FORMATS[tm][int(rng.integers(0, 2))]
+        place(list(ue), random_dl_msg(ref, rng, fmt, nof_prb, nports), crnti)
+    elif com:
+        place(list(com), random_dl_msg(ref, rng, F1A, nof_prb, nports), crnti)
+    si = 0xFFFF
+    if com and rng.random() < 0.8:
+        fmt = F1A if rng.random() < 0.5 else F1C
+        place(list(com), random_dl_msg(ref, rng, fmt, nof_prb, nports, crc_is_crnti=False), si)
+    rarnti = int(rng.integers(1, 11))
+    if com and rng.random() < 0.5:
+        place(list(com), random_dl_msg(ref, rng, F1A, nof_prb, nports, crc_is_crnti=False), rarnti)
+    x = pdcch_encode(ref, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, msgs)
+    n4 = 4 * 12 * nof_prb
+    sigma = 10 ** (-snr_db / 20) / np.sqrt(2)
+    h = [[None] * nrx for _ in range(nports)]
+    y = []
+    for a in range(nrx):
+        acc = np.zeros(n4, np.complex64)
+        for p in range(nports):
+            g = np.exp(2j * np.pi * rng.random()) * (0.8 + 0.4 * rng.random())
+            ripple = 1 + 0.05 * (rng.standard_normal(n4) + 1j * rng.standard_normal(n4))
+            h[p][a] = (g * ripple).astype(np.complex64)
+            acc += h[p][a] * x[p][:n4]
+        acc += (sigma * (rng.standard_normal(n4) + 1j * rng.standard_normal(n4))).astype(np.complex64)
+        y.append(acc.astype(np.complex64))
+    searches = [(crnti, tm, -1), (si, tm, -1), (rarnti, tm, -1), (int(rng.integers(0x000B, 0xFFF4)), tm, -1),
+                (si, tm, 1), (crnti, tm, 0)]
+    noise = float(2 * sigma * sigma) if rng.random() < 0.7 else 0.0
+    return y, h, searches, noise
