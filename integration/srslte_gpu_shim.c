@@ -14,10 +14,13 @@
  *   srslte_dlsch_decode2(q, cfg, sb, e_bits, data, tb_idx)  (sch.c:506-517, 16-bit LLRs)
  *   srslte_rm_turbo_rx_lut(in, out, in_len, cb_idx, rv)      (rm_turbo.c:378-381)
  *   srslte_pcfich_decode_multi(q, sf, ce, noise, sf_idx, cfi, corr)  (pcfich.c:178-241)
+ *   srslte_pdcch_extract_llr_multi(q, sf, ce, noise, sf_idx, cfi)      (pdcch.c:442-508)
+ *   srslte_pdcch_decode_msg(q, msg, location, format, cfi, crc_rem)    (pdcch.c:366-420)
  *   srslte_softbuffer_rx_init / _free / _reset / _reset_tbs / _reset_cb  (softbuffer.c:46-153):
  *                                        the reference's host work, plus the GPU softbuffer state
  *   srsgpu_shim_release(q)               called from srslte_ofdm_rx_free / srslte_chest_dl_free /
- *                                        srslte_pdsch_free / srslte_sch_free / srslte_pcfich_free
+ *                                        srslte_pdsch_free / srslte_sch_free / srslte_pcfich_free /
+ *                                        srslte_pdcch_free
  *                                        (one added line each)
  *
  * Build it with -DSRSGPU_SHIM and drop the replaced functions from their reference translation
@@ -46,6 +49,7 @@
 #include "srslte/phy/fec/rm_turbo.h"
 #include "srslte/phy/fec/softbuffer.h"
 #include "srslte/phy/phch/pcfich.h"
+#include "srslte/phy/phch/pdcch.h"
 #include "srslte/phy/phch/pdsch.h"
 #include "srslte/phy/phch/sch.h"
 
@@ -53,7 +57,9 @@
 #include "srsgpu/dlsch_batch.h"
 #include "srsgpu/ofdm_batch.h"
 #include "srsgpu/pcfich_batch.h"
+#include "srsgpu/pdcch_batch.h"
 #include "srsgpu/pdsch_batch.h"
+#include "srsgpu/viterbi_batch.h"
 
 /* ---- HIP runtime entry points used for the host <-> device staging (libamdhip64) ---- */
 typedef int hipError_t;
@@ -88,7 +94,7 @@ static int shim_copy(void *dst, const void *src, size_t n, int kind) {
 
 /* ---- object registry ---- */
 #define SHIM_MAX 64
-typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH, SHIM_SCH, SHIM_PCFICH } shim_kind_t;
+typedef enum { SHIM_NONE = 0, SHIM_OFDM, SHIM_CHEST, SHIM_PDSCH, SHIM_SCH, SHIM_PCFICH, SHIM_PDCCH } shim_kind_t;
 typedef struct {
   const void *owner;
   shim_kind_t kind;
@@ -135,6 +141,7 @@ static void shim_reset(shim_entry_t *e) {
     if (e->kind == SHIM_PDSCH) srsgpu_pdsch_destroy((srsgpu_pdsch_t *)e->gpu);
     if (e->kind == SHIM_SCH) srsgpu_dlsch_destroy((srsgpu_dlsch_t *)e->gpu);
     if (e->kind == SHIM_PCFICH) srsgpu_pcfich_destroy((srsgpu_pcfich_t *)e->gpu);
+    if (e->kind == SHIM_PDCCH) srsgpu_pdcch_destroy((srsgpu_pdcch_t *)e->gpu);
   }
   if (e->d_a) hipFree(e->d_a);
   if (e->d_b) hipFree(e->d_b);
@@ -241,6 +248,110 @@ int srslte_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_P
   if (cfi) *cfi = out[0];
   if (corr_result) memcpy(corr_result, &out[1], sizeof(float));
   return 1;
+}
+
+/* ------------------------------------------------------------------ PDCCH ---- */
+/* srslte_pdcch_extract_llr_multi (pdcch.c:442-508): the control symbols of the grids and estimates go
+ * to the GPU (srsgpu_pdcch_extract_llr_dev); the 72 NOF_CCE(cfi) LLRs come back into q->llr, the rest
+ * of q->llr zeroed as the reference does, bit-exact. The reference's scratch buffers (symbols, ce, x,
+ * d) are not filled. */
+#define SHIM_PDCCH_LLR_CAP (72 * 128)
+int srslte_pdcch_extract_llr_multi(srslte_pdcch_t *q, cf_t *sf_symbols[SRSLTE_MAX_PORTS],
+                                   cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
+                                   uint32_t nsubframe, uint32_t cfi) {
+  if (!q || nsubframe >= SRSLTE_NSUBFRAMES_X_FRAME || cfi < 1 || cfi > 3) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->nof_rx_antennas < 1 || q->nof_rx_antennas > 2 ||
+      !sf_symbols || !ce) {
+    fprintf(stderr, "srsgpu shim: GPU PDCCH covers 1-2 ports, normal CP, 1-2 rx antennas\n");
+    return SRSLTE_ERROR;
+  }
+  shim_entry_t *e = shim_get(q, SHIM_PDCCH);
+  if (!e) return SRSLTE_ERROR;
+  const uint32_t np = q->cell.nof_ports, nrx = q->nof_rx_antennas, nprb = q->cell.nof_prb;
+  const uint32_t key = ((q->cell.phich_length * 4u + q->cell.phich_resources) * 4u + np) * 4u + nrx;
+  const size_t n = SRSLTE_SF_LEN_RE(nprb, SRSLTE_CP_NORM);
+  if (e->nof_prb != nprb || e->cell_id != q->cell.id || e->aux != key || !e->gpu) {
+    shim_reset(e);
+    srsgpu_cell_t c = {nprb, q->cell.id, np, nrx};
+    if (srsgpu_pdcch_create((srsgpu_pdcch_t **)&e->gpu, &c, q->cell.phich_length, q->cell.phich_resources) ||
+        shim_alloc(&e->d_a, sizeof(cf_t) * n * nrx) || shim_alloc(&e->d_b, sizeof(cf_t) * n * nrx * np) ||
+        shim_alloc(&e->d_c, sizeof(float) * SHIM_PDCCH_LLR_CAP)) {
+      shim_reset(e);
+      fprintf(stderr, "srsgpu shim: srslte_pdcch_extract_llr_multi: GPU setup failed\n");
+      return SRSLTE_ERROR;
+    }
+    e->nof_prb = nprb;
+    e->cell_id = q->cell.id;
+    e->aux = key;
+  }
+  const uint32_t e_bits = 72 * srsgpu_pdcch_nof_cce((srsgpu_pdcch_t *)e->gpu, cfi);
+  if (e_bits != 72 * q->nof_cce[cfi - 1] || e_bits > SHIM_PDCCH_LLR_CAP || e_bits > q->max_bits) {
+    fprintf(stderr, "srsgpu shim: PDCCH REG map differs from the object's (%u / %u CCEs)\n", e_bits / 72,
+            q->nof_cce[cfi - 1]);
+    return SRSLTE_ERROR;
+  }
+  /* only the control region is read: cfi symbols (cfi + 1 below 11 PRB) */
+  const size_t nctrl = (size_t)(nprb <= 10 ? cfi + 1 : cfi) * nprb * SRSLTE_NRE;
+  for (uint32_t a = 0; a < nrx; a++) {
+    if (!sf_symbols[a] || shim_copy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * nctrl, H2D))
+      return SRSLTE_ERROR;
+    for (uint32_t p = 0; p < np; p++) /* reference ce[port][rx]; GPU planes [rx][port] */
+      if (!ce[p][a] || shim_copy(e->d_b + 2 * (size_t)(a * np + p) * n, ce[p][a], sizeof(cf_t) * nctrl, H2D))
+        return SRSLTE_ERROR;
+  }
+  const srsgpu_pdcch_sf_t sf = {0, 0, 0, nsubframe, cfi, noise_estimate, 0};
+  if (srsgpu_pdcch_extract_llr_dev((srsgpu_pdcch_t *)e->gpu, &sf, 1, e->d_a, e->d_b, n, e->d_c, NULL))
+    return SRSLTE_ERROR;
+  bzero(q->llr, sizeof(float) * q->max_bits);
+  if (shim_copy(q->llr, e->d_c, sizeof(float) * e_bits, D2H)) return SRSLTE_ERROR;
+  return SRSLTE_SUCCESS;
+}
+
+/* srslte_pdcch_decode_msg (pdcch.c:366-420): the candidate's LLRs from q->llr through the GPU DCI
+ * decoder (srsgpu_dci_decode_dev: the mean |llr| > 0.5 check, rate recovery, tail-biting Viterbi,
+ * CRC remainder). msg->data receives nof_bits + 16 bits and *crc_rem the remainder as in the
+ * reference; a candidate under the mean threshold leaves msg and *crc_rem untouched. */
+#define SHIM_DCI_LLR_OFF 16                                  /* floats: after the descriptor */
+#define SHIM_DCI_OUT_OFF (4 * (SHIM_DCI_LLR_OFF + SRSGPU_DCI_MAX_E)) /* bytes */
+int srslte_pdcch_decode_msg(srslte_pdcch_t *q, srslte_dci_msg_t *msg, srslte_dci_location_t *location,
+                            srslte_dci_format_t format, uint32_t cfi, uint16_t *crc_rem) {
+  if (!q || !msg || !location || !srslte_dci_location_isvalid(location)) {
+    if (location) fprintf(stderr, "Invalid parameters, location=%d,%d\n", location->ncce, location->L);
+    return SRSLTE_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t nof_cce = (cfi > 0 && cfi < 4) ? q->nof_cce[cfi - 1] : 0;
+  const uint32_t E = 72u << location->L;
+  if (location->ncce * 72 + E > nof_cce * 72) {
+    fprintf(stderr, "Invalid location: nCCE: %d, L: %d, NofCCE: %d\n", location->ncce, location->L, nof_cce);
+    return SRSLTE_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t nof_bits = srslte_dci_format_sizeof(format, q->cell.nof_prb, q->cell.nof_ports);
+  if (nof_bits > SRSGPU_DCI_MAX_BITS - 16) return SRSLTE_ERROR; /* the reference's buffers end there */
+  shim_entry_t *e = shim_get(q, SHIM_PDCCH);
+  if (!e) return SRSLTE_ERROR;
+  if (!e->d_d && shim_alloc(&e->d_d, SHIM_DCI_OUT_OFF + SRSGPU_DCI_MAX_BITS + 16 + 4)) return SRSLTE_ERROR;
+  /* one upload: the candidate descriptor, then its E LLRs */
+  float stage[SHIM_DCI_LLR_OFF + SRSGPU_DCI_MAX_E];
+  const srsgpu_dci_cand_t cand = {SHIM_DCI_LLR_OFF, SHIM_DCI_OUT_OFF, E, nof_bits};
+  memcpy(stage, &cand, sizeof(cand));
+  memcpy(stage + SHIM_DCI_LLR_OFF, &q->llr[location->ncce * 72], sizeof(float) * E);
+  uint8_t *d = (uint8_t *)e->d_d;
+  const size_t crc_off = SHIM_DCI_OUT_OFF + SRSGPU_DCI_MAX_BITS + 16; /* 2-byte aligned */
+  if (shim_copy(d, stage, sizeof(float) * (SHIM_DCI_LLR_OFF + E), H2D) ||
+      srsgpu_dci_decode_dev((const srsgpu_dci_cand_t *)d, 1, (const float *)d, d, (uint16_t *)(d + crc_off),
+                            d + crc_off + 2, NULL))
+    return SRSLTE_ERROR;
+  uint8_t out[SRSGPU_DCI_MAX_BITS + 16 + 4];
+  if (shim_copy(out, d + SHIM_DCI_OUT_OFF, sizeof(out), D2H)) return SRSLTE_ERROR;
+  if (!out[SRSGPU_DCI_MAX_BITS + 16 + 2]) return SRSLTE_SUCCESS; /* mean |llr| <= 0.5: skipped */
+  memcpy(msg->data, out, nof_bits + 16);
+  if (crc_rem) memcpy(crc_rem, out + SRSGPU_DCI_MAX_BITS + 16, sizeof(uint16_t));
+  msg->nof_bits = nof_bits;
+  if (format == SRSLTE_DCI_FORMAT0 || format == SRSLTE_DCI_FORMAT1A)
+    msg->format = msg->data[0] == 0 ? SRSLTE_DCI_FORMAT0 : SRSLTE_DCI_FORMAT1A; /* pdcch.c:398-403 */
+  else
+    msg->format = format;
+  return SRSLTE_SUCCESS;
 }
 
 /* ------------------------------------------------------------------ channel estimation ---- */

@@ -26,6 +26,12 @@
  * srslte_softbuffer_rx_reset): return value, data and CRC bytes, nof_iterations, cb_crc and tb_crc
  * must agree exactly in every configuration. srslte_rm_turbo_rx_lut (rm_turbo.c:378) is compared
  * with the reference on random LLRs accumulated into random rows for every rv and a K sweep.
+ *
+ * PDCCH drop-ins: DCIs the reference's srslte_pdcch_encode places at UE-specific and common
+ * candidates of this cell go through a flat channel with AWGN; srslte_pdcch_extract_llr_multi
+ * (q->llr, return value) and srslte_pdcch_decode_msg on every candidate of the search spaces for
+ * every DL format (the whole srslte_dci_msg_t, the CRC remainder, the return value, including
+ * refused locations) must agree bit for bit ("pdcch_mismatches").
  */
 #include <complex.h>
 #include <math.h>
@@ -38,6 +44,7 @@
 #include "srslte/phy/fec/softbuffer.h"
 #include "srslte/phy/phch/sch.h"
 #include "srslte/phy/phch/pcfich.h"
+#include "srslte/phy/phch/pdcch.h"
 #include "srslte/phy/phch/pdsch.h"
 #include "srslte/phy/phch/ra.h"
 #include "srslte/phy/utils/vector.h"
@@ -61,6 +68,11 @@ void srsgpu_shim_softbuffer_rx_free(srslte_softbuffer_rx_t *q);
 int srsgpu_shim_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_PORTS],
                                     cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
                                     uint32_t nsubframe, uint32_t *cfi, float *corr_result);
+int srsgpu_shim_pdcch_extract_llr_multi(srslte_pdcch_t *q, cf_t *sf_symbols[SRSLTE_MAX_PORTS],
+                                        cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
+                                        uint32_t nsubframe, uint32_t cfi);
+int srsgpu_shim_pdcch_decode_msg(srslte_pdcch_t *q, srslte_dci_msg_t *msg, srslte_dci_location_t *location,
+                                 srslte_dci_format_t format, uint32_t cfi, uint16_t *crc_rem);
 int srsgpu_shim_release(const void *owner);
 
 static uint64_t rng = 1;
@@ -334,7 +346,89 @@ int main(int argc, char **argv) {
     srslte_regs_free(&regs);
     rng = rng_saved;
   }
+  /* PDCCH: the reference's srslte_pdcch_extract_llr_multi + srslte_pdcch_decode_msg and the shim's on
+   * the same control regions (own rng stream) */
+  uint32_t npd = 0, npd_found = 0, npd_bad = 0;
+  {
+    const uint64_t rng_saved = rng;
+    srslte_regs_t regs;
+    static srslte_pdcch_t ptx, pa, pb;
+    if (srslte_regs_init(&regs, cell) || srslte_pdcch_init_enb(&ptx, nof_prb) ||
+        srslte_pdcch_set_cell(&ptx, &regs, cell) || srslte_pdcch_init_ue(&pa, nof_prb, nof_rx) ||
+        srslte_pdcch_set_cell(&pa, &regs, cell) || srslte_pdcch_init_ue(&pb, nof_prb, nof_rx) ||
+        srslte_pdcch_set_cell(&pb, &regs, cell))
+      return 2;
+    const srslte_dci_format_t fmts[6] = {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1, SRSLTE_DCI_FORMAT1C,
+                                         SRSLTE_DCI_FORMAT2A, SRSLTE_DCI_FORMAT2, SRSLTE_DCI_FORMAT1B};
+    const size_t nctrl = (size_t)(nof_prb <= 10 ? 4 : 3) * nof_prb * SRSLTE_NRE;
+    for (uint32_t it = 0; it < 12; it++) {
+      const uint32_t sf = (it * 7) % 10, c = 1 + it % 3;
+      const uint16_t ue_rnti = (uint16_t)(0x0100 + 97 * it);
+      for (uint32_t p = 0; p < nports; p++) memset(txg[p], 0, sizeof(cf_t) * n);
+      srslte_dci_location_t ue[64], com[64];
+      const uint32_t nue = srslte_pdcch_ue_locations(&ptx, ue, 64, sf, c, ue_rnti);
+      const uint32_t ncom = srslte_pdcch_common_locations(&ptx, com, 64, c);
+      srslte_dci_msg_t m;
+      memset(&m, 0, sizeof(m));
+      if (nue && ue[it % nue].ncce <= 87) { /* a UE-specific DCI of one of the formats */
+        const srslte_dci_format_t f = fmts[it % 6];
+        m.nof_bits = srslte_dci_format_sizeof(f, nof_prb, nports);
+        for (uint32_t b = 0; b < m.nof_bits; b++) m.data[b] = urand() < 0.5;
+        if (f == SRSLTE_DCI_FORMAT1A) m.data[0] = 1;
+        if (srslte_pdcch_encode(&ptx, &m, ue[it % nue], ue_rnti, txg, sf, c)) return 2;
+      }
+      if (ncom && (it & 1)) { /* an SI-RNTI 1A / 1C in the last common candidate */
+        const srslte_dci_format_t f = (it & 2) ? SRSLTE_DCI_FORMAT1C : SRSLTE_DCI_FORMAT1A;
+        m.nof_bits = srslte_dci_format_sizeof(f, nof_prb, nports);
+        for (uint32_t b = 0; b < m.nof_bits; b++) m.data[b] = urand() < 0.5;
+        if (srslte_pdcch_encode(&ptx, &m, com[ncom - 1], SRSLTE_SIRNTI, txg, sf, c)) return 2;
+      }
+      cf_t g[2][2];
+      for (uint32_t a = 0; a < nof_rx; a++)
+        for (uint32_t p = 0; p < nports; p++) g[p][a] = (0.7f + 0.5f * (float)urand()) * cexpf(6.2831853f * (float)urand() * _Complex_I);
+      const float sigma = (it % 4 == 3) ? 0.7f : 0.1f;
+      for (uint32_t a = 0; a < nof_rx; a++)
+        for (size_t i = 0; i < nctrl; i++) {
+          cf_t acc = sigma * (gauss() + gauss() * _Complex_I);
+          for (uint32_t p = 0; p < nports; p++) {
+            h[p][a][i] = g[p][a] * (1.0f + 0.05f * (gauss() + gauss() * _Complex_I));
+            acc += h[p][a][i] * txg[p][i];
+          }
+          y[a][i] = acc;
+        }
+      const float nz = (it & 1) ? 2 * sigma * sigma : 0.0f;
+      const int e1 = srslte_pdcch_extract_llr_multi(&pa, y, h, nz, sf, c);
+      const int e2 = srsgpu_shim_pdcch_extract_llr_multi(&pb, y, h, nz, sf, c);
+      if (e1 != e2 || memcmp(pa.llr, pb.llr, sizeof(float) * pa.max_bits)) npd_bad++;
+      /* every candidate of both spaces (and one refused location) for every format */
+      srslte_dci_location_t cand[130];
+      uint32_t nc = 0;
+      for (uint32_t i = 0; i < nue; i++) cand[nc++] = ue[i];
+      for (uint32_t i = 0; i < ncom; i++) cand[nc++] = com[i];
+      cand[nc].L = 0;
+      cand[nc++].ncce = 88;
+      for (uint32_t i = 0; i < nc; i++)
+        for (int f = 0; f < 6; f++) {
+          srslte_dci_msg_t m1, m2;
+          memset(&m1, 0xA5, sizeof(m1));
+          memset(&m2, 0xA5, sizeof(m2));
+          uint16_t r1 = 0x5A5A, r2 = 0x5A5A;
+          const int d1 = srslte_pdcch_decode_msg(&pa, &m1, &cand[i], fmts[f], c, &r1);
+          const int d2 = srsgpu_shim_pdcch_decode_msg(&pb, &m2, &cand[i], fmts[f], c, &r2);
+          if (d1 != d2 || r1 != r2 || memcmp(&m1, &m2, sizeof(m1))) npd_bad++;
+          npd_found += d1 == 0 && (r1 == ue_rnti || r1 == SRSLTE_SIRNTI);
+          npd++;
+        }
+    }
+    srsgpu_shim_release(&pb);
+    srslte_pdcch_free(&ptx);
+    srslte_pdcch_free(&pa);
+    srslte_pdcch_free(&pb);
+    srslte_regs_free(&regs);
+    rng = rng_saved;
+  }
   printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u dlsch=%u dlsch_mismatches=%u rm_mismatches=%u "
-         "pcfich_mismatches=%u\n", ntx, nacks, nbad, nsoft, tbs, ndl, ndl_bad, nrm_bad, npc_bad);
-  return nbad || ndl_bad || nrm_bad || npc_bad ? 1 : 0;
+         "pcfich_mismatches=%u pdcch=%u pdcch_found=%u pdcch_mismatches=%u\n", ntx, nacks, nbad, nsoft, tbs, ndl,
+         ndl_bad, nrm_bad, npc_bad, npd, npd_found, npd_bad);
+  return nbad || ndl_bad || nrm_bad || npc_bad || npd_bad ? 1 : 0;
 }

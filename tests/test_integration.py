@@ -65,6 +65,10 @@ def test_shim_pdsch_decode_matches_reference(case):
     assert int(stats["rm_mismatches"]) == 0, r.stdout + r.stderr
     # srslte_pcfich_decode_multi drop-in on this cell's ports / rx antennas: CFI and correlation exact
     assert int(stats["pcfich_mismatches"]) == 0, r.stdout + r.stderr
+    # srslte_pdcch_extract_llr_multi / srslte_pdcch_decode_msg drop-ins: q->llr and every candidate's
+    # message, CRC remainder and return value exact
+    assert int(stats["pdcch"]) >= 100 and int(stats["pdcch_mismatches"]) == 0, r.stdout + r.stderr
+    assert int(stats["pdcch_found"]) >= 1, r.stdout + r.stderr
 
 
 # the 8-bit LLR chain (llr_is_8bit on the PDSCH and its DL-SCH, pdsch.c:795-806, sch.c:344-364):
