@@ -709,7 +709,7 @@ int ref_pdcch_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32
   srslte_cell_t cell;
   srslte_pdcch_t q;
   if (ref_regs_cell(&regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
-  if (srslte_pdcch_init_ue(&q, nof_prb, 1) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
+  if (srslte_pdcch_init_ue(&q, SRSLTE_MAX_PRB, 1) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
   const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
   cf_t *g = srslte_vec_malloc(sizeof(cf_t) * n), *out = srslte_vec_malloc(sizeof(cf_t) * n);
   for (uint32_t i = 0; i < n; i++) g[i] = (float)i;
@@ -734,7 +734,7 @@ int ref_pdcch_encode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uin
   srslte_cell_t cell;
   srslte_pdcch_t q;
   if (ref_regs_cell(&regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
-  if (srslte_pdcch_init_enb(&q, nof_prb) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
+  if (srslte_pdcch_init_enb(&q, SRSLTE_MAX_PRB) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
   cf_t *sf[SRSLTE_MAX_PORTS] = {(cf_t *)grid0, (cf_t *)grid1, NULL, NULL};
   int ret = 0;
   for (uint32_t i = 0; i < n && !ret; i++) {
@@ -754,7 +754,7 @@ static int ref_pdcch_rx(srslte_regs_t *regs, srslte_pdcch_t *q, uint32_t nof_prb
                         uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res, uint32_t nrx) {
   srslte_cell_t cell;
   if (ref_regs_cell(regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
-  if (srslte_pdcch_init_ue(q, nof_prb, nrx) || srslte_pdcch_set_cell(q, regs, cell)) return -1;
+  if (srslte_pdcch_init_ue(q, SRSLTE_MAX_PRB, nrx) || srslte_pdcch_set_cell(q, regs, cell)) return -1;
   return 0;
 }
 

@@ -203,7 +203,7 @@ def test_gpu_golden_batch(gold):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
-@pytest.mark.parametrize("nof_prb,nports,nrx", [(6, 1, 1), (15, 2, 1), (25, 1, 2), (50, 2, 2), (75, 1, 1),
+@pytest.mark.parametrize("nof_prb,nports,nrx", [(6, 1, 1), (9, 2, 2), (10, 1, 2), (15, 2, 1), (25, 1, 2), (50, 2, 2), (75, 1, 1),
                                                 (100, 2, 2), (110, 2, 1)])
 def test_gpu_random_vs_reference(nof_prb, nports, nrx):
     """random cells and subframes generated live with the reference's encoder; 40 subframes in one launch,
