@@ -530,6 +530,58 @@ def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
             "ms_per_launch": round(el / steps * 1e3, 3), "subframes_per_s": round(nsf * steps / el, 1)}
 
 
+def pdcch_receive(s, torch, steps, nsf=1024, nof_prb=100):
+    """The PDCCH receive of srslte_ue_dl_decode_rnti for nsf subframes of a
+    20 MHz 2-port cell with 2 rx antennas: srslte_pdcch_extract_llr_multi (transmit diversity, one
+    launch for all subframes, srsgpu_pdcch_extract_llr_dev) and the srslte_ue_dl_find_dl_dci search
+    for a C-RNTI (TM3: 1A and 2A in the UE-specific space, 1A in the common space) and the SI-RNTI
+    (1A and 1C in the common space) per subframe (srsgpu_pdcch_find_dl_dci_dev: host candidate lists,
+    one decode launch for every candidate, one selection launch). Random grids: nothing is found, so
+    every candidate is decoded and every search runs to its end (the search's worst case)."""
+    rng = np.random.default_rng(5)
+    stride, nrx, nports = nof_prb * 12 * 14, 2, 2
+    n3 = 3 * nof_prb * 12
+    grid = torch.zeros((nsf, nrx, stride, 2), dtype=torch.float32, device="cuda")
+    ce = torch.zeros((nsf, nrx * nports, stride, 2), dtype=torch.float32, device="cuda")
+    grid[:, :, :n3] = torch.from_numpy(rng.standard_normal((nsf, nrx, n3, 2)).astype(np.float32)).cuda()
+    ce[:, :, :n3] = torch.from_numpy(rng.standard_normal((nsf, nrx * nports, n3, 2)).astype(np.float32)).cuda()
+    q = s.Pdcch(nof_prb, 1, nports, nrx, 0, 1)
+    llr_stride = 72 * 128
+    d_llr = torch.zeros(nsf * llr_stride, dtype=torch.float32, device="cuda")
+    sfs = [(i * nrx * stride, i * nrx * nports * stride, i * llr_stride, i % 10, 3, 0.01) for i in range(nsf)]
+    sfs = (q.make_sf_array(sfs), nsf)
+    searches = []
+    for i in range(nsf):
+        searches.append((i * llr_stride, i % 10, 3, 0x3000 + 17 * i, 2))
+        searches.append((i * llr_stride, i % 10, 3, 0xFFFF, 2))
+    d_res = torch.zeros(len(searches) * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ncand = sum(len(s.pdcch_locations(q.nof_cce(3), i % 10, 0x3000 + 17 * i)) * 2 for i in range(nsf)) + \
+        len(s.pdcch_locations(q.nof_cce(3), common=True)) * 3 * nsf
+    torch.cuda.synchronize()
+
+    def step():
+        if q.extract_llr_dev(sfs, grid.data_ptr(), ce.data_ptr(), stride, d_llr.data_ptr(), st) != 0:
+            raise RuntimeError("srsgpu_pdcch_extract_llr_dev failed")
+        if q.find_dl_dci_dev(searches, d_llr.data_ptr(), d_res.data_ptr(), st) != 0:
+            raise RuntimeError("srsgpu_pdcch_find_dl_dci_dev failed")
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    found = sum(r[0] for r in s.Pdcch.parse_results(d_res.cpu().numpy().tobytes()))
+    del grid, ce
+    return {"workload": "pdcch_receive_%dsf_%dprb_2ports_2rx_cfi3" % (nsf, nof_prb),
+            "searches_per_step": len(searches), "candidates_per_step": ncand,
+            "ms_per_step": round(el / steps * 1e3, 3), "subframes_per_s": round(nsf * steps / el, 1),
+            "found": int(found)}
+
+
 def dropin_latency(s, llr, ncb=16):
     """The drop-in srslte_tdec_iteration path (include/srslte/phy/fec/turbodecoder.h) as an
     unmodified decode_tb_cb loop drives it (sch.c:356-391): per code block srslte_tdec_new_cb, then
@@ -565,7 +617,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich,pdcch",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -817,6 +869,9 @@ def main():
     pcf = None
     if "pcfich" in legs and rank == 0:
         pcf = pcfich_cfi(s, torch, max(4, args.steps // 2))
+    pdc = None
+    if "pdcch" in legs and rank == 0:
+        pdc = pdcch_receive(s, torch, max(4, args.steps // 2))
     dropin = None
     if "dropin" in legs and rank == 0:
         dropin = dropin_latency(s, llr)
@@ -827,6 +882,8 @@ def main():
         result["pdcch_dci"] = dci
     if rank == 0 and pcf:
         result["pcfich"] = pcf
+    if rank == 0 and pdc:
+        result["pdcch"] = pdc
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:
