@@ -47,11 +47,19 @@ _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
 
+SRSLTE_TDEC_REF_SIZEOF = 18264  # include/srslte/phy/fec/turbodecoder.h: the reference's sizeof
+
+
 class srslte_tdec_t(ctypes.Structure):
-    """Layout of srslte_tdec_t in include/srslte/phy/fec/turbodecoder.h."""
+    """Layout of srslte_tdec_t in include/srslte/phy/fec/turbodecoder.h, padding included (the
+    library clears and writes the whole struct)."""
     _fields_ = [("max_long_cb", ctypes.c_uint32), ("dec_type", ctypes.c_int),
                 ("force_not_sb", ctypes.c_bool), ("current_long_cb", ctypes.c_uint32),
-                ("current_cbidx", ctypes.c_int), ("n_iter", ctypes.c_int), ("gpu", ctypes.c_void_p)]
+                ("current_cbidx", ctypes.c_int), ("n_iter", ctypes.c_int), ("gpu", ctypes.c_void_p),
+                ("reserved", ctypes.c_uint8 * (SRSLTE_TDEC_REF_SIZEOF - 32))]
+
+
+assert ctypes.sizeof(srslte_tdec_t) == SRSLTE_TDEC_REF_SIZEOF
 
 
 class srslte_tcod_t(ctypes.Structure):

@@ -28,3 +28,13 @@ def golden():
     z = np.load(os.path.join(HERE, "golden", "tdec_golden.npz"))
     manifest = json.loads(bytes(z["manifest"]).decode())
     return z, manifest
+
+
+@pytest.fixture(autouse=True)
+def _gc_after_each_test():
+    """SRSGPU_GC_EACH=1: collect garbage after every test, so a failing native destructor shows up
+    in the test that created the object (debugging aid)"""
+    yield
+    if os.environ.get("SRSGPU_GC_EACH") == "1":
+        import gc
+        gc.collect()

@@ -90,3 +90,13 @@ def test_tdec_struct_layout_matches_reference(tmp_path):
     ref = _sizeof([ref_inc])
     ours = _sizeof([os.path.join(REPO, "include")])
     assert ours == ref, (ours, ref)
+
+
+def test_python_tdec_struct_has_the_c_size():
+    """the ctypes mirror allocates the whole C struct: srslte_tdec_init clears sizeof(srslte_tdec_t)
+    bytes, so a shorter Python struct would be overrun"""
+    import ctypes
+    import srsgpu_phy
+    assert ctypes.sizeof(srsgpu_phy.srslte_tdec_t) == srsgpu_phy.SRSLTE_TDEC_REF_SIZEOF
+    hdr = open(os.path.join(REPO, "include", "srslte", "phy", "fec", "turbodecoder.h")).read()
+    assert "#define SRSLTE_TDEC_REF_SIZEOF %d" % srsgpu_phy.SRSLTE_TDEC_REF_SIZEOF in hdr
