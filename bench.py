@@ -163,17 +163,20 @@ def cpu_baseline(llr, nthreads=None):
 C3_PRB, C3_CELL, C3_TBS, C3_SF = 100, 1, 75376, 1024   # BASELINE configs[2]: 20 MHz SISO 64QAM
 
 
-def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1):
-    """n_sf time-domain 20 MHz subframes per rx antenna (N = 2048, 15 N samples): random 64QAM
-    symbols on every RE of each layer through frequency-selective channels plus AWGN, built with
-    numpy only -> [n_sf][nrx][15 N]. The symbols are not codewords, so every code block runs the
-    full 8 half-iterations (the fixed-8 throughput case; early stop never triggers)."""
+def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1, first=0, noise_seed=None):
+    """Subframes first .. first+n_sf-1 of a global job (a rank's contiguous shard), each
+    time-domain 20 MHz subframe per rx antenna (N = 2048, 15 N samples): random 64QAM symbols on
+    every RE of each layer through frequency-selective channels plus AWGN, built with numpy only ->
+    [n_sf][nrx][15 N]. Global subframe i uses template i % 16 (templates drawn from `rng`, the
+    same on every rank); the noise is seeded by the shard. The symbols are not codewords, so
+    every code block runs the full 8 half-iterations (the fixed-8 throughput case; early stop
+    never triggers)."""
     N = s.symbol_sz(C3_PRB, True)
     nsc = 12 * C3_PRB
     k = np.arange(nsc)
     lev = np.array([-7, -5, -3, -1, 1, 3, 5, 7], np.float32) / np.sqrt(42)
     cp0, cp = int(np.ceil(160 * N / 2048)), int(np.ceil(144 * N / 2048))
-    ntmpl = min(n_sf, 16)
+    ntmpl = 16
     tmpl = np.zeros((ntmpl, nrx, 15 * N), np.complex64)
     for t in range(ntmpl):
         layers = [lev[rng.integers(0, 8, (14, nsc))] + 1j * lev[rng.integers(0, 8, (14, nsc))]
@@ -194,8 +197,9 @@ def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1):
                 tmpl[t, a, pos:pos + c] = sym[i, N - c:]
                 tmpl[t, a, pos + c:pos + c + N] = sym[i]
                 pos += c + N
-    x = tmpl[np.arange(n_sf) % ntmpl]
-    x += (1e-3 / np.sqrt(N)) * (rng.standard_normal(x.shape) + 1j * rng.standard_normal(x.shape)).astype(np.complex64)
+    x = tmpl[(first + np.arange(n_sf)) % ntmpl]
+    nrng = rng if noise_seed is None else np.random.default_rng(noise_seed)
+    x += (1e-3 / np.sqrt(N)) * (nrng.standard_normal(x.shape) + 1j * nrng.standard_normal(x.shape)).astype(np.complex64)
     return N, x
 
 
@@ -222,7 +226,7 @@ def stage_profile(s, torch, step, steps):
     return out
 
 
-def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
+def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None):
     """tm 1 — BASELINE configs[2]: one step = 1024 subframes through OFDM FFT -> CRS channel
     estimation -> PDSCH (RE extraction, MMSE, 64QAM demap, descramble) -> DL-SCH (de-RM, turbo
     decoding with CRC early stop up to 8 half-iterations, TB CRC) for TBS 75376 (13 x K=5824).
@@ -230,11 +234,23 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
     antennas, CDD 2x2 MMSE, two MCS-28 TBs per subframe) through the same stages.
     lanes: the batch is split over that many HIP streams, each with its own OFDM / estimator /
     PDSCH handles (a worker per stream, as srsUE runs one phch_worker per subframe): one lane's
-    front end and small kernels fill the SIMDs the other lane's decoder leaves idle."""
+    front end and small kernels fill the SIMDs the other lane's decoder leaves idle.
+    Multi-GPU (BASELINE configs[3] "8192-subframe batch sharded across 8 GPUs"): the
+    job is nranks x 1024 subframes, split in contiguous subframe ranges by the native partitioner
+    (srsgpu_shard_contiguous, the analogue of srsUE's worker pool handing out whole subframes,
+    phy.cc:141-168); every rank synthesises and decodes its own range, then the results of every
+    subframe (per TB: return code, nof_iterations, cb_crc, TB bytes) go to rank 0 in one grouped
+    send/recv batch (srsgpu_shard.gather_records), timed separately as gather_ms."""
+    import srsgpu_shard as sh
+    rank = dist.get_rank() if dist else 0
+    nranks = dist.get_world_size() if dist else 1
+    n_global = C3_SF * nranks
+    first = sh.contiguous(n_global, nranks)
+    assert first[rank + 1] - first[rank] == C3_SF
     nrx = nports = 2 if tm == 3 else 1
     ntb = 2 if tm == 3 else 1
     rng = np.random.default_rng(99)
-    N, x = pipeline_inputs(s, C3_SF, rng, nrx, nports)
+    N, x = pipeline_inputs(s, C3_SF, rng, nrx, nports, first=first[rank], noise_seed=1000 + rank)
     gsz = 14 * 12 * C3_PRB
     nsf = C3_SF // lanes
     ngrid = nsf * nrx
@@ -281,15 +297,43 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     gc.disable()  # the host-bound legs must not pay a collector pause inside the timed loop
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     el = time.perf_counter() - t0
     gc.enable()
     stages = stage_profile(s, torch, step, steps)
     noi = np.concatenate([o["noi"].cpu().numpy() for o in L])
+    # results of this rank's subframes (lane li holds subframes li*nsf .. of the range), one record
+    # per subframe = its TBs' records, then the gather to rank 0
+    recs = []
+    for o in L:
+        ret, noiv, data = o["ret"].cpu().numpy(), o["noi"].cpu().numpy(), o["data"].cpu().numpy()
+        for i in range(nsf):
+            recs.append(np.concatenate([
+                sh.pack_tb_record(ret[ntb * i + t], noiv[ntb * i + t],
+                                  data[(ntb * i + t) * dlen:(ntb * i + t) * dlen + C3_TBS // 8],
+                                  o["pd"].read_cb_crc(ntb * i + t), C3_TBS) for t in range(ntb)]))
+    gdev = dev if (dist and dist.get_backend() == "nccl") else torch.device("cpu")  # gloo: host tensors
+    local = torch.from_numpy(np.concatenate(recs)).to(gdev)
+    gather_ms, gathered = None, None
+    if dist:
+        owner = np.repeat(np.arange(nranks), np.diff(first))
+        sizes = [ntb * sh.tb_record_len(C3_TBS)] * n_global
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        got = sh.gather_records(dist, torch, gdev, owner, sizes, local)
+        torch.cuda.synchronize()
+        gather_ms = round((time.perf_counter() - tg) * 1e3, 3)
+        if got is not None:
+            gathered = sum(1 for r in got if r is not None and r.size == sizes[0])
     for o in L:
         for k in ("ofdm", "chest", "pd"):
             o[k].close()
@@ -299,6 +343,9 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2):
             "processing_mbps": round(C3_SF * ntb * steps * C3_TBS / el / 1e6, 1),
             "ms_per_batch": round(el / steps * 1e3, 3), "symbol_size": N, "rx_antennas": nrx,
             "streams": lanes, "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
+            "global_subframes": n_global, "partition": {"kind": "contiguous", "balance": 1.0},
+            "subframes_this_rank": C3_SF, "gather_ms": gather_ms, "gathered_subframes": gathered,
+            "result_bytes_per_rank": int(local.numel()),
             "data": "synthetic 64QAM symbols (not codewords: every CB runs the full 8 half-iterations "
                     "and fails its CRC, so this is the fixed-8 processing rate in TB bits per second, "
                     "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
@@ -735,6 +782,21 @@ def main():
         b.close()
     el_ms, ms_err = reduce_over_ranks(dist, dev, el_ms, ms_err)
     elapsed, bit_errors = reduce_over_ranks(dist, dev, elapsed, bit_errors)
+    # the decoded bytes of every rank's code blocks go to rank 0 in one grouped
+    # send/recv batch (RCCL over xGMI on the GPU box), timed separately; not part of the step
+    gather = None
+    if dist:
+        gdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        local_out = d_out.reshape(-1) if gdev.type == "cuda" else d_out.reshape(-1).cpu()
+        owner = np.repeat(np.arange(nranks), np.diff(first))
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        got = sh.gather_records(dist, torch, gdev, owner, [K // 8] * (nranks * NCB), local_out)
+        torch.cuda.synchronize()
+        gather = {"gather_ms": round((time.perf_counter() - tg) * 1e3, 3),
+                  "bytes_per_rank": NCB * K // 8,
+                  "gathered_code_blocks": (sum(1 for r in got if r is not None) if got is not None else None)}
 
     bits_total = nranks * NCB * K * args.steps
     mbps = decoded_mbps(nranks, NCB, K, args.steps, elapsed)
@@ -772,6 +834,8 @@ def main():
                        "bit_errors": bit_errors},
             "roofline": roofline,
         }
+        if gather:
+            result["gather"] = gather
         result["streaming"] = {
             "streams": NSTREAMS, "mbps": round(decoded_mbps(nranks, NCB, K, args.steps, el_ms), 2),
             "ms_per_step": round(el_ms / args.steps * 1e3, 3), "bit_errors": ms_err,
@@ -792,14 +856,14 @@ def main():
     legs = set() if args.no_pipeline else set(args.legs.split(","))
     pipe = None
     if "c3" in legs:
-        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2)
+        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2, dist=dist)
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
             pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe["processing_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
     pipe3 = None
     if "tm3" in legs:
-        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3)
+        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3, dist=dist)
         if dist:
             ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
             pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)

@@ -20,6 +20,7 @@
 
 #include "dlsch_kernels.h"
 #include "srsgpu/dlsch_batch.h"
+#include "srsgpu/ulsch_batch.h"
 #include "tdec_engine.h"
 
 namespace srsgpu {
@@ -136,6 +137,8 @@ struct DlschEngine {
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
   EncItem *h_enc = nullptr, *d_enc = nullptr;
   uint32_t *d_crc_a = nullptr;
+  // UL-SCH deinterleaver descriptors (lazily allocated)
+  UlItem *h_ul = nullptr, *d_ul = nullptr;
   // host-pointer API staging
   int16_t *e_stage = nullptr;
   uint8_t *data_stage = nullptr;
@@ -191,9 +194,10 @@ struct DlschEngine {
     for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
                     (void *)d_noi, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
-                    (void *)data_stage, (void *)d_enc, (void *)d_crc_a})
+                    (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc})
+    for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
+                    (void *)h_ul})
       if (p) (void)hipHostFree(p);
     for (auto &kv : tables) (void)hipFree(kv.second);
     tables.clear();
@@ -450,6 +454,9 @@ struct DlschEngine {
 } // namespace srsgpu
 
 using srsgpu::DlschEngine;
+using srsgpu::ProfScope;
+using srsgpu::UlItem;
+using srsgpu::launch_ulsch_deinterleave;
 
 struct srsgpu_dlsch {
   DlschEngine e;
@@ -506,6 +513,54 @@ int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
     d[i] = d_data + tb[i].data_offset;
   }
   return q->e.decode(tb, ntb, e.data(), d.data(), maxh, d_ret, d_noi);
+}
+
+// srslte_ulsch_decode (sch.c:883-889 -> srslte_ulsch_uci_decode :944-985 without UCI): the channel
+// deinterleaver of every TB (ulsch_deinterleave, :860-881) into the caller's g bits, then decode_tb
+// on them through the DL-SCH path (the reference's decode_tb is the same function for both links)
+int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb,
+                            const int16_t *d_q, int16_t *d_g, uint8_t *d_data, uint32_t maxh,
+                            int32_t *d_ret, uint32_t *d_noi) {
+  if (!q || (!tb && ntb) || !d_q || !d_g || !d_data || !d_ret || !d_noi) return -1;
+  if (ntb == 0) return 0;
+  DlschEngine &E = q->e;
+  if (ntb > E.cap) return -1;
+  for (uint32_t i = 0; i < ntb; i++) {
+    const uint32_t Qm = tb[i].Qm, ns = tb[i].nof_symb;
+    if ((Qm != 2 && Qm != 4 && Qm != 6) || ns == 0 || tb[i].nof_bits % (Qm * ns)) {
+      fprintf(stderr, "srsgpu: UL-SCH TB %u: %u coded bits are not a %u x %u-column matrix\n", i,
+              tb[i].nof_bits, Qm, ns);
+      return -1;
+    }
+  }
+  if (!E.h_ul) {
+    HIPCHK(hipHostMalloc(&E.h_ul, sizeof(UlItem) * E.cap));
+    HIPCHK(hipMalloc(&E.d_ul, sizeof(UlItem) * E.cap));
+  }
+  if (E.staged_pending) HIPCHK(hipEventSynchronize(E.staged));
+  uint32_t max_bits = 0;
+  std::vector<srsgpu_dlsch_tb_t> dl(ntb);
+  std::vector<const int16_t *> e(ntb);
+  std::vector<uint8_t *> d(ntb);
+  for (uint32_t i = 0; i < ntb; i++) {
+    const uint32_t Qm = tb[i].Qm, cols = tb[i].nof_symb;
+    E.h_ul[i] = UlItem{tb[i].q_offset, tb[i].nof_bits / Qm / cols, cols, Qm};
+    max_bits = std::max(max_bits, tb[i].nof_bits);
+    // G = nb_q / Qm - Q'_ri - Q'_cqi with no UCI: every coded bit is data (sch.c:976-979)
+    dl[i] = srsgpu_dlsch_tb_t{tb[i].tbs, tb[i].rv, Qm, tb[i].nof_bits, tb[i].softbuffer,
+                              tb[i].q_offset, tb[i].data_offset};
+    e[i] = d_g + tb[i].q_offset;
+    d[i] = d_data + tb[i].data_offset;
+  }
+  HIPCHK(hipMemcpyAsync(E.d_ul, E.h_ul, sizeof(UlItem) * ntb, hipMemcpyHostToDevice, E.st));
+  {
+    ProfScope ps("k_ulsch_deinterleave", E.st);
+    HIPCHK(launch_ulsch_deinterleave(E.d_ul, (int)ntb, max_bits, d_q, d_g, E.st));
+  }
+  // decode() waits for this copy (its own staging reuses the event after recording it)
+  HIPCHK(hipEventRecord(E.staged, E.st));
+  E.staged_pending = true;
+  return E.decode(dl.data(), ntb, e.data(), d.data(), maxh, d_ret, d_noi);
 }
 
 int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,

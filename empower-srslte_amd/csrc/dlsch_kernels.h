@@ -58,5 +58,13 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
 // crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
 hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
                                const uint32_t *crc_b, hipStream_t st);
+// UL-SCH channel deinterleaver (sch.c:550-568,860-881) of one TB per blockIdx.y: g[(j cols + i) Qm
+// + k] = q[(i rows + j) Qm + k] for row j < rows, column i < cols, bit k < Qm
+struct UlItem {
+  uint64_t q_offset;
+  uint32_t rows, cols, Qm;
+};
+hipError_t launch_ulsch_deinterleave(const UlItem *d_items, int n, uint32_t max_bits, const int16_t *q,
+                                     int16_t *g, hipStream_t st);
 } // namespace srsgpu
 #endif

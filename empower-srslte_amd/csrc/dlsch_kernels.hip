@@ -268,6 +268,32 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ UL-SCH ----
+// ulsch_deinterleave (sch.c:860-881) without RI bits: ulsch_interleave_gen numbers the entries
+// (row j, column i, bit k) row by row, entry (j, i, k) sits at q index (i rows + j) Qm + k, and
+// srslte_vec_lut_sis writes g[lut[x]] = q[x]. One thread per g element (coalesced stores, the
+// gathered reads are rows x Qm apart).
+__global__ __launch_bounds__(256) void k_ulsch_deinterleave(const UlItem *__restrict__ items,
+                                                            const int16_t *__restrict__ q,
+                                                            int16_t *__restrict__ g) {
+  const UlItem it = items[blockIdx.y];
+  const uint32_t n = it.rows * it.cols * it.Qm;
+  const uint32_t x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= n) return;
+  const uint32_t rowlen = it.cols * it.Qm;
+  const uint32_t j = x / rowlen, r = x - j * rowlen;
+  const uint32_t i = r / it.Qm, k = r - i * it.Qm;
+  g[it.q_offset + x] = q[it.q_offset + (size_t)(i * it.rows + j) * it.Qm + k];
+}
+
+hipError_t launch_ulsch_deinterleave(const UlItem *d_items, int n, uint32_t max_bits, const int16_t *q,
+                                     int16_t *g, hipStream_t st) {
+  if (n <= 0 || max_bits == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ulsch_deinterleave, dim3((max_bits + 255) / 256, (unsigned)n), dim3(256), 0, st,
+                     d_items, q, g);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ transmit ----
 // encode_tb_off (sch.c:187-296) for one code block per workgroup: the code block's bits are
 // assembled in LDS (TB bits, the TB CRC24A on the last block, the CB CRC24B when C > 1; both

@@ -553,10 +553,42 @@ struct TdecEngine {
     return 0;
   }
 
-  // early-stop decoding of one pass (planned groups) — maxh half-iterations at most
+  // early-stop decoding of one pass (planned groups) — maxh half-iterations at most. The windowed
+  // kinds run every half-iteration with its CRC check in one launch each (k_win_bidir_es); the
+  // sequential decoders (K <= 400 under AUTO, GENERIC) one launch per half-iteration plus a
+  // decide launch, which skips the pairs the fused launches finished.
+  // SRSGPU_TDEC_FUSED=0 selects the per-half-iteration launches everywhere (A/B measurements).
   int decode_planned(uint32_t maxh, uint8_t *d_out, size_t out_stride) {
+    static const bool fused = [] {
+      const char *e = getenv("SRSGPU_TDEC_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    bool seq = false;
+    const TdArrays a = arrays();
+    const TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh};
+    for (int k = 0; k < TD_NKIND; k++) {
+      const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+      if (g1 <= g0) continue;
+      if (fused && halfits_fusable(k)) {
+        ProfScope ps("k_win_bidir_es", st);
+        HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+      } else {
+        seq = true;
+      }
+    }
+    last_n = (int)maxh - 1;
+    if (!seq) return 0;
     for (uint32_t h = 0; h < maxh; h++) {
-      if (halfit((int)h, true)) return -1;
+      last_n = (int)h;
+      for (int k = 0; k < TD_NKIND; k++) {
+        const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+        if (g1 <= g0 || (fused && halfits_fusable(k))) continue;
+        static const char *const names[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
+                                                     "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
+        ProfScope ps(names[k], st);
+        HIPCHK(launch_halfit((int)h, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a,
+                             pair_done, st));
+      }
       if (decide((int)h, d_out, out_stride, true, maxh)) return -1;
     }
     return 0;

@@ -85,6 +85,20 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
 bool halfits_fusable(int kind);
 hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, int nblocks,
                           size_t lds, bool dec, const TdArrays &a, hipStream_t st);
+// Early-stop state of k_win_bidir_es (sch.c:361-391 per code block): natural-order decision
+// bytes, done / ok flags and the half-iteration count of every CB in the caller's numbering.
+struct TdEs {
+  uint8_t *outb;
+  size_t out_stride;
+  uint8_t *cb_done, *cb_ok;
+  uint32_t *noi;
+  int max_halfits;
+};
+// every half-iteration of an early-stop job for the groups of one windowed kind in one launch:
+// the CRC after each half-iteration, done / ok / noi and the decision bytes of finished blocks
+// as launch_decide with early = true does, workgroups leave when all their blocks are done
+hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
+                             const TdArrays &a, const TdEs &es, hipStream_t st);
 // hard decision after half-iteration n for every pair of the job (npairs in total); early: also
 // the CRC, cb_done / cb_ok / noi and pair_done (turbodecoder.c:353-360, sch.c:361-391)
 hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,

@@ -1117,6 +1117,211 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
   }
 }
 
+// After half-iteration n of the workgroup's pairs (their decision words in D, written by this
+// workgroup before the barrier): the CRC of every unfinished code block, as k_decide folds it
+// (crc.c:144-155 is linear: XOR of the chain-major weights TdGroup::wc over the set decision
+// bits), the done / ok / noi update of sch.c:361-391, and the natural-order bytes of the blocks
+// that end at this half-iteration. Returns (uniformly) whether every block of the workgroup is done.
+template <int NB>
+__device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const uint32_t *__restrict__ Darr,
+                                      const TdEs &es, uint32_t *red, int *fin) {
+  constexpr int NP = 64 / NB; // pairs per workgroup
+  const int K = G.K;
+  const int pw = (blk * 64) / NB;
+  const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
+  const bool dec2 = n & 1;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const gptr_t<uint32_t> wc = gptr(G.wc[dec2 ? 1 : 0]);
+  // per pair: done flags after the previous half-iteration (fin bit 0; finished blocks are skipped)
+  bool skip[NP][2];
+#pragma unroll
+  for (int lp = 0; lp < NP; lp++) {
+    skip[lp][0] = fin[2 * lp] & 1;
+    skip[lp][1] = fin[2 * lp + 1] & 1;
+  }
+#pragma unroll
+  for (int lp = 0; lp < NP; lp++) {
+    uint32_t c0 = 0, c1 = 0;
+    if (!(skip[lp][0] && skip[lp][1])) {
+      const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
+      for (int q = t; q < nw; q += 128) {
+        const uint32_t w = dw[q];
+        if (w == 0u) continue;
+        const gptr_t<u4> wq = (gptr_t<u4>)(wc + (size_t)q * 16);
+        uint32_t wt[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const u4 v = wq[i];
+          wt[4 * i] = v[0];
+          wt[4 * i + 1] = v[1];
+          wt[4 * i + 2] = v[2];
+          wt[4 * i + 3] = v[3];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          c0 ^= ((w >> j) & 1u) ? wt[j] : 0u;
+          c1 ^= ((w >> (16 + j)) & 1u) ? wt[j] : 0u;
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 ^= __shfl_xor(c0, o);
+      c1 ^= __shfl_xor(c1, o);
+    }
+    if (lane == 0) {
+      red[(lp * 2 + 0) * 2 + wv] = c0;
+      red[(lp * 2 + 1) * 2 + wv] = c1;
+    }
+  }
+  __syncthreads();
+  if (t < 2 * NP) {
+    const int lp = t >> 1, h = t & 1;
+    int done = 1, now = 0;
+    if (!skip[lp][h]) {
+      const int cb = G.cb0 + 2 * (pw + lp) + h;
+      const uint32_t crc = red[t * 2] ^ red[t * 2 + 1];
+      es.noi[cb] = (uint32_t)(n + 1);
+      if (crc == 0u) {
+        es.cb_ok[cb] = 1;
+        es.cb_done[cb] = 1;
+        now = 1;
+      } else if (n + 1 >= es.max_halfits) {
+        es.cb_done[cb] = 1;
+        now = 1;
+      } else {
+        done = 0;
+      }
+    }
+    fin[t] = done | (now << 1);
+  }
+  __syncthreads();
+  // natural-order bytes (turbodecoder.c:353-360 + decision_byte, MSB first) of the blocks that
+  // ended now: 64 consecutive positions per ballot, as k_decide
+  const gptr_t<uint16_t> dmap = gptr(G.dmap);
+  const float invL = 1.0f / (float)L;
+  const int gap = 16 * G16 - L;
+  bool all = true;
+#pragma unroll
+  for (int lp = 0; lp < NP; lp++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int f = fin[lp * 2 + h];
+      all = all && (f & 1);
+      if (!(f & 2)) continue;
+      const int cb = G.cb0 + 2 * (pw + lp) + h;
+      const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
+      uint8_t *ob = es.outb + (size_t)cb * es.out_stride;
+      for (int p0 = wv * 64; p0 < K; p0 += 128) {
+        const int p = p0 + lane;
+        uint32_t bit = 0u;
+        if (p < K) {
+          int ci;
+          if (dec2) {
+            ci = (int)dmap[p];
+          } else {
+            const int d = (int)(((float)p + 0.5f) * invL);
+            ci = p + d * gap;
+          }
+          bit = (dw[ci >> 4] >> ((ci & 15) + 16 * h)) & 1u;
+        }
+        const uint64_t m = __ballot(bit);
+        if (lane < 8 && p0 + 8 * lane < K) {
+          const uint32_t v = (uint32_t)((m >> (8 * lane)) & 0xffu);
+          ob[(p0 >> 3) + lane] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
+        }
+      }
+    }
+  }
+  return all;
+}
+
+// The early-stop form of k_win_bidir_run (the DL-SCH path: srslte_tdec_iteration + CRC check per
+// half-iteration, sch.c:361-391): up to max_halfits half-iterations in ONE launch; after each one
+// the workgroup checks the CRC of its own code blocks (es_check) and leaves once all of them are
+// done, so a batch at high SNR costs the half-iterations its blocks need and no decide launches.
+// Blocks done at entry (HARQ retransmissions whose CRC passed before, cb_done seeded) are
+// skipped; a partly finished workgroup decodes on, its finished blocks' results stay frozen.
+template <int NB, int DIV, bool B8>
+__global__ __launch_bounds__(128) void k_win_bidir_es(const TdGroup *__restrict__ groups, int ngroups,
+                                                      const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                      s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                      const s2 *__restrict__ T, size_t plane, TdEs es) {
+  extern __shared__ s4 cks[];
+  __shared__ uint32_t red[(64 / NB) * 2 * 2];
+  __shared__ int fin[(64 / NB) * 2];
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K_ = G.K, npairs = G.npairs;
+  const int blk = blockIdx.x - G.blk_half;
+  // fin[2 lp + h]: bit 0 = CB h of the workgroup's pair lp is done (seeded from cb_done: HARQ
+  // blocks that passed earlier; absent blocks count as done), bit 1 = it ended at this check
+  if (threadIdx.x < 2 * (64 / NB)) {
+    const int p = (blk * 64) / NB + (threadIdx.x >> 1), h = threadIdx.x & 1;
+    fin[threadIdx.x] = (p >= npairs || 2 * p + h >= G.ncb || es.cb_done[G.cb0 + 2 * p + h]) ? 1 : 0;
+  }
+  __syncthreads();
+  {
+    bool all_done = true;
+    for (int i = 0; i < 2 * (64 / NB); i++) all_done = all_done && (fin[i] & 1);
+    if (all_done) return;
+  }
+  const int lane_ = threadIdx.x & 63;
+  const int gl = blk * 64 + lane_;
+  const int nlanes = npairs * NB;
+  const int g = gl < nlanes ? gl : nlanes - 1;
+  const int pair = g / NB;
+  const int d_ = g % NB;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K_, NB);
+  const s4 *sp0_ = SP0 + base;
+  s2 *xp1_ = XP1 + base;
+  const s2 *p1_ = XP1 + plane + base;
+  s2 *A_ = Aarr + base;
+  uint32_t *D_ = Darr + G.dw0 + (size_t)pair * dec_words(K_, NB);
+  const s2 *tl_ = T + (size_t)(G.pair0 + pair) * 12;
+  const int pe = t4_pair_elems(K_, NB), pw = (blk * 64) / NB;
+  const size_t wb = (size_t)G.elem0 + (size_t)pw * pe;
+  const s4 *wsp0_ = SP0 + wb;
+  s2 *wx2_ = XP1 + wb, *wa_ = Aarr + wb;
+  const s2 *wp1_ = XP1 + plane + wb;
+  const uint32_t po_ = (uint32_t)((pair - pw) * pe) * 4u;
+  const uint16_t *fwd0 = G.fwd, *rev0 = G.rev;
+  for (int n = 0; n < es.max_halfits; n++) {
+    if (n > 0) __syncthreads();
+    // opaque loop-invariant copies, global address space (see k_win_bidir_run)
+    gptr_t<s4> gsp0 = gptr(sp0_);
+    gmut_t<s2> gxp1 = gmut<s2>(xp1_), gA = gmut<s2>(A_);
+    gptr_t<s2> gp1 = gptr(p1_), gtl = gptr(tl_);
+    gmut_t<uint32_t> gD = gmut<uint32_t>(D_);
+    gptr_t<uint16_t> fwd = gptr(fwd0), rev = gptr(rev0);
+    int K = K_, d = d_, lane = lane_;
+    uint32_t po = po_;
+    gptr_t<s4> wsp0 = gptr(wsp0_);
+    gptr_t<s2> wp1 = gptr(wp1_);
+    gmut_t<s2> wx2 = gmut<s2>(wx2_), wa = gmut<s2>(wa_);
+    asm volatile("" : "+v"(gsp0), "+v"(gxp1), "+v"(gA), "+v"(gp1), "+v"(gtl), "+v"(gD), "+v"(d), "+v"(lane), "+v"(po));
+    asm volatile("" : "+s"(fwd), "+s"(rev), "+s"(K), "+s"(wsp0), "+s"(wp1), "+s"(wx2), "+s"(wa));
+    WinRes R;
+    R.sp0 = mk_rsrc((const void *)wsp0);
+    R.x2 = mk_rsrc((const void *)wx2);
+    R.p1 = mk_rsrc((const void *)wp1);
+    R.a = mk_rsrc((const void *)wa);
+    R.tb = mk_rsrc((const void *)((n & 1) ? fwd : rev));
+    R.po = po;
+    const s4 *sp0 = (const s4 *)gsp0;
+    s2 *xp1 = (s2 *)gxp1, *A = (s2 *)gA;
+    const s2 *p1 = (const s2 *)gp1, *tl = (const s2 *)gtl;
+    uint32_t *D = (uint32_t *)gD;
+    if (n & 1)
+      win_bidir_body<NB, DIV, 1, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
+    else if (n == 0)
+      win_bidir_body<NB, DIV, 2, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
+    else
+      win_bidir_body<NB, DIV, 0, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
+    __syncthreads(); // the half-iteration's decision words of both waves are written
+    if (es_check<NB>(G, blk, n, Darr, es, red, fin)) break;
+  }
+}
+
 // ------------------------------------------------------------------ SSE non-window ----
 #define TD_SP 8 // steps per prefetch group of the sequential decoders: must divide 8 (every LTE K is a multiple of 8, not of 16)
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
@@ -1750,6 +1955,9 @@ hipError_t halfit_part(int mode, const TdGroup *dg, int ng, int nblocks, size_t 
 template <int KIND>
 hipError_t halfits_part(int n0, int nh, const TdGroup *dg, int ng, int nblocks, size_t lds, bool dec,
                         const TdArrays &a, hipStream_t st);
+template <int KIND>
+hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, const TdArrays &a,
+                           const TdEs &es, hipStream_t st);
 
 #define BIDIR1(nb, div, m, dout, b8)                                                               \
   do {                                                                                             \
@@ -1783,7 +1991,14 @@ hipError_t halfits_part(int n0, int nh, const TdGroup *dg, int ng, int nblocks, 
                        (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,                 \
                        (const s2 *)a.T, a.plane, n0, nh, dec ? 1 : 0);                             \
   } while (0)
-#define PART_FUNCS(KIND, HALFIT_BODY, RUN_BODY)                                                    \
+#define RUNES(nb, div, b8)                                                                         \
+  do {                                                                                             \
+    allow_big_lds((const void *)(k_win_bidir_es<nb, div, b8>));                                    \
+    hipLaunchKernelGGL((k_win_bidir_es<nb, div, b8>), dim3(nblocks), dim3(128), lds, st, dg, ng,   \
+                       (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,                 \
+                       (const s2 *)a.T, a.plane, es);                                              \
+  } while (0)
+#define PART_FUNCS(KIND, HALFIT_BODY, RUN_BODY, ES_BODY)                                           \
   template <>                                                                                      \
   hipError_t halfit_part<KIND>(int mode, const TdGroup *dg, int ng, int nblocks, size_t lds,       \
                                bool dec, const TdArrays &a, const uint8_t *pair_done,              \
@@ -1796,21 +2011,30 @@ hipError_t halfits_part(int n0, int nh, const TdGroup *dg, int ng, int nblocks, 
                                 bool dec, const TdArrays &a, hipStream_t st) {                     \
     RUN_BODY;                                                                                      \
     return hipGetLastError();                                                                      \
+  }                                                                                                \
+  template <>                                                                                      \
+  hipError_t halfits_es_part<KIND>(const TdGroup *dg, int ng, int nblocks, size_t lds,             \
+                                   const TdArrays &a, const TdEs &es, hipStream_t st) {            \
+    ES_BODY;                                                                                       \
+    return hipGetLastError();                                                                      \
   }
 
+#define NO_ES (void)dg; (void)ng; (void)nblocks; (void)lds; (void)a; (void)es; (void)st; return hipErrorInvalidValue
 #if TD_PART == 1
-PART_FUNCS(TD_KIND_W16, BIDIR(16, 0, false), RUN1(16, 0, false))
+PART_FUNCS(TD_KIND_W16, BIDIR(16, 0, false), RUN1(16, 0, false), RUNES(16, 0, false))
 #elif TD_PART == 2
-PART_FUNCS(TD_KIND_W8, BIDIR(8, 1, false), RUN1(8, 1, false))
+PART_FUNCS(TD_KIND_W8, BIDIR(8, 1, false), RUN1(8, 1, false), RUNES(8, 1, false))
 PART_FUNCS(TD_KIND_SSE, SEQ(k_sse_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
-           return hipErrorInvalidValue)
+           return hipErrorInvalidValue, NO_ES)
 PART_FUNCS(TD_KIND_GEN, SEQ(k_gen_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
-           return hipErrorInvalidValue)
+           return hipErrorInvalidValue, NO_ES)
 #elif TD_PART == 3
-PART_FUNCS(TD_KIND_B16, BIDIR(16, 1, true), RUN1(16, 1, true))
+PART_FUNCS(TD_KIND_B16, BIDIR(16, 1, true), RUN1(16, 1, true), RUNES(16, 1, true))
 #elif TD_PART == 4
-PART_FUNCS(TD_KIND_B32, BIDIR(32, 1, true), RUN1(32, 1, true))
+PART_FUNCS(TD_KIND_B32, BIDIR(32, 1, true), RUN1(32, 1, true), RUNES(32, 1, true))
 #endif
+#undef NO_ES
+#undef RUNES
 #undef PART_FUNCS
 #undef RUN1
 #undef SEQ1
@@ -1848,6 +2072,18 @@ hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, i
   case TD_KIND_W8: return halfits_part<TD_KIND_W8>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
   case TD_KIND_B16: return halfits_part<TD_KIND_B16>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
   case TD_KIND_B32: return halfits_part<TD_KIND_B32>(n0, nh, dg, ng, nblocks, lds, dec, a, st);
+  default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
+                             const TdArrays &a, const TdEs &es, hipStream_t st) {
+  if (ng <= 0 || nblocks <= 0 || es.max_halfits <= 0) return hipSuccess;
+  switch (kind) {
+  case TD_KIND_W16: return halfits_es_part<TD_KIND_W16>(dg, ng, nblocks, lds, a, es, st);
+  case TD_KIND_W8: return halfits_es_part<TD_KIND_W8>(dg, ng, nblocks, lds, a, es, st);
+  case TD_KIND_B16: return halfits_es_part<TD_KIND_B16>(dg, ng, nblocks, lds, a, es, st);
+  case TD_KIND_B32: return halfits_es_part<TD_KIND_B32>(dg, ng, nblocks, lds, a, es, st);
   default: return hipErrorInvalidValue;
   }
 }

@@ -74,6 +74,14 @@ class srsgpu_dlsch_tb_t(ctypes.Structure):
                 ("e_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64)]
 
 
+class srsgpu_ulsch_tb_t(ctypes.Structure):
+    """include/srsgpu/ulsch_batch.h"""
+    _fields_ = [("tbs", ctypes.c_uint32), ("rv", ctypes.c_uint32), ("Qm", ctypes.c_uint32),
+                ("nof_bits", ctypes.c_uint32), ("nof_symb", ctypes.c_uint32),
+                ("softbuffer", ctypes.c_uint32), ("q_offset", ctypes.c_uint64),
+                ("data_offset", ctypes.c_uint64)]
+
+
 SOFTBUFFER_SIZE = 18600
 
 
@@ -225,6 +233,8 @@ _sig = {
     "srsgpu_dlsch_softbuffer_reset": (_i32, [_vp, _u32]),
     "srsgpu_dlsch_softbuffer_reset_tbs": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_softbuffer_reset_range": (_i32, [_vp, _u32, _u32]),
+    "srsgpu_ulsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), _u32, _vp, _vp, _vp, _u32,
+                                       _vp, _vp]),
     "srsgpu_dlsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp, _u32,
                                        _vp, _vp]),
     "srsgpu_dlsch_decode": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32,
@@ -521,6 +531,15 @@ class Dlsch:
         return _lib.srsgpu_dlsch_decode_dev(self.q, arr, len(tbs_list), _vp(d_e), _vp(d_data),
                                             max_halfits, _vp(d_ret), _vp(d_noi))
 
+    def ulsch_decode_dev(self, tbs_list, d_q, d_g, d_data, max_halfits, d_ret, d_noi):
+        """srsgpu_ulsch_decode_dev (srslte_ulsch_decode): tbs_list of dicts with tbs, rv, Qm,
+        nof_bits, nof_symb, softbuffer, q_offset, data_offset"""
+        arr = (srsgpu_ulsch_tb_t * len(tbs_list))(*[
+            srsgpu_ulsch_tb_t(t["tbs"], t["rv"], t["Qm"], t["nof_bits"], t["nof_symb"], t["softbuffer"],
+                              t["q_offset"], t["data_offset"]) for t in tbs_list])
+        return _lib.srsgpu_ulsch_decode_dev(self.q, arr, len(tbs_list), _vp(d_q), _vp(d_g), _vp(d_data),
+                                            max_halfits, _vp(d_ret), _vp(d_noi))
+
     def read_cb_crc(self, slot):
         """cb_crc flags of softbuffer `slot` (the soft bits are not copied)"""
         crc = np.zeros(self.max_cb, np.uint8)
@@ -773,6 +792,13 @@ class Pdsch:
 
     def nof_re(self, sf):
         return _lib.srsgpu_pdsch_nof_re(ctypes.byref(self.cell), ctypes.byref(sf))
+
+    def read_cb_crc(self, slot, max_cb=13):
+        """cb_crc flags of softbuffer `slot` of the PDSCH's DL-SCH (srsgpu_dlsch_softbuffer_read)"""
+        crc = np.zeros(max_cb, np.uint8)
+        if _lib.srsgpu_dlsch_softbuffer_read(_vp(self.dlsch_q), slot, None, _u8(crc)) != 0:
+            raise RuntimeError("softbuffer read failed")
+        return crc
 
     def llr_dev(self, sfs, d_grid, d_ce, ant_stride, d_e, e_offsets):
         arr = make_sf_array(sfs)

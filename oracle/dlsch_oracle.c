@@ -324,3 +324,32 @@ int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Q
                           data[tbs / 8 + 2];
   return (par_rx == par_tx && par_rx) ? 0 : -1;
 }
+
+/* ---------------------------------------------------------------- UL-SCH ---------------------- */
+/* ulsch_deinterleave (sch.c:860-881) with no RI bits: ulsch_interleave_gen (:550-568) numbers the
+ * (row j, column i, bit k) entries of a rows x cols matrix of Qm-bit entries row by row and places
+ * entry (j, i, k) at q index j Qm + i rows Qm + k; srslte_vec_lut_sis then sets g[lut[x]] = q[x].
+ * rows = H' / cols with H' = nof_bits / Qm. -1 when nof_bits is not a whole matrix. */
+int orc_ulsch_deinterleave(const int16_t *q_bits, uint32_t Qm, uint32_t nof_bits, uint32_t nof_symb,
+                           int16_t *g_bits) {
+  if (Qm == 0 || nof_symb == 0 || nof_bits % (Qm * nof_symb)) return -1;
+  const uint32_t rows = nof_bits / Qm / nof_symb, cols = nof_symb;
+  uint32_t idx = 0;
+  for (uint32_t j = 0; j < rows; j++)
+    for (uint32_t i = 0; i < cols; i++)
+      for (uint32_t k = 0; k < Qm; k++) g_bits[idx++] = q_bits[j * Qm + i * rows * Qm + k];
+  return 0;
+}
+
+/* srslte_ulsch_decode -> srslte_ulsch_uci_decode with uci_data = {0}: Q'_ri = Q'_cqi = 0, so
+ * G Qm = nof_bits and decode_tb runs on the whole deinterleaved g (sch.c:956-983) */
+int orc_ulsch_decode(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_bits,
+                     uint32_t nof_symb, const int16_t *q_bits, uint8_t *data, uint32_t max_halfits,
+                     uint32_t *nof_iterations) {
+  int16_t *g = malloc((size_t)(nof_bits + 1) * sizeof(int16_t));
+  if (!g) return -1;
+  int r = orc_ulsch_deinterleave(q_bits, Qm, nof_bits, nof_symb, g);
+  if (!r) r = orc_dlsch_decode(q, tbs, rv, Qm, nof_bits, g, data, max_halfits, nof_iterations);
+  free(g);
+  return r;
+}

@@ -36,4 +36,11 @@ int orc_dlsch_decode8(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Q
 int orc_dlsch_decode(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm,
                      uint32_t nof_e_bits, const int16_t *e_bits, uint8_t *data,
                      uint32_t max_halfits, uint32_t *nof_iterations);
+/* UL-SCH (§8(f) rank 3): ulsch_deinterleave without RI bits (sch.c:550-568,860-881) and
+ * srslte_ulsch_decode (sch.c:883-889 -> :944-985 with no UCI) */
+int orc_ulsch_deinterleave(const int16_t *q_bits, uint32_t Qm, uint32_t nof_bits, uint32_t nof_symb,
+                           int16_t *g_bits);
+int orc_ulsch_decode(orc_softbuffer_t *q, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_bits,
+                     uint32_t nof_symb, const int16_t *q_bits, uint8_t *data, uint32_t max_halfits,
+                     uint32_t *nof_iterations);
 #endif

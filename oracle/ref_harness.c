@@ -244,6 +244,66 @@ int ref_dlsch_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t 
   return r;
 }
 
+/* ---------------------------------------------------------------- UL-SCH (§8(f) rank 3) ---- */
+#include "srslte/phy/phch/pusch_cfg.h"
+
+static void ref_ul_cfg(srslte_pusch_cfg_t *cfg, uint32_t tbs, uint32_t rv, uint32_t Qm,
+                       uint32_t nof_bits, uint32_t nof_symb) {
+  memset(cfg, 0, sizeof(*cfg));
+  srslte_cbsegm(&cfg->cb_segm, tbs);
+  cfg->grant.Qm = Qm;
+  cfg->nbits.nof_bits = nof_bits;
+  cfg->nbits.nof_symb = nof_symb;
+  cfg->nbits.nof_re = nof_bits / Qm;
+  cfg->rv = rv;
+}
+
+/* srslte_ulsch_encode (sch.c:987-1090, no UCI): data (tbs/8 bytes) -> packed q bits (nof_bits),
+ * the rv 0 transmission first as a HARQ process makes it (rm_turbo.c:332-343) */
+int ref_ulsch_encode(uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_bits, uint32_t nof_symb,
+                     const uint8_t *data, uint8_t *q_packed, uint32_t nof_prb) {
+  if (ref_sch_get()) return -1;
+  srslte_softbuffer_tx_t sb;
+  if (srslte_softbuffer_tx_init(&sb, nof_prb)) return -1;
+  srslte_softbuffer_tx_reset(&sb);
+  uint8_t *d = calloc(tbs / 8 + 16, 1);
+  uint8_t *g = calloc(nof_bits / 8 + 64, 1);
+  memcpy(d, data, tbs / 8);
+  int r = 0;
+  for (uint32_t pass = (rv == 0); pass < 2 && !r; pass++) {
+    srslte_pusch_cfg_t cfg;
+    ref_ul_cfg(&cfg, tbs, pass ? rv : 0, Qm, nof_bits, nof_symb);
+    memset(g, 0, nof_bits / 8 + 64);
+    r = srslte_ulsch_encode(&ref_sch, &cfg, &sb, d, g, q_packed);
+  }
+  free(d);
+  free(g);
+  srslte_softbuffer_tx_free(&sb);
+  return r;
+}
+
+/* srslte_ulsch_decode (sch.c:883-889): int16 q bits -> data, on the HARQ slot's softbuffer */
+int ref_ulsch_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_bits,
+                     uint32_t nof_symb, const int16_t *q_bits, uint8_t *data, uint32_t max_halfits,
+                     uint32_t *noi, uint8_t *cb_crc) {
+  if (ref_sch_get()) return -100;
+  if (slot < 0 || slot >= REF_NSLOT || !ref_sbrx_ready[slot]) return -100;
+  srslte_pusch_cfg_t cfg;
+  ref_ul_cfg(&cfg, tbs, rv, Qm, nof_bits, nof_symb);
+  srslte_sch_set_max_noi(&ref_sch, max_halfits);
+  int16_t *q = NULL, *g = NULL;
+  if (posix_memalign((void **)&q, 64, (nof_bits + 64) * sizeof(int16_t))) return -100;
+  if (posix_memalign((void **)&g, 64, (nof_bits + 64) * sizeof(int16_t))) return -100;
+  memcpy(q, q_bits, nof_bits * sizeof(int16_t));
+  memset(g, 0, (nof_bits + 64) * sizeof(int16_t));
+  int r = srslte_ulsch_decode(&ref_sch, &cfg, &ref_sbrx[slot], q, g, data);
+  free(q);
+  free(g);
+  *noi = srslte_sch_last_noi(&ref_sch);
+  for (uint32_t i = 0; i < cfg.cb_segm.C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
+  return r;
+}
+
 /* ---------------------------------------------------------------- PDSCH front-end ---------- */
 #include "srslte/phy/mimo/precoding.h"
 #include "srslte/phy/modem/demod_soft.h"

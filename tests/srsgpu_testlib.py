@@ -185,6 +185,30 @@ class DlschOracle:
         cb_crc = np.ctypeslib.as_array(sb.cb_crc, shape=(sb.max_cb,))[:C].copy()
         return r, data, noi.value, cb_crc
 
+    def ulsch_decode(self, sb, tbs, rv, Qm, nof_symb, q_bits, max_halfits):
+        """orc_ulsch_decode (srslte_ulsch_decode restated): -> (ret, data, noi, cb_crc)"""
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.orc_ulsch_decode.argtypes = [ctypes.POINTER(OrcSoftbuffer), u32, u32, u32, u32, u32, _i16p,
+                                       _u8p, u32, _u32p]
+        q = np.ascontiguousarray(q_bits, np.int16)
+        data = np.zeros(tbs // 8 + 8, np.uint8)
+        noi = ctypes.c_uint32(0)
+        r = L.orc_ulsch_decode(ctypes.byref(sb), tbs, rv, Qm, q.size, nof_symb, _ptr(q, _i16p),
+                               _ptr(data, _u8p), max_halfits, ctypes.byref(noi))
+        C = self.lib_segm_C(tbs)
+        cb_crc = np.ctypeslib.as_array(sb.cb_crc, shape=(sb.max_cb,))[:C].copy()
+        return r, data, noi.value, cb_crc
+
+    def ulsch_deinterleave(self, q_bits, Qm, nof_symb):
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.orc_ulsch_deinterleave.argtypes = [_i16p, u32, u32, u32, _i16p]
+        q = np.ascontiguousarray(q_bits, np.int16)
+        g = np.zeros(q.size, np.int16)
+        assert L.orc_ulsch_deinterleave(_ptr(q, _i16p), Qm, q.size, nof_symb, _ptr(g, _i16p)) == 0
+        return g
+
     def lib_segm_C(self, tbs):
         v = [ctypes.c_uint32(0) for _ in range(6)]
         self.lib.orc_cbsegm(tbs, *[ctypes.byref(x) for x in v])
@@ -259,6 +283,33 @@ class Ref(_Lib):
         crc = np.zeros(64, np.uint8)
         r = self.lib.ref_dlsch_decode(slot, tbs, rv, Qm, e.size, _ptr(e, _i16p), _ptr(data, _u8p),
                                       max_halfits, ctypes.byref(noi), _ptr(crc, _u8p))
+        C = self.cbsegm(tbs)[0]
+        return r, data, noi.value, crc[:C]
+
+
+    # ---- UL-SCH (srslte_ulsch_encode / srslte_ulsch_decode through ref_harness.c) ----
+    def ul_encode(self, tbs, rv, Qm, nbits, nof_symb, data, nof_prb=100):
+        """-> unpacked q bits (after the channel interleaver)"""
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.ref_ulsch_encode.argtypes = [u32, u32, u32, u32, u32, _u8p, _u8p, u32]
+        data = np.ascontiguousarray(data, np.uint8)
+        q = np.zeros((nbits + 7) // 8 + 8, np.uint8)
+        assert L.ref_ulsch_encode(tbs, rv, Qm, nbits, nof_symb, _ptr(data, _u8p), _ptr(q, _u8p),
+                                  nof_prb) == 0
+        return np.unpackbits(q)[:nbits]
+
+    def ul_decode(self, slot, tbs, rv, Qm, nof_symb, q_bits, max_halfits):
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.ref_ulsch_decode.argtypes = [ctypes.c_int, u32, u32, u32, u32, u32, _i16p, _u8p, u32, _u32p,
+                                       _u8p]
+        q = np.ascontiguousarray(q_bits, np.int16)
+        data = np.zeros(tbs // 8 + 8, np.uint8)
+        noi = ctypes.c_uint32(0)
+        crc = np.zeros(64, np.uint8)
+        r = L.ref_ulsch_decode(slot, tbs, rv, Qm, q.size, nof_symb, _ptr(q, _i16p), _ptr(data, _u8p),
+                               max_halfits, ctypes.byref(noi), _ptr(crc, _u8p))
         C = self.cbsegm(tbs)[0]
         return r, data, noi.value, crc[:C]
 

@@ -145,3 +145,63 @@ def test_two_rank_c5_partition_gather_gloo():
     assert sh.balance(load) <= 1.10, load
     ks = {table["cbsegm_C_C1_K1_C2_K2_F"][str(t[0])][2] for t in job}
     assert len(ks) >= 10  # mixed K
+
+
+def _rank_tm3(rank, world, port, q):
+    """BASELINE configs[3]'s multi-GPU form: a global job of TM3 subframes (two codewords each),
+    split in contiguous subframe ranges (srsgpu_shard_contiguous, as bench.py's pipeline_tm3 leg
+    splits nranks x 1024 subframes); each rank decodes its own subframes' two TBs and gathers one
+    record per subframe (the two TB records back to back) to rank 0."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(REPO, "empower-srslte_amd"))
+    import srsgpu_shard as sh
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _table, job = _job(n_tb=2 * TM3_SF, seed=7)
+        first = sh.contiguous(TM3_SF, world)
+        owner = np.repeat(np.arange(world), np.diff(first))
+        mine = range(first[rank], first[rank + 1])
+        recs = [np.concatenate(_decode(job, [2 * i, 2 * i + 1])) for i in mine]
+        local = torch.from_numpy(np.concatenate(recs) if recs else np.zeros(0, np.uint8))
+        sizes = [sh.tb_record_len(job[2 * i][0]) + sh.tb_record_len(job[2 * i + 1][0]) for i in range(TM3_SF)]
+        out = sh.gather_records(dist, torch, torch.device("cpu"), owner, sizes, local)
+        q.put((rank, None if out is None else [r.tobytes() for r in out], list(map(int, first))))
+    finally:
+        dist.destroy_process_group()
+
+
+TM3_SF = 11  # odd: the two ranks get 5 and 6 subframes
+
+
+def test_two_rank_tm3_subframe_partition_gather_gloo():
+    """The TM3 job's partition and gather over two gloo ranks (the DL-SCH decode of each codeword
+    by the CPU oracle stands in for the GPU receive chain): rank 0's gathered per-subframe records
+    equal a single-process decode of the whole job, in subframe order."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_rank_tm3, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    root = got[0]
+    assert root[0] == 0 and got[1][1] is None
+    assert root[2] == [0, 5, 11]
+    _table, job = _job(n_tb=2 * TM3_SF, seed=7)
+    import srsgpu_shard as sh
+    assert len(root[1]) == TM3_SF
+    rets = set()
+    for i, rec in enumerate(root[1]):
+        single = np.concatenate(_decode(job, [2 * i, 2 * i + 1]))
+        assert rec == single.tobytes(), i
+        n0 = sh.tb_record_len(job[2 * i][0])
+        rets.add(sh.unpack_tb_record(single[:n0], job[2 * i][0])[0])
+        rets.add(sh.unpack_tb_record(single[n0:], job[2 * i + 1][0])[0])
+    assert len(rets) > 1  # acked and failed codewords both present
