@@ -539,6 +539,88 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
             "decoded_fraction": round(float(d_dec.float().mean().item()), 3)}
 
 
+def rx_queue_leg(s, torch, dev, nsf=4096, batches=(64, 256, 1024), producers=8, snr_db=30.0):
+    """The real srsUE caller path: host threads hand single time-domain C3
+    subframes (20 MHz, MCS 28 codewords from the GPU transmitter at snr_db, copied to host memory
+    once) to the subframe batch queue (include/srsgpu/rx_queue.h) — each submission copies its
+    245 KB of samples into the queue's pinned staging — and a waiter thread collects them in
+    ticket order. Per batch size: subframes/s over nsf submissions and the per-subframe latency
+    (submit -> results written) p50 / p99. Two batches in flight: staging of batch k+1 overlaps the
+    decode of batch k."""
+    import threading
+    import srsgpu_traffic as tr
+    table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
+    m = tr.MixedCells(table, 1024, torch, dev, seed=22, snr_db=snr_db, prbs=(100,), mcs=28, full_band=True)
+    c = m.cells[0]
+    N = c["N"]
+    x_host = c["x"].cpu().numpy().reshape(c["n"], 15 * N)
+    tx = m.d_data_tx.cpu().numpy()
+    sfs = [m.tb_list[i] for i in range(c["n"])]
+    base = c["sfs"]
+    m.close()
+    out = {"workload": "c3_coded_queue_%dsf_20MHz_64QAM_tbs%d" % (nsf, C3_TBS), "snr_db": snr_db,
+           "producers": producers, "batches": {}}
+    for B in batches:
+        q = s.RxQueue(C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
+        outs = [np.zeros(C3_TBS // 8 + 6, np.uint8) for _ in range(4 * B)]
+        items = []
+        for i in range(nsf):
+            j = i % c["n"]
+            sf = base[j]
+            sf.softbuffer[0] = i % (4 * B)
+            items.append(q.item([x_host[j]], sf, [outs[i % (4 * B)]]))
+        t_sub = np.zeros(nsf)
+        t_done = np.zeros(nsf)
+        tickets = [0] * nsf
+        ready = [threading.Event() for _ in range(nsf)]
+
+        def produce(p):
+            for i in range(p, nsf, producers):
+                # a softbuffer / output slot is reused 4 B submissions later: wait for its last user
+                if i >= 4 * B:
+                    ready[i - 4 * B].wait()
+                t_sub[i] = time.perf_counter()
+                tickets[i] = q.submit(items[i])
+                ready_sub[i].set()
+
+        ready_sub = [threading.Event() for _ in range(nsf)]
+        fails = [0]
+
+        def collect():
+            for i in range(nsf):
+                ready_sub[i].wait()
+                if q.wait(tickets[i]) != 0:
+                    fails[0] += 1
+                t_done[i] = time.perf_counter()
+                ready[i].set()
+
+        # warm-up batch (kernels, tables, first-use allocations)
+        warm = [q.submit(items[i]) for i in range(min(B, nsf))]
+        q.flush()
+        assert all(q.wait(t) == 0 for t in warm)
+        th = [threading.Thread(target=produce, args=(p,)) for p in range(producers)]
+        tc = threading.Thread(target=collect)
+        t0 = time.perf_counter()
+        tc.start()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        tc.join()
+        el = time.perf_counter() - t0
+        nb, done = q.stats()
+        lat = (t_done - t_sub) * 1e3
+        acked = sum(1 for it in items[-min(nsf, 4 * B):] if it.ret[0] == 0)
+        out["batches"][str(B)] = {"subframes_per_s": round(nsf / el, 1), "latency_ms_p50": round(float(np.percentile(lat, 50)), 3),
+                                  "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
+                                  "mean_batch": round(done / max(nb, 1), 1), "failed": fails[0],
+                                  "acked_of_last": "%d/%d" % (acked, min(nsf, 4 * B))}
+        q.close()
+    del tx, sfs
+    return out
+
+
 def pcfich_cfi(s, torch, steps, nsf=4096, nof_prb=100):
     """PCFICH CFI detection: srslte_pcfich_decode_multi for nsf subframes of
     a 20 MHz 2-port cell with 2 rx antennas (transmit diversity) per launch (srsgpu_pcfich_decode_dev),
@@ -664,7 +746,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich,pdcch",
+    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich,pdcch,rxq",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
 
@@ -936,6 +1018,9 @@ def main():
     pdc = None
     if "pdcch" in legs and rank == 0:
         pdc = pdcch_receive(s, torch, max(4, args.steps // 2))
+    rxq = None
+    if "rxq" in legs and rank == 0:
+        rxq = rx_queue_leg(s, torch, dev)
     dropin = None
     if "dropin" in legs and rank == 0:
         dropin = dropin_latency(s, llr)
@@ -948,6 +1033,8 @@ def main():
         result["pcfich"] = pcf
     if rank == 0 and pdc:
         result["pdcch"] = pdc
+    if rank == 0 and rxq:
+        result["rx_queue"] = rxq
     if rank == 0 and dec8:
         result["decoder_8bit"] = dec8
     if rank == 0 and pipe:

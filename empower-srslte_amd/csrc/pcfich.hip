@@ -18,6 +18,7 @@ struct srsgpu_pcfich {
   hipEvent_t copied = nullptr; // the last descriptor upload out of h_it has finished
   bool recorded = false;
   hipStream_t last = nullptr; // stream of the last call (its kernel may still read d_it)
+  const float *d_noise = nullptr; // srsgpu_pcfich_set_noise_dev
 };
 
 // 36.211 7.2 Gold sequence, first 32 bits packed LSB first: x1 starts at 1, x2 at c_init, N_c = 1600
@@ -76,6 +77,10 @@ void srsgpu_pcfich_destroy(srsgpu_pcfich_t *q) {
   delete q;
 }
 
+void srsgpu_pcfich_set_noise_dev(srsgpu_pcfich_t *q, const float *d_noise) {
+  if (q) q->d_noise = d_noise;
+}
+
 int srsgpu_pcfich_re_map(const srsgpu_pcfich_t *q, uint32_t idx[16]) {
   if (!q || !idx) return -1;
   memcpy(idx, q->idx, sizeof(q->idx));
@@ -108,7 +113,8 @@ int srsgpu_pcfich_decode_dev(srsgpu_pcfich_t *q, const srsgpu_pcfich_sf_t *sf, u
   }
   for (uint32_t i = 0; i < nof_sf; i++) {
     if (sf[i].sf_idx > 9) return -1;
-    q->h_it[i] = {sf[i].grid_offset, sf[i].ce_offset, sf[i].sf_idx, sf[i].noise_estimate};
+    q->h_it[i] = {sf[i].grid_offset, sf[i].ce_offset, sf[i].sf_idx, sf[i].noise_estimate,
+                  q->d_noise ? q->d_noise + i : nullptr};
   }
   if (hipMemcpyAsync(q->d_it, q->h_it, sizeof(srsgpu::PcfichItem) * nof_sf, hipMemcpyHostToDevice, st) ||
       hipEventRecord(q->copied, st))

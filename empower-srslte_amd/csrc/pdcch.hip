@@ -261,6 +261,7 @@ struct srsgpu_pdcch {
   size_t cand_cap = 0;
   hipEvent_t search_done = nullptr;
   bool search_pending = false;
+  const float *d_noise = nullptr; // srsgpu_pdcch_set_noise_dev
 };
 
 extern "C" {
@@ -340,6 +341,10 @@ uint32_t srsgpu_pdcch_nof_cce(const srsgpu_pdcch_t *q, uint32_t cfi) {
   return q && cfi >= 1 && cfi <= 3 ? q->nof_cce[cfi - 1] : 0;
 }
 
+void srsgpu_pdcch_set_noise_dev(srsgpu_pdcch_t *q, const float *d_noise) {
+  if (q) q->d_noise = d_noise;
+}
+
 int srsgpu_pdcch_re_map(const srsgpu_pdcch_t *q, uint32_t cfi, uint32_t *idx, uint32_t max) {
   if (!q || cfi < 1 || cfi > 3 || !idx) return -1;
   const std::vector<uint32_t> &m = q->map[cfi - 1];
@@ -365,7 +370,8 @@ int srsgpu_pdcch_extract_llr_dev(srsgpu_pdcch_t *q, const srsgpu_pdcch_sf_t *sf,
     if (sf[i].sf_idx > 9 || cfi < 1 || cfi > 3 || (sf[i].llr_offset & 1)) return -1;
     const uint32_t nsym = 36 * q->nof_cce[cfi - 1];
     h[i] = {sf[i].grid_offset, sf[i].ce_offset, sf[i].llr_offset, q->d_map + q->map_off[cfi - 1],
-            q->d_seq + (size_t)sf[i].sf_idx * q->seq_words, nsym, sf[i].noise_estimate};
+            q->d_seq + (size_t)sf[i].sf_idx * q->seq_words, nsym, sf[i].noise_estimate,
+            q->d_noise ? q->d_noise + i : nullptr};
     if (nsym > max_sym) max_sym = nsym;
   }
   if (hipMemcpyAsync(s.d, s.h, sizeof(srsgpu::PdcchItem) * nof_sf, hipMemcpyHostToDevice, st) ||

@@ -184,7 +184,9 @@ struct PdschEngine {
 
   // TBs of a call in order: (subframe, tb); tb t of a CDD subframe sits on codeword
   // cw = t ^ tb_cw_swap (pdsch.c:959-995)
-  static uint32_t nof_tb(const srsgpu_pdsch_sf_t &s) { return s.mimo_type == SRSGPU_MIMO_CDD ? 2 : 1; }
+  static uint32_t nof_tb(const srsgpu_pdsch_sf_t &s) {
+    return s.mimo_type == SRSGPU_MIMO_CDD || (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.tbs[1] > 0) ? 2 : 1;
+  }
 
   int check(const srsgpu_pdsch_sf_t &s, uint32_t i) {
     const uint32_t nt = nof_tb(s);
@@ -209,6 +211,16 @@ struct PdschEngine {
       if (cell.nof_ports != 2 || cell.nof_rx_ant != 2) {
         fprintf(stderr, "Error predecoding CCD: Invalid combination of ports %u and rx antennax %u\n",
                 cell.nof_ports, cell.nof_rx_ant);
+        return -1;
+      }
+    } else if (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX) { // precoding.c:1715-1760
+      // the 2x2 MMSE and 2x1 MRC equalisers read both rx antennas
+      if (cell.nof_ports != 2 || cell.nof_rx_ant != 2) {
+        fprintf(stderr, "srsgpu: spatial multiplexing on the GPU needs 2 ports and 2 rx antennas\n");
+        return -1;
+      }
+      if (s.codebook_idx > (nof_tb(s) == 2 ? 2u : 3u)) { // precoding.c:1350-1352, :1581-1583
+        fprintf(stderr, "Wrong codebook_idx=%u\n", s.codebook_idx);
         return -1;
       }
     } else {
@@ -262,6 +274,8 @@ struct PdschEngine {
         t.nrx = (int)cell.nof_rx_ant;
         t.nports = (int)cell.nof_ports;
         t.cdd = s.mimo_type == SRSGPU_MIMO_CDD;
+        if (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX)
+          t.mux = nt == 2 ? 1 + (int)s.codebook_idx : -(1 + (int)s.codebook_idx);
         t.txdiv = s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY;
         t.layer = (int)cw;
         t.csi_mode = csi ? 1 : 0;

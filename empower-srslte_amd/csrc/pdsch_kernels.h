@@ -27,6 +27,8 @@ struct LlrItem {
   uint32_t nof_re;
   int qm, mod, nrx, csi_mode;
   int cdd, layer;          // TM3 CDD 2x2 MMSE: this TB's codeword / layer (0 or 1)
+  int mux;                 // TM4 spatial multiplexing: 1 + codebook_idx (2 layers: 2x2 MMSE) or
+                           // -(1 + codebook_idx) (1 layer: 2x1 MRC); 0 otherwise
   int txdiv;               // TM2 transmit diversity, 2 ports (SFBC over RE pairs), 1-2 rx
   int aligned;             // e is 4-byte aligned: LLR pairs stored as 32-bit words
   float noise, inv_scaling, scaling;
@@ -57,6 +59,7 @@ struct PcfichItem {
   uint64_t grid_off, ce_off; // this subframe's [rx] grid planes / [rx][port] estimate planes
   uint32_t sf_idx;
   float noise;
+  const float *dnoise; // non-null: the noise estimate in device memory (overrides noise)
 };
 // idx: the 16 RE indices of symbol 0; seq[sf]: the 32 scrambling bits of subframe sf
 hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, const float2 *ce,
@@ -69,6 +72,7 @@ struct PdcchItem {
   const uint32_t *c;                  // the subframe's scrambling bits, packed LSB first
   uint32_t nof_symbols;               // 36 NOF_CCE(cfi)
   float noise;                        // the noise_estimate argument
+  const float *dnoise;                // non-null: the noise estimate in device memory (overrides noise)
 };
 hipError_t launch_pdcch_llr(const PdcchItem *d_items, int n, uint32_t max_symbols, const float2 *grid,
                             const float2 *ce, size_t ant_stride, int nports, int nrx, float *llr,

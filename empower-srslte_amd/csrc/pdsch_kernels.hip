@@ -140,11 +140,28 @@ __device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
 // alternates per RE (even: H = [[h00+h10, h00-h10], [h01+h11, h01-h11]] with h[port][rx], odd: the
 // columns swap); MMSE row `layer` of B = (H'H + n0 I)^-1 (2/scaling), then x = (B H') y
 // (srslte_mat_2x2_mmse_csi_gen, mat.c:63-98) and csi = 1 / Re(B[layer][layer]).
+// TM4 spatial multiplexing with two layers (srslte_predecoding_multiplex_2x2_mmse(_csi),
+// precoding.c:1331-1542) is the same MMSE with the codebook's fixed precoder: codebook 0
+// H = [[h00, h10], [h01, h11]] (norm sqrt 2 / scaling), 1 [[h00+h10, h00-h10], [h01+h11, h01-h11]],
+// 2 [[h00+j h10, h00-j h10], [h01+j h11, h01-j h11]] (norm 2 / scaling), j h = (-h.i, h.r) exactly.
+__device__ __forceinline__ cf c_mulj(cf a) { return {-a.i, a.r}; }
 __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint32_t j) {
   const cf p00 = c_ld(t.h[0][0], pos), p01 = c_ld(t.h[0][1], pos);
   const cf p10 = c_ld(t.h[1][0], pos), p11 = c_ld(t.h[1][1], pos);
   cf h00, h01, h10, h11;
-  if ((j & 1) == 0) {
+  float norm = 2.0f / t.scaling;
+  if (t.mux == 1) { // codebook 0
+    h00 = p00;
+    h01 = p10;
+    h10 = p01;
+    h11 = p11;
+    norm = 1.41421354f / t.scaling; // (float) M_SQRT2 / scaling
+  } else if (t.mux == 3) { // codebook 2
+    h00 = c_add(p00, c_mulj(p10));
+    h01 = c_sub(p00, c_mulj(p10));
+    h10 = c_add(p01, c_mulj(p11));
+    h11 = c_sub(p01, c_mulj(p11));
+  } else if (t.mux == 2 || (j & 1) == 0) { // codebook 1, or the even CDD REs
     h00 = c_add(p00, p10);
     h10 = c_add(p01, p11);
     h01 = c_sub(p00, p10);
@@ -165,7 +182,6 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint3
   const cf det = c_sub(c_mul(a00, a11), c_mul(a01, a10));
   const float m2 = det.r * det.r + det.i * det.i;
   const cf rcp = {det.r / m2, -det.i / m2};
-  const float norm = 2.0f / t.scaling;
   const cf nrm = {norm * rcp.r, norm * rcp.i};
   cf bd, bo; // diagonal and off-diagonal entries of row `layer` of B
   if (t.layer == 0) {
@@ -186,6 +202,41 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint3
   e.xr = x.r;
   e.xi = x.i;
   e.csi = 1.0f / bd.r;
+  return e;
+}
+
+// TM4 spatial multiplexing with one layer: 2x1 MRC (srslte_predecoding_multiplex_2x1_mrc(_csi),
+// precoding.c:1546-1713) in the order of the reference's C loop: h0 / h1 = the codebook's
+// combination of the two ports at rx 0 / 1 (0: h0+h1, 1: h0-h1, 2: h0+j h1, 3: h0-j h1),
+// hh = norm / (|h0|^2 + |h1|^2) summed left to right, x = (conj(h0) y0 + conj(h1) y1) hh,
+// csi = (|h0|^2 + |h1|^2) / norm * (float) M_SQRT1_2, norm = (float) M_SQRT2 / scaling.
+__device__ __forceinline__ Eq equalise_mrc(const LlrItem &t, uint32_t pos) {
+  const int cb = -t.mux - 1;
+  const cf p00 = c_ld(t.h[0][0], pos), p01 = c_ld(t.h[0][1], pos);
+  const cf p10 = c_ld(t.h[1][0], pos), p11 = c_ld(t.h[1][1], pos);
+  cf h0, h1;
+  if (cb == 0) {
+    h0 = c_add(p00, p10);
+    h1 = c_add(p01, p11);
+  } else if (cb == 1) {
+    h0 = c_sub(p00, p10);
+    h1 = c_sub(p01, p11);
+  } else if (cb == 2) {
+    h0 = c_add(p00, c_mulj(p10));
+    h1 = c_add(p01, c_mulj(p11));
+  } else {
+    h0 = c_sub(p00, c_mulj(p10));
+    h1 = c_sub(p01, c_mulj(p11));
+  }
+  const float norm = 1.41421354f / t.scaling;
+  const float s = h0.r * h0.r + h0.i * h0.i + h1.r * h1.r + h1.i * h1.i;
+  const float hh = norm / s;
+  const cf y0 = c_ld(t.y[0], pos), y1 = c_ld(t.y[1], pos);
+  const cf x = c_add(c_mul(c_conj(h0), y0), c_mul(c_conj(h1), y1));
+  Eq e;
+  e.xr = x.r * hh;
+  e.xi = x.i * hh;
+  e.csi = s / norm * 0.707106769f; // (float) M_SQRT1_2
   return e;
 }
 
@@ -383,7 +434,10 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
     const uint32_t pos = t.map[j];
-    const Eq e = t.txdiv ? equalise_txdiv(t, j) : t.cdd ? equalise_cdd(t, pos, j) : equalise(t, pos, j);
+    const Eq e = t.txdiv ? equalise_txdiv(t, j)
+                 : (t.cdd || t.mux > 0) ? equalise_cdd(t, pos, j)
+                 : t.mux < 0 ? equalise_mrc(t, pos)
+                             : equalise(t, pos, j);
     int16_t o[Q];
     if (t.llr8)
       demap8(MOD, j, t.nof_re, e.xr, e.xi, o);
@@ -575,7 +629,7 @@ __global__ __launch_bounds__(64) void k_pcfich(const PcfichItem *__restrict__ it
   t.map = idx;
   t.nof_re = 16;
   t.nrx = nrx;
-  t.noise = it.noise;
+  t.noise = it.dnoise ? *it.dnoise : it.noise;
   t.scaling = 1.0f;
   t.inv_scaling = 1.0f;
   if (j < 16) {
@@ -640,7 +694,7 @@ __global__ __launch_bounds__(256) void k_pdcch_llr(const PdcchItem *__restrict__
   t.map = it.map;
   t.nof_re = it.nof_symbols;
   t.nrx = nrx;
-  t.noise = nports == 2 ? 0.f : it.noise / 2;
+  t.noise = nports == 2 ? 0.f : (it.dnoise ? *it.dnoise : it.noise) / 2;
   t.scaling = 1.0f;
   t.inv_scaling = 1.0f;
   const Eq e = nports == 2 ? equalise_txdiv(t, j) : equalise(t, it.map[j], j);

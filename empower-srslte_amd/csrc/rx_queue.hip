@@ -1,8 +1,18 @@
 // Subframe batch queue (include/srsgpu/rx_queue.h): PHY-worker threads submit single subframes,
-// one dispatcher thread runs them through OFDM -> channel estimation -> PDSCH / DL-SCH in batches
-// (the GPU counterpart of srsUE's per-subframe worker pool, srsue/src/phy/phy.cc:141-168,
-// phch_worker.cc:548-806).
+// batches of them run through OFDM -> channel estimation -> [PCFICH -> PDCCH search -> grant] ->
+// PDSCH / DL-SCH (the GPU counterpart of srsUE's per-subframe worker pool,
+// srsue/src/phy/phy.cc:141-168, phch_worker.cc:548-806, and of srslte_ue_dl_decode_rnti,
+// lib/src/phy/ue/ue_dl.c:467-620).
+//
+// Two batches in flight. Submissions fill one of two staging slots: the submitting worker copies
+// its time-domain samples into the slot's pinned buffer itself (the copies of many workers run in
+// parallel). A closer thread closes the filling slot (max_batch subframes, the oldest waited
+// max_wait_us, or a flush), switches the workers to the other slot as soon as that one is free,
+// waits for the closed slot's copies and starts its host-to-device transfer on a copy stream. The
+// dispatcher thread runs the closed batches in order on the compute stream, each after its
+// transfer's event. So the staging (host copies + DMA) of batch k+1 overlaps the decode of batch k.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -15,8 +25,11 @@
 #include <vector>
 
 #include "srsgpu/chest_batch.h"
+#include "srsgpu/dci.h"
 #include "srsgpu/dlsch_batch.h"
 #include "srsgpu/ofdm_batch.h"
+#include "srsgpu/pcfich_batch.h"
+#include "srsgpu/pdcch_batch.h"
 #include "srsgpu/pdsch_batch.h"
 #include "srsgpu/rx_queue.h"
 
@@ -31,10 +44,14 @@ namespace {
     }                                                                                              \
   } while (0)
 
+// one queued subframe: a grant item or a ue_dl item
 struct Pending {
   srsgpu_rxq_item_t *it;
+  srsgpu_rxq_ue_dl_t *ue;
   uint64_t ticket;
   std::chrono::steady_clock::time_point t;
+  const void *td(int a) const { return it ? it->td[a] : ue->td[a]; }
+  uint32_t sf_idx() const { return it ? it->sf.sf_idx : ue->tti % 10; }
 };
 
 // PSS / EMPTY noise (chest_dl.c:628-637): only subframes 0 and 5 estimate the noise; every other
@@ -55,35 +72,89 @@ __global__ void k_noise_carry(float *__restrict__ noise, const uint8_t *__restri
   last[c] = v;
 }
 
+// srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750) of the listed subframes, in the
+// reference's float order: per antenna the sum over ports / nports, summed over antennas, / nrx
+__global__ void k_sf_noise(const float *__restrict__ noise, const uint32_t *__restrict__ sel, int n, int nrx,
+                           int nports, float *__restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const float *v = noise + (size_t)sel[j] * nrx * nports;
+  float s = 0.f;
+  for (int a = 0; a < nrx; a++) {
+    float acc = 0.f;
+    for (int p = 0; p < nports; p++) acc += v[a * nports + p];
+    s += acc / (float)nports;
+  }
+  out[j] = nrx ? s / (float)nrx : s;
+}
+
+// noise rows (nrx * nports values) of the listed subframes, packed in list order: the PDSCH call of
+// a batch where some subframes carry no PDSCH reads its noise by call position
+__global__ void k_noise_gather(const float *__restrict__ noise, const uint32_t *__restrict__ sel, int n, int cols,
+                               float *__restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n * cols) return;
+  out[j] = noise[(size_t)sel[j / cols] * cols + j % cols];
+}
+
+// transport blocks of a PDSCH subframe (srsgpu/pdsch_batch.h)
+uint32_t sf_ntb(const srsgpu_pdsch_sf_t &s) {
+  return s.mimo_type == SRSGPU_MIMO_CDD || (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.tbs[1] > 0) ? 2 : 1;
+}
+
 } // namespace
 
 struct srsgpu_rxq {
   srsgpu_cell_t cell{};
   uint32_t N = 0, max_batch = 0, max_wait_us = 0, max_halfits = 8, nports = 1, nrx = 1;
+  uint32_t phich_len = 0, phich_res = 2;
   size_t td_len = 0, gsz = 0, dlen = 0; // complex samples per antenna / grid elements / TB bytes
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr, cst = nullptr; // compute / copy streams
   srsgpu_ofdm_t *ofdm = nullptr;
   srsgpu_chest_t *chest = nullptr;
   srsgpu_pdsch_t *pdsch = nullptr;
-  float *d_td = nullptr, *d_grid = nullptr, *d_ce = nullptr, *d_noise = nullptr;
+  srsgpu_pcfich_t *pcfich = nullptr;
+  srsgpu_pdcch_t *pdcch = nullptr; // created with the PHICH configuration on the first ue_dl batch
+  float *d_grid = nullptr, *d_ce = nullptr, *d_noise = nullptr;
   float *d_noise_last = nullptr; // PSS / EMPTY: the estimate carried between batches
   uint8_t *d_est = nullptr, *h_est = nullptr; // per subframe: 1 if it estimates the noise
   uint8_t *d_data = nullptr;
   int32_t *d_ret = nullptr;
   uint32_t *d_noi = nullptr;
-  float *h_td = nullptr, *h_noise = nullptr; // pinned staging
+  float *h_noise = nullptr; // pinned result staging
   uint8_t *h_data = nullptr;
   int32_t *h_ret = nullptr;
   uint32_t *h_noi = nullptr;
+  // control channel of the ue_dl items
+  uint32_t *d_sel = nullptr, *h_sel = nullptr; // their subframe indices in the batch
+  float *d_uenoise = nullptr;                  // their noise estimates
+  uint32_t *d_who = nullptr, *h_who = nullptr; // subframes of the PDSCH call
+  float *d_pnoise = nullptr;                   // their noise rows
+  uint32_t *d_cfi = nullptr, *h_cfi = nullptr;
+  float *d_corr = nullptr, *h_corr = nullptr;
+  float *d_llr = nullptr;
+  size_t llr_stride = 0;
+  srsgpu_dci_result_t *d_res = nullptr, *h_res = nullptr;
+
+  // staging slots
+  enum { FILLING = 0, CLOSED = 1, STAGED = 2 };
+  struct Slot {
+    float *h_td = nullptr, *d_td = nullptr;
+    hipEvent_t staged = nullptr;
+    std::vector<Pending> items;
+    int state = FILLING;
+    int copying = 0; // submitters still copying their samples in
+  } slot[2];
+  int fill = 0; // the slot submissions go to
 
   std::mutex m;
-  std::condition_variable cv_work, cv_done;
-  std::deque<Pending> queue;
+  std::condition_variable cv_close, cv_ready, cv_done, cv_slot;
+  std::deque<int> ready; // staged slots, in batch order
   uint64_t next_ticket = 1, done_upto = 0; // tickets are completed in order
   std::set<uint64_t> failed;               // tickets whose batch failed, until waited for
   bool stop = false, flush = false;
   uint64_t nbatches = 0, nsf = 0;
-  std::thread worker;
+  std::thread closer, worker;
 
   int setup(const srsgpu_cell_t *c, uint32_t symbol_sz, uint32_t nsb, uint32_t mb, uint32_t wait_us,
             uint32_t maxh) {
@@ -97,16 +168,21 @@ struct srsgpu_rxq {
     td_len = (size_t)15 * N;
     gsz = (size_t)14 * 12 * cell.nof_prb;
     dlen = SRSGPU_DLSCH_DATA_LEN(75376) + 16;
+    llr_stride = 72 * 88; // 72 NOF_CCE(3) floats at most (20 MHz: 87 CCEs)
     const uint32_t max_cb = 13;
     RXQ_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    if (srsgpu_ofdm_rx_create(&ofdm, cell.nof_prb, N) ||
-        srsgpu_chest_create(&chest, &cell, mb * nrx) ||
-        srsgpu_pdsch_create(&pdsch, &cell, nsb, max_cb, mb))
+    RXQ_CHK(hipStreamCreateWithFlags(&cst, hipStreamNonBlocking));
+    if (srsgpu_ofdm_rx_create(&ofdm, cell.nof_prb, N) || srsgpu_chest_create(&chest, &cell, mb * nrx) ||
+        srsgpu_pdsch_create(&pdsch, &cell, nsb, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
       return -1;
     srsgpu_ofdm_rx_set_stream(ofdm, st);
     srsgpu_chest_set_stream(chest, st);
     srsgpu_pdsch_set_stream(pdsch, st);
-    RXQ_CHK(hipMalloc(&d_td, sizeof(float) * 2 * td_len * mb * nrx));
+    for (Slot &s : slot) {
+      RXQ_CHK(hipMalloc(&s.d_td, sizeof(float) * 2 * td_len * mb * nrx));
+      RXQ_CHK(hipHostMalloc(&s.h_td, sizeof(float) * 2 * td_len * mb * nrx));
+      RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
+    }
     RXQ_CHK(hipMalloc(&d_grid, sizeof(float) * 2 * gsz * mb * nrx));
     RXQ_CHK(hipMalloc(&d_ce, sizeof(float) * 2 * gsz * mb * nrx * nports));
     RXQ_CHK(hipMalloc(&d_noise, sizeof(float) * mb * nrx * nports));
@@ -117,12 +193,26 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMemset(d_noise_last, 0, sizeof(float) * nrx * nports)); // srslte_chest_dl_init: 0
     RXQ_CHK(hipMalloc(&d_est, mb));
     RXQ_CHK(hipHostMalloc(&h_est, mb));
-    RXQ_CHK(hipHostMalloc(&h_td, sizeof(float) * 2 * td_len * mb * nrx));
     RXQ_CHK(hipHostMalloc(&h_noise, sizeof(float) * mb * nrx * nports));
     RXQ_CHK(hipHostMalloc(&h_data, dlen * 2 * mb));
     RXQ_CHK(hipHostMalloc(&h_ret, sizeof(int32_t) * 2 * mb));
     RXQ_CHK(hipHostMalloc(&h_noi, sizeof(uint32_t) * 2 * mb));
-    worker = std::thread([this] { loop(); });
+    RXQ_CHK(hipMalloc(&d_sel, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_sel, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipMalloc(&d_uenoise, sizeof(float) * mb));
+    RXQ_CHK(hipMalloc(&d_who, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_who, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipMalloc(&d_pnoise, sizeof(float) * mb * nrx * nports));
+    RXQ_CHK(hipMalloc(&d_cfi, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_cfi, sizeof(uint32_t) * mb));
+    RXQ_CHK(hipMalloc(&d_corr, sizeof(float) * mb));
+    RXQ_CHK(hipHostMalloc(&h_corr, sizeof(float) * mb));
+    RXQ_CHK(hipMalloc(&d_llr, sizeof(float) * llr_stride * mb));
+    RXQ_CHK(hipMalloc(&d_res, sizeof(srsgpu_dci_result_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_res, sizeof(srsgpu_dci_result_t) * mb));
+    srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
+    closer = std::thread([this] { close_loop(); });
+    worker = std::thread([this] { run_loop(); });
     return 0;
   }
 
@@ -131,31 +221,253 @@ struct srsgpu_rxq {
       std::lock_guard<std::mutex> l(m);
       stop = true;
     }
-    cv_work.notify_all();
+    cv_close.notify_all();
+    cv_ready.notify_all();
+    cv_slot.notify_all();
+    if (closer.joinable()) closer.join();
     if (worker.joinable()) worker.join();
     if (ofdm) srsgpu_ofdm_rx_destroy(ofdm);
     if (chest) srsgpu_chest_destroy(chest);
     if (pdsch) srsgpu_pdsch_destroy(pdsch);
-    for (void *p : {(void *)d_td, (void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data,
-                    (void *)d_ret, (void *)d_noi, (void *)d_noise_last, (void *)d_est})
+    if (pcfich) srsgpu_pcfich_destroy(pcfich);
+    if (pdcch) srsgpu_pdcch_destroy(pdcch);
+    for (Slot &s : slot) {
+      if (s.d_td) (void)hipFree(s.d_td);
+      if (s.h_td) (void)hipHostFree(s.h_td);
+      if (s.staged) (void)hipEventDestroy(s.staged);
+    }
+    for (void *p : {(void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data, (void *)d_ret,
+                    (void *)d_noi, (void *)d_noise_last, (void *)d_est, (void *)d_sel, (void *)d_uenoise,
+                    (void *)d_cfi, (void *)d_corr, (void *)d_llr, (void *)d_res, (void *)d_who,
+                    (void *)d_pnoise})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_td, (void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est})
+    for (void *p : {(void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est,
+                    (void *)h_sel, (void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_who})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
+    if (cst) (void)hipStreamDestroy(cst);
   }
 
-  // one batch: inputs staged and copied in one transfer, three pipeline calls, one copy back
-  int run(std::vector<Pending> &b) {
+  // ---------------------------------------------------------------- submission ----
+  int submit(srsgpu_rxq_item_t *it, srsgpu_rxq_ue_dl_t *ue, uint64_t *ticket) {
+    const void *td0 = it ? it->td[0] : ue->td[0], *td1 = it ? it->td[1] : ue->td[1];
+    if (!td0 || (nrx > 1 && !td1)) return -1;
+    int s, idx;
+    {
+      std::unique_lock<std::mutex> l(m);
+      // the filling slot has room (else wait for the closer to switch to the other slot)
+      cv_slot.wait(l, [&] {
+        return stop || (slot[fill].state == FILLING && slot[fill].items.size() < max_batch);
+      });
+      if (stop) return -1;
+      s = fill;
+      idx = (int)slot[s].items.size();
+      *ticket = next_ticket++;
+      slot[s].items.push_back({it, ue, *ticket, std::chrono::steady_clock::now()});
+      slot[s].copying++;
+    }
+    cv_close.notify_one();
+    // the worker stages its own samples (outside the lock: many workers copy at once)
+    const size_t sfc = 2 * td_len;
+    memcpy(slot[s].h_td + ((size_t)idx * nrx) * sfc, td0, sizeof(float) * sfc);
+    if (nrx > 1) memcpy(slot[s].h_td + ((size_t)idx * nrx + 1) * sfc, td1, sizeof(float) * sfc);
+    {
+      std::lock_guard<std::mutex> l(m);
+      slot[s].copying--;
+    }
+    cv_close.notify_one();
+    return 0;
+  }
+
+  // closer thread: close the filling slot, switch the workers to the other one once it is free,
+  // wait for the closed slot's copies, start its transfer and hand it to the dispatcher
+  void close_loop() {
+    std::unique_lock<std::mutex> l(m);
+    for (;;) {
+      cv_close.wait(l, [this] { return stop || !slot[fill].items.empty(); });
+      if (stop) return;
+      const int s = fill;
+      const auto deadline = slot[s].items.front().t + std::chrono::microseconds(max_wait_us);
+      cv_close.wait_until(l, deadline, [&] { return stop || flush || slot[s].items.size() >= max_batch; });
+      if (stop) return;
+      flush = false;
+      slot[s].state = CLOSED;
+      // the other slot takes submissions once its batch has been decoded
+      cv_slot.wait(l, [&] { return stop || slot[s ^ 1].state == FILLING; });
+      if (stop) return;
+      fill = s ^ 1;
+      cv_slot.notify_all();
+      cv_close.wait(l, [&] { return stop || slot[s].copying == 0; });
+      if (stop) return;
+      const size_t n = slot[s].items.size();
+      l.unlock();
+      const size_t bytes = sizeof(float) * 2 * td_len * nrx * n;
+      const bool ok = hipMemcpyAsync(slot[s].d_td, slot[s].h_td, bytes, hipMemcpyHostToDevice, cst) == hipSuccess &&
+                      hipEventRecord(slot[s].staged, cst) == hipSuccess;
+      l.lock();
+      if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed\n");
+      slot[s].state = STAGED;
+      ready.push_back(ok ? s : -1 - s);
+      cv_ready.notify_one();
+    }
+  }
+
+  // dispatcher thread: decode the staged batches in order
+  void run_loop() {
+    std::unique_lock<std::mutex> l(m);
+    for (;;) {
+      cv_ready.wait(l, [this] { return stop || !ready.empty(); });
+      if (ready.empty() && stop) return;
+      const int tag = ready.front();
+      ready.pop_front();
+      const int s = tag < 0 ? -1 - tag : tag;
+      std::vector<Pending> b = slot[s].items;
+      l.unlock();
+      int r = tag < 0 ? -1 : 0;
+      if (!r) r = hipStreamWaitEvent(st, slot[s].staged, 0) == hipSuccess ? 0 : -1;
+      if (!r) r = run(b, slot[s].d_td);
+      // a failed batch may have left work in flight that reads its buffers: drain before reuse
+      if (r) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamSynchronize(cst);
+      }
+      l.lock();
+      if (r) {
+        fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", b.size());
+        for (const Pending &p : b) failed.insert(p.ticket);
+      }
+      done_upto = b.back().ticket;
+      nbatches++;
+      nsf += b.size();
+      slot[s].items.clear();
+      slot[s].state = FILLING;
+      cv_done.notify_all();
+      cv_slot.notify_all();
+    }
+  }
+
+  // ---------------------------------------------------------------- one batch ----
+  // the control channel of the batch's ue_dl items (ue_dl.c:408-433, :484-497): PCFICH on their
+  // grids with the estimator's noise, CFI back to the host, PDCCH LLRs and the DL DCI search,
+  // results back to the host
+  int control(const std::vector<Pending> &b, const std::vector<uint32_t> &ue) {
+    const uint32_t nu = (uint32_t)ue.size();
+    for (uint32_t j = 0; j < nu; j++) h_sel[j] = ue[j];
+    RXQ_CHK(hipMemcpyAsync(d_sel, h_sel, sizeof(uint32_t) * nu, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_sf_noise, dim3((nu + 63) / 64), dim3(64), 0, st, d_noise, d_sel, (int)nu, (int)nrx,
+                       (int)nports, d_uenoise);
+    RXQ_CHK(hipGetLastError());
+    std::vector<srsgpu_pcfich_sf_t> pc(nu);
+    for (uint32_t j = 0; j < nu; j++)
+      pc[j] = {(uint64_t)ue[j] * nrx * gsz, (uint64_t)ue[j] * nrx * nports * gsz, b[ue[j]].sf_idx(), 0.f};
+    if (srsgpu_pcfich_decode_dev(pcfich, pc.data(), nu, d_grid, d_ce, gsz, d_cfi, d_corr, st)) return -1;
+    RXQ_CHK(hipMemcpyAsync(h_cfi, d_cfi, sizeof(uint32_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(hipMemcpyAsync(h_corr, d_corr, sizeof(float) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(hipStreamSynchronize(st));
+    if (!pdcch) {
+      if (srsgpu_pdcch_create(&pdcch, &cell, phich_len, phich_res)) return -1;
+      srsgpu_pdcch_set_noise_dev(pdcch, d_uenoise);
+    }
+    std::vector<srsgpu_pdcch_sf_t> ps(nu);
+    std::vector<srsgpu_dci_search_t> se(nu);
+    for (uint32_t j = 0; j < nu; j++) {
+      const srsgpu_rxq_ue_dl_t *u = b[ue[j]].ue;
+      ps[j] = {(uint64_t)ue[j] * nrx * gsz, (uint64_t)ue[j] * nrx * nports * gsz, (uint64_t)j * llr_stride,
+               u->tti % 10, h_cfi[j], 0.f, 0};
+      se[j] = {(uint64_t)j * llr_stride, u->tti % 10, h_cfi[j], u->rnti, u->tm, u->rnti_type, 0};
+    }
+    if (srsgpu_pdcch_extract_llr_dev(pdcch, ps.data(), nu, d_grid, d_ce, gsz, d_llr, st) ||
+        srsgpu_pdcch_find_dl_dci_dev(pdcch, se.data(), nu, d_llr, d_res, st))
+      return -1;
+    RXQ_CHK(hipMemcpyAsync(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(hipStreamSynchronize(st));
+    return 0;
+  }
+
+  // the grant of a found DCI as srslte_ue_dl_decode_rnti configures it (ue_dl.c:498-574): unpack,
+  // redundancy versions, softbuffer resets, MIMO type of the format, srslte_pdsch_cfg_mimo's
+  // lstart / RE count. Returns 1 with sf filled (decode it), 0 (no PDSCH call), -1 (error).
+  int grant_of(srsgpu_rxq_ue_dl_t *u, const srsgpu_dci_result_t &res, uint32_t cfi, srsgpu_dlsch_t *dl,
+               srsgpu_pdsch_sf_t &sf) {
+    srsgpu_ra_dl_dci_t dci;
+    memset(&dci, 0, sizeof(dci));
+    memset(&u->grant, 0, sizeof(u->grant));
+    if (srsgpu_dci_msg_to_dl_grant(res.data, res.nof_bits, res.format, u->rnti, cell.nof_prb, cell.nof_ports, &dci,
+                                   &u->grant))
+      return -1;
+    const srsgpu_ra_dl_grant_t &g = u->grant;
+    const uint32_t ntb = (g.tb_en[0] ? 1 : 0) + (g.tb_en[1] ? 1 : 0);
+    uint32_t rv[2] = {1, 0}; // int rvidx[SRSLTE_MAX_CODEWORDS] = {1}
+    for (int i = 0; i < 2; i++) {
+      if (!g.tb_en[i]) continue;
+      if (dci.rv_idx < 0) { // 36.321 5.3.1 SI redundancy version (ue_dl.c:503-509)
+        const uint32_t k = (u->tti / 10 / 2) % 4;
+        rv[i] = ((uint32_t)ceilf(1.5f * (float)k)) % 4;
+      } else {
+        rv[i] = (uint32_t)(i == 0 ? dci.rv_idx : dci.rv_idx_1);
+      }
+      if (srsgpu_dlsch_softbuffer_reset_tbs(dl, u->softbuffer[i], (uint32_t)g.tbs[i])) return -1;
+    }
+    u->rv[0] = rv[0];
+    u->rv[1] = rv[1];
+    uint32_t mimo;
+    switch (res.format) {
+    case SRSGPU_DCI_FORMAT1:
+    case SRSGPU_DCI_FORMAT1A:
+    case SRSGPU_DCI_FORMAT1C:
+      mimo = cell.nof_ports == 1 ? SRSGPU_MIMO_SINGLE_ANTENNA : SRSGPU_MIMO_TX_DIVERSITY;
+      break;
+    case SRSGPU_DCI_FORMAT2A:
+      mimo = (ntb == 1 && dci.pinfo == 0) ? SRSGPU_MIMO_TX_DIVERSITY : SRSGPU_MIMO_CDD;
+      break;
+    case SRSGPU_DCI_FORMAT2: // spatial multiplexing unless one TB with pinfo 0
+      mimo = (ntb == 1 && dci.pinfo == 0) ? SRSGPU_MIMO_TX_DIVERSITY : SRSGPU_MIMO_SPATIAL_MULTIPLEX;
+      break;
+    default: // formats the reference does not decode (ue_dl.c:560-566)
+      return -1;
+    }
+    u->mimo_type = mimo;
+    // q->pdsch_cfg.grant.mcs[0].mod > 0 && tbs >= 0 (ue_dl.c:581)
+    if (!(g.mod[0] > 0 && g.tbs[0] >= 0)) return 0;
+    if (!g.tb_en[0] || ((mimo == SRSGPU_MIMO_CDD || (mimo == SRSGPU_MIMO_SPATIAL_MULTIPLEX && ntb == 2)) &&
+                        !g.tb_en[1])) {
+      fprintf(stderr, "srsgpu rxq: grant without transport block 0 / CDD with one TB is not on the GPU path\n");
+      return -1;
+    }
+    memset(&sf, 0, sizeof(sf));
+    sf.sf_idx = u->tti % 10;
+    sf.lstart = cell.nof_prb < 10 ? cfi + 1 : cfi; // srslte_ra_dl_grant_to_nbits (ra.c:570)
+    memcpy(sf.prb_idx, g.prb_idx, sizeof(sf.prb_idx));
+    sf.rnti = u->rnti;
+    sf.scaling = 1.0f;
+    sf.mimo_type = mimo;
+    sf.tb_cw_swap = g.tb_cw_swap;
+    if (mimo == SRSGPU_MIMO_SPATIAL_MULTIPLEX) {
+      // srslte_ue_dl_cfg_grant's pinfo -> pmi (ue_dl.c:438-456, 36.212 Table 5.3.3.1.5-4) and
+      // srslte_pdsch_cfg_mimo's codebook (pdsch.c:586-596): pmi with one TB, pmi + 1 with two
+      const uint32_t pmi = ntb == 1 ? (g.pinfo > 0 && g.pinfo < 5 ? g.pinfo - 1 : g.pinfo % 4) : g.pinfo % 2;
+      sf.codebook_idx = ntb == 1 ? pmi : pmi + 1;
+    }
+    for (int i = 0; i < 2; i++) {
+      sf.mod[i] = g.mod[i];
+      sf.tbs[i] = g.tb_en[i] ? (uint32_t)g.tbs[i] : 0;
+      sf.rv[i] = rv[i];
+      sf.softbuffer[i] = u->softbuffer[i];
+    }
+    const int nre = srsgpu_pdsch_nof_re(&cell, &sf);
+    if (nre <= 0) return -1;
+    sf.nof_re = (uint32_t)nre;
+    return 1;
+  }
+
+  // one batch: OFDM of the staged samples, channel estimation, the ue_dl items' control channel and
+  // grants, the PDSCH / DL-SCH of every subframe with a grant, one copy of the results back
+  int run(std::vector<Pending> &b, const float *d_td) {
     const uint32_t n = (uint32_t)b.size();
-    const size_t sfc = 2 * td_len; // floats per antenna plane
-    for (uint32_t i = 0; i < n; i++)
-      for (uint32_t a = 0; a < nrx; a++)
-        memcpy(h_td + (i * nrx + a) * sfc, b[i].it->td[a], sizeof(float) * sfc);
-    RXQ_CHK(hipMemcpyAsync(d_td, h_td, sizeof(float) * sfc * n * nrx, hipMemcpyHostToDevice, st));
     if (srsgpu_ofdm_rx_sf_dev(ofdm, n * nrx, d_td, td_len, d_grid, gsz)) return -1;
     std::vector<uint32_t> sfi(n * nrx);
     for (uint32_t i = 0; i < n; i++)
-      for (uint32_t a = 0; a < nrx; a++) sfi[i * nrx + a] = b[i].it->sf.sf_idx;
+      for (uint32_t a = 0; a < nrx; a++) sfi[i * nrx + a] = b[i].sf_idx();
     srsgpu_chest_cfg_t ccfg;
     if (srsgpu_chest_get_cfg(chest, &ccfg)) return -1;
     if (ccfg.noise_alg != 0 && ccfg.smooth_filter_auto) {
@@ -165,49 +477,96 @@ struct srsgpu_rxq {
     }
     if (srsgpu_chest_estimate_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise)) return -1;
     if (ccfg.noise_alg != 0) { // PSS / EMPTY: carry the estimate across subframes in order
-      for (uint32_t i = 0; i < n; i++) h_est[i] = (uint8_t)(b[i].it->sf.sf_idx == 0 || b[i].it->sf.sf_idx == 5);
+      for (uint32_t i = 0; i < n; i++) h_est[i] = (uint8_t)(b[i].sf_idx() == 0 || b[i].sf_idx() == 5);
       RXQ_CHK(hipMemcpyAsync(d_est, h_est, n, hipMemcpyHostToDevice, st));
       // grids of one subframe's rx antennas are consecutive: n rows of nrx * nports columns
       hipLaunchKernelGGL(k_noise_carry, dim3(1), dim3(64), 0, st, d_noise, d_est, (int)n, (int)(nrx * nports),
                          d_noise_last);
       RXQ_CHK(hipGetLastError());
     }
-    srsgpu_pdsch_set_noise_dev(pdsch, d_noise);
     srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(pdsch);
-    std::vector<srsgpu_pdsch_sf_t> sfs(n);
-    for (uint32_t i = 0; i < n; i++) {
-      srsgpu_pdsch_sf_t &s = sfs[i];
-      s = b[i].it->sf;
+    std::vector<uint32_t> ue;
+    for (uint32_t i = 0; i < n; i++)
+      if (b[i].ue) ue.push_back(i);
+    if (!ue.empty() && control(b, ue)) return -1;
+    // grants: the grant items' own, the ue_dl items' from their DCI
+    std::vector<srsgpu_pdsch_sf_t> sfs;
+    std::vector<uint32_t> who;       // batch index of each PDSCH subframe
+    std::vector<int> state(n, 1);    // ue_dl: 1 decode, 0 no PDSCH call, -1 error
+    for (uint32_t i = 0, j = 0; i < n; i++) {
+      srsgpu_pdsch_sf_t s;
+      if (b[i].ue) {
+        srsgpu_rxq_ue_dl_t *u = b[i].ue;
+        const srsgpu_dci_result_t &res = h_res[j];
+        u->cfi = h_cfi[j];
+        u->cfi_corr = h_corr[j];
+        u->found = res.found;
+        u->format = res.format;
+        u->L = res.L;
+        u->ncce = res.ncce;
+        u->noi[0] = u->noi[1] = 0;
+        j++;
+        if (res.found != 1) { // no DCI, or the search's error: srslte_ue_dl_decode_rnti returns 0
+          state[i] = 0;
+          continue;
+        }
+        state[i] = grant_of(u, res, u->cfi, dl, s);
+        if (state[i] != 1) continue;
+      } else {
+        s = b[i].it->sf;
+        const uint32_t ntb = sf_ntb(s);
+        for (uint32_t t = 0; t < ntb; t++)
+          if (b[i].it->reset_softbuffer[t] && srsgpu_dlsch_softbuffer_reset(dl, s.softbuffer[t])) return -1;
+      }
+      const uint32_t k = (uint32_t)sfs.size();
       s.grid_offset = (uint64_t)i * nrx * gsz;
       s.ce_offset = (uint64_t)i * nrx * nports * gsz;
-      s.data_offset[0] = (uint64_t)(2 * i) * dlen;
-      s.data_offset[1] = (uint64_t)(2 * i + 1) * dlen;
-      const uint32_t ntb = s.mimo_type == SRSGPU_MIMO_CDD ? 2 : 1;
-      for (uint32_t t = 0; t < ntb; t++)
-        if (b[i].it->reset_softbuffer[t] && srsgpu_dlsch_softbuffer_reset(dl, s.softbuffer[t]))
-          return -1;
+      s.data_offset[0] = (uint64_t)(2 * k) * dlen;
+      s.data_offset[1] = (uint64_t)(2 * k + 1) * dlen;
+      sfs.push_back(s);
+      who.push_back(i);
     }
-    // TB results come back in call order: (subframe, tb), CDD subframes holding two
-    if (srsgpu_pdsch_decode_dev(pdsch, sfs.data(), n, d_grid, d_ce, gsz, d_data, max_halfits, d_ret,
-                                d_noi))
-      return -1;
+    const uint32_t np = (uint32_t)sfs.size();
     uint32_t ntbs = 0;
-    for (uint32_t i = 0; i < n; i++) ntbs += sfs[i].mimo_type == SRSGPU_MIMO_CDD ? 2 : 1;
-    RXQ_CHK(hipMemcpyAsync(h_data, d_data, dlen * 2 * n, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipMemcpyAsync(h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipMemcpyAsync(h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
+    for (uint32_t k = 0; k < np; k++) ntbs += sf_ntb(sfs[k]);
+    if (np) {
+      srsgpu_pdsch_set_noise_dev(pdsch, d_noise);
+      // the PDSCH's per-subframe noise comes from d_noise at the subframe's position in the call:
+      // compact the noise rows of the decoded subframes when some subframes have no PDSCH
+      if (np != n) {
+        for (uint32_t k = 0; k < np; k++) h_who[k] = who[k];
+        const int cols = (int)(nrx * nports);
+        RXQ_CHK(hipMemcpyAsync(d_who, h_who, sizeof(uint32_t) * np, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_noise_gather, dim3((np * cols + 255) / 256), dim3(256), 0, st, d_noise, d_who,
+                           (int)np, cols, d_pnoise);
+        RXQ_CHK(hipGetLastError());
+        srsgpu_pdsch_set_noise_dev(pdsch, d_pnoise);
+      }
+      // TB results come back in call order: (subframe, tb), CDD subframes holding two
+      if (srsgpu_pdsch_decode_dev(pdsch, sfs.data(), np, d_grid, d_ce, gsz, d_data, max_halfits, d_ret, d_noi))
+        return -1;
+      RXQ_CHK(hipMemcpyAsync(h_data, d_data, dlen * 2 * np, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(hipMemcpyAsync(h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(hipMemcpyAsync(h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
+    }
     RXQ_CHK(hipMemcpyAsync(h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipStreamSynchronize(st));
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      srsgpu_rxq_item_t *it = b[i].it;
-      const uint32_t ntb = sfs[i].mimo_type == SRSGPU_MIMO_CDD ? 2 : 1;
-      for (uint32_t t = 0; t < ntb; t++, k++) {
-        it->ret[t] = h_ret[k];
-        it->noi[t] = h_noi[k];
-        if (it->data[t])
-          memcpy(it->data[t], h_data + (2 * i + t) * dlen, SRSGPU_DLSCH_DATA_LEN(sfs[i].tbs[t]));
+    for (uint32_t k = 0, t0 = 0; k < np; k++) {
+      const Pending &p = b[who[k]];
+      const uint32_t ntb = sf_ntb(sfs[k]);
+      for (uint32_t t = 0; t < ntb; t++, t0++) {
+        uint8_t *out = p.it ? p.it->data[t] : p.ue->data[t];
+        if (p.it) {
+          p.it->ret[t] = h_ret[t0];
+          p.it->noi[t] = h_noi[t0];
+        } else {
+          p.ue->noi[t] = h_noi[t0];
+          if (!p.ue->acks[t]) p.ue->acks[t] = h_ret[t0] == 0;
+        }
+        if (out) memcpy(out, h_data + (2 * k + t) * dlen, SRSGPU_DLSCH_DATA_LEN(sfs[k].tbs[t]));
       }
+    }
+    for (uint32_t i = 0; i < n; i++) {
       // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): mean over ports, then antennas
       float nn = 0.f;
       for (uint32_t a = 0; a < nrx; a++) {
@@ -215,40 +574,17 @@ struct srsgpu_rxq {
         for (uint32_t p = 0; p < nports; p++) acc += h_noise[(i * nrx + a) * nports + p];
         nn += acc / (float)nports;
       }
-      it->noise = nn / (float)nrx;
+      nn /= (float)nrx;
+      if (b[i].it) {
+        b[i].it->noise = nn;
+      } else {
+        srsgpu_rxq_ue_dl_t *u = b[i].ue;
+        u->noise = nn;
+        // ue_dl.c:612-616: TB 0's size when a DCI was found and the PDSCH call succeeded
+        u->ret = state[i] < 0 ? -1 : (u->found == 1 ? u->grant.tbs[0] : 0);
+      }
     }
     return 0;
-  }
-
-  void loop() {
-    std::unique_lock<std::mutex> l(m);
-    for (;;) {
-      cv_work.wait(l, [this] { return stop || !queue.empty(); });
-      if (queue.empty() && stop) return;
-      // let the batch fill: up to max_batch, or until the oldest waited max_wait_us
-      const auto deadline = queue.front().t + std::chrono::microseconds(max_wait_us);
-      cv_work.wait_until(l, deadline, [this] { return stop || flush || queue.size() >= max_batch; });
-      flush = false;
-      std::vector<Pending> b;
-      while (!queue.empty() && b.size() < max_batch) {
-        b.push_back(queue.front());
-        queue.pop_front();
-      }
-      l.unlock();
-      const int r = run(b);
-      // a failed batch may have left copies in flight that still read the pinned staging
-      // buffers: drain the stream before they are reused
-      if (r) (void)hipStreamSynchronize(st);
-      l.lock();
-      if (r) {
-        fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", b.size());
-        for (const Pending &p : b) failed.insert(p.ticket);
-      }
-      done_upto = b.back().ticket;
-      nbatches++;
-      nsf += b.size();
-      cv_done.notify_all();
-    }
   }
 };
 
@@ -278,15 +614,13 @@ void srsgpu_rxq_destroy(srsgpu_rxq_t *q) {
 }
 
 int srsgpu_rxq_submit(srsgpu_rxq_t *q, srsgpu_rxq_item_t *it, uint64_t *ticket) {
-  if (!q || !it || !ticket || !it->td[0] || (q->nrx > 1 && !it->td[1])) return -1;
-  {
-    std::lock_guard<std::mutex> l(q->m);
-    if (q->stop) return -1;
-    *ticket = q->next_ticket++;
-    q->queue.push_back({it, *ticket, std::chrono::steady_clock::now()});
-  }
-  q->cv_work.notify_one();
-  return 0;
+  if (!q || !it || !ticket) return -1;
+  return q->submit(it, nullptr, ticket);
+}
+
+int srsgpu_rxq_submit_ue_dl(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *u, uint64_t *ticket) {
+  if (!q || !u || !ticket || u->tm > 7) return -1;
+  return q->submit(nullptr, u, ticket);
 }
 
 int srsgpu_rxq_wait(srsgpu_rxq_t *q, uint64_t ticket) {
@@ -304,14 +638,32 @@ int srsgpu_rxq_decode(srsgpu_rxq_t *q, srsgpu_rxq_item_t *it) {
   return srsgpu_rxq_wait(q, t);
 }
 
+int srsgpu_rxq_decode_rnti(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *u) {
+  uint64_t t = 0;
+  if (srsgpu_rxq_submit_ue_dl(q, u, &t)) return -1;
+  return srsgpu_rxq_wait(q, t);
+}
+
+int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_resources) {
+  if (!q || phich_length > 1 || phich_resources > 3) return -1;
+  std::lock_guard<std::mutex> l(q->m);
+  q->phich_len = phich_length;
+  q->phich_res = phich_resources;
+  if (q->pdcch) { // rebuilt with the new map on the next ue_dl batch
+    srsgpu_pdcch_destroy(q->pdcch);
+    q->pdcch = nullptr;
+  }
+  return 0;
+}
+
 void srsgpu_rxq_flush(srsgpu_rxq_t *q) {
   if (!q) return;
   {
     std::lock_guard<std::mutex> l(q->m);
-    if (q->queue.empty()) return; // nothing to close: the next submission waits as usual
+    if (q->slot[q->fill].items.empty()) return; // nothing to close: the next submission waits as usual
     q->flush = true;
   }
-  q->cv_work.notify_one();
+  q->cv_close.notify_one();
 }
 
 struct srsgpu_chest *srsgpu_rxq_get_chest(srsgpu_rxq_t *q) { return q ? q->chest : nullptr; }

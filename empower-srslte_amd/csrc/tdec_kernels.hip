@@ -1890,8 +1890,9 @@ __global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int
 static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 // dynamic LDS above 64 KiB (the 8-sub-block decoder at large K) needs the per-kernel opt-in
-[[maybe_unused]] static void allow_big_lds(const void *f) {
-  (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+[[maybe_unused]] static void allow_big_lds(const void *f, int static_bytes = 0) {
+  const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - static_bytes);
+  if (e != hipSuccess) fprintf(stderr, "srsgpu: dynamic LDS opt-in failed: %s\n", hipGetErrorString(e));
 }
 
 #if TD_PART == 0
@@ -1993,7 +1994,7 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
   } while (0)
 #define RUNES(nb, div, b8)                                                                         \
   do {                                                                                             \
-    allow_big_lds((const void *)(k_win_bidir_es<nb, div, b8>));                                    \
+    allow_big_lds((const void *)(k_win_bidir_es<nb, div, b8>), 1024); /* + its static LDS */       \
     hipLaunchKernelGGL((k_win_bidir_es<nb, div, b8>), dim3(nblocks), dim3(128), lds, st, dg, ng,   \
                        (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,                 \
                        (const s2 *)a.T, a.plane, es);                                              \

@@ -91,7 +91,7 @@ class srsgpu_cell_t(ctypes.Structure):
                 ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32)]
 
 
-MIMO_SINGLE_ANTENNA, MIMO_TX_DIVERSITY, MIMO_CDD = 0, 1, 3
+MIMO_SINGLE_ANTENNA, MIMO_TX_DIVERSITY, MIMO_SPATIAL_MULTIPLEX, MIMO_CDD = 0, 1, 2, 3
 
 
 class srsgpu_pdsch_sf_t(ctypes.Structure):
@@ -103,7 +103,8 @@ class srsgpu_pdsch_sf_t(ctypes.Structure):
                 ("tb_cw_swap", ctypes.c_uint32), ("mod", ctypes.c_uint32 * 2),
                 ("tbs", ctypes.c_uint32 * 2), ("rv", ctypes.c_uint32 * 2),
                 ("softbuffer", ctypes.c_uint32 * 2), ("grid_offset", ctypes.c_uint64),
-                ("ce_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64 * 2)]
+                ("ce_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64 * 2),
+                ("codebook_idx", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class srsgpu_rxq_item_t(ctypes.Structure):
@@ -191,6 +192,17 @@ class srsgpu_ra_dl_grant_t(ctypes.Structure):
         """the reference harness's 13-field order (oracle/ref_harness.c ref_dci_to_dl_grant)"""
         return [self.nof_prb, self.Qm[0], self.Qm[1], self.mod[0], self.tbs[0], self.mcs_idx[0], self.mod[1],
                 self.tbs[1], self.mcs_idx[1], self.tb_en[0], self.tb_en[1], self.pinfo, self.tb_cw_swap]
+
+
+class srsgpu_rxq_ue_dl_t(ctypes.Structure):
+    """include/srsgpu/rx_queue.h: one srslte_ue_dl_decode_rnti subframe"""
+    _fields_ = [("td", ctypes.c_void_p * 2), ("tti", ctypes.c_uint32), ("rnti", ctypes.c_uint16),
+                ("tm", ctypes.c_uint32), ("rnti_type", ctypes.c_int32), ("softbuffer", ctypes.c_uint32 * 2),
+                ("data", ctypes.c_void_p * 2), ("acks", ctypes.c_uint8 * 2), ("ret", ctypes.c_int32),
+                ("cfi", ctypes.c_uint32), ("cfi_corr", ctypes.c_float), ("found", ctypes.c_int32),
+                ("format", ctypes.c_uint32), ("L", ctypes.c_uint32), ("ncce", ctypes.c_uint32),
+                ("mimo_type", ctypes.c_uint32), ("rv", ctypes.c_uint32 * 2), ("grant", srsgpu_ra_dl_grant_t),
+                ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float)]
 
 
 def dlsch_data_len(tbs):
@@ -287,6 +299,9 @@ _sig = {
     "srsgpu_rxq_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "srsgpu_rxq_get_chest": (_vp, [_vp]),
     "srsgpu_rxq_get_pdsch": (_vp, [_vp]),
+    "srsgpu_rxq_submit_ue_dl": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_rxq_decode_rnti": (_i32, [_vp, _vp]),
+    "srsgpu_rxq_set_phich": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
     "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
@@ -584,13 +599,14 @@ class Dlsch:
 
 def make_sf(sf_idx=1, lstart=1, prb=None, nof_prb=100, mod=3, nof_re=0, rnti=1234, noise=0.0,
             scaling=1.0, tbs=0, rv=0, softbuffer=0, grid_offset=0, data_offset=0, mimo=0,
-            ce_offset=None, tb_cw_swap=0):
+            ce_offset=None, tb_cw_swap=0, codebook_idx=0):
     """srsgpu_pdsch_sf_t from keyword arguments; prb: None (all) or a (2, nof_prb) 0/1 array.
     Per-TB fields (mod, tbs, rv, softbuffer, data_offset) take a value or a (tb0, tb1) pair;
     ce_offset defaults to grid_offset (1-port cells: one estimate plane per rx antenna)."""
     s = srsgpu_pdsch_sf_t()
     s.sf_idx, s.lstart, s.nof_re, s.rnti = sf_idx, lstart, nof_re, rnti
     s.noise_estimate, s.scaling, s.mimo_type, s.tb_cw_swap = noise, scaling, mimo, tb_cw_swap
+    s.codebook_idx = codebook_idx
     for name, v in (("mod", mod), ("tbs", tbs), ("rv", rv), ("softbuffer", softbuffer),
                     ("data_offset", data_offset)):
         pair = tuple(v) if isinstance(v, (tuple, list)) else (v, 0)
@@ -1003,6 +1019,32 @@ class RxQueue:
 
     def decode(self, it):
         return _lib.srsgpu_rxq_decode(self.q, ctypes.byref(it))
+
+    @staticmethod
+    def ue_item(td, tti, rnti, data, tm=0, rnti_type=-1, softbuffer=(0, 1)):
+        """srsgpu_rxq_ue_dl_t: td complex64 arrays per rx antenna, data uint8 arrays per TB (both kept
+        alive by the caller)"""
+        u = srsgpu_rxq_ue_dl_t()
+        for a, x in enumerate(td):
+            u.td[a] = x.ctypes.data
+        u.tti, u.rnti, u.tm, u.rnti_type = tti, rnti, tm, rnti_type
+        u.softbuffer[0], u.softbuffer[1] = softbuffer
+        for t, d in enumerate(data):
+            u.data[t] = d.ctypes.data
+        return u
+
+    def decode_rnti(self, u):
+        return _lib.srsgpu_rxq_decode_rnti(self.q, ctypes.byref(u))
+
+    def submit_ue_dl(self, u):
+        t = ctypes.c_uint64(0)
+        if _lib.srsgpu_rxq_submit_ue_dl(self.q, ctypes.byref(u), ctypes.byref(t)) != 0:
+            raise RuntimeError("srsgpu_rxq_submit_ue_dl failed")
+        return t.value
+
+    def set_phich(self, length, resources):
+        if _lib.srsgpu_rxq_set_phich(self.q, length, resources) != 0:
+            raise RuntimeError("invalid PHICH configuration")
 
     def submit(self, it):
         t = ctypes.c_uint64(0)

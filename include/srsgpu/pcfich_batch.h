@@ -34,6 +34,10 @@ typedef struct {
  * invalid cell (1 or 2 ports, 1 or 2 rx antennas, 6..110 PRB). */
 int srsgpu_pcfich_create(srsgpu_pcfich_t **q, const srsgpu_cell_t *cell);
 void srsgpu_pcfich_destroy(srsgpu_pcfich_t *q);
+/* Take each subframe's noise estimate from device memory instead of sf[i].noise_estimate: subframe
+ * i of a call uses d_noise[i] (e.g. the batch's srslte_chest_dl_get_noise_estimate values, left in
+ * HBM by the estimator). NULL restores sf[i].noise_estimate. */
+void srsgpu_pcfich_set_noise_dev(srsgpu_pcfich_t *q, const float *d_noise);
 /* the 16 RE indices of symbol 0 (srslte_regs_pcfich_get order) */
 int srsgpu_pcfich_re_map(const srsgpu_pcfich_t *q, uint32_t idx[16]);
 /* srslte_pcfich_decode_multi for nof_sf subframes: d_cfi[i] = the detected CFI (1..3; 1 when no

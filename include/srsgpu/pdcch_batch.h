@@ -43,6 +43,9 @@ int srsgpu_pdcch_cell_map(const srsgpu_cell_t *cell, uint32_t phich_length, uint
                           uint32_t cfi, uint32_t *idx, uint32_t max, uint32_t *nof_cce);
 /* NOF_CCE(cfi) of pdcch.c (0 for cfi outside 1..3) */
 uint32_t srsgpu_pdcch_nof_cce(const srsgpu_pdcch_t *q, uint32_t cfi);
+/* Take each subframe's noise estimate from device memory instead of sf[i].noise_estimate: subframe
+ * i of a srsgpu_pdcch_extract_llr_dev call uses d_noise[i]. NULL restores sf[i].noise_estimate. */
+void srsgpu_pdcch_set_noise_dev(srsgpu_pdcch_t *q, const float *d_noise);
 /* the 36 NOF_CCE(cfi) grid indices (l * 12 nof_prb + k) in srslte_regs_pdcch_get order; returns
  * their count, or -1 if max is too small */
 int srsgpu_pdcch_re_map(const srsgpu_pdcch_t *q, uint32_t cfi, uint32_t *idx, uint32_t max);

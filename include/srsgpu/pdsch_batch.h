@@ -52,6 +52,9 @@ typedef struct {
 /* srslte_mimo_type_t values accepted by the GPU receiver */
 #define SRSGPU_MIMO_SINGLE_ANTENNA 0 /* 1 CRS port, 1 layer, 1 TB (TM1), 1-2 rx antennas */
 #define SRSGPU_MIMO_TX_DIVERSITY 1   /* TM2 / DCI 1A on 2-port cells: SFBC over RE pairs, 1 TB, 1-2 rx */
+#define SRSGPU_MIMO_SPATIAL_MULTIPLEX 2 /* TM4 closed-loop spatial multiplexing: 2 ports, 2 rx antennas;
+                                          2 TBs on 2 layers (2x2 MMSE, codebook_idx 0..2) or 1 TB on
+                                          1 layer (2x1 MRC, codebook_idx 0..3) */
 #define SRSGPU_MIMO_CDD 3            /* TM3 large-delay CDD: 2 ports, 2 layers, 2 TBs, 2 rx antennas */
 
 typedef struct {
@@ -70,6 +73,9 @@ typedef struct {
   uint64_t grid_offset;     /* this subframe's [rx antenna] grid planes in d_grid (complex elements) */
   uint64_t ce_offset;       /* this subframe's [rx antenna][port] estimate planes in d_ce */
   uint64_t data_offset[2];  /* first output byte of each TB in d_data */
+  uint32_t codebook_idx;    /* srslte_pdsch_cfg_t.codebook_idx (spatial multiplexing only; with
+                               tbs[1] > 0 two TBs on two layers, else one TB on one layer) */
+  uint32_t reserved;
 } srsgpu_pdsch_sf_t;
 
 /* nof_softbuffers HARQ softbuffers of max_cb code blocks; up to max_sf subframes per call. */

@@ -17,6 +17,7 @@
 
 #include <stdint.h>
 
+#include "srsgpu/dci.h"
 #include "srsgpu/pdsch_batch.h"
 
 #ifdef __cplusplus
@@ -38,6 +39,42 @@ typedef struct {
   float noise;              /* srslte_chest_dl_get_noise_estimate of the subframe */
 } srsgpu_rxq_item_t;
 
+/* srslte_ue_dl_decode_rnti (src/phy/ue/ue_dl.c:467-620) of one subframe, the call srsUE's PHY worker
+ * makes when it has no grant yet (phch_worker.cc:548-806 -> ue_dl): FFT, channel estimation,
+ * PCFICH (CFI), PDCCH LLRs and the DL DCI blind search for rnti, the DCI unpacked into the grant
+ * (srslte_dci_msg_to_dl_grant), the redundancy version and softbuffer resets of ue_dl.c:503-534,
+ * the MIMO type of the format (:536-566), then the PDSCH / DL-SCH decode of the grant. In a batch
+ * the grids, estimates and LLRs stay in HBM; only the CFIs and the DCI search results (a few hundred
+ * bytes per subframe) come back to the host between the stages, to build the next stage's
+ * descriptors as the reference's host code does. */
+typedef struct {
+  /* in */
+  const void *td[2];       /* time-domain subframe per rx antenna, as srsgpu_rxq_item_t */
+  uint32_t tti;            /* sf_idx = tti % 10; the SI-RNTI redundancy version uses tti / 10 */
+  uint16_t rnti;
+  uint32_t tm;             /* the ue_dci_formats row (ue_dl.c:41-50): 0..7 for TM1..TM8 */
+  int32_t rnti_type;       /* < 0: from the RNTI value (srslte_ue_dl_find_dl_dci); else the
+                              srslte_rnti_type_t of srslte_ue_dl_find_dl_dci_type */
+  uint32_t softbuffer[2];  /* q->softbuffers[0..1]: reset_tbs'd for every found grant */
+  uint8_t *data[2];        /* host output per TB: SRSGPU_DLSCH_DATA_LEN(tbs) bytes */
+  uint8_t acks[2];         /* in/out, as srslte_pdsch_decode's acks: a true ack skips the TB */
+  /* out (valid once srsgpu_rxq_wait returned 0) */
+  int32_t ret;             /* srslte_ue_dl_decode_rnti's return: the grant's TB 0 size when a DCI
+                              was found and the PDSCH decoded, 0 when no DCI was found, -1 on the
+                              reference's error paths (DCI that does not unpack, a format the
+                              reference does not decode, a PDSCH configuration error) */
+  uint32_t cfi;            /* PCFICH result */
+  float cfi_corr;
+  int32_t found;           /* the search's result: 1 found, 0 not, -1 error (ue_dl.c:768-810) */
+  uint32_t format;         /* SRSGPU_DCI_FORMAT* of the found DCI */
+  uint32_t L, ncce;        /* its location */
+  uint32_t mimo_type;      /* SRSGPU_MIMO_* the grant was decoded with */
+  uint32_t rv[2];
+  srsgpu_ra_dl_grant_t grant;
+  uint32_t noi[2];
+  float noise;             /* srslte_chest_dl_get_noise_estimate */
+} srsgpu_rxq_ue_dl_t;
+
 /* One cell (srsgpu_cell_t), FFT size symbol_sz (srsgpu_symbol_sz), nof_softbuffers HARQ
  * softbuffers of the cell's maximum code blocks, max_halfits (srslte_sch_set_max_noi). */
 int srsgpu_rxq_create(srsgpu_rxq_t **q, const srsgpu_cell_t *cell, uint32_t symbol_sz,
@@ -51,6 +88,15 @@ int srsgpu_rxq_submit(srsgpu_rxq_t *q, srsgpu_rxq_item_t *item, uint64_t *ticket
 int srsgpu_rxq_wait(srsgpu_rxq_t *q, uint64_t ticket);
 /* submit + wait: the synchronous call a PHY worker makes per subframe */
 int srsgpu_rxq_decode(srsgpu_rxq_t *q, srsgpu_rxq_item_t *item);
+/* srslte_ue_dl_decode_rnti through the queue: submit (the item, its inputs and outputs stay valid
+ * until the wait returns) and the synchronous form. Grant items (srsgpu_rxq_submit) and ue_dl items
+ * share the queue and its batches. */
+int srsgpu_rxq_submit_ue_dl(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item, uint64_t *ticket);
+int srsgpu_rxq_decode_rnti(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item);
+/* PHICH configuration of the cell (srslte_regs_init from the MIB: length 0 normal / 1 extended,
+ * resources 0..3 = 1/6, 1/2, 1, 2): sets the PDCCH REG map of the ue_dl items. Default normal, 1.
+ * Change it only while nothing is queued. */
+int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_resources);
 /* close the current batch now */
 void srsgpu_rxq_flush(srsgpu_rxq_t *q);
 /* the queue's estimator and receiver, for their settings (srsgpu_chest_set_cfg / _set_smooth_filter,

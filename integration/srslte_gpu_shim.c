@@ -10,8 +10,11 @@
  *   srslte_chest_dl_estimate(_multi)(q, in, ce, sf_idx[, nof_rx])  (chest_dl.c:681-715, ports 0-1,
  *                                        every estimator setting of srsUE's phch_worker)
  *   srslte_pdsch_decode(q, cfg, sb, sf_symbols, ce, noise, rnti, data, acks)
- *                                        (pdsch.c:868-1007, TM1 single antenna port and TM3 CDD)
- *   srslte_dlsch_decode2(q, cfg, sb, e_bits, data, tb_idx)  (sch.c:506-517, 16-bit LLRs)
+ *                                        (pdsch.c:868-1007, TM1 single antenna port, TM2 transmit
+ *                                        diversity, TM3 CDD, TM4 spatial multiplexing)
+ *   srslte_dlsch_decode2(q, cfg, sb, e_bits, data, tb_idx)  (sch.c:506-517, 16- or 8-bit LLRs)
+ *   srslte_ulsch_decode(q, cfg, sb, q_bits, g_bits, data)   (sch.c:883-889, no UCI: enb_ul.c's
+ *                                        PUSCH data decode)
  *   srslte_rm_turbo_rx_lut(in, out, in_len, cb_idx, rv)      (rm_turbo.c:378-381)
  *   srslte_pcfich_decode_multi(q, sf, ce, noise, sf_idx, cfi, corr)  (pcfich.c:178-241)
  *   srslte_pdcch_extract_llr_multi(q, sf, ce, noise, sf_idx, cfi)      (pdcch.c:442-508)
@@ -59,6 +62,7 @@
 #include "srsgpu/pcfich_batch.h"
 #include "srsgpu/pdcch_batch.h"
 #include "srsgpu/pdsch_batch.h"
+#include "srsgpu/ulsch_batch.h"
 #include "srsgpu/viterbi_batch.h"
 
 /* ---- HIP runtime entry points used for the host <-> device staging (libamdhip64) ---- */
@@ -566,6 +570,46 @@ static uint32_t shim_sch_max_cb(void) {
   return (uint32_t)srslte_ra_tbs_from_idx(26, SRSLTE_MAX_PRB) / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1;
 }
 
+/* The GPU DL-SCH object of `q` with staging for nof_e LLR elements (d_a) and a TB of tbs bits
+ * (d_b), and the GPU softbuffer index of `softbuffer`; NULL on failure */
+static shim_entry_t *shim_sch_stage(srslte_sch_t *q, srslte_softbuffer_rx_t *softbuffer, uint32_t nof_e,
+                                    uint32_t tbs, int *slot) {
+  shim_entry_t *e = shim_get(q, SHIM_SCH);
+  if (!e) return NULL;
+  if (!e->gpu) {
+    const uint32_t max_cb = shim_sch_max_cb();
+    if (srsgpu_dlsch_create((srsgpu_dlsch_t **)&e->gpu, SHIM_MAX, max_cb, max_cb) ||
+        shim_alloc(&e->d_c, 2 * sizeof(int32_t))) {
+      shim_reset(e);
+      return NULL;
+    }
+    e->nof_prb = max_cb; /* SCH entries: the pool's code blocks per softbuffer */
+  }
+  if (softbuffer->max_cb > e->nof_prb) {
+    fprintf(stderr, "srsgpu shim: softbuffer with %u code blocks, the GPU pool holds %u\n",
+            softbuffer->max_cb, e->nof_prb);
+    return NULL;
+  }
+  /* staging: e-bits (d_a, capacity aux) and TB bytes (d_b, capacity cell_id) grow on demand */
+  if (e->aux < nof_e || !e->d_a) {
+    if (e->d_a) hipFree(e->d_a);
+    e->d_a = NULL;
+    e->aux = 0;
+    if (shim_alloc(&e->d_a, sizeof(int16_t) * nof_e)) return NULL;
+    e->aux = nof_e;
+  }
+  const uint32_t dlen = SRSGPU_DLSCH_DATA_LEN(tbs) + 16;
+  if (e->cell_id < dlen || !e->d_b) {
+    if (e->d_b) hipFree(e->d_b);
+    e->d_b = NULL;
+    e->cell_id = 0;
+    if (shim_alloc(&e->d_b, dlen)) return NULL;
+    e->cell_id = dlen;
+  }
+  *slot = shim_softbuffer(e, (srsgpu_dlsch_t *)e->gpu, softbuffer);
+  return *slot < 0 ? NULL : e;
+}
+
 /* srslte_dlsch_decode2 (sch.c:506-517 -> decode_tb :430-497): one transport block from host
  * LLRs; sets q->nof_iterations (srslte_sch_last_noi) and the softbuffer's cb_crc / tb_crc */
 int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
@@ -574,41 +618,10 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
     return SRSLTE_ERROR_INVALID_INPUTS;
   const uint32_t Nl = cfg->nof_layers != (uint32_t)SRSLTE_RA_DL_GRANT_NOF_TB(&cfg->grant) ? 2 : 1;
   const uint32_t tbs = cfg->cb_segm[tb_idx].tbs, nof_e = cfg->nbits[tb_idx].nof_bits;
-  shim_entry_t *e = shim_get(q, SHIM_SCH);
+  int slot = -1;
+  shim_entry_t *e = shim_sch_stage(q, softbuffer, nof_e, tbs, &slot);
   if (!e) return SRSLTE_ERROR;
-  if (!e->gpu) {
-    const uint32_t max_cb = shim_sch_max_cb();
-    if (srsgpu_dlsch_create((srsgpu_dlsch_t **)&e->gpu, SHIM_MAX, max_cb, max_cb) ||
-        shim_alloc(&e->d_c, 2 * sizeof(int32_t))) {
-      shim_reset(e);
-      return SRSLTE_ERROR;
-    }
-    e->nof_prb = max_cb; /* SCH entries: the pool's code blocks per softbuffer */
-  }
-  if (softbuffer->max_cb > e->nof_prb) {
-    fprintf(stderr, "srsgpu shim: softbuffer with %u code blocks, the GPU pool holds %u\n",
-            softbuffer->max_cb, e->nof_prb);
-    return SRSLTE_ERROR;
-  }
-  /* staging: e-bits (d_a, capacity aux) and TB bytes (d_b, capacity cell_id) grow on demand */
-  if (e->aux < nof_e || !e->d_a) {
-    if (e->d_a) hipFree(e->d_a);
-    e->d_a = NULL;
-    e->aux = 0;
-    if (shim_alloc(&e->d_a, sizeof(int16_t) * nof_e)) return SRSLTE_ERROR;
-    e->aux = nof_e;
-  }
-  const uint32_t dlen = SRSGPU_DLSCH_DATA_LEN(tbs) + 16;
-  if (e->cell_id < dlen || !e->d_b) {
-    if (e->d_b) hipFree(e->d_b);
-    e->d_b = NULL;
-    e->cell_id = 0;
-    if (shim_alloc(&e->d_b, dlen)) return SRSLTE_ERROR;
-    e->cell_id = dlen;
-  }
   srsgpu_dlsch_t *dl = (srsgpu_dlsch_t *)e->gpu;
-  const int slot = shim_softbuffer(e, dl, softbuffer);
-  if (slot < 0) return SRSLTE_ERROR;
   srsgpu_dlsch_tb_t tb = {tbs, cfg->rv[tb_idx], cfg->grant.Qm[tb_idx] * Nl, nof_e, (uint32_t)slot, 0, 0};
   /* llr_is_8bit (sch.c:344-364): e_bits holds int8 LLRs; the GPU takes them as int16 elements */
   srsgpu_dlsch_set_llr_8bit(dl, q->llr_is_8bit);
@@ -634,6 +647,51 @@ int srslte_dlsch_decode2(srslte_sch_t *q, srslte_pdsch_cfg_t *cfg, srslte_softbu
     if (shim_copy(data, e->d_b, tbs / 8 + 3, D2H)) return SRSLTE_ERROR;
     q->nof_iterations = (uint32_t)rn[1];
     shim_mirror_crc(dl, (uint32_t)slot, softbuffer, cfg->cb_segm[tb_idx].C);
+  }
+  return rn[0];
+}
+
+/* ------------------------------------------------------------------ UL-SCH ---- */
+/* srslte_ulsch_decode (sch.c:883-889 -> srslte_ulsch_uci_decode :944-985 without UCI): the channel
+ * deinterleaver into g_bits and decode_tb on the GPU (srsgpu_ulsch_decode_dev), on the same GPU
+ * softbuffer pool as the object's DL-SCH calls. Writes data, g_bits (the deinterleaved LLRs, as
+ * the reference leaves them), q->nof_iterations and the softbuffer's cb_crc / tb_crc. RI / ACK bits
+ * left on the object by srslte_ulsch_uci_decode_ri_ack (q->nof_ri_ack_bits) are out of scope. */
+int srslte_ulsch_decode(srslte_sch_t *q, srslte_pusch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
+                        int16_t *q_bits, int16_t *g_bits, uint8_t *data) {
+  if (!q || !cfg || !softbuffer || !q_bits || !g_bits || !data) return SRSLTE_ERROR_INVALID_INPUTS;
+  if (q->nof_ri_ack_bits) {
+    fprintf(stderr, "srsgpu shim: UL-SCH with RI / ACK bits is not on the GPU path\n");
+    return SRSLTE_ERROR;
+  }
+  const uint32_t tbs = cfg->cb_segm.tbs, nb = cfg->nbits.nof_bits;
+  int slot = -1;
+  /* d_a holds the q bits in its first half and the g bits in its second */
+  shim_entry_t *e = shim_sch_stage(q, softbuffer, 2 * nb, tbs, &slot);
+  if (!e) return SRSLTE_ERROR;
+  srsgpu_dlsch_t *dl = (srsgpu_dlsch_t *)e->gpu;
+  const uint32_t Qm = cfg->grant.Qm, ns = cfg->nbits.nof_symb;
+  if (!Qm || !ns || nb % (Qm * ns)) {
+    fprintf(stderr, "srsgpu shim: UL-SCH with %u bits is not a %u x %u-column matrix\n", nb, Qm, ns);
+    return SRSLTE_ERROR;
+  }
+  srsgpu_ulsch_tb_t tb = {tbs, cfg->rv, Qm, nb, ns, (uint32_t)slot, 0, 0};
+  srsgpu_dlsch_set_llr_8bit(dl, 0);
+  int16_t *d_q = (int16_t *)e->d_a, *d_g = (int16_t *)e->d_a + nb;
+  if (shim_copy(d_q, q_bits, sizeof(int16_t) * nb, H2D)) return SRSLTE_ERROR;
+  int32_t *d_ret = (int32_t *)e->d_c;
+  uint32_t *d_noi = (uint32_t *)e->d_c + 1;
+  if (tbs == 0) /* sch.c:975: a PUSCH without data (UCI only, not on this path) decodes nothing */
+    return SRSLTE_SUCCESS;
+  if (srsgpu_ulsch_decode_dev(dl, &tb, 1, d_q, d_g, (uint8_t *)e->d_b, q->max_iterations, d_ret, d_noi))
+    return SRSLTE_ERROR;
+  int32_t rn[2];
+  if (shim_copy(rn, e->d_c, sizeof(rn), D2H) || shim_copy(g_bits, d_g, sizeof(int16_t) * nb, D2H))
+    return SRSLTE_ERROR;
+  if (rn[0] != SRSLTE_ERROR_INVALID_INPUTS) {
+    if (shim_copy(data, e->d_b, tbs / 8 + 3, D2H)) return SRSLTE_ERROR;
+    q->nof_iterations = (uint32_t)rn[1];
+    shim_mirror_crc(dl, (uint32_t)slot, softbuffer, cfg->cb_segm.C);
   }
   return rn[0];
 }
@@ -752,14 +810,19 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   /* TM2 / DCI 1A on a 2-port cell: SFBC transmit diversity, one TB (precoding.c:1811-1818) */
   const bool txdiv = cfg->mimo_type == SRSLTE_MIMO_TYPE_TX_DIVERSITY && q->cell.nof_ports == 2 &&
                      nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
-  if ((!siso && !cdd && !txdiv) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
+  /* TM4 closed-loop spatial multiplexing (precoding.c:1715-1760): 2 TBs on 2 layers (2x2 MMSE) or
+   * TB 0 on 1 layer (2x1 MRC), 2 ports, 2 rx */
+  const bool sm = cfg->mimo_type == SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX && q->cell.nof_ports == 2 &&
+                  q->nof_rx_antennas == 2 &&
+                  ((nof_tb == 2 && cfg->nof_layers == 2) || (nof_tb == 1 && cfg->nof_layers == 1 && cfg->grant.tb_en[0]));
+  if ((!siso && !cdd && !txdiv && !sm) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
     fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port), TM2 transmit diversity (2 ports, 1-2 "
-                    "rx) and TM3 CDD (2 ports, 2 layers, 2 rx), normal CP, 16-bit or 8-bit LLRs (the "
-                    "same in the PDSCH and its DL-SCH)\n");
+                    "rx), TM3 CDD (2 ports, 2 layers, 2 rx) and TM4 spatial multiplexing (2 ports, 2 rx, "
+                    "1-2 layers), normal CP, 16-bit or 8-bit LLRs (the same in the PDSCH and its DL-SCH)\n");
     return SRSLTE_ERROR;
   }
-  if ((siso || txdiv) && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
-  if (cdd && acks[0] && acks[1]) return SRSLTE_SUCCESS;
+  if (nof_tb == 1 && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
+  if (nof_tb == 2 && acks[0] && acks[1]) return SRSLTE_SUCCESS;
   shim_entry_t *e = shim_get(q, SHIM_PDSCH);
   if (!e) return SRSLTE_ERROR;
   const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
@@ -792,7 +855,11 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   sf.rnti = rnti;
   sf.noise_estimate = noise_estimate;
   sf.scaling = q->rho_a != 0.0f ? q->rho_a : 1.0f; /* pdsch.c:924-927 */
-  sf.mimo_type = cdd ? SRSGPU_MIMO_CDD : txdiv ? SRSGPU_MIMO_TX_DIVERSITY : SRSGPU_MIMO_SINGLE_ANTENNA;
+  sf.mimo_type = cdd     ? SRSGPU_MIMO_CDD
+                 : sm    ? SRSGPU_MIMO_SPATIAL_MULTIPLEX
+                 : txdiv ? SRSGPU_MIMO_TX_DIVERSITY
+                         : SRSGPU_MIMO_SINGLE_ANTENNA;
+  sf.codebook_idx = sm ? cfg->codebook_idx : 0;
   sf.tb_cw_swap = cfg->tb_cw_swap ? 1 : 0;
   sf.grid_offset = 0;
   sf.ce_offset = 0;
@@ -828,7 +895,7 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
     srslte_softbuffer_rx_t *sb = softbuffers[t];
     if (shim_copy(data[t], (uint8_t *)e->d_c + t * dlen, (size_t)sf.tbs[t] / 8, D2H)) return SRSLTE_ERROR;
     /* last_nof_iterations is indexed by codeword (pdsch.c:815) */
-    const uint32_t cw = cdd ? (t ^ sf.tb_cw_swap) : 0;
+    const uint32_t cw = nof_tb == 2 ? (t ^ sf.tb_cw_swap) : 0;
     q->last_nof_iterations[cw] = noi[t];
     /* srslte_pdsch_codeword_decode (pdsch.c:811-822): ack on a good TB CRC; srslte_pdsch_decode
      * returns SRSLTE_SUCCESS whatever the codeword result (pdsch.c:966-985) */

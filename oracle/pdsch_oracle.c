@@ -204,6 +204,66 @@ void orc_predecode_ccd_2x2(const float *y0, const float *y1, const float *h00, c
   }
 }
 
+/* ---------------------------------------------------------------- TM4: spatial multiplexing ---- */
+static orc_cf cf_mulj(orc_cf a) { return (orc_cf){-a.i, a.r}; } /* _Complex_I * a, exact */
+
+/* srslte_predecoding_multiplex (mimo/precoding.c:1715-1760), 2 ports, 2 rx antennas, restated as
+ * the reference's C loops (the exact tails; the AVX bodies use rcpps):
+ *  - 2 layers: srslte_predecoding_multiplex_2x2_mmse(_csi) (:1331-1542): the codebook's precoder
+ *    (0: [[h00, h10], [h01, h11]], 1: [[h00+h10, h00-h10], [h01+h11, h01-h11]], 2: with j h10 /
+ *    j h11) into srslte_mat_2x2_mmse_csi_gen, norm (float) M_SQRT2 / scaling for codebook 0 else
+ *    2 / scaling; h[port][rx] with h01 = port 0 / rx 1;
+ *  - 1 layer: srslte_predecoding_multiplex_2x1_mrc(_csi) (:1546-1713): h0 / h1 the codebook's
+ *    port combination at rx 0 / 1, hh = norm / (|h0|^2 + |h1|^2), x = (conj(h0) y0 + conj(h1) y1) hh,
+ *    csi = (|h0|^2 + |h1|^2) / norm * (float) M_SQRT1_2.
+ * Returns -1 on a codebook the reference refuses. */
+int orc_predecode_multiplex(const float *y0, const float *y1, const float *h00, const float *h01,
+                            const float *h10, const float *h11, float *x0, float *x1, float *csi0,
+                            float *csi1, int n, float scaling, float noise, int codebook_idx,
+                            int nof_layers) {
+  if (codebook_idx < 0 || codebook_idx > (nof_layers == 2 ? 2 : 3)) return -1;
+  for (int i = 0; i < n; i++) {
+    const orc_cf p00 = {h00[2 * i], h00[2 * i + 1]}, p01 = {h01[2 * i], h01[2 * i + 1]};
+    const orc_cf p10 = {h10[2 * i], h10[2 * i + 1]}, p11 = {h11[2 * i], h11[2 * i + 1]};
+    const orc_cf ya = {y0[2 * i], y0[2 * i + 1]}, yb = {y1[2 * i], y1[2 * i + 1]};
+    if (nof_layers == 2) {
+      orc_cf g00, g01, g10, g11;
+      float norm = 2.0f / scaling;
+      if (codebook_idx == 0) {
+        g00 = p00, g01 = p10, g10 = p01, g11 = p11;
+        norm = 1.41421354f / scaling; /* (float) M_SQRT2 */
+      } else if (codebook_idx == 1) {
+        g00 = cf_add(p00, p10), g01 = cf_sub(p00, p10), g10 = cf_add(p01, p11), g11 = cf_sub(p01, p11);
+      } else {
+        g00 = cf_add(p00, cf_mulj(p10)), g01 = cf_sub(p00, cf_mulj(p10));
+        g10 = cf_add(p01, cf_mulj(p11)), g11 = cf_sub(p01, cf_mulj(p11));
+      }
+      orc_cf a, b;
+      float c0, c1;
+      mmse_csi_gen(ya, yb, g00, g01, g10, g11, &a, &b, &c0, &c1, noise, norm);
+      x0[2 * i] = a.r, x0[2 * i + 1] = a.i;
+      x1[2 * i] = b.r, x1[2 * i + 1] = b.i;
+      if (csi0) csi0[i] = c0;
+      if (csi1) csi1[i] = c1;
+    } else {
+      orc_cf g0, g1;
+      switch (codebook_idx) {
+      case 0: g0 = cf_add(p00, p10), g1 = cf_add(p01, p11); break;
+      case 1: g0 = cf_sub(p00, p10), g1 = cf_sub(p01, p11); break;
+      case 2: g0 = cf_add(p00, cf_mulj(p10)), g1 = cf_add(p01, cf_mulj(p11)); break;
+      default: g0 = cf_sub(p00, cf_mulj(p10)), g1 = cf_sub(p01, cf_mulj(p11)); break;
+      }
+      const float norm = 1.41421354f / scaling; /* (float) M_SQRT2 */
+      const float s = g0.r * g0.r + g0.i * g0.i + g1.r * g1.r + g1.i * g1.i;
+      const float hh = norm / s;
+      const orc_cf x = cf_add(cf_mul(cf_conj(g0), ya), cf_mul(cf_conj(g1), yb));
+      x0[2 * i] = x.r * hh, x0[2 * i + 1] = x.i * hh;
+      if (csi0) csi0[i] = s / norm * 0.707106769f; /* (float) M_SQRT1_2 */
+    }
+  }
+  return 0;
+}
+
 /* ---------------------------------------------------------------- soft demapping ---------- */
 static int16_t sat16(int64_t v) { return (int16_t)(v > 32767 ? 32767 : v < -32768 ? -32768 : v); }
 static int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }

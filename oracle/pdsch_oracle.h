@@ -7,6 +7,10 @@ int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uin
                      uint32_t sf_idx, const uint8_t *prb_mask, uint32_t *idx);
 void orc_predecode_single(const float *y, const float *h, float *x, float *csi, int n,
                           float scaling, float noise);
+int orc_predecode_multiplex(const float *y0, const float *y1, const float *h00, const float *h01,
+                            const float *h10, const float *h11, float *x0, float *x1, float *csi0,
+                            float *csi1, int n, float scaling, float noise, int codebook_idx,
+                            int nof_layers);
 void orc_predecode_ccd_2x2(const float *y0, const float *y1, const float *h00, const float *h01,
                            const float *h10, const float *h11, float *x0, float *x1, float *csi0,
                            float *csi1, int n, float scaling, float noise);

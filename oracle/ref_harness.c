@@ -414,6 +414,42 @@ int ref_predecode_ccd(const float *y0, const float *y1, const float *h00, const 
   return r;
 }
 
+/* srslte_predecoding_type(..., SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX, ...) (precoding.c:1771-, :1715-1760):
+ * 2 ports, 2 rx antennas, nof_layers 1 or 2; x1 / csi1 unused for one layer */
+int ref_predecode_multiplex(const float *y0, const float *y1, const float *h00, const float *h01,
+                            const float *h10, const float *h11, float *x0, float *x1, float *csi0,
+                            float *csi1, int n, float scaling, float noise, int codebook_idx,
+                            int nof_layers) {
+  size_t sz = (n + 32) * sizeof(cf_t);
+  cf_t *b[8] = {NULL};
+  float *c[2] = {NULL};
+  for (int i = 0; i < 8; i++)
+    if (posix_memalign((void **)&b[i], 64, sz)) return -1;
+  for (int i = 0; i < 2; i++)
+    if (posix_memalign((void **)&c[i], 64, sz)) return -1;
+  memcpy(b[0], y0, n * sizeof(cf_t));
+  memcpy(b[1], y1, n * sizeof(cf_t));
+  memcpy(b[2], h00, n * sizeof(cf_t));
+  memcpy(b[3], h01, n * sizeof(cf_t));
+  memcpy(b[4], h10, n * sizeof(cf_t));
+  memcpy(b[5], h11, n * sizeof(cf_t));
+  cf_t *ya[SRSLTE_MAX_PORTS] = {b[0], b[1]};
+  cf_t *ha[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{b[2], b[3]}, {b[4], b[5]}};
+  cf_t *xa[SRSLTE_MAX_LAYERS] = {b[6], b[7]};
+  float *ca[SRSLTE_MAX_CODEWORDS] = {csi0 ? c[0] : NULL, csi0 ? c[1] : NULL};
+  int r = srslte_predecoding_type(ya, ha, xa, csi0 ? ca : NULL, 2, 2, nof_layers, codebook_idx, n,
+                                  SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX, scaling, noise);
+  memcpy(x0, b[6], n * sizeof(cf_t));
+  if (nof_layers == 2) memcpy(x1, b[7], n * sizeof(cf_t));
+  if (csi0) {
+    memcpy(csi0, c[0], n * sizeof(float));
+    if (nof_layers == 2) memcpy(csi1, c[1], n * sizeof(float));
+  }
+  for (int i = 0; i < 8; i++) free(b[i]);
+  for (int i = 0; i < 2; i++) free(c[i]);
+  return r;
+}
+
 /* defined in pdsch.c:229 without a declaration in pdsch.h */
 int srslte_pdsch_get(srslte_pdsch_t *q, cf_t *sf_symbols, cf_t *symbols, srslte_ra_dl_grant_t *grant,
                      uint32_t lstart, uint32_t subframe);

@@ -43,6 +43,7 @@
 #include "srslte/phy/fec/rm_turbo.h"
 #include "srslte/phy/fec/softbuffer.h"
 #include "srslte/phy/phch/sch.h"
+#include "srslte/phy/phch/pusch_cfg.h"
 #include "srslte/phy/phch/pcfich.h"
 #include "srslte/phy/phch/pdcch.h"
 #include "srslte/phy/phch/pdsch.h"
@@ -74,6 +75,8 @@ int srsgpu_shim_pdcch_extract_llr_multi(srslte_pdcch_t *q, cf_t *sf_symbols[SRSL
 int srsgpu_shim_pdcch_decode_msg(srslte_pdcch_t *q, srslte_dci_msg_t *msg, srslte_dci_location_t *location,
                                  srslte_dci_format_t format, uint32_t cfi, uint16_t *crc_rem);
 int srsgpu_shim_release(const void *owner);
+int srsgpu_shim_ulsch_decode(srslte_sch_t *q, srslte_pusch_cfg_t *cfg, srslte_softbuffer_rx_t *softbuffer,
+                             int16_t *q_bits, int16_t *g_bits, uint8_t *data);
 
 static uint64_t rng = 1;
 static double urand(void) {
@@ -90,8 +93,10 @@ int main(int argc, char **argv) {
   /* llr8: the 8-bit LLR chain (llr_is_8bit, pdsch.c:795-806, sch.c:344-364) on both sides */
   const bool llr8 = argc == 12 && atoi(argv[11]) != 0;
   const int tm = atoi(argv[10]);
-  /* tm 1: one port; tm 2: transmit diversity on a 2-port cell (one TB); tm 3: CDD, two TBs */
-  const uint32_t nports = tm >= 2 ? 2 : 1, ntb = tm == 3 ? 2 : 1;
+  /* tm 1: one port; tm 2: transmit diversity on a 2-port cell (one TB); tm 3: CDD, two TBs;
+   * tm 4: spatial multiplexing, two TBs on two layers (codebook 1 / 2 from pmi = k % 2);
+   * tm 5: spatial multiplexing, one TB on one layer (codebook pmi = k % 4) */
+  const uint32_t nports = tm >= 2 ? 2 : 1, ntb = (tm == 3 || tm == 4) ? 2 : 1;
   const uint32_t nof_prb = atoi(argv[1]), cell_id = atoi(argv[2]), mcs = atoi(argv[3]);
   const uint32_t cfi = atoi(argv[4]), nof_rx = atoi(argv[5]), nof_tb = atoi(argv[7]);
   const int csi = atoi(argv[6]);
@@ -230,9 +235,11 @@ int main(int argc, char **argv) {
       memset(&cfg, 0, sizeof(cfg));
       int rv2[SRSLTE_MAX_CODEWORDS] = {(int)rvs[r], (int)rvs[r]};
       if (srslte_pdsch_cfg_mimo(&cfg, cell, &grant, cfi, sf_idx, rv2,
-                                tm == 3 ? SRSLTE_MIMO_TYPE_CDD
-                                        : tm == 2 ? SRSLTE_MIMO_TYPE_TX_DIVERSITY : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA,
-                                0))
+                                tm >= 4   ? SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX
+                                : tm == 3 ? SRSLTE_MIMO_TYPE_CDD
+                                : tm == 2 ? SRSLTE_MIMO_TYPE_TX_DIVERSITY
+                                          : SRSLTE_MIMO_TYPE_SINGLE_ANTENNA,
+                                tm == 4 ? k % 2 : tm == 5 ? k % 4 : 0))
         return 2;
       for (uint32_t p = 0; p < nports; p++) memset(txg[p], 0, sizeof(cf_t) * n);
       if (srslte_pdsch_encode(&tx, &cfg, sbt_p, dtx_p, rnti, txg)) return 2;
@@ -261,7 +268,7 @@ int main(int argc, char **argv) {
       /* DL-SCH drop-in on the reference's codeword LLRs */
       for (uint32_t t = 0; t < ntb; t++) {
         if (acka0[t]) continue;
-        const uint32_t cw = tm == 3 ? (t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
+        const uint32_t cw = ntb == 2 ? (t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
         const uint32_t nb = cfg.nbits[t].nof_bits, nbytes = (uint32_t)grant.mcs[t].tbs / 8 + 3;
         memcpy(ebuf, rx.e[cw], sizeof(int16_t) * nb);
         memset(d2a, 0, dl);
@@ -287,7 +294,7 @@ int main(int argc, char **argv) {
         const int dbad = (exact || (acka[t] && ackb[t])) && memcmp(da_p[t], db_p[t], nb) != 0;
         int crcbad = sra[t].tb_crc != srb[t].tb_crc;
         for (uint32_t i = 0; i < cfg.cb_segm[t].C; i++) crcbad |= sra[t].cb_crc[i] != srb[t].cb_crc[i];
-        const int cw = tm == 3 ? (int)(t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
+        const int cw = ntb == 2 ? (int)(t ^ (cfg.tb_cw_swap ? 1u : 0u)) : 0;
         const int state = acka[t] != ackb[t] || noia[cw] != noib[cw] || crcbad;
         if (exact)
           bad |= dbad || state;
@@ -427,8 +434,86 @@ int main(int argc, char **argv) {
     srslte_regs_free(&regs);
     rng = rng_saved;
   }
+  /* UL-SCH: srslte_ulsch_decode and the shim's on the same PUSCH transport blocks of this cell's
+   * bandwidth (srslte_ulsch_encode's q bits through AWGN), HARQ rv 0, 2, 3, 1 into one softbuffer
+   * each, with and without an SRS-shortened subframe (own rng stream): return code, data, g bits,
+   * nof_iterations, cb_crc and tb_crc */
+  uint32_t nul = 0, nul_ok = 0, nul_bad = 0;
+  {
+    const uint64_t rng_saved = rng;
+    static srslte_sch_t utx, ua, ub;
+    if (srslte_sch_init(&utx) || srslte_sch_init(&ua) || srslte_sch_init(&ub)) return 2;
+    const uint32_t qms[3] = {2, 4, 6}, idxs[3] = {6, 14, 22};
+    for (uint32_t it = 0; it < 6; it++) {
+      srslte_pusch_cfg_t uc;
+      memset(&uc, 0, sizeof(uc));
+      const uint32_t Qm = qms[it % 3], ns = (it & 1) ? 11 : 12;
+      const uint32_t utbs = (uint32_t)srslte_ra_tbs_from_idx(idxs[it % 3], nof_prb);
+      if (srslte_cbsegm(&uc.cb_segm, utbs) || uc.cb_segm.F) continue;
+      uc.grant.Qm = Qm;
+      uc.nbits.nof_symb = ns;
+      uc.nbits.nof_re = 12 * nof_prb * ns;
+      uc.nbits.nof_bits = uc.nbits.nof_re * Qm;
+      const uint32_t nb = uc.nbits.nof_bits;
+      uint8_t *tx = calloc(utbs / 8 + 16, 1), *ga = calloc(nb / 8 + 64, 1), *qp = calloc(nb / 8 + 64, 1);
+      uint8_t *ra_ = calloc(utbs / 8 + 16, 1), *rb_ = calloc(utbs / 8 + 16, 1);
+      int16_t *llr = malloc(sizeof(int16_t) * nb), *qa = malloc(sizeof(int16_t) * nb);
+      int16_t *g1 = calloc(nb + 64, sizeof(int16_t)), *g2 = calloc(nb + 64, sizeof(int16_t));
+      srslte_softbuffer_tx_t stx;
+      srslte_softbuffer_rx_t sa, sb2;
+      if (!tx || !ga || !qp || !ra_ || !rb_ || !llr || !qa || !g1 || !g2 ||
+          srslte_softbuffer_tx_init(&stx, nof_prb) || srslte_softbuffer_rx_init(&sa, nof_prb) ||
+          srsgpu_shim_softbuffer_rx_init(&sb2, nof_prb))
+        return 2;
+      srslte_softbuffer_tx_reset(&stx);
+      srslte_softbuffer_rx_reset(&sa);
+      srsgpu_shim_softbuffer_rx_reset(&sb2);
+      for (uint32_t i = 0; i < utbs / 8; i++) tx[i] = (uint8_t)(urand() * 256);
+      const uint32_t rvs_ul[4] = {0, 2, 3, 1};
+      const float snr0 = -2.0f + 2.0f * (float)(it % 3);
+      for (uint32_t r = 0; r < 4; r++) {
+        uc.rv = rvs_ul[r];
+        memset(ga, 0, nb / 8 + 64);
+        memset(qp, 0, nb / 8 + 64);
+        if (srslte_ulsch_encode(&utx, &uc, &stx, tx, ga, qp)) return 2;
+        const float sg = powf(10.0f, -(snr0 + 1.5f * (float)r) / 20.0f);
+        for (uint32_t i = 0; i < nb; i++) {
+          const float v = ((qp[i / 8] >> (7 - i % 8)) & 1 ? 1.0f : -1.0f) + sg * (float)gauss();
+          llr[i] = (int16_t)(100.0f * v);
+        }
+        memcpy(qa, llr, sizeof(int16_t) * nb);
+        memset(ra_, 0, utbs / 8 + 16);
+        memset(rb_, 0, utbs / 8 + 16);
+        const int r1 = srslte_ulsch_decode(&ua, &uc, &sa, qa, g1, ra_);
+        memcpy(qa, llr, sizeof(int16_t) * nb);
+        const int r2 = srsgpu_shim_ulsch_decode(&ub, &uc, &sb2, qa, g2, rb_);
+        int b = r1 != r2 || ua.nof_iterations != ub.nof_iterations || sa.tb_crc != sb2.tb_crc ||
+                memcmp(g1, g2, sizeof(int16_t) * nb) || memcmp(ra_, rb_, utbs / 8 + 3);
+        for (uint32_t i = 0; i < uc.cb_segm.C; i++) b |= sa.cb_crc[i] != sb2.cb_crc[i];
+        if (b)
+          fprintf(stderr, "ulsch mismatch tbs %u Qm %u rv %u: ret %d/%d noi %u/%u\n", utbs, Qm, uc.rv, r1, r2,
+                  ua.nof_iterations, ub.nof_iterations);
+        nul++;
+        nul_bad += b;
+        if (r1 == 0) {
+          nul_ok++;
+          break;
+        }
+      }
+      srslte_softbuffer_tx_free(&stx);
+      srslte_softbuffer_rx_free(&sa);
+      srsgpu_shim_softbuffer_rx_free(&sb2);
+      free(tx); free(ga); free(qp); free(ra_); free(rb_); free(llr); free(qa); free(g1); free(g2);
+    }
+    srsgpu_shim_release(&ub);
+    srslte_sch_free(&utx);
+    srslte_sch_free(&ua);
+    srslte_sch_free(&ub);
+    rng = rng_saved;
+  }
   printf("tx=%u acks=%u mismatches=%u soft=%u tbs=%u dlsch=%u dlsch_mismatches=%u rm_mismatches=%u "
-         "pcfich_mismatches=%u pdcch=%u pdcch_found=%u pdcch_mismatches=%u\n", ntx, nacks, nbad, nsoft, tbs, ndl,
-         ndl_bad, nrm_bad, npc_bad, npd, npd_found, npd_bad);
-  return nbad || ndl_bad || nrm_bad || npc_bad || npd_bad ? 1 : 0;
+         "pcfich_mismatches=%u pdcch=%u pdcch_found=%u pdcch_mismatches=%u ulsch=%u ulsch_ok=%u "
+         "ulsch_mismatches=%u\n", ntx, nacks, nbad, nsoft, tbs, ndl, ndl_bad, nrm_bad, npc_bad, npd, npd_found,
+         npd_bad, nul, nul_ok, nul_bad);
+  return nbad || ndl_bad || nrm_bad || npc_bad || npd_bad || nul_bad ? 1 : 0;
 }

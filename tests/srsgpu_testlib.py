@@ -426,6 +426,24 @@ class PdschOracle:
                                        _ptr(c[0], _f32p), _ptr(c[1], _f32p), n, scaling, noise)
         return (x, c) if csi else x
 
+    def predecode_multiplex(self, y, h, codebook, layers, scaling=1.0, noise=0.0, csi=False, lib=None):
+        """TM4 spatial multiplexing (orc_predecode_multiplex, or ref_predecode_multiplex when lib is
+        the reference build): y [2 rx][n], h [2 ports][2 rx][n] -> x [layers][n] (+ csi)"""
+        L = lib.lib if lib is not None else self.lib
+        name = "ref_predecode_multiplex" if lib is not None else "orc_predecode_multiplex"
+        f = getattr(L, name)
+        f.argtypes = [_f32p] * 10 + [ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_int, ctypes.c_int]
+        y = [np.ascontiguousarray(v, np.complex64) for v in y]
+        hh = [np.ascontiguousarray(h[p][a], np.complex64) for p in (0, 1) for a in (0, 1)]
+        n = y[0].size
+        x = [np.zeros(n, np.complex64) for _ in range(2)]
+        c = [np.zeros(n, np.float32) for _ in range(2)] if csi else [None, None]
+        r = f(*[v.ctypes.data_as(_f32p) for v in y + hh + x], _ptr(c[0], _f32p), _ptr(c[1], _f32p), n, scaling,
+              noise, codebook, layers)
+        assert r == 0, r
+        x, c = x[:layers], c[:layers]
+        return (x, c) if csi else x
+
     def csi_correction(self, mod, csi, llr):
         csi = np.ascontiguousarray(csi, np.float32)
         llr = np.array(llr, np.int16)

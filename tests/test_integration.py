@@ -43,6 +43,9 @@ CASES = [
     (6, 3, 9, 3, 2, 0, 8, 4.0, 21, 2),     # TM2 transmit diversity, QPSK, 2 rx (SIB-like)
     (25, 33, 16, 2, 1, 0, 6, 12.0, 22, 2),  # TM2, 16QAM, 1 rx
     (50, 211, 27, 1, 2, 1, 4, 20.0, 23, 2),  # TM2, 64QAM, 2 rx, CSI
+    (25, 9, 16, 2, 2, 0, 8, 18.0, 31, 4),   # TM4 spatial multiplexing, 2 TBs on 2 layers, codebook 1-2
+    (50, 140, 22, 1, 2, 1, 6, 22.0, 32, 4),  # TM4, 2 layers, CSI
+    (25, 61, 16, 2, 2, 0, 8, 14.0, 33, 5),  # TM4 rank 1: one TB on one layer, codebook 0-3 (2x1 MRC)
 ]
 
 
@@ -69,6 +72,10 @@ def test_shim_pdsch_decode_matches_reference(case):
     # message, CRC remainder and return value exact
     assert int(stats["pdcch"]) >= 100 and int(stats["pdcch_mismatches"]) == 0, r.stdout + r.stderr
     assert int(stats["pdcch_found"]) >= 1, r.stdout + r.stderr
+    # srslte_ulsch_decode drop-in (PUSCH data at this cell's bandwidth, QPSK / 16QAM / 64QAM, with
+    # and without SRS, HARQ rv 0-2-3-1): return code, data, g bits, noi and cb_crc exact
+    assert int(stats["ulsch"]) >= 6 and int(stats["ulsch_mismatches"]) == 0, r.stdout + r.stderr
+    assert int(stats["ulsch_ok"]) >= 1, r.stdout + r.stderr
 
 
 # the 8-bit LLR chain (llr_is_8bit on the PDSCH and its DL-SCH, pdsch.c:795-806, sch.c:344-364):
