@@ -746,6 +746,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--coded-snr", type=float, default=None,
+                    help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
     ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich,pdcch,rxq",
                     help="subframe-pipeline legs after the decoder headline (profiling aid)")
     args = ap.parse_args()
@@ -963,7 +965,8 @@ def main():
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
             # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
-            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind, dist=dist))
+            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind, dist=dist,
+                                                  snr_db=args.coded_snr if kind == "c3_coded" else None))
     sweep = None
     if "sweep" in legs:
         # SURVEY §8(d) C3 points: coded subframes at 20 / 25 / 30 dB, CRC early stop (max 8

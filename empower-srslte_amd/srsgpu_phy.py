@@ -269,6 +269,8 @@ _sig = {
     "srsgpu_pcfich_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t)]),
     "srsgpu_pcfich_destroy": (None, [_vp]),
     "srsgpu_pcfich_re_map": (_i32, [_vp, _u32p]),
+    "srsgpu_pcfich_set_noise_dev": (None, [_vp, _vp]),
+    "srsgpu_pdcch_set_noise_dev": (None, [_vp, _vp]),
     "srsgpu_pcfich_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pcfich_sf_t), _u32, _vp, _vp, _sz,
                                         _vp, _vp, _vp]),
     "srsgpu_pdcch_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t), _u32, _u32]),

@@ -133,3 +133,65 @@ def test_create_rejects_invalid_cells(nof_prb, cell_id, nports, nrx):
     import srsgpu_phy as s
     with pytest.raises(RuntimeError):
         s.Pcfich(nof_prb, cell_id, nports, nrx)
+
+
+@pytest.mark.gpu
+def test_gpu_back_to_back_calls_and_streams(oracle):
+    """srsgpu_pcfich_decode_dev reuses its pinned descriptor buffer: several calls back to back with
+    different descriptor contents and counts, no host sync in between, on one stream and then on a
+    second stream (the call waits for the previous upload, or for the previous stream), plus one
+    call with the noise estimates taken from device memory (srsgpu_pcfich_set_noise_dev). Every
+    result equals the oracle."""
+    import torch
+    import srsgpu_phy as s
+    nof_prb, cell_id, nports, nrx = 25, 33, 1, 2  # one port: the noise estimate enters the equaliser
+    rng = np.random.default_rng(9)
+    n0, stride = nof_prb * 12, nof_prb * 12 * 14
+    ns = 48
+    subs = []
+    for i in range(ns):
+        y = [(rng.standard_normal(n0) + 1j * rng.standard_normal(n0)).astype(np.complex64) for _ in range(nrx)]
+        h = [[(rng.standard_normal(n0) + 1j * rng.standard_normal(n0)).astype(np.complex64) for _ in range(nrx)]
+             for _ in range(nports)]
+        subs.append((y, h, float(rng.choice([0.0, 0.3])), i % 10))
+    grid = np.zeros((ns, nrx, stride), np.complex64)
+    ce = np.zeros((ns, nrx * nports, stride), np.complex64)
+    for i, (y, h, _, _) in enumerate(subs):
+        for a in range(nrx):
+            grid[i, a, :n0] = y[a]
+            for p in range(nports):
+                ce[i, a * nports + p, :n0] = h[p][a]
+    d_grid = torch.from_numpy(grid.view(np.float32)).cuda()
+    d_ce = torch.from_numpy(ce.view(np.float32)).cuda()
+    q = s.Pcfich(nof_prb, cell_id, nports, nrx)
+    st1, st2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    # calls of 7, 16, 25 subframes (different windows of the batch) into separate outputs
+    windows = [(0, 7), (5, 21), (20, 45), (30, 48)]
+    outs = []
+    for k, (a, b) in enumerate(windows):
+        st = st1 if k < 3 else st2
+        d_cfi = torch.full((b - a,), 9, dtype=torch.int32, device="cuda")
+        d_corr = torch.zeros(b - a, dtype=torch.float32, device="cuda")
+        sfs = [(i * nrx * stride, i * nrx * nports * stride, subs[i][3], subs[i][2]) for i in range(a, b)]
+        assert q.decode_dev(sfs, d_grid.data_ptr(), d_ce.data_ptr(), stride, d_cfi.data_ptr(), d_corr.data_ptr(),
+                            stream=st.cuda_stream) == 0
+        outs.append((a, b, d_cfi, d_corr))
+    # device-resident noise for the last window, on the first stream again
+    d_noise = torch.tensor([subs[i][2] for i in range(ns)], dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    s._lib.srsgpu_pcfich_set_noise_dev(q.q, s._vp(d_noise.data_ptr()))
+    d_cfi = torch.full((ns,), 9, dtype=torch.int32, device="cuda")
+    d_corr = torch.zeros(ns, dtype=torch.float32, device="cuda")
+    sfs = [(i * nrx * stride, i * nrx * nports * stride, subs[i][3], -1.0) for i in range(ns)]  # noise ignored
+    assert q.decode_dev(sfs, d_grid.data_ptr(), d_ce.data_ptr(), stride, d_cfi.data_ptr(), d_corr.data_ptr(),
+                        stream=st1.cuda_stream) == 0
+    outs.append((0, ns, d_cfi, d_corr))
+    torch.cuda.synchronize()
+    s._lib.srsgpu_pcfich_set_noise_dev(q.q, None)
+    for a, b, d_cfi, d_corr in outs:
+        cfi, corr = d_cfi.cpu().numpy(), d_corr.cpu().numpy()
+        for j, i in enumerate(range(a, b)):
+            y, h, noise, sf = subs[i]
+            w = pcfich_decode(oracle, nof_prb, cell_id, nports, nrx, y, h, noise, sf)
+            assert cfi[j] == w[0] and corr[j] == np.float32(w[1]), (a, b, i)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# r03 profiles: decoder scaling probe, kernel-trace stats of the coded C3 leg at 16 and 30 dB and of
+# the TM3 leg (separate runs, each under its own limit)
+set -e
+export TMPDIR=/tmp
+TAG=${1:-r03}
+O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 120 python tools/dec_scale.py > $O/dec_scale.txt 2>&1 || { tail -5 $O/dec_scale.txt; exit 1; }
+cat $O/dec_scale.txt
+cd /tmp
+for snr in 16 30; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_coded$snr -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline --legs coded --coded-snr $snr > $O/kt_coded$snr.log 2>&1
+  echo coded $snr done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_tm3 -o kt -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 2 --no-cpu-baseline --legs tm3 > $O/kt_tm3.log 2>&1
+cd $GRAFT_REPO_ROOT
+bash tools/dist_rehearsal.sh $TAG
+echo all done
