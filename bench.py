@@ -226,7 +226,29 @@ def stage_profile(s, torch, step, steps):
     return out
 
 
-def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None):
+def schedule_ab(s, torch, step, steps, schedules, reps=3):
+    """A/B of decoder launch schedules (srsgpu_tdec_set_schedule; results are identical under all)
+    in one process on the same inputs: reps rounds, each timing `steps` steps per schedule in turn
+    after one warm-up step; ms per batch per schedule, then the schedule in force before is restored."""
+    if not schedules:
+        return None
+    keep = s.get_schedule()
+    res = {name: [] for name in schedules}
+    for _ in range(reps):
+        for name, sch in schedules.items():
+            s.set_schedule(**sch)
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            res[name].append(round((time.perf_counter() - t0) / steps * 1e3, 3))
+    s.set_schedule(**keep)
+    return {name: {"ms_per_batch": v, "median": float(np.median(v))} for name, v in res.items()}
+
+
+def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedules=None):
     """tm 1 — BASELINE configs[2]: one step = 1024 subframes through OFDM FFT -> CRS channel
     estimation -> PDSCH (RE extraction, MMSE, 64QAM demap, descramble) -> DL-SCH (de-RM, turbo
     decoding with CRC early stop up to 8 half-iterations, TB CRC) for TBS 75376 (13 x K=5824).
@@ -309,6 +331,7 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None):
     el = time.perf_counter() - t0
     gc.enable()
     stages = stage_profile(s, torch, step, steps)
+    ab = schedule_ab(s, torch, step, steps, schedules)
     noi = np.concatenate([o["noi"].cpu().numpy() for o in L])
     # results of this rank's subframes (lane li holds subframes li*nsf .. of the range), one record
     # per subframe = its TBs' records, then the gather to rank 0
@@ -345,13 +368,13 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None):
             "streams": lanes, "nof_iterations_mean": float(noi.mean()), "stage_ms_per_batch": stages,
             "global_subframes": n_global, "partition": {"kind": "contiguous", "balance": 1.0},
             "subframes_this_rank": C3_SF, "gather_ms": gather_ms, "gathered_subframes": gathered,
-            "result_bytes_per_rank": int(local.numel()),
+            "result_bytes_per_rank": int(local.numel()), "schedule_ab": ab,
             "data": "synthetic 64QAM symbols (not codewords: every CB runs the full 8 half-iterations "
                     "and fails its CRC, so this is the fixed-8 processing rate in TB bits per second, "
                     "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
 
 
-def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None):
+def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
@@ -411,6 +434,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     el = time.perf_counter() - t0
     gc.enable()
     stages = stage_profile(s, torch, step, steps)
+    ab = schedule_ab(s, torch, step, steps, schedules)
     chk = [m.check() for m in ms]
     acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
     noi = float(np.mean([c[2] for c in chk]))
@@ -448,7 +472,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
            "K_range": [ks[0], ks[-1]], "acked_tbs": acks, "tbs_bytes_ok": good, "tbs": len(tbl),
            "nof_iterations_mean": noi, "stage_ms_per_batch": stages, "partition": part,
            "subframes_this_rank": len(mine), "gather_ms": gather_ms,
-           "result_bytes_per_rank": int(local.numel()),
+           "result_bytes_per_rank": int(local.numel()), "schedule_ab": ab,
            "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % snr}
     for m in ms:
         m.close()
@@ -544,10 +568,10 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(64, 256, 1024), producers=8, 
     subframes (20 MHz, MCS 28 codewords from the GPU transmitter at snr_db, copied to host memory
     once) to the subframe batch queue (include/srsgpu/rx_queue.h) — each submission copies its
     245 KB of samples into the queue's pinned staging — and a waiter thread collects them in
-    ticket order. Per batch size: subframes/s over nsf submissions and the per-subframe latency
+    ticket order. The threads are native (srsgpu_rxq_drive), as srsUE's PHY workers are: Python
+    threads contending for the GIL capped the rate at ~50 K subframes/s (r03_s6). Per batch size: subframes/s over nsf submissions and the per-subframe latency
     (submit -> results written) p50 / p99. Two batches in flight: staging of batch k+1 overlaps the
     decode of batch k."""
-    import threading
     import srsgpu_traffic as tr
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
     m = tr.MixedCells(table, 1024, torch, dev, seed=22, snr_db=snr_db, prbs=(100,), mcs=28, full_band=True)
@@ -569,47 +593,17 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(64, 256, 1024), producers=8, 
             sf = base[j]
             sf.softbuffer[0] = i % (4 * B)
             items.append(q.item([x_host[j]], sf, [outs[i % (4 * B)]]))
-        t_sub = np.zeros(nsf)
-        t_done = np.zeros(nsf)
-        tickets = [0] * nsf
-        ready = [threading.Event() for _ in range(nsf)]
-
-        def produce(p):
-            for i in range(p, nsf, producers):
-                # a softbuffer / output slot is reused 4 B submissions later: wait for its last user
-                if i >= 4 * B:
-                    ready[i - 4 * B].wait()
-                t_sub[i] = time.perf_counter()
-                tickets[i] = q.submit(items[i])
-                ready_sub[i].set()
-
-        ready_sub = [threading.Event() for _ in range(nsf)]
-        fails = [0]
-
-        def collect():
-            for i in range(nsf):
-                ready_sub[i].wait()
-                if q.wait(tickets[i]) != 0:
-                    fails[0] += 1
-                t_done[i] = time.perf_counter()
-                ready[i].set()
-
         # warm-up batch (kernels, tables, first-use allocations)
         warm = [q.submit(items[i]) for i in range(min(B, nsf))]
         q.flush()
         assert all(q.wait(t) == 0 for t in warm)
-        th = [threading.Thread(target=produce, args=(p,)) for p in range(producers)]
-        tc = threading.Thread(target=collect)
+        nb0, done0 = q.stats()
         t0 = time.perf_counter()
-        tc.start()
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        q.flush()
-        tc.join()
+        t_sub, t_done, status = q.drive(items, producers, reuse=4 * B)
         el = time.perf_counter() - t0
+        fails = [int((status != 0).sum())]
         nb, done = q.stats()
+        nb, done = nb - nb0, done - done0
         lat = (t_done - t_sub) * 1e3
         acked = sum(1 for it in items[-min(nsf, 4 * B):] if it.ret[0] == 0)
         out["batches"][str(B)] = {"subframes_per_s": round(nsf / el, 1), "latency_ms_p50": round(float(np.percentile(lat, 50)), 3),

@@ -676,4 +676,70 @@ void srsgpu_rxq_stats(srsgpu_rxq_t *q, uint64_t *batches, uint64_t *subframes) {
   if (subframes) *subframes = q->nsf;
 }
 
+int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t n, uint32_t workers,
+                     uint32_t reuse, double *t_sub, double *t_done, int32_t *status) {
+  if (!q || !items || !workers || workers > 256 || !t_sub || !t_done || !status) return -1;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<uint64_t> tickets(n, 0);
+  std::vector<uint8_t> state(n, 0); // 1 submitted, 2 refused
+  uint32_t ndone = 0, producing = workers;
+  int err = 0;
+  auto now = [] {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  };
+  auto produce = [&](uint32_t w) {
+    for (uint32_t i = w; i < n; i += workers) {
+      if (reuse && i >= reuse) { // the item's softbuffer / output slot: wait for its last user
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return ndone > i - reuse || err; });
+      }
+      {
+        std::lock_guard<std::mutex> l(m);
+        if (err) break;
+      }
+      t_sub[i] = now();
+      uint64_t t = 0;
+      const int r = srsgpu_rxq_submit(q, items[i], &t);
+      {
+        std::lock_guard<std::mutex> l(m);
+        tickets[i] = t;
+        state[i] = r ? 2 : 1;
+        if (r && !err) err = r;
+      }
+      cv.notify_all();
+    }
+    {
+      std::lock_guard<std::mutex> l(m);
+      producing--;
+    }
+    cv.notify_all();
+  };
+  std::thread collector([&] {
+    for (uint32_t i = 0; i < n; i++) {
+      uint8_t s;
+      uint64_t t;
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return state[i] != 0 || producing == 0; });
+        s = state[i];
+        t = tickets[i];
+      }
+      status[i] = s == 1 ? srsgpu_rxq_wait(q, t) : -1;
+      t_done[i] = now();
+      {
+        std::lock_guard<std::mutex> l(m);
+        ndone = i + 1;
+      }
+      cv.notify_all();
+    }
+  });
+  std::vector<std::thread> pool;
+  for (uint32_t w = 0; w < workers; w++) pool.emplace_back(produce, w);
+  for (auto &t : pool) t.join();
+  srsgpu_rxq_flush(q); // the last, partial batch
+  collector.join();
+  return err ? -1 : 0;
+}
+
 } // extern "C"

@@ -525,10 +525,7 @@ struct TdecEngine {
   // one launch each (k_win_bidir_run), the sequential decoders one launch per half-iteration.
   // SRSGPU_TDEC_FUSED=0 selects the per-half-iteration launches everywhere (A/B measurements).
   int halfits_fixed(int nh) {
-    static const bool fused = [] {
-      const char *e = getenv("SRSGPU_TDEC_FUSED");
-      return !(e && e[0] == '0');
-    }();
+    const bool fused = td_sched().fused != 0;
     if (!fused || nh < 2) {
       for (int h = 0; h < nh; h++)
         if (halfit(h, false, h + 1 == nh)) return -1;
@@ -554,24 +551,27 @@ struct TdecEngine {
   }
 
   // early-stop decoding of one pass (planned groups) — maxh half-iterations at most. The windowed
-  // kinds run every half-iteration with its CRC check in one launch each (k_win_bidir_es); the
-  // sequential decoders (K <= 400 under AUTO, GENERIC) one launch per half-iteration plus a
-  // decide launch, which skips the pairs the fused launches finished.
+  // kinds and the SSE decoder (K <= 400 under AUTO) run every half-iteration with its CRC check in
+  // one launch each (k_win_bidir_es, k_sse_es); GENERIC one launch per half-iteration plus a decide
+  // launch, which skips the pairs the fused launches finished.
   // SRSGPU_TDEC_FUSED=0 selects the per-half-iteration launches everywhere (A/B measurements).
   int decode_planned(uint32_t maxh, uint8_t *d_out, size_t out_stride) {
-    static const bool fused = [] {
-      const char *e = getenv("SRSGPU_TDEC_FUSED");
-      return !(e && e[0] == '0');
-    }();
+    // td_sched().es_chunk: half-iterations per early-stop launch. One launch per half-iteration
+    // (with the CRC check inside, no decide launch) lets the kernels of other streams in between;
+    // longer launches save launches but hold every CU until they end
+    const bool fused = td_sched().fused != 0;
+    const int chunk = td_sched().es_chunk;
     bool seq = false;
     const TdArrays a = arrays();
-    const TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh};
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      if (fused && halfits_fusable(k)) {
-        ProfScope ps("k_win_bidir_es", st);
-        HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+      if (fused && halfits_es_fusable(k)) {
+        for (int n0 = 0; n0 < (int)maxh; n0 += chunk) {
+          const TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, n0, std::min(n0 + chunk, (int)maxh)};
+          ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", st);
+          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+        }
       } else {
         seq = true;
       }
@@ -582,7 +582,7 @@ struct TdecEngine {
       last_n = (int)h;
       for (int k = 0; k < TD_NKIND; k++) {
         const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
-        if (g1 <= g0 || (fused && halfits_fusable(k))) continue;
+        if (g1 <= g0 || (fused && halfits_es_fusable(k))) continue;
         static const char *const names[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
                                                      "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
         ProfScope ps(names[k], st);

@@ -83,6 +83,12 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
 // half-iterations n0 .. n0+nh-1 of every group of one windowed kind in one launch (fixed-iteration
 // jobs: no early stop in between); dec: decisions after the last one
 bool halfits_fusable(int kind);
+// the process-wide launch schedule (srsgpu_tdec_set_schedule)
+struct TdSched {
+  int fused, es_chunk, sse_bidir;
+};
+TdSched &td_sched();
+bool halfits_es_fusable(int kind);
 hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, int nblocks,
                           size_t lds, bool dec, const TdArrays &a, hipStream_t st);
 // Early-stop state of k_win_bidir_es (sch.c:361-391 per code block): natural-order decision
@@ -93,8 +99,9 @@ struct TdEs {
   uint8_t *cb_done, *cb_ok;
   uint32_t *noi;
   int max_halfits;
+  int n0, n1; // this launch runs half-iterations n0 .. n1-1 (0 <= n0 < n1 <= max_halfits)
 };
-// every half-iteration of an early-stop job for the groups of one windowed kind in one launch:
+// half-iterations es.n0 .. es.n1-1 of an early-stop job for the groups of one kind in one launch:
 // the CRC after each half-iteration, done / ok / noi and the decision bytes of finished blocks
 // as launch_decide with early = true does, workgroups leave when all their blocks are done
 hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,

@@ -1285,8 +1285,8 @@ __global__ __launch_bounds__(128) void k_win_bidir_es(const TdGroup *__restrict_
   const s2 *wp1_ = XP1 + plane + wb;
   const uint32_t po_ = (uint32_t)((pair - pw) * pe) * 4u;
   const uint16_t *fwd0 = G.fwd, *rev0 = G.rev;
-  for (int n = 0; n < es.max_halfits; n++) {
-    if (n > 0) __syncthreads();
+  for (int n = es.n0; n < es.n1; n++) {
+    if (n > es.n0) __syncthreads();
     // opaque loop-invariant copies, global address space (see k_win_bidir_run)
     gptr_t<s4> gsp0 = gptr(sp0_);
     gmut_t<s2> gxp1 = gmut<s2>(xp1_), gA = gmut<s2>(A_);
@@ -1473,6 +1473,401 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ g
         for (int i = 0; i < 8; i++) b[i] = wsub(b[i], z);
       }
     }
+  }
+}
+
+// The SSE decoder run bidirectionally: the same arithmetic as k_sse_halfit, half its serial
+// chain. Two waves per 64 CB pairs, wave 0 owns the alpha recursion, wave 1 the beta recursion.
+//   phase 1  wave 0: alphas of steps 0..M-1, stored as k_sse_halfit stores them (AL(k) = the
+//            state leaving step k-1, before its normalisation); wave 1: the tail steps, then the
+//            betas of steps K-1..M, storing B(k) = the state entering step k in the scratch slot
+//            AL(k), k >= M (no alpha past M is stored, so the slots are free).
+//   phase 2  (after one workgroup barrier) wave 0 runs the alphas of steps M..K-1 and emits their
+//            LLRs from its own AL(k) and the stored B(k); wave 1 runs the betas of steps M-1..0 and
+//            emits their LLRs from its own B(k) and the stored AL(k).
+// Each recursion keeps the reference's order and normalisation steps and every LLR combines the
+// same AL(k), B(k) and branch metrics as turbodecoder_sse.c:105-206, so the outputs are
+// bit-identical to k_sse_halfit. M = 16*floor(K/32) is a multiple of 16, so the two waves'
+// decision words never share a word.
+// One half-iteration of the workgroup's 64 pairs; pair p = this lane's pair within the group;
+// `done` lanes (finished pairs, lanes past the group) touch no memory but reach the barrier.
+template <int MODE>
+__device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool done,
+                                               const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                               s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                               const s2 *__restrict__ T, size_t plane,
+                                               s2 *__restrict__ scratch_base) {
+  const int K = G.K, npairs = G.npairs;
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
+  const int pair = p < npairs ? p : npairs - 1;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, 1);
+  const s4 *sp0 = SP0 + base;
+  s2 *xp1 = XP1 + base;
+  const s2 *p1 = XP1 + plane + base;
+  s2 *A = Aarr + base;
+  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, 1) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
+  s2 *scratch = scratch_base + G.sc0;
+  auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
+  const int M = 16 * (K / 32); // K >= 40, a multiple of 8: 16 <= M <= K/2
+  constexpr int P = TD_SP;
+  // beta candidates of one step (bp: bit 1, bn: bit 0), their merge, and the LLR against alphas
+  auto bpn = [](const s2 bb[8], s2 g0, s2 g1, s2 bp[8], s2 bn[8]) {
+    bp[0] = wadd(bb[4], g1); bp[1] = wadd(bb[0], g1); bp[2] = wadd(bb[1], g0); bp[3] = wadd(bb[5], g0);
+    bp[4] = wadd(bb[6], g0); bp[5] = wadd(bb[2], g0); bp[6] = wadd(bb[3], g1); bp[7] = wadd(bb[7], g1);
+    bn[0] = wsub(bb[0], g1); bn[1] = wsub(bb[4], g1); bn[2] = wsub(bb[5], g0); bn[3] = wsub(bb[1], g0);
+    bn[4] = wsub(bb[2], g0); bn[5] = wsub(bb[6], g0); bn[6] = wsub(bb[7], g1); bn[7] = wsub(bb[3], g1);
+  };
+  auto llr_of = [](const s2 bp[8], const s2 bn[8], const s2 aa[8]) -> s2 {
+    s2 mp = splat(-32768), mn = splat(-32768);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      mp = smax(mp, wadd(bp[i], aa[i]));
+      mn = smax(mn, wadd(bn[i], aa[i]));
+    }
+    return wsub(wsub(splat(0x7FFF), mn), wsub(splat(0x7FFF), mp)); // hMax(bn) - hMax(bp)
+  };
+  auto astep = [](const s2 a[8], s2 g0, s2 g1, s2 n[8]) { // :211-297
+    n[0] = smax(wadd(a[1], g1), wsub(a[0], g1));
+    n[1] = smax(wadd(a[2], g0), wsub(a[3], g0));
+    n[2] = smax(wadd(a[5], g0), wsub(a[4], g0));
+    n[3] = smax(wadd(a[6], g1), wsub(a[7], g1));
+    n[4] = smax(wadd(a[0], g1), wsub(a[1], g1));
+    n[5] = smax(wadd(a[3], g0), wsub(a[2], g0));
+    n[6] = smax(wadd(a[4], g0), wsub(a[5], g0));
+    n[7] = smax(wadd(a[7], g1), wsub(a[6], g1));
+  };
+  uint32_t dacc = 0;
+  if (role == 0) {
+    s2 a[8], apre[8]; // a: the recursion state, apre: AL(k) of the next step
+    a[0] = splat(0);
+#pragma unroll
+    for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
+#pragma unroll
+    for (int i = 0; i < 8; i++) apre[i] = a[i];
+    if (!done) { // phase 1: alphas of steps 0..M-1
+#pragma unroll
+      for (int i = 0; i < 8; i++) AL(0, i) = a[i];
+      StepIn nx[P];
+#pragma unroll
+      for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, u);
+      for (int k0 = 0; k0 < M; k0 += P) {
+        StepIn cu[P];
+#pragma unroll
+        for (int u = 0; u < P; u++) cu[u] = nx[u];
+#pragma unroll
+        for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, k0 + P + u);
+#pragma unroll
+        for (int u = 0; u < P; u++) {
+          const int k = k0 + u;
+          const s2 g1 = wadd(cu[u].x, cu[u].y) >> 1, g0 = wsub(cu[u].x, cu[u].y) >> 1;
+          s2 n[8];
+          astep(a, g0, g1, n);
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            a[i] = n[i];
+            apre[i] = n[i];
+          }
+          if (k + 1 < M) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) AL(k + 1, i) = n[i];
+          }
+          if ((k & 3) == 3) {
+            const s2 z = a[0];
+#pragma unroll
+            for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (done) return;
+    // phase 2: alphas and LLRs of steps M..K-1; inputs, stored betas and scatter targets are
+    // loaded one group ahead
+    StepIn nx[P];
+    s2 nb[P][8];
+    int nt[P];
+    auto fetch = [&](int k1, StepIn *fs, s2 (*fb)[8], int *ft) {
+#pragma unroll
+      for (int u = 0; u < P; u++) {
+        const int k = k1 + u;
+        fs[u] = load_step<MODE, true>(sp0, xp1, p1, A, k);
+#pragma unroll
+        for (int i = 0; i < 8; i++) fb[u][i] = AL(k, i);
+        ft[u] = tbl[k];
+      }
+    };
+    fetch(M, nx, nb, nt);
+    for (int k0 = M; k0 < K; k0 += P) {
+      StepIn cs[P];
+      s2 cb[P][8];
+      int ct[P];
+#pragma unroll
+      for (int u = 0; u < P; u++) {
+        cs[u] = nx[u];
+        ct[u] = nt[u];
+#pragma unroll
+        for (int i = 0; i < 8; i++) cb[u][i] = nb[u][i];
+      }
+      fetch(min(k0 + P, K - P), nx, nb, nt);
+#pragma unroll
+      for (int u = 0; u < P; u++) {
+        const int k = k0 + u;
+        const StepIn &st = cs[u];
+        const s2 g1 = wadd(st.x, st.y) >> 1, g0 = wsub(st.x, st.y) >> 1;
+        s2 bp[8], bn[8];
+        bpn(cb[u], g0, g1, bp, bn);
+        const s2 llr = llr_of(bp, bn, apre);
+        store_out<MODE == 1>(xp1, A, ct[u], llr, st.e);
+        if (D) { // k ascends: flush each 16-step group at its last step
+          dacc |= dec_bits(llr) << (k & 15);
+          if ((k & 15) == 15 || k == K - 1) {
+            D[k >> 4] = dacc;
+            dacc = 0;
+          }
+        }
+        s2 n[8];
+        astep(a, g0, g1, n);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          a[i] = n[i];
+          apre[i] = n[i];
+        }
+        if ((k & 3) == 3) {
+          const s2 z = a[0];
+#pragma unroll
+          for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
+        }
+      }
+    }
+    return;
+  }
+  s2 b[8];
+  b[0] = splat(0);
+#pragma unroll
+  for (int i = 1; i < 8; i++) b[i] = splat(-TD_INF);
+  if (!done) { // phase 1: tail steps K+2..K (C-division gammas, :349-352), then betas K-1..M
+    const int tail_xoff = MODE == 1 ? 6 : 0;
+    for (int k = K + 2; k >= K; k--) {
+      const s2 x = tl[tail_xoff + 2 * (k - K)], y = tl[tail_xoff + 2 * (k - K) + 1];
+      const s2 g0 = s2{(short)(((int)x.x - y.x) / 2), (short)(((int)x.y - y.y) / 2)};
+      const s2 g1 = s2{(short)(((int)x.x + y.x) / 2), (short)(((int)x.y + y.y) / 2)};
+      s2 bp[8], bn[8];
+      bpn(b, g0, g1, bp, bn);
+#pragma unroll
+      for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
+    }
+    StepIn nx[P];
+#pragma unroll
+    for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, K - 1 - u);
+    for (int k1 = K - 1; k1 >= M; k1 -= P) {
+      StepIn cu[P];
+#pragma unroll
+      for (int u = 0; u < P; u++) cu[u] = nx[u];
+#pragma unroll
+      for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, k1 - P - u);
+#pragma unroll
+      for (int u = 0; u < P; u++) {
+        const int k = k1 - u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) AL(k, i) = b[i]; // B(k)
+        const s2 g1 = wadd(cu[u].x, cu[u].y) >> 1, g0 = wsub(cu[u].x, cu[u].y) >> 1;
+        s2 bp[8], bn[8];
+        bpn(b, g0, g1, bp, bn);
+#pragma unroll
+        for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
+        if ((k & 3) == 0) {
+          const s2 z = b[0];
+#pragma unroll
+          for (int i = 0; i < 8; i++) b[i] = wsub(b[i], z);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (done) return;
+  // phase 2: betas and LLRs of steps M-1..0 from the stored alphas
+  StepIn ns[P];
+  s2 na[P][8];
+  int nt[P];
+  auto fetchb = [&](int k1, StepIn *fs, s2 (*fa)[8], int *ft) {
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int k = k1 - u;
+      fs[u] = load_step<MODE, true>(sp0, xp1, p1, A, k);
+#pragma unroll
+      for (int i = 0; i < 8; i++) fa[u][i] = AL(k, i);
+      ft[u] = tbl[k];
+    }
+  };
+  fetchb(M - 1, ns, na, nt);
+  for (int k1 = M - 1; k1 >= 0; k1 -= P) {
+    StepIn cs[P];
+    s2 ca[P][8];
+    int ct[P];
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      cs[u] = ns[u];
+      ct[u] = nt[u];
+#pragma unroll
+      for (int i = 0; i < 8; i++) ca[u][i] = na[u][i];
+    }
+    fetchb(max(k1 - P, P - 1), ns, na, nt);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int k = k1 - u;
+      const StepIn &st = cs[u];
+      const s2 g1 = wadd(st.x, st.y) >> 1, g0 = wsub(st.x, st.y) >> 1;
+      s2 bp[8], bn[8];
+      bpn(b, g0, g1, bp, bn);
+#pragma unroll
+      for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
+      const s2 llr = llr_of(bp, bn, ca[u]);
+      store_out<MODE == 1>(xp1, A, ct[u], llr, st.e);
+      if (D) { // k descends: flush each 16-step group at its first step
+        dacc |= dec_bits(llr) << (k & 15);
+        if ((k & 15) == 0) {
+          D[k >> 4] = dacc;
+          dacc = 0;
+        }
+      }
+      if ((k & 3) == 0) {
+        const s2 z = b[0];
+#pragma unroll
+        for (int i = 0; i < 8; i++) b[i] = wsub(b[i], z);
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(128) void k_sse_bidir(const TdGroup *__restrict__ groups, int ngroups,
+                                                   const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                   s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                   const s2 *__restrict__ T, size_t plane,
+                                                   s2 *__restrict__ scratch_base,
+                                                   const uint8_t *__restrict__ pair_done) {
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int p = (blockIdx.x - G.blk_half) * 64 + (threadIdx.x & 63);
+  const bool done = p >= G.npairs || (pair_done && pair_done[G.pair0 + p]);
+  sse_bidir_body<MODE>(G, p, done, SP0, XP1, Aarr, Darr, T, plane, scratch_base);
+}
+
+// The early stop of the SSE decoder after half-iteration n, as es_check does it for the window
+// kernels (CRC as the XOR of the weights TdGroup::wc over the set decision bits, crc.c:144-155;
+// the done / ok / noi update of sch.c:361-391; natural-order bytes of the blocks ending now), one
+// pair per lane: each wave folds the decision words it wrote (wave 1 those below M / 16, wave 0
+// the rest), wave 0 combines and decides, then wave h writes the bytes of CB h of its pair.
+// fin[2 lane + h]: bit 0 = done, bit 1 = ended at this check. Returns (uniformly) whether every
+// pair of the workgroup is done.
+template <int V = 0> // a template so that only the part that launches k_sse_es instantiates it
+__device__ __noinline__ bool sse_es_check(const TdGroup &G, int p, int n, const uint32_t *__restrict__ Darr,
+                                          const TdEs &es, uint32_t *red, int *fin) {
+  const int K = G.K, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nw = dec_words(K, 1), mw = (16 * (K / 32)) / 16;
+  const bool dec2 = n & 1;
+  const bool live = !((fin[2 * lane] & 1) && (fin[2 * lane + 1] & 1));
+  const int pair = p < G.npairs ? p : G.npairs - 1;
+  const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)pair * nw);
+  uint32_t c0 = 0, c1 = 0;
+  if (live) {
+    const gptr_t<uint32_t> wc = gptr(G.wc[dec2 ? 1 : 0]);
+    const int q0 = wv ? 0 : mw, q1 = wv ? mw : nw;
+    for (int q = q0; q < q1; q++) {
+      const uint32_t w = dw[q];
+      if (w == 0u) continue;
+      const gptr_t<u4> wq = (gptr_t<u4>)(wc + (size_t)q * 16);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const u4 v = wq[i];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int b = 4 * i + j;
+          c0 ^= ((w >> b) & 1u) ? v[j] : 0u;
+          c1 ^= ((w >> (16 + b)) & 1u) ? v[j] : 0u;
+        }
+      }
+    }
+  }
+  if (wv) {
+    red[2 * lane] = c0;
+    red[2 * lane + 1] = c1;
+  }
+  __syncthreads();
+  if (!wv) {
+    const uint32_t crc[2] = {c0 ^ red[2 * lane], c1 ^ red[2 * lane + 1]};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      int f = fin[2 * lane + h] & 1;
+      if (!f) {
+        const int cb = G.cb0 + 2 * p + h;
+        es.noi[cb] = (uint32_t)(n + 1);
+        if (crc[h] == 0u) {
+          es.cb_ok[cb] = 1;
+          es.cb_done[cb] = 1;
+          f = 3;
+        } else if (n + 1 >= es.max_halfits) {
+          es.cb_done[cb] = 1;
+          f = 3;
+        }
+      }
+      fin[2 * lane + h] = f & 1 ? f : 0;
+    }
+  }
+  __syncthreads();
+  const int f = fin[2 * lane + wv];
+  if (f & 2) { // CB wv of this pair ended now: its K / 8 bytes, MSB first
+    const gptr_t<uint16_t> dmap = gptr(G.dmap);
+    uint8_t *ob = es.outb + (size_t)(G.cb0 + 2 * p + wv) * es.out_stride;
+    for (int b = 0; b < K / 8; b++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int pos = 8 * b + i;
+        const int ci = dec2 ? (int)dmap[pos] : pos;
+        v = (v << 1) | ((dw[ci >> 4] >> ((ci & 15) + 16 * wv)) & 1u);
+      }
+      ob[b] = (uint8_t)v;
+    }
+  }
+  return __syncthreads_and((fin[2 * lane] & 1) && (fin[2 * lane + 1] & 1));
+}
+
+// The early-stop form of the SSE decoder (the DL-SCH path for K <= 400 under AUTO): up to
+// max_halfits half-iterations of k_sse_bidir in ONE launch, each followed by sse_es_check; the
+// workgroup leaves once all of its pairs are done, a finished pair's lanes idle through the rest.
+// Blocks done at entry (HARQ retransmissions whose CRC passed before) are seeded from cb_done.
+template <int V = 0>
+__global__ __launch_bounds__(128) void k_sse_es(const TdGroup *__restrict__ groups, int ngroups,
+                                                const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                const s2 *__restrict__ T, size_t plane,
+                                                s2 *__restrict__ scratch_base, TdEs es) {
+  __shared__ uint32_t red[128];
+  __shared__ int fin[128];
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int p = (blockIdx.x - G.blk_half) * 64 + (threadIdx.x & 63);
+  if (threadIdx.x < 64) {
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+      fin[2 * threadIdx.x + h] =
+          (p >= G.npairs || 2 * p + h >= G.ncb || es.cb_done[G.cb0 + 2 * p + h]) ? 1 : 0;
+  }
+  __syncthreads();
+  if (__syncthreads_and((fin[2 * (threadIdx.x & 63)] & 1) && (fin[2 * (threadIdx.x & 63) + 1] & 1)))
+    return;
+  for (int n = es.n0; n < es.n1; n++) {
+    const int l = threadIdx.x & 63;
+    const bool done = (fin[2 * l] & 1) && (fin[2 * l + 1] & 1);
+    if (n & 1)
+      sse_bidir_body<1>(G, p, done, SP0, XP1, Aarr, Darr, T, plane, scratch_base);
+    else if (n == 0)
+      sse_bidir_body<2>(G, p, done, SP0, XP1, Aarr, Darr, T, plane, scratch_base);
+    else
+      sse_bidir_body<0>(G, p, done, SP0, XP1, Aarr, Darr, T, plane, scratch_base);
+    __syncthreads(); // both waves' decision words and outputs of the half-iteration are written
+    if (sse_es_check<V>(G, p, n, Darr, es, red, fin)) break;
   }
 }
 
@@ -1977,12 +2372,13 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
       if (dec) BIDIR1(nb, div, 0, true, b8); else BIDIR1(nb, div, 0, false, b8);                   \
     }                                                                                              \
   } while (0)
-#define SEQ(kern)                                                                                  \
+#define SEQT(kern, nt)                                                                             \
   do {                                                                                             \
-    if (mode == 1) SEQ1(kern, 1); else if (mode == 2) SEQ1(kern, 2); else SEQ1(kern, 0);           \
+    if (mode == 1) SEQ1(kern, 1, nt); else if (mode == 2) SEQ1(kern, 2, nt); else SEQ1(kern, 0, nt); \
   } while (0)
-#define SEQ1(kern, m)                                                                              \
-  hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(64), 0, st, dg, ng, (const s4 *)a.SP0,            \
+#define SEQ(kern) SEQT(kern, 64)
+#define SEQ1(kern, m, nt)                                                                          \
+  hipLaunchKernelGGL(kern<m>, dim3(nblocks), dim3(nt), 0, st, dg, ng, (const s4 *)a.SP0,            \
                      (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D, (const s2 *)a.T, a.plane,             \
                      (s2 *)a.scratch, pair_done)
 #define RUN1(nb, div, b8)                                                                          \
@@ -2025,8 +2421,11 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
 PART_FUNCS(TD_KIND_W16, BIDIR(16, 0, false), RUN1(16, 0, false), RUNES(16, 0, false))
 #elif TD_PART == 2
 PART_FUNCS(TD_KIND_W8, BIDIR(8, 1, false), RUN1(8, 1, false), RUNES(8, 1, false))
-PART_FUNCS(TD_KIND_SSE, SEQ(k_sse_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
-           return hipErrorInvalidValue, NO_ES)
+PART_FUNCS(TD_KIND_SSE, if (td_sched().sse_bidir) SEQT(k_sse_bidir, 128); else SEQ(k_sse_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
+           return hipErrorInvalidValue,
+           (void)lds; hipLaunchKernelGGL(k_sse_es<0>, dim3(nblocks), dim3(128), 0, st, dg, ng,
+                                         (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,
+                                         (const s2 *)a.T, a.plane, (s2 *)a.scratch, es))
 PART_FUNCS(TD_KIND_GEN, SEQ(k_gen_halfit), (void)n0; (void)nh; (void)lds; (void)dec; (void)a;
            return hipErrorInvalidValue, NO_ES)
 #elif TD_PART == 3
@@ -2040,6 +2439,7 @@ PART_FUNCS(TD_KIND_B32, BIDIR(32, 1, true), RUN1(32, 1, true), RUNES(32, 1, true
 #undef RUN1
 #undef SEQ1
 #undef SEQ
+#undef SEQT
 #undef BIDIR
 #undef BIDIR1
 
@@ -2065,6 +2465,25 @@ bool halfits_fusable(int kind) {
   return kind == TD_KIND_W16 || kind == TD_KIND_W8 || kind == TD_KIND_B16 || kind == TD_KIND_B32;
 }
 
+// early stop in one launch: the window kinds (k_win_bidir_es) and the two-wave SSE decoder (k_sse_es)
+bool halfits_es_fusable(int kind) {
+  if (kind == TD_KIND_SSE) return td_sched().sse_bidir != 0;
+  return halfits_fusable(kind);
+}
+
+TdSched &td_sched() {
+  static TdSched s = [] {
+    auto env = [](const char *n, int d) {
+      const char *e = getenv(n);
+      return e && e[0] ? atoi(e) : d;
+    };
+    TdSched t{env("SRSGPU_TDEC_FUSED", 1) != 0, env("SRSGPU_ES_CHUNK", 1), env("SRSGPU_SSE_BIDIR", 1) != 0};
+    if (t.es_chunk < 1) t.es_chunk = 1;
+    return t;
+  }();
+  return s;
+}
+
 hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, int nblocks,
                           size_t lds, bool dec, const TdArrays &a, hipStream_t st) {
   if (ng <= 0 || nblocks <= 0 || nh <= 0) return hipSuccess;
@@ -2079,8 +2498,9 @@ hipError_t launch_halfits(int n0, int nh, int kind, const TdGroup *dg, int ng, i
 
 hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
                              const TdArrays &a, const TdEs &es, hipStream_t st) {
-  if (ng <= 0 || nblocks <= 0 || es.max_halfits <= 0) return hipSuccess;
+  if (ng <= 0 || nblocks <= 0 || es.n1 <= es.n0) return hipSuccess;
   switch (kind) {
+  case TD_KIND_SSE: return halfits_es_part<TD_KIND_SSE>(dg, ng, nblocks, lds, a, es, st);
   case TD_KIND_W16: return halfits_es_part<TD_KIND_W16>(dg, ng, nblocks, lds, a, es, st);
   case TD_KIND_W8: return halfits_es_part<TD_KIND_W8>(dg, ng, nblocks, lds, a, es, st);
   case TD_KIND_B16: return halfits_es_part<TD_KIND_B16>(dg, ng, nblocks, lds, a, es, st);

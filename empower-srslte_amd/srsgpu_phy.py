@@ -299,6 +299,10 @@ _sig = {
     "srsgpu_rxq_decode": (_i32, [_vp, _vp]),
     "srsgpu_rxq_flush": (None, [_vp]),
     "srsgpu_rxq_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_tdec_set_schedule": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 3),
+    "srsgpu_rxq_drive": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint32, _vp, _vp, _vp]),
     "srsgpu_rxq_get_chest": (_vp, [_vp]),
     "srsgpu_rxq_get_pdsch": (_vp, [_vp]),
     "srsgpu_rxq_submit_ue_dl": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -986,6 +990,18 @@ def shard_weighted(weights, world):
     return owner, load
 
 
+def set_schedule(fused=-1, es_chunk=-1, sse_bidir=-1):
+    """srsgpu_tdec_set_schedule: the decoder launch schedule (results are identical under all)"""
+    if _lib.srsgpu_tdec_set_schedule(fused, es_chunk, sse_bidir) != 0:
+        raise ValueError("invalid decoder schedule")
+
+
+def get_schedule():
+    v = [ctypes.c_int(0) for _ in range(3)]
+    _lib.srsgpu_tdec_get_schedule(*[ctypes.byref(x) for x in v])
+    return {"fused": v[0].value, "es_chunk": v[1].value, "sse_bidir": v[2].value}
+
+
 class RxQueue:
     """srsgpu_rxq_t (include/srsgpu/rx_queue.h): PHY-worker threads hand over single time-domain
     subframes; one dispatcher thread decodes them in batches (OFDM -> chest -> PDSCH / DL-SCH)."""
@@ -1059,6 +1075,19 @@ class RxQueue:
 
     def flush(self):
         _lib.srsgpu_rxq_flush(self.q)
+
+    def drive(self, items, workers, reuse=0):
+        """srsgpu_rxq_drive: native worker threads submit items (in index order per worker) while a
+        collector waits for them; returns (t_sub, t_done, status) arrays"""
+        import numpy as np
+        n = len(items)
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(it) for it in items])
+        t_sub, t_done = np.zeros(n), np.zeros(n)
+        status = np.zeros(n, np.int32)
+        if _lib.srsgpu_rxq_drive(self.q, ptrs, n, workers, reuse, t_sub.ctypes.data, t_done.ctypes.data,
+                                 status.ctypes.data) != 0:
+            raise RuntimeError("srsgpu_rxq_drive: a submission was refused")
+        return t_sub, t_done, status
 
     def stats(self):
         b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)

@@ -106,6 +106,15 @@ struct srsgpu_chest *srsgpu_rxq_get_chest(srsgpu_rxq_t *q);
 srsgpu_pdsch_t *srsgpu_rxq_get_pdsch(srsgpu_rxq_t *q);
 /* batches run and subframes decoded so far */
 void srsgpu_rxq_stats(srsgpu_rxq_t *q, uint64_t *batches, uint64_t *subframes);
+/* Load generator for the queue (no reference counterpart; it stands in for srsUE's pool of PHY
+ * worker threads, phch_worker.cc:548-806): `workers` native threads submit items[i] for
+ * i = w, w + workers, ... and one collector thread waits for the tickets in index order. Item i
+ * reuses the softbuffer / output slot of item i - reuse (0: no reuse), so its submission waits until
+ * that item's results are in. Per item: t_sub / t_done (steady-clock seconds at submission and
+ * after its wait returned) and status (the wait's result, -1 if it was never submitted). Flushes
+ * after the last submission. Returns 0, or -1 if a submission was refused (the rest are skipped). */
+int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t n, uint32_t workers,
+                     uint32_t reuse, double *t_sub, double *t_done, int32_t *status);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,18 @@ int srsgpu_tdec_batch_read_state(srsgpu_tdec_batch_t *q, uint32_t cb, int16_t *a
 /* Input length (int16 elements) one CB needs for (impl, sb_layout, K). */
 uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t long_cb);
 
+/* Decoder launch schedule (process-wide; results are identical under every setting):
+ *   fused      1: fixed-iteration jobs run all half-iterations in one launch per decoder kind and
+ *                 early-stop jobs check the CRC inside the decoder launch; 0: one decoder launch per
+ *                 half-iteration plus a k_decide launch (SRSGPU_TDEC_FUSED)
+ *   es_chunk   half-iterations per early-stop launch, >= 1 (SRSGPU_ES_CHUNK)
+ *   sse_bidir  1: the two-wave SSE decoder (with fused early stop), 0: the one-wave one
+ *                 (SRSGPU_SSE_BIDIR)
+ * A negative argument keeps the current value; the defaults come from those environment variables.
+ * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0. */
+int srsgpu_tdec_set_schedule(int fused, int es_chunk, int sse_bidir);
+void srsgpu_tdec_get_schedule(int *fused, int *es_chunk, int *sse_bidir);
+
 /* Live kernel timing with HIP events on the batch stream (for bench.py's roofline). */
 void srsgpu_prof_enable(int on);
 void srsgpu_prof_reset(void);

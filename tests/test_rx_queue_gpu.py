@@ -101,6 +101,17 @@ def test_worker_threads_through_the_queue(oracle):
     q.flush()
     assert all(q.wait(t) == 0 for t in tickets)
     assert all(items[i].ret[0] == ret_d[i] for i in range(n))
+    # native worker pool (srsgpu_rxq_drive): 3 threads, every item submitted twice in a row of
+    # 2n where item j + n reuses item j's softbuffer and output, so its submission must wait
+    for i in range(n):
+        items[i].ret[0] = 9
+        outs[i][:] = 0
+    t_sub, t_done, status = q.drive(items + items, 3, reuse=n)
+    assert (status == 0).all() and (t_done >= t_sub).all()
+    assert (t_sub[n:] >= t_done[:n]).all()  # reuse: the second round waited for the first
+    for i in range(n):
+        assert items[i].ret[0] == ret_d[i] and items[i].noi[0] == noi_d[i], i
+        assert (outs[i][:nb] == data_d[i][:nb]).all(), i
     q.close()
 
 

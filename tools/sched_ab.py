@@ -1,0 +1,52 @@
+"""In-process A/B of the decoder launch schedules (srsgpu_tdec_set_schedule) on the subframe legs:
+the same inputs, the schedules timed in turn for several rounds (bench.schedule_ab). Prints one
+JSON object: per leg, ms per batch per schedule (each round) and the median.
+
+  python tools/sched_ab.py [--legs c3,coded30,coded16,c5,tm3] [--steps N]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+SCHEDULES = {
+    "fused_es1": dict(fused=1, es_chunk=1, sse_bidir=1),
+    "fused_es2": dict(fused=1, es_chunk=2, sse_bidir=1),
+    "fused_es8": dict(fused=1, es_chunk=8, sse_bidir=1),
+    "per_halfit": dict(fused=0, es_chunk=1, sse_bidir=1),
+    "per_halfit_sse1": dict(fused=0, es_chunk=1, sse_bidir=0),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--legs", default="c3,coded30,coded16,c5")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    import bench
+    import srsgpu_phy as s
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    bench.schedule_ab.__defaults__ = (args.reps,)
+    out = {}
+    for leg in args.legs.split(","):
+        if leg in ("c3", "tm3"):
+            r = bench.run_pipeline(s, torch, dev, args.steps, 2, tm=3 if leg == "tm3" else 1, schedules=SCHEDULES)
+        elif leg.startswith("coded"):
+            r = bench.run_traffic(s, torch, dev, 2 * args.steps, 2, "c3_coded", snr_db=float(leg[5:]),
+                                  schedules=SCHEDULES)
+        else:
+            r = bench.run_traffic(s, torch, dev, 2 * args.steps, 2, "c5", schedules=SCHEDULES)
+        out[leg] = {"ms_per_batch": r["ms_per_batch"], "nof_iterations_mean": r["nof_iterations_mean"],
+                    "schedule_ab": r["schedule_ab"]}
+        print(leg, {k: v["median"] for k, v in r["schedule_ab"].items()}, file=sys.stderr, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
