@@ -139,6 +139,11 @@ __device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
   return r;
 }
 
+// One workgroup per TB. The per-CB bookkeeping is gathered first (thread i: CB i's index,
+// init_done, sizes; the cb_crc / noi update), then every byte is moved by all threads at once and
+// the CRC weights are fetched eight bytes per thread and round: the TB's dependent loads are a few
+// round trips, not one chain per CB (the CB-serial form spent ~60 us per 512-TB launch waiting).
+#define TBF_MAXC 64 // > SRSLTE_MAX_CODEBLOCKS (phy_common.h:57)
 __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tbs_, int ntb,
                                                    const uint32_t *__restrict__ cbmap,
                                                    const uint8_t *__restrict__ dec, size_t dec_stride,
@@ -147,6 +152,8 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint32_t *__restrict__ noi_in,
                                                    const uint32_t *__restrict__ crc_a) {
   __shared__ uint32_t red[4];
+  __shared__ uint32_t c_g[TBF_MAXC], c_dst[TBF_MAXC], c_nb[TBF_MAXC], c_rb[TBF_MAXC];
+  __shared__ uint8_t c_init[TBF_MAXC], c_ok[TBF_MAXC];
   __shared__ int all_ok;
   __shared__ uint32_t noi_sum;
   const int b = blockIdx.x;
@@ -157,83 +164,121 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   t.saved = glob_g(t.saved);
   t.ret = glob_g(t.ret);
   t.noi = glob_g(t.noi);
-  if (t.C == 0) { // tbs == 0 (sch.c:451-453) or invalid inputs: result set on the host
+  if (t.C == 0 || t.C > TBF_MAXC) { // tbs == 0 (sch.c:451-453) or invalid inputs: result set on the host
     if (threadIdx.x == 0) {
-      *t.ret = t.preset_ret;
+      *t.ret = t.C ? -1 : t.preset_ret;
       *t.noi = 0;
     }
     return;
   }
-  if (threadIdx.x == 0) {
-    all_ok = 1;
-    noi_sum = 0;
-  }
-  __syncthreads();
-  // 1. TB bytes: CB i owns [i*rlen/8, (i+1)*rlen/8); the last CB also writes its 3 CRC bytes,
-  //    as its full K/8-byte decision lands last in the reference (sch.c:363-366)
-  for (uint32_t i = 0; i < t.C; i++) {
-    const uint32_t K = i < t.C1 ? t.K1 : t.K2;
-    const uint32_t rlen = t.C == 1 ? K : K - 24;
-    const uint32_t g = cbmap[t.first + i];
-    uint8_t *dst = t.data + (size_t)i * (rlen / 8);
-    if (init_done[g]) {
-      const uint8_t *src = t.saved + (size_t)i * 768;
-      for (uint32_t j = threadIdx.x; j < rlen / 8; j += blockDim.x) dst[j] = src[j];
-    } else {
-      const uint32_t nb = (i == t.C - 1) ? K / 8 : rlen / 8;
-      const uint8_t *src = dec + (size_t)g * dec_stride;
-      for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) dst[j] = src[j];
-    }
-  }
-  __syncthreads();
-  // 2. cb_crc flags, tb_crc, nof_iterations (sch.c:394-419)
-  if (threadIdx.x == 0) {
+  const uint32_t C = t.C;
+  // 1. per CB i (thread i): its global index, where its bytes go (CB i owns [i*rlen/8, ...); the last
+  //    CB also writes its 3 CRC bytes, as its full K/8-byte decision lands last in the reference,
+  //    sch.c:363-366), init_done, and the cb_crc / nof_iterations update of sch.c:394-419
+  if (threadIdx.x < 64) {
+    const uint32_t i = threadIdx.x;
     uint32_t s = 0;
     int ok = 1;
-    for (uint32_t i = 0; i < t.C; i++) {
+    if (i < C) {
+      const uint32_t K = i < t.C1 ? t.K1 : t.K2;
+      const uint32_t rlen = C == 1 ? K : K - 24;
       const uint32_t g = cbmap[t.first + i];
-      if (!init_done[g]) {
-        s += noi_in[g];
-        if (cb_ok_in[g]) t.cb_crc[i] = 1;
+      const uint8_t ini = init_done[g];
+      c_g[i] = g;
+      c_dst[i] = i * (rlen / 8);
+      c_rb[i] = rlen / 8;
+      c_nb[i] = ini ? rlen / 8 : (i == C - 1 ? K / 8 : rlen / 8);
+      c_init[i] = ini;
+      uint8_t crc_i = t.cb_crc[i];
+      if (!ini) {
+        s = noi_in[g];
+        if (cb_ok_in[g]) {
+          crc_i = 1;
+          t.cb_crc[i] = 1;
+        }
       }
-      ok = ok && t.cb_crc[i];
+      c_ok[i] = crc_i;
+      ok = crc_i != 0;
     }
-    all_ok = ok;
-    noi_sum = s;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    ok = __all(ok);
+    if (i == 0) {
+      all_ok = ok;
+      noi_sum = s;
+    }
   }
   __syncthreads();
-  if (!all_ok) {
-    // keep the bytes of the blocks that passed for the retransmission (sch.c:407-416)
-    for (uint32_t i = 0; i < t.C; i++) {
-      if (!t.cb_crc[i]) continue;
-      const uint32_t K = i < t.C1 ? t.K1 : t.K2;
-      const uint32_t rlen = t.C == 1 ? K : K - 24;
-      const uint8_t *src = t.data + (size_t)i * (rlen / 8);
-      uint8_t *dst = t.saved + (size_t)i * 768;
-      for (uint32_t j = threadIdx.x; j < rlen / 8; j += blockDim.x) dst[j] = src[j];
+  // 2. TB bytes, CBs in order (a later CB's bytes win where the regions meet, as the reference's
+  //    sequential copies): the (CB, byte) pairs of the TB spread over all threads
+  //    Eight CBs at a time: their bytes (at most 768 = 3 x 256 per CB) are all loaded before any
+  //    is stored, so the loads are not ordered behind the stores of earlier CBs.
+  for (uint32_t i0 = 0; i0 < C; i0 += 8) {
+    uint8_t v[8][3];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t i = i0 + u;
+      if (i >= C) break;
+      const uint8_t *src = c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const uint32_t j = threadIdx.x + r * 256;
+        v[u][r] = j < c_nb[i] ? src[j] : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t i = i0 + u;
+      if (i >= C) break;
+      uint8_t *dst = t.data + c_dst[i];
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const uint32_t j = threadIdx.x + r * 256;
+        if (j < c_nb[i]) dst[j] = v[u][r];
+      }
+      if (i + 1 < C && c_dst[i] + c_nb[i] > c_dst[i + 1]) __syncthreads(); // overlaps keep their order
     }
   }
-  // TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491), as a parallel XOR fold:
-  // crc.c:144-155 is linear, the checksum is the XOR of x^(tbs-1-p+24) mod P over set bits p
+  __syncthreads();
+  const int ok_all = all_ok;
+  if (!ok_all) {
+    // keep the bytes of the blocks that passed for the retransmission (sch.c:407-416)
+    for (uint32_t i = 0; i < C; i++) {
+      if (!c_ok[i]) continue;
+      const uint8_t *src = t.data + c_dst[i];
+      uint8_t *dst = t.saved + (size_t)i * 768;
+      for (uint32_t j = threadIdx.x; j < c_rb[i]; j += blockDim.x) dst[j] = src[j];
+    }
+  }
+  // 3. TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491), as a parallel XOR fold:
+  //    crc.c:144-155 is linear, the checksum is the XOR of x^(tbs-1-p+24) mod P over set bits p.
+  //    Eight bytes per thread and round: their 64 weight loads are issued before any is used.
   uint32_t crc = 0;
-  if (all_ok) {
+  if (ok_all) {
     uint32_t acc = 0;
     const uint32_t nbytes = t.tbs / 8;
-    // the 8 weights of a byte are loaded unconditionally and masked, so a thread's loads do not
-    // wait behind data-dependent branches; two bytes per thread and round in flight
-#pragma unroll 2
-    for (uint32_t j = threadIdx.x; j < nbytes; j += blockDim.x) {
-      const uint32_t v = t.data[j];
-      const uint32_t *w = crc_a + (t.tbs - 1 - 8 * j); // w[-b]: bit b (MSB first) of byte j
+    constexpr int U = 8;
+    for (uint32_t j0 = threadIdx.x; j0 < nbytes; j0 += blockDim.x * U) {
+      uint32_t v[U], w[U][8];
 #pragma unroll
-      for (int b = 0; b < 8; b++) acc ^= w[-b] & (0u - ((v >> (7 - b)) & 1u));
+      for (int u = 0; u < U; u++) {
+        const uint32_t j = j0 + u * blockDim.x;
+        const uint32_t jj = j < nbytes ? j : j0;
+        v[u] = j < nbytes ? t.data[jj] : 0u;
+        const uint32_t *wp = crc_a + (t.tbs - 1 - 8 * jj); // wp[-b]: bit b (MSB first) of byte j
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) w[u][bb] = wp[-bb];
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int bb = 0; bb < 8; bb++) acc ^= w[u][bb] & (0u - ((v[u] >> (7 - bb)) & 1u));
     }
     crc = wg_xor(acc, red);
   }
   if (threadIdx.x == 0) {
-    *t.noi = noi_sum / t.C;
+    *t.noi = noi_sum / C;
     int ret = -1;
-    if (all_ok) {
+    if (ok_all) {
       const uint32_t nbytes = t.tbs / 8;
       const uint32_t tx = ((uint32_t)t.data[nbytes] << 16) | ((uint32_t)t.data[nbytes + 1] << 8) |
                           t.data[nbytes + 2];

@@ -106,85 +106,112 @@ __global__ __launch_bounds__(256) void k_ofdm_rx(const float2 *__restrict__ in, 
 // Radix 8 first (then 4, 2, 3): 2048 = 8.8.8.4 is four LDS passes instead of six, and with N, R
 // and Ns constants every index division is a shift or a multiply. Small symbols share a
 // workgroup (256 / S threads per symbol) so every size launches full 256-thread workgroups.
-template <int R, int N, int Ns, int TPS>
-__device__ __forceinline__ void stage_c(const cf *__restrict__ d0, cf *__restrict__ d1,
-                                        const float2 *__restrict__ tw, int t) {
-  constexpr int nb = N / R;
-  for (int j = t; j < nb; j += TPS) {
-    const int k = j % Ns;
-    cf v[R];
+// the R-point DFT of one butterfly (v in, y out)
+template <int R> __device__ __forceinline__ void bfly(const cf *v, cf *y) {
+  if constexpr (R == 8) {
+    // two 4-point DFTs (even / odd inputs) joined with W8^k = e^{-i pi k / 4}
+    const float c = 0.70710678118654752f;
+    cf e[4], o[4];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      cf a = d0[j + r * nb];
-      if (Ns > 1 && r) { // e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
-        const float2 w = tw[r * k * (N / (Ns * R))];
-        a = cmul(a, cf{w.x, w.y});
-      }
-      v[r] = a;
+    for (int h = 0; h < 2; h++) {
+      const cf a0 = v[h], a1 = v[h + 2], a2 = v[h + 4], a3 = v[h + 6];
+      const cf s02 = cadd(a0, a2), d02 = csub(a0, a2);
+      const cf s13 = cadd(a1, a3), d13 = mul_mi(csub(a1, a3));
+      cf *z = h ? o : e;
+      z[0] = cadd(s02, s13);
+      z[2] = csub(s02, s13);
+      z[1] = cadd(d02, d13);
+      z[3] = csub(d02, d13);
     }
-    cf y[R];
-    if constexpr (R == 8) {
-      // two 4-point DFTs (even / odd inputs) joined with W8^k = e^{-i pi k / 4}
-      const float c = 0.70710678118654752f;
-      cf e[4], o[4];
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const cf a0 = v[h], a1 = v[h + 2], a2 = v[h + 4], a3 = v[h + 6];
-        const cf s02 = cadd(a0, a2), d02 = csub(a0, a2);
-        const cf s13 = cadd(a1, a3), d13 = mul_mi(csub(a1, a3));
-        cf *z = h ? o : e;
-        z[0] = cadd(s02, s13);
-        z[2] = csub(s02, s13);
-        z[1] = cadd(d02, d13);
-        z[3] = csub(d02, d13);
-      }
-      const cf o1 = {c * (o[1].x + o[1].y), c * (o[1].y - o[1].x)}; // * (c - ic)
-      const cf o2 = mul_mi(o[2]);                                    // * -i
-      const cf o3 = {c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)}; // * (-c - ic)
-      y[0] = cadd(e[0], o[0]);
-      y[4] = csub(e[0], o[0]);
-      y[1] = cadd(e[1], o1);
-      y[5] = csub(e[1], o1);
-      y[2] = cadd(e[2], o2);
-      y[6] = csub(e[2], o2);
-      y[3] = cadd(e[3], o3);
-      y[7] = csub(e[3], o3);
-    } else if constexpr (R == 4) {
-      const cf s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
-      const cf s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
-      y[0] = cadd(s02, s13);
-      y[2] = csub(s02, s13);
-      y[1] = cadd(d02, d13);
-      y[3] = csub(d02, d13);
-    } else if constexpr (R == 2) {
-      y[0] = cadd(v[0], v[1]);
-      y[1] = csub(v[0], v[1]);
-    } else {
-      const float cc = -0.5f, sn = -0.86602540378443865f;
-      const cf tt = cadd(v[1], v[2]), u = csub(v[1], v[2]);
-      y[0] = cadd(v[0], tt);
-      const cf m = {v[0].x + cc * tt.x, v[0].y + cc * tt.y};
-      const cf q = {-sn * u.y, sn * u.x};
-      y[1] = cadd(m, q);
-      y[2] = csub(m, q);
-    }
-    const int o = (j / Ns) * Ns * R + k;
-#pragma unroll
-    for (int r = 0; r < R; r++) d1[o + r * Ns] = y[r];
+    const cf o1 = {c * (o[1].x + o[1].y), c * (o[1].y - o[1].x)}; // * (c - ic)
+    const cf o2 = mul_mi(o[2]);                                    // * -i
+    const cf o3 = {c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y)}; // * (-c - ic)
+    y[0] = cadd(e[0], o[0]);
+    y[4] = csub(e[0], o[0]);
+    y[1] = cadd(e[1], o1);
+    y[5] = csub(e[1], o1);
+    y[2] = cadd(e[2], o2);
+    y[6] = csub(e[2], o2);
+    y[3] = cadd(e[3], o3);
+    y[7] = csub(e[3], o3);
+  } else if constexpr (R == 4) {
+    const cf s02 = cadd(v[0], v[2]), d02 = csub(v[0], v[2]);
+    const cf s13 = cadd(v[1], v[3]), d13 = mul_mi(csub(v[1], v[3]));
+    y[0] = cadd(s02, s13);
+    y[2] = csub(s02, s13);
+    y[1] = cadd(d02, d13);
+    y[3] = csub(d02, d13);
+  } else if constexpr (R == 2) {
+    y[0] = cadd(v[0], v[1]);
+    y[1] = csub(v[0], v[1]);
+  } else {
+    const float cc = -0.5f, sn = -0.86602540378443865f;
+    const cf tt = cadd(v[1], v[2]), u = csub(v[1], v[2]);
+    y[0] = cadd(v[0], tt);
+    const cf m = {v[0].x + cc * tt.x, v[0].y + cc * tt.y};
+    const cf q = {-sn * u.y, sn * u.x};
+    y[1] = cadd(m, q);
+    y[2] = csub(m, q);
   }
 }
 
-// stages Ns .. N; returns the buffer holding the result
+// One Stockham stage in place on a single LDS buffer: each thread reads the inputs of its
+// butterflies (the first stage straight from the time-domain samples in HBM, Ns = 1: no twiddles),
+// the workgroup waits until every read is done, then the outputs are written back. One 8 N-byte
+// buffer per symbol instead of a ping-pong pair, so twice the workgroups fit in a CU's LDS, and no
+// separate pass copies the input into LDS. `live` = the thread's symbol exists (others compute on
+// zeros and only keep the barriers).
+template <int R, int N, int Ns, int TPS, bool FIRST>
+__device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, const float2 *__restrict__ tw,
+                                         int t, bool live) {
+  constexpr int nb = N / R;
+  constexpr int NPT = (nb + TPS - 1) / TPS;
+  cf v[NPT][R];
+#pragma unroll
+  for (int q = 0; q < NPT; q++) {
+    const int j = t + q * TPS;
+    const int k = j % Ns;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      cf a = {0.f, 0.f};
+      if (j < nb) {
+        if (FIRST) {
+          if (live) a = src[j + r * nb];
+        } else {
+          a = buf[j + r * nb];
+          if (Ns > 1 && r) { // e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
+            const float2 w = tw[r * k * (N / (Ns * R))];
+            a = cmul(a, cf{w.x, w.y});
+          }
+        }
+      }
+      v[q][r] = a;
+    }
+  }
+  if (!FIRST) __syncthreads(); // every read of buf done before the first write
+#pragma unroll
+  for (int q = 0; q < NPT; q++) {
+    const int j = t + q * TPS;
+    if (j >= nb) break;
+    const int k = j % Ns;
+    cf y[R];
+    bfly<R>(v[q], y);
+    const int o = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; r++) buf[o + r * Ns] = y[r];
+  }
+  __syncthreads();
+}
+
+// stages Ns .. N in place (radix 8 first, then 4, 2, 3); the result is left in buf
 template <int N, int Ns, int TPS>
-__device__ __forceinline__ cf *fft_c(cf *b0, cf *b1, const float2 *__restrict__ tw, int t) {
-  if constexpr (Ns >= N) {
-    return b0;
-  } else {
+__device__ __forceinline__ void fft_ip(const cf *__restrict__ src, cf *buf, const float2 *__restrict__ tw,
+                                       int t, bool live) {
+  if constexpr (Ns < N) {
     constexpr int rem = N / Ns;
     constexpr int R = rem % 8 == 0 ? 8 : rem % 4 == 0 ? 4 : rem % 2 == 0 ? 2 : 3;
-    stage_c<R, N, Ns, TPS>(b0, b1, tw, t);
-    __syncthreads();
-    return fft_c<N, Ns * R, TPS>(b1, b0, tw, t);
+    stage_ip<R, N, Ns, TPS, Ns == 1>(src, buf, tw, t, live);
+    fft_ip<N, Ns * R, TPS>(src, buf, tw, t, live);
   }
 }
 
@@ -199,19 +226,16 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
                                                    int nre, int cp0, int cp,
                                                    const float2 *__restrict__ tw, float scale) {
   constexpr int S = syms_per_wg<N>(), TPS = 256 / S;
-  __shared__ cf buf[S][2][N];
+  __shared__ cf buf[S][N];
   const int s = threadIdx.x / TPS, t = threadIdx.x % TPS;
   const int g = blockIdx.x * S + s; // symbol of this thread group (past nsym: idle, but at barriers)
   const bool live = g < nsym;
   const int sym = g % 14, sf = g / 14;
   const int slot = sym / 7, l = sym % 7;
   const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
-  if (live) {
-    const cf *src = (const cf *)(in + (size_t)sf * in_stride + start);
-    for (int n = t; n < N; n += TPS) buf[s][0][n] = src[n];
-  }
-  __syncthreads();
-  const cf *res = fft_c<N, 1, TPS>(buf[s][0], buf[s][1], tw, t);
+  const cf *src = (const cf *)(in + (size_t)(live ? sf : 0) * in_stride + start);
+  fft_ip<N, 1, TPS>(src, buf[s], tw, t, live);
+  const cf *res = buf[s];
   if (live) {
     cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
     const int h = nre / 2;

@@ -77,7 +77,26 @@ struct Eq {
   float xr, xi, csi;
 };
 
-__device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t j) {
+// One RE's received values and estimates, loaded ahead of the arithmetic (llr_body gathers
+// several REs' inputs before computing any of them): y[rx], h[port][rx]; entries the
+// configuration does not use are left unset.
+struct ReIn {
+  float2 y[2];
+  float2 h[2][2];
+};
+__device__ __forceinline__ ReIn load_re(const LlrItem &t, uint32_t pos, bool two_ports) {
+  ReIn in;
+#pragma unroll
+  for (int a = 0; a < 2; a++) {
+    if (a == 1 && t.nrx < 2) break;
+    in.y[a] = t.y[a][pos];
+    in.h[0][a] = t.h[0][a][pos];
+    if (two_ports) in.h[1][a] = t.h[1][a][pos];
+  }
+  return in;
+}
+
+__device__ __forceinline__ Eq equalise(const LlrItem &t, const ReIn &in, uint32_t j) {
   Eq e;
   if (!t.csi_mode && (t.nof_re <= 32 || j >= 16 * (t.nof_re / 16))) { // AVX only above 32 (:330)
     // symbols after the last whole 16 take the reference's C path (precoding.c:231-240), whose
@@ -86,7 +105,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
     float hh = 0.f, rr = 0.f, ri = 0.f;
     for (int a = 0; a < 2; a++) {
       if (a == 1 && t.nrx < 2) break;
-      const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[0][1][pos] : t.h[0][0][pos];
+      const float2 y = in.y[a], h = in.h[0][a];
       const double yr = y.x, yi = y.y, hr = h.x, hi = h.y;
       rr = (float)__dadd_rn((double)rr, __dsub_rn(__dmul_rn(yr, hr), __dmul_rn(yi, -hi)));
       ri = (float)__dadd_rn((double)ri, __dadd_rn(__dmul_rn(yr, -hi), __dmul_rn(yi, hr)));
@@ -101,7 +120,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
   float hh = 0.f, rr = 0.f, ri = 0.f;
   for (int a = 0; a < 2; a++) {
     if (a == 1 && t.nrx < 2) break;
-    const float2 y = a ? t.y[1][pos] : t.y[0][pos], h = a ? t.h[0][1][pos] : t.h[0][0][pos];
+    const float2 y = in.y[a], h = in.h[0][a];
     // |h|^2 as hadd(h*h) (precoding.c:179-187), antenna sums in order
     hh = __fadd_rn(hh, __fadd_rn(__fmul_rn(h.x, h.x), __fmul_rn(h.y, h.y)));
     // y * conj(h) as PROD_AVX (addsub of products, :150): re = yr*hr - yi*(-hi)
@@ -121,6 +140,9 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t 
   }
   return e;
 }
+__device__ __forceinline__ Eq equalise(const LlrItem &t, uint32_t pos, uint32_t j) {
+  return equalise(t, load_re(t, pos, false), j);
+}
 
 // complex float arithmetic in the order gcc evaluates the reference's cf_t expressions
 struct cf {
@@ -135,6 +157,7 @@ __device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
   const float2 v = p[pos];
   return {v.x, v.y};
 }
+__device__ __forceinline__ cf c_of(float2 v) { return {v.x, v.y}; }
 
 // TM3 large-delay CDD, 2 ports x 2 rx antennas, 2 layers (precoding.c:930-1019): the precoder
 // alternates per RE (even: H = [[h00+h10, h00-h10], [h01+h11, h01-h11]] with h[port][rx], odd: the
@@ -145,9 +168,9 @@ __device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
 // H = [[h00, h10], [h01, h11]] (norm sqrt 2 / scaling), 1 [[h00+h10, h00-h10], [h01+h11, h01-h11]],
 // 2 [[h00+j h10, h00-j h10], [h01+j h11, h01-j h11]] (norm 2 / scaling), j h = (-h.i, h.r) exactly.
 __device__ __forceinline__ cf c_mulj(cf a) { return {-a.i, a.r}; }
-__device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint32_t j) {
-  const cf p00 = c_ld(t.h[0][0], pos), p01 = c_ld(t.h[0][1], pos);
-  const cf p10 = c_ld(t.h[1][0], pos), p11 = c_ld(t.h[1][1], pos);
+__device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, const ReIn &in, uint32_t j) {
+  const cf p00 = c_of(in.h[0][0]), p01 = c_of(in.h[0][1]);
+  const cf p10 = c_of(in.h[1][0]), p11 = c_of(in.h[1][1]);
   cf h00, h01, h10, h11;
   float norm = 2.0f / t.scaling;
   if (t.mux == 1) { // codebook 0
@@ -196,7 +219,7 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint3
   const cf b0 = t.layer == 0 ? bd : bo, b1 = t.layer == 0 ? bo : bd;
   const cf wa = c_add(c_mul(b0, _h00), c_mul(b1, _h01));
   const cf wb = c_add(c_mul(b0, _h10), c_mul(b1, _h11));
-  const cf y0 = c_ld(t.y[0], pos), y1 = c_ld(t.y[1], pos);
+  const cf y0 = c_of(in.y[0]), y1 = c_of(in.y[1]);
   const cf x = c_add(c_mul(y0, wa), c_mul(y1, wb));
   Eq e;
   e.xr = x.r;
@@ -210,10 +233,10 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, uint32_t pos, uint3
 // combination of the two ports at rx 0 / 1 (0: h0+h1, 1: h0-h1, 2: h0+j h1, 3: h0-j h1),
 // hh = norm / (|h0|^2 + |h1|^2) summed left to right, x = (conj(h0) y0 + conj(h1) y1) hh,
 // csi = (|h0|^2 + |h1|^2) / norm * (float) M_SQRT1_2, norm = (float) M_SQRT2 / scaling.
-__device__ __forceinline__ Eq equalise_mrc(const LlrItem &t, uint32_t pos) {
+__device__ __forceinline__ Eq equalise_mrc(const LlrItem &t, const ReIn &in) {
   const int cb = -t.mux - 1;
-  const cf p00 = c_ld(t.h[0][0], pos), p01 = c_ld(t.h[0][1], pos);
-  const cf p10 = c_ld(t.h[1][0], pos), p11 = c_ld(t.h[1][1], pos);
+  const cf p00 = c_of(in.h[0][0]), p01 = c_of(in.h[0][1]);
+  const cf p10 = c_of(in.h[1][0]), p11 = c_of(in.h[1][1]);
   cf h0, h1;
   if (cb == 0) {
     h0 = c_add(p00, p10);
@@ -231,7 +254,7 @@ __device__ __forceinline__ Eq equalise_mrc(const LlrItem &t, uint32_t pos) {
   const float norm = 1.41421354f / t.scaling;
   const float s = h0.r * h0.r + h0.i * h0.i + h1.r * h1.r + h1.i * h1.i;
   const float hh = norm / s;
-  const cf y0 = c_ld(t.y[0], pos), y1 = c_ld(t.y[1], pos);
+  const cf y0 = c_of(in.y[0]), y1 = c_of(in.y[1]);
   const cf x = c_add(c_mul(c_conj(h0), y0), c_mul(c_conj(h1), y1));
   Eq e;
   e.xr = x.r * hh;
@@ -429,39 +452,79 @@ __device__ __forceinline__ void demap8(int mod, uint32_t j, uint32_t n, float xr
   }
 }
 
+// demap, descramble and store the LLRs of RE j (and its CSI)
+template <int MOD>
+__device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &e, uint32_t c0, uint32_t c1) {
+  constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
+  int16_t o[Q];
+  if (t.llr8)
+    demap8(MOD, j, t.nof_re, e.xr, e.xi, o);
+  else
+    demap(MOD, j, t.nof_re, e.xr, e.xi, o);
+  // scrambling bits b0 .. b0+Q-1 (may straddle the two words c0, c1)
+  const uint32_t b0 = j * Q, sh = b0 & 31;
+  const uint32_t cb = (uint32_t)((((uint64_t)c1 << 32) | c0) >> sh);
+#pragma unroll
+  for (int k = 0; k < Q; k++)
+    if ((cb >> k) & 1) // _mm256_sign_epi16 / _epi8 (scrambling_sb_offset) by c = 1 - 2c
+      o[k] = t.llr8 ? wrap8(-(int32_t)o[k]) : wrap16(-(int32_t)o[k]);
+  if (Q % 2 == 0 && t.aligned) {
+    uint32_t *dst = reinterpret_cast<uint32_t *>(t.e + b0);
+#pragma unroll
+    for (int k = 0; k < Q; k += 2) dst[k / 2] = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
+  } else {
+#pragma unroll
+    for (int k = 0; k < Q; k++) t.e[b0 + k] = o[k];
+  }
+  if (t.csi_mode) {
+    t.csi[j] = e.csi;
+    atomicMax(t.csi_max, __float_as_uint(e.csi)); // csi >= 0: uint order == float order
+  }
+}
+
+// LLR_RES REs per thread (stride gridDim.x * 256): every RE's map entry, then its grid / estimate
+// values and scrambling words are loaded before the first one is computed, so a thread waits for
+// two round trips per LLR_RES REs instead of per RE (one RE per thread left the kernel at ~1.5 TB/s,
+// bound by the dependent map -> grid load chain). TM2 pairs REs across the map and keeps the
+// one-RE loop.
+#define LLR_RES 4
 template <int MOD>
 __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
-  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
-    const uint32_t pos = t.map[j];
-    const Eq e = t.txdiv ? equalise_txdiv(t, j)
-                 : (t.cdd || t.mux > 0) ? equalise_cdd(t, pos, j)
-                 : t.mux < 0 ? equalise_mrc(t, pos)
-                             : equalise(t, pos, j);
-    int16_t o[Q];
-    if (t.llr8)
-      demap8(MOD, j, t.nof_re, e.xr, e.xi, o);
-    else
-      demap(MOD, j, t.nof_re, e.xr, e.xi, o);
-    // scrambling bits b0 .. b0+Q-1 (may straddle two words)
-    const uint32_t b0 = j * Q, w = b0 >> 5, sh = b0 & 31;
-    const uint64_t cw = (uint64_t)t.c[w] | ((uint64_t)t.c[w + 1] << 32);
-    const uint32_t cb = (uint32_t)(cw >> sh);
-#pragma unroll
-    for (int k = 0; k < Q; k++)
-      if ((cb >> k) & 1) // _mm256_sign_epi16 / _epi8 (scrambling_sb_offset) by c = 1 - 2c
-        o[k] = t.llr8 ? wrap8(-(int32_t)o[k]) : wrap16(-(int32_t)o[k]);
-    if (Q % 2 == 0 && t.aligned) {
-      uint32_t *dst = reinterpret_cast<uint32_t *>(t.e + b0);
-#pragma unroll
-      for (int k = 0; k < Q; k += 2) dst[k / 2] = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
-    } else {
-#pragma unroll
-      for (int k = 0; k < Q; k++) t.e[b0 + k] = o[k];
+  const uint32_t stride = gridDim.x * 256;
+  if (t.txdiv) {
+    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += stride) {
+      const uint32_t w = (j * Q) >> 5;
+      llr_out<MOD>(t, j, equalise_txdiv(t, j), t.c[w], t.c[w + 1]);
     }
-    if (t.csi_mode) {
-      t.csi[j] = e.csi;
-      atomicMax(t.csi_max, __float_as_uint(e.csi)); // csi >= 0: uint order == float order
+    return;
+  }
+  const bool two_ports = t.cdd || t.mux != 0;
+  for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
+    uint32_t pos[LLR_RES];
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      pos[r] = t.map[j < t.nof_re ? j : j0];
+    }
+    ReIn in[LLR_RES];
+    uint32_t c0[LLR_RES], c1[LLR_RES];
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
+      in[r] = load_re(t, pos[r], two_ports);
+      c0[r] = t.c[w];
+      c1[r] = t.c[w + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      if (j >= t.nof_re) break;
+      const Eq e = (t.cdd || t.mux > 0) ? equalise_cdd(t, in[r], j)
+                   : t.mux < 0          ? equalise_mrc(t, in[r])
+                                        : equalise(t, in[r], j);
+      llr_out<MOD>(t, j, e, c0[r], c1[r]);
     }
   }
 }
@@ -559,7 +622,7 @@ hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const u
 
 hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const unsigned gx = std::min(cdiv(max_re, 256), 64u);
+  const unsigned gx = std::min(cdiv(max_re, 256 * LLR_RES), 64u);
   hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
   if (csi) {
     const unsigned gb = std::min(cdiv((size_t)max_re * 6, 256), 256u);

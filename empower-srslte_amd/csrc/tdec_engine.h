@@ -78,6 +78,8 @@ struct TdecEngine {
   // concatenated per-group arrays: SP0 short4; XP1 = X2, P1 short2 planes of cap_elems; A short2;
   // T short2 [pairs][12]; D packed decisions; scratch (sequential decoders)
   void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr, *D = nullptr, *scratch = nullptr;
+  uint32_t *Dfz = nullptr; // frozen decision words of the fused early stop (TdEs::dfz)
+  uint8_t *cb_end = nullptr; // TdEs::cb_end, zero between jobs
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
   uint32_t *noi = nullptr;
   int16_t *in_stage = nullptr; // host-pointer API staging
@@ -99,6 +101,16 @@ struct TdecEngine {
   int kind_blocks[TD_NKIND] = {0};
   size_t kind_lds[TD_NKIND] = {0};
   int total_pairs = 0;
+  static int num_cus() {
+    static const int n = [] {
+      int dev = 0, v = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+        return 256;
+      return v;
+    }();
+    return n;
+  }
   // K and interleaver of the last single-size job (the drop-in srslte_tdec_* path)
   uint32_t K = 0;
   const uint16_t *fwd = nullptr, *rev = nullptr, *dmap = nullptr;
@@ -132,6 +144,9 @@ struct TdecEngine {
     HIPCHK(hipMalloc(&cb_ok, cap_cbs));
     HIPCHK(hipMalloc(&pair_done, cap_pairs));
     HIPCHK(hipMalloc(&noi, (size_t)cap_cbs * 4));
+    HIPCHK(hipMalloc(&Dfz, cap_dw * 4));
+    HIPCHK(hipMalloc(&cb_end, cap_cbs));
+    HIPCHK(hipMemset(cb_end, 0, cap_cbs));
     HIPCHK(hipEventCreateWithFlags(&gev, hipEventDisableTiming));
     return 0;
   }
@@ -141,7 +156,7 @@ struct TdecEngine {
     for (void *p : {SP0, XP1, A, D, T, scratch, (void *)d_groups})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
-                    (void *)out_stage})
+                    (void *)out_stage, (void *)Dfz, (void *)cb_end})
       if (p) (void)hipFree(p);
     if (h_groups) (void)hipHostFree(h_groups);
     if (gev) (void)hipEventDestroy(gev);
@@ -559,16 +574,29 @@ struct TdecEngine {
     // td_sched().es_chunk: half-iterations per early-stop launch. One launch per half-iteration
     // (with the CRC check inside, no decide launch) lets the kernels of other streams in between;
     // longer launches save launches but hold every CU until they end
-    const bool fused = td_sched().fused != 0;
+    const int es_mode = td_sched().es_fused;
+    // es_fused 2 (auto): a kind runs fused when its workgroups fit on the chip at once (small,
+    // launch-bound jobs such as C5's); a larger job keeps one launch per half-iteration, whose
+    // kernel boundaries let the front end of other streams in and bound the tail of the last
+    // round of workgroups to one half-iteration
+    auto es_on = [&](int k) {
+      if (!halfits_es_fusable(k) || es_mode == 0) return false;
+      if (es_mode == 1) return true;
+      const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, 160 * 1024 / (kind_lds[k] + 2048)));
+      return (size_t)kind_blocks[k] <= (size_t)num_cus() * per_cu;
+    };
     const int chunk = td_sched().es_chunk;
-    bool seq = false;
+    bool seq = false, es_any = false;
     const TdArrays a = arrays();
+    TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end};
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      if (fused && halfits_es_fusable(k)) {
+      if (es_on(k)) {
+        es_any = true;
         for (int n0 = 0; n0 < (int)maxh; n0 += chunk) {
-          const TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, n0, std::min(n0 + chunk, (int)maxh)};
+          es.n0 = n0;
+          es.n1 = std::min(n0 + chunk, (int)maxh);
           ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", st);
           HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
         }
@@ -576,13 +604,17 @@ struct TdecEngine {
         seq = true;
       }
     }
+    if (es_any) {
+      ProfScope ps("k_es_bytes", st);
+      HIPCHK(launch_es_bytes(d_groups, (int)groups.size(), total_pairs, es, st));
+    }
     last_n = (int)maxh - 1;
     if (!seq) return 0;
     for (uint32_t h = 0; h < maxh; h++) {
       last_n = (int)h;
       for (int k = 0; k < TD_NKIND; k++) {
         const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
-        if (g1 <= g0 || (fused && halfits_es_fusable(k))) continue;
+        if (g1 <= g0 || es_on(k)) continue;
         static const char *const names[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
                                                      "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
         ProfScope ps(names[k], st);

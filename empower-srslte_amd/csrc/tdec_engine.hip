@@ -258,18 +258,21 @@ int srsgpu_tdec_batch_decode(srsgpu_tdec_batch_t *q, int impl, int sb_layout, co
   return 0;
 }
 
-int srsgpu_tdec_set_schedule(int fused, int es_chunk, int sse_bidir) {
-  if (es_chunk == 0) return -1;
+int srsgpu_tdec_set_schedule(int fused, int es_fused, int es_chunk, int sse_bidir) {
+  if (es_chunk == 0 || es_fused > 2) return -1;
   srsgpu::TdSched &t = srsgpu::td_sched();
   if (fused >= 0) t.fused = fused != 0;
+  if (es_fused > 2) return -1;
+  if (es_fused >= 0) t.es_fused = es_fused;
   if (es_chunk > 0) t.es_chunk = es_chunk;
   if (sse_bidir >= 0) t.sse_bidir = sse_bidir != 0;
   return 0;
 }
 
-void srsgpu_tdec_get_schedule(int *fused, int *es_chunk, int *sse_bidir) {
+void srsgpu_tdec_get_schedule(int *fused, int *es_fused, int *es_chunk, int *sse_bidir) {
   const srsgpu::TdSched &t = srsgpu::td_sched();
   if (fused) *fused = t.fused;
+  if (es_fused) *es_fused = t.es_fused;
   if (es_chunk) *es_chunk = t.es_chunk;
   if (sse_bidir) *sse_bidir = t.sse_bidir;
 }

@@ -85,7 +85,7 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
 bool halfits_fusable(int kind);
 // the process-wide launch schedule (srsgpu_tdec_set_schedule)
 struct TdSched {
-  int fused, es_chunk, sse_bidir;
+  int fused, es_fused, es_chunk, sse_bidir;
 };
 TdSched &td_sched();
 bool halfits_es_fusable(int kind);
@@ -100,7 +100,11 @@ struct TdEs {
   uint32_t *noi;
   int max_halfits;
   int n0, n1; // this launch runs half-iterations n0 .. n1-1 (0 <= n0 < n1 <= max_halfits)
+  uint32_t *dfz;  // decision words of the blocks that ended (layout of D), for k_es_bytes
+  uint8_t *cb_end; // per CB: 0, or 1 + parity of the half-iteration that ended it (kept zero between jobs)
 };
+// the natural-order bytes of the blocks the fused launches ended (after the last of them)
+hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st);
 // half-iterations es.n0 .. es.n1-1 of an early-stop job for the groups of one kind in one launch:
 // the CRC after each half-iteration, done / ok / noi and the decision bytes of finished blocks
 // as launch_decide with early = true does, workgroups leave when all their blocks are done

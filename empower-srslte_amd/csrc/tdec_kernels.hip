@@ -41,6 +41,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "tdec_kernels.h"
 
 // translation-unit part (see the launchers at the end); the file alone is part 0
@@ -1121,7 +1123,8 @@ __global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict
 // workgroup before the barrier): the CRC of every unfinished code block, as k_decide folds it
 // (crc.c:144-155 is linear: XOR of the chain-major weights TdGroup::wc over the set decision
 // bits), the done / ok / noi update of sch.c:361-391, and the natural-order bytes of the blocks
-// that end at this half-iteration. Returns (uniformly) whether every block of the workgroup is done.
+// that end at this half-iteration (via Dfz / cb_end and k_es_bytes). Returns (uniformly) whether
+// every block of the workgroup is done.
 template <int NB>
 __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const uint32_t *__restrict__ Darr,
                                       const TdEs &es, uint32_t *red, int *fin) {
@@ -1195,42 +1198,21 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
     fin[t] = done | (now << 1);
   }
   __syncthreads();
-  // natural-order bytes (turbodecoder.c:353-360 + decision_byte, MSB first) of the blocks that
-  // ended now: 64 consecutive positions per ballot, as k_decide
-  const gptr_t<uint16_t> dmap = gptr(G.dmap);
-  const float invL = 1.0f / (float)L;
-  const int gap = 16 * G16 - L;
+  // The blocks that ended now keep their decision words: copied (their 16-bit halves) into the
+  // frozen plane Dfz, the half-iteration's parity in cb_end; k_es_bytes turns them into bytes
+  // after the launches (a byte loop here held the workgroup, and with it its CU's LDS, for
+  // ~100 us per launch).
   bool all = true;
 #pragma unroll
   for (int lp = 0; lp < NP; lp++) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int f = fin[lp * 2 + h];
-      all = all && (f & 1);
-      if (!(f & 2)) continue;
-      const int cb = G.cb0 + 2 * (pw + lp) + h;
-      const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
-      uint8_t *ob = es.outb + (size_t)cb * es.out_stride;
-      for (int p0 = wv * 64; p0 < K; p0 += 128) {
-        const int p = p0 + lane;
-        uint32_t bit = 0u;
-        if (p < K) {
-          int ci;
-          if (dec2) {
-            ci = (int)dmap[p];
-          } else {
-            const int d = (int)(((float)p + 0.5f) * invL);
-            ci = p + d * gap;
-          }
-          bit = (dw[ci >> 4] >> ((ci & 15) + 16 * h)) & 1u;
-        }
-        const uint64_t m = __ballot(bit);
-        if (lane < 8 && p0 + 8 * lane < K) {
-          const uint32_t v = (uint32_t)((m >> (8 * lane)) & 0xffu);
-          ob[(p0 >> 3) + lane] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
-        }
-      }
-    }
+    const int f0 = fin[lp * 2], f1 = fin[lp * 2 + 1];
+    all = all && (f0 & 1) && (f1 & 1);
+    const uint32_t mask = ((f0 & 2) ? 0xffffu : 0u) | ((f1 & 2) ? 0xffff0000u : 0u);
+    if (!mask) continue;
+    const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
+    const gmut_t<uint32_t> fz = gmut<uint32_t>(es.dfz + G.dw0 + (size_t)(pw + lp) * nw);
+    for (int q = t; q < nw; q += 128) fz[q] = (fz[q] & ~mask) | (dw[q] & mask);
+    if (t < 2 && (fin[lp * 2 + t] & 2)) es.cb_end[G.cb0 + 2 * (pw + lp) + t] = (uint8_t)(1 + (n & 1));
   }
   return all;
 }
@@ -1489,6 +1471,39 @@ __global__ __launch_bounds__(64) void k_sse_halfit(const TdGroup *__restrict__ g
 // same AL(k), B(k) and branch metrics as turbodecoder_sse.c:105-206, so the outputs are
 // bit-identical to k_sse_halfit. M = 16*floor(K/32) is a multiple of 16, so the two waves'
 // decision words never share a word.
+// Buffer addressing of the SSE decoders: per-group resources (SGPRs), per-lane byte offsets fixed
+// for the launch (VGPRs) and per-step offsets that are wave-uniform (SGPRs), so no load or store
+// needs per-access VGPR address arithmetic (the flat 64-bit form spent one v_lshl_add_u64 and an
+// s_add/s_addc pair per access, more than the recursions themselves).
+struct SseRes {
+  rsrc_t sp0, x2, p1, a, sc, d;
+  uint32_t vo8, vo4, vsc, vd; // lane offsets: SP0 (8-byte elements), X2/P1/A, scratch, D
+  uint32_t row;               // bytes per scratch row (one state of one step for every pair)
+};
+__device__ __forceinline__ void bst32s(uint32_t v, rsrc_t r, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, vo, so, 0);
+}
+__device__ __forceinline__ s2 u2s(uint32_t v) { return __builtin_bit_cast(s2, v); }
+__device__ __forceinline__ uint32_t s2u(s2 v) { return __builtin_bit_cast(uint32_t, v); }
+// the inputs of step k as load_step<MODE, true> reads them (SSE: wrapping app add)
+template <int MODE>
+__device__ __forceinline__ StepIn sse_ld(const SseRes &R, int k) {
+  StepIn r;
+  if (MODE == 1) {
+    r.x = u2s(bld32(R.x2, R.vo4, (uint32_t)k * 4));
+    r.y = u2s(bld32(R.p1, R.vo4, (uint32_t)k * 4));
+    r.e = r.x;
+  } else {
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    const u2v v = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(R.sp0, R.vo8, (uint32_t)k * 8, 0));
+    const s2 a = MODE == 2 ? splat(0) : u2s(bld32(R.a, R.vo4, (uint32_t)k * 4));
+    r.x = wadd(u2s(v.x), a);
+    r.y = u2s(v.y);
+    r.e = a;
+  }
+  return r;
+}
+
 // One half-iteration of the workgroup's 64 pairs; pair p = this lane's pair within the group;
 // `done` lanes (finished pairs, lanes past the group) touch no memory but reach the barrier.
 template <int MODE>
@@ -1500,19 +1515,40 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
   const int K = G.K, npairs = G.npairs;
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
   const int pair = p < npairs ? p : npairs - 1;
-  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, 1);
-  const s4 *sp0 = SP0 + base;
-  s2 *xp1 = XP1 + base;
-  const s2 *p1 = XP1 + plane + base;
-  s2 *A = Aarr + base;
-  uint32_t *D = Darr ? Darr + G.dw0 + (size_t)pair * dec_words(K, 1) : nullptr;
+  const uint32_t pe = (uint32_t)t4_pair_elems(K, 1);
+  SseRes R;
+  R.sp0 = mk_rsrc(SP0 + G.elem0);
+  R.x2 = mk_rsrc(XP1 + G.elem0);
+  R.p1 = mk_rsrc(XP1 + plane + G.elem0);
+  R.a = mk_rsrc(Aarr + G.elem0);
+  R.sc = mk_rsrc(scratch_base + G.sc0);
+  R.d = mk_rsrc(Darr ? Darr + G.dw0 : Darr);
+  R.vo8 = (uint32_t)pair * pe * 8;
+  R.vo4 = (uint32_t)pair * pe * 4;
+  R.vsc = (uint32_t)pair * 4;
+  R.vd = (uint32_t)pair * (uint32_t)dec_words(K, 1) * 4;
+  R.row = (uint32_t)npairs * 4;
+  const bool dout = Darr != nullptr;
   const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
-  const gptr_t<uint16_t> tbl = gptr(MODE == 1 ? G.fwd : G.rev);
-  s2 *scratch = scratch_base + G.sc0;
-  auto AL = [&](int k, int i) -> s2 & { return scratch[((size_t)k * 8 + i) * npairs + pair]; };
+  // the scatter table of the half-iteration, 8 entries (one aligned 16-byte word) per step group,
+  // read through the constant address space: a scalar load into SGPRs (wave-uniform targets, used
+  // as buffer soffsets), waited on with lgkmcnt rather than behind the vector prefetches
+  typedef const __attribute__((address_space(4))) u4 cu4;
+  cu4 *tb4 = (cu4 *)(const __attribute__((address_space(4))) void *)(uintptr_t)(MODE == 1 ? G.fwd : G.rev);
+  auto tbl8 = [&](int k0, int *t) { // k0 a multiple of 8: entries k0 .. k0 + 7
+    const u4 w = tb4[k0 >> 3];
+#pragma unroll
+    for (int u = 0; u < 8; u++) t[u] = (int)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+  };
+  auto al_ld = [&](int k, int i) { return u2s(bld32(R.sc, R.vsc, ((uint32_t)k * 8 + i) * R.row)); };
+  auto al_st = [&](int k, int i, s2 v) { bst32s(s2u(v), R.sc, R.vsc, ((uint32_t)k * 8 + i) * R.row); };
+  auto out_st = [&](int t, s2 llr, s2 e) { // store_out: DEC1 E' into app2, DEC2 into A
+    bst32s(s2u(wsub(llr, e)), MODE == 1 ? R.a : R.x2, R.vo4, (uint32_t)t * 4);
+  };
   const int M = 16 * (K / 32); // K >= 40, a multiple of 8: 16 <= M <= K/2
   constexpr int P = TD_SP;
-  // beta candidates of one step (bp: bit 1, bn: bit 0), their merge, and the LLR against alphas
+  static_assert(P == 8, "tbl8 loads 8 scatter targets per step group");
+  // beta candidates of one step (bp: bit 1, bn: bit 0) and the LLR against the alphas aa
   auto bpn = [](const s2 bb[8], s2 g0, s2 g1, s2 bp[8], s2 bn[8]) {
     bp[0] = wadd(bb[4], g1); bp[1] = wadd(bb[0], g1); bp[2] = wadd(bb[1], g0); bp[3] = wadd(bb[5], g0);
     bp[4] = wadd(bb[6], g0); bp[5] = wadd(bb[2], g0); bp[6] = wadd(bb[3], g1); bp[7] = wadd(bb[7], g1);
@@ -1538,6 +1574,11 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
     n[6] = smax(wadd(a[4], g0), wsub(a[5], g0));
     n[7] = smax(wadd(a[7], g1), wsub(a[6], g1));
   };
+  auto norm = [](s2 v[8]) {
+    const s2 z = v[0];
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = wsub(v[i], z);
+  };
   uint32_t dacc = 0;
   if (role == 0) {
     s2 a[8], apre[8]; // a: the recursion state, apre: AL(k) of the next step
@@ -1546,21 +1587,21 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
     for (int i = 1; i < 8; i++) a[i] = splat(-TD_INF);
 #pragma unroll
     for (int i = 0; i < 8; i++) apre[i] = a[i];
-    if (!done) { // phase 1: alphas of steps 0..M-1
+    if (!done) { // phase 1: alphas of steps 0..M-1 (groups of 8: k & 3 known per unrolled step)
 #pragma unroll
-      for (int i = 0; i < 8; i++) AL(0, i) = a[i];
+      for (int i = 0; i < 8; i++) al_st(0, i, a[i]);
       StepIn nx[P];
 #pragma unroll
-      for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, u);
-      for (int k0 = 0; k0 < M; k0 += P) {
+      for (int u = 0; u < P; u++) nx[u] = sse_ld<MODE>(R, u);
+      for (int g = 0; g < M / P; g++) {
+        const int k0 = g * P;
         StepIn cu[P];
 #pragma unroll
         for (int u = 0; u < P; u++) cu[u] = nx[u];
 #pragma unroll
-        for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, k0 + P + u);
+        for (int u = 0; u < P; u++) nx[u] = sse_ld<MODE>(R, k0 + P + u); // < K: M <= K - 8
 #pragma unroll
         for (int u = 0; u < P; u++) {
-          const int k = k0 + u;
           const s2 g1 = wadd(cu[u].x, cu[u].y) >> 1, g0 = wsub(cu[u].x, cu[u].y) >> 1;
           s2 n[8];
           astep(a, g0, g1, n);
@@ -1569,15 +1610,11 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
             a[i] = n[i];
             apre[i] = n[i];
           }
-          if (k + 1 < M) {
+          if (u < P - 1 || k0 + P < M) { // AL(M) is the beta wave's slot
 #pragma unroll
-            for (int i = 0; i < 8; i++) AL(k + 1, i) = n[i];
+            for (int i = 0; i < 8; i++) al_st(k0 + u + 1, i, n[i]);
           }
-          if ((k & 3) == 3) {
-            const s2 z = a[0];
-#pragma unroll
-            for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
-          }
+          if ((u & 3) == 3) norm(a);
         }
       }
     }
@@ -1591,15 +1628,15 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
     auto fetch = [&](int k1, StepIn *fs, s2 (*fb)[8], int *ft) {
 #pragma unroll
       for (int u = 0; u < P; u++) {
-        const int k = k1 + u;
-        fs[u] = load_step<MODE, true>(sp0, xp1, p1, A, k);
+        fs[u] = sse_ld<MODE>(R, k1 + u);
 #pragma unroll
-        for (int i = 0; i < 8; i++) fb[u][i] = AL(k, i);
-        ft[u] = tbl[k];
+        for (int i = 0; i < 8; i++) fb[u][i] = al_ld(k1 + u, i);
       }
+      tbl8(k1, ft);
     };
     fetch(M, nx, nb, nt);
-    for (int k0 = M; k0 < K; k0 += P) {
+    for (int g = 0; g < (K - M) / P; g++) {
+      const int k0 = M + g * P;
       StepIn cs[P];
       s2 cb[P][8];
       int ct[P];
@@ -1619,11 +1656,11 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
         s2 bp[8], bn[8];
         bpn(cb[u], g0, g1, bp, bn);
         const s2 llr = llr_of(bp, bn, apre);
-        store_out<MODE == 1>(xp1, A, ct[u], llr, st.e);
-        if (D) { // k ascends: flush each 16-step group at its last step
+        out_st(ct[u], llr, st.e);
+        if (dout) { // k ascends: flush each 16-step group at its last step (M and K multiples of 8)
           dacc |= dec_bits(llr) << (k & 15);
-          if ((k & 15) == 15 || k == K - 1) {
-            D[k >> 4] = dacc;
+          if (u == P - 1 && ((k & 15) == 15 || k == K - 1)) {
+            bst32s(dacc, R.d, R.vd, (uint32_t)(k >> 4) * 4);
             dacc = 0;
           }
         }
@@ -1634,11 +1671,7 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
           a[i] = n[i];
           apre[i] = n[i];
         }
-        if ((k & 3) == 3) {
-          const s2 z = a[0];
-#pragma unroll
-          for (int i = 0; i < 8; i++) a[i] = wsub(a[i], z);
-        }
+        if ((u & 3) == 3) norm(a);
       }
     }
     return;
@@ -1660,28 +1693,25 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
     }
     StepIn nx[P];
 #pragma unroll
-    for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, K - 1 - u);
-    for (int k1 = K - 1; k1 >= M; k1 -= P) {
+    for (int u = 0; u < P; u++) nx[u] = sse_ld<MODE>(R, K - 1 - u);
+    for (int g = 0; g < (K - M) / P; g++) {
+      const int k1 = K - 1 - g * P; // k1 - u = 8 j + 7 - u: (k & 3) == 0 at u = 3, 7
       StepIn cu[P];
 #pragma unroll
       for (int u = 0; u < P; u++) cu[u] = nx[u];
 #pragma unroll
-      for (int u = 0; u < P; u++) nx[u] = load_step<MODE, true>(sp0, xp1, p1, A, k1 - P - u);
+      for (int u = 0; u < P; u++) nx[u] = sse_ld<MODE>(R, k1 - P - u); // >= M - 8 >= 8
 #pragma unroll
       for (int u = 0; u < P; u++) {
         const int k = k1 - u;
 #pragma unroll
-        for (int i = 0; i < 8; i++) AL(k, i) = b[i]; // B(k)
+        for (int i = 0; i < 8; i++) al_st(k, i, b[i]); // B(k)
         const s2 g1 = wadd(cu[u].x, cu[u].y) >> 1, g0 = wsub(cu[u].x, cu[u].y) >> 1;
         s2 bp[8], bn[8];
         bpn(b, g0, g1, bp, bn);
 #pragma unroll
         for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
-        if ((k & 3) == 0) {
-          const s2 z = b[0];
-#pragma unroll
-          for (int i = 0; i < 8; i++) b[i] = wsub(b[i], z);
-        }
+        if ((u & 3) == 3) norm(b);
       }
     }
   }
@@ -1694,15 +1724,18 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
   auto fetchb = [&](int k1, StepIn *fs, s2 (*fa)[8], int *ft) {
 #pragma unroll
     for (int u = 0; u < P; u++) {
-      const int k = k1 - u;
-      fs[u] = load_step<MODE, true>(sp0, xp1, p1, A, k);
+      fs[u] = sse_ld<MODE>(R, k1 - u);
 #pragma unroll
-      for (int i = 0; i < 8; i++) fa[u][i] = AL(k, i);
-      ft[u] = tbl[k];
+      for (int i = 0; i < 8; i++) fa[u][i] = al_ld(k1 - u, i);
     }
+    int t8[8];
+    tbl8(k1 - (P - 1), t8);
+#pragma unroll
+    for (int u = 0; u < P; u++) ft[u] = t8[P - 1 - u];
   };
   fetchb(M - 1, ns, na, nt);
-  for (int k1 = M - 1; k1 >= 0; k1 -= P) {
+  for (int g = 0; g < M / P; g++) {
+    const int k1 = M - 1 - g * P;
     StepIn cs[P];
     s2 ca[P][8];
     int ct[P];
@@ -1724,19 +1757,15 @@ __device__ __forceinline__ void sse_bidir_body(const TdGroup &G, int p, bool don
 #pragma unroll
       for (int i = 0; i < 8; i++) b[i] = smax(bp[i], bn[i]);
       const s2 llr = llr_of(bp, bn, ca[u]);
-      store_out<MODE == 1>(xp1, A, ct[u], llr, st.e);
-      if (D) { // k descends: flush each 16-step group at its first step
+      out_st(ct[u], llr, st.e);
+      if (dout) { // k descends: flush each 16-step group at its first step
         dacc |= dec_bits(llr) << (k & 15);
-        if ((k & 15) == 0) {
-          D[k >> 4] = dacc;
+        if (u == P - 1 && (k & 15) == 0) {
+          bst32s(dacc, R.d, R.vd, (uint32_t)(k >> 4) * 4);
           dacc = 0;
         }
       }
-      if ((k & 3) == 0) {
-        const s2 z = b[0];
-#pragma unroll
-        for (int i = 0; i < 8; i++) b[i] = wsub(b[i], z);
-      }
+      if ((u & 3) == 3) norm(b);
     }
   }
 }
@@ -1756,9 +1785,9 @@ __global__ __launch_bounds__(128) void k_sse_bidir(const TdGroup *__restrict__ g
 
 // The early stop of the SSE decoder after half-iteration n, as es_check does it for the window
 // kernels (CRC as the XOR of the weights TdGroup::wc over the set decision bits, crc.c:144-155;
-// the done / ok / noi update of sch.c:361-391; natural-order bytes of the blocks ending now), one
-// pair per lane: each wave folds the decision words it wrote (wave 1 those below M / 16, wave 0
-// the rest), wave 0 combines and decides, then wave h writes the bytes of CB h of its pair.
+// the done / ok / noi update of sch.c:361-391; the decision words of the blocks ending now kept
+// for k_es_bytes), one pair per lane: each wave folds the decision words it wrote (wave 1 those
+// below M / 16, wave 0 the rest), wave 0 combines, decides and keeps the words.
 // fin[2 lane + h]: bit 0 = done, bit 1 = ended at this check. Returns (uniformly) whether every
 // pair of the workgroup is done.
 template <int V = 0> // a template so that only the part that launches k_sse_es instantiates it
@@ -1815,22 +1844,17 @@ __device__ __noinline__ bool sse_es_check(const TdGroup &G, int p, int n, const 
       fin[2 * lane + h] = f & 1 ? f : 0;
     }
   }
-  __syncthreads();
-  const int f = fin[2 * lane + wv];
-  if (f & 2) { // CB wv of this pair ended now: its K / 8 bytes, MSB first
-    const gptr_t<uint16_t> dmap = gptr(G.dmap);
-    uint8_t *ob = es.outb + (size_t)(G.cb0 + 2 * p + wv) * es.out_stride;
-    for (int b = 0; b < K / 8; b++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const int pos = 8 * b + i;
-        const int ci = dec2 ? (int)dmap[pos] : pos;
-        v = (v << 1) | ((dw[ci >> 4] >> ((ci & 15) + 16 * wv)) & 1u);
-      }
-      ob[b] = (uint8_t)v;
+  if (!wv) { // blocks that ended now: their decision words into Dfz, parity into cb_end (es_check)
+    const int f0 = fin[2 * lane], f1 = fin[2 * lane + 1];
+    const uint32_t mask = ((f0 & 2) ? 0xffffu : 0u) | ((f1 & 2) ? 0xffff0000u : 0u);
+    if (mask) {
+      const gmut_t<uint32_t> fz = gmut<uint32_t>(es.dfz + G.dw0 + (size_t)pair * nw);
+      for (int q = 0; q < nw; q++) fz[q] = (fz[q] & ~mask) | (dw[q] & mask);
+      if (f0 & 2) es.cb_end[G.cb0 + 2 * p] = (uint8_t)(1 + (n & 1));
+      if (f1 & 2) es.cb_end[G.cb0 + 2 * p + 1] = (uint8_t)(1 + (n & 1));
     }
   }
+  __syncthreads();
   return __syncthreads_and((fin[2 * lane] & 1) && (fin[2 * lane + 1] & 1));
 }
 
@@ -2267,6 +2291,68 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
   }
 }
 
+// Natural-order bytes of the blocks a fused early-stop decode ended (es_check / sse_es_check kept
+// their decision words in Dfz and 1 + the parity of the ending half-iteration in cb_end), as
+// k_decide writes them (turbodecoder.c:353-360 + decision_byte, MSB first); one workgroup per CB
+// pair, many pairs in flight. Clears cb_end behind it.
+__global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ groups, int ngroups,
+                                                  const uint32_t *__restrict__ Dfz,
+                                                  uint8_t *__restrict__ outb, size_t out_stride,
+                                                  uint8_t *__restrict__ cb_end) {
+  __shared__ uint32_t dw[6144 / 16 + 16];
+  const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, NB = G.nb, ncb = G.ncb;
+  const int pair = blockIdx.x - G.pair0;
+  if (pair >= G.npairs) return;
+  const int cbs[2] = {G.cb0 + 2 * pair, 2 * pair + 1 < ncb ? G.cb0 + 2 * pair + 1 : -1};
+  const int ends[2] = {cb_end[cbs[0]], cbs[1] >= 0 ? cb_end[cbs[1]] : 0};
+  if (!ends[0] && !ends[1]) return;
+  const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
+  const uint32_t *src = Dfz + G.dw0 + (size_t)pair * nw;
+  for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
+  __syncthreads();
+  const gptr_t<uint16_t> dmap = gptr(G.dmap);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float invL = 1.0f / (float)L;
+  const int gap = 16 * G16 - L;
+  constexpr int PMAX = 6144 / 256;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    if (!ends[h]) continue;
+    const bool dec2 = ends[h] == 2;
+    int ci[PMAX];
+#pragma unroll
+    for (int u = 0; u < PMAX; u++) { // every map load issued before the first use
+      const int p = wv * 64 + u * 256 + lane;
+      int c = 0;
+      if (p < K) {
+        if (dec2) {
+          c = (int)dmap[p];
+        } else {
+          const int d = (int)(((float)p + 0.5f) * invL);
+          c = p + d * gap;
+        }
+      }
+      ci[u] = c;
+    }
+    uint8_t *ob = outb + (size_t)cbs[h] * out_stride;
+#pragma unroll
+    for (int u = 0; u < PMAX; u++) {
+      const int p0 = wv * 64 + u * 256;
+      if (p0 >= K) break;
+      const int p = p0 + lane;
+      const uint32_t bit = p < K ? (dw[ci[u] >> 4] >> ((ci[u] & 15) + 16 * h)) & 1u : 0u;
+      const uint64_t m = __ballot(bit);
+      if (lane < 8 && p0 + 8 * lane < K) {
+        const uint32_t v = (uint32_t)((m >> (8 * lane)) & 0xffu);
+        ob[(p0 >> 3) + lane] = (uint8_t)(__builtin_bitreverse32(v) >> 24);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && cbs[threadIdx.x] >= 0) cb_end[cbs[threadIdx.x]] = 0;
+}
+
 // pair_done = both code blocks finished (seeding after init_done)
 __global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
                             const uint8_t *__restrict__ cb_done, uint8_t *__restrict__ pair_done) {
@@ -2477,7 +2563,8 @@ TdSched &td_sched() {
       const char *e = getenv(n);
       return e && e[0] ? atoi(e) : d;
     };
-    TdSched t{env("SRSGPU_TDEC_FUSED", 1) != 0, env("SRSGPU_ES_CHUNK", 1), env("SRSGPU_SSE_BIDIR", 1) != 0};
+    TdSched t{env("SRSGPU_TDEC_FUSED", 1) != 0, std::min(std::max(env("SRSGPU_ES_FUSED", 2), 0), 2),
+              env("SRSGPU_ES_CHUNK", 8), env("SRSGPU_SSE_BIDIR", 1) != 0};
     if (t.es_chunk < 1) t.es_chunk = 1;
     return t;
   }();
@@ -2514,6 +2601,13 @@ hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, dg, ng, npairs, cb_done,
                      pair_done);
+  return hipGetLastError();
+}
+
+hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_es_bytes, dim3(npairs), dim3(256), 0, st, dg, ng, (const uint32_t *)es.dfz,
+                     es.outb, es.out_stride, es.cb_end);
   return hipGetLastError();
 }
 

@@ -299,8 +299,8 @@ _sig = {
     "srsgpu_rxq_decode": (_i32, [_vp, _vp]),
     "srsgpu_rxq_flush": (None, [_vp]),
     "srsgpu_rxq_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
-    "srsgpu_tdec_set_schedule": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 3),
+    "srsgpu_tdec_set_schedule": (ctypes.c_int, [ctypes.c_int] * 4),
+    "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 4),
     "srsgpu_rxq_drive": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint32, _vp, _vp, _vp]),
     "srsgpu_rxq_get_chest": (_vp, [_vp]),
@@ -990,16 +990,16 @@ def shard_weighted(weights, world):
     return owner, load
 
 
-def set_schedule(fused=-1, es_chunk=-1, sse_bidir=-1):
+def set_schedule(fused=-1, es_fused=-1, es_chunk=-1, sse_bidir=-1):
     """srsgpu_tdec_set_schedule: the decoder launch schedule (results are identical under all)"""
-    if _lib.srsgpu_tdec_set_schedule(fused, es_chunk, sse_bidir) != 0:
+    if _lib.srsgpu_tdec_set_schedule(fused, es_fused, es_chunk, sse_bidir) != 0:
         raise ValueError("invalid decoder schedule")
 
 
 def get_schedule():
-    v = [ctypes.c_int(0) for _ in range(3)]
+    v = [ctypes.c_int(0) for _ in range(4)]
     _lib.srsgpu_tdec_get_schedule(*[ctypes.byref(x) for x in v])
-    return {"fused": v[0].value, "es_chunk": v[1].value, "sse_bidir": v[2].value}
+    return dict(zip(("fused", "es_fused", "es_chunk", "sse_bidir"), (x.value for x in v)))
 
 
 class RxQueue:

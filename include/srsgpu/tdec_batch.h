@@ -84,16 +84,19 @@ int srsgpu_tdec_batch_read_state(srsgpu_tdec_batch_t *q, uint32_t cb, int16_t *a
 uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t long_cb);
 
 /* Decoder launch schedule (process-wide; results are identical under every setting):
- *   fused      1: fixed-iteration jobs run all half-iterations in one launch per decoder kind and
- *                 early-stop jobs check the CRC inside the decoder launch; 0: one decoder launch per
- *                 half-iteration plus a k_decide launch (SRSGPU_TDEC_FUSED)
- *   es_chunk   half-iterations per early-stop launch, >= 1 (SRSGPU_ES_CHUNK)
- *   sse_bidir  1: the two-wave SSE decoder (with fused early stop), 0: the one-wave one
- *                 (SRSGPU_SSE_BIDIR)
+ *   fused      1: fixed-iteration jobs run all half-iterations in one launch per decoder kind;
+ *              0: one launch per half-iteration (SRSGPU_TDEC_FUSED)
+ *   es_fused   1: early-stop jobs check the CRC inside the decoder launches (k_win_bidir_es,
+ *                 k_sse_es) and write the bytes in one k_es_bytes launch; 0: one decoder launch
+ *                 and one k_decide launch per half-iteration; 2 (default): per decoder kind, fused
+ *                 when its workgroups fit on the chip at once (SRSGPU_ES_FUSED)
+ *   es_chunk   half-iterations per fused early-stop launch, >= 1, default 8 (SRSGPU_ES_CHUNK)
+ *   sse_bidir  1: the two-wave SSE decoder, 0: the one-wave one (SRSGPU_SSE_BIDIR; the fused early
+ *                 stop of the SSE kind needs the two-wave one)
  * A negative argument keeps the current value; the defaults come from those environment variables.
- * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0. */
-int srsgpu_tdec_set_schedule(int fused, int es_chunk, int sse_bidir);
-void srsgpu_tdec_get_schedule(int *fused, int *es_chunk, int *sse_bidir);
+ * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0 or es_fused > 2. */
+int srsgpu_tdec_set_schedule(int fused, int es_fused, int es_chunk, int sse_bidir);
+void srsgpu_tdec_get_schedule(int *fused, int *es_fused, int *es_chunk, int *sse_bidir);
 
 /* Live kernel timing with HIP events on the batch stream (for bench.py's roofline). */
 void srsgpu_prof_enable(int on);

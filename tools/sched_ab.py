@@ -13,11 +13,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 SCHEDULES = {
-    "fused_es1": dict(fused=1, es_chunk=1, sse_bidir=1),
-    "fused_es2": dict(fused=1, es_chunk=2, sse_bidir=1),
-    "fused_es8": dict(fused=1, es_chunk=8, sse_bidir=1),
-    "per_halfit": dict(fused=0, es_chunk=1, sse_bidir=1),
-    "per_halfit_sse1": dict(fused=0, es_chunk=1, sse_bidir=0),
+    "auto": dict(es_fused=2, es_chunk=8, sse_bidir=1),
+    "es_fused8": dict(es_fused=1, es_chunk=8, sse_bidir=1),
+    "es_fused1": dict(es_fused=1, es_chunk=1, sse_bidir=1),
+    "per_halfit": dict(es_fused=0, es_chunk=8, sse_bidir=1),
+    "per_halfit_sse1": dict(es_fused=0, es_chunk=8, sse_bidir=0),
 }
 
 
