@@ -69,9 +69,25 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
     // one address-unit slot per lane)
     const uint32_t nw = (ne + 1) / 2;
     if (((uintptr_t)it.e & 3) == 0) { // E is even for every Qm; an odd tail is read alone
+      // 16-byte loads for the aligned middle, 4-byte loads for the head and tail words
       const gp_t<const uint32_t> e32 = glob(reinterpret_cast<const uint32_t *>(it.e));
-      for (uint32_t w = threadIdx.x; w < ne / 2; w += blockDim.x) es[w] = e32[w];
-      if ((ne & 1) && threadIdx.x == 0) es[ne / 2] = e[ne - 1];
+      const uint32_t nw2 = ne / 2;
+      const uint32_t head = (uint32_t)((16 - ((uintptr_t)it.e & 15)) & 15) / 4; // words to alignment
+      const uint32_t h = head < nw2 ? head : nw2;
+      const uint32_t nq = (nw2 - h) / 4;
+      const gp_t<const u4v> e4 = glob(reinterpret_cast<const u4v *>(it.e + 2 * h));
+#pragma unroll 4
+      for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+        const u4v v = e4[q];
+        es[h + 4 * q] = v.x;
+        es[h + 4 * q + 1] = v.y;
+        es[h + 4 * q + 2] = v.z;
+        es[h + 4 * q + 3] = v.w;
+      }
+      const uint32_t t0 = h + 4 * nq; // tail words t0 .. nw2-1 (at most 3) and the head words
+      if (threadIdx.x < h) es[threadIdx.x] = e32[threadIdx.x];
+      if (threadIdx.x >= 64 && threadIdx.x - 64 < nw2 - t0) es[t0 + threadIdx.x - 64] = e32[t0 + threadIdx.x - 64];
+      if ((ne & 1) && threadIdx.x == 128) es[ne / 2] = e[ne - 1];
     } else {
       for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
         es[w] = (uint32_t)e[2 * w] | (2 * w + 1 < ne ? (uint32_t)e[2 * w + 1] << 16 : 0u);

@@ -100,3 +100,37 @@ def test_python_tdec_struct_has_the_c_size():
     assert ctypes.sizeof(srsgpu_phy.srslte_tdec_t) == srsgpu_phy.SRSLTE_TDEC_REF_SIZEOF
     hdr = open(os.path.join(REPO, "include", "srslte", "phy", "fec", "turbodecoder.h")).read()
     assert "#define SRSLTE_TDEC_REF_SIZEOF %d" % srsgpu_phy.SRSLTE_TDEC_REF_SIZEOF in hdr
+
+
+def test_decoder_schedule_api():
+    """srsgpu_tdec_set_schedule / _get_schedule (host only): defaults, keep-on-negative, refusals."""
+    import srsgpu_phy as s
+    keep = s.get_schedule()
+    try:
+        assert set(keep) == {"fused", "es_fused", "es_chunk", "sse_bidir"}
+        s.set_schedule(fused=0, es_fused=1, es_chunk=3, sse_bidir=0)
+        assert s.get_schedule() == {"fused": 0, "es_fused": 1, "es_chunk": 3, "sse_bidir": 0}
+        s.set_schedule(es_chunk=5)  # the others kept
+        assert s.get_schedule() == {"fused": 0, "es_fused": 1, "es_chunk": 5, "sse_bidir": 0}
+        for bad in (dict(es_chunk=0), dict(es_fused=3)):
+            try:
+                s.set_schedule(**bad)
+                raise AssertionError(bad)
+            except ValueError:
+                pass
+        assert s.get_schedule()["es_chunk"] == 5
+    finally:
+        s.set_schedule(**keep)
+    assert s.get_schedule() == keep
+
+
+def test_rxq_drive_refuses_bad_arguments():
+    """srsgpu_rxq_drive without a queue or with no workers returns -1 (no GPU call)."""
+    lib = ctypes.CDLL(LIB)
+    lib.srsgpu_rxq_drive.restype = ctypes.c_int
+    lib.srsgpu_rxq_drive.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint32] * 3 + [ctypes.c_void_p] * 3
+    t = (ctypes.c_double * 1)()
+    st = (ctypes.c_int32 * 1)()
+    assert lib.srsgpu_rxq_drive(None, None, 0, 1, 0, t, t, st) == -1
+    items = (ctypes.c_void_p * 1)()
+    assert lib.srsgpu_rxq_drive(ctypes.c_void_p(1), items, 1, 0, 0, t, t, st) == -1
