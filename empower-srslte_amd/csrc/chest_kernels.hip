@@ -22,6 +22,8 @@
 // Float arithmetic in the reference's operation order; the stage is checked with a tolerance
 // (float stages 1e-4 relative).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <stdint.h>
 
@@ -109,6 +111,17 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   t.noise = gmem(t.noise);
   t.meas = gmem(t.meas);
   const int nprb = cfg.nprb, cell_id = cfg.cell_id, np = 2 * nprb, nsc = 12 * nprb;
+  // gridDim.y workgroups share a grid: each repeats steps 1-5 (pilots only) and writes its own
+  // range of subcarrier columns; part 0 writes the measurements and the noise. A subframe whose
+  // PSS / EMPTY noise this call updates (read at step 4, written at step 8) stays in part 0 alone.
+  const bool nz05 = t.noise && cfg.noise_alg != 0 && (t.sf_idx == 0 || t.sf_idx == 5);
+  const int part = nz05 ? 0 : (int)blockIdx.y, nparts = nz05 ? 1 : (int)gridDim.y;
+  if (nz05 && blockIdx.y > 0) return;
+  if (part > 0) {
+    t.meas = nullptr;
+    t.cfo = 0;
+  }
+  const int kb = (nsc * part) / nparts, ke = (nsc * (part + 1)) / nparts;
   const c32 *grid = (const c32 *)t.grid;
   const c32 *pil = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);
   const int sym[4] = {0, 4, 7, 11};
@@ -161,7 +174,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
     if (tid == 0) {
       if (refs) {
         s_noise = red[0][0] / (float)np / 4.0f * sqrtf(5.0f);
-        if (t.noise) *t.noise = s_noise;
+        if (t.noise && part == 0) *t.noise = s_noise;
       }
       if (t.meas) {
         const float npil = (float)(4 * np);
@@ -219,11 +232,10 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   }
   // 6 + 7. per subcarrier column: frequency interpolation, then time
   c32 *ce = (c32 *)t.ce;
-  const bool nz05 = t.noise && cfg.noise_alg != 0 && (t.sf_idx == 0 || t.sf_idx == 5);
   const bool pss_on = nz05 && cfg.noise_alg == 1;
   const int k0 = nsc / 2 - 31; // srslte_pss_get_slot position within symbol 6
   float pacc = 0.f;
-  for (int k = tid; k < nsc; k += blockDim.x) {
+  for (int k = kb + tid; k < ke; k += blockDim.x) {
     c32 c6;
     if (cfg.average) {
       const c32 v = interp_at(rows, 2 * np, k, cell_id % 3, 3, 1.0f / 3);
@@ -278,7 +290,9 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
 hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, const float2 *crs,
                         const float *filt, const float2 *pss, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chest, dim3((unsigned)n), dim3(256), 0, st, d_items, n, cfg, crs, filt, pss);
+  // columns split over up to 4 workgroups per grid (12 nprb / 256 of them): steps 1-5 are small
+  const unsigned parts = (unsigned)std::max(1, std::min(4, 12 * cfg.nprb / 256));
+  hipLaunchKernelGGL(k_chest, dim3((unsigned)n, parts), dim3(256), 0, st, d_items, n, cfg, crs, filt, pss);
   return hipGetLastError();
 }
 

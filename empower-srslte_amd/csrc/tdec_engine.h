@@ -96,6 +96,9 @@ struct TdecEngine {
   TdGroup *d_groups = nullptr, *h_groups = nullptr;
   size_t groups_cap = 0, uploaded = 0;
   hipEvent_t gev = nullptr;
+  // second stream of the fused early stop: the SSE kind beside the window kinds
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool gev_pending = false;
   int kind_g0[TD_NKIND + 1] = {0};
   int kind_blocks[TD_NKIND] = {0};
@@ -160,6 +163,10 @@ struct TdecEngine {
       if (p) (void)hipFree(p);
     if (h_groups) (void)hipHostFree(h_groups);
     if (gev) (void)hipEventDestroy(gev);
+    if (aux) (void)hipStreamSynchronize(aux);
+    for (hipEvent_t e : {ev_fork, ev_join})
+      if (e) (void)hipEventDestroy(e);
+    if (aux) (void)hipStreamDestroy(aux);
     for (auto &kv : crc_tables) (void)hipFree(kv.second);
     crc_tables.clear();
     for (auto &kv : wc_tables) {
@@ -589,20 +596,41 @@ struct TdecEngine {
     bool seq = false, es_any = false;
     const TdArrays a = arrays();
     TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end};
+    // The SSE kind (K <= 400: a few workgroups, each a long serial chain) runs fused on a second
+    // stream beside the fused window kinds: the kinds are disjoint groups (their own arrays,
+    // flags and Dfz ranges), so the launch's critical path is the longer of the two, not the sum.
+    int n_es = 0;
+    for (int k = 0; k < TD_NKIND; k++)
+      if (kind_g0[k + 1] > kind_g0[k] && es_on(k)) n_es++;
+    const bool fork = n_es > 1 && kind_g0[TD_KIND_SSE + 1] > kind_g0[TD_KIND_SSE] && es_on(TD_KIND_SSE);
+    if (fork) {
+      if (!aux) {
+        HIPCHK(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+      }
+      HIPCHK(hipEventRecord(ev_fork, st));
+      HIPCHK(hipStreamWaitEvent(aux, ev_fork, 0));
+    }
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
       if (es_on(k)) {
         es_any = true;
+        hipStream_t ks = fork && k == TD_KIND_SSE ? aux : st;
         for (int n0 = 0; n0 < (int)maxh; n0 += chunk) {
           es.n0 = n0;
           es.n1 = std::min(n0 + chunk, (int)maxh);
-          ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", st);
-          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+          ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", ks);
+          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, ks));
         }
       } else {
         seq = true;
       }
+    }
+    if (fork) {
+      HIPCHK(hipEventRecord(ev_join, aux));
+      HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
     }
     if (es_any) {
       ProfScope ps("k_es_bytes", st);

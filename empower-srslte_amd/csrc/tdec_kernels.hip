@@ -2158,58 +2158,63 @@ __global__ __launch_bounds__(256) void k_load_sb8(const TdGroup *__restrict__ gr
   }
 }
 
-// The same copy for nb a multiple of 8 (the window decoders' rows), one thread per T4 group and
-// chain octet of a pair: 16-byte loads of 8 chains x 4 steps per stream and CB (24 loads), then the
-// octet's 32 SP0 elements (256 contiguous bytes) and 32 P1 elements (128 bytes) as 16-byte stores.
-// A quarter of k_load_sb8's load instructions for the same bytes.
-__global__ __launch_bounds__(256) void k_load_sb16(const TdGroup *__restrict__ groups, int ngroups,
-                                                   const int16_t *__restrict__ in, size_t in_stride,
-                                                   const int16_t *const *__restrict__ rows,
-                                                   TdArrays arr) {
+// The same copy through LDS for nb a multiple of 8 (the window decoders' rows): a workgroup takes
+// 1024 / nb steps of one pair (2 KB per CB and stream), loads its 6 chunks with coalesced 16-byte
+// loads (3 per thread), and writes the steps' SP0 (8 KB) and P1 (4 KB) T4 tiles, which are
+// contiguous, with coalesced 16-byte stores (3 per thread). The per-thread forms read and write
+// 16-byte pieces whose neighbours belong to other instructions.
+#define LSBT_STEPS(nb) (1024 / (nb))
+__global__ __launch_bounds__(256) void k_load_sbt(const TdGroup *__restrict__ groups, int ngroups,
+                                                  const int16_t *__restrict__ in, size_t in_stride,
+                                                  const int16_t *const *__restrict__ rows,
+                                                  TdArrays arr) {
+  __shared__ uint16_t lds[6][1024];
   const TdGroup &G = groups[grp_find<GF_LOAD>(groups, ngroups, blockIdx.x)];
   const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
-  const int L = K / nb, G4 = (L + 3) >> 2, no = nb >> 3;
-  const int per = G4 * no;
-  const size_t gid = (size_t)(blockIdx.x - G.blk_load) * 256 + threadIdx.x;
-  const int pair = (int)(gid / per);
+  const int L = K / nb, G4 = (L + 3) >> 2, S = LSBT_STEPS(nb);
+  const int per = (4 * G4 + S - 1) / S; // workgroups per pair
+  const int w = blockIdx.x - G.blk_load;
+  const int pair = w / per, ch = w - pair * per;
   if (pair >= npairs) return;
-  const int r = (int)(gid - (size_t)pair * per);
-  const int g4 = r / no, o = r - g4 * no;
+  const int k0 = ch * S;
   const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
-  const gptr_t<int16_t> a = cb_row(in, in_stride, rows, c0), b = cb_row(in, in_stride, rows, c1);
+  const gptr_t<int16_t> rw[2] = {cb_row(in, in_stride, rows, c0), cb_row(in, in_stride, rows, c1)};
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-  auto ld16 = [](gptr_t<int16_t> p) { return *(const __attribute__((address_space(1))) u4v *)p; };
-  u4v sa[4], sb[4], pa[4], pb[4], qa[4], qb[4];
 #pragma unroll
-  for (int u = 0; u < 4; u++) {
-    const int k = min(4 * g4 + u, L - 1); // the last group may run past L: values unused
-    const int i = k * nb + 8 * o;         // a multiple of 8 elements: 16-byte aligned
-    sa[u] = ld16(a + i);
-    sb[u] = ld16(b + i);
-    pa[u] = ld16(a + K + 32 + i);
-    pb[u] = ld16(b + K + 32 + i);
-    qa[u] = ld16(a + 2 * (K + 32) + i);
-    qb[u] = ld16(b + 2 * (K + 32) + i);
+  for (int q = 0; q < 3; q++) {
+    const int idx = threadIdx.x + 256 * q; // 6 chunks x 128 pieces of 8 elements
+    const int c = idx >> 7, piece = idx & 127;
+    const int st = c >> 1, h = c & 1; // stream (sys, p0, p1), CB
+    int e = k0 * nb + piece * 8;      // element in the stream; past the last step: its copy
+    if (e >= L * nb) e = (L - 1) * nb + (e & (nb - 1));
+    const u4v v = *(const __attribute__((address_space(1))) u4v *)(rw[h] + st * (K + 32) + e);
+    *(u4v *)&lds[c][piece * 8] = v;
   }
-  // chain c of the octet: half (c & 1) of word c >> 1; CB x in the low, CB y in the high half
-  auto pk = [](const u4v &x, const u4v &y, int c) {
-    const uint32_t wx = x[c >> 1], wy = y[c >> 1];
-    return (c & 1) ? (wx >> 16) | (wy & 0xffff0000u) : (wx & 0xffffu) | (wy << 16);
+  __syncthreads();
+  const size_t e0 = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb) + (size_t)k0 * nb;
+  const int nel = min(S, 4 * G4 - k0) * nb; // T4 elements of this tile (the pair's padded steps)
+  auto at = [&](int c, int el) -> uint32_t { // T4 element el of the tile -> stream value
+    const int g4l = el / (4 * nb), d = (el >> 2) % nb, u = el & 3;
+    return lds[c][(4 * g4l + u) * nb + d];
   };
-  const size_t e0 = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb) + (size_t)(g4 * nb + 8 * o) * 4;
-  const gmut_t<u4v> SP0 = gmut<u4v>((s4 *)arr.SP0 + e0);             // 32 elements x 8 B: 16 u4v
-  const gmut_t<u4v> P1 = gmut<u4v>((s2 *)arr.XP1 + arr.plane + e0); // 32 elements x 4 B: 8 u4v
+  const gmut_t<u4v> SP0 = gmut<u4v>((s4 *)arr.SP0 + e0);
+  const gmut_t<u4v> P1 = gmut<u4v>((s2 *)arr.XP1 + arr.plane + e0);
 #pragma unroll
-  for (int c = 0; c < 8; c++) {
-    SP0[2 * c] = u4v{pk(sa[0], sb[0], c), pk(pa[0], pb[0], c), pk(sa[1], sb[1], c), pk(pa[1], pb[1], c)};
-    SP0[2 * c + 1] = u4v{pk(sa[2], sb[2], c), pk(pa[2], pb[2], c), pk(sa[3], sb[3], c), pk(pa[3], pb[3], c)};
-    P1[c] = u4v{pk(qa[0], qb[0], c), pk(qa[1], qb[1], c), pk(qa[2], qb[2], c), pk(qa[3], qb[3], c)};
+  for (int q = 0; q < 2; q++) {
+    const int v = threadIdx.x + 256 * q; // SP0 elements 2v, 2v + 1
+    if (2 * v >= nel) break;
+    const int ea = 2 * v, eb = 2 * v + 1;
+    SP0[v] = u4v{at(0, ea) | (at(1, ea) << 16), at(2, ea) | (at(3, ea) << 16),
+                 at(0, eb) | (at(1, eb) << 16), at(2, eb) | (at(3, eb) << 16)};
   }
-  if (r == 0) { // one thread per pair: the tails
-    const int tb = 3 * (K + 32);
-    const gmut_t<s2> T = gmut<s2>(arr.T);
-#pragma unroll
-    for (int t = 0; t < 12; t++) T[(size_t)(G.pair0 + pair) * 12 + t] = s2{a[tb + t], b[tb + t]};
+  if (4 * (int)threadIdx.x < nel) {
+    const int e = 4 * threadIdx.x;
+    P1[threadIdx.x] = u4v{at(4, e) | (at(5, e) << 16), at(4, e + 1) | (at(5, e + 1) << 16),
+                          at(4, e + 2) | (at(5, e + 2) << 16), at(4, e + 3) | (at(5, e + 3) << 16)};
+  }
+  if (ch == 0 && threadIdx.x < 12) { // the tails
+    const int tb = 3 * (K + 32), t = threadIdx.x;
+    gmut<s2>(arr.T)[(size_t)(G.pair0 + pair) * 12 + t] = s2{rw[0][tb + t], rw[1][tb + t]};
   }
 }
 
@@ -2434,7 +2439,8 @@ static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1
 #if TD_PART == 0
 int load_blocks(int K, int nb, int npairs, int sb_input, bool vec16) {
   if (sb_input && vec16)
-    return (int)nblk((size_t)npairs * ((K / nb + 3) / 4) * (nb % 8 == 0 ? nb / 8 : nb / 2), 256);
+    return nb % 8 == 0 ? npairs * ((4 * ((K / nb + 3) / 4) + 1024 / nb - 1) / (1024 / nb))
+                       : (int)nblk((size_t)npairs * ((K / nb + 3) / 4) * (nb / 2), 256);
   if (sb_input) return (int)nblk((size_t)npairs * (K / 2), 256);
   return npairs * ((K / nb + LOAD_KT - 1) / LOAD_KT);
 }
@@ -2455,8 +2461,8 @@ hipError_t launch_load(const TdGroup *dg, int ng, int nblocks, int nb, int sb_in
                        const TdArrays &a, hipStream_t st) {
   if (ng <= 0 || nblocks <= 0) return hipSuccess;
   if (sb_input) {
-    if (vec && nb % 8 == 0) // 16-byte aligned rows, chain octets (load_blocks counted 32 elements per thread)
-      hipLaunchKernelGGL(k_load_sb16, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
+    if (vec && nb % 8 == 0) // 16-byte aligned rows, LDS-transposed tiles (load_blocks counted tiles)
+      hipLaunchKernelGGL(k_load_sbt, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
     else if (vec) // 16-byte aligned rows (load_blocks counted 8 elements per thread)
       hipLaunchKernelGGL(k_load_sb8, dim3(nblocks), dim3(256), 0, st, dg, ng, in, in_stride, rows, a);
     else

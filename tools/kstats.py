@@ -1,7 +1,7 @@
 """Per-kernel durations of a pipeline leg from a rocprofv3 kernel trace, per 512-subframe stream
 batch, with the HBM fraction of the kernel's algorithmic bytes.
 
-  python tools/kstats.py gpurun_out/<tag>/kt_coded30/kt_kernel_trace.csv [--batches N]
+  python tools/kstats.py gpurun_out/<tag>/kt_coded30/kt_kernel_trace.csv [--c3]
 
 The bench runs the decoder headline and the traffic synthesis first: only kernels from the leg's
 first receive FFT on are counted. A leg's kernels run once per stream batch: the count of
@@ -28,6 +28,7 @@ C3_BYTES = {
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
+    ap.add_argument("--c3", action="store_true", help="HBM fractions with the C3 stream batch's bytes")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     # the leg starts at its first receive FFT (the headline and the traffic synthesis run before)
@@ -46,7 +47,7 @@ def main():
             continue
         per_batch = sum(d) / nb
         tot += per_batch
-        key = next((k for k in C3_BYTES if name.startswith(k)), None)
+        key = next((k for k in C3_BYTES if name.startswith(k)), None) if args.c3 else None
         frac = ""
         if key:
             avg = sum(d) / len(d)
