@@ -911,6 +911,7 @@ def main():
                        "subframes_per_s_equiv": round(bits_total / elapsed / SF_BITS, 1),
                        "bit_errors": bit_errors},
             "roofline": roofline,
+            "decoder_schedule": s.get_schedule(),  # srsgpu_tdec_set_schedule (results identical under all)
         }
         if gather:
             result["gather"] = gather

@@ -285,6 +285,11 @@ struct PdschEngine {
         t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant * cell.nof_ports : nullptr;
         t.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
         t.inv_scaling = 1.0f / t.scaling;
+        // the two TBs of a 2-layer MMSE with one modulation: one 2x2 solve per RE for both
+        if (tb == 1 && (t.cdd || t.mux > 0) && s.mod[0] == s.mod[1]) {
+          h_llr[k - 1].dual = 1;
+          t.dual = 2;
+        }
         mre = std::max(mre, nre);
         mbits = std::max(mbits, nre * q);
       }

@@ -35,6 +35,9 @@ struct LlrItem {
   const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does
   int nports;              // ports in noise_dev
   int llr8;                // llr_is_8bit: int8 demapping / scrambling / CSI, values sign-extended in e
+  int dual;                // 2-layer MMSE (TM3 / TM4) with both TBs of one modulation: 1 = this item
+                           // also computes the next item's layer from the same 2x2 solve, 2 = done
+                           // by the previous item (its workgroups return at once)
 };
 
 // one codeword to transmit: scramble + modulate + map

@@ -168,7 +168,9 @@ __device__ __forceinline__ cf c_of(float2 v) { return {v.x, v.y}; }
 // H = [[h00, h10], [h01, h11]] (norm sqrt 2 / scaling), 1 [[h00+h10, h00-h10], [h01+h11, h01-h11]],
 // 2 [[h00+j h10, h00-j h10], [h01+j h11, h01-j h11]] (norm 2 / scaling), j h = (-h.i, h.r) exactly.
 __device__ __forceinline__ cf c_mulj(cf a) { return {-a.i, a.r}; }
-__device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, const ReIn &in, uint32_t j) {
+// both layers' outputs (eq[0] layer 0, eq[1] layer 1) of one RE's 2x2 MMSE: the shared terms once,
+// then each row with exactly the operations of the one-layer form
+__device__ __forceinline__ void equalise_cdd2(const LlrItem &t, const ReIn &in, uint32_t j, Eq eq[2]) {
   const cf p00 = c_of(in.h[0][0]), p01 = c_of(in.h[0][1]);
   const cf p10 = c_of(in.h[1][0]), p11 = c_of(in.h[1][1]);
   cf h00, h01, h10, h11;
@@ -206,26 +208,32 @@ __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, const ReIn &in, uin
   const float m2 = det.r * det.r + det.i * det.i;
   const cf rcp = {det.r / m2, -det.i / m2};
   const cf nrm = {norm * rcp.r, norm * rcp.i};
-  cf bd, bo; // diagonal and off-diagonal entries of row `layer` of B
-  if (t.layer == 0) {
-    bd = c_mul(a11, nrm);          // b00
-    bo = c_mul(c_neg(a01), nrm);   // b01
-  } else {
-    bo = c_mul(c_neg(a10), nrm);   // b10
-    bd = c_mul(a00, nrm);          // b11
-  }
-  // row 0: w00 = b00 _h00 + b01 _h01, w01 = b00 _h10 + b01 _h11
-  // row 1: w10 = b10 _h00 + b11 _h01, w11 = b10 _h10 + b11 _h11
-  const cf b0 = t.layer == 0 ? bd : bo, b1 = t.layer == 0 ? bo : bd;
-  const cf wa = c_add(c_mul(b0, _h00), c_mul(b1, _h01));
-  const cf wb = c_add(c_mul(b0, _h10), c_mul(b1, _h11));
   const cf y0 = c_of(in.y[0]), y1 = c_of(in.y[1]);
-  const cf x = c_add(c_mul(y0, wa), c_mul(y1, wb));
-  Eq e;
-  e.xr = x.r;
-  e.xi = x.i;
-  e.csi = 1.0f / bd.r;
-  return e;
+#pragma unroll
+  for (int layer = 0; layer < 2; layer++) {
+    cf bd, bo; // diagonal and off-diagonal entries of row `layer` of B
+    if (layer == 0) {
+      bd = c_mul(a11, nrm);          // b00
+      bo = c_mul(c_neg(a01), nrm);   // b01
+    } else {
+      bo = c_mul(c_neg(a10), nrm);   // b10
+      bd = c_mul(a00, nrm);          // b11
+    }
+    // row 0: w00 = b00 _h00 + b01 _h01, w01 = b00 _h10 + b01 _h11
+    // row 1: w10 = b10 _h00 + b11 _h01, w11 = b10 _h10 + b11 _h11
+    const cf b0 = layer == 0 ? bd : bo, b1 = layer == 0 ? bo : bd;
+    const cf wa = c_add(c_mul(b0, _h00), c_mul(b1, _h01));
+    const cf wb = c_add(c_mul(b0, _h10), c_mul(b1, _h11));
+    const cf x = c_add(c_mul(y0, wa), c_mul(y1, wb));
+    eq[layer].xr = x.r;
+    eq[layer].xi = x.i;
+    eq[layer].csi = 1.0f / bd.r;
+  }
+}
+__device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, const ReIn &in, uint32_t j) {
+  Eq eq[2];
+  equalise_cdd2(t, in, j, eq);
+  return eq[t.layer];
 }
 
 // TM4 spatial multiplexing with one layer: 2x1 MRC (srslte_predecoding_multiplex_2x1_mrc(_csi),
@@ -489,7 +497,7 @@ __device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &
 // one-RE loop.
 #define LLR_RES 4
 template <int MOD>
-__device__ __forceinline__ void llr_body(const LlrItem &t) {
+__device__ __forceinline__ void llr_body(const LlrItem &t, const LlrItem *t2) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   const uint32_t stride = gridDim.x * 256;
   if (t.txdiv) {
@@ -500,6 +508,38 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     return;
   }
   const bool two_ports = t.cdd || t.mux != 0;
+  if (t2) { // both layers of a 2-layer MMSE from one solve per RE (t2: the other TB's item)
+    for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
+      uint32_t pos[LLR_RES];
+#pragma unroll
+      for (int r = 0; r < LLR_RES; r++) {
+        const uint32_t j = j0 + r * stride;
+        pos[r] = t.map[j < t.nof_re ? j : j0];
+      }
+      ReIn in[LLR_RES];
+      uint32_t c0[LLR_RES], c1[LLR_RES], d0[LLR_RES], d1[LLR_RES];
+#pragma unroll
+      for (int r = 0; r < LLR_RES; r++) {
+        const uint32_t j = j0 + r * stride;
+        const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
+        in[r] = load_re(t, pos[r], true);
+        c0[r] = t.c[w];
+        c1[r] = t.c[w + 1];
+        d0[r] = t2->c[w];
+        d1[r] = t2->c[w + 1];
+      }
+#pragma unroll
+      for (int r = 0; r < LLR_RES; r++) {
+        const uint32_t j = j0 + r * stride;
+        if (j >= t.nof_re) break;
+        Eq eq[2];
+        equalise_cdd2(t, in[r], j, eq);
+        llr_out<MOD>(t, j, eq[t.layer], c0[r], c1[r]);
+        llr_out<MOD>(*t2, j, eq[t2->layer], d0[r], d1[r]);
+      }
+    }
+    return;
+  }
   for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
     uint32_t pos[LLR_RES];
 #pragma unroll
@@ -533,32 +573,42 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
   const int it = blockIdx.y;
   if (it >= nitems) return;
   LlrItem t = items[it];
-  for (int a = 0; a < 2; a++) {
-    t.y[a] = gmem(t.y[a]);
-    t.h[0][a] = gmem(t.h[0][a]);
-    t.h[1][a] = gmem(t.h[1][a]);
-  }
-  t.map = gmem(t.map);
-  t.c = gmem(t.c);
-  t.e = gmem(t.e);
-  t.csi = gmem(t.csi);
-  t.csi_max = gmem(t.csi_max);
-  t.noise_dev = gmem(t.noise_dev);
-  if (t.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
-                     // the mean over ports, then the mean over antennas
-    float n = 0.f;
-    for (int a = 0; a < t.nrx; a++) {
-      float acc = 0.f;
-      for (int p = 0; p < t.nports; p++) acc += t.noise_dev[a * t.nports + p];
-      n += acc / (float)t.nports;
+  if (t.dual == 2) return; // computed with the previous item
+  auto fix = [](LlrItem &u) {
+    for (int a = 0; a < 2; a++) {
+      u.y[a] = gmem(u.y[a]);
+      u.h[0][a] = gmem(u.h[0][a]);
+      u.h[1][a] = gmem(u.h[1][a]);
     }
-    t.noise = n / (float)t.nrx;
+    u.map = gmem(u.map);
+    u.c = gmem(u.c);
+    u.e = gmem(u.e);
+    u.csi = gmem(u.csi);
+    u.csi_max = gmem(u.csi_max);
+    u.noise_dev = gmem(u.noise_dev);
+    if (u.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
+                       // the mean over ports, then the mean over antennas
+      float n = 0.f;
+      for (int a = 0; a < u.nrx; a++) {
+        float acc = 0.f;
+        for (int p = 0; p < u.nports; p++) acc += u.noise_dev[a * u.nports + p];
+        n += acc / (float)u.nports;
+      }
+      u.noise = n / (float)u.nrx;
+    }
+  };
+  fix(t);
+  LlrItem t2;
+  if (t.dual == 1) {
+    t2 = items[it + 1];
+    fix(t2);
   }
+  const LlrItem *pt2 = t.dual == 1 ? &t2 : nullptr;
   switch (t.mod) {
-  case 0: llr_body<0>(t); break;
-  case 1: llr_body<1>(t); break;
-  case 2: llr_body<2>(t); break;
-  default: llr_body<3>(t); break;
+  case 0: llr_body<0>(t, pt2); break;
+  case 1: llr_body<1>(t, pt2); break;
+  case 2: llr_body<2>(t, pt2); break;
+  default: llr_body<3>(t, pt2); break;
   }
 }
 
