@@ -226,6 +226,22 @@ def stage_profile(s, torch, step, steps):
     return out
 
 
+def warm_up(torch, step, warmup, seconds=0.25):
+    """The leg's warmup steps, then more until `seconds` of decoding have run: the legs are set up
+    on the host for seconds with the GPU idle, and a GPU ramps its clock over the first tens of ms
+    of load (the first timed loop after two warmup steps ran up to 1.8x slower than the same steps
+    a moment later: profiles/r03_s13_sched_ab.json, ms_per_batch against the schedule rounds). As
+    the headline's pre-heat, this times the steady clock of a receiver that decodes continuously."""
+    t0 = time.perf_counter()
+    n = 0
+    while n < warmup or time.perf_counter() - t0 < seconds:
+        step()
+        n += 1
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+
+
 def schedule_ab(s, torch, step, steps, schedules, reps=3):
     """A/B of decoder launch schedules (srsgpu_tdec_set_schedule; results are identical under all)
     in one process on the same inputs: reps rounds, each timing `steps` steps per schedule in turn
@@ -316,9 +332,7 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedul
             assert o["pd"].decode_dev(o["sfs"], o["grid"].data_ptr(), o["ce"].data_ptr(), gsz,
                                       o["data"].data_ptr(), 8, o["ret"].data_ptr(), o["noi"].data_ptr()) == 0
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    warm_up(torch, step, warmup)
     if dist:
         dist.barrier()
     gc.disable()  # the host-bound legs must not pay a collector pause inside the timed loop
@@ -419,9 +433,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
         for m in ms:
             m.step()
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    warm_up(torch, step, warmup)
     if dist:
         dist.barrier()
     gc.disable()
