@@ -238,6 +238,7 @@ struct PdschEngine {
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
     uint32_t mre = 0, mbits = 0, k = 0;
+    int n_dual = 0;
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
@@ -289,6 +290,7 @@ struct PdschEngine {
         if (tb == 1 && (t.cdd || t.mux > 0) && s.mod[0] == s.mod[1]) {
           h_llr[k - 1].dual = 1;
           t.dual = 2;
+          n_dual++;
         }
         mre = std::max(mre, nre);
         mbits = std::max(mbits, nre * q);
@@ -304,7 +306,7 @@ struct PdschEngine {
       HIPCHK(launch_gold(d_gold, (int)k, mbits, d_x1, d_x2b, gold_words, st));
     }
     ProfScope ps("k_pdsch_llr", st);
-    HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st));
+    HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual));
     return 0;
   }
 

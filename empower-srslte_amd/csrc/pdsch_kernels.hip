@@ -233,7 +233,8 @@ __device__ __forceinline__ void equalise_cdd2(const LlrItem &t, const ReIn &in, 
 __device__ __forceinline__ Eq equalise_cdd(const LlrItem &t, const ReIn &in, uint32_t j) {
   Eq eq[2];
   equalise_cdd2(t, in, j, eq);
-  return eq[t.layer];
+  const Eq e0 = eq[0], e1 = eq[1];
+  return t.layer ? e1 : e0;
 }
 
 // TM4 spatial multiplexing with one layer: 2x1 MRC (srslte_predecoding_multiplex_2x1_mrc(_csi),
@@ -497,7 +498,7 @@ __device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &
 // one-RE loop.
 #define LLR_RES 4
 template <int MOD>
-__device__ __forceinline__ void llr_body(const LlrItem &t, const LlrItem *t2) {
+__device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   const uint32_t stride = gridDim.x * 256;
   if (t.txdiv) {
@@ -508,38 +509,6 @@ __device__ __forceinline__ void llr_body(const LlrItem &t, const LlrItem *t2) {
     return;
   }
   const bool two_ports = t.cdd || t.mux != 0;
-  if (t2) { // both layers of a 2-layer MMSE from one solve per RE (t2: the other TB's item)
-    for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
-      uint32_t pos[LLR_RES];
-#pragma unroll
-      for (int r = 0; r < LLR_RES; r++) {
-        const uint32_t j = j0 + r * stride;
-        pos[r] = t.map[j < t.nof_re ? j : j0];
-      }
-      ReIn in[LLR_RES];
-      uint32_t c0[LLR_RES], c1[LLR_RES], d0[LLR_RES], d1[LLR_RES];
-#pragma unroll
-      for (int r = 0; r < LLR_RES; r++) {
-        const uint32_t j = j0 + r * stride;
-        const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
-        in[r] = load_re(t, pos[r], true);
-        c0[r] = t.c[w];
-        c1[r] = t.c[w + 1];
-        d0[r] = t2->c[w];
-        d1[r] = t2->c[w + 1];
-      }
-#pragma unroll
-      for (int r = 0; r < LLR_RES; r++) {
-        const uint32_t j = j0 + r * stride;
-        if (j >= t.nof_re) break;
-        Eq eq[2];
-        equalise_cdd2(t, in[r], j, eq);
-        llr_out<MOD>(t, j, eq[t.layer], c0[r], c1[r]);
-        llr_out<MOD>(*t2, j, eq[t2->layer], d0[r], d1[r]);
-      }
-    }
-    return;
-  }
   for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
     uint32_t pos[LLR_RES];
 #pragma unroll
@@ -569,46 +538,99 @@ __device__ __forceinline__ void llr_body(const LlrItem &t, const LlrItem *t2) {
   }
 }
 
+// both layers of a 2-layer MMSE from one solve per RE: t and t2 are the two TBs' items (t2 by
+// reference, so it stays in registers)
+template <int MOD>
+__device__ __forceinline__ void llr_body_dual(const LlrItem &t, const LlrItem &t2) {
+  constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
+  const uint32_t stride = gridDim.x * 256;
+  for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
+    uint32_t pos[LLR_RES];
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      pos[r] = t.map[j < t.nof_re ? j : j0];
+    }
+    ReIn in[LLR_RES];
+    uint32_t c0[LLR_RES], c1[LLR_RES], d0[LLR_RES], d1[LLR_RES];
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
+      in[r] = load_re(t, pos[r], true);
+      c0[r] = t.c[w];
+      c1[r] = t.c[w + 1];
+      d0[r] = t2.c[w];
+      d1[r] = t2.c[w + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < LLR_RES; r++) {
+      const uint32_t j = j0 + r * stride;
+      if (j >= t.nof_re) break;
+      Eq eq[2];
+      equalise_cdd2(t, in[r], j, eq);
+      const Eq e0 = eq[0], e1 = eq[1];
+      llr_out<MOD>(t, j, t.layer ? e1 : e0, c0[r], c1[r]);
+      llr_out<MOD>(t2, j, t2.layer ? e1 : e0, d0[r], d1[r]);
+    }
+  }
+}
+
+// the item's device pointers as global, and the noise from the estimator when it is on the device
+__device__ __forceinline__ void llr_item_fix(LlrItem &u) {
+  for (int a = 0; a < 2; a++) {
+    u.y[a] = gmem(u.y[a]);
+    u.h[0][a] = gmem(u.h[0][a]);
+    u.h[1][a] = gmem(u.h[1][a]);
+  }
+  u.map = gmem(u.map);
+  u.c = gmem(u.c);
+  u.e = gmem(u.e);
+  u.csi = gmem(u.csi);
+  u.csi_max = gmem(u.csi_max);
+  u.noise_dev = gmem(u.noise_dev);
+  if (u.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
+                     // the mean over ports, then the mean over antennas
+    float n = 0.f;
+    for (int a = 0; a < u.nrx; a++) {
+      float acc = 0.f;
+      for (int p = 0; p < u.nports; p++) acc += u.noise_dev[a * u.nports + p];
+      n += acc / (float)u.nports;
+    }
+    u.noise = n / (float)u.nrx;
+  }
+}
+
+// one item per TB (the dual items are k_pdsch_llr2's)
 __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ items, int nitems) {
   const int it = blockIdx.y;
   if (it >= nitems) return;
   LlrItem t = items[it];
-  if (t.dual == 2) return; // computed with the previous item
-  auto fix = [](LlrItem &u) {
-    for (int a = 0; a < 2; a++) {
-      u.y[a] = gmem(u.y[a]);
-      u.h[0][a] = gmem(u.h[0][a]);
-      u.h[1][a] = gmem(u.h[1][a]);
-    }
-    u.map = gmem(u.map);
-    u.c = gmem(u.c);
-    u.e = gmem(u.e);
-    u.csi = gmem(u.csi);
-    u.csi_max = gmem(u.csi_max);
-    u.noise_dev = gmem(u.noise_dev);
-    if (u.noise_dev) { // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): per rx antenna
-                       // the mean over ports, then the mean over antennas
-      float n = 0.f;
-      for (int a = 0; a < u.nrx; a++) {
-        float acc = 0.f;
-        for (int p = 0; p < u.nports; p++) acc += u.noise_dev[a * u.nports + p];
-        n += acc / (float)u.nports;
-      }
-      u.noise = n / (float)u.nrx;
-    }
-  };
-  fix(t);
-  LlrItem t2;
-  if (t.dual == 1) {
-    t2 = items[it + 1];
-    fix(t2);
-  }
-  const LlrItem *pt2 = t.dual == 1 ? &t2 : nullptr;
+  if (t.dual) return;
+  llr_item_fix(t);
   switch (t.mod) {
-  case 0: llr_body<0>(t, pt2); break;
-  case 1: llr_body<1>(t, pt2); break;
-  case 2: llr_body<2>(t, pt2); break;
-  default: llr_body<3>(t, pt2); break;
+  case 0: llr_body<0>(t); break;
+  case 1: llr_body<1>(t); break;
+  case 2: llr_body<2>(t); break;
+  default: llr_body<3>(t); break;
+  }
+}
+
+// both TBs of a 2-layer MMSE subframe (item it with dual = 1 and item it + 1) from one solve per
+// RE; a kernel of its own, so the single-TB kernel keeps its smaller register budget
+__global__ __launch_bounds__(256) void k_pdsch_llr2(const LlrItem *__restrict__ items, int nitems) {
+  const int it = blockIdx.y;
+  if (it + 1 >= nitems) return;
+  LlrItem t = items[it];
+  if (t.dual != 1) return;
+  LlrItem t2 = items[it + 1];
+  llr_item_fix(t);
+  llr_item_fix(t2);
+  switch (t.mod) {
+  case 0: llr_body_dual<0>(t, t2); break;
+  case 1: llr_body_dual<1>(t, t2); break;
+  case 2: llr_body_dual<2>(t, t2); break;
+  default: llr_body_dual<3>(t, t2); break;
   }
 }
 
@@ -670,10 +692,14 @@ hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const u
   return hipGetLastError();
 }
 
-hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st) {
+hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st,
+                            int n_dual) {
   if (n <= 0) return hipSuccess;
   const unsigned gx = std::min(cdiv(max_re, 256 * LLR_RES), 64u);
-  hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+  if (n > 2 * n_dual)
+    hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+  if (n_dual > 0)
+    hipLaunchKernelGGL(k_pdsch_llr2, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
   if (csi) {
     const unsigned gb = std::min(cdiv((size_t)max_re * 6, 256), 256u);
     hipLaunchKernelGGL(k_csi_correct, dim3(gb ? gb : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
