@@ -49,15 +49,26 @@ __device__ __forceinline__ float cpow(c32 a) { return a.x * a.x + a.y * a.y; }
 #define CH_MAXP (2 * 110) // pilots per CRS symbol
 #define CH_NRED 7
 
-// block-wide sums of nv per-thread values (block-uniform call); results in red[j][0]
+// block-wide sums of nv per-thread values (block-uniform call, 256 threads); results in red[j][0].
+// The pairwise tree red[t] += red[t + s], s = 128 .. 1: the two wide levels in LDS, the six levels
+// inside wave 0 with shuffles (lane t adds lane t + s, as the tree does), so the sums are the
+// tree's, with 4 barriers instead of 9.
 __device__ __forceinline__ void block_sum(float (*red)[256], const float *v, int nv) {
   for (int j = 0; j < nv; j++) red[j][threadIdx.x] = v[j];
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
+  for (int s = 128; s >= 64; s >>= 1) {
     if ((int)threadIdx.x < s)
       for (int j = 0; j < nv; j++) red[j][threadIdx.x] += red[j][threadIdx.x + s];
     __syncthreads();
   }
+  if (threadIdx.x < 64) {
+    for (int j = 0; j < nv; j++) {
+      float x = red[j][threadIdx.x];
+      for (int s = 32; s > 0; s >>= 1) x += __shfl_down(x, s);
+      if (threadIdx.x == 0) red[j][0] = x;
+    }
+  }
+  __syncthreads();
 }
 
 // srslte_conv_same_cf output i (convolution.c:172-211), any filter length M: outputs i < M/2 read
