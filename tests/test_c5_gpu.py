@@ -60,3 +60,38 @@ def test_c5_mixed_k_decode_vs_oracle(table, oracle):
     assert len(set(ret.tolist())) > 1 and len(set(noi.tolist())) > 2  # failures and varied noi
     assert len(ks) > 10
     m.close()
+
+
+def test_c5_decode_identical_under_every_schedule(table):
+    """srsgpu_tdec_set_schedule changes only how the decoders are launched: the same mixed-K job
+    (window and SSE kinds, failures and varied nof_iterations at 6 dB) decodes to the same return
+    codes, nof_iterations, bytes and cb_crc under the auto, fused (1 and 8 half-iterations per
+    launch), per-half-iteration and one-wave SSE schedules."""
+    import torch
+    import srsgpu_phy as s
+    import srsgpu_traffic as tr
+    keep = s.get_schedule()
+    m = tr.MixedCells(table, 40, torch, torch.device("cuda", 0), seed=13, snr_db=6.0)
+    try:
+        m.front_end()
+        torch.cuda.synchronize()
+        outs = {}
+        for name, sch in {"auto": dict(es_fused=2, es_chunk=8, sse_bidir=1),
+                          "fused1": dict(es_fused=1, es_chunk=1, sse_bidir=1),
+                          "fused8": dict(es_fused=1, es_chunk=8, sse_bidir=1),
+                          "per_halfit": dict(es_fused=0, sse_bidir=1),
+                          "sse_one_wave": dict(es_fused=0, sse_bidir=0)}.items():
+            s.set_schedule(**sch)
+            m.d_data.zero_()
+            m.decode()
+            torch.cuda.synchronize()
+            crc = [bytes(m.dlsch.read_cb_crc(t["softbuffer"])) for t in m.tb_list]
+            outs[name] = (m.d_ret.cpu().numpy(), m.d_noi.cpu().numpy(), m.d_data.cpu().numpy(), crc)
+        ref = outs["auto"]
+        assert len(set(ref[0].tolist())) > 1 and len(set(ref[1].tolist())) > 2
+        for name, o in outs.items():
+            assert (o[0] == ref[0]).all() and (o[1] == ref[1]).all(), name
+            assert (o[2] == ref[2]).all() and o[3] == ref[3], name
+    finally:
+        s.set_schedule(**keep)
+        m.close()
