@@ -224,6 +224,21 @@ void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w) { // ches
   q->e.filt_dirty = true;
 }
 
+int srsgpu_chest_set_smooth_filter_gauss(srsgpu_chest_t *q, uint32_t order, float std_dev) {
+  // chest_dl.c:475-494 in the reference's float arithmetic: exp(-(i - c)^2 / (2 std^2)) normalised
+  // by its sum (accumulated in order); order 0 leaves the filter as it is
+  if (!q || order + 1 >= 65) return -1;
+  const uint32_t len = order + 1;
+  const int c = (int)(len - 1) / 2;
+  float f[64];
+  for (uint32_t i = 0; i < len; i++) f[i] = expf(-powf((float)((int)i - c), 2) / (2.0f * powf(std_dev, 2)));
+  float norm = 0.f;
+  for (uint32_t i = 0; i < len; i++) norm += f[i];
+  const float inv = 1.0f / norm;
+  for (uint32_t i = 0; i < len; i++) f[i] *= inv;
+  return srsgpu_chest_set_smooth_filter(q, f, len);
+}
+
 int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg) {
   if (!q || !cfg || cfg->noise_alg > 2 || !cfg->symbol_sz) return -1;
   q->e.cfg = *cfg;

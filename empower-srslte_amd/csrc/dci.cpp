@@ -496,4 +496,76 @@ int srsgpu_ra_dl_dci_to_grant(srsgpu_ra_dl_dci_t *d, uint32_t nof_prb, uint16_t 
   return 0;
 }
 
+// dci.c:165-197: dci_format0_unpack (:571-626), then srslte_ra_ul_dci_to_grant (ra.c:228-245) with the
+// PRB allocation of ra.c:118-187 and the MCS of ra.c:189-218
+int srsgpu_dci_msg_to_ul_grant(const uint8_t *bits, uint32_t nof_bits, uint32_t nof_prb, uint32_t n_rb_ho,
+                               srsgpu_ra_ul_dci_t *d, srsgpu_ra_ul_grant_t *g) {
+  if (!bits || !d || !g || nof_prb < 1 || nof_prb > 110) return -1;
+  memset(d, 0, sizeof(*d));
+  memset(g, 0, sizeof(*g));
+  // format 0 unpack: size, format flag, hopping flag and bits (36.213 Table 8.4-1), RIV, MCS, NDI, TPC,
+  // DMRS cyclic shift, CQI request
+  if (nof_bits != f0_sizeof(nof_prb) || bits[0] != 0) return -1;
+  const uint8_t *y = bits + 1;
+  uint32_t n_ul_hop = 0;
+  if (*y++ == 0) {
+    d->freq_hop_fl = -1;
+  } else if (nof_prb < 50) {
+    n_ul_hop = 1;
+    d->freq_hop_fl = *y++;
+  } else {
+    n_ul_hop = 2;
+    d->freq_hop_fl = y[0] << 1 | y[1];
+    y += 2;
+  }
+  const uint32_t riv = bit_pack(&y, (int)(riv_nbits(nof_prb) - n_ul_hop));
+  ra_type2_from_riv(riv, &d->L_crb, &d->RB_start, nof_prb, nof_prb);
+  d->riv = riv;
+  d->mcs_idx = bit_pack(&y, 5);
+  d->ndi = *y++ ? 1 : 0;
+  d->tpc_pusch = bit_pack(&y, 2);
+  d->n_dmrs = bit_pack(&y, 3);
+  d->cqi_request = *y++ ? 1 : 0;
+  // PRB allocation (8.1 and 8.4 of 36.213)
+  g->ncs_dmrs = d->n_dmrs;
+  g->L_prb = d->L_crb;
+  const uint32_t n_prb_1 = d->RB_start;
+  if (n_rb_ho % 2) n_rb_ho++;
+  if (d->freq_hop_fl == -1 || d->freq_hop_fl == 3) {
+    g->n_prb[0] = g->n_prb[1] = n_prb_1; // type 2 hopping is applied at resource mapping
+    g->freq_hopping = d->freq_hop_fl == -1 ? 0 : 2;
+  } else { // type 1: a fixed offset between the slots
+    const uint32_t n_rb_pusch = nof_prb - n_rb_ho - (nof_prb % 2);
+    g->n_prb[0] = n_prb_1;
+    if (n_prb_1 < n_rb_ho / 2) return -1;
+    switch (d->freq_hop_fl) {
+    case 0: g->n_prb[1] = (n_rb_pusch / 4 + n_prb_1) % n_rb_pusch; break;
+    case 1: g->n_prb[1] = n_prb_1 < n_rb_pusch / 4 ? n_rb_pusch + n_prb_1 - n_rb_pusch / 4 : n_prb_1 - n_rb_pusch / 4; break;
+    case 2: g->n_prb[1] = (n_rb_pusch / 2 + n_prb_1) % n_rb_pusch; break;
+    default: break;
+    }
+    g->freq_hopping = 1;
+  }
+  if (!(g->n_prb[0] + g->L_prb <= nof_prb && g->n_prb[1] + g->L_prb <= nof_prb)) return -1;
+  // MCS (8.6.1 / 8.6.2)
+  if (d->mcs_idx <= 28) {
+    const uint32_t off = d->mcs_idx < 11 ? 0 : d->mcs_idx < 21 ? 1 : 2;
+    g->mod = d->mcs_idx < 11 ? 1 : d->mcs_idx < 21 ? 2 : 3;
+    g->tbs = srsgpu_ra_tbs_from_idx(d->mcs_idx - off, g->L_prb);
+  } else if (d->mcs_idx == 29 && d->cqi_request && g->L_prb <= 4) {
+    g->mod = 1; // CQI only
+    g->tbs = 0;
+    d->rv_idx = 1;
+  } else {
+    g->tbs = -1;
+    g->mod = 4; // SRSLTE_MOD_LAST
+    d->rv_idx = d->mcs_idx - 28;
+  }
+  g->mcs_idx = d->mcs_idx;
+  g->M_sc = g->L_prb * 12;
+  g->M_sc_init = g->M_sc;
+  g->Qm = g->mod < 4 ? mod_bits(g->mod) : 0;
+  return 0;
+}
+
 } // extern "C"

@@ -518,11 +518,9 @@ int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
 // srslte_ulsch_decode (sch.c:883-889 -> srslte_ulsch_uci_decode :944-985 without UCI): the channel
 // deinterleaver of every TB (ulsch_deinterleave, :860-881) into the caller's g bits, then decode_tb
 // on them through the DL-SCH path (the reference's decode_tb is the same function for both links)
-int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb,
-                            const int16_t *d_q, int16_t *d_g, uint8_t *d_data, uint32_t maxh,
-                            int32_t *d_ret, uint32_t *d_noi) {
-  if (!q || (!tb && ntb) || !d_q || !d_g || !d_data || !d_ret || !d_noi) return -1;
-  if (ntb == 0) return 0;
+// the channel deinterleaver launch of ntb UL-SCH TBs (q -> g, sch.c:550-568, 860-881)
+static int ulsch_deinterleave(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb, const int16_t *d_q,
+                              int16_t *d_g) {
   DlschEngine &E = q->e;
   if (ntb > E.cap) return -1;
   for (uint32_t i = 0; i < ntb; i++) {
@@ -539,28 +537,46 @@ int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint
   }
   if (E.staged_pending) HIPCHK(hipEventSynchronize(E.staged));
   uint32_t max_bits = 0;
-  std::vector<srsgpu_dlsch_tb_t> dl(ntb);
-  std::vector<const int16_t *> e(ntb);
-  std::vector<uint8_t *> d(ntb);
   for (uint32_t i = 0; i < ntb; i++) {
     const uint32_t Qm = tb[i].Qm, cols = tb[i].nof_symb;
     E.h_ul[i] = UlItem{tb[i].q_offset, tb[i].nof_bits / Qm / cols, cols, Qm};
     max_bits = std::max(max_bits, tb[i].nof_bits);
-    // G = nb_q / Qm - Q'_ri - Q'_cqi with no UCI: every coded bit is data (sch.c:976-979)
-    dl[i] = srsgpu_dlsch_tb_t{tb[i].tbs, tb[i].rv, Qm, tb[i].nof_bits, tb[i].softbuffer,
-                              tb[i].q_offset, tb[i].data_offset};
-    e[i] = d_g + tb[i].q_offset;
-    d[i] = d_data + tb[i].data_offset;
   }
   HIPCHK(hipMemcpyAsync(E.d_ul, E.h_ul, sizeof(UlItem) * ntb, hipMemcpyHostToDevice, E.st));
   {
     ProfScope ps("k_ulsch_deinterleave", E.st);
     HIPCHK(launch_ulsch_deinterleave(E.d_ul, (int)ntb, max_bits, d_q, d_g, E.st));
   }
-  // decode() waits for this copy (its own staging reuses the event after recording it)
+  // the next staging of E.h_ul (here or in decode()) waits for this copy
   HIPCHK(hipEventRecord(E.staged, E.st));
   E.staged_pending = true;
-  return E.decode(dl.data(), ntb, e.data(), d.data(), maxh, d_ret, d_noi);
+  return 0;
+}
+
+int srsgpu_ulsch_deinterleave_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb, const int16_t *d_q,
+                                  int16_t *d_g) {
+  if (!q || (!tb && ntb) || !d_q || !d_g) return -1;
+  if (ntb == 0) return 0;
+  return ulsch_deinterleave(q, tb, ntb, d_q, d_g);
+}
+
+int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb,
+                            const int16_t *d_q, int16_t *d_g, uint8_t *d_data, uint32_t maxh,
+                            int32_t *d_ret, uint32_t *d_noi) {
+  if (!q || (!tb && ntb) || !d_q || !d_g || !d_data || !d_ret || !d_noi) return -1;
+  if (ntb == 0) return 0;
+  if (ulsch_deinterleave(q, tb, ntb, d_q, d_g)) return -1;
+  std::vector<srsgpu_dlsch_tb_t> dl(ntb);
+  std::vector<const int16_t *> e(ntb);
+  std::vector<uint8_t *> d(ntb);
+  for (uint32_t i = 0; i < ntb; i++) {
+    // G = nb_q / Qm - Q'_ri - Q'_cqi with no UCI: every coded bit is data (sch.c:976-979)
+    dl[i] = srsgpu_dlsch_tb_t{tb[i].tbs, tb[i].rv, tb[i].Qm, tb[i].nof_bits, tb[i].softbuffer,
+                              tb[i].q_offset, tb[i].data_offset};
+    e[i] = d_g + tb[i].q_offset;
+    d[i] = d_data + tb[i].data_offset;
+  }
+  return q->e.decode(dl.data(), ntb, e.data(), d.data(), maxh, d_ret, d_noi);
 }
 
 int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -69,29 +71,51 @@ const uint8_t kPdcchPerm[32] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 2
 
 // k_dci_select: the first candidate of each search whose CRC remainder equals the RNTI and whose
 // format is the searched one (ue_dl.c:768-810 dci_blind_search, over the concatenated searches of
-// find_dl_dci_type_crnti / _siprarnti); format 0 found while searching 1A is the UL DCI and is
-// passed over. A candidate the reference's decode_msg refuses before that ends the search with
-// found = -1, as the reference's search then returns SRSLTE_ERROR.
+// find_dl_dci_type_crnti / _siprarnti). A candidate the reference's decode_msg refuses before that ends
+// the search with found = -1, as the reference's search then returns SRSLTE_ERROR. Format 0 found while
+// searching 1A is the UL DCI: the first one is set aside (ue_dl.c:785-792) and, when the UL search that
+// follows (srslte_ue_dl_find_ul_dci, ue_dl.c:811-838) is for the same RNTI, is its result; otherwise the
+// UL search scans its own list (the UE-specific locations of its RNTI, format 0).
 struct SelCand {
   uint32_t format, L, ncce, nof_bits;
   uint64_t out_offset;
   uint32_t refused, pad; // srslte_dci_location_isvalid fails (ncce > 87, dci.c:215-221)
 };
 struct SelSearch {
-  uint32_t c0, nc, rnti, pad;
+  uint32_t c0, nc, rnti, ul_rnti; // rnti 0: no DL search (the reference's "RNTI not specified")
+  uint32_t ul_c0, ul_nc, pad0, pad1;
 };
+__device__ inline uint32_t dci_format_of(const SelCand &c, const uint8_t *bits) {
+  // pdcch.c:386-391: 0 / 1A share a size, the first bit tells them apart
+  return (c.format == SRSGPU_DCI_FORMAT0 || c.format == SRSGPU_DCI_FORMAT1A)
+             ? (bits[0] == 0 ? (uint32_t)SRSGPU_DCI_FORMAT0 : (uint32_t)SRSGPU_DCI_FORMAT1A)
+             : c.format;
+}
+__device__ inline void dci_take(srsgpu_dci_result_t &r, const SelCand &c, uint32_t f, const uint8_t *bits) {
+  r.found = 1;
+  r.format = f;
+  r.L = c.L;
+  r.ncce = c.ncce;
+  r.nof_bits = c.nof_bits;
+  for (uint32_t b = 0; b < c.nof_bits + 16 && b < SRSGPU_DCI_MAX_BITS; b++) r.data[b] = bits[b];
+}
+__device__ inline void dci_none(srsgpu_dci_result_t &r, int32_t found) {
+  r.found = found;
+  r.format = 0xFFFFFFFFu;
+  r.L = r.ncce = r.nof_bits = 0;
+  for (int b = 0; b < SRSGPU_DCI_MAX_BITS; b++) r.data[b] = 0;
+}
 __global__ void k_dci_select(const SelSearch *__restrict__ ss, int n, const SelCand *__restrict__ cand,
                              const uint8_t *__restrict__ data, const uint16_t *__restrict__ crc_rem,
-                             const uint8_t *__restrict__ decoded, srsgpu_dci_result_t *__restrict__ res) {
+                             const uint8_t *__restrict__ decoded, srsgpu_dci_result_t *__restrict__ res,
+                             srsgpu_dci_result_t *__restrict__ res_ul) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const SelSearch q = ss[s];
   srsgpu_dci_result_t r;
-  r.found = 0;
-  r.format = 0xFFFFFFFFu;
-  r.L = r.ncce = r.nof_bits = 0;
-  for (int b = 0; b < SRSGPU_DCI_MAX_BITS; b++) r.data[b] = 0;
-  for (uint32_t i = q.c0; i < q.c0 + q.nc; i++) {
+  dci_none(r, q.rnti ? 0 : -1);
+  int pend = -1; // the UL DCI set aside by the DL search
+  for (uint32_t i = q.c0; q.rnti && i < q.c0 + q.nc; i++) {
     if (cand[i].refused) { // srslte_pdcch_decode_msg fails, the search returns SRSLTE_ERROR (ue_dl.c:785-788)
       r.found = -1;
       break;
@@ -99,18 +123,38 @@ __global__ void k_dci_select(const SelSearch *__restrict__ ss, int n, const SelC
     if (!decoded[i] || crc_rem[i] != (uint16_t)q.rnti) continue;
     const SelCand c = cand[i];
     const uint8_t *bits = data + c.out_offset;
-    uint32_t f = c.format; // pdcch.c:386-391: 0 / 1A share a size, the first bit tells them apart
-    if (f == SRSGPU_DCI_FORMAT0 || f == SRSGPU_DCI_FORMAT1A) f = bits[0] == 0 ? SRSGPU_DCI_FORMAT0 : SRSGPU_DCI_FORMAT1A;
+    const uint32_t f = dci_format_of(c, bits);
+    if (f == SRSGPU_DCI_FORMAT0 && c.format == SRSGPU_DCI_FORMAT1A) {
+      if (pend < 0) pend = (int)i;
+      continue;
+    }
     if (f != c.format) continue;
-    r.found = 1;
-    r.format = f;
-    r.L = c.L;
-    r.ncce = c.ncce;
-    r.nof_bits = c.nof_bits;
-    for (uint32_t b = 0; b < c.nof_bits + 16 && b < SRSGPU_DCI_MAX_BITS; b++) r.data[b] = bits[b];
+    dci_take(r, c, f, bits);
     break;
   }
   res[s] = r;
+  if (!res_ul) return;
+  srsgpu_dci_result_t u;
+  dci_none(u, 0);
+  if (q.ul_rnti) {
+    if (pend >= 0 && q.ul_rnti == q.rnti) { // ue_dl.c:815-819
+      dci_take(u, cand[pend], SRSGPU_DCI_FORMAT0, data + cand[pend].out_offset);
+    } else {
+      for (uint32_t i = q.ul_c0; i < q.ul_c0 + q.ul_nc; i++) {
+        if (cand[i].refused) {
+          u.found = -1;
+          break;
+        }
+        if (!decoded[i] || crc_rem[i] != (uint16_t)q.ul_rnti) continue;
+        const SelCand c = cand[i];
+        const uint8_t *bits = data + c.out_offset;
+        if (bits[0] != 0) continue; // a format 1A message: not what the UL search looks for
+        dci_take(u, c, SRSGPU_DCI_FORMAT0, bits);
+        break;
+      }
+    }
+  }
+  res_ul[s] = u;
 }
 
 // ue_dl.c:41-50
@@ -374,6 +418,16 @@ int srsgpu_pdcch_extract_llr_dev(srsgpu_pdcch_t *q, const srsgpu_pdcch_sf_t *sf,
             q->d_noise ? q->d_noise + i : nullptr};
     if (nsym > max_sym) max_sym = nsym;
   }
+  { // every subframe's 72 NOF_CCE(cfi) LLRs in a region of its own: overlapping ones would be written twice
+    std::vector<std::pair<uint64_t, uint64_t>> reg(nof_sf);
+    for (uint32_t i = 0; i < nof_sf; i++) reg[i] = {sf[i].llr_offset, 2 * (uint64_t)h[i].nof_symbols};
+    std::sort(reg.begin(), reg.end());
+    for (uint32_t i = 1; i < nof_sf; i++)
+      if (reg[i - 1].first + reg[i - 1].second > reg[i].first) {
+        fprintf(stderr, "srsgpu pdcch: LLR regions of two subframes overlap (llr_offset spacing below 72 NOF_CCE)\n");
+        return -1;
+      }
+  }
   if (hipMemcpyAsync(s.d, s.h, sizeof(srsgpu::PdcchItem) * nof_sf, hipMemcpyHostToDevice, st) ||
       srsgpu::launch_pdcch_llr((const srsgpu::PdcchItem *)s.d, (int)nof_sf, max_sym, (const float2 *)d_grid,
                                (const float2 *)d_ce, ant_stride, (int)q->cell.nof_ports,
@@ -420,8 +474,9 @@ uint32_t srsgpu_pdcch_common_locations(uint32_t nof_cce, srsgpu_dci_location_t *
   return k;
 }
 
-int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s, uint32_t nof_search,
-                                 const float *d_llr, srsgpu_dci_result_t *d_res, void *hip_stream) {
+int srsgpu_pdcch_find_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s, uint32_t nof_search,
+                              const float *d_llr, srsgpu_dci_result_t *d_res, srsgpu_dci_result_t *d_res_ul,
+                              void *hip_stream) {
   if (!q || (nof_search && (!s || !d_llr || !d_res))) return -1;
   if (nof_search == 0) return 0;
   hipStream_t st = (hipStream_t)hip_stream;
@@ -432,10 +487,12 @@ int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s
   const uint32_t nprb = q->cell.nof_prb, np = q->cell.nof_ports;
   for (uint32_t i = 0; i < nof_search; i++) {
     const srsgpu_dci_search_t &x = s[i];
-    if (x.cfi < 1 || x.cfi > 3 || x.sf_idx > 9 || x.rnti == 0 || x.rnti > 0xFFFF || x.tm > 7 || x.rnti_type > 6)
+    const uint32_t ul_rnti = d_res_ul ? x.ul_rnti : 0;
+    if (x.cfi < 1 || x.cfi > 3 || x.sf_idx > 9 || x.rnti > 0xFFFF || ul_rnti > 0xFFFF || x.tm > 7 ||
+        x.rnti_type > 6 || (x.rnti == 0 && ul_rnti == 0))
       return -1;
     const uint32_t ncce = q->nof_cce[x.cfi - 1];
-    ss[i] = {(uint32_t)cand.size(), 0, x.rnti, 0};
+    ss[i] = {(uint32_t)cand.size(), 0, x.rnti, ul_rnti, 0, 0, 0, 0};
     srsgpu_dci_location_t ue[64], com[64];
     const uint32_t ncom = srsgpu_pdcch_common_locations(ncce, com, 64);
     auto add = [&](const srsgpu_dci_location_t *loc, uint32_t nl, uint32_t format) {
@@ -446,19 +503,33 @@ int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s
         dc.push_back({x.llr_offset + 72 * (uint64_t)loc[j].ncce, off, 72u << loc[j].L, nb});
       }
     };
-    // ue_dl.c:840-852: the RNTI type from the value (SI-RNTI, P-RNTI, RA-RNTI range) unless given
-    const bool common = x.rnti_type < 0 ? (x.rnti == 0xFFFF || x.rnti == 0xFFFE || x.rnti <= 0x000A)
-                                        : (x.rnti_type == 1 || x.rnti_type == 2 || x.rnti_type == 5);
-    if (common) { // find_dl_dci_type_siprarnti (ue_dl.c:855-874)
-      add(com, ncom, SRSGPU_DCI_FORMAT1A);
-      add(com, ncom, SRSGPU_DCI_FORMAT1C);
-    } else { // find_dl_dci_type_crnti (ue_dl.c:877-913)
-      const uint32_t nue = srsgpu_pdcch_ue_locations(ncce, x.sf_idx, (uint16_t)x.rnti, ue, 64);
-      add(ue, nue, kUeFormats[x.tm][0]);
-      add(ue, nue, kUeFormats[x.tm][1]);
-      add(com, ncom, SRSGPU_DCI_FORMAT1A);
+    bool ul_shared = false;
+    if (x.rnti) {
+      // ue_dl.c:840-852: the RNTI type from the value (SI-RNTI, P-RNTI, RA-RNTI range) unless given
+      const bool common = x.rnti_type < 0 ? (x.rnti == 0xFFFF || x.rnti == 0xFFFE || x.rnti <= 0x000A)
+                                          : (x.rnti_type == 1 || x.rnti_type == 2 || x.rnti_type == 5);
+      if (common) { // find_dl_dci_type_siprarnti (ue_dl.c:855-874)
+        add(com, ncom, SRSGPU_DCI_FORMAT1A);
+        add(com, ncom, SRSGPU_DCI_FORMAT1C);
+      } else { // find_dl_dci_type_crnti (ue_dl.c:877-913)
+        const uint32_t nue = srsgpu_pdcch_ue_locations(ncce, x.sf_idx, (uint16_t)x.rnti, ue, 64);
+        add(ue, nue, kUeFormats[x.tm][0]); // 1A: the UL search's candidates too when the RNTIs agree
+        add(ue, nue, kUeFormats[x.tm][1]);
+        add(com, ncom, SRSGPU_DCI_FORMAT1A);
+        if (ul_rnti == x.rnti) {
+          ss[i].ul_c0 = ss[i].c0;
+          ss[i].ul_nc = nue;
+          ul_shared = true;
+        }
+      }
+      ss[i].nc = (uint32_t)cand.size() - ss[i].c0;
     }
-    ss[i].nc = (uint32_t)cand.size() - ss[i].c0;
+    if (ul_rnti && !ul_shared) { // srslte_ue_dl_find_ul_dci's own list (ue_dl.c:825-832)
+      const uint32_t nue = srsgpu_pdcch_ue_locations(ncce, x.sf_idx, (uint16_t)ul_rnti, ue, 64);
+      ss[i].ul_c0 = (uint32_t)cand.size();
+      add(ue, nue, SRSGPU_DCI_FORMAT0);
+      ss[i].ul_nc = nue;
+    }
   }
   const size_t nc = cand.size();
   // scratch for the candidate decodes (reused once the previous search has finished with it)
@@ -485,14 +556,23 @@ int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s
   memcpy(h, dc.data(), b_dc);
   memcpy(h + b_dc, cand.data(), b_sel);
   memcpy(h + b_dc + b_sel, ss.data(), b_ss);
-  if (hipMemcpyAsync(d, h, b_dc + b_sel + b_ss, hipMemcpyHostToDevice, st) ||
-      srsgpu_dci_decode_dev((const srsgpu_dci_cand_t *)d, (uint32_t)nc, d_llr, q->d_bits, q->d_crc, q->d_dec, st))
+  if (hipMemcpyAsync(d, h, b_dc + b_sel + b_ss, hipMemcpyHostToDevice, st)) return -1;
+  if (nc && srsgpu_dci_decode_dev((const srsgpu_dci_cand_t *)d, (uint32_t)nc, d_llr, q->d_bits, q->d_crc, q->d_dec,
+                                  st))
     return -1;
   hipLaunchKernelGGL(k_dci_select, dim3((nof_search + 63) / 64), dim3(64), 0, st, (const SelSearch *)(d + b_dc + b_sel),
-                     (int)nof_search, (const SelCand *)(d + b_dc), q->d_bits, q->d_crc, q->d_dec, d_res);
+                     (int)nof_search, (const SelCand *)(d + b_dc), q->d_bits, q->d_crc, q->d_dec, d_res, d_res_ul);
   if (hipGetLastError() != hipSuccess || sl.mark(st) || hipEventRecord(q->search_done, st)) return -1;
   q->search_pending = true;
   return 0;
+}
+
+int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s, uint32_t nof_search,
+                                 const float *d_llr, srsgpu_dci_result_t *d_res, void *hip_stream) {
+  if (!q || (nof_search && !s)) return -1;
+  for (uint32_t i = 0; i < nof_search; i++)
+    if (s[i].rnti == 0) return -1; // a DL search needs its RNTI
+  return srsgpu_pdcch_find_dci_dev(q, s, nof_search, d_llr, d_res, nullptr, hip_stream);
 }
 
 } // extern "C"

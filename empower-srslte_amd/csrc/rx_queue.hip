@@ -108,6 +108,8 @@ struct srsgpu_rxq {
   srsgpu_cell_t cell{};
   uint32_t N = 0, max_batch = 0, max_wait_us = 0, max_halfits = 8, nports = 1, nrx = 1;
   uint32_t phich_len = 0, phich_res = 2;
+  bool phich_dirty = false; // srsgpu_rxq_set_phich: the dispatcher rebuilds pdcch before its next use
+  uint32_t scratch_sb = 0;  // softbuffer of TBs the caller already acked (decoded, result dropped)
   size_t td_len = 0, gsz = 0, dlen = 0; // complex samples per antenna / grid elements / TB bytes
   hipStream_t st = nullptr, cst = nullptr; // compute / copy streams
   srsgpu_ofdm_t *ofdm = nullptr;
@@ -135,6 +137,7 @@ struct srsgpu_rxq {
   float *d_llr = nullptr;
   size_t llr_stride = 0;
   srsgpu_dci_result_t *d_res = nullptr, *h_res = nullptr;
+  srsgpu_dci_result_t *d_res_ul = nullptr, *h_res_ul = nullptr;
 
   // staging slots
   enum { FILLING = 0, CLOSED = 1, STAGED = 2 };
@@ -168,12 +171,21 @@ struct srsgpu_rxq {
     td_len = (size_t)15 * N;
     gsz = (size_t)14 * 12 * cell.nof_prb;
     dlen = SRSGPU_DLSCH_DATA_LEN(75376) + 16;
-    llr_stride = 72 * 88; // 72 NOF_CCE(3) floats at most (20 MHz: 87 CCEs)
+    // 72 NOF_CCE(cfi) floats per subframe at most: the largest CCE count of the cell, which the
+    // smallest PHICH allocation (normal length, Ng = 1/6) leaves (110 PRB: 96 CCEs)
+    uint32_t max_cce = 0;
+    for (uint32_t cfi = 1; cfi <= 3; cfi++) {
+      uint32_t nc = 0;
+      if (srsgpu_pdcch_cell_map(&cell, 0, 0, cfi, nullptr, 0, &nc) < 0) return -1;
+      if (nc > max_cce) max_cce = nc;
+    }
+    llr_stride = 72 * (size_t)max_cce;
     const uint32_t max_cb = 13;
+    scratch_sb = nsb; // one more softbuffer than the caller's
     RXQ_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     RXQ_CHK(hipStreamCreateWithFlags(&cst, hipStreamNonBlocking));
     if (srsgpu_ofdm_rx_create(&ofdm, cell.nof_prb, N) || srsgpu_chest_create(&chest, &cell, mb * nrx) ||
-        srsgpu_pdsch_create(&pdsch, &cell, nsb, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
+        srsgpu_pdsch_create(&pdsch, &cell, nsb + 1, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
       return -1;
     srsgpu_ofdm_rx_set_stream(ofdm, st);
     srsgpu_chest_set_stream(chest, st);
@@ -210,6 +222,8 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMalloc(&d_llr, sizeof(float) * llr_stride * mb));
     RXQ_CHK(hipMalloc(&d_res, sizeof(srsgpu_dci_result_t) * mb));
     RXQ_CHK(hipHostMalloc(&h_res, sizeof(srsgpu_dci_result_t) * mb));
+    RXQ_CHK(hipMalloc(&d_res_ul, sizeof(srsgpu_dci_result_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_res_ul, sizeof(srsgpu_dci_result_t) * mb));
     srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
     closer = std::thread([this] { close_loop(); });
     worker = std::thread([this] { run_loop(); });
@@ -239,10 +253,11 @@ struct srsgpu_rxq {
     for (void *p : {(void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data, (void *)d_ret,
                     (void *)d_noi, (void *)d_noise_last, (void *)d_est, (void *)d_sel, (void *)d_uenoise,
                     (void *)d_cfi, (void *)d_corr, (void *)d_llr, (void *)d_res, (void *)d_who,
-                    (void *)d_pnoise})
+                    (void *)d_pnoise, (void *)d_res_ul})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est,
-                    (void *)h_sel, (void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_who})
+                    (void *)h_sel, (void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_who,
+                    (void *)h_res_ul})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
@@ -364,8 +379,21 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMemcpyAsync(h_cfi, d_cfi, sizeof(uint32_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipMemcpyAsync(h_corr, d_corr, sizeof(float) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipStreamSynchronize(st));
+    uint32_t plen, pres;
+    bool rebuild;
+    {
+      std::lock_guard<std::mutex> l(m);
+      plen = phich_len;
+      pres = phich_res;
+      rebuild = phich_dirty;
+      phich_dirty = false;
+    }
+    if (pdcch && rebuild) { // only this thread uses pdcch, and its previous batch has finished
+      srsgpu_pdcch_destroy(pdcch);
+      pdcch = nullptr;
+    }
     if (!pdcch) {
-      if (srsgpu_pdcch_create(&pdcch, &cell, phich_len, phich_res)) return -1;
+      if (srsgpu_pdcch_create(&pdcch, &cell, plen, pres)) return -1;
       srsgpu_pdcch_set_noise_dev(pdcch, d_uenoise);
     }
     std::vector<srsgpu_pdcch_sf_t> ps(nu);
@@ -374,12 +402,13 @@ struct srsgpu_rxq {
       const srsgpu_rxq_ue_dl_t *u = b[ue[j]].ue;
       ps[j] = {(uint64_t)ue[j] * nrx * gsz, (uint64_t)ue[j] * nrx * nports * gsz, (uint64_t)j * llr_stride,
                u->tti % 10, h_cfi[j], 0.f, 0};
-      se[j] = {(uint64_t)j * llr_stride, u->tti % 10, h_cfi[j], u->rnti, u->tm, u->rnti_type, 0};
+      se[j] = {(uint64_t)j * llr_stride, u->tti % 10, h_cfi[j], u->rnti, u->tm, u->rnti_type, u->ul_rnti};
     }
     if (srsgpu_pdcch_extract_llr_dev(pdcch, ps.data(), nu, d_grid, d_ce, gsz, d_llr, st) ||
-        srsgpu_pdcch_find_dl_dci_dev(pdcch, se.data(), nu, d_llr, d_res, st))
+        srsgpu_pdcch_find_dci_dev(pdcch, se.data(), nu, d_llr, d_res, d_res_ul, st))
       return -1;
     RXQ_CHK(hipMemcpyAsync(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(hipMemcpyAsync(h_res_ul, d_res_ul, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipStreamSynchronize(st));
     return 0;
   }
@@ -452,7 +481,10 @@ struct srsgpu_rxq {
       sf.mod[i] = g.mod[i];
       sf.tbs[i] = g.tb_en[i] ? (uint32_t)g.tbs[i] : 0;
       sf.rv[i] = rv[i];
-      sf.softbuffer[i] = u->softbuffer[i];
+      // a TB the caller already acked is skipped by srslte_pdsch_decode (pdsch.c:946-947): decode it into
+      // the scratch softbuffer and drop the result, the caller's softbuffer and data stay as they are
+      sf.softbuffer[i] = u->acks[i] ? scratch_sb : u->softbuffer[i];
+      if (u->acks[i] && g.tb_en[i] && srsgpu_dlsch_softbuffer_reset(dl, scratch_sb)) return -1;
     }
     const int nre = srsgpu_pdsch_nof_re(&cell, &sf);
     if (nre <= 0) return -1;
@@ -504,6 +536,20 @@ struct srsgpu_rxq {
         u->format = res.format;
         u->L = res.L;
         u->ncce = res.ncce;
+        // srslte_ue_dl_find_ul_dci + srslte_dci_msg_to_ul_grant (phch_worker.cc:938-967)
+        const srsgpu_dci_result_t &ur = h_res_ul[j];
+        u->ul_found = u->ul_rnti ? ur.found : 0;
+        u->ul_L = ur.L;
+        u->ul_ncce = ur.ncce;
+        u->ul_nof_bits = ur.nof_bits;
+        memcpy(u->ul_data, ur.data, sizeof(u->ul_data));
+        memset(&u->ul_dci, 0, sizeof(u->ul_dci));
+        memset(&u->ul_grant, 0, sizeof(u->ul_grant));
+        u->ul_grant_ret = u->ul_found == 1 ? srsgpu_dci_msg_to_ul_grant(ur.data, ur.nof_bits, cell.nof_prb, u->n_rb_ho,
+                                                                         &u->ul_dci, &u->ul_grant)
+                                           : -1;
+        u->acked_in[0] = u->acks[0];
+        u->acked_in[1] = u->acks[1];
         u->noi[0] = u->noi[1] = 0;
         j++;
         if (res.found != 1) { // no DCI, or the search's error: srslte_ue_dl_decode_rnti returns 0
@@ -560,8 +606,9 @@ struct srsgpu_rxq {
           p.it->ret[t] = h_ret[t0];
           p.it->noi[t] = h_noi[t0];
         } else {
+          if (p.ue->acked_in[t]) continue; // skipped as srslte_pdsch_decode skips it: nothing written
           p.ue->noi[t] = h_noi[t0];
-          if (!p.ue->acks[t]) p.ue->acks[t] = h_ret[t0] == 0;
+          p.ue->acks[t] = h_ret[t0] == 0;
         }
         if (out) memcpy(out, h_data + (2 * k + t) * dlen, SRSGPU_DLSCH_DATA_LEN(sfs[k].tbs[t]));
       }
@@ -649,10 +696,7 @@ int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_
   std::lock_guard<std::mutex> l(q->m);
   q->phich_len = phich_length;
   q->phich_res = phich_resources;
-  if (q->pdcch) { // rebuilt with the new map on the next ue_dl batch
-    srsgpu_pdcch_destroy(q->pdcch);
-    q->pdcch = nullptr;
-  }
+  q->phich_dirty = true; // the dispatcher rebuilds the map before its next ue_dl batch
   return 0;
 }
 

@@ -148,7 +148,7 @@ class srsgpu_dci_search_t(ctypes.Structure):
     """include/srsgpu/pdcch_batch.h"""
     _fields_ = [("llr_offset", ctypes.c_uint64), ("sf_idx", ctypes.c_uint32), ("cfi", ctypes.c_uint32),
                 ("rnti", ctypes.c_uint32), ("tm", ctypes.c_uint32), ("rnti_type", ctypes.c_int32),
-                ("reserved", ctypes.c_uint32)]
+                ("ul_rnti", ctypes.c_uint32)]
 
 
 class srsgpu_dci_result_t(ctypes.Structure):
@@ -194,6 +194,29 @@ class srsgpu_ra_dl_grant_t(ctypes.Structure):
                 self.tbs[1], self.mcs_idx[1], self.tb_en[0], self.tb_en[1], self.pinfo, self.tb_cw_swap]
 
 
+class srsgpu_ra_ul_dci_t(ctypes.Structure):
+    """include/srsgpu/dci.h (format 0)"""
+    _fields_ = [("freq_hop_fl", ctypes.c_int32)] + [(n, ctypes.c_uint32) for n in (
+        "riv", "L_crb", "RB_start", "mcs_idx", "rv_idx", "n_dmrs", "ndi", "cqi_request", "tpc_pusch")]
+
+    def fields11(self):
+        """oracle/ref_front.c's order"""
+        return [self.freq_hop_fl, self.riv, self.L_crb, self.RB_start, self.mcs_idx, self.rv_idx, self.n_dmrs,
+                self.ndi, self.cqi_request, self.tpc_pusch, 0]
+
+
+class srsgpu_ra_ul_grant_t(ctypes.Structure):
+    """include/srsgpu/dci.h"""
+    _fields_ = [("L_prb", ctypes.c_uint32), ("n_prb", ctypes.c_uint32 * 2)] + \
+        [(n, ctypes.c_uint32) for n in ("freq_hopping", "M_sc", "M_sc_init", "Qm", "mod")] + \
+        [("tbs", ctypes.c_int32), ("mcs_idx", ctypes.c_uint32), ("ncs_dmrs", ctypes.c_uint32)]
+
+    def fields10(self):
+        """oracle/ref_front.c's order"""
+        return [self.L_prb, self.n_prb[0], self.n_prb[1], self.freq_hopping, self.M_sc, self.Qm, self.mod, self.tbs,
+                self.mcs_idx, self.ncs_dmrs]
+
+
 class srsgpu_rxq_ue_dl_t(ctypes.Structure):
     """include/srsgpu/rx_queue.h: one srslte_ue_dl_decode_rnti subframe"""
     _fields_ = [("td", ctypes.c_void_p * 2), ("tti", ctypes.c_uint32), ("rnti", ctypes.c_uint16),
@@ -202,7 +225,11 @@ class srsgpu_rxq_ue_dl_t(ctypes.Structure):
                 ("cfi", ctypes.c_uint32), ("cfi_corr", ctypes.c_float), ("found", ctypes.c_int32),
                 ("format", ctypes.c_uint32), ("L", ctypes.c_uint32), ("ncce", ctypes.c_uint32),
                 ("mimo_type", ctypes.c_uint32), ("rv", ctypes.c_uint32 * 2), ("grant", srsgpu_ra_dl_grant_t),
-                ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float)]
+                ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float),
+                ("ul_rnti", ctypes.c_uint16), ("n_rb_ho", ctypes.c_uint32), ("ul_found", ctypes.c_int32),
+                ("ul_L", ctypes.c_uint32), ("ul_ncce", ctypes.c_uint32), ("ul_nof_bits", ctypes.c_uint32),
+                ("ul_data", ctypes.c_uint8 * 128), ("ul_grant_ret", ctypes.c_int32), ("ul_dci", srsgpu_ra_ul_dci_t),
+                ("ul_grant", srsgpu_ra_ul_grant_t), ("acked_in", ctypes.c_uint8 * 2)]
 
 
 def dlsch_data_len(tbs):
@@ -245,6 +272,7 @@ _sig = {
     "srsgpu_dlsch_softbuffer_reset": (_i32, [_vp, _u32]),
     "srsgpu_dlsch_softbuffer_reset_tbs": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_softbuffer_reset_range": (_i32, [_vp, _u32, _u32]),
+    "srsgpu_ulsch_deinterleave_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), _u32, _vp, _vp]),
     "srsgpu_ulsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), _u32, _vp, _vp, _vp, _u32,
                                        _vp, _vp]),
     "srsgpu_dlsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp, _u32,
@@ -284,6 +312,9 @@ _sig = {
                                          _u32]),
     "srsgpu_pdcch_common_locations": (_u32, [_u32, ctypes.POINTER(srsgpu_dci_location_t), _u32]),
     "srsgpu_pdcch_find_dl_dci_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dci_search_t), _u32, _vp, _vp, _vp]),
+    "srsgpu_pdcch_find_dci_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dci_search_t), _u32, _vp, _vp, _vp, _vp]),
+    "srsgpu_dci_msg_to_ul_grant": (_i32, [_u8p, _u32, _u32, _u32, ctypes.POINTER(srsgpu_ra_ul_dci_t),
+                                          ctypes.POINTER(srsgpu_ra_ul_grant_t)]),
     "srsgpu_dci_format_sizeof": (_u32, [_u32, _u32, _u32]),
     "srsgpu_dci_msg_to_dl_grant": (_i32, [_u8p, _u32, _u32, ctypes.c_uint16, _u32, _u32,
                                           ctypes.POINTER(srsgpu_ra_dl_dci_t),
@@ -322,6 +353,7 @@ _sig = {
     "srsgpu_chest_set_stream": (None, [_vp, _vp]),
     "srsgpu_chest_set_smooth_filter": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _u32]),
     "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
+    "srsgpu_chest_set_smooth_filter_gauss": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_float]),
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
     "srsgpu_chest_estimate_meas_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp, _vp]),
     "srsgpu_chest_set_cfg": (_i32, [_vp, _vp]),
@@ -699,6 +731,17 @@ def dci_format_sizeof(fmt, nof_prb, nof_ports):
     return _lib.srsgpu_dci_format_sizeof(fmt, nof_prb, nof_ports)
 
 
+def dci_msg_to_ul_grant(bits, nof_prb, n_rb_ho=0, nof_bits=None):
+    """srsgpu_dci_msg_to_ul_grant -> (ret, srsgpu_ra_ul_dci_t, srsgpu_ra_ul_grant_t)"""
+    b = np.zeros(128, np.uint8)
+    b[:len(bits)] = bits
+    nof_bits = len(bits) if nof_bits is None else nof_bits
+    d, g = srsgpu_ra_ul_dci_t(), srsgpu_ra_ul_grant_t()
+    r = _lib.srsgpu_dci_msg_to_ul_grant(b.ctypes.data_as(_u8p), nof_bits, nof_prb, n_rb_ho, ctypes.byref(d),
+                                        ctypes.byref(g))
+    return r, d, g
+
+
 def dci_msg_to_dl_grant(bits, fmt, rnti, nof_prb, nof_ports, nof_bits=None):
     """srsgpu_dci_msg_to_dl_grant of bits[:nof_bits] (default: all of bits), read from a zero-padded
     128-byte message buffer: (ret, srsgpu_ra_dl_dci_t, srsgpu_ra_dl_grant_t)"""
@@ -747,12 +790,19 @@ class Pdcch:
 
     @staticmethod
     def make_search_array(searches):
-        """list of (llr_offset, sf_idx, cfi, rnti, tm[, rnti_type]) -> srsgpu_dci_search_t array"""
+        """list of (llr_offset, sf_idx, cfi, rnti, tm[, rnti_type[, ul_rnti]]) -> srsgpu_dci_search_t array"""
         arr = (srsgpu_dci_search_t * max(len(searches), 1))()
         for i, s in enumerate(searches):
             arr[i].llr_offset, arr[i].sf_idx, arr[i].cfi, arr[i].rnti, arr[i].tm = s[:5]
             arr[i].rnti_type = s[5] if len(s) > 5 else -1
+            arr[i].ul_rnti = s[6] if len(s) > 6 else 0
         return arr
+
+    def find_dci_dev(self, searches, d_llr, d_res, d_res_ul, stream=None):
+        """srsgpu_pdcch_find_dci_dev: DL then UL searches; d_res / d_res_ul: len(searches) results each"""
+        arr = self.make_search_array(searches)
+        return _lib.srsgpu_pdcch_find_dci_dev(self.q, arr, len(searches), _vp(d_llr), _vp(d_res), _vp(d_res_ul),
+                                              _vp(stream))
 
     def find_dl_dci_dev(self, searches, d_llr, d_res, stream=None):
         """d_res: device buffer of len(searches) srsgpu_dci_result_t (RESULT_SIZE bytes each)"""
@@ -876,6 +926,10 @@ class Chest:
 
     def set_filter3(self, w):
         _lib.srsgpu_chest_set_smooth_filter3_coeff(self.q, w)
+
+    def set_filter_gauss(self, order, std_dev):
+        if _lib.srsgpu_chest_set_smooth_filter_gauss(self.q, order, ctypes.c_float(std_dev)) != 0:
+            raise RuntimeError("invalid Gaussian smoothing filter")
 
     def put_crs_dev(self, sf_idx, d_grid, stride):
         n = len(sf_idx)
@@ -1039,13 +1093,15 @@ class RxQueue:
         return _lib.srsgpu_rxq_decode(self.q, ctypes.byref(it))
 
     @staticmethod
-    def ue_item(td, tti, rnti, data, tm=0, rnti_type=-1, softbuffer=(0, 1)):
+    def ue_item(td, tti, rnti, data, tm=0, rnti_type=-1, softbuffer=(0, 1), ul_rnti=0, n_rb_ho=0, acks=(0, 0)):
         """srsgpu_rxq_ue_dl_t: td complex64 arrays per rx antenna, data uint8 arrays per TB (both kept
         alive by the caller)"""
         u = srsgpu_rxq_ue_dl_t()
         for a, x in enumerate(td):
             u.td[a] = x.ctypes.data
         u.tti, u.rnti, u.tm, u.rnti_type = tti, rnti, tm, rnti_type
+        u.ul_rnti, u.n_rb_ho = ul_rnti, n_rb_ho
+        u.acks[0], u.acks[1] = acks
         u.softbuffer[0], u.softbuffer[1] = softbuffer
         for t, d in enumerate(data):
             u.data[t] = d.ctypes.data

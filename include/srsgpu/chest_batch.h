@@ -35,6 +35,9 @@ void srsgpu_chest_set_stream(srsgpu_chest_t *q, void *hip_stream);
 int srsgpu_chest_set_smooth_filter(srsgpu_chest_t *q, const float *filter, uint32_t filter_len);
 /* srslte_chest_dl_set_smooth_filter3_coeff: [w, 1-2w, w] */
 void srsgpu_chest_set_smooth_filter3_coeff(srsgpu_chest_t *q, float w);
+/* srslte_chest_dl_set_smooth_filter_gauss (chest_dl.c:475-494): order + 1 taps, the reference's float
+ * arithmetic (srsUE: order 4, std dev 1.0, phch_worker.cc:553-556); -1 above 64 taps */
+int srsgpu_chest_set_smooth_filter_gauss(srsgpu_chest_t *q, uint32_t order, float std_dev);
 
 /* the srslte_chest_dl_t settings chest_dl.c reads (defaults as srslte_chest_dl_init leaves them:
  * all zero = per-symbol, REFS, fixed filter, no neighbour RSRP, no CFO) */

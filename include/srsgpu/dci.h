@@ -10,6 +10,9 @@
  *   srslte_ra_dl_dci_to_grant         src/phy/phch/ra.c:292-425 (PRB allocation types 0, 1, 2
  *                                     localised and distributed), :427-455, :509-561, :583-612
  *   srslte_ra_tbs_from_idx            src/phy/phch/ra.c:725 (36.213 Table 7.1.7.2.1-1)
+ *   srslte_dci_msg_to_ul_grant        src/phy/phch/dci.c:165-197 with dci_format0_unpack (:571-626),
+ *                                     srslte_ra_ul_dci_to_grant (ra.c:118-245: PUSCH hopping type 1 / 2,
+ *                                     MCS / TBS / redundancy version of 36.213 8.6)
  * with the reference's field semantics and error returns; tests/test_dci.py checks every function
  * against the reference build. Pure host code: no GPU needed.
  */
@@ -64,6 +67,21 @@ typedef struct {
   uint32_t pinfo, tb_cw_swap;
 } srsgpu_ra_dl_grant_t;
 
+/* srslte_ra_ul_dci_t (ra.h:172-194), format 0 */
+typedef struct {
+  int32_t freq_hop_fl;      /* -1 disabled, 0 quarter, 1 minus quarter, 2 half, 3 type 2 */
+  uint32_t riv, L_crb, RB_start;
+  uint32_t mcs_idx, rv_idx, n_dmrs, ndi, cqi_request, tpc_pusch;
+} srsgpu_ra_ul_dci_t;
+
+/* srslte_ra_ul_grant_t (ra.h:150-169) */
+typedef struct {
+  uint32_t L_prb, n_prb[2], freq_hopping, M_sc, M_sc_init, Qm;
+  uint32_t mod;             /* srslte_mod_t; 4 = SRSLTE_MOD_LAST (mcs 29-31: keep the last one) */
+  int32_t tbs;              /* -1 with SRSLTE_MOD_LAST */
+  uint32_t mcs_idx, ncs_dmrs;
+} srsgpu_ra_ul_grant_t;
+
 uint32_t srsgpu_dci_format_sizeof(uint32_t format, uint32_t nof_prb, uint32_t nof_ports);
 /* srslte_dci_msg_to_dl_grant: bits is the message buffer as srslte_dci_msg_t.data holds it
  * (SRSGPU_DCI_MAX_BITS = 128 bytes, one bit per byte: nof_bits payload bits, then what the decoder
@@ -80,6 +98,12 @@ int srsgpu_dci_msg_to_dl_grant(const uint8_t *bits, uint32_t nof_bits, uint32_t 
  * RA- or P-RNTI sets dci->rv_idx = 0 (36.213 7.1.7.3). */
 int srsgpu_ra_dl_dci_to_grant(srsgpu_ra_dl_dci_t *dci, uint32_t nof_prb, uint16_t rnti,
                               srsgpu_ra_dl_grant_t *grant);
+/* srslte_dci_msg_to_ul_grant (dci.c:165-197): unpack a format 0 message (bits / nof_bits as above) and
+ * compute its PUSCH grant with hopping offset n_rb_ho (pusch_hopping.hopping_offset). -1 (SRSLTE_ERROR)
+ * if the message is not a format 0 of this bandwidth or the allocation does not fit (dci / grant as far
+ * as the reference filled them), else 0. */
+int srsgpu_dci_msg_to_ul_grant(const uint8_t *bits, uint32_t nof_bits, uint32_t nof_prb, uint32_t n_rb_ho,
+                               srsgpu_ra_ul_dci_t *dci, srsgpu_ra_ul_grant_t *grant);
 /* 36.213 Table 7.1.7.2.1-1: -1 outside tbs_idx < 27, 1 <= nof_prb <= 110 */
 int srsgpu_ra_tbs_from_idx(uint32_t tbs_idx, uint32_t nof_prb);
 /* srslte_ra_tbs_idx_from_mcs (ra.c:697): -1 for mcs >= 29 */

@@ -85,10 +85,10 @@ uint32_t srsgpu_pdcch_common_locations(uint32_t nof_cce, srsgpu_dci_location_t *
 typedef struct {
   uint64_t llr_offset;
   uint32_t sf_idx, cfi;
-  uint32_t rnti;
+  uint32_t rnti;       /* the DL search's RNTI (srsgpu_pdcch_find_dci_dev: 0 = no DL search) */
   uint32_t tm;
   int32_t rnti_type;
-  uint32_t reserved;
+  uint32_t ul_rnti;    /* srsgpu_pdcch_find_dci_dev only: the UL search's RNTI, 0 = none */
 } srsgpu_dci_search_t;
 
 /* result: found 1 / 0, or -1 where the reference's search returns SRSLTE_ERROR (it reaches a
@@ -103,9 +103,20 @@ typedef struct {
 } srsgpu_dci_result_t;
 
 /* srslte_ue_dl_find_dl_dci for nof_search searches (host array) on device LLRs; d_res: device
- * array of nof_search results. Asynchronous on hip_stream. 0, or -1 on invalid input. */
+ * array of nof_search results. Asynchronous on hip_stream. 0, or -1 on invalid input (ul_rnti is
+ * ignored). */
 int srsgpu_pdcch_find_dl_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s, uint32_t nof_search,
                                  const float *d_llr, srsgpu_dci_result_t *d_res, void *hip_stream);
+/* srsUE's per-subframe PDCCH searches (phch_worker.cc:548-806 then :938-967): the DL search of
+ * srslte_ue_dl_find_dl_dci(_type) for rnti (none if 0: d_res then reports -1, the reference's "RNTI not
+ * specified" error, ue_dl.c:805-807), then srslte_ue_dl_find_ul_dci for ul_rnti (none if 0: found 0),
+ * format 0 in the UE-specific space (ue_dl.c:811-838). A format 0 message the DL 1A search passed over
+ * (ue_dl.c:785-792) is the UL result when ul_rnti equals rnti; the search keeps no state between calls
+ * (the reference's ue_dl object carries such a message to a later UL search of that RNTI when this
+ * subframe's UL search is for another one). d_res_ul: nof_search results (format 0, same layout). */
+int srsgpu_pdcch_find_dci_dev(srsgpu_pdcch_t *q, const srsgpu_dci_search_t *s, uint32_t nof_search,
+                              const float *d_llr, srsgpu_dci_result_t *d_res, srsgpu_dci_result_t *d_res_ul,
+                              void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -57,7 +57,8 @@ typedef struct {
                               srslte_rnti_type_t of srslte_ue_dl_find_dl_dci_type */
   uint32_t softbuffer[2];  /* q->softbuffers[0..1]: reset_tbs'd for every found grant */
   uint8_t *data[2];        /* host output per TB: SRSGPU_DLSCH_DATA_LEN(tbs) bytes */
-  uint8_t acks[2];         /* in/out, as srslte_pdsch_decode's acks: a true ack skips the TB */
+  uint8_t acks[2];         /* in/out, as srslte_pdsch_decode's acks: a true ack skips the TB (its data,
+                              noi and softbuffer are left as they are) */
   /* out (valid once srsgpu_rxq_wait returned 0) */
   int32_t ret;             /* srslte_ue_dl_decode_rnti's return: the grant's TB 0 size when a DCI
                               was found and the PDSCH decoded, 0 when no DCI was found, -1 on the
@@ -73,6 +74,17 @@ typedef struct {
   srsgpu_ra_dl_grant_t grant;
   uint32_t noi[2];
   float noise;             /* srslte_chest_dl_get_noise_estimate */
+  /* the UL search that phch_worker runs on the same PDCCH after the DL one (phch_worker.cc:938-967):
+   * srslte_ue_dl_find_ul_dci (ue_dl.c:811-838) and srslte_dci_msg_to_ul_grant of its result */
+  uint16_t ul_rnti;        /* in: 0 = no UL search */
+  uint32_t n_rb_ho;        /* in: PUSCH hopping offset (pusch_hopping.hopping_offset) */
+  int32_t ul_found;        /* out: 1 found (a format 0 message), 0 not, -1 the search's error */
+  uint32_t ul_L, ul_ncce, ul_nof_bits;
+  uint8_t ul_data[128];    /* the message buffer (payload, 16 CRC bits) */
+  int32_t ul_grant_ret;    /* srslte_dci_msg_to_ul_grant's return (-1 when nothing was found) */
+  srsgpu_ra_ul_dci_t ul_dci;
+  srsgpu_ra_ul_grant_t ul_grant;
+  uint8_t acked_in[2];     /* internal: acks as submitted */
 } srsgpu_rxq_ue_dl_t;
 
 /* One cell (srsgpu_cell_t), FFT size symbol_sz (srsgpu_symbol_sz), nof_softbuffers HARQ
@@ -95,7 +107,7 @@ int srsgpu_rxq_submit_ue_dl(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item, uint64_t 
 int srsgpu_rxq_decode_rnti(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item);
 /* PHICH configuration of the cell (srslte_regs_init from the MIB: length 0 normal / 1 extended,
  * resources 0..3 = 1/6, 1/2, 1, 2): sets the PDCCH REG map of the ue_dl items. Default normal, 1.
- * Change it only while nothing is queued. */
+ * Takes effect from the next batch the dispatcher starts (safe while batches are in flight). */
 int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_resources);
 /* close the current batch now */
 void srsgpu_rxq_flush(srsgpu_rxq_t *q);

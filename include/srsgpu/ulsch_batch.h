@@ -44,6 +44,10 @@ typedef struct {
 int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t nof_tb,
                             const int16_t *d_q_bits, int16_t *d_g_bits, uint8_t *d_data,
                             uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
+/* The channel deinterleaver alone (d_q -> d_g, same TB descriptors; tbs, rv, softbuffer and data_offset
+ * unused): srslte_ulsch_decode of a PUSCH without data (tbs 0, sch.c:957-975) still writes g_bits. */
+int srsgpu_ulsch_deinterleave_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t nof_tb,
+                                  const int16_t *d_q_bits, int16_t *d_g_bits);
 
 #ifdef __cplusplus
 }

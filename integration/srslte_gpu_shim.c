@@ -681,8 +681,11 @@ int srslte_ulsch_decode(srslte_sch_t *q, srslte_pusch_cfg_t *cfg, srslte_softbuf
   if (shim_copy(d_q, q_bits, sizeof(int16_t) * nb, H2D)) return SRSLTE_ERROR;
   int32_t *d_ret = (int32_t *)e->d_c;
   uint32_t *d_noi = (uint32_t *)e->d_c + 1;
-  if (tbs == 0) /* sch.c:975: a PUSCH without data (UCI only, not on this path) decodes nothing */
+  if (tbs == 0) { /* sch.c:957-975: deinterleaved into g_bits, then nothing to decode */
+    if (srsgpu_ulsch_deinterleave_dev(dl, &tb, 1, d_q, d_g) || shim_copy(g_bits, d_g, sizeof(int16_t) * nb, D2H))
+      return SRSLTE_ERROR;
     return SRSLTE_SUCCESS;
+  }
   if (srsgpu_ulsch_decode_dev(dl, &tb, 1, d_q, d_g, (uint8_t *)e->d_b, q->max_iterations, d_ret, d_noi))
     return SRSLTE_ERROR;
   int32_t rn[2];

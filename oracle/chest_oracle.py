@@ -19,10 +19,11 @@ channel estimation for CRS ports 0 and 1, normal CP (paths relative to
   noise_empty       chest_dl.c:351-361 estimate_noise_empty_sc; both only in subframes 0 and 5
   measurements      chest_dl.c:500-515 rssi, :562-587 CFO, :652-657 RSRP / RSRP correlation
 
-The reference chest (chest_dl.c) cannot be compiled here: through sync/pss.c and
-utils/convolution.c it needs the FFTW-backed DFT, which the image lacks. Its CRS generation and
-pilot extraction (refsignal_dl.c) do compile and pin crs_pilots / ls_estimates; the rest is
-parity-unpinned restatement (float stage, compared with a tolerance).
+Pinned to the reference: chest_dl.c itself (with sync/pss.c, utils/convolution.c, resampling/interp.c)
+is compiled where it lies into oracle/_ref/ref_front (srslte_dft_* left unresolved: the estimation path
+never calls them). tests/golden/chest_golden.npz holds its outputs (tests/golden/make_chest_golden.py)
+and tests/test_chest.py checks this restatement against them (and against live runs in the build
+container) within 1e-4 relative; CRS generation and pilot extraction equal refsignal_dl.c bit for bit.
 Only tests/ may import this module.
 """
 import numpy as np

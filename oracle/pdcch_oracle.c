@@ -9,8 +9,10 @@
  *                        of srslte_regs_pdcch_get (:200-236); NOF_CCE (pdcch.c:183-186)
  *   orc_pdcch_llr        srslte_pdcch_extract_llr_multi (phch/pdcch.c:442-508)
  *   orc_pdcch_locations  srslte_pdcch_ue_locations_ncce / _common_locations_ncce (pdcch.c:227-300)
- *   orc_find_dl_dci      srslte_ue_dl_find_dl_dci(_type) (ue/ue_dl.c:768-923) over
- *                        srslte_pdcch_decode_msg (pdcch.c:366-420) = orc_dci_decode
+ *   orc_find_dci         srslte_ue_dl_find_dl_dci(_type) then srslte_ue_dl_find_ul_dci
+ *                        (ue/ue_dl.c:768-932, the UL DCI a 1A search sets aside included) over
+ *                        srslte_pdcch_decode_msg (pdcch.c:366-420) = orc_dci_decode; pinned to the
+ *                        reference's ue_dl.c itself (oracle/_ref/ref_front)
  */
 #include <math.h>
 #include <stdint.h>
@@ -310,10 +312,18 @@ uint32_t orc_dci_sizeof(uint32_t format, uint32_t n, uint32_t nports) {
 
 static const uint32_t ORC_UE_FORMATS[8][2] = {{2, 1}, {2, 1}, {2, 7}, {2, 6}, {2, 5}, {2, 4}, {2, 1}, {2, 8}};
 
+/* the UL DCI a DL search set aside (ue_dl.c:785-792: format 0 found while searching 1A, first one) */
+typedef struct {
+  int set;
+  uint16_t rnti;
+  int32_t out5[5];
+  uint8_t data[128];
+} orc_pending_t;
+
 /* dci_blind_search (ue_dl.c:768-810) over one format and a candidate list: 1 found, 0 not, -1 the
  * reference's SRSLTE_ERROR (decode_msg refuses a location past nCCE 87) */
 static int orc_blind(const float *llr, const uint32_t *loc, uint32_t nloc, uint32_t format, uint32_t nbits,
-                     uint16_t rnti, int32_t *out5, uint8_t *data) {
+                     uint16_t rnti, int32_t *out5, uint8_t *data, orc_pending_t *pend) {
   uint8_t buf[160];
   for (uint32_t i = 0; i < nloc; i++) {
     const uint32_t L = loc[2 * i], c = loc[2 * i + 1];
@@ -321,7 +331,21 @@ static int orc_blind(const float *llr, const uint32_t *loc, uint32_t nloc, uint3
     uint16_t rem = 0;
     if (orc_dci_decode(llr + 72 * c, 72u << L, nbits, buf, &rem) != 1 || rem != rnti) continue;
     const uint32_t got = (format == 0 || format == 2) ? (buf[0] ? 2u : 0u) : format;
-    if (got != format) continue; /* format 0 while searching 1A: the pending UL DCI */
+    if (got == 0 && format == 2) { /* the UL DCI, kept for srslte_ue_dl_find_ul_dci */
+      if (pend && !pend->set) {
+        pend->set = 1;
+        pend->rnti = rem;
+        pend->out5[0] = 1;
+        pend->out5[1] = 0;
+        pend->out5[2] = (int32_t)L;
+        pend->out5[3] = (int32_t)c;
+        pend->out5[4] = (int32_t)nbits;
+        memset(pend->data, 0, 128);
+        memcpy(pend->data, buf, nbits + 16);
+      }
+      continue;
+    }
+    if (got != format) continue;
     out5[0] = 1;
     out5[1] = (int32_t)format;
     out5[2] = (int32_t)L;
@@ -334,39 +358,67 @@ static int orc_blind(const float *llr, const uint32_t *loc, uint32_t nloc, uint3
   return 0;
 }
 
-int orc_find_dl_dci(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
-                    uint32_t phich_res, uint32_t cfi, uint32_t sf_idx, const float *llr, uint16_t rnti,
-                    uint32_t tm, int rnti_type, int32_t *out5, uint8_t *data) {
+static void orc_none(int32_t *out5, int r) {
+  out5[0] = r < 0 ? -1 : 0;
+  out5[1] = -1;
+  out5[2] = out5[3] = out5[4] = 0;
+}
+
+/* srslte_ue_dl_find_dl_dci(_type) (rnti != 0) and then srslte_ue_dl_find_ul_dci (ul_rnti != 0,
+ * ue_dl.c:811-838) on one subframe's LLRs, in phch_worker's order (phch_worker.cc:548-806, 938-967) on a
+ * ue_dl object with no UL DCI pending from an earlier subframe. rnti 0: no DL search (out5 reports the
+ * reference's "RNTI not specified" error, -1). */
+int orc_find_dci(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res,
+                 uint32_t cfi, uint32_t sf_idx, const float *llr, uint16_t rnti, uint32_t tm, int rnti_type,
+                 uint16_t ul_rnti, int32_t *out5, uint8_t *data, int32_t *ul5, uint8_t *uldata) {
   uint32_t ncce, *idx = malloc(sizeof(uint32_t) * 36 * 110 * 4);
   if (orc_pdcch_map(nof_prb, cell_id, nof_ports, phich_len, phich_res, cfi, idx, &ncce) < 0 || tm > 7) {
     free(idx);
     return -1;
   }
   free(idx);
-  out5[0] = 0;
-  out5[1] = -1;
-  out5[2] = out5[3] = out5[4] = 0;
+  orc_none(out5, 0);
+  if (ul5) orc_none(ul5, 0);
+  orc_pending_t pend;
+  memset(&pend, 0, sizeof(pend));
   uint32_t ue[128], com[128];
   const uint32_t ncom = (uint32_t)orc_pdcch_locations(ncce, sf_idx, rnti, 1, com);
-  const int common = rnti_type < 0 ? (rnti == 0xFFFF || rnti == 0xFFFE || rnti <= 0x000A)
-                                   : (rnti_type == 1 || rnti_type == 2 || rnti_type == 5);
-  int r = 0;
-  if (common) {
-    const uint32_t f[2] = {2, 3}; /* 1A, 1C */
-    for (int i = 0; i < 2 && ncom && !r; i++)
-      r = orc_blind(llr, com, ncom, f[i], orc_dci_sizeof(f[i], nof_prb, nof_ports), rnti, out5, data);
-  } else {
-    const uint32_t nue = (uint32_t)orc_pdcch_locations(ncce, sf_idx, rnti, 0, ue);
-    for (int i = 0; i < 2 && !r; i++) {
-      const uint32_t f = ORC_UE_FORMATS[tm][i];
-      r = orc_blind(llr, ue, nue, f, orc_dci_sizeof(f, nof_prb, nof_ports), rnti, out5, data);
+  if (rnti) {
+    const int common = rnti_type < 0 ? (rnti == 0xFFFF || rnti == 0xFFFE || rnti <= 0x000A)
+                                     : (rnti_type == 1 || rnti_type == 2 || rnti_type == 5);
+    int r = 0;
+    if (common) {
+      const uint32_t f[2] = {2, 3}; /* 1A, 1C */
+      for (int i = 0; i < 2 && ncom && !r; i++)
+        r = orc_blind(llr, com, ncom, f[i], orc_dci_sizeof(f[i], nof_prb, nof_ports), rnti, out5, data, &pend);
+    } else {
+      const uint32_t nue = (uint32_t)orc_pdcch_locations(ncce, sf_idx, rnti, 0, ue);
+      for (int i = 0; i < 2 && !r; i++) {
+        const uint32_t f = ORC_UE_FORMATS[tm][i];
+        r = orc_blind(llr, ue, nue, f, orc_dci_sizeof(f, nof_prb, nof_ports), rnti, out5, data, &pend);
+      }
+      if (!r && ncom) r = orc_blind(llr, com, ncom, 2, orc_dci_sizeof(2, nof_prb, nof_ports), rnti, out5, data, &pend);
     }
-    if (!r && ncom) r = orc_blind(llr, com, ncom, 2, orc_dci_sizeof(2, nof_prb, nof_ports), rnti, out5, data);
+    if (r < 0) orc_none(out5, -1);
+  } else {
+    orc_none(out5, -1); /* dci_blind_search: "RNTI not specified" (ue_dl.c:805-807) */
   }
-  if (r < 0) {
-    out5[0] = -1;
-    out5[1] = -1;
-    out5[2] = out5[3] = out5[4] = 0;
+  if (ul5 && ul_rnti && cfi >= 1 && cfi <= 3) {
+    if (pend.set && pend.rnti == ul_rnti) { /* ue_dl.c:815-819 */
+      memcpy(ul5, pend.out5, sizeof(pend.out5));
+      memcpy(uldata, pend.data, 128);
+    } else {
+      const uint32_t nue = (uint32_t)orc_pdcch_locations(ncce, sf_idx, ul_rnti, 0, ue);
+      const int r = orc_blind(llr, ue, nue, 0, orc_dci_sizeof(0, nof_prb, nof_ports), ul_rnti, ul5, uldata, NULL);
+      if (r < 0) orc_none(ul5, -1);
+    }
   }
   return 0;
+}
+
+int orc_find_dl_dci(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                    uint32_t phich_res, uint32_t cfi, uint32_t sf_idx, const float *llr, uint16_t rnti,
+                    uint32_t tm, int rnti_type, int32_t *out5, uint8_t *data) {
+  return orc_find_dci(nof_prb, cell_id, nof_ports, phich_len, phich_res, cfi, sf_idx, llr, rnti, tm, rnti_type, 0,
+                      out5, data, NULL, NULL);
 }

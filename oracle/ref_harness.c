@@ -886,69 +886,51 @@ int ref_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32
   return r ? -1 : e;
 }
 
-/* ue_dl.c:768-923 (dci_blind_search, find_dl_dci_type_siprarnti / _crnti, the formats of
- * ue_dci_formats[tm] (tm 0..7) and common_formats; rnti_type < 0: from the RNTI value as
- * srslte_ue_dl_find_dl_dci, else srslte_ue_dl_find_dl_dci_type's), restated over the reference's
- * srslte_pdcch_decode_msg and location functions, on LLRs the caller puts in q->llr.
- * out5 = {found (1, 0, or -1 where the reference's search returns SRSLTE_ERROR: decode_msg refuses
- * a location past nCCE 87, dci.c:215-221), format, L, ncce, nof_bits}, data = the message buffer.
- * Returns 0, or -1 on a harness error. */
-static const srslte_dci_format_t ref_ue_formats[8][2] = {
-    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},  {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},
-    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2A}, {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2},
-    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1D}, {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1B},
-    {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1},  {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT2B}};
-static int ref_blind(srslte_pdcch_t *q, srslte_dci_location_t *loc, uint32_t nloc, srslte_dci_format_t f,
-                     uint16_t rnti, uint32_t cfi, srslte_dci_msg_t *msg, srslte_dci_location_t *found) {
-  uint16_t crc_rem = 0;
-  for (uint32_t i = 0; i < nloc; i++) {
-    if (srslte_pdcch_decode_msg(q, msg, &loc[i], f, cfi, &crc_rem)) return -1;
-    if (crc_rem == rnti) {
-      if (msg->format == SRSLTE_DCI_FORMAT0 && f == SRSLTE_DCI_FORMAT1A) continue; /* UL: pending */
-      if (msg->format == f) {
-        *found = loc[i];
-        return 1;
-      }
-    }
-  }
-  return 0;
-}
-int ref_find_dl_dci(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
-                    uint32_t phich_res, uint32_t cfi, uint32_t sf_idx, const float *llr, uint16_t rnti,
-                    uint32_t tm, int rnti_type, int32_t *out5, uint8_t *data) {
-  srslte_regs_t regs;
-  srslte_pdcch_t q;
-  if (ref_pdcch_rx(&regs, &q, nof_prb, cell_id, nof_ports, phich_len, phich_res, 1)) return -1;
-  memcpy(q.llr, llr, sizeof(float) * 72 * q.nof_cce[cfi - 1]);
+/* The DL / UL DCI blind searches (ue_dl.c:768-932) run from the reference's own ue_dl.c in
+ * oracle/ref_front.c (ue_dl.c reaches the DFT through ofdm.c, so it cannot be in this library). */
+
+/* srslte_dci_msg_pack_pusch (dci.c:511-569, format 0) from 8 fields: freq_hop_fl (-1 disabled, 0..3),
+ * L_crb, RB_start, mcs_idx, ndi, tpc_pusch, n_dmrs, cqi_request; returns nof_bits */
+int ref_dci_pack_ul(uint32_t nof_prb, const int32_t *f, uint8_t *bits) {
+  srslte_ra_ul_dci_t d;
+  memset(&d, 0, sizeof(d));
+  d.freq_hop_fl = f[0];
+  d.type2_alloc.L_crb = (uint32_t)f[1];
+  d.type2_alloc.RB_start = (uint32_t)f[2];
+  d.mcs_idx = (uint32_t)f[3];
+  d.ndi = f[4] != 0;
+  d.tpc_pusch = (uint8_t)f[5];
+  d.n_dmrs = (uint32_t)f[6];
+  d.cqi_request = f[7] != 0;
   srslte_dci_msg_t msg;
   memset(&msg, 0, sizeof(msg));
-  srslte_dci_location_t loc[64], found = {0, 0};
-  int r = 0;
-  const int common = rnti_type < 0 ? (rnti == SRSLTE_SIRNTI || rnti == SRSLTE_PRNTI || rnti <= SRSLTE_RARNTI_END)
-                                   : (rnti_type == SRSLTE_RNTI_SI || rnti_type == SRSLTE_RNTI_PCH ||
-                                      rnti_type == SRSLTE_RNTI_RAR);
-  if (common) {
-    const uint32_t n = srslte_pdcch_common_locations(&q, loc, 64, cfi);
-    const srslte_dci_format_t cf[2] = {SRSLTE_DCI_FORMAT1A, SRSLTE_DCI_FORMAT1C};
-    for (int f = 0; f < 2 && n > 0 && r == 0; f++) r = ref_blind(&q, loc, n, cf[f], rnti, cfi, &msg, &found);
-  } else {
-    uint32_t n = srslte_pdcch_ue_locations(&q, loc, 64, sf_idx, cfi, rnti);
-    for (int f = 0; f < 2 && r == 0; f++)
-      r = ref_blind(&q, loc, n, ref_ue_formats[tm][f], rnti, cfi, &msg, &found);
-    if (r == 0) {
-      n = srslte_pdcch_common_locations(&q, loc, 64, cfi);
-      if (n > 0) r = ref_blind(&q, loc, n, SRSLTE_DCI_FORMAT1A, rnti, cfi, &msg, &found);
-    }
-  }
-  out5[0] = r < 0 ? -1 : r > 0; /* -1: the search fails (srslte_pdcch_decode_msg refuses a location) */
-  out5[1] = r > 0 ? (int32_t)msg.format : -1;
-  out5[2] = (int32_t)found.L;
-  out5[3] = (int32_t)found.ncce;
-  out5[4] = r > 0 ? (int32_t)msg.nof_bits : 0;
-  if (r > 0) memcpy(data, msg.data, SRSLTE_DCI_MAX_BITS); /* the payload and, after it, the CRC bits */
-  srslte_pdcch_free(&q);
-  srslte_regs_free(&regs);
-  return 0;
+  if (srslte_dci_msg_pack_pusch(&d, &msg, nof_prb)) return -1;
+  memcpy(bits, msg.data, msg.nof_bits);
+  return (int)msg.nof_bits;
+}
+
+/* srslte_dci_msg_to_ul_grant (dci.c:165-197): dci11 = freq_hop_fl riv L_crb RB_start mcs_idx rv_idx
+ * n_dmrs ndi cqi_request tpc_pusch 0; grant10 = L_prb n_prb[0] n_prb[1] freq_hopping M_sc Qm mod tbs
+ * mcs.idx ncs_dmrs (the order of ref_front.c) */
+int ref_dci_to_ul_grant(const uint8_t *bits, uint32_t nof_bits, uint32_t nof_prb, uint32_t n_rb_ho,
+                        int32_t *dci11, int32_t *grant10) {
+  srslte_dci_msg_t msg;
+  memset(&msg, 0, sizeof(msg));
+  memcpy(msg.data, bits, SRSLTE_DCI_MAX_BITS);
+  msg.nof_bits = nof_bits;
+  msg.format = SRSLTE_DCI_FORMAT0;
+  srslte_ra_ul_dci_t d;
+  srslte_ra_ul_grant_t g;
+  const int r = srslte_dci_msg_to_ul_grant(&msg, nof_prb, n_rb_ho, &d, &g, 0);
+  const int32_t dv[11] = {(int32_t)d.freq_hop_fl, (int32_t)d.type2_alloc.riv, (int32_t)d.type2_alloc.L_crb,
+                          (int32_t)d.type2_alloc.RB_start, (int32_t)d.mcs_idx, (int32_t)d.rv_idx, (int32_t)d.n_dmrs,
+                          (int32_t)d.ndi, (int32_t)d.cqi_request, (int32_t)d.tpc_pusch, 0};
+  const int32_t gv[10] = {(int32_t)g.L_prb, (int32_t)g.n_prb[0], (int32_t)g.n_prb[1], (int32_t)g.freq_hopping,
+                          (int32_t)g.M_sc, (int32_t)g.Qm, (int32_t)g.mcs.mod, (int32_t)g.mcs.tbs,
+                          (int32_t)g.mcs.idx, (int32_t)g.ncs_dmrs};
+  memcpy(dci11, dv, sizeof(dv));
+  memcpy(grant10, gv, sizeof(gv));
+  return r;
 }
 
 /* bits: SRSLTE_DCI_MAX_BITS bytes as srslte_dci_msg_t.data holds them */

@@ -318,6 +318,107 @@ def have_ref():
     return os.path.exists(REF_SO)
 
 
+REF_FRONT = os.path.join(REPO, "oracle", "_ref", "ref_front")
+
+
+def have_ref_front():
+    return os.path.exists(REF_FRONT)
+
+
+def _run_ref_front(mode, payload):
+    """run oracle/_ref/ref_front (the reference's chest_dl.c / ue_dl.c, this container only) on one
+    request; -> the response bytes"""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fi, fo = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
+        with open(fi, "wb") as f:
+            f.write(payload)
+        r = subprocess.run([REF_FRONT, mode, fi, fo], capture_output=True, text=True)
+        assert r.returncode == 0, "ref_front %s failed (%d): %s" % (mode, r.returncode, r.stderr[-2000:])
+        with open(fo, "rb") as f:
+            return f.read()
+
+
+def ref_front_chest(nof_prb, cell_id, nports, nrx, sfs, grids, filt=(0.1, 0.8, 0.1), gauss=None,
+                    smooth_auto=False, average=False, noise_alg=0, rsrp_neighbour=True, cfo_enable=True,
+                    cfo_mask=0x3FF, noise_init=0.0):
+    """srslte_chest_dl_* of the reference on ONE estimator over the subframe sequence sfs; grids[i][a]
+    complex64 [14 * 12 nof_prb]. filt: explicit filter (srslte_chest_dl_set_smooth_filter), or
+    gauss=(order, std) for srslte_chest_dl_set_smooth_filter_gauss. -> list per subframe of dict(
+    noise_before [nrx][np], ce [nrx][np][n], noise / rsrp / rssi / rsrp_corr / cfo [nrx][np],
+    getters [noise, snr, rssi, rsrq, rsrp, rsrp_neighbour, cfo])"""
+    n = 14 * 12 * nof_prb
+    f = np.zeros(32, np.float32)
+    f[:len(filt)] = filt
+    head = np.array([nof_prb, cell_id, nports, nrx, len(sfs), 1 if gauss else 0, len(filt)], np.uint32).tobytes()
+    head += f.tobytes()
+    head += np.array([gauss[0] if gauss else 0], np.uint32).tobytes()
+    head += np.array([gauss[1] if gauss else 0.0], np.float32).tobytes()
+    head += np.array([int(smooth_auto), int(average), noise_alg, int(rsrp_neighbour), int(cfo_enable), cfo_mask],
+                     np.uint32).tobytes()
+    head += np.array([noise_init], np.float32).tobytes()
+    body = b"".join(np.array([sf], np.uint32).tobytes() +
+                    b"".join(np.ascontiguousarray(grids[i][a], np.complex64).tobytes() for a in range(nrx))
+                    for i, sf in enumerate(sfs))
+    raw = _run_ref_front("chest", head + body)
+    out, o, m = [], 0, nrx * nports
+    for _ in sfs:
+        nb = np.frombuffer(raw, np.float32, m, o).reshape(nrx, nports).copy()
+        o += 4 * m
+        ce = np.frombuffer(raw, np.complex64, m * n, o).reshape(nrx, nports, n).copy()
+        o += 8 * m * n
+        meas = np.frombuffer(raw, np.float32, 5 * m, o).reshape(nrx, nports, 5).copy()
+        o += 20 * m
+        get = np.frombuffer(raw, np.float32, 7, o).copy()
+        o += 28
+        out.append(dict(noise_before=nb, ce=ce, noise=meas[..., 0], rsrp=meas[..., 1], rssi=meas[..., 2],
+                        rsrp_corr=meas[..., 3], cfo=meas[..., 4], getters=get))
+    assert o == len(raw)
+    return out
+
+
+def ref_front_dci(nof_prb, cell_id, nports, nrx, phich_len, phich_res, subframes):
+    """srslte_pdcch_extract_llr_multi + srslte_ue_dl_find_dl_dci(_type) + srslte_ue_dl_find_ul_dci +
+    srslte_dci_msg_to_ul_grant of the reference (ue_dl.c on ONE srslte_ue_dl_t, in phch_worker's order)
+    over a subframe sequence. subframes: dicts with sf_idx, cfi, noise, rnti, tm, rnti_type, ul_rnti
+    (0: no UL search), n_rb_ho, y [nrx] and h [nports][nrx] (complex64, zero-padded to 14 * 12 nof_prb).
+    -> per subframe dict(llr, dl=(found, format, L, ncce, nof_bits, buf), ul=(...), ul_grant=(ret,
+    dci 11 fields, grant 10 fields), pending)"""
+    n = 14 * 12 * nof_prb
+    pad = lambda a: np.concatenate([np.asarray(a, np.complex64), np.zeros(n - len(a), np.complex64)])
+    pay = np.array([nof_prb, cell_id, nports, nrx, phich_len, phich_res, len(subframes)], np.uint32).tobytes()
+    for s in subframes:
+        pay += np.array([s["sf_idx"], s["cfi"]], np.uint32).tobytes()
+        pay += np.array([s["noise"]], np.float32).tobytes()
+        pay += np.array([s["rnti"], s["tm"], s["rnti_type"], s.get("ul_rnti", 0), s.get("n_rb_ho", 0)],
+                        np.int64).astype(np.uint32).tobytes()
+        pay += b"".join(pad(s["y"][a]).tobytes() for a in range(nrx))
+        pay += b"".join(pad(s["h"][p][a]).tobytes() for p in range(nports) for a in range(nrx))
+    raw = _run_ref_front("dci", pay)
+    out, o = [], 0
+
+    def msg():
+        nonlocal o
+        v = np.frombuffer(raw, np.int32, 5, o)
+        o += 20
+        buf = np.frombuffer(raw, np.uint8, 128, o).copy()
+        o += 128
+        return (int(v[0]), int(v[1]), int(v[2]), int(v[3]), int(v[4]), buf if v[0] > 0 else buf[:0])
+
+    for _ in subframes:
+        nl = int(np.frombuffer(raw, np.int32, 1, o)[0])
+        o += 4
+        llr = np.frombuffer(raw, np.float32, nl, o).copy()
+        o += 4 * nl
+        dl, ul = msg(), msg()
+        g = np.frombuffer(raw, np.int32, 23, o).copy()
+        o += 92
+        out.append(dict(llr=llr, dl=dl, ul=ul, ul_grant=(int(g[0]), g[1:12], g[12:22]), pending=int(g[22])))
+    assert o == len(raw)
+    return out
+
+
 # ------------------------------------------------------------------ synthetic data ----
 
 def cb_sizes():
@@ -712,7 +813,10 @@ def pdcch_map(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, ref=Fals
 
 def pdcch_encode(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, msgs):
     """srslte_pdcch_encode of msgs [(bits, L, ncce, rnti)] -> port grids complex64 [nports][14 * 12 nof_prb]
-    (reference build only)"""
+    (reference build only). The reference cannot encode a message whose E = 72 * 2^L is not below
+    q->max_bits = 72 NOF_CCE(3) (pdcch.c:548): srslte_pdcch_dci_encode then returns an error that
+    srslte_pdcch_encode ignores, and uninitialised bits go out. Callers avoid such locations
+    (pdcch_encodable); the result is checked to be finite."""
     f = _L(lib).ref_pdcch_encode
     f.argtypes = [ctypes.c_uint32] * 8 + [_u8p, _u32p, _u32p, _u32p, _u16p, _f32p, _f32p]
     n = 14 * 12 * nof_prb
@@ -727,7 +831,14 @@ def pdcch_encode(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_id
     assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, len(msgs), _ptr(bits, _u8p),
              _ptr(nb, _u32p), _ptr(Ls, _u32p), _ptr(nc, _u32p), _ptr(rn, _u16p), _pf(grids[0]),
              _pf(grids[1])) == 0
+    assert all(np.isfinite(g).all() for g in grids), "the reference PDCCH encoder sent uninitialised bits"
     return grids[:nports]
+
+
+def pdcch_encodable(lib, nof_prb, cell_id, nports, phich_len, phich_res, L):
+    """whether the reference's srslte_pdcch_encode can encode aggregation level L in this cell
+    (72 * 2^L < q->max_bits = 72 NOF_CCE(3), pdcch.c:193, :548)"""
+    return (1 << L) < pdcch_map(lib, nof_prb, cell_id, nports, phich_len, phich_res, 3, ref=True)[1]
 
 
 def pdcch_llr(lib, nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_idx, noise, y, h, ref=False):
@@ -747,19 +858,77 @@ def pdcch_llr(lib, nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_
     return llr[:e].copy()
 
 
+def find_dci(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, llr, rnti, tm, rnti_type=-1,
+             ul_rnti=0):
+    """the oracle's srslte_ue_dl_find_dl_dci (rnti != 0) then srslte_ue_dl_find_ul_dci (ul_rnti != 0) on LLRs
+    -> (dl, ul), each (found, format, L, ncce, nof_bits, buf): buf is the message buffer (128 bytes: the
+    payload, then the 16 CRC bits) when found, else empty"""
+    f = _L(lib).orc_find_dci
+    f.argtypes = [ctypes.c_uint32] * 7 + [_f32p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint16,
+                                          _i32p, _u8p, _i32p, _u8p]
+    llr = np.ascontiguousarray(llr, np.float32)
+    o1, o2 = np.zeros(5, np.int32), np.zeros(5, np.int32)
+    d1, d2 = np.zeros(128, np.uint8), np.zeros(128, np.uint8)
+    assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, _pf(llr), rnti, tm, rnti_type, ul_rnti,
+             _ptr(o1, _i32p), _ptr(d1, _u8p), _ptr(o2, _i32p), _ptr(d2, _u8p)) == 0
+    tup = lambda o, d: (int(o[0]), int(o[1]), int(o[2]), int(o[3]), int(o[4]), d.copy() if o[0] > 0 else d[:0].copy())
+    return tup(o1, d1), tup(o2, d2)
+
+
 def find_dl_dci(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, llr, rnti, tm,
                 rnti_type=-1, ref=False):
-    """the srslte_ue_dl_find_dl_dci blind search on LLRs -> (found, format, L, ncce, nof_bits, buf): buf is
-    the message buffer (128 bytes: the payload, then the 16 CRC bits) when found, else empty"""
-    f = getattr(_L(lib), "ref_find_dl_dci" if ref else "orc_find_dl_dci")
-    f.argtypes = [ctypes.c_uint32] * 7 + [_f32p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_int, _i32p, _u8p]
-    llr = np.ascontiguousarray(llr, np.float32)
-    out = np.zeros(5, np.int32)
-    data = np.zeros(128, np.uint8)
-    assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, _pf(llr), rnti, tm, rnti_type,
-             _ptr(out, _i32p), _ptr(data, _u8p)) == 0
-    return (int(out[0]), int(out[1]), int(out[2]), int(out[3]), int(out[4]),
-            data.copy() if out[0] > 0 else data[:0].copy())
+    """the oracle's srslte_ue_dl_find_dl_dci blind search on LLRs -> (found, format, L, ncce, nof_bits, buf).
+    The reference's own search runs from grids: find_dci_ref."""
+    assert not ref, "the reference search is ue_dl.c in oracle/_ref/ref_front: use find_dci_ref"
+    return find_dci(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, llr, rnti, tm, rnti_type)[0]
+
+
+def find_dci_ref(nof_prb, cell_id, nports, nrx, phich_len, phich_res, cfi, sf_idx, noise, y, h, searches):
+    """the reference's ue_dl.c (oracle/_ref/ref_front): srslte_pdcch_extract_llr_multi of y / h, then per
+    search (rnti, tm, rnti_type, ul_rnti) srslte_ue_dl_find_dl_dci(_type) and srslte_ue_dl_find_ul_dci.
+    -> (llr, [(dl, ul, ul_grant)]) with dl / ul as find_dci returns them"""
+    sfs = [dict(sf_idx=sf_idx, cfi=cfi, noise=noise, rnti=r, tm=t, rnti_type=rt, ul_rnti=u, y=y, h=h)
+           for r, t, rt, u in searches]
+    res = ref_front_dci(nof_prb, cell_id, nports, nrx, phich_len, phich_res, sfs)
+    for x in res:
+        assert np.array_equal(x["llr"].view(np.uint32), res[0]["llr"].view(np.uint32))
+    return res[0]["llr"], [(x["dl"], x["ul"], x["ul_grant"]) for x in res]
+
+
+def dci_pack_ul_ref(lib, nof_prb, fields):
+    """srslte_dci_msg_pack_pusch (format 0) of 8 fields (freq_hop_fl, L_crb, RB_start, mcs, ndi, tpc, n_dmrs,
+    cqi_request) -> bits, or None"""
+    f = _L(lib).ref_dci_pack_ul
+    f.argtypes = [ctypes.c_uint32, _i32p, _u8p]
+    fl = np.asarray(fields, np.int32)
+    b = np.zeros(128, np.uint8)
+    n = f(nof_prb, _ptr(fl, _i32p), _ptr(b, _u8p))
+    return None if n < 0 else b[:n].copy()
+
+
+def dci_to_ul_grant_ref(lib, bits, nof_prb, n_rb_ho=0, nof_bits=None):
+    """srslte_dci_msg_to_ul_grant -> (ret, dci 11 fields, grant 10 fields) (ref_front.c's order)"""
+    f = _L(lib).ref_dci_to_ul_grant
+    f.argtypes = [_u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _i32p, _i32p]
+    b = np.zeros(128, np.uint8)
+    b[:len(bits)] = bits
+    d, g = np.zeros(11, np.int32), np.zeros(10, np.int32)
+    r = f(_ptr(b, _u8p), len(bits) if nof_bits is None else nof_bits, nof_prb, n_rb_ho, _ptr(d, _i32p),
+          _ptr(g, _i32p))
+    return r, d, g
+
+
+def random_ul_msg(ref, rng, nof_prb, hop_p=0.2):
+    """a format 0 DCI packed by the reference from random fields (hopping with probability hop_p)"""
+    for _ in range(40):
+        L = int(rng.integers(1, nof_prb + 1))
+        hop = int(rng.integers(0, 4)) if rng.random() < hop_p else -1
+        fields = [hop, L, int(rng.integers(0, nof_prb - L + 1)), int(rng.integers(0, 32)), int(rng.integers(0, 2)),
+                  int(rng.integers(0, 4)), int(rng.integers(0, 8)), int(rng.integers(0, 2))]
+        b = dci_pack_ul_ref(ref, nof_prb, fields)
+        if b is not None:
+            return b
+    raise AssertionError("no format 0 message")
 
 
 def pdcch_locations(lib, nof_cce, sf_idx, rnti, common, ref=True):
@@ -864,15 +1033,18 @@ def pdcch_subframe(ref, rng, nof_prb, cell_id, nports, nrx, phich_len, phich_res
     C-RNTI in its UE-specific space (the tm's formats, sometimes a format 0 look-alike before it) and
     for SI- / RA-RNTIs in the common space, through a flat per-(port, antenna) channel with small
     per-RE ripple and AWGN. Returns (y[nrx], h[nports][nrx] over the 4 leading symbols, searches
-    [(rnti, tm, rnti_type)], noise estimate)."""
+    [(rnti, tm, rnti_type, ul_rnti)], noise estimate)."""
     idx, ncce = pdcch_map(ref, nof_prb, cell_id, nports, phich_len, phich_res, cfi, ref=True)
     used = np.zeros(max(ncce, 1), bool)
     msgs = []
 
+    ncce3 = pdcch_map(ref, nof_prb, cell_id, nports, phich_len, phich_res, 3, ref=True)[1]
+
     def place(locs, bits, rnti):
         rng.shuffle(locs)
         for L, c in locs:
-            if c <= 87 and not used[c:c + (1 << L)].any():  # srslte_dci_location_isvalid
+            # srslte_dci_location_isvalid, and a level the reference's encoder can encode (pdcch_encode)
+            if c <= 87 and (1 << L) < ncce3 and not used[c:c + (1 << L)].any():
                 used[c:c + (1 << L)] = True
                 msgs.append((bits, L, c, rnti))
                 return True
@@ -881,9 +1053,12 @@ def pdcch_subframe(ref, rng, nof_prb, cell_id, nports, nrx, phich_len, phich_res
     crnti = int(rng.integers(0x000B, 0xFFF4))
     ue = pdcch_locations(ref, ncce, sf_idx, crnti, False)
     com = pdcch_locations(ref, ncce, sf_idx, 0, True)
-    if ue and rng.random() < 0.3:  # a UL grant (format 0 shares 1A's size) the DL search passes over
-        b = rng.integers(0, 2, dci_sizeof_ref(ref, F0, nof_prb, nports)).astype(np.uint8)
-        b[0] = 0
+    if ue and rng.random() < 0.4:  # a UL grant (format 0 shares 1A's size): the DL search sets it aside
+        if rng.random() < 0.5:
+            b = random_ul_msg(ref, rng, nof_prb)
+        else:
+            b = rng.integers(0, 2, dci_sizeof_ref(ref, F0, nof_prb, nports)).astype(np.uint8)
+            b[0] = 0
         place(list(ue), b, crnti)
     if ue and rng.random() < 0.9:
         fmt = UE_FORMATS[tm][int(rng.integers(0, 2))]
@@ -911,7 +1086,9 @@ def pdcch_subframe(ref, rng, nof_prb, cell_id, nports, nrx, phich_len, phich_res
             acc += h[p][a] * x[p][:n4]
         acc += (sigma * (rng.standard_normal(n4) + 1j * rng.standard_normal(n4))).astype(np.complex64)
         y.append(acc.astype(np.complex64))
-    searches = [(crnti, tm, -1), (si, tm, -1), (rarnti, tm, -1), (int(rng.integers(0x000B, 0xFFF4)), tm, -1),
-                (si, tm, 1), (crnti, tm, 0)]
+    # (DL rnti, tm, rnti_type, UL rnti): phch_worker's DL search, then its UL search for the C-RNTI
+    searches = [(crnti, tm, -1, crnti), (si, tm, -1, crnti), (rarnti, tm, -1, 0),
+                (int(rng.integers(0x000B, 0xFFF4)), tm, -1, crnti), (si, tm, 1, 0), (crnti, tm, 0, crnti),
+                (crnti, tm, -1, 0)]
     noise = float(2 * sigma * sigma) if rng.random() < 0.7 else 0.0
     return y, h, searches, noise

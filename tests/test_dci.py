@@ -90,3 +90,53 @@ def test_random_messages_vs_reference(nof_prb):
                 _check(bits, fmt, rnti, nof_prb, nports, ret, d, g, p, (fmt, nports, k))
                 n += ret == 0
     assert n > 100
+
+
+def _check_ul(bits, nof_prb, n_rb_ho, ret, dci, grant, what, nof_bits=None):
+    r, d, g = s.dci_msg_to_ul_grant(bits, nof_prb, n_rb_ho, nof_bits)
+    assert r == ret, (what, r, ret)
+    assert d.fields11() == list(dci), (what, d.fields11(), list(dci))
+    if ret == 0:
+        assert g.fields10() == list(grant), (what, g.fields10(), list(grant))
+
+
+def test_golden_ul_grants(gold):
+    """srsgpu_dci_msg_to_ul_grant against the reference's srslte_dci_msg_to_ul_grant (dci.c:165-197):
+    format 0 messages the reference packed and the UL DCIs its ue_dl.c search found, with and without a
+    PUSCH hopping offset"""
+    z, man = gold
+    gs = man["ul_grants"]
+    assert len(gs) >= 150 and sum(g["ret"] == 0 for g in gs) >= 100
+    assert {g["dci"][0] for g in gs} >= {-1, 0, 1, 2, 3}  # every hopping kind
+    for g in gs:
+        _check_ul(z[g["key"] + "_bits"], g["nof_prb"], g["n_rb_ho"], g["ret"], g["dci"], g["grant"], g["key"])
+    # the grants of the UL searches of the recorded subframes (as ue_dl.c's caller unpacks them)
+    n = 0
+    for c in man["cases"]:
+        for j, r in enumerate(c["searches"]):
+            if r["ul_found"] > 0:
+                b = z["%s_s%d_ulbits" % (c["key"], j)][:r["ul_nof_bits"]]
+                _check_ul(b, c["nof_prb"], 0, r["ul_grant_ret"], r["ul_dci"], r["ul_grant"], (c["key"], j))
+                n += 1
+    assert n >= 30
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
+def test_ul_grants_vs_reference():
+    """random reference-packed and random-bit format 0 messages of every bandwidth and hopping offset"""
+    from srsgpu_testlib import dci_to_ul_grant_ref, random_ul_msg
+    ref = Ref()
+    rng = np.random.default_rng(5)
+    for nof_prb in list(range(6, 111, 7)) + [100, 110]:
+        for k in range(8):
+            if k < 5:
+                b = random_ul_msg(ref, rng, nof_prb)
+            else:
+                b = rng.integers(0, 2, s.dci_format_sizeof(0, nof_prb, 1)).astype(np.uint8)
+                b[0] = int(k == 7)  # a 1A look-alike is refused
+            for n_rb_ho in (0, 3, int(rng.integers(0, nof_prb // 2 + 1))):
+                r, d, g = dci_to_ul_grant_ref(ref, b, nof_prb, n_rb_ho)
+                _check_ul(b, nof_prb, n_rb_ho, r, d, g, (nof_prb, k, n_rb_ho))
+    # wrong length: refused
+    r, _, _ = s.dci_msg_to_ul_grant(np.zeros(10, np.uint8), 50)
+    assert r == -1

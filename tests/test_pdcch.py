@@ -7,10 +7,11 @@ include/srsgpu/pdcch_batch.h):
   - srsgpu_pdcch_extract_llr_dev against srslte_pdcch_extract_llr_multi (pdcch.c:424-506), bit-exact
     in every float LLR, one subframe per launch and many subframes of mixed CFI / subframe index /
     noise estimate per launch (GPU);
-  - srsgpu_pdcch_find_dl_dci_dev against the srslte_ue_dl_find_dl_dci blind search (ue_dl.c:768-923)
-    over the reference's srslte_pdcch_decode_msg: found / format / location / message buffer, for C-,
-    SI- and RA-RNTIs, absent RNTIs, explicit RNTI types, format-0 look-alikes, and the found message
-    through srsgpu_dci_msg_to_dl_grant (GPU)."""
+  - srsgpu_pdcch_find_dci_dev against the reference's own ue_dl.c (oracle/_ref/ref_front):
+    srslte_ue_dl_find_dl_dci(_type) then srslte_ue_dl_find_ul_dci (ue_dl.c:768-932, phch_worker's
+    order): found / format / location / message buffer of both searches, for C-, SI- and RA-RNTIs,
+    absent RNTIs, explicit RNTI types, format 0 set aside by the 1A search and taken by the UL search,
+    and the found messages through srsgpu_dci_msg_to_dl_grant / _ul_grant (GPU)."""
 import json
 import os
 
@@ -18,8 +19,8 @@ import numpy as np
 import pytest
 
 import srsgpu_phy as s
-from srsgpu_testlib import (Ref, dci_to_dl_grant_ref, find_dl_dci, have_ref, pdcch_llr, pdcch_locations,
-                            pdcch_map, pdcch_subframe)
+from srsgpu_testlib import (Ref, dci_to_dl_grant_ref, find_dci_ref, have_ref, have_ref_front, pdcch_llr,
+                            pdcch_locations, pdcch_map, pdcch_subframe)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LLR_STRIDE = 72 * 128  # per-subframe LLR slots (NOF_CCE reaches 96 at 110 PRB)
@@ -120,11 +121,25 @@ class _Dev:
 
 
 def _search_gpu(torch, q, searches, d_llr):
-    """searches: [(llr_offset, sf_idx, cfi, rnti, tm, rnti_type)] -> parsed results"""
+    """searches: [(llr_offset, sf_idx, cfi, rnti, tm, rnti_type, ul_rnti)] -> [(dl, ul)] parsed results"""
     res = torch.zeros(len(searches) * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
-    assert q.find_dl_dci_dev(searches, d_llr, res.data_ptr()) == 0
+    ul = torch.zeros(len(searches) * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
+    assert q.find_dci_dev(searches, d_llr, res.data_ptr(), ul.data_ptr()) == 0
     torch.cuda.synchronize()
-    return s.Pdcch.parse_results(res.cpu().numpy().tobytes())
+    return list(zip(s.Pdcch.parse_results(res.cpu().numpy().tobytes()),
+                    s.Pdcch.parse_results(ul.cpu().numpy().tobytes())))
+
+
+def _ul_want(r, z, key, j):
+    return dict(found=r["ul_found"], format=r["ul_format"], L=r["ul_L"], ncce=r["ul_ncce"], nof_bits=r["ul_nof_bits"],
+                bits=z["%s_s%d_ulbits" % (key, j)])
+
+
+def _check_ul_grant(got, r, nof_prb, what):
+    """a found UL DCI unpacked as phch_worker does (srslte_dci_msg_to_ul_grant, hopping offset 0)"""
+    ret, d, g = s.dci_msg_to_ul_grant(got[4], nof_prb, 0, r["ul_nof_bits"])
+    assert ret == r["ul_grant_ret"] and d.fields11() == r["ul_dci"], what
+    assert ret or g.fields10() == r["ul_grant"], what
 
 
 def _same_result(got, want, what):
@@ -144,7 +159,7 @@ def test_gpu_golden_subframes(gold):
     z, man = gold
     grants = {(g["format"], g["rnti"], g["nof_prb"], g["nports"], z[g["key"] + "_bits"].tobytes()): g
               for g in man["grants"]}
-    nfound = 0
+    nfound = nul = 0
     for c in man["cases"]:
         if c["group"] == "batch":
             continue
@@ -159,18 +174,22 @@ def test_gpu_golden_subframes(gold):
         got = dev.llr[:want.size].cpu().numpy()
         assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), c["key"]
         assert torch.isnan(dev.llr[want.size:]).all()  # nothing written past NOF_CCE(cfi)
-        srch = [(0, c["sf_idx"], c["cfi"], r["rnti"], r["tm"], r["rnti_type"]) for r in c["searches"]]
+        srch = [(0, c["sf_idx"], c["cfi"], r["rnti"], r["tm"], r["rnti_type"], r["ul_rnti"]) for r in c["searches"]]
         res = _search_gpu(torch, q, srch, dev.llr.data_ptr())
-        for j, (r, got) in enumerate(zip(c["searches"], res)):
+        for j, (r, (got, gul)) in enumerate(zip(c["searches"], res)):
             want = dict(r, bits=z["%s_s%d_bits" % (c["key"], j)])
             _same_result(got, want, (c["key"], j))
+            _same_result(gul, _ul_want(r, z, c["key"], j), (c["key"], j, "UL"))
+            if gul[0] > 0:
+                nul += 1
+                _check_ul_grant(gul, r, c["nof_prb"], (c["key"], j))
             if got[0] > 0:
                 nfound += 1
                 g = grants[(r["format"], r["rnti"], c["nof_prb"], c["nports"], want["bits"].tobytes())]
                 ret, d, gr = s.dci_msg_to_dl_grant(got[4], got[1], r["rnti"], c["nof_prb"], c["nports"],
                                                    r["nof_bits"])
                 assert ret == g["ret"] and (ret or d.fields30() == g["dci"]), (c["key"], j)
-    assert nfound >= 50
+    assert nfound >= 50 and nul >= 25
 
 
 @pytest.mark.gpu
@@ -190,19 +209,20 @@ def test_gpu_golden_batch(gold):
     srch, want = [], []
     for i, c in enumerate(cs):
         for j, r in enumerate(c["searches"]):
-            srch.append((i * LLR_STRIDE, c["sf_idx"], c["cfi"], r["rnti"], r["tm"], r["rnti_type"]))
-            want.append((dict(r, bits=z["%s_s%d_bits" % (c["key"], j)]), (c["key"], j)))
+            srch.append((i * LLR_STRIDE, c["sf_idx"], c["cfi"], r["rnti"], r["tm"], r["rnti_type"], r["ul_rnti"]))
+            want.append((dict(r, bits=z["%s_s%d_bits" % (c["key"], j)]), _ul_want(r, z, c["key"], j), (c["key"], j)))
     res = _search_gpu(torch, q, srch, dev.llr.data_ptr())
     llr = dev.llr.cpu().numpy()
     for i, c in enumerate(cs):
         w = z[c["key"] + "_llr"]
         assert np.array_equal(llr[i * LLR_STRIDE:i * LLR_STRIDE + w.size].view(np.uint32), w.view(np.uint32)), c["key"]
-    for got, (w, what) in zip(res, want):
+    for (got, gul), (w, wu, what) in zip(res, want):
         _same_result(got, w, what)
+        _same_result(gul, wu, what + ("UL",))
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
+@pytest.mark.skipif(not (have_ref() and have_ref_front()), reason="oracle/_ref not built")
 @pytest.mark.parametrize("nof_prb,nports,nrx", [(6, 1, 1), (9, 2, 2), (10, 1, 2), (15, 2, 1), (25, 1, 2), (50, 2, 2), (75, 1, 1),
                                                 (100, 2, 2), (110, 2, 1)])
 def test_gpu_random_vs_reference(nof_prb, nports, nrx):
@@ -230,30 +250,38 @@ def test_gpu_random_vs_reference(nof_prb, nports, nrx):
         assert q.extract_llr_dev(sfs, dev.g.data_ptr(), dev.c.data_ptr(), dev.stride, dev.llr.data_ptr()) == 0
     bufs = []
     for lo, hi in ((0, half), (half, 40)):
-        srch = [(i * LLR_STRIDE, meta[i][1], meta[i][0], r, t, rt) for i in range(lo, hi) for (r, t, rt) in meta[i][3]]
+        srch = [(i * LLR_STRIDE, meta[i][1], meta[i][0], r, t, rt, u) for i in range(lo, hi)
+                for (r, t, rt, u) in meta[i][3]]
         res = torch.zeros(len(srch) * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
-        assert q.find_dl_dci_dev(srch, dev.llr.data_ptr(), res.data_ptr()) == 0
-        bufs.append((srch, res))
+        rul = torch.zeros(len(srch) * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
+        assert q.find_dci_dev(srch, dev.llr.data_ptr(), res.data_ptr(), rul.data_ptr()) == 0
+        bufs.append((srch, res, rul))
     torch.cuda.synchronize()
-    for srch, res in bufs:
-        results += list(zip(srch, s.Pdcch.parse_results(res.cpu().numpy().tobytes())))
+    for srch, res, rul in bufs:
+        results += list(zip(srch, s.Pdcch.parse_results(res.cpu().numpy().tobytes()),
+                            s.Pdcch.parse_results(rul.cpu().numpy().tobytes())))
     llr = dev.llr.cpu().numpy()
-    nfound = 0
+    nfound = nul = 0
     k = 0
     for i, (cfi, sf_idx, noise, searches, y, h) in enumerate(meta):
-        w = pdcch_llr(ref, nof_prb, cell_id, nports, pl, pr, nrx, cfi, sf_idx, noise, y, h, ref=True)
+        w, found = find_dci_ref(nof_prb, cell_id, nports, nrx, pl, pr, cfi, sf_idx, noise, y, h, searches)
         assert np.array_equal(llr[i * LLR_STRIDE:i * LLR_STRIDE + w.size].view(np.uint32), w.view(np.uint32)), i
-        for (rnti, tm, rt) in searches:
-            f, fmt, L, ncce, nb, buf = find_dl_dci(ref, nof_prb, cell_id, nports, pl, pr, cfi, sf_idx, w, rnti, tm,
-                                                   rt, ref=True)
+        for (rnti, tm, rt, ur), (dl, ul, ulg) in zip(searches, found):
+            f, fmt, L, ncce, nb, buf = dl
             _same_result(results[k][1], dict(found=f, format=fmt, L=L, ncce=ncce, nof_bits=nb, bits=buf), (i, rnti))
+            _same_result(results[k][2], dict(found=ul[0], format=ul[1], L=ul[2], ncce=ul[3], nof_bits=ul[4],
+                                             bits=ul[5]), (i, rnti, "UL"))
+            if ul[0] > 0:
+                nul += 1
+                a = s.dci_msg_to_ul_grant(ul[5], nof_prb, 0, ul[4])
+                assert a[0] == ulg[0] and a[1].fields11() == list(ulg[1]), (i, ur)
             if f > 0:
                 nfound += 1
                 a = s.dci_msg_to_dl_grant(buf, fmt, rnti, nof_prb, nports, nb)
                 b = dci_to_dl_grant_ref(ref, buf, fmt, rnti, nof_prb, nports, nof_bits=nb)
                 assert a[0] == b[0] and (a[0] or a[1].fields30() == list(b[1])), (i, rnti)
             k += 1
-    assert nfound >= 20
+    assert nfound >= 20 and nul >= 5
 
 
 @pytest.mark.gpu
@@ -273,4 +301,11 @@ def test_gpu_invalid_requests():
                 (0, 0, 1, 0x1234, 0, 7)]:
         assert q.find_dl_dci_dev([bad], p, res.data_ptr()) == -1, bad
     assert q.find_dl_dci_dev([], p, res.data_ptr()) == 0
+    ul = torch.zeros(4 * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
+    assert q.find_dci_dev([(0, 0, 1, 0, 0, -1, 0)], p, res.data_ptr(), ul.data_ptr()) == -1  # no search at all
+    assert q.find_dci_dev([(0, 0, 1, 0x1234, 0, -1, 0x10000)], p, res.data_ptr(), ul.data_ptr()) == -1
+    # a UL search alone: the DL result reports the reference's "RNTI not specified" error
+    p0 = torch.zeros(72 * 128, dtype=torch.float32, device="cuda")
+    got = _search_gpu(torch, q, [(0, 3, 2, 0, 0, -1, 0x4321)], p0.data_ptr())
+    assert got[0][0][0] == -1 and got[0][1][0] == 0
     torch.cuda.synchronize()

@@ -1,15 +1,16 @@
-"""The PDCCH oracle (oracle/pdcch_oracle.c: REG map, LLR extraction, candidate locations and the DL
-blind search, restated in scalar C) against the golden receptions recorded from the reference build
-(tests/golden/make_pdcch_golden.py) and, with oracle/_ref, against the reference on random cells and
-subframes. CPU only: this pins the checker the GPU tests can fall back on."""
+"""The PDCCH oracle (oracle/pdcch_oracle.c: REG map, LLR extraction, candidate locations, the DL blind
+search and the UL (format 0) search after it, restated in scalar C) against the golden receptions recorded
+from the reference build and its own ue_dl.c (tests/golden/make_pdcch_golden.py, oracle/_ref/ref_front)
+and, with oracle/_ref, against the reference on random cells and subframes. CPU only: this pins the
+checker the GPU tests can fall back on."""
 import json
 import os
 
 import numpy as np
 import pytest
 
-from srsgpu_testlib import (Ref, find_dl_dci, have_ref, pdcch_llr, pdcch_locations, pdcch_map,
-                            pdcch_subframe)
+from srsgpu_testlib import (Ref, find_dci, find_dci_ref, have_ref, have_ref_front, pdcch_llr, pdcch_locations,
+                            pdcch_map, pdcch_subframe)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -30,7 +31,7 @@ def test_golden_maps(oracle, gold):
 
 def test_golden_llrs_and_searches(oracle, gold):
     z, man = gold
-    nfound = nref = 0
+    nfound = nref = nul = 0
     for c in man["cases"]:
         y = [z["%s_y%d" % (c["key"], a)] for a in range(c["nrx"])]
         h = [[z["%s_h%d%d" % (c["key"], p, a)] for a in range(c["nrx"])] for p in range(c["nports"])]
@@ -39,8 +40,9 @@ def test_golden_llrs_and_searches(oracle, gold):
         want = z[c["key"] + "_llr"]
         assert np.array_equal(llr.view(np.uint32), want.view(np.uint32)), c["key"]
         for j, r in enumerate(c["searches"]):
-            f, fmt, L, ncce, nb, buf = find_dl_dci(oracle, *args, c["cfi"], c["sf_idx"], llr, r["rnti"], r["tm"],
-                                                   r["rnti_type"])
+            dl, ul = find_dci(oracle, *args, c["cfi"], c["sf_idx"], llr, r["rnti"], r["tm"], r["rnti_type"],
+                              r["ul_rnti"])
+            f, fmt, L, ncce, nb, buf = dl
             assert f == r["found"], (c["key"], j)
             if f > 0:
                 nfound += 1
@@ -48,10 +50,16 @@ def test_golden_llrs_and_searches(oracle, gold):
                 # the payload and CRC bits; past them the reference's buffer holds earlier candidates' bits
                 assert np.array_equal(buf[:nb + 16], z["%s_s%d_bits" % (c["key"], j)][:nb + 16]), (c["key"], j)
             nref += f < 0
-    assert nfound >= 60 and nref >= 4
+            f, fmt, L, ncce, nb, buf = ul
+            assert f == r["ul_found"], (c["key"], j, "UL")
+            if f > 0:
+                nul += 1
+                assert (fmt, L, ncce, nb) == (r["ul_format"], r["ul_L"], r["ul_ncce"], r["ul_nof_bits"]), (c["key"], j)
+                assert np.array_equal(buf[:nb + 16], z["%s_s%d_ulbits" % (c["key"], j)][:nb + 16]), (c["key"], j)
+    assert nfound >= 60 and nref >= 4 and nul >= 30
 
 
-@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
+@pytest.mark.skipif(not (have_ref() and have_ref_front()), reason="oracle/_ref not built")
 def test_random_vs_reference(oracle):
     ref = Ref()
     rng = np.random.default_rng(77)
@@ -73,10 +81,10 @@ def test_random_vs_reference(oracle):
                                                    snr_db=float(rng.choice([4.0, 15.0])))
             args = (nof_prb, cell_id, nports, pl, pr)
             la = pdcch_llr(oracle, *args, nrx, cfi, sf, noise, y, h)
-            lb = pdcch_llr(ref, *args, nrx, cfi, sf, noise, y, h, ref=True)
+            lb, found = find_dci_ref(nof_prb, cell_id, nports, nrx, pl, pr, cfi, sf, noise, y, h, searches)
             assert np.array_equal(la.view(np.uint32), lb.view(np.uint32)), (nof_prb, k)
-            for rnti, t, rt in searches:
-                ra = find_dl_dci(oracle, *args, cfi, sf, la, rnti, t, rt)
-                rb = find_dl_dci(ref, *args, cfi, sf, lb, rnti, t, rt, ref=True)
-                nb = ra[4]
-                assert ra[:5] == rb[:5] and np.array_equal(ra[5][:nb + 16], rb[5][:nb + 16]), (nof_prb, k, rnti)
+            for (rnti, t, rt, ur), (rdl, rul, _) in zip(searches, found):
+                for got, want in zip(find_dci(oracle, *args, cfi, sf, la, rnti, t, rt, ur), (rdl, rul)):
+                    nb = got[4]
+                    assert got[:5] == want[:5] and np.array_equal(got[5][:nb + 16], want[5][:nb + 16]), \
+                        (nof_prb, k, rnti, ur)

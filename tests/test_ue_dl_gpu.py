@@ -43,13 +43,21 @@ def _pcfich_symbols(po, nof_prb, cell_id, sf_idx, cfi):
     return ((1 - 2.0 * z[0::2]) + 1j * (1 - 2.0 * z[1::2])) / np.sqrt(2)
 
 
-def build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti, rnti, cfi, snr_db, flat=False):
+def build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti, rnti, cfi, snr_db, flat=False,
+                      ul=None):
     """(time-domain subframe, tx data, DCI bits, (L, ncce), grant) of one TM1 subframe (flat: no
-    frequency-selective channel)"""
+    frequency-selective channel). ul: a format 0 message for the same RNTI, placed at another free
+    UE-specific location (the UL grant phch_worker looks for after the DL one)"""
     sf_idx = tti % 10
     _, nof_cce = s.pdcch_cell_map(nof_prb, cell_id, 1, PHICH_LEN, PHICH_RES, cfi)
     locs = [lc for lc in s.pdcch_locations(nof_cce, sf_idx, rnti) if lc[1] <= 87]
     L, ncce = locs[int(rng.integers(0, len(locs)))]
+    msgs = []
+    if ul is not None:
+        free = [lc for lc in locs if lc[1] + (1 << lc[0]) <= ncce or lc[1] >= ncce + (1 << L)]
+        if free:
+            uL, uc = free[int(rng.integers(0, len(free)))]
+            msgs.append((ul, uL, uc, rnti))
     Lcrb = int(rng.integers(2, nof_prb + 1))
     start = int(rng.integers(0, nof_prb - Lcrb + 1))
     mcs = int(rng.integers(0, 17))
@@ -69,7 +77,7 @@ def build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti, rnt
     grid = np.zeros(14 * 12 * nof_prb, np.complex128)
     grid[idx] = _modulate(e ^ c, mod)
     grid += pdcch_encode(ref, nof_prb, cell_id, 1, PHICH_LEN, PHICH_RES, cfi, sf_idx,
-                         [(bits, L, ncce, rnti)])[0]
+                         [(bits, L, ncce, rnti)] + msgs)[0]
     grid[pcfich_re_map(oracle, nof_prb, cell_id)] = _pcfich_symbols(po, nof_prb, cell_id, sf_idx, cfi)
     g2 = grid.reshape(14, -1)
     pil = co.crs_pilots(nof_prb, cell_id, sf_idx)
@@ -81,7 +89,7 @@ def build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti, rnt
     x = oo.tx_sf(grid * h, nof_prb, N) / N
     sig = 10 ** (-snr_db / 20) / np.sqrt(2 * N)
     x = x + sig * (rng.standard_normal(x.size) + 1j * rng.standard_normal(x.size))
-    return x.astype(np.complex64), data, bits, (L, ncce), g
+    return x.astype(np.complex64), data, bits, (L, ncce), g, bool(msgs)
 
 
 def _direct(s, torch, xs, ttis, rntis, nof_prb, cell_id, N):
@@ -109,44 +117,52 @@ def _direct(s, torch, xs, ttis, rntis, nof_prb, cell_id, N):
     d_llr = torch.zeros(n * stride, dtype=torch.float32, device="cuda")
     psf = [(i * gsz, i * gsz, i * stride, ttis[i] % 10, int(cfi[i]), float(noise[i])) for i in range(n)]
     assert pd.extract_llr_dev(psf, d_grid.data_ptr(), d_ce.data_ptr(), gsz, d_llr.data_ptr()) == 0
-    se = [(i * stride, ttis[i] % 10, int(cfi[i]), rntis[i], 0, -1) for i in range(n)]
+    se = [(i * stride, ttis[i] % 10, int(cfi[i]), rntis[i], 0, -1, rntis[i]) for i in range(n)]
     d_res = torch.zeros(n * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
-    assert pd.find_dl_dci_dev(se, d_llr.data_ptr(), d_res.data_ptr()) == 0
+    d_ul = torch.zeros(n * s.Pdcch.RESULT_SIZE, dtype=torch.uint8, device="cuda")
+    assert pd.find_dci_dev(se, d_llr.data_ptr(), d_res.data_ptr(), d_ul.data_ptr()) == 0
     torch.cuda.synchronize()
     res = s.Pdcch.parse_results(d_res.cpu().numpy().tobytes())
+    ul = s.Pdcch.parse_results(d_ul.cpu().numpy().tobytes())
     for h in (ofdm, chest):
         h.close()
-    return cfi, corr, res, noise
+    return cfi, corr, res, noise, ul
 
 
 def test_decode_rnti_through_the_queue(oracle):
+    """every item also runs phch_worker's UL search for its RNTI (srslte_ue_dl_find_ul_dci): two thirds of
+    the subframes carry a format 0 message, whose grant must come back unpacked as the reference's
+    srslte_dci_msg_to_ul_grant unpacks the transmitted bits"""
     import torch
     import srsgpu_phy as s
-    from srsgpu_testlib import Ref
+    from srsgpu_testlib import Ref, dci_to_ul_grant_ref, random_ul_msg
     ref = Ref()
     po, dl = PdschOracle(oracle), DlschOracle(oracle)
     rng = np.random.default_rng(31)
     nof_prb, cell_id, rnti = 25, 77, 0x4601
     N = s.symbol_sz(nof_prb, True)
     n, nthreads = 24, 4
-    xs, datas, dcis, ttis, rntis, grants = [], [], [], [], [], []
+    xs, datas, dcis, ttis, rntis, grants, uls = [], [], [], [], [], [], []
     for i in range(n):
         tti = 1000 + 7 * i + (1 if (1000 + 7 * i) % 10 in (0, 5) else 0)  # not 0 / 5: no PSS / SSS
         cfi = 1 + i % 3
-        x, data, bits, loc, g = build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti, rnti,
-                                                  cfi, 28.0 if i % 4 else 20.0)
+        ulb = random_ul_msg(ref, rng, nof_prb, hop_p=0.3) if i % 3 else None
+        x, data, bits, loc, g, placed = build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, tti,
+                                                          rnti, cfi, 28.0 if i % 4 else 20.0, ul=ulb)
+        uls.append(ulb if placed else None)
         xs.append(x)
         datas.append(data)
         dcis.append((bits, loc, cfi))
         ttis.append(tti)
         rntis.append(rnti if i % 6 != 5 else rnti + 1)  # every 6th worker call looks for another UE
         grants.append(g)
-    cfi_d, corr_d, res_d, noise_d = _direct(s, torch, xs, ttis, rntis, nof_prb, cell_id, N)
+    cfi_d, corr_d, res_d, noise_d, ul_d = _direct(s, torch, xs, ttis, rntis, nof_prb, cell_id, N)
 
     q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=2 * n, max_batch=8, max_wait_us=3000)
     q.set_phich(PHICH_LEN, PHICH_RES)
     outs = [np.zeros(int(g.tbs[0]) // 8 + 6, np.uint8) for g in grants]
-    items = [q.ue_item([xs[i]], ttis[i], rntis[i], [outs[i]], softbuffer=(2 * i, 2 * i + 1)) for i in range(n)]
+    items = [q.ue_item([xs[i]], ttis[i], rntis[i], [outs[i]], softbuffer=(2 * i, 2 * i + 1), ul_rnti=rntis[i],
+                       n_rb_ho=2 * (i % 2)) for i in range(n)]
     rcs = [None] * n
 
     def worker(w):
@@ -161,9 +177,19 @@ def test_decode_rnti_through_the_queue(oracle):
     assert rcs == [0] * n
     batches, done = q.stats()
     assert done == n and batches < n
-    found = 0
+    found = nul = 0
     for i, u in enumerate(items):
         bits, (L, ncce), cfi = dcis[i]
+        # the UL search: as the direct search call, and the transmitted format 0 message where there is one
+        assert u.ul_found == ul_d[i][0] and (u.ul_found < 1 or (u.ul_L, u.ul_ncce) == ul_d[i][2:4]), i
+        if uls[i] is not None and rntis[i] == rnti:
+            assert u.ul_found == 1 and list(u.ul_data[:len(uls[i])]) == list(uls[i]), i
+            r, d, g = dci_to_ul_grant_ref(ref, uls[i], nof_prb, 2 * (i % 2))
+            assert u.ul_grant_ret == r and u.ul_dci.fields11() == list(d), i
+            assert r or u.ul_grant.fields10() == list(g), i
+            nul += 1
+        elif rntis[i] != rnti or uls[i] is None:
+            assert u.ul_found == 0 and u.ul_grant_ret == -1, i
         # every stage equals the direct batch APIs on the same samples
         assert u.cfi == cfi_d[i] and u.cfi_corr == corr_d[i], i
         assert abs(u.noise - noise_d[i]) <= 1e-6 * max(1.0, abs(noise_d[i])), i
@@ -184,7 +210,7 @@ def test_decode_rnti_through_the_queue(oracle):
         assert u.ret == int(grants[i].tbs[0]), (i, u.ret)
         assert u.acks[0] == 1 and (outs[i][:len(datas[i])] == datas[i]).all(), i
         found += 1
-    assert found >= n - n // 6 - 1
+    assert found >= n - n // 6 - 1 and nul >= 10
 
 
 def test_mixed_grant_and_ue_dl_items(oracle):
@@ -199,7 +225,7 @@ def test_mixed_grant_and_ue_dl_items(oracle):
     nof_prb, cell_id, rnti = 15, 12, 0x1234
     N = s.symbol_sz(nof_prb, True)
     n = 10
-    built = [build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, 2 + i, rnti, 2, 30.0)
+    built = [build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, 2 + i, rnti, 2, 30.0)[:5]
              for i in range(n)]
     q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=2 * n, max_batch=4, max_wait_us=100000)
     q.set_phich(PHICH_LEN, PHICH_RES)
@@ -227,4 +253,45 @@ def test_mixed_grant_and_ue_dl_items(oracle):
         assert it.ret[0] == 0, i
     for i in range(n):
         assert (outs[i][:len(built[i][1])] == built[i][1]).all(), i
+    q.close()
+
+
+def test_acked_tb_is_left_alone(oracle):
+    """srslte_pdsch_decode skips a TB whose ack the caller already set (pdsch.c:946-947): through the queue
+    its data buffer, nof_iterations and softbuffer stay untouched while the other items decode"""
+    import srsgpu_phy as s
+    from srsgpu_testlib import Ref
+    ref = Ref()
+    po, dl = PdschOracle(oracle), DlschOracle(oracle)
+    rng = np.random.default_rng(12)
+    nof_prb, cell_id, rnti = 25, 5, 0x2222
+    N = s.symbol_sz(nof_prb, True)
+    n = 6
+    built = [build_ue_subframe(s, ref, oracle, po, dl, rng, nof_prb, cell_id, N, 11 + i, rnti, 2, 30.0)[:5]
+             for i in range(n)]
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=2 * n, max_batch=n, max_wait_us=100000)
+    q.set_phich(PHICH_LEN, PHICH_RES)
+    sentinel = 0xA5
+    outs = [np.full(int(b[4].tbs[0]) // 8 + 6, sentinel, np.uint8) for b in built]
+    items = [q.ue_item([b[0]], 11 + i, rnti, [outs[i]], softbuffer=(2 * i, 2 * i + 1), acks=(i % 2, 0))
+             for i, b in enumerate(built)]
+    for u in items:
+        u.noi[0] = 77
+    tickets = [q.submit_ue_dl(u) for u in items]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in tickets)
+    for i, u in enumerate(items):
+        assert u.found == 1 and u.ret == int(built[i][4].tbs[0]), i
+        if i % 2:
+            assert u.acks[0] == 1 and u.noi[0] == 77 and (outs[i] == sentinel).all(), i
+        else:
+            assert u.acks[0] == 1 and u.noi[0] >= 1 and (outs[i][:len(built[i][1])] == built[i][1]).all(), i
+    # a later retransmission into an acked item's softbuffer decodes as if that softbuffer were fresh
+    # (the skipped TB never touched it): the same subframe with acks cleared decodes
+    items2 = [q.ue_item([built[i][0]], 11 + i, rnti, [outs[i]], softbuffer=(2 * i, 2 * i + 1)) for i in (1, 3)]
+    t2 = [q.submit_ue_dl(u) for u in items2]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in t2)
+    for j, i in enumerate((1, 3)):
+        assert items2[j].acks[0] == 1 and (outs[i][:len(built[i][1])] == built[i][1]).all(), i
     q.close()
