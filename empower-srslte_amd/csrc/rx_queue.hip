@@ -550,7 +550,8 @@ struct srsgpu_rxq {
                                            : -1;
         u->acked_in[0] = u->acks[0];
         u->acked_in[1] = u->acks[1];
-        u->noi[0] = u->noi[1] = 0;
+        for (int t = 0; t < 2; t++)
+          if (!u->acks[t]) u->noi[t] = 0; // an acked TB keeps what it had (the reference's last noi)
         j++;
         if (res.found != 1) { // no DCI, or the search's error: srslte_ue_dl_decode_rnti returns 0
           state[i] = 0;
