@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X turbo-decoder hot path (BASELINE.json configs[1]).
+"""Benchmark of the MI355X PDSCH receive path on BASELINE.json's metric configuration, configs[2]:
+20 MHz (2048-point FFT) SISO 64QAM subframes, 1024 per GPU per step, time domain -> TB bytes (OFDM FFT,
+CRS channel estimation, MMSE, 64QAM demapping, descrambling, de-rate-matching, turbo decoding with CRC
+early stop up to 8 half-iterations, TB CRC), coded traffic from the GPU transmitter at 20 dB, inputs
+resident in HBM. value = decoded Mbps (the sum of K over CRC-passing code blocks per
+second); config carries subframes/s. The CPU baseline is the reference's own srslte_chest_dl_estimate
++ srslte_pdsch_decode (oracle/_ref/ref_front) on the same received grids, FFT excluded.
 
-One "step" = decode one batch of 4096 code blocks of K=6144 bits with 8 half-iterations
-(srslte_tdec_run_all semantics, AUTO decoder = AVX16 window, 16 sub-blocks), inputs resident in
-HBM, through the C ABI (srsgpu_tdec_batch_run_dev). Synthetic traffic: random bits -> turbo
-encoder -> BPSK/AWGN -> int16 LLRs (turbodecoder_test.c:236-252 quantisation).
+Further legs on the same JSON line: BASELINE configs[1] (4096 x K=6144 code blocks, 8 half-iterations:
+decoder_c2, with its own roofline and the reference AVX2 decoder as its CPU baseline), the same C3
+subframes with all 8 half-iterations (no early stop), an SNR sweep into the waterfall, the 1536-point
+FFT, TM3 (configs[3] shard), mixed bandwidths (configs[4] shard), the 8-bit decoders, PDCCH / PCFICH,
+the subframe queue and the per-call drop-in.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-For N > 1 run under torch.distributed.run: one rank per GPU, each decodes its own batch
-(independent code blocks, no data-path collective) -> weak scaling.
+For N > 1 run under torch.distributed.run: one rank per GPU, each decodes its own shard of the global
+job (independent subframes, no data-path collective; results gathered to rank 0) -> weak scaling.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -205,13 +212,19 @@ def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1, first=0, noise_seed=None):
 
 STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_bidir",
           "k_sse_halfit", "k_decide", "k_tb_finish")
+# kernels of the coded subframe legs, for the per-kernel table and the roofline of the dominant one
+# (names as the library's ProfScope records them; prof_get matches substrings, so the decoder's
+# early-stop launches are asked for by their full name)
+KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_bidir_es",
+           "k_sse_es", "k_es_bytes", "k_win_bidir_run", "k_decide", "k_tb_finish")
 
 
-def stage_profile(s, torch, step, steps):
+def stage_profile(s, torch, step, steps, kernels=None):
     """Per-stage device time per batch, from HIP events around every launch (srsgpu_prof_*), in
     a separate pass after the timed loop: creating and recording the events costs host time that
     would otherwise show in the host-bound legs' wall clock. With several streams the spans of
-    concurrent launches overlap, so the stage sums then exceed the wall time per batch."""
+    concurrent launches overlap, so the stage sums then exceed the wall time per batch.
+    kernels: also return {name: (total ms per batch, launches per batch)} for these names."""
     s.prof_reset()
     s.prof_enable(True)
     for _ in range(steps):
@@ -223,7 +236,14 @@ def stage_profile(s, torch, step, steps):
         ms, cnt = s.prof_get(name)
         if cnt:
             out[name] = round(ms / steps, 4)
-    return out
+    if kernels is None:
+        return out
+    kt = {}
+    for name in kernels:
+        ms, cnt = s.prof_get(name)
+        if cnt:
+            kt[name] = (ms / steps, cnt / steps)
+    return out, kt
 
 
 def warm_up(torch, step, warmup, seconds=0.25):
@@ -388,7 +408,8 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedul
                     "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
 
 
-def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None):
+def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None,
+                standard_rate=True, early_stop=True, cpu_sample=0):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
@@ -403,7 +424,11 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     rank (TB bytes, return code, nof_iterations, cb_crc) go to rank 0 in one grouped send/recv
     batch (srsgpu_shard.gather_records), timed separately as gather_ms.
     lanes: a rank's subframes are split over that many HIP streams (run_pipeline).
-    decoded_mbps is SURVEY §8(d)'s metric: the sum of K over CRC-passing code blocks per second."""
+    decoded_mbps is SURVEY §8(d)'s metric: the sum of K over CRC-passing code blocks per second.
+    standard_rate False: srsLTE's 1536-point FFT at 20 MHz instead of 2048. early_stop False: every
+    code block runs all 8 half-iterations (srsgpu_dlsch_set_early_stop, the fixed-8 rate on real
+    codewords). cpu_sample > 0: the first cpu_sample received resource grids of lane 0 (after the
+    FFT) come back as host arrays for the CPU baseline ("_cpu_grids", "_cpu_sf_idx")."""
     import srsgpu_shard as sh
     import srsgpu_traffic as tr
     rank = dist.get_rank() if dist else 0
@@ -426,7 +451,8 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     for li in range(lanes):
         st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
         ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
-                                keep=mine[li::lanes], **kw))  # one plan: the same seed everywhere
+                                keep=mine[li::lanes], standard_rate=standard_rate, early_stop=early_stop,
+                                **kw))  # one plan: the same seed everywhere
     torch.cuda.synchronize()
 
     def step():
@@ -445,7 +471,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
         dist.barrier()
     el = time.perf_counter() - t0
     gc.enable()
-    stages = stage_profile(s, torch, step, steps)
+    stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
     ab = schedule_ab(s, torch, step, steps, schedules)
     chk = [m.check() for m in ms]
     acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
@@ -485,7 +511,14 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
            "nof_iterations_mean": noi, "stage_ms_per_batch": stages, "partition": part,
            "subframes_this_rank": len(mine), "gather_ms": gather_ms,
            "result_bytes_per_rank": int(local.numel()), "schedule_ab": ab,
+           "symbol_size": ms[0].cells[0]["N"], "early_stop": early_stop,
+           "kernels_per_batch": {k: {"ms": round(v[0], 4), "launches": v[1]} for k, v in ktab.items()},
            "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % snr}
+    if cpu_sample:
+        c = ms[0].cells[0]
+        n = min(cpu_sample, c["n"])
+        out["_cpu_grids"] = c["grid"][:n * c["gsz"]].cpu().numpy().reshape(n, c["gsz"])
+        out["_cpu_sf_idx"] = [int(c["sf_idx"][i]) for i in range(n)]
     for m in ms:
         m.close()
     return out
@@ -745,17 +778,228 @@ def dropin_latency(s, llr, ncb=16):
                     "batch APIs carry the throughput"}
 
 
+# SURVEY §8(d) per-subframe algorithmic HBM bytes of the C3 (20 MHz SISO, 100 PRB, MCS 28, CFI 1,
+# N = 2048) kernels: what each must read and write at least, per subframe
+C3_NRE, C3_NLLR, C3_GRID = 15000, 90000, 14 * 12 * 100
+C3_KS = [5824] * 13
+ALG_BYTES_PER_SF = {
+    # 14 symbols of N complex-float samples in (CPs skipped), the 16,800-RE grid out
+    "k_ofdm_rx": lambda N: 14 * N * 8 + C3_GRID * 8,
+    # 4 x 200 CRS pilots in, the 16,800-RE estimate grid and the noise estimate out
+    "k_chest": lambda N: 800 * 8 + C3_GRID * 8 + 4,
+    # the subframe's Gold sequence bits out
+    "k_gold": lambda N: C3_NLLR // 8,
+    # grid and estimate of the 15,000 PDSCH REs in, 90,000 int16 LLRs out
+    "k_pdsch_llr": lambda N: C3_NRE * 8 * 2 + C3_NLLR * 2,
+    # LLRs in, the 13 softbuffer rows (3(K+32)+12 int16) out
+    "k_derm": lambda N: C3_NLLR * 2 + sum((3 * (k + 32) + 12) * 2 for k in C3_KS),
+    # rows in, the decoder's systematic / parity planes out: 6 B + 6 B per info bit
+    "k_load": lambda N: 12 * sum(C3_KS),
+    # (3(K+32)+12)*2 + K/8 B per code block per decode
+    "k_win_bidir_es": lambda N: sum((3 * (k + 32) + 12) * 2 + k // 8 for k in C3_KS),
+    "k_win_bidir_run": lambda N: sum((3 * (k + 32) + 12) * 2 + k // 8 for k in C3_KS),
+    # decision bytes in, TB bytes out
+    "k_es_bytes": lambda N: 2 * sum(k // 8 for k in C3_KS),
+    "k_tb_finish": lambda N: sum(k // 8 for k in C3_KS) + C3_TBS // 8,
+}
+HEADLINE_SNR_DB = 20.0
+
+
+def pipeline_roofline(leg, nsf_per_batch):
+    """roofline of the leg's dominant kernel (the largest device time per batch among the ones with
+    §8(d) algorithmic bytes): achieved = algorithmic bytes per launch / average launch time (HIP
+    events on the launch stream, stage_profile); plus the whole per-kernel table"""
+    N = leg["symbol_size"]
+    table = {}
+    for k, v in leg["kernels_per_batch"].items():
+        if k not in ALG_BYTES_PER_SF or not v["launches"]:
+            continue
+        alg = ALG_BYTES_PER_SF[k](N) * nsf_per_batch / v["launches"]
+        avg = v["ms"] / v["launches"]
+        table[k] = {"ms_per_batch": v["ms"], "launches_per_batch": v["launches"], "avg_launch_ms": round(avg, 4),
+                    "alg_bytes_per_launch": int(alg), "achieved_GBs": round(alg / (avg / 1e3) / 1e9, 1),
+                    "frac": round(alg / (avg / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if not table:
+        return None, table
+    dom = max(table, key=lambda k: table[k]["ms_per_batch"])
+    t = table[dom]
+    pmc = load_profile_json(leg["workload"] + ":" + dom)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    roof = {"bound": "hbm", "kernel": dom, "achieved": t["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": t["frac"], "traffic": traffic,
+            "traffic_over_alg": round(traffic / t["alg_bytes_per_launch"], 2) if traffic else None,
+            "traffic_source": pmc.get("source") if pmc else None,
+            "alg_bytes_per_launch": t["alg_bytes_per_launch"], "avg_launch_ms": t["avg_launch_ms"],
+            "launches_per_batch": t["launches_per_batch"],
+            "alg_bytes_def": "SURVEY 8(d) per-subframe algorithmic bytes of %s (bench.py ALG_BYTES_PER_SF) x "
+                             "%d subframes per launch" % (dom, nsf_per_batch / t["launches_per_batch"])}
+    return roof, table
+
+
+def cpu_baseline_pipeline(grids, sf_idx, snr_db, nthreads=None, target_thread_s=15.0):
+    """BASELINE configs[2] on the host: the reference's own srslte_chest_dl_estimate +
+    srslte_pdsch_decode (CRC early stop, max 8 half-iterations), compiled from its sources into
+    oracle/_ref/ref_front, one chest / PDSCH / softbuffer per pthread, each pinned to its own physical
+    core, on the GPU leg's own received grids (after its FFT: FFTW is absent, so the OFDM stage is
+    excluded here and stated). Threads as cpu_baseline. None if the executable is absent."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_front")
+    if not os.path.exists(exe):
+        return None
+    cores = physical_cpus()
+    cap = int(os.environ.get("SRSGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", len(cores))))
+    if nthreads is None:
+        nthreads = max(1, min(len(cores), cap))
+    pin = cores[:nthreads]
+    nsf = len(sf_idx)
+
+    def run(reps):
+        head = np.array([C3_PRB, C3_CELL, 1, 1234, 28, 8, nthreads, reps, nsf, len(pin)] + list(pin), np.uint32)
+        body = b"".join(np.array([sf], np.uint32).tobytes() + np.ascontiguousarray(g, np.complex64).tobytes()
+                        for sf, g in zip(sf_idx, grids))
+        with tempfile.TemporaryDirectory() as d:
+            fi, fo = os.path.join(d, "in.bin"), os.path.join(d, "out.json")
+            with open(fi, "wb") as f:
+                f.write(head.tobytes() + body)
+            r = subprocess.run([exe, "pdsch_bench", fi, fo], capture_output=True, text=True, timeout=300)
+            if r.returncode != 0:
+                raise RuntimeError("ref_front pdsch_bench failed: " + r.stderr[-400:])
+            return json.load(open(fo))
+
+    cal = run(1)
+    per_sf_thread_s = cal["wall_s"] * nthreads / max(cal["subframes"], 1)
+    reps = int(max(1, min(2000, np.ceil(target_thread_s / max(per_sf_thread_s * nsf, 1e-6)))))
+    res = run(reps)
+    wall = res["wall_s"]
+    return {"value": round(res["cb_bits_ok"] / wall / 1e6, 2), "unit": "Mbps", "cores": nthreads, "kind": "reference",
+            "subframes_per_s": round(res["subframes"] / wall, 1), "acked_tbs": res["acked"],
+            "subframes": res["subframes"], "nof_iterations_mean": res["noi_mean"], "pinned_cpus": pin,
+            "physical_cores_available": len(cores),
+            "sample": "%d subframe decodes (%d distinct received grids of the GPU headline leg at %.0f dB x %d "
+                      "passes) through the reference's srslte_chest_dl_estimate + srslte_pdsch_decode "
+                      "(oracle/_ref/ref_front, compiled from the reference's sources, AVX2, CRC early stop max 8 "
+                      "half-iterations), %d threads each pinned to its own physical core (%d physical cores in "
+                      "the affinity set, CPU share cap %d), %.2f s wall (%.0f thread-seconds); OFDM FFT excluded "
+                      "(FFTW absent)" % (res["subframes"], nsf, snr_db, reps, nthreads, len(cores), cap, wall,
+                                         wall * nthreads)}
+
+
+def decoder_leg(s, torch, dev, args, dist, rank, nranks):
+    """BASELINE configs[1]: 4096 x K=6144 code blocks per GPU, 8 half-iterations, AUTO decoder (AVX16
+    window), inputs resident in HBM; one step = one srsgpu_tdec_batch_run_dev. Returns (dict, llr) —
+    the dict carries its own roofline (compulsory HBM bytes) and VALU roofline."""
+    import srsgpu_shard as sh
+    tcod = s.Tcod(K)
+    first = sh.contiguous(nranks * NCB, nranks)
+    assert first[rank + 1] - first[rank] == NCB
+    bits, idx, llr = make_inputs(NCB, 1234, tcod, first=first[rank])
+    d_in = torch.from_numpy(llr).to(dev)
+    d_out = torch.zeros((NCB, K // 8), dtype=torch.uint8, device=dev)
+    # a dedicated stream: launches on the null stream carry HIP's implicit cross-stream
+    # synchronisation and cost ~6 % of the step here
+    stream = torch.cuda.Stream(dev)
+    batch = s.TdecBatch(NCB, K, stream=stream.cuda_stream)
+    stride = 3 * K + 12
+
+    def step():
+        if batch.run_dev(0, 0, d_in.data_ptr(), stride, K, NCB, NHALF, d_out.data_ptr(), K // 8) != 0:
+            raise RuntimeError("srsgpu_tdec_batch_run_dev failed")
+
+    # pre-heat: ~0.3 s of decoding so the timed steps see the steady clock of a receiver that decodes
+    # continuously (a cold GPU ramps its clock over the first few ms of load)
+    t_heat = time.perf_counter()
+    while time.perf_counter() - t_heat < 0.3:
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    expect = np.packbits(bits, axis=1)[idx]
+    bit_errors = int(np.unpackbits(d_out.cpu().numpy() ^ expect).sum())
+    steps = args.steps
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gc.enable()
+    # the decoder kernel's launch duration: HIP events around every launch on the batch stream,
+    # over the same number of steps right after the timed loop
+    s.prof_reset()
+    s.prof_enable(True)
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    s.prof_enable(False)
+    kern_name, halfits_per_launch = "k_win_bidir_run", NHALF
+    kern_ms, kern_n = s.prof_get(kern_name)
+    if not kern_n:
+        kern_name, halfits_per_launch = "k_win_bidir", 1
+        kern_ms, kern_n = s.prof_get(kern_name)
+    elapsed, bit_errors = reduce_over_ranks(dist, dev, elapsed, bit_errors)
+    gather = None
+    if dist:  # SURVEY §8(e): decoded bytes to rank 0 in one grouped send/recv batch (not in the step)
+        gdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        local_out = d_out.reshape(-1) if gdev.type == "cuda" else d_out.reshape(-1).cpu()
+        owner = np.repeat(np.arange(nranks), np.diff(first))
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        got = sh.gather_records(dist, torch, gdev, owner, [K // 8] * (nranks * NCB), local_out)
+        torch.cuda.synchronize()
+        gather = {"gather_ms": round((time.perf_counter() - tg) * 1e3, 3), "bytes_per_rank": NCB * K // 8,
+                  "gathered_code_blocks": (sum(1 for r in got if r is not None) if got is not None else None)}
+    workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
+    avg_launch_ms = kern_ms / max(kern_n, 1)
+    alg_bytes = COMPULSORY_BYTES_PER_CB * NCB / NHALF * halfits_per_launch
+    achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
+    pmc = load_profile_json(workload)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc and pmc.get("kernel") == kern_name else None
+    out = {"workload": workload, "config": "BASELINE configs[1]", "mbps": round(decoded_mbps(nranks, NCB, K, steps, elapsed), 2),
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "code_blocks_per_gpu": NCB, "K": K,
+           "half_iterations": NHALF, "decoder": "AUTO (AVX16 window, 16 sub-blocks)", "ebno_db_ref_convention": EBNO_DB,
+           "bit_errors": bit_errors, "decoder_schedule": s.get_schedule(),
+           "roofline": {"bound": "hbm", "kernel": kern_name, "achieved": round(achieved, 1) if achieved else None,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                        "traffic": traffic, "traffic_over_compulsory": round(traffic / alg_bytes, 2) if traffic else None,
+                        "traffic_source": pmc.get("source") if pmc else None, "alg_bytes_per_launch": int(alg_bytes),
+                        "alg_bytes_def": "SURVEY 8(d): (3(K+32)+12)*2 + K/8 = %d B per CB per decode" % COMPULSORY_BYTES_PER_CB,
+                        "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n,
+                        "halfits_per_launch": halfits_per_launch, "avg_halfit_ms": round(avg_launch_ms / halfits_per_launch, 4)}}
+    if kern_n:
+        ops = ALG_OPS_PER_BIT_HALFIT * NCB * K * halfits_per_launch
+        rate_t = ops / (avg_launch_ms / 1e3) / 1e12
+        out["valu_roofline"] = {
+            "bound": "valu (packed int16)", "kernel": kern_name, "achieved": round(rate_t, 2), "peak": VALU_INT16_PEAK_T,
+            "unit": "T int16-ops/s", "frac": round(rate_t / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": ops,
+            "alg_ops_def": "SURVEY 8(d): %d int16 ops per info bit per half-iteration" % ALG_OPS_PER_BIT_HALFIT,
+            "measured_issue_peaks_T": VALU_INT16_MEASURED_T,
+            "frac_of_1wave_issue_peak": round(rate_t / VALU_INT16_MEASURED_T["1_wave_per_simd_ilp8"], 4)}
+    if gather:
+        out["gather"] = gather
+    out["_batch"], out["_d_in"], out["_d_out"], out["_expect"], out["_stride"] = batch, d_in, d_out, expect, stride
+    return out, llr
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="headline and configs[1] decoder only")
     ap.add_argument("--coded-snr", type=float, default=None,
                     help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
-    ap.add_argument("--legs", default="c3,tm3,coded,sweep,c5,d8,dropin,dci,pcfich,pdcch,rxq",
-                    help="subframe-pipeline legs after the decoder headline (profiling aid)")
+    ap.add_argument("--legs", default="c2,fixed8,c3,tm3,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
+                    help="legs after the headline (profiling aid)")
     args = ap.parse_args()
 
     import torch
@@ -773,193 +1017,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-
-    tcod = s.Tcod(K)
     nranks = max(1, world)
-    # the global job is nranks x NCB code blocks, split in contiguous ranges by the
-    # native partitioner (include/srsgpu/shard.h); every rank decodes its own range
-    import srsgpu_shard as sh
-    first = sh.contiguous(nranks * NCB, nranks)
-    assert first[rank + 1] - first[rank] == NCB
-    bits, idx, llr = make_inputs(NCB, 1234, tcod, first=first[rank])
-    d_in = torch.from_numpy(llr).to(dev)
-    d_out = torch.zeros((NCB, K // 8), dtype=torch.uint8, device=dev)
-    # a dedicated stream: launches on the null stream carry HIP's implicit cross-stream
-    # synchronisation and cost ~6 % of the step here
-    stream = torch.cuda.Stream(dev)
-    batch = s.TdecBatch(NCB, K, stream=stream.cuda_stream)
-    stride = 3 * K + 12
-
-    def step():
-        r = batch.run_dev(0, 0, d_in.data_ptr(), stride, K, NCB, NHALF, d_out.data_ptr(), K // 8)
-        if r != 0:
-            raise RuntimeError("srsgpu_tdec_batch_run_dev failed")
-
-    # pre-heat: ~0.3 s of decoding before the warmup steps, so the timed steps see the steady-state
-    # clocks of a receiver that decodes continuously (a cold GPU ramps its clock over the first
-    # few ms of load: 10 steps right after start-up run ~6 % slower per kernel)
-    t_heat = time.perf_counter()
-    while time.perf_counter() - t_heat < 0.3:
-        for _ in range(8):
-            step()
-        torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # sanity: the decoded bits equal the transmitted ones (error-free SNR)
-    got = d_out.cpu().numpy()
-    expect = np.packbits(bits, axis=1)[idx]
-    bit_errors = int(np.unpackbits(got ^ expect).sum())
-
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    gc.disable()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
-    # The decoder kernel's launch duration for the roofline: HIP events around every launch on the
-    # batch stream (srsgpu_prof_*), over the same number of steps right after the timed loop.
-    # Events inside the timed loop would cost ~9% of the step (event records between launches).
-    s.prof_reset()
-    s.prof_enable(True)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    s.prof_enable(False)
-    # the decoder kernel: k_win_bidir_run (all NHALF half-iterations in one launch) unless
-    # SRSGPU_TDEC_FUSED=0 selects one k_win_bidir launch per half-iteration
-    kern_name, halfits_per_launch = "k_win_bidir_run", NHALF
-    kern_ms, kern_n = s.prof_get(kern_name)
-    if not kern_n:
-        kern_name, halfits_per_launch = "k_win_bidir", 1
-        kern_ms, kern_n = s.prof_get(kern_name)
-    # streaming: NSTREAMS batches in flight on their own streams (a receiver double/triple
-    # buffering its batches); every batch is the full 4096-CB step
-    ms_batches = [batch] + [s.TdecBatch(NCB, K, stream=torch.cuda.Stream(dev).cuda_stream)
-                            for _ in range(NSTREAMS - 1)]
-    ms_outs = [d_out] + [torch.zeros_like(d_out) for _ in range(NSTREAMS - 1)]
-    torch.cuda.synchronize()  # the fills ran on the current stream; the batches use their own
-
-    def step_ms(i):
-        j = i % NSTREAMS
-        if ms_batches[j].run_dev(0, 0, d_in.data_ptr(), stride, K, NCB, NHALF, ms_outs[j].data_ptr(),
-                                 K // 8) != 0:
-            raise RuntimeError("srsgpu_tdec_batch_run_dev failed")
-
-    for i in range(NSTREAMS):
-        step_ms(i)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    gc.disable()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step_ms(i)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el_ms = time.perf_counter() - t0
-    gc.enable()
-    ms_err = sum(int(np.unpackbits(o.cpu().numpy() ^ expect).sum()) for o in ms_outs)
-    for b in ms_batches[1:]:
-        b.close()
-    el_ms, ms_err = reduce_over_ranks(dist, dev, el_ms, ms_err)
-    elapsed, bit_errors = reduce_over_ranks(dist, dev, elapsed, bit_errors)
-    # the decoded bytes of every rank's code blocks go to rank 0 in one grouped
-    # send/recv batch (RCCL over xGMI on the GPU box), timed separately; not part of the step
-    gather = None
-    if dist:
-        gdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-        local_out = d_out.reshape(-1) if gdev.type == "cuda" else d_out.reshape(-1).cpu()
-        owner = np.repeat(np.arange(nranks), np.diff(first))
-        dist.barrier()
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        got = sh.gather_records(dist, torch, gdev, owner, [K // 8] * (nranks * NCB), local_out)
-        torch.cuda.synchronize()
-        gather = {"gather_ms": round((time.perf_counter() - tg) * 1e3, 3),
-                  "bytes_per_rank": NCB * K // 8,
-                  "gathered_code_blocks": (sum(1 for r in got if r is not None) if got is not None else None)}
-
-    bits_total = nranks * NCB * K * args.steps
-    mbps = decoded_mbps(nranks, NCB, K, args.steps, elapsed)
-    result = None
-    if rank == 0:
-        workload = "batched_turbo_decode_%dxK%d_%dhalfits" % (NCB, K, NHALF)
-        avg_launch_ms = kern_ms / max(kern_n, 1)
-        # compulsory bytes of the whole decode, one NHALF-th per half-iteration
-        alg_bytes = COMPULSORY_BYTES_PER_CB * NCB / NHALF * halfits_per_launch
-        achieved = alg_bytes / (avg_launch_ms / 1e3) / 1e9 if kern_n else None
-        pmc = load_profile_json(workload)
-        # PMC bytes only from a profile of this same kernel (per launch)
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc and pmc.get("kernel") == kern_name else None
-        roofline = {"bound": "hbm", "kernel": kern_name,
-                    "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": traffic, "layout_traffic": traffic,
-                    "traffic_over_compulsory": round(traffic / alg_bytes, 2) if traffic else None,
-                    "traffic_source": pmc.get("source") if pmc else None,
-                    "alg_bytes_per_launch": int(alg_bytes),
-                    "alg_bytes_def": "SURVEY 8(d): (3(K+32)+12)*2 + K/8 = %d B per CB per decode, / %d "
-                                     "half-iterations" % (COMPULSORY_BYTES_PER_CB, NHALF),
-                    "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n,
-                    "halfits_per_launch": halfits_per_launch,
-                    "avg_halfit_ms": round(avg_launch_ms / halfits_per_launch, 4)}
-        result = {
-            "metric": METRIC, "value": round(mbps, 2), "unit": "Mbps", "n_gpus": nranks,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int16", "data": "synthetic",
-            "config": {"workload": workload, "code_blocks_per_gpu": NCB, "K": K,
-                       "half_iterations": NHALF, "decoder": "AUTO (AVX16 window, 16 sub-blocks)",
-                       "ebno_db_ref_convention": EBNO_DB, "parallelism": "dp%d" % nranks,
-                       "subframes_per_s_equiv": round(bits_total / elapsed / SF_BITS, 1),
-                       "bit_errors": bit_errors},
-            "roofline": roofline,
-            "decoder_schedule": s.get_schedule(),  # srsgpu_tdec_set_schedule (results identical under all)
-        }
-        if gather:
-            result["gather"] = gather
-        result["streaming"] = {
-            "streams": NSTREAMS, "mbps": round(decoded_mbps(nranks, NCB, K, args.steps, el_ms), 2),
-            "ms_per_step": round(el_ms / args.steps * 1e3, 3), "bit_errors": ms_err,
-            "note": "the same steps with %d batches in flight on separate streams; value above is "
-                    "one stream, one batch at a time" % NSTREAMS}
-        if kern_n:
-            # the decoder's actual bound: int16 VALU work, SURVEY §8(d)'s algorithmic 90 ops per
-            # info bit per half-iteration over the live launch time, against §8(d)'s peak
-            ops = ALG_OPS_PER_BIT_HALFIT * NCB * K * halfits_per_launch
-            rate_t = ops / (avg_launch_ms / 1e3) / 1e12
-            result["valu_roofline"] = {
-                "bound": "valu (packed int16)", "kernel": kern_name,
-                "achieved": round(rate_t, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
-                "frac": round(rate_t / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": ops,
-                "alg_ops_def": "SURVEY 8(d): %d int16 ops per info bit per half-iteration" % ALG_OPS_PER_BIT_HALFIT,
-                "measured_issue_peaks_T": VALU_INT16_MEASURED_T,
-                "frac_of_1wave_issue_peak": round(rate_t / VALU_INT16_MEASURED_T["1_wave_per_simd_ilp8"], 4)}
     legs = set() if args.no_pipeline else set(args.legs.split(","))
-    pipe = None
-    if "c3" in legs:
-        pipe = run_pipeline(s, torch, dev, max(2, args.steps), 2, dist=dist)
-        if dist:
-            ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
-            pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe["processing_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
-    pipe3 = None
-    if "tm3" in legs:
-        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps), 2, tm=3, dist=dist)
-        if dist:
-            ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
-            pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
-            pipe3["processing_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
-    extra = {}
+    if args.no_pipeline:
+        legs = {"c2"}
+
     def scale_ranks(r):
         if dist:  # whole job: every rank's bits and subframes over the slowest rank's batch time
             ms, _ = reduce_over_ranks(dist, dev, r["ms_per_batch"], 0)
@@ -969,30 +1031,85 @@ def main():
             r["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
         return r
 
+    # ---- headline: BASELINE configs[2] (the metric's own configuration) ----
+    # 1024 coded 20 MHz SISO 64QAM subframes per GPU (MCS 28, TBS 75376, 13 x K=5824) from the GPU
+    # transmitter at 20 dB, time domain -> TB bytes: OFDM FFT, CRS channel estimation, PDSCH (RE
+    # extraction, MMSE, 64QAM demap, descramble), DL-SCH (de-RM, turbo decoding with CRC early stop up
+    # to 8 half-iterations as srsUE runs it, TB CRC). One step = one 1024-subframe batch.
+    head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
+                                   dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0))
+    cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
+    result = None
+    if rank == 0:
+        roof, ktable = pipeline_roofline(head, C3_SF)
+        head["kernel_table"] = ktable
+        result = {
+            "metric": METRIC, "value": head["decoded_mbps"], "unit": "Mbps", "n_gpus": nranks, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_batch"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32+int16",
+            "data": "synthetic (coded subframes from the GPU transmitter, AWGN %.0f dB)" % HEADLINE_SNR_DB,
+            "config": {"workload": "pdsch_test_c3_20MHz_siso_64qam_%dsf_snr%d_earlystop8" % (C3_SF, HEADLINE_SNR_DB),
+                       "baseline_config": "BASELINE configs[2]", "subframes_per_batch_per_gpu": C3_SF,
+                       "nof_prb": C3_PRB, "fft_size": head["symbol_size"], "mcs": 28, "tbs": C3_TBS,
+                       "code_blocks_per_subframe": 13, "K": 5824, "snr_db": HEADLINE_SNR_DB,
+                       "early_stop_max_halfits": 8, "subframes_per_s": head["subframes_per_s"],
+                       "nof_iterations_mean": head["nof_iterations_mean"], "acked_tbs": head["acked_tbs"],
+                       "tbs_bytes_ok": head["tbs_bytes_ok"], "parallelism": "dp%d" % nranks},
+            "value_def": "decoded Mbps = sum of K over CRC-passing code blocks per second (SURVEY 8(d)), whole "
+                         "job over the slowest rank's batch time",
+            "roofline": roof,
+            "headline_detail": head,
+        }
+    # ---- further legs ----
+    dec = None
+    llr = None
+    if "c2" in legs:
+        dec, llr = decoder_leg(s, torch, dev, args, dist, rank, nranks)
+    extra = {}
+    if "fixed8" in legs:
+        # the same coded subframes with every code block running all 8 half-iterations (no early stop):
+        # the worst-case processing rate on real codewords
+        extra["fixed8"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
+                                                  snr_db=HEADLINE_SNR_DB, dist=dist, early_stop=False))
+    if "n1536" in legs:
+        # srsLTE's reduced 20 MHz sampling (1536-point FFT, SURVEY 8(d) "N=1536")
+        extra["n1536"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
+                                                 snr_db=HEADLINE_SNR_DB, dist=dist, standard_rate=False))
+    pipe = None
+    if "c3" in legs:
+        pipe = run_pipeline(s, torch, dev, max(2, args.steps // 2), 2, dist=dist)
+        if dist:
+            ms, _ = reduce_over_ranks(dist, dev, pipe["ms_per_batch"], 0)
+            pipe["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            pipe["processing_mbps"] = round(pipe["subframes_per_s"] * C3_TBS / 1e6, 1)
+    pipe3 = None
+    if "tm3" in legs:
+        pipe3 = run_pipeline(s, torch, dev, max(2, args.steps // 2), 2, tm=3, dist=dist)
+        if dist:
+            ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
+            pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
+            pipe3["processing_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
-            # host-bound legs: 4x the steps, so an OS scheduling hiccup on the host averages out
-            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, kind, dist=dist,
+            extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, kind, dist=dist,
                                                   snr_db=args.coded_snr if kind == "c3_coded" else None))
     sweep = None
     if "sweep" in legs:
-        # SURVEY §8(d) C3 points: coded subframes at 20 / 25 / 30 dB, CRC early stop (max 8
-        # half-iterations); decoded Mbps = sum of K over CRC-passing code blocks per second
+        # SURVEY §8(d) C3 points with CRC early stop (max 8 half-iterations), down into the waterfall
+        # (14-16 dB: 2..8 half-iterations, failing TBs) and up to 30 dB
         sweep = []
-        # (16 and 18 dB added: with this channel the 20 dB point already decodes every TB at the
-        # first half-iteration; below it the early stop runs 2..8 half-iterations)
-        for snr in (16.0, 18.0, 20.0, 25.0, 30.0):
-            r = scale_ranks(run_traffic(s, torch, dev, max(8, 4 * args.steps), 2, "c3_coded", snr_db=snr,
-                                        dist=dist))
+        for snr in (14.0, 15.0, 16.0, 18.0, 20.0, 25.0, 30.0):
+            r = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps // 2), 2, "c3_coded", snr_db=snr, dist=dist))
             sweep.append({k: r[k] for k in ("snr_db", "decoded_mbps", "acked_tb_mbps", "offered_tb_mbps",
                                              "subframes_per_s", "ms_per_batch", "nof_iterations_mean",
                                              "acked_tbs", "tbs")})
     dec8 = None
-    if "d8" in legs:  # last: the subframe legs above are timed as before
-        # the reference's 8-bit path (srslte_tdec_iteration_8bit: AUTO -> int8 AVX8 window, 32
-        # sub-blocks at K = 6144) on the same code blocks, LLRs requantised to int8
+    if "d8" in legs and dec:
+        # the reference's 8-bit path (srslte_tdec_iteration_8bit: AUTO -> int8 AVX8 window, 32 sub-blocks
+        # at K = 6144) on the same code blocks, LLRs requantised to int8
+        batch, d_in, d_out, expect, stride = dec["_batch"], dec["_d_in"], dec["_d_out"], dec["_expect"], dec["_stride"]
         d_in8 = torch.clamp(torch.div(d_in, 6, rounding_mode="trunc"), -128, 127).contiguous()
-        torch.cuda.synchronize()  # built on the current stream, read on the batch stream
+        torch.cuda.synchronize()
 
         def step8():
             if batch.run_dev(s.SRSGPU_TDEC_AUTO_8BIT, 0, d_in8.data_ptr(), stride, K, NCB, NHALF,
@@ -1017,56 +1134,56 @@ def main():
         gc.enable()
         el8, err8 = reduce_over_ranks(dist, dev, el8, err8)
         dec8 = {"decoder": "AUTO 8-bit (int8 AVX8 window, 32 sub-blocks)",
-                "mbps": round(decoded_mbps(max(1, world), NCB, K, args.steps, el8), 1),
+                "mbps": round(decoded_mbps(nranks, NCB, K, args.steps, el8), 1),
                 "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
-    dci = None
+    dci = pcf = pdc = rxq = dropin = None
     if "dci" in legs and rank == 0:
-        dci = dci_blind_decode(s, torch, max(4, args.steps // 2))
-    pcf = None
+        dci = dci_blind_decode(s, torch, max(4, args.steps // 4))
     if "pcfich" in legs and rank == 0:
-        pcf = pcfich_cfi(s, torch, max(4, args.steps // 2))
-    pdc = None
+        pcf = pcfich_cfi(s, torch, max(4, args.steps // 4))
     if "pdcch" in legs and rank == 0:
-        pdc = pdcch_receive(s, torch, max(4, args.steps // 2))
-    rxq = None
+        pdc = pdcch_receive(s, torch, max(4, args.steps // 4))
     if "rxq" in legs and rank == 0:
         rxq = rx_queue_leg(s, torch, dev)
-    dropin = None
-    if "dropin" in legs and rank == 0:
+    if "dropin" in legs and rank == 0 and llr is not None:
         dropin = dropin_latency(s, llr)
-    batch.close()
-    if rank == 0 and dropin:
-        result["dropin_latency"] = dropin
-    if rank == 0 and dci:
-        result["pdcch_dci"] = dci
-    if rank == 0 and pcf:
-        result["pcfich"] = pcf
-    if rank == 0 and pdc:
-        result["pdcch"] = pdc
-    if rank == 0 and rxq:
-        result["rx_queue"] = rxq
-    if rank == 0 and dec8:
-        result["decoder_8bit"] = dec8
-    if rank == 0 and pipe:
-        result["config"]["subframes_per_s"] = pipe["subframes_per_s"]
-        result["pipeline"] = pipe
-    if rank == 0 and pipe3:
-        result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
-        result["pipeline_tm3"] = pipe3
-    if rank == 0 and sweep:
-        result["c3_coded_sweep"] = {"workload": "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS),
-                                    "early_stop_max_halfits": 8, "points": sweep}
+    if dec:
+        dec.pop("_batch").close()
+        for k in ("_d_in", "_d_out", "_expect", "_stride"):
+            dec.pop(k)
     if rank == 0:
+        if dec:
+            result["decoder_c2"] = dec
+        for key, val in (("dropin_latency", dropin), ("pdcch_dci", dci), ("pcfich", pcf), ("pdcch", pdc),
+                         ("rx_queue", rxq), ("decoder_8bit", dec8)):
+            if val:
+                result[key] = val
+        if "fixed8" in extra:
+            result["c3_fixed8_codewords"] = extra["fixed8"]
+            result["config"]["subframes_per_s_fixed8"] = extra["fixed8"]["subframes_per_s"]
+        if "n1536" in extra:
+            result["c3_fft1536"] = extra["n1536"]
+        if pipe:
+            result["config"]["subframes_per_s_random_symbols_fixed8"] = pipe["subframes_per_s"]
+            result["pipeline"] = pipe
+        if pipe3:
+            result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
+            result["pipeline_tm3"] = pipe3
+        if sweep:
+            result["c3_coded_sweep"] = {"workload": "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS),
+                                        "early_stop_max_halfits": 8, "points": sweep}
         for kind, key in (("c3_coded", "coded"), ("c5", "c5")):
             if kind in extra:
                 result["config"]["subframes_per_s_" + key] = extra[kind]["subframes_per_s"]
                 result["pipeline_" + key] = extra[kind]
     if rank == 0 and not args.no_cpu_baseline and nranks == 1:
-        result["cpu_baseline"] = cpu_baseline(llr)
-        if dropin:  # the reference's own per-call cost on one pinned thread, for comparison
-            cb = result["cpu_baseline"]
-            per_thread_mbps = cb["value"] / max(cb["cores"], 1)
-            dropin["cpu_reference_us_per_halfit_one_thread"] = round(K / per_thread_mbps / NHALF, 2)
+        if cpu_grids is not None:
+            result["cpu_baseline"] = cpu_baseline_pipeline(cpu_grids, cpu_sf, HEADLINE_SNR_DB)
+        if llr is not None:
+            result["decoder_c2"]["cpu_baseline"] = cpu_baseline(llr)
+            if dropin:  # the reference's own per-call cost on one pinned thread, for comparison
+                cb = result["decoder_c2"]["cpu_baseline"]
+                dropin["cpu_reference_us_per_halfit_one_thread"] = round(K / (cb["value"] / max(cb["cores"], 1)) / NHALF, 2)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

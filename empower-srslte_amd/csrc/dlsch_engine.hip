@@ -132,6 +132,7 @@ struct DlschEngine {
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
   bool llr8 = false; // srslte_sch_t.llr_is_8bit: int8 LLRs, 8-bit de-RM and decoders
+  bool fixed = false; // srsgpu_dlsch_set_early_stop(0): every CB runs max_halfits, one CRC check
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
@@ -441,7 +442,7 @@ struct DlschEngine {
     }
     if (!specs.empty() &&
         tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
-                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi))
+                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed))
       return -1;
     {
       ProfScope ps("k_tb_finish", st);
@@ -684,6 +685,10 @@ int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_ou
 int srsgpu_rm_turbo_rx_8bit_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out,
                                 uint32_t in_len, uint32_t K, uint32_t rv) {
   return rm_rx_dev(q, d_in, d_out, in_len, K, rv, srsgpu::auto_subblocks_8bit(K), true);
+}
+
+void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable) {
+  if (q) q->e.fixed = enable == 0;
 }
 
 void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable) {

@@ -660,7 +660,7 @@ struct TdecEngine {
   int decode_multi(int impl, int sb_layout, const std::vector<TdSpec> &specs, uint32_t total_cbs,
                    const int16_t *d_in, size_t in_stride, const int16_t *const *rows, int rows_aligned,
                    const uint8_t *init_done, uint32_t maxh, uint8_t *d_out, size_t out_stride,
-                   uint8_t *d_ok, uint32_t *d_noi) {
+                   uint8_t *d_ok, uint32_t *d_noi, bool fixed = false) {
     if (maxh == 0 || total_cbs > cap_cbs) {
       fprintf(stderr, "srsgpu: invalid early-stop job (max_halfits=%u, %u code blocks)\n", maxh, total_cbs);
       return -1;
@@ -687,7 +687,11 @@ struct TdecEngine {
         return -1;
       }
       if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs)) return -1;
-      if (decode_planned(maxh, d_out, out_stride)) return -1;
+      if (fixed) { // all maxh half-iterations, then one CRC check (no early stop: measurement mode)
+        if (halfits_fixed((int)maxh) || decide((int)maxh - 1, d_out, out_stride, true, maxh)) return -1;
+      } else if (decode_planned(maxh, d_out, out_stride)) {
+        return -1;
+      }
       first = false;
       s0 = s1;
     }

@@ -339,6 +339,7 @@ _sig = {
     "srsgpu_rxq_submit_ue_dl": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
     "srsgpu_rxq_decode_rnti": (_i32, [_vp, _vp]),
     "srsgpu_rxq_set_phich": (_i32, [_vp, _u32, _u32]),
+    "srsgpu_dlsch_set_early_stop": (None, [_vp, _i32]),
     "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
     "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
@@ -558,6 +559,10 @@ class Dlsch:
              else _lib.srsgpu_dlsch_softbuffer_reset_tbs(self.q, slot, tbs))
         if r != 0:
             raise RuntimeError("softbuffer reset failed")
+
+    def set_early_stop(self, on):
+        """srsgpu_dlsch_set_early_stop (off: every CB runs max_halfits, one CRC check at the end)"""
+        _lib.srsgpu_dlsch_set_early_stop(self.q, int(bool(on)))
 
     def reset_range(self, first, count):
         if _lib.srsgpu_dlsch_softbuffer_reset_range(self.q, first, count) != 0:

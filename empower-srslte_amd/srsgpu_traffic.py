@@ -64,11 +64,14 @@ def tb_weights(table, sf_plan, max_halfits=8):
 
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
-                 snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None):
+                 snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None, standard_rate=True,
+                 early_stop=True):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
         traffic). keep: the subframe indices this instance builds and receives (a rank's shard
-        of one planned job, srsgpu_shard); default all."""
+        of one planned job, srsgpu_shard); default all. standard_rate: the 3GPP FFT sizes (2048 at
+        20 MHz) or srsLTE's reduced ones (1536, srslte_symbol_sz without standard rates).
+        early_stop False: every code block runs max_halfits (srsgpu_dlsch_set_early_stop)."""
         self.torch, self.dev = torch, dev
         self.max_halfits = max_halfits
         sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
@@ -83,7 +86,7 @@ class MixedCells:
             n = len(mine)
             if n == 0:
                 continue
-            N = s.symbol_sz(prb, True)
+            N = s.symbol_sz(prb, standard_rate)
             gsz = 14 * 12 * prb
             c = {"prb": prb, "N": N, "gsz": gsz, "n": n, "id": 1 + ci,
                  "lstart": 2 if prb <= 10 else 1}
@@ -116,6 +119,7 @@ class MixedCells:
         self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
         self.bits = sum(t["tbs"] for t in tb_list)
         self.dlsch = s.Dlsch(max(self.ntb, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
+        self.dlsch.set_early_stop(early_stop)
         z = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         self.d_e = z(max(e_off, 1), torch.int16)
         self.d_data_tx = torch.randint(0, 256, (max(d_off, 1),), dtype=torch.uint8, device=dev,

@@ -99,6 +99,11 @@ int srsgpu_rm_turbo_rx_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_ou
  * 400 < K <= 800 returns -2: the reference's 8-bit AUTO choice has no defined result there
  * (turbodecoder.c:439-459). Softbuffers must not change mode between transmissions of a TB. */
 void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable);
+/* CRC early stop between half-iterations (default on: sch.c:361-391, srsUE's decoder). Off is a
+ * measurement mode with no reference counterpart: every code block runs max_halfits
+ * half-iterations and its CRC is checked once after the last (the fixed-iteration processing rate
+ * on real codewords; nof_iterations then reports max_halfits). */
+void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable);
 /* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469) on device buffers, int8 values held in int16
  * elements: d_out[t[i % (3K+12)]] += d_in[i], wrapping at 8 bits, 8-bit decoder sub-block table. */
 int srsgpu_rm_turbo_rx_8bit_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out,

@@ -20,17 +20,30 @@
  *                            (ue_dl.c:768-932) in phch_worker's order (DL search, then the UL search,
  *                            phch_worker.cc:548-806, 938-967) on ONE srslte_ue_dl_t, and
  *                            srslte_dci_msg_to_ul_grant (dci.c:165-197) of a found UL DCI.
+ *   ref_front pdsch_bench IN OUT   the CPU baseline of BASELINE configs[2] (bench.py): per pthread,
+ *                            pinned to its own CPU, one srslte_chest_dl_t + srslte_pdsch_t +
+ *                            softbuffer, running what srslte_ue_dl_decode_rnti runs after the FFT
+ *                            (ue_dl.c:408-433, 580: srslte_chest_dl_estimate, the noise estimate,
+ *                            srslte_pdsch_cfg, srslte_pdsch_decode with CRC early stop) over given
+ *                            resource grids; prints one JSON line (wall time, subframes, acks,
+ *                            code blocks that passed their CRC).
  *
  * Formats of IN / OUT: see the readers below (little-endian 32-bit words, complex float pairs);
  * tests/srsgpu_testlib.py (ref_front_chest / ref_front_dci) writes and reads them.
  */
+#define _GNU_SOURCE
 #include <complex.h>
+#include <pthread.h>
+#include <sched.h>
+#include <time.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "srslte/phy/ch_estimation/chest_dl.h"
 #include "srslte/phy/phch/dci.h"
+#include "srslte/phy/phch/pdsch.h"
+#include "srslte/phy/phch/ra.h"
 #include "srslte/phy/phch/pdcch.h"
 #include "srslte/phy/phch/ra.h"
 #include "srslte/phy/phch/regs.h"
@@ -271,15 +284,186 @@ static int run_dci(void) {
   return 0;
 }
 
+/* ---------------------------------------------------------------- CPU baseline ---- */
+/* One worker's objects. They are built one after the other on the main thread: srslte_tcod_init /
+ * srslte_tcod_free share unguarded static tables (turbocoder.c:48-79: the first init builds them, any
+ * free releases them), so concurrent set-up races and a second free double-frees; the objects are
+ * never freed (the process exits after the run). */
+typedef struct {
+  srslte_cell_t cell;
+  uint32_t cfi, rnti, mcs, max_noi, nsf, nthreads, reps, cpu;
+  int tid;
+  const uint32_t *sf_idx;
+  const cf_t *grids; /* nsf x SF_LEN_RE */
+  pthread_barrier_t *bar;
+  srslte_chest_dl_t chest;
+  srslte_pdsch_t pdsch;
+  srslte_softbuffer_rx_t sb;
+  uint64_t decoded, acked, cb_ok, cb_bits_ok, noi_sum;
+  int err;
+} bench_arg_t;
+
+static int bench_setup(bench_arg_t *a) {
+  if (srslte_chest_dl_init(&a->chest, a->cell.nof_prb) || srslte_chest_dl_set_cell(&a->chest, a->cell) ||
+      srslte_pdsch_init_ue(&a->pdsch, a->cell.nof_prb, 1) || srslte_pdsch_set_cell(&a->pdsch, a->cell) ||
+      srslte_pdsch_set_rnti(&a->pdsch, (uint16_t)a->rnti) || srslte_softbuffer_rx_init(&a->sb, a->cell.nof_prb))
+    return -1;
+  srslte_pdsch_set_max_noi(&a->pdsch, a->max_noi);
+  return 0;
+}
+
+static void *bench_thread(void *p) {
+  bench_arg_t *a = (bench_arg_t *)p;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(a->cpu, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  const uint32_t n = SRSLTE_SF_LEN_RE(a->cell.nof_prb, a->cell.cp);
+  srslte_chest_dl_t *chest = &a->chest;
+  srslte_pdsch_t *pdsch = &a->pdsch;
+  srslte_softbuffer_rx_t *sb = &a->sb;
+  cf_t *sf = srslte_vec_malloc(sizeof(cf_t) * n), *ce[SRSLTE_MAX_PORTS] = {NULL};
+  ce[0] = srslte_vec_malloc(sizeof(cf_t) * n);
+  cf_t *sf_m[SRSLTE_MAX_PORTS] = {sf, NULL, NULL, NULL};
+  cf_t *ce_m[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{ce[0], NULL}, {NULL}};
+  uint8_t *data[SRSLTE_MAX_CODEWORDS] = {srslte_vec_malloc(128 * 1024) /* >= TBS / 8 of any grant */, NULL};
+  srslte_softbuffer_rx_t *sbs[SRSLTE_MAX_CODEWORDS] = {sb, NULL};
+  srslte_ra_dl_grant_t grant;
+  memset(&grant, 0, sizeof(grant));
+  grant.nof_prb = a->cell.nof_prb;
+  for (int sl = 0; sl < 2; sl++)
+    for (uint32_t q = 0; q < a->cell.nof_prb; q++) grant.prb_idx[sl][q] = true;
+  grant.tb_en[0] = true;
+  grant.mcs[0].idx = a->mcs;
+  grant.mcs[0].mod = srslte_ra_mod_from_mcs(a->mcs);
+  grant.mcs[0].tbs = srslte_ra_tbs_from_idx(srslte_ra_tbs_idx_from_mcs(a->mcs), a->cell.nof_prb);
+  grant.Qm[0] = srslte_mod_bits_x_symbol(grant.mcs[0].mod);
+  pthread_barrier_wait(a->bar);
+  for (uint32_t r = 0; r < a->reps && !a->err; r++) {
+    for (uint32_t i = (uint32_t)a->tid; i < a->nsf; i += a->nthreads) {
+      /* srslte_ue_dl_decode_estimate after the FFT (ue_dl.c:408-433), then ue_dl.c:580 */
+      memcpy(sf, a->grids + (size_t)i * n, sizeof(cf_t) * n);
+      if (srslte_chest_dl_estimate(chest, sf, ce, a->sf_idx[i])) {
+        a->err = 2;
+        break;
+      }
+      const float noise = srslte_chest_dl_get_noise_estimate(chest);
+      srslte_pdsch_cfg_t cfg;
+      if (srslte_pdsch_cfg(&cfg, a->cell, &grant, a->cfi, a->sf_idx[i], 0)) {
+        a->err = 3;
+        break;
+      }
+      srslte_softbuffer_rx_reset(sb); /* a new transport block every subframe */
+      bool acks[SRSLTE_MAX_CODEWORDS] = {false, false};
+      if (srslte_pdsch_decode(pdsch, &cfg, sbs, sf_m, ce_m, noise, (uint16_t)a->rnti, data, acks)) {
+        a->err = 4;
+        break;
+      }
+      a->decoded++;
+      a->acked += acks[0];
+      a->noi_sum += srslte_pdsch_last_noi_cw(pdsch, 0);
+      for (uint32_t c = 0; c < cfg.cb_segm[0].C; c++)
+        if (sb->cb_crc[c]) {
+          a->cb_ok++;
+          a->cb_bits_ok += c < cfg.cb_segm[0].C2 ? cfg.cb_segm[0].K2 : cfg.cb_segm[0].K1;
+        }
+    }
+  }
+  free(sf);
+  free(ce[0]);
+  free(data[0]);
+  return NULL;
+}
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* IN: nof_prb id cfi rnti mcs max_noi nthreads reps nsf ncpu cpus[ncpu] | nsf x {sf_idx, grid cf32}
+ * (one rx antenna, one port: BASELINE configs[2]). OUT (text): one JSON object */
+static int run_pdsch_bench(void) {
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = rd_u32();
+  cell.id = rd_u32();
+  cell.nof_ports = 1;
+  cell.cp = SRSLTE_CP_NORM;
+  cell.phich_length = SRSLTE_PHICH_NORM;
+  cell.phich_resources = SRSLTE_PHICH_R_1;
+  const uint32_t cfi = rd_u32(), rnti = rd_u32(), mcs = rd_u32(), max_noi = rd_u32(), nthreads = rd_u32(),
+                 reps = rd_u32(), nsf = rd_u32(), ncpu = rd_u32();
+  if (!nthreads || !nsf || !ncpu || ncpu > 4096) return -1;
+  uint32_t *cpus = malloc(sizeof(uint32_t) * ncpu), *sfi = malloc(sizeof(uint32_t) * nsf);
+  for (uint32_t i = 0; i < ncpu; i++) cpus[i] = rd_u32();
+  const uint32_t n = SRSLTE_SF_LEN_RE(cell.nof_prb, cell.cp);
+  cf_t *grids = srslte_vec_malloc(sizeof(cf_t) * n * nsf);
+  for (uint32_t i = 0; i < nsf; i++) {
+    sfi[i] = rd_u32();
+    rd_buf(grids + (size_t)i * n, sizeof(cf_t) * n);
+  }
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, nthreads + 1);
+  bench_arg_t *args = calloc(nthreads, sizeof(bench_arg_t));
+  pthread_t *th = malloc(sizeof(pthread_t) * nthreads);
+  for (uint32_t t = 0; t < nthreads; t++) {
+    bench_arg_t *a = &args[t];
+    a->cell = cell;
+    a->cfi = cfi;
+    a->rnti = rnti;
+    a->mcs = mcs;
+    a->max_noi = max_noi;
+    a->nsf = nsf;
+    a->nthreads = nthreads;
+    a->reps = reps;
+    a->cpu = cpus[t % ncpu];
+    a->tid = (int)t;
+    a->sf_idx = sfi;
+    a->grids = grids;
+    a->bar = &bar;
+    if (bench_setup(a)) return -1;
+  }
+  for (uint32_t t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, bench_thread, &args[t]);
+  pthread_barrier_wait(&bar); /* every thread has built its objects */
+  const double t0 = now_s();
+  for (uint32_t t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+  const double wall = now_s() - t0;
+  uint64_t dec = 0, ack = 0, cbok = 0, bits = 0, noi = 0;
+  int err = 0;
+  for (uint32_t t = 0; t < nthreads; t++) {
+    dec += args[t].decoded;
+    ack += args[t].acked;
+    cbok += args[t].cb_ok;
+    bits += args[t].cb_bits_ok;
+    noi += args[t].noi_sum;
+    err |= args[t].err;
+  }
+  fprintf(fout,
+          "{\"wall_s\": %.6f, \"subframes\": %llu, \"acked\": %llu, \"cb_ok\": %llu, \"cb_bits_ok\": %llu, "
+          "\"noi_mean\": %.4f, \"threads\": %u, \"error\": %d}\n",
+          wall, (unsigned long long)dec, (unsigned long long)ack, (unsigned long long)cbok, (unsigned long long)bits,
+          dec ? (double)noi / (double)dec : 0.0, nthreads, err);
+  free(args);
+  free(th);
+  free(grids);
+  free(cpus);
+  free(sfi);
+  return err ? -1 : 0;
+}
+
 int main(int argc, char **argv) {
   if (argc != 4) {
-    fprintf(stderr, "usage: ref_front chest|dci IN OUT\n");
+    fprintf(stderr, "usage: ref_front chest|dci|pdsch_bench IN OUT\n");
     return 2;
   }
   fin = fopen(argv[2], "rb");
   fout = fopen(argv[3], "wb");
   if (!fin || !fout) return 2;
-  int r = !strcmp(argv[1], "chest") ? run_chest() : !strcmp(argv[1], "dci") ? run_dci() : -1;
+  int r = !strcmp(argv[1], "chest")         ? run_chest()
+          : !strcmp(argv[1], "dci")         ? run_dci()
+          : !strcmp(argv[1], "pdsch_bench") ? run_pdsch_bench()
+                                            : -1;
   fclose(fin);
   fclose(fout);
   return r ? 1 : 0;
