@@ -310,9 +310,12 @@ struct PdschEngine {
     return 0;
   }
 
-  // srslte_pdsch_encode (pdsch.c:1048-1131), single antenna port: DL-SCH encoding of each TB,
-  // then scrambling, modulation and RE mapping into the subframe's grid (other REs untouched)
-  int encode(const srsgpu_pdsch_sf_t *sf, uint32_t n, const uint8_t *d_data, float *d_grid) {
+  // srslte_pdsch_encode (pdsch.c:1048-1131): DL-SCH encoding of each TB (codeword cw = tb ^ tb_cw_swap
+  // with two TBs, pdsch.c:1083-1089), then per RE the codewords' scrambled symbols, layer mapping and
+  // precoding of the MIMO type, mapped into every port's grid (port p at grid_offset + p port_stride;
+  // other REs untouched). Single antenna, transmit diversity (2 ports), CDD (2 ports, 2 TBs) and
+  // spatial multiplexing (2 ports, 1 TB on 1 layer or 2 TBs on 2 layers, codebook_idx).
+  int encode(const srsgpu_pdsch_sf_t *sf, uint32_t n, const uint8_t *d_data, float *d_grid, uint64_t port_stride) {
     if (n > max_sf) {
       fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
       return -1;
@@ -320,7 +323,7 @@ struct PdschEngine {
     if (!h_tx) {
       HIPCHK(hipHostMalloc(&h_tx, sizeof(TxItem) * max_sf));
       HIPCHK(hipMalloc(&d_tx, sizeof(TxItem) * max_sf));
-      HIPCHK(hipMalloc(&d_ebits, (size_t)max_sf * max_bits + 64));
+      HIPCHK(hipMalloc(&d_ebits, (size_t)2 * max_sf * max_bits + 64));
       // modem/lte_tables.c: levels k / sqrt(N) in double, stored as float; 36.211 7.1 bit order
       std::vector<float2> t;
       const float b = (float)(1 / sqrt(2.0));
@@ -342,12 +345,16 @@ struct PdschEngine {
       HIPCHK(hipMemcpy(d_mod, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
-    uint32_t mre = 0, mbits = 0;
+    uint32_t mre = 0, mbits = 0, k = 0;
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
-      if (s.mimo_type != SRSGPU_MIMO_SINGLE_ANTENNA) {
-        fprintf(stderr, "srsgpu: the GPU transmitter covers single-antenna PDSCH\n");
+      if (s.mimo_type != SRSGPU_MIMO_SINGLE_ANTENNA && port_stride < (uint64_t)14 * 12 * cell.nof_prb) {
+        fprintf(stderr, "srsgpu: a %u-port transmission needs a port stride of at least one grid\n", cell.nof_ports);
+        return -1;
+      }
+      if (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.codebook_idx > (s.tbs[1] > 0 ? 2u : 3u)) {
+        fprintf(stderr, "Invalid multiplex combination: codebook_idx=%u\n", s.codebook_idx); // precoding.c:2009
         return -1;
       }
       uint32_t nre = 0;
@@ -357,36 +364,53 @@ struct PdschEngine {
         fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
         return -1;
       }
-      const int q = kQm[s.mod[0]];
-      srsgpu_dlsch_tb_t &t = h_tb[i];
-      t.tbs = s.tbs[0];
-      t.rv = s.rv[0];
-      t.Qm = (uint32_t)q;
-      t.nof_e_bits = nre * q;
-      t.softbuffer = 0;
-      t.e_offset = (uint64_t)i * max_bits;
-      t.data_offset = s.data_offset[0];
-      GoldItem &g = h_gold[i];
-      g.seed = ((uint32_t)s.rnti << 14) + ((2 * s.sf_idx / 2) << 9) + cell.id;
-      g.len = nre * q;
-      g.c = d_c + (size_t)i * cwords;
+      const uint32_t ntb = nof_tb(s);
+      const float sc = s.scaling != 0.f ? s.scaling : 1.0f;
       TxItem &x = h_tx[i];
-      x.e = d_ebits + (size_t)i * max_bits;
-      x.c = g.c;
+      memset(&x, 0, sizeof(x));
+      for (uint32_t tb = 0; tb < ntb; tb++, k++) {
+        const uint32_t cw = ntb == 2 ? (tb ^ (s.tb_cw_swap ? 1u : 0u)) : 0u;
+        const int q = kQm[s.mod[tb]];
+        srsgpu_dlsch_tb_t &t = h_tb[k];
+        t.tbs = s.tbs[tb];
+        t.rv = s.rv[tb];
+        t.Qm = (uint32_t)q;
+        t.nof_e_bits = nre * q;
+        t.softbuffer = 0;
+        t.e_offset = (uint64_t)k * max_bits;
+        t.data_offset = s.data_offset[tb];
+        GoldItem &g = h_gold[k]; // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID, q = codeword
+        g.seed = ((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id;
+        g.len = nre * q;
+        g.c = d_c + (size_t)k * cwords;
+        x.e[cw] = d_ebits + (size_t)k * max_bits;
+        x.c[cw] = g.c;
+        x.qm[cw] = q;
+        mbits = std::max(mbits, nre * q);
+      }
       x.map = m;
       x.grid = (float2 *)d_grid + s.grid_offset;
+      x.port_stride = port_stride;
       x.nof_re = nre;
-      x.qm = q;
-      x.scaling = s.scaling != 0.f ? s.scaling : 1.0f;
+      x.mimo = (int)s.mimo_type;
+      x.nlayers = s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX ? (int)ntb : (int)cell.nof_ports;
+      x.codebook = (int)s.codebook_idx;
+      switch (s.mimo_type) {
+      case SRSGPU_MIMO_TX_DIVERSITY: x.scaling = sc / sqrtf(2.0f); break;
+      case SRSGPU_MIMO_CDD: x.scaling = 0.5f * sc; break;
+      case SRSGPU_MIMO_SPATIAL_MULTIPLEX:
+        x.scaling = (ntb == 1 || s.codebook_idx == 0) ? sc / sqrtf(2.0f) : sc / 2.0f;
+        break;
+      default: x.scaling = sc;
+      }
       mre = std::max(mre, nre);
-      mbits = std::max(mbits, nre * q);
     }
-    if (srsgpu_dlsch_encode_dev(dl, h_tb, n, d_data, d_ebits)) return -1;
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * n, hipMemcpyHostToDevice, st));
+    if (srsgpu_dlsch_encode_dev(dl, h_tb, k, d_data, d_ebits)) return -1;
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * k, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    HIPCHK(launch_gold(d_gold, (int)n, mbits, d_x1, d_x2b, gold_words, st));
+    HIPCHK(launch_gold(d_gold, (int)k, mbits, d_x1, d_x2b, gold_words, st));
     ProfScope ps("k_pdsch_tx", st);
     HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));
     return 0;
@@ -470,7 +494,13 @@ int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_
 int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n,
                             const uint8_t *d_data, float *d_grid) {
   if (!q || (!sf && n) || !d_data || !d_grid) return -1;
-  return q->e.encode(sf, n, d_data, d_grid);
+  return q->e.encode(sf, n, d_data, d_grid, 0);
+}
+
+int srsgpu_pdsch_encode_ports_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const uint8_t *d_data,
+                                  float *d_grid, size_t port_stride) {
+  if (!q || (!sf && n) || !d_data || !d_grid) return -1;
+  return q->e.encode(sf, n, d_data, d_grid, (uint64_t)port_stride);
 }
 
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,

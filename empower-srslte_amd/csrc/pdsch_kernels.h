@@ -42,13 +42,16 @@ struct LlrItem {
 
 // one codeword to transmit: scramble + modulate + map
 struct TxItem {
-  const uint8_t *e;        // nof_re * qm coded bits, one per byte
-  const uint32_t *c;       // packed scrambling bits
+  const uint8_t *e[2];     // per codeword: nof_re * qm coded bits, one per byte
+  const uint32_t *c[2];    // per codeword: packed scrambling bits
   const uint32_t *map;     // RE j -> grid position
   float2 *grid;            // port-0 grid of the subframe
+  uint64_t port_stride;    // complex elements between the ports' grids
   uint32_t nof_re;
-  int qm;
-  float scaling;
+  int qm[2];
+  int mimo;                // SRSGPU_MIMO_*
+  int nlayers, codebook;   // spatial multiplexing
+  float scaling;           // rho_a
 };
 
 hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,

@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "pdsch_kernels.h"
+#include "srsgpu/pdsch_batch.h"
 #include "gmem.h"
 
 // The equaliser must round like the reference's separate SSE/AVX multiplies and adds: no FMA
@@ -708,24 +709,85 @@ hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool
 }
 
 // ------------------------------------------------------------------ transmit ----
-// srslte_pdsch_encode for one single-antenna codeword (pdsch.c:1048-1131): scrambling of the
-// coded bits (srslte_scrambling_bytes), modulation (srslte_mod_modulate_bytes with the LTE tables
-// of modem/lte_tables.c: index = bits MSB first), optional rho_a scaling, RE mapping (pdsch_put).
+// srslte_pdsch_encode (pdsch.c:1048-1131) after the DL-SCH encoding: per codeword scrambling
+// (srslte_scrambling_bytes, the codeword's own sequence) and modulation (srslte_mod_modulate_bytes with
+// the LTE tables of modem/lte_tables.c: index = bits MSB first), layer mapping and precoding
+// (srslte_layermap_type / srslte_precoding_type, mimo/layermap.c:43-130, mimo/precoding.c:1849-2143),
+// rho_a scaling and the RE mapping of every port (srslte_pdsch_put). One thread per RE j: it builds the
+// codeword symbols it needs and writes port p's value at grid + p * port_stride + map[j].
+__device__ __forceinline__ float2 tx_symbol(const TxItem &t, int cw, uint32_t j, const float2 *tables) {
+  const int qm = t.qm[cw];
+  const float2 *tab = tables + (qm == 1 ? 0 : qm == 2 ? 2 : qm == 4 ? 6 : 22);
+  const uint32_t b0 = j * (uint32_t)qm, w = b0 >> 5, sh = b0 & 31;
+  const uint64_t cw64 = (uint64_t)t.c[cw][w] | ((uint64_t)t.c[cw][w + 1] << 32);
+  const uint32_t cb = (uint32_t)(cw64 >> sh);
+  uint32_t idx = 0;
+  for (int k = 0; k < qm; k++) idx = (idx << 1) | ((t.e[cw][b0 + k] ^ (cb >> k)) & 1u);
+  return tab[idx];
+}
+__device__ __forceinline__ float2 cscale(float2 v, float k) { return make_float2(__fmul_rn(v.x, k), __fmul_rn(v.y, k)); }
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(__fadd_rn(a.x, b.x), __fadd_rn(a.y, b.y)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(__fsub_rn(a.x, b.x), __fsub_rn(a.y, b.y)); }
+
 __global__ __launch_bounds__(256) void k_pdsch_tx(const TxItem *__restrict__ items, int nitems,
                                                   const float2 *__restrict__ tables) {
   const int it = blockIdx.y;
   if (it >= nitems) return;
   const TxItem t = items[it];
-  const float2 *tab = tables + (t.qm == 1 ? 0 : t.qm == 2 ? 2 : t.qm == 4 ? 6 : 22);
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += gridDim.x * 256) {
-    const uint32_t b0 = j * (uint32_t)t.qm, w = b0 >> 5, sh = b0 & 31;
-    const uint64_t cw = (uint64_t)t.c[w] | ((uint64_t)t.c[w + 1] << 32);
-    const uint32_t cb = (uint32_t)(cw >> sh);
-    uint32_t idx = 0;
-    for (int k = 0; k < t.qm; k++) idx = (idx << 1) | ((t.e[b0 + k] ^ (cb >> k)) & 1u);
-    float2 v = tab[idx];
-    if (t.scaling != 1.0f) v = make_float2(v.x * t.scaling, v.y * t.scaling);
-    t.grid[t.map[j]] = v;
+    float2 y0, y1 = make_float2(0.f, 0.f);
+    bool two = true;
+    switch (t.mimo) {
+    case SRSGPU_MIMO_TX_DIVERSITY: { // layermap_diversity + 2-port SFBC, scaled by rho_a / sqrt 2
+      const uint32_t j0 = j & ~1u;
+      if (j0 + 1 >= t.nof_re) continue; // 2 floor(n / 2) symbols per port (precoding.c:1853-1862)
+      const float2 a = tx_symbol(t, 0, j0, tables), b = tx_symbol(t, 0, j0 + 1, tables);
+      const float k = t.scaling; // scaling / sqrtf(2) on the host
+      if (j == j0) {
+        y0 = cscale(a, k);
+        y1 = cscale(make_float2(-b.x, b.y), k); // -conj(x1)
+      } else {
+        y0 = cscale(b, k);
+        y1 = cscale(make_float2(a.x, -a.y), k); // conj(x0)
+      }
+      break;
+    }
+    case SRSGPU_MIMO_CDD: { // precoding_cdd_2x2 (precoding.c:1898-1958), layers = codewords
+      const float2 x0 = tx_symbol(t, 0, j, tables), x1 = tx_symbol(t, 1, j, tables);
+      const float k = t.scaling; // 0.5 scaling
+      y0 = cscale(cadd(x0, x1), k);
+      y1 = cscale((j & 1) ? csub(x1, x0) : csub(x0, x1), k);
+      break;
+    }
+    case SRSGPU_MIMO_SPATIAL_MULTIPLEX: { // precoding_multiplex 2 ports (precoding.c:1985-2100)
+      const float k = t.scaling; // scaling / sqrt 2 (one layer, codebook 0 of two), scaling / 2 otherwise
+      const float2 x0 = tx_symbol(t, 0, j, tables);
+      if (t.nlayers == 1) {
+        y0 = cscale(x0, k);
+        y1 = t.codebook == 0 ? y0 : t.codebook == 1 ? cscale(x0, -k)
+             : t.codebook == 2 ? make_float2(-__fmul_rn(x0.y, k), __fmul_rn(x0.x, k))   // x (j k)
+                               : make_float2(__fmul_rn(x0.y, k), -__fmul_rn(x0.x, k)); // x (-j k)
+      } else {
+        const float2 x1 = tx_symbol(t, 1, j, tables);
+        if (t.codebook == 0) {
+          y0 = cscale(x0, k);
+          y1 = cscale(x1, k);
+        } else {
+          y0 = cscale(cadd(x0, x1), k);
+          const float2 d = csub(x0, x1);
+          y1 = t.codebook == 1 ? cscale(d, k) : cscale(make_float2(-d.y, d.x), k); // j (x0 - x1)
+        }
+      }
+      break;
+    }
+    default: // single antenna port
+      y0 = tx_symbol(t, 0, j, tables);
+      if (t.scaling != 1.0f) y0 = cscale(y0, t.scaling);
+      two = false;
+    }
+    const uint32_t m = t.map[j];
+    t.grid[m] = y0;
+    if (two) t.grid[t.port_stride + m] = y1;
   }
 }
 

@@ -367,6 +367,7 @@ _sig = {
     "srsgpu_ofdm_rx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
     "srsgpu_ofdm_tx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
     "srsgpu_chest_put_crs_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz]),
+    "srsgpu_pdsch_encode_ports_dev": (_i32, [_vp, _vp, _u32, _vp, _vp, _sz]),
     "srsgpu_pdsch_encode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp]),
     "srsgpu_prof_enable": (None, [_i32]),
     "srsgpu_prof_reset": (None, []),
@@ -884,10 +885,13 @@ class Pdsch:
         return _lib.srsgpu_pdsch_llr_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                          _vp(d_e), offs)
 
-    def encode_dev(self, sfs, d_data, d_grid):
-        """srsgpu_pdsch_encode_dev: TB bytes (data_offset[0]) -> PDSCH REs of each grid"""
-        arr = make_sf_array(sfs)
-        return _lib.srsgpu_pdsch_encode_dev(self.q, arr, len(sfs), _vp(d_data), _vp(d_grid))
+    def encode_dev(self, sfs, d_data, d_grid, port_stride=None):
+        """srsgpu_pdsch_encode_dev: TB bytes (data_offset[0]) -> PDSCH REs of each grid; with port_stride
+        srsgpu_pdsch_encode_ports_dev (every MIMO type, port p's grid port_stride elements after p - 1)"""
+        arr, n = (sfs if isinstance(sfs, tuple) else (make_sf_array(sfs), len(sfs)))
+        if port_stride is None:
+            return _lib.srsgpu_pdsch_encode_dev(self.q, arr, n, _vp(d_data), _vp(d_grid))
+        return _lib.srsgpu_pdsch_encode_ports_dev(self.q, arr, n, _vp(d_data), _vp(d_grid), port_stride)
 
     def decode_dev(self, sfs, d_grid, d_ce, ant_stride, d_data, max_halfits, d_ret, d_noi):
         arr = make_sf_array(sfs)

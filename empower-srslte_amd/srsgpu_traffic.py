@@ -206,3 +206,122 @@ class MixedCells:
                 c[k].close()
         self.dlsch.close()
 
+
+
+class MimoSubframes:
+    """Coded two-port subframes on one GPU (BASELINE configs[3] as real codewords): n subframes of a
+    20 MHz cell with 2 CRS ports and 2 rx antennas, each carrying the full-band PDSCH of one MIMO type
+    (default TM3 large-delay CDD with two MCS-28 TBs of TBS 75376, tb_cw_swap on odd subframes).
+
+    Transmit side (untimed, on the GPU): srsgpu_pdsch_encode_ports_dev (DL-SCH encoding, per-codeword
+    scrambling and modulation, CDD / transmit-diversity / codebook precoding into both ports' grids),
+    the CRS of both ports (srsgpu_chest_put_crs_dev), OFDM TX per port, a 2x2 flat channel per
+    subframe (well conditioned, random phases) and AWGN at snr_db.
+    Receive step: OFDM FFT of both antennas, channel estimation of both ports on each antenna, PDSCH
+    (2x2 MMSE for CDD / spatial multiplexing, SFBC for transmit diversity) and DL-SCH with CRC early
+    stop, all through srsgpu_pdsch_decode_dev. keep: the subframe indices of a global job this instance
+    handles (a rank's shard); subframe i's content depends only on i."""
+
+    def __init__(self, torch, dev, n_sf, seed=31, stream=None, snr_db=30.0, mimo=None, mcs=28, nof_prb=100,
+                 cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True):
+        import ctypes as ct
+        self.torch, self.dev, self.max_halfits = torch, dev, max_halfits
+        mimo = s.MIMO_CDD if mimo is None else mimo
+        self.kept = sorted(set(range(n_sf)) if keep is None else set(int(k) for k in keep))
+        n = len(self.kept)
+        self.n = n
+        self.nof_prb, self.cell_id = nof_prb, cell_id
+        N = s.symbol_sz(nof_prb, True)
+        self.N, gsz = N, 14 * 12 * nof_prb
+        self.gsz = gsz
+        ntb = 1 if mimo == s.MIMO_TX_DIVERSITY else nof_tb
+        self.ntb = ntb
+        tbs = s._lib.srsgpu_ra_tbs_from_idx(s._lib.srsgpu_ra_tbs_idx_from_mcs(mcs), nof_prb)
+        mod = 1 if mcs < 10 else 2 if mcs < 17 else 3
+        self.tbs = tbs
+        self.ofdm = s.OfdmRx(nof_prb, N, stream=stream)
+        self.chest = s.Chest(nof_prb, cell_id, max_grids=2 * n, stream=stream, nof_ports=2)
+        self.pd = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=2, nof_softbuffers=2 * n, max_cb=13, max_sf=n,
+                          stream=stream)
+        s._lib.srsgpu_dlsch_set_early_stop(s._vp(self.pd.dlsch_q), int(bool(early_stop)))
+        dlen = s.dlsch_data_len(tbs) + 2
+        self.dlen = dlen
+        sfs = []
+        for j, i in enumerate(self.kept):
+            sfi = 1 + (i % 4)
+            sf = s.make_sf(sf_idx=sfi, lstart=1, nof_prb=nof_prb, mod=(mod, mod), rnti=1234,
+                           tbs=(tbs, tbs if ntb == 2 else 0), softbuffer=(2 * j, 2 * j + 1), mimo=mimo,
+                           grid_offset=j * 2 * gsz, ce_offset=j * 4 * gsz,
+                           data_offset=(2 * j * dlen, (2 * j + 1) * dlen), tb_cw_swap=i % 2 if ntb == 2 else 0,
+                           codebook_idx=codebook if mimo == s.MIMO_SPATIAL_MULTIPLEX else 0)
+            sf.nof_re = self.pd.nof_re(sf)
+            sfs.append(sf)
+        self.sfs = s.make_sf_array(sfs)
+        self.nre = sfs[0].nof_re
+        self.grid_sf = (ct.c_uint32 * (2 * n))(*[1 + (i % 4) for i in self.kept for _ in range(2)])
+        z = lambda k, dt: torch.zeros(k, dtype=dt, device=dev)  # noqa: E731
+        # TB bytes: subframe i's content is a function of i (the same on every rank)
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        base = torch.randint(0, 256, (16, 2, dlen), dtype=torch.uint8, generator=g)
+        idx = torch.tensor([i % 16 for i in self.kept])
+        self.d_data_tx = base[idx].reshape(-1).to(dev)
+        self.d_data = z(2 * n * dlen, torch.uint8)
+        self.d_ret = z(2 * n, torch.int32)
+        self.d_noi = z(2 * n, torch.int32)
+        self.grid = z(2 * n * gsz, torch.complex64)
+        self.ce = z(4 * n * gsz, torch.complex64)
+        self.noise = z(4 * n, torch.float32)
+        self.x = z(2 * n * 15 * N, torch.complex64)
+        self.pd.set_noise_dev(self.noise.data_ptr())
+        self._transmit(snr_db, seed, stream)
+
+    def _transmit(self, snr_db, seed, stream):
+        torch, n, gsz, N = self.torch, self.n, self.gsz, self.N
+        txg = torch.zeros(2 * n * gsz, dtype=torch.complex64, device=self.dev)  # [sf][port] grids
+        assert self.pd.encode_dev((self.sfs, n), self.d_data_tx.data_ptr(), txg.data_ptr(), port_stride=gsz) == 0
+        assert self.chest.put_crs_dev(self.grid_sf, txg.data_ptr(), gsz) == 0  # [sf][port] planes
+        xp = torch.zeros(2 * n * 15 * N, dtype=torch.complex64, device=self.dev)
+        assert self.ofdm.tx_dev(2 * n, txg.data_ptr(), gsz, xp.data_ptr(), 15 * N) == 0
+        torch.cuda.synchronize(self.dev)
+        del txg
+        xp = xp.reshape(n, 2, 15 * N)
+        # a flat 2x2 channel per subframe, from the subframe's global index
+        g = torch.Generator(device="cpu").manual_seed(seed + 7)
+        ph = torch.rand(16, 2, 2, generator=g) * 6.283
+        amp = torch.tensor([[1.0, 0.45], [0.45, 1.0]])
+        H = (amp * torch.exp(1j * ph)).to(torch.complex64)
+        Hs = H[torch.tensor([i % 16 for i in self.kept])].to(self.dev)  # [sf][rx][port]
+        y = torch.einsum("sap,spt->sat", Hs, xp)
+        del xp
+        p = y.abs().pow(2).mean().item()
+        sd = float(np.sqrt(p / 10 ** (snr_db / 10) / 2))
+        gn = torch.Generator(device=self.dev).manual_seed(seed + 11)
+        y += (sd * torch.randn(y.shape, dtype=torch.complex64, device=self.dev, generator=gn)).to(torch.complex64)
+        self.x.copy_(y.reshape(-1))
+        torch.cuda.synchronize(self.dev)
+
+    def step(self):
+        n, gsz, N = self.n, self.gsz, self.N
+        self.pd.reset_softbuffer(0, 2 * n)  # new TBs
+        assert self.ofdm.rx_dev(2 * n, self.x.data_ptr(), 15 * N, self.grid.data_ptr(), gsz) == 0
+        assert self.chest.estimate_dev(self.grid_sf, self.grid.data_ptr(), gsz, self.ce.data_ptr(),
+                                       self.noise.data_ptr()) == 0
+        assert self.pd.decode_dev(self.sfs, self.grid.data_ptr(), self.ce.data_ptr(), gsz, self.d_data.data_ptr(),
+                                  self.max_halfits, self.d_ret.data_ptr(), self.d_noi.data_ptr()) == 0
+
+    def check(self):
+        """(acked TBs, TBs whose bytes equal the transmitted ones, mean nof_iterations)"""
+        ret = self.d_ret.cpu().numpy()[:self.ntb * self.n] if self.ntb == 2 else self.d_ret.cpu().numpy()[:self.n]
+        tx, rx = self.d_data_tx.cpu().numpy(), self.d_data.cpu().numpy()
+        good = 0
+        nb = self.tbs // 8
+        for k, r in enumerate(ret):
+            j, t = (k // 2, k % 2) if self.ntb == 2 else (k, 0)
+            o = (2 * j + t) * self.dlen
+            good += int(r == 0 and (tx[o:o + nb] == rx[o:o + nb]).all())
+        noi = self.d_noi.cpu().numpy()[:len(ret)]
+        return int((ret == 0).sum()), good, float(noi.mean())
+
+    def close(self):
+        for h in (self.ofdm, self.chest, self.pd):
+            h.close()

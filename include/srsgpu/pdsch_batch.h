@@ -116,6 +116,16 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
  * as they are: srsgpu_chest_put_crs_dev writes the CRS. */
 int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
                             const uint8_t *d_data, float *d_grid);
+/* The same for every MIMO type of the receiver (srslte_pdsch_encode with srslte_layermap_type and
+ * srslte_precoding_type, pdsch.c:1048-1131, layermap.c:43-130, precoding.c:1849-2143): per TB the DL-SCH
+ * encoding (rv, data at data_offset[tb]), each codeword (cw = tb ^ tb_cw_swap with two TBs) scrambled
+ * with its own sequence and modulated, then single antenna, transmit diversity (2-port SFBC), large-delay
+ * CDD (2 ports, 2 TBs) or codebook precoding (2 ports, codebook_idx; 1 TB on 1 layer or 2 TBs on 2
+ * layers), rho_a scaling, and the RE mapping of every port: port p of subframe i at
+ * d_grid + sf[i].grid_offset + p * port_stride. Transmit diversity with an odd RE count leaves the last
+ * RE of each port as it is (the reference precodes 2 floor(n / 2) symbols). */
+int srsgpu_pdsch_encode_ports_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
+                                  const uint8_t *d_data, float *d_grid, size_t port_stride);
 
 /* RE count of a grant (srslte_pdsch_get's return value). */
 int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf);

@@ -1022,3 +1022,113 @@ int ref_pdcch_locations(uint32_t nof_cce, uint32_t sf_idx, uint16_t rnti, int co
   }
   return (int)n;
 }
+
+/* ---------------------------------------------------------------- PDSCH with MIMO ---------- */
+/* the grant of a full-band allocation with tb_en / mcs per TB (ra.c's tables), CFI lstart */
+static void ref_full_grant(srslte_ra_dl_grant_t *g, uint32_t nof_prb, uint32_t nof_tb, const uint32_t *mcs,
+                           uint32_t tb_cw_swap) {
+  memset(g, 0, sizeof(*g));
+  g->nof_prb = nof_prb;
+  for (int s = 0; s < 2; s++)
+    for (uint32_t p = 0; p < nof_prb; p++) g->prb_idx[s][p] = true;
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    g->tb_en[t] = true;
+    g->mcs[t].idx = mcs[t];
+    g->mcs[t].mod = srslte_ra_mod_from_mcs(mcs[t]);
+    g->mcs[t].tbs = srslte_ra_tbs_from_idx(srslte_ra_tbs_idx_from_mcs(mcs[t]), nof_prb);
+    g->Qm[t] = srslte_mod_bits_x_symbol(g->mcs[t].mod);
+  }
+  g->tb_cw_swap = tb_cw_swap != 0;
+}
+
+/* srslte_pdsch_encode (pdsch.c:1048-1131) of a full-band grant: mimo_type srslte_mimo_type_t, pmi as
+ * srslte_pdsch_cfg_mimo takes it, data per TB; port p's grid (14 x 12 nof_prb cf32) written at
+ * grids + p * 2 * SF_LEN_RE floats (REs outside the grant untouched). Returns the RE count or -1. */
+int ref_pdsch_encode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t cfi, uint32_t sf_idx,
+                     uint16_t rnti, uint32_t mimo_type, uint32_t pmi, uint32_t tb_cw_swap, uint32_t nof_tb,
+                     const uint32_t *mcs, const uint32_t *rv, const uint8_t *data0, const uint8_t *data1,
+                     float *grids) {
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = nof_ports;
+  cell.cp = SRSLTE_CP_NORM;
+  cell.phich_length = SRSLTE_PHICH_NORM;
+  cell.phich_resources = SRSLTE_PHICH_R_1;
+  srslte_pdsch_t q;
+  if (srslte_pdsch_init_enb(&q, nof_prb) || srslte_pdsch_set_cell(&q, cell) || srslte_pdsch_set_rnti(&q, rnti))
+    return -1;
+  srslte_ra_dl_grant_t g;
+  ref_full_grant(&g, nof_prb, nof_tb, mcs, tb_cw_swap);
+  srslte_pdsch_cfg_t cfg;
+  int rvs[SRSLTE_MAX_CODEWORDS] = {(int)rv[0], nof_tb > 1 ? (int)rv[1] : 0};
+  if (srslte_pdsch_cfg_mimo(&cfg, cell, &g, cfi, sf_idx, rvs, (srslte_mimo_type_t)mimo_type, pmi)) return -1;
+  srslte_softbuffer_tx_t sb[2], *sbp[SRSLTE_MAX_CODEWORDS] = {&sb[0], &sb[1]};
+  for (int t = 0; t < 2; t++)
+    if (srslte_softbuffer_tx_init(&sb[t], nof_prb)) return -1;
+  uint8_t *data[SRSLTE_MAX_CODEWORDS] = {(uint8_t *)data0, (uint8_t *)data1};
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL};
+  for (uint32_t p = 0; p < nof_ports; p++) sf[p] = (cf_t *)grids + (size_t)p * n;
+  const int r = srslte_pdsch_encode(&q, &cfg, sbp, data, rnti, sf);
+  for (int t = 0; t < 2; t++) srslte_softbuffer_tx_free(&sb[t]);
+  srslte_pdsch_free(&q);
+  return r ? -1 : (int)cfg.nbits[0].nof_re;
+}
+
+/* srslte_pdsch_decode (pdsch.c:868-1007) of the same full-band grant: y [nrx] grids, h [port][rx]
+ * estimates (each SF_LEN_RE cf32, y at ys + a n, h at hs + (p nrx + a) n), fresh softbuffers, max 8
+ * half-iterations; data per TB (tbs / 8 + 3 bytes), ok[t] (1 acked), noi[t] (last_nof_iterations of the
+ * TB's codeword). Returns srslte_pdsch_decode's value. */
+int ref_pdsch_decode_mimo(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx, uint32_t cfi,
+                          uint32_t sf_idx, uint16_t rnti, uint32_t mimo_type, uint32_t pmi, uint32_t tb_cw_swap,
+                          uint32_t nof_tb, const uint32_t *mcs, const uint32_t *rv, float noise, const float *ys,
+                          const float *hs, uint8_t *data0, uint8_t *data1, int32_t *ok, uint32_t *noi) {
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = nof_ports;
+  cell.cp = SRSLTE_CP_NORM;
+  cell.phich_length = SRSLTE_PHICH_NORM;
+  cell.phich_resources = SRSLTE_PHICH_R_1;
+  srslte_pdsch_t q;
+  if (srslte_pdsch_init_ue(&q, nof_prb, nrx) || srslte_pdsch_set_cell(&q, cell) || srslte_pdsch_set_rnti(&q, rnti))
+    return -1;
+  srslte_pdsch_set_max_noi(&q, 8);
+  srslte_ra_dl_grant_t g;
+  ref_full_grant(&g, nof_prb, nof_tb, mcs, tb_cw_swap);
+  srslte_pdsch_cfg_t cfg;
+  int rvs[SRSLTE_MAX_CODEWORDS] = {(int)rv[0], nof_tb > 1 ? (int)rv[1] : 0};
+  if (srslte_pdsch_cfg_mimo(&cfg, cell, &g, cfi, sf_idx, rvs, (srslte_mimo_type_t)mimo_type, pmi)) return -1;
+  srslte_softbuffer_rx_t sb[2], *sbp[SRSLTE_MAX_CODEWORDS] = {&sb[0], &sb[1]};
+  for (int t = 0; t < 2; t++) {
+    if (srslte_softbuffer_rx_init(&sb[t], nof_prb)) return -1;
+    srslte_softbuffer_rx_reset(&sb[t]);
+  }
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  cf_t *y[SRSLTE_MAX_PORTS] = {NULL}, *h[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  for (uint32_t a = 0; a < nrx; a++) {
+    y[a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    memcpy(y[a], ys + 2 * (size_t)a * n, sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nof_ports; p++) {
+      h[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+      memcpy(h[p][a], hs + 2 * (size_t)(p * nrx + a) * n, sizeof(cf_t) * n);
+    }
+  }
+  uint8_t *data[SRSLTE_MAX_CODEWORDS] = {data0, data1};
+  bool acks[SRSLTE_MAX_CODEWORDS] = {false, false};
+  const int r = srslte_pdsch_decode(&q, &cfg, sbp, y, h, noise, rnti, data, acks);
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    ok[t] = acks[t];
+    noi[t] = srslte_pdsch_last_noi_cw(&q, nof_tb == 2 ? (t ^ (tb_cw_swap ? 1u : 0u)) : 0u);
+  }
+  for (uint32_t a = 0; a < nrx; a++) {
+    free(y[a]);
+    for (uint32_t p = 0; p < nof_ports; p++) free(h[p][a]);
+  }
+  for (int t = 0; t < 2; t++) srslte_softbuffer_rx_free(&sb[t]);
+  srslte_pdsch_free(&q);
+  return r;
+}
