@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -97,6 +98,39 @@ __global__ void k_noise_gather(const float *__restrict__ noise, const uint32_t *
   out[j] = noise[(size_t)sel[j / cols] * cols + j % cols];
 }
 
+// Ingest of one batch's time-domain samples into the slot's device buffer (dst: [item][antenna] rows of
+// `row` complex floats). src[r] is a device-visible pointer to row r's samples: host memory the caller
+// registered (srsgpu_rxq_register, read over PCIe by the GPU: no host copy, no per-item DMA call) or the
+// slot's raw staging buffer. sc16: int16 I/Q pairs scaled by `scale` (the radio's native format, half the
+// PCIe bytes), else complex floats. Rows with a null src were staged by the DMA already.
+__global__ __launch_bounds__(256) void k_ingest(const void *const *__restrict__ src, int nrows, size_t row,
+                                                int sc16, float scale, float2 *__restrict__ dst) {
+  const int r = blockIdx.y;
+  if (r >= nrows || !src[r]) return;
+  float2 *d = dst + (size_t)r * row;
+  if (sc16) {
+    const uint4 *s4 = (const uint4 *)src[r]; // 4 samples per 16 B
+    const size_t n4 = row / 4;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+      const uint4 v = s4[i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      float4 *o = (float4 *)(d + 4 * i);
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const uint32_t a = w[2 * k], b = w[2 * k + 1];
+        o[k] = make_float4((float)(int16_t)(a & 0xffff) * scale, (float)(int16_t)(a >> 16) * scale,
+                           (float)(int16_t)(b & 0xffff) * scale, (float)(int16_t)(b >> 16) * scale);
+      }
+    }
+  } else {
+    const float4 *s4 = (const float4 *)src[r]; // 2 samples per 16 B
+    float4 *o = (float4 *)d;
+    const size_t n2 = row / 2;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n2; i += (size_t)gridDim.x * 256)
+      o[i] = s4[i];
+  }
+}
+
 // transport blocks of a PDSCH subframe (srsgpu/pdsch_batch.h)
 uint32_t sf_ntb(const srsgpu_pdsch_sf_t &s) {
   return s.mimo_type == SRSGPU_MIMO_CDD || (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.tbs[1] > 0) ? 2 : 1;
@@ -142,12 +176,36 @@ struct srsgpu_rxq {
   // staging slots
   enum { FILLING = 0, CLOSED = 1, STAGED = 2 };
   struct Slot {
-    float *h_td = nullptr, *d_td = nullptr;
+    float *h_td = nullptr, *d_td = nullptr; // pinned staging (raw format) / device samples (cf32)
+    float *d_raw = nullptr;                  // SC16: the staged raw samples before conversion
+    const void **h_src = nullptr, **d_src = nullptr; // per row: registered host source (device view) or null
     hipEvent_t staged = nullptr;
     std::vector<Pending> items;
     int state = FILLING;
     int copying = 0; // submitters still copying their samples in
+    uint32_t nstaged = 0; // items whose samples went through the staging buffer
   } slot[2];
+  // input format (srsgpu_rxq_set_input_format) and caller memory the GPU reads directly
+  int sc16 = 0;
+  float sc16_scale = 1.0f / 32768.0f;
+  struct Region {
+    const char *h;
+    size_t bytes;
+    const char *d; // device view of the same memory
+  };
+  std::vector<Region> regions; // guarded by m
+  uint64_t zero_copy_rows = 0, staged_rows = 0;
+  size_t sample_bytes() const { return sc16 ? 4 : 8; }
+  // device view of a registered host pointer holding `bytes`, or null (caller holds m)
+  const void *device_view(const void *p, size_t bytes) const {
+    const char *c = (const char *)p;
+    for (const Region &r : regions)
+      if (c >= r.h && c + bytes <= r.h + r.bytes) {
+        const char *d = r.d + (c - r.h);
+        return ((uintptr_t)d & 15) ? nullptr : d; // the ingest kernel reads 16 B vectors: else staged
+      }
+    return nullptr;
+  }
   int fill = 0; // the slot submissions go to
 
   std::mutex m;
@@ -192,7 +250,10 @@ struct srsgpu_rxq {
     srsgpu_pdsch_set_stream(pdsch, st);
     for (Slot &s : slot) {
       RXQ_CHK(hipMalloc(&s.d_td, sizeof(float) * 2 * td_len * mb * nrx));
+      RXQ_CHK(hipMalloc(&s.d_raw, sizeof(float) * td_len * mb * nrx)); // SC16 rows: 4 B per sample
       RXQ_CHK(hipHostMalloc(&s.h_td, sizeof(float) * 2 * td_len * mb * nrx));
+      RXQ_CHK(hipHostMalloc(&s.h_src, sizeof(void *) * mb * nrx));
+      RXQ_CHK(hipMalloc(&s.d_src, sizeof(void *) * mb * nrx));
       RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
     }
     RXQ_CHK(hipMalloc(&d_grid, sizeof(float) * 2 * gsz * mb * nrx));
@@ -247,9 +308,14 @@ struct srsgpu_rxq {
     if (pdcch) srsgpu_pdcch_destroy(pdcch);
     for (Slot &s : slot) {
       if (s.d_td) (void)hipFree(s.d_td);
+      if (s.d_raw) (void)hipFree(s.d_raw);
       if (s.h_td) (void)hipHostFree(s.h_td);
+      if (s.h_src) (void)hipHostFree(s.h_src);
+      if (s.d_src) (void)hipFree(s.d_src);
       if (s.staged) (void)hipEventDestroy(s.staged);
     }
+    for (const Region &r : regions) (void)hipHostUnregister((void *)r.h);
+    regions.clear();
     for (void *p : {(void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data, (void *)d_ret,
                     (void *)d_noi, (void *)d_noise_last, (void *)d_est, (void *)d_sel, (void *)d_uenoise,
                     (void *)d_cfi, (void *)d_corr, (void *)d_llr, (void *)d_res, (void *)d_who,
@@ -265,9 +331,11 @@ struct srsgpu_rxq {
 
   // ---------------------------------------------------------------- submission ----
   int submit(srsgpu_rxq_item_t *it, srsgpu_rxq_ue_dl_t *ue, uint64_t *ticket) {
-    const void *td0 = it ? it->td[0] : ue->td[0], *td1 = it ? it->td[1] : ue->td[1];
-    if (!td0 || (nrx > 1 && !td1)) return -1;
+    const void *td[2] = {it ? it->td[0] : ue->td[0], it ? it->td[1] : ue->td[1]};
+    if (!td[0] || (nrx > 1 && !td[1])) return -1;
+    const size_t row_bytes = sample_bytes() * td_len;
     int s, idx;
+    const void *dv[2] = {nullptr, nullptr};
     {
       std::unique_lock<std::mutex> l(m);
       // the filling slot has room (else wait for the closer to switch to the other slot)
@@ -279,19 +347,53 @@ struct srsgpu_rxq {
       idx = (int)slot[s].items.size();
       *ticket = next_ticket++;
       slot[s].items.push_back({it, ue, *ticket, std::chrono::steady_clock::now()});
+      for (uint32_t a = 0; a < nrx; a++) {
+        dv[a] = device_view(td[a], row_bytes);
+        slot[s].h_src[(size_t)idx * nrx + a] = dv[a]; // null: staged by the host copy below
+      }
       slot[s].copying++;
     }
     cv_close.notify_one();
-    // the worker stages its own samples (outside the lock: many workers copy at once)
-    const size_t sfc = 2 * td_len;
-    memcpy(slot[s].h_td + ((size_t)idx * nrx) * sfc, td0, sizeof(float) * sfc);
-    if (nrx > 1) memcpy(slot[s].h_td + ((size_t)idx * nrx + 1) * sfc, td1, sizeof(float) * sfc);
+    // the worker stages its own unregistered samples (outside the lock: many workers copy at once)
+    for (uint32_t a = 0; a < nrx; a++)
+      if (!dv[a]) memcpy((char *)slot[s].h_td + ((size_t)idx * nrx + a) * row_bytes, td[a], row_bytes);
     {
       std::lock_guard<std::mutex> l(m);
       slot[s].copying--;
     }
     cv_close.notify_one();
     return 0;
+  }
+
+  // the closed slot's samples to the device: one DMA of the staged rows' region (up to the last staged
+  // row), then the ingest kernel for rows read from registered memory and for SC16 conversion
+  bool stage(Slot &sl, size_t n) {
+    const size_t rows = n * nrx, row_bytes = sample_bytes() * td_len;
+    size_t last = 0, nst = 0;
+    for (size_t r = 0; r < rows; r++)
+      if (!sl.h_src[r]) {
+        last = r + 1;
+        nst++;
+      }
+    sl.nstaged = (uint32_t)nst;
+    char *dst_raw = sc16 ? (char *)sl.d_raw : (char *)sl.d_td;
+    if (last && hipMemcpyAsync(dst_raw, sl.h_td, last * row_bytes, hipMemcpyHostToDevice, cst) != hipSuccess)
+      return false;
+    const bool kernel = sc16 || nst < rows;
+    if (kernel) {
+      // staged SC16 rows convert from the raw device copy; staged cf32 rows are in place already
+      for (size_t r = 0; r < rows; r++)
+        if (!sl.h_src[r]) sl.h_src[r] = sc16 ? (const void *)(dst_raw + r * row_bytes) : nullptr;
+      if (hipMemcpyAsync(sl.d_src, sl.h_src, sizeof(void *) * rows, hipMemcpyHostToDevice, cst) != hipSuccess)
+        return false;
+      const unsigned gx = (unsigned)std::min<size_t>(64, (td_len / 2 + 255) / 256);
+      hipLaunchKernelGGL(k_ingest, dim3(gx, (unsigned)rows), dim3(256), 0, cst, (const void *const *)sl.d_src,
+                         (int)rows, td_len, sc16, sc16_scale, (float2 *)sl.d_td);
+      if (hipGetLastError() != hipSuccess) return false;
+    }
+    zero_copy_rows += rows - nst;
+    staged_rows += nst;
+    return hipEventRecord(sl.staged, cst) == hipSuccess;
   }
 
   // closer thread: close the filling slot, switch the workers to the other one once it is free,
@@ -316,9 +418,7 @@ struct srsgpu_rxq {
       if (stop) return;
       const size_t n = slot[s].items.size();
       l.unlock();
-      const size_t bytes = sizeof(float) * 2 * td_len * nrx * n;
-      const bool ok = hipMemcpyAsync(slot[s].d_td, slot[s].h_td, bytes, hipMemcpyHostToDevice, cst) == hipSuccess &&
-                      hipEventRecord(slot[s].staged, cst) == hipSuccess;
+      const bool ok = stage(slot[s], n);
       l.lock();
       if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed\n");
       slot[s].state = STAGED;
@@ -711,6 +811,51 @@ void srsgpu_rxq_flush(srsgpu_rxq_t *q) {
   q->cv_close.notify_one();
 }
 
+int srsgpu_rxq_register(srsgpu_rxq_t *q, void *host, size_t bytes) {
+  if (!q || !host || !bytes) return -1;
+  if (hipHostRegister(host, bytes, hipHostRegisterMapped) != hipSuccess) {
+    fprintf(stderr, "srsgpu rxq: hipHostRegister of %zu bytes failed\n", bytes);
+    return -1;
+  }
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess || !d) {
+    (void)hipHostUnregister(host);
+    return -1;
+  }
+  std::lock_guard<std::mutex> l(q->m);
+  q->regions.push_back({(const char *)host, bytes, (const char *)d});
+  return 0;
+}
+
+int srsgpu_rxq_unregister(srsgpu_rxq_t *q, void *host) {
+  if (!q || !host) return -1;
+  {
+    std::unique_lock<std::mutex> l(q->m);
+    // nothing queued or in flight may still point into it
+    q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; });
+    auto it = std::find_if(q->regions.begin(), q->regions.end(), [&](const srsgpu_rxq::Region &r) { return r.h == host; });
+    if (it == q->regions.end()) return -1;
+    q->regions.erase(it);
+  }
+  return hipHostUnregister(host) == hipSuccess ? 0 : -1;
+}
+
+int srsgpu_rxq_set_input_format(srsgpu_rxq_t *q, uint32_t format, float scale) {
+  if (!q || format > SRSGPU_RXQ_SC16) return -1;
+  std::unique_lock<std::mutex> l(q->m);
+  q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; }); // only while nothing is queued
+  q->sc16 = format == SRSGPU_RXQ_SC16;
+  q->sc16_scale = scale != 0.f ? scale : 1.0f / 32768.0f;
+  return 0;
+}
+
+void srsgpu_rxq_ingest_stats(srsgpu_rxq_t *q, uint64_t *zero_copy_rows, uint64_t *staged_rows) {
+  if (!q) return;
+  std::lock_guard<std::mutex> l(q->m);
+  if (zero_copy_rows) *zero_copy_rows = q->zero_copy_rows;
+  if (staged_rows) *staged_rows = q->staged_rows;
+}
+
 struct srsgpu_chest *srsgpu_rxq_get_chest(srsgpu_rxq_t *q) { return q ? q->chest : nullptr; }
 srsgpu_pdsch_t *srsgpu_rxq_get_pdsch(srsgpu_rxq_t *q) { return q ? q->pdsch : nullptr; }
 
@@ -784,6 +929,90 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
   for (auto &t : pool) t.join();
   srsgpu_rxq_flush(q); // the last, partial batch
   collector.join();
+  return err ? -1 : 0;
+}
+
+int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
+                           uint32_t ticks, uint32_t period_us, uint32_t workers, float *latency_ms, int32_t *status,
+                           uint32_t *acked, double *late_ms) {
+  if (!q || !items || !streams || !depth || !ticks || !period_us || !workers || workers > 256 || !latency_ms ||
+      !status)
+    return -1;
+  using clk = std::chrono::steady_clock;
+  const uint64_t n = (uint64_t)streams * ticks;
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<uint64_t> tickets(n, 0);
+  std::vector<uint8_t> state(n, 0); // 1 submitted, 2 refused / skipped
+  uint64_t ndone = 0;
+  uint32_t producing = std::min(workers, streams), nack = 0;
+  int err = 0;
+  double worst_late = 0; // how far behind its tick a submission went out (a producer that falls behind)
+  const clk::time_point t0 = clk::now() + std::chrono::milliseconds(2);
+  auto tick_time = [&](uint64_t t) { return t0 + std::chrono::microseconds((uint64_t)period_us * t); };
+  // producer w owns streams w, w + W, ...: at each tick it submits their subframes
+  auto produce = [&](uint32_t w) {
+    for (uint64_t t = 0; t < ticks; t++) {
+      std::this_thread::sleep_until(tick_time(t));
+      for (uint32_t st = w; st < streams; st += producing) {
+        const uint64_t i = t * streams + st;
+        if (t >= depth) { // the item's softbuffer / output slot: its use depth ticks ago is collected
+          std::unique_lock<std::mutex> l(m);
+          cv.wait(l, [&] { return ndone > i - (uint64_t)depth * streams || err; });
+        }
+        int r = -1;
+        uint64_t tk = 0;
+        bool skip;
+        {
+          std::lock_guard<std::mutex> l(m);
+          skip = err != 0;
+        }
+        if (!skip) {
+          const double late = std::chrono::duration<double, std::milli>(clk::now() - tick_time(t)).count();
+          r = srsgpu_rxq_submit(q, items[(t % depth) * streams + st], &tk);
+          std::lock_guard<std::mutex> l(m);
+          if (late > worst_late) worst_late = late;
+        }
+        {
+          std::lock_guard<std::mutex> l(m);
+          tickets[i] = tk;
+          state[i] = r ? 2 : 1;
+          if (r && !err) err = -1;
+        }
+        cv.notify_all();
+      }
+    }
+  };
+  std::thread collector([&] {
+    for (uint64_t i = 0; i < n; i++) {
+      uint8_t s;
+      uint64_t tk;
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return state[i] != 0; });
+        s = state[i];
+        tk = tickets[i];
+      }
+      const int r = s == 1 ? srsgpu_rxq_wait(q, tk) : -1;
+      const clk::time_point done = clk::now();
+      status[i] = r;
+      latency_ms[i] = (float)std::chrono::duration<double, std::milli>(done - tick_time(i / streams)).count();
+      const srsgpu_rxq_item_t *it = items[((i / streams) % depth) * streams + i % streams];
+      {
+        std::lock_guard<std::mutex> l(m);
+        if (!r && it->ret[0] == 0) nack++;
+        ndone = i + 1;
+      }
+      cv.notify_all();
+    }
+  });
+  std::vector<std::thread> pool;
+  for (uint32_t w = 0; w < producing; w++) pool.emplace_back(produce, w);
+  for (auto &t : pool) t.join();
+  srsgpu_rxq_flush(q);
+  collector.join();
+  if (acked) *acked = nack;
+  if (late_ms) *late_ms = worst_late;
   return err ? -1 : 0;
 }
 

@@ -334,6 +334,12 @@ _sig = {
     "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 4),
     "srsgpu_rxq_drive": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint32, _vp, _vp, _vp]),
+    "srsgpu_rxq_drive_paced": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)] + [ctypes.c_uint32] * 5 +
+                               [_vp, _vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]),
+    "srsgpu_rxq_register": (_i32, [_vp, _vp, ctypes.c_size_t]),
+    "srsgpu_rxq_unregister": (_i32, [_vp, _vp]),
+    "srsgpu_rxq_set_input_format": (_i32, [_vp, _u32, ctypes.c_float]),
+    "srsgpu_rxq_ingest_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "srsgpu_rxq_get_chest": (_vp, [_vp]),
     "srsgpu_rxq_get_pdsch": (_vp, [_vp]),
     "srsgpu_rxq_submit_ue_dl": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -1153,6 +1159,42 @@ class RxQueue:
                                  status.ctypes.data) != 0:
             raise RuntimeError("srsgpu_rxq_drive: a submission was refused")
         return t_sub, t_done, status
+
+    def drive_paced(self, items, streams, depth, ticks, period_us=1000, workers=8):
+        """srsgpu_rxq_drive_paced: `streams` streams submit one subframe each per period_us for `ticks`
+        ticks, through items[(t % depth) * streams + s]; returns (latency_ms, status, acked, late_ms)"""
+        import numpy as np
+        assert len(items) == streams * depth
+        ptrs = (ctypes.c_void_p * len(items))(*[ctypes.addressof(it) for it in items])
+        lat = np.zeros(streams * ticks, np.float32)
+        status = np.zeros(streams * ticks, np.int32)
+        acked, late = ctypes.c_uint32(0), ctypes.c_double(0)
+        if _lib.srsgpu_rxq_drive_paced(self.q, ptrs, streams, depth, ticks, period_us, workers, lat.ctypes.data,
+                                       status.ctypes.data, ctypes.byref(acked), ctypes.byref(late)) != 0:
+            raise RuntimeError("srsgpu_rxq_drive_paced: a submission was refused")
+        return lat, status, acked.value, late.value
+
+    def register(self, arr):
+        """srsgpu_rxq_register: the GPU reads submissions whose samples lie in arr in place"""
+        if _lib.srsgpu_rxq_register(self.q, arr.ctypes.data, arr.nbytes) != 0:
+            raise RuntimeError("srsgpu_rxq_register failed")
+        self._registered = getattr(self, "_registered", []) + [arr]
+
+    def unregister(self, arr):
+        if _lib.srsgpu_rxq_unregister(self.q, arr.ctypes.data) != 0:
+            raise RuntimeError("srsgpu_rxq_unregister failed")
+        self._registered = [a for a in self._registered if a is not arr]
+
+    SC16, CF32 = 1, 0
+
+    def set_input_format(self, fmt, scale=0.0):
+        if _lib.srsgpu_rxq_set_input_format(self.q, fmt, scale) != 0:
+            raise RuntimeError("srsgpu_rxq_set_input_format failed")
+
+    def ingest_stats(self):
+        z, st = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _lib.srsgpu_rxq_ingest_stats(self.q, ctypes.byref(z), ctypes.byref(st))
+        return z.value, st.value
 
     def stats(self):
         b, n = ctypes.c_uint64(0), ctypes.c_uint64(0)

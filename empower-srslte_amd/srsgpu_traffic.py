@@ -258,7 +258,8 @@ class MimoSubframes:
             sfs.append(sf)
         self.sfs = s.make_sf_array(sfs)
         self.nre = sfs[0].nof_re
-        self.grid_sf = (ct.c_uint32 * (2 * n))(*[1 + (i % 4) for i in self.kept for _ in range(2)])
+        self.grid_sf = (ct.c_uint32 * (2 * n))(*[1 + (i % 4) for i in self.kept for _ in range(2)])  # [sf][rx]
+        self.sf_list = (ct.c_uint32 * n)(*[1 + (i % 4) for i in self.kept])  # [sf]
         z = lambda k, dt: torch.zeros(k, dtype=dt, device=dev)  # noqa: E731
         # TB bytes: subframe i's content is a function of i (the same on every rank)
         g = torch.Generator(device="cpu").manual_seed(seed)
@@ -279,7 +280,8 @@ class MimoSubframes:
         torch, n, gsz, N = self.torch, self.n, self.gsz, self.N
         txg = torch.zeros(2 * n * gsz, dtype=torch.complex64, device=self.dev)  # [sf][port] grids
         assert self.pd.encode_dev((self.sfs, n), self.d_data_tx.data_ptr(), txg.data_ptr(), port_stride=gsz) == 0
-        assert self.chest.put_crs_dev(self.grid_sf, txg.data_ptr(), gsz) == 0  # [sf][port] planes
+        # both ports' CRS: grid i's port p at plane i * 2 + p, n grids (one per subframe)
+        assert self.chest.put_crs_dev(self.sf_list, txg.data_ptr(), gsz) == 0
         xp = torch.zeros(2 * n * 15 * N, dtype=torch.complex64, device=self.dev)
         assert self.ofdm.tx_dev(2 * n, txg.data_ptr(), gsz, xp.data_ptr(), 15 * N) == 0
         torch.cuda.synchronize(self.dev)

@@ -29,7 +29,8 @@ typedef struct srsgpu_rxq srsgpu_rxq_t;
 typedef struct {
   /* in */
   const void *td[2];        /* host time-domain subframe per rx antenna: 15 * symbol_sz complex
-                               float samples (srslte_ofdm_rx_sf's input, cyclic prefixes included) */
+                               float samples (srslte_ofdm_rx_sf's input, cyclic prefixes included;
+                               int16 I/Q pairs with SRSGPU_RXQ_SC16) */
   srsgpu_pdsch_sf_t sf;     /* the grant; grid_offset / ce_offset / data_offset are the queue's */
   uint32_t reset_softbuffer[2]; /* new transport block: srslte_softbuffer_rx_reset first */
   uint8_t *data[2];         /* host output per TB: SRSGPU_DLSCH_DATA_LEN(tbs) bytes */
@@ -109,6 +110,23 @@ int srsgpu_rxq_decode_rnti(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item);
  * resources 0..3 = 1/6, 1/2, 1, 2): sets the PDCCH REG map of the ue_dl items. Default normal, 1.
  * Takes effect from the next batch the dispatcher starts (safe while batches are in flight). */
 int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_resources);
+/* Zero-copy ingest: pin caller memory that holds time-domain subframes (hipHostRegister, mapped).
+ * Submissions whose td buffers lie inside a registered region skip the host copy into the queue's
+ * staging: one kernel per batch reads them over PCIe (no per-subframe copy or DMA call). Such a td
+ * buffer is read after srsgpu_rxq_submit returns: keep it unchanged until the ticket is waited for
+ * (unregistered ones are copied before submit returns). td pointers must be 16-byte aligned to be
+ * read in place (others are staged). The region must stay valid until unregistered; unregister waits
+ * until nothing queued points into it. */
+int srsgpu_rxq_register(srsgpu_rxq_t *q, void *host, size_t bytes);
+int srsgpu_rxq_unregister(srsgpu_rxq_t *q, void *host);
+/* Sample format of every td buffer: complex float (default; srslte_ofdm_rx_sf's input) or the radio's
+ * int16 I/Q pairs (4 bytes per sample, half the PCIe bytes), converted on the GPU as value * scale
+ * (0: 1 / 32768, UHD's sc16 -> fc32). Waits until nothing is queued. */
+#define SRSGPU_RXQ_CF32 0
+#define SRSGPU_RXQ_SC16 1
+int srsgpu_rxq_set_input_format(srsgpu_rxq_t *q, uint32_t format, float scale);
+/* antenna rows ingested so far: read from registered memory / staged by a host copy */
+void srsgpu_rxq_ingest_stats(srsgpu_rxq_t *q, uint64_t *zero_copy_rows, uint64_t *staged_rows);
 /* close the current batch now */
 void srsgpu_rxq_flush(srsgpu_rxq_t *q);
 /* the queue's estimator and receiver, for their settings (srsgpu_chest_set_cfg / _set_smooth_filter,
@@ -127,6 +145,18 @@ void srsgpu_rxq_stats(srsgpu_rxq_t *q, uint64_t *batches, uint64_t *subframes);
  * after the last submission. Returns 0, or -1 if a submission was refused (the rest are skipped). */
 int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t n, uint32_t workers,
                      uint32_t reuse, double *t_sub, double *t_done, int32_t *status);
+/* Paced load (srsUE's real-time arrival, one subframe per stream per TTI): `streams` radio streams
+ * each hand one subframe to the queue every period_us (1000: the LTE TTI). Submission i = t * streams
+ * + s (tick t, stream s) uses items[(t % depth) * streams + s] (depth HARQ slots per stream: its
+ * softbuffer / outputs) and is submitted at t0 + t * period_us by one of `workers` native producer
+ * threads (stream s belongs to producer s mod workers); a slot is reused only once its previous
+ * submission is collected. latency_ms[i] = results written - tick time (collected in submission
+ * order, so an early finisher counts when every earlier one is in: an upper bound); status[i] as
+ * srsgpu_rxq_wait (-1: not submitted). *acked: collected submissions whose TB 0 acked; *late_ms: the
+ * furthest a submission went out behind its tick. Returns 0, or -1 if a submission was refused. */
+int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
+                           uint32_t ticks, uint32_t period_us, uint32_t workers, float *latency_ms, int32_t *status,
+                           uint32_t *acked, double *late_ms);
 
 #ifdef __cplusplus
 }

@@ -134,3 +134,25 @@ def test_rxq_drive_refuses_bad_arguments():
     assert lib.srsgpu_rxq_drive(None, None, 0, 1, 0, t, t, st) == -1
     items = (ctypes.c_void_p * 1)()
     assert lib.srsgpu_rxq_drive(ctypes.c_void_p(1), items, 1, 0, 0, t, t, st) == -1
+
+
+def test_rxq_ingest_and_paced_refuse_bad_arguments():
+    """srsgpu_rxq_drive_paced / _register / _set_input_format / _unregister without a queue or with
+    bad arguments return -1 (no GPU call)."""
+    lib = ctypes.CDLL(LIB)
+    vp = ctypes.c_void_p
+    lib.srsgpu_rxq_drive_paced.restype = ctypes.c_int
+    lib.srsgpu_rxq_drive_paced.argtypes = [vp, vp] + [ctypes.c_uint32] * 5 + [vp] * 4
+    lat = (ctypes.c_float * 4)()
+    st = (ctypes.c_int32 * 4)()
+    items = (vp * 4)()
+    assert lib.srsgpu_rxq_drive_paced(None, items, 1, 1, 1, 1000, 1, lat, st, None, None) == -1
+    for bad in ((0, 1, 1, 1000, 1), (1, 0, 1, 1000, 1), (1, 1, 0, 1000, 1), (1, 1, 1, 0, 1), (1, 1, 1, 1000, 0)):
+        assert lib.srsgpu_rxq_drive_paced(vp(1), items, *bad, lat, st, None, None) == -1
+    lib.srsgpu_rxq_register.argtypes = [vp, vp, ctypes.c_size_t]
+    lib.srsgpu_rxq_unregister.argtypes = [vp, vp]
+    lib.srsgpu_rxq_set_input_format.argtypes = [vp, ctypes.c_uint32, ctypes.c_float]
+    buf = (ctypes.c_uint8 * 64)()
+    assert lib.srsgpu_rxq_register(None, buf, 64) == -1
+    assert lib.srsgpu_rxq_unregister(None, buf) == -1
+    assert lib.srsgpu_rxq_set_input_format(None, 1, 0.0) == -1

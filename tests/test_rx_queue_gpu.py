@@ -166,3 +166,110 @@ def test_empty_noise_carried_across_batches(oracle):
     assert done == n and batches >= 4
     for h in (q, chest, ofdm):
         h.close()
+
+
+def _queue_case(oracle, n=12, seed=41):
+    import srsgpu_phy as s
+    po, dl = PdschOracle(oracle), DlschOracle(oracle)
+    rng = np.random.default_rng(seed)
+    nof_prb, cell_id, tbs = 25, 7, 18336  # 5 MHz, MCS 28
+    N = s.symbol_sz(nof_prb, True)
+    xs, datas, sfs = [], [], []
+    for i in range(n):
+        sf_idx = [1, 2, 3, 4, 6, 7, 8, 9][i % 8]
+        x, data, idx = build_subframe(po, dl, rng, nof_prb, cell_id, N, sf_idx, tbs, 1234, 30.0,
+                                      rng.uniform(0, 6.28))
+        xs.append(x)
+        datas.append(data)
+        sfs.append((sf_idx, idx.size))
+    return nof_prb, cell_id, tbs, N, xs, datas, sfs
+
+
+def _run_queue(s, q, xs, sfs, nof_prb, tbs):
+    n = len(xs)
+    outs = [np.zeros(tbs // 8 + 6, np.uint8) for _ in range(n)]
+    items = [q.item([xs[i]], s.make_sf(sf_idx=sfs[i][0], lstart=1, nof_prb=nof_prb, mod=3,
+                                        nof_re=sfs[i][1], rnti=1234, tbs=tbs, softbuffer=i),
+                    [outs[i]]) for i in range(n)]
+    tickets = [q.submit(it) for it in items]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in tickets)
+    return [it.ret[0] for it in items], [it.noi[0] for it in items], [it.noise for it in items], outs
+
+
+def test_registered_and_sc16_ingest(oracle):
+    """Zero-copy ingest (srsgpu_rxq_register: the batch's ingest kernel reads the caller's pinned
+    samples in place) and SC16 input (int16 I/Q converted on the GPU): the same TBs, iterations and
+    noise estimates, bit for bit, as the staged complex-float path on the same sample values — with
+    registered and staged subframes mixed in one batch, and misaligned pointers falling back to
+    staging."""
+    import torch
+    import srsgpu_phy as s
+    nof_prb, cell_id, tbs, N, xs, datas, sfs = _queue_case(oracle)
+    n = len(xs)
+    # the radio's int16 samples and their float values (what a staged cf32 caller would hand over)
+    scale = float(max(np.abs(x.view(np.float32)).max() for x in xs)) / 30000.0
+    sc = [np.round(x.view(np.float32) / scale).astype(np.int16) for x in xs]
+    xq = [(v.astype(np.float32) * np.float32(scale)).view(np.complex64) for v in sc]
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=n, max_batch=n, max_wait_us=200000)
+    want = _run_queue(s, q, xq, sfs, nof_prb, tbs)  # staged cf32
+    assert q.ingest_stats() == (0, n)
+    assert all(r == 0 for r in want[0])
+    for i in range(n):
+        assert (want[3][i][:tbs // 8] == datas[i]).all(), i
+    # registered cf32: every other subframe lies in the registered block
+    block = np.stack(xq[::2])
+    q.register(block)
+    mixed = [block[i // 2] if i % 2 == 0 else xq[i] for i in range(n)]
+    got = _run_queue(s, q, mixed, sfs, nof_prb, tbs)
+    assert got[:3] == want[:3] and all((a == b).all() for a, b in zip(got[3], want[3]))
+    assert q.ingest_stats() == ((n + 1) // 2, n + n // 2)
+    # a td pointer that is not 16-byte aligned is staged
+    raw = np.zeros(block.nbytes + 16, np.uint8)
+    q.register(raw)
+    mis = raw[8:8 + xq[0].nbytes].view(np.complex64)
+    mis[:] = xq[0]
+    got1 = _run_queue(s, q, [mis] + xq[1:], sfs, nof_prb, tbs)
+    assert got1[:3] == want[:3]
+    z0, s0 = q.ingest_stats()
+    assert (z0, s0) == ((n + 1) // 2, n + n // 2 + n)
+    q.unregister(raw)
+    q.unregister(block)
+    # SC16: staged, then registered
+    q.set_input_format(q.SC16, scale)
+    got = _run_queue(s, q, sc, sfs, nof_prb, tbs)
+    assert got[:3] == want[:3] and all((a == b).all() for a, b in zip(got[3], want[3]))
+    blk16 = np.stack(sc)
+    q.register(blk16)
+    got = _run_queue(s, q, list(blk16), sfs, nof_prb, tbs)
+    assert got[:3] == want[:3] and all((a == b).all() for a, b in zip(got[3], want[3]))
+    assert q.ingest_stats()[0] == z0 + n
+    q.close()
+    torch.cuda.synchronize()
+
+
+def test_paced_streams(oracle):
+    """srsgpu_rxq_drive_paced: 6 streams, one subframe each per 1 ms tick for 40 ticks, 3 HARQ slots
+    per stream, registered samples: every submission is decoded (acked, the transmitted bytes) and
+    latencies are measured from the tick."""
+    import srsgpu_phy as s
+    nof_prb, cell_id, tbs, N, xs, datas, sfs = _queue_case(oracle, n=6, seed=43)
+    streams, depth, ticks = 6, 3, 40
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=streams * depth, max_batch=streams, max_wait_us=500)
+    block = np.stack(xs)
+    q.register(block)
+    outs = [np.zeros(tbs // 8 + 6, np.uint8) for _ in range(streams * depth)]
+    items = []
+    for d in range(depth):
+        for st in range(streams):
+            k = d * streams + st
+            items.append(q.item([block[st]], s.make_sf(sf_idx=sfs[st][0], lstart=1, nof_prb=nof_prb, mod=3,
+                                                       nof_re=sfs[st][1], rnti=1234, tbs=tbs, softbuffer=k),
+                                [outs[k]]))
+    lat, status, acked, late = q.drive_paced(items, streams, depth, ticks, 1000, workers=2)
+    assert (status == 0).all() and acked == streams * ticks
+    assert (lat > 0).all() and np.isfinite(lat).all()
+    for k in range(streams * depth):
+        assert (outs[k][:tbs // 8] == datas[k % streams]).all(), k
+    assert q.ingest_stats()[0] == streams * ticks
+    q.close()

@@ -74,15 +74,15 @@ def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
     data = rng.integers(0, 256, (len(sfs_idx), 2, dlen)).astype(np.uint8)
     sfs, refs = [], []
     for j, sf_idx in enumerate(sfs_idx):
-        sf = s.make_sf(sf_idx=sf_idx, lstart=cfi, nof_prb=nof_prb, mod=(tb[0][1], tb[1][1]), rnti=0x3321,
-                       tbs=(tb[0][0], tb[1][0] if ntb == 2 else 0), rv=(j % 4, (j + 2) % 4), mimo=mimo,
+        sf = s.make_sf(sf_idx=sf_idx, lstart=cfi + 1 if nof_prb < 10 else cfi, nof_prb=nof_prb, mod=(tb[0][1], tb[1][1]), rnti=0x3321,
+                       tbs=(tb[0][0], tb[1][0] if ntb == 2 else 0), rv=(0, 0), mimo=mimo,
                        grid_offset=j * 2 * gsz, data_offset=((2 * j) * dlen, (2 * j + 1) * dlen), tb_cw_swap=swap,
                        codebook_idx=pmi + (1 if (mimo == 2 and ntb == 2) else 0))
         sf.nof_re = pd.nof_re(sf)
         sfs.append(sf)
         g = np.zeros(2 * gsz, np.complex64)
         mc = np.array(mcs, np.uint32)
-        rv = np.array([j % 4, (j + 2) % 4], np.uint32)
+        rv = np.zeros(2, np.uint32)  # the reference encodes a fresh softbuffer only at rv 0 (sch.c)
         nre = L.ref_pdsch_encode(nof_prb, cell_id, 2, cfi, sf_idx, 0x3321, mimo, pmi, swap, ntb, _p(mc, _u32p),
                                  _p(rv, _u32p), _p(data[j, 0], _u8p), _p(data[j, 1], _u8p), _p(g, _f32p))
         assert nre == sf.nof_re, (nre, sf.nof_re)
@@ -99,7 +99,7 @@ def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
         if mimo == 3 and n % 4:
             # the reference's AVX CDD precoder (precoding.c:1898-1917) leaves the last nof_re mod 4
             # symbols of each port as whatever its buffer held: those REs are not compared
-            idx = po.re_map(nof_prb, cell_id, 2, cfi, sfs_idx[j], np.ones((2, nof_prb), np.uint8))
+            idx = po.re_map(nof_prb, cell_id, 2, sfs[j].lstart, sfs_idx[j], np.ones((2, nof_prb), np.uint8))
             assert idx.size == n
             for p in range(2):
                 want[p * gsz + idx[4 * (n // 4):]] = got[j][p * gsz + idx[4 * (n // 4):]]
