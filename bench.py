@@ -524,6 +524,68 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     return out
 
 
+def run_tm3_coded(s, torch, dev, steps, warmup, snr_db=30.0, lanes=2, dist=None):
+    """BASELINE configs[3] per-GPU shard as real codewords: 1024 TM3 subframes per GPU (20 MHz, 2 CRS
+    ports, 2 rx antennas, large-delay CDD with two MCS-28 TBs of TBS 75376 = 26 code blocks per
+    subframe) from the GPU transmitter (srsgpu_traffic.MimoSubframes: pdsch_encode_ports, CRS of both
+    ports, OFDM TX, a 2x2 flat channel, AWGN at snr_db). Timed step: OFDM FFT of both antennas, channel
+    estimation of both ports on each antenna, CDD 2x2 MMSE PDSCH and DL-SCH with CRC early stop (max 8
+    half-iterations). Multi-GPU: the job is nranks x 1024 subframes in contiguous ranges (subframe i's
+    content depends only on i); no data-path collective. decoded_mbps = sum of K over CRC-passing
+    code blocks per second, whole job over the slowest rank's time."""
+    import srsgpu_shard as sh
+    import srsgpu_traffic as tr
+    rank = dist.get_rank() if dist else 0
+    nranks = dist.get_world_size() if dist else 1
+    table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
+    n_global = C3_SF * nranks
+    f = sh.contiguous(n_global, nranks)
+    mine = list(range(int(f[rank]), int(f[rank + 1])))
+    ms = []
+    for li in range(lanes):
+        st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
+        ms.append(tr.MimoSubframes(torch, dev, n_global, seed=5, stream=st, snr_db=snr_db, keep=mine[li::lanes]))
+    torch.cuda.synchronize()
+
+    def step():
+        for m in ms:
+            m.step()
+
+    warm_up(torch, step, warmup, 0.5)
+    if dist:
+        dist.barrier()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    gc.enable()
+    stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
+    chk = [m.check() for m in ms]
+    acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
+    noi = float(np.mean([c[2] for c in chk]))
+    cb_bits = sum(m.decoded_bits(table) for m in ms)
+    ntb = sum(m.ntb * m.n for m in ms)
+    el_job, _ = reduce_over_ranks(dist, dev, el, 0)
+    bits_job, _ = reduce_over_ranks(dist, dev, float(cb_bits), 0, op="sum")
+    acked_job, _ = reduce_over_ranks(dist, dev, float(acks * C3_TBS), 0, op="sum")
+    for m in ms:
+        m.close()
+    return {"workload": "c3_tm3_coded_%dsf_per_gpu_20MHz_2x2_cdd_64QAM_2x_tbs%d" % (C3_SF, C3_TBS),
+            "baseline_config": "BASELINE configs[3] (per-GPU shard)", "snr_db": snr_db,
+            "decoded_mbps": round(bits_job * steps / el_job / 1e6, 1),
+            "acked_tb_mbps": round(acked_job * steps / el_job / 1e6, 1),
+            "subframes_per_s": round(n_global * steps / el_job, 1), "ms_per_batch": round(el_job / steps * 1e3, 3),
+            "streams": lanes, "tbs": ntb, "acked_tbs": acks, "tbs_bytes_ok": good, "nof_iterations_mean": noi,
+            "code_blocks_per_subframe": 26, "stage_ms_per_batch": stages,
+            "kernels_per_batch": {k: {"ms": round(v[0], 4), "launches": v[1]} for k, v in ktab.items()},
+            "partition": "contiguous", "data": "synthetic coded TM3 subframes (GPU transmitter, 2x2 flat channel, "
+                                               "AWGN %.0f dB)" % snr_db}
+
+
 def reduce_over_ranks(dist, dev, elapsed, bit_errors, op="max"):
     """Job time = the slowest rank's timed region (it is bracketed by barriers); bit errors are
     summed (op="sum" sums the first value too). Identity on a single process."""
@@ -864,6 +926,10 @@ ALG_BYTES_PER_SF = {
     "k_tb_finish": lambda N: sum(k // 8 for k in C3_KS) + C3_TBS // 8,
 }
 HEADLINE_SNR_DB = 20.0
+# decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
+HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 1}, "per_halfit": {"es_fused": 0},
+               "fused_c1": {"es_fused": 1, "es_chunk": 1}, "fused_c2": {"es_fused": 1, "es_chunk": 2},
+               "fused_c8": {"es_fused": 1, "es_chunk": 8}}
 
 
 def pipeline_roofline(leg, nsf_per_batch):
@@ -1061,7 +1127,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="headline and configs[1] decoder only")
     ap.add_argument("--coded-snr", type=float, default=None,
                     help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
-    ap.add_argument("--legs", default="c2,fixed8,c3,tm3,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
+    ap.add_argument("--ab-headline", action="store_true",
+                    help="A/B the decoder's early-stop launch schedules on the headline workload")
+    ap.add_argument("--legs", default="c2,fixed8,c3,tm3,tm3c,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
                     help="legs after the headline (profiling aid)")
     args = ap.parse_args()
 
@@ -1101,7 +1169,7 @@ def main():
     # to 8 half-iterations as srsUE runs it, TB CRC). One step = one 1024-subframe batch.
     head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
                                    dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0,
-                                   warm_seconds=1.0))
+                                   warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None))
     cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
     result = None
     if rank == 0:
@@ -1153,6 +1221,9 @@ def main():
             ms, _ = reduce_over_ranks(dist, dev, pipe3["ms_per_batch"], 0)
             pipe3["subframes_per_s"] = round(nranks * C3_SF / (ms / 1e3), 1)
             pipe3["processing_mbps"] = round(pipe3["subframes_per_s"] * 2 * C3_TBS / 1e6, 1)
+    tm3c = None
+    if "tm3c" in legs:
+        tm3c = run_tm3_coded(s, torch, dev, max(8, args.steps // 2), 2, dist=dist)
     for kind in ("c3_coded", "c5"):
         if kind.split("_")[-1] in legs:
             extra[kind] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, kind, dist=dist,
@@ -1233,6 +1304,9 @@ def main():
         if pipe3:
             result["config"]["subframes_per_s_tm3"] = pipe3["subframes_per_s"]
             result["pipeline_tm3"] = pipe3
+        if tm3c:
+            result["config"]["tm3_coded_decoded_mbps"] = tm3c["decoded_mbps"]
+            result["pipeline_tm3_coded"] = tm3c
         if sweep:
             result["c3_coded_sweep"] = {"workload": "c3_coded_%dsf_20MHz_64QAM_tbs%d" % (C3_SF, C3_TBS),
                                         "early_stop_max_halfits": 8, "points": sweep}

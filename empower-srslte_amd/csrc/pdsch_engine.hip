@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <unordered_map>
 #include <stdio.h>
 #include <string.h>
 #include <string>
@@ -93,6 +94,28 @@ struct PdschEngine {
   uint32_t *d_csimax = nullptr;
   int16_t *d_e = nullptr;    // [max_sf][max_bits]
   uint32_t max_re = 0, max_bits = 0, cwords = 0;
+  // one scrambling sequence per distinct seed of a call (a UE's TBs use at most 10 subframe seeds per
+  // codeword): the TBs that share a seed read the same words
+  std::unordered_map<uint32_t, uint32_t> gold_slot;
+  uint32_t ngold = 0;
+  const uint32_t *gold(uint32_t seed, uint32_t len) {
+    auto it = gold_slot.find(seed);
+    if (it == gold_slot.end()) {
+      GoldItem &g = h_gold[ngold];
+      g.seed = seed;
+      g.len = len;
+      g.c = d_c + (size_t)ngold * cwords;
+      it = gold_slot.emplace(seed, ngold++).first;
+    } else if (h_gold[it->second].len < len) {
+      h_gold[it->second].len = len; // the sequence's prefix does not depend on its length
+    }
+    return h_gold[it->second].c;
+  }
+  uint32_t gold_bits() const {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < ngold; i++) m = std::max(m, h_gold[i].len);
+    return m;
+  }
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
   // transmit side (lazily allocated)
@@ -237,8 +260,10 @@ struct PdschEngine {
       return -1;
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
-    uint32_t mre = 0, mbits = 0, k = 0;
+    uint32_t mre = 0, k = 0;
     int n_dual = 0;
+    gold_slot.clear();
+    ngold = 0;
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
@@ -253,10 +278,9 @@ struct PdschEngine {
       for (uint32_t tb = 0; tb < nt; tb++, k++) {
         const uint32_t cw = nt == 2 ? (tb ^ (s.tb_cw_swap ? 1u : 0u)) : 0u;
         const int q = kQm[s.mod[tb]];
-        GoldItem &g = h_gold[k]; // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID
-        g.seed = ((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id;
-        g.len = nre * q;
-        g.c = d_c + (size_t)k * cwords;
+        // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID
+        const uint32_t *gc = gold(((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id,
+                                  nre * q);
         LlrItem &t = h_llr[k];
         memset(&t, 0, sizeof(t));
         for (uint32_t a = 0; a < cell.nof_rx_ant; a++) {
@@ -265,7 +289,7 @@ struct PdschEngine {
             t.h[p][a] = (const float2 *)d_ce + s.ce_offset + (a * cell.nof_ports + p) * ant_stride;
         }
         t.map = m;
-        t.c = g.c;
+        t.c = gc;
         t.e = e_ptr[k];
         t.csi = d_csi + (size_t)k * max_re;
         t.csi_max = d_csimax + k;
@@ -293,17 +317,16 @@ struct PdschEngine {
           n_dual++;
         }
         mre = std::max(mre, nre);
-        mbits = std::max(mbits, nre * q);
       }
     }
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * k, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * k, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
     if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)k * 4, st));
     {
       ProfScope ps("k_gold", st);
-      HIPCHK(launch_gold(d_gold, (int)k, mbits, d_x1, d_x2b, gold_words, st));
+      HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
     }
     ProfScope ps("k_pdsch_llr", st);
     HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual));
@@ -345,7 +368,9 @@ struct PdschEngine {
       HIPCHK(hipMemcpy(d_mod, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
-    uint32_t mre = 0, mbits = 0, k = 0;
+    uint32_t mre = 0, k = 0;
+    gold_slot.clear();
+    ngold = 0;
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
@@ -379,14 +404,12 @@ struct PdschEngine {
         t.softbuffer = 0;
         t.e_offset = (uint64_t)k * max_bits;
         t.data_offset = s.data_offset[tb];
-        GoldItem &g = h_gold[k]; // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID, q = codeword
-        g.seed = ((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id;
-        g.len = nre * q;
-        g.c = d_c + (size_t)k * cwords;
+        // sequences.c:64-66: rnti 2^14 + q 2^13 + (ns/2) 2^9 + N_ID, q = codeword
+        const uint32_t *gc = gold(((uint32_t)s.rnti << 14) + (cw << 13) + ((2 * s.sf_idx / 2) << 9) + cell.id,
+                                  nre * q);
         x.e[cw] = d_ebits + (size_t)k * max_bits;
-        x.c[cw] = g.c;
+        x.c[cw] = gc;
         x.qm[cw] = q;
-        mbits = std::max(mbits, nre * q);
       }
       x.map = m;
       x.grid = (float2 *)d_grid + s.grid_offset;
@@ -406,11 +429,11 @@ struct PdschEngine {
       mre = std::max(mre, nre);
     }
     if (srsgpu_dlsch_encode_dev(dl, h_tb, k, d_data, d_ebits)) return -1;
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * k, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    HIPCHK(launch_gold(d_gold, (int)k, mbits, d_x1, d_x2b, gold_words, st));
+    HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
     ProfScope ps("k_pdsch_tx", st);
     HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));
     return 0;

@@ -324,6 +324,22 @@ class MimoSubframes:
         noi = self.d_noi.cpu().numpy()[:len(ret)]
         return int((ret == 0).sum()), good, float(noi.mean())
 
+    def decoded_bits(self, table):
+        """SURVEY §8(d)'s decoded bits of the last decode (as MixedCells.decoded_bits): the sum of K
+        over the code blocks whose CRC passed, from the return codes and the softbuffers' cb_crc"""
+        C, _c1, K1, C2, K2, _f = table["cbsegm_C_C1_K1_C2_K2_F"][str(self.tbs)]
+        ret = self.d_ret.cpu().numpy()
+        ks = [K2] * C2 + [K1] * (C - C2)  # the C2 smaller blocks first (36.212 5.1.2)
+        total = 0
+        for k in range(self.ntb * self.n):
+            j, t = (k // 2, k % 2) if self.ntb == 2 else (k, 0)
+            if ret[k] == 0:
+                total += sum(ks)
+            else:
+                crc = self.pd.read_cb_crc(2 * j + t)
+                total += sum(kk for kk, ok in zip(ks, crc[:C]) if ok)
+        return total
+
     def close(self):
         for h in (self.ofdm, self.chest, self.pd):
             h.close()
