@@ -210,12 +210,12 @@ def pipeline_inputs(s, n_sf, rng, nrx=1, nports=1, first=0, noise_seed=None):
     return N, x
 
 
-STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_bidir",
+STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_ldderm", "k_rows_late", "k_win_bidir",
           "k_sse_halfit", "k_decide", "k_tb_finish")
 # kernels of the coded subframe legs, for the per-kernel table and the roofline of the dominant one
 # (names as the library's ProfScope records them; prof_get matches substrings, so the decoder's
 # early-stop launches are asked for by their full name)
-KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_win_bidir_es",
+KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_ldderm", "k_rows_late", "k_win_bidir_es",
            "k_sse_es", "k_es_bytes", "k_win_bidir_run", "k_win_bidir", "k_decide", "k_tb_finish")
 
 
@@ -913,6 +913,8 @@ ALG_BYTES_PER_SF = {
     "k_derm": lambda N: C3_NLLR * 2 + sum((3 * (k + 32) + 12) * 2 for k in C3_KS),
     # rows in, the decoder's systematic / parity planes out: 6 B + 6 B per info bit
     "k_load": lambda N: 12 * sum(C3_KS),
+    # direct de-rate-matching (fresh softbuffers): LLRs in, the decoder's planes out (6 B per info bit)
+    "k_ldderm": lambda N: C3_NLLR * 2 + 6 * sum(C3_KS),
     # (3(K+32)+12)*2 + K/8 B per code block per decode
     "k_win_bidir_es": lambda N: sum((3 * (k + 32) + 12) * 2 + k // 8 for k in C3_KS),
     "k_win_bidir_run": lambda N: sum((3 * (k + 32) + 12) * 2 + k // 8 for k in C3_KS),
@@ -1127,6 +1129,7 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="headline and configs[1] decoder only")
     ap.add_argument("--coded-snr", type=float, default=None,
                     help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
+    ap.add_argument("--lanes", type=int, default=2, help="HIP streams per rank for the headline leg")
     ap.add_argument("--ab-headline", action="store_true",
                     help="A/B the decoder's early-stop launch schedules on the headline workload")
     ap.add_argument("--legs", default="c2,fixed8,c3,tm3,tm3c,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
@@ -1168,7 +1171,7 @@ def main():
     # extraction, MMSE, 64QAM demap, descramble), DL-SCH (de-RM, turbo decoding with CRC early stop up
     # to 8 half-iterations as srsUE runs it, TB CRC). One step = one 1024-subframe batch.
     head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
-                                   dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0,
+                                   dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0, lanes=args.lanes,
                                    warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None))
     cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
     result = None

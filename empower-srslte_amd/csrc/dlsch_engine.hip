@@ -133,6 +133,10 @@ struct DlschEngine {
   bool staged_pending = false;
   bool llr8 = false; // srslte_sch_t.llr_is_8bit: int8 LLRs, 8-bit de-RM and decoders
   bool fixed = false; // srsgpu_dlsch_set_early_stop(0): every CB runs max_halfits, one CRC check
+  // srsgpu_dlsch_set_direct_derm: window-decoder code blocks are de-rate-matched straight into the
+  // decoder inputs (k_load_derm) and their softbuffer rows written after the decode, only for TBs
+  // that failed (the only rows the reference reads again)
+  bool direct_derm = true;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
@@ -400,6 +404,13 @@ struct DlschEngine {
         it.rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
         it.fresh = fresh + (size_t)t.softbuffer * max_cb + i;
         it.w8 = llr8;
+        it.tb_ret = d_ret + b;
+        {
+          // the loader the decoder job will pick for this block (TdecEngine::derm_direct)
+          const int r = resolve_impl(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, K);
+          it.direct = direct_derm && sb_input_for(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, r) &&
+                      impl_nb(r) % 8 == 0;
+        }
         max_n = std::max(max_n, std::min(ne, it.N));
         cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
       }
@@ -410,11 +421,20 @@ struct DlschEngine {
       return std::tie(cbs[a].K, cbs[a].poly, cbs[a].crclen) <
              std::tie(cbs[b].K, cbs[b].poly, cbs[b].crclen);
     });
+    // items in decoder order (k_load_derm reads them by decoder position)
+    std::vector<DermItem> tb_order(h_items, h_items + ncb);
+    uint32_t ndirect = 0;
+    tdec.derm_max_ne = 0;
     for (uint32_t p = 0; p < order.size(); p++) {
       const uint32_t u = cbs[order[p]].u;
       h_cbmap[u] = p;
-      h_items[u].pos = p;
-      h_rows[p] = h_items[u].row;
+      h_items[p] = tb_order[u];
+      h_items[p].pos = p;
+      h_rows[p] = h_items[p].row;
+      if (h_items[p].direct) {
+        ndirect++;
+        tdec.derm_max_ne = std::max(tdec.derm_max_ne, h_items[p].ne);
+      }
     }
     // ---- device ----
     if (ncb) {
@@ -425,9 +445,10 @@ struct DlschEngine {
     HIPCHK(hipMemcpyAsync(d_tbs, h_tbs, sizeof(TbItem) * ntb, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    {
+    if (ndirect) HIPCHK(launch_derm_flags(d_items, (int)ncb, d_init, st));
+    if (ndirect < ncb) {
       ProfScope ps("k_derm", st);
-      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st));
+      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st, 0));
     }
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;
@@ -442,11 +463,16 @@ struct DlschEngine {
     }
     if (!specs.empty() &&
         tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
-                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed))
+                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed,
+                          ndirect ? d_items : nullptr))
       return -1;
     {
       ProfScope ps("k_tb_finish", st);
       HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st));
+    }
+    if (ndirect) { // rows of the direct blocks of failed TBs, for the retransmission
+      ProfScope ps("k_rows_late", st); // k_derm, phase 1
+      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st, 1));
     }
     return 0;
   }
@@ -693,6 +719,10 @@ void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable) {
 
 void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable) {
   if (q) q->e.llr8 = enable != 0;
+}
+
+void srsgpu_dlsch_set_direct_derm(srsgpu_dlsch_t *q, int enable) {
+  if (q) q->e.direct_derm = enable != 0;
 }
 
 } // extern "C"

@@ -22,6 +22,9 @@ struct DermItem {
   uint8_t *fresh;         // row reset since its last use: content counts as zero (cleared here)
   uint32_t w8;            // 8-bit LLR chain (llr_is_8bit, rm_turbo.c:432-469): int8 values held
                           // sign-extended in the int16 row, sums wrapping at 8 bits
+  uint32_t direct;        // de-rate-matched straight into the decoder inputs (k_load_derm); the
+                          // row itself is written after the decode, only if the TB failed
+  const int32_t *tb_ret;  // its TB's return code (k_tb_finish), read by the deferred row pass
 };
 
 // one transport block's epilogue
@@ -47,8 +50,12 @@ struct EncItem {
   uint32_t crc_cb;         // C > 1: CB CRC24B
 };
 
+// phase 0: rows of the items that are not `direct` (before the decode); phase 1: rows of the
+// direct items whose TB failed and that were not decoded before this call (after k_tb_finish)
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st);
+                       hipStream_t st, int phase = 0);
+// init_done[pos] = cb_crc before this call, for every item
+hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, hipStream_t st);
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
 // crc_a[d] = x^(d+24) mod P_24A for d < the largest TBS + 24
@@ -66,5 +73,16 @@ struct UlItem {
 };
 hipError_t launch_ulsch_deinterleave(const UlItem *d_items, int n, uint32_t max_bits, const int16_t *q,
                                      int16_t *g, hipStream_t st);
+} // namespace srsgpu
+
+#include "tdec_kernels.h"
+namespace srsgpu {
+// Direct de-rate-matching for the window decoders: the decoder inputs SP0 / P1 / T of groups
+// [0, ng) of dg (sub-block rows, nb a multiple of 8) computed from each code block's LLRs and its
+// softbuffer row (skipped when fresh) as k_derm + k_load_sbt would, without writing the row.
+// items are indexed by decoder position (TdGroup::cb0 numbering); one workgroup per pair.
+// max_ne: the largest E among the items (sizes the LDS staging of the LLRs)
+hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermItem *items,
+                            const TdArrays &a, uint32_t max_ne, hipStream_t st);
 } // namespace srsgpu
 #endif

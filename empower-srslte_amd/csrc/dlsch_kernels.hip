@@ -40,15 +40,54 @@ __device__ __forceinline__ uint32_t derm_fold(uint32_t v, bool w8) {
 // from L1/L2. Wrapping int16 sums, as rm_turbo.c:394-430's `output[j] += input[i]`, so the order
 // of the additions does not matter.
 #define DERM_LDS 12288 // LLRs staged per code block (24 KB of LDS)
+// The E LLRs of one code block into LDS words (two per word) by a 256-thread workgroup: 16-byte
+// loads for the aligned middle, 4-byte loads for the head and tail words (E is even for every Qm,
+// so the block's LLRs start 4-byte aligned; an odd tail is read alone), 2-byte pairs otherwise.
+__device__ __forceinline__ void stage_llrs(uint32_t *es, const int16_t *ep, uint32_t ne) {
+  const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(ep));
+  if (((uintptr_t)ep & 3) == 0) {
+    const gp_t<const uint32_t> e32 = glob(reinterpret_cast<const uint32_t *>(ep));
+    const uint32_t nw2 = ne / 2;
+    const uint32_t head = (uint32_t)((16 - ((uintptr_t)ep & 15)) & 15) / 4; // words to alignment
+    const uint32_t h = head < nw2 ? head : nw2;
+    const uint32_t nq = (nw2 - h) / 4;
+    const gp_t<const u4v> e4 = glob(reinterpret_cast<const u4v *>(ep + 2 * h));
+#pragma unroll 4
+    for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+      const u4v v = e4[q];
+      es[h + 4 * q] = v.x;
+      es[h + 4 * q + 1] = v.y;
+      es[h + 4 * q + 2] = v.z;
+      es[h + 4 * q + 3] = v.w;
+    }
+    const uint32_t t0 = h + 4 * nq; // tail words t0 .. nw2-1 (at most 3) and the head words
+    if (threadIdx.x < h) es[threadIdx.x] = e32[threadIdx.x];
+    if (threadIdx.x >= 64 && threadIdx.x - 64 < nw2 - t0) es[t0 + threadIdx.x - 64] = e32[t0 + threadIdx.x - 64];
+    if ((ne & 1) && threadIdx.x == 128) es[ne / 2] = e[ne - 1];
+  } else {
+    const uint32_t nw = (ne + 1) / 2;
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
+      es[w] = (uint32_t)e[2 * w] | (2 * w + 1 < ne ? (uint32_t)e[2 * w + 1] << 16 : 0u);
+  }
+}
+
+// phase 0: before the decode, every item not `direct`; phase 1: after k_tb_finish, the direct
+// items of failed TBs that were not decoded before this call (their rows as the reference leaves
+// them; an acked TB's rows are never read again: sch.c:323 skips blocks whose CRC passed, and the
+// next TB resets the softbuffer)
 __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
-                                              uint8_t *__restrict__ init_done) {
+                                              uint8_t *__restrict__ init_done, int phase) {
   __shared__ uint32_t es[DERM_LDS / 2];
   const int g = blockIdx.x;
   if (g >= nitems) return;
   const DermItem it = items[g];
-  const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
-  if (threadIdx.x == 0) init_done[it.pos] = skip;
-  if (skip) return; // sch.c:323: blocks whose CRC passed before are not combined again
+  if (phase == 0) {
+    const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
+    if (threadIdx.x == 0) init_done[it.pos] = skip;
+    if (skip || it.direct) return; // sch.c:323: blocks whose CRC passed before are not combined again
+  } else {
+    if (!it.direct || init_done[it.pos] || *glob(it.tb_ret) == 0) return;
+  }
   const bool fresh = it.fresh && *glob(it.fresh);
   const bool w8 = it.w8 != 0;
   const uint32_t N = it.N, ne = it.ne, len = it.rowlen;
@@ -67,31 +106,7 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
     // each circular-buffer entry received at most once (the usual case): the E LLRs are staged
     // in LDS with 16-byte loads and gathered from there (scattered 2-byte global gathers cost
     // one address-unit slot per lane)
-    const uint32_t nw = (ne + 1) / 2;
-    if (((uintptr_t)it.e & 3) == 0) { // E is even for every Qm; an odd tail is read alone
-      // 16-byte loads for the aligned middle, 4-byte loads for the head and tail words
-      const gp_t<const uint32_t> e32 = glob(reinterpret_cast<const uint32_t *>(it.e));
-      const uint32_t nw2 = ne / 2;
-      const uint32_t head = (uint32_t)((16 - ((uintptr_t)it.e & 15)) & 15) / 4; // words to alignment
-      const uint32_t h = head < nw2 ? head : nw2;
-      const uint32_t nq = (nw2 - h) / 4;
-      const gp_t<const u4v> e4 = glob(reinterpret_cast<const u4v *>(it.e + 2 * h));
-#pragma unroll 4
-      for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
-        const u4v v = e4[q];
-        es[h + 4 * q] = v.x;
-        es[h + 4 * q + 1] = v.y;
-        es[h + 4 * q + 2] = v.z;
-        es[h + 4 * q + 3] = v.w;
-      }
-      const uint32_t t0 = h + 4 * nq; // tail words t0 .. nw2-1 (at most 3) and the head words
-      if (threadIdx.x < h) es[threadIdx.x] = e32[threadIdx.x];
-      if (threadIdx.x >= 64 && threadIdx.x - 64 < nw2 - t0) es[t0 + threadIdx.x - 64] = e32[t0 + threadIdx.x - 64];
-      if ((ne & 1) && threadIdx.x == 128) es[ne / 2] = e[ne - 1];
-    } else {
-      for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
-        es[w] = (uint32_t)e[2 * w] | (2 * w + 1 < ne ? (uint32_t)e[2 * w + 1] << 16 : 0u);
-    }
+    stage_llrs(es, it.e, ne);
     __syncthreads();
     const uint16_t *el = reinterpret_cast<const uint16_t *>(es);
 #pragma unroll 4
@@ -144,6 +159,162 @@ __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ i
   }
 }
 
+__global__ __launch_bounds__(256) void k_derm_flags(const DermItem *__restrict__ items, int n,
+                                                    uint8_t *__restrict__ init_done) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *c = items[i].cb_crc;
+  init_done[items[i].pos] = c ? *glob(c) : 0;
+}
+
+// ------------------------------------------------------------------ direct de-RM ----
+// k_derm followed by k_load_sbt (tdec_kernels.hip) in one pass, for the window decoders' groups:
+// the decoder input at softbuffer-row position o of code block c is what k_derm would store
+// there, (fresh ? 0 : row[o]) + the LLRs e[i] with i = inv[o] (mod N), computed where k_load_sbt
+// would read it. One 512-thread workgroup per code-block pair: both blocks' LLRs are staged in LDS
+// once (dynamic LDS, `stage` LLRs per block), then for each tile of 2048 / nb steps the six
+// (stream, block) chunks of 2048 row positions are formed in LDS from 16-byte inverse-table (and,
+// unless fresh, row) loads, and written out in the T4 layout with coalesced 16-byte stores; the
+// next tile's table loads are issued before the current tile is written out. HBM traffic per code
+// block: its E LLRs in and the 12 B per info bit of SP0 / P1 out (the separate passes also wrote
+// and re-read the 3(K+32)+12 row entries).
+#define LDR_THREADS 512
+#define LDR_TILE 2048                      // row positions per (stream, block) chunk of a tile
+#define LDR_PIECES (6 * LDR_TILE / 8)      // 16-byte pieces of a tile
+#define LDR_PPT (LDR_PIECES / LDR_THREADS) // pieces per thread
+__global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
+                                                           const DermItem *__restrict__ items, TdArrays arr,
+                                                           uint32_t stage) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
+  uint16_t(*tile)[LDR_TILE] = reinterpret_cast<uint16_t(*)[LDR_TILE]>(ldr_lds); // [6][LDR_TILE]
+  uint32_t *llr0 = ldr_lds + 6 * LDR_TILE / 2, *llr1 = llr0 + stage / 2;
+  int gi = 0;
+  { // the last group whose first workgroup is <= blockIdx.x
+    int lo = 0, hi = ngroups - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (groups[mid].blk_load <= (int)blockIdx.x)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    gi = lo;
+  }
+  const TdGroup &G = groups[gi];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
+  const int pair = blockIdx.x - G.blk_load;
+  if (pair >= npairs) return;
+  const int L = K / nb, G4 = (L + 3) >> 2, S = LDR_TILE / nb;
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
+  // the two blocks' fields (selected by h, which is wave-uniform: no indexed private arrays)
+  struct Blk {
+    const int16_t *e, *row;
+    const uint16_t *inv;
+    uint32_t ne, N;
+    bool fresh, staged;
+  };
+  auto blk = [&](int c) {
+    const DermItem &it = items[c];
+    return Blk{it.e, it.row, it.inv, it.ne, it.N, it.fresh && *glob(it.fresh),
+               it.ne <= it.N && it.ne <= stage};
+  };
+  const Blk ba = blk(c0), bb = blk(c1);
+  const bool w8 = items[c0].w8 != 0; // one LLR width per call
+  // tile pieces: chunk c = (stream, block), 8 row positions from sub-block index e
+  auto piece_at = [&](int q, int k0, int &c, int &pc, uint32_t &o8) {
+    const int idx = threadIdx.x + LDR_THREADS * q;
+    c = idx / (LDR_TILE / 8);
+    pc = idx - c * (LDR_TILE / 8);
+    const int st = c >> 1;
+    int e = k0 * nb + pc * 8; // past the last step: its copy (values unused)
+    if (e >= L * nb) e = (L - 1) * nb + (e & (nb - 1));
+    o8 = (uint32_t)(st * (K + 32) + e) / 8;
+  };
+  u4v iv[LDR_PPT], ov[LDR_PPT];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < LDR_PPT; q++) {
+      int c, pc;
+      uint32_t o8;
+      piece_at(q, k0, c, pc, o8);
+      const Blk &b = (c & 1) ? bb : ba;
+      iv[q] = glob(reinterpret_cast<const u4v *>(b.inv))[o8];
+      ov[q] = b.fresh ? u4v{0, 0, 0, 0} : glob(reinterpret_cast<const u4v *>(b.row))[o8];
+    }
+  };
+  fetch(0); // the first tile's table loads fly while the LLRs are staged
+  if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
+  if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
+  __syncthreads();
+  // value of a row position of block b given its inverse-table entry m and the row's old value
+  auto value = [&](const Blk &b, const uint16_t *lds, uint32_t m, uint32_t old) -> uint32_t {
+    uint32_t acc = b.fresh ? 0u : old;
+    if (b.staged) {
+      acc += m < b.ne ? (uint32_t)lds[m] : 0u; // 0xFFFF >= ne
+    } else if (m != 0xFFFFu) {
+      const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(b.e));
+      for (uint32_t i = m; i < b.ne; i += b.N) acc += e[i];
+    }
+    return derm_fold(acc, w8);
+  };
+  const size_t pbase = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
+  const gp_t<u4v> SP0 = glob(reinterpret_cast<u4v *>((int16_t *)arr.SP0 + 4 * pbase));
+  const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
+  for (int k0 = 0; k0 < 4 * G4; k0 += S) {
+#pragma unroll
+    for (int q = 0; q < LDR_PPT; q++) {
+      int c, pc;
+      uint32_t o8;
+      piece_at(q, k0, c, pc, o8);
+      const bool h = c & 1;
+      const Blk &b = h ? bb : ba;
+      const uint16_t *lds = reinterpret_cast<const uint16_t *>(h ? llr1 : llr0);
+      const uint32_t im[4] = {iv[q].x, iv[q].y, iv[q].z, iv[q].w}, om[4] = {ov[q].x, ov[q].y, ov[q].z, ov[q].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        r[u] = (value(b, lds, im[u] & 0xFFFFu, om[u] & 0xFFFFu) & 0xFFFFu) |
+               (value(b, lds, im[u] >> 16, om[u] >> 16) << 16);
+      *reinterpret_cast<u4v *>(&tile[c][pc * 8]) = u4v{r[0], r[1], r[2], r[3]};
+    }
+    __syncthreads();
+    if (k0 + S < 4 * G4) fetch(k0 + S);
+    // the tile's steps as T4 elements: el -> step (el / 4 / nb) * 4 + el % 4, chain el / 4 % nb
+    const int nel = min(S, 4 * G4 - k0) * nb;
+    auto at = [&](int c, int el) -> uint32_t {
+      const int g4l = el / (4 * nb), d = (el >> 2) % nb, u = el & 3;
+      return tile[c][(4 * g4l + u) * nb + d];
+    };
+    const size_t e0 = (size_t)k0 * nb; // T4 element of the tile's first step
+#pragma unroll
+    for (int q = 0; q < LDR_TILE / 2 / LDR_THREADS; q++) {
+      const int v = threadIdx.x + LDR_THREADS * q; // SP0 elements 2v, 2v + 1
+      if (2 * v < nel) {
+        const int ea = 2 * v, eb = 2 * v + 1;
+        SP0[e0 / 2 + v] = u4v{at(0, ea) | (at(1, ea) << 16), at(2, ea) | (at(3, ea) << 16),
+                              at(0, eb) | (at(1, eb) << 16), at(2, eb) | (at(3, eb) << 16)};
+      }
+    }
+    if (4 * (int)threadIdx.x < nel) {
+      const int e = 4 * threadIdx.x;
+      P1[e0 / 4 + threadIdx.x] = u4v{at(4, e) | (at(5, e) << 16), at(4, e + 1) | (at(5, e + 1) << 16),
+                                     at(4, e + 2) | (at(5, e + 2) << 16), at(4, e + 3) | (at(5, e + 3) << 16)};
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 12) { // the tails: row positions 3(K+32) .. +11
+    const int t = threadIdx.x;
+    const uint32_t o = 3u * (K + 32) + t;
+    auto tail = [&](const Blk &b, const uint32_t *l) -> uint32_t {
+      const uint32_t m = glob(b.inv)[o];
+      const uint32_t old = b.fresh ? 0u : (uint16_t)glob(b.row)[o];
+      return value(b, reinterpret_cast<const uint16_t *>(l), m, old) & 0xFFFFu;
+    };
+    const uint32_t va = tail(ba, llr0), vb = tail(bb, llr1);
+    glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = va | (vb << 16);
+  }
+}
+
 // XOR-reduce one value per thread over the workgroup
 __device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
@@ -168,6 +339,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint32_t *__restrict__ noi_in,
                                                    const uint32_t *__restrict__ crc_a) {
   __shared__ uint32_t red[4];
+  __shared__ uint32_t crc_tab[256];
   __shared__ uint32_t c_g[TBF_MAXC], c_dst[TBF_MAXC], c_nb[TBF_MAXC], c_rb[TBF_MAXC];
   __shared__ uint8_t c_init[TBF_MAXC], c_ok[TBF_MAXC];
   __shared__ int all_ok;
@@ -265,29 +437,44 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       for (uint32_t j = threadIdx.x; j < c_rb[i]; j += blockDim.x) dst[j] = src[j];
     }
   }
-  // 3. TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491), as a parallel XOR fold:
-  //    crc.c:144-155 is linear, the checksum is the XOR of x^(tbs-1-p+24) mod P over set bits p.
-  //    Eight bytes per thread and round: their 64 weight loads are issued before any is used.
+  // 3. TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491). crc.c:144-155 (MSB
+  //    first, zero init) is linear: the checksum is M(x) x^24 mod P. The TB's bytes are cut into
+  //    32-byte chunks counted from the end; thread c runs the byte-table CRC over chunk c (chunk
+  //    c ends 256 c bits before the message end) and shifts it into place, x^(256 c) mod P =
+  //    crc_a[256 c - 24] (c > 0), by a carry-less multiply mod P; the chunks' values are XORed.
+  //    (The bit-weight fold this replaces read 4 B of weights per message bit.)
   uint32_t crc = 0;
   if (ok_all) {
+    if (threadIdx.x < 256) { // byte table: T[i] = i x^24 mod P, i.e. i << 16 through 8 shift steps
+      uint32_t r = threadIdx.x << 16;
+#pragma unroll
+      for (int k = 0; k < 8; k++) r = ((r << 1) ^ ((r & 0x800000u) ? 0x864CFBu : 0u)) & 0xFFFFFFu;
+      crc_tab[threadIdx.x] = r;
+    }
+    __syncthreads();
+    constexpr uint32_t B = 32;
+    const uint32_t nbytes = t.tbs / 8, nch = (nbytes + B - 1) / B;
     uint32_t acc = 0;
-    const uint32_t nbytes = t.tbs / 8;
-    constexpr int U = 8;
-    for (uint32_t j0 = threadIdx.x; j0 < nbytes; j0 += blockDim.x * U) {
-      uint32_t v[U], w[U][8];
+    for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+      const uint32_t end = nbytes - c * B, beg = end > B ? end - B : 0;
+      const uint8_t *src = t.data + beg;
+      uint8_t v[B];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t j = j0 + u * blockDim.x;
-        const uint32_t jj = j < nbytes ? j : j0;
-        v[u] = j < nbytes ? t.data[jj] : 0u;
-        const uint32_t *wp = crc_a + (t.tbs - 1 - 8 * jj); // wp[-b]: bit b (MSB first) of byte j
+      for (uint32_t k = 0; k < B; k++) v[k] = k < end - beg ? src[k] : 0;
+      uint32_t r = 0;
 #pragma unroll
-        for (int bb = 0; bb < 8; bb++) w[u][bb] = wp[-bb];
+      for (uint32_t k = 0; k < B; k++)
+        if (k < end - beg) r = ((r << 8) & 0xFFFFFFu) ^ crc_tab[((r >> 16) ^ v[k]) & 0xFFu];
+      if (c > 0) { // r x^(256 c) mod P
+        const uint32_t w = crc_a[256 * c - 24];
+        uint64_t m = 0;
+        for (int i = 0; i < 24; i++)
+          if ((w >> i) & 1u) m ^= (uint64_t)r << i;
+        for (int bit = 46; bit >= 24; bit--)
+          if ((m >> bit) & 1u) m ^= (uint64_t)0x1864CFBu << (bit - 24);
+        r = (uint32_t)m & 0xFFFFFFu;
       }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-#pragma unroll
-        for (int bb = 0; bb < 8; bb++) acc ^= w[u][bb] & (0u - ((v[u] >> (7 - bb)) & 1u));
+      acc ^= r;
     }
     crc = wg_xor(acc, red);
   }
@@ -307,10 +494,28 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
 static inline unsigned cdiv(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st) {
+                       hipStream_t st, int phase) {
   if (nitems <= 0) return hipSuccess;
   (void)max_n;
-  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done);
+  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done, phase);
+  return hipGetLastError();
+}
+
+hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, hipStream_t st) {
+  if (nitems <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_derm_flags, dim3(cdiv((size_t)nitems, 256)), dim3(256), 0, st, d_items, nitems,
+                     init_done);
+  return hipGetLastError();
+}
+
+hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermItem *items,
+                            const TdArrays &a, uint32_t max_ne, hipStream_t st) {
+  if (ng <= 0 || nblocks <= 0) return hipSuccess;
+  // LLRs staged per block: the largest E of the call, rounded to 8, at most 8192 (16 KB); blocks
+  // with more (or with repetition, E > 3K+12) gather theirs from HBM
+  const uint32_t stage = std::min<uint32_t>(8192, (max_ne + 7) / 8 * 8);
+  const size_t lds = 6 * LDR_TILE * 2 + 4 * (size_t)stage;
+  hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, items, a, stage);
   return hipGetLastError();
 }
 

@@ -17,8 +17,9 @@
 #include "srsgpu/tdec_batch.h"
 #include "srslte/phy/fec/turbodecoder.h"
 #include "tdec_kernels.h"
+#include "dlsch_kernels.h"
 
-#define HIPCHK(x)                                                                                 \
+#define HIPCHK(x)                                                                               \
   do {                                                                                            \
     hipError_t e_ = (x);                                                                          \
     if (e_ != hipSuccess) {                                                                       \
@@ -394,16 +395,23 @@ struct TdecEngine {
   // load the inputs of the planned groups; first: reset the per-CB flags of the whole job
   // (total_cbs code blocks; init_done seeds cb_done: blocks already decoded are skipped, noi 0).
   // flags = false: a fixed-half-iteration job, which never reads the early-stop flags
+  // derm: the DL-SCH's de-rate-matching items by decoder position; groups whose loader would be
+  // k_load_sbt (16-byte aligned sub-block rows, nb a multiple of 8) are loaded by k_load_derm
+  // from the items' LLRs instead of from their rows (the items are marked `direct` by the caller)
+  uint32_t derm_max_ne = 0; // the largest E among the direct items of the next job (set by the caller)
+  static bool derm_direct(const TdGroup &g, int rows_aligned) {
+    return g.sb_input && rows_aligned >= 16 && g.nb % 8 == 0;
+  }
   int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
                    int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs,
-                   bool flags = true) {
+                   bool flags = true, const DermItem *derm = nullptr) {
     // load launches: runs of groups with the same loader (nb, sb_input); rows_aligned is the
     // byte alignment every row is guaranteed to have (0: none)
     const size_t ng = groups.size();
     struct Run {
       size_t g0, g1;
       int blocks;
-      bool vec;
+      bool vec, direct;
     };
     std::vector<Run> runs;
     for (size_t g0 = 0; g0 < ng;) {
@@ -411,6 +419,7 @@ struct TdecEngine {
       bool vec = f.sb_input ? (rows ? rows_aligned >= 16
                                     : ((uintptr_t)d_in % 16 == 0 && (in_stride * 2) % 16 == 0))
                             : (rows ? rows_aligned >= 8 : ((uintptr_t)d_in % 8 == 0 && in_stride % 4 == 0));
+      const bool direct = derm && rows && derm_direct(f, rows_aligned);
       size_t g1 = g0;
       while (g1 < ng && groups[g1].nb == f.nb && groups[g1].sb_input == f.sb_input) {
         if (!f.sb_input) vec = vec && (groups[g1].K / groups[g1].nb) % 4 == 0;
@@ -419,16 +428,22 @@ struct TdecEngine {
       int blocks = 0;
       for (size_t g = g0; g < g1; g++) {
         groups[g].blk_load = blocks;
-        blocks += load_blocks(groups[g].K, groups[g].nb, groups[g].npairs, groups[g].sb_input,
-                              f.sb_input && vec);
+        blocks += direct ? groups[g].npairs
+                         : load_blocks(groups[g].K, groups[g].nb, groups[g].npairs, groups[g].sb_input,
+                                       f.sb_input && vec);
       }
-      runs.push_back(Run{g0, g1, blocks, vec});
+      runs.push_back(Run{g0, g1, blocks, vec, direct});
       g0 = g1;
     }
     if (upload_groups()) return -1;
     const TdArrays a = arrays();
     for (const Run &r : runs) {
       const TdGroup &f = groups[r.g0];
+      if (r.direct) {
+        ProfScope ps("k_ldderm", st); // k_load_derm (a name no other scope contains: srsgpu_prof_get matches substrings)
+        HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, derm, a, derm_max_ne, st));
+        continue;
+      }
       ProfScope ps("k_load", st);
       HIPCHK(launch_load(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, f.nb, f.sb_input, r.vec, d_in,
                          in_stride, rows, a, st));
@@ -660,7 +675,7 @@ struct TdecEngine {
   int decode_multi(int impl, int sb_layout, const std::vector<TdSpec> &specs, uint32_t total_cbs,
                    const int16_t *d_in, size_t in_stride, const int16_t *const *rows, int rows_aligned,
                    const uint8_t *init_done, uint32_t maxh, uint8_t *d_out, size_t out_stride,
-                   uint8_t *d_ok, uint32_t *d_noi, bool fixed = false) {
+                   uint8_t *d_ok, uint32_t *d_noi, bool fixed = false, const DermItem *derm = nullptr) {
     if (maxh == 0 || total_cbs > cap_cbs) {
       fprintf(stderr, "srsgpu: invalid early-stop job (max_halfits=%u, %u code blocks)\n", maxh, total_cbs);
       return -1;
@@ -686,7 +701,7 @@ struct TdecEngine {
         if (r > 0) fprintf(stderr, "srsgpu: code block group exceeds the decoder capacity\n");
         return -1;
       }
-      if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs)) return -1;
+      if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs, true, derm)) return -1;
       if (fixed) { // all maxh half-iterations, then one CRC check (no early stop: measurement mode)
         if (halfits_fixed((int)maxh) || decide((int)maxh - 1, d_out, out_stride, true, maxh)) return -1;
       } else if (decode_planned(maxh, d_out, out_stride)) {

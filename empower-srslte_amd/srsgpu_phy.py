@@ -347,6 +347,7 @@ _sig = {
     "srsgpu_rxq_set_phich": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_set_early_stop": (None, [_vp, _i32]),
     "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_dlsch_set_direct_derm": (None, [_vp, _i32]),
     "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
     "srsgpu_pdsch_set_noise_dev": (None, [_vp, _vp]),
     "srsgpu_pdsch_get_dlsch": (_vp, [_vp]),
@@ -570,6 +571,10 @@ class Dlsch:
     def set_early_stop(self, on):
         """srsgpu_dlsch_set_early_stop (off: every CB runs max_halfits, one CRC check at the end)"""
         _lib.srsgpu_dlsch_set_early_stop(self.q, int(bool(on)))
+
+    def set_direct_derm(self, on):
+        """srsgpu_dlsch_set_direct_derm (off: every softbuffer row written before the decode)"""
+        _lib.srsgpu_dlsch_set_direct_derm(self.q, int(bool(on)))
 
     def reset_range(self, first, count):
         if _lib.srsgpu_dlsch_softbuffer_reset_range(self.q, first, count) != 0:

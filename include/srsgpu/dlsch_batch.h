@@ -104,6 +104,15 @@ void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable);
  * half-iterations and its CRC is checked once after the last (the fixed-iteration processing rate
  * on real codewords; nof_iterations then reports max_halfits). */
 void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable);
+/* Direct de-rate-matching (default on). Code blocks of the window decoders (K > 400 under AUTO)
+ * are de-rate-matched and HARQ-combined straight into the decoder's inputs, and their softbuffer
+ * rows are written after the decode only when their TB failed (every block not decoded before
+ * the call, exactly as srslte_rm_turbo_rx_lut leaves them). Decoded bytes, return codes,
+ * nof_iterations and cb_crc are identical either way. The rows of an acked TB are left as they
+ * were: the reference never reads them again (sch.c:323 skips blocks whose CRC passed, and the
+ * next TB resets the softbuffer), so only srsgpu_dlsch_softbuffer_read can tell. Off: every row is
+ * written before the decode (the reference's order). */
+void srsgpu_dlsch_set_direct_derm(srsgpu_dlsch_t *q, int enable);
 /* srslte_rm_turbo_rx_lut_8bit (rm_turbo.c:432-469) on device buffers, int8 values held in int16
  * elements: d_out[t[i % (3K+12)]] += d_in[i], wrapping at 8 bits, 8-bit decoder sub-block table. */
 int srsgpu_rm_turbo_rx_8bit_dev(srsgpu_dlsch_t *q, const int16_t *d_in, int16_t *d_out,

@@ -87,6 +87,42 @@ def test_softbuffer_soft_bits_vs_oracle(s, dl, dgold):
     g.close()
 
 
+def test_direct_derm_rows(s, dl, dgold):
+    """Direct de-rate-matching: a failed TB leaves every row of its not-yet-decoded blocks as the
+    oracle's srslte_rm_turbo_rx_lut (all C rows, also those whose CRC passed in this call); an
+    acked TB's rows are not written (read back as a reset row); decoded bytes, ret, noi and cb_crc
+    equal the reference over the whole HARQ sequence in both modes."""
+    z, man = dgold
+    tbc = [c for c in man if c["kind"] == "tb" and c["C"] > 1]
+    for c in tbc:
+        outs = {}
+        for direct in (True, False):
+            g = s.Dlsch(1, 16, 32)
+            g.set_direct_derm(direct)
+            g.reset(0)
+            sb = dl.softbuffer(16)
+            dl.reset(sb)
+            res = []
+            for t, st in enumerate(c["steps"]):
+                llr = z["%s_t%d_llr" % (c["key"], t)]
+                ret, data, noi = g.decode([_tb(c["tbs"], st["rv"], c["Qm"], c["nbits"], 0)], [llr],
+                                          c["max_halfits"])
+                dl.decode(sb, c["tbs"], st["rv"], c["Qm"], llr, c["max_halfits"])
+                rows, crc = g.read_softbuffer(0)
+                orows = np.ctypeslib.as_array(sb.buffer, shape=(16 * SOFTBUFFER_SIZE,)).reshape(16, -1)
+                if st["ret"] != 0 or not direct:
+                    assert (rows[:c["C"]] == orows[:c["C"]]).all(), (c["key"], t, direct)
+                res.append((ret[0], noi[0], data[0][:(c["tbs"] + 24) // 8].tobytes(), crc[:c["C"]].tobytes()))
+                assert ret[0] == st["ret"] and noi[0] == st["noi"], (c["key"], t, direct)
+            if direct and c["steps"][0]["ret"] == 0:
+                rows, _ = g.read_softbuffer(0)
+                assert not rows[:c["C"]].any()  # acked on the first transmission: rows never written
+            outs[direct] = res
+            dl.free(sb)
+            g.close()
+        assert outs[True] == outs[False], c["key"]
+
+
 def test_rate_dematching_dev_golden(s, oracle, dgold):
     import torch
     z, man = dgold
@@ -103,14 +139,19 @@ def test_rate_dematching_dev_golden(s, oracle, dgold):
     g.close()
 
 
-def test_random_harq_batches_vs_oracle(s, dl, oracle):
+@pytest.mark.parametrize("direct", [True, False])
+def test_random_harq_batches_vs_oracle(s, dl, oracle, direct):
     """Batches of random TBs (varied TBS/Qm/E/SNR/rv) across several HARQ rounds, one call per
-    round, against the oracle with its own softbuffers."""
+    round, against the oracle with its own softbuffers; with the direct de-rate-matching
+    (srsgpu_dlsch_set_direct_derm, the default: rows written after the decode for failed TBs only)
+    and without it. E spans short blocks, E > 8192 (LLRs gathered from HBM) and E > 3K+12
+    (repetition)."""
     rng = np.random.default_rng(77)
     good = [t for t in list(range(16, 6200, 24)) + list(range(6200, 80000, 312))
             if oracle.cbsegm(t)[5] == 0]
     n = 12
     g = s.Dlsch(n, 16, 256)
+    g.set_direct_derm(direct)
     osb = [dl.softbuffer(16) for _ in range(n)]
     tbl, datas = [], []
     for i in range(n):
