@@ -903,12 +903,13 @@ C3_KS = [5824] * 13
 ALG_BYTES_PER_SF = {
     # 14 symbols of N complex-float samples in (CPs skipped), the 16,800-RE grid out
     "k_ofdm_rx": lambda N: 14 * N * 8 + C3_GRID * 8,
-    # 4 x 200 CRS pilots in, the 16,800-RE estimate grid and the noise estimate out
-    "k_chest": lambda N: 800 * 8 + C3_GRID * 8 + 4,
+    # 4 x 200 CRS pilots in, the estimator's compact rows (4 x 1200 RE: srsgpu_chest_set_ce_rows, the
+    # traffic legs' form) and the noise estimate out
+    "k_chest": lambda N: 800 * 8 + 4 * 1200 * 8 + 4,
     # the subframe's Gold sequence bits out
     "k_gold": lambda N: C3_NLLR // 8,
-    # grid and estimate of the 15,000 PDSCH REs in, 90,000 int16 LLRs out
-    "k_pdsch_llr": lambda N: C3_NRE * 8 * 2 + C3_NLLR * 2,
+    # grid of the 15,000 PDSCH REs and the 4 estimate rows in, 90,000 int16 LLRs out
+    "k_pdsch_llr": lambda N: C3_NRE * 8 + 4 * 1200 * 8 + C3_NLLR * 2,
     # LLRs in, the 13 softbuffer rows (3(K+32)+12 int16) out
     "k_derm": lambda N: C3_NLLR * 2 + sum((3 * (k + 32) + 12) * 2 for k in C3_KS),
     # rows in, the decoder's systematic / parity planes out: 6 B + 6 B per info bit
@@ -931,7 +932,7 @@ HEADLINE_SNR_DB = 20.0
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
 HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 1}, "per_halfit": {"es_fused": 0},
                "fused_c1": {"es_fused": 1, "es_chunk": 1}, "fused_c2": {"es_fused": 1, "es_chunk": 2},
-               "fused_c8": {"es_fused": 1, "es_chunk": 8}}
+               "fused_c8": {"es_fused": 1, "es_chunk": 8}, "hybrid": {"es_fused": 3, "es_chunk": 8}}
 
 
 def pipeline_roofline(leg, nsf_per_batch):

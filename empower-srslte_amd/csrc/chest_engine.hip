@@ -54,6 +54,7 @@ struct ChestEngine {
   int flen = 3;
   float filt[64] = {0.1f, 1 - 2 * 0.1f, 0.1f};
   bool filt_dirty = true;
+  bool ce_rows = false; // srsgpu_chest_set_ce_rows
   ChestItem *h_items = nullptr, *d_items = nullptr;
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
@@ -140,6 +141,7 @@ struct ChestEngine {
     kc.rsrp_neighbour = cfg.rsrp_neighbour ? 1 : 0;
     kc.cfo_n = (float)cfg.symbol_sz;
     kc.cfo_ng = ceilf((144.0f * (float)cfg.symbol_sz) / 2048.0f); // SRSLTE_CP_LEN_NORM(1, n)
+    kc.rows = ce_rows ? 1 : 0;
     ProfScope ps("k_chest", st);
     HIPCHK(launch_chest(d_items, (int)(n * np), kc, d_crs, d_filt, d_pss, st));
     return 0;
@@ -237,6 +239,10 @@ int srsgpu_chest_set_smooth_filter_gauss(srsgpu_chest_t *q, uint32_t order, floa
   const float inv = 1.0f / norm;
   for (uint32_t i = 0; i < len; i++) f[i] *= inv;
   return srsgpu_chest_set_smooth_filter(q, f, len);
+}
+
+void srsgpu_chest_set_ce_rows(srsgpu_chest_t *q, int enable) {
+  if (q) q->e.ce_rows = enable != 0;
 }
 
 int srsgpu_chest_set_cfg(srsgpu_chest_t *q, const srsgpu_chest_cfg_t *cfg) {

@@ -25,6 +25,8 @@ struct ChestCfg {
   int filt_auto;      // smooth_filter_auto: order-4 Gaussian from the noise estimate
   int rsrp_neighbour; // rsrp_corr computed
   float cfo_n, cfo_ng; // CFO formula: symbol size and normal-CP length of symbol 1
+  int rows;           // compact output: the CRS symbols' frequency-interpolated rows (4 x nsc, or
+                      // the averaged row, 1 x nsc) instead of the 14 x nsc grid (srsgpu_chest_set_ce_rows)
 };
 // crs: [10 subframes][4 CRS symbols][2*nof_prb] port-0/1 pilots; filt: up to 64 taps; pss: the
 // 62-element PSS of the cell's N_id_2

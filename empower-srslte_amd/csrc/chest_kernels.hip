@@ -50,22 +50,28 @@ __device__ __forceinline__ float cpow(c32 a) { return a.x * a.x + a.y * a.y; }
 #define CH_NRED 7
 
 // block-wide sums of nv per-thread values (block-uniform call, 256 threads); results in red[j][0].
-// The pairwise tree red[t] += red[t + s], s = 128 .. 1: the two wide levels in LDS, the six levels
-// inside wave 0 with shuffles (lane t adds lane t + s, as the tree does), so the sums are the
-// tree's, with 4 barriers instead of 9.
-__device__ __forceinline__ void block_sum(float (*red)[256], const float *v, int nv) {
-  for (int j = 0; j < nv; j++) red[j][threadIdx.x] = v[j];
+// The pairwise tree red[t] += red[t + s], s = 128 .. 1: the two wide levels through LDS (the upper
+// half hands its values to the lower half, which adds them in registers), the six levels inside
+// wave 0 with shuffles (lane t adds lane t + s, as the tree does), so the sums are the tree's, with
+// 4 barriers instead of 9 and 128 LDS words per value instead of 256.
+template <int nv> __device__ __forceinline__ void block_sum(float (*red)[128], const float *v) {
+  const int t = threadIdx.x;
+  float x[nv];
+  _Pragma("unroll") for (int j = 0; j < nv; j++) x[j] = v[j];
+  if (t >= 128)
+    _Pragma("unroll") for (int j = 0; j < nv; j++) red[j][t - 128] = x[j];
   __syncthreads();
-  for (int s = 128; s >= 64; s >>= 1) {
-    if ((int)threadIdx.x < s)
-      for (int j = 0; j < nv; j++) red[j][threadIdx.x] += red[j][threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x < 64) {
-    for (int j = 0; j < nv; j++) {
-      float x = red[j][threadIdx.x];
-      for (int s = 32; s > 0; s >>= 1) x += __shfl_down(x, s);
-      if (threadIdx.x == 0) red[j][0] = x;
+  if (t < 128)
+    _Pragma("unroll") for (int j = 0; j < nv; j++) x[j] += red[j][t];
+  __syncthreads();
+  if (t >= 64 && t < 128)
+    _Pragma("unroll") for (int j = 0; j < nv; j++) red[j][t - 64] = x[j];
+  __syncthreads();
+  if (t < 64) {
+    _Pragma("unroll") for (int j = 0; j < nv; j++) {
+      float y = x[j] + red[j][t];
+      for (int s = 32; s > 0; s >>= 1) y += __shfl_down(y, s);
+      if (t == 0) red[j][0] = y;
     }
   }
   __syncthreads();
@@ -111,7 +117,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
                                                const float2 *__restrict__ pss) {
   __shared__ c32 ls[4 * CH_MAXP]; // LS estimates, row l at l * np (the reference's pilot_estimates)
   __shared__ c32 sm[4 * CH_MAXP];
-  __shared__ float red[CH_NRED][256];
+  __shared__ float red[CH_NRED][128];
   __shared__ float fs[64];
   __shared__ float s_noise;
   const int it = blockIdx.x;
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
         v[6] += p.y;
       }
     }
-    block_sum(red, v, CH_NRED);
+    block_sum<CH_NRED>(red, v);
     if (tid == 0) {
       if (refs) {
         s_noise = red[0][0] / (float)np / 4.0f * sqrtf(5.0f);
@@ -250,7 +256,10 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
     c32 c6;
     if (cfg.average) {
       const c32 v = interp_at(rows, 2 * np, k, cell_id % 3, 3, 1.0f / 3);
-      for (int s = 0; s < 14; s++) ce[s * nsc + k] = v;
+      if (cfg.rows)
+        ce[k] = v;
+      else
+        for (int s = 0; s < 14; s++) ce[s * nsc + k] = v;
       c6 = v;
     } else {
       c32 f[4];
@@ -273,7 +282,10 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
       col[10] = cadd(col[9], d);
       col[12] = cadd(f[3], d);
       col[13] = cadd(col[12], d);
-      for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
+      if (cfg.rows) // the reader interpolates in time with these same operations (pdsch ce_at)
+        for (int l = 0; l < 4; l++) ce[l * nsc + k] = f[l];
+      else
+        for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
       c6 = col[6];
     }
     if (pss_on && k >= k0 && k < k0 + 62) // estimate_noise_pss: ce * PSS - received
@@ -281,7 +293,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   }
   // 8. PSS / EMPTY noise, subframes 0 and 5 only (otherwise the value is left as it was)
   if (pss_on) {
-    block_sum(red, &pacc, 1);
+    block_sum<1>(red, &pacc);
     if (tid == 0) *t.noise = (float)((double)((float)cfg.nof_ports * (red[0][0] / 62.0f)) / sqrt(2.0));
   } else if (nz05 && tid == 0) { // estimate_noise_empty_sc: 5 empty subcarriers either side of SSS / PSS
     float np_ = 0.f;

@@ -122,6 +122,7 @@ struct DlschEngine {
   uint32_t *d_cbmap = nullptr;
   uint8_t *d_init = nullptr, *d_dec = nullptr, *d_ok = nullptr;
   uint32_t *d_noi = nullptr;
+  uint32_t *d_late = nullptr; // [1 + cap]: count, then the decoder positions of the deferred rows
   int32_t *d_ret_stage = nullptr;
   uint32_t *d_noi_stage = nullptr;
   // pinned staging for the per-call descriptors, reused once the previous copies completed
@@ -171,6 +172,7 @@ struct DlschEngine {
     HIPCHK(hipMalloc(&d_dec, (size_t)cap * 768));
     HIPCHK(hipMalloc(&d_ok, cap));
     HIPCHK(hipMalloc(&d_noi, sizeof(uint32_t) * cap));
+    HIPCHK(hipMalloc(&d_late, sizeof(uint32_t) * (cap + 1)));
     HIPCHK(hipMalloc(&d_ret_stage, sizeof(int32_t) * cap));
     HIPCHK(hipMalloc(&d_noi_stage, sizeof(uint32_t) * cap));
     HIPCHK(hipHostMalloc(&h_items, sizeof(DermItem) * cap));
@@ -198,7 +200,7 @@ struct DlschEngine {
     if (st) (void)hipStreamSynchronize(st);
     for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
-                    (void *)d_noi, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
+                    (void *)d_noi, (void *)d_late, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
                     (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
@@ -306,13 +308,9 @@ struct DlschEngine {
   // next de-rate-matching pass treats a fresh softbuffer's rows as zero and rewrites them whole)
   int reset(uint32_t slot, uint32_t count, uint32_t ncb) {
     if (slot + count > nslots) return -1;
-    if (ncb < max_cb) { // reset_tbs: the first ncb rows only
-      for (uint32_t s = slot; s < slot + count; s++)
-        HIPCHK(hipMemsetAsync(fresh + (size_t)s * max_cb, 1, ncb, st));
-    } else {
-      HIPCHK(hipMemsetAsync(fresh + (size_t)slot * max_cb, 1, (size_t)count * max_cb, st));
-    }
-    HIPCHK(hipMemsetAsync(cbcrc + (size_t)slot * max_cb, 0, (size_t)count * max_cb, st));
+    // one launch: fresh = 1 for the first ncb rows of each slot (reset_tbs), cb_crc = 0 for all
+    HIPCHK(launch_sb_reset(fresh + (size_t)slot * max_cb, cbcrc + (size_t)slot * max_cb, count, max_cb,
+                           std::min(ncb, max_cb), st));
     return 0;
   }
 
@@ -445,10 +443,10 @@ struct DlschEngine {
     HIPCHK(hipMemcpyAsync(d_tbs, h_tbs, sizeof(TbItem) * ntb, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    if (ndirect) HIPCHK(launch_derm_flags(d_items, (int)ncb, d_init, st));
+    if (ndirect) HIPCHK(launch_derm_flags(d_items, (int)ncb, d_init, d_late, st));
     if (ndirect < ncb) {
       ProfScope ps("k_derm", st);
-      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st, 0));
+      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st));
     }
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;
@@ -468,11 +466,12 @@ struct DlschEngine {
       return -1;
     {
       ProfScope ps("k_tb_finish", st);
-      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st));
+      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st,
+                              ndirect ? d_items : nullptr, ndirect ? d_late : nullptr));
     }
     if (ndirect) { // rows of the direct blocks of failed TBs, for the retransmission
-      ProfScope ps("k_rows_late", st); // k_derm, phase 1
-      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st, 1));
+      ProfScope ps("k_rows_late", st); // k_derm_late
+      HIPCHK(launch_derm_late(d_items, (int)ncb, d_late, st));
     }
     return 0;
   }

@@ -50,18 +50,28 @@ struct EncItem {
   uint32_t crc_cb;         // C > 1: CB CRC24B
 };
 
-// phase 0: rows of the items that are not `direct` (before the decode); phase 1: rows of the
-// direct items whose TB failed and that were not decoded before this call (after k_tb_finish)
+// rows of the items that are not `direct` (before the decode), init_done of every item
 hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st, int phase = 0);
-// init_done[pos] = cb_crc before this call, for every item
-hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, hipStream_t st);
+                       hipStream_t st);
+// after k_tb_finish: rows of the direct items it listed in late (late[0] of them at late[1..]:
+// blocks of failed TBs not decoded before this call)
+hipError_t launch_derm_late(const DermItem *d_items, int nitems, const uint32_t *late, hipStream_t st);
+// init_done[pos] = cb_crc before this call, for every item; late[0] = 0 (late may be null)
+hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, uint32_t *late,
+                             hipStream_t st);
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
+// softbuffer reset of count slots of max_cb rows from fresh / cbcrc: cb_crc = 0, the first ncb
+// rows of each slot fresh
+hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint32_t max_cb, uint32_t ncb,
+                           hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
 // crc_a[d] = x^(d+24) mod P_24A for d < the largest TBS + 24
+// items / late (both or neither): a failed TB appends its direct blocks not decoded before the
+// call to late (launch_derm_late)
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
-                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st);
+                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
+                            const DermItem *items = nullptr, uint32_t *late = nullptr);
 // crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
 hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
                                const uint32_t *crc_b, hipStream_t st);

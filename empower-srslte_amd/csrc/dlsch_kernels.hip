@@ -75,19 +75,8 @@ __device__ __forceinline__ void stage_llrs(uint32_t *es, const int16_t *ep, uint
 // items of failed TBs that were not decoded before this call (their rows as the reference leaves
 // them; an acked TB's rows are never read again: sch.c:323 skips blocks whose CRC passed, and the
 // next TB resets the softbuffer)
-__global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
-                                              uint8_t *__restrict__ init_done, int phase) {
-  __shared__ uint32_t es[DERM_LDS / 2];
-  const int g = blockIdx.x;
-  if (g >= nitems) return;
-  const DermItem it = items[g];
-  if (phase == 0) {
-    const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
-    if (threadIdx.x == 0) init_done[it.pos] = skip;
-    if (skip || it.direct) return; // sch.c:323: blocks whose CRC passed before are not combined again
-  } else {
-    if (!it.direct || init_done[it.pos] || *glob(it.tb_ret) == 0) return;
-  }
+// one code block into its row by the whole workgroup (es: DERM_LDS / 2 words of LDS)
+__device__ __forceinline__ void derm_item(const DermItem &it, uint32_t *es) {
   const bool fresh = it.fresh && *glob(it.fresh);
   const bool w8 = it.w8 != 0;
   const uint32_t N = it.N, ne = it.ne, len = it.rowlen;
@@ -146,6 +135,32 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
   if (fresh && threadIdx.x == 0) *glob(it.fresh) = 0; // the row now holds real soft bits
 }
 
+__global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
+                                              uint8_t *__restrict__ init_done) {
+  __shared__ uint32_t es[DERM_LDS / 2];
+  const int g = blockIdx.x;
+  if (g >= nitems) return;
+  const DermItem it = items[g];
+  const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
+  if (threadIdx.x == 0) init_done[it.pos] = skip;
+  if (skip || it.direct) return; // sch.c:323: blocks whose CRC passed before are not combined again
+  derm_item(it, es);
+}
+
+// the deferred rows: the direct blocks k_tb_finish listed (late[0] of them at late[1..], decoder
+// positions: blocks of failed TBs not decoded before the call), a few workgroups looping over the
+// list, so an all-acked batch costs one short launch
+__global__ __launch_bounds__(256) void k_derm_late(const DermItem *__restrict__ items,
+                                                   const uint32_t *__restrict__ late) {
+  __shared__ uint32_t es[DERM_LDS / 2];
+  const uint32_t n = late[0];
+  for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+    const DermItem it = items[late[1 + q]];
+    derm_item(it, es);
+    __syncthreads(); // es is reused by the next block
+  }
+}
+
 // srsgpu_rm_turbo_rx_dev: arbitrary output buffers, read-modify-write in place (one block)
 __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ items) {
   const DermItem it = items[0];
@@ -160,8 +175,9 @@ __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ i
 }
 
 __global__ __launch_bounds__(256) void k_derm_flags(const DermItem *__restrict__ items, int n,
-                                                    uint8_t *__restrict__ init_done) {
+                                                    uint8_t *__restrict__ init_done, uint32_t *__restrict__ late) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0 && late) late[0] = 0;
   if (i >= n) return;
   const uint8_t *c = items[i].cb_crc;
   init_done[items[i].pos] = c ? *glob(c) : 0;
@@ -337,7 +353,9 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint8_t *__restrict__ cb_ok_in,
                                                    const uint8_t *__restrict__ init_done,
                                                    const uint32_t *__restrict__ noi_in,
-                                                   const uint32_t *__restrict__ crc_a) {
+                                                   const uint32_t *__restrict__ crc_a,
+                                                   const DermItem *__restrict__ items,
+                                                   uint32_t *__restrict__ late) {
   __shared__ uint32_t red[4];
   __shared__ uint32_t crc_tab[256];
   __shared__ uint32_t c_g[TBF_MAXC], c_dst[TBF_MAXC], c_nb[TBF_MAXC], c_rb[TBF_MAXC];
@@ -429,6 +447,9 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   __syncthreads();
   const int ok_all = all_ok;
   if (!ok_all) {
+    // the direct blocks of this failed TB that were not decoded before: their rows are due
+    if (late && threadIdx.x < C && !c_init[threadIdx.x] && items[c_g[threadIdx.x]].direct)
+      late[1 + atomicAdd(late, 1u)] = c_g[threadIdx.x];
     // keep the bytes of the blocks that passed for the retransmission (sch.c:407-416)
     for (uint32_t i = 0; i < C; i++) {
       if (!c_ok[i]) continue;
@@ -493,18 +514,43 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
 
 static inline unsigned cdiv(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
-hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st, int phase) {
-  if (nitems <= 0) return hipSuccess;
-  (void)max_n;
-  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done, phase);
+// srslte_softbuffer_rx_reset(_tbs) of count consecutive softbuffers: cb_crc cleared, the first ncb
+// rows marked fresh (their soft bits count as zero until rewritten)
+__global__ __launch_bounds__(256) void k_sb_reset(uint8_t *__restrict__ fresh, uint8_t *__restrict__ cbcrc,
+                                                  uint32_t n, uint32_t max_cb, uint32_t ncb) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  cbcrc[i] = 0;
+  if (i % max_cb < ncb) fresh[i] = 1;
+}
+
+hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint32_t max_cb, uint32_t ncb,
+                           hipStream_t st) {
+  const size_t n = (size_t)count * max_cb;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sb_reset, dim3(cdiv(n, 256)), dim3(256), 0, st, fresh, cbcrc, (uint32_t)n, max_cb, ncb);
   return hipGetLastError();
 }
 
-hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, hipStream_t st) {
+hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
+                       hipStream_t st) {
+  if (nitems <= 0) return hipSuccess;
+  (void)max_n;
+  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done);
+  return hipGetLastError();
+}
+
+hipError_t launch_derm_late(const DermItem *d_items, int nitems, const uint32_t *late, hipStream_t st) {
+  if (nitems <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_derm_late, dim3((unsigned)std::min(nitems, 512)), dim3(256), 0, st, d_items, late);
+  return hipGetLastError();
+}
+
+hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, uint32_t *late,
+                             hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_derm_flags, dim3(cdiv((size_t)nitems, 256)), dim3(256), 0, st, d_items, nitems,
-                     init_done);
+                     init_done, late);
   return hipGetLastError();
 }
 
@@ -527,10 +573,11 @@ hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st) {
 
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
-                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st) {
+                            const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
+                            const DermItem *items, uint32_t *late) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi, crc_a);
+                     dec_stride, cb_ok, init_done, noi, crc_a, items, late);
   return hipGetLastError();
 }
 

@@ -161,6 +161,12 @@ template <int R> __device__ __forceinline__ void bfly(const cf *v, cf *y) {
 // buffer per symbol instead of a ping-pong pair, so twice the workgroups fit in a CU's LDS, and no
 // separate pass copies the input into LDS. `live` = the thread's symbol exists (others compute on
 // zeros and only keep the barriers).
+// LDS slot of element p: one pad slot after every 16 elements (128 B), so the strided butterfly
+// writes of the first stages (element stride 8 and 64) spread over all banks instead of landing 8-
+// and 16-fold on the same ones
+__device__ __forceinline__ int lpad(int p) { return p + (p >> 4); }
+template <int N> constexpr int lds_slots() { return N + N / 16; }
+
 template <int R, int N, int Ns, int TPS, bool FIRST>
 __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, const float2 *__restrict__ tw,
                                          int t, bool live) {
@@ -178,7 +184,7 @@ __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, co
         if (FIRST) {
           if (live) a = src[j + r * nb];
         } else {
-          a = buf[j + r * nb];
+          a = buf[lpad(j + r * nb)];
           if (Ns > 1 && r) { // e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
             const float2 w = tw[r * k * (N / (Ns * R))];
             a = cmul(a, cf{w.x, w.y});
@@ -198,7 +204,7 @@ __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, co
     bfly<R>(v[q], y);
     const int o = (j / Ns) * Ns * R + k;
 #pragma unroll
-    for (int r = 0; r < R; r++) buf[o + r * Ns] = y[r];
+    for (int r = 0; r < R; r++) buf[lpad(o + r * Ns)] = y[r];
   }
   __syncthreads();
 }
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
                                                    int nre, int cp0, int cp,
                                                    const float2 *__restrict__ tw, float scale) {
   constexpr int S = syms_per_wg<N>(), TPS = 256 / S;
-  __shared__ cf buf[S][N];
+  __shared__ cf buf[S][lds_slots<N>()];
   const int s = threadIdx.x / TPS, t = threadIdx.x % TPS;
   const int g = blockIdx.x * S + s; // symbol of this thread group (past nsym: idle, but at barriers)
   const bool live = g < nsym;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
     cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
     const int h = nre / 2;
     for (int k = t; k < nre; k += TPS) {
-      const cf v = res[k < h ? N - h + k : 1 + k - h];
+      const cf v = res[lpad(k < h ? N - h + k : 1 + k - h)];
       dst[k] = cf{v.x * scale, v.y * scale};
     }
   }

@@ -79,6 +79,7 @@ struct PdschEngine {
   uint32_t max_sf = 0;
   bool csi = false;
   bool llr8 = false; // srslte_pdsch_t.llr_is_8bit
+  int ce_rows = 0;   // srsgpu_pdsch_set_ce_rows: 0 full estimate planes, 4 / 1 the chest's compact rows
   const float *noise_dev = nullptr; // per-subframe chest noise estimates (nof_rx_ant each)
   srsgpu_dlsch_t *dl = nullptr;
   // Gold tables: x1 and the 31 x2 basis sequences, bits 0 .. 32*words-1
@@ -305,6 +306,9 @@ struct PdschEngine {
         t.layer = (int)cw;
         t.csi_mode = csi ? 1 : 0;
         t.llr8 = llr8 ? 1 : 0;
+        t.ce_rows = ce_rows;
+        t.nsc = 12 * cell.nof_prb;
+        t.inv_nsc = 1.0f / (float)t.nsc;
         t.aligned = ((uintptr_t)t.e % 4) == 0;
         t.noise = s.noise_estimate;
         t.noise_dev = noise_dev ? noise_dev + (size_t)i * cell.nof_rx_ant * cell.nof_ports : nullptr;
@@ -488,6 +492,12 @@ void srsgpu_pdsch_set_noise_dev(srsgpu_pdsch_t *q, const float *d_noise) {
 
 void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {
   if (q) q->e.csi = enable != 0;
+}
+
+int srsgpu_pdsch_set_ce_rows(srsgpu_pdsch_t *q, int rows) {
+  if (!q || (rows != 0 && rows != 1 && rows != 4)) return -1;
+  q->e.ce_rows = rows;
+  return 0;
 }
 
 void srsgpu_pdsch_set_llr_8bit(srsgpu_pdsch_t *q, int enable) {

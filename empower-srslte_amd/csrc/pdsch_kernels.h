@@ -35,6 +35,11 @@ struct LlrItem {
   const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does
   int nports;              // ports in noise_dev
   int llr8;                // llr_is_8bit: int8 demapping / scrambling / CSI, values sign-extended in e
+  int ce_rows;             // h planes hold the chest's compact rows (srsgpu_pdsch_set_ce_rows): 0 = full
+                           // 14-symbol planes, 4 = the CRS symbols' rows (time interpolation here),
+                           // 1 = one averaged row
+  uint32_t nsc;            // subcarriers per symbol (12 nof_prb)
+  float inv_nsc;           // 1 / nsc (RE position -> symbol)
   int dual;                // 2-layer MMSE (TM3 / TM4) with both TBs of one modulation: 1 = this item
                            // also computes the next item's layer from the same 2x2 solve, 2 = done
                            // by the previous item (its workgroups return at once)

@@ -85,14 +85,38 @@ struct ReIn {
   float2 y[2];
   float2 h[2][2];
 };
+// The channel estimate at grid position pos. Compact rows (srsgpu_chest_set_ce_rows): the
+// estimator's time interpolation (chest_dl.c:416-421 via srslte_interp_linear_vector, k_chest's
+// column loop) redone here in the same operation order, from the frequency-interpolated rows of
+// CRS symbols 0 / 4 / 7 / 11: d = (f[l+1] - f[l]) x w, then sequential additions of d (symbols
+// 12-13 continue from symbol 11 with the 7-11 step); or the one averaged row. The same floats as
+// the full estimate grid.
+__device__ __forceinline__ float2 ce_at(const LlrItem &t, const float2 *h, uint32_t pos) {
+  if (t.ce_rows == 0) return h[pos];
+  const uint32_t s = (uint32_t)(((float)pos + 0.5f) * t.inv_nsc); // exact: pos < 2^15, >= 1/(2 nsc) from an integer
+  const uint32_t k = pos - s * t.nsc;
+  if (t.ce_rows == 1) return h[k];
+  const uint32_t l0 = s < 4 ? 0 : s < 7 ? 1 : 2; // rows l0, l0 + 1 bracket the symbol
+  const uint32_t m = s < 4 ? s : s < 7 ? s - 4 : s < 11 ? s - 7 : s - 11;
+  const float w = s >= 4 && s < 7 ? 1.0f / 3.0f : 0.25f;
+  const float2 a = h[l0 * t.nsc + k], b = h[(l0 + 1) * t.nsc + k];
+  const float dx = __fmul_rn(__fsub_rn(b.x, a.x), w), dy = __fmul_rn(__fsub_rn(b.y, a.y), w);
+  float2 c = s >= 11 ? b : a;
+  for (uint32_t i = 0; i < m; i++) {
+    c.x = __fadd_rn(c.x, dx);
+    c.y = __fadd_rn(c.y, dy);
+  }
+  return c;
+}
+
 __device__ __forceinline__ ReIn load_re(const LlrItem &t, uint32_t pos, bool two_ports) {
   ReIn in;
 #pragma unroll
   for (int a = 0; a < 2; a++) {
     if (a == 1 && t.nrx < 2) break;
     in.y[a] = t.y[a][pos];
-    in.h[0][a] = t.h[0][a][pos];
-    if (two_ports) in.h[1][a] = t.h[1][a][pos];
+    in.h[0][a] = ce_at(t, t.h[0][a], pos);
+    if (two_ports) in.h[1][a] = ce_at(t, t.h[1][a], pos);
   }
   return in;
 }
@@ -159,6 +183,7 @@ __device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
   return {v.x, v.y};
 }
 __device__ __forceinline__ cf c_of(float2 v) { return {v.x, v.y}; }
+__device__ __forceinline__ cf ce_ld(const LlrItem &t, const float2 *h, uint32_t pos) { return c_of(ce_at(t, h, pos)); }
 
 // TM3 large-delay CDD, 2 ports x 2 rx antennas, 2 layers (precoding.c:930-1019): the precoder
 // alternates per RE (even: H = [[h00+h10, h00-h10], [h01+h11, h01-h11]] with h[port][rx], odd: the
@@ -290,8 +315,8 @@ __device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
     cf x0 = {0.f, 0.f}, x1 = {0.f, 0.f};
     for (int a = 0; a < 2; a++) {
       if (a == 1 && t.nrx < 2) break;
-      const cf h00 = c_ld(t.h[0][a], p0), h01 = c_ld(t.h[0][a], p1);
-      const cf h10 = c_ld(t.h[1][a], p0), h11 = c_ld(t.h[1][a], p1);
+      const cf h00 = ce_ld(t, t.h[0][a], p0), h01 = ce_ld(t, t.h[0][a], p1);
+      const cf h10 = ce_ld(t, t.h[1][a], p0), h11 = ce_ld(t, t.h[1][a], p1);
       const cf r0 = c_ld(t.y[a], p0), r1 = c_ld(t.y[a], p1);
       const float g = __fadd_rn(__fadd_rn(__fmul_rn(h00.r, h00.r), __fmul_rn(h00.i, h00.i)),
                                 __fadd_rn(__fmul_rn(h11.r, h11.r), __fmul_rn(h11.i, h11.i)));
@@ -312,8 +337,8 @@ __device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
   cf x0 = {0.f, 0.f}, x1 = {0.f, 0.f};
   for (int a = 0; a < 2; a++) {
     if (a == 1 && t.nrx < 2) break;
-    const cf h00 = c_ld(t.h[0][a], p0), h01 = c_ld(t.h[0][a], p1);
-    const cf h10 = c_ld(t.h[1][a], p0), h11 = c_ld(t.h[1][a], p1);
+    const cf h00 = ce_ld(t, t.h[0][a], p0), h01 = ce_ld(t, t.h[0][a], p1);
+    const cf h10 = ce_ld(t, t.h[1][a], p0), h11 = ce_ld(t, t.h[1][a], p1);
     hh = __fadd_rn(hh, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h00.r, h00.r), __fmul_rn(h00.i, h00.i)),
                                            __fmul_rn(h11.r, h11.r)),
                                  __fmul_rn(h11.i, h11.i)));

@@ -449,18 +449,11 @@ struct TdecEngine {
                          in_stride, rows, a, st));
     }
     if (!flags) return 0;
-    if (first) {
-      HIPCHK(hipMemsetAsync(cb_ok, 0, total_cbs, st));
-      HIPCHK(hipMemsetAsync(noi, 0, (size_t)total_cbs * 4, st));
-      if (init_done)
-        HIPCHK(hipMemcpyAsync(cb_done, init_done, total_cbs, hipMemcpyDeviceToDevice, st));
-      else
-        HIPCHK(hipMemsetAsync(cb_done, 0, total_cbs, st));
-    }
-    if (init_done)
-      HIPCHK(launch_pair_done(d_groups, (int)ng, total_pairs, cb_done, pair_done, st));
-    else
-      HIPCHK(hipMemsetAsync(pair_done, 0, (size_t)total_pairs, st));
+    // every code block of this pass: done = init_done, ok = noi = 0, and the pair flags (a job in
+    // several passes seeds each pass's blocks before its decode)
+    (void)first;
+    (void)total_cbs;
+    HIPCHK(launch_pair_done(d_groups, (int)ng, total_pairs, init_done, cb_done, cb_ok, noi, pair_done, st));
     return 0;
   }
 
@@ -603,7 +596,7 @@ struct TdecEngine {
     // round of workgroups to one half-iteration
     auto es_on = [&](int k) {
       if (!halfits_es_fusable(k) || es_mode == 0) return false;
-      if (es_mode == 1) return true;
+      if (es_mode == 1 || es_mode == 3) return true;
       const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, 160 * 1024 / (kind_lds[k] + 2048)));
       return (size_t)kind_blocks[k] <= (size_t)num_cus() * per_cu;
     };
@@ -611,6 +604,49 @@ struct TdecEngine {
     bool seq = false, es_any = false;
     const TdArrays a = arrays();
     TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end};
+    // es_fused 3 (hybrid): the first half-iteration of every kind as one launch per kind plus one
+    // k_decide (the whole batch's heavy pass, with kernel boundaries that let other streams in), then
+    // the blocks still running (a few at high SNR) through the remaining half-iterations in ONE
+    // early-stop launch per kind, where they loop without a launch and a k_decide per half-iteration
+    // es_fused 2 (auto) takes this form too when a kind's workgroups do not fit on the chip at once
+    // (a fused launch would leave its last round of workgroups to run every half-iteration alone)
+    auto fits = [&](int k) {
+      const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, 160 * 1024 / (kind_lds[k] + 2048)));
+      return (size_t)kind_blocks[k] <= (size_t)num_cus() * per_cu;
+    };
+    if ((es_mode == 3 || es_mode == 2) && maxh > 1) {
+      bool all_es = true, any_big = false;
+      for (int k = 0; k < TD_NKIND; k++)
+        if (kind_g0[k + 1] > kind_g0[k]) {
+          if (!halfits_es_fusable(k)) all_es = false;
+          if (!fits(k)) any_big = true;
+        }
+      if (all_es && (es_mode == 3 || any_big)) {
+        static const char *const names0[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
+                                                      "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
+        for (int k = 0; k < TD_NKIND; k++) {
+          const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+          if (g1 <= g0) continue;
+          ProfScope ps(names0[k], st);
+          HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
+        }
+        if (decide(0, d_out, out_stride, true, maxh)) return -1;
+        es.n0 = 1;
+        es.n1 = (int)maxh;
+        for (int k = 0; k < TD_NKIND; k++) {
+          const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+          if (g1 <= g0) continue;
+          ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", st);
+          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+        }
+        {
+          ProfScope ps("k_es_bytes", st);
+          HIPCHK(launch_es_bytes(d_groups, (int)groups.size(), total_pairs, es, st));
+        }
+        last_n = (int)maxh - 1;
+        return 0;
+      }
+    }
     // The SSE kind (K <= 400: a few workgroups, each a long serial chain) runs fused on a second
     // stream beside the fused window kinds: the kinds are disjoint groups (their own arrays,
     // flags and Dfz ranges), so the launch's critical path is the longer of the two, not the sum.
@@ -691,6 +727,19 @@ struct TdecEngine {
         return -1;
       }
     }
+    // the caller's ok / noi arrays (total_cbs entries) take the place of the engine's own for this
+    // job, so the flags land there without a copy; restored on every return
+    struct Swap {
+      TdecEngine &e;
+      uint8_t *ok;
+      uint32_t *ni;
+      ~Swap() {
+        e.cb_ok = ok;
+        e.noi = ni;
+      }
+    } swap{*this, cb_ok, noi};
+    if (d_ok) cb_ok = d_ok;
+    if (d_noi) noi = d_noi;
     bool first = true;
     for (size_t s0 = 0; s0 < specs.size();) {
       size_t s1 = specs.size();
@@ -710,8 +759,6 @@ struct TdecEngine {
       first = false;
       s0 = s1;
     }
-    if (d_ok) HIPCHK(hipMemcpyAsync(d_ok, cb_ok, total_cbs, hipMemcpyDeviceToDevice, st));
-    if (d_noi) HIPCHK(hipMemcpyAsync(d_noi, noi, (size_t)total_cbs * 4, hipMemcpyDeviceToDevice, st));
     return 0;
   }
 

@@ -259,10 +259,9 @@ int srsgpu_tdec_batch_decode(srsgpu_tdec_batch_t *q, int impl, int sb_layout, co
 }
 
 int srsgpu_tdec_set_schedule(int fused, int es_fused, int es_chunk, int sse_bidir) {
-  if (es_chunk == 0 || es_fused > 2) return -1;
+  if (es_chunk == 0 || es_fused > 3) return -1;
   srsgpu::TdSched &t = srsgpu::td_sched();
   if (fused >= 0) t.fused = fused != 0;
-  if (es_fused > 2) return -1;
   if (es_fused >= 0) t.es_fused = es_fused;
   if (es_chunk > 0) t.es_chunk = es_chunk;
   if (sse_bidir >= 0) t.sse_bidir = sse_bidir != 0;

@@ -116,8 +116,9 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
                          uint8_t *outb, size_t out_stride, bool early, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int max_halfits, uint8_t *pair_done,
                          hipStream_t st);
-// pair_done[p] = both code blocks of pair p done (after cb_done was seeded)
-hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *cb_done,
-                            uint8_t *pair_done, hipStream_t st);
+// the early-stop flags of the job's code blocks: cb_done = init_done (0 without), cb_ok = noi = 0,
+// pair_done[p] = both code blocks of pair p done
+hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *init_done, uint8_t *cb_done,
+                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -2413,15 +2413,26 @@ __global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ gr
   if (threadIdx.x < 2 && cbs[threadIdx.x] >= 0) cb_end[cbs[threadIdx.x]] = 0;
 }
 
-// pair_done = both code blocks finished (seeding after init_done)
+// The early-stop flags of the job's code blocks, one thread per pair: done = init_done (blocks
+// decoded in an earlier transmission; none without init_done), ok = 0, noi = 0, and pair_done =
+// both blocks done. One launch instead of two fills, a copy and the pair pass.
 __global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
-                            const uint8_t *__restrict__ cb_done, uint8_t *__restrict__ pair_done) {
+                            const uint8_t *__restrict__ init_done, uint8_t *__restrict__ cb_done,
+                            uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
+                            uint8_t *__restrict__ pair_done) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npairs_total) return;
   const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, p)];
   const int lp = p - G.pair0;
   const int c0 = G.cb0 + 2 * lp, c1 = 2 * lp + 1 < G.ncb ? c0 + 1 : c0;
-  pair_done[p] = cb_done[c0] && cb_done[c1];
+  const uint8_t d0 = init_done ? init_done[c0] : 0, d1 = init_done ? init_done[c1] : 0;
+  cb_done[c0] = d0;
+  cb_ok[c0] = 0;
+  noi[c0] = 0;
+  cb_done[c1] = d1;
+  cb_ok[c1] = 0;
+  noi[c1] = 0;
+  pair_done[p] = d0 && d1;
 }
 
 #endif // TD_PART == 0
@@ -2627,7 +2638,7 @@ TdSched &td_sched() {
       const char *e = getenv(n);
       return e && e[0] ? atoi(e) : d;
     };
-    TdSched t{env("SRSGPU_TDEC_FUSED", 1) != 0, std::min(std::max(env("SRSGPU_ES_FUSED", 2), 0), 2),
+    TdSched t{env("SRSGPU_TDEC_FUSED", 1) != 0, std::min(std::max(env("SRSGPU_ES_FUSED", 2), 0), 3),
               env("SRSGPU_ES_CHUNK", 8), env("SRSGPU_SSE_BIDIR", 1) != 0};
     if (t.es_chunk < 1) t.es_chunk = 1;
     return t;
@@ -2660,11 +2671,11 @@ hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, s
   }
 }
 
-hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *cb_done,
-                            uint8_t *pair_done, hipStream_t st) {
+hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *init_done, uint8_t *cb_done,
+                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, dg, ng, npairs, cb_done,
-                     pair_done);
+  hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, dg, ng, npairs, init_done,
+                     cb_done, cb_ok, noi, pair_done);
   return hipGetLastError();
 }
 

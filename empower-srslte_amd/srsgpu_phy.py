@@ -292,6 +292,8 @@ _sig = {
     "srsgpu_pdsch_set_stream": (None, [_vp, _vp]),
     "srsgpu_pdsch_set_csi": (None, [_vp, _i32]),
     "srsgpu_pdsch_set_llr_8bit": (None, [_vp, _i32]),
+    "srsgpu_pdsch_set_ce_rows": (_i32, [_vp, _i32]),
+    "srsgpu_chest_set_ce_rows": (None, [_vp, _i32]),
     "srsgpu_viterbi37_tb_decode_f_dev": (_i32, [_vp, _u32, _vp, _vp, _vp]),
     "srsgpu_dci_decode_dev": (_i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     "srsgpu_pcfich_create": (_i32, [ctypes.POINTER(_vp), ctypes.POINTER(srsgpu_cell_t)]),
@@ -866,6 +868,11 @@ class Pdsch:
     def set_csi(self, on):
         _lib.srsgpu_pdsch_set_csi(self.q, 1 if on else 0)
 
+    def set_ce_rows(self, rows):
+        """srsgpu_pdsch_set_ce_rows: 0 full estimate planes, 4 / 1 the chest's compact rows"""
+        if _lib.srsgpu_pdsch_set_ce_rows(self.q, rows) != 0:
+            raise ValueError("invalid ce_rows")
+
     def set_llr_8bit(self, on):
         """srslte_pdsch_t.llr_is_8bit: int8 LLR chain (values held in the int16 LLR elements)"""
         _lib.srsgpu_pdsch_set_llr_8bit(self.q, 1 if on else 0)
@@ -946,6 +953,10 @@ class Chest:
 
     def set_filter3(self, w):
         _lib.srsgpu_chest_set_smooth_filter3_coeff(self.q, w)
+
+    def set_ce_rows(self, on):
+        """srsgpu_chest_set_ce_rows: compact estimate rows (4, or 1 with average_subframe)"""
+        _lib.srsgpu_chest_set_ce_rows(self.q, int(bool(on)))
 
     def set_filter_gauss(self, order, std_dev):
         if _lib.srsgpu_chest_set_smooth_filter_gauss(self.q, order, ctypes.c_float(std_dev)) != 0:

@@ -65,13 +65,15 @@ def tb_weights(table, sf_plan, max_halfits=8):
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
                  snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None, standard_rate=True,
-                 early_stop=True):
+                 early_stop=True, ce_rows=True):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
         traffic). keep: the subframe indices this instance builds and receives (a rank's shard
         of one planned job, srsgpu_shard); default all. standard_rate: the 3GPP FFT sizes (2048 at
         20 MHz) or srsLTE's reduced ones (1536, srslte_symbol_sz without standard rates).
-        early_stop False: every code block runs max_halfits (srsgpu_dlsch_set_early_stop)."""
+        early_stop False: every code block runs max_halfits (srsgpu_dlsch_set_early_stop).
+        ce_rows: the estimator hands the PDSCH stage its compact rows (srsgpu_chest_set_ce_rows /
+        srsgpu_pdsch_set_ce_rows: identical LLRs, 3.5x fewer estimate bytes)."""
         self.torch, self.dev = torch, dev
         self.max_halfits = max_halfits
         sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
@@ -93,6 +95,8 @@ class MixedCells:
             c["ofdm"] = s.OfdmRx(prb, N, stream=stream)
             c["chest"] = s.Chest(prb, c["id"], max_grids=n, stream=stream)
             c["pd"] = s.Pdsch(prb, c["id"], nof_softbuffers=1, max_cb=13, max_sf=n, stream=stream)
+            c["chest"].set_ce_rows(ce_rows)
+            c["pd"].set_ce_rows(4 if ce_rows else 0)
             sfs, e_offs, sf_idx = [], [], []
             for j, p in enumerate(mine):
                 mask = np.zeros((2, prb), np.uint8)
@@ -223,7 +227,7 @@ class MimoSubframes:
     handles (a rank's shard); subframe i's content depends only on i."""
 
     def __init__(self, torch, dev, n_sf, seed=31, stream=None, snr_db=30.0, mimo=None, mcs=28, nof_prb=100,
-                 cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True):
+                 cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True, ce_rows=True):
         import ctypes as ct
         self.torch, self.dev, self.max_halfits = torch, dev, max_halfits
         mimo = s.MIMO_CDD if mimo is None else mimo
@@ -244,6 +248,8 @@ class MimoSubframes:
         self.pd = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=2, nof_softbuffers=2 * n, max_cb=13, max_sf=n,
                           stream=stream)
         s._lib.srsgpu_dlsch_set_early_stop(s._vp(self.pd.dlsch_q), int(bool(early_stop)))
+        self.chest.set_ce_rows(ce_rows)  # compact estimate rows, identical LLRs (as MixedCells)
+        self.pd.set_ce_rows(4 if ce_rows else 0)
         dlen = s.dlsch_data_len(tbs) + 2
         self.dlen = dlen
         sfs = []

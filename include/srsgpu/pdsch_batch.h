@@ -89,6 +89,12 @@ void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable); /* srslte_pdsch_enable
  * weighting (pdsch.c:707-713), 8-bit de-rate-matching and decoders (pdsch.c:795-806,
  * sch.c:344-364). The LLRs stay int16 elements holding int8 values. */
 void srsgpu_pdsch_set_llr_8bit(srsgpu_pdsch_t *q, int enable);
+/* The estimate planes passed to srsgpu_pdsch_decode(_dev) hold the compact rows of
+ * srsgpu_chest_set_ce_rows: rows = 4 (per-symbol estimation: the CRS symbols' rows, time
+ * interpolation done per resource element with the estimator's operations, so the LLRs are
+ * identical), 1 (average_subframe: the averaged row), 0 (default: full 14-symbol planes).
+ * Returns -1 for any other value. */
+int srsgpu_pdsch_set_ce_rows(srsgpu_pdsch_t *q, int rows);
 /* Take the MMSE noise term from device memory instead of sf[i].noise_estimate: subframe i of a
  * call uses the mean of d_noise[i*nof_rx_ant + a] (the channel estimator's per-antenna outputs,
  * as srslte_chest_dl_get_noise_estimate averages them). NULL restores sf[i].noise_estimate. */

@@ -88,13 +88,16 @@ uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t long_cb);
  *              0: one launch per half-iteration (SRSGPU_TDEC_FUSED)
  *   es_fused   1: early-stop jobs check the CRC inside the decoder launches (k_win_bidir_es,
  *                 k_sse_es) and write the bytes in one k_es_bytes launch; 0: one decoder launch
- *                 and one k_decide launch per half-iteration; 2 (default): per decoder kind, fused
- *                 when its workgroups fit on the chip at once (SRSGPU_ES_FUSED)
+ *                 and one k_decide launch per half-iteration; 2 (default): fused when every kind's
+ *                 workgroups fit on the chip at once, the hybrid form when one does not (all kinds
+ *                 fusable), else per decoder kind (SRSGPU_ES_FUSED); 3 (hybrid): the
+ *                 first half-iteration per launch with k_decide, then the blocks still running
+ *                 through the rest in one fused early-stop launch per kind
  *   es_chunk   half-iterations per fused early-stop launch, >= 1, default 8 (SRSGPU_ES_CHUNK)
  *   sse_bidir  1: the two-wave SSE decoder, 0: the one-wave one (SRSGPU_SSE_BIDIR; the fused early
  *                 stop of the SSE kind needs the two-wave one)
  * A negative argument keeps the current value; the defaults come from those environment variables.
- * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0 or es_fused > 2. */
+ * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0 or es_fused > 3. */
 int srsgpu_tdec_set_schedule(int fused, int es_fused, int es_chunk, int sse_bidir);
 void srsgpu_tdec_get_schedule(int *fused, int *es_fused, int *es_chunk, int *sse_bidir);
 

@@ -66,7 +66,8 @@ def test_c5_decode_identical_under_every_schedule(table):
     """srsgpu_tdec_set_schedule changes only how the decoders are launched: the same mixed-K job
     (window and SSE kinds, failures and varied nof_iterations at 6 dB) decodes to the same return
     codes, nof_iterations, bytes and cb_crc under the auto, fused (1 and 8 half-iterations per
-    launch), per-half-iteration and one-wave SSE schedules."""
+    launch), per-half-iteration, hybrid (first half-iteration per launch, the rest fused; with the
+    one-wave SSE decoder the hybrid falls back) and one-wave SSE schedules."""
     import torch
     import srsgpu_phy as s
     import srsgpu_traffic as tr
@@ -80,6 +81,8 @@ def test_c5_decode_identical_under_every_schedule(table):
                           "fused1": dict(es_fused=1, es_chunk=1, sse_bidir=1),
                           "fused8": dict(es_fused=1, es_chunk=8, sse_bidir=1),
                           "per_halfit": dict(es_fused=0, sse_bidir=1),
+                          "hybrid": dict(es_fused=3, es_chunk=8, sse_bidir=1),
+                          "hybrid_one_wave": dict(es_fused=3, es_chunk=8, sse_bidir=0),
                           "sse_one_wave": dict(es_fused=0, sse_bidir=0)}.items():
             s.set_schedule(**sch)
             m.d_data.zero_()

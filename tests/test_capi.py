@@ -112,7 +112,7 @@ def test_decoder_schedule_api():
         assert s.get_schedule() == {"fused": 0, "es_fused": 1, "es_chunk": 3, "sse_bidir": 0}
         s.set_schedule(es_chunk=5)  # the others kept
         assert s.get_schedule() == {"fused": 0, "es_fused": 1, "es_chunk": 5, "sse_bidir": 0}
-        for bad in (dict(es_chunk=0), dict(es_fused=3)):
+        for bad in (dict(es_chunk=0), dict(es_fused=4)):
             try:
                 s.set_schedule(**bad)
                 raise AssertionError(bad)
