@@ -252,12 +252,103 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
   }
 }
 
+// Large symbols (N >= 1024, one symbol per workgroup): a resident grid of workgroups, each taking
+// symbols g, g + gridDim.x, ... The first stage's inputs of the next symbol are loaded into
+// registers as soon as the current symbol's first stage is in LDS, so they are in flight while the
+// remaining stages and the output of the current symbol run (one symbol per workgroup left every
+// wave waiting on its 16 KB read with nothing else to do).
+template <int N>
+__global__ __launch_bounds__(256) void k_ofdm_rx_p(const float2 *__restrict__ in, size_t in_stride,
+                                                   float2 *__restrict__ out, size_t out_stride, int nsym,
+                                                   int nre, int cp0, int cp, const float2 *__restrict__ tw,
+                                                   float scale) {
+  constexpr int R0 = N % 8 == 0 ? 8 : N % 4 == 0 ? 4 : N % 2 == 0 ? 2 : 3;
+  constexpr int nb0 = N / R0, NPT = (nb0 + 255) / 256;
+  __shared__ cf buf[lds_slots<N>()];
+  const int t = threadIdx.x;
+  cf v[NPT][R0];
+  auto load = [&](int g) {
+    const int sym = g % 14, sf = g / 14;
+    const int slot = sym / 7, l = sym % 7;
+    const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
+    const cf *src = (const cf *)(in + (size_t)sf * in_stride + start);
+#pragma unroll
+    for (int q = 0; q < NPT; q++) {
+      const int j = t + q * 256;
+#pragma unroll
+      for (int r = 0; r < R0; r++) v[q][r] = j < nb0 ? src[j + r * nb0] : cf{0.f, 0.f};
+    }
+  };
+  int g = blockIdx.x;
+  if (g < nsym) load(g);
+#pragma unroll 1
+  for (; g < nsym; g += gridDim.x) {
+    // first stage (Ns = 1, no twiddles) from the registers into LDS
+#pragma unroll
+    for (int q = 0; q < NPT; q++) {
+      const int j = t + q * 256;
+      if (j >= nb0) break;
+      cf y[R0];
+      bfly<R0>(v[q], y);
+#pragma unroll
+      for (int r = 0; r < R0; r++) buf[lpad(j * R0 + r)] = y[r];
+    }
+    __syncthreads();
+    if (g + (int)gridDim.x < nsym) load(g + gridDim.x); // next symbol's samples, in flight from here
+    __builtin_amdgcn_sched_barrier(0);
+    // opaque copies of the twiddle pointer and the thread index per symbol: left alone, the compiler
+    // hoists every stage's twiddle addressing out of the symbol loop and holds it in registers
+    // (130 VGPRs: a third of the occupancy)
+    const float2 *twl = tw;
+    int tl = t; // and of the thread index: the stages' twiddle offsets are recomputed per symbol
+    asm volatile("" : "+s"(twl), "+v"(tl));
+    fft_ip<N, R0, 256>(nullptr, buf, twl, tl, true);
+    const int sym = g % 14, sf = g / 14;
+    cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
+    const int h = nre / 2;
+    for (int k = t; k < nre; k += 256) {
+      const cf w = buf[lpad(k < h ? N - h + k : 1 + k - h)];
+      dst[k] = cf{w.x * scale, w.y * scale};
+    }
+    __syncthreads(); // every read of buf done before the next symbol's first stage writes it
+  }
+}
+
+// resident workgroups of k_ofdm_rx_p<N> on the device (CUs x workgroups per CU by its registers
+// and LDS)
+template <int N> static int ofdm_resident_wgs() {
+  static const int n = [] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_ofdm_rx_p<N>, 256, 0) != hipSuccess || per <= 0)
+      per = 4;
+    return cus * per;
+  }();
+  return n;
+}
+
 hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
                           int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
                           hipStream_t st) {
   if (nsf <= 0) return hipSuccess;
   const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
   const int nsym = nsf * 14;
+  if (N == 2048 || N == 1536 || N == 1024) {
+    // every workgroup takes the same number of symbols (no partial last round)
+#define OFDM_RX_P(n)                                                                               \
+  if (N == n) {                                                                                    \
+    const int res = ofdm_resident_wgs<n>(), per = (nsym + res - 1) / res;                          \
+    hipLaunchKernelGGL(k_ofdm_rx_p<n>, dim3((unsigned)((nsym + per - 1) / per)), dim3(256), 0, st, in, \
+                       in_stride, out, out_stride, nsym, nre, cp0, cp, tw, scale);                 \
+    return hipGetLastError();                                                                      \
+  }
+    OFDM_RX_P(2048)
+    OFDM_RX_P(1536)
+    OFDM_RX_P(1024)
+#undef OFDM_RX_P
+  }
 #define OFDM_RX_C(n)                                                                               \
   case n:                                                                                          \
     hipLaunchKernelGGL(k_ofdm_rx_c<n>, dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \

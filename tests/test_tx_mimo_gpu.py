@@ -138,7 +138,8 @@ def test_tm3_full_size_tx_rx():
     import srsgpu_phy as s
     import srsgpu_traffic as tr
     L = _ref_sigs(Ref().lib)
-    m = tr.MimoSubframes(torch, torch.device("cuda"), 1024, seed=5, snr_db=30.0)
+    # full estimate planes: the reference decoder below reads them (compact rows: test_ce_rows_gpu.py)
+    m = tr.MimoSubframes(torch, torch.device("cuda"), 1024, seed=5, snr_db=30.0, ce_rows=False)
     m.step()
     torch.cuda.synchronize()
     acks, good, noi = m.check()
@@ -166,7 +167,7 @@ def test_tm2_tm4_tx_rx(mimo, ntb, codebook, mcs):
     import srsgpu_traffic as tr
     L = _ref_sigs(Ref().lib)
     m = tr.MimoSubframes(torch, torch.device("cuda"), 64, seed=9 + codebook, snr_db=32.0, mimo=mimo, mcs=mcs,
-                         nof_prb=50, cell_id=88, codebook=codebook, nof_tb=ntb)
+                         nof_prb=50, cell_id=88, codebook=codebook, nof_tb=ntb, ce_rows=False)
     m.step()
     torch.cuda.synchronize()
     acks, good, _ = m.check()
