@@ -9,6 +9,7 @@
 // subcarriers are written back.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ofdm_kernels.h"
 
@@ -335,7 +336,12 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
   if (nsf <= 0) return hipSuccess;
   const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
   const int nsym = nsf * 14;
-  if (N == 2048 || N == 1536 || N == 1024) {
+  // SRSGPU_OFDM_PERSIST=0: the one-symbol-per-workgroup kernel for every size (A/B measurements)
+  static const bool persist = [] {
+    const char *e = getenv("SRSGPU_OFDM_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  if (persist && (N == 2048 || N == 1536 || N == 1024)) {
     // every workgroup takes the same number of symbols (no partial last round)
 #define OFDM_RX_P(n)                                                                               \
   if (N == n) {                                                                                    \

@@ -1,0 +1,14 @@
+#!/bin/bash
+# isolated kernel timings (tools/kbench.py) under schedule / OFDM variants, plus a kernel trace of
+# the default one. Each GPU step under its own time limit.
+set -e
+export TMPDIR=/tmp
+TAG=${1:-r04kb}
+O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python tools/kbench.py --schedule auto --out $O/kb_auto.json > $O/kb_auto.log 2>&1 || { tail -20 $O/kb_auto.log; exit 1; }
+SRSGPU_OFDM_PERSIST=0 timeout -k 10 200 python tools/kbench.py --schedule auto --out $O/kb_ofdm_old.json > $O/kb_ofdm_old.log 2>&1 || { tail -20 $O/kb_ofdm_old.log; exit 1; }
+timeout -k 10 200 python tools/kbench.py --schedule per_halfit --out $O/kb_perhalfit.json > $O/kb_perhalfit.log 2>&1 || { tail -20 $O/kb_perhalfit.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_kb -o kt -- python3 tools/kbench.py --schedule auto > $O/trace_kb.log 2>&1 || { tail -20 $O/trace_kb.log; exit 1; }
+echo all done
