@@ -215,7 +215,8 @@ STAGES = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "
 # kernels of the coded subframe legs, for the per-kernel table and the roofline of the dominant one
 # (names as the library's ProfScope records them; prof_get matches substrings, so the decoder's
 # early-stop launches are asked for by their full name)
-KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_ldderm", "k_rows_late", "k_win_bidir_es",
+KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", "k_ldderm", "k_rows_late",
+           "k_win_bidir_h0", "k_win_bidir_es",
            "k_sse_es", "k_es_bytes", "k_win_bidir_run", "k_win_bidir", "k_decide", "k_tb_finish")
 
 
@@ -942,7 +943,7 @@ def pipeline_roofline(leg, nsf_per_batch):
     N = leg["symbol_size"]
     table = {}
     for k, v in leg["kernels_per_batch"].items():
-        if k not in ALG_BYTES_PER_SF or not v["launches"]:
+        if k not in ALG_BYTES_PER_SF or not v["launches"] or k == "k_win_bidir_h0":
             continue
         alg = ALG_BYTES_PER_SF[k](N) * nsf_per_batch / v["launches"]
         avg = v["ms"] / v["launches"]
@@ -955,15 +956,45 @@ def pipeline_roofline(leg, nsf_per_batch):
     t = table[dom]
     pmc = load_profile_json(leg["workload"] + ":" + dom)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    src = pmc.get("source") if pmc else None
+    if traffic is None:
+        traffic, src = pipeline_pmc_traffic(dom)
     roof = {"bound": "hbm", "kernel": dom, "achieved": t["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": t["frac"], "traffic": traffic,
             "traffic_over_alg": round(traffic / t["alg_bytes_per_launch"], 2) if traffic else None,
-            "traffic_source": pmc.get("source") if pmc else None,
+            "traffic_source": src,
             "alg_bytes_per_launch": t["alg_bytes_per_launch"], "avg_launch_ms": t["avg_launch_ms"],
             "launches_per_batch": t["launches_per_batch"],
             "alg_bytes_def": "SURVEY 8(d) per-subframe algorithmic bytes of %s (bench.py ALG_BYTES_PER_SF) x "
                              "%d subframes per launch" % (dom, nsf_per_batch / t["launches_per_batch"])}
     return roof, table
+
+
+# library scope name -> rocprof kernel name prefixes (tools/pmc_pipeline.py keys)
+PMC_NAMES = {"k_ldderm": ("k_load_derm",), "k_ofdm_rx": ("k_ofdm_rx_p", "k_ofdm_rx_c"),
+             "k_win_bidir": ("k_win_bidir<", "k_win_bidir_es<")}
+
+
+def pipeline_pmc_traffic(kernel):
+    """HBM bytes per launch of a pipeline kernel from the newest committed
+    profiles/*pmc_pipeline.json (tools/pmc_pipeline.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch,
+    separate passes), averaged over its variants by dispatch count; (None, None) without one"""
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None, None
+    natural = lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f)]  # noqa: E731
+    files = sorted((f for f in os.listdir(pdir) if f.endswith("pmc_pipeline.json")), key=natural)
+    if not files:
+        return None, None
+    d = json.load(open(os.path.join(pdir, files[-1])))
+    pre = PMC_NAMES.get(kernel, (kernel,))
+    tot = n = 0
+    for k, r in d.items():
+        if any(k.startswith(p) for p in pre):
+            c = max(r["dispatches"])
+            tot += (r["fetch_bytes_x2"] + r["write_bytes"]) * c
+            n += c
+    return (int(tot / n), "profiles/" + files[-1]) if n else (None, None)
 
 
 def cpu_baseline_pipeline(grids, sf_idx, snr_db, nthreads=None, target_thread_s=15.0):
@@ -1179,6 +1210,17 @@ def main():
     if rank == 0:
         roof, ktable = pipeline_roofline(head, C3_SF)
         head["kernel_table"] = ktable
+        h0 = head["kernels_per_batch"].get("k_win_bidir_h0")
+        valu = None
+        if h0 and h0["launches"]:
+            # the first half-iteration of every code block: SURVEY 8(d)'s 90 int16 ops per info bit
+            avg = h0["ms"] / h0["launches"]
+            ops = ALG_OPS_PER_BIT_HALFIT * sum(C3_KS) * C3_SF / h0["launches"]
+            rate = ops / (avg / 1e3) / 1e12
+            valu = {"bound": "valu (packed int16)", "kernel": "k_win_bidir (first half-iteration, early-stop job)",
+                    "achieved": round(rate, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
+                    "frac": round(rate / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": int(ops),
+                    "avg_launch_ms": round(avg, 4)}
         result = {
             "metric": METRIC, "value": head["decoded_mbps"], "unit": "Mbps", "n_gpus": nranks, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": head["ms_per_batch"], "higher_is_better": True, "scaling": "weak",
@@ -1194,6 +1236,7 @@ def main():
             "value_def": "decoded Mbps = sum of K over CRC-passing code blocks per second (SURVEY 8(d)), whole "
                          "job over the slowest rank's batch time",
             "roofline": roof,
+            "valu_roofline": valu,
             "headline_detail": head,
         }
     # ---- further legs ----

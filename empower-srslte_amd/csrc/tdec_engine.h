@@ -622,7 +622,9 @@ struct TdecEngine {
           if (!fits(k)) any_big = true;
         }
       if (all_es && (es_mode == 3 || any_big)) {
-        static const char *const names0[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
+        // "_h0": the first half-iteration's own scope name (a subset of "k_win_bidir" for
+        // srsgpu_prof_get, which matches substrings)
+        static const char *const names0[TD_NKIND] = {"k_win_bidir_h0", "k_win_bidir_h0", "k_sse_halfit",
                                                       "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
         for (int k = 0; k < TD_NKIND; k++) {
           const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
