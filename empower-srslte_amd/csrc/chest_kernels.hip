@@ -147,9 +147,25 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   auto fidx = [&](int l) { return (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6; };
   // 1. LS: v = 0 / 3 alternating over the CRS symbols (port 1: 3 / 0), fidx = (v + id % 6) % 6;
   //    ports 0 and 1 share the pilot sequence (csr_refs.pilots[port / 2])
-  for (int e = tid; e < 4 * np; e += blockDim.x) {
-    const int l = e / np, m = e % np;
-    ls[e] = cmulconj(grid[sym[l] * nsc + fidx(l) + 6 * m], pil[e]);
+  //    Every load of the thread (at most 4 pilots: 4 np <= 880 < 4 x 256) issued before the
+  //    first product: one memory round trip instead of four in a row
+  {
+    constexpr int PPT = (4 * CH_MAXP + 255) / 256;
+    c32 g[PPT], c[PPT];
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {
+      const int e = tid + 256 * u;
+      if (e < 4 * np) {
+        const int l = e / np, m = e % np;
+        g[u] = grid[sym[l] * nsc + fidx(l) + 6 * m];
+        c[u] = pil[e];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PPT; u++) {
+      const int e = tid + 256 * u;
+      if (e < 4 * np) ls[e] = cmulconj(g[u], c[u]);
+    }
   }
   __syncthreads();
   // 2 + 3. block sums: REFS residual power, RSRP, RSSI, sum of estimates, CFO correlation
