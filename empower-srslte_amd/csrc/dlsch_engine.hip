@@ -138,7 +138,7 @@ struct DlschEngine {
   // decoder inputs (k_load_derm) and their softbuffer rows written after the decode, only for TBs
   // that failed (the only rows the reference reads again)
   bool direct_derm = true;
-  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables;
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables, inv_t4_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
   EncItem *h_enc = nullptr, *d_enc = nullptr;
@@ -210,6 +210,8 @@ struct DlschEngine {
     tables.clear();
     for (auto &kv : inv_tables) (void)hipFree(kv.second);
     inv_tables.clear();
+    for (auto &kv : inv_t4_tables) (void)hipFree(kv.second);
+    inv_t4_tables.clear();
     if (staged) (void)hipEventDestroy(staged);
     tdec.destroy();
   }
@@ -229,6 +231,33 @@ struct DlschEngine {
     if (hipMalloc(&d, inv.size() * 2) != hipSuccess) return nullptr;
     if (hipMemcpy(d, inv.data(), inv.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
     inv_tables.emplace(key, d);
+    return d;
+  }
+
+  // the inverse table in the window decoders' T4 order (k_load_derm): entry st * ne + el is the
+  // table entry m that lands on stream st (sys, p0, p1) of T4 element el of a pair region (step
+  // k = 4 (el / 4nb) + el % 4 of chain d = el / 4 % nb; padded steps k >= L repeat step L - 1, as
+  // k_load_sbt fills them), then the 12 tail positions; ne = nsb * 4 * ceil(K / nsb / 4)
+  const uint16_t *inv_t4_table(uint32_t K, uint32_t rv, uint32_t nsb) {
+    auto key = std::make_tuple(K, rv, nsb);
+    auto it = inv_t4_tables.find(key);
+    if (it != inv_t4_tables.end()) return it->second;
+    std::vector<uint16_t> t;
+    rm_rx_table(K, rv, nsb, t);
+    std::vector<uint16_t> inv(3 * (K + 32) + 16, 0xFFFF);
+    for (uint32_t m = 0; m < t.size(); m++) inv[t[m]] = (uint16_t)m;
+    const uint32_t L = K / nsb, G4 = (L + 3) / 4, ne = nsb * 4 * G4;
+    std::vector<uint16_t> t4(3 * ne + 16, 0xFFFF);
+    for (uint32_t st = 0; st < 3; st++)
+      for (uint32_t el = 0; el < ne; el++) {
+        const uint32_t k = std::min(4 * (el / (4 * nsb)) + el % 4, L - 1), d = el / 4 % nsb;
+        t4[st * ne + el] = inv[st * (K + 32) + k * nsb + d];
+      }
+    for (uint32_t i = 0; i < 12; i++) t4[3 * ne + i] = inv[3 * (K + 32) + i];
+    uint16_t *d = nullptr;
+    if (hipMalloc(&d, t4.size() * 2) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, t4.data(), t4.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    inv_t4_tables.emplace(key, d);
     return d;
   }
 
@@ -408,6 +437,8 @@ struct DlschEngine {
           const int r = resolve_impl(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, K);
           it.direct = direct_derm && sb_input_for(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, r) &&
                       impl_nb(r) % 8 == 0;
+          it.inv_t4 = nullptr;
+          if (it.direct && !(it.inv_t4 = inv_t4_table(K, t.rv, nsb))) return -1;
         }
         max_n = std::max(max_n, std::min(ne, it.N));
         cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});

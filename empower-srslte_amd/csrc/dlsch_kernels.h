@@ -25,6 +25,7 @@ struct DermItem {
   uint32_t direct;        // de-rate-matched straight into the decoder inputs (k_load_derm); the
                           // row itself is written after the decode, only if the TB failed
   const int32_t *tb_ret;  // its TB's return code (k_tb_finish), read by the deferred row pass
+  const uint16_t *inv_t4; // direct: the inverse table in the decoder's T4 order, [3][ne] + 12 tails
 };
 
 // one transport block's epilogue

@@ -186,24 +186,20 @@ __global__ __launch_bounds__(256) void k_derm_flags(const DermItem *__restrict__
 // ------------------------------------------------------------------ direct de-RM ----
 // k_derm followed by k_load_sbt (tdec_kernels.hip) in one pass, for the window decoders' groups:
 // the decoder input at softbuffer-row position o of code block c is what k_derm would store
-// there, (fresh ? 0 : row[o]) + the LLRs e[i] with i = inv[o] (mod N), computed where k_load_sbt
-// would read it. One 512-thread workgroup per code-block pair: both blocks' LLRs are staged in LDS
-// once (dynamic LDS, `stage` LLRs per block), then for each tile of 2048 / nb steps the six
-// (stream, block) chunks of 2048 row positions are formed in LDS from 16-byte inverse-table (and,
-// unless fresh, row) loads, and written out in the T4 layout with coalesced 16-byte stores; the
-// next tile's table loads are issued before the current tile is written out. HBM traffic per code
-// block: its E LLRs in and the 12 B per info bit of SP0 / P1 out (the separate passes also wrote
-// and re-read the 3(K+32)+12 row entries).
-#define LDR_THREADS 512
-#define LDR_TILE 2048                      // row positions per (stream, block) chunk of a tile
-#define LDR_PIECES (6 * LDR_TILE / 8)      // 16-byte pieces of a tile
-#define LDR_PPT (LDR_PIECES / LDR_THREADS) // pieces per thread
+// there, (fresh ? 0 : row[o]) + the LLRs e[i] with i = inv[o] (mod N). The inverse table comes in
+// the decoder's own T4 order (DermItem::inv_t4, built per (K, rv) on the host), so every output is
+// computed where it is stored: one workgroup per code-block pair stages both blocks' LLRs in LDS
+// (dynamic, `stage` per block), then each thread forms whole 16-byte SP0 / P1 vectors from
+// coalesced table loads and LDS gathers, consecutive lanes storing consecutive vectors. Reused
+// rows (HARQ retransmissions, not fresh) add their old entries, read at their row positions. HBM
+// traffic per code block: its E LLRs in and the 12 B per info bit of SP0 / P1 out (the separate
+// passes also wrote and re-read the 3(K+32)+12 row entries).
+#define LDR_THREADS 256
 __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
                                                            const DermItem *__restrict__ items, TdArrays arr,
                                                            uint32_t stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
-  uint16_t(*tile)[LDR_TILE] = reinterpret_cast<uint16_t(*)[LDR_TILE]>(ldr_lds); // [6][LDR_TILE]
-  uint32_t *llr0 = ldr_lds + 6 * LDR_TILE / 2, *llr1 = llr0 + stage / 2;
+  uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
   int gi = 0;
   { // the last group whose first workgroup is <= blockIdx.x
     int lo = 0, hi = ngroups - 1;
@@ -220,113 +216,82 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
   const int pair = blockIdx.x - G.blk_load;
   if (pair >= npairs) return;
-  const int L = K / nb, G4 = (L + 3) >> 2, S = LDR_TILE / nb;
+  const int L = K / nb, G4 = (L + 3) >> 2, ne = nb * 4 * G4;
   const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
-  // the two blocks' fields (selected by h, which is wave-uniform: no indexed private arrays)
   struct Blk {
     const int16_t *e, *row;
-    const uint16_t *inv;
+    const uint16_t *t4;
     uint32_t ne, N;
     bool fresh, staged;
   };
   auto blk = [&](int c) {
     const DermItem &it = items[c];
-    return Blk{it.e, it.row, it.inv, it.ne, it.N, it.fresh && *glob(it.fresh),
+    return Blk{it.e, it.row, it.inv_t4, it.ne, it.N, it.fresh && *glob(it.fresh),
                it.ne <= it.N && it.ne <= stage};
   };
   const Blk ba = blk(c0), bb = blk(c1);
   const bool w8 = items[c0].w8 != 0; // one LLR width per call
-  // tile pieces: chunk c = (stream, block), 8 row positions from sub-block index e
-  auto piece_at = [&](int q, int k0, int &c, int &pc, uint32_t &o8) {
-    const int idx = threadIdx.x + LDR_THREADS * q;
-    c = idx / (LDR_TILE / 8);
-    pc = idx - c * (LDR_TILE / 8);
-    const int st = c >> 1;
-    int e = k0 * nb + pc * 8; // past the last step: its copy (values unused)
-    if (e >= L * nb) e = (L - 1) * nb + (e & (nb - 1));
-    o8 = (uint32_t)(st * (K + 32) + e) / 8;
-  };
-  u4v iv[LDR_PPT], ov[LDR_PPT];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < LDR_PPT; q++) {
-      int c, pc;
-      uint32_t o8;
-      piece_at(q, k0, c, pc, o8);
-      const Blk &b = (c & 1) ? bb : ba;
-      iv[q] = glob(reinterpret_cast<const u4v *>(b.inv))[o8];
-      ov[q] = b.fresh ? u4v{0, 0, 0, 0} : glob(reinterpret_cast<const u4v *>(b.row))[o8];
-    }
-  };
-  fetch(0); // the first tile's table loads fly while the LLRs are staged
   if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
   if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
   __syncthreads();
-  // value of a row position of block b given its inverse-table entry m and the row's old value
-  auto value = [&](const Blk &b, const uint16_t *lds, uint32_t m, uint32_t old) -> uint32_t {
-    uint32_t acc = b.fresh ? 0u : old;
+  const uint16_t *l0 = reinterpret_cast<const uint16_t *>(llr0), *l1 = reinterpret_cast<const uint16_t *>(llr1);
+  // value of T4 element el of stream st of block b, given its table entry m
+  auto value = [&](const Blk &b, const uint16_t *lds, int st, int el, uint32_t m) -> uint32_t {
+    uint32_t acc = 0;
+    if (!b.fresh) { // the row's old entry at its row position (padded steps: step L - 1's)
+      const int k = min(4 * (el / (4 * nb)) + (el & 3), L - 1), d = (el >> 2) % nb;
+      acc = (uint16_t)glob(b.row)[st * (K + 32) + k * nb + d];
+    }
     if (b.staged) {
       acc += m < b.ne ? (uint32_t)lds[m] : 0u; // 0xFFFF >= ne
     } else if (m != 0xFFFFu) {
       const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(b.e));
       for (uint32_t i = m; i < b.ne; i += b.N) acc += e[i];
     }
-    return derm_fold(acc, w8);
+    return derm_fold(acc, w8) & 0xFFFFu;
   };
   const size_t pbase = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
   const gp_t<u4v> SP0 = glob(reinterpret_cast<u4v *>((int16_t *)arr.SP0 + 4 * pbase));
   const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
-  for (int k0 = 0; k0 < 4 * G4; k0 += S) {
-#pragma unroll
-    for (int q = 0; q < LDR_PPT; q++) {
-      int c, pc;
-      uint32_t o8;
-      piece_at(q, k0, c, pc, o8);
-      const bool h = c & 1;
-      const Blk &b = h ? bb : ba;
-      const uint16_t *lds = reinterpret_cast<const uint16_t *>(h ? llr1 : llr0);
-      const uint32_t im[4] = {iv[q].x, iv[q].y, iv[q].z, iv[q].w}, om[4] = {ov[q].x, ov[q].y, ov[q].z, ov[q].w};
-      uint32_t r[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        r[u] = (value(b, lds, im[u] & 0xFFFFu, om[u] & 0xFFFFu) & 0xFFFFu) |
-               (value(b, lds, im[u] >> 16, om[u] >> 16) << 16);
-      *reinterpret_cast<u4v *>(&tile[c][pc * 8]) = u4v{r[0], r[1], r[2], r[3]};
-    }
-    __syncthreads();
-    if (k0 + S < 4 * G4) fetch(k0 + S);
-    // the tile's steps as T4 elements: el -> step (el / 4 / nb) * 4 + el % 4, chain el / 4 % nb
-    const int nel = min(S, 4 * G4 - k0) * nb;
-    auto at = [&](int c, int el) -> uint32_t {
-      const int g4l = el / (4 * nb), d = (el >> 2) % nb, u = el & 3;
-      return tile[c][(4 * g4l + u) * nb + d];
-    };
-    const size_t e0 = (size_t)k0 * nb; // T4 element of the tile's first step
-#pragma unroll
-    for (int q = 0; q < LDR_TILE / 2 / LDR_THREADS; q++) {
-      const int v = threadIdx.x + LDR_THREADS * q; // SP0 elements 2v, 2v + 1
-      if (2 * v < nel) {
-        const int ea = 2 * v, eb = 2 * v + 1;
-        SP0[e0 / 2 + v] = u4v{at(0, ea) | (at(1, ea) << 16), at(2, ea) | (at(3, ea) << 16),
-                              at(0, eb) | (at(1, eb) << 16), at(2, eb) | (at(3, eb) << 16)};
-      }
-    }
-    if (4 * (int)threadIdx.x < nel) {
-      const int e = 4 * threadIdx.x;
-      P1[e0 / 4 + threadIdx.x] = u4v{at(4, e) | (at(5, e) << 16), at(4, e + 1) | (at(5, e + 1) << 16),
-                                     at(4, e + 2) | (at(5, e + 2) << 16), at(4, e + 3) | (at(5, e + 3) << 16)};
-    }
-    __syncthreads();
+  const gp_t<const uint32_t> ta = glob(reinterpret_cast<const uint32_t *>(ba.t4));
+  const gp_t<const uint32_t> tb = glob(reinterpret_cast<const uint32_t *>(bb.t4));
+  // SP0: vector v holds T4 elements 2v, 2v + 1 as (sys a, sys b, p0 a, p0 b) each
+#pragma unroll 4
+  for (int v = threadIdx.x; v < ne / 2; v += LDR_THREADS) {
+    const uint32_t sa = ta[v], pa = ta[ne / 2 + v], sb = tb[v], pb = tb[ne / 2 + v];
+    const int el = 2 * v;
+    SP0[v] = u4v{value(ba, l0, 0, el, sa & 0xFFFFu) | (value(bb, l1, 0, el, sb & 0xFFFFu) << 16),
+                 value(ba, l0, 1, el, pa & 0xFFFFu) | (value(bb, l1, 1, el, pb & 0xFFFFu) << 16),
+                 value(ba, l0, 0, el + 1, sa >> 16) | (value(bb, l1, 0, el + 1, sb >> 16) << 16),
+                 value(ba, l0, 1, el + 1, pa >> 16) | (value(bb, l1, 1, el + 1, pb >> 16) << 16)};
   }
-  if (threadIdx.x < 12) { // the tails: row positions 3(K+32) .. +11
+  // P1: vector v holds T4 elements 4v .. 4v + 3 as (p1 a, p1 b) each
+  typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+  const gp_t<const u2v> qa = glob(reinterpret_cast<const u2v *>(ba.t4 + 2 * ne));
+  const gp_t<const u2v> qb = glob(reinterpret_cast<const u2v *>(bb.t4 + 2 * ne));
+#pragma unroll 4
+  for (int v = threadIdx.x; v < ne / 4; v += LDR_THREADS) {
+    const u2v ma = qa[v], mb = qb[v];
+    const int el = 4 * v;
+    P1[v] = u4v{value(ba, l0, 2, el, ma.x & 0xFFFFu) | (value(bb, l1, 2, el, mb.x & 0xFFFFu) << 16),
+                value(ba, l0, 2, el + 1, ma.x >> 16) | (value(bb, l1, 2, el + 1, mb.x >> 16) << 16),
+                value(ba, l0, 2, el + 2, ma.y & 0xFFFFu) | (value(bb, l1, 2, el + 2, mb.y & 0xFFFFu) << 16),
+                value(ba, l0, 2, el + 3, ma.y >> 16) | (value(bb, l1, 2, el + 3, mb.y >> 16) << 16)};
+  }
+  if (threadIdx.x < 12) { // the tails: row positions 3(K+32) .. +11, table entries 3 ne + t
     const int t = threadIdx.x;
-    const uint32_t o = 3u * (K + 32) + t;
-    auto tail = [&](const Blk &b, const uint32_t *l) -> uint32_t {
-      const uint32_t m = glob(b.inv)[o];
-      const uint32_t old = b.fresh ? 0u : (uint16_t)glob(b.row)[o];
-      return value(b, reinterpret_cast<const uint16_t *>(l), m, old) & 0xFFFFu;
+    auto tail = [&](const Blk &b, const uint16_t *lds) -> uint32_t {
+      const uint32_t m = glob(b.t4)[3 * ne + t];
+      uint32_t acc = b.fresh ? 0u : (uint16_t)glob(b.row)[3 * (K + 32) + t];
+      if (b.staged) {
+        acc += m < b.ne ? (uint32_t)lds[m] : 0u;
+      } else if (m != 0xFFFFu) {
+        const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(b.e));
+        for (uint32_t i = m; i < b.ne; i += b.N) acc += e[i];
+      }
+      return derm_fold(acc, w8) & 0xFFFFu;
     };
-    const uint32_t va = tail(ba, llr0), vb = tail(bb, llr1);
+    const uint32_t va = tail(ba, l0), vb = tail(bb, l1);
     glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = va | (vb << 16);
   }
 }
@@ -560,7 +525,7 @@ hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermIt
   // LLRs staged per block: the largest E of the call, rounded to 8, at most 8192 (16 KB); blocks
   // with more (or with repetition, E > 3K+12) gather theirs from HBM
   const uint32_t stage = std::min<uint32_t>(8192, (max_ne + 7) / 8 * 8);
-  const size_t lds = 6 * LDR_TILE * 2 + 4 * (size_t)stage;
+  const size_t lds = 4 * (size_t)stage;
   hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, items, a, stage);
   return hipGetLastError();
 }
