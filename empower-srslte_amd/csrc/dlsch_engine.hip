@@ -126,10 +126,18 @@ struct DlschEngine {
   int32_t *d_ret_stage = nullptr;
   uint32_t *d_noi_stage = nullptr;
   // pinned staging for the per-call descriptors, reused once the previous copies completed
-  DermItem *h_items = nullptr;
+  DermItem *h_items = nullptr; // rm_rx_dev's single item
   TbItem *h_tbs = nullptr;
   const int16_t **h_rows = nullptr;
   uint32_t *h_cbmap = nullptr;
+  // a decode call's descriptors packed into one block (records, row pointers, CB map, TBs), one
+  // upload per call
+  uint8_t *h_blk = nullptr, *d_blk = nullptr;
+  std::vector<DermRec> rec_tb; // records in TB order while the call is planned
+  // table sets per (K, rv, layout): index into d_tabs (device, append-only)
+  std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t> tab_index;
+  DermTabs *d_tabs = nullptr;
+  static constexpr uint32_t TABS_CAP = 4096;
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
   bool llr8 = false; // srslte_sch_t.llr_is_8bit: int8 LLRs, 8-bit de-RM and decoders
@@ -176,6 +184,9 @@ struct DlschEngine {
     HIPCHK(hipMalloc(&d_ret_stage, sizeof(int32_t) * cap));
     HIPCHK(hipMalloc(&d_noi_stage, sizeof(uint32_t) * cap));
     HIPCHK(hipHostMalloc(&h_items, sizeof(DermItem) * cap));
+    HIPCHK(hipHostMalloc(&h_blk, blk_bytes(cap, cap)));
+    HIPCHK(hipMalloc(&d_blk, blk_bytes(cap, cap)));
+    HIPCHK(hipMalloc(&d_tabs, sizeof(DermTabs) * TABS_CAP));
     HIPCHK(hipHostMalloc(&h_tbs, sizeof(TbItem) * cap));
     HIPCHK(hipHostMalloc(&h_rows, sizeof(int16_t *) * cap));
     HIPCHK(hipHostMalloc(&h_cbmap, sizeof(uint32_t) * cap));
@@ -204,8 +215,10 @@ struct DlschEngine {
                     (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
-                    (void *)h_ul})
+                    (void *)h_ul, (void *)h_blk})
       if (p) (void)hipHostFree(p);
+    for (void *p : {(void *)d_blk, (void *)d_tabs})
+      if (p) (void)hipFree(p);
     for (auto &kv : tables) (void)hipFree(kv.second);
     tables.clear();
     for (auto &kv : inv_tables) (void)hipFree(kv.second);
@@ -259,6 +272,26 @@ struct DlschEngine {
     if (hipMemcpy(d, t4.data(), t4.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
     inv_t4_tables.emplace(key, d);
     return d;
+  }
+
+  // the packed block of a call: records, row pointers, CB map, TBs (256-byte aligned regions)
+  static size_t al(size_t n) { return (n + 255) & ~(size_t)255; }
+  static size_t blk_bytes(uint32_t ncb, uint32_t ntb) {
+    return al(sizeof(DermRec) * ncb) + al(sizeof(int16_t *) * ncb) + al(4 * (size_t)ncb) + al(sizeof(TbItem) * ntb);
+  }
+
+  // index of the table set of (K, rv, layout) in d_tabs (created and uploaded on first use)
+  int tab_of(uint32_t K, uint32_t rv, uint32_t nsb) {
+    const auto key = std::make_tuple(K, rv, nsb);
+    auto it = tab_index.find(key);
+    if (it != tab_index.end()) return it->second;
+    if (tab_index.size() >= TABS_CAP) return -1;
+    DermTabs t{table(K, rv, nsb), inv_table(K, rv, nsb), nsb && nsb % 8 == 0 ? inv_t4_table(K, rv, nsb) : nullptr};
+    if (!t.table || !t.inv || (nsb && nsb % 8 == 0 && !t.inv_t4)) return -1;
+    const uint16_t idx = (uint16_t)tab_index.size();
+    if (hipMemcpy(d_tabs + idx, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) return -1;
+    tab_index.emplace(key, idx);
+    return idx;
   }
 
   const uint16_t *table(uint32_t K, uint32_t rv, uint32_t nsb) {
@@ -361,6 +394,10 @@ struct DlschEngine {
     };
     std::vector<Cb> cbs;
     uint32_t ncb = 0, max_n = 0;
+    rec_tb.resize(cap);
+    const int16_t *e_base = nullptr; // the records' LLR offsets are relative to the lowest TB pointer
+    for (uint32_t b = 0; b < ntb; b++)
+      if (e_ptr[b] && (!e_base || e_ptr[b] < e_base)) e_base = e_ptr[b];
     for (uint32_t b = 0; b < ntb; b++) {
       const srsgpu_dlsch_tb_t &t = tb[b];
       TbItem &ti = h_tbs[b];
@@ -417,30 +454,29 @@ struct DlschEngine {
           rp = (s.C - gamma) * n_e + (i - (s.C - gamma)) * ne;
         }
         const uint32_t nsb = llr8 ? auto_subblocks_8bit(K) : auto_subblocks(K);
-        const uint16_t *tab = table(K, t.rv, nsb);
-        const uint16_t *inv = inv_table(K, t.rv, nsb);
-        if (!tab || !inv) return -1;
-        DermItem &it = h_items[ncb];
-        it.e = e_ptr[b] + rp;
+        const int tab = tab_of(K, t.rv, nsb);
+        if (tab < 0) return -1;
+        const ptrdiff_t eo = (e_ptr[b] + rp) - e_base;
+        if (eo < 0 || eo > (ptrdiff_t)UINT32_MAX) {
+          fprintf(stderr, "srsgpu: the LLRs of a call must lie within 2^32 elements of each other\n");
+          return -1;
+        }
+        DermRec &it = rec_tb[ncb];
+        it.e_off = (uint32_t)eo;
         it.ne = ne;
-        it.N = 3 * K + 12;
-        it.table = tab;
-        it.inv = inv;
-        it.row = row(t.softbuffer, i);
-        it.cb_crc = ti.cb_crc + i;
-        it.rowlen = nsb ? 3 * (K + 32) + 12 : 3 * K + 12;
-        it.fresh = fresh + (size_t)t.softbuffer * max_cb + i;
+        it.N = (uint16_t)(3 * K + 12);
+        it.tab = (uint16_t)tab;
+        it.row = t.softbuffer * max_cb + i;
+        it.rowlen = (uint16_t)(nsb ? 3 * (K + 32) + 12 : 3 * K + 12);
         it.w8 = llr8;
-        it.tb_ret = d_ret + b;
+        it.tb = b;
         {
           // the loader the decoder job will pick for this block (TdecEngine::derm_direct)
           const int r = resolve_impl(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, K);
           it.direct = direct_derm && sb_input_for(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, r) &&
                       impl_nb(r) % 8 == 0;
-          it.inv_t4 = nullptr;
-          if (it.direct && !(it.inv_t4 = inv_t4_table(K, t.rv, nsb))) return -1;
         }
-        max_n = std::max(max_n, std::min(ne, it.N));
+        max_n = std::max(max_n, std::min(ne, 3 * K + 12));
         cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
       }
     }
@@ -450,34 +486,39 @@ struct DlschEngine {
       return std::tie(cbs[a].K, cbs[a].poly, cbs[a].crclen) <
              std::tie(cbs[b].K, cbs[b].poly, cbs[b].crclen);
     });
-    // items in decoder order (k_load_derm reads them by decoder position)
-    std::vector<DermItem> tb_order(h_items, h_items + ncb);
+    // records in decoder order (k_load_derm reads them by decoder position), packed with the row
+    // pointers, the CB map and the TBs into one block: one upload
+    const size_t o_rows = al(sizeof(DermRec) * ncb), o_map = o_rows + al(sizeof(int16_t *) * ncb),
+                 o_tbs = o_map + al(4 * (size_t)ncb), o_end = o_tbs + sizeof(TbItem) * ntb;
+    DermRec *b_rec = reinterpret_cast<DermRec *>(h_blk);
+    const int16_t **b_rows = reinterpret_cast<const int16_t **>(h_blk + o_rows);
+    uint32_t *b_map = reinterpret_cast<uint32_t *>(h_blk + o_map);
     uint32_t ndirect = 0;
     tdec.derm_max_ne = 0;
     for (uint32_t p = 0; p < order.size(); p++) {
       const uint32_t u = cbs[order[p]].u;
-      h_cbmap[u] = p;
-      h_items[p] = tb_order[u];
-      h_items[p].pos = p;
-      h_rows[p] = h_items[p].row;
-      if (h_items[p].direct) {
+      b_map[u] = p;
+      b_rec[p] = rec_tb[u];
+      b_rec[p].pos = p;
+      b_rows[p] = soft + (size_t)b_rec[p].row * SRSGPU_SOFTBUFFER_SIZE;
+      if (b_rec[p].direct) {
         ndirect++;
-        tdec.derm_max_ne = std::max(tdec.derm_max_ne, h_items[p].ne);
+        tdec.derm_max_ne = std::max(tdec.derm_max_ne, b_rec[p].ne);
       }
     }
+    memcpy(h_blk + o_tbs, h_tbs, sizeof(TbItem) * ntb);
     // ---- device ----
-    if (ncb) {
-      HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(DermItem) * ncb, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(d_rows, h_rows, sizeof(int16_t *) * ncb, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(d_cbmap, h_cbmap, sizeof(uint32_t) * ncb, hipMemcpyHostToDevice, st));
-    }
-    HIPCHK(hipMemcpyAsync(d_tbs, h_tbs, sizeof(TbItem) * ntb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_blk, h_blk, o_end, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    if (ndirect) HIPCHK(launch_derm_flags(d_items, (int)ncb, d_init, d_late, st));
+    const TbItem *d_tbs_c = reinterpret_cast<const TbItem *>(d_blk + o_tbs);
+    const uint32_t *d_map_c = reinterpret_cast<const uint32_t *>(d_blk + o_map);
+    const int16_t *const *d_rows_c = reinterpret_cast<const int16_t *const *>(d_blk + o_rows);
+    const DermCall dc{reinterpret_cast<const DermRec *>(d_blk), d_tabs, e_base, soft, cbcrc, fresh, d_ret};
+    if (ndirect) HIPCHK(launch_derm_flags(dc, (int)ncb, d_init, d_late, st));
     if (ndirect < ncb) {
       ProfScope ps("k_derm", st);
-      HIPCHK(launch_derm(d_items, (int)ncb, max_n, d_init, st));
+      HIPCHK(launch_derm(dc, (int)ncb, d_init, st));
     }
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;
@@ -492,17 +533,16 @@ struct DlschEngine {
     }
     if (!specs.empty() &&
         tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, (uint32_t)order.size(), nullptr, 0,
-                          (const int16_t *const *)d_rows, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed,
-                          ndirect ? d_items : nullptr))
+                          d_rows_c, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed, ndirect ? &dc : nullptr))
       return -1;
     {
       ProfScope ps("k_tb_finish", st);
-      HIPCHK(launch_tb_finish(d_tbs, (int)ntb, d_cbmap, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st,
-                              ndirect ? d_items : nullptr, ndirect ? d_late : nullptr));
+      HIPCHK(launch_tb_finish(d_tbs_c, (int)ntb, d_map_c, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st,
+                              ndirect ? dc : DermCall{}, ndirect ? d_late : nullptr));
     }
     if (ndirect) { // rows of the direct blocks of failed TBs, for the retransmission
       ProfScope ps("k_rows_late", st); // k_derm_late
-      HIPCHK(launch_derm_late(d_items, (int)ncb, d_late, st));
+      HIPCHK(launch_derm_late(dc, (int)ncb, d_late, st));
     }
     return 0;
   }

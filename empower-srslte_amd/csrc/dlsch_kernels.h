@@ -28,6 +28,32 @@ struct DermItem {
   const uint16_t *inv_t4; // direct: the inverse table in the decoder's T4 order, [3][ne] + 12 tails
 };
 
+// The per-call form of the DermItems of a decode: 32 bytes per code block uploaded per call (the
+// full DermItem, 104 bytes of pointers and sizes, made the descriptor upload the largest copy of a
+// 512-subframe batch); the pointers come from the call (DermCall) and a table set per (K, rv,
+// layout) that stays on the device (DermTabs). derm_get() expands a record.
+struct DermRec {
+  uint32_t e_off;  // its LLRs: DermCall::e + e_off
+  uint32_t ne;     // E
+  uint32_t row;    // softbuffer row index (slot * max_cb + cb): the row, its cb_crc and fresh flags
+  uint32_t pos;    // position in the decoder's order
+  uint32_t tb;     // its TB in the call: DermCall::ret + tb
+  uint16_t N, rowlen;
+  uint16_t tab;    // its table set in DermCall::tabs
+  uint8_t w8, direct;
+};
+struct DermTabs {
+  const uint16_t *table, *inv, *inv_t4;
+};
+struct DermCall {
+  const DermRec *rec;     // by decoder position
+  const DermTabs *tabs;
+  const int16_t *e;       // LLR base of the call
+  int16_t *soft;          // softbuffer rows (SRSGPU_SOFTBUFFER_SIZE int16 each)
+  uint8_t *cbcrc, *fresh; // per row
+  const int32_t *ret;     // per TB
+};
+
 // one transport block's epilogue
 struct TbItem {
   uint8_t *data;      // output bytes
@@ -52,13 +78,12 @@ struct EncItem {
 };
 
 // rows of the items that are not `direct` (before the decode), init_done of every item
-hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st);
+hipError_t launch_derm(const DermCall &c, int nitems, uint8_t *init_done, hipStream_t st);
 // after k_tb_finish: rows of the direct items it listed in late (late[0] of them at late[1..]:
 // blocks of failed TBs not decoded before this call)
-hipError_t launch_derm_late(const DermItem *d_items, int nitems, const uint32_t *late, hipStream_t st);
+hipError_t launch_derm_late(const DermCall &c, int nitems, const uint32_t *late, hipStream_t st);
 // init_done[pos] = cb_crc before this call, for every item; late[0] = 0 (late may be null)
-hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, uint32_t *late,
+hipError_t launch_derm_flags(const DermCall &c, int nitems, uint8_t *init_done, uint32_t *late,
                              hipStream_t st);
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 // softbuffer reset of count slots of max_cb rows from fresh / cbcrc: cb_crc = 0, the first ncb
@@ -67,12 +92,12 @@ hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint3
                            hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there
 // crc_a[d] = x^(d+24) mod P_24A for d < the largest TBS + 24
-// items / late (both or neither): a failed TB appends its direct blocks not decoded before the
+// dc.rec / late (both or neither): a failed TB appends its direct blocks not decoded before the
 // call to late (launch_derm_late)
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
                             const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
-                            const DermItem *items = nullptr, uint32_t *late = nullptr);
+                            const DermCall &dc = DermCall{}, uint32_t *late = nullptr);
 // crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
 hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
                                const uint32_t *crc_b, hipStream_t st);
@@ -91,9 +116,9 @@ namespace srsgpu {
 // Direct de-rate-matching for the window decoders: the decoder inputs SP0 / P1 / T of groups
 // [0, ng) of dg (sub-block rows, nb a multiple of 8) computed from each code block's LLRs and its
 // softbuffer row (skipped when fresh) as k_derm + k_load_sbt would, without writing the row.
-// items are indexed by decoder position (TdGroup::cb0 numbering); one workgroup per pair.
+// c.rec is indexed by decoder position (TdGroup::cb0 numbering); one workgroup per pair.
 // max_ne: the largest E among the items (sizes the LDS staging of the LLRs)
-hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermItem *items,
+hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCall &c,
                             const TdArrays &a, uint32_t max_ne, hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "dlsch_kernels.h"
+#include "srsgpu/dlsch_batch.h"
 
 #include <algorithm>
 
@@ -69,6 +70,28 @@ __device__ __forceinline__ void stage_llrs(uint32_t *es, const int16_t *ep, uint
     for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x)
       es[w] = (uint32_t)e[2 * w] | (2 * w + 1 < ne ? (uint32_t)e[2 * w + 1] << 16 : 0u);
   }
+}
+
+// the full descriptor of record i of a call
+__device__ __forceinline__ DermItem derm_get(const DermCall &c, uint32_t i) {
+  const DermRec r = c.rec[i];
+  const DermTabs t = c.tabs[r.tab];
+  DermItem it;
+  it.e = c.e + r.e_off;
+  it.ne = r.ne;
+  it.N = r.N;
+  it.table = t.table;
+  it.inv = t.inv;
+  it.inv_t4 = t.inv_t4;
+  it.row = c.soft + (size_t)r.row * SRSGPU_SOFTBUFFER_SIZE;
+  it.cb_crc = c.cbcrc + r.row;
+  it.fresh = c.fresh + r.row;
+  it.pos = r.pos;
+  it.rowlen = r.rowlen;
+  it.w8 = r.w8;
+  it.direct = r.direct;
+  it.tb_ret = c.ret + r.tb;
+  return it;
 }
 
 // phase 0: before the decode, every item not `direct`; phase 1: after k_tb_finish, the direct
@@ -135,12 +158,11 @@ __device__ __forceinline__ void derm_item(const DermItem &it, uint32_t *es) {
   if (fresh && threadIdx.x == 0) *glob(it.fresh) = 0; // the row now holds real soft bits
 }
 
-__global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items, int nitems,
-                                              uint8_t *__restrict__ init_done) {
+__global__ __launch_bounds__(256) void k_derm(DermCall dc, int nitems, uint8_t *__restrict__ init_done) {
   __shared__ uint32_t es[DERM_LDS / 2];
   const int g = blockIdx.x;
   if (g >= nitems) return;
-  const DermItem it = items[g];
+  const DermItem it = derm_get(dc, g);
   const uint8_t skip = it.cb_crc ? *glob(it.cb_crc) : 0;
   if (threadIdx.x == 0) init_done[it.pos] = skip;
   if (skip || it.direct) return; // sch.c:323: blocks whose CRC passed before are not combined again
@@ -150,12 +172,11 @@ __global__ __launch_bounds__(256) void k_derm(const DermItem *__restrict__ items
 // the deferred rows: the direct blocks k_tb_finish listed (late[0] of them at late[1..], decoder
 // positions: blocks of failed TBs not decoded before the call), a few workgroups looping over the
 // list, so an all-acked batch costs one short launch
-__global__ __launch_bounds__(256) void k_derm_late(const DermItem *__restrict__ items,
-                                                   const uint32_t *__restrict__ late) {
+__global__ __launch_bounds__(256) void k_derm_late(DermCall dc, const uint32_t *__restrict__ late) {
   __shared__ uint32_t es[DERM_LDS / 2];
   const uint32_t n = late[0];
   for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
-    const DermItem it = items[late[1 + q]];
+    const DermItem it = derm_get(dc, late[1 + q]);
     derm_item(it, es);
     __syncthreads(); // es is reused by the next block
   }
@@ -174,13 +195,13 @@ __global__ __launch_bounds__(256) void k_derm_rmw(const DermItem *__restrict__ i
   }
 }
 
-__global__ __launch_bounds__(256) void k_derm_flags(const DermItem *__restrict__ items, int n,
-                                                    uint8_t *__restrict__ init_done, uint32_t *__restrict__ late) {
+__global__ __launch_bounds__(256) void k_derm_flags(DermCall dc, int n, uint8_t *__restrict__ init_done,
+                                                    uint32_t *__restrict__ late) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0 && late) late[0] = 0;
   if (i >= n) return;
-  const uint8_t *c = items[i].cb_crc;
-  init_done[items[i].pos] = c ? *glob(c) : 0;
+  const DermRec r = dc.rec[i];
+  init_done[r.pos] = dc.cbcrc[r.row];
 }
 
 // ------------------------------------------------------------------ direct de-RM ----
@@ -196,8 +217,7 @@ __global__ __launch_bounds__(256) void k_derm_flags(const DermItem *__restrict__
 // passes also wrote and re-read the 3(K+32)+12 row entries).
 #define LDR_THREADS 256
 __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
-                                                           const DermItem *__restrict__ items, TdArrays arr,
-                                                           uint32_t stage) {
+                                                           DermCall dc, TdArrays arr, uint32_t stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
   uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
   int gi = 0;
@@ -225,12 +245,12 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
     bool fresh, staged;
   };
   auto blk = [&](int c) {
-    const DermItem &it = items[c];
+    const DermItem it = derm_get(dc, c);
     return Blk{it.e, it.row, it.inv_t4, it.ne, it.N, it.fresh && *glob(it.fresh),
                it.ne <= it.N && it.ne <= stage};
   };
   const Blk ba = blk(c0), bb = blk(c1);
-  const bool w8 = items[c0].w8 != 0; // one LLR width per call
+  const bool w8 = dc.rec[c0].w8 != 0; // one LLR width per call
   if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
   if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
   __syncthreads();
@@ -318,8 +338,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint8_t *__restrict__ cb_ok_in,
                                                    const uint8_t *__restrict__ init_done,
                                                    const uint32_t *__restrict__ noi_in,
-                                                   const uint32_t *__restrict__ crc_a,
-                                                   const DermItem *__restrict__ items,
+                                                   const uint32_t *__restrict__ crc_a, DermCall dc,
                                                    uint32_t *__restrict__ late) {
   __shared__ uint32_t red[4];
   __shared__ uint32_t crc_tab[256];
@@ -413,7 +432,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   const int ok_all = all_ok;
   if (!ok_all) {
     // the direct blocks of this failed TB that were not decoded before: their rows are due
-    if (late && threadIdx.x < C && !c_init[threadIdx.x] && items[c_g[threadIdx.x]].direct)
+    if (late && threadIdx.x < C && !c_init[threadIdx.x] && dc.rec[c_g[threadIdx.x]].direct)
       late[1 + atomicAdd(late, 1u)] = c_g[threadIdx.x];
     // keep the bytes of the blocks that passed for the retransmission (sch.c:407-416)
     for (uint32_t i = 0; i < C; i++) {
@@ -497,36 +516,34 @@ hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint3
   return hipGetLastError();
 }
 
-hipError_t launch_derm(const DermItem *d_items, int nitems, uint32_t max_n, uint8_t *init_done,
-                       hipStream_t st) {
+hipError_t launch_derm(const DermCall &c, int nitems, uint8_t *init_done, hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
-  (void)max_n;
-  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, d_items, nitems, init_done);
+  hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, c, nitems, init_done);
   return hipGetLastError();
 }
 
-hipError_t launch_derm_late(const DermItem *d_items, int nitems, const uint32_t *late, hipStream_t st) {
+hipError_t launch_derm_late(const DermCall &c, int nitems, const uint32_t *late, hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_derm_late, dim3((unsigned)std::min(nitems, 512)), dim3(256), 0, st, d_items, late);
+  hipLaunchKernelGGL(k_derm_late, dim3((unsigned)std::min(nitems, 512)), dim3(256), 0, st, c, late);
   return hipGetLastError();
 }
 
-hipError_t launch_derm_flags(const DermItem *d_items, int nitems, uint8_t *init_done, uint32_t *late,
+hipError_t launch_derm_flags(const DermCall &c, int nitems, uint8_t *init_done, uint32_t *late,
                              hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_derm_flags, dim3(cdiv((size_t)nitems, 256)), dim3(256), 0, st, d_items, nitems,
+  hipLaunchKernelGGL(k_derm_flags, dim3(cdiv((size_t)nitems, 256)), dim3(256), 0, st, c, nitems,
                      init_done, late);
   return hipGetLastError();
 }
 
-hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermItem *items,
+hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCall &c,
                             const TdArrays &a, uint32_t max_ne, hipStream_t st) {
   if (ng <= 0 || nblocks <= 0) return hipSuccess;
   // LLRs staged per block: the largest E of the call, rounded to 8, at most 8192 (16 KB); blocks
   // with more (or with repetition, E > 3K+12) gather theirs from HBM
   const uint32_t stage = std::min<uint32_t>(8192, (max_ne + 7) / 8 * 8);
   const size_t lds = 4 * (size_t)stage;
-  hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, items, a, stage);
+  hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, c, a, stage);
   return hipGetLastError();
 }
 
@@ -539,10 +556,10 @@ hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st) {
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
                             const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
-                            const DermItem *items, uint32_t *late) {
+                            const DermCall &dc, uint32_t *late) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi, crc_a, items, late);
+                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late);
   return hipGetLastError();
 }
 

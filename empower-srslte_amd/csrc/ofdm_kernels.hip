@@ -336,10 +336,13 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
   if (nsf <= 0) return hipSuccess;
   const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
   const int nsym = nsf * 14;
-  // SRSGPU_OFDM_PERSIST=0: the one-symbol-per-workgroup kernel for every size (A/B measurements)
+  // SRSGPU_OFDM_PERSIST=1: the resident-grid kernel with next-symbol prefetch for the large sizes.
+  // Off by default: alone on the GPU it took 68 us per 512 20 MHz subframes against 59 us for one
+  // symbol per workgroup (profiles/r04_s6_kb_*.json), and its fixed grid fares worse still beside
+  // another stream's kernels.
   static const bool persist = [] {
     const char *e = getenv("SRSGPU_OFDM_PERSIST");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (persist && (N == 2048 || N == 1536 || N == 1024)) {
     // every workgroup takes the same number of symbols (no partial last round)

@@ -404,7 +404,7 @@ struct TdecEngine {
   }
   int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
                    int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs,
-                   bool flags = true, const DermItem *derm = nullptr) {
+                   bool flags = true, const DermCall *derm = nullptr) {
     // load launches: runs of groups with the same loader (nb, sb_input); rows_aligned is the
     // byte alignment every row is guaranteed to have (0: none)
     const size_t ng = groups.size();
@@ -441,7 +441,7 @@ struct TdecEngine {
       const TdGroup &f = groups[r.g0];
       if (r.direct) {
         ProfScope ps("k_ldderm", st); // k_load_derm (a name no other scope contains: srsgpu_prof_get matches substrings)
-        HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, derm, a, derm_max_ne, st));
+        HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, *derm, a, derm_max_ne, st));
         continue;
       }
       ProfScope ps("k_load", st);
@@ -713,7 +713,7 @@ struct TdecEngine {
   int decode_multi(int impl, int sb_layout, const std::vector<TdSpec> &specs, uint32_t total_cbs,
                    const int16_t *d_in, size_t in_stride, const int16_t *const *rows, int rows_aligned,
                    const uint8_t *init_done, uint32_t maxh, uint8_t *d_out, size_t out_stride,
-                   uint8_t *d_ok, uint32_t *d_noi, bool fixed = false, const DermItem *derm = nullptr) {
+                   uint8_t *d_ok, uint32_t *d_noi, bool fixed = false, const DermCall *derm = nullptr) {
     if (maxh == 0 || total_cbs > cap_cbs) {
       fprintf(stderr, "srsgpu: invalid early-stop job (max_halfits=%u, %u code blocks)\n", maxh, total_cbs);
       return -1;
