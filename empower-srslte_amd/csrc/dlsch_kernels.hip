@@ -10,6 +10,7 @@
 //                 the TB CRC24A check.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dlsch_kernels.h"
 #include "srsgpu/dlsch_batch.h"
@@ -316,6 +317,145 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   }
 }
 
+// The previous form of k_load_derm, kept for A/B measurements (SRSGPU_LDERM=tile): row-order
+// inverse tables, six (stream, block) chunks of 2048 row positions formed in LDS per tile and
+// written out in the T4 layout through an LDS transposition, 512 threads per pair.
+#define LDT_THREADS 512
+#define LDT_TILE 2048                      // row positions per (stream, block) chunk of a tile
+#define LDT_PIECES (6 * LDT_TILE / 8)      // 16-byte pieces of a tile
+#define LDT_PPT (LDT_PIECES / LDT_THREADS) // pieces per thread
+__global__ __launch_bounds__(LDT_THREADS) void k_load_derm_tile(const TdGroup *__restrict__ groups, int ngroups,
+                                                           DermCall dc, TdArrays arr, uint32_t stage) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t ldt_lds[];
+  uint16_t(*tile)[LDT_TILE] = reinterpret_cast<uint16_t(*)[LDT_TILE]>(ldt_lds); // [6][LDT_TILE]
+  uint32_t *llr0 = ldt_lds + 6 * LDT_TILE / 2, *llr1 = llr0 + stage / 2;
+  int gi = 0;
+  { // the last group whose first workgroup is <= blockIdx.x
+    int lo = 0, hi = ngroups - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (groups[mid].blk_load <= (int)blockIdx.x)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    gi = lo;
+  }
+  const TdGroup &G = groups[gi];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
+  const int pair = blockIdx.x - G.blk_load;
+  if (pair >= npairs) return;
+  const int L = K / nb, G4 = (L + 3) >> 2, S = LDT_TILE / nb;
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
+  // the two blocks' fields (selected by h, which is wave-uniform: no indexed private arrays)
+  struct Blk {
+    const int16_t *e, *row;
+    const uint16_t *inv;
+    uint32_t ne, N;
+    bool fresh, staged;
+  };
+  auto blk = [&](int c) {
+    const DermItem it = derm_get(dc, c);
+    return Blk{it.e, it.row, it.inv, it.ne, it.N, it.fresh && *glob(it.fresh),
+               it.ne <= it.N && it.ne <= stage};
+  };
+  const Blk ba = blk(c0), bb = blk(c1);
+  const bool w8 = dc.rec[c0].w8 != 0; // one LLR width per call
+  // tile pieces: chunk c = (stream, block), 8 row positions from sub-block index e
+  auto piece_at = [&](int q, int k0, int &c, int &pc, uint32_t &o8) {
+    const int idx = threadIdx.x + LDT_THREADS * q;
+    c = idx / (LDT_TILE / 8);
+    pc = idx - c * (LDT_TILE / 8);
+    const int st = c >> 1;
+    int e = k0 * nb + pc * 8; // past the last step: its copy (values unused)
+    if (e >= L * nb) e = (L - 1) * nb + (e & (nb - 1));
+    o8 = (uint32_t)(st * (K + 32) + e) / 8;
+  };
+  u4v iv[LDT_PPT], ov[LDT_PPT];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < LDT_PPT; q++) {
+      int c, pc;
+      uint32_t o8;
+      piece_at(q, k0, c, pc, o8);
+      const Blk &b = (c & 1) ? bb : ba;
+      iv[q] = glob(reinterpret_cast<const u4v *>(b.inv))[o8];
+      ov[q] = b.fresh ? u4v{0, 0, 0, 0} : glob(reinterpret_cast<const u4v *>(b.row))[o8];
+    }
+  };
+  fetch(0); // the first tile's table loads fly while the LLRs are staged
+  if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
+  if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
+  __syncthreads();
+  // value of a row position of block b given its inverse-table entry m and the row's old value
+  auto value = [&](const Blk &b, const uint16_t *lds, uint32_t m, uint32_t old) -> uint32_t {
+    uint32_t acc = b.fresh ? 0u : old;
+    if (b.staged) {
+      acc += m < b.ne ? (uint32_t)lds[m] : 0u; // 0xFFFF >= ne
+    } else if (m != 0xFFFFu) {
+      const gp_t<const uint16_t> e = glob(reinterpret_cast<const uint16_t *>(b.e));
+      for (uint32_t i = m; i < b.ne; i += b.N) acc += e[i];
+    }
+    return derm_fold(acc, w8);
+  };
+  const size_t pbase = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
+  const gp_t<u4v> SP0 = glob(reinterpret_cast<u4v *>((int16_t *)arr.SP0 + 4 * pbase));
+  const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
+  for (int k0 = 0; k0 < 4 * G4; k0 += S) {
+#pragma unroll
+    for (int q = 0; q < LDT_PPT; q++) {
+      int c, pc;
+      uint32_t o8;
+      piece_at(q, k0, c, pc, o8);
+      const bool h = c & 1;
+      const Blk &b = h ? bb : ba;
+      const uint16_t *lds = reinterpret_cast<const uint16_t *>(h ? llr1 : llr0);
+      const uint32_t im[4] = {iv[q].x, iv[q].y, iv[q].z, iv[q].w}, om[4] = {ov[q].x, ov[q].y, ov[q].z, ov[q].w};
+      uint32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        r[u] = (value(b, lds, im[u] & 0xFFFFu, om[u] & 0xFFFFu) & 0xFFFFu) |
+               (value(b, lds, im[u] >> 16, om[u] >> 16) << 16);
+      *reinterpret_cast<u4v *>(&tile[c][pc * 8]) = u4v{r[0], r[1], r[2], r[3]};
+    }
+    __syncthreads();
+    if (k0 + S < 4 * G4) fetch(k0 + S);
+    // the tile's steps as T4 elements: el -> step (el / 4 / nb) * 4 + el % 4, chain el / 4 % nb
+    const int nel = min(S, 4 * G4 - k0) * nb;
+    auto at = [&](int c, int el) -> uint32_t {
+      const int g4l = el / (4 * nb), d = (el >> 2) % nb, u = el & 3;
+      return tile[c][(4 * g4l + u) * nb + d];
+    };
+    const size_t e0 = (size_t)k0 * nb; // T4 element of the tile's first step
+#pragma unroll
+    for (int q = 0; q < LDT_TILE / 2 / LDT_THREADS; q++) {
+      const int v = threadIdx.x + LDT_THREADS * q; // SP0 elements 2v, 2v + 1
+      if (2 * v < nel) {
+        const int ea = 2 * v, eb = 2 * v + 1;
+        SP0[e0 / 2 + v] = u4v{at(0, ea) | (at(1, ea) << 16), at(2, ea) | (at(3, ea) << 16),
+                              at(0, eb) | (at(1, eb) << 16), at(2, eb) | (at(3, eb) << 16)};
+      }
+    }
+    if (4 * (int)threadIdx.x < nel) {
+      const int e = 4 * threadIdx.x;
+      P1[e0 / 4 + threadIdx.x] = u4v{at(4, e) | (at(5, e) << 16), at(4, e + 1) | (at(5, e + 1) << 16),
+                                     at(4, e + 2) | (at(5, e + 2) << 16), at(4, e + 3) | (at(5, e + 3) << 16)};
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 12) { // the tails: row positions 3(K+32) .. +11
+    const int t = threadIdx.x;
+    const uint32_t o = 3u * (K + 32) + t;
+    auto tail = [&](const Blk &b, const uint32_t *l) -> uint32_t {
+      const uint32_t m = glob(b.inv)[o];
+      const uint32_t old = b.fresh ? 0u : (uint16_t)glob(b.row)[o];
+      return value(b, reinterpret_cast<const uint16_t *>(l), m, old) & 0xFFFFu;
+    };
+    const uint32_t va = tail(ba, llr0), vb = tail(bb, llr1);
+    glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = va | (vb << 16);
+  }
+}
+
 // XOR-reduce one value per thread over the workgroup
 __device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
   for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o);
@@ -342,6 +482,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    uint32_t *__restrict__ late) {
   __shared__ uint32_t red[4];
   __shared__ uint32_t crc_tab[256];
+  __shared__ uint32_t c_ck0[TBF_MAXC + 1];
   __shared__ uint32_t c_g[TBF_MAXC], c_dst[TBF_MAXC], c_nb[TBF_MAXC], c_rb[TBF_MAXC];
   __shared__ uint8_t c_init[TBF_MAXC], c_ok[TBF_MAXC];
   __shared__ int all_ok;
@@ -443,11 +584,11 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
     }
   }
   // 3. TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491). crc.c:144-155 (MSB
-  //    first, zero init) is linear: the checksum is M(x) x^24 mod P. The TB's bytes are cut into
-  //    32-byte chunks counted from the end; thread c runs the byte-table CRC over chunk c (chunk
-  //    c ends 256 c bits before the message end) and shifts it into place, x^(256 c) mod P =
-  //    crc_a[256 c - 24] (c > 0), by a carry-less multiply mod P; the chunks' values are XORed.
-  //    (The bit-weight fold this replaces read 4 B of weights per message bit.)
+  //    first, zero init) is linear: the checksum is M(x) x^24 mod P, the XOR over any cut of the
+  //    message into pieces of each piece's byte-table CRC shifted by x^(8 bytes after it) mod P
+  //    (crc_a[n - 24], or x^n itself below 24 bits; a carry-less multiply mod P). The pieces are
+  //    32-byte chunks of each code block's bytes, read straight from its decision row (or its
+  //    saved bytes) with 16-byte loads, so the CRC does not wait for the TB bytes of step 2.
   uint32_t crc = 0;
   if (ok_all) {
     if (threadIdx.x < 256) { // byte table: T[i] = i x^24 mod P, i.e. i << 16 through 8 shift steps
@@ -456,25 +597,37 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       for (int k = 0; k < 8; k++) r = ((r << 1) ^ ((r & 0x800000u) ? 0x864CFBu : 0u)) & 0xFFFFFFu;
       crc_tab[threadIdx.x] = r;
     }
+    const uint32_t nbytes = t.tbs / 8;
+    if (threadIdx.x == 0) { // chunks per code block: its bytes within [0, nbytes), 32 per chunk
+      uint32_t q = 0;
+      for (uint32_t i = 0; i < C; i++) {
+        c_ck0[i] = q;
+        const uint32_t len = c_dst[i] < nbytes ? min(c_rb[i], nbytes - c_dst[i]) : 0u;
+        q += (len + 31) / 32;
+      }
+      c_ck0[C] = q;
+    }
     __syncthreads();
-    constexpr uint32_t B = 32;
-    const uint32_t nbytes = t.tbs / 8, nch = (nbytes + B - 1) / B;
+    const uint32_t nck = c_ck0[C];
     uint32_t acc = 0;
-    for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
-      const uint32_t end = nbytes - c * B, beg = end > B ? end - B : 0;
-      const uint8_t *src = t.data + beg;
-      uint8_t v[B];
-#pragma unroll
-      for (uint32_t k = 0; k < B; k++) v[k] = k < end - beg ? src[k] : 0;
+    for (uint32_t q = threadIdx.x; q < nck; q += blockDim.x) {
+      uint32_t i = 0;
+      while (c_ck0[i + 1] <= q) i++;
+      const uint32_t off = 32 * (q - c_ck0[i]);
+      const uint32_t len = min(c_rb[i], nbytes - c_dst[i]), n = min(32u, len - off);
+      const uint8_t *src = (c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride) + off;
+      const u4v w0 = *glob(reinterpret_cast<const u4v *>(src)), w1 = *glob(reinterpret_cast<const u4v *>(src + 16));
+      const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const uint32_t after = nbytes - (c_dst[i] + off + n); // bytes after the chunk
+      const uint32_t shift = after == 0 ? 1u : 8 * after < 24 ? (1u << (8 * after)) : crc_a[8 * after - 24];
       uint32_t r = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < B; k++)
-        if (k < end - beg) r = ((r << 8) & 0xFFFFFFu) ^ crc_tab[((r >> 16) ^ v[k]) & 0xFFu];
-      if (c > 0) { // r x^(256 c) mod P
-        const uint32_t w = crc_a[256 * c - 24];
+      for (uint32_t k = 0; k < 32; k++)
+        if (k < n) r = ((r << 8) & 0xFFFFFFu) ^ crc_tab[((r >> 16) ^ (wv[k >> 2] >> (8 * (k & 3)))) & 0xFFu];
+      if (after) { // r x^(8 after) mod P
         uint64_t m = 0;
-        for (int i = 0; i < 24; i++)
-          if ((w >> i) & 1u) m ^= (uint64_t)r << i;
+        for (int b = 0; b < 24; b++)
+          if ((shift >> b) & 1u) m ^= (uint64_t)r << b;
         for (int bit = 46; bit >= 24; bit--)
           if ((m >> bit) & 1u) m ^= (uint64_t)0x1864CFBu << (bit - 24);
         r = (uint32_t)m & 0xFFFFFFu;
@@ -543,6 +696,15 @@ hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCa
   // with more (or with repetition, E > 3K+12) gather theirs from HBM
   const uint32_t stage = std::min<uint32_t>(8192, (max_ne + 7) / 8 * 8);
   const size_t lds = 4 * (size_t)stage;
+  static const bool tile = [] {
+    const char *e = getenv("SRSGPU_LDERM");
+    return e && e[0] == 't';
+  }();
+  if (tile) {
+    hipLaunchKernelGGL(k_load_derm_tile, dim3((unsigned)nblocks), dim3(LDT_THREADS), lds + 6 * LDT_TILE * 2, st, dg,
+                       ng, c, a, stage);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, c, a, stage);
   return hipGetLastError();
 }

@@ -2355,18 +2355,20 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
 // their decision words in Dfz and 1 + the parity of the ending half-iteration in cb_end), as
 // k_decide writes them (turbodecoder.c:353-360 + decision_byte, MSB first); one workgroup per CB
 // pair, many pairs in flight. Clears cb_end behind it.
-__global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ groups, int ngroups,
+#define ESB_PAIRS 8 // pairs per workgroup: most pairs of a batch ended before the fused launch
+__global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
                                                   const uint32_t *__restrict__ Dfz,
                                                   uint8_t *__restrict__ outb, size_t out_stride,
                                                   uint8_t *__restrict__ cb_end) {
   __shared__ uint32_t dw[6144 / 16 + 16];
-  const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, blockIdx.x)];
+  for (int gp = blockIdx.x * ESB_PAIRS; gp < min((int)(blockIdx.x + 1) * ESB_PAIRS, npairs_total); gp++) {
+  const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, gp)];
   const int K = G.K, NB = G.nb, ncb = G.ncb;
-  const int pair = blockIdx.x - G.pair0;
-  if (pair >= G.npairs) return;
+  const int pair = gp - G.pair0;
+  if (pair >= G.npairs) continue;
   const int cbs[2] = {G.cb0 + 2 * pair, 2 * pair + 1 < ncb ? G.cb0 + 2 * pair + 1 : -1};
   const int ends[2] = {cb_end[cbs[0]], cbs[1] >= 0 ? cb_end[cbs[1]] : 0};
-  if (!ends[0] && !ends[1]) return;
+  if (!ends[0] && !ends[1]) continue;
   const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
   const uint32_t *src = Dfz + G.dw0 + (size_t)pair * nw;
   for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
@@ -2411,6 +2413,7 @@ __global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ gr
   }
   __syncthreads();
   if (threadIdx.x < 2 && cbs[threadIdx.x] >= 0) cb_end[cbs[threadIdx.x]] = 0;
+  }
 }
 
 // The early-stop flags of the job's code blocks, one thread per pair: done = init_done (blocks
@@ -2681,8 +2684,8 @@ hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t
 
 hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_es_bytes, dim3(npairs), dim3(256), 0, st, dg, ng, (const uint32_t *)es.dfz,
-                     es.outb, es.out_stride, es.cb_end);
+  hipLaunchKernelGGL(k_es_bytes, dim3(nblk(npairs, ESB_PAIRS)), dim3(256), 0, st, dg, ng, npairs,
+                     (const uint32_t *)es.dfz, es.outb, es.out_stride, es.cb_end);
   return hipGetLastError();
 }
 
