@@ -603,6 +603,77 @@ int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
   return 0;
 }
 
+/* 4 ports (srslte_predecoding_diversity_multi with nof_ports == 4, precoding.c:670-685: no SSE form),
+ * then srslte_layerdemap_diversity over 4 layers (layermap.c:143-151): d[4i+k] = x_k[i] for the RE
+ * quadruplet 4i..4i+3, ports (0, 2) on REs 4i / 4i+1 and ports (1, 3) on 4i+2 / 4i+3 (the transmitter
+ * of precoding.c:1863-1889).
+ * - CSI off: srslte_predecoding_diversity_gen_ (:388-423): one channel per port pair read at the
+ *   first RE of its pair (h0 = h[0][4i], h2 = h[2][4i], h1 = h[1][4i+2], h3 = h[3][4i+2]), gains
+ *   hh02 / hh13 summed over rx antennas without the 1e-4 guard, float complex arithmetic,
+ *   x / (hh * scaling) * sqrt(2) in double;
+ * - CSI on: srslte_predecoding_diversity_csi (:604-662): per-RE gains a0..a3 (a0 from h[0][4i] and
+ *   h[2][4i+1], a1 from h[0][4i+1] and h[2][4i], likewise a2 / a3 on ports 1 / 3 at 4i+2 / 4i+3),
+ *   csi[4i+k] = a_k scaling / nof_rxant, x_k / (a_k scaling) * sqrtf(2) in float.
+ * Layer symbols: m_ap = n / 4 (n % 4 == 2: (n - 2) / 4), and srslte_pdsch_decode demaps n / 4 per
+ * layer, so d[4 (n / 4) ..] would be whatever the reference's buffer last held: n % 4 != 0 is refused.
+ * y: [rx][2n floats], h: [port * 2 + rx][2n floats]. */
+static txd_cf txd_conj(txd_cf a) { return (txd_cf){a.r, -a.i}; }
+static txd_cf txd_add(txd_cf a, txd_cf b) { return (txd_cf){a.r + b.r, a.i + b.i}; }
+static txd_cf txd_neg(txd_cf a) { return (txd_cf){-a.r, -a.i}; }
+static float txd_pow(txd_cf a) { return a.r * a.r + a.i * a.i; }
+
+int orc_predecode_txdiv4(const float *const *y, const float *const *h, int nrx, int n, float scaling, float *d,
+                         float *csi) {
+  if (n % 4 || nrx < 1 || nrx > 2) return -1;
+  for (int i = 0; i < n / 4; i++) {
+    txd_cf x[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    if (!csi) {
+      float hh02 = 0, hh13 = 0;
+      for (int p = 0; p < nrx; p++) {
+        const txd_cf h0 = txd_ld(h[0 * 2 + p], 4 * i), h1 = txd_ld(h[1 * 2 + p], 4 * i + 2);
+        const txd_cf h2 = txd_ld(h[2 * 2 + p], 4 * i), h3 = txd_ld(h[3 * 2 + p], 4 * i + 2);
+        hh02 += h0.r * h0.r + h0.i * h0.i + h2.r * h2.r + h2.i * h2.i;
+        hh13 += h1.r * h1.r + h1.i * h1.i + h3.r * h3.r + h3.i * h3.i;
+        const txd_cf r0 = txd_ld(y[p], 4 * i), r1 = txd_ld(y[p], 4 * i + 1);
+        const txd_cf r2 = txd_ld(y[p], 4 * i + 2), r3 = txd_ld(y[p], 4 * i + 3);
+        x[0] = txd_add(x[0], txd_add(txd_mul(txd_conj(h0), r0), txd_mul(h2, txd_conj(r1))));
+        x[1] = txd_add(x[1], txd_add(txd_mul(txd_neg(h2), txd_conj(r0)), txd_mul(txd_conj(h0), r1)));
+        x[2] = txd_add(x[2], txd_add(txd_mul(txd_conj(h1), r2), txd_mul(h3, txd_conj(r3))));
+        x[3] = txd_add(x[3], txd_add(txd_mul(txd_neg(h3), txd_conj(r2)), txd_mul(txd_conj(h1), r3)));
+      }
+      hh02 *= scaling;
+      hh13 *= scaling;
+      for (int k = 0; k < 4; k++) {
+        const float g = k < 2 ? hh02 : hh13;
+        d[8 * i + 2 * k] = (float)((double)(x[k].r / g) * sqrt(2));
+        d[8 * i + 2 * k + 1] = (float)((double)(x[k].i / g) * sqrt(2));
+      }
+    } else {
+      float a[4] = {0, 0, 0, 0};
+      for (int p = 0; p < nrx; p++) {
+        for (int q = 0; q < 2; q++) { /* q = 0: ports 0 / 2 on REs 4i, 4i+1; q = 1: ports 1 / 3 on 4i+2, 4i+3 */
+          const int b = 4 * i + 2 * q;
+          const txd_cf h00 = txd_ld(h[(q + 0) * 2 + p], b), h01 = txd_ld(h[(q + 2) * 2 + p], b);
+          const txd_cf h10 = txd_ld(h[(q + 0) * 2 + p], b + 1), h11 = txd_ld(h[(q + 2) * 2 + p], b + 1);
+          a[2 * q] += txd_pow(h00) + h11.r * h11.r + h11.i * h11.i;
+          a[2 * q + 1] += txd_pow(h10) + h01.r * h01.r + h01.i * h01.i;
+          const txd_cf r0 = txd_ld(y[p], b), r1 = txd_ld(y[p], b + 1);
+          x[2 * q] = txd_add(x[2 * q], txd_add(txd_mul(txd_conj(h00), r0), txd_mul(h11, txd_conj(r1))));
+          x[2 * q + 1] =
+              txd_add(x[2 * q + 1], txd_add(txd_mul(txd_neg(h01), txd_conj(r0)), txd_mul(txd_conj(h10), r1)));
+        }
+      }
+      for (int k = 0; k < 4; k++) {
+        a[k] *= scaling;
+        csi[4 * i + k] = a[k] / nrx;
+        d[8 * i + 2 * k] = x[k].r / a[k] * sqrtf(2.0f);
+        d[8 * i + 2 * k + 1] = x[k].i / a[k] * sqrtf(2.0f);
+      }
+    }
+  }
+  return 0;
+}
+
 /* ---------------------------------------------------------------- Viterbi (PDCCH) ---------- */
 /* srslte_viterbi_decode_f with the tail-biting K=7 r=1/3 decoder srsLTE builds for the PDCCH
  * (pdcch.c:79,341). With AVX2 viterbi.c defines VITERBI_16 (:46-50), so decode_f quantises to

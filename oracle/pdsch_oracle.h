@@ -23,6 +23,9 @@ int orc_csi_correction(int mod, const float *csi, int nsym, int16_t *e);
 int orc_predecode_txdiv(const float *y0, const float *y1, const float *h00, const float *h01,
                         const float *h10, const float *h11, int nrx, int n, float scaling, float *d,
                         float *csi);
+/* TM2 transmit diversity, 4 ports (n % 4 == 0): y [rx], h [port * 2 + rx] */
+int orc_predecode_txdiv4(const float *const *y, const float *const *h, int nrx, int n, float scaling, float *d,
+                         float *csi);
 /* PDCCH Viterbi: srslte_viterbi_decode_f, tail-biting K=7 r=1/3, F bits out (one per byte) */
 int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out);
 /* one DCI candidate as srslte_pdcch_decode_msg: 1 decoded (data: nof_bits + 16 bits), 0 skipped */

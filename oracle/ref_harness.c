@@ -665,6 +665,41 @@ int ref_predecode_txdiv(const float *y0, const float *y1, const float *h00, cons
   return r < 0 ? -1 : 0;
 }
 
+/* the same with 4 ports and 4 layers; y [rx], h [port * 2 + rx]; n % 4 == 0 */
+int ref_predecode_txdiv4(const float *const *ys, const float *const *hs, int nrx, int n, float scaling, float *d,
+                         float *csi) {
+  cf_t *y[SRSLTE_MAX_PORTS] = {NULL}, *h[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  cf_t *x[SRSLTE_MAX_LAYERS] = {NULL}, *dd = NULL;
+  float *c[SRSLTE_MAX_CODEWORDS] = {NULL};
+  if (n % 4) return -1;
+  for (int a = 0; a < nrx; a++) {
+    if (posix_memalign((void **)&y[a], 64, (n + 16) * sizeof(cf_t))) return -1;
+    memcpy(y[a], ys[a], n * sizeof(cf_t));
+    for (int p = 0; p < 4; p++) {
+      if (posix_memalign((void **)&h[p][a], 64, (n + 16) * sizeof(cf_t))) return -1;
+      memcpy(h[p][a], hs[p * 2 + a], n * sizeof(cf_t));
+    }
+  }
+  for (int l = 0; l < 4; l++)
+    if (posix_memalign((void **)&x[l], 64, (n + 16) * sizeof(cf_t))) return -1;
+  if (posix_memalign((void **)&dd, 64, (n + 16) * sizeof(cf_t))) return -1;
+  if (csi && posix_memalign((void **)&c[0], 64, (n + 16) * sizeof(float))) return -1;
+  int r = srslte_predecoding_type(y, h, x, c, nrx, 4, 4, 0, n, SRSLTE_MIMO_TYPE_TX_DIVERSITY, scaling, 0.0f);
+  int nsym[SRSLTE_MAX_CODEWORDS] = {0};
+  cf_t *dp[SRSLTE_MAX_CODEWORDS] = {dd, NULL};
+  if (r >= 0) r = srslte_layerdemap_type(x, dp, 4, 1, n / 4, nsym, SRSLTE_MIMO_TYPE_TX_DIVERSITY);
+  memcpy(d, dd, n * sizeof(cf_t));
+  if (csi) memcpy(csi, c[0], n * sizeof(float));
+  for (int a = 0; a < nrx; a++) {
+    free(y[a]);
+    for (int p = 0; p < 4; p++) free(h[p][a]);
+  }
+  for (int l = 0; l < 4; l++) free(x[l]);
+  free(dd);
+  free(c[0]);
+  return r < 0 ? -1 : 0;
+}
+
 /* ---------------------------------------------------------------- Viterbi (PDCCH) ---------- */
 #include "srslte/phy/fec/viterbi.h"
 /* srslte_viterbi_decode_f on a tail-biting K=7 r=1/3 decoder (pdcch.c:79,341: poly {0x6D, 0x4F,

@@ -698,9 +698,24 @@ class Llr8:
 
 # ------------------------------------------------------------------ TM2 transmit diversity ----
 def predecode_txdiv(lib, y, h, scaling=1.0, csi=False, ref=False):
-    """srslte_predecoding_diversity_multi (2 ports) + srslte_layerdemap_diversity: y [nrx][n],
-    h [2 ports][nrx][n] -> d [n] (+ csi [n]); lib: the oracle (orc_) or the reference (ref_)"""
+    """srslte_predecoding_diversity_multi (2 or 4 ports) + srslte_layerdemap_diversity: y [nrx][n],
+    h [ports][nrx][n] -> d [n] (+ csi [n]); lib: the oracle (orc_) or the reference (ref_)"""
     L = lib.lib if hasattr(lib, "lib") else lib
+    if len(h) == 4:
+        f = getattr(L, "ref_predecode_txdiv4" if ref else "orc_predecode_txdiv4")
+        f.argtypes = [ctypes.POINTER(_f32p), ctypes.POINTER(_f32p), ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                      _f32p, _f32p]
+        nrx = len(y)
+        ys = [np.ascontiguousarray(v, np.complex64) for v in y]
+        hs = [np.ascontiguousarray(h[p][a], np.complex64) if a < nrx else None for p in range(4) for a in (0, 1)]
+        n = ys[0].size
+        d = np.zeros(n, np.complex64)
+        c = np.zeros(n, np.float32) if csi else None
+        P = lambda a: a.ctypes.data_as(_f32p) if a is not None else None
+        ya = (_f32p * 2)(*[P(v) for v in ys + [None] * (2 - nrx)])
+        ha = (_f32p * 8)(*[P(v) for v in hs])
+        assert f(ya, ha, nrx, n, scaling, P(d), P(c)) == 0
+        return (d, c) if csi else d
     f = getattr(L, "ref_predecode_txdiv" if ref else "orc_predecode_txdiv")
     f.argtypes = [_f32p] * 6 + [ctypes.c_int, ctypes.c_int, ctypes.c_float, _f32p, _f32p]
     nrx = len(y)

@@ -22,13 +22,13 @@ def gold():
 
 def _case(z, c):
     y = [z[c["key"] + "_y%d" % a] for a in range(c["nrx"])]
-    h = [[z[c["key"] + "_h%d%d" % (p, a)] for a in range(c["nrx"])] for p in range(2)]
+    h = [[z[c["key"] + "_h%d%d" % (p, a)] for a in range(c["nrx"])] for p in range(c.get("ports", 2))]
     return y, h
 
 
 def test_golden_txdiv(oracle, gold):
     z, man = gold
-    assert len(man) == 24
+    assert len(man) == 24 + 16
     for c in man:
         y, h = _case(z, c)
         out = predecode_txdiv(oracle, y, h, c["scaling"], c["csi"])
@@ -36,6 +36,25 @@ def test_golden_txdiv(oracle, gold):
         assert (d.view(np.uint64) == z[c["key"] + "_d"].view(np.uint64)).all(), c["key"]
         if c["csi"]:
             assert (out[1] == z[c["key"] + "_csi"]).all(), c["key"]
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
+def test_random_txdiv4_vs_reference(oracle):
+    """4 ports: RE quadruplets on ports 0/2 and 1/3 (precoding.c:388-423, 604-662)"""
+    ref = Ref()
+    rng = np.random.default_rng(44)
+    for n in (8, 32, 40, 404):
+        for nrx in (1, 2):
+            for csi in (False, True):
+                y = [(rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64) for _ in range(nrx)]
+                h = [[(rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+                      for _ in range(nrx)] for _ in range(4)]
+                a = predecode_txdiv(oracle, y, h, 0.9, csi)
+                b = predecode_txdiv(ref, y, h, 0.9, csi, ref=True)
+                if csi:
+                    assert (a[0].view(np.uint64) == b[0].view(np.uint64)).all() and (a[1] == b[1]).all()
+                else:
+                    assert (a.view(np.uint64) == b.view(np.uint64)).all()
 
 
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built")
