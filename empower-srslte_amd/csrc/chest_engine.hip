@@ -13,16 +13,17 @@
 
 namespace srsgpu {
 
-// CRS of ports 0/1, normal CP (refsignal_dl.c:265-318, 36.211 6.10.1.1): for slot ns and OFDM
-// symbol lp in {0, 4}, c_init = 2^10 (7(ns+1) + lp + 1)(2 N_ID + 1) + 2 N_ID + 1 and
-// r(m) = ((1 - 2c(2m')) + j(1 - 2c(2m'+1))) / sqrt(2), m' = m + 110 - nof_prb.
+// CRS, normal CP (refsignal_dl.c:265-318, 36.211 6.10.1.1): for slot ns and OFDM symbol lp in
+// {0, 4} (ports 0/1) or {1} (ports 2/3), c_init = 2^10 (7(ns+1) + lp + 1)(2 N_ID + 1) + 2 N_ID + 1
+// and r(m) = ((1 - 2c(2m')) + j(1 - 2c(2m'+1))) / sqrt(2), m' = m + 110 - nof_prb.
+// Layout: [10 subframes][4 symbols][2 nof_prb] of ports 0/1, then [10][2][2 nof_prb] of ports 2/3.
 static void crs_table(uint32_t nprb, uint32_t id, std::vector<float> &t) {
   const uint32_t np = 2 * nprb, len = 4 * 110, Nc = 1600;
-  t.assign((size_t)10 * 4 * np * 2, 0.f);
+  t.assign((size_t)10 * 6 * np * 2, 0.f);
   std::vector<uint8_t> x1(Nc + len + 31), x2(Nc + len + 31);
   for (uint32_t ns = 0; ns < 20; ns++)
-    for (uint32_t l = 0; l < 2; l++) {
-      const uint32_t lp = l ? 4 : 0;
+    for (uint32_t l = 0; l < 3; l++) {
+      const uint32_t lp = l == 0 ? 0 : l == 1 ? 4 : 1;
       const uint32_t cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * id + 1) + 2 * id + 1;
       std::fill(x1.begin(), x1.end(), 0);
       std::fill(x2.begin(), x2.end(), 0);
@@ -32,12 +33,13 @@ static void crs_table(uint32_t nprb, uint32_t id, std::vector<float> &t) {
         x1[n + 31] = (x1[n + 3] + x1[n]) & 1;
         x2[n + 31] = (x2[n + 3] + x2[n + 2] + x2[n + 1] + x2[n]) & 1;
       }
-      const uint32_t sf = ns / 2, sym = (ns % 2) * 2 + l;
+      const uint32_t sf = ns / 2;
+      const size_t row = l < 2 ? (size_t)sf * 4 + (ns % 2) * 2 + l : 40 + (size_t)sf * 2 + ns % 2;
       for (uint32_t m = 0; m < np; m++) {
         const uint32_t mp = m + 110 - nprb;
         const uint8_t c0 = (x1[2 * mp + Nc] + x2[2 * mp + Nc]) & 1;
         const uint8_t c1 = (x1[2 * mp + 1 + Nc] + x2[2 * mp + 1 + Nc]) & 1;
-        const size_t o = (((size_t)sf * 4 + sym) * np + m) * 2;
+        const size_t o = (row * np + m) * 2;
         t[o] = (float)((1 - 2 * (float)c0) / sqrt(2));
         t[o + 1] = (float)((1 - 2 * (float)c1) / sqrt(2));
       }
@@ -60,8 +62,8 @@ struct ChestEngine {
   bool staged_pending = false;
 
   int create(const srsgpu_cell_t &c, uint32_t n) {
-    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || c.nof_ports < 1 || c.nof_ports > 2) {
-      fprintf(stderr, "srsgpu: invalid cell for channel estimation (1 or 2 CRS ports)\n");
+    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4)) {
+      fprintf(stderr, "srsgpu: invalid cell for channel estimation (1, 2 or 4 CRS ports)\n");
       return -1;
     }
     cell = c;
@@ -104,6 +106,10 @@ struct ChestEngine {
                float *d_noise, float *d_meas) {
     if (n > cap) {
       fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
+      return -1;
+    }
+    if (ce_rows && cell.nof_ports > 2) { // the compact rows are the 4-symbol (ports 0/1) layout
+      fprintf(stderr, "srsgpu: compact estimate rows need a 1- or 2-port cell\n");
       return -1;
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));

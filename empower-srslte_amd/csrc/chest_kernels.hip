@@ -1,9 +1,10 @@
-// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0 and 1) for
+// MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0-3) for
 // normal-CP, non-MBSFN subframes, in every configuration srsUE's phch_worker sets
 // (srsue/src/phy/phch_worker.cc:149,553-565; reference: lib/src/phy/ch_estimation/chest_dl.c:641-694
 // and the helpers it calls):
-//   1. least squares   pilots received at the CRS REs of symbols 0/4/7/11 (refsignal_cs_get_sf,
-//                      refsignal_dl.c:404-430) times conj(CRS) (refsignal_dl.c:265-318)
+//   1. least squares   pilots received at the CRS REs of symbols 0/4/7/11 (ports 0/1) or 1/8 (ports
+//                      2/3) (refsignal_cs_get_sf, refsignal_dl.c:404-430) times conj(CRS)
+//                      (refsignal_dl.c:265-318)
 //   2. measurements    RSRP, RSSI (chest_dl.c:500-511), RSRP correlation (:652-656), CFO (:562-587)
 //   3. noise (REFS)    estimate_noise_pilots (chest_dl.c:268-329), including its reference behaviour
 //                      of keeping only the last symbol's residual power
@@ -14,7 +15,7 @@
 //                      (convolution.c:172-211)
 //   6. frequency       srslte_interp_linear_offset (interp.c:245-272): per CRS symbol with M = 6, or
 //                      the averaged row with M = 3 and offset cell_id % 3 (chest_dl.c:393-399)
-//   7. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:416-421,
+//   7. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:421-431,
 //                      interp.c:150-173), or the averaged row copied to all 14 symbols (:410-414)
 //   8. noise (PSS/EMPTY) in subframes 0 and 5 only (chest_dl.c:628-637, 332-361)
 // One workgroup per (subframe, rx antenna, port): pilots and their smoothed copy stay in LDS, each
@@ -140,22 +141,24 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   }
   const int kb = (nsc * part) / nparts, ke = (nsc * (part + 1)) / nparts;
   const c32 *grid = (const c32 *)t.grid;
-  const c32 *pil = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);
-  const int sym[4] = {0, 4, 7, 11};
   const int port = (int)t.port;
+  // ports 0/1: CRS symbols 0, 4, 7, 11; ports 2/3: 1 and 8 (refsignal_dl.c:76-85, 112-122), their
+  // pilots (csr_refs.pilots[port / 2]) after the 10 x 4 rows of ports 0/1 in the table
+  const int nsym = port < 2 ? 4 : 2;
+  const c32 *pil = (const c32 *)(port < 2 ? crs + (size_t)t.sf_idx * 4 * np : crs + (size_t)(40 + 2 * t.sf_idx) * np);
+  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? 4 : 8, 7, 11};
   const int tid = threadIdx.x;
-  auto fidx = [&](int l) { return (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6; };
-  // 1. LS: v = 0 / 3 alternating over the CRS symbols (port 1: 3 / 0), fidx = (v + id % 6) % 6;
-  //    ports 0 and 1 share the pilot sequence (csr_refs.pilots[port / 2])
-  //    Every load of the thread (at most 4 pilots: 4 np <= 880 < 4 x 256) issued before the
-  //    first product: one memory round trip instead of four in a row
+  // v = 0 / 3 alternating over the CRS symbols, ports 1 / 3 starting at 3 (refsignal_dl.c:40-74)
+  auto fidx = [&](int l) { return (((l & 1) ^ (port & 1) ? 3 : 0) + cell_id % 6) % 6; };
+  // 1. LS: fidx = (v + id % 6) % 6. Every load of the thread (at most 4 pilots: 4 np <= 880 <
+  //    4 x 256) issued before the first product: one memory round trip instead of four in a row
   {
     constexpr int PPT = (4 * CH_MAXP + 255) / 256;
     c32 g[PPT], c[PPT];
 #pragma unroll
     for (int u = 0; u < PPT; u++) {
       const int e = tid + 256 * u;
-      if (e < 4 * np) {
+      if (e < nsym * np) {
         const int l = e / np, m = e % np;
         g[u] = grid[sym[l] * nsc + fidx(l) + 6 * m];
         c[u] = pil[e];
@@ -164,7 +167,18 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
 #pragma unroll
     for (int u = 0; u < PPT; u++) {
       const int e = tid + 256 * u;
-      if (e < 4 * np) ls[e] = cmulconj(g[u], c[u]);
+      if (e < nsym * np) ls[e] = cmulconj(g[u], c[u]);
+    }
+  }
+  // the CFO of ports 2 / 3 (chest_estimate_cfo, chest_dl.c:583-603) reads rows 2 and 3 of the
+  // shared pilot buffer, which still hold port 1's estimates of symbols 7 and 11 for this rx
+  // antenna (estimate_multi runs the ports in order): they are recomputed into ls rows 2-3
+  if (nsym == 2 && t.cfo) {
+    const c32 *pil01 = (const c32 *)(crs + (size_t)t.sf_idx * 4 * np);
+    for (int e = 2 * np + tid; e < 4 * np; e += blockDim.x) {
+      const int l = e / np, m = e % np;
+      const int f1 = (((l & 1) ^ 1 ? 3 : 0) + cell_id % 6) % 6; // port 1
+      ls[e] = cmulconj(grid[(l == 2 ? 7 : 11) * nsc + f1 + 6 * m], pil01[e]);
     }
   }
   __syncthreads();
@@ -172,31 +186,34 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   const bool refs = cfg.noise_alg == 0 && (t.noise || cfg.filt_auto);
   if (refs || t.meas) {
     float v[CH_NRED] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (refs) { // residual of the last CRS symbol against its staggered neighbours (bottom one
-                // extrapolated as 2 ls[2] - ls[0]), power / 4 * sqrt(5)
-      const int off = fidx(0) < 3 ? 0 : 1; // ((fidx < 3) ^ (4 & 1)) ? 0 : 1
-      const c32 *r0 = ls, *r2 = ls + 2 * np, *r3 = ls + 3 * np;
+    if (refs) { // residual of the last CRS symbol against its staggered neighbours: 4 symbols,
+                // ls[2] and the extrapolated 2 ls[2] - ls[0]; 2 symbols, ls[0] on both sides
+                // (chest_dl.c:285-299); power / nsymbols * sqrt(5)
+      const int off = fidx(0) < 3 ? 0 : 1; // ((fidx < 3) ^ (nsymbols & 1)) ? 0 : 1
+      const c32 *r0 = ls, *rp = ls + (nsym - 2) * np, *rl = ls + (nsym - 1) * np;
       for (int k = tid; k < np; k += blockDim.x) {
-        c32 tmp = r3[k];
+        c32 tmp = rl[k];
         for (int nb = 0; nb < 2; nb++) {
-          auto row = [&](int q) -> c32 { return nb == 0 ? r2[q] : csub(cscale(r2[q], 2.0f), r0[q]); };
+          auto row = [&](int q) -> c32 {
+            return nb == 0 || nsym == 2 ? rp[q] : csub(cscale(rp[q], 2.0f), r0[q]);
+          };
           if (k >= off) tmp = cadd(tmp, row(k - off));            // tmp[off + t] += prev[t]
           if (k < np + off - 1) tmp = cadd(tmp, row(1 - off + k)); // tmp[t] += prev[1 - off + t]
           if (off && k == 0) tmp = cadd(tmp, csub(cscale(row(0), 2.0f), row(1)));
           if (!off && k == np - 1) tmp = cadd(tmp, csub(cscale(row(np - 2), 2.0f), row(np - 1)));
         }
         tmp = cscale(tmp, 1.0f / 5.0f);
-        v[0] += cpow(csub(r3[k], tmp));
+        v[0] += cpow(csub(rl[k], tmp));
       }
     }
     if (t.meas) {
-      for (int e = tid; e < 4 * np; e += blockDim.x) {
+      for (int e = tid; e < nsym * np; e += blockDim.x) {
         const int l = e / np, m = e % np;
         v[1] += cpow(grid[sym[l] * nsc + fidx(l) + 6 * m]); // pilot_recv_signal power
         v[3] += ls[e].x;
         v[4] += ls[e].y;
       }
-      for (int e = tid; e < 4 * nsc; e += blockDim.x) v[2] += cpow(grid[sym[e / nsc] * nsc + e % nsc]);
+      for (int e = tid; e < nsym * nsc; e += blockDim.x) v[2] += cpow(grid[sym[e / nsc] * nsc + e % nsc]);
       for (int e = tid; e < 2 * np; e += blockDim.x) { // slot 0 against slot 1, per CRS symbol
         const c32 p = cmulconj(ls[e], ls[e + 2 * np]);
         v[5] += p.x;
@@ -206,13 +223,13 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
     block_sum<CH_NRED>(red, v);
     if (tid == 0) {
       if (refs) {
-        s_noise = red[0][0] / (float)np / 4.0f * sqrtf(5.0f);
+        s_noise = red[0][0] / (float)np / (float)nsym * sqrtf(5.0f);
         if (t.noise && part == 0) *t.noise = s_noise;
       }
       if (t.meas) {
-        const float npil = (float)(4 * np);
+        const float npil = (float)(nsym * np);
         t.meas[0] = red[1][0] / npil;
-        t.meas[1] = red[2][0] / 4.0f;
+        t.meas[1] = red[2][0] / (float)nsym;
         if (cfg.rsrp_neighbour) {
           const double e = hypot((double)(red[3][0] / npil), (double)(red[4][0] / npil));
           t.meas[2] = (float)(e * e);
@@ -245,18 +262,23 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   // 5. averaging / smoothing; rows: what the frequency interpolation reads
   const c32 *rows = ls;
   if (cfg.average) {
-    if (fl) { // average_pilots: interleave the slot pairs, scale 2 / 4, then smooth the 2np row
+    if (fl) { // average_pilots: interleave the slot pairs, scale 2 / nsymbols, then smooth the 2np row
       const int a = fidx(0) < 3 ? 0 : 1, b = 1 - a;
       for (int m = tid; m < np; m += blockDim.x) {
-        sm[2 * m] = cscale(cadd(ls[a * np + m], ls[(a + 2) * np + m]), 0.5f);
-        sm[2 * m + 1] = cscale(cadd(ls[b * np + m], ls[(b + 2) * np + m]), 0.5f);
+        if (nsym == 4) {
+          sm[2 * m] = cscale(cadd(ls[a * np + m], ls[(a + 2) * np + m]), 0.5f);
+          sm[2 * m + 1] = cscale(cadd(ls[b * np + m], ls[(b + 2) * np + m]), 0.5f);
+        } else {
+          sm[2 * m] = ls[a * np + m]; // x (2 / 2)
+          sm[2 * m + 1] = ls[b * np + m];
+        }
       }
       __syncthreads();
       for (int i = tid; i < 2 * np; i += blockDim.x) ls[i] = conv_same_at(sm, 2 * np, i, fs, fl);
       __syncthreads();
     } // no smoothing: the raw buffer (symbols 0 and 4 back to back) is interpolated as the row
   } else if (fl) {
-    for (int e = tid; e < 4 * np; e += blockDim.x) {
+    for (int e = tid; e < nsym * np; e += blockDim.x) {
       const int l = e / np;
       sm[e] = conv_same_at(ls + l * np, np, e - l * np, fs, fl);
     }
@@ -277,6 +299,20 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
       else
         for (int s = 0; s < 14; s++) ce[s * nsc + k] = v;
       c6 = v;
+    } else if (nsym == 2) { // ports 2 / 3 (chest_dl.c:428-430): symbol 0 extrapolated back from 1 with
+                            // (c1 - c8) / 7; 2-7 forward from 1 with (c8 - c1) / 7; 9-13 forward from
+                            // symbol 1 again (the reference's in0 for that segment), i.e. 2-6 repeated
+      const c32 f0 = interp_at(rows, np, k, fidx(0), 6, 1.0f / 6), f1 = interp_at(rows + np, np, k, fidx(1), 6, 1.0f / 6);
+      c32 col[14];
+      col[1] = f0;
+      col[8] = f1;
+      col[0] = cadd(f0, cscale(csub(f0, f1), 1.0f / 7.0f));
+      const c32 d = cscale(csub(f1, f0), 1.0f / 7.0f);
+      col[2] = cadd(f0, d);
+      for (int s = 3; s < 8; s++) col[s] = cadd(col[s - 1], d);
+      for (int s = 9; s < 14; s++) col[s] = col[s - 7];
+      for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
+      c6 = col[6];
     } else {
       c32 f[4];
       for (int l = 0; l < 4; l++) f[l] = interp_at(rows + l * np, np, k, fidx(l), 6, 1.0f / 6);
@@ -335,20 +371,20 @@ hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, co
   return hipGetLastError();
 }
 
-// srslte_refsignal_cs_put_sf (refsignal_dl.c:380-402): the CRS of a port into its grid plane at
-// symbols 0/4/7/11, subcarriers fidx + 6m
+// srslte_refsignal_cs_put_sf (refsignal_dl.c:338-360): the CRS of a port into its grid plane at
+// symbols 0/4/7/11 (ports 0/1) or 1/8 (ports 2/3), subcarriers fidx + 6m
 __global__ __launch_bounds__(256) void k_crs_put(const ChestItem *__restrict__ items, int nitems, int nprb,
                                                  int cell_id, const float2 *__restrict__ crs) {
   const int it = blockIdx.x;
   if (it >= nitems) return;
   const ChestItem t = items[it];
-  const int np = 2 * nprb, nsc = 12 * nprb, port = (int)t.port;
-  const int sym[4] = {0, 4, 7, 11};
-  const float2 *pil = crs + (size_t)t.sf_idx * 4 * np;
+  const int np = 2 * nprb, nsc = 12 * nprb, port = (int)t.port, nsym = port < 2 ? 4 : 2;
+  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? 4 : 8, 7, 11};
+  const float2 *pil = port < 2 ? crs + (size_t)t.sf_idx * 4 * np : crs + (size_t)(40 + 2 * t.sf_idx) * np;
   float2 *g = t.ce; // the grid plane written
-  for (int e = threadIdx.x; e < 4 * np; e += blockDim.x) {
+  for (int e = threadIdx.x; e < nsym * np; e += blockDim.x) {
     const int l = e / np, m = e % np;
-    const int f = (((l & 1) ^ port ? 3 : 0) + cell_id % 6) % 6;
+    const int f = (((l & 1) ^ (port & 1) ? 3 : 0) + cell_id % 6) % 6;
     g[sym[l] * nsc + f + 6 * m] = pil[l * np + m];
   }
 }

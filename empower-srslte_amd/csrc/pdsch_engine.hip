@@ -212,6 +212,16 @@ struct PdschEngine {
     return s.mimo_type == SRSGPU_MIMO_CDD || (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.tbs[1] > 0) ? 2 : 1;
   }
 
+  // 4-port transmit diversity demaps 4 floor(n / 4) symbols (srslte_pdsch_decode's n / nof_layers,
+  // pdsch.c:908, and m_ap of precoding.c:391 / :605); the reference would read any remaining symbol
+  // from whatever its layer buffer last held. Normal-CP grants of a 4-port cell always hold whole
+  // quadruplets (tests/test_txdiv.py), so this only guards the layout assumption.
+  int txdiv4_ragged(const srsgpu_pdsch_sf_t &s, uint32_t nre) const {
+    if (s.mimo_type != SRSGPU_MIMO_TX_DIVERSITY || cell.nof_ports != 4 || nre % 4 == 0) return 0;
+    fprintf(stderr, "srsgpu: 4-port transmit diversity needs a multiple of 4 REs (grant has %u)\n", nre);
+    return -1;
+  }
+
   int check(const srsgpu_pdsch_sf_t &s, uint32_t i) {
     const uint32_t nt = nof_tb(s);
     bool ok = s.sf_idx <= 9 && s.lstart <= 4;
@@ -226,9 +236,9 @@ struct PdschEngine {
         fprintf(stderr, "srsgpu: single-antenna PDSCH needs a 1-port cell\n");
         return -1;
       }
-    } else if (s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY) { // precoding.c:1811-1818, 2 ports
-      if (cell.nof_ports != 2) {
-        fprintf(stderr, "srsgpu: transmit diversity on the GPU needs a 2-port cell\n");
+    } else if (s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY) { // precoding.c:1811-1818, 2 or 4 ports
+      if (cell.nof_ports != 2 && cell.nof_ports != 4) {
+        fprintf(stderr, "Number of ports must be 2 or 4 for transmit diversity (nof_ports=%d)\n", cell.nof_ports);
         return -1;
       }
     } else if (s.mimo_type == SRSGPU_MIMO_CDD) { // precoding.c:1085-1097
@@ -275,6 +285,7 @@ struct PdschEngine {
         fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
         return -1;
       }
+      if (txdiv4_ragged(s, nre)) return -1;
       const uint32_t nt = nof_tb(s);
       for (uint32_t tb = 0; tb < nt; tb++, k++) {
         const uint32_t cw = nt == 2 ? (tb ^ (s.tb_cw_swap ? 1u : 0u)) : 0u;
@@ -286,7 +297,7 @@ struct PdschEngine {
         memset(&t, 0, sizeof(t));
         for (uint32_t a = 0; a < cell.nof_rx_ant; a++) {
           t.y[a] = (const float2 *)d_grid + s.grid_offset + a * ant_stride;
-          for (uint32_t p = 0; p < cell.nof_ports && p < 2; p++)
+          for (uint32_t p = 0; p < cell.nof_ports; p++)
             t.h[p][a] = (const float2 *)d_ce + s.ce_offset + (a * cell.nof_ports + p) * ant_stride;
         }
         t.map = m;
@@ -302,7 +313,7 @@ struct PdschEngine {
         t.cdd = s.mimo_type == SRSGPU_MIMO_CDD;
         if (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX)
           t.mux = nt == 2 ? 1 + (int)s.codebook_idx : -(1 + (int)s.codebook_idx);
-        t.txdiv = s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY;
+        t.txdiv = s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY ? (int)cell.nof_ports : 0;
         t.layer = (int)cw;
         t.csi_mode = csi ? 1 : 0;
         t.llr8 = llr8 ? 1 : 0;
@@ -393,6 +404,7 @@ struct PdschEngine {
         fprintf(stderr, "Error expecting %d symbols but got %d\n", s.nof_re, nre);
         return -1;
       }
+      if (txdiv4_ragged(s, nre)) return -1;
       const uint32_t ntb = nof_tb(s);
       const float sc = s.scaling != 0.f ? s.scaling : 1.0f;
       TxItem &x = h_tx[i];

@@ -18,7 +18,7 @@ struct GoldItem {
 // one transport block: gather + equalise + demap + descramble (+ CSI)
 struct LlrItem {
   const float2 *y[2];      // received grid of each rx antenna
-  const float2 *h[2][2];   // channel estimate [port][rx antenna], same layout
+  const float2 *h[4][2];   // channel estimate [port][rx antenna], same layout
   const uint32_t *map;     // RE j -> grid position
   const uint32_t *c;       // packed scrambling bits
   int16_t *e;              // LLRs out (nof_re * qm)
@@ -29,7 +29,8 @@ struct LlrItem {
   int cdd, layer;          // TM3 CDD 2x2 MMSE: this TB's codeword / layer (0 or 1)
   int mux;                 // TM4 spatial multiplexing: 1 + codebook_idx (2 layers: 2x2 MMSE) or
                            // -(1 + codebook_idx) (1 layer: 2x1 MRC); 0 otherwise
-  int txdiv;               // TM2 transmit diversity, 2 ports (SFBC over RE pairs), 1-2 rx
+  int txdiv;               // TM2 transmit diversity: 2 (SFBC over RE pairs) or 4 ports (RE
+                           // quadruplets, port pairs 0/2 and 1/3); 0 otherwise; 1-2 rx
   int aligned;             // e is 4-byte aligned: LLR pairs stored as 32-bit words
   float noise, inv_scaling, scaling;
   const float *noise_dev;  // if set: chest noise [rx][port] averaged as chest_dl.c:741-750 does

@@ -364,6 +364,60 @@ __device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
   return e;
 }
 
+// TM2 transmit diversity, 4 ports (srslte_predecoding_diversity_multi with nof_ports == 4,
+// precoding.c:388-423 / 604-662, then srslte_layerdemap_diversity over 4 layers): symbol j is x_k
+// (k = j mod 4) of RE quadruplet i = j / 4; x0 / x1 come from ports 0 and 2 on REs 4i, 4i+1 and
+// x2 / x3 from ports 1 and 3 on REs 4i+2, 4i+3. Without CSI (the generic C form, no SSE variant
+// for 4 ports): the pair's channels read at its first RE, gains summed over rx antennas with no
+// zero guard, float complex products, x / (hh scaling) * sqrt(2) in double. With CSI: per-symbol
+// gains (x0: h[p][4i] and h[p+2][4i+1]; x1: h[p][4i+1] and h[p+2][4i]), csi = a scaling / nof_rx,
+// x / (a scaling) * sqrtf(2) in float. The host refuses nof_re % 4 != 0 (the reference leaves
+// those symbols to whatever its buffer held).
+__device__ __forceinline__ Eq equalise_txdiv4(const LlrItem &t, uint32_t j) {
+  const uint32_t k = j & 3, q = k >> 1, b = (j & ~3u) + 2 * q;
+  const uint32_t p0 = t.map[b], p1 = t.map[b + 1];
+  const bool odd = k & 1;
+  cf x = {0.f, 0.f};
+  float g = 0.f;
+  Eq e;
+  for (int a = 0; a < 2; a++) {
+    if (a == 1 && t.nrx < 2) break;
+    const cf r0 = c_ld(t.y[a], p0), r1 = c_ld(t.y[a], p1);
+    const cf hA = ce_ld(t, t.h[q][a], p0), hB = ce_ld(t, t.h[q + 2][a], t.csi_mode && !odd ? p1 : p0);
+    cf u;
+    if (!t.csi_mode) { // hA = h[q][4i+2q], hB = h[q+2][4i+2q]
+      g = __fadd_rn(g, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(hA.r, hA.r), __fmul_rn(hA.i, hA.i)),
+                                           __fmul_rn(hB.r, hB.r)),
+                                 __fmul_rn(hB.i, hB.i)));
+      u = odd ? c_add(c_mul(c_neg(hB), c_conj(r0)), c_mul(c_conj(hA), r1))
+              : c_add(c_mul(c_conj(hA), r0), c_mul(hB, c_conj(r1)));
+    } else if (!odd) { // h00 = h[q][b] (hA), h11 = h[q+2][b+1] (hB)
+      g = __fadd_rn(g, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(hA.r, hA.r), __fmul_rn(hA.i, hA.i)),
+                                           __fmul_rn(hB.r, hB.r)),
+                                 __fmul_rn(hB.i, hB.i)));
+      u = c_add(c_mul(c_conj(hA), r0), c_mul(hB, c_conj(r1)));
+    } else { // h10 = h[q][b+1], h01 = h[q+2][b] (hB)
+      const cf h10 = ce_ld(t, t.h[q][a], p1);
+      g = __fadd_rn(g, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h10.r, h10.r), __fmul_rn(h10.i, h10.i)),
+                                           __fmul_rn(hB.r, hB.r)),
+                                 __fmul_rn(hB.i, hB.i)));
+      u = c_add(c_mul(c_neg(hB), c_conj(r0)), c_mul(c_conj(h10), r1));
+    }
+    x = c_add(x, u);
+  }
+  const float gs = __fmul_rn(g, t.scaling);
+  if (t.csi_mode) {
+    e.csi = __fdiv_rn(gs, (float)t.nrx);
+    e.xr = __fmul_rn(__fdiv_rn(x.r, gs), 1.41421354f);
+    e.xi = __fmul_rn(__fdiv_rn(x.i, gs), 1.41421354f);
+  } else {
+    e.csi = g;
+    e.xr = (float)__dmul_rn((double)__fdiv_rn(x.r, gs), 1.4142135623730951);
+    e.xi = (float)__dmul_rn((double)__fdiv_rn(x.i, gs), 1.4142135623730951);
+  }
+  return e;
+}
+
 // LLRs of symbol j (q per symbol) into out[0..q)
 __device__ __forceinline__ void demap(int mod, uint32_t j, uint32_t n, float xr, float xi,
                                       int16_t *o) {
@@ -530,7 +584,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
   if (t.txdiv) {
     for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += stride) {
       const uint32_t w = (j * Q) >> 5;
-      llr_out<MOD>(t, j, equalise_txdiv(t, j), t.c[w], t.c[w + 1]);
+      llr_out<MOD>(t, j, t.txdiv == 4 ? equalise_txdiv4(t, j) : equalise_txdiv(t, j), t.c[w], t.c[w + 1]);
     }
     return;
   }
@@ -606,8 +660,7 @@ __device__ __forceinline__ void llr_body_dual(const LlrItem &t, const LlrItem &t
 __device__ __forceinline__ void llr_item_fix(LlrItem &u) {
   for (int a = 0; a < 2; a++) {
     u.y[a] = gmem(u.y[a]);
-    u.h[0][a] = gmem(u.h[0][a]);
-    u.h[1][a] = gmem(u.h[1][a]);
+    for (int p = 0; p < 4; p++) u.h[p][a] = gmem(u.h[p][a]);
   }
   u.map = gmem(u.map);
   u.c = gmem(u.c);
@@ -764,6 +817,19 @@ __global__ __launch_bounds__(256) void k_pdsch_tx(const TxItem *__restrict__ ite
     bool two = true;
     switch (t.mimo) {
     case SRSGPU_MIMO_TX_DIVERSITY: { // layermap_diversity + 2-port SFBC, scaled by rho_a / sqrt 2
+      if (t.nlayers == 4) { // 4 ports (precoding.c:1863-1889): RE 4i+2q+r on ports q and q+2,
+                            // the other two ports 0; 4 floor(n / 4) symbols per port
+        const uint32_t j0 = j & ~3u, q = (j >> 1) & 1;
+        if (j0 + 3 >= t.nof_re) continue;
+        const float2 a = tx_symbol(t, 0, j0 + 2 * q, tables), b = tx_symbol(t, 0, j0 + 2 * q + 1, tables);
+        const float k = t.scaling; // scaling / sqrtf(2) on the host
+        const float2 ya = (j & 1) ? cscale(b, k) : cscale(a, k);
+        const float2 yb = (j & 1) ? cscale(make_float2(a.x, -a.y), k) : cscale(make_float2(-b.x, b.y), k);
+        const uint32_t m = t.map[j];
+        for (uint32_t p = 0; p < 4; p++)
+          t.grid[p * t.port_stride + m] = p == q ? ya : p == q + 2 ? yb : make_float2(0.f, 0.f);
+        continue;
+      }
       const uint32_t j0 = j & ~1u;
       if (j0 + 1 >= t.nof_re) continue; // 2 floor(n / 2) symbols per port (precoding.c:1853-1862)
       const float2 a = tx_symbol(t, 0, j0, tables), b = tx_symbol(t, 0, j0 + 1, tables);

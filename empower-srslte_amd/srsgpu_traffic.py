@@ -227,7 +227,8 @@ class MimoSubframes:
     handles (a rank's shard); subframe i's content depends only on i."""
 
     def __init__(self, torch, dev, n_sf, seed=31, stream=None, snr_db=30.0, mimo=None, mcs=28, nof_prb=100,
-                 cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True, ce_rows=True):
+                 cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True, ce_rows=True,
+                 nof_ports=2):
         import ctypes as ct
         self.torch, self.dev, self.max_halfits = torch, dev, max_halfits
         mimo = s.MIMO_CDD if mimo is None else mimo
@@ -240,12 +241,14 @@ class MimoSubframes:
         self.gsz = gsz
         ntb = 1 if mimo == s.MIMO_TX_DIVERSITY else nof_tb
         self.ntb = ntb
+        P = self.nports = nof_ports  # 4: transmit diversity over ports 0-3 (estimates in full grids)
+        assert P == 2 or (P == 4 and mimo == s.MIMO_TX_DIVERSITY and not ce_rows)
         tbs = s._lib.srsgpu_ra_tbs_from_idx(s._lib.srsgpu_ra_tbs_idx_from_mcs(mcs), nof_prb)
         mod = 1 if mcs < 10 else 2 if mcs < 17 else 3
         self.tbs = tbs
         self.ofdm = s.OfdmRx(nof_prb, N, stream=stream)
-        self.chest = s.Chest(nof_prb, cell_id, max_grids=2 * n, stream=stream, nof_ports=2)
-        self.pd = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=2, nof_softbuffers=2 * n, max_cb=13, max_sf=n,
+        self.chest = s.Chest(nof_prb, cell_id, max_grids=2 * n, stream=stream, nof_ports=P)
+        self.pd = s.Pdsch(nof_prb, cell_id, nof_ports=P, nof_rx_ant=2, nof_softbuffers=2 * n, max_cb=13, max_sf=n,
                           stream=stream)
         s._lib.srsgpu_dlsch_set_early_stop(s._vp(self.pd.dlsch_q), int(bool(early_stop)))
         self.chest.set_ce_rows(ce_rows)  # compact estimate rows, identical LLRs (as MixedCells)
@@ -257,7 +260,7 @@ class MimoSubframes:
             sfi = 1 + (i % 4)
             sf = s.make_sf(sf_idx=sfi, lstart=1, nof_prb=nof_prb, mod=(mod, mod), rnti=1234,
                            tbs=(tbs, tbs if ntb == 2 else 0), softbuffer=(2 * j, 2 * j + 1), mimo=mimo,
-                           grid_offset=j * 2 * gsz, ce_offset=j * 4 * gsz,
+                           grid_offset=j * 2 * gsz, ce_offset=j * 2 * P * gsz,
                            data_offset=(2 * j * dlen, (2 * j + 1) * dlen), tb_cw_swap=i % 2 if ntb == 2 else 0,
                            codebook_idx=codebook if mimo == s.MIMO_SPATIAL_MULTIPLEX else 0)
             sf.nof_re = self.pd.nof_re(sf)
@@ -276,27 +279,28 @@ class MimoSubframes:
         self.d_ret = z(2 * n, torch.int32)
         self.d_noi = z(2 * n, torch.int32)
         self.grid = z(2 * n * gsz, torch.complex64)
-        self.ce = z(4 * n * gsz, torch.complex64)
-        self.noise = z(4 * n, torch.float32)
+        self.ce = z(2 * P * n * gsz, torch.complex64)
+        self.noise = z(2 * P * n, torch.float32)
         self.x = z(2 * n * 15 * N, torch.complex64)
         self.pd.set_noise_dev(self.noise.data_ptr())
         self._transmit(snr_db, seed, stream)
 
     def _transmit(self, snr_db, seed, stream):
-        torch, n, gsz, N = self.torch, self.n, self.gsz, self.N
-        txg = torch.zeros(2 * n * gsz, dtype=torch.complex64, device=self.dev)  # [sf][port] grids
+        torch, n, gsz, N, P = self.torch, self.n, self.gsz, self.N, self.nports
+        txg = torch.zeros(P * n * gsz, dtype=torch.complex64, device=self.dev)  # [sf][port] grids
         assert self.pd.encode_dev((self.sfs, n), self.d_data_tx.data_ptr(), txg.data_ptr(), port_stride=gsz) == 0
-        # both ports' CRS: grid i's port p at plane i * 2 + p, n grids (one per subframe)
+        # every port's CRS: grid i's port p at plane i * P + p, n grids (one per subframe)
         assert self.chest.put_crs_dev(self.sf_list, txg.data_ptr(), gsz) == 0
-        xp = torch.zeros(2 * n * 15 * N, dtype=torch.complex64, device=self.dev)
-        assert self.ofdm.tx_dev(2 * n, txg.data_ptr(), gsz, xp.data_ptr(), 15 * N) == 0
+        xp = torch.zeros(P * n * 15 * N, dtype=torch.complex64, device=self.dev)
+        assert self.ofdm.tx_dev(P * n, txg.data_ptr(), gsz, xp.data_ptr(), 15 * N) == 0
         torch.cuda.synchronize(self.dev)
         del txg
-        xp = xp.reshape(n, 2, 15 * N)
-        # a flat 2x2 channel per subframe, from the subframe's global index
+        xp = xp.reshape(n, P, 15 * N)
+        # a flat 2 x P channel per subframe, from the subframe's global index
         g = torch.Generator(device="cpu").manual_seed(seed + 7)
-        ph = torch.rand(16, 2, 2, generator=g) * 6.283
-        amp = torch.tensor([[1.0, 0.45], [0.45, 1.0]])
+        ph = torch.rand(16, 2, P, generator=g) * 6.283
+        amp = torch.tensor([[1.0, 0.45], [0.45, 1.0]]) if P == 2 else torch.tensor([[1.0, 0.45, 0.8, 0.3],
+                                                                                  [0.45, 1.0, 0.3, 0.8]])
         H = (amp * torch.exp(1j * ph)).to(torch.complex64)
         Hs = H[torch.tensor([i % 16 for i in self.kept])].to(self.dev)  # [sf][rx][port]
         y = torch.einsum("sap,spt->sat", Hs, xp)

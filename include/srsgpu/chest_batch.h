@@ -3,7 +3,9 @@
  * estimation (reference: lib/src/phy/ch_estimation/chest_dl.c, srslte_chest_dl_estimate_port
  * :641-664 and the helpers it calls).
  *
- * Supported: CRS ports 0 and 1 (cell.nof_ports 1 or 2), normal cyclic prefix, non-MBSFN subframes,
+ * Supported: CRS ports 0-3 (cell.nof_ports 1, 2 or 4; ports 2 / 3 carry their CRS in symbols 1 and
+ * 8 only, refsignal_dl.c:76-122, and are interpolated in time as chest_dl.c:427-431 does), normal
+ * cyclic prefix, non-MBSFN subframes,
  * every estimator setting srsUE's phch_worker uses (phch_worker.cc:149,553-565). Processing per grid:
  *   - least-squares pilot estimates; RSRP / RSSI / RSRP correlation / CFO measurements;
  *   - noise estimate: REFS (estimate_noise_pilots), PSS or EMPTY (subframes 0 and 5 only);

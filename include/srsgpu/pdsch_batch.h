@@ -7,9 +7,10 @@
  *   - RE extraction of the grant (srslte_pdsch_get, pdsch.c:95-234);
  *   - SISO ZF/MMSE equalisation over 1-2 rx antennas (srslte_predecoding_single_multi,
  *     mimo/precoding.c:243-352), or TM3 large-delay CDD 2x2 MMSE over 2 ports and 2 rx antennas
- *     (srslte_predecoding_ccd_mmse, precoding.c:930-1097), or TM2 transmit diversity over 2 ports
- *     and 1-2 rx antennas (srslte_predecoding_diversity_multi + srslte_layerdemap_diversity,
- *     precoding.c:356-685, layermap.c:143-151), optionally with CSI;
+ *     (srslte_predecoding_ccd_mmse, precoding.c:930-1097), or TM2 transmit diversity over 2 or 4
+ *     ports and 1-2 rx antennas (srslte_predecoding_diversity_multi + srslte_layerdemap_diversity,
+ *     precoding.c:356-685, layermap.c:143-151; with 4 ports over RE quadruplets, which normal-CP
+ *     grants always fill), optionally with CSI;
  *   - soft demapping to int16 LLRs (srslte_demod_soft_demodulate_s, modem/demod_soft.c);
  *   - descrambling with the PDSCH Gold sequence (scrambling.c:48-51, sequences.c:64-66);
  *   - optional CSI weighting (csi_correction, pdsch.c:676-776);
@@ -125,7 +126,8 @@ int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
 /* The same for every MIMO type of the receiver (srslte_pdsch_encode with srslte_layermap_type and
  * srslte_precoding_type, pdsch.c:1048-1131, layermap.c:43-130, precoding.c:1849-2143): per TB the DL-SCH
  * encoding (rv, data at data_offset[tb]), each codeword (cw = tb ^ tb_cw_swap with two TBs) scrambled
- * with its own sequence and modulated, then single antenna, transmit diversity (2-port SFBC), large-delay
+ * with its own sequence and modulated, then single antenna, transmit diversity (2-port SFBC or 4-port
+ * SFBC over RE quadruplets on port pairs 0/2 and 1/3, precoding.c:1863-1889), large-delay
  * CDD (2 ports, 2 TBs) or codebook precoding (2 ports, codebook_idx; 1 TB on 1 layer or 2 TBs on 2
  * layers), rho_a scaling, and the RE mapping of every port: port p of subframe i at
  * d_grid + sf[i].grid_offset + p * port_stride. Transmit diversity with an odd RE count leaves the last

@@ -1,5 +1,5 @@
 """CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's downlink CRS
-channel estimation for CRS ports 0 and 1, normal CP (paths relative to
+channel estimation for CRS ports 0-3, normal CP (paths relative to
 /root/reference/lib/src/phy):
 
   crs_pilots        ch_estimation/refsignal_dl.c:265-318 (Gold sequence per slot/symbol)
@@ -8,7 +8,10 @@ channel estimation for CRS ports 0 and 1, normal CP (paths relative to
                     power is kept: the loop assigns, it does not accumulate)
   smooth            utils/convolution.c:172-211 srslte_conv_same_cf with extrapolated extremes
   interp_freq       resampling/interp.c:245-272 srslte_interp_linear_offset (M = 6)
-  interp_time       chest_dl.c:392-397 + interp.c:150-173 (running sums of (b - a) / d)
+  interp_time       chest_dl.c:421-431 + interp.c:150-173 (running sums of (b - a) / d); ports 2 / 3
+                    (CRS in symbols 1 and 8 only): symbol 0 extrapolated back from 1, symbols 2-7
+                    forward from 1 with (c8 - c1) / 7, and 9-13 forward from symbol 1 again (the
+                    reference's in0 is c1 for that segment, so they repeat 2-6)
   average_row       chest_dl.c:528-548 average_pilots with average_subframe (srsUE's default,
                     srsue/src/main.cc:287-289): the 4 CRS symbols folded into one row of 4*nof_prb
                     pilots at spacing 3, interpolated with M = 3 (chest_dl.c:393-399) and copied to
@@ -43,41 +46,51 @@ def gold(cinit, n):
     return x1[NC:NC + n] ^ x2[NC:NC + n]
 
 
-def crs_pilots(nof_prb, cell_id, sf_idx):
-    """[4 CRS symbols (0, 4, 7, 11)][2*nof_prb] complex pilots of ports 0/1."""
-    out = np.zeros((4, 2 * nof_prb), np.complex128)
+def syms(port=0):
+    """refsignal_dl.c:76-85, 112-122: the CRS symbols of a port in a normal-CP subframe"""
+    return (0, 4, 7, 11) if port < 2 else (1, 8)
+
+
+def crs_pilots(nof_prb, cell_id, sf_idx, port=0):
+    """[CRS symbols][2*nof_prb] complex pilots of ports 0/1 (symbols 0, 4, 7, 11) or 2/3 (1, 8):
+    csr_refs.pilots[port / 2] (refsignal_dl.c:291-313, l' = 0 / 4 or 1 in each slot)"""
+    lps = (0, 4) if port < 2 else (1,)
+    out = np.zeros((2 * len(lps), 2 * nof_prb), np.complex128)
     m = np.arange(2 * nof_prb) + 110 - nof_prb
     for s in range(2):
         ns = 2 * sf_idx + s
-        for li, lp in enumerate((0, 4)):
+        for li, lp in enumerate(lps):
             cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + 1
             c = gold(cinit, 4 * 110).astype(np.float64)
-            out[2 * s + li] = ((1 - 2 * c[2 * m]) + 1j * (1 - 2 * c[2 * m + 1])) / np.sqrt(2)
+            out[len(lps) * s + li] = ((1 - 2 * c[2 * m]) + 1j * (1 - 2 * c[2 * m + 1])) / np.sqrt(2)
     return out
 
 
-SYMS = (0, 4, 7, 11)
+SYMS = syms(0)
 
 
 def fidx(cell_id, l, port=0):
-    """refsignal_dl.c:40-95: v = 0 / 3 alternating over the CRS symbols, port 1 shifted by 3"""
-    return ((3 if (l % 2) ^ port else 0) + cell_id % 6) % 6
+    """refsignal_dl.c:40-95: v = 0 / 3 alternating over the CRS symbols, ports 1 and 3 shifted by 3"""
+    return ((3 if (l % 2) ^ (port % 2) else 0) + cell_id % 6) % 6
 
 
 def ls_estimates(grid, nof_prb, cell_id, sf_idx, port=0):
     g = grid.reshape(14, 12 * nof_prb)
-    pil = crs_pilots(nof_prb, cell_id, sf_idx)  # ports 0 and 1 share the sequence (pilots[p/2])
+    pil = crs_pilots(nof_prb, cell_id, sf_idx, port)  # ports 2p and 2p+1 share pilots[p]
     est = np.zeros_like(pil)
-    for l, s in enumerate(SYMS):
+    for l, s in enumerate(syms(port)):
         est[l] = g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] * np.conj(pil[l])
     return est
 
 
 def noise_refs(est, cell_id, port=0):
-    n = est.shape[1]
-    row3, prev, nxt = est[3], est[2], 2 * est[2] - est[0]
+    """the last CRS symbol's residual against its neighbours: with 4 symbols est[2] and the
+    extrapolated 2 est[2] - est[0]; with 2 (ports 2 / 3) est[0] on both sides (chest_dl.c:285-299)"""
+    n, ns = est.shape[1], est.shape[0]
+    last = est[ns - 1]
+    prev, nxt = (est[2], 2 * est[2] - est[0]) if ns == 4 else (est[0], est[0])
     off = 0 if fidx(cell_id, 0, port) < 3 else 1
-    tmp = row3.copy()
+    tmp = last.copy()
     for r in (prev, nxt):
         tmp[off:] += r[:n - off]
         tmp[:n + off - 1] += r[1 - off:]
@@ -85,8 +98,22 @@ def noise_refs(est, cell_id, port=0):
             tmp[0] += 2 * r[0] - r[1]
         else:
             tmp[n - 1] += 2 * r[n - 2] - r[n - 1]
-    tmp = row3 - tmp / 5.0
-    return np.mean(np.abs(tmp) ** 2) / 4.0 * np.sqrt(5.0)
+    tmp = last - tmp / 5.0
+    return np.mean(np.abs(tmp) ** 2) / ns * np.sqrt(5.0)
+
+
+def interp_time(ce, port=0):
+    """chest_dl.c:421-431 on a [14][nsc] grid whose CRS rows are filled"""
+    if port < 2:
+        segs = ((0, 4, 4, 1, 3, 0), (4, 7, 3, 5, 2, 4), (7, 11, 4, 8, 3, 7), (7, 11, 4, 12, 2, 11))
+    else:
+        segs = ((8, 1, 7, 0, 1, 1), (1, 8, 7, 2, 6, 1), (1, 8, 7, 9, 5, 1))
+    for a, b, d, first, cnt, start in segs:
+        diff = (ce[b] - ce[a]) / d
+        prev = ce[start]
+        for k in range(cnt):
+            prev = prev + diff
+            ce[first + k] = prev
 
 
 def smooth(x, filt):
@@ -128,25 +155,20 @@ def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0):
     f = np.asarray(filt, np.float64)
     sm = est if (len(f) == 0 or (len(f) == 3 and f[0] == 0)) else np.stack([smooth(r, f) for r in est])
     ce = np.zeros((14, 12 * nof_prb), np.complex128)
-    for l, s in enumerate(SYMS):
+    for l, s in enumerate(syms(port)):
         ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
-    for a, b, d, first, cnt in ((0, 4, 4, 1, 3), (4, 7, 3, 5, 2), (7, 11, 4, 8, 3), (7, 11, 4, 12, 2)):
-        diff = (ce[b] - ce[a]) / d
-        prev = ce[b] if first == 12 else ce[a]
-        for k in range(cnt):
-            prev = prev + diff
-            ce[first + k] = prev
+    interp_time(ce, port)
     return ce.reshape(-1), noise
 
 
 def average_row(est, cell_id, port=0):
-    """chest_dl.c:528-548: slot-pair interleave of the 4 CRS symbols, scaled by 2 / 4"""
-    n = est.shape[1]
+    """chest_dl.c:528-548: slot-pair interleave of the CRS symbols, scaled by 2 / nsymbols"""
+    n, ns = est.shape[1], est.shape[0]
     a, b = (0, 1) if fidx(cell_id, 0, port) < 3 else (1, 0)
     t = np.zeros(2 * n, np.complex128)
-    t[0::2] = est[a] + est[a + 2]
-    t[1::2] = est[b] + est[b + 2]
-    return t * 0.5
+    t[0::2] = est[a] + est[a + 2] if ns == 4 else est[a]
+    t[1::2] = est[b] + est[b + 2] if ns == 4 else est[b]
+    return t * (2.0 / ns)
 
 
 def gauss_filter(order, std_dev):
@@ -188,14 +210,19 @@ def noise_empty(grid, nof_prb):
 
 
 def measurements(grid, nof_prb, cell_id, sf_idx, port=0, symbol_sz=1536):
-    """(rsrp, rssi, rsrp_corr, cfo) as srslte_chest_dl_estimate_port leaves them in q"""
+    """(rsrp, rssi, rsrp_corr, cfo) as srslte_chest_dl_estimate_port leaves them in q. The CFO
+    (chest_dl.c:583-603) always reads 4 rows of the shared pilot buffer: for ports 2 / 3, which
+    fill only the first 2, rows 2 and 3 still hold port 1's estimates of the same rx antenna
+    (srslte_chest_dl_estimate_multi runs the ports in order)"""
     g = grid.reshape(14, 12 * nof_prb)
-    recv = np.stack([g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] for l, s in enumerate(SYMS)])
+    sy = syms(port)
+    recv = np.stack([g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] for l, s in enumerate(sy)])
     est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
     rsrp = _avg_power(recv)
-    rssi = float(sum(np.sum(np.abs(g[s]) ** 2) for s in SYMS) / 4)
+    rssi = float(sum(np.sum(np.abs(g[s]) ** 2) for s in sy) / len(sy))
     corr = abs(est.sum() / est.size) ** 2
-    acc = np.sum(est[0] * np.conj(est[2])) + np.sum(est[1] * np.conj(est[3]))
+    e4 = est if port < 2 else np.concatenate([est, ls_estimates(grid, nof_prb, cell_id, sf_idx, 1)[2:]])
+    acc = np.sum(e4[0] * np.conj(e4[2])) + np.sum(e4[1] * np.conj(e4[3]))
     n = float(symbol_sz)
     ng = float(np.ceil(144 * n / 2048))
     cfo = -np.angle(acc) * n / (7 * (n + ng)) / 2 / np.pi
@@ -220,14 +247,9 @@ def estimate_full(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0, 
         ce[:] = interp_freq(row, cell_id % 3, M=3)[None, :]
     else:
         sm = np.stack([smooth(r, f) for r in est]) if smoothing else est
-        for l, s in enumerate(SYMS):
+        for l, s in enumerate(syms(port)):
             ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
-        for a, b, d, first, cnt in ((0, 4, 4, 1, 3), (4, 7, 3, 5, 2), (7, 11, 4, 8, 3), (7, 11, 4, 12, 2)):
-            diff = (ce[b] - ce[a]) / d
-            prev = ce[b] if first == 12 else ce[a]
-            for k in range(cnt):
-                prev = prev + diff
-                ce[first + k] = prev
+        interp_time(ce, port)
     ce = ce.reshape(-1)
     if noise_alg != "refs" and sf_idx in (0, 5):
         noise = noise_pss(grid, ce, nof_prb, cell_id, nof_ports) if noise_alg == "pss" else noise_empty(grid, nof_prb)

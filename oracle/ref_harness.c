@@ -491,6 +491,23 @@ int ref_crs_pilots(uint32_t nof_prb, uint32_t cell_id, uint32_t sf_idx, float *o
   return 0;
 }
 
+/* the pilots of ports 2/3 (csr_refs.pilots[1]: symbol 1 of each slot, refsignal_dl.c:291-313) */
+int ref_crs_pilots23(uint32_t nof_prb, uint32_t cell_id, uint32_t sf_idx, float *out) {
+  srslte_refsignal_t q;
+  memset(&q, 0, sizeof(q));
+  if (srslte_refsignal_cs_init(&q, nof_prb)) return -1;
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = 4;
+  cell.cp = SRSLTE_CP_NORM;
+  if (srslte_refsignal_cs_set_cell(&q, cell)) return -1;
+  memcpy(out, q.pilots[1][sf_idx], 2 * 2 * nof_prb * sizeof(cf_t));
+  srslte_refsignal_free(&q);
+  return 0;
+}
+
 /* srslte_refsignal_cs_get_sf (refsignal_dl.c:404-430) */
 int ref_crs_get_sf(uint32_t nof_prb, uint32_t cell_id, uint32_t port, const float *grid, float *out) {
   srslte_cell_t cell;

@@ -23,8 +23,8 @@ def smooth_channel(nof_prb):
 def crs_grid(nof_prb, cell_id, sf_idx, rng, port=0):
     """random data REs with the CRS of `port` placed (refsignal_cs_put_sf)"""
     g = ((0.5 - rng.random((14, 12 * nof_prb))) + 1j * (0.5 - rng.random((14, 12 * nof_prb))))
-    pil = co.crs_pilots(nof_prb, cell_id, sf_idx)
-    for l, s in enumerate(co.SYMS):
+    pil = co.crs_pilots(nof_prb, cell_id, sf_idx, port)
+    for l, s in enumerate(co.syms(port)):
         g[s, co.fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] = pil[l]
     return g.reshape(-1)
 
@@ -43,7 +43,7 @@ def sync_grid(nof_prb, cell_id, sf_idx, nports, rng, sigma=0.02, flat=False):
         hs.append(h)
         x = crs_grid(nof_prb, cell_id, sf_idx, rng, port)
         mask = np.zeros((14, nsc), bool)
-        for l, sy in enumerate(co.SYMS):
+        for l, sy in enumerate(co.syms(port)):
             mask[sy, co.fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] = True
         g += np.where(mask.reshape(-1), x * h, 0)
     if sf_idx in (0, 5):

@@ -42,6 +42,15 @@ CASES = [
     # no smoothing: the average_subframe quirk (raw pilot buffer interpolated, chest_dl.c:619-621)
     ("nosmooth_avg_25_1x1", 25, 301, 1, 1, [1, 5], (), None, False, True, 0, 0.0),
     ("nosmooth_6_1x1", 6, 0, 1, 1, [7], (), None, False, False, 0, 0.0),
+    # 4 CRS ports: ports 2 / 3 in symbols 1 and 8 (refsignal_dl.c:76-122), their 2-symbol time
+    # interpolation (chest_dl.c:427-431), noise and averaging over 2 symbols, and the CFO reading
+    # port 1's rows of the shared pilot buffer
+    ("srsue_25_4x2", 25, 5, 4, 2, [0, 1, 5], (), (4, 1.0), False, True, 0, 0.0),
+    ("interp_50_4x1", 50, 13, 4, 1, [2, 5], (0.1, 0.8, 0.1), None, False, False, 0, 0.0),
+    ("pss_6_4x2", 6, 8, 4, 2, [4, 5, 6], (), (4, 1.0), False, True, 1, 0.004),
+    ("nosmooth_avg_15_4x1", 15, 2, 4, 1, [3], (), None, False, True, 0, 0.0),
+    ("auto_25_4x1", 25, 20, 4, 1, [1], (), (4, 1.0), True, False, 0, 0.0),
+    ("empty_interp_6_4x1", 6, 1, 4, 1, [0, 7], (0.05, 0.2, 0.5, 0.2, 0.05), None, False, False, 2, 0.004),
 ]
 
 

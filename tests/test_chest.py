@@ -35,20 +35,24 @@ def test_crs_and_pilot_extraction_vs_reference():
     L = Ref().lib
     L.ref_crs_pilots.argtypes = [ctypes.c_uint32] * 3 + [f32]
     L.ref_crs_get_sf.argtypes = [ctypes.c_uint32] * 3 + [f32, f32]
+    L.ref_crs_pilots23.argtypes = [ctypes.c_uint32] * 3 + [f32]
     rng = np.random.default_rng(0)
     for nof_prb, cid in ((100, 1), (6, 0), (25, 503), (50, 17), (75, 254)):
         for sf in (0, 3, 9):
             out = np.zeros(4 * 2 * nof_prb, np.complex64)
             assert L.ref_crs_pilots(nof_prb, cid, sf, out.ctypes.data_as(f32)) == 0
             assert np.allclose(out.reshape(4, -1), co.crs_pilots(nof_prb, cid, sf), atol=1e-7)
+            out = np.zeros(2 * 2 * nof_prb, np.complex64)
+            assert L.ref_crs_pilots23(nof_prb, cid, sf, out.ctypes.data_as(f32)) == 0
+            assert np.allclose(out.reshape(2, -1), co.crs_pilots(nof_prb, cid, sf, port=2), atol=1e-7)
         grid = (rng.standard_normal(14 * 12 * nof_prb) + 1j * rng.standard_normal(14 * 12 * nof_prb)).astype(np.complex64)
-        for port in (0, 1):
-            got = np.zeros(4 * 2 * nof_prb, np.complex64)
+        for port in (0, 1, 2, 3):
+            sy = co.syms(port)
+            got = np.zeros(len(sy) * 2 * nof_prb, np.complex64)
             assert L.ref_crs_get_sf(nof_prb, cid, port, grid.ctypes.data_as(f32), got.ctypes.data_as(f32)) == 0
             g = grid.reshape(14, -1)
-            exp = np.stack([g[s, co.fidx(cid, l, port) + 6 * np.arange(2 * nof_prb)]
-                            for l, s in enumerate(co.SYMS)])
-            assert (got.reshape(4, -1) == exp).all(), port
+            exp = np.stack([g[s, co.fidx(cid, l, port) + 6 * np.arange(2 * nof_prb)] for l, s in enumerate(sy)])
+            assert (got.reshape(len(sy), -1) == exp).all(), port
 
 
 def test_oracle_reference_test_property():
@@ -181,7 +185,7 @@ def _run_modes(nof_prb, cell_id, nports, sfs, filt, average, noise_alg, filt_aut
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nof_prb,cell_id,nports", [(6, 3, 1), (6, 10, 2), (25, 1, 1), (25, 2, 2),
-                                                    (100, 7, 1), (100, 500, 2)])
+                                                    (100, 7, 1), (100, 500, 2), (25, 4, 4), (100, 9, 4)])
 def test_chest_srsue_default_gpu_vs_oracle(nof_prb, cell_id, nports):
     """srsUE's phch_worker configuration (srsue/src/main.cc:287-301, phch_worker.cc:148-150,
     553-565): average_subframe, Gaussian filter order 4 / std dev 1, REFS noise, neighbour RSRP,
@@ -199,6 +203,17 @@ def test_chest_modes_gpu_vs_oracle(average, noise_alg, filt_auto):
     subframes 0 / 5 (PSS / EMPTY update the noise) and others (the caller's value stays)"""
     rng = np.random.default_rng(int(average) * 100 + len(noise_alg) * 10 + int(filt_auto))
     _run_modes(25, 11, 2, [0, 3, 5, 8], (0.1, 0.8, 0.1), average, noise_alg, filt_auto, 0.004, rng)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("average", [False, True])
+@pytest.mark.parametrize("noise_alg", ["refs", "pss", "empty"])
+def test_chest_four_ports_gpu_vs_oracle(average, noise_alg):
+    """4 CRS ports: ports 2 / 3 from symbols 1 and 8 (2-symbol noise, averaging and time
+    interpolation, chest_dl.c:285-299, 427-431, 538-550), with smoothing and smooth_filter_auto"""
+    rng = np.random.default_rng(int(average) * 10 + len(noise_alg))
+    _run_modes(50, 23, 4, [0, 2, 5, 9], (0.1, 0.8, 0.1), average, noise_alg, False, 0.004, rng)
+    _run_modes(15, 200, 4, [1, 5], (), average, noise_alg, True, 0.004, rng)
 
 
 @pytest.mark.gpu
@@ -311,7 +326,8 @@ def test_golden_getters_follow_the_per_port_values():
 @pytest.mark.skipif(not have_ref_front(), reason="oracle/_ref/ref_front not built (build container only)")
 @pytest.mark.parametrize("nof_prb,cell_id,nports,nrx,average,alg,auto", [
     (25, 11, 2, 2, False, 0, False), (50, 301, 1, 1, True, 1, False), (6, 3, 1, 2, False, 2, False),
-    (75, 40, 2, 1, True, 0, True), (100, 7, 1, 1, False, 1, False)])
+    (75, 40, 2, 1, True, 0, True), (100, 7, 1, 1, False, 1, False), (25, 19, 4, 2, False, 0, False),
+    (50, 6, 4, 1, True, 1, False), (15, 100, 4, 2, True, 0, True)])
 def test_oracle_vs_reference_live(nof_prb, cell_id, nports, nrx, average, alg, auto):
     """fresh random cells through the reference's chest_dl.c and the oracle"""
     rng = np.random.default_rng(nof_prb * 7 + cell_id)

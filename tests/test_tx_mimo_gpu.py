@@ -56,11 +56,13 @@ CASES = [  # (nof_prb, cell_id, mimo, ntb, pmi, swap, mcs)
     (50, 140, 2, 2, 0, 0, (24, 17)),  # TM4, two layers, codebooks 1 and 2
     (50, 140, 2, 2, 1, 1, (24, 17)),
 ]
+CASES = [c + (2,) for c in CASES] + [  # 4-port transmit diversity (precoding.c:1863-1889)
+    (25, 3, 1, 1, 0, 0, (12, 0), 4), (100, 41, 1, 1, 0, 0, (28, 0), 4), (15, 502, 1, 1, 0, 0, (7, 0), 4)]
 
 
 @pytest.mark.skipif(not have_ref(), reason="needs the reference build (oracle/_ref)")
-@pytest.mark.parametrize("nof_prb,cell_id,mimo,ntb,pmi,swap,mcs", CASES)
-def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
+@pytest.mark.parametrize("nof_prb,cell_id,mimo,ntb,pmi,swap,mcs,nports", CASES)
+def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs, nports):
     import torch
     import srsgpu_phy as s
     L = _ref_sigs(Ref().lib)
@@ -68,7 +70,7 @@ def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
     gsz = 14 * 12 * nof_prb
     sfs_idx = [0, 1, 5, 8]
     cfi = 2 if nof_prb > 10 else 3
-    pd = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=2, max_sf=len(sfs_idx))
+    pd = s.Pdsch(nof_prb, cell_id, nof_ports=nports, nof_rx_ant=2, max_sf=len(sfs_idx))
     tb = [_mcs_tbs(L, m, nof_prb) for m in mcs]
     dlen = s.dlsch_data_len(max(t[0] for t in tb)) + 2
     data = rng.integers(0, 256, (len(sfs_idx), 2, dlen)).astype(np.uint8)
@@ -76,22 +78,22 @@ def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
     for j, sf_idx in enumerate(sfs_idx):
         sf = s.make_sf(sf_idx=sf_idx, lstart=cfi + 1 if nof_prb < 10 else cfi, nof_prb=nof_prb, mod=(tb[0][1], tb[1][1]), rnti=0x3321,
                        tbs=(tb[0][0], tb[1][0] if ntb == 2 else 0), rv=(0, 0), mimo=mimo,
-                       grid_offset=j * 2 * gsz, data_offset=((2 * j) * dlen, (2 * j + 1) * dlen), tb_cw_swap=swap,
+                       grid_offset=j * nports * gsz, data_offset=((2 * j) * dlen, (2 * j + 1) * dlen), tb_cw_swap=swap,
                        codebook_idx=pmi + (1 if (mimo == 2 and ntb == 2) else 0))
         sf.nof_re = pd.nof_re(sf)
         sfs.append(sf)
-        g = np.zeros(2 * gsz, np.complex64)
+        g = np.zeros(nports * gsz, np.complex64)
         mc = np.array(mcs, np.uint32)
         rv = np.zeros(2, np.uint32)  # the reference encodes a fresh softbuffer only at rv 0 (sch.c)
-        nre = L.ref_pdsch_encode(nof_prb, cell_id, 2, cfi, sf_idx, 0x3321, mimo, pmi, swap, ntb, _p(mc, _u32p),
+        nre = L.ref_pdsch_encode(nof_prb, cell_id, nports, cfi, sf_idx, 0x3321, mimo, pmi, swap, ntb, _p(mc, _u32p),
                                  _p(rv, _u32p), _p(data[j, 0], _u8p), _p(data[j, 1], _u8p), _p(g, _f32p))
         assert nre == sf.nof_re, (nre, sf.nof_re)
         refs.append(g)
     d_data = torch.from_numpy(data.reshape(-1)).cuda()
-    d_grid = torch.zeros(len(sfs_idx) * 2 * gsz, dtype=torch.complex64, device="cuda")
+    d_grid = torch.zeros(len(sfs_idx) * nports * gsz, dtype=torch.complex64, device="cuda")
     assert pd.encode_dev(sfs, d_data.data_ptr(), d_grid.data_ptr(), port_stride=gsz) == 0
     torch.cuda.synchronize()
-    got = d_grid.cpu().numpy().reshape(len(sfs_idx), 2 * gsz)
+    got = d_grid.cpu().numpy().reshape(len(sfs_idx), nports * gsz)
     po = PdschOracle(Oracle())
     for j in range(len(sfs_idx)):
         want = refs[j].copy()
@@ -110,13 +112,19 @@ def test_encode_ports_vs_reference(nof_prb, cell_id, mimo, ntb, pmi, swap, mcs):
 
 def _ref_decode(L, m, j, mimo, pmi, ntb, mcs):
     """the reference's srslte_pdsch_decode of subframe j of a MimoSubframes m on its grids / estimates"""
-    gsz = m.gsz
+    gsz, P = m.gsz, m.nports
     y = m.grid.cpu().numpy().reshape(m.n, 2, gsz)[j]
-    ce = m.ce.cpu().numpy().reshape(m.n, 2, 2, gsz)[j]          # [rx][port]
+    ce = m.ce.cpu().numpy().reshape(m.n, 2, P, gsz)[j]          # [rx][port]
     h = np.ascontiguousarray(np.transpose(ce, (1, 0, 2)))        # [port][rx]
-    nz = m.noise.cpu().numpy().reshape(m.n, 2, 2)[j]  # [rx][port]
+    nz = m.noise.cpu().numpy().reshape(m.n, 2, P)[j]  # [rx][port]
     f = np.float32  # srslte_chest_dl_get_noise_estimate's float order (chest_dl.c:741-750)
-    noise = float((f(nz[0, 0] + nz[0, 1]) / f(2) + f(nz[1, 0] + nz[1, 1]) / f(2)) / f(2))
+    acc = f(0)
+    for a in range(2):
+        sa = f(0)
+        for p in range(P):
+            sa = f(sa + nz[a, p])
+        acc = f(acc + sa / f(P))
+    noise = float(acc / f(2))
     sf = m.sfs[j]
     d0 = np.zeros(m.tbs // 8 + 8, np.uint8)
     d1 = np.zeros(m.tbs // 8 + 8, np.uint8)
@@ -124,7 +132,7 @@ def _ref_decode(L, m, j, mimo, pmi, ntb, mcs):
     noi = np.zeros(2, np.uint32)
     mc = np.array(mcs, np.uint32)
     rv = np.zeros(2, np.uint32)
-    r = L.ref_pdsch_decode_mimo(m.nof_prb, m.cell_id, 2, 2, sf.lstart, sf.sf_idx, sf.rnti, mimo, pmi, sf.tb_cw_swap,
+    r = L.ref_pdsch_decode_mimo(m.nof_prb, m.cell_id, P, 2, sf.lstart, sf.sf_idx, sf.rnti, mimo, pmi, sf.tb_cw_swap,
                                 ntb, _p(mc, _u32p), _p(rv, _u32p), noise, _p(np.ascontiguousarray(y), _f32p),
                                 _p(h, _f32p), _p(d0, _u8p), _p(d1, _u8p), _p(ok, _i32p), _p(noi, _u32p))
     assert r == 0
@@ -181,4 +189,31 @@ def test_tm2_tm4_tx_rx(mimo, ntb, codebook, mcs):
             o = (2 * j + t) * m.dlen
             assert ok[t] == 1 and ret[k] == 0 and nois[k] == noiref[t], (j, t)
             assert (data[o:o + m.tbs // 8] == dref[t][:m.tbs // 8]).all(), (j, t)
+    m.close()
+
+
+@pytest.mark.skipif(not have_ref(), reason="needs the reference build (oracle/_ref)")
+@pytest.mark.parametrize("nof_prb,cell_id,mcs,csi", [(50, 21, 20, False), (100, 6, 27, True)])
+def test_tm2_four_ports_tx_rx(nof_prb, cell_id, mcs, csi):
+    """4-port transmit diversity end to end: GPU encoder (RE quadruplets on port pairs 0/2 and 1/3), the
+    CRS of ports 0-3, OFDM, a 2x4 channel; GPU OFDM / channel estimation of all four ports / SFBC
+    predecoding / DL-SCH: every TB acks with its bytes, and the reference's srslte_pdsch_decode on the
+    same grids and estimates of two subframes agrees (ack, bytes, nof_iterations)"""
+    import torch
+    import srsgpu_traffic as tr
+    L = _ref_sigs(Ref().lib)
+    m = tr.MimoSubframes(torch, torch.device("cuda"), 48, seed=13 + nof_prb, snr_db=30.0, mimo=1, mcs=mcs,
+                         nof_prb=nof_prb, cell_id=cell_id, nof_tb=1, ce_rows=False, nof_ports=4)
+    m.pd.set_csi(csi)
+    m.step()
+    torch.cuda.synchronize()
+    acks, good, _ = m.check()
+    assert acks == good == 48, (acks, good)
+    ret, nois, data = m.d_ret.cpu().numpy(), m.d_noi.cpu().numpy(), m.d_data.cpu().numpy()
+    if not csi:  # the reference harness decodes with CSI off
+        for j in (0, 29):
+            ok, dref, noiref = _ref_decode(L, m, j, 1, 0, 1, (mcs, mcs))
+            o = 2 * j * m.dlen
+            assert ok[0] == 1 and ret[j] == 0 and nois[j] == noiref[0], (j, nois[j], noiref[0])
+            assert (data[o:o + m.tbs // 8] == dref[0][:m.tbs // 8]).all(), j
     m.close()

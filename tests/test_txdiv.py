@@ -76,10 +76,12 @@ def test_random_txdiv_vs_reference(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nof_prb,cell_id,nrx,csi", [(100, 1, 1, False), (25, 17, 2, False),
-                                                     (50, 300, 2, True), (6, 501, 1, True)])
-def test_gpu_txdiv_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi):
-    """random grids and 2-port channels, QPSK/16QAM/64QAM, subframes 0/1/5, random PRB masks:
+@pytest.mark.parametrize("nof_prb,cell_id,nrx,csi,nports", [(100, 1, 1, False, 2), (25, 17, 2, False, 2),
+                                                            (50, 300, 2, True, 2), (6, 501, 1, True, 2),
+                                                            (100, 7, 2, False, 4), (50, 33, 1, True, 4),
+                                                            (6, 2, 2, True, 4), (16, 401, 1, False, 4)])
+def test_gpu_txdiv_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi, nports):
+    """random grids and 2- or 4-port channels, QPSK/16QAM/64QAM, subframes 0/1/5, random PRB masks:
     descrambled (CSI-weighted) int16 LLRs equal the oracle chain"""
     import torch
     import srsgpu_phy as s
@@ -88,8 +90,9 @@ def test_gpu_txdiv_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi):
     size = nof_prb * 12 * 14
     n_sf = 6
     y = (rng.standard_normal((n_sf, nrx, size)) + 1j * rng.standard_normal((n_sf, nrx, size))).astype(np.complex64)
-    h = (rng.standard_normal((n_sf, nrx, 2, size)) + 1j * rng.standard_normal((n_sf, nrx, 2, size))).astype(np.complex64)
-    p = s.Pdsch(nof_prb, cell_id, nof_ports=2, nof_rx_ant=nrx, max_sf=n_sf)
+    h = (rng.standard_normal((n_sf, nrx, nports, size)) +
+         1j * rng.standard_normal((n_sf, nrx, nports, size))).astype(np.complex64)
+    p = s.Pdsch(nof_prb, cell_id, nof_ports=nports, nof_rx_ant=nrx, max_sf=n_sf)
     p.set_csi(csi)
     sfs, expect, offs, off = [], [], [], 0
     for i in range(n_sf):
@@ -99,12 +102,12 @@ def test_gpu_txdiv_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi):
         mod = [1, 2, 3][i % 3]
         rnti = int(rng.integers(1, 65535))
         scaling = 1.0 if i % 2 else 0.7943
-        idx = po.re_map(nof_prb, cell_id, 2, lstart, sf_idx, mask)
+        idx = po.re_map(nof_prb, cell_id, nports, lstart, sf_idx, mask)
         sfs.append(s.make_sf(sf_idx=sf_idx, lstart=lstart, prb=mask, nof_prb=nof_prb, mod=mod,
                              nof_re=idx.size, rnti=rnti, scaling=scaling, mimo=s.MIMO_TX_DIVERSITY,
-                             grid_offset=i * nrx * size, ce_offset=i * nrx * 2 * size))
+                             grid_offset=i * nrx * size, ce_offset=i * nrx * nports * size))
         out = predecode_txdiv(oracle, [y[i, a][idx] for a in range(nrx)],
-                              [[h[i, a, pp][idx] for a in range(nrx)] for pp in range(2)], scaling, csi)
+                              [[h[i, a, pp][idx] for a in range(nrx)] for pp in range(nports)], scaling, csi)
         d = out[0] if csi else out
         llr = po.scramble(po.seed(rnti, 0, 2 * sf_idx, cell_id), po.demod(mod, d))
         expect.append(po.csi_correction(mod, out[1], llr) if csi else llr)
@@ -131,3 +134,18 @@ def test_gpu_txdiv_needs_two_ports():
     sf = s.make_sf(sf_idx=1, lstart=1, nof_prb=25, mod=1, nof_re=1, mimo=s.MIMO_TX_DIVERSITY)
     assert p.llr_dev([sf], d.data_ptr(), d.data_ptr(), 25 * 12 * 14, d.data_ptr(), [0]) == -1
     p.close()
+
+
+
+def test_txdiv4_grants_are_whole_quadruplets(oracle):
+    """with 4 CRS ports every normal-CP PDSCH grant has a multiple of 4 REs (full PRBs give 12 or 8 per
+    symbol, the half PRBs around PBCH / sync 6 + 6, 4 + 4 and 6 + 6 over symbol pairs), so the
+    reference's 4 floor(n / 4) layer symbols always cover the grant"""
+    po = PdschOracle(oracle)
+    rng = np.random.default_rng(5)
+    for nof_prb in (6, 15, 25, 75, 100):
+        for sf in (0, 1, 5):
+            for lstart in (1, 2, 3, 4):
+                for _ in range(3):
+                    mask = (rng.random((2, nof_prb)) < 0.5).astype(np.uint8)
+                    assert po.re_map(nof_prb, 7, 4, lstart, sf, mask).size % 4 == 0
