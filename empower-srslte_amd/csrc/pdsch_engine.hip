@@ -71,6 +71,12 @@ static void re_map(const srsgpu_cell_t &c, uint32_t lstart_grant, uint32_t sf_id
 }
 
 static const int kQm[4] = {1, 2, 4, 6};
+// The Qm srslte_dlsch_encode2 / srslte_dlsch_decode2 hand to encode_tb / decode_tb (sch.c:506-545):
+// the modulation order times Nl = 2 when the layers outnumber the TBs (transmit diversity over 2 or 4
+// layers), which changes how the codeword's E bits split over the code blocks (36.212 5.1.4.1.2)
+static uint32_t dlsch_qm(const srsgpu_pdsch_sf_t &s, uint32_t tb) {
+  return (uint32_t)kQm[s.mod[tb]] * (s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY ? 2u : 1u);
+}
 
 // ------------------------------------------------------------------ engine ----
 struct PdschEngine {
@@ -415,7 +421,7 @@ struct PdschEngine {
         srsgpu_dlsch_tb_t &t = h_tb[k];
         t.tbs = s.tbs[tb];
         t.rv = s.rv[tb];
-        t.Qm = (uint32_t)q;
+        t.Qm = dlsch_qm(s, tb);
         t.nof_e_bits = nre * q;
         t.softbuffer = 0;
         t.e_offset = (uint64_t)k * max_bits;
@@ -563,8 +569,8 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
       srsgpu_dlsch_tb_t &t = E.h_tb[j];
       t.tbs = sf[i].tbs[tb];
       t.rv = sf[i].rv[tb];
-      t.Qm = (uint32_t)srsgpu::kQm[sf[i].mod[tb]];
-      t.nof_e_bits = sf[i].nof_re * t.Qm;
+      t.Qm = srsgpu::dlsch_qm(sf[i], tb);
+      t.nof_e_bits = sf[i].nof_re * srsgpu::kQm[sf[i].mod[tb]];
       t.softbuffer = sf[i].softbuffer[tb];
       t.e_offset = (uint64_t)j * E.max_bits;
       t.data_offset = sf[i].data_offset[tb];

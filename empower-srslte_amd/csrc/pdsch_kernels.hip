@@ -92,6 +92,7 @@ struct ReIn {
 // 12-13 continue from symbol 11 with the 7-11 step); or the one averaged row. The same floats as
 // the full estimate grid.
 __device__ __forceinline__ float2 ce_at(const LlrItem &t, const float2 *h, uint32_t pos) {
+  h = gmem(h); // descriptor pointers: global accesses, not flat (gmem.h)
   if (t.ce_rows == 0) return h[pos];
   const uint32_t s = (uint32_t)(((float)pos + 0.5f) * t.inv_nsc); // exact: pos < 2^15, >= 1/(2 nsc) from an integer
   const uint32_t k = pos - s * t.nsc;
@@ -114,7 +115,7 @@ __device__ __forceinline__ ReIn load_re(const LlrItem &t, uint32_t pos, bool two
 #pragma unroll
   for (int a = 0; a < 2; a++) {
     if (a == 1 && t.nrx < 2) break;
-    in.y[a] = t.y[a][pos];
+    in.y[a] = gmem(t.y[a])[pos];
     in.h[0][a] = ce_at(t, t.h[0][a], pos);
     if (two_ports) in.h[1][a] = ce_at(t, t.h[1][a], pos);
   }
@@ -179,7 +180,7 @@ __device__ __forceinline__ cf c_sub(cf a, cf b) { return {a.r - b.r, a.i - b.i};
 __device__ __forceinline__ cf c_conj(cf a) { return {a.r, -a.i}; }
 __device__ __forceinline__ cf c_neg(cf a) { return {-a.r, -a.i}; }
 __device__ __forceinline__ cf c_ld(const float2 *p, uint32_t pos) {
-  const float2 v = p[pos];
+  const float2 v = gmem(p)[pos];
   return {v.x, v.y};
 }
 __device__ __forceinline__ cf c_of(float2 v) { return {v.x, v.y}; }
@@ -307,7 +308,7 @@ __device__ __forceinline__ Eq equalise_mrc(const LlrItem &t, const ReIn &in) {
 // terms in double (the double conj()), hh = 1e-4 when 0, x / (hh * scaling) * sqrt(2) in double;
 // csi = hh before scaling.
 __device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
-  const uint32_t i = j >> 1, p0 = t.map[2 * i], p1 = t.map[2 * i + 1];
+  const uint32_t i = j >> 1, p0 = gmem(t.map)[2 * i], p1 = gmem(t.map)[2 * i + 1];
   const bool odd = j & 1;
   Eq e;
   if (!t.csi_mode && t.nof_re > 32 && i < 2 * (t.nof_re / 4)) {
@@ -375,7 +376,7 @@ __device__ __forceinline__ Eq equalise_txdiv(const LlrItem &t, uint32_t j) {
 // those symbols to whatever its buffer held).
 __device__ __forceinline__ Eq equalise_txdiv4(const LlrItem &t, uint32_t j) {
   const uint32_t k = j & 3, q = k >> 1, b = (j & ~3u) + 2 * q;
-  const uint32_t p0 = t.map[b], p1 = t.map[b + 1];
+  const uint32_t p0 = gmem(t.map)[b], p1 = gmem(t.map)[b + 1];
   const bool odd = k & 1;
   cf x = {0.f, 0.f};
   float g = 0.f;
@@ -558,16 +559,16 @@ __device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &
     if ((cb >> k) & 1) // _mm256_sign_epi16 / _epi8 (scrambling_sb_offset) by c = 1 - 2c
       o[k] = t.llr8 ? wrap8(-(int32_t)o[k]) : wrap16(-(int32_t)o[k]);
   if (Q % 2 == 0 && t.aligned) {
-    uint32_t *dst = reinterpret_cast<uint32_t *>(t.e + b0);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(gmem(t.e) + b0);
 #pragma unroll
     for (int k = 0; k < Q; k += 2) dst[k / 2] = (uint16_t)o[k] | ((uint32_t)(uint16_t)o[k + 1] << 16);
   } else {
 #pragma unroll
-    for (int k = 0; k < Q; k++) t.e[b0 + k] = o[k];
+    for (int k = 0; k < Q; k++) gmem(t.e)[b0 + k] = o[k];
   }
   if (t.csi_mode) {
-    t.csi[j] = e.csi;
-    atomicMax(t.csi_max, __float_as_uint(e.csi)); // csi >= 0: uint order == float order
+    gmem(t.csi)[j] = e.csi;
+    atomicMax(gmem(t.csi_max), __float_as_uint(e.csi)); // csi >= 0: uint order == float order
   }
 }
 
@@ -584,7 +585,8 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
   if (t.txdiv) {
     for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += stride) {
       const uint32_t w = (j * Q) >> 5;
-      llr_out<MOD>(t, j, t.txdiv == 4 ? equalise_txdiv4(t, j) : equalise_txdiv(t, j), t.c[w], t.c[w + 1]);
+      llr_out<MOD>(t, j, t.txdiv == 4 ? equalise_txdiv4(t, j) : equalise_txdiv(t, j), gmem(t.c)[w],
+                   gmem(t.c)[w + 1]);
     }
     return;
   }
@@ -594,7 +596,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
 #pragma unroll
     for (int r = 0; r < LLR_RES; r++) {
       const uint32_t j = j0 + r * stride;
-      pos[r] = t.map[j < t.nof_re ? j : j0];
+      pos[r] = gmem(t.map)[j < t.nof_re ? j : j0];
     }
     ReIn in[LLR_RES];
     uint32_t c0[LLR_RES], c1[LLR_RES];
@@ -603,8 +605,8 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
       const uint32_t j = j0 + r * stride;
       const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
       in[r] = load_re(t, pos[r], two_ports);
-      c0[r] = t.c[w];
-      c1[r] = t.c[w + 1];
+      c0[r] = gmem(t.c)[w];
+      c1[r] = gmem(t.c)[w + 1];
     }
 #pragma unroll
     for (int r = 0; r < LLR_RES; r++) {
@@ -629,7 +631,7 @@ __device__ __forceinline__ void llr_body_dual(const LlrItem &t, const LlrItem &t
 #pragma unroll
     for (int r = 0; r < LLR_RES; r++) {
       const uint32_t j = j0 + r * stride;
-      pos[r] = t.map[j < t.nof_re ? j : j0];
+      pos[r] = gmem(t.map)[j < t.nof_re ? j : j0];
     }
     ReIn in[LLR_RES];
     uint32_t c0[LLR_RES], c1[LLR_RES], d0[LLR_RES], d1[LLR_RES];
@@ -638,10 +640,10 @@ __device__ __forceinline__ void llr_body_dual(const LlrItem &t, const LlrItem &t
       const uint32_t j = j0 + r * stride;
       const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
       in[r] = load_re(t, pos[r], true);
-      c0[r] = t.c[w];
-      c1[r] = t.c[w + 1];
-      d0[r] = t2.c[w];
-      d1[r] = t2.c[w + 1];
+      c0[r] = gmem(t.c)[w];
+      c1[r] = gmem(t.c)[w + 1];
+      d0[r] = gmem(t2.c)[w];
+      d1[r] = gmem(t2.c)[w + 1];
     }
 #pragma unroll
     for (int r = 0; r < LLR_RES; r++) {

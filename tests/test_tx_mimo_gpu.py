@@ -56,7 +56,11 @@ CASES = [  # (nof_prb, cell_id, mimo, ntb, pmi, swap, mcs)
     (50, 140, 2, 2, 0, 0, (24, 17)),  # TM4, two layers, codebooks 1 and 2
     (50, 140, 2, 2, 1, 1, (24, 17)),
 ]
-CASES = [c + (2,) for c in CASES] + [  # 4-port transmit diversity (precoding.c:1863-1889)
+CASES = [c + (2,) for c in CASES] + [
+    # transmit diversity at MCS 28: the codeword's E bits split over 13 blocks with Qm x Nl = 12
+    # (sch.c:535-545), which differs from a split by Qm in these subframes
+    (100, 41, 1, 1, 0, 0, (28, 0), 2),
+    # 4-port transmit diversity (precoding.c:1863-1889)
     (25, 3, 1, 1, 0, 0, (12, 0), 4), (100, 41, 1, 1, 0, 0, (28, 0), 4), (15, 502, 1, 1, 0, 0, (7, 0), 4)]
 
 
