@@ -267,6 +267,10 @@ class MimoSubframes:
             sfs.append(sf)
         self.sfs = s.make_sf_array(sfs)
         self.nre = sfs[0].nof_re
+        # the transmitter's [sf][port] grids: P planes per subframe (the receive grids hold 2 rx antennas)
+        for j, sf in enumerate(sfs):
+            sf.grid_offset = j * P * gsz
+        self.sfs_tx = s.make_sf_array(sfs)
         self.grid_sf = (ct.c_uint32 * (2 * n))(*[1 + (i % 4) for i in self.kept for _ in range(2)])  # [sf][rx]
         self.sf_list = (ct.c_uint32 * n)(*[1 + (i % 4) for i in self.kept])  # [sf]
         z = lambda k, dt: torch.zeros(k, dtype=dt, device=dev)  # noqa: E731
@@ -288,7 +292,7 @@ class MimoSubframes:
     def _transmit(self, snr_db, seed, stream):
         torch, n, gsz, N, P = self.torch, self.n, self.gsz, self.N, self.nports
         txg = torch.zeros(P * n * gsz, dtype=torch.complex64, device=self.dev)  # [sf][port] grids
-        assert self.pd.encode_dev((self.sfs, n), self.d_data_tx.data_ptr(), txg.data_ptr(), port_stride=gsz) == 0
+        assert self.pd.encode_dev((self.sfs_tx, n), self.d_data_tx.data_ptr(), txg.data_ptr(), port_stride=gsz) == 0
         # every port's CRS: grid i's port p at plane i * P + p, n grids (one per subframe)
         assert self.chest.put_crs_dev(self.sf_list, txg.data_ptr(), gsz) == 0
         xp = torch.zeros(P * n * 15 * N, dtype=torch.complex64, device=self.dev)
