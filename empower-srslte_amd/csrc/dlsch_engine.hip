@@ -20,6 +20,7 @@
 
 #include "dlsch_kernels.h"
 #include "srsgpu/dlsch_batch.h"
+#include "srsgpu/uci_tables.h"
 #include "srsgpu/ulsch_batch.h"
 #include "tdec_engine.h"
 
@@ -153,6 +154,7 @@ struct DlschEngine {
   uint32_t *d_crc_a = nullptr;
   // UL-SCH deinterleaver descriptors (lazily allocated)
   UlItem *h_ul = nullptr, *d_ul = nullptr;
+  int32_t *d_uci_ret = nullptr; // [2 cap]: ret / noi of the data TBs of a UCI call (lazily allocated)
   // host-pointer API staging
   int16_t *e_stage = nullptr;
   uint8_t *data_stage = nullptr;
@@ -212,7 +214,7 @@ struct DlschEngine {
     for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
                     (void *)d_noi, (void *)d_late, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
-                    (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul})
+                    (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul, (void *)d_uci_ret})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
                     (void *)h_ul, (void *)h_blk})
@@ -553,6 +555,8 @@ struct DlschEngine {
 using srsgpu::DlschEngine;
 using srsgpu::ProfScope;
 using srsgpu::UlItem;
+using srsgpu::launch_uci_ack_ri;
+using srsgpu::launch_uci_cqi;
 using srsgpu::launch_ulsch_deinterleave;
 
 struct srsgpu_dlsch {
@@ -674,6 +678,128 @@ int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint
     d[i] = d_data + tb[i].data_offset;
   }
   return q->e.decode(dl.data(), ntb, e.data(), d.data(), maxh, d_ret, d_noi);
+}
+
+// srsgpu_ulsch_uci_decode_dev: Q' of each UCI kind on the host (uci.c:270-290, 548-572, in the
+// reference's float order), then k_uci_ack_ri on the scrambled q bits, the deinterleaver in its UCI
+// mode, k_uci_cqi (g[0], CQI, ret / noi of TBs without data) and decode_tb of the data part.
+static uint32_t uci_qp_ack_ri(uint32_t O, uint32_t O_cqi, float beta, uint32_t K, uint32_t M_sc, uint32_t M_sc_init,
+                              uint32_t nsymb) {
+  if (K == 0) K = O_cqi <= 11 ? O_cqi : O_cqi + 8;
+  const uint32_t x = (uint32_t)ceilf((float)O * M_sc_init * nsymb * beta / K);
+  return std::min(x, 4 * M_sc);
+}
+
+int srsgpu_ulsch_uci_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, const srsgpu_uci_cfg_t *uci,
+                                uint32_t ntb, const int16_t *d_q, const uint8_t *d_c, int16_t *d_g, uint8_t *d_data,
+                                uint32_t maxh, int32_t *d_ret, uint32_t *d_noi, srsgpu_uci_result_t *d_uci) {
+  if (!q || (!tb && ntb) || (!uci && ntb) || !d_q || !d_c || !d_g || !d_data || !d_ret || !d_noi || !d_uci) return -1;
+  if (ntb == 0) return 0;
+  DlschEngine &E = q->e;
+  if (ntb > E.cap) return -1;
+  std::vector<srsgpu::UlItem> it(ntb);
+  uint32_t max_bits = 0;
+  for (uint32_t i = 0; i < ntb; i++) {
+    const srsgpu_ulsch_tb_t &t = tb[i];
+    const srsgpu_uci_cfg_t &u = uci[i];
+    const uint32_t Qm = t.Qm, ns = t.nof_symb;
+    if ((Qm != 2 && Qm != 4 && Qm != 6) || ns < 11 || t.nof_bits % (Qm * ns) || u.O_ack > 2 || u.O_ri > 2 ||
+        u.O_cqi > SRSGPU_UCI_MAX_CQI_BITS || u.I_offset_ack > 15 || u.I_offset_ri > 15 || u.I_offset_cqi > 15 ||
+        !u.M_sc || t.nof_bits / Qm != u.M_sc * ns) {
+      fprintf(stderr, "srsgpu: invalid UCI PUSCH configuration for TB %u\n", i);
+      return -1;
+    }
+    srsgpu::Segm sg;
+    if (srsgpu::segm(t.tbs, sg)) return -1;
+    const uint32_t K = sg.C1 * sg.K1 + sg.C2 * sg.K2;
+    const float bcqi = SRSGPU_BETA_CQI[u.I_offset_cqi];
+    srsgpu::UlItem &x = it[i];
+    x = srsgpu::UlItem{t.q_offset, t.nof_bits / Qm / ns, ns, Qm};
+    x.uci = 1;
+    x.O_ack = u.O_ack;
+    x.O_ri = u.O_ri;
+    x.O_cqi = u.O_cqi;
+    x.tbs = t.tbs;
+    x.c_offset = u.c_offset;
+    if (u.O_ack) { // sch.c:906-910: beta / beta_cqi without data
+      float beta = SRSGPU_BETA_ACK[u.I_offset_ack];
+      if (t.tbs == 0) beta /= bcqi;
+      if (beta < 0) {
+        fprintf(stderr, "Error beta is reserved\n");
+        return -1;
+      }
+      x.Q_ack = uci_qp_ack_ri(u.O_ack, u.O_cqi, beta, K, u.M_sc, u.M_sc_init, ns);
+    }
+    if (u.O_ri) {
+      float beta = SRSGPU_BETA_RI[u.I_offset_ri];
+      if (t.tbs == 0) beta /= bcqi;
+      if (beta < 0) {
+        fprintf(stderr, "Error beta is reserved\n");
+        return -1;
+      }
+      x.Q_ri = uci_qp_ack_ri(u.O_ri, u.O_cqi, beta, K, u.M_sc, u.M_sc_init, ns);
+    }
+    if (u.O_cqi) { // uci.c:270-290
+      if (bcqi < 0) {
+        fprintf(stderr, "Error beta is reserved\n");
+        return -1;
+      }
+      const uint32_t L = u.O_cqi < 11 ? 0 : 8;
+      uint32_t v = 999999;
+      if (K > 0) v = (uint32_t)ceilf((float)(u.O_cqi + L) * u.M_sc_init * ns * bcqi / K);
+      x.Q_cqi = std::min(v, u.M_sc * ns - x.Q_ri);
+    }
+    if (x.Q_ack * Qm > 12 * 288 || x.Q_ri * Qm > 12 * 288) { // srslte_sch_t.ack_ri_bits[12 * 288] (sch.h:70)
+      fprintf(stderr, "srsgpu: HARQ-ACK / RI of TB %u exceed the reference's 3456 positions\n", i);
+      return -1;
+    }
+    if (x.Q_ri + x.Q_cqi >= t.nof_bits / Qm && t.tbs) {
+      fprintf(stderr, "srsgpu: UCI leaves no data symbols in TB %u\n", i);
+      return -1;
+    }
+    max_bits = std::max(max_bits, t.nof_bits);
+  }
+  if (!E.h_ul) {
+    HIPCHK(hipHostMalloc(&E.h_ul, sizeof(UlItem) * E.cap));
+    HIPCHK(hipMalloc(&E.d_ul, sizeof(UlItem) * E.cap));
+  }
+  if (E.staged_pending) HIPCHK(hipEventSynchronize(E.staged));
+  memcpy(E.h_ul, it.data(), sizeof(srsgpu::UlItem) * ntb);
+  HIPCHK(hipMemcpyAsync(E.d_ul, E.h_ul, sizeof(srsgpu::UlItem) * ntb, hipMemcpyHostToDevice, E.st));
+  HIPCHK(hipEventRecord(E.staged, E.st));
+  E.staged_pending = true;
+  {
+    ProfScope ps("k_uci", E.st);
+    HIPCHK(launch_uci_ack_ri(E.d_ul, (int)ntb, d_q, d_c, d_uci, E.st));
+    HIPCHK(launch_ulsch_deinterleave(E.d_ul, (int)ntb, max_bits, d_q, d_g, E.st, d_c));
+    HIPCHK(launch_uci_cqi(E.d_ul, (int)ntb, d_q, d_c, d_g, d_uci, d_ret, d_noi, E.st));
+  }
+  // decode_tb of the data: G = H' - Q'_ri - Q'_cqi symbols after the CQI (sch.c:972-983)
+  std::vector<srsgpu_dlsch_tb_t> dl;
+  std::vector<const int16_t *> e;
+  std::vector<uint8_t *> d;
+  std::vector<uint32_t> idx;
+  for (uint32_t i = 0; i < ntb; i++) {
+    if (!tb[i].tbs) continue;
+    const uint32_t Qm = tb[i].Qm, G = tb[i].nof_bits / Qm - it[i].Q_ri - it[i].Q_cqi;
+    dl.push_back(srsgpu_dlsch_tb_t{tb[i].tbs, tb[i].rv, Qm, G * Qm, tb[i].softbuffer, 0, 0});
+    e.push_back(d_g + tb[i].q_offset + (size_t)it[i].Q_cqi * Qm);
+    d.push_back(d_data + tb[i].data_offset);
+    idx.push_back(i);
+  }
+  if (dl.empty()) return 0;
+  // the data TBs' results land at their own indices: decode into a contiguous run, then scatter
+  // only when some TB carries no data
+  if (dl.size() == ntb) return q->e.decode(dl.data(), (uint32_t)dl.size(), e.data(), d.data(), maxh, d_ret, d_noi);
+  if (!E.d_uci_ret) HIPCHK(hipMalloc(&E.d_uci_ret, sizeof(int32_t) * 2 * E.cap));
+  int32_t *r_tmp = E.d_uci_ret;
+  uint32_t *n_tmp = (uint32_t *)(r_tmp + E.cap);
+  if (q->e.decode(dl.data(), (uint32_t)dl.size(), e.data(), d.data(), maxh, r_tmp, n_tmp)) return -1;
+  for (size_t k = 0; k < dl.size(); k++) {
+    HIPCHK(hipMemcpyAsync(d_ret + idx[k], r_tmp + k, 4, hipMemcpyDeviceToDevice, E.st));
+    HIPCHK(hipMemcpyAsync(d_noi + idx[k], n_tmp + k, 4, hipMemcpyDeviceToDevice, E.st));
+  }
+  return 0;
 }
 
 int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb,

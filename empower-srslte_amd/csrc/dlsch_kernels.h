@@ -106,9 +106,20 @@ hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *cr
 struct UlItem {
   uint64_t q_offset;
   uint32_t rows, cols, Qm;
+  // UCI on the PUSCH (srsgpu_ulsch_uci_decode_dev; uci = 0: the plain UL-SCH, q already descrambled)
+  uint32_t uci;
+  uint32_t O_ack, O_ri, O_cqi;
+  uint32_t Q_ack, Q_ri, Q_cqi;
+  uint32_t tbs;      // 0: no data (the UCI kernel writes ret / noi)
+  uint64_t c_offset; // scrambling bytes of the TB (q still scrambled)
 };
 hipError_t launch_ulsch_deinterleave(const UlItem *d_items, int n, uint32_t max_bits, const int16_t *q,
-                                     int16_t *g, hipStream_t st);
+                                     int16_t *g, hipStream_t st, const uint8_t *c = nullptr);
+// UCI steps (uci_kernels.hip): HARQ-ACK / RI before the deinterleaver, g[0] and CQI after it
+hipError_t launch_uci_ack_ri(const UlItem *d_items, int n, const int16_t *q, const uint8_t *c, void *res,
+                             hipStream_t st);
+hipError_t launch_uci_cqi(const UlItem *d_items, int n, const int16_t *q, const uint8_t *c, int16_t *g, void *res,
+                          int32_t *ret, uint32_t *noi, hipStream_t st);
 } // namespace srsgpu
 
 #include "tdec_kernels.h"

@@ -13,6 +13,7 @@
 #include <stdlib.h>
 
 #include "dlsch_kernels.h"
+#include "uci_dev.h"
 #include "srsgpu/dlsch_batch.h"
 
 #include <algorithm>
@@ -730,9 +731,14 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
 // (row j, column i, bit k) row by row, entry (j, i, k) sits at q index (i rows + j) Qm + k, and
 // srslte_vec_lut_sis writes g[lut[x]] = q[x]. One thread per g element (coalesced stores, the
 // gathered reads are rows x Qm apart).
+// With UCI (srsgpu_ulsch_uci_decode_dev, sch.c:860-881 with RI bits): q is still scrambled; the RI
+// entries are left out of g (the g index drops by Qm per RI group before the entry in row-major
+// order), HARQ-ACK entries read as 0 (sch.c:921-924) and every value is descrambled on the way
+// (srslte_scrambling_s_offset, c ? -q : q). The lut's extra writes to g[0] are k_uci_cqi's.
 __global__ __launch_bounds__(256) void k_ulsch_deinterleave(const UlItem *__restrict__ items,
                                                             const int16_t *__restrict__ q,
-                                                            int16_t *__restrict__ g) {
+                                                            int16_t *__restrict__ g,
+                                                            const uint8_t *__restrict__ c) {
   const UlItem it = items[blockIdx.y];
   const uint32_t n = it.rows * it.cols * it.Qm;
   const uint32_t x = blockIdx.x * 256 + threadIdx.x;
@@ -740,14 +746,22 @@ __global__ __launch_bounds__(256) void k_ulsch_deinterleave(const UlItem *__rest
   const uint32_t rowlen = it.cols * it.Qm;
   const uint32_t j = x / rowlen, r = x - j * rowlen;
   const uint32_t i = r / it.Qm, k = r - i * it.Qm;
-  g[it.q_offset + x] = q[it.q_offset + (size_t)(i * it.rows + j) * it.Qm + k];
+  const size_t src = (size_t)(i * it.rows + j) * it.Qm + k;
+  if (!it.uci) {
+    g[it.q_offset + x] = q[it.q_offset + src];
+    return;
+  }
+  if (uci_group(j, i, it.rows, true) < it.Q_ri) return; // an RI entry
+  int16_t v = uci_group(j, i, it.rows, false) < it.Q_ack ? (int16_t)0 : q[it.q_offset + src];
+  if (c[it.c_offset + src]) v = (int16_t)(-(int32_t)v);
+  g[it.q_offset + x - (size_t)uci_ri_before(j, i, it.rows, it.Q_ri) * it.Qm] = v;
 }
 
 hipError_t launch_ulsch_deinterleave(const UlItem *d_items, int n, uint32_t max_bits, const int16_t *q,
-                                     int16_t *g, hipStream_t st) {
+                                     int16_t *g, hipStream_t st, const uint8_t *c) {
   if (n <= 0 || max_bits == 0) return hipSuccess;
   hipLaunchKernelGGL(k_ulsch_deinterleave, dim3((max_bits + 255) / 256, (unsigned)n), dim3(256), 0, st,
-                     d_items, q, g);
+                     d_items, q, g, c);
   return hipGetLastError();
 }
 

@@ -17,66 +17,9 @@
 
 #include "gmem.h"
 #include "srsgpu/viterbi_batch.h"
+#include "viterbi_dev.h"
 
 namespace srsgpu {
-
-__device__ __forceinline__ int vparity(int x) { return __popc((unsigned)x) & 1; }
-
-// One tail-biting frame of F bits on one wavefront: symbols at sym (3F floats, global or LDS),
-// decoded bits (the middle copy) into bits[0..F) in LDS. q / dec are LDS scratch.
-__device__ __forceinline__ void vit_frame(const float *sym, int F, uint8_t *bits, uint16_t *q,
-                                          uint64_t *dec) {
-  const int lane = threadIdx.x, len = 3 * F, nb = 3 * F;
-  // max |x| (viterbi.c:531-536: float max starting at -9e9, fabs compared in double)
-  float mx = -9e9f;
-  for (int i = lane; i < len; i += 64) mx = fmaxf(mx, fabsf(sym[i]));
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  const float gain = __fdiv_rn(1000.0f, mx);
-  for (int i = lane; i < len; i += 64) {
-    const float v = __fadd_rn(32767.5f, __fmul_rn(gain, sym[i]));
-    long t = (v == v && v >= -9.2e18f && v < 9.2e18f) ? (long)v : (long)INT64_MIN; // cvttss2si
-    t = t < 0 ? 0 : t > 65535 ? 65535 : t;
-    q[i] = (uint16_t)t;
-  }
-  for (int i = lane; i < 8; i += 64) dec[nb + i] = 0; // chainback reads up to 6 past the end
-  __syncthreads();
-  const int b = lane >> 1, h = lane & 1;
-  const uint32_t B0 = vparity((2 * b) & 0x6D) ? 65535u : 0u;
-  const uint32_t B1 = vparity((2 * b) & 0x4F) ? 65535u : 0u;
-  const uint32_t B2 = vparity((2 * b) & 0x57) ? 65535u : 0u;
-  uint32_t m = 63; // this lane's state metric (uint16 held in 32 bits)
-  int k = 0;       // t mod F
-  for (int t = 0; t < nb; t++) {
-    const uint32_t s0 = q[3 * k], s1 = q[3 * k + 1], s2 = q[3 * k + 2];
-    if (++k == F) k = 0;
-    const uint32_t m0a = ((B0 ^ s0) + (B1 ^ s1) + 1) >> 1;
-    const uint32_t metric = (((B2 ^ s2) + m0a + 1) >> 1) >> 3;
-    const uint32_t mm = (8191u - metric) & 0xFFFFu;
-    const uint32_t ob = (uint32_t)__shfl((int)m, b), ob32 = (uint32_t)__shfl((int)m, b + 32);
-    // h = 0: m0 = ob + metric vs m1 = ob32 + mm; h = 1: m2 = ob + mm vs m3 = ob32 + metric
-    const uint32_t a = (ob + (h ? mm : metric)) & 0xFFFFu;
-    const uint32_t c = (ob32 + (h ? metric : mm)) & 0xFFFFu;
-    const bool d = (int16_t)(uint16_t)(a - c) > 0;
-    m = d ? c : a;
-    const uint64_t w = __ballot(d);
-    if (lane == 0) dec[t] = w;
-  }
-  // best end state: the last index holding the minimum metric
-  uint32_t mn = m;
-  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-  int best = m == mn ? lane : -1;
-  for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o));
-  __syncthreads();
-  if (lane == 0) {
-    uint32_t es = (uint32_t)best << 2;
-    for (int t = nb - 1; t >= 0; t--) {
-      const uint32_t bit = (uint32_t)((dec[t + 6] >> (es >> 2)) & 1u);
-      es = (es >> 1) | (bit << 7);
-      if (t >= F && t < 2 * F) bits[t - F] = (uint8_t)bit;
-    }
-  }
-  __syncthreads();
-}
 
 __global__ __launch_bounds__(64) void k_viterbi37_tb(const srsgpu_viterbi_frame_t *__restrict__ frames,
                                                      int nframes, const float *__restrict__ sym_base,
@@ -98,10 +41,6 @@ __global__ __launch_bounds__(64) void k_viterbi37_tb(const srsgpu_viterbi_frame_
 // mean |llr| check (double, in order), srslte_rm_conv_rx (rm_conv.c:99-157), the Viterbi frame
 // of nof_bits + 16, CRC16 remainder. One wavefront per candidate; the sequential parts (the mean,
 // the bit collection whose soft combining adds in input order) on lane 0.
-__constant__ uint8_t kPermCC[32] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
-                                    0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
-__constant__ uint8_t kPermCCInv[32] = {16, 0, 24, 8, 20, 4, 28, 12, 18, 2, 26, 10, 22, 6, 30, 14,
-                                       17, 1, 25, 9, 21, 5, 29, 13, 19, 3, 27, 11, 23, 7, 31, 15};
 
 __global__ __launch_bounds__(64) void k_dci_decode(const srsgpu_dci_cand_t *__restrict__ cands, int n,
                                                    const float *__restrict__ llr_base,

@@ -82,6 +82,22 @@ class srsgpu_ulsch_tb_t(ctypes.Structure):
                 ("data_offset", ctypes.c_uint64)]
 
 
+UCI_MAX_CQI_BITS = 183
+
+
+class srsgpu_uci_cfg_t(ctypes.Structure):
+    """include/srsgpu/ulsch_batch.h"""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("O_ack", "O_ri", "O_cqi", "I_offset_ack", "I_offset_ri",
+                                                 "I_offset_cqi", "M_sc", "M_sc_init")] + [("c_offset", ctypes.c_uint64)]
+
+
+class srsgpu_uci_result_t(ctypes.Structure):
+    """include/srsgpu/ulsch_batch.h"""
+    _fields_ = [("ack", ctypes.c_uint8 * 2), ("ri", ctypes.c_uint8), ("cqi_ack", ctypes.c_uint8),
+                ("cqi", ctypes.c_uint8 * (UCI_MAX_CQI_BITS + 1)), ("Q_ack", ctypes.c_uint32),
+                ("Q_ri", ctypes.c_uint32), ("Q_cqi", ctypes.c_uint32)]
+
+
 SOFTBUFFER_SIZE = 18600
 
 
@@ -275,6 +291,8 @@ _sig = {
     "srsgpu_ulsch_deinterleave_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), _u32, _vp, _vp]),
     "srsgpu_ulsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), _u32, _vp, _vp, _vp, _u32,
                                        _vp, _vp]),
+    "srsgpu_ulsch_uci_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_ulsch_tb_t), ctypes.POINTER(srsgpu_uci_cfg_t),
+                                           _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "srsgpu_dlsch_decode_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32, _vp, _vp, _u32,
                                        _vp, _vp]),
     "srsgpu_dlsch_decode": (_i32, [_vp, ctypes.POINTER(srsgpu_dlsch_tb_t), _u32,
@@ -611,6 +629,20 @@ class Dlsch:
                               t["q_offset"], t["data_offset"]) for t in tbs_list])
         return _lib.srsgpu_ulsch_decode_dev(self.q, arr, len(tbs_list), _vp(d_q), _vp(d_g), _vp(d_data),
                                             max_halfits, _vp(d_ret), _vp(d_noi))
+
+    def ulsch_uci_decode_dev(self, tbs_list, uci_list, d_q, d_c, d_g, d_data, max_halfits, d_ret, d_noi, d_uci):
+        """srsgpu_ulsch_uci_decode_dev (srslte_pusch_decode's UCI and data steps): tbs_list as for
+        ulsch_decode_dev, uci_list of dicts O (ack, ri, cqi), I_off (ack, ri, cqi), M_sc, M_sc_init,
+        c_offset; d_q scrambled soft bits, d_c scrambling bytes, d_uci srsgpu_uci_result_t[n]"""
+        n = len(tbs_list)
+        arr = (srsgpu_ulsch_tb_t * n)(*[
+            srsgpu_ulsch_tb_t(t["tbs"], t["rv"], t["Qm"], t["nof_bits"], t["nof_symb"], t["softbuffer"],
+                              t["q_offset"], t["data_offset"]) for t in tbs_list])
+        ua = (srsgpu_uci_cfg_t * n)(*[
+            srsgpu_uci_cfg_t(u["O"][0], u["O"][1], u["O"][2], u["I_off"][0], u["I_off"][1], u["I_off"][2], u["M_sc"],
+                             u["M_sc_init"], u["c_offset"]) for u in uci_list])
+        return _lib.srsgpu_ulsch_uci_decode_dev(self.q, arr, ua, n, _vp(d_q), _vp(d_c), _vp(d_g), _vp(d_data),
+                                                max_halfits, _vp(d_ret), _vp(d_noi), _vp(d_uci))
 
     def read_cb_crc(self, slot):
         """cb_crc flags of softbuffer `slot` (the soft bits are not copied)"""

@@ -10,9 +10,8 @@
  * early stop, TB CRC). The decode runs on the DL-SCH object's softbuffers and decoder
  * (include/srsgpu/dlsch_batch.h), as the reference shares one srslte_sch_t.
  *
- * Not covered: UCI multiplexed on the PUSCH (ACK / RI / CQI, srslte_ulsch_uci_decode_ri_ack and
- * srslte_uci_decode_cqi_pusch); the data decode here is the uci_data = {0} case that
- * srslte_ulsch_decode runs.
+ * srsgpu_ulsch_decode_dev is the uci_data = {0} case that srslte_ulsch_decode runs;
+ * srsgpu_ulsch_uci_decode_dev below adds the UCI multiplexed on the PUSCH (HARQ-ACK, RI, CQI).
  */
 #ifndef SRSGPU_ULSCH_BATCH_H
 #define SRSGPU_ULSCH_BATCH_H
@@ -48,6 +47,43 @@ int srsgpu_ulsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint
  * unused): srslte_ulsch_decode of a PUSCH without data (tbs 0, sch.c:957-975) still writes g_bits. */
 int srsgpu_ulsch_deinterleave_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t nof_tb,
                                   const int16_t *d_q_bits, int16_t *d_g_bits);
+
+/* UCI multiplexed on the PUSCH (srslte_pusch_decode, lib/src/phy/phch/pusch.c:626-657, with
+ * srslte_ulsch_uci_decode_ri_ack / srslte_ulsch_uci_decode, sch.c:892-985, and uci.c): per TB
+ *   - HARQ-ACK (1-2 bits) and RI from the STILL SCRAMBLED q bits and the PUSCH sequence c, with the
+ *     reference's decoders (uci.c:746-790: Q' from the beta offsets, the bit positions of
+ *     uci_ulsch_interleave_ack_gen / _ri_gen, decode_ri_ack_1bit / _2bits as they are); the ACK
+ *     positions then count as zero;
+ *   - descrambling, then the channel deinterleaver with the RI positions taken out (sch.c:550-568,
+ *     860-881, the lut's write order included);
+ *   - CQI (srslte_uci_decode_cqi_pusch, uci.c:428-464): the (32, O) block code by ML up to 11 bits,
+ *     above that rate dematching, srslte_viterbi_decode_s and CRC8 (cqi_ack);
+ *   - the data (decode_tb on the G = H' - Q'_ri - Q'_cqi symbols after the CQI) when tbs > 0.
+ * q_bits are the scrambled soft bits (nof_bits per TB at q_offset, as srslte_pusch_decode holds them
+ * before srslte_scrambling_s_offset); d_c holds each TB's scrambling sequence, one byte per bit
+ * (srslte_sequence_t.c) at c_offset; d_g_bits receives the deinterleaved bits (CQI bits summed in
+ * place as the reference's short-CQI decoder leaves them). d_uci[i] receives TB i's UCI. Returns -1
+ * without launching anything on a reserved beta offset, an unsupported length, a matrix mismatch, or
+ * HARQ-ACK / RI positions beyond the reference's array (Q' Qm > 3456, srslte_sch_t.ack_ri_bits, sch.h:70:
+ * the reference writes past it). */
+#define SRSGPU_UCI_MAX_CQI_BITS 183 /* O_cqi + 8 within the 191-bit Viterbi frame */
+typedef struct {
+  uint32_t O_ack, O_ri, O_cqi;                    /* uci_ack_len (0-2), uci_ri_len (0-2), uci_cqi_len */
+  uint32_t I_offset_ack, I_offset_ri, I_offset_cqi; /* cfg->uci_cfg */
+  uint32_t M_sc, M_sc_init;                       /* cfg->grant */
+  uint64_t c_offset;                              /* the TB's scrambling sequence in d_c */
+} srsgpu_uci_cfg_t;
+typedef struct {
+  uint8_t ack[2];  /* uci_ack, uci_ack_2 */
+  uint8_t ri;      /* uci_ri */
+  uint8_t cqi_ack; /* CRC8 of a CQI above 11 bits checked */
+  uint8_t cqi[SRSGPU_UCI_MAX_CQI_BITS + 1]; /* uci_cqi, one bit per byte */
+  uint32_t Q_ack, Q_ri, Q_cqi; /* Q' of each (the data starts at Q_cqi Qm in g) */
+} srsgpu_uci_result_t;
+int srsgpu_ulsch_uci_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, const srsgpu_uci_cfg_t *uci,
+                                uint32_t nof_tb, const int16_t *d_q_bits, const uint8_t *d_c, int16_t *d_g_bits,
+                                uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi,
+                                srsgpu_uci_result_t *d_uci);
 
 #ifdef __cplusplus
 }

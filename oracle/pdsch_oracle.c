@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "dlsch_oracle.h"
 #include "pdsch_oracle.h"
 
 /* ---------------------------------------------------------------- RE extraction ---------- */
@@ -695,17 +696,15 @@ static int orc_parity(int x) {
   return x & 1;
 }
 
+static int orc_vit_core(uint16_t *q, uint32_t F, uint8_t *out);
 int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
-  const int poly[3] = {0x6D, 0x4F, 0x57};
-  const uint32_t len = 3 * F, nb = 3 * F;
+  const uint32_t len = 3 * F;
   float mx = -9e9f;
   for (uint32_t i = 0; i < len; i++)
     if (fabs(sym[i]) > mx) mx = (float)fabs(sym[i]);
   const float gain = 1000.0f / mx;
   uint16_t *q = malloc(len * sizeof(uint16_t));
-  uint64_t *dec = calloc(nb + 6, sizeof(uint64_t));
-  uint8_t *tmp = malloc(nb);
-  if (!q || !dec || !tmp) return -1;
+  if (!q) return -1;
   for (uint32_t i = 0; i < len; i++) {
     const float v = 32767.5f + gain * sym[i];
     long t = (v == v && v >= -9.2e18f && v < 9.2e18f) ? (long)v : LONG_MIN; /* cvttss2si 64 */
@@ -713,6 +712,30 @@ int orc_viterbi37_tb_decode_f(const float *sym, uint32_t F, uint8_t *out) {
     if (t > 65535) t = 65535;
     q[i] = (uint16_t)t;
   }
+  return orc_vit_core(q, F, out);
+}
+
+/* srslte_viterbi_decode_s on the same decoder (viterbi.c:558-584 with VITERBI_16): srslte_vec_quant_sus
+ * (vector.c:450-460) with gain 1 and offset 32767, i.e. tmp = (int16_t)(32767 + (float)x) -- the float
+ * converted as cvttss2si to 32 bits then truncated to 16 -- and 0 where that is negative: x <= 0 gives
+ * 32767 + x (0 for x = -32768), x > 0 wraps negative and gives 0. Then decode37_avx2_16bit. */
+int orc_viterbi37_tb_decode_s(const int16_t *sym, uint32_t F, uint8_t *out) {
+  uint16_t *q = malloc(3 * F * sizeof(uint16_t));
+  if (!q) return -1;
+  for (uint32_t i = 0; i < 3 * F; i++) {
+    const int16_t t = (int16_t)(int32_t)(32767.0f + (float)sym[i] * 1.0f);
+    q[i] = (uint16_t)(t < 0 ? 0 : t);
+  }
+  return orc_vit_core(q, F, out);
+}
+
+/* the tail-biting trellis of decode37_avx2_16bit on quantised symbols q (3F, freed here) */
+static int orc_vit_core(uint16_t *q, uint32_t F, uint8_t *out) {
+  const int poly[3] = {0x6D, 0x4F, 0x57};
+  const uint32_t nb = 3 * F;
+  uint64_t *dec = calloc(nb + 6, sizeof(uint64_t));
+  uint8_t *tmp = malloc(nb);
+  if (!dec || !tmp) return -1;
   uint16_t B[3][32];
   for (int st = 0; st < 32; st++)
     for (int j = 0; j < 3; j++) B[j][st] = orc_parity((2 * st) & poly[j]) ? 65535 : 0;
@@ -889,5 +912,218 @@ int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, ui
   }
   *cfi = (uint32_t)index + 1;
   *corr = mx;
+  return 0;
+}
+
+/* ---------------------------------------------------------------- UCI on the PUSCH ---------- */
+/* srslte_pusch_decode's UCI steps (pusch.c:626-657) on a TB's q soft bits, still scrambled (q_in,
+ * nof_bits int16) with the PUSCH sequence c (one byte per bit):
+ *  1. HARQ-ACK (O[0] = 1 or 2 bits) and RI (O[1]) from the scrambled bits, srslte_uci_decode_ack_ri
+ *     (uci.c:746-790): Q' = min(ceilf((float)O M_sc_init N_symb beta / K), 4 M_sc) (uci.c:548-572; K
+ *     the TB's C1 K1 + C2 K2, or O_cqi (+8 above 11 bits) without data; beta / beta_cqi without data);
+ *     bit group i at row H'/N - 1 - i/4, column {2,3,8,9} (ACK) or {1,4,7,10} (RI)[(3i) mod 4]
+ *     (uci.c:499-546); one bit: the sum of -(q0 + q1) with q = c[p0] ? q : -q for BOTH positions
+ *     (decode_ri_ack_1bit reads c at p0 twice, uint32 arithmetic); two bits: the groups in threes,
+ *     each triple added when the loop reaches the next multiple of 3 (so a last, complete or partial,
+ *     triple is never added); bit = sum > 0. The ACK positions are then zeroed (sch.c:921-924).
+ *  2. descrambling, q = c ? -q : q (int16, srslte_scrambling_s_offset);
+ *  3. the channel deinterleaver with the RI positions taken out (sch.c:550-568, 860-881): entries
+ *     numbered row by row skipping RI, g[lut[x]] = q[x] in q order with the RI entries' lut = 0, so
+ *     g[0] ends as the RI entry with the largest q index when there is one;
+ *  4. CQI (O[2] bits, srslte_uci_decode_cqi_pusch uci.c:428-464): Q' = min(ceilf((float)(O + L)
+ *     M_sc_init N_symb beta / K), M_sc N_symb - Q'_ri), L = 8 from 11 bits on (O < 11: 0), 999999 for
+ *     K = 0; up to 11 bits the (32, O) block code by ML (uci.c:312-351): copies of 32 summed into
+ *     g[0..32) (int16 wrap), then per word w the correlation with the +-1 code word over min(32, Q')
+ *     as srslte_vec_dot_prod_sss computes it (16 int16 lanes of mullo + add with wrap, summed, then
+ *     an int tail), the first maximum wins, bits MSB first; above 11 bits srslte_rm_conv_rx_s,
+ *     srslte_viterbi_decode_s over O + 8 bits and CRC8 0x19B, the CQI taken only when it checks.
+ * out: ack[0], ack[1], ri, cqi_ack, then the O[2] CQI bits; g: nof_bits deinterleaved bits;
+ * qp: Q'_ack, Q'_ri, Q'_cqi (the data bits start at Q'_cqi Qm, G = nof_bits - (Q'_ri + Q'_cqi) Qm).
+ * Returns -1 on a reserved beta index, a CQI longer than 183 bits, or HARQ-ACK / RI bits beyond the
+ * reference's position array (srslte_sch_t.ack_ri_bits[12 * 288], sch.h:70: Q' Qm above 3456 writes past
+ * it, so such a configuration has no defined result). */
+#include "srsgpu/uci_tables.h"
+
+static uint32_t uci_qp_ack_ri(uint32_t O, uint32_t O_cqi, float beta, uint32_t K, uint32_t M_sc,
+                              uint32_t M_sc_init, uint32_t nsymb) {
+  if (K == 0) K = O_cqi <= 11 ? O_cqi : O_cqi + 8;
+  const uint32_t x = (uint32_t)ceilf((float)O * M_sc_init * nsymb * beta / K);
+  return x < 4 * M_sc ? x : 4 * M_sc;
+}
+
+static uint32_t uci_pos(uint32_t i, uint32_t k, uint32_t Qm, uint32_t rows, int ri) {
+  static const uint32_t ack_cols[4] = {2, 3, 8, 9}, ri_cols[4] = {1, 4, 7, 10};
+  const uint32_t row = rows - 1 - i / 4, col = (ri ? ri_cols : ack_cols)[(3 * i) % 4];
+  return row * Qm + rows * col * Qm + k;
+}
+
+static void uci_ack_ri(const int16_t *q, const uint8_t *c, uint32_t Qp, uint32_t O, uint32_t Qm, uint32_t rows,
+                       int ri, uint8_t *data) {
+  int32_t sum[3] = {0, 0, 0};
+  for (uint32_t i = 0; i < Qp; i++) {
+    if (O == 2 && i % 3 == 0 && i > 0) {
+      int32_t v[6];
+      for (int g = 0; g < 3; g++)
+        for (int k = 0; k < 2; k++) {
+          const uint32_t p = uci_pos(i - 3 + g, k, Qm, rows, ri);
+          v[2 * g + k] = c[p] ? q[p] : -q[p];
+        }
+      sum[0] -= v[0] + v[3];
+      sum[1] -= v[1] + v[4];
+      sum[2] -= v[2] + v[5];
+    } else if (O == 1) {
+      const uint32_t p0 = uci_pos(i, 0, Qm, rows, ri), p1 = uci_pos(i, 1, Qm, rows, ri);
+      const uint32_t q0 = c[p0] ? q[p0] : -q[p0], q1 = c[p0] ? q[p1] : -q[p1];
+      sum[0] = (int32_t)((uint32_t)sum[0] + (uint32_t)(-(q0 + q1)));
+    }
+  }
+  data[0] = sum[0] > 0;
+  if (O == 2) data[1] = sum[1] > 0;
+}
+
+static uint32_t orc_crc8_bits(const uint8_t *b, uint32_t n) {
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t fb = ((r >> 7) & 1) ^ (b[i] & 1);
+    r = (r << 1) & 0xFF;
+    if (fb) r ^= 0x9B;
+  }
+  return r;
+}
+
+int orc_ulsch_uci(uint32_t tbs, uint32_t Qm, uint32_t nof_bits, uint32_t nsymb, uint32_t M_sc, uint32_t M_sc_init,
+                  const uint32_t *I_off, const uint32_t *O, const int16_t *q_in, const uint8_t *c, uint8_t *out,
+                  int16_t *g, uint32_t *qp) {
+  const uint32_t Hp = nof_bits / Qm, rows = Hp / nsymb, O_ack = O[0], O_ri = O[1], O_cqi = O[2];
+  uint32_t K = 0;
+  if (tbs) {
+    orc_cbsegm_t sg;
+    if (orc_segm(tbs, &sg)) return -1;
+    K = sg.C1 * sg.K1 + sg.C2 * sg.K2;
+  }
+  if (O_cqi + 8 > 191 || O_ack > 2 || O_ri > 2) return -1;
+  int16_t *q = malloc((nof_bits + 64) * sizeof(int16_t));
+  uint8_t *ri_at = calloc(nof_bits + 64, 1);
+  memcpy(q, q_in, nof_bits * sizeof(int16_t));
+  memset(out, 0, 4 + O_cqi);
+  uint32_t Q_ack = 0, Q_ri = 0, Q_cqi = 0;
+  const float bcqi = SRSGPU_BETA_CQI[I_off[2] & 15];
+  if (O_ack) {
+    float beta = SRSGPU_BETA_ACK[I_off[0] & 15];
+    if (!tbs) beta /= bcqi;
+    if (beta < 0) return -1;
+    Q_ack = uci_qp_ack_ri(O_ack, O_cqi, beta, K, M_sc, M_sc_init, nsymb);
+    if (Q_ack * Qm > 12 * 288) return -1;
+    uci_ack_ri(q, c, Q_ack, O_ack, Qm, rows, 0, out);
+    for (uint32_t i = 0; i < Q_ack; i++)
+      for (uint32_t k = 0; k < Qm; k++) q[uci_pos(i, k, Qm, rows, 0)] = 0;
+  }
+  if (O_ri) {
+    float beta = SRSGPU_BETA_RI[I_off[1] & 15];
+    if (!tbs) beta /= bcqi;
+    if (beta < 0) return -1;
+    Q_ri = uci_qp_ack_ri(O_ri, O_cqi, beta, K, M_sc, M_sc_init, nsymb);
+    if (Q_ri * Qm > 12 * 288) return -1;
+    uint8_t ri[2] = {0, 0};
+    uci_ack_ri(q, c, Q_ri, O_ri, Qm, rows, 1, ri);
+    out[2] = ri[0];
+    for (uint32_t i = 0; i < Q_ri; i++)
+      for (uint32_t k = 0; k < Qm; k++) ri_at[uci_pos(i, k, Qm, rows, 1)] = 1;
+  }
+  for (uint32_t x = 0; x < nof_bits; x++) q[x] = c[x] ? (int16_t)-q[x] : q[x];
+  uint32_t idx = 0, x0 = 0, xr = 0;
+  int any_ri = 0;
+  for (uint32_t j = 0; j < rows; j++)
+    for (uint32_t i = 0; i < nsymb; i++)
+      for (uint32_t k = 0; k < Qm; k++) {
+        const uint32_t x = j * Qm + i * rows * Qm + k;
+        if (!ri_at[x]) {
+          if (idx == 0) x0 = x;
+          g[idx++] = q[x];
+        } else {
+          any_ri = 1;
+          if (x > xr) xr = x;
+        }
+      }
+  if (any_ri) g[0] = q[xr > x0 ? xr : x0]; /* the last of the writes to g[0], in q order */
+  if (O_cqi) {
+    if (bcqi < 0) return -1;
+    const uint32_t L = O_cqi < 11 ? 0 : 8;
+    uint32_t x = 999999;
+    if (K > 0) x = (uint32_t)ceilf((float)(O_cqi + L) * M_sc_init * nsymb * bcqi / K);
+    const uint32_t lim = M_sc * nsymb - Q_ri;
+    Q_cqi = x < lim ? x : lim;
+    const uint32_t Q = Q_cqi * Qm;
+    if (O_cqi <= 11) {
+      if (Q > 32) {
+        uint32_t i = 1;
+        for (; i < Q / 32; i++)
+          for (int k = 0; k < 32; k++) g[k] = (int16_t)(g[k] + g[i * 32 + k]);
+        for (uint32_t k = 0; k < Q % 32; k++) g[k] = (int16_t)(g[k] + g[i * 32 + k]);
+      }
+      const uint32_t len = Q < 32 ? Q : 32;
+      uint32_t best = 0;
+      int32_t bmax = INT32_MIN;
+      for (uint32_t w = 0; w < (1u << O_cqi); w++) {
+        int16_t cw[32];
+        for (int i = 0; i < 32; i++) {
+          uint32_t b = 0;
+          for (uint32_t n = 0; n < O_cqi; n++) b ^= ((w >> (O_cqi - 1 - n)) & 1) & SRSGPU_CQI_BASIS[i][n];
+          cw[i] = (int16_t)(2 * b - 1);
+        }
+        int16_t lane[16] = {0};
+        uint32_t i = 0;
+        for (; i + 16 <= len; i += 16)
+          for (int k = 0; k < 16; k++) lane[k] = (int16_t)(lane[k] + (int16_t)(cw[i + k] * g[i + k]));
+        int32_t corr = 0;
+        for (int k = 0; k < 16; k++) corr += lane[k];
+        for (; i < len; i++) corr += cw[i] * g[i];
+        if (corr > bmax) {
+          bmax = corr;
+          best = w;
+        }
+      }
+      for (uint32_t n = 0; n < O_cqi; n++) out[4 + n] = (uint8_t)((best >> (O_cqi - 1 - n)) & 1);
+    } else {
+      /* srslte_rm_conv_rx_s (rm_conv.c:166-223) to 3 (O + 8) soft bits */
+      const uint32_t out_len = 3 * (O_cqi + 8);
+      const int nrows = (int)((out_len / 3 - 1) / 32 + 1), K_p = nrows * 32;
+      int ndummy = K_p - (int)(out_len / 3);
+      if (ndummy < 0) ndummy = 0;
+      int16_t tmp[3 * 32 * 32], rm[3 * 200];
+      for (int i = 0; i < 3 * K_p; i++) tmp[i] = 10000;
+      uint32_t k = 0;
+      int j = 0;
+      while (k < Q) {
+        const int d_i = (j % K_p) / nrows, d_j = (j % K_p) % nrows;
+        if (d_j * 32 + RM_PERM_CC[d_i] >= ndummy) {
+          if (tmp[j] == 10000)
+            tmp[j] = g[k];
+          else if (g[k] != 10000)
+            tmp[j] = (int16_t)(tmp[j] + g[k]);
+          k++;
+        }
+        if (++j == 3 * K_p) j = 0;
+      }
+      for (uint32_t i = 0; i < out_len / 3; i++) {
+        const int d_i = (int)(i + ndummy) / 32, d_j = (int)(i + ndummy) % 32;
+        for (int s = 0; s < 3; s++) {
+          const int16_t o = tmp[K_p * s + RM_PERM_CC_INV[d_j] * nrows + d_i];
+          rm[i * 3 + s] = o != 10000 ? o : 0;
+        }
+      }
+      uint8_t bits[200];
+      if (orc_viterbi37_tb_decode_s(rm, O_cqi + 8, bits)) return -1;
+      if (orc_crc8_bits(bits, O_cqi + 8) == 0) {
+        out[3] = 1;
+        memcpy(out + 4, bits, O_cqi);
+      }
+    }
+  }
+  qp[0] = Q_ack;
+  qp[1] = Q_ri;
+  qp[2] = Q_cqi;
+  free(q);
+  free(ri_at);
   return 0;
 }

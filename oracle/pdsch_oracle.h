@@ -35,6 +35,11 @@ int orc_pcfich_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t *idx);
 int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx,
                       const float *const *y, const float *const *h, float noise, uint32_t sf_idx,
                       uint32_t *cfi, float *corr);
+/* UCI on the PUSCH: HARQ-ACK / RI / CQI and the deinterleaved g bits (see pdsch_oracle.c) */
+int orc_viterbi37_tb_decode_s(const int16_t *sym, uint32_t F, uint8_t *out);
+int orc_ulsch_uci(uint32_t tbs, uint32_t Qm, uint32_t nof_bits, uint32_t nsymb, uint32_t M_sc, uint32_t M_sc_init,
+                  const uint32_t *I_off, const uint32_t *O, const int16_t *q_in, const uint8_t *c, uint8_t *out,
+                  int16_t *g, uint32_t *qp);
 /* 8-bit LLR chain (llr_is_8bit) */
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);

@@ -304,6 +304,111 @@ int ref_ulsch_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t 
   return r;
 }
 
+/* ---------------------------------------------------------------- UCI on the PUSCH ---------- */
+#include "srslte/phy/common/sequence.h"
+#include "srslte/phy/phch/uci.h"
+#include "srslte/phy/scrambling/scrambling.h"
+/* the PUSCH configuration fields the UCI multiplexing reads (uci.c:270-290, 548-572): grant M_sc /
+ * M_sc_init, the beta offset indices (36.213 Table 8.6.3-1..3), normal CP */
+static void ref_uci_cfg(srslte_pusch_cfg_t *cfg, uint32_t M_sc, uint32_t M_sc_init, const uint32_t *I_off) {
+  cfg->grant.M_sc = M_sc;
+  cfg->grant.M_sc_init = M_sc_init;
+  cfg->uci_cfg.I_offset_ack = I_off[0];
+  cfg->uci_cfg.I_offset_ri = I_off[1];
+  cfg->uci_cfg.I_offset_cqi = I_off[2];
+  cfg->cp = SRSLTE_CP_NORM;
+}
+
+/* srslte_ulsch_uci_encode (sch.c:994-1090): data (tbs/8 bytes, tbs may be 0) with HARQ-ACK (O[0] bits
+ * ack[]), RI (O[1] bits, ri) and CQI (O[2] bits cqi[], one per byte) -> packed q bits (nof_bits) */
+int ref_ulsch_uci_encode(uint32_t tbs, uint32_t Qm, uint32_t nof_bits, uint32_t nof_symb, uint32_t M_sc,
+                         uint32_t M_sc_init, const uint32_t *I_off, const uint32_t *O, const uint8_t *ack,
+                         uint32_t ri, const uint8_t *cqi, const uint8_t *data, uint8_t *q_packed, uint32_t nof_prb) {
+  if (ref_sch_get()) return -1;
+  srslte_softbuffer_tx_t sb;
+  if (srslte_softbuffer_tx_init(&sb, nof_prb)) return -1;
+  srslte_softbuffer_tx_reset(&sb);
+  uint8_t *d = calloc(tbs / 8 + 16, 1);
+  uint8_t *g = calloc(nof_bits / 8 + 64, 1);
+  if (tbs) memcpy(d, data, tbs / 8);
+  srslte_pusch_cfg_t cfg;
+  ref_ul_cfg(&cfg, tbs, 0, Qm, nof_bits, nof_symb);
+  ref_uci_cfg(&cfg, M_sc, M_sc_init, I_off);
+  srslte_uci_data_t u;
+  memset(&u, 0, sizeof(u));
+  u.uci_ack_len = O[0];
+  u.uci_ack = ack[0];
+  u.uci_ack_2 = ack[1];
+  u.uci_ri_len = O[1];
+  u.uci_ri = (uint8_t)ri;
+  u.uci_cqi_len = O[2];
+  for (uint32_t i = 0; i < O[2]; i++) u.uci_cqi[i] = cqi[i];
+  const int r = srslte_ulsch_uci_encode(&ref_sch, &cfg, &sb, d, u, g, q_packed);
+  free(d);
+  free(g);
+  srslte_softbuffer_tx_free(&sb);
+  return r;
+}
+
+/* srslte_pusch_decode's UCI and data steps on received soft bits (pusch.c:626-657): HARQ-ACK and RI
+ * from the still scrambled q bits with the sequence c (srslte_ulsch_uci_decode_ri_ack, sch.c:892-942),
+ * descrambling (srslte_scrambling_s_offset), then srslte_ulsch_uci_decode (sch.c:944-985): the channel
+ * deinterleaver without the RI positions, CQI (srslte_uci_decode_cqi_pusch) and the UL-SCH data on the
+ * HARQ slot's softbuffer when tbs > 0. q: nof_bits int16 (scrambled), c: one byte per bit.
+ * out: ack[0], ack[1], ri, cqi_ack, then the O[2] CQI bits; g_out: the deinterleaved g bits
+ * (nof_bits). Returns srslte_ulsch_uci_decode's value (or the ri/ack step's error). */
+int ref_ulsch_uci_decode(int slot, uint32_t tbs, uint32_t rv, uint32_t Qm, uint32_t nof_bits, uint32_t nof_symb,
+                         uint32_t M_sc, uint32_t M_sc_init, const uint32_t *I_off, const uint32_t *O,
+                         const int16_t *q_bits, const uint8_t *c, uint8_t *data, uint32_t max_halfits, uint32_t *noi,
+                         uint8_t *cb_crc, uint8_t *out, int16_t *g_out) {
+  if (ref_sch_get()) return -100;
+  if (tbs && (slot < 0 || slot >= REF_NSLOT || !ref_sbrx_ready[slot])) return -100;
+  srslte_pusch_cfg_t cfg;
+  ref_ul_cfg(&cfg, tbs, rv, Qm, nof_bits, nof_symb);
+  ref_uci_cfg(&cfg, M_sc, M_sc_init, I_off);
+  srslte_sch_set_max_noi(&ref_sch, max_halfits);
+  srslte_uci_data_t u;
+  memset(&u, 0, sizeof(u));
+  u.uci_ack_len = O[0];
+  u.uci_ri_len = O[1];
+  u.uci_cqi_len = O[2];
+  int16_t *q = NULL, *g = NULL;
+  short *cs = NULL;
+  uint8_t *cc = NULL;
+  if (posix_memalign((void **)&q, 64, (nof_bits + 64) * sizeof(int16_t))) return -100;
+  if (posix_memalign((void **)&g, 64, (nof_bits + 64) * sizeof(int16_t))) return -100;
+  if (posix_memalign((void **)&cs, 64, (nof_bits + 64) * sizeof(short))) return -100;
+  if (posix_memalign((void **)&cc, 64, nof_bits + 64)) return -100;
+  memcpy(q, q_bits, nof_bits * sizeof(int16_t));
+  memset(g, 0, (nof_bits + 64) * sizeof(int16_t));
+  memcpy(cc, c, nof_bits);
+  for (uint32_t i = 0; i < nof_bits; i++) cs[i] = c[i] ? -1 : 1; /* sequence.c: c_short = 1 - 2c */
+  srslte_sequence_t seq;
+  memset(&seq, 0, sizeof(seq));
+  seq.c = cc;
+  seq.c_short = cs;
+  seq.cur_len = seq.max_len = nof_bits;
+  srslte_softbuffer_rx_t *sb = tbs ? &ref_sbrx[slot] : NULL;
+  int r = srslte_ulsch_uci_decode_ri_ack(&ref_sch, &cfg, sb, q, cc, &u);
+  if (!r) {
+    srslte_scrambling_s_offset(&seq, q, 0, nof_bits);
+    r = srslte_ulsch_uci_decode(&ref_sch, &cfg, sb, q, g, data, &u);
+  }
+  out[0] = u.uci_ack;
+  out[1] = u.uci_ack_2;
+  out[2] = u.uci_ri;
+  out[3] = u.cqi_ack;
+  for (uint32_t i = 0; i < O[2]; i++) out[4 + i] = u.uci_cqi[i];
+  if (g_out) memcpy(g_out, g, nof_bits * sizeof(int16_t));
+  *noi = tbs ? srslte_sch_last_noi(&ref_sch) : 0;
+  for (uint32_t i = 0; tbs && i < cfg.cb_segm.C && cb_crc; i++) cb_crc[i] = ref_sbrx[slot].cb_crc[i];
+  free(q);
+  free(g);
+  free(cs);
+  free(cc);
+  return r;
+}
+
 /* ---------------------------------------------------------------- PDSCH front-end ---------- */
 #include "srslte/phy/mimo/precoding.h"
 #include "srslte/phy/modem/demod_soft.h"

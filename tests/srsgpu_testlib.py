@@ -313,6 +313,76 @@ class Ref(_Lib):
         C = self.cbsegm(tbs)[0]
         return r, data, noi.value, crc[:C]
 
+    # ---- UCI on the PUSCH (srslte_ulsch_uci_encode / the srslte_pusch_decode UCI steps) ----
+    def uci_encode(self, u, data=None, nof_prb=100):
+        """u: uci_case() dict -> unpacked q bits (UL-SCH with HARQ-ACK / RI / CQI multiplexed)"""
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.ref_ulsch_uci_encode.argtypes = [u32] * 6 + [_u32p, _u32p, _u8p, u32, _u8p, _u8p, _u8p, u32]
+        data = np.ascontiguousarray(data if data is not None else np.zeros(8, np.uint8), np.uint8)
+        q = np.zeros((u["nof_bits"] + 7) // 8 + 8, np.uint8)
+        I, O = np.array(u["I_off"], np.uint32), np.array(u["O"], np.uint32)
+        ack, cqi = np.array(u["ack"], np.uint8), np.array(list(u["cqi"]) + [0], np.uint8)
+        r = L.ref_ulsch_uci_encode(u["tbs"], u["Qm"], u["nof_bits"], u["nof_symb"], u["M_sc"], u["M_sc_init"],
+                                   _ptr(I, _u32p), _ptr(O, _u32p), _ptr(ack, _u8p), u["ri"], _ptr(cqi, _u8p),
+                                   _ptr(data, _u8p), _ptr(q, _u8p), nof_prb)
+        assert r == 0, r
+        return np.unpackbits(q)[:u["nof_bits"]]
+
+    def uci_decode(self, slot, u, q_scrambled, c, max_halfits=8):
+        """the reference's UCI + data decode of scrambled soft bits -> (ret, out[4 + O_cqi], g, data, noi, cb_crc)"""
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.ref_ulsch_uci_decode.argtypes = ([ctypes.c_int] + [u32] * 7 + [_u32p, _u32p, _i16p, _u8p, _u8p, u32, _u32p,
+                                           _u8p, _u8p, _i16p])
+        q = np.ascontiguousarray(q_scrambled, np.int16)
+        c = np.ascontiguousarray(c, np.uint8)
+        I, O = np.array(u["I_off"], np.uint32), np.array(u["O"], np.uint32)
+        data = np.zeros(u["tbs"] // 8 + 8, np.uint8)
+        out = np.zeros(4 + u["O"][2] + 4, np.uint8)
+        g = np.zeros(u["nof_bits"] + 8, np.int16)
+        noi = ctypes.c_uint32(0)
+        crc = np.zeros(64, np.uint8)
+        r = L.ref_ulsch_uci_decode(slot, u["tbs"], u["rv"], u["Qm"], u["nof_bits"], u["nof_symb"], u["M_sc"],
+                                   u["M_sc_init"], _ptr(I, _u32p), _ptr(O, _u32p), _ptr(q, _i16p), _ptr(c, _u8p),
+                                   _ptr(data, _u8p), max_halfits, ctypes.byref(noi), _ptr(crc, _u8p),
+                                   _ptr(out, _u8p), _ptr(g, _i16p))
+        C = self.cbsegm(u["tbs"])[0] if u["tbs"] else 0
+        return r, out[:4 + u["O"][2]], g[:u["nof_bits"]], data, noi.value, crc[:C]
+
+
+def uci_case(tbs, Qm, nof_prb_alloc, nof_symb=12, O=(1, 1, 0), I_off=(0, 2, 2), ack=(1, 0), ri=1, cqi=(), rv=0,
+             M_sc_init=None):
+    """a PUSCH configuration with UCI: M_sc = 12 nof_prb_alloc, H' = M_sc N_symb, nof_bits = H' Qm"""
+    M_sc = 12 * nof_prb_alloc
+    return dict(tbs=tbs, rv=rv, Qm=Qm, nof_symb=nof_symb, M_sc=M_sc, M_sc_init=M_sc_init or M_sc,
+                nof_bits=M_sc * nof_symb * Qm, O=tuple(O), I_off=tuple(I_off), ack=tuple(ack), ri=ri, cqi=tuple(cqi))
+
+
+def orc_ulsch_uci(oracle, u, q_scrambled, c):
+    """the oracle's UCI steps -> (ret, out[4 + O_cqi], g, (Q'_ack, Q'_ri, Q'_cqi))"""
+    L = oracle.lib
+    u32 = ctypes.c_uint32
+    L.orc_ulsch_uci.argtypes = [u32] * 6 + [_u32p, _u32p, _i16p, _u8p, _u8p, _i16p, _u32p]
+    q = np.ascontiguousarray(q_scrambled, np.int16)
+    c = np.ascontiguousarray(c, np.uint8)
+    I, O = np.array(u["I_off"], np.uint32), np.array(u["O"], np.uint32)
+    out = np.zeros(4 + u["O"][2] + 4, np.uint8)
+    g = np.zeros(u["nof_bits"] + 8, np.int16)
+    qp = np.zeros(3, np.uint32)
+    r = L.orc_ulsch_uci(u["tbs"], u["Qm"], u["nof_bits"], u["nof_symb"], u["M_sc"], u["M_sc_init"], _ptr(I, _u32p),
+                        _ptr(O, _u32p), _ptr(q, _i16p), _ptr(c, _u8p), _ptr(out, _u8p), _ptr(g, _i16p), _ptr(qp, _u32p))
+    return r, out[:4 + u["O"][2]], g[:u["nof_bits"]], tuple(int(v) for v in qp)
+
+
+def uci_rx(rng, q_bits, c, amp=40, sigma=25):
+    """received soft bits of transmitted q bits: LLR = (2b - 1) amp + noise (int16; srsLTE's soft
+    demapper gives bit 0 a negative value), then scrambled by c (negated where c = 1), as the PUSCH
+    receiver holds them before descrambling"""
+    llr = (2 * q_bits.astype(np.int32) - 1) * amp + np.round(rng.normal(0, sigma, q_bits.size)).astype(np.int32)
+    llr = np.clip(llr, -32768, 32767).astype(np.int16)
+    return np.where(c.astype(bool), -llr, llr).astype(np.int16)
+
 
 def have_ref():
     return os.path.exists(REF_SO)
