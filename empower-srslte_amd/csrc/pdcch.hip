@@ -312,8 +312,8 @@ extern "C" {
 
 int srsgpu_pdcch_create(srsgpu_pdcch_t **q, const srsgpu_cell_t *cell, uint32_t phich_length,
                         uint32_t phich_resources) {
-  if (!q || !cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || cell->nof_ports < 1 ||
-      cell->nof_ports > 2 || cell->nof_rx_ant < 1 || cell->nof_rx_ant > 2 || phich_length > 1 ||
+  if (!q || !cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || (cell->nof_ports != 1 &&
+      cell->nof_ports != 2 && cell->nof_ports != 4) || cell->nof_rx_ant < 1 || cell->nof_rx_ant > 2 || phich_length > 1 ||
       phich_resources > 3)
     return -1;
   srsgpu_pdcch *p = new srsgpu_pdcch;
@@ -368,8 +368,8 @@ void srsgpu_pdcch_destroy(srsgpu_pdcch_t *q) {
 
 int srsgpu_pdcch_cell_map(const srsgpu_cell_t *cell, uint32_t phich_length, uint32_t phich_resources,
                           uint32_t cfi, uint32_t *idx, uint32_t max, uint32_t *nof_cce) {
-  if (!cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || cell->nof_ports < 1 ||
-      cell->nof_ports > 2 || phich_length > 1 || phich_resources > 3 || cfi < 1 || cfi > 3)
+  if (!cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || (cell->nof_ports != 1 &&
+      cell->nof_ports != 2 && cell->nof_ports != 4) || phich_length > 1 || phich_resources > 3 || cfi < 1 || cfi > 3)
     return -1;
   std::vector<uint32_t> maps[3];
   uint32_t ncce[3];

@@ -896,7 +896,7 @@ hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const 
 // srslte_pcfich_decode_multi (pcfich.c:178-241) per subframe, one wavefront: lane j < 16
 // equalises RE j of the 16 PCFICH REs (regs.c:477-512 + :622-665: four REGs of symbol 0) with the
 // PDSCH equalisers above on the reference's paths for 16 <= 32 symbols (SISO: the C path with the
-// noise estimate, scaling 1; 2 ports: generic transmit diversity + layer demapping), demaps QPSK
+// noise estimate, scaling 1; 2 / 4 ports: generic transmit diversity + layer demapping), demaps QPSK
 // (x times (float) -sqrt 2, demod_soft.c:71-73) and descrambles (+-1, sequences.c:42-44); lane 0
 // correlates with the three CFI codewords as +-1 in order (pcfich.c:129-147, vector.c:359-366).
 __device__ __forceinline__ int cfi_bit(int c, int i) { // 36.212 Table 5.3.4-1: 011 / 101 / 110 repeated
@@ -927,7 +927,9 @@ __global__ __launch_bounds__(64) void k_pcfich(const PcfichItem *__restrict__ it
   t.scaling = 1.0f;
   t.inv_scaling = 1.0f;
   if (j < 16) {
-    const Eq e = nports == 2 ? equalise_txdiv(t, (uint32_t)j) : equalise(t, idx[j], (uint32_t)j);
+    const Eq e = nports == 4   ? equalise_txdiv4(t, (uint32_t)j)
+                 : nports == 2 ? equalise_txdiv(t, (uint32_t)j)
+                               : equalise(t, idx[j], (uint32_t)j);
     const float s2 = -1.41421354f; // (float) -sqrt(2)
     const uint32_t c = seq[it.sf_idx];
     float a0 = __fmul_rn(e.xr, s2), a1 = __fmul_rn(e.xi, s2);
@@ -966,7 +968,7 @@ hipError_t launch_pcfich(const PcfichItem *d_items, int n, const float2 *grid, c
 // srslte_pdcch_extract_llr_multi (pdcch.c:424-506) for many subframes, one thread per PDCCH
 // symbol j (blockIdx.y = subframe): the symbol is gathered at map[j] from every rx antenna's grid
 // and estimate (srslte_regs_pdcch_get), equalised on the reference's path for nof_symbols symbols
-// (1 port: srslte_predecoding_single_multi with noise_estimate / 2 and scaling 1; 2 ports:
+// (1 port: srslte_predecoding_single_multi with noise_estimate / 2 and scaling 1; 2 or 4 ports:
 // srslte_predecoding_diversity_multi + srslte_layerdemap_diversity), QPSK soft-demapped as float
 // (demod_qpsk_lte: x (float) -sqrt(2), demod_soft.c:75-77) and descrambled
 // (srslte_scrambling_f_offset: a product with +-1, scrambling.c:39-42).
@@ -988,10 +990,10 @@ __global__ __launch_bounds__(256) void k_pdcch_llr(const PdcchItem *__restrict__
   t.map = it.map;
   t.nof_re = it.nof_symbols;
   t.nrx = nrx;
-  t.noise = nports == 2 ? 0.f : (it.dnoise ? *it.dnoise : it.noise) / 2;
+  t.noise = nports >= 2 ? 0.f : (it.dnoise ? *it.dnoise : it.noise) / 2;
   t.scaling = 1.0f;
   t.inv_scaling = 1.0f;
-  const Eq e = nports == 2 ? equalise_txdiv(t, j) : equalise(t, it.map[j], j);
+  const Eq e = nports == 4 ? equalise_txdiv4(t, j) : nports == 2 ? equalise_txdiv(t, j) : equalise(t, it.map[j], j);
   const float s2 = -1.41421354f; // (float) -sqrt(2)
   float a0 = __fmul_rn(e.xr, s2), a1 = __fmul_rn(e.xi, s2);
   const uint32_t b = 2 * j, w = it.c[b >> 5] >> (b & 31);

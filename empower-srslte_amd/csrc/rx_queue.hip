@@ -742,7 +742,7 @@ int srsgpu_rxq_create(srsgpu_rxq_t **q, const srsgpu_cell_t *cell, uint32_t symb
                       uint32_t nof_softbuffers, uint32_t max_batch, uint32_t max_wait_us,
                       uint32_t max_halfits) {
   if (!q || !cell || !symbol_sz || !max_batch || !max_halfits || cell->nof_rx_ant < 1 ||
-      cell->nof_rx_ant > 2 || cell->nof_ports < 1 || cell->nof_ports > 2)
+      cell->nof_rx_ant > 2 || (cell->nof_ports != 1 && cell->nof_ports != 2 && cell->nof_ports != 4))
     return -1;
   auto *r = new srsgpu_rxq();
   if (r->setup(cell, symbol_sz, nof_softbuffers, max_batch, max_wait_us, max_halfits)) {

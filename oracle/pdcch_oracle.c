@@ -170,6 +170,22 @@ static void orc_single_multi(const float *const *y, const float *const *h, uint3
   }
 }
 
+static int orc_pdcch_llr4(uint32_t nof_prb, uint32_t cell_id, uint32_t phich_len, uint32_t phich_res, uint32_t nrx,
+                          uint32_t cfi, uint32_t sf_idx, const float *const *gs, const float *const *hs, float *llr);
+int orc_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
+                  uint32_t phich_res, uint32_t nrx, uint32_t cfi, uint32_t sf_idx, float noise,
+                  const float *g0, const float *g1, const float *h00, const float *h01, const float *h10,
+                  const float *h11, float *llr);
+
+/* 4 ports as well: g [rx], h [port * 2 + rx] (4-port transmit diversity over the symbol quadruplets) */
+int orc_pdcch_llr_n(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res,
+                    uint32_t nrx, uint32_t cfi, uint32_t sf_idx, float noise, const float *const *g,
+                    const float *const *h, float *llr) {
+  if (nof_ports == 4) return orc_pdcch_llr4(nof_prb, cell_id, phich_len, phich_res, nrx, cfi, sf_idx, g, h, llr);
+  return orc_pdcch_llr(nof_prb, cell_id, nof_ports, phich_len, phich_res, nrx, cfi, sf_idx, noise, g[0], g[1], h[0],
+                       h[1], h[2], h[3], llr);
+}
+
 int orc_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
                   uint32_t phich_res, uint32_t nrx, uint32_t cfi, uint32_t sf_idx, float noise,
                   const float *g0, const float *g1, const float *h00, const float *h01, const float *h10,
@@ -213,6 +229,41 @@ int orc_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32
     free(ys[a]);
     for (uint32_t p = 0; p < 2; p++) free(hh[p][a]);
   }
+  free(d);
+  free(idx);
+  return 2 * nsym;
+}
+
+static int orc_pdcch_llr4(uint32_t nof_prb, uint32_t cell_id, uint32_t phich_len, uint32_t phich_res, uint32_t nrx,
+                          uint32_t cfi, uint32_t sf_idx, const float *const *gs, const float *const *hs, float *llr) {
+  uint32_t ncce;
+  uint32_t *idx = malloc(sizeof(uint32_t) * 36 * 110 * 4);
+  const int nsym = orc_pdcch_map(nof_prb, cell_id, 4, phich_len, phich_res, cfi, idx, &ncce);
+  if (nsym < 0 || nsym % 4) {
+    free(idx);
+    return -1;
+  }
+  float *ys[2], *hh[8], *d = malloc(sizeof(float) * 2 * (nsym + 1));
+  for (uint32_t a = 0; a < 2; a++) ys[a] = calloc(2 * (nsym + 1), sizeof(float));
+  for (int p = 0; p < 8; p++) hh[p] = calloc(2 * (nsym + 1), sizeof(float));
+  for (uint32_t a = 0; a < nrx; a++)
+    for (int i = 0; i < nsym; i++) {
+      memcpy(&ys[a][2 * i], &gs[a][2 * idx[i]], 8);
+      for (uint32_t p = 0; p < 4; p++) memcpy(&hh[p * 2 + a][2 * i], &hs[p * 2 + a][2 * idx[i]], 8);
+    }
+  const float *yy[2] = {ys[0], ys[1]}, *h4[8];
+  for (int p = 0; p < 8; p++) h4[p] = hh[p];
+  orc_predecode_txdiv4(yy, h4, (int)nrx, nsym, 1.0f, d, NULL); /* pdcch.c:495-496, no noise term */
+  uint8_t *c = malloc(2 * (size_t)nsym + 64);
+  orc_sequence(sf_idx * 512 + cell_id, 2 * (uint32_t)nsym, c);
+  const float s2 = (float)(-sqrt(2));
+  for (int i = 0; i < 2 * nsym; i++) {
+    const float v = d[i] * s2;
+    llr[i] = c[i] ? -v : v;
+  }
+  free(c);
+  for (uint32_t a = 0; a < 2; a++) free(ys[a]);
+  for (int p = 0; p < 8; p++) free(hh[p]);
   free(d);
   free(idx);
   return 2 * nsym;

@@ -864,7 +864,7 @@ int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, ui
       {1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1, 0, 1, 1}};
   uint32_t idx[16];
   orc_pcfich_re_map(nof_prb, cell_id, idx);
-  float ys[2][32], hs[2][2][32], d[32];
+  float ys[2][32], hs[4][2][32], d[32];
   for (uint32_t a = 0; a < nrx; a++)
     for (int i = 0; i < 16; i++) {
       ys[a][2 * i] = y[a][2 * idx[i]];
@@ -888,6 +888,12 @@ int orc_pcfich_decode(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, ui
       d[2 * i] = rr / den;
       d[2 * i + 1] = ri / den;
     }
+  } else if (nof_ports == 4) { /* 4-port transmit diversity over the 4 REGs' quadruplets */
+    const float *yy[2] = {ys[0], ys[1]};
+    const float *h4[8];
+    for (int p = 0; p < 4; p++)
+      for (int a = 0; a < 2; a++) h4[2 * p + a] = hs[p][a];
+    orc_predecode_txdiv4(yy, h4, (int)nrx, 16, 1.0f, d, NULL);
   } else {
     orc_predecode_txdiv(ys[0], nrx > 1 ? ys[1] : NULL, hs[0][0], nrx > 1 ? hs[0][1] : NULL, hs[1][0],
                         nrx > 1 ? hs[1][1] : NULL, (int)nrx, 16, 1.0f, d, NULL);

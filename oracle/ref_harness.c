@@ -1043,6 +1043,86 @@ int ref_pdcch_llr(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32
   return r ? -1 : e;
 }
 
+/* 4-port forms (any port count): grids / estimates as arrays, h[p * 2 + a] */
+int ref_pdcch_encode_n(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res,
+                       uint32_t cfi, uint32_t sf_idx, uint32_t n, const uint8_t *bits, const uint32_t *nof_bits,
+                       const uint32_t *L, const uint32_t *ncce, const uint16_t *rnti, float *const *grids) {
+  srslte_regs_t regs;
+  srslte_cell_t cell;
+  srslte_pdcch_t q;
+  if (ref_regs_cell(&regs, &cell, nof_prb, cell_id, nof_ports, phich_len, phich_res)) return -1;
+  if (srslte_pdcch_init_enb(&q, SRSLTE_MAX_PRB) || srslte_pdcch_set_cell(&q, &regs, cell)) return -1;
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL};
+  for (uint32_t p = 0; p < nof_ports; p++) sf[p] = (cf_t *)grids[p];
+  int ret = 0;
+  for (uint32_t i = 0; i < n && !ret; i++) {
+    srslte_dci_msg_t msg;
+    memset(&msg, 0, sizeof(msg));
+    memcpy(msg.data, bits + 128 * i, nof_bits[i]);
+    msg.nof_bits = nof_bits[i];
+    srslte_dci_location_t loc = {L[i], ncce[i]};
+    ret = srslte_pdcch_encode(&q, &msg, loc, rnti[i], sf, sf_idx, cfi) ? -1 : 0;
+  }
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return ret;
+}
+
+int ref_pdcch_llr_n(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res,
+                    uint32_t nrx, uint32_t cfi, uint32_t sf_idx, float noise, const float *const *gs,
+                    const float *const *hs, float *llr) {
+  srslte_regs_t regs;
+  srslte_pdcch_t q;
+  if (ref_pdcch_rx(&regs, &q, nof_prb, cell_id, nof_ports, phich_len, phich_res, nrx)) return -1;
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL}, *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  for (uint32_t a = 0; a < nrx; a++) {
+    sf[a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    memcpy(sf[a], gs[a], sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nof_ports; p++) {
+      ce[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+      memcpy(ce[p][a], hs[p * 2 + a], sizeof(cf_t) * n);
+    }
+  }
+  int r = srslte_pdcch_extract_llr_multi(&q, sf, ce, noise, sf_idx, cfi);
+  const int e = 72 * (int)q.nof_cce[cfi - 1];
+  if (r == 0) memcpy(llr, q.llr, sizeof(float) * e);
+  for (uint32_t a = 0; a < nrx; a++) {
+    free(sf[a]);
+    for (uint32_t p = 0; p < nof_ports; p++) free(ce[p][a]);
+  }
+  srslte_pdcch_free(&q);
+  srslte_regs_free(&regs);
+  return r ? -1 : e;
+}
+
+int ref_pcfich_n(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t nrx, const float *const *gs,
+                 const float *const *hs, float noise, uint32_t sf_idx, uint32_t *cfi, float *corr) {
+  srslte_cell_t cell = {nof_prb, nof_ports, cell_id, SRSLTE_CP_NORM, SRSLTE_PHICH_NORM, SRSLTE_PHICH_R_1};
+  srslte_regs_t regs;
+  srslte_pcfich_t q;
+  if (srslte_regs_init(&regs, cell)) return -1;
+  const uint32_t n = SRSLTE_SF_LEN_RE(nof_prb, SRSLTE_CP_NORM);
+  if (srslte_pcfich_init(&q, nrx) || srslte_pcfich_set_cell(&q, &regs, cell)) return -1;
+  cf_t *sf[SRSLTE_MAX_PORTS] = {NULL}, *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS] = {{NULL}};
+  for (uint32_t a = 0; a < nrx; a++) {
+    sf[a] = srslte_vec_malloc(sizeof(cf_t) * n);
+    memcpy(sf[a], gs[a], sizeof(cf_t) * n);
+    for (uint32_t p = 0; p < nof_ports; p++) {
+      ce[p][a] = srslte_vec_malloc(sizeof(cf_t) * n);
+      memcpy(ce[p][a], hs[p * 2 + a], sizeof(cf_t) * n);
+    }
+  }
+  const int r = srslte_pcfich_decode_multi(&q, sf, ce, noise, sf_idx, cfi, corr);
+  for (uint32_t a = 0; a < nrx; a++) {
+    free(sf[a]);
+    for (uint32_t p = 0; p < nof_ports; p++) free(ce[p][a]);
+  }
+  srslte_pcfich_free(&q);
+  srslte_regs_free(&regs);
+  return r < 0 ? -1 : 0;
+}
+
 /* The DL / UL DCI blind searches (ue_dl.c:768-932) run from the reference's own ue_dl.c in
  * oracle/ref_front.c (ue_dl.c reaches the DFT through ofdm.c, so it cannot be in this library). */
 

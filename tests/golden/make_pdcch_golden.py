@@ -118,6 +118,48 @@ def main():
             arrays[key + "_bits"] = np.asarray(b, np.uint8)
             ugman.append(dict(key=key, nof_prb=nof_prb, n_rb_ho=n_rb_ho, nof_bits=len(b), ret=r,
                               dci=[int(v) for v in d], grant=[int(v) for v in g]))
+    # 4 CRS ports (a separate stream, after everything above): symbol orders and received subframes,
+    # transmit diversity over the REG quadruplets (precoding.c:388-423 via pdcch.c:495-496)
+    rng4 = np.random.default_rng(4444)
+    for nof_prb in (6, 25, 100):
+        for cfi in (1, 2, 3):
+            cell_id = int(rng4.integers(0, 504))
+            pl, pr = int(rng4.integers(0, 2)), int(rng4.integers(0, 4))
+            idx, ncce = pdcch_map(ref, nof_prb, cell_id, 4, pl, pr, cfi, ref=True)
+            key = "m%d" % len(maps)
+            arrays[key] = idx
+            maps.append(dict(key=key, nof_prb=nof_prb, cell_id=cell_id, nports=4, phich_len=pl, phich_res=pr,
+                             cfi=cfi, nof_cce=ncce))
+    for nof_prb, nrx in ((6, 1), (15, 2), (25, 1), (50, 2), (100, 2), (100, 1)):
+        cell_id = int(rng4.integers(0, 504))
+        pl, pr = int(rng4.integers(0, 2)), int(rng4.integers(0, 4))
+        for r in range(2):
+            cfi, sf_idx, tm = int(rng4.integers(1, 4)), int(rng4.integers(0, 10)), int(rng4.integers(0, 8))
+            y, h, searches, noise = pdcch_subframe(ref, rng4, nof_prb, cell_id, 4, nrx, pl, pr, cfi, sf_idx, tm,
+                                                   snr_db=float(rng4.choice([6.0, 12.0, 30.0])))
+            nre = (cfi + (1 if nof_prb <= 10 else 0)) * 12 * nof_prb
+            y = [v[:nre] for v in y]
+            h = [[v[:nre] for v in hp] for hp in h]
+            llr = pdcch_llr(ref, nof_prb, cell_id, 4, pl, pr, nrx, cfi, sf_idx, noise, y, h, ref=True)
+            llr2, found = find_dci_ref(nof_prb, cell_id, 4, nrx, pl, pr, cfi, sf_idx, noise, y, h, searches)
+            assert np.array_equal(llr.view(np.uint32), llr2.view(np.uint32))
+            key = "c%d" % len(cases)
+            for a in range(nrx):
+                arrays["%s_y%d" % (key, a)] = y[a]
+                for p in range(4):
+                    arrays["%s_h%d%d" % (key, p, a)] = h[p][a]
+            arrays[key + "_llr"] = llr
+            res = []
+            for j, ((rnti, stm, rtype, ul_rnti), (dl, ul, ulg)) in enumerate(zip(searches, found)):
+                found_, fmt, L, ncce, nb, bits = dl
+                arrays["%s_s%d_bits" % (key, j)] = bits
+                arrays["%s_s%d_ulbits" % (key, j)] = ul[5]
+                res.append(dict(rnti=rnti, tm=stm, rnti_type=rtype, found=found_, format=fmt, L=L, ncce=ncce,
+                                nof_bits=nb, ul_rnti=ul_rnti, ul_found=ul[0], ul_format=ul[1], ul_L=ul[2],
+                                ul_ncce=ul[3], ul_nof_bits=ul[4], ul_grant_ret=ulg[0],
+                                ul_dci=[int(v) for v in ulg[1]], ul_grant=[int(v) for v in ulg[2]]))
+            cases.append(dict(key=key, group="ports4", nof_prb=nof_prb, cell_id=cell_id, nports=4, nrx=nrx,
+                              phich_len=pl, phich_res=pr, cfi=cfi, sf_idx=sf_idx, noise=noise, searches=res))
     man = dict(maps=maps, cases=cases, grants=gman, ul_grants=ugman)
     arrays["manifest"] = np.frombuffer(json.dumps(man).encode(), np.uint8)
     np.savez_compressed(os.path.join(HERE, "pdcch_golden.npz"), **arrays)

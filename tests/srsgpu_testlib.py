@@ -852,7 +852,14 @@ def pcfich_decode(lib, nof_prb, cell_id, nports, nrx, y, h, noise, sf_idx, ref=F
     hs = [[pad(h[p][a]) for a in range(nrx)] for p in range(nports)]
     P = lambda a: a.ctypes.data_as(_f32p) if a is not None else None
     cfi, corr = ctypes.c_uint32(0), ctypes.c_float(0)
-    if ref:
+    if ref and nports == 4:
+        f = L.ref_pcfich_n
+        f.argtypes = [ctypes.c_uint32] * 4 + [ctypes.POINTER(_f32p), ctypes.POINTER(_f32p), ctypes.c_float,
+                                              ctypes.c_uint32, _u32p, _f32p]
+        ya = (_f32p * 2)(*[P(v) for v in ys] + [None] * (2 - nrx))
+        ha = (_f32p * 8)(*[P(hs[p][a]) if a < nrx else None for p in range(4) for a in range(2)])
+        r = f(nof_prb, cell_id, nports, nrx, ya, ha, noise, sf_idx, ctypes.byref(cfi), ctypes.byref(corr))
+    elif ref:
         f = L.ref_pcfich
         f.argtypes = [ctypes.c_uint32] * 4 + [_f32p] * 6 + [ctypes.c_float, ctypes.c_uint32, _u32p,
                                                             _f32p, _u32p]
@@ -865,8 +872,8 @@ def pcfich_decode(lib, nof_prb, cell_id, nports, nrx, y, h, noise, sf_idx, ref=F
         f.argtypes = [ctypes.c_uint32] * 4 + [ctypes.POINTER(_f32p), ctypes.POINTER(_f32p),
                                               ctypes.c_float, ctypes.c_uint32, _u32p, _f32p]
         ya = (_f32p * 2)(*[P(v) for v in ys] + [None] * (2 - nrx))
-        ha = (_f32p * 4)(*[P(hs[p][a]) for p in range(nports) for a in range(nrx)] +
-                         [None] * (4 - nports * nrx))
+        ha = (_f32p * 8)(*[P(hs[p][a]) for p in range(nports) for a in range(nrx)] +
+                         [None] * (8 - nports * nrx))
         r = f(nof_prb, cell_id, nports, nrx, ya, ha, noise, sf_idx, ctypes.byref(cfi), ctypes.byref(corr))
     assert r == 0, r
     return cfi.value, corr.value
@@ -902,10 +909,11 @@ def pdcch_encode(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_id
     q->max_bits = 72 NOF_CCE(3) (pdcch.c:548): srslte_pdcch_dci_encode then returns an error that
     srslte_pdcch_encode ignores, and uninitialised bits go out. Callers avoid such locations
     (pdcch_encodable); the result is checked to be finite."""
-    f = _L(lib).ref_pdcch_encode
-    f.argtypes = [ctypes.c_uint32] * 8 + [_u8p, _u32p, _u32p, _u32p, _u16p, _f32p, _f32p]
+    f = _L(lib).ref_pdcch_encode if nports <= 2 else _L(lib).ref_pdcch_encode_n
+    f.argtypes = [ctypes.c_uint32] * 8 + [_u8p, _u32p, _u32p, _u32p, _u16p] + (
+        [_f32p, _f32p] if nports <= 2 else [ctypes.POINTER(_f32p)])
     n = 14 * 12 * nof_prb
-    grids = [np.zeros(n, np.complex64) for _ in range(2)]
+    grids = [np.zeros(n, np.complex64) for _ in range(max(2, nports))]
     bits = np.zeros(128 * max(len(msgs), 1), np.uint8)
     nb = np.zeros(max(len(msgs), 1), np.uint32)
     Ls, nc = nb.copy(), nb.copy()
@@ -913,9 +921,9 @@ def pdcch_encode(lib, nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_id
     for i, (b, L, c, r) in enumerate(msgs):
         bits[128 * i:128 * i + len(b)] = b
         nb[i], Ls[i], nc[i], rn[i] = len(b), L, c, r
+    gp = [_pf(grids[0]), _pf(grids[1])] if nports <= 2 else [(_f32p * 4)(*[_pf(g) for g in grids])]
     assert f(nof_prb, cell_id, nports, phich_len, phich_res, cfi, sf_idx, len(msgs), _ptr(bits, _u8p),
-             _ptr(nb, _u32p), _ptr(Ls, _u32p), _ptr(nc, _u32p), _ptr(rn, _u16p), _pf(grids[0]),
-             _pf(grids[1])) == 0
+             _ptr(nb, _u32p), _ptr(Ls, _u32p), _ptr(nc, _u32p), _ptr(rn, _u16p), *gp) == 0
     assert all(np.isfinite(g).all() for g in grids), "the reference PDCCH encoder sent uninitialised bits"
     return grids[:nports]
 
@@ -929,11 +937,21 @@ def pdcch_encodable(lib, nof_prb, cell_id, nports, phich_len, phich_res, L):
 def pdcch_llr(lib, nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_idx, noise, y, h, ref=False):
     """srslte_pdcch_extract_llr_multi: y[a] grids, h[p][a] estimates (complex64, 14 * 12 nof_prb or the
     leading control symbols, zero-padded) -> the 72 NOF_CCE(cfi) float LLRs"""
-    f = getattr(_L(lib), "ref_pdcch_llr" if ref else "orc_pdcch_llr")
-    f.argtypes = [ctypes.c_uint32] * 8 + [ctypes.c_float] + [_f32p] * 7
     n = 14 * 12 * nof_prb
     pad = lambda a: np.ascontiguousarray(np.concatenate([a, np.zeros(n - a.size, np.complex64)])
                                          if a.size < n else a, np.complex64)
+    if nports == 4:
+        f = getattr(_L(lib), "ref_pdcch_llr_n" if ref else "orc_pdcch_llr_n")
+        f.argtypes = [ctypes.c_uint32] * 8 + [ctypes.c_float, ctypes.POINTER(_f32p), ctypes.POINTER(_f32p), _f32p]
+        ys = [pad(y[a]) if a < nrx else None for a in range(2)]
+        hs = [pad(h[p][a]) if a < nrx else None for p in range(4) for a in range(2)]
+        llr = np.zeros(72 * 128, np.float32)
+        e = f(nof_prb, cell_id, nports, phich_len, phich_res, nrx, cfi, sf_idx, noise,
+              (_f32p * 2)(*[_pf(v) for v in ys]), (_f32p * 8)(*[_pf(v) for v in hs]), _pf(llr))
+        assert e > 0, e
+        return llr[:e].copy()
+    f = getattr(_L(lib), "ref_pdcch_llr" if ref else "orc_pdcch_llr")
+    f.argtypes = [ctypes.c_uint32] * 8 + [ctypes.c_float] + [_f32p] * 7
     ys = [pad(y[a]) if a < nrx else None for a in range(2)]
     hs = [[pad(h[p][a]) if p < nports and a < nrx else None for a in range(2)] for p in range(2)]
     llr = np.zeros(72 * 128, np.float32)  # NOF_CCE reaches 96 at 110 PRB

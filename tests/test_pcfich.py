@@ -29,7 +29,7 @@ def _case(z, c):
 
 def test_golden_oracle(oracle, gold):
     z, man = gold
-    assert len(man) == 72
+    assert len(man) == 72 + 24  # 24 of them with 4 CRS ports
     assert sum(c["cfi"] == c["sent_cfi"] for c in man) >= 60  # the fixture exercises real detection
     for c in man:
         assert (pcfich_re_map(oracle, c["nof_prb"], c["cell_id"]) == z[c["key"] + "_idx"]).all()
@@ -46,7 +46,7 @@ def test_random_vs_reference(oracle):
     for nof_prb in (6, 25, 100):
         for cell_id in (0, 1, 2, 301, 503):
             assert (pcfich_re_map(oracle, nof_prb, cell_id) == pcfich_re_map(ref, nof_prb, cell_id, ref=True)).all()
-            for nports in (1, 2):
+            for nports in (1, 2, 4):
                 for nrx in (1, 2):
                     n0 = nof_prb * 12
                     y = [(rng.standard_normal(n0) + 1j * rng.standard_normal(n0)).astype(np.complex64)

@@ -86,7 +86,7 @@ def test_golden_search_spaces_cover_the_cases(gold):
 
 
 @pytest.mark.parametrize("nof_prb,cell_id,nports,nrx,pl,pr", [(5, 0, 1, 1, 0, 0), (111, 0, 1, 1, 0, 0),
-                                                             (6, 504, 1, 1, 0, 0), (6, 0, 4, 1, 0, 0),
+                                                             (6, 504, 1, 1, 0, 0), (6, 0, 3, 1, 0, 0),
                                                              (6, 0, 1, 3, 0, 0), (6, 0, 1, 1, 2, 0),
                                                              (6, 0, 1, 1, 0, 4)])
 def test_create_rejects_invalid_cells(nof_prb, cell_id, nports, nrx, pl, pr):
@@ -224,7 +224,7 @@ def test_gpu_golden_batch(gold):
 @pytest.mark.gpu
 @pytest.mark.skipif(not (have_ref() and have_ref_front()), reason="oracle/_ref not built")
 @pytest.mark.parametrize("nof_prb,nports,nrx", [(6, 1, 1), (9, 2, 2), (10, 1, 2), (15, 2, 1), (25, 1, 2), (50, 2, 2), (75, 1, 1),
-                                                (100, 2, 2), (110, 2, 1)])
+                                                (100, 2, 2), (110, 2, 1), (25, 4, 2), (100, 4, 1)])
 def test_gpu_random_vs_reference(nof_prb, nports, nrx):
     """random cells and subframes generated live with the reference's encoder; 40 subframes in one launch,
     back-to-back extraction / search calls on one stream with no host sync in between"""
