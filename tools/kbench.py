@@ -58,8 +58,11 @@ def main():
         s.prof_reset()
         s.prof_enable(True)
         t0 = time.perf_counter()
+        host = 0.0
         for _ in range(a.reps):
+            h0 = time.perf_counter()
             assert f() == 0
+            host += time.perf_counter() - h0
             torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.reps * 1e3
         s.prof_enable(False)
@@ -72,7 +75,7 @@ def main():
                 if k in ALG:
                     e["hbm_frac"] = round(ALG[k] * n / (ms / a.reps / 1e3) / 8e12, 3)
                 ks[k] = e
-        res[name] = {"wall_ms": round(wall, 4), "kernels": ks}
+        res[name] = {"wall_ms": round(wall, 4), "host_ms": round(host / a.reps * 1e3, 4), "kernels": ks}
     acks, good, noi = m.check()
     out = {"subframes": n, "snr_db": a.snr, "schedule": a.schedule, "acked": acks, "good": good,
            "nof_iterations_mean": noi, "stages": res,
