@@ -270,11 +270,37 @@ struct PdschEngine {
     return 0;
   }
 
+  // The previous llr() call's inputs: a repeat (same subframes, pointers and settings) launches on
+  // the LLR items and scrambling sequences already on the device. The sequences depend only on the
+  // (RNTI, codeword, subframe, cell) seeds, as the reference's per-user pre-generated ones do
+  // (pdsch.c:436-440). encode() reuses those buffers and clears the memo.
+  std::vector<uint8_t> memo_key, memo_scratch;
+  bool memo_valid = false;
+  uint32_t memo_k = 0, memo_mre = 0;
+  int memo_ndual = 0;
+
   int llr(const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid, const float *d_ce,
           size_t ant_stride, int16_t *const *e_ptr) {
     if (n > max_sf) {
       fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
       return -1;
+    }
+    {
+      const uint32_t nt = count_tb(sf, n);
+      const size_t n1 = sizeof(srsgpu_pdsch_sf_t) * n, n2 = sizeof(void *) * nt;
+      const uintptr_t tail[9] = {(uintptr_t)d_grid, (uintptr_t)d_ce, ant_stride, csi, llr8, (uintptr_t)ce_rows,
+                                 (uintptr_t)noise_dev, n, nt};
+      memo_scratch.resize(n1 + n2 + sizeof(tail));
+      memcpy(memo_scratch.data(), sf, n1);
+      memcpy(memo_scratch.data() + n1, e_ptr, n2);
+      memcpy(memo_scratch.data() + n1 + n2, tail, sizeof(tail));
+      if (memo_valid && memo_scratch == memo_key) {
+        if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)memo_k * 4, st));
+        ProfScope ps("k_pdsch_llr", st);
+        HIPCHK(launch_pdsch_llr(d_llr, (int)memo_k, memo_mre, csi, st, memo_ndual));
+        return 0;
+      }
+      memo_valid = false;
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
     uint32_t mre = 0, k = 0;
@@ -351,6 +377,11 @@ struct PdschEngine {
     }
     ProfScope ps("k_pdsch_llr", st);
     HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual));
+    memo_key.swap(memo_scratch);
+    memo_k = k;
+    memo_mre = mre;
+    memo_ndual = n_dual;
+    memo_valid = true;
     return 0;
   }
 
@@ -389,6 +420,7 @@ struct PdschEngine {
       HIPCHK(hipMemcpy(d_mod, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    memo_valid = false; // the sequences and items below overwrite the ones llr() keeps
     uint32_t mre = 0, k = 0;
     gold_slot.clear();
     ngold = 0;
