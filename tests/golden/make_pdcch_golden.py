@@ -160,6 +160,15 @@ def main():
                                 ul_dci=[int(v) for v in ulg[1]], ul_grant=[int(v) for v in ulg[2]]))
             cases.append(dict(key=key, group="ports4", nof_prb=nof_prb, cell_id=cell_id, nports=4, nrx=nrx,
                               phich_len=pl, phich_res=pr, cfi=cfi, sf_idx=sf_idx, noise=noise, searches=res))
+            for j, (rnti, _, _, _) in enumerate(searches):  # the found messages' grants, 4-port unpacking
+                found_, fmt, _, _, nb, bits = found[j][0]
+                if found_ > 0:
+                    r_, d, g, p = dci_to_dl_grant_ref(ref, bits, fmt, rnti, nof_prb, 4, nof_bits=nb)
+                    gkey = "g%d" % len(gman)
+                    arrays[gkey + "_bits"] = np.asarray(bits, np.uint8)
+                    arrays[gkey + "_prb"] = p
+                    gman.append(dict(key=gkey, format=fmt, rnti=rnti, nof_prb=nof_prb, nports=4, nof_bits=nb,
+                                     ret=r_, dci=[int(v) for v in d], grant=[int(v) for v in g]))
     man = dict(maps=maps, cases=cases, grants=gman, ul_grants=ugman)
     arrays["manifest"] = np.frombuffer(json.dumps(man).encode(), np.uint8)
     np.savez_compressed(os.path.join(HERE, "pdcch_golden.npz"), **arrays)

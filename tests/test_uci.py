@@ -80,7 +80,7 @@ def _gpu_run(s, torch, cases, rng_ok=True):
         cs.append(c)
         offs += (u["nof_bits"] + 63) // 64 * 64
         doff += s.dlsch_data_len(max(u["tbs"], 8)) + 2
-    dl.reset_softbuffer(0, len(cases))
+    dl.reset_range(0, len(cases))
     d_q = torch.zeros(offs, dtype=torch.int16, device="cuda")
     d_c = torch.zeros(offs, dtype=torch.uint8, device="cuda")
     for t, q, c in zip(tbs_list, qs, cs):
