@@ -13,18 +13,19 @@
 
 namespace srsgpu {
 
-// CRS, normal CP (refsignal_dl.c:265-318, 36.211 6.10.1.1): for slot ns and OFDM symbol lp in
-// {0, 4} (ports 0/1) or {1} (ports 2/3), c_init = 2^10 (7(ns+1) + lp + 1)(2 N_ID + 1) + 2 N_ID + 1
-// and r(m) = ((1 - 2c(2m')) + j(1 - 2c(2m'+1))) / sqrt(2), m' = m + 110 - nof_prb.
+// CRS (refsignal_dl.c:265-318, 36.211 6.10.1.1): for slot ns and OFDM symbol lp in {0, 4} (ports
+// 0/1; {0, 3} with extended CP) or {1} (ports 2/3), c_init = 2^10 (7(ns+1) + lp + 1)(2 N_ID + 1) +
+// 2 N_ID + N_cp (N_cp 1 normal, 0 extended CP) and r(m) = ((1 - 2c(2m')) + j(1 - 2c(2m'+1))) /
+// sqrt(2), m' = m + 110 - nof_prb.
 // Layout: [10 subframes][4 symbols][2 nof_prb] of ports 0/1, then [10][2][2 nof_prb] of ports 2/3.
-static void crs_table(uint32_t nprb, uint32_t id, std::vector<float> &t) {
+static void crs_table(uint32_t nprb, uint32_t id, bool ext, std::vector<float> &t) {
   const uint32_t np = 2 * nprb, len = 4 * 110, Nc = 1600;
   t.assign((size_t)10 * 6 * np * 2, 0.f);
   std::vector<uint8_t> x1(Nc + len + 31), x2(Nc + len + 31);
   for (uint32_t ns = 0; ns < 20; ns++)
     for (uint32_t l = 0; l < 3; l++) {
-      const uint32_t lp = l == 0 ? 0 : l == 1 ? 4 : 1;
-      const uint32_t cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * id + 1) + 2 * id + 1;
+      const uint32_t lp = l == 0 ? 0 : l == 1 ? (ext ? 3 : 4) : 1;
+      const uint32_t cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * id + 1) + 2 * id + (ext ? 0 : 1);
       std::fill(x1.begin(), x1.end(), 0);
       std::fill(x2.begin(), x2.end(), 0);
       x1[0] = 1;
@@ -62,15 +63,16 @@ struct ChestEngine {
   bool staged_pending = false;
 
   int create(const srsgpu_cell_t &c, uint32_t n) {
-    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4)) {
-      fprintf(stderr, "srsgpu: invalid cell for channel estimation (1, 2 or 4 CRS ports)\n");
+    if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4) ||
+        c.cp > 1) {
+      fprintf(stderr, "srsgpu: invalid cell for channel estimation (1, 2 or 4 CRS ports, normal or extended CP)\n");
       return -1;
     }
     cell = c;
     cap = n;
     n *= c.nof_ports; // one work item per (grid, port)
     std::vector<float> t;
-    crs_table(c.nof_prb, c.id, t);
+    crs_table(c.nof_prb, c.id, c.cp == 1, t);
     HIPCHK(hipMalloc(&d_crs, t.size() * 4));
     HIPCHK(hipMemcpy(d_crs, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&d_filt, 64 * 4));
@@ -108,8 +110,9 @@ struct ChestEngine {
       fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
       return -1;
     }
-    if (ce_rows && cell.nof_ports > 2) { // the compact rows are the 4-symbol (ports 0/1) layout
-      fprintf(stderr, "srsgpu: compact estimate rows need a 1- or 2-port cell\n");
+    if (ce_rows && (cell.nof_ports > 2 || (cell.cp == 1 && !cfg.average_subframe))) {
+      // the 4 compact rows are the normal-CP ports 0/1 layout; the averaged row fits any CP
+      fprintf(stderr, "srsgpu: compact estimate rows need a 1- or 2-port cell, and average_subframe with extended CP\n");
       return -1;
     }
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
@@ -148,6 +151,7 @@ struct ChestEngine {
     kc.cfo_n = (float)cfg.symbol_sz;
     kc.cfo_ng = ceilf((144.0f * (float)cfg.symbol_sz) / 2048.0f); // SRSLTE_CP_LEN_NORM(1, n)
     kc.rows = ce_rows ? 1 : 0;
+    kc.ns = cell.cp == 1 ? 6 : 7;
     ProfScope ps("k_chest", st);
     HIPCHK(launch_chest(d_items, (int)(n * np), kc, d_crs, d_filt, d_pss, st));
     return 0;
@@ -176,7 +180,7 @@ struct ChestEngine {
     HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
     HIPCHK(hipEventRecord(staged, st));
     staged_pending = true;
-    HIPCHK(launch_crs_put(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, d_crs, st));
+    HIPCHK(launch_crs_put(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, cell.cp == 1 ? 6 : 7, d_crs, st));
     return 0;
   }
 };

@@ -5,7 +5,7 @@
 #include <stdint.h>
 
 namespace srsgpu {
-// one (subframe, rx antenna, CRS port): grid and ce are 14 x 12*nof_prb complex planes
+// one (subframe, rx antenna, CRS port): grid and ce are 14 (12 extended CP) x 12*nof_prb complex planes
 struct ChestItem {
   const float2 *grid;
   float2 *ce;
@@ -25,6 +25,7 @@ struct ChestCfg {
   int filt_auto;      // smooth_filter_auto: order-4 Gaussian from the noise estimate
   int rsrp_neighbour; // rsrp_corr computed
   float cfo_n, cfo_ng; // CFO formula: symbol size and normal-CP length of symbol 1
+  int ns;             // OFDM symbols per slot: 7 normal CP, 6 extended CP (grid rows 2 ns)
   int rows;           // compact output: the CRS symbols' frequency-interpolated rows (4 x nsc, or
                       // the averaged row, 1 x nsc) instead of the 14 x nsc grid (srsgpu_chest_set_ce_rows)
 };
@@ -33,7 +34,7 @@ struct ChestCfg {
 hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, const float2 *crs,
                         const float *filt, const float2 *pss, hipStream_t st);
 // items[i].ce is the grid plane the port's CRS is written into
-hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
+hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, int ns, const float2 *crs,
                           hipStream_t st);
 } // namespace srsgpu
 #endif

@@ -1,9 +1,9 @@
 // MI355X downlink CRS channel estimation, srslte_chest_dl_estimate_port (ports 0-3) for
-// normal-CP, non-MBSFN subframes, in every configuration srsUE's phch_worker sets
+// normal- and extended-CP, non-MBSFN subframes, in every configuration srsUE's phch_worker sets
 // (srsue/src/phy/phch_worker.cc:149,553-565; reference: lib/src/phy/ch_estimation/chest_dl.c:641-694
 // and the helpers it calls):
 //   1. least squares   pilots received at the CRS REs of symbols 0/4/7/11 (ports 0/1) or 1/8 (ports
-//                      2/3) (refsignal_cs_get_sf, refsignal_dl.c:404-430) times conj(CRS)
+//                      2/3); extended CP 0/3/6/9 or 1/7 (refsignal_cs_get_sf, refsignal_dl.c:404-430) times conj(CRS)
 //                      (refsignal_dl.c:265-318)
 //   2. measurements    RSRP, RSSI (chest_dl.c:500-511), RSRP correlation (:652-656), CFO (:562-587)
 //   3. noise (REFS)    estimate_noise_pilots (chest_dl.c:268-329), including its reference behaviour
@@ -15,8 +15,8 @@
 //                      (convolution.c:172-211)
 //   6. frequency       srslte_interp_linear_offset (interp.c:245-272): per CRS symbol with M = 6, or
 //                      the averaged row with M = 3 and offset cell_id % 3 (chest_dl.c:393-399)
-//   7. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:421-431,
-//                      interp.c:150-173), or the averaged row copied to all 14 symbols (:410-414)
+//   7. time            srslte_interp_linear_vector(2) between CRS symbols (chest_dl.c:421-442,
+//                      interp.c:150-173), or the averaged row copied to all 14 (12) symbols (:410-414)
 //   8. noise (PSS/EMPTY) in subframes 0 and 5 only (chest_dl.c:628-637, 332-361)
 // One workgroup per (subframe, rx antenna, port): pilots and their smoothed copy stay in LDS, each
 // thread then produces whole subcarrier columns (14 symbols) in registers and streams them out.
@@ -142,11 +142,13 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   const int kb = (nsc * part) / nparts, ke = (nsc * (part + 1)) / nparts;
   const c32 *grid = (const c32 *)t.grid;
   const int port = (int)t.port;
-  // ports 0/1: CRS symbols 0, 4, 7, 11; ports 2/3: 1 and 8 (refsignal_dl.c:76-85, 112-122), their
-  // pilots (csr_refs.pilots[port / 2]) after the 10 x 4 rows of ports 0/1 in the table
+  // ports 0/1: CRS symbols 0, ns - 3, ns, 2 ns - 3; ports 2/3: 1 and ns + 1 (srslte_refsignal_cs_nsymbol,
+  // refsignal_dl.c:112-122; ns = 7 normal, 6 extended CP), their pilots (csr_refs.pilots[port / 2])
+  // after the 10 x 4 rows of ports 0/1 in the table
+  const int ns = cfg.ns, nsf = 2 * ns;
   const int nsym = port < 2 ? 4 : 2;
   const c32 *pil = (const c32 *)(port < 2 ? crs + (size_t)t.sf_idx * 4 * np : crs + (size_t)(40 + 2 * t.sf_idx) * np);
-  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? 4 : 8, 7, 11};
+  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? ns - 3 : ns + 1, ns, 2 * ns - 3};
   const int tid = threadIdx.x;
   // v = 0 / 3 alternating over the CRS symbols, ports 1 / 3 starting at 3 (refsignal_dl.c:40-74)
   auto fidx = [&](int l) { return (((l & 1) ^ (port & 1) ? 3 : 0) + cell_id % 6) % 6; };
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
     for (int e = 2 * np + tid; e < 4 * np; e += blockDim.x) {
       const int l = e / np, m = e % np;
       const int f1 = (((l & 1) ^ 1 ? 3 : 0) + cell_id % 6) % 6; // port 1
-      ls[e] = cmulconj(grid[(l == 2 ? 7 : 11) * nsc + f1 + 6 * m], pil01[e]);
+      ls[e] = cmulconj(grid[(l == 2 ? ns : 2 * ns - 3) * nsc + f1 + 6 * m], pil01[e]);
     }
   }
   __syncthreads();
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
           t.meas[2] = (float)(e * e);
         }
         if (t.cfo) {
-          const float a = -atan2f(red[6][0], red[5][0]) * cfg.cfo_n / (7.0f * (cfg.cfo_n + cfg.cfo_ng)) / 2;
+          const float a = -atan2f(red[6][0], red[5][0]) * cfg.cfo_n / ((float)ns * (cfg.cfo_n + cfg.cfo_ng)) / 2;
           t.meas[3] = (float)((double)a / M_PI);
         }
       }
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
   // 6 + 7. per subcarrier column: frequency interpolation, then time
   c32 *ce = (c32 *)t.ce;
   const bool pss_on = nz05 && cfg.noise_alg == 1;
-  const int k0 = nsc / 2 - 31; // srslte_pss_get_slot position within symbol 6
+  const int k0 = nsc / 2 - 31; // srslte_pss_get_slot position within symbol ns - 1
   float pacc = 0.f;
   for (int k = kb + tid; k < ke; k += blockDim.x) {
     c32 c6;
@@ -297,9 +299,9 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
       if (cfg.rows)
         ce[k] = v;
       else
-        for (int s = 0; s < 14; s++) ce[s * nsc + k] = v;
+        for (int s = 0; s < nsf; s++) ce[s * nsc + k] = v;
       c6 = v;
-    } else if (nsym == 2) { // ports 2 / 3 (chest_dl.c:428-430): symbol 0 extrapolated back from 1 with
+    } else if (nsym == 2 && ns == 7) { // ports 2 / 3 (chest_dl.c:428-430): symbol 0 extrapolated back from 1 with
                             // (c1 - c8) / 7; 2-7 forward from 1 with (c8 - c1) / 7; 9-13 forward from
                             // symbol 1 again (the reference's in0 for that segment), i.e. 2-6 repeated
       const c32 f0 = interp_at(rows, np, k, fidx(0), 6, 1.0f / 6), f1 = interp_at(rows + np, np, k, fidx(1), 6, 1.0f / 6);
@@ -313,6 +315,31 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
       for (int s = 9; s < 14; s++) col[s] = col[s - 7];
       for (int s = 0; s < 14; s++) ce[s * nsc + k] = col[s];
       c6 = col[6];
+    } else if (nsym == 2) { // extended CP (chest_dl.c:439-441): 1 and 7, M = 6; 8-11 repeat 2-5
+      const c32 f0 = interp_at(rows, np, k, fidx(0), 6, 1.0f / 6), f1 = interp_at(rows + np, np, k, fidx(1), 6, 1.0f / 6);
+      c32 col[12];
+      col[1] = f0;
+      col[7] = f1;
+      col[0] = cadd(f0, cscale(csub(f0, f1), 1.0f / 6.0f));
+      const c32 d = cscale(csub(f1, f0), 1.0f / 6.0f);
+      col[2] = cadd(f0, d);
+      for (int s = 3; s < 7; s++) col[s] = cadd(col[s - 1], d);
+      for (int s = 8; s < 12; s++) col[s] = col[s - 6];
+      for (int s = 0; s < 12; s++) ce[s * nsc + k] = col[s];
+      c6 = col[5];
+    } else if (ns == 6) { // extended CP, ports 0/1 (chest_dl.c:434-437): 0 / 3 / 6 / 9, M = 3, 10-11
+                          // extrapolated from 9
+      c32 f[4];
+      for (int l = 0; l < 4; l++) f[l] = interp_at(rows + l * np, np, k, fidx(l), 6, 1.0f / 6);
+      c32 col[12];
+      for (int l = 0; l < 4; l++) col[3 * l] = f[l];
+      for (int l = 0; l < 4; l++) {
+        const c32 d = cscale(csub(f[l < 3 ? l + 1 : 3], f[l < 3 ? l : 2]), 1.0f / 3.0f);
+        col[3 * l + 1] = cadd(f[l], d);
+        col[3 * l + 2] = cadd(col[3 * l + 1], d);
+      }
+      for (int s = 0; s < 12; s++) ce[s * nsc + k] = col[s];
+      c6 = col[5];
     } else {
       c32 f[4];
       for (int l = 0; l < 4; l++) f[l] = interp_at(rows + l * np, np, k, fidx(l), 6, 1.0f / 6);
@@ -341,7 +368,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
       c6 = col[6];
     }
     if (pss_on && k >= k0 && k < k0 + 62) // estimate_noise_pss: ce * PSS - received
-      pacc += cpow(csub(cmul(c6, ((const c32 *)pss)[k - k0]), grid[6 * nsc + k]));
+      pacc += cpow(csub(cmul(c6, ((const c32 *)pss)[k - k0]), grid[(ns - 1) * nsc + k]));
   }
   // 8. PSS / EMPTY noise, subframes 0 and 5 only (otherwise the value is left as it was)
   if (pss_on) {
@@ -349,7 +376,7 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
     if (tid == 0) *t.noise = (float)((double)((float)cfg.nof_ports * (red[0][0] / 62.0f)) / sqrt(2.0));
   } else if (nz05 && tid == 0) { // estimate_noise_empty_sc: 5 empty subcarriers either side of SSS / PSS
     float np_ = 0.f;
-    for (int s = 5; s <= 6; s++) {
+    for (int s = ns - 2; s <= ns - 1; s++) {
       const int kk = s * nsc + k0;
       for (int side = 0; side < 2; side++) {
         const c32 *x = grid + (side ? kk + 62 : kk - 5);
@@ -372,14 +399,14 @@ hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, co
 }
 
 // srslte_refsignal_cs_put_sf (refsignal_dl.c:338-360): the CRS of a port into its grid plane at
-// symbols 0/4/7/11 (ports 0/1) or 1/8 (ports 2/3), subcarriers fidx + 6m
+// symbols 0/4/7/11 (ports 0/1) or 1/8 (ports 2/3) (extended CP: 0/3/6/9 or 1/7), subcarriers fidx + 6m
 __global__ __launch_bounds__(256) void k_crs_put(const ChestItem *__restrict__ items, int nitems, int nprb,
-                                                 int cell_id, const float2 *__restrict__ crs) {
+                                                 int cell_id, int ns, const float2 *__restrict__ crs) {
   const int it = blockIdx.x;
   if (it >= nitems) return;
   const ChestItem t = items[it];
   const int np = 2 * nprb, nsc = 12 * nprb, port = (int)t.port, nsym = port < 2 ? 4 : 2;
-  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? 4 : 8, 7, 11};
+  const int sym[4] = {port < 2 ? 0 : 1, port < 2 ? ns - 3 : ns + 1, ns, 2 * ns - 3};
   const float2 *pil = port < 2 ? crs + (size_t)t.sf_idx * 4 * np : crs + (size_t)(40 + 2 * t.sf_idx) * np;
   float2 *g = t.ce; // the grid plane written
   for (int e = threadIdx.x; e < nsym * np; e += blockDim.x) {
@@ -389,10 +416,10 @@ __global__ __launch_bounds__(256) void k_crs_put(const ChestItem *__restrict__ i
   }
 }
 
-hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, const float2 *crs,
+hipError_t launch_crs_put(const ChestItem *d_items, int n, int nprb, int cell_id, int ns, const float2 *crs,
                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_crs_put, dim3((unsigned)n), dim3(256), 0, st, d_items, n, nprb, cell_id, crs);
+  hipLaunchKernelGGL(k_crs_put, dim3((unsigned)n), dim3(256), 0, st, d_items, n, nprb, cell_id, ns, crs);
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ struct srsgpu_ofdm {
   uint32_t radices = 0;
   int nstages = 0;
   bool normalize = false;
+  bool ext_cp = false; // srslte_cp_t SRSLTE_CP_EXT: 12 symbols per subframe
 };
 
 extern "C" {
@@ -86,27 +87,35 @@ void srsgpu_ofdm_rx_set_normalize(srsgpu_ofdm_t *q, int enable) {
   if (q) q->normalize = enable != 0;
 }
 
+int srsgpu_ofdm_set_cp(srsgpu_ofdm_t *q, uint32_t cp) {
+  if (!q || cp > 1) return -1;
+  q->ext_cp = cp == 1;
+  return 0;
+}
+
 int srsgpu_ofdm_rx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
                           float *d_out, size_t out_stride) {
   if (!q || !d_in || !d_out) return -1;
-  if (in_stride < 15 * (size_t)q->N || out_stride < 14 * 12 * (size_t)q->nof_prb) return -1;
+  const size_t nsym = q->ext_cp ? 12 : 14;
+  if (in_stride < 15 * (size_t)q->N || out_stride < nsym * 12 * q->nof_prb) return -1;
   const float scale = q->normalize ? 1.0f / sqrtf((float)q->N) : 1.0f;
   srsgpu::ProfScope ps("k_ofdm_rx", q->st);
   HIPCHK(srsgpu::launch_ofdm_rx((const float2 *)d_in, in_stride, (float2 *)d_out, out_stride, (int)nof_sf,
                                 (int)q->N, (int)(12 * q->nof_prb), q->d_tw, q->radices, q->nstages, scale,
-                                q->st));
+                                q->ext_cp, q->st));
   return 0;
 }
 
 int srsgpu_ofdm_tx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
                           float *d_out, size_t out_stride) {
   if (!q || !d_in || !d_out) return -1;
-  if (out_stride < 15 * (size_t)q->N || in_stride < 14 * 12 * (size_t)q->nof_prb) return -1;
+  const size_t nsym = q->ext_cp ? 12 : 14;
+  if (out_stride < 15 * (size_t)q->N || in_stride < nsym * 12 * q->nof_prb) return -1;
   const float scale = q->normalize ? 1.0f / sqrtf((float)q->N) : 1.0f;
   srsgpu::ProfScope ps("k_ofdm_tx", q->st);
   HIPCHK(srsgpu::launch_ofdm_tx((const float2 *)d_in, in_stride, (float2 *)d_out, out_stride, (int)nof_sf,
                                 (int)q->N, (int)(12 * q->nof_prb), q->d_tw, q->radices, q->nstages, scale,
-                                q->st));
+                                q->ext_cp, q->st));
   return 0;
 }
 

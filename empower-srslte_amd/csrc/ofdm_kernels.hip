@@ -71,11 +71,11 @@ __device__ __forceinline__ void stage(const cf *__restrict__ d0, cf *__restrict_
 
 __global__ __launch_bounds__(256) void k_ofdm_rx(const float2 *__restrict__ in, size_t in_stride,
                                                  float2 *__restrict__ out, size_t out_stride, int N,
-                                                 int nre, int cp0, int cp, const float2 *__restrict__ tw,
+                                                 int nre, int cp0, int cp, int ns, const float2 *__restrict__ tw,
                                                  const uint32_t radices, int nstages, float scale) {
   __shared__ cf buf[2][OFDM_MAXN];
-  const int sym = blockIdx.x % 14, sf = blockIdx.x / 14;
-  const int slot = sym / 7, l = sym % 7;
+  const int sym = blockIdx.x % (2 * ns), sf = blockIdx.x / (2 * ns);
+  const int slot = sym / ns, l = sym % ns;
   // symbol start: slot * 7.5 N + cp0 + l * (N + cp)   (ofdm.c:98-103 guru plan strides)
   const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
   const cf *src = (const cf *)(in + (size_t)sf * in_stride + start);
@@ -230,15 +230,15 @@ constexpr int syms_per_wg() {
 template <int N>
 __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in, size_t in_stride,
                                                    float2 *__restrict__ out, size_t out_stride, int nsym,
-                                                   int nre, int cp0, int cp,
+                                                   int nre, int cp0, int cp, int ns,
                                                    const float2 *__restrict__ tw, float scale) {
   constexpr int S = syms_per_wg<N>(), TPS = 256 / S;
   __shared__ cf buf[S][lds_slots<N>()];
   const int s = threadIdx.x / TPS, t = threadIdx.x % TPS;
   const int g = blockIdx.x * S + s; // symbol of this thread group (past nsym: idle, but at barriers)
   const bool live = g < nsym;
-  const int sym = g % 14, sf = g / 14;
-  const int slot = sym / 7, l = sym % 7;
+  const int sym = g % (2 * ns), sf = g / (2 * ns);
+  const int slot = sym / ns, l = sym % ns;
   const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
   const cf *src = (const cf *)(in + (size_t)(live ? sf : 0) * in_stride + start);
   fft_ip<N, 1, TPS>(src, buf[s], tw, t, live);
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
 template <int N>
 __global__ __launch_bounds__(256) void k_ofdm_rx_p(const float2 *__restrict__ in, size_t in_stride,
                                                    float2 *__restrict__ out, size_t out_stride, int nsym,
-                                                   int nre, int cp0, int cp, const float2 *__restrict__ tw,
+                                                   int nre, int cp0, int cp, int ns, const float2 *__restrict__ tw,
                                                    float scale) {
   constexpr int R0 = N % 8 == 0 ? 8 : N % 4 == 0 ? 4 : N % 2 == 0 ? 2 : 3;
   constexpr int nb0 = N / R0, NPT = (nb0 + 255) / 256;
@@ -269,8 +269,8 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_p(const float2 *__restrict__ in
   const int t = threadIdx.x;
   cf v[NPT][R0];
   auto load = [&](int g) {
-    const int sym = g % 14, sf = g / 14;
-    const int slot = sym / 7, l = sym % 7;
+    const int sym = g % (2 * ns), sf = g / (2 * ns);
+    const int slot = sym / ns, l = sym % ns;
     const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
     const cf *src = (const cf *)(in + (size_t)sf * in_stride + start);
 #pragma unroll
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_p(const float2 *__restrict__ in
     int tl = t; // and of the thread index: the stages' twiddle offsets are recomputed per symbol
     asm volatile("" : "+s"(twl), "+v"(tl));
     fft_ip<N, R0, 256>(nullptr, buf, twl, tl, true);
-    const int sym = g % 14, sf = g / 14;
+    const int sym = g % (2 * ns), sf = g / (2 * ns);
     cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
     const int h = nre / 2;
     for (int k = t; k < nre; k += 256) {
@@ -330,12 +330,26 @@ template <int N> static int ofdm_resident_wgs() {
   return n;
 }
 
+// CP lengths and symbols per slot (ofdm.c:75-76): normal CP ceil(160 N / 2048) then ceil(144 N / 2048),
+// 7 symbols; extended CP ceil(512 N / 2048) for all 6 symbols. Both fill 7.5 N samples per slot.
+static void cp_layout(int N, bool ext, int &cp0, int &cp, int &ns) {
+  if (ext) {
+    cp0 = cp = (int)ceilf(512.0f * N / 2048.0f);
+    ns = 6;
+  } else {
+    cp0 = (int)ceilf(160.0f * N / 2048.0f);
+    cp = (int)ceilf(144.0f * N / 2048.0f);
+    ns = 7;
+  }
+}
+
 hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
                           int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
-                          hipStream_t st) {
+                          bool ext_cp, hipStream_t st) {
   if (nsf <= 0) return hipSuccess;
-  const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
-  const int nsym = nsf * 14;
+  int cp0, cp, ns;
+  cp_layout(N, ext_cp, cp0, cp, ns);
+  const int nsym = nsf * 2 * ns;
   // SRSGPU_OFDM_PERSIST=1: the resident-grid kernel with next-symbol prefetch for the large sizes.
   // Off by default: alone on the GPU it took 68 us per 512 20 MHz subframes against 59 us for one
   // symbol per workgroup (profiles/r04_s6_kb_*.json), and its fixed grid fares worse still beside
@@ -350,7 +364,7 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
   if (N == n) {                                                                                    \
     const int res = ofdm_resident_wgs<n>(), per = (nsym + res - 1) / res;                          \
     hipLaunchKernelGGL(k_ofdm_rx_p<n>, dim3((unsigned)((nsym + per - 1) / per)), dim3(256), 0, st, in, \
-                       in_stride, out, out_stride, nsym, nre, cp0, cp, tw, scale);                 \
+                       in_stride, out, out_stride, nsym, nre, cp0, cp, ns, tw, scale);                 \
     return hipGetLastError();                                                                      \
   }
     OFDM_RX_P(2048)
@@ -361,7 +375,7 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
 #define OFDM_RX_C(n)                                                                               \
   case n:                                                                                          \
     hipLaunchKernelGGL(k_ofdm_rx_c<n>, dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \
-                       dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, tw, scale); \
+                       dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, ns, tw, scale); \
     return hipGetLastError();
   switch (N) {
     OFDM_RX_C(128)
@@ -377,7 +391,7 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
   }
 #undef OFDM_RX_C
   hipLaunchKernelGGL(k_ofdm_rx, dim3((unsigned)nsym), dim3(256), 0, st, in, in_stride, out, out_stride,
-                     N, nre, cp0, cp, tw, radices, nstages, scale);
+                     N, nre, cp0, cp, ns, tw, radices, nstages, scale);
   return hipGetLastError();
 }
 
@@ -387,11 +401,11 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
 // optional 1/sqrt(N) scaling, and the last cp samples copied in front of the symbol.
 __global__ __launch_bounds__(256) void k_ofdm_tx(const float2 *__restrict__ in, size_t in_stride,
                                                  float2 *__restrict__ out, size_t out_stride, int N,
-                                                 int nre, int cp0, int cp, const float2 *__restrict__ tw,
+                                                 int nre, int cp0, int cp, int ns, const float2 *__restrict__ tw,
                                                  const uint32_t radices, int nstages, float scale) {
   __shared__ cf buf[2][OFDM_MAXN];
-  const int sym = blockIdx.x % 14, sf = blockIdx.x / 14;
-  const int slot = sym / 7, l = sym % 7;
+  const int sym = blockIdx.x % (2 * ns), sf = blockIdx.x / (2 * ns);
+  const int slot = sym / ns, l = sym % ns;
   const cf *src = (const cf *)(in + (size_t)sf * in_stride + (size_t)sym * nre);
   const int h = nre / 2;
   for (int n = threadIdx.x; n < N; n += blockDim.x) {
@@ -427,11 +441,12 @@ __global__ __launch_bounds__(256) void k_ofdm_tx(const float2 *__restrict__ in, 
 
 hipError_t launch_ofdm_tx(const float2 *in, size_t in_stride, float2 *out, size_t out_stride, int nsf,
                           int N, int nre, const float2 *tw, uint32_t radices, int nstages, float scale,
-                          hipStream_t st) {
+                          bool ext_cp, hipStream_t st) {
   if (nsf <= 0) return hipSuccess;
-  const int cp0 = (int)ceilf(160.0f * N / 2048.0f), cp = (int)ceilf(144.0f * N / 2048.0f);
-  hipLaunchKernelGGL(k_ofdm_tx, dim3((unsigned)nsf * 14), dim3(256), 0, st, in, in_stride, out, out_stride,
-                     N, nre, cp0, cp, tw, radices, nstages, scale);
+  int cp0, cp, ns;
+  cp_layout(N, ext_cp, cp0, cp, ns);
+  hipLaunchKernelGGL(k_ofdm_tx, dim3((unsigned)nsf * 2 * ns), dim3(256), 0, st, in, in_stride, out, out_stride,
+                     N, nre, cp0, cp, ns, tw, radices, nstages, scale);
   return hipGetLastError();
 }
 

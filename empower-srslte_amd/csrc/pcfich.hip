@@ -39,7 +39,8 @@ extern "C" {
 
 int srsgpu_pcfich_create(srsgpu_pcfich_t **q, const srsgpu_cell_t *cell) {
   if (!q || !cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 ||
-      (cell->nof_ports != 1 && cell->nof_ports != 2 && cell->nof_ports != 4) || cell->nof_rx_ant < 1 || cell->nof_rx_ant > 2)
+      (cell->nof_ports != 1 && cell->nof_ports != 2 && cell->nof_ports != 4) || cell->nof_rx_ant < 1 || cell->nof_rx_ant > 2 ||
+      cell->cp > 1) // the PCFICH REGs lie in symbol 0, the same for both CPs (regs.c:477-512)
     return -1;
   srsgpu_pcfich *p = new srsgpu_pcfich;
   p->cell = *cell;

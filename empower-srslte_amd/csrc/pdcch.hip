@@ -23,11 +23,13 @@ struct Reg {
   bool assigned;
 };
 
-// regs.c:579-606 regs_num_x_symbol (normal cyclic prefix)
-int regs_num_x_symbol(uint32_t symbol, uint32_t nof_ports) {
+// regs.c:587-616 regs_num_x_symbol: symbol 3 (control regions of 4 symbols, nof_prb <= 10) carries
+// CRS with extended CP
+int regs_num_x_symbol(uint32_t symbol, uint32_t nof_ports, bool ext_cp) {
   switch (symbol) {
   case 0: return 2;
   case 1: return nof_ports == 4 ? 2 : 3;
+  case 3: return ext_cp ? 2 : 3;
   default: return 3;
   }
 }
@@ -203,7 +205,7 @@ int build_maps(const srsgpu_cell_t &cell, uint32_t phich_length, uint32_t phich_
   const uint32_t max_ctrl = nprb <= 10 ? 4 : 3, vo = id % 3;
   uint32_t n[4] = {0, 0, 0, 0}, nof_regs = 0;
   for (uint32_t i = 0; i < max_ctrl; i++) {
-    n[i] = (uint32_t)regs_num_x_symbol(i, np);
+    n[i] = (uint32_t)regs_num_x_symbol(i, np, cell.cp == 1);
     nof_regs += nprb * n[i];
   }
   std::vector<Reg> regs(nof_regs);
@@ -314,7 +316,7 @@ int srsgpu_pdcch_create(srsgpu_pdcch_t **q, const srsgpu_cell_t *cell, uint32_t 
                         uint32_t phich_resources) {
   if (!q || !cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || (cell->nof_ports != 1 &&
       cell->nof_ports != 2 && cell->nof_ports != 4) || cell->nof_rx_ant < 1 || cell->nof_rx_ant > 2 || phich_length > 1 ||
-      phich_resources > 3)
+      phich_resources > 3 || cell->cp > 1)
     return -1;
   srsgpu_pdcch *p = new srsgpu_pdcch;
   p->cell = *cell;
@@ -369,7 +371,8 @@ void srsgpu_pdcch_destroy(srsgpu_pdcch_t *q) {
 int srsgpu_pdcch_cell_map(const srsgpu_cell_t *cell, uint32_t phich_length, uint32_t phich_resources,
                           uint32_t cfi, uint32_t *idx, uint32_t max, uint32_t *nof_cce) {
   if (!cell || cell->nof_prb < 6 || cell->nof_prb > 110 || cell->id > 503 || (cell->nof_ports != 1 &&
-      cell->nof_ports != 2 && cell->nof_ports != 4) || phich_length > 1 || phich_resources > 3 || cfi < 1 || cfi > 3)
+      cell->nof_ports != 2 && cell->nof_ports != 4) || phich_length > 1 || phich_resources > 3 || cfi < 1 || cfi > 3 ||
+      cell->cp > 1)
     return -1;
   std::vector<uint32_t> maps[3];
   uint32_t ncce[3];

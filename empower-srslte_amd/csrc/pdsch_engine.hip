@@ -16,13 +16,13 @@
 namespace srsgpu {
 
 // ------------------------------------------------------------------ RE map ----
-// Gather order of srslte_pdsch_cp in read mode (pdsch.c:95-234): slots, OFDM symbols, allocated
-// PRBs; PSS/SSS (subframes 0/5, slot 0, last two symbols) and PBCH (subframe 0, slot 1, first 4
+// Gather order of srslte_pdsch_cp in read mode (pdsch.c:95-234): slots, OFDM symbols (7 per slot,
+// 6 with extended CP), allocated PRBs; PSS/SSS (subframes 0/5, slot 0, last two symbols) and PBCH (subframe 0, slot 1, first 4
 // symbols) cut the 6 (or, for odd nof_prb, 7) central PRBs; in symbols carrying CRS the
 // reference REs are skipped with prb_cp_ref's interval walk (prb_dl.c:51-82).
 static void re_map(const srsgpu_cell_t &c, uint32_t lstart_grant, uint32_t sf_idx,
                    const uint8_t prb[2][110], std::vector<uint32_t> &m) {
-  const uint32_t N = c.nof_prb, ns = 7, nref = c.nof_ports == 1 ? 2 : 4;
+  const uint32_t N = c.nof_prb, ns = c.cp == 1 ? 6 : 7, nref = c.nof_ports == 1 ? 2 : 4;
   m.clear();
   auto refsym = [&](uint32_t l) { return (l == 1 && c.nof_ports == 4) || l == 0 || l == ns - 3; };
   // prb_cp_ref: 'offset' REs, then (intervals-1) x [skip 1, take ri], then [skip 1, take ri-offset]
@@ -133,7 +133,7 @@ struct PdschEngine {
   int create(const srsgpu_cell_t &c, uint32_t nsb, uint32_t max_cb, uint32_t msf) {
     if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !msf ||
         (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4) || c.nof_rx_ant < 1 ||
-        c.nof_rx_ant > 2) {
+        c.nof_rx_ant > 2 || c.cp > 1) {
       fprintf(stderr, "srsgpu: invalid cell (nof_prb=%u id=%u ports=%u rx=%u)\n", c.nof_prb, c.id,
               c.nof_ports, c.nof_rx_ant);
       return -1;
@@ -546,6 +546,7 @@ void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {
 
 int srsgpu_pdsch_set_ce_rows(srsgpu_pdsch_t *q, int rows) {
   if (!q || (rows != 0 && rows != 1 && rows != 4)) return -1;
+  if (rows == 4 && q->e.cell.cp == 1) return -1; // 4 rows: the normal-CP CRS symbols 0 / 4 / 7 / 11
   q->e.ce_rows = rows;
   return 0;
 }

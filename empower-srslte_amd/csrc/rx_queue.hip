@@ -227,7 +227,7 @@ struct srsgpu_rxq {
     nports = cell.nof_ports;
     nrx = cell.nof_rx_ant;
     td_len = (size_t)15 * N;
-    gsz = (size_t)14 * 12 * cell.nof_prb;
+    gsz = (size_t)(cell.cp == 1 ? 12 : 14) * 12 * cell.nof_prb; // grid rows: OFDM symbols per subframe
     dlen = SRSGPU_DLSCH_DATA_LEN(75376) + 16;
     // 72 NOF_CCE(cfi) floats per subframe at most: the largest CCE count of the cell, which the
     // smallest PHICH allocation (normal length, Ng = 1/6) leaves (110 PRB: 96 CCEs)
@@ -246,6 +246,7 @@ struct srsgpu_rxq {
         srsgpu_pdsch_create(&pdsch, &cell, nsb + 1, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
       return -1;
     srsgpu_ofdm_rx_set_stream(ofdm, st);
+    if (srsgpu_ofdm_set_cp(ofdm, cell.cp)) return -1;
     srsgpu_chest_set_stream(chest, st);
     srsgpu_pdsch_set_stream(pdsch, st);
     for (Slot &s : slot) {

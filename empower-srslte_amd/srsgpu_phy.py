@@ -104,7 +104,7 @@ SOFTBUFFER_SIZE = 18600
 class srsgpu_cell_t(ctypes.Structure):
     """include/srsgpu/pdsch_batch.h"""
     _fields_ = [("nof_prb", ctypes.c_uint32), ("id", ctypes.c_uint32),
-                ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32)]
+                ("nof_ports", ctypes.c_uint32), ("nof_rx_ant", ctypes.c_uint32), ("cp", ctypes.c_uint32)]
 
 
 MIMO_SINGLE_ANTENNA, MIMO_TX_DIVERSITY, MIMO_SPATIAL_MULTIPLEX, MIMO_CDD = 0, 1, 2, 3
@@ -391,6 +391,7 @@ _sig = {
     "srsgpu_ofdm_rx_destroy": (None, [_vp]),
     "srsgpu_ofdm_rx_set_stream": (None, [_vp, _vp]),
     "srsgpu_ofdm_rx_set_normalize": (None, [_vp, _i32]),
+    "srsgpu_ofdm_set_cp": (_i32, [_vp, _u32]),
     "srsgpu_ofdm_rx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
     "srsgpu_ofdm_tx_sf_dev": (_i32, [_vp, _u32, _vp, _sz, _vp, _sz]),
     "srsgpu_chest_put_crs_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz]),
@@ -723,8 +724,8 @@ class Pcfich:
     """srsgpu_pcfich_t: batched srslte_pcfich_decode_multi (CFI detection) on device grids laid
     out as Pdsch's (include/srsgpu/pcfich_batch.h)."""
 
-    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, cp=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant, cp)
         self.q = _vp()
         if _lib.srsgpu_pcfich_create(ctypes.byref(self.q), ctypes.byref(self.cell)) != 0:
             raise RuntimeError("srsgpu_pcfich_create failed")
@@ -755,10 +756,10 @@ class Pcfich:
             self.q = None
 
 
-def pdcch_cell_map(nof_prb, cell_id, nof_ports, phich_length, phich_resources, cfi):
+def pdcch_cell_map(nof_prb, cell_id, nof_ports, phich_length, phich_resources, cfi, cp=0):
     """srsgpu_pdcch_cell_map (host only): (grid indices of the PDCCH symbols in srslte_regs_pdcch_get
     order, NOF_CCE(cfi)); None for an invalid cell"""
-    cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1)
+    cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1, cp)
     ncce = ctypes.c_uint32(0)
     n = _lib.srsgpu_pdcch_cell_map(ctypes.byref(cell), phich_length, phich_resources, cfi, None, 0,
                                    ctypes.byref(ncce))
@@ -809,8 +810,8 @@ class Pdcch:
     """srsgpu_pdcch_t: batched srslte_pdcch_extract_llr_multi and the srslte_ue_dl_find_dl_dci blind
     search on device grids laid out as Pdsch's (include/srsgpu/pdcch_batch.h)."""
 
-    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, phich_length=0, phich_resources=0):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+    def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, phich_length=0, phich_resources=0, cp=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant, cp)
         self.q = _vp()
         if _lib.srsgpu_pdcch_create(ctypes.byref(self.q), ctypes.byref(self.cell), phich_length,
                                     phich_resources) != 0:
@@ -887,8 +888,8 @@ class Pdsch:
     descrambling, CSI, DL-SCH decoding) on device grids."""
 
     def __init__(self, nof_prb, cell_id, nof_ports=1, nof_rx_ant=1, nof_softbuffers=16, max_cb=13,
-                 max_sf=64, stream=None):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+                 max_sf=64, stream=None, cp=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant, cp)
         self.q = _vp()
         if _lib.srsgpu_pdsch_create(ctypes.byref(self.q), ctypes.byref(self.cell), nof_softbuffers,
                                     max_cb, max_sf) != 0:
@@ -970,8 +971,8 @@ class Chest:
     """srsgpu_chest_t: batched CRS channel estimation (ports 0/1, normal CP) on device grids.
     With nof_ports = 2 grid i yields estimates i*2 (port 0) and i*2 + 1 (port 1)."""
 
-    def __init__(self, nof_prb, cell_id, max_grids=64, stream=None, nof_ports=1):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1)
+    def __init__(self, nof_prb, cell_id, max_grids=64, stream=None, nof_ports=1, cp=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, 1, cp)
         self.q = _vp()
         if _lib.srsgpu_chest_create(ctypes.byref(self.q), ctypes.byref(self.cell), max_grids) != 0:
             raise RuntimeError("srsgpu_chest_create failed")
@@ -1043,13 +1044,16 @@ def symbol_sz(nof_prb, standard_rates=False):
 
 
 class OfdmRx:
-    """srsgpu_ofdm_t: batched OFDM receive FFT (normal CP) on device sample buffers."""
+    """srsgpu_ofdm_t: batched OFDM receive FFT (normal CP, or extended with cp=1) on device sample
+    buffers."""
 
-    def __init__(self, nof_prb, symbol_size, normalize=False, stream=None):
+    def __init__(self, nof_prb, symbol_size, normalize=False, stream=None, cp=0):
         self.q = _vp()
         if _lib.srsgpu_ofdm_rx_create(ctypes.byref(self.q), nof_prb, symbol_size) != 0:
             raise RuntimeError("srsgpu_ofdm_rx_create failed")
         _lib.srsgpu_ofdm_rx_set_normalize(self.q, 1 if normalize else 0)
+        if _lib.srsgpu_ofdm_set_cp(self.q, cp) != 0:
+            raise RuntimeError("srsgpu_ofdm_set_cp failed")
         if stream is not None:
             _lib.srsgpu_ofdm_rx_set_stream(self.q, _vp(stream))
 
@@ -1124,8 +1128,8 @@ class RxQueue:
     subframes; one dispatcher thread decodes them in batches (OFDM -> chest -> PDSCH / DL-SCH)."""
 
     def __init__(self, nof_prb, cell_id, symbol_sz, nof_ports=1, nof_rx_ant=1, nof_softbuffers=16,
-                 max_batch=32, max_wait_us=500, max_halfits=8):
-        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant)
+                 max_batch=32, max_wait_us=500, max_halfits=8, cp=0):
+        self.cell = srsgpu_cell_t(nof_prb, cell_id, nof_ports, nof_rx_ant, cp)
         self.q = _vp()
         if _lib.srsgpu_rxq_create(ctypes.byref(self.q), ctypes.byref(self.cell), symbol_sz,
                                   nof_softbuffers, max_batch, max_wait_us, max_halfits) != 0:

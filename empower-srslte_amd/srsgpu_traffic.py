@@ -228,7 +228,7 @@ class MimoSubframes:
 
     def __init__(self, torch, dev, n_sf, seed=31, stream=None, snr_db=30.0, mimo=None, mcs=28, nof_prb=100,
                  cell_id=1, keep=None, max_halfits=8, codebook=1, nof_tb=2, early_stop=True, ce_rows=True,
-                 nof_ports=2):
+                 nof_ports=2, cp=0):
         import ctypes as ct
         self.torch, self.dev, self.max_halfits = torch, dev, max_halfits
         mimo = s.MIMO_CDD if mimo is None else mimo
@@ -237,19 +237,21 @@ class MimoSubframes:
         self.n = n
         self.nof_prb, self.cell_id = nof_prb, cell_id
         N = s.symbol_sz(nof_prb, True)
-        self.N, gsz = N, 14 * 12 * nof_prb
+        self.N, gsz = N, (12 if cp else 14) * 12 * nof_prb  # extended CP (cp=1): 12 symbols
         self.gsz = gsz
-        ntb = 1 if mimo == s.MIMO_TX_DIVERSITY else nof_tb
+        ntb = 1 if mimo in (s.MIMO_TX_DIVERSITY, s.MIMO_SINGLE_ANTENNA) else nof_tb
         self.ntb = ntb
         P = self.nports = nof_ports  # 4: transmit diversity over ports 0-3 (estimates in full grids)
-        assert P == 2 or (P == 4 and mimo == s.MIMO_TX_DIVERSITY and not ce_rows)
+        assert (P == 2 or (P == 4 and mimo == s.MIMO_TX_DIVERSITY and not ce_rows) or
+                (P == 1 and mimo == s.MIMO_SINGLE_ANTENNA))
+        assert not (cp and ce_rows)  # the 4 compact rows are the normal-CP CRS symbols
         tbs = s._lib.srsgpu_ra_tbs_from_idx(s._lib.srsgpu_ra_tbs_idx_from_mcs(mcs), nof_prb)
         mod = 1 if mcs < 10 else 2 if mcs < 17 else 3
         self.tbs = tbs
-        self.ofdm = s.OfdmRx(nof_prb, N, stream=stream)
-        self.chest = s.Chest(nof_prb, cell_id, max_grids=2 * n, stream=stream, nof_ports=P)
+        self.ofdm = s.OfdmRx(nof_prb, N, stream=stream, cp=cp)
+        self.chest = s.Chest(nof_prb, cell_id, max_grids=2 * n, stream=stream, nof_ports=P, cp=cp)
         self.pd = s.Pdsch(nof_prb, cell_id, nof_ports=P, nof_rx_ant=2, nof_softbuffers=2 * n, max_cb=13, max_sf=n,
-                          stream=stream)
+                          stream=stream, cp=cp)
         s._lib.srsgpu_dlsch_set_early_stop(s._vp(self.pd.dlsch_q), int(bool(early_stop)))
         self.chest.set_ce_rows(ce_rows)  # compact estimate rows, identical LLRs (as MixedCells)
         self.pd.set_ce_rows(4 if ce_rows else 0)
@@ -303,8 +305,8 @@ class MimoSubframes:
         # a flat 2 x P channel per subframe, from the subframe's global index
         g = torch.Generator(device="cpu").manual_seed(seed + 7)
         ph = torch.rand(16, 2, P, generator=g) * 6.283
-        amp = torch.tensor([[1.0, 0.45], [0.45, 1.0]]) if P == 2 else torch.tensor([[1.0, 0.45, 0.8, 0.3],
-                                                                                  [0.45, 1.0, 0.3, 0.8]])
+        amp = {1: torch.tensor([[1.0], [0.45]]), 2: torch.tensor([[1.0, 0.45], [0.45, 1.0]]),
+               4: torch.tensor([[1.0, 0.45, 0.8, 0.3], [0.45, 1.0, 0.3, 0.8]])}[P]
         H = (amp * torch.exp(1j * ph)).to(torch.complex64)
         Hs = H[torch.tensor([i % 16 for i in self.kept])].to(self.dev)  # [sf][rx][port]
         y = torch.einsum("sap,spt->sat", Hs, xp)

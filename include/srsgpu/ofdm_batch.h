@@ -9,7 +9,9 @@
  * srsgpu_ofdm_rx_set_normalize(q, 1)). The grid row is bins [N - nre/2, N) followed by
  * [1, 1 + nre/2): the DC bin is skipped. Output: 14 x nof_prb*12 complex float per subframe, the
  * layout the channel estimator and PDSCH receiver take.
- * Normal CP, non-MBSFN subframes; frequency shift (srslte_ofdm_set_freq_shift) is not supported.
+ * With srsgpu_ofdm_set_cp(q, 1) (SRSLTE_CP_EXT, ofdm.c:75-76): 12 symbols, every CP
+ * ceil(512 N/2048) samples, still 15 N samples per subframe; the grid has 12 rows.
+ * Non-MBSFN subframes; frequency shift (srslte_ofdm_set_freq_shift) is not supported.
  */
 #ifndef SRSGPU_OFDM_BATCH_H
 #define SRSGPU_OFDM_BATCH_H
@@ -30,8 +32,10 @@ int srsgpu_ofdm_rx_create(srsgpu_ofdm_t **q, uint32_t nof_prb, uint32_t symbol_s
 void srsgpu_ofdm_rx_destroy(srsgpu_ofdm_t *q);
 void srsgpu_ofdm_rx_set_stream(srsgpu_ofdm_t *q, void *hip_stream);
 void srsgpu_ofdm_rx_set_normalize(srsgpu_ofdm_t *q, int enable);
+/* cyclic prefix of the handle, receive and transmit (srslte_cp_t: 0 normal, default; 1 extended) */
+int srsgpu_ofdm_set_cp(srsgpu_ofdm_t *q, uint32_t cp);
 /* nof_sf subframes: input i at d_in + i*in_stride complex samples (>= 15 symbol_sz), grid i at
- * d_out + i*out_stride complex elements (>= 14 * 12 * nof_prb). Asynchronous on the stream. */
+ * d_out + i*out_stride complex elements (>= 14 * 12 * nof_prb, 12 * 12 * nof_prb for extended CP). Asynchronous on the stream. */
 int srsgpu_ofdm_rx_sf_dev(srsgpu_ofdm_t *q, uint32_t nof_sf, const float *d_in, size_t in_stride,
                           float *d_out, size_t out_stride);
 

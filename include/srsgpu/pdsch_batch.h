@@ -48,6 +48,8 @@ typedef struct {
   uint32_t nof_ports;  /* CRS ports: the RE map skips their reference signals; SISO decoding
                           needs 1 port */
   uint32_t nof_rx_ant; /* 1 or 2 */
+  uint32_t cp;         /* srslte_cp_t: 0 normal (7 symbols per slot), 1 extended (6 symbols per slot,
+                          CRS in symbols 0 / 3 of each slot, srslte_refsignal_cs_nsymbol) */
 } srsgpu_cell_t;
 
 /* srslte_mimo_type_t values accepted by the GPU receiver */

@@ -31,8 +31,9 @@
  * a small registry keyed by the object's address, because the reference structs have no spare
  * field. The registry is shared by srsUE's PHY worker threads (phch_worker.cc, one ue_dl per
  * worker): lookups and claims hold a mutex; a registered object is only used by the thread that
- * owns the object, as in the reference. Calls that are out of the GPU path's scope (MBSFN,
- * extended CP, spatial multiplexing, 4 ports) return SRSLTE_ERROR and print a message. There is no
+ * owns the object, as in the reference. Calls that are out of the GPU path's scope (MBSFN, frequency
+ * shift, 3 ports, 4-port CDD / spatial multiplexing) return SRSLTE_ERROR and print a message. Normal
+ * and extended CP and 1, 2 or 4 CRS ports run on the GPU. There is no
  * hidden CPU path behind them. Every device allocation and copy is checked: a failure returns
  * SRSLTE_ERROR (srslte_ofdm_rx_sf, void in the reference, prints and returns) and leaves the
  * object's GPU state released, so the next call starts afresh.
@@ -185,23 +186,25 @@ int srsgpu_shim_live(void) {
 
 /* ------------------------------------------------------------------ OFDM ---- */
 void srslte_ofdm_rx_sf(srslte_ofdm_t *q) {
-  if (q->cp != SRSLTE_CP_NORM || q->mbsfn_subframe || q->freq_shift) {
-    fprintf(stderr, "srsgpu shim: only normal-CP, non-MBSFN, unshifted OFDM runs on the GPU\n");
+  if (q->mbsfn_subframe || q->freq_shift) {
+    fprintf(stderr, "srsgpu shim: only non-MBSFN, unshifted OFDM runs on the GPU\n");
     return;
   }
   const uint32_t nof_prb = q->nof_re / SRSLTE_NRE;
   shim_entry_t *e = shim_get(q, SHIM_OFDM);
   if (!e) return;
   const size_t nout = SRSLTE_SF_LEN_RE(nof_prb, q->cp);
-  if (e->aux != q->symbol_sz || e->nof_prb != nof_prb || !e->gpu) {
+  const uint32_t ext = q->cp == SRSLTE_CP_EXT;
+  if (e->aux != 2 * q->symbol_sz + ext || e->nof_prb != nof_prb || !e->gpu) {
     shim_reset(e);
     if (srsgpu_ofdm_rx_create((srsgpu_ofdm_t **)&e->gpu, nof_prb, q->symbol_sz) ||
+        srsgpu_ofdm_set_cp((srsgpu_ofdm_t *)e->gpu, ext) ||
         shim_alloc(&e->d_a, sizeof(cf_t) * q->sf_sz) || shim_alloc(&e->d_b, sizeof(cf_t) * nout)) {
       shim_reset(e);
       fprintf(stderr, "srsgpu shim: srslte_ofdm_rx_sf: GPU setup failed\n");
       return;
     }
-    e->aux = q->symbol_sz;
+    e->aux = 2 * q->symbol_sz + ext;
     e->nof_prb = nof_prb;
   }
   srsgpu_ofdm_rx_set_normalize((srsgpu_ofdm_t *)e->gpu, q->fft_plan.norm);
@@ -219,24 +222,25 @@ int srslte_pcfich_decode_multi(srslte_pcfich_t *q, cf_t *sf_symbols[SRSLTE_MAX_P
                                cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
                                uint32_t nsubframe, uint32_t *cfi, float *corr_result) {
   if (!q || !sf_symbols || nsubframe >= SRSLTE_NSUBFRAMES_X_FRAME) return SRSLTE_ERROR_INVALID_INPUTS;
-  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->nof_rx_antennas > 2 || !ce) {
-    fprintf(stderr, "srsgpu shim: GPU PCFICH covers 1-2 ports, normal CP, 1-2 rx antennas\n");
+  if (q->cell.nof_ports == 3 || q->cell.nof_ports > 4 || q->nof_rx_antennas > 2 || !ce) {
+    fprintf(stderr, "srsgpu shim: GPU PCFICH covers 1, 2 or 4 ports, 1-2 rx antennas\n");
     return SRSLTE_ERROR;
   }
   shim_entry_t *e = shim_get(q, SHIM_PCFICH);
   if (!e) return SRSLTE_ERROR;
   const uint32_t np = q->cell.nof_ports, nrx = q->nof_rx_antennas, n = q->cell.nof_prb * SRSLTE_NRE;
-  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np * 4 + nrx || !e->gpu) {
+  const uint32_t key = (np * 4 + nrx) * 2 + (q->cell.cp == SRSLTE_CP_EXT);
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != key || !e->gpu) {
     shim_reset(e);
-    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, nrx};
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, nrx, q->cell.cp == SRSLTE_CP_EXT};
     if (srsgpu_pcfich_create((srsgpu_pcfich_t **)&e->gpu, &c) || shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) ||
-        shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) || shim_alloc(&e->d_c, sizeof(float) * 2)) { /* cfi, corr */
+        shim_alloc(&e->d_b, sizeof(cf_t) * n * 8) || shim_alloc(&e->d_c, sizeof(float) * 2)) { /* cfi, corr */
       shim_reset(e);
       return SRSLTE_ERROR;
     }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
-    e->aux = np * 4 + nrx;
+    e->aux = key;
   }
   for (uint32_t a = 0; a < nrx; a++) {
     if (shim_copy(e->d_a + 2 * (size_t)a * n, sf_symbols[a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
@@ -264,19 +268,20 @@ int srslte_pdcch_extract_llr_multi(srslte_pdcch_t *q, cf_t *sf_symbols[SRSLTE_MA
                                    cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], float noise_estimate,
                                    uint32_t nsubframe, uint32_t cfi) {
   if (!q || nsubframe >= SRSLTE_NSUBFRAMES_X_FRAME || cfi < 1 || cfi > 3) return SRSLTE_ERROR_INVALID_INPUTS;
-  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || q->nof_rx_antennas < 1 || q->nof_rx_antennas > 2 ||
+  if (q->cell.nof_ports == 3 || q->cell.nof_ports > 4 || q->nof_rx_antennas < 1 || q->nof_rx_antennas > 2 ||
       !sf_symbols || !ce) {
-    fprintf(stderr, "srsgpu shim: GPU PDCCH covers 1-2 ports, normal CP, 1-2 rx antennas\n");
+    fprintf(stderr, "srsgpu shim: GPU PDCCH covers 1, 2 or 4 ports, 1-2 rx antennas\n");
     return SRSLTE_ERROR;
   }
   shim_entry_t *e = shim_get(q, SHIM_PDCCH);
   if (!e) return SRSLTE_ERROR;
   const uint32_t np = q->cell.nof_ports, nrx = q->nof_rx_antennas, nprb = q->cell.nof_prb;
-  const uint32_t key = ((q->cell.phich_length * 4u + q->cell.phich_resources) * 4u + np) * 4u + nrx;
-  const size_t n = SRSLTE_SF_LEN_RE(nprb, SRSLTE_CP_NORM);
+  const uint32_t ext = q->cell.cp == SRSLTE_CP_EXT;
+  const uint32_t key = (((q->cell.phich_length * 4u + q->cell.phich_resources) * 8u + np) * 4u + nrx) * 2u + ext;
+  const size_t n = SRSLTE_SF_LEN_RE(nprb, q->cell.cp);
   if (e->nof_prb != nprb || e->cell_id != q->cell.id || e->aux != key || !e->gpu) {
     shim_reset(e);
-    srsgpu_cell_t c = {nprb, q->cell.id, np, nrx};
+    srsgpu_cell_t c = {nprb, q->cell.id, np, nrx, ext};
     if (srsgpu_pdcch_create((srsgpu_pdcch_t **)&e->gpu, &c, q->cell.phich_length, q->cell.phich_resources) ||
         shim_alloc(&e->d_a, sizeof(cf_t) * n * nrx) || shim_alloc(&e->d_b, sizeof(cf_t) * n * nrx * np) ||
         shim_alloc(&e->d_c, sizeof(float) * SHIM_PDCCH_LLR_CAP)) {
@@ -379,25 +384,26 @@ static void shim_gauss(srslte_chest_dl_t *q, uint32_t order, float std_dev) {
 int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_PORTS],
                                    cf_t *ce[SRSLTE_MAX_PORTS][SRSLTE_MAX_PORTS], uint32_t sf_idx,
                                    uint32_t nof_rx_antennas) {
-  if (q->cell.nof_ports > 2 || q->cell.cp != SRSLTE_CP_NORM || nof_rx_antennas > 2) {
-    fprintf(stderr, "srsgpu shim: GPU channel estimation covers CRS ports 0-1, normal CP, 2 rx\n");
+  if (q->cell.nof_ports == 3 || q->cell.nof_ports > 4 || nof_rx_antennas > 2) {
+    fprintf(stderr, "srsgpu shim: GPU channel estimation covers 1, 2 or 4 CRS ports, 1-2 rx\n");
     return SRSLTE_ERROR;
   }
   shim_entry_t *e = shim_get(q, SHIM_CHEST);
   if (!e) return SRSLTE_ERROR;
   const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
-  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
+  const uint32_t key = np * 2 + (q->cell.cp == SRSLTE_CP_EXT);
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != key || !e->gpu) {
     shim_reset(e);
-    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, 1};
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, 1, q->cell.cp == SRSLTE_CP_EXT};
     if (srsgpu_chest_create((srsgpu_chest_t **)&e->gpu, &c, 2) || shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) ||
-        shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) ||
-        shim_alloc(&e->d_c, sizeof(float) * 4 * 5)) { /* noise [4] + measurements [4][4] */
+        shim_alloc(&e->d_b, sizeof(cf_t) * n * 8) ||
+        shim_alloc(&e->d_c, sizeof(float) * 8 * 5)) { /* noise [8] + measurements [8][4] */
       shim_reset(e);
       return SRSLTE_ERROR;
     }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
-    e->aux = np;
+    e->aux = key;
   }
   srsgpu_chest_t *g = (srsgpu_chest_t *)e->gpu;
   const srsgpu_chest_cfg_t cfg = {q->average_subframe, (uint32_t)q->noise_alg, q->smooth_filter_auto,
@@ -408,10 +414,10 @@ int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_
     return SRSLTE_ERROR;
   /* in/out state: the noise estimate (kept by PSS / EMPTY outside subframes 0 and 5) and the
    * measurements left untouched when disabled */
-  float st[4 + 16];
+  float st[8 + 32];
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
     for (uint32_t p = 0; p < np; p++) {
-      float *m = &st[4 + 4 * (a * np + p)];
+      float *m = &st[8 + 4 * (a * np + p)];
       st[a * np + p] = q->noise_estimate[a][p];
       m[0] = q->rsrp[a][p];
       m[1] = q->rssi[a][p];
@@ -422,7 +428,7 @@ int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_
   uint32_t sfs[2] = {sf_idx, sf_idx};
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
     if (shim_copy(e->d_a + 2 * (size_t)a * n, input[a], sizeof(cf_t) * n, H2D)) return SRSLTE_ERROR;
-  if (srsgpu_chest_estimate_meas_dev(g, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c, e->d_c + 4))
+  if (srsgpu_chest_estimate_meas_dev(g, sfs, nof_rx_antennas, e->d_a, n, e->d_b, e->d_c, e->d_c + 8))
     return SRSLTE_ERROR;
   if (shim_copy(st, e->d_c, sizeof(st), D2H)) return SRSLTE_ERROR;
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
@@ -431,7 +437,7 @@ int srslte_chest_dl_estimate_multi(srslte_chest_dl_t *q, cf_t *input[SRSLTE_MAX_
         return SRSLTE_ERROR;
   for (uint32_t a = 0; a < nof_rx_antennas; a++)
     for (uint32_t p = 0; p < np; p++) {
-      const float *m = &st[4 + 4 * (a * np + p)];
+      const float *m = &st[8 + 4 * (a * np + p)];
       q->noise_estimate[a][p] = st[a * np + p];
       q->rsrp[a][p] = m[0];
       q->rssi[a][p] = m[1];
@@ -810,18 +816,19 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
                     nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
   const bool cdd = cfg->mimo_type == SRSLTE_MIMO_TYPE_CDD && q->cell.nof_ports == 2 && nof_tb == 2 &&
                    cfg->nof_layers == 2 && q->nof_rx_antennas == 2;
-  /* TM2 / DCI 1A on a 2-port cell: SFBC transmit diversity, one TB (precoding.c:1811-1818) */
-  const bool txdiv = cfg->mimo_type == SRSLTE_MIMO_TYPE_TX_DIVERSITY && q->cell.nof_ports == 2 &&
+  /* TM2 / DCI 1A on a 2- or 4-port cell: SFBC (SFBC-FSTD) transmit diversity, one TB (precoding.c:1811-1818) */
+  const bool txdiv = cfg->mimo_type == SRSLTE_MIMO_TYPE_TX_DIVERSITY && (q->cell.nof_ports == 2 || q->cell.nof_ports == 4) &&
                      nof_tb == 1 && cfg->grant.tb_en[0] && q->nof_rx_antennas <= 2;
   /* TM4 closed-loop spatial multiplexing (precoding.c:1715-1760): 2 TBs on 2 layers (2x2 MMSE) or
    * TB 0 on 1 layer (2x1 MRC), 2 ports, 2 rx */
   const bool sm = cfg->mimo_type == SRSLTE_MIMO_TYPE_SPATIAL_MULTIPLEX && q->cell.nof_ports == 2 &&
                   q->nof_rx_antennas == 2 &&
                   ((nof_tb == 2 && cfg->nof_layers == 2) || (nof_tb == 1 && cfg->nof_layers == 1 && cfg->grant.tb_en[0]));
-  if ((!siso && !cdd && !txdiv && !sm) || q->cell.cp != SRSLTE_CP_NORM || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
-    fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port), TM2 transmit diversity (2 ports, 1-2 "
+  if ((!siso && !cdd && !txdiv && !sm) || q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
+    fprintf(stderr, "srsgpu shim: GPU PDSCH covers TM1 (1 port), TM2 transmit diversity (2 or 4 ports, 1-2 "
                     "rx), TM3 CDD (2 ports, 2 layers, 2 rx) and TM4 spatial multiplexing (2 ports, 2 rx, "
-                    "1-2 layers), normal CP, 16-bit or 8-bit LLRs (the same in the PDSCH and its DL-SCH)\n");
+                    "1-2 layers), normal or extended CP, 16-bit or 8-bit LLRs (the same in the PDSCH and its "
+                    "DL-SCH)\n");
     return SRSLTE_ERROR;
   }
   if (nof_tb == 1 && acks[0]) return SRSLTE_SUCCESS; /* pdsch.c:963-965 */
@@ -831,19 +838,20 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   const uint32_t n = SRSLTE_SF_LEN_RE(q->cell.nof_prb, q->cell.cp), np = q->cell.nof_ports;
   const uint32_t max_tbs = (uint32_t)srslte_ra_tbs_from_idx(26, q->cell.nof_prb);
   const size_t dlen = SRSGPU_DLSCH_DATA_LEN(max_tbs) + 16;
-  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != np || !e->gpu) {
+  const uint32_t key = (np * 4 + q->nof_rx_antennas) * 2 + (q->cell.cp == SRSLTE_CP_EXT);
+  if (e->nof_prb != q->cell.nof_prb || e->cell_id != q->cell.id || e->aux != key || !e->gpu) {
     shim_reset(e);
-    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, q->nof_rx_antennas};
+    srsgpu_cell_t c = {q->cell.nof_prb, q->cell.id, np, q->nof_rx_antennas, q->cell.cp == SRSLTE_CP_EXT};
     const uint32_t max_cb = max_tbs / (SRSLTE_TCOD_MAX_LEN_CB - 24) + 1; /* softbuffer.c:56 */
     if (srsgpu_pdsch_create((srsgpu_pdsch_t **)&e->gpu, &c, SHIM_MAX, max_cb, 1) ||
-        shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) || shim_alloc(&e->d_b, sizeof(cf_t) * n * 4) ||
+        shim_alloc(&e->d_a, sizeof(cf_t) * n * 2) || shim_alloc(&e->d_b, sizeof(cf_t) * n * 8) ||
         shim_alloc(&e->d_c, 2 * dlen) || shim_alloc(&e->d_d, 4 * sizeof(int32_t))) {
       shim_reset(e);
       return SRSLTE_ERROR;
     }
     e->nof_prb = q->cell.nof_prb;
     e->cell_id = q->cell.id;
-    e->aux = np;
+    e->aux = key;
   }
   srsgpu_pdsch_t *g = (srsgpu_pdsch_t *)e->gpu;
   srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(g);

@@ -1,5 +1,5 @@
 """CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's downlink CRS
-channel estimation for CRS ports 0-3, normal CP (paths relative to
+channel estimation for CRS ports 0-3, normal and extended CP (cp=1: 6 symbols per slot; paths relative to
 /root/reference/lib/src/phy):
 
   crs_pilots        ch_estimation/refsignal_dl.c:265-318 (Gold sequence per slot/symbol)
@@ -46,27 +46,36 @@ def gold(cinit, n):
     return x1[NC:NC + n] ^ x2[NC:NC + n]
 
 
-def syms(port=0):
-    """refsignal_dl.c:76-85, 112-122: the CRS symbols of a port in a normal-CP subframe"""
-    return (0, 4, 7, 11) if port < 2 else (1, 8)
+def nsymb(cp=0):
+    """SRSLTE_CP_NSYMB: OFDM symbols per slot"""
+    return 6 if cp else 7
 
 
-def crs_pilots(nof_prb, cell_id, sf_idx, port=0):
-    """[CRS symbols][2*nof_prb] complex pilots of ports 0/1 (symbols 0, 4, 7, 11) or 2/3 (1, 8):
-    csr_refs.pilots[port / 2] (refsignal_dl.c:291-313, l' = 0 / 4 or 1 in each slot)"""
-    lps = (0, 4) if port < 2 else (1,)
+def syms(port=0, cp=0):
+    """srslte_refsignal_cs_nsymbol (refsignal_dl.c:112-122): the CRS symbols of a port in a subframe,
+    normal CP 0 / 4 / 7 / 11 or 1 / 8, extended CP 0 / 3 / 6 / 9 or 1 / 7"""
+    n = nsymb(cp)
+    return (0, n - 3, n, 2 * n - 3) if port < 2 else (1, n + 1)
+
+
+SYMS = syms(0)
+
+
+def crs_pilots(nof_prb, cell_id, sf_idx, port=0, cp=0):
+    """[CRS symbols][2*nof_prb] complex pilots of ports 0/1 or 2/3: csr_refs.pilots[port / 2]
+    (refsignal_dl.c:291-313, l' = 0 / nsymb - 3 or 1 in each slot, N_cp = 1 normal, 0 extended)"""
+    lps = (0, nsymb(cp) - 3) if port < 2 else (1,)
     out = np.zeros((2 * len(lps), 2 * nof_prb), np.complex128)
     m = np.arange(2 * nof_prb) + 110 - nof_prb
     for s in range(2):
         ns = 2 * sf_idx + s
         for li, lp in enumerate(lps):
-            cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + 1
+            cinit = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + (0 if cp else 1)
             c = gold(cinit, 4 * 110).astype(np.float64)
             out[len(lps) * s + li] = ((1 - 2 * c[2 * m]) + 1j * (1 - 2 * c[2 * m + 1])) / np.sqrt(2)
     return out
 
 
-SYMS = syms(0)
 
 
 def fidx(cell_id, l, port=0):
@@ -74,11 +83,11 @@ def fidx(cell_id, l, port=0):
     return ((3 if (l % 2) ^ (port % 2) else 0) + cell_id % 6) % 6
 
 
-def ls_estimates(grid, nof_prb, cell_id, sf_idx, port=0):
-    g = grid.reshape(14, 12 * nof_prb)
-    pil = crs_pilots(nof_prb, cell_id, sf_idx, port)  # ports 2p and 2p+1 share pilots[p]
+def ls_estimates(grid, nof_prb, cell_id, sf_idx, port=0, cp=0):
+    g = grid.reshape(2 * nsymb(cp), 12 * nof_prb)
+    pil = crs_pilots(nof_prb, cell_id, sf_idx, port, cp)  # ports 2p and 2p+1 share pilots[p]
     est = np.zeros_like(pil)
-    for l, s in enumerate(syms(port)):
+    for l, s in enumerate(syms(port, cp)):
         est[l] = g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] * np.conj(pil[l])
     return est
 
@@ -102,9 +111,14 @@ def noise_refs(est, cell_id, port=0):
     return np.mean(np.abs(tmp) ** 2) / ns * np.sqrt(5.0)
 
 
-def interp_time(ce, port=0):
-    """chest_dl.c:421-431 on a [14][nsc] grid whose CRS rows are filled"""
-    if port < 2:
+def interp_time(ce, port=0, cp=0):
+    """chest_dl.c:421-442 on a [14][nsc] (extended CP [12][nsc]) grid whose CRS rows are filled;
+    segments (a, b, d, first, count, start): rows first .. first+count-1 = running sums of (b - a) / d
+    from row start"""
+    if cp:  # chest_dl.c:433-441
+        segs = (((0, 3, 3, 1, 2, 0), (3, 6, 3, 4, 2, 3), (6, 9, 3, 7, 2, 6), (6, 9, 3, 10, 2, 9)) if port < 2 else
+                ((7, 1, 6, 0, 1, 1), (1, 7, 6, 2, 5, 1), (1, 7, 6, 8, 4, 1)))
+    elif port < 2:
         segs = ((0, 4, 4, 1, 3, 0), (4, 7, 3, 5, 2, 4), (7, 11, 4, 8, 3, 7), (7, 11, 4, 12, 2, 11))
     else:
         segs = ((8, 1, 7, 0, 1, 1), (1, 8, 7, 2, 6, 1), (1, 8, 7, 9, 5, 1))
@@ -148,16 +162,16 @@ def interp_freq(x, off_st, M=6):
     return out
 
 
-def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0):
-    """-> (ce grid [14 * 12*nof_prb] complex128, noise estimate) of CRS port `port`"""
-    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+def estimate(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0, cp=0):
+    """-> (ce grid [14 (12) * 12*nof_prb] complex128, noise estimate) of CRS port `port`"""
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port, cp)
     noise = noise_refs(est, cell_id, port)
     f = np.asarray(filt, np.float64)
     sm = est if (len(f) == 0 or (len(f) == 3 and f[0] == 0)) else np.stack([smooth(r, f) for r in est])
-    ce = np.zeros((14, 12 * nof_prb), np.complex128)
-    for l, s in enumerate(syms(port)):
+    ce = np.zeros((2 * nsymb(cp), 12 * nof_prb), np.complex128)
+    for l, s in enumerate(syms(port, cp)):
         ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
-    interp_time(ce, port)
+    interp_time(ce, port, cp)
     return ce.reshape(-1), noise
 
 
@@ -194,52 +208,52 @@ def _avg_power(x):
     return float(np.mean(np.abs(x) ** 2))
 
 
-def noise_pss(grid, ce, nof_prb, cell_id, nof_ports):
+def noise_pss(grid, ce, nof_prb, cell_id, nof_ports, cp=0):
     nsc = 12 * nof_prb
-    k = 6 * nsc + nsc // 2 - 31  # srslte_pss_get_slot: last symbol of slot 0
+    k = (nsymb(cp) - 1) * nsc + nsc // 2 - 31  # srslte_pss_get_slot: last symbol of slot 0
     r = ce[k:k + 62] * pss_sequence(cell_id % 3) - grid[k:k + 62]
     return nof_ports * _avg_power(r) / np.sqrt(2)
 
 
-def noise_empty(grid, nof_prb):
+def noise_empty(grid, nof_prb, cp=0):
     nsc = 12 * nof_prb
-    ks = 5 * nsc + nsc // 2 - 31
-    kp = 6 * nsc + nsc // 2 - 31
+    ks = (nsymb(cp) - 2) * nsc + nsc // 2 - 31
+    kp = (nsymb(cp) - 1) * nsc + nsc // 2 - 31
     return (_avg_power(grid[ks - 5:ks]) + _avg_power(grid[ks + 62:ks + 67]) +
             _avg_power(grid[kp - 5:kp]) + _avg_power(grid[kp + 62:kp + 67]))
 
 
-def measurements(grid, nof_prb, cell_id, sf_idx, port=0, symbol_sz=1536):
+def measurements(grid, nof_prb, cell_id, sf_idx, port=0, symbol_sz=1536, cp=0):
     """(rsrp, rssi, rsrp_corr, cfo) as srslte_chest_dl_estimate_port leaves them in q. The CFO
     (chest_dl.c:583-603) always reads 4 rows of the shared pilot buffer: for ports 2 / 3, which
     fill only the first 2, rows 2 and 3 still hold port 1's estimates of the same rx antenna
     (srslte_chest_dl_estimate_multi runs the ports in order)"""
-    g = grid.reshape(14, 12 * nof_prb)
-    sy = syms(port)
+    g = grid.reshape(2 * nsymb(cp), 12 * nof_prb)
+    sy = syms(port, cp)
     recv = np.stack([g[s, fidx(cell_id, l, port) + 6 * np.arange(2 * nof_prb)] for l, s in enumerate(sy)])
-    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port, cp)
     rsrp = _avg_power(recv)
     rssi = float(sum(np.sum(np.abs(g[s]) ** 2) for s in sy) / len(sy))
     corr = abs(est.sum() / est.size) ** 2
-    e4 = est if port < 2 else np.concatenate([est, ls_estimates(grid, nof_prb, cell_id, sf_idx, 1)[2:]])
+    e4 = est if port < 2 else np.concatenate([est, ls_estimates(grid, nof_prb, cell_id, sf_idx, 1, cp)[2:]])
     acc = np.sum(e4[0] * np.conj(e4[2])) + np.sum(e4[1] * np.conj(e4[3]))
     n = float(symbol_sz)
     ng = float(np.ceil(144 * n / 2048))
-    cfo = -np.angle(acc) * n / (7 * (n + ng)) / 2 / np.pi
+    cfo = -np.angle(acc) * n / (nsymb(cp) * (n + ng)) / 2 / np.pi
     return rsrp, rssi, corr, cfo
 
 
 def estimate_full(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0, average=False,
-                  noise_alg="refs", filt_auto=False, noise_in=0.0, nof_ports=1):
+                  noise_alg="refs", filt_auto=False, noise_in=0.0, nof_ports=1, cp=0):
     """chest_interpolate_noise_est (chest_dl.c:606-639) in any of srsUE's configurations.
     -> (ce, noise): noise is the value q->noise_estimate[rx][port] holds afterwards (noise_in when
     the algorithm leaves it alone: PSS / EMPTY outside subframes 0 and 5)"""
-    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port)
+    est = ls_estimates(grid, nof_prb, cell_id, sf_idx, port, cp)
     noise = noise_refs(est, cell_id, port) if noise_alg == "refs" else noise_in
     f = gauss_filter(4, noise * 200.0) if filt_auto else np.asarray(filt, np.float64)
     smoothing = not (len(f) == 0 or (len(f) == 3 and f[0] == 0))
     nsc = 12 * nof_prb
-    ce = np.zeros((14, nsc), np.complex128)
+    ce = np.zeros((2 * nsymb(cp), nsc), np.complex128)
     if average:
         # without smoothing the reference interpolates the raw pilot buffer (symbols 0 and 4
         # back to back) as if it were the averaged row (chest_dl.c:619-621 + 393-399)
@@ -247,10 +261,11 @@ def estimate_full(grid, nof_prb, cell_id, sf_idx, filt=(0.1, 0.8, 0.1), port=0, 
         ce[:] = interp_freq(row, cell_id % 3, M=3)[None, :]
     else:
         sm = np.stack([smooth(r, f) for r in est]) if smoothing else est
-        for l, s in enumerate(syms(port)):
+        for l, s in enumerate(syms(port, cp)):
             ce[s] = interp_freq(sm[l], fidx(cell_id, l, port))
-        interp_time(ce, port)
+        interp_time(ce, port, cp)
     ce = ce.reshape(-1)
     if noise_alg != "refs" and sf_idx in (0, 5):
-        noise = noise_pss(grid, ce, nof_prb, cell_id, nof_ports) if noise_alg == "pss" else noise_empty(grid, nof_prb)
+        noise = (noise_pss(grid, ce, nof_prb, cell_id, nof_ports, cp) if noise_alg == "pss"
+                 else noise_empty(grid, nof_prb, cp))
     return ce, noise

@@ -1,4 +1,4 @@
-"""CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's normal-CP OFDM
+"""CPU ORACLE — TEST INFRASTRUCTURE ONLY. numpy (float64) restatement of srsLTE's normal- and extended-CP OFDM
 modulator / demodulator (paths relative to /root/reference/lib/src/phy):
 
   rx_sf   dft/ofdm.c:401-470 srslte_ofdm_rx_sf with the guru plan of :86-104: per symbol the N
@@ -15,20 +15,25 @@ import math
 import numpy as np
 
 
-def cp_lens(N):
+def cp_lens(N, ext=False):
+    """(first, other) CP lengths of a slot (ofdm.c:75-76): normal ceil(160 N/2048), ceil(144 N/2048);
+    extended ceil(512 N/2048) for all 6 symbols"""
+    if ext:
+        return math.ceil(512 * N / 2048), math.ceil(512 * N / 2048)
     return math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
 
 
-def symbol_starts(N):
-    cp0, cp = cp_lens(N)
-    return [s * (N * 15 // 2) + cp0 + l * (N + cp) for s in range(2) for l in range(7)]
+def symbol_starts(N, ext=False):
+    cp0, cp = cp_lens(N, ext)
+    ns = 6 if ext else 7
+    return [s * (N * 15 // 2) + cp0 + l * (N + cp) for s in range(2) for l in range(ns)]
 
 
-def rx_sf(x, nof_prb, N, normalize=False):
+def rx_sf(x, nof_prb, N, normalize=False, ext=False):
     nre = 12 * nof_prb
     h = nre // 2
-    out = np.zeros((14, nre), np.complex128)
-    for i, st in enumerate(symbol_starts(N)):
+    out = np.zeros((12 if ext else 14, nre), np.complex128)
+    for i, st in enumerate(symbol_starts(N, ext)):
         X = np.fft.fft(np.asarray(x[st:st + N], np.complex128))
         out[i, :h] = X[N - h:]
         out[i, h:] = X[1:1 + h]
@@ -37,18 +42,19 @@ def rx_sf(x, nof_prb, N, normalize=False):
     return out.reshape(-1)
 
 
-def tx_sf(grid, nof_prb, N):
+def tx_sf(grid, nof_prb, N, ext=False):
     nre = 12 * nof_prb
     h = nre // 2
-    g = np.asarray(grid).reshape(14, nre)
-    cp0, cp = cp_lens(N)
+    ns = 6 if ext else 7
+    g = np.asarray(grid).reshape(2 * ns, nre)
+    cp0, cp = cp_lens(N, ext)
     out = np.zeros(15 * N, np.complex128)
-    for i, st in enumerate(symbol_starts(N)):
+    for i, st in enumerate(symbol_starts(N, ext)):
         X = np.zeros(N, np.complex128)
         X[N - h:] = g[i, :h]
         X[1:1 + h] = g[i, h:]
         t = np.fft.ifft(X) * N
-        c = cp0 if i % 7 == 0 else cp
+        c = cp0 if i % ns == 0 else cp
         out[st - c:st] = t[N - c:]
         out[st:st + N] = t
     return out

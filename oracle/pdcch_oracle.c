@@ -32,10 +32,11 @@ typedef struct {
  * returns the count or -1 */
 static int orc_regs(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t phich_len,
                     uint32_t phich_res, orc_reg_t **out) {
-  const uint32_t nctrl = nof_prb <= 10 ? 4 : 3, vo = cell_id % 3;
+  const uint32_t nctrl = nof_prb <= 10 ? 4 : 3, vo = cell_id % 3, ext = (nof_ports >> 8) & 1;
+  nof_ports &= 0xff;
   uint32_t nper[4], total = 0;
-  for (uint32_t l = 0; l < nctrl; l++) {
-    nper[l] = l == 0 ? 2 : (l == 1 && nof_ports == 4) ? 2 : 3; /* regs_num_x_symbol, normal CP */
+  for (uint32_t l = 0; l < nctrl; l++) { /* regs_num_x_symbol (regs.c:587-616): symbol 3 has CRS with extended CP */
+    nper[l] = l == 0 ? 2 : (l == 1 && nof_ports == 4) ? 2 : (l == 3 && ext) ? 2 : 3;
     total += nof_prb * nper[l];
   }
   orc_reg_t *r = calloc(total, sizeof(orc_reg_t));

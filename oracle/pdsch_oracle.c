@@ -36,13 +36,16 @@ static void cp_ref(uint32_t *in, uint32_t **out, int offset, int nof_refs, int n
   }
 }
 
-static int has_ref(uint32_t l, uint32_t nof_ports) { /* phy_common.h:132-134, normal CP */
-  return (l == 1 && nof_ports == 4) || l == 0 || l == 7 - 3;
+static int has_ref(uint32_t l, uint32_t nof_ports, uint32_t nsymb) { /* SRSLTE_SYMBOL_HAS_REF, phy_common.h:132-134 */
+  return (l == 1 && nof_ports == 4) || l == 0 || l == nsymb - 3;
 }
 
+/* nof_ports: the CRS port count, plus 256 for an extended-CP cell (SRSLTE_CP_NSYMB 6) */
 int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart_grant,
                      uint32_t sf_idx, const uint8_t *prb_mask, uint32_t *idx) {
-  const uint32_t nsymb = 7, nof_refs = nof_ports == 1 ? 2 : 4;
+  const uint32_t nsymb = (nof_ports >> 8) & 1 ? 6 : 7;
+  nof_ports &= 0xff;
+  const uint32_t nof_refs = nof_ports == 1 ? 2 : 4;
   uint32_t *out = idx;
   uint32_t offset = 0;
   for (uint32_t s = 0; s < 2; s++) {
@@ -63,7 +66,7 @@ int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uin
         const uint32_t lp = l + s * nsymb;
         uint32_t in = (lp * nof_prb + n) * 12;
         if (l >= lstart && l < lend) {
-          if (has_ref(l, nof_ports)) {
+          if (has_ref(l, nof_ports, nsymb)) {
             offset = nof_refs == 2 ? (l == 0 ? cell_id % 6 : (cell_id + 3) % 6) : cell_id % 3;
             cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs);
           } else {
@@ -72,13 +75,13 @@ int orc_pdsch_re_map(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uin
         }
         if ((nof_prb % 2) && ((is_pbch && l < lstart) || (is_sss && l >= lend))) {
           if (n == nof_prb / 2 - 3) {
-            if (has_ref(l, nof_ports))
+            if (has_ref(l, nof_ports, nsymb))
               cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs / 2);
             else
               for (int j = 0; j < 6; j++) *out++ = in++;
           } else if (n == nof_prb / 2 + 3) {
             in += 6;
-            if (has_ref(l, nof_ports))
+            if (has_ref(l, nof_ports, nsymb))
               cp_ref(&in, &out, (int)offset, (int)nof_refs, (int)nof_refs / 2);
             else
               for (int j = 0; j < 6; j++) *out++ = in++;

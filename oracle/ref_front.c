@@ -82,7 +82,7 @@ static void wr_i32(int32_t v) { wr(&v, 4); }
 
 /* IN: nof_prb id nof_ports nrx nsf | filt_mode(0 list, 1 gauss) flen filt[32] g_order g_std |
  *     smooth_auto average noise_alg rsrp_neighbour cfo_enable cfo_mask | noise_init |
- *     nsf x { sf_idx, grid[nrx][14*12*nof_prb] cf32 }
+ *     nsf x { sf_idx, grid[nrx][14*12*nof_prb] cf32 (12 rows with extended CP) }
  * OUT per subframe: noise_before[nrx][nports] | ce[rx][port] grids | noise rsrp rssi rsrp_corr cfo
  *     [rx][port] (cfo: q->cfo right after that (rx, port) estimate) | get_noise_estimate get_snr
  *     get_rssi get_rsrq get_rsrp get_rsrp_neighbour get_cfo */
@@ -91,8 +91,9 @@ static int run_chest(void) {
   memset(&cell, 0, sizeof(cell));
   cell.nof_prb = rd_u32();
   cell.id = rd_u32();
-  cell.nof_ports = rd_u32();
-  cell.cp = SRSLTE_CP_NORM;
+  cell.nof_ports = rd_u32(); /* plus 256 for an extended-CP cell */
+  cell.cp = (cell.nof_ports >> 8) & 1 ? SRSLTE_CP_EXT : SRSLTE_CP_NORM;
+  cell.nof_ports &= 0xff;
   cell.phich_length = SRSLTE_PHICH_NORM;
   cell.phich_resources = SRSLTE_PHICH_R_1;
   const uint32_t nrx = rd_u32(), nsf = rd_u32();
@@ -188,8 +189,9 @@ static int run_dci(void) {
   memset(&cell, 0, sizeof(cell));
   cell.nof_prb = rd_u32();
   cell.id = rd_u32();
-  cell.nof_ports = rd_u32();
-  cell.cp = SRSLTE_CP_NORM;
+  cell.nof_ports = rd_u32(); /* plus 256 for an extended-CP cell */
+  cell.cp = (cell.nof_ports >> 8) & 1 ? SRSLTE_CP_EXT : SRSLTE_CP_NORM;
+  cell.nof_ports &= 0xff;
   const uint32_t nrx = rd_u32();
   cell.phich_length = rd_u32() ? SRSLTE_PHICH_EXT : SRSLTE_PHICH_NORM;
   cell.phich_resources = (srslte_phich_resources_t)rd_u32();

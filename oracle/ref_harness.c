@@ -560,15 +560,16 @@ int srslte_pdsch_get(srslte_pdsch_t *q, cf_t *sf_symbols, cf_t *symbols, srslte_
                      uint32_t lstart, uint32_t subframe);
 
 /* srslte_pdsch_get (pdsch.c:95-234, 250-255): RE extraction of one grant from a subframe grid
- * (nof_prb*12 x 14 cf32); prb_mask[s*nof_prb + n] marks PRB n allocated in slot s. */
+ * (nof_prb*12 x 14 cf32, 12 rows with extended CP); prb_mask[s*nof_prb + n] marks PRB n allocated in
+ * slot s. nof_ports: the port count plus 256 for an extended-CP cell. */
 int ref_pdsch_get(uint32_t nof_prb, uint32_t cell_id, uint32_t nof_ports, uint32_t lstart,
                   uint32_t sf_idx, const uint8_t *prb_mask, const float *grid, float *out) {
   srslte_pdsch_t q;
   memset(&q, 0, sizeof(q));
   q.cell.nof_prb = nof_prb;
   q.cell.id = cell_id;
-  q.cell.nof_ports = nof_ports;
-  q.cell.cp = SRSLTE_CP_NORM;
+  q.cell.nof_ports = nof_ports & 0xff;
+  q.cell.cp = (nof_ports >> 8) & 1 ? SRSLTE_CP_EXT : SRSLTE_CP_NORM;
   srslte_ra_dl_grant_t g;
   memset(&g, 0, sizeof(g));
   for (uint32_t s = 0; s < 2; s++)
@@ -609,6 +610,24 @@ int ref_crs_pilots23(uint32_t nof_prb, uint32_t cell_id, uint32_t sf_idx, float 
   cell.cp = SRSLTE_CP_NORM;
   if (srslte_refsignal_cs_set_cell(&q, cell)) return -1;
   memcpy(out, q.pilots[1][sf_idx], 2 * 2 * nof_prb * sizeof(cf_t));
+  srslte_refsignal_free(&q);
+  return 0;
+}
+
+/* the pilots of either CP (refsignal_dl.c:265-318): pair 0 (ports 0/1, 4 symbols) or 1 (ports 2/3,
+ * 2 symbols) of subframe sf_idx, cp 0 normal / 1 extended */
+int ref_crs_pilots_cp(uint32_t nof_prb, uint32_t cell_id, uint32_t cp, uint32_t pair, uint32_t sf_idx, float *out) {
+  srslte_refsignal_t q;
+  memset(&q, 0, sizeof(q));
+  if (pair > 1 || srslte_refsignal_cs_init(&q, nof_prb)) return -1;
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = nof_prb;
+  cell.id = cell_id;
+  cell.nof_ports = 4;
+  cell.cp = cp ? SRSLTE_CP_EXT : SRSLTE_CP_NORM;
+  if (srslte_refsignal_cs_set_cell(&q, cell)) return -1;
+  memcpy(out, q.pilots[pair][sf_idx], (pair ? 2 : 4) * 2 * nof_prb * sizeof(cf_t));
   srslte_refsignal_free(&q);
   return 0;
 }
@@ -948,8 +967,9 @@ uint32_t ref_dci_sizeof(uint32_t format, uint32_t nof_prb, uint32_t nof_ports) {
 
 static int ref_regs_cell(srslte_regs_t *regs, srslte_cell_t *cell, uint32_t nof_prb, uint32_t cell_id,
                          uint32_t nof_ports, uint32_t phich_len, uint32_t phich_res) {
-  srslte_cell_t c = {nof_prb, nof_ports, cell_id, SRSLTE_CP_NORM, (srslte_phich_length_t)phich_len,
-                     (srslte_phich_resources_t)phich_res};
+  /* nof_ports: the port count plus 256 for an extended-CP cell */
+  srslte_cell_t c = {nof_prb, nof_ports & 0xff, cell_id, (nof_ports >> 8) & 1 ? SRSLTE_CP_EXT : SRSLTE_CP_NORM,
+                     (srslte_phich_length_t)phich_len, (srslte_phich_resources_t)phich_res};
   *cell = c;
   return srslte_regs_init(regs, c);
 }

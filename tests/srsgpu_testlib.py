@@ -412,16 +412,17 @@ def _run_ref_front(mode, payload):
 
 def ref_front_chest(nof_prb, cell_id, nports, nrx, sfs, grids, filt=(0.1, 0.8, 0.1), gauss=None,
                     smooth_auto=False, average=False, noise_alg=0, rsrp_neighbour=True, cfo_enable=True,
-                    cfo_mask=0x3FF, noise_init=0.0):
+                    cfo_mask=0x3FF, noise_init=0.0, cp=0):
     """srslte_chest_dl_* of the reference on ONE estimator over the subframe sequence sfs; grids[i][a]
-    complex64 [14 * 12 nof_prb]. filt: explicit filter (srslte_chest_dl_set_smooth_filter), or
+    complex64 [14 * 12 nof_prb] (12 * 12 nof_prb for an extended-CP cell, cp=1). filt: explicit filter (srslte_chest_dl_set_smooth_filter), or
     gauss=(order, std) for srslte_chest_dl_set_smooth_filter_gauss. -> list per subframe of dict(
     noise_before [nrx][np], ce [nrx][np][n], noise / rsrp / rssi / rsrp_corr / cfo [nrx][np],
     getters [noise, snr, rssi, rsrq, rsrp, rsrp_neighbour, cfo])"""
-    n = 14 * 12 * nof_prb
+    n = (12 if cp else 14) * 12 * nof_prb
     f = np.zeros(32, np.float32)
     f[:len(filt)] = filt
-    head = np.array([nof_prb, cell_id, nports, nrx, len(sfs), 1 if gauss else 0, len(filt)], np.uint32).tobytes()
+    head = np.array([nof_prb, cell_id, nports | (cp << 8), nrx, len(sfs), 1 if gauss else 0, len(filt)],
+                    np.uint32).tobytes()
     head += f.tobytes()
     head += np.array([gauss[0] if gauss else 0], np.uint32).tobytes()
     head += np.array([gauss[1] if gauss else 0.0], np.float32).tobytes()
