@@ -294,3 +294,33 @@ def test_gpu_ext_tx_rx(mimo, nports):
     acked, good, _ = m.check()
     assert acked == good == m.ntb * m.n, (acked, good, m.ntb * m.n)
     m.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ext_queue():
+    """an extended-CP cell through the subframe queue (srsgpu_rxq_*: OFDM, channel estimation and the
+    PDSCH of the cell's CP): SISO subframes on 2 rx antennas decode as the direct batch call does"""
+    import torch
+    import srsgpu_phy as s
+    import srsgpu_traffic as tr
+    m = tr.MimoSubframes(torch, torch.device("cuda"), 12, seed=23, snr_db=30.0, mimo=s.MIMO_SINGLE_ANTENNA, mcs=20,
+                         nof_prb=25, ce_rows=False, nof_ports=1, cp=1)
+    m.step()
+    torch.cuda.synchronize()
+    acked, good, _ = m.check()
+    assert acked == good == m.n
+    x = m.x.cpu().numpy().reshape(m.n, 2, 15 * m.N)
+    q = s.RxQueue(25, m.cell_id, m.N, nof_ports=1, nof_rx_ant=2, nof_softbuffers=m.n, max_batch=4,
+                  max_wait_us=2000, cp=1)
+    tx = m.d_data_tx.cpu().numpy().reshape(m.n, 2, m.dlen)
+    nb = m.tbs // 8
+    for j, i in enumerate(m.kept):
+        td = [np.ascontiguousarray(x[j, a]) for a in range(2)]
+        out = np.zeros(m.dlen, np.uint8)
+        sf = s.make_sf(sf_idx=1 + (i % 4), lstart=1, nof_prb=25, mod=3, rnti=1234, tbs=m.tbs, softbuffer=j)
+        sf.nof_re = m.pd.nof_re(sf)
+        it = q.item(td, sf, [out])
+        assert q.decode(it) == 0 and it.ret[0] == 0, j
+        assert (out[:nb] == tx[j, 0, :nb]).all(), j
+    q.close()
+    m.close()
