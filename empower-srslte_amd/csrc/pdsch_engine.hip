@@ -221,7 +221,9 @@ struct PdschEngine {
   // 4-port transmit diversity demaps 4 floor(n / 4) symbols (srslte_pdsch_decode's n / nof_layers,
   // pdsch.c:908, and m_ap of precoding.c:391 / :605); the reference would read any remaining symbol
   // from whatever its layer buffer last held. Normal-CP grants of a 4-port cell always hold whole
-  // quadruplets (tests/test_txdiv.py), so this only guards the layout assumption.
+  // quadruplets (tests/test_txdiv.py); extended-CP grants of subframe 0 that hold only one of the
+  // half PRBs beside the PBCH of an odd-sized cell do not (4 + 4 + 6 + 4 REs in slot 1's symbols
+  // 0-3), and are refused here since the reference's result is undefined for them.
   int txdiv4_ragged(const srsgpu_pdsch_sf_t &s, uint32_t nre) const {
     if (s.mimo_type != SRSGPU_MIMO_TX_DIVERSITY || cell.nof_ports != 4 || nre % 4 == 0) return 0;
     fprintf(stderr, "srsgpu: 4-port transmit diversity needs a multiple of 4 REs (grant has %u)\n", nre);
@@ -427,7 +429,7 @@ struct PdschEngine {
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
-      if (s.mimo_type != SRSGPU_MIMO_SINGLE_ANTENNA && port_stride < (uint64_t)14 * 12 * cell.nof_prb) {
+      if (s.mimo_type != SRSGPU_MIMO_SINGLE_ANTENNA && port_stride < (uint64_t)(cell.cp == 1 ? 12 : 14) * 12 * cell.nof_prb) {
         fprintf(stderr, "srsgpu: a %u-port transmission needs a port stride of at least one grid\n", cell.nof_ports);
         return -1;
       }

@@ -245,6 +245,7 @@ def test_gpu_pdsch_ext_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi, nports)
     p = s.Pdsch(nof_prb, cell_id, nof_ports=nports, nof_rx_ant=nrx, max_sf=n_sf, cp=1)
     p.set_csi(csi)
     sfs, expect, offs, off = [], [], [], 0
+    ragged = []
     for i in range(n_sf):
         sf_idx = [0, 1, 5][i % 3]
         lstart = 1 + i % 3
@@ -254,6 +255,12 @@ def test_gpu_pdsch_ext_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi, nports)
         scaling = 1.0 if i % 2 else 0.7943
         idx = po.re_map(nof_prb, cell_id, nports | EXT, lstart, sf_idx, mask)
         mimo = s.MIMO_SINGLE_ANTENNA if nports == 1 else s.MIMO_TX_DIVERSITY
+        if nports == 4 and idx.size % 4:  # a ragged 4-port grant (one half PRB beside the PBCH): refused
+            bad = s.make_sf(sf_idx=sf_idx, lstart=lstart, prb=mask, nof_prb=nof_prb, mod=mod, nof_re=idx.size,
+                            mimo=mimo)
+            ragged.append(bad)
+            mask[:] = 1
+            idx = po.re_map(nof_prb, cell_id, nports | EXT, lstart, sf_idx, mask)
         sfs.append(s.make_sf(sf_idx=sf_idx, lstart=lstart, prb=mask, nof_prb=nof_prb, mod=mod, nof_re=idx.size,
                              rnti=rnti, scaling=scaling, mimo=mimo, grid_offset=i * nrx * size,
                              ce_offset=i * nrx * nports * size))
@@ -271,6 +278,8 @@ def test_gpu_pdsch_ext_llr_vs_oracle(oracle, nof_prb, cell_id, nrx, csi, nports)
     d_y = torch.from_numpy(y.reshape(-1)).cuda()
     d_h = torch.from_numpy(h.reshape(-1)).cuda()
     d_e = torch.zeros(off + 8, dtype=torch.int16, device="cuda")
+    for bad in ragged:
+        assert p.llr_dev([bad], d_y.data_ptr(), d_h.data_ptr(), size, d_e.data_ptr(), [0]) == -1
     assert p.llr_dev(sfs, d_y.data_ptr(), d_h.data_ptr(), size, d_e.data_ptr(), offs) == 0
     torch.cuda.synchronize()
     e = d_e.cpu().numpy()
