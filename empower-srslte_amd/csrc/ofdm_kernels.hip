@@ -8,6 +8,7 @@
 // autosort FFT runs in LDS with exact twiddles from a per-size table, and only the nof_re used
 // subcarriers are written back.
 #include <hip/hip_runtime.h>
+#include <string.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -168,7 +169,10 @@ template <int R> __device__ __forceinline__ void bfly(const cf *v, cf *y) {
 __device__ __forceinline__ int lpad(int p) { return p + (p >> 4); }
 template <int N> constexpr int lds_slots() { return N + N / 16; }
 
-template <int R, int N, int Ns, int TPS, bool FIRST>
+// TWC: twiddles from the hardware sine / cosine (v_sin_f32 / v_cos_f32 take the angle in revolutions,
+// here -r k / (Ns R) exactly for the power-of-two stages) instead of loads from the table: no L2 round
+// trip between a stage's LDS reads and its butterflies. Results within a few ulp of the table's.
+template <int R, int N, int Ns, int TPS, bool FIRST, bool TWC = false>
 __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, const float2 *__restrict__ tw,
                                          int t, bool live) {
   constexpr int nb = N / R;
@@ -187,8 +191,13 @@ __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, co
         } else {
           a = buf[lpad(j + r * nb)];
           if (Ns > 1 && r) { // e^{-2 pi i r k / (Ns R)} = tw[r k N / (Ns R)]
-            const float2 w = tw[r * k * (N / (Ns * R))];
-            a = cmul(a, cf{w.x, w.y});
+            if constexpr (TWC) {
+              const float rev = -(float)(r * k) * (1.0f / (float)(Ns * R));
+              a = cmul(a, cf{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)});
+            } else {
+              const float2 w = tw[r * k * (N / (Ns * R))];
+              a = cmul(a, cf{w.x, w.y});
+            }
           }
         }
       }
@@ -211,14 +220,14 @@ __device__ __forceinline__ void stage_ip(const cf *__restrict__ src, cf *buf, co
 }
 
 // stages Ns .. N in place (radix 8 first, then 4, 2, 3); the result is left in buf
-template <int N, int Ns, int TPS>
+template <int N, int Ns, int TPS, bool TWC = false>
 __device__ __forceinline__ void fft_ip(const cf *__restrict__ src, cf *buf, const float2 *__restrict__ tw,
                                        int t, bool live) {
   if constexpr (Ns < N) {
     constexpr int rem = N / Ns;
     constexpr int R = rem % 8 == 0 ? 8 : rem % 4 == 0 ? 4 : rem % 2 == 0 ? 2 : 3;
-    stage_ip<R, N, Ns, TPS, Ns == 1>(src, buf, tw, t, live);
-    fft_ip<N, Ns * R, TPS>(src, buf, tw, t, live);
+    stage_ip<R, N, Ns, TPS, Ns == 1, TWC>(src, buf, tw, t, live);
+    fft_ip<N, Ns * R, TPS, TWC>(src, buf, tw, t, live);
   }
 }
 
@@ -227,7 +236,7 @@ constexpr int syms_per_wg() {
   return N >= 1024 ? 1 : N >= 512 ? 2 : N >= 256 ? 4 : 8;
 }
 
-template <int N>
+template <int N, bool TWC>
 __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in, size_t in_stride,
                                                    float2 *__restrict__ out, size_t out_stride, int nsym,
                                                    int nre, int cp0, int cp, int ns,
@@ -241,7 +250,7 @@ __global__ __launch_bounds__(256) void k_ofdm_rx_c(const float2 *__restrict__ in
   const int slot = sym / ns, l = sym % ns;
   const size_t start = (size_t)slot * (N * 15 / 2) + cp0 + (size_t)l * (N + cp);
   const cf *src = (const cf *)(in + (size_t)(live ? sf : 0) * in_stride + start);
-  fft_ip<N, 1, TPS>(src, buf[s], tw, t, live);
+  fft_ip<N, 1, TPS, TWC>(src, buf[s], tw, t, live);
   const cf *res = buf[s];
   if (live) {
     cf *dst = (cf *)(out + (size_t)sf * out_stride + (size_t)sym * nre);
@@ -372,10 +381,19 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
     OFDM_RX_P(1024)
 #undef OFDM_RX_P
   }
+  // SRSGPU_OFDM_TW=sincos: twiddles computed in the kernel (see stage_ip); default: the table
+  static const bool twc = [] {
+    const char *e = getenv("SRSGPU_OFDM_TW");
+    return e && strcmp(e, "sincos") == 0;
+  }();
 #define OFDM_RX_C(n)                                                                               \
   case n:                                                                                          \
-    hipLaunchKernelGGL(k_ofdm_rx_c<n>, dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \
-                       dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, ns, tw, scale); \
+    if (twc)                                                                                       \
+      hipLaunchKernelGGL((k_ofdm_rx_c<n, true>), dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \
+                         dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, ns, tw, scale); \
+    else                                                                                           \
+      hipLaunchKernelGGL((k_ofdm_rx_c<n, false>), dim3((unsigned)((nsym + syms_per_wg<n>() - 1) / syms_per_wg<n>())), \
+                         dim3(256), 0, st, in, in_stride, out, out_stride, nsym, nre, cp0, cp, ns, tw, scale); \
     return hipGetLastError();
   switch (N) {
     OFDM_RX_C(128)
