@@ -381,10 +381,12 @@ hipError_t launch_ofdm_rx(const float2 *in, size_t in_stride, float2 *out, size_
     OFDM_RX_P(1024)
 #undef OFDM_RX_P
   }
-  // SRSGPU_OFDM_TW=sincos: twiddles computed in the kernel (see stage_ip); default: the table
+  // twiddles computed in the kernel (see stage_ip) by default: 41 us against 58 us with the table
+  // loads per 512 20 MHz subframes, alone on the GPU (profiles/r04_s13_kb_*.json);
+  // SRSGPU_OFDM_TW=table restores the loads
   static const bool twc = [] {
     const char *e = getenv("SRSGPU_OFDM_TW");
-    return e && strcmp(e, "sincos") == 0;
+    return !(e && strcmp(e, "table") == 0);
   }();
 #define OFDM_RX_C(n)                                                                               \
   case n:                                                                                          \

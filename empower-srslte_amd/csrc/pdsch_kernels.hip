@@ -381,10 +381,14 @@ __device__ __forceinline__ Eq equalise_txdiv4(const LlrItem &t, uint32_t j) {
   cf x = {0.f, 0.f};
   float g = 0.f;
   Eq e;
-  for (int a = 0; a < 2; a++) {
+#pragma unroll
+  for (int a = 0; a < 2; a++) { // unrolled: a run-time a would index the descriptor in scratch
     if (a == 1 && t.nrx < 2) break;
     const cf r0 = c_ld(t.y[a], p0), r1 = c_ld(t.y[a], p1);
-    const cf hA = ce_ld(t, t.h[q][a], p0), hB = ce_ld(t, t.h[q + 2][a], t.csi_mode && !odd ? p1 : p0);
+    // the pair's planes by select, not by a run-time index into the descriptor (which would put the
+    // whole item in scratch memory)
+    const float2 *hq = q ? t.h[1][a] : t.h[0][a], *hq2 = q ? t.h[3][a] : t.h[2][a];
+    const cf hA = ce_ld(t, hq, p0), hB = ce_ld(t, hq2, t.csi_mode && !odd ? p1 : p0);
     cf u;
     if (!t.csi_mode) { // hA = h[q][4i+2q], hB = h[q+2][4i+2q]
       g = __fadd_rn(g, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(hA.r, hA.r), __fmul_rn(hA.i, hA.i)),
@@ -398,7 +402,7 @@ __device__ __forceinline__ Eq equalise_txdiv4(const LlrItem &t, uint32_t j) {
                                  __fmul_rn(hB.i, hB.i)));
       u = c_add(c_mul(c_conj(hA), r0), c_mul(hB, c_conj(r1)));
     } else { // h10 = h[q][b+1], h01 = h[q+2][b] (hB)
-      const cf h10 = ce_ld(t, t.h[q][a], p1);
+      const cf h10 = ce_ld(t, hq, p1);
       g = __fadd_rn(g, __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(h10.r, h10.r), __fmul_rn(h10.i, h10.i)),
                                            __fmul_rn(hB.r, hB.r)),
                                  __fmul_rn(hB.i, hB.i)));
@@ -660,8 +664,10 @@ __device__ __forceinline__ void llr_body_dual(const LlrItem &t, const LlrItem &t
 
 // the item's device pointers as global, and the noise from the estimator when it is on the device
 __device__ __forceinline__ void llr_item_fix(LlrItem &u) {
+#pragma unroll
   for (int a = 0; a < 2; a++) {
     u.y[a] = gmem(u.y[a]);
+#pragma unroll
     for (int p = 0; p < 4; p++) u.h[p][a] = gmem(u.h[p][a]);
   }
   u.map = gmem(u.map);
@@ -916,9 +922,13 @@ __global__ __launch_bounds__(64) void k_pcfich(const PcfichItem *__restrict__ it
   const PcfichItem it = items[s];
   LlrItem t;
   memset(&t, 0, sizeof(t));
-  for (int a = 0; a < nrx; a++) {
+#pragma unroll
+  for (int a = 0; a < 2; a++) { // constant indices only: the descriptor stays in registers
+    if (a >= nrx) break;
     t.y[a] = grid + it.grid_off + (size_t)a * ant_stride;
-    for (int p = 0; p < nports; p++) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+      if (p < nports) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
   }
   t.map = idx;
   t.nof_re = 16;
@@ -983,9 +993,13 @@ __global__ __launch_bounds__(256) void k_pdcch_llr(const PdcchItem *__restrict__
   if (j >= it.nof_symbols) return;
   LlrItem t;
   memset(&t, 0, sizeof(t));
-  for (int a = 0; a < nrx; a++) {
+#pragma unroll
+  for (int a = 0; a < 2; a++) { // constant indices only: the descriptor stays in registers
+    if (a >= nrx) break;
     t.y[a] = grid + it.grid_off + (size_t)a * ant_stride;
-    for (int p = 0; p < nports; p++) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+      if (p < nports) t.h[p][a] = ce + it.ce_off + (size_t)(a * nports + p) * ant_stride;
   }
   t.map = it.map;
   t.nof_re = it.nof_symbols;
