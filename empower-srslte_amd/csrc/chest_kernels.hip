@@ -393,12 +393,13 @@ __global__ __launch_bounds__(256) void k_chest(const ChestItem *__restrict__ ite
 hipError_t launch_chest(const ChestItem *d_items, int n, const ChestCfg &cfg, const float2 *crs,
                         const float *filt, const float2 *pss, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  // columns split over up to 4 workgroups per grid (12 nprb / 256 of them): steps 1-5 are small.
-  // SRSGPU_CHEST_PARTS overrides the cap (A/B)
+  // columns split over up to 2 workgroups per grid (12 nprb / 256 of them), each repeating steps 1-5:
+  // 19.3 us per 512 20 MHz grids against 25.4 us with 4 (profiles/r04_s16_kb_parts*.json, compact
+  // rows). SRSGPU_CHEST_PARTS overrides the cap (A/B)
   static const int cap = [] {
     const char *e = getenv("SRSGPU_CHEST_PARTS");
     const int v = e ? atoi(e) : 0;
-    return v >= 1 && v <= 16 ? v : 4;
+    return v >= 1 && v <= 16 ? v : 2;
   }();
   const unsigned parts = (unsigned)std::max(1, std::min(cap, std::max(1, 12 * cfg.nprb / 256)));
   hipLaunchKernelGGL(k_chest, dim3((unsigned)n, parts), dim3(256), 0, st, d_items, n, cfg, crs, filt, pss);
