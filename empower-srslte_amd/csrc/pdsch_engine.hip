@@ -549,6 +549,7 @@ void srsgpu_pdsch_set_csi(srsgpu_pdsch_t *q, int enable) {
 int srsgpu_pdsch_set_ce_rows(srsgpu_pdsch_t *q, int rows) {
   if (!q || (rows != 0 && rows != 1 && rows != 4)) return -1;
   if (rows == 4 && q->e.cell.cp == 1) return -1; // 4 rows: the normal-CP CRS symbols 0 / 4 / 7 / 11
+  if (rows == 4 && q->e.cell.nof_ports > 2) return -1; // the estimator writes compact rows for <= 2 ports
   q->e.ce_rows = rows;
   return 0;
 }
@@ -602,11 +603,12 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
   for (uint32_t i = 0; i < n; i++)
     for (uint32_t tb = 0; tb < PdschEngine::nof_tb(sf[i]); tb++, j++) {
       srsgpu_dlsch_tb_t &t = E.h_tb[j];
-      t.tbs = sf[i].tbs[tb];
+      const bool skip = (sf[i].skip_tb >> tb) & 1u; // acked earlier: no decode (pdsch.c:946-947)
+      t.tbs = skip ? 0 : sf[i].tbs[tb];
       t.rv = sf[i].rv[tb];
       t.Qm = srsgpu::dlsch_qm(sf[i], tb);
       t.nof_e_bits = sf[i].nof_re * srsgpu::kQm[sf[i].mod[tb]];
-      t.softbuffer = sf[i].softbuffer[tb];
+      t.softbuffer = skip ? 0 : sf[i].softbuffer[tb];
       t.e_offset = (uint64_t)j * E.max_bits;
       t.data_offset = sf[i].data_offset[tb];
     }

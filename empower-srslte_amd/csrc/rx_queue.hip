@@ -143,7 +143,6 @@ struct srsgpu_rxq {
   uint32_t N = 0, max_batch = 0, max_wait_us = 0, max_halfits = 8, nports = 1, nrx = 1;
   uint32_t phich_len = 0, phich_res = 2;
   bool phich_dirty = false; // srsgpu_rxq_set_phich: the dispatcher rebuilds pdcch before its next use
-  uint32_t scratch_sb = 0;  // softbuffer of TBs the caller already acked (decoded, result dropped)
   size_t td_len = 0, gsz = 0, dlen = 0; // complex samples per antenna / grid elements / TB bytes
   hipStream_t st = nullptr, cst = nullptr; // compute / copy streams
   srsgpu_ofdm_t *ofdm = nullptr;
@@ -184,10 +183,13 @@ struct srsgpu_rxq {
     int state = FILLING;
     int copying = 0; // submitters still copying their samples in
     uint32_t nstaged = 0; // items whose samples went through the staging buffer
+    int sc16 = 0;          // the input format of this slot's items (set with its first item)
+    float sc16_scale = 1.0f / 32768.0f;
   } slot[2];
   // input format (srsgpu_rxq_set_input_format) and caller memory the GPU reads directly
-  int sc16 = 0;
+  int sc16 = 0; // guarded by m; a change waits until nothing is queued and holds new submissions
   float sc16_scale = 1.0f / 32768.0f;
+  bool fmt_busy = false;
   struct Region {
     const char *h;
     size_t bytes;
@@ -195,7 +197,6 @@ struct srsgpu_rxq {
   };
   std::vector<Region> regions; // guarded by m
   uint64_t zero_copy_rows = 0, staged_rows = 0;
-  size_t sample_bytes() const { return sc16 ? 4 : 8; }
   // device view of a registered host pointer holding `bytes`, or null (caller holds m)
   const void *device_view(const void *p, size_t bytes) const {
     const char *c = (const char *)p;
@@ -239,11 +240,10 @@ struct srsgpu_rxq {
     }
     llr_stride = 72 * (size_t)max_cce;
     const uint32_t max_cb = 13;
-    scratch_sb = nsb; // one more softbuffer than the caller's
     RXQ_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     RXQ_CHK(hipStreamCreateWithFlags(&cst, hipStreamNonBlocking));
     if (srsgpu_ofdm_rx_create(&ofdm, cell.nof_prb, N) || srsgpu_chest_create(&chest, &cell, mb * nrx) ||
-        srsgpu_pdsch_create(&pdsch, &cell, nsb + 1, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
+        srsgpu_pdsch_create(&pdsch, &cell, nsb, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
       return -1;
     srsgpu_ofdm_rx_set_stream(ofdm, st);
     if (srsgpu_ofdm_set_cp(ofdm, cell.cp)) return -1;
@@ -334,18 +334,24 @@ struct srsgpu_rxq {
   int submit(srsgpu_rxq_item_t *it, srsgpu_rxq_ue_dl_t *ue, uint64_t *ticket) {
     const void *td[2] = {it ? it->td[0] : ue->td[0], it ? it->td[1] : ue->td[1]};
     if (!td[0] || (nrx > 1 && !td[1])) return -1;
-    const size_t row_bytes = sample_bytes() * td_len;
+    size_t row_bytes;
     int s, idx;
     const void *dv[2] = {nullptr, nullptr};
     {
       std::unique_lock<std::mutex> l(m);
-      // the filling slot has room (else wait for the closer to switch to the other slot)
+      // the filling slot has room (else wait for the closer to switch to the other slot), and no
+      // input format change is under way
       cv_slot.wait(l, [&] {
-        return stop || (slot[fill].state == FILLING && slot[fill].items.size() < max_batch);
+        return stop || (!fmt_busy && slot[fill].state == FILLING && slot[fill].items.size() < max_batch);
       });
       if (stop) return -1;
       s = fill;
       idx = (int)slot[s].items.size();
+      if (idx == 0) { // the slot's format: every item of it is submitted under the same one
+        slot[s].sc16 = sc16;
+        slot[s].sc16_scale = sc16_scale;
+      }
+      row_bytes = (slot[s].sc16 ? 4 : 8) * td_len;
       *ticket = next_ticket++;
       slot[s].items.push_back({it, ue, *ticket, std::chrono::steady_clock::now()});
       for (uint32_t a = 0; a < nrx; a++) {
@@ -369,7 +375,8 @@ struct srsgpu_rxq {
   // the closed slot's samples to the device: one DMA of the staged rows' region (up to the last staged
   // row), then the ingest kernel for rows read from registered memory and for SC16 conversion
   bool stage(Slot &sl, size_t n) {
-    const size_t rows = n * nrx, row_bytes = sample_bytes() * td_len;
+    const int sc16 = sl.sc16;
+    const size_t rows = n * nrx, row_bytes = (sc16 ? 4 : 8) * td_len;
     size_t last = 0, nst = 0;
     for (size_t r = 0; r < rows; r++)
       if (!sl.h_src[r]) {
@@ -389,7 +396,7 @@ struct srsgpu_rxq {
         return false;
       const unsigned gx = (unsigned)std::min<size_t>(64, (td_len / 2 + 255) / 256);
       hipLaunchKernelGGL(k_ingest, dim3(gx, (unsigned)rows), dim3(256), 0, cst, (const void *const *)sl.d_src,
-                         (int)rows, td_len, sc16, sc16_scale, (float2 *)sl.d_td);
+                         (int)rows, td_len, sc16, sl.sc16_scale, (float2 *)sl.d_td);
       if (hipGetLastError() != hipSuccess) return false;
     }
     zero_copy_rows += rows - nst;
@@ -582,10 +589,10 @@ struct srsgpu_rxq {
       sf.mod[i] = g.mod[i];
       sf.tbs[i] = g.tb_en[i] ? (uint32_t)g.tbs[i] : 0;
       sf.rv[i] = rv[i];
-      // a TB the caller already acked is skipped by srslte_pdsch_decode (pdsch.c:946-947): decode it into
-      // the scratch softbuffer and drop the result, the caller's softbuffer and data stay as they are
-      sf.softbuffer[i] = u->acks[i] ? scratch_sb : u->softbuffer[i];
-      if (u->acks[i] && g.tb_en[i] && srsgpu_dlsch_softbuffer_reset(dl, scratch_sb)) return -1;
+      // a TB the caller already acked is skipped by srslte_pdsch_decode (pdsch.c:946-947): no decode,
+      // the caller's softbuffer and data stay as they are
+      sf.softbuffer[i] = u->softbuffer[i];
+      if (u->acks[i]) sf.skip_tb |= 1u << i;
     }
     const int nre = srsgpu_pdsch_nof_re(&cell, &sf);
     if (nre <= 0) return -1;
@@ -843,10 +850,17 @@ int srsgpu_rxq_unregister(srsgpu_rxq_t *q, void *host) {
 
 int srsgpu_rxq_set_input_format(srsgpu_rxq_t *q, uint32_t format, float scale) {
   if (!q || format > SRSGPU_RXQ_SC16) return -1;
-  std::unique_lock<std::mutex> l(q->m);
-  q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; }); // only while nothing is queued
-  q->sc16 = format == SRSGPU_RXQ_SC16;
-  q->sc16_scale = scale != 0.f ? scale : 1.0f / 32768.0f;
+  {
+    std::unique_lock<std::mutex> l(q->m);
+    q->cv_done.wait(l, [&] { return !q->fmt_busy; });
+    q->fmt_busy = true; // new submissions wait; the queued ones drain under the old format
+    q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; });
+    q->sc16 = format == SRSGPU_RXQ_SC16;
+    q->sc16_scale = scale != 0.f ? scale : 1.0f / 32768.0f;
+    q->fmt_busy = false;
+  }
+  q->cv_slot.notify_all();
+  q->cv_done.notify_all();
   return 0;
 }
 

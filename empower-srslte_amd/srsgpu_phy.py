@@ -120,7 +120,7 @@ class srsgpu_pdsch_sf_t(ctypes.Structure):
                 ("tbs", ctypes.c_uint32 * 2), ("rv", ctypes.c_uint32 * 2),
                 ("softbuffer", ctypes.c_uint32 * 2), ("grid_offset", ctypes.c_uint64),
                 ("ce_offset", ctypes.c_uint64), ("data_offset", ctypes.c_uint64 * 2),
-                ("codebook_idx", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("codebook_idx", ctypes.c_uint32), ("skip_tb", ctypes.c_uint32)]
 
 
 class srsgpu_rxq_item_t(ctypes.Structure):

@@ -65,7 +65,7 @@ def tb_weights(table, sf_plan, max_halfits=8):
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
                  snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None, standard_rate=True,
-                 early_stop=True, ce_rows=True):
+                 early_stop=True, ce_rows=True, rotate=1):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
         traffic). keep: the subframe indices this instance builds and receives (a rank's shard
@@ -73,12 +73,17 @@ class MixedCells:
         20 MHz) or srsLTE's reduced ones (1536, srslte_symbol_sz without standard rates).
         early_stop False: every code block runs max_halfits (srsgpu_dlsch_set_early_stop).
         ce_rows: the estimator hands the PDSCH stage its compact rows (srsgpu_chest_set_ce_rows /
-        srsgpu_pdsch_set_ce_rows: identical LLRs, 3.5x fewer estimate bytes)."""
+        srsgpu_pdsch_set_ce_rows: identical LLRs, 3.5x fewer estimate bytes).
+        rotate R > 1: R descriptor sets that differ in their softbuffers (set r uses softbuffers
+        r * ntb ..), used in turn by successive steps, so no two consecutive calls of the PDSCH and
+        DL-SCH stages repeat their inputs and their repeat-call caches never hit, as for a receiver
+        whose grants change every subframe."""
         self.torch, self.dev = torch, dev
         self.max_halfits = max_halfits
         sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
         keep = set(range(n_sf)) if keep is None else set(int(k) for k in keep)
         self.kept = sorted(keep)
+        self.rotate, self.cur = max(1, int(rotate)), 0
         self.cells = []
         self.sf_total = len(self.kept)
         e_off = d_off = 0
@@ -116,13 +121,22 @@ class MixedCells:
             # descriptor arrays built once (the receive step reuses them every batch)
             c.update(sfs=s.make_sf_array(sfs), e_offs=(ctypes.c_uint64 * n)(*e_offs),
                      sf_idx=(ctypes.c_uint32 * n)(*sf_idx))
+            c["sfs_rot"] = [c["sfs"]]
+            for r in range(1, self.rotate):
+                arr = (s.srsgpu_pdsch_sf_t * n)(*sfs)
+                for j in range(n):
+                    arr[j].softbuffer[0] = sfs[j].softbuffer[0] + r * n_sf
+                c["sfs_rot"].append(arr)
             self.cells.append(c)
         self.tb_list = tb_list
         self.tb_array = s.make_tb_array(tb_list)
         self.ntb = len(tb_list)
+        self.tb_rot = [self.tb_array] + [
+            s.make_tb_array([dict(t, softbuffer=t["softbuffer"] + r * self.ntb) for t in tb_list])
+            for r in range(1, self.rotate)]
         self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
         self.bits = sum(t["tbs"] for t in tb_list)
-        self.dlsch = s.Dlsch(max(self.ntb, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
+        self.dlsch = s.Dlsch(max(self.ntb * self.rotate, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
         self.dlsch.set_early_stop(early_stop)
         z = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         self.d_e = z(max(e_off, 1), torch.int16)
@@ -162,17 +176,18 @@ class MixedCells:
             assert c["ofdm"].rx_dev(n, c["x"].data_ptr(), 15 * N, c["grid"].data_ptr(), gsz) == 0
             assert c["chest"].estimate_dev(c["sf_idx"], c["grid"].data_ptr(), gsz, c["ce"].data_ptr(),
                                            c["noise"].data_ptr()) == 0
-            assert c["pd"].llr_dev(c["sfs"], c["grid"].data_ptr(), c["ce"].data_ptr(), gsz,
+            assert c["pd"].llr_dev(c["sfs_rot"][self.cur], c["grid"].data_ptr(), c["ce"].data_ptr(), gsz,
                                    self.d_e.data_ptr(), c["e_offs"]) == 0
 
     def decode(self):
         """one DL-SCH call over every cell's transport blocks (new TBs: softbuffers reset)"""
-        self.dlsch.reset_range(0, self.ntb)
-        assert self.dlsch.decode_dev(self.tb_array, self.d_e.data_ptr(), self.d_data.data_ptr(),
+        self.dlsch.reset_range(self.cur * self.ntb, self.ntb)
+        assert self.dlsch.decode_dev(self.tb_rot[self.cur], self.d_e.data_ptr(), self.d_data.data_ptr(),
                                      self.max_halfits, self.d_ret.data_ptr(),
                                      self.d_noi.data_ptr()) == 0
 
     def step(self):
+        self.cur = (self.cur + 1) % self.rotate
         self.front_end()
         self.decode()
 
@@ -200,9 +215,13 @@ class MixedCells:
             if r == 0:
                 total += sum(ks)
             else:
-                crc = self.dlsch.read_cb_crc(t["softbuffer"])
+                crc = self.dlsch.read_cb_crc(self.softbuffer_of(t))
                 total += sum(k for k, c in zip(ks, crc) if c)
         return total
+
+    def softbuffer_of(self, t):
+        """the softbuffer TB t used in the last step (descriptor set self.cur)"""
+        return t["softbuffer"] + self.cur * self.ntb
 
     def close(self):
         for c in self.cells:

@@ -78,7 +78,10 @@ typedef struct {
   uint64_t data_offset[2];  /* first output byte of each TB in d_data */
   uint32_t codebook_idx;    /* srslte_pdsch_cfg_t.codebook_idx (spatial multiplexing only; with
                                tbs[1] > 0 two TBs on two layers, else one TB on one layer) */
-  uint32_t reserved;
+  uint32_t skip_tb;         /* bit t set: TB t is not decoded, as srslte_pdsch_decode skips a TB whose
+                               acks[t] is already true (pdsch.c:946-947). Its softbuffer and data bytes
+                               are not touched; its d_ret / d_noi entries are written as 0. The
+                               subframe's equalisation still runs (a 2-layer equaliser needs both). */
 } srsgpu_pdsch_sf_t;
 
 /* nof_softbuffers HARQ softbuffers of max_cb code blocks; up to max_sf subframes per call. */
@@ -96,7 +99,8 @@ void srsgpu_pdsch_set_llr_8bit(srsgpu_pdsch_t *q, int enable);
  * srsgpu_chest_set_ce_rows: rows = 4 (per-symbol estimation: the CRS symbols' rows, time
  * interpolation done per resource element with the estimator's operations, so the LLRs are
  * identical), 1 (average_subframe: the averaged row), 0 (default: full 14-symbol planes).
- * Returns -1 for any other value. */
+ * Returns -1 for any other value, and for rows = 4 on an extended-CP cell or a cell of more than
+ * 2 ports (the estimator writes compact rows only for those it can: chest_batch.h). */
 int srsgpu_pdsch_set_ce_rows(srsgpu_pdsch_t *q, int rows);
 /* Take the MMSE noise term from device memory instead of sf[i].noise_estimate: subframe i of a
  * call uses the mean of d_noise[i*nof_rx_ant + a] (the channel estimator's per-antenna outputs,

@@ -529,16 +529,14 @@ void srslte_softbuffer_rx_reset_cb(srslte_softbuffer_rx_t *q, uint32_t nof_cb) {
 }
 
 /* GPU softbuffer index of a reference softbuffer in the object's pool, with the resets recorded
- * since its last decode applied; the last index is a scratch buffer for TBs the caller already
- * acked (the reference skips them, pdsch.c:963-965) */
-#define SHIM_SCRATCH (SHIM_MAX - 1)
+ * since its last decode applied */
 static int shim_softbuffer(shim_entry_t *e, srsgpu_dlsch_t *dl, srslte_softbuffer_rx_t *sb) {
   int slot = -1, fresh = 0;
   uint32_t nreset = 0;
   pthread_mutex_lock(&shim_mutex);
-  for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
+  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
     if (e->sb[i] == sb) slot = i;
-  for (int i = 0; i < SHIM_SCRATCH && slot < 0; i++)
+  for (int i = 0; i < SHIM_MAX && slot < 0; i++)
     if (!e->sb[i]) {
       e->sb[i] = sb;
       slot = i;
@@ -875,9 +873,10 @@ int srslte_pdsch_decode(srslte_pdsch_t *q, srslte_pdsch_cfg_t *cfg,
   sf.grid_offset = 0;
   sf.ce_offset = 0;
   for (uint32_t t = 0; t < nof_tb; t++) {
-    const int slot = acks[t] ? SHIM_SCRATCH : shim_softbuffer(e, dl, softbuffers[t]);
+    /* an acked TB is skipped as srslte_pdsch_decode skips it (pdsch.c:946-947): no decode */
+    const int slot = acks[t] ? 0 : shim_softbuffer(e, dl, softbuffers[t]);
     if (slot < 0) return SRSLTE_ERROR;
-    if (acks[t]) srsgpu_dlsch_softbuffer_reset(dl, SHIM_SCRATCH);
+    if (acks[t]) sf.skip_tb |= 1u << t;
     sf.mod[t] = (uint32_t)cfg->grant.mcs[t].mod;
     sf.tbs[t] = (uint32_t)cfg->grant.mcs[t].tbs;
     sf.rv[t] = cfg->rv[t];
