@@ -20,6 +20,8 @@
  *                            (ue_dl.c:768-932) in phch_worker's order (DL search, then the UL search,
  *                            phch_worker.cc:548-806, 938-967) on ONE srslte_ue_dl_t, and
  *                            srslte_dci_msg_to_ul_grant (dci.c:165-197) of a found UL DCI.
+ *   ref_front ue_dl IN OUT   srslte_ue_dl_decode_rnti's steps after the FFT (chest, PCFICH, PDCCH, DCI
+ *                            search, grant, PDSCH) on given grids: the recorded-signal fixtures.
  *   ref_front pdsch_bench IN OUT   the CPU baseline of BASELINE configs[2] (bench.py): per pthread,
  *                            pinned to its own CPU, one srslte_chest_dl_t + srslte_pdsch_t +
  *                            softbuffer, running what srslte_ue_dl_decode_rnti runs after the FFT
@@ -286,6 +288,127 @@ static int run_dci(void) {
   return 0;
 }
 
+/* ---------------------------------------------------------------- recorded signals ---- */
+/* srslte_ue_dl_decode_rnti (ue_dl.c:467-620) after its FFT, on given resource grids: the reference's
+ * recorded-signal tests run srslte_ofdm_rx_sf on a capture (FFTW, absent here), so the grids come from
+ * the numpy OFDM oracle and everything after the FFT is the reference's own code, called in
+ * decode_rnti's order on ONE ue_dl-shaped object (built as srslte_ue_dl_init / _set_cell /
+ * _set_rnti build it, minus the FFT objects): srslte_chest_dl_estimate_multi and
+ * srslte_pcfich_decode_multi (the body of srslte_ue_dl_decode_estimate_mbsfn, :409-433, here with the
+ * correlation kept), the noise estimate, srslte_pdcch_extract_llr_multi, srslte_ue_dl_find_dl_dci,
+ * srslte_dci_msg_to_dl_grant, the redundancy versions and softbuffer resets (:498-534), the MIMO type
+ * of the format (:536-566), srslte_ue_dl_cfg_grant and srslte_pdsch_decode (:580-584).
+ * IN: nof_prb id nof_ports nrx phich_len phich_res max_prb rnti tm nsf | nsf x { tti, grid[nrx][n] cf32 }
+ * OUT per subframe: cfi corr(f32) noise(f32) | DL search (wr_msg) | ret(i32) tbs(i32) rv(i32) mod(i32)
+ *     ack(i32) noi(i32) nof_re(i32) | data[12000] | ce[port][rx] grids cf32 */
+static int run_ue_dl(void) {
+  srslte_cell_t cell;
+  memset(&cell, 0, sizeof(cell));
+  cell.nof_prb = rd_u32();
+  cell.id = rd_u32();
+  cell.nof_ports = rd_u32();
+  cell.cp = SRSLTE_CP_NORM;
+  const uint32_t nrx = rd_u32();
+  cell.phich_length = rd_u32() ? SRSLTE_PHICH_EXT : SRSLTE_PHICH_NORM;
+  cell.phich_resources = (srslte_phich_resources_t)rd_u32();
+  const uint32_t max_prb = rd_u32();
+  const uint16_t rnti = (uint16_t)rd_u32();
+  const uint32_t tm = rd_u32(), nsf = rd_u32();
+  if (!nrx || nrx > 2 || max_prb < cell.nof_prb) return -1;
+
+  srslte_ue_dl_t *q = calloc(1, sizeof(srslte_ue_dl_t));
+  q->nof_rx_antennas = nrx;
+  const uint32_t n = SRSLTE_SF_LEN_RE(cell.nof_prb, cell.cp), nmax = SRSLTE_SF_LEN_RE(max_prb, cell.cp);
+  for (int j = 0; j < SRSLTE_MAX_PORTS; j++) {
+    q->sf_symbols_m[j] = srslte_vec_malloc(nmax * sizeof(cf_t));
+    for (int i = 0; i < SRSLTE_MAX_PORTS; i++) {
+      q->ce_m[i][j] = srslte_vec_malloc(nmax * sizeof(cf_t));
+      bzero(q->ce_m[i][j], nmax * sizeof(cf_t));
+    }
+  }
+  for (int i = 0; i < SRSLTE_MAX_TB; i++) {
+    q->softbuffers[i] = srslte_vec_malloc(sizeof(srslte_softbuffer_rx_t));
+    if (srslte_softbuffer_rx_init(q->softbuffers[i], max_prb)) return -1;
+  }
+  q->cell = cell;
+  if (srslte_chest_dl_init(&q->chest, max_prb) || srslte_pcfich_init(&q->pcfich, nrx) ||
+      srslte_pdcch_init_ue(&q->pdcch, max_prb, nrx) || srslte_pdsch_init_ue(&q->pdsch, max_prb, nrx) ||
+      srslte_regs_init(&q->regs, cell) || srslte_chest_dl_set_cell(&q->chest, cell) ||
+      srslte_pcfich_set_cell(&q->pcfich, &q->regs, cell) || srslte_pdcch_set_cell(&q->pdcch, &q->regs, cell) ||
+      srslte_pdsch_set_cell(&q->pdsch, cell))
+    return -1;
+  srslte_ue_dl_set_rnti(q, rnti);
+  uint8_t *data[SRSLTE_MAX_CODEWORDS] = {calloc(1, 100000), calloc(1, 100000)};
+  for (uint32_t s = 0; s < nsf; s++) {
+    const uint32_t tti = rd_u32(), sf_idx = tti % 10;
+    for (uint32_t a = 0; a < nrx; a++) rd_buf(q->sf_symbols_m[a], sizeof(cf_t) * n);
+    uint32_t cfi = 0;
+    float corr = 0.f;
+    srslte_chest_dl_estimate_multi(&q->chest, q->sf_symbols_m, q->ce_m, sf_idx, nrx);
+    if (srslte_pcfich_decode_multi(&q->pcfich, q->sf_symbols_m, q->ce_m, srslte_chest_dl_get_noise_estimate(&q->chest),
+                                   sf_idx, &cfi, &corr) < 0)
+      return -1;
+    const float noise = srslte_chest_dl_get_noise_estimate(&q->chest);
+    wr_i32((int32_t)cfi);
+    wr_f32(corr);
+    wr_f32(noise);
+    int32_t ret = 0, tbs = 0, rv = 0, mod = 0, ack = 0, noi = 0, nre = 0;
+    srslte_dci_msg_t msg;
+    memset(&msg, 0, sizeof(msg));
+    memset(&q->last_location, 0, sizeof(q->last_location));
+    int found = 0;
+    if (cfi >= 1 && cfi <= 3) {
+      if (srslte_pdcch_extract_llr_multi(&q->pdcch, q->sf_symbols_m, q->ce_m, noise, sf_idx, cfi)) return -1;
+      found = srslte_ue_dl_find_dl_dci(q, tm, cfi, sf_idx, rnti, &msg);
+    }
+    wr_msg(found, &msg, &q->last_location);
+    memset(data[0], 0, 100000);
+    if (found == 1) {
+      srslte_ra_dl_dci_t dci;
+      srslte_ra_dl_grant_t grant;
+      bool acks[SRSLTE_MAX_CODEWORDS] = {false, false};
+      if (srslte_dci_msg_to_dl_grant(&msg, rnti, cell.nof_prb, cell.nof_ports, &dci, &grant)) return -1;
+      int rvidx[SRSLTE_MAX_CODEWORDS] = {1};
+      for (int i = 0; i < SRSLTE_MAX_CODEWORDS; i++) {
+        if (!grant.tb_en[i]) continue;
+        if (dci.rv_idx < 0) {
+          const uint32_t k = (tti / 10 / 2) % 4;
+          rvidx[i] = ((uint32_t)ceilf((float)1.5 * k)) % 4;
+        } else {
+          rvidx[i] = (uint32_t)(i == 0 ? dci.rv_idx : dci.rv_idx_1);
+        }
+        srslte_softbuffer_rx_reset_tbs(q->softbuffers[i], (uint32_t)grant.mcs[i].tbs);
+      }
+      srslte_mimo_type_t mimo = cell.nof_ports == 1 ? SRSLTE_MIMO_TYPE_SINGLE_ANTENNA : SRSLTE_MIMO_TYPE_TX_DIVERSITY;
+      if (msg.format != SRSLTE_DCI_FORMAT1 && msg.format != SRSLTE_DCI_FORMAT1A && msg.format != SRSLTE_DCI_FORMAT1C)
+        return -1; /* the recordings carry 1A / 1C only */
+      if (srslte_ue_dl_cfg_grant(q, &grant, cfi, sf_idx, rvidx, mimo)) return -1;
+      tbs = q->pdsch_cfg.grant.mcs[0].tbs;
+      rv = rvidx[0];
+      mod = (int32_t)q->pdsch_cfg.grant.mcs[0].mod;
+      nre = (int32_t)q->pdsch_cfg.nbits[0].nof_re;
+      if (q->pdsch_cfg.grant.mcs[0].mod > 0 && q->pdsch_cfg.grant.mcs[0].tbs >= 0) {
+        const int r = srslte_pdsch_decode(&q->pdsch, &q->pdsch_cfg, q->softbuffers, q->sf_symbols_m, q->ce_m, noise,
+                                          rnti, data, acks);
+        ack = acks[0];
+        noi = (int32_t)srslte_pdsch_last_noi_cw(&q->pdsch, 0);
+        ret = r == SRSLTE_SUCCESS ? tbs : 0; /* ue_dl.c:612-616 */
+      }
+    }
+    wr_i32(ret);
+    wr_i32(tbs);
+    wr_i32(rv);
+    wr_i32(mod);
+    wr_i32(ack);
+    wr_i32(noi);
+    wr_i32(nre);
+    wr(data[0], 12000);
+    for (uint32_t p = 0; p < cell.nof_ports; p++)
+      for (uint32_t a = 0; a < nrx; a++) wr(q->ce_m[p][a], sizeof(cf_t) * n);
+  }
+  return 0;
+}
+
 /* ---------------------------------------------------------------- CPU baseline ---- */
 /* One worker's objects. They are built one after the other on the main thread: srslte_tcod_init /
  * srslte_tcod_free share unguarded static tables (turbocoder.c:48-79: the first init builds them, any
@@ -456,7 +579,7 @@ static int run_pdsch_bench(void) {
 
 int main(int argc, char **argv) {
   if (argc != 4) {
-    fprintf(stderr, "usage: ref_front chest|dci|pdsch_bench IN OUT\n");
+    fprintf(stderr, "usage: ref_front chest|dci|ue_dl|pdsch_bench IN OUT\n");
     return 2;
   }
   fin = fopen(argv[2], "rb");
@@ -464,6 +587,7 @@ int main(int argc, char **argv) {
   if (!fin || !fout) return 2;
   int r = !strcmp(argv[1], "chest")         ? run_chest()
           : !strcmp(argv[1], "dci")         ? run_dci()
+          : !strcmp(argv[1], "ue_dl")       ? run_ue_dl()
           : !strcmp(argv[1], "pdsch_bench") ? run_pdsch_bench()
                                             : -1;
   fclose(fin);

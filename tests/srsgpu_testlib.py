@@ -490,6 +490,41 @@ def ref_front_dci(nof_prb, cell_id, nports, nrx, phich_len, phich_res, subframes
     return out
 
 
+def ref_front_ue_dl(nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb, rnti, tm, ttis, grids):
+    """srslte_ue_dl_decode_rnti's steps after the FFT (ue_dl.c:467-620: chest, PCFICH, PDCCH, DL DCI search,
+    grant, PDSCH) of the reference on ONE ue_dl-shaped object over a subframe sequence; grids[i][a]
+    complex64 [14 * 12 nof_prb]. -> per subframe dict(cfi, corr, noise, dl=(found, format, L, ncce,
+    nof_bits, buf), ret, tbs, rv, mod, ack, noi, nre, data [12000] u8, ce [nports][nrx][n])"""
+    n = 14 * 12 * nof_prb
+    pay = np.array([nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb, rnti, tm, len(ttis)],
+                   np.uint32).tobytes()
+    for i, t in enumerate(ttis):
+        pay += np.array([t], np.uint32).tobytes()
+        pay += b"".join(np.ascontiguousarray(grids[i][a], np.complex64).tobytes() for a in range(nrx))
+    raw = _run_ref_front("ue_dl", pay)
+    out, o = [], 0
+    for _ in ttis:
+        cfi = int(np.frombuffer(raw, np.int32, 1, o)[0])
+        corr, noise = np.frombuffer(raw, np.float32, 2, o + 4)
+        o += 12
+        v = np.frombuffer(raw, np.int32, 5, o)
+        o += 20
+        buf = np.frombuffer(raw, np.uint8, 128, o).copy()
+        o += 128
+        r = np.frombuffer(raw, np.int32, 7, o)
+        o += 28
+        data = np.frombuffer(raw, np.uint8, 12000, o).copy()
+        o += 12000
+        ce = np.frombuffer(raw, np.complex64, nports * nrx * n, o).reshape(nports, nrx, n).copy()
+        o += 8 * nports * nrx * n
+        out.append(dict(cfi=cfi, corr=float(corr), noise=float(noise),
+                        dl=(int(v[0]), int(v[1]), int(v[2]), int(v[3]), int(v[4]), buf if v[0] > 0 else buf[:0]),
+                        ret=int(r[0]), tbs=int(r[1]), rv=int(r[2]), mod=int(r[3]), ack=int(r[4]), noi=int(r[5]),
+                        nre=int(r[6]), data=data, ce=ce))
+    assert o == len(raw)
+    return out
+
+
 # ------------------------------------------------------------------ synthetic data ----
 
 def cb_sizes():
