@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "feedback_kernels.h"
 #include "pdsch_kernels.h"
 #include "srsgpu/pdsch_batch.h"
 #include "tdec_engine.h"
@@ -125,6 +126,10 @@ struct PdschEngine {
   }
   hipEvent_t staged = nullptr;
   bool staged_pending = false;
+  // TM3 / TM4 feedback items (lazily allocated; the host array is reused once its upload is done)
+  FbItem *h_fb = nullptr, *d_fb = nullptr;
+  hipEvent_t fb_staged = nullptr;
+  bool fb_pending = false;
   // transmit side (lazily allocated)
   TxItem *h_tx = nullptr, *d_tx = nullptr;
   uint8_t *d_ebits = nullptr; // [2 max_sf][max_bits] coded bits
@@ -181,10 +186,11 @@ struct PdschEngine {
     if (st) (void)hipStreamSynchronize(st);
     for (void *p : {(void *)d_x1, (void *)d_x2b, (void *)d_gold, (void *)d_llr, (void *)d_c,
                     (void *)d_csi, (void *)d_csimax, (void *)d_e, (void *)d_tx, (void *)d_ebits,
-                    (void *)d_mod})
+                    (void *)d_mod, (void *)d_fb})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb, (void *)h_tx})
+    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb, (void *)h_tx, (void *)h_fb})
       if (p) (void)hipHostFree(p);
+    if (fb_staged) (void)hipEventDestroy(fb_staged);
     for (auto &kv : maps) (void)hipFree(kv.second.first);
     maps.clear();
     if (staged) (void)hipEventDestroy(staged);
@@ -495,6 +501,47 @@ struct PdschEngine {
     return 0;
   }
 
+  // srsgpu_pdsch_feedback_dev: one FbItem per subframe, one launch
+  int feedback(const srsgpu_feedback_sf_t *sf, uint32_t n, const float *d_ce, size_t ant_stride, const float *d_noise,
+               srsgpu_feedback_t *out) {
+    if (n > max_sf) {
+      fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
+      return -1;
+    }
+    if (!h_fb) {
+      HIPCHK(hipHostMalloc(&h_fb, sizeof(FbItem) * max_sf));
+      HIPCHK(hipMalloc(&d_fb, sizeof(FbItem) * max_sf));
+      HIPCHK(hipEventCreateWithFlags(&fb_staged, hipEventDisableTiming));
+    }
+    if (fb_pending) HIPCHK(hipEventSynchronize(fb_staged));
+    const uint32_t nof_ce = (cell.cp == 1 ? 12u : 14u) * 12u * cell.nof_prb; // SRSLTE_SF_LEN_RE
+    if (ant_stride < nof_ce) {
+      fprintf(stderr, "srsgpu: feedback needs full estimate planes (stride %zu < %u)\n", ant_stride, nof_ce);
+      return -1;
+    }
+    const uint32_t P = cell.nof_ports, R = cell.nof_rx_ant;
+    for (uint32_t i = 0; i < n; i++) {
+      FbItem &t = h_fb[i];
+      memset(&t, 0, sizeof(t));
+      const float2 *base = (const float2 *)d_ce + sf[i].ce_offset;
+      for (uint32_t p = 0; p < 2 && p < P; p++)
+        for (uint32_t a = 0; a < R; a++) t.h[p][a] = base + (size_t)(a * P + p) * ant_stride; // [rx][port] planes
+      t.noise = sf[i].noise_estimate;
+      t.noise_dev = d_noise ? d_noise + i : nullptr;
+      t.flags = sf[i].flags;
+      t.nof_ce = nof_ce;
+      t.nrx = (int)R;
+      t.nports = (int)P;
+      t.out = out + i;
+    }
+    HIPCHK(hipMemcpyAsync(d_fb, h_fb, sizeof(FbItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(fb_staged, st));
+    fb_pending = true;
+    ProfScope ps("k_feedback", st);
+    HIPCHK(launch_feedback(d_fb, (int)n, st));
+    return 0;
+  }
+
   uint32_t count_tb(const srsgpu_pdsch_sf_t *sf, uint32_t n) const {
     uint32_t k = 0;
     for (uint32_t i = 0; i < n; i++) k += nof_tb(sf[i]);
@@ -588,6 +635,12 @@ int srsgpu_pdsch_encode_ports_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf
                                   float *d_grid, size_t port_stride) {
   if (!q || (!sf && n) || !d_data || !d_grid) return -1;
   return q->e.encode(sf, n, d_data, d_grid, (uint64_t)port_stride);
+}
+
+int srsgpu_pdsch_feedback_dev(srsgpu_pdsch_t *q, const srsgpu_feedback_sf_t *sf, uint32_t n, const float *d_ce,
+                              size_t ant_stride, const float *d_noise, srsgpu_feedback_t *d_out) {
+  if (!q || (!sf && n) || !d_ce || !d_out) return -1;
+  return q->e.feedback(sf, n, d_ce, ant_stride, d_noise, d_out);
 }
 
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,

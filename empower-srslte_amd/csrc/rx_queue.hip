@@ -131,6 +131,63 @@ __global__ __launch_bounds__(256) void k_ingest(const void *const *__restrict__ 
   }
 }
 
+// srslte_chest_dl_get_* (chest_dl.c:737-846) of every subframe of a batch, in the reference's float
+// order, one thread per subframe: out[i] = {cfo, snr, rsrp, rsrq, rssi, rsrp_neighbour}. meas holds
+// the estimator's [subframe][rx][port] {rsrp, rssi, rsrp_corr, cfo} (srsgpu_chest_estimate_meas_dev),
+// noise the per-(rx, port) noise after the PSS / EMPTY carry. The reference's q->cfo is the last
+// (rx, port) estimate of the latest subframe that estimated it: cfo_src[i] (-1: the carried value in
+// last), and q->rsrp_corr is only rewritten with rsrp_neighbour on.
+__global__ void k_getters(const float *__restrict__ noise, const float *__restrict__ meas,
+                          const int32_t *__restrict__ cfo_src, int rsrp_nb, const float *__restrict__ last, int n,
+                          int nrx, int np, int nof_prb, float *__restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int cols = nrx * np;
+  const float *m = meas + (size_t)i * cols * 4;
+  const float *nb = rsrp_nb ? m : last;
+  float nn = 0.f; // srslte_chest_dl_get_noise_estimate
+  for (int a = 0; a < nrx; a++) {
+    float acc = 0.f;
+    for (int p = 0; p < np; p++) acc += noise[(size_t)i * cols + a * np + p];
+    nn += acc / (float)np;
+  }
+  nn /= (float)nrx;
+  float rs = 0.f; // srslte_chest_dl_get_snr's sum
+  for (int a = 0; a < nrx; a++)
+    for (int p = 0; p < np; p++) rs += m[(a * np + p) * 4] / (float)np;
+  float rssi = 0.f, rsrq = 0.f, rsrp = -1e9f, nbr = -1e9f;
+  for (int a = 0; a < nrx; a++) {
+    rssi += 4.f * m[(a * np) * 4 + 1] / (float)nof_prb / 12.f;
+    rsrq += (float)nof_prb * m[(a * np) * 4] / m[(a * np) * 4 + 1];
+    float v = 0.f, w = 0.f;
+    for (int p = 0; p < np; p++) {
+      v += m[(a * np + p) * 4];
+      w += nb[(a * np + p) * 4 + 2];
+    }
+    v /= (float)np;
+    w /= (float)np;
+    if (v > rsrp) rsrp = v;
+    if (w > nbr) nbr = w;
+  }
+  const int lc = (nrx - 1) * np + np - 1;
+  float *o = out + (size_t)i * 6;
+  o[0] = cfo_src[i] >= 0 ? meas[((size_t)cfo_src[i] * cols + lc) * 4 + 3] : last[lc * 4 + 3];
+  o[1] = rs / nn;
+  o[2] = rsrp;
+  o[3] = rsrq / (float)nrx;
+  o[4] = rssi / (float)nrx;
+  o[5] = nbr;
+}
+
+// the estimator state the next batch starts from: the CFO of the last subframe that estimated it, and
+// the neighbour RSRP of the batch's last subframe when it was computed
+__global__ void k_meas_last(const float *__restrict__ meas, int cfo_from, int nb_from, int cols, float *__restrict__ last) {
+  const int c = threadIdx.x;
+  if (c >= cols) return;
+  if (cfo_from >= 0) last[c * 4 + 3] = meas[((size_t)cfo_from * cols + c) * 4 + 3];
+  if (nb_from >= 0) last[c * 4 + 2] = meas[((size_t)nb_from * cols + c) * 4 + 2];
+}
+
 // transport blocks of a PDSCH subframe (srsgpu/pdsch_batch.h)
 uint32_t sf_ntb(const srsgpu_pdsch_sf_t &s) {
   return s.mimo_type == SRSGPU_MIMO_CDD || (s.mimo_type == SRSGPU_MIMO_SPATIAL_MULTIPLEX && s.tbs[1] > 0) ? 2 : 1;
@@ -152,6 +209,12 @@ struct srsgpu_rxq {
   srsgpu_pdcch_t *pdcch = nullptr; // created with the PHICH configuration on the first ue_dl batch
   float *d_grid = nullptr, *d_ce = nullptr, *d_noise = nullptr;
   float *d_noise_last = nullptr; // PSS / EMPTY: the estimate carried between batches
+  float *d_meas = nullptr;       // [subframe][rx][port] {rsrp, rssi, rsrp_corr, cfo}
+  float *d_meas_last = nullptr;  // [rx][port] x 4: q->cfo / q->rsrp_corr carried between batches
+  int32_t *d_cfo_src = nullptr, *h_cfo_src = nullptr;
+  float *d_getters = nullptr, *h_getters = nullptr; // [subframe] x 6 (srsgpu_rxq_meas_t)
+  srsgpu_feedback_t *d_fb = nullptr, *h_fb = nullptr; // the ue_dl items' TM3 / TM4 feedback
+  std::vector<srsgpu_feedback_sf_t> fb_sf;
   uint8_t *d_est = nullptr, *h_est = nullptr; // per subframe: 1 if it estimates the noise
   uint8_t *d_data = nullptr;
   int32_t *d_ret = nullptr;
@@ -265,6 +328,15 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMalloc(&d_noi, sizeof(uint32_t) * 2 * mb));
     RXQ_CHK(hipMalloc(&d_noise_last, sizeof(float) * nrx * nports));
     RXQ_CHK(hipMemset(d_noise_last, 0, sizeof(float) * nrx * nports)); // srslte_chest_dl_init: 0
+    RXQ_CHK(hipMalloc(&d_meas, sizeof(float) * 4 * mb * nrx * nports));
+    RXQ_CHK(hipMalloc(&d_meas_last, sizeof(float) * 4 * nrx * nports));
+    RXQ_CHK(hipMemset(d_meas_last, 0, sizeof(float) * 4 * nrx * nports)); // bzero'd estimator
+    RXQ_CHK(hipMalloc(&d_cfo_src, sizeof(int32_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_cfo_src, sizeof(int32_t) * mb));
+    RXQ_CHK(hipMalloc(&d_getters, sizeof(float) * 6 * mb));
+    RXQ_CHK(hipHostMalloc(&h_getters, sizeof(float) * 6 * mb));
+    RXQ_CHK(hipMalloc(&d_fb, sizeof(srsgpu_feedback_t) * mb));
+    RXQ_CHK(hipHostMalloc(&h_fb, sizeof(srsgpu_feedback_t) * mb));
     RXQ_CHK(hipMalloc(&d_est, mb));
     RXQ_CHK(hipHostMalloc(&h_est, mb));
     RXQ_CHK(hipHostMalloc(&h_noise, sizeof(float) * mb * nrx * nports));
@@ -320,11 +392,12 @@ struct srsgpu_rxq {
     for (void *p : {(void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data, (void *)d_ret,
                     (void *)d_noi, (void *)d_noise_last, (void *)d_est, (void *)d_sel, (void *)d_uenoise,
                     (void *)d_cfi, (void *)d_corr, (void *)d_llr, (void *)d_res, (void *)d_who,
-                    (void *)d_pnoise, (void *)d_res_ul})
+                    (void *)d_pnoise, (void *)d_res_ul, (void *)d_meas, (void *)d_meas_last, (void *)d_cfo_src,
+                    (void *)d_getters, (void *)d_fb})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est,
                     (void *)h_sel, (void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_who,
-                    (void *)h_res_ul})
+                    (void *)h_res_ul, (void *)h_cfo_src, (void *)h_getters, (void *)h_fb})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
@@ -518,8 +591,19 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMemcpyAsync(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipMemcpyAsync(h_res_ul, d_res_ul, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipStreamSynchronize(st));
+    // the workers' TM3 / TM4 feedback on the same estimates (phch_worker.cc:522-540); its results come
+    // back with the batch's other results
+    bool any = false;
+    fb_sf.resize(nu);
+    for (uint32_t j = 0; j < nu; j++) {
+      fb_sf[j] = {(uint64_t)ue[j] * nrx * nports * gsz, 0.f, b[ue[j]].ue->feedback};
+      any = any || b[ue[j]].ue->feedback;
+    }
+    if (any && srsgpu_pdsch_feedback_dev(pdsch, fb_sf.data(), nu, d_ce, gsz, d_uenoise, d_fb)) return -1;
+    fb_any = any;
     return 0;
   }
+  bool fb_any = false;
 
   // the grant of a found DCI as srslte_ue_dl_decode_rnti configures it (ue_dl.c:498-574): unpack,
   // redundancy versions, softbuffer resets, MIMO type of the format, srslte_pdsch_cfg_mimo's
@@ -615,7 +699,7 @@ struct srsgpu_rxq {
       fprintf(stderr, "srsgpu rxq: smooth_filter_auto with PSS / EMPTY noise is not batched\n");
       return -1;
     }
-    if (srsgpu_chest_estimate_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise)) return -1;
+    if (srsgpu_chest_estimate_meas_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise, d_meas)) return -1;
     if (ccfg.noise_alg != 0) { // PSS / EMPTY: carry the estimate across subframes in order
       for (uint32_t i = 0; i < n; i++) h_est[i] = (uint8_t)(b[i].sf_idx() == 0 || b[i].sf_idx() == 5);
       RXQ_CHK(hipMemcpyAsync(d_est, h_est, n, hipMemcpyHostToDevice, st));
@@ -624,11 +708,31 @@ struct srsgpu_rxq {
                          d_noise_last);
       RXQ_CHK(hipGetLastError());
     }
+    { // the estimator getters of every subframe (srsgpu_rxq_meas_t)
+      int32_t src = -1;
+      for (uint32_t i = 0; i < n; i++) {
+        if (ccfg.cfo_estimate_enable && ((ccfg.cfo_estimate_sf_mask >> b[i].sf_idx()) & 1u)) src = (int32_t)i;
+        h_cfo_src[i] = src;
+      }
+      const int cols = (int)(nrx * nports);
+      RXQ_CHK(hipMemcpyAsync(d_cfo_src, h_cfo_src, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_getters, dim3((n + 63) / 64), dim3(64), 0, st, d_noise, d_meas, d_cfo_src,
+                         (int)ccfg.rsrp_neighbour, d_meas_last, (int)n, (int)nrx, (int)nports, (int)cell.nof_prb,
+                         d_getters);
+      RXQ_CHK(hipGetLastError());
+      hipLaunchKernelGGL(k_meas_last, dim3(1), dim3(64), 0, st, d_meas, src, ccfg.rsrp_neighbour ? (int)n - 1 : -1,
+                         cols, d_meas_last);
+      RXQ_CHK(hipGetLastError());
+      RXQ_CHK(hipMemcpyAsync(h_getters, d_getters, sizeof(float) * 6 * n, hipMemcpyDeviceToHost, st));
+    }
     srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(pdsch);
     std::vector<uint32_t> ue;
     for (uint32_t i = 0; i < n; i++)
       if (b[i].ue) ue.push_back(i);
+    fb_any = false;
     if (!ue.empty() && control(b, ue)) return -1;
+    if (fb_any)
+      RXQ_CHK(hipMemcpyAsync(h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
     // grants: the grant items' own, the ue_dl items' from their DCI
     std::vector<srsgpu_pdsch_sf_t> sfs;
     std::vector<uint32_t> who;       // batch index of each PDSCH subframe
@@ -644,6 +748,9 @@ struct srsgpu_rxq {
         u->format = res.format;
         u->L = res.L;
         u->ncce = res.ncce;
+        u->dci_nof_bits = res.found == 1 ? res.nof_bits : 0;
+        memset(u->dci_data, 0, sizeof(u->dci_data));
+        if (res.found == 1) memcpy(u->dci_data, res.data, std::min(sizeof(u->dci_data), sizeof(res.data)));
         // srslte_ue_dl_find_ul_dci + srslte_dci_msg_to_ul_grant (phch_worker.cc:938-967)
         const srsgpu_dci_result_t &ur = h_res_ul[j];
         u->ul_found = u->ul_rnti ? ur.found : 0;
@@ -722,7 +829,7 @@ struct srsgpu_rxq {
         if (out) memcpy(out, h_data + (2 * k + t) * dlen, SRSGPU_DLSCH_DATA_LEN(sfs[k].tbs[t]));
       }
     }
-    for (uint32_t i = 0; i < n; i++) {
+    for (uint32_t i = 0, jf = 0; i < n; i++) {
       // srslte_chest_dl_get_noise_estimate (chest_dl.c:741-750): mean over ports, then antennas
       float nn = 0.f;
       for (uint32_t a = 0; a < nrx; a++) {
@@ -731,13 +838,24 @@ struct srsgpu_rxq {
         nn += acc / (float)nports;
       }
       nn /= (float)nrx;
+      const float *g = h_getters + (size_t)i * 6;
+      const srsgpu_rxq_meas_t meas = {g[0], g[1], g[2], g[3], g[4], g[5]};
       if (b[i].it) {
         b[i].it->noise = nn;
+        b[i].it->meas = meas;
       } else {
         srsgpu_rxq_ue_dl_t *u = b[i].ue;
         u->noise = nn;
+        u->meas = meas;
         // ue_dl.c:612-616: TB 0's size when a DCI was found and the PDSCH call succeeded
         u->ret = state[i] < 0 ? -1 : (u->found == 1 ? u->grant.tbs[0] : 0);
+        if (u->feedback) {
+          u->fb = h_fb[jf];
+        } else {
+          memset(&u->fb, 0, sizeof(u->fb));
+          u->fb.ret_cn = u->fb.ret_pmi = -1;
+        }
+        jf++;
       }
     }
     return 0;

@@ -123,11 +123,40 @@ class srsgpu_pdsch_sf_t(ctypes.Structure):
                 ("codebook_idx", ctypes.c_uint32), ("skip_tb", ctypes.c_uint32)]
 
 
+class srsgpu_rxq_meas_t(ctypes.Structure):
+    """include/srsgpu/rx_queue.h: srslte_chest_dl_get_* of a subframe"""
+    _fields_ = [("cfo", ctypes.c_float), ("snr", ctypes.c_float), ("rsrp", ctypes.c_float), ("rsrq", ctypes.c_float),
+                ("rssi", ctypes.c_float), ("rsrp_neighbour", ctypes.c_float)]
+
+    def values(self):
+        return [self.cfo, self.snr, self.rsrp, self.rsrq, self.rssi, self.rsrp_neighbour]
+
+
+class srsgpu_feedback_sf_t(ctypes.Structure):
+    """include/srsgpu/pdsch_batch.h"""
+    _fields_ = [("ce_offset", ctypes.c_uint64), ("noise_estimate", ctypes.c_float), ("flags", ctypes.c_uint32)]
+
+
+class srsgpu_feedback_t(ctypes.Structure):
+    """include/srsgpu/pdsch_batch.h: TM3 / TM4 feedback of a subframe"""
+    _fields_ = [("cn", ctypes.c_float), ("ri_tm3", ctypes.c_uint32), ("ret_cn", ctypes.c_int32),
+                ("ri", ctypes.c_uint32), ("pmi", ctypes.c_uint32), ("pmi_l", ctypes.c_uint32 * 2),
+                ("ret_pmi", ctypes.c_int32), ("sinr", (ctypes.c_float * 4) * 2)]
+
+    def sinr_array(self):
+        import numpy as np
+        return np.array([[self.sinr[l][c] for c in range(4)] for l in range(2)], np.float32)
+
+
+FEEDBACK_CN, FEEDBACK_PMI = 1, 2
+
+
 class srsgpu_rxq_item_t(ctypes.Structure):
     """include/srsgpu/rx_queue.h"""
     _fields_ = [("td", ctypes.c_void_p * 2), ("sf", srsgpu_pdsch_sf_t),
                 ("reset_softbuffer", ctypes.c_uint32 * 2), ("data", ctypes.c_void_p * 2),
-                ("ret", ctypes.c_int32 * 2), ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float)]
+                ("ret", ctypes.c_int32 * 2), ("noi", ctypes.c_uint32 * 2), ("noise", ctypes.c_float),
+                ("meas", srsgpu_rxq_meas_t)]
 
 
 class srsgpu_viterbi_frame_t(ctypes.Structure):
@@ -245,7 +274,12 @@ class srsgpu_rxq_ue_dl_t(ctypes.Structure):
                 ("ul_rnti", ctypes.c_uint16), ("n_rb_ho", ctypes.c_uint32), ("ul_found", ctypes.c_int32),
                 ("ul_L", ctypes.c_uint32), ("ul_ncce", ctypes.c_uint32), ("ul_nof_bits", ctypes.c_uint32),
                 ("ul_data", ctypes.c_uint8 * 128), ("ul_grant_ret", ctypes.c_int32), ("ul_dci", srsgpu_ra_ul_dci_t),
-                ("ul_grant", srsgpu_ra_ul_grant_t), ("acked_in", ctypes.c_uint8 * 2)]
+                ("ul_grant", srsgpu_ra_ul_grant_t), ("acked_in", ctypes.c_uint8 * 2),
+                ("dci_nof_bits", ctypes.c_uint32), ("dci_data", ctypes.c_uint8 * 128), ("meas", srsgpu_rxq_meas_t),
+                ("feedback", ctypes.c_uint32), ("fb", srsgpu_feedback_t)]
+
+    def dci_bits(self):
+        return list(self.dci_data[:self.dci_nof_bits])
 
 
 def dlsch_data_len(tbs):
@@ -383,6 +417,7 @@ _sig = {
     "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
     "srsgpu_chest_set_smooth_filter_gauss": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_float]),
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
+    "srsgpu_pdsch_feedback_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_feedback_sf_t), _u32, _vp, _sz, _vp, _vp]),
     "srsgpu_chest_estimate_meas_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp, _vp]),
     "srsgpu_chest_set_cfg": (_i32, [_vp, _vp]),
     "srsgpu_chest_get_cfg": (_i32, [_vp, _vp]),
@@ -949,6 +984,16 @@ class Pdsch:
         return _lib.srsgpu_pdsch_decode_dev(self.q, arr, len(sfs), _vp(d_grid), _vp(d_ce), ant_stride,
                                             _vp(d_data), max_halfits, _vp(d_ret), _vp(d_noi))
 
+    def feedback_dev(self, items, d_ce, ant_stride, d_out, d_noise=None):
+        """srsgpu_pdsch_feedback_dev: items of (ce_offset, noise_estimate, flags); d_out device memory of
+        len(items) srsgpu_feedback_t"""
+        arr = (srsgpu_feedback_sf_t * len(items))(*[srsgpu_feedback_sf_t(o, nz, f) for o, nz, f in items])
+        return _lib.srsgpu_pdsch_feedback_dev(self.q, arr, len(items), _vp(d_ce), ant_stride, _vp(d_noise), _vp(d_out))
+
+    @staticmethod
+    def parse_feedback(raw, n):
+        return list((srsgpu_feedback_t * n).from_buffer_copy(raw[:n * ctypes.sizeof(srsgpu_feedback_t)]))
+
     def close(self):
         if self.q:
             _lib.srsgpu_pdsch_destroy(self.q)
@@ -1149,21 +1194,31 @@ class RxQueue:
         return it
 
     def set_chest_cfg(self, average_subframe=False, noise_alg=0, smooth_filter_auto=False,
-                      symbol_sz=None):
-        """the queue estimator's settings (srsgpu_chest_set_cfg on srsgpu_rxq_get_chest)"""
-        c = srsgpu_chest_cfg_t(int(average_subframe), noise_alg, int(smooth_filter_auto), 0, 0, 0,
-                               symbol_sz or symbol_sz_of(self.cell.nof_prb))
-        if _lib.srsgpu_chest_set_cfg(_lib.srsgpu_rxq_get_chest(self.q), ctypes.byref(c)) != 0:
+                      symbol_sz=None, rsrp_neighbour=False, cfo_enable=False, cfo_mask=0, gauss=None, filt=None):
+        """the queue estimator's settings (srsgpu_chest_set_cfg on srsgpu_rxq_get_chest); gauss=(order, std)
+        or filt (taps) sets the smoothing filter"""
+        ch = _lib.srsgpu_rxq_get_chest(self.q)
+        c = srsgpu_chest_cfg_t(int(average_subframe), noise_alg, int(smooth_filter_auto), int(rsrp_neighbour),
+                               int(cfo_enable), cfo_mask, symbol_sz or symbol_sz_of(self.cell.nof_prb))
+        if _lib.srsgpu_chest_set_cfg(ch, ctypes.byref(c)) != 0:
             raise RuntimeError("invalid chest configuration")
+        if gauss is not None and _lib.srsgpu_chest_set_smooth_filter_gauss(ch, gauss[0], ctypes.c_float(gauss[1])) != 0:
+            raise RuntimeError("invalid filter")
+        if filt is not None:
+            f = (ctypes.c_float * max(1, len(filt)))(*filt)
+            if _lib.srsgpu_chest_set_smooth_filter(ch, f, len(filt)) != 0:
+                raise RuntimeError("invalid filter")
 
     def decode(self, it):
         return _lib.srsgpu_rxq_decode(self.q, ctypes.byref(it))
 
     @staticmethod
-    def ue_item(td, tti, rnti, data, tm=0, rnti_type=-1, softbuffer=(0, 1), ul_rnti=0, n_rb_ho=0, acks=(0, 0)):
+    def ue_item(td, tti, rnti, data, tm=0, rnti_type=-1, softbuffer=(0, 1), ul_rnti=0, n_rb_ho=0, acks=(0, 0),
+                feedback=0):
         """srsgpu_rxq_ue_dl_t: td complex64 arrays per rx antenna, data uint8 arrays per TB (both kept
-        alive by the caller)"""
+        alive by the caller); feedback: FEEDBACK_CN | FEEDBACK_PMI"""
         u = srsgpu_rxq_ue_dl_t()
+        u.feedback = feedback
         for a, x in enumerate(td):
             u.td[a] = x.ctypes.data
         u.tti, u.rnti, u.tm, u.rnti_type = tti, rnti, tm, rnti_type

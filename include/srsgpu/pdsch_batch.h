@@ -141,6 +141,41 @@ int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
 int srsgpu_pdsch_encode_ports_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
                                   const uint8_t *d_data, float *d_grid, size_t port_stride);
 
+/* TM3 / TM4 feedback from a subframe's channel estimates, as srsUE's PHY worker computes it for its
+ * uplink control information (phch_worker.cc:522-540):
+ *   - condition number (srslte_pdsch_cn_compute -> srslte_precoding_cn, precoding.c:2889-2922: the mean
+ *     over every 24th estimate of 10 log10(lambda_max / lambda_min) of H H', 2 ports x 2 rx antennas only)
+ *     and the TM3 rank of srslte_ue_dl_ri_select (ue_dl.c:747-764: 1 below 17 dB);
+ *   - the per-layer PMI choice of srslte_pdsch_pmi_select (pdsch.c:1009-1041 ->
+ *     srslte_precoding_pmi_select_1l / _2l, precoding.c:2335-2860, AVX forms: four estimates every 96,
+ *     every 24 apart) and the rank / PMI of srslte_ue_dl_ri_pmi_select (ue_dl.c:684-745), 2 ports, 1-2 rx.
+ * The one-layer SINRs follow the reference's operations (FMA complex products) exactly; the two-layer
+ * ones use exact reciprocals where the reference uses _mm256_rcp_ps (relative error <= 1.5 * 2^-12), and
+ * the condition number the device log10f. A codebook whose SINR never exceeds 0 leaves its PMI at 0 (the
+ * reference keeps the value its object held). */
+typedef struct {
+  uint64_t ce_offset;   /* the subframe's full [rx antenna][port] estimate planes in d_ce (complex elements) */
+  float noise_estimate; /* srslte_chest_dl_get_noise_estimate of the subframe */
+  uint32_t flags;       /* SRSGPU_FEEDBACK_CN | SRSGPU_FEEDBACK_PMI */
+} srsgpu_feedback_sf_t;
+#define SRSGPU_FEEDBACK_CN 1u  /* condition number + TM3 rank (2 ports, 2 rx antennas) */
+#define SRSGPU_FEEDBACK_PMI 2u /* per-layer PMI / SINR + TM4 rank / PMI (2 ports) */
+typedef struct {
+  float cn;             /* dB; 0 when not computed */
+  uint32_t ri_tm3;      /* srslte_ue_dl_ri_select: 1 (two layers) when cn < 17 dB */
+  int32_t ret_cn;       /* 0, or -1 where the reference's call fails (not 2 x 2) or it was not asked */
+  uint32_t ri, pmi;     /* srslte_ue_dl_ri_pmi_select's rank index (layers - 1) and PMI */
+  uint32_t pmi_l[2];    /* srslte_precoding_pmi_select's PMI for 1 and 2 layers */
+  int32_t ret_pmi;      /* 0, or -1 (not 2 ports, or not asked) */
+  float sinr[2][4];     /* q->sinr[layers - 1][codebook]; layers above the rx antennas: -inf; the two-layer
+                           codebooks 2, 3: 0 */
+} srsgpu_feedback_t;
+/* nof_sf subframes of the cell's estimate planes (ant_stride complex elements apart) -> d_out[nof_sf]
+ * (device memory), one launch on the handle's stream. d_noise (may be NULL): subframe i's noise estimate
+ * is d_noise[i] instead of sf[i].noise_estimate. */
+int srsgpu_pdsch_feedback_dev(srsgpu_pdsch_t *q, const srsgpu_feedback_sf_t *sf, uint32_t nof_sf,
+                              const float *d_ce, size_t ant_stride, const float *d_noise, srsgpu_feedback_t *d_out);
+
 /* RE count of a grant (srslte_pdsch_get's return value). */
 int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf);
 

@@ -26,6 +26,15 @@ extern "C" {
 
 typedef struct srsgpu_rxq srsgpu_rxq_t;
 
+/* The estimator's per-subframe measurements as srsUE's PHY worker reads them after each subframe
+ * (srslte_chest_dl_get_cfo / _get_snr / _get_rsrp / _get_rsrq / _get_rssi / _get_rsrp_neighbour,
+ * chest_dl.c:737-846; phch_worker.cc:226-241, 301, 313, 1618-1628), linear values. Like the reference's
+ * estimator object, the queue carries the CFO across subframes that do not estimate it
+ * (srsgpu_chest_cfg_t.cfo_estimate_sf_mask) and the neighbour RSRP while rsrp_neighbour is off. */
+typedef struct {
+  float cfo, snr, rsrp, rsrq, rssi, rsrp_neighbour;
+} srsgpu_rxq_meas_t;
+
 typedef struct {
   /* in */
   const void *td[2];        /* host time-domain subframe per rx antenna: 15 * symbol_sz complex
@@ -38,6 +47,7 @@ typedef struct {
   int32_t ret[2];           /* srslte_dlsch_decode2's result per TB: 0 ack, -1 CRC error, -2 invalid */
   uint32_t noi[2];          /* nof_iterations per TB */
   float noise;              /* srslte_chest_dl_get_noise_estimate of the subframe */
+  srsgpu_rxq_meas_t meas;
 } srsgpu_rxq_item_t;
 
 /* srslte_ue_dl_decode_rnti (src/phy/ue/ue_dl.c:467-620) of one subframe, the call srsUE's PHY worker
@@ -86,6 +96,15 @@ typedef struct {
   srsgpu_ra_ul_dci_t ul_dci;
   srsgpu_ra_ul_grant_t ul_grant;
   uint8_t acked_in[2];     /* internal: acks as submitted */
+  /* out: the found DL DCI (srslte_dci_msg_t's nof_bits and message buffer: payload + 16 CRC bits) */
+  uint32_t dci_nof_bits;
+  uint8_t dci_data[128];
+  srsgpu_rxq_meas_t meas;  /* out */
+  /* in: the worker's TM3 / TM4 feedback for its UCI (phch_worker::compute_ri, phch_worker.cc:522-540):
+   * SRSGPU_FEEDBACK_CN (srslte_ue_dl_ri_select) and / or SRSGPU_FEEDBACK_PMI
+   * (srslte_ue_dl_ri_pmi_select) on this subframe's estimates (srsgpu_pdsch_feedback_dev) */
+  uint32_t feedback;
+  srsgpu_feedback_t fb;    /* out */
 } srsgpu_rxq_ue_dl_t;
 
 /* One cell (srsgpu_cell_t), FFT size symbol_sz (srsgpu_symbol_sz), nof_softbuffers HARQ

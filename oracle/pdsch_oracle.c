@@ -1136,3 +1136,178 @@ int orc_ulsch_uci(uint32_t tbs, uint32_t Qm, uint32_t nof_bits, uint32_t nsymb, 
   free(ri_at);
   return 0;
 }
+
+/* ---------------------------------------------------------------- TM3 / TM4 feedback ---------- */
+/* srslte_precoding_pmi_select_1l_avx / _2l_avx (src/phy/mimo/precoding.c:2335-2450, 2699-2845) with
+ * LV_HAVE_FMA: the complex products of simd.h:64-91 (PROD = fmaddsub(a, ldup(b), swap(a) * hdup(b)),
+ * PROD_ADD / PROD_SUB with the inner fmaddsub / fmsubadd), four estimates every 96, 24 apart, summed in
+ * the reference's order; _mm256_rcp_ps restated as an exact reciprocal (the reference's is approximate).
+ * srslte_precoding_2x2_cn_gen + srslte_mat_2x2_cn (:2889-2912, utils/mat.c:107-127). The rank / PMI
+ * choices of srslte_ue_dl_ri_select / srslte_ue_dl_ri_pmi_select (src/phy/ue/ue_dl.c:684-764). */
+typedef struct {
+  float r, i;
+} ocf;
+static ocf oc_ld(const float *p, uint32_t k) {
+  ocf v = {0.f, 0.f};
+  if (p) {
+    v.r = p[2 * k];
+    v.i = p[2 * k + 1];
+  }
+  return v;
+}
+static ocf oc_cj(ocf a) { return (ocf){a.r, -a.i}; }
+static ocf oc_mulj(ocf a) { return (ocf){-a.i, a.r}; }
+static ocf oc_add(ocf a, ocf b) { return (ocf){a.r + b.r, a.i + b.i}; }
+static ocf oc_sub(ocf a, ocf b) { return (ocf){a.r - b.r, a.i - b.i}; }
+static ocf oc_prod(ocf a, ocf b) { return (ocf){fmaf(a.r, b.r, -(a.i * b.i)), fmaf(a.i, b.r, a.r * b.i)}; }
+static ocf oc_prod_add(ocf a, ocf b, ocf c) {
+  const float ur = fmaf(a.i, b.i, -c.r), ui = fmaf(a.r, b.i, c.i);
+  return (ocf){fmaf(a.r, b.r, -ur), fmaf(a.i, b.r, ui)};
+}
+static ocf oc_prod_sub(ocf a, ocf b, ocf c) {
+  const float ur = fmaf(a.i, b.i, c.r), ui = fmaf(a.r, b.i, -c.i);
+  return (ocf){fmaf(a.r, b.r, -ur), fmaf(a.i, b.r, ui)};
+}
+
+#define ORC_PMI_PREC 24
+
+static float orc_pmi_1l(const float *const h[2][2], uint32_t nof_ce, float noise, int cb) {
+  float s = 0.f;
+  uint32_t count = 0;
+  for (uint32_t j = 0; j < nof_ce - ORC_PMI_PREC * 4 + 1; j += ORC_PMI_PREC * 4) {
+    float g[4];
+    for (int k = 0; k < 4; k++) {
+      const uint32_t p = j + ORC_PMI_PREC * k;
+      const ocf h00 = oc_ld(h[0][0], p), h01 = oc_ld(h[1][0], p), h10 = oc_ld(h[0][1], p), h11 = oc_ld(h[1][1], p);
+      ocf a0, a1, c;
+      if (cb == 0) {
+        a0 = oc_add(oc_cj(h00), oc_cj(h01));
+        a1 = oc_add(oc_cj(h10), oc_cj(h11));
+      } else if (cb == 1) {
+        a0 = oc_sub(oc_cj(h00), oc_cj(h01));
+        a1 = oc_sub(oc_cj(h10), oc_cj(h11));
+      } else if (cb == 2) {
+        a0 = oc_sub(oc_cj(h00), oc_mulj(oc_cj(h01)));
+        a1 = oc_sub(oc_cj(h10), oc_mulj(oc_cj(h11)));
+      } else {
+        a0 = oc_add(oc_cj(h00), oc_mulj(oc_cj(h01)));
+        a1 = oc_add(oc_cj(h10), oc_mulj(oc_cj(h11)));
+      }
+      const ocf b0 = oc_prod_add(a0, h00, oc_prod(a1, h10)), b1 = oc_prod_add(a0, h01, oc_prod(a1, h11));
+      c = cb == 0 ? oc_add(b0, b1) : cb == 1 ? oc_sub(b0, b1) : cb == 2 ? oc_add(b0, oc_mulj(b1)) : oc_sub(b0, oc_mulj(b1));
+      g[k] = c.r * 0.5f;
+    }
+    s += g[0] + g[1] + g[2] + g[3];
+    count += 4;
+  }
+  return s / (noise * (float)count);
+}
+
+static float orc_pmi_2l(const float *const h[2][2], uint32_t nof_ce, float noise, int cb) {
+  float s = 0.f;
+  uint32_t count = 0;
+  for (uint32_t j = 0; j < nof_ce - ORC_PMI_PREC * 4 + 1; j += ORC_PMI_PREC * 4) {
+    float v[4];
+    for (int k = 0; k < 4; k++) {
+      const uint32_t p = j + ORC_PMI_PREC * k;
+      const ocf h00 = oc_ld(h[0][0], p), h01 = oc_ld(h[1][0], p), h10 = oc_ld(h[0][1], p), h11 = oc_ld(h[1][1], p);
+      ocf a00, a01, a10, a11, c00, c01, c10, c11;
+      if (cb == 0) {
+        a00 = oc_add(oc_cj(h00), oc_cj(h01));
+        a01 = oc_add(oc_cj(h10), oc_cj(h11));
+        a10 = oc_sub(oc_cj(h00), oc_cj(h01));
+        a11 = oc_sub(oc_cj(h10), oc_cj(h11));
+      } else {
+        a00 = oc_sub(oc_cj(h00), oc_mulj(oc_cj(h01)));
+        a01 = oc_sub(oc_cj(h10), oc_mulj(oc_cj(h11)));
+        a10 = oc_add(oc_cj(h00), oc_mulj(oc_cj(h01)));
+        a11 = oc_add(oc_cj(h10), oc_mulj(oc_cj(h11)));
+      }
+      const ocf b00 = oc_prod_add(a00, h00, oc_prod(a01, h10)), b01 = oc_prod_add(a00, h01, oc_prod(a01, h11));
+      const ocf b10 = oc_prod_add(a10, h00, oc_prod(a11, h10)), b11 = oc_prod_add(a10, h01, oc_prod(a11, h11));
+      if (cb == 0) {
+        c00 = oc_add(b00, b01);
+        c01 = oc_sub(b00, b01);
+        c10 = oc_add(b10, b11);
+        c11 = oc_sub(b10, b11);
+      } else {
+        c00 = oc_add(b00, oc_mulj(b01));
+        c01 = oc_sub(b00, oc_mulj(b01));
+        c10 = oc_add(b10, oc_mulj(b11));
+        c11 = oc_sub(b10, oc_mulj(b11));
+      }
+      c00 = (ocf){c00.r * 0.25f + noise, c00.i * 0.25f + 0.f};
+      c01 = (ocf){c01.r * 0.25f, c01.i * 0.25f};
+      c10 = (ocf){c10.r * 0.25f, c10.i * 0.25f};
+      c11 = (ocf){c11.r * 0.25f + noise, c11.i * 0.25f + 0.f};
+      const ocf det = oc_prod_sub(c00, c11, oc_prod(c01, c10));
+      const float rc = 1.0f / (det.i * det.i + det.r * det.r);
+      const ocf inv = {noise * (rc * det.r), 0.f * (rc * -det.i)};
+      const ocf den0 = oc_prod(c00, inv), den1 = oc_prod(c11, inv);
+      v[k] = (1.0f / den0.r - 1.f) + (1.0f / den1.r - 1.f);
+    }
+    s += v[0] + v[1] + v[2] + v[3];
+    count += 4;
+  }
+  return count ? s / (float)count : s;
+}
+
+static float orc_cn_2x2(const float *const h[2][2], uint32_t nof_ce) {
+  float acc = 0.f;
+  uint32_t count = 0;
+  for (uint32_t i = 0; i < nof_ce; i += ORC_PMI_PREC) {
+    const ocf h00 = oc_ld(h[0][0], i), h01 = oc_ld(h[1][0], i), h10 = oc_ld(h[0][1], i), h11 = oc_ld(h[1][1], i);
+    const float a00 = h00.r * h00.r + h01.r * h01.r + h00.i * h00.i + h01.i * h01.i;
+    const float a01r = (h00.r * h10.r - h00.i * -h10.i) + (h01.r * h11.r - h01.i * -h11.i);
+    const float a01i = (h00.r * -h10.i + h00.i * h10.r) + (h01.r * -h11.i + h01.i * h11.r);
+    const float a11 = h10.r * h10.r + h11.r * h11.r + h10.i * h10.i + h11.i * h11.i;
+    const float b = a00 + a11, c = a00 * a11 - (a01r * a01r + a01i * a01i);
+    const float sqr = sqrtf(b * b - 4.0f * c);
+    acc += 10 * log10f((b + sqr) / (b - sqr));
+    count++;
+  }
+  return count ? acc / (float)count : acc;
+}
+
+/* h[port][rx] estimate planes (complex float pairs; NULL = the zero plane of an absent rx antenna).
+ * out_i: ri_tm3, ret_cn, ri, pmi, pmi_l0, pmi_l1, ret_pmi; sinr[2][4] */
+int orc_feedback(const float *h00, const float *h01, const float *h10, const float *h11, uint32_t nof_ce, float noise,
+                 uint32_t flags, int nports, int nrx, float *out_cn, int32_t *out_i, float *sinr) {
+  const float *const h[2][2] = {{h00, h10}, {h01, h11}};
+  const int do_pmi = (flags & 2u) && nports == 2, do_cn = (flags & 1u) && nports == 2 && nrx == 2;
+  float cn = do_cn ? orc_cn_2x2(h, nof_ce) : 0.f;
+  for (int c = 0; c < 4; c++) {
+    sinr[c] = do_pmi ? orc_pmi_1l(h, nof_ce, noise, c) : 0.f;
+    sinr[4 + c] = !do_pmi ? 0.f : nrx < 2 ? -INFINITY : c < 2 ? orc_pmi_2l(h, nof_ce, noise, c) : 0.f;
+  }
+  uint32_t pmi_l[2] = {0, 0};
+  for (int L = 0; L < 2; L++) {
+    float mx = 0.f;
+    for (int c = 0; c < (L ? 2 : 4); c++)
+      if (sinr[4 * L + c] > mx) {
+        mx = sinr[4 * L + c];
+        pmi_l[L] = (uint32_t)c;
+      }
+  }
+  float best = -INFINITY;
+  uint32_t best_ri = 0, best_pmi = 0;
+  if (do_pmi)
+    for (uint32_t L = 1; L <= 4; L++) {
+      const float s = L <= 2 ? sinr[4 * (L - 1) + pmi_l[L - 1]] : -INFINITY;
+      const float v = s * L * L;
+      if (v > best + 0.1 || v > 1.0e+3) {
+        best = v;
+        best_pmi = L <= 2 ? pmi_l[L - 1] : 0;
+        best_ri = L - 1;
+      }
+    }
+  *out_cn = cn;
+  out_i[0] = do_cn ? (cn < 17.0f ? 1 : 0) : 0;
+  out_i[1] = do_cn ? 0 : -1;
+  out_i[2] = (int32_t)best_ri;
+  out_i[3] = (int32_t)best_pmi;
+  out_i[4] = (int32_t)pmi_l[0];
+  out_i[5] = (int32_t)pmi_l[1];
+  out_i[6] = do_pmi ? 0 : -1;
+  return 0;
+}

@@ -44,4 +44,6 @@ int orc_ulsch_uci(uint32_t tbs, uint32_t Qm, uint32_t nof_bits, uint32_t nsymb, 
 int orc_demod_b(int mod, const float *sym, int nsym, int8_t *llr);
 int orc_scramble_sb(uint32_t seed, int8_t *llr, uint32_t len);
 int orc_csi_correction_b(int mod, const float *csi, int nsym, int8_t *e);
+int orc_feedback(const float *h00, const float *h01, const float *h10, const float *h11, uint32_t nof_ce, float noise,
+                 uint32_t flags, int nports, int nrx, float *out_cn, int32_t *out_i, float *sinr);
 #endif

@@ -298,9 +298,17 @@ static int run_dci(void) {
  * correlation kept), the noise estimate, srslte_pdcch_extract_llr_multi, srslte_ue_dl_find_dl_dci,
  * srslte_dci_msg_to_dl_grant, the redundancy versions and softbuffer resets (:498-534), the MIMO type
  * of the format (:536-566), srslte_ue_dl_cfg_grant and srslte_pdsch_decode (:580-584).
- * IN: nof_prb id nof_ports nrx phich_len phich_res max_prb rnti tm nsf | nsf x { tti, grid[nrx][n] cf32 }
+ * After the decode, phch_worker's per-subframe reads of the estimator (srslte_chest_dl_get_*,
+ * phch_worker.cc:226-241, 301, 313, 1618-1628) and its TM3 / TM4 feedback (compute_ri, :522-540:
+ * srslte_ue_dl_ri_select with 2 ports and 2 rx antennas, srslte_ue_dl_ri_pmi_select with 2 ports;
+ * q->pmi is cleared before each subframe so that a subframe's PMI does not depend on the previous one).
+ * IN: nof_prb id nof_ports nrx phich_len phich_res max_prb rnti tm nsf | filt_mode(0 list, 1 gauss, 2 the
+ *     init default) flen filt[32] g_order g_std average noise_alg rsrp_neighbour cfo_enable cfo_mask |
+ *     nsf x { tti, grid[nrx][n] cf32 }
  * OUT per subframe: cfi corr(f32) noise(f32) | DL search (wr_msg) | ret(i32) tbs(i32) rv(i32) mod(i32)
- *     ack(i32) noi(i32) nof_re(i32) | data[12000] | ce[port][rx] grids cf32 */
+ *     ack(i32) noi(i32) nof_re(i32) | data[12000] | ce[port][rx] grids cf32 | getters: noise snr rssi rsrq
+ *     rsrp rsrp_neighbour cfo (f32) | feedback: cn(f32) ri_tm3 ret_cn ri pmi pmi_l[2] ret_pmi (i32)
+ *     sinr[2][4] (f32) */
 static int run_ue_dl(void) {
   srslte_cell_t cell;
   memset(&cell, 0, sizeof(cell));
@@ -314,6 +322,13 @@ static int run_ue_dl(void) {
   const uint32_t max_prb = rd_u32();
   const uint16_t rnti = (uint16_t)rd_u32();
   const uint32_t tm = rd_u32(), nsf = rd_u32();
+  const uint32_t filt_mode = rd_u32(), flen = rd_u32();
+  float filt[32];
+  for (int i = 0; i < 32; i++) filt[i] = rd_f32();
+  const uint32_t g_order = rd_u32();
+  const float g_std = rd_f32();
+  const uint32_t average = rd_u32(), noise_alg = rd_u32(), rsrp_nb = rd_u32(), cfo_en = rd_u32(),
+                 cfo_mask = rd_u32();
   if (!nrx || nrx > 2 || max_prb < cell.nof_prb) return -1;
 
   srslte_ue_dl_t *q = calloc(1, sizeof(srslte_ue_dl_t));
@@ -338,6 +353,14 @@ static int run_ue_dl(void) {
       srslte_pdsch_set_cell(&q->pdsch, cell))
     return -1;
   srslte_ue_dl_set_rnti(q, rnti);
+  if (filt_mode == 1)
+    srslte_chest_dl_set_smooth_filter_gauss(&q->chest, g_order, g_std);
+  else if (filt_mode == 0)
+    srslte_chest_dl_set_smooth_filter(&q->chest, flen ? filt : NULL, flen);
+  srslte_chest_dl_average_subframe(&q->chest, average != 0);
+  srslte_chest_dl_set_noise_alg(&q->chest, (srslte_chest_dl_noise_alg_t)noise_alg);
+  srslte_chest_dl_set_rsrp_neighbour(&q->chest, rsrp_nb != 0);
+  srslte_chest_dl_cfo_estimate_enable(&q->chest, cfo_en != 0, cfo_mask);
   uint8_t *data[SRSLTE_MAX_CODEWORDS] = {calloc(1, 100000), calloc(1, 100000)};
   for (uint32_t s = 0; s < nsf; s++) {
     const uint32_t tti = rd_u32(), sf_idx = tti % 10;
@@ -405,6 +428,32 @@ static int run_ue_dl(void) {
     wr(data[0], 12000);
     for (uint32_t p = 0; p < cell.nof_ports; p++)
       for (uint32_t a = 0; a < nrx; a++) wr(q->ce_m[p][a], sizeof(cf_t) * n);
+    wr_f32(srslte_chest_dl_get_noise_estimate(&q->chest));
+    wr_f32(srslte_chest_dl_get_snr(&q->chest));
+    wr_f32(srslte_chest_dl_get_rssi(&q->chest));
+    wr_f32(srslte_chest_dl_get_rsrq(&q->chest));
+    wr_f32(srslte_chest_dl_get_rsrp(&q->chest));
+    wr_f32(srslte_chest_dl_get_rsrp_neighbour(&q->chest));
+    wr_f32(srslte_chest_dl_get_cfo(&q->chest));
+    float cn = 0.f;
+    uint8_t ri3 = 0, ri4 = 0, pmi4 = 0;
+    int ret_cn = -1, ret_pmi = -1;
+    for (int l = 0; l < SRSLTE_MAX_LAYERS; l++) {
+      q->pmi[l] = 0;
+      for (int c = 0; c < SRSLTE_MAX_CODEBOOKS; c++) q->sinr[l][c] = 0.f;
+    }
+    if (cell.nof_ports == 2 && nrx == 2) ret_cn = srslte_ue_dl_ri_select(q, &ri3, &cn);
+    if (cell.nof_ports == 2) ret_pmi = srslte_ue_dl_ri_pmi_select(q, &ri4, &pmi4, NULL);
+    wr_f32(cn);
+    wr_i32(ri3);
+    wr_i32(ret_cn);
+    wr_i32(ri4);
+    wr_i32(pmi4);
+    wr_i32((int32_t)q->pmi[0]);
+    wr_i32((int32_t)q->pmi[1]);
+    wr_i32(ret_pmi);
+    for (int l = 0; l < 2; l++)
+      for (int c = 0; c < 4; c++) wr_f32(q->sinr[l][c]);
   }
   return 0;
 }

@@ -490,14 +490,27 @@ def ref_front_dci(nof_prb, cell_id, nports, nrx, phich_len, phich_res, subframes
     return out
 
 
-def ref_front_ue_dl(nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb, rnti, tm, ttis, grids):
+def ref_front_ue_dl(nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb, rnti, tm, ttis, grids,
+                    filt=None, gauss=None, average=False, noise_alg=0, rsrp_neighbour=False, cfo_enable=False,
+                    cfo_mask=0):
     """srslte_ue_dl_decode_rnti's steps after the FFT (ue_dl.c:467-620: chest, PCFICH, PDCCH, DL DCI search,
-    grant, PDSCH) of the reference on ONE ue_dl-shaped object over a subframe sequence; grids[i][a]
-    complex64 [14 * 12 nof_prb]. -> per subframe dict(cfi, corr, noise, dl=(found, format, L, ncce,
-    nof_bits, buf), ret, tbs, rv, mod, ack, noi, nre, data [12000] u8, ce [nports][nrx][n])"""
+    grant, PDSCH) of the reference on ONE ue_dl-shaped object over a subframe sequence, then the
+    estimator getters and the TM3 / TM4 feedback phch_worker reads; grids[i][a] complex64
+    [14 * 12 nof_prb]. Estimator settings as ref_front_chest (filt / gauss None: srslte_chest_dl_init's
+    default filter). -> per subframe dict(cfi, corr, noise, dl=(found, format, L, ncce, nof_bits, buf),
+    ret, tbs, rv, mod, ack, noi, nre, data [12000] u8, ce [nports][nrx][n], getters [noise, snr, rssi,
+    rsrq, rsrp, rsrp_neighbour, cfo], cn, ri_tm3, ret_cn, ri, pmi, pmi_l [2], ret_pmi, sinr [2][4])"""
     n = 14 * 12 * nof_prb
     pay = np.array([nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb, rnti, tm, len(ttis)],
                    np.uint32).tobytes()
+    f = np.zeros(32, np.float32)
+    if filt is not None:
+        f[:len(filt)] = filt
+    mode = 1 if gauss else 0 if filt is not None else 2
+    pay += np.array([mode, len(filt) if filt is not None else 0], np.uint32).tobytes() + f.tobytes()
+    pay += np.array([gauss[0] if gauss else 0], np.uint32).tobytes()
+    pay += np.array([gauss[1] if gauss else 0.0], np.float32).tobytes()
+    pay += np.array([int(average), noise_alg, int(rsrp_neighbour), int(cfo_enable), cfo_mask], np.uint32).tobytes()
     for i, t in enumerate(ttis):
         pay += np.array([t], np.uint32).tobytes()
         pay += b"".join(np.ascontiguousarray(grids[i][a], np.complex64).tobytes() for a in range(nrx))
@@ -517,10 +530,19 @@ def ref_front_ue_dl(nof_prb, cell_id, nports, nrx, phich_len, phich_res, max_prb
         o += 12000
         ce = np.frombuffer(raw, np.complex64, nports * nrx * n, o).reshape(nports, nrx, n).copy()
         o += 8 * nports * nrx * n
+        get = np.frombuffer(raw, np.float32, 7, o).copy()
+        o += 28
+        cn = float(np.frombuffer(raw, np.float32, 1, o)[0])
+        fb = np.frombuffer(raw, np.int32, 7, o + 4)
+        o += 32
+        sinr = np.frombuffer(raw, np.float32, 8, o).reshape(2, 4).copy()
+        o += 32
         out.append(dict(cfi=cfi, corr=float(corr), noise=float(noise),
                         dl=(int(v[0]), int(v[1]), int(v[2]), int(v[3]), int(v[4]), buf if v[0] > 0 else buf[:0]),
                         ret=int(r[0]), tbs=int(r[1]), rv=int(r[2]), mod=int(r[3]), ack=int(r[4]), noi=int(r[5]),
-                        nre=int(r[6]), data=data, ce=ce))
+                        nre=int(r[6]), data=data, ce=ce, getters=get, cn=cn, ri_tm3=int(fb[0]), ret_cn=int(fb[1]),
+                        ri=int(fb[2]), pmi=int(fb[3]), pmi_l=[int(fb[4]), int(fb[5])], ret_pmi=int(fb[6]),
+                        sinr=sinr))
     assert o == len(raw)
     return out
 

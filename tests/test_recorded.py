@@ -171,6 +171,7 @@ def test_gpu_pdsch_pdcch_file_test():
         assert u.ret == int(z["amar_ret"][i]), (i, u.ret)
         if found == 1:
             assert (u.format, u.L, u.ncce) == (fmt, L, ncce), i
+            assert u.dci_nof_bits == nbits and u.dci_bits() == list(z["amar_msg"][i][:nbits]), i
             assert int(u.grant.tbs[0]) == int(z["amar_tbs"][i]) and int(u.grant.mod[0]) == int(z["amar_mod"][i]), i
             assert int(u.acks[0]) == int(z["amar_ack"][i]) and u.rv[0] == int(z["amar_rv"][i]), i
             nb = int(z["amar_tbs"][i]) // 8
