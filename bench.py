@@ -471,6 +471,8 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
         dist.barrier()
     gc.disable()
     host = 0.0
+    for m in ms:
+        m.host_s = [0.0, 0.0]
     t0 = time.perf_counter()
     for _ in range(steps):
         th = time.perf_counter()
@@ -481,6 +483,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
         dist.barrier()
     el = time.perf_counter() - t0
     gc.enable()
+    host_split = [sum(m.host_s[i] for m in ms) for i in (0, 1)]
     stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
     ab = schedule_ab(s, torch, step, steps, schedules)
     chk = [m.check() for m in ms]
@@ -523,6 +526,8 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
            "result_bytes_per_rank": int(local.numel()), "schedule_ab": ab,
            "symbol_size": ms[0].cells[0]["N"], "early_stop": early_stop,
            "host_ms_per_step": round(host / steps * 1e3, 3), "descriptor_sets": rotate,
+           "host_ms_front_end": round(host_split[0] / steps * 1e3, 3),
+           "host_ms_dlsch": round(host_split[1] / steps * 1e3, 3),
            "kernels_per_batch": {k: {"ms": round(v[0], 4), "launches": v[1]} for k, v in ktab.items()},
            "data": "synthetic coded subframes (GPU transmitter, AWGN %s dB)" % snr}
     if cpu_sample:
@@ -1249,7 +1254,8 @@ def dist_check(dist, torch, rank, nranks):
 # keys of a leg's result reported in the compact summary line (one or two numbers per leg)
 LEG_SUMMARY = (
     ("c3_fixed8_codewords", "fixed8", ("subframes_per_s", "decoded_mbps", "ms_per_batch")),
-    ("c3_uncached", "uncached", ("subframes_per_s", "decoded_mbps", "host_ms_per_step")),
+    ("c3_uncached", "uncached", ("subframes_per_s", "decoded_mbps", "host_ms_per_step", "host_ms_front_end",
+                                 "host_ms_dlsch")),
     ("pipeline_tm3_coded", "tm3_coded", ("subframes_per_s", "decoded_mbps")),
     ("pipeline_c5", "c5", ("subframes_per_s", "decoded_mbps")),
     ("pipeline_coded", "coded30", ("subframes_per_s", "decoded_mbps")),

@@ -390,6 +390,18 @@ struct DlschEngine {
     std::vector<TdSpec> specs;
   } memo;
   std::vector<uint8_t> memo_scratch;
+  std::vector<uint32_t> cb_key, key_start;                // per code block of a call: its group key
+  std::vector<std::pair<uint32_t, uint32_t>> key_list;    // distinct keys, code blocks per key
+  // a decoder group's key, ordered as (K, poly, crc length): K < 2^13, the CRC polynomial 24B (0) or
+  // 24A (1), the CRC length K (24B) or tbs + 24 <= 6144 (24A, C = 1)
+  static uint32_t group_key(uint32_t K, uint32_t poly, uint32_t crclen) {
+    return (K << 14) | ((poly == 0x1864CFBu ? 1u : 0u) << 13) | crclen;
+  }
+  static void group_unkey(uint32_t key, uint32_t &K, uint32_t &poly, uint32_t &crclen) {
+    K = key >> 14;
+    poly = ((key >> 13) & 1u) ? 0x1864CFBu : 0x1800063u;
+    crclen = key & 0x1FFFu;
+  }
 
   void memo_key(std::vector<uint8_t> &k, const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const int16_t *const *e_ptr,
                 uint8_t *const *data_ptr, uint32_t maxh, const int32_t *d_ret, const uint32_t *d_noi_out) const {
@@ -421,12 +433,9 @@ struct DlschEngine {
     memo.valid = false;
     if (staged_pending) HIPCHK(hipEventSynchronize(staged));
     // ---- host: segmentation, CB list in TB order, groups by (K, CRC) ----
-    struct Cb {
-      uint32_t K, poly, crclen, u;
-    };
-    std::vector<Cb> cbs;
     uint32_t ncb = 0, max_n = 0;
     rec_tb.resize(cap);
+    cb_key.resize(cap);
     const int16_t *e_base = nullptr; // the records' LLR offsets are relative to the lowest TB pointer
     for (uint32_t b = 0; b < ntb; b++)
       if (e_ptr[b] && (!e_base || e_ptr[b] < e_base)) e_base = e_ptr[b];
@@ -478,46 +487,78 @@ struct DlschEngine {
       const uint32_t Gp = t.nof_e_bits / t.Qm;
       const uint32_t gamma = Gp % s.C;
       const uint32_t n_e = t.Qm * (Gp / s.C);
+      // per distinct block size of the TB (K1, K2): de-RM table, row length, loader kind, group key
+      struct PerK {
+        uint32_t K, nsb;
+        int tab;
+        bool direct;
+        uint32_t key;
+      } pk[2];
+      for (int w = 0; w < 2; w++) {
+        const uint32_t K = w == 0 ? s.K1 : (s.C2 ? s.K2 : s.K1);
+        PerK &q = pk[w];
+        q.K = K;
+        q.nsb = llr8 ? auto_subblocks_8bit(K) : auto_subblocks(K);
+        q.tab = tab_of(K, t.rv, q.nsb);
+        if (q.tab < 0) return -1;
+        // the loader the decoder job will pick for this block (TdecEngine::derm_direct)
+        const int r = resolve_impl(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, K);
+        q.direct = direct_derm && sb_input_for(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, r) && impl_nb(r) % 8 == 0;
+        q.key = group_key(K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24);
+      }
+      const ptrdiff_t eo0 = e_ptr[b] - e_base;
+      if (eo0 < 0 || eo0 + (ptrdiff_t)t.nof_e_bits > (ptrdiff_t)UINT32_MAX) {
+        fprintf(stderr, "srsgpu: the LLRs of a call must lie within 2^32 elements of each other\n");
+        return -1;
+      }
       for (uint32_t i = 0; i < s.C; i++, ncb++) {
-        const uint32_t K = i < s.C1 ? s.K1 : s.K2;
+        const PerK &q = pk[i < s.C1 ? 0 : 1];
+        const uint32_t K = q.K;
         uint32_t rp = i * n_e, ne = n_e;
         if (i > s.C - gamma) { // sch.c:339-342
           ne = n_e + t.Qm;
           rp = (s.C - gamma) * n_e + (i - (s.C - gamma)) * ne;
         }
-        const uint32_t nsb = llr8 ? auto_subblocks_8bit(K) : auto_subblocks(K);
-        const int tab = tab_of(K, t.rv, nsb);
-        if (tab < 0) return -1;
-        const ptrdiff_t eo = (e_ptr[b] + rp) - e_base;
-        if (eo < 0 || eo > (ptrdiff_t)UINT32_MAX) {
-          fprintf(stderr, "srsgpu: the LLRs of a call must lie within 2^32 elements of each other\n");
-          return -1;
-        }
         DermRec &it = rec_tb[ncb];
-        it.e_off = (uint32_t)eo;
+        it.e_off = (uint32_t)(eo0 + rp);
         it.ne = ne;
         it.N = (uint16_t)(3 * K + 12);
-        it.tab = (uint16_t)tab;
+        it.tab = (uint16_t)q.tab;
         it.row = t.softbuffer * max_cb + i;
-        it.rowlen = (uint16_t)(nsb ? 3 * (K + 32) + 12 : 3 * K + 12);
+        it.rowlen = (uint16_t)(q.nsb ? 3 * (K + 32) + 12 : 3 * K + 12);
         it.w8 = llr8;
         it.tb = b;
-        {
-          // the loader the decoder job will pick for this block (TdecEngine::derm_direct)
-          const int r = resolve_impl(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, K);
-          it.direct = direct_derm && sb_input_for(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, r) &&
-                      impl_nb(r) % 8 == 0;
-        }
+        it.direct = q.direct;
         max_n = std::max(max_n, std::min(ne, 3 * K + 12));
-        cbs.push_back({K, s.C > 1 ? 0x1800063u : 0x1864CFBu, s.C > 1 ? K : s.tbs + 24, ncb});
+        cb_key[ncb] = q.key;
       }
     }
-    std::vector<uint32_t> order(cbs.size());
-    for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-      return std::tie(cbs[a].K, cbs[a].poly, cbs[a].crclen) <
-             std::tie(cbs[b].K, cbs[b].poly, cbs[b].crclen);
-    });
+    // code blocks grouped by (K, CRC) in key order, stable within a group (a counting sort: a call
+    // holds thousands of blocks and a handful of keys)
+    std::vector<uint32_t> order(ncb);
+    {
+      key_list.clear();
+      for (uint32_t u = 0; u < ncb; u++) {
+        const uint32_t k = cb_key[u];
+        if (key_list.empty() || key_list.back().first != k) {
+          auto f = std::find_if(key_list.begin(), key_list.end(), [&](const std::pair<uint32_t, uint32_t> &e) { return e.first == k; });
+          if (f == key_list.end()) {
+            key_list.push_back({k, 1});
+            continue;
+          }
+          std::iter_swap(f, key_list.end() - 1); // the list's order does not matter until sorted below
+        }
+        key_list.back().second++;
+      }
+      std::sort(key_list.begin(), key_list.end());
+      std::vector<uint32_t> &start = key_start;
+      start.assign(key_list.size(), 0);
+      for (size_t g = 1; g < key_list.size(); g++) start[g] = start[g - 1] + key_list[g - 1].second;
+      for (uint32_t u = 0; u < ncb; u++) {
+        const size_t g = std::lower_bound(key_list.begin(), key_list.end(), std::make_pair(cb_key[u], 0u)) - key_list.begin();
+        order[start[g]++] = u;
+      }
+    }
     // records in decoder order (k_load_derm reads them by decoder position), packed with the row
     // pointers, the CB map and the TBs into one block: one upload
     const size_t o_rows = al(sizeof(DermRec) * ncb), o_map = o_rows + al(sizeof(int16_t *) * ncb),
@@ -528,7 +569,7 @@ struct DlschEngine {
     uint32_t ndirect = 0;
     tdec.derm_max_ne = 0;
     for (uint32_t p = 0; p < order.size(); p++) {
-      const uint32_t u = cbs[order[p]].u;
+      const uint32_t u = order[p];
       b_map[u] = p;
       b_rec[p] = rec_tb[u];
       b_rec[p].pos = p;
@@ -545,14 +586,11 @@ struct DlschEngine {
     staged_pending = true;
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;
-    for (uint32_t p0 = 0; p0 < order.size();) {
-      const Cb &c = cbs[order[p0]];
-      uint32_t p1 = p0 + 1;
-      while (p1 < order.size() && cbs[order[p1]].K == c.K && cbs[order[p1]].poly == c.poly &&
-             cbs[order[p1]].crclen == c.crclen)
-        p1++;
-      specs.push_back(TdSpec{c.K, p1 - p0, c.poly, c.crclen, p0});
-      p0 = p1;
+    for (uint32_t g = 0, p0 = 0; g < key_list.size(); g++) {
+      uint32_t K, poly, crclen;
+      group_unkey(key_list[g].first, K, poly, crclen);
+      specs.push_back(TdSpec{K, key_list[g].second, poly, crclen, p0});
+      p0 += key_list[g].second;
     }
     const int r = launch_decode(ncb, ndirect, (uint32_t)order.size(), o_rows, o_map, o_tbs, e_base, specs, ntb, maxh,
                                 d_ret, tdec.derm_max_ne);

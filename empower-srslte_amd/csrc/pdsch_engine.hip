@@ -199,8 +199,27 @@ struct PdschEngine {
   }
 
   // device RE map of a grant, cached; returns its RE count
+  // the previous lookup's key: consecutive subframes of a call mostly share their allocation class
+  uint8_t last_prb[2 * 110];
+  uint32_t last_cls = ~0u, last_lstart = ~0u, last_nre = 0;
+  const uint32_t *last_map = nullptr;
   const uint32_t *map(const srsgpu_pdsch_sf_t &s, uint32_t *nre) {
     const uint32_t cls = s.sf_idx == 0 ? 0 : s.sf_idx == 5 ? 5 : 1;
+    if (last_map && cls == last_cls && s.lstart == last_lstart && !memcmp(last_prb, s.prb_idx, sizeof(last_prb))) {
+      *nre = last_nre;
+      return last_map;
+    }
+    const uint32_t *m = map_lookup(s, cls, nre);
+    if (m) {
+      memcpy(last_prb, s.prb_idx, sizeof(last_prb));
+      last_cls = cls;
+      last_lstart = s.lstart;
+      last_nre = *nre;
+      last_map = m;
+    }
+    return m;
+  }
+  const uint32_t *map_lookup(const srsgpu_pdsch_sf_t &s, uint32_t cls, uint32_t *nre) {
     std::string key((const char *)s.prb_idx, 2 * 110);
     key += (char)cls;
     key += (char)s.lstart;

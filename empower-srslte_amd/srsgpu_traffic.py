@@ -17,6 +17,7 @@ Reference flow per subframe: srslte_ofdm_rx_sf -> srslte_chest_dl_estimate -> sr
 (lib/src/phy/ue/ue_dl.c:379-433,580).
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -84,6 +85,7 @@ class MixedCells:
         keep = set(range(n_sf)) if keep is None else set(int(k) for k in keep)
         self.kept = sorted(keep)
         self.rotate, self.cur = max(1, int(rotate)), 0
+        self.host_s = [0.0, 0.0]
         self.cells = []
         self.sf_total = len(self.kept)
         e_off = d_off = 0
@@ -187,9 +189,15 @@ class MixedCells:
                                      self.d_noi.data_ptr()) == 0
 
     def step(self):
+        """one receive batch; host_s accumulates the host (enqueue) seconds of the front end and of the
+        DL-SCH call"""
         self.cur = (self.cur + 1) % self.rotate
+        t0 = time.perf_counter()
         self.front_end()
+        t1 = time.perf_counter()
         self.decode()
+        self.host_s[0] += t1 - t0
+        self.host_s[1] += time.perf_counter() - t1
 
     def check(self):
         """(acked TBs, TBs whose bytes equal the transmitted ones, mean nof_iterations)"""
