@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "chest_kernels.h"
+#include "host_ring.h"
 #include "srsgpu/chest_batch.h"
 #include "tdec_engine.h"
 
@@ -58,9 +59,8 @@ struct ChestEngine {
   float filt[64] = {0.1f, 1 - 2 * 0.1f, 0.1f};
   bool filt_dirty = true;
   bool ce_rows = false; // srsgpu_chest_set_ce_rows
-  ChestItem *h_items = nullptr, *d_items = nullptr;
-  hipEvent_t staged = nullptr;
-  bool staged_pending = false;
+  ChestItem *d_items = nullptr;
+  HostRing ring; // pinned item staging (host_ring.h)
 
   int create(const srsgpu_cell_t &c, uint32_t n) {
     if (c.nof_prb < 6 || c.nof_prb > 110 || c.id > 503 || !n || (c.nof_ports != 1 && c.nof_ports != 2 && c.nof_ports != 4) ||
@@ -90,9 +90,8 @@ struct ChestEngine {
     HIPCHK(hipMemcpy(d_pss, pss, sizeof(pss), hipMemcpyHostToDevice));
     cfg.symbol_sz = c.nof_prb <= 6 ? 128 : c.nof_prb <= 15 ? 256 : c.nof_prb <= 25 ? 384
                   : c.nof_prb <= 50 ? 768 : c.nof_prb <= 75 ? 1024 : 1536;
-    HIPCHK(hipHostMalloc(&h_items, sizeof(ChestItem) * n));
+    HIPCHK(ring.create(sizeof(ChestItem) * n));
     HIPCHK(hipMalloc(&d_items, sizeof(ChestItem) * n));
-    HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
     return 0;
   }
 
@@ -100,8 +99,7 @@ struct ChestEngine {
     if (st) (void)hipStreamSynchronize(st);
     for (void *p : {(void *)d_crs, (void *)d_pss, (void *)d_filt, (void *)d_items})
       if (p) (void)hipFree(p);
-    if (h_items) (void)hipHostFree(h_items);
-    if (staged) (void)hipEventDestroy(staged);
+    ring.destroy();
   }
 
   int estimate(const uint32_t *sf_idx, uint32_t n, const float *d_grid, size_t stride, float *d_ce,
@@ -115,7 +113,9 @@ struct ChestEngine {
       fprintf(stderr, "srsgpu: compact estimate rows need a 1- or 2-port cell, and average_subframe with extended CP\n");
       return -1;
     }
-    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    hipError_t re;
+    ChestItem *h_items = (ChestItem *)ring.acquire(&re);
+    HIPCHK(re);
     if (filt_dirty) {
       HIPCHK(hipMemcpy(d_filt, filt, sizeof(filt), hipMemcpyHostToDevice));
       filt_dirty = false;
@@ -136,8 +136,7 @@ struct ChestEngine {
       }
     }
     HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(staged, st));
-    staged_pending = true;
+    HIPCHK(ring.mark(st));
     // chest_dl.c:620-621: no smoothing for an empty filter or a 3-tap one with w == 0
     ChestCfg kc;
     kc.nprb = (int)cell.nof_prb;
@@ -162,7 +161,9 @@ struct ChestEngine {
       fprintf(stderr, "srsgpu: %u grids exceed the capacity %u\n", n, cap);
       return -1;
     }
-    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    hipError_t re;
+    ChestItem *h_items = (ChestItem *)ring.acquire(&re);
+    HIPCHK(re);
     const uint32_t np = cell.nof_ports;
     for (uint32_t i = 0; i < n; i++) {
       if (sf_idx[i] > 9) return -1;
@@ -178,8 +179,7 @@ struct ChestEngine {
       }
     }
     HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(staged, st));
-    staged_pending = true;
+    HIPCHK(ring.mark(st));
     HIPCHK(launch_crs_put(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, cell.cp == 1 ? 6 : 7, d_crs, st));
     return 0;
   }

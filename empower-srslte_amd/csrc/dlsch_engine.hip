@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "dlsch_kernels.h"
+#include "host_ring.h"
 #include "srsgpu/dlsch_batch.h"
 #include "srsgpu/uci_tables.h"
 #include "srsgpu/ulsch_batch.h"
@@ -133,7 +134,8 @@ struct DlschEngine {
   uint32_t *h_cbmap = nullptr;
   // a decode call's descriptors packed into one block (records, row pointers, CB map, TBs), one
   // upload per call
-  uint8_t *h_blk = nullptr, *d_blk = nullptr;
+  uint8_t *h_blk = nullptr, *d_blk = nullptr; // h_blk: the current slot of blk_ring
+  HostRing blk_ring;                           // pinned staging of the blocks (host_ring.h)
   std::vector<DermRec> rec_tb; // records in TB order while the call is planned
   // table sets per (K, rv, layout): index into d_tabs (device, append-only)
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t> tab_index;
@@ -186,7 +188,7 @@ struct DlschEngine {
     HIPCHK(hipMalloc(&d_ret_stage, sizeof(int32_t) * cap));
     HIPCHK(hipMalloc(&d_noi_stage, sizeof(uint32_t) * cap));
     HIPCHK(hipHostMalloc(&h_items, sizeof(DermItem) * cap));
-    HIPCHK(hipHostMalloc(&h_blk, blk_bytes(cap, cap)));
+    HIPCHK(blk_ring.create(blk_bytes(cap, cap)));
     HIPCHK(hipMalloc(&d_blk, blk_bytes(cap, cap)));
     HIPCHK(hipMalloc(&d_tabs, sizeof(DermTabs) * TABS_CAP));
     HIPCHK(hipHostMalloc(&h_tbs, sizeof(TbItem) * cap));
@@ -216,8 +218,9 @@ struct DlschEngine {
                     (void *)d_noi, (void *)d_late, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
                     (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul, (void *)d_uci_ret})
       if (p) (void)hipFree(p);
+    blk_ring.destroy();
     for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
-                    (void *)h_ul, (void *)h_blk})
+                    (void *)h_ul})
       if (p) (void)hipHostFree(p);
     for (void *p : {(void *)d_blk, (void *)d_tabs})
       if (p) (void)hipFree(p);
@@ -431,7 +434,11 @@ struct DlschEngine {
       return launch_decode(memo.ncb, memo.ndirect, memo.norder, memo.o_rows, memo.o_map, memo.o_tbs, memo.e_base,
                            memo.specs, ntb, maxh, d_ret, memo.derm_max_ne);
     memo.valid = false;
-    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    {
+      hipError_t re;
+      h_blk = (uint8_t *)blk_ring.acquire(&re);
+      HIPCHK(re);
+    }
     // ---- host: segmentation, CB list in TB order, groups by (K, CRC) ----
     uint32_t ncb = 0, max_n = 0;
     rec_tb.resize(cap);
@@ -582,8 +589,7 @@ struct DlschEngine {
     memcpy(h_blk + o_tbs, h_tbs, sizeof(TbItem) * ntb);
     // ---- device ----
     HIPCHK(hipMemcpyAsync(d_blk, h_blk, o_end, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(staged, st));
-    staged_pending = true;
+    HIPCHK(blk_ring.mark(st));
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;
     for (uint32_t g = 0, p0 = 0; g < key_list.size(); g++) {

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "feedback_kernels.h"
+#include "host_ring.h"
 #include "pdsch_kernels.h"
 #include "srsgpu/pdsch_batch.h"
 #include "tdec_engine.h"
@@ -124,8 +125,19 @@ struct PdschEngine {
     for (uint32_t i = 0; i < ngold; i++) m = std::max(m, h_gold[i].len);
     return m;
   }
-  hipEvent_t staged = nullptr;
-  bool staged_pending = false;
+  // pinned per-call staging, one ring slot = [GoldItem x 2 max_sf][LlrItem x 2 max_sf][TxItem x max_sf];
+  // h_gold / h_llr / h_tx point into the slot of the current call (host_ring.h)
+  HostRing ring;
+  int ring_take() {
+    hipError_t e;
+    uint8_t *b = (uint8_t *)ring.acquire(&e);
+    if (e != hipSuccess) return -1;
+    const uint32_t mtb = 2 * max_sf;
+    h_gold = (GoldItem *)b;
+    h_llr = (LlrItem *)(b + sizeof(GoldItem) * mtb);
+    h_tx = (TxItem *)(b + (sizeof(GoldItem) + sizeof(LlrItem)) * mtb);
+    return 0;
+  }
   // TM3 / TM4 feedback items (lazily allocated; the host array is reused once its upload is done)
   FbItem *h_fb = nullptr, *d_fb = nullptr;
   hipEvent_t fb_staged = nullptr;
@@ -169,8 +181,7 @@ struct PdschEngine {
     HIPCHK(hipMemcpy(d_x1, x1w.data(), x1w.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_x2b, x2w.data(), x2w.size() * 4, hipMemcpyHostToDevice));
     const uint32_t mtb = 2 * msf; // up to 2 TBs per subframe (CDD)
-    HIPCHK(hipHostMalloc(&h_gold, sizeof(GoldItem) * mtb));
-    HIPCHK(hipHostMalloc(&h_llr, sizeof(LlrItem) * mtb));
+    HIPCHK(ring.create((sizeof(GoldItem) + sizeof(LlrItem)) * mtb + sizeof(TxItem) * max_sf));
     HIPCHK(hipHostMalloc(&h_tb, sizeof(srsgpu_dlsch_tb_t) * mtb));
     HIPCHK(hipMalloc(&d_gold, sizeof(GoldItem) * mtb));
     HIPCHK(hipMalloc(&d_llr, sizeof(LlrItem) * mtb));
@@ -178,7 +189,6 @@ struct PdschEngine {
     HIPCHK(hipMalloc(&d_csi, (size_t)mtb * max_re * 4));
     HIPCHK(hipMalloc(&d_csimax, (size_t)mtb * 4));
     HIPCHK(hipMalloc(&d_e, (size_t)mtb * max_bits * 2));
-    HIPCHK(hipEventCreateWithFlags(&staged, hipEventDisableTiming));
     return 0;
   }
 
@@ -188,12 +198,12 @@ struct PdschEngine {
                     (void *)d_csi, (void *)d_csimax, (void *)d_e, (void *)d_tx, (void *)d_ebits,
                     (void *)d_mod, (void *)d_fb})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_gold, (void *)h_llr, (void *)h_tb, (void *)h_tx, (void *)h_fb})
+    ring.destroy();
+    for (void *p : {(void *)h_tb, (void *)h_fb})
       if (p) (void)hipHostFree(p);
     if (fb_staged) (void)hipEventDestroy(fb_staged);
     for (auto &kv : maps) (void)hipFree(kv.second.first);
     maps.clear();
-    if (staged) (void)hipEventDestroy(staged);
     if (dl) srsgpu_dlsch_destroy(dl);
     dl = nullptr;
   }
@@ -329,7 +339,7 @@ struct PdschEngine {
       }
       memo_valid = false;
     }
-    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    if (ring_take()) return -1;
     uint32_t mre = 0, k = 0;
     int n_dual = 0;
     gold_slot.clear();
@@ -395,8 +405,7 @@ struct PdschEngine {
     }
     HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * k, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(staged, st));
-    staged_pending = true;
+    HIPCHK(ring.mark(st));
     if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)k * 4, st));
     {
       ProfScope ps("k_gold", st);
@@ -422,8 +431,7 @@ struct PdschEngine {
       fprintf(stderr, "srsgpu: %u subframes exceed the capacity %u\n", n, max_sf);
       return -1;
     }
-    if (!h_tx) {
-      HIPCHK(hipHostMalloc(&h_tx, sizeof(TxItem) * max_sf));
+    if (!d_tx) {
       HIPCHK(hipMalloc(&d_tx, sizeof(TxItem) * max_sf));
       HIPCHK(hipMalloc(&d_ebits, (size_t)2 * max_sf * max_bits + 64));
       // modem/lte_tables.c: levels k / sqrt(N) in double, stored as float; 36.211 7.1 bit order
@@ -446,7 +454,7 @@ struct PdschEngine {
       HIPCHK(hipMalloc(&d_mod, t.size() * sizeof(float2)));
       HIPCHK(hipMemcpy(d_mod, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
     }
-    if (staged_pending) HIPCHK(hipEventSynchronize(staged));
+    if (ring_take()) return -1;
     memo_valid = false; // the sequences and items below overwrite the ones llr() keeps
     uint32_t mre = 0, k = 0;
     gold_slot.clear();
@@ -512,8 +520,7 @@ struct PdschEngine {
     if (srsgpu_dlsch_encode_dev(dl, h_tb, k, d_data, d_ebits)) return -1;
     HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(staged, st));
-    staged_pending = true;
+    HIPCHK(ring.mark(st));
     HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
     ProfScope ps("k_pdsch_tx", st);
     HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));
