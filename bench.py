@@ -222,6 +222,18 @@ KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", 
            "k_sse_es", "k_es_bytes", "k_win_bidir_run", "k_win_bidir", "k_decide", "k_tb_finish")
 
 
+_LANE_STREAMS = {}
+
+
+def lane_stream(torch, dev, li):
+    """lane li's HIP stream, created once and shared by every leg: each leg then runs on the same
+    streams (and so the same hardware queues) as the headline. Fresh streams per leg land on other
+    hardware queues of the process (4 on the box), and two lanes on one queue run one after the other."""
+    if li not in _LANE_STREAMS:
+        _LANE_STREAMS[li] = torch.cuda.Stream(dev)
+    return _LANE_STREAMS[li]
+
+
 def stage_profile(s, torch, step, steps, kernels=None):
     """Per-stage device time per batch, from HIP events around every launch (srsgpu_prof_*), in
     a separate pass after the timed loop: creating and recording the events costs host time that
@@ -322,7 +334,7 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedul
     mimo = s.MIMO_CDD if tm == 3 else s.MIMO_SINGLE_ANTENNA
     L = []
     for li in range(lanes):
-        st = torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)
+        st = lane_stream(torch, dev, li) if lanes > 1 else torch.cuda.current_stream(dev)
         o = {"st": st, "x": d_x[li * ngrid * 15 * N:(li + 1) * ngrid * 15 * N]}
         o["ofdm"] = s.OfdmRx(C3_PRB, N, stream=st.cuda_stream)
         o["chest"] = s.Chest(C3_PRB, C3_CELL, max_grids=ngrid, stream=st.cuda_stream, nof_ports=nports)
@@ -456,7 +468,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     mine = [i for i in range(n_global) if owner[i] == rank]
     ms = []
     for li in range(lanes):
-        st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
+        st = (lane_stream(torch, dev, li) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
         ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
                                 keep=mine[li::lanes], standard_rate=standard_rate, early_stop=early_stop,
                                 rotate=rotate, **kw))  # one plan: the same seed everywhere
@@ -559,7 +571,7 @@ def run_tm3_coded(s, torch, dev, steps, warmup, snr_db=30.0, lanes=2, dist=None)
     mine = list(range(int(f[rank]), int(f[rank + 1])))
     ms = []
     for li in range(lanes):
-        st = (torch.cuda.Stream(dev) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
+        st = (lane_stream(torch, dev, li) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
         ms.append(tr.MimoSubframes(torch, dev, n_global, seed=5, stream=st, snr_db=snr_db, keep=mine[li::lanes]))
     torch.cuda.synchronize()
 
@@ -1076,7 +1088,7 @@ def decoder_leg(s, torch, dev, args, dist, rank, nranks):
     d_out = torch.zeros((NCB, K // 8), dtype=torch.uint8, device=dev)
     # a dedicated stream: launches on the null stream carry HIP's implicit cross-stream
     # synchronisation and cost ~6 % of the step here
-    stream = torch.cuda.Stream(dev)
+    stream = lane_stream(torch, dev, 0)
     batch = s.TdecBatch(NCB, K, stream=stream.cuda_stream)
     stride = 3 * K + 12
 
