@@ -764,7 +764,9 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             lat = (t_done - t_sub) * 1e3
             acked = sum(1 for it in items[-min(nsf, 4 * B):] if it.ret[0] == 0)
             zc, st = q.ingest_stats()
+            tmg = q.timing()
             out["saturated"]["%s_b%d" % (mode, B)] = {
+                "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
                 "subframes_per_s": round(nsf / el, 1),
                 "ingest_GBps": round(nsf * sf_bytes["sc16" if mode.endswith("sc16") else "cf32"] / el / 1e9, 2),
                 "latency_ms_p50": round(float(np.percentile(lat, 50)), 3),
@@ -786,11 +788,13 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         assert all(q.wait(t) == 0 for t in warm)
         lat, status, acked, late = q.drive_paced(items, ns, depth, ticks, 1000, workers=min(8, ns))
         nb, done = q.stats()
+        tmg = q.timing()
         p99 = float(np.percentile(lat, 99))
         rec = {"latency_ms_p50": round(float(np.percentile(lat, 50)), 3), "latency_ms_p99": round(p99, 3),
                "latency_ms_max": round(float(lat.max()), 3), "acked": "%d/%d" % (acked, ns * ticks),
                "failed": int((status != 0).sum()), "mean_batch": round(done / max(nb, 1), 1),
                "producer_late_ms_max": round(late, 3), "subframes_per_s": round(ns * 1000.0, 1),
+               "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
                "ingest_GBps": round(ns * 1000.0 * sf_bytes["sc16"] / 1e9, 2)}
         out["paced"][str(ns)] = rec
         q.close()

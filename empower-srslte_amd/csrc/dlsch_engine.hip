@@ -219,6 +219,8 @@ struct DlschEngine {
                     (void *)data_stage, (void *)d_enc, (void *)d_crc_a, (void *)d_ul, (void *)d_uci_ret})
       if (p) (void)hipFree(p);
     blk_ring.destroy();
+    list_ring.destroy();
+    if (d_list) (void)hipFree(d_list);
     for (void *p : {(void *)h_items, (void *)h_tbs, (void *)h_rows, (void *)h_cbmap, (void *)h_enc,
                     (void *)h_ul})
       if (p) (void)hipHostFree(p);
@@ -373,6 +375,33 @@ struct DlschEngine {
 
   // srslte_softbuffer_rx_reset(_cb): cb_crc cleared now; the soft bits are zeroed lazily (the
   // next de-rate-matching pass treats a fresh softbuffer's rows as zero and rewrites them whole)
+  // srsgpu_dlsch_softbuffer_reset_list: one upload (ring-staged) and one launch for n softbuffers
+  HostRing list_ring;
+  uint32_t *d_list = nullptr;
+  static constexpr uint32_t LIST_CAP = 4096;
+  int reset_list(const uint32_t *slots, const uint32_t *ncb, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+      if (slots[i] >= nslots) return -1;
+    if (!d_list) {
+      HIPCHK(list_ring.create(sizeof(uint32_t) * 2 * LIST_CAP));
+      HIPCHK(hipMalloc(&d_list, sizeof(uint32_t) * 2 * LIST_CAP));
+    }
+    for (uint32_t i0 = 0; i0 < n; i0 += LIST_CAP) {
+      const uint32_t m = std::min(LIST_CAP, n - i0);
+      hipError_t re;
+      uint32_t *h = (uint32_t *)list_ring.acquire(&re);
+      HIPCHK(re);
+      for (uint32_t i = 0; i < m; i++) {
+        h[2 * i] = slots[i0 + i];
+        h[2 * i + 1] = ncb ? std::min(ncb[i0 + i], max_cb) : max_cb;
+      }
+      HIPCHK(hipMemcpyAsync(d_list, h, sizeof(uint32_t) * 2 * m, hipMemcpyHostToDevice, st));
+      HIPCHK(list_ring.mark(st));
+      HIPCHK(launch_sb_reset_list(fresh, cbcrc, d_list, m, max_cb, st));
+    }
+    return 0;
+  }
+
   int reset(uint32_t slot, uint32_t count, uint32_t ncb) {
     if (slot + count > nslots) return -1;
     // one launch: fresh = 1 for the first ncb rows of each slot (reset_tbs), cb_crc = 0 for all
@@ -691,6 +720,11 @@ int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t slot) {
 
 int srsgpu_dlsch_softbuffer_reset_range(srsgpu_dlsch_t *q, uint32_t first, uint32_t count) {
   return q ? q->e.reset(first, count, q->e.max_cb) : -1;
+}
+
+int srsgpu_dlsch_softbuffer_reset_list(srsgpu_dlsch_t *q, const uint32_t *slots, const uint32_t *ncb, uint32_t n) {
+  if (!q || (!slots && n)) return -1;
+  return q->e.reset_list(slots, ncb, n);
 }
 
 int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t slot, uint32_t tbs) {

@@ -88,6 +88,8 @@ hipError_t launch_derm_flags(const DermCall &c, int nitems, uint8_t *init_done, 
 hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st);
 // softbuffer reset of count slots of max_cb rows from fresh / cbcrc: cb_crc = 0, the first ncb
 // rows of each slot fresh
+hipError_t launch_sb_reset_list(uint8_t *fresh, uint8_t *cbcrc, const uint32_t *d_list, uint32_t n, uint32_t max_cb,
+                                hipStream_t st);
 hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint32_t max_cb, uint32_t ncb,
                            hipStream_t st);
 // dec / cb_ok / init_done / noi are in decoder order; cbmap[first + i] is CB i's position there

@@ -670,6 +670,25 @@ hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint3
   return hipGetLastError();
 }
 
+// many softbuffers at once: list[2 k] = slot, list[2 k + 1] = rows of it marked fresh (reset_tbs' count)
+__global__ __launch_bounds__(256) void k_sb_reset_list(uint8_t *__restrict__ fresh, uint8_t *__restrict__ cbcrc,
+                                                       const uint32_t *__restrict__ list, uint32_t n, uint32_t max_cb) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * max_cb) return;
+  const uint32_t k = i / max_cb, c = i - k * max_cb;
+  const size_t r = (size_t)list[2 * k] * max_cb + c;
+  cbcrc[r] = 0;
+  if (c < list[2 * k + 1]) fresh[r] = 1;
+}
+
+hipError_t launch_sb_reset_list(uint8_t *fresh, uint8_t *cbcrc, const uint32_t *d_list, uint32_t n, uint32_t max_cb,
+                                hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sb_reset_list, dim3(cdiv((size_t)n * max_cb, 256)), dim3(256), 0, st, fresh, cbcrc, d_list, n,
+                     max_cb);
+  return hipGetLastError();
+}
+
 hipError_t launch_derm(const DermCall &c, int nitems, uint8_t *init_done, hipStream_t st) {
   if (nitems <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_derm, dim3((unsigned)nitems), dim3(256), 0, st, c, nitems, init_done);

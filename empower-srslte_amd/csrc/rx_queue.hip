@@ -279,15 +279,22 @@ struct srsgpu_rxq {
   std::set<uint64_t> failed;               // tickets whose batch failed, until waited for
   bool stop = false, flush = false;
   uint64_t nbatches = 0, nsf = 0;
+  uint32_t nsb = 0; // softbuffers of the caller
+  // dispatcher time per stage, seconds (srsgpu_rxq_timing): 0 front end enqueue (OFDM, chest,
+  // getters), 1 control channel (PCFICH / PDCCH round trips), 2 grants and softbuffer resets, 3 PDSCH /
+  // DL-SCH enqueue, 4 waiting for the batch's results, 5 result copy-out, 6 staging (closer thread)
+  double tm[8] = {};
+  std::vector<uint32_t> rs_slot, rs_ncb; // the batch's softbuffer resets, one launch
   std::thread closer, worker;
 
-  int setup(const srsgpu_cell_t *c, uint32_t symbol_sz, uint32_t nsb, uint32_t mb, uint32_t wait_us,
+  int setup(const srsgpu_cell_t *c, uint32_t symbol_sz, uint32_t nsb_in, uint32_t mb, uint32_t wait_us,
             uint32_t maxh) {
     cell = *c;
     N = symbol_sz;
     max_batch = mb;
     max_wait_us = wait_us;
     max_halfits = maxh;
+    nsb = nsb_in;
     nports = cell.nof_ports;
     nrx = cell.nof_rx_ant;
     td_len = (size_t)15 * N;
@@ -306,7 +313,7 @@ struct srsgpu_rxq {
     RXQ_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     RXQ_CHK(hipStreamCreateWithFlags(&cst, hipStreamNonBlocking));
     if (srsgpu_ofdm_rx_create(&ofdm, cell.nof_prb, N) || srsgpu_chest_create(&chest, &cell, mb * nrx) ||
-        srsgpu_pdsch_create(&pdsch, &cell, nsb, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
+        srsgpu_pdsch_create(&pdsch, &cell, nsb_in, max_cb, mb) || srsgpu_pcfich_create(&pcfich, &cell))
       return -1;
     srsgpu_ofdm_rx_set_stream(ofdm, st);
     if (srsgpu_ofdm_set_cp(ofdm, cell.cp)) return -1;
@@ -499,8 +506,11 @@ struct srsgpu_rxq {
       if (stop) return;
       const size_t n = slot[s].items.size();
       l.unlock();
+      const double ts = now_s();
       const bool ok = stage(slot[s], n);
+      const double te = now_s();
       l.lock();
+      tm[6] += te - ts;
       if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed\n");
       slot[s].state = STAGED;
       ready.push_back(ok ? s : -1 - s);
@@ -528,6 +538,7 @@ struct srsgpu_rxq {
         (void)hipStreamSynchronize(cst);
       }
       l.lock();
+      for (int k = 0; k < 6; k++) tm[k] += run_tm[k];
       if (r) {
         fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", b.size());
         for (const Pending &p : b) failed.insert(p.ticket);
@@ -627,7 +638,9 @@ struct srsgpu_rxq {
       } else {
         rv[i] = (uint32_t)(i == 0 ? dci.rv_idx : dci.rv_idx_1);
       }
-      if (srsgpu_dlsch_softbuffer_reset_tbs(dl, u->softbuffer[i], (uint32_t)g.tbs[i])) return -1;
+      if (u->softbuffer[i] >= nsb) return -1; // srsgpu_dlsch_softbuffer_reset_tbs's check
+      rs_slot.push_back(u->softbuffer[i]); // reset_tbs: (tbs + 24) / 6120 + 1 blocks (softbuffer.c:113-116)
+      rs_ncb.push_back(((uint32_t)g.tbs[i] + 24) / 6120 + 1);
     }
     u->rv[0] = rv[0];
     u->rv[1] = rv[1];
@@ -686,8 +699,21 @@ struct srsgpu_rxq {
 
   // one batch: OFDM of the staged samples, channel estimation, the ue_dl items' control channel and
   // grants, the PDSCH / DL-SCH of every subframe with a grant, one copy of the results back
+  static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  double run_tm[8] = {}; // this batch's stage times, added to tm under the lock by run_loop
   int run(std::vector<Pending> &b, const float *d_td) {
     const uint32_t n = (uint32_t)b.size();
+    for (double &v : run_tm) v = 0;
+    double t0 = now_s(), t1;
+    auto lap = [&](int k) {
+      t1 = now_s();
+      run_tm[k] += t1 - t0;
+      t0 = t1;
+    };
+    rs_slot.clear();
+    rs_ncb.clear();
     if (srsgpu_ofdm_rx_sf_dev(ofdm, n * nrx, d_td, td_len, d_grid, gsz)) return -1;
     std::vector<uint32_t> sfi(n * nrx);
     for (uint32_t i = 0; i < n; i++)
@@ -730,7 +756,9 @@ struct srsgpu_rxq {
     for (uint32_t i = 0; i < n; i++)
       if (b[i].ue) ue.push_back(i);
     fb_any = false;
+    lap(0);
     if (!ue.empty() && control(b, ue)) return -1;
+    lap(1);
     if (fb_any)
       RXQ_CHK(hipMemcpyAsync(h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
     // grants: the grant items' own, the ue_dl items' from their DCI
@@ -778,7 +806,11 @@ struct srsgpu_rxq {
         s = b[i].it->sf;
         const uint32_t ntb = sf_ntb(s);
         for (uint32_t t = 0; t < ntb; t++)
-          if (b[i].it->reset_softbuffer[t] && srsgpu_dlsch_softbuffer_reset(dl, s.softbuffer[t])) return -1;
+          if (b[i].it->reset_softbuffer[t]) {
+            if (s.softbuffer[t] >= nsb) return -1;
+            rs_slot.push_back(s.softbuffer[t]);
+            rs_ncb.push_back(UINT32_MAX); // srslte_softbuffer_rx_reset: every block
+          }
       }
       const uint32_t k = (uint32_t)sfs.size();
       s.grid_offset = (uint64_t)i * nrx * gsz;
@@ -791,6 +823,9 @@ struct srsgpu_rxq {
     const uint32_t np = (uint32_t)sfs.size();
     uint32_t ntbs = 0;
     for (uint32_t k = 0; k < np; k++) ntbs += sf_ntb(sfs[k]);
+    if (!rs_slot.empty() && srsgpu_dlsch_softbuffer_reset_list(dl, rs_slot.data(), rs_ncb.data(), (uint32_t)rs_slot.size()))
+      return -1;
+    lap(2);
     if (np) {
       srsgpu_pdsch_set_noise_dev(pdsch, d_noise);
       // the PDSCH's per-subframe noise comes from d_noise at the subframe's position in the call:
@@ -812,7 +847,9 @@ struct srsgpu_rxq {
       RXQ_CHK(hipMemcpyAsync(h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
     }
     RXQ_CHK(hipMemcpyAsync(h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
+    lap(3);
     RXQ_CHK(hipStreamSynchronize(st));
+    lap(4);
     for (uint32_t k = 0, t0 = 0; k < np; k++) {
       const Pending &p = b[who[k]];
       const uint32_t ntb = sf_ntb(sfs[k]);
@@ -858,6 +895,7 @@ struct srsgpu_rxq {
         jf++;
       }
     }
+    lap(5);
     return 0;
   }
 };
@@ -987,6 +1025,12 @@ void srsgpu_rxq_ingest_stats(srsgpu_rxq_t *q, uint64_t *zero_copy_rows, uint64_t
   std::lock_guard<std::mutex> l(q->m);
   if (zero_copy_rows) *zero_copy_rows = q->zero_copy_rows;
   if (staged_rows) *staged_rows = q->staged_rows;
+}
+
+void srsgpu_rxq_timing(srsgpu_rxq_t *q, double *sec, uint32_t n) {
+  if (!q || !sec) return;
+  std::lock_guard<std::mutex> l(q->m);
+  for (uint32_t i = 0; i < n && i < 8; i++) sec[i] = q->tm[i];
 }
 
 struct srsgpu_chest *srsgpu_rxq_get_chest(srsgpu_rxq_t *q) { return q ? q->chest : nullptr; }

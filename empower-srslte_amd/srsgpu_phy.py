@@ -384,6 +384,8 @@ _sig = {
     "srsgpu_rxq_decode": (_i32, [_vp, _vp]),
     "srsgpu_rxq_flush": (None, [_vp]),
     "srsgpu_rxq_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "srsgpu_rxq_timing": (None, [_vp, ctypes.POINTER(ctypes.c_double), _u32]),
+    "srsgpu_dlsch_softbuffer_reset_list": (_i32, [_vp, _u32p, _u32p, _u32]),
     "srsgpu_tdec_set_schedule": (ctypes.c_int, [ctypes.c_int] * 4),
     "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 4),
     "srsgpu_rxq_drive": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
@@ -1253,6 +1255,13 @@ class RxQueue:
 
     def flush(self):
         _lib.srsgpu_rxq_flush(self.q)
+
+    def timing(self):
+        """srsgpu_rxq_timing: seconds per dispatcher stage so far"""
+        v = (ctypes.c_double * 8)()
+        _lib.srsgpu_rxq_timing(self.q, v, 8)
+        names = ("front_end", "control", "grants", "pdsch_enqueue", "gpu_wait", "copy_out", "staging")
+        return {k: v[i] for i, k in enumerate(names)}
 
     def drive(self, items, workers, reuse=0):
         """srsgpu_rxq_drive: native worker threads submit items (in index order per worker) while a

@@ -58,6 +58,10 @@ int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t softbuffer);
 int srsgpu_dlsch_softbuffer_reset_range(srsgpu_dlsch_t *q, uint32_t first, uint32_t count);
 /* srslte_softbuffer_rx_reset_tbs: only the first (tbs+24)/6120+1 code blocks. */
 int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t softbuffer, uint32_t tbs);
+/* Many softbuffers in one launch: softbuffer slots[i] as srsgpu_dlsch_softbuffer_reset_tbs with its
+ * first ncb[i] code blocks (NULL ncb: all, srslte_softbuffer_rx_reset). -1 on a slot out of range
+ * (nothing reset). */
+int srsgpu_dlsch_softbuffer_reset_list(srsgpu_dlsch_t *q, const uint32_t *slots, const uint32_t *ncb, uint32_t n);
 
 /* Device pointers, asynchronous on the handle's stream. d_ret[i]: 0 TB decoded and CRC OK,
  * -1 CRC error, -2 invalid inputs (filler bits, too many CBs) — sch.c's return values.

@@ -153,6 +153,11 @@ void srsgpu_rxq_flush(srsgpu_rxq_t *q);
 struct srsgpu_chest;
 struct srsgpu_chest *srsgpu_rxq_get_chest(srsgpu_rxq_t *q);
 srsgpu_pdsch_t *srsgpu_rxq_get_pdsch(srsgpu_rxq_t *q);
+/* Seconds the queue's threads spent so far per stage (n <= 8 values): 0 front end enqueue (OFDM, channel
+ * estimation, measurements), 1 control channel (PCFICH / PDCCH / DCI search round trips), 2 grants and
+ * softbuffer resets, 3 PDSCH / DL-SCH enqueue, 4 waiting for the batch's results on the GPU, 5 result
+ * copy-out into the items, 6 staging of the samples (closer thread). */
+void srsgpu_rxq_timing(srsgpu_rxq_t *q, double *sec, uint32_t n);
 /* batches run and subframes decoded so far */
 void srsgpu_rxq_stats(srsgpu_rxq_t *q, uint64_t *batches, uint64_t *subframes);
 /* Load generator for the queue (no reference counterpart; it stands in for srsUE's pool of PHY
