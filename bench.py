@@ -734,7 +734,12 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
            "producers": producers, "saturated": {}, "paced": {}}
 
     def make_items(q, count, nsb, src):
-        outs = [np.zeros(C3_TBS // 8 + 6, np.uint8) for _ in range(nsb)]
+        """outputs in one registered block (srsgpu_rxq_register): the decoder writes the TB bytes into
+        them over PCIe, with no copy-back through the queue"""
+        dl = (C3_TBS // 8 + 6 + 63) // 64 * 64
+        block = np.zeros((nsb, dl), np.uint8)
+        q.register(block)
+        outs = [block[k, :C3_TBS // 8 + 6] for k in range(nsb)]
         items = []
         for i in range(count):
             j = i % n_src

@@ -747,6 +747,18 @@ int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
   return q->e.decode(tb, ntb, e.data(), d.data(), maxh, d_ret, d_noi);
 }
 
+int srsgpu_dlsch_decode_out_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const int16_t *d_e,
+                                uint8_t *const *d_out, uint32_t maxh, int32_t *d_ret, uint32_t *d_noi) {
+  if (!q || (!tb && ntb) || !d_e || (!d_out && ntb) || !d_ret || !d_noi) return -1;
+  if (ntb == 0) return 0;
+  std::vector<const int16_t *> e(ntb);
+  for (uint32_t i = 0; i < ntb; i++) {
+    if (!d_out[i]) return -1;
+    e[i] = d_e + tb[i].e_offset;
+  }
+  return q->e.decode(tb, ntb, e.data(), d_out, maxh, d_ret, d_noi);
+}
+
 // srslte_ulsch_decode (sch.c:883-889 -> srslte_ulsch_uci_decode :944-985 without UCI): the channel
 // deinterleaver of every TB (ulsch_deinterleave, :860-881) into the caller's g bits, then decode_tb
 // on them through the DL-SCH path (the reference's decode_tb is the same function for both links)

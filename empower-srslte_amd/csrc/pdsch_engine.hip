@@ -669,10 +669,28 @@ int srsgpu_pdsch_feedback_dev(srsgpu_pdsch_t *q, const srsgpu_feedback_sf_t *sf,
   return q->e.feedback(sf, n, d_ce, ant_stride, d_noise, d_out);
 }
 
+static int pdsch_decode(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
+                        const float *d_ce, size_t ant_stride, uint8_t *d_data, uint8_t *const *d_out, uint32_t maxh,
+                        int32_t *d_ret, uint32_t *d_noi);
+
 int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
                             const float *d_ce, size_t ant_stride, uint8_t *d_data, uint32_t maxh,
                             int32_t *d_ret, uint32_t *d_noi) {
-  if (!q || (!sf && n) || !d_grid || !d_ce || !d_data || !d_ret || !d_noi) return -1;
+  if (!d_data) return -1;
+  return pdsch_decode(q, sf, n, d_grid, d_ce, ant_stride, d_data, nullptr, maxh, d_ret, d_noi);
+}
+
+int srsgpu_pdsch_decode_out_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
+                                const float *d_ce, size_t ant_stride, uint8_t *const *d_out, uint32_t maxh,
+                                int32_t *d_ret, uint32_t *d_noi) {
+  if (!d_out) return -1;
+  return pdsch_decode(q, sf, n, d_grid, d_ce, ant_stride, nullptr, d_out, maxh, d_ret, d_noi);
+}
+
+static int pdsch_decode(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
+                        const float *d_ce, size_t ant_stride, uint8_t *d_data, uint8_t *const *d_out, uint32_t maxh,
+                        int32_t *d_ret, uint32_t *d_noi) {
+  if (!q || (!sf && n) || !d_grid || !d_ce || !d_ret || !d_noi) return -1;
   PdschEngine &E = q->e;
   const uint32_t k = E.count_tb(sf, n);
   std::vector<int16_t *> e(k);
@@ -691,6 +709,7 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
       t.e_offset = (uint64_t)j * E.max_bits;
       t.data_offset = sf[i].data_offset[tb];
     }
+  if (d_out) return srsgpu_dlsch_decode_out_dev(E.dl, E.h_tb, k, E.d_e, d_out, maxh, d_ret, d_noi);
   return srsgpu_dlsch_decode_dev(E.dl, E.h_tb, k, E.d_e, d_data, maxh, d_ret, d_noi);
 }
 

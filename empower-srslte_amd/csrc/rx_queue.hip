@@ -207,27 +207,24 @@ struct srsgpu_rxq {
   srsgpu_pdsch_t *pdsch = nullptr;
   srsgpu_pcfich_t *pcfich = nullptr;
   srsgpu_pdcch_t *pdcch = nullptr; // created with the PHICH configuration on the first ue_dl batch
+  // device working buffers: one batch's kernels use them after the previous batch's, in stream order
   float *d_grid = nullptr, *d_ce = nullptr, *d_noise = nullptr;
   float *d_noise_last = nullptr; // PSS / EMPTY: the estimate carried between batches
   float *d_meas = nullptr;       // [subframe][rx][port] {rsrp, rssi, rsrp_corr, cfo}
   float *d_meas_last = nullptr;  // [rx][port] x 4: q->cfo / q->rsrp_corr carried between batches
-  int32_t *d_cfo_src = nullptr, *h_cfo_src = nullptr;
-  float *d_getters = nullptr, *h_getters = nullptr; // [subframe] x 6 (srsgpu_rxq_meas_t)
-  srsgpu_feedback_t *d_fb = nullptr, *h_fb = nullptr; // the ue_dl items' TM3 / TM4 feedback
+  int32_t *d_cfo_src = nullptr;
+  float *d_getters = nullptr;    // [subframe] x 6 (srsgpu_rxq_meas_t)
+  srsgpu_feedback_t *d_fb = nullptr; // the ue_dl items' TM3 / TM4 feedback
   std::vector<srsgpu_feedback_sf_t> fb_sf;
-  uint8_t *d_est = nullptr, *h_est = nullptr; // per subframe: 1 if it estimates the noise
-  uint8_t *d_data = nullptr;
+  uint8_t *d_est = nullptr;      // per subframe: 1 if it estimates the noise
+  uint8_t *d_data = nullptr;     // TB bytes of outputs the device cannot address (then copied back)
   int32_t *d_ret = nullptr;
   uint32_t *d_noi = nullptr;
-  float *h_noise = nullptr; // pinned result staging
-  uint8_t *h_data = nullptr;
-  int32_t *h_ret = nullptr;
-  uint32_t *h_noi = nullptr;
-  // control channel of the ue_dl items
-  uint32_t *d_sel = nullptr, *h_sel = nullptr; // their subframe indices in the batch
-  float *d_uenoise = nullptr;                  // their noise estimates
-  uint32_t *d_who = nullptr, *h_who = nullptr; // subframes of the PDSCH call
-  float *d_pnoise = nullptr;                   // their noise rows
+  // control channel of the ue_dl items (consumed by the dispatcher within the batch)
+  uint32_t *d_sel = nullptr;   // their subframe indices in the batch
+  float *d_uenoise = nullptr;  // their noise estimates
+  uint32_t *d_who = nullptr;   // subframes of the PDSCH call
+  float *d_pnoise = nullptr;   // their noise rows
   uint32_t *d_cfi = nullptr, *h_cfi = nullptr;
   float *d_corr = nullptr, *h_corr = nullptr;
   float *d_llr = nullptr;
@@ -235,8 +232,13 @@ struct srsgpu_rxq {
   srsgpu_dci_result_t *d_res = nullptr, *h_res = nullptr;
   srsgpu_dci_result_t *d_res_ul = nullptr, *h_res_ul = nullptr;
 
-  // staging slots
-  enum { FILLING = 0, CLOSED = 1, STAGED = 2 };
+  // Batch slots. A slot takes submissions (FILLING), is closed and its samples staged (CLOSED ->
+  // STAGED, closer thread), dispatched (RUNNING: the dispatcher enqueues the whole batch on the GPU
+  // and moves on to the next slot) and completed (the completer waits for the batch's results and
+  // writes them into the items) before it takes submissions again. Three slots: one filling, one on
+  // the GPU, one completing; the GPU gets the next batch while the host finishes the last.
+  enum { FILLING = 0, CLOSED = 1, STAGED = 2, RUNNING = 3 };
+  static constexpr int NSLOT = 3;
   struct Slot {
     float *h_td = nullptr, *d_td = nullptr; // pinned staging (raw format) / device samples (cf32)
     float *d_raw = nullptr;                  // SC16: the staged raw samples before conversion
@@ -248,7 +250,28 @@ struct srsgpu_rxq {
     uint32_t nstaged = 0; // items whose samples went through the staging buffer
     int sc16 = 0;          // the input format of this slot's items (set with its first item)
     float sc16_scale = 1.0f / 32768.0f;
-  } slot[2];
+    // the batch's pinned host inputs of H2D copies and its results (per slot: the next batch is
+    // prepared while this one's copies may still be in flight)
+    uint8_t *h_est = nullptr;
+    int32_t *h_cfo_src = nullptr;
+    uint32_t *h_sel = nullptr, *h_who = nullptr;
+    float *h_noise = nullptr, *h_getters = nullptr;
+    int32_t *h_ret = nullptr;
+    uint32_t *h_noi = nullptr;
+    uint8_t *h_data = nullptr;
+    srsgpu_feedback_t *h_fb = nullptr;
+    hipEvent_t done = nullptr;
+    // what the completer needs: the PDSCH subframes (batch index, TB count, TB sizes), each TB's
+    // staging offset in h_data (-1: written by the device into the caller's registered buffer), the
+    // ue_dl items' states
+    int r = 0;
+    bool fb_any = false;
+    std::vector<uint32_t> who, ntb_of;
+    std::vector<uint32_t> tbs_of;   // per TB of the call
+    std::vector<int64_t> stage_off; // per TB of the call
+    std::vector<int> ue_state;      // per item: ue_dl 1 decoded, 0 no PDSCH call, -1 error
+    size_t staged_bytes = 0;
+  } slot[NSLOT];
   // input format (srsgpu_rxq_set_input_format) and caller memory the GPU reads directly
   int sc16 = 0; // guarded by m; a change waits until nothing is queued and holds new submissions
   float sc16_scale = 1.0f / 32768.0f;
@@ -259,33 +282,35 @@ struct srsgpu_rxq {
     const char *d; // device view of the same memory
   };
   std::vector<Region> regions; // guarded by m
-  uint64_t zero_copy_rows = 0, staged_rows = 0;
-  // device view of a registered host pointer holding `bytes`, or null (caller holds m)
-  const void *device_view(const void *p, size_t bytes) const {
+  uint64_t zero_copy_rows = 0, staged_rows = 0, zero_copy_tbs = 0, staged_tbs = 0;
+  // device view of a registered host pointer holding `bytes`, or null (caller holds m); aligned16: the
+  // ingest kernel reads 16 B vectors (else the samples are staged)
+  const void *device_view(const void *p, size_t bytes, bool aligned16 = true) const {
     const char *c = (const char *)p;
     for (const Region &r : regions)
       if (c >= r.h && c + bytes <= r.h + r.bytes) {
         const char *d = r.d + (c - r.h);
-        return ((uintptr_t)d & 15) ? nullptr : d; // the ingest kernel reads 16 B vectors: else staged
+        return (aligned16 && ((uintptr_t)d & 15)) ? nullptr : d;
       }
     return nullptr;
   }
   int fill = 0; // the slot submissions go to
 
   std::mutex m;
-  std::condition_variable cv_close, cv_ready, cv_done, cv_slot;
-  std::deque<int> ready; // staged slots, in batch order
+  std::condition_variable cv_close, cv_ready, cv_done, cv_slot, cv_comp;
+  std::deque<int> ready;      // staged slots, in batch order
+  std::deque<int> completing; // dispatched slots, in batch order
   uint64_t next_ticket = 1, done_upto = 0; // tickets are completed in order
   std::set<uint64_t> failed;               // tickets whose batch failed, until waited for
-  bool stop = false, flush = false;
+  bool stop = false, flush = false, comp_stop = false;
   uint64_t nbatches = 0, nsf = 0;
   uint32_t nsb = 0; // softbuffers of the caller
-  // dispatcher time per stage, seconds (srsgpu_rxq_timing): 0 front end enqueue (OFDM, chest,
-  // getters), 1 control channel (PCFICH / PDCCH round trips), 2 grants and softbuffer resets, 3 PDSCH /
-  // DL-SCH enqueue, 4 waiting for the batch's results, 5 result copy-out, 6 staging (closer thread)
+  // time per stage, seconds (srsgpu_rxq_timing): 0 front end enqueue (OFDM, chest, getters), 1 control
+  // channel (PCFICH / PDCCH round trips), 2 grants and softbuffer resets, 3 PDSCH / DL-SCH enqueue, 4 the
+  // completer waiting for a batch's results, 5 result copy-out, 6 staging (closer thread)
   double tm[8] = {};
   std::vector<uint32_t> rs_slot, rs_ncb; // the batch's softbuffer resets, one launch
-  std::thread closer, worker;
+  std::thread closer, worker, completer;
 
   int setup(const srsgpu_cell_t *c, uint32_t symbol_sz, uint32_t nsb_in, uint32_t mb, uint32_t wait_us,
             uint32_t maxh) {
@@ -326,6 +351,17 @@ struct srsgpu_rxq {
       RXQ_CHK(hipHostMalloc(&s.h_src, sizeof(void *) * mb * nrx));
       RXQ_CHK(hipMalloc(&s.d_src, sizeof(void *) * mb * nrx));
       RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
+      RXQ_CHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+      RXQ_CHK(hipHostMalloc(&s.h_est, mb));
+      RXQ_CHK(hipHostMalloc(&s.h_cfo_src, sizeof(int32_t) * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_sel, sizeof(uint32_t) * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_who, sizeof(uint32_t) * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_noise, sizeof(float) * mb * nrx * nports));
+      RXQ_CHK(hipHostMalloc(&s.h_getters, sizeof(float) * 6 * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_ret, sizeof(int32_t) * 2 * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_noi, sizeof(uint32_t) * 2 * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_data, dlen * 2 * mb));
+      RXQ_CHK(hipHostMalloc(&s.h_fb, sizeof(srsgpu_feedback_t) * mb));
     }
     RXQ_CHK(hipMalloc(&d_grid, sizeof(float) * 2 * gsz * mb * nrx));
     RXQ_CHK(hipMalloc(&d_ce, sizeof(float) * 2 * gsz * mb * nrx * nports));
@@ -339,22 +375,12 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMalloc(&d_meas_last, sizeof(float) * 4 * nrx * nports));
     RXQ_CHK(hipMemset(d_meas_last, 0, sizeof(float) * 4 * nrx * nports)); // bzero'd estimator
     RXQ_CHK(hipMalloc(&d_cfo_src, sizeof(int32_t) * mb));
-    RXQ_CHK(hipHostMalloc(&h_cfo_src, sizeof(int32_t) * mb));
     RXQ_CHK(hipMalloc(&d_getters, sizeof(float) * 6 * mb));
-    RXQ_CHK(hipHostMalloc(&h_getters, sizeof(float) * 6 * mb));
     RXQ_CHK(hipMalloc(&d_fb, sizeof(srsgpu_feedback_t) * mb));
-    RXQ_CHK(hipHostMalloc(&h_fb, sizeof(srsgpu_feedback_t) * mb));
     RXQ_CHK(hipMalloc(&d_est, mb));
-    RXQ_CHK(hipHostMalloc(&h_est, mb));
-    RXQ_CHK(hipHostMalloc(&h_noise, sizeof(float) * mb * nrx * nports));
-    RXQ_CHK(hipHostMalloc(&h_data, dlen * 2 * mb));
-    RXQ_CHK(hipHostMalloc(&h_ret, sizeof(int32_t) * 2 * mb));
-    RXQ_CHK(hipHostMalloc(&h_noi, sizeof(uint32_t) * 2 * mb));
     RXQ_CHK(hipMalloc(&d_sel, sizeof(uint32_t) * mb));
-    RXQ_CHK(hipHostMalloc(&h_sel, sizeof(uint32_t) * mb));
     RXQ_CHK(hipMalloc(&d_uenoise, sizeof(float) * mb));
     RXQ_CHK(hipMalloc(&d_who, sizeof(uint32_t) * mb));
-    RXQ_CHK(hipHostMalloc(&h_who, sizeof(uint32_t) * mb));
     RXQ_CHK(hipMalloc(&d_pnoise, sizeof(float) * mb * nrx * nports));
     RXQ_CHK(hipMalloc(&d_cfi, sizeof(uint32_t) * mb));
     RXQ_CHK(hipHostMalloc(&h_cfi, sizeof(uint32_t) * mb));
@@ -368,6 +394,7 @@ struct srsgpu_rxq {
     srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
     closer = std::thread([this] { close_loop(); });
     worker = std::thread([this] { run_loop(); });
+    completer = std::thread([this] { comp_loop(); });
     return 0;
   }
 
@@ -381,18 +408,28 @@ struct srsgpu_rxq {
     cv_slot.notify_all();
     if (closer.joinable()) closer.join();
     if (worker.joinable()) worker.join();
+    {
+      std::lock_guard<std::mutex> l(m);
+      comp_stop = true; // the dispatcher is gone: the completer finishes what it was handed, then leaves
+    }
+    cv_comp.notify_all();
+    if (completer.joinable()) completer.join();
+    if (st) (void)hipStreamSynchronize(st);
+    if (cst) (void)hipStreamSynchronize(cst);
     if (ofdm) srsgpu_ofdm_rx_destroy(ofdm);
     if (chest) srsgpu_chest_destroy(chest);
     if (pdsch) srsgpu_pdsch_destroy(pdsch);
     if (pcfich) srsgpu_pcfich_destroy(pcfich);
     if (pdcch) srsgpu_pdcch_destroy(pdcch);
     for (Slot &s : slot) {
-      if (s.d_td) (void)hipFree(s.d_td);
-      if (s.d_raw) (void)hipFree(s.d_raw);
-      if (s.h_td) (void)hipHostFree(s.h_td);
-      if (s.h_src) (void)hipHostFree(s.h_src);
-      if (s.d_src) (void)hipFree(s.d_src);
+      for (void *p : {(void *)s.d_td, (void *)s.d_raw, (void *)s.d_src})
+        if (p) (void)hipFree(p);
+      for (void *p : {(void *)s.h_td, (void *)s.h_src, (void *)s.h_est, (void *)s.h_cfo_src, (void *)s.h_sel,
+                      (void *)s.h_who, (void *)s.h_noise, (void *)s.h_getters, (void *)s.h_ret, (void *)s.h_noi,
+                      (void *)s.h_data, (void *)s.h_fb})
+        if (p) (void)hipHostFree(p);
       if (s.staged) (void)hipEventDestroy(s.staged);
+      if (s.done) (void)hipEventDestroy(s.done);
     }
     for (const Region &r : regions) (void)hipHostUnregister((void *)r.h);
     regions.clear();
@@ -402,9 +439,7 @@ struct srsgpu_rxq {
                     (void *)d_pnoise, (void *)d_res_ul, (void *)d_meas, (void *)d_meas_last, (void *)d_cfo_src,
                     (void *)d_getters, (void *)d_fb})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)h_noise, (void *)h_data, (void *)h_ret, (void *)h_noi, (void *)h_est,
-                    (void *)h_sel, (void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_who,
-                    (void *)h_res_ul, (void *)h_cfo_src, (void *)h_getters, (void *)h_fb})
+    for (void *p : {(void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_res_ul})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
@@ -484,8 +519,8 @@ struct srsgpu_rxq {
     return hipEventRecord(sl.staged, cst) == hipSuccess;
   }
 
-  // closer thread: close the filling slot, switch the workers to the other one once it is free,
-  // wait for the closed slot's copies, start its transfer and hand it to the dispatcher
+  // closer thread: close the filling slot, switch the workers to the next one once it is free, wait
+  // for the closed slot's copies, start its transfer and hand it to the dispatcher
   void close_loop() {
     std::unique_lock<std::mutex> l(m);
     for (;;) {
@@ -497,10 +532,11 @@ struct srsgpu_rxq {
       if (stop) return;
       flush = false;
       slot[s].state = CLOSED;
-      // the other slot takes submissions once its batch has been decoded
-      cv_slot.wait(l, [&] { return stop || slot[s ^ 1].state == FILLING; });
+      // the next slot takes submissions once its batch has been completed
+      const int nx = (s + 1) % NSLOT;
+      cv_slot.wait(l, [&] { return stop || slot[nx].state == FILLING; });
       if (stop) return;
-      fill = s ^ 1;
+      fill = nx;
       cv_slot.notify_all();
       cv_close.wait(l, [&] { return stop || slot[s].copying == 0; });
       if (stop) return;
@@ -518,7 +554,8 @@ struct srsgpu_rxq {
     }
   }
 
-  // dispatcher thread: decode the staged batches in order
+  // dispatcher thread: enqueue the staged batches in order, each on the GPU as a whole, and hand them
+  // to the completer
   void run_loop() {
     std::unique_lock<std::mutex> l(m);
     for (;;) {
@@ -527,27 +564,58 @@ struct srsgpu_rxq {
       const int tag = ready.front();
       ready.pop_front();
       const int s = tag < 0 ? -1 - tag : tag;
-      std::vector<Pending> b = slot[s].items;
+      Slot &sl = slot[s];
+      sl.state = RUNNING;
+      std::vector<Pending> b = sl.items;
       l.unlock();
       int r = tag < 0 ? -1 : 0;
-      if (!r) r = hipStreamWaitEvent(st, slot[s].staged, 0) == hipSuccess ? 0 : -1;
-      if (!r) r = run(b, slot[s].d_td);
+      if (!r) r = hipStreamWaitEvent(st, sl.staged, 0) == hipSuccess ? 0 : -1;
+      if (!r) r = enqueue(sl, b, sl.d_td);
+      if (!r) r = hipEventRecord(sl.done, st) == hipSuccess ? 0 : -1;
       // a failed batch may have left work in flight that reads its buffers: drain before reuse
       if (r) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamSynchronize(cst);
       }
+      sl.r = r;
       l.lock();
-      for (int k = 0; k < 6; k++) tm[k] += run_tm[k];
-      if (r) {
-        fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", b.size());
-        for (const Pending &p : b) failed.insert(p.ticket);
+      for (int k = 0; k < 4; k++) tm[k] += run_tm[k];
+      completing.push_back(s);
+      cv_comp.notify_one();
+    }
+  }
+
+  // completer thread: wait for each dispatched batch's results, write them into its items, free the slot
+  void comp_loop() {
+    std::unique_lock<std::mutex> l(m);
+    for (;;) {
+      cv_comp.wait(l, [this] { return comp_stop || !completing.empty(); });
+      if (completing.empty()) return;
+      const int s = completing.front();
+      completing.pop_front();
+      Slot &sl = slot[s];
+      l.unlock();
+      double w = 0, c = 0;
+      if (!sl.r) {
+        const double t0 = now_s();
+        if (hipEventSynchronize(sl.done) != hipSuccess) sl.r = -1;
+        const double t1 = now_s();
+        if (!sl.r) complete(sl);
+        w = t1 - t0;
+        c = now_s() - t1;
       }
-      done_upto = b.back().ticket;
+      l.lock();
+      tm[4] += w;
+      tm[5] += c;
+      if (sl.r) {
+        fprintf(stderr, "srsgpu rxq: batch of %zu subframes failed\n", sl.items.size());
+        for (const Pending &p : sl.items) failed.insert(p.ticket);
+      }
+      done_upto = sl.items.back().ticket;
       nbatches++;
-      nsf += b.size();
-      slot[s].items.clear();
-      slot[s].state = FILLING;
+      nsf += sl.items.size();
+      sl.items.clear();
+      sl.state = FILLING;
       cv_done.notify_all();
       cv_slot.notify_all();
     }
@@ -557,10 +625,10 @@ struct srsgpu_rxq {
   // the control channel of the batch's ue_dl items (ue_dl.c:408-433, :484-497): PCFICH on their
   // grids with the estimator's noise, CFI back to the host, PDCCH LLRs and the DL DCI search,
   // results back to the host
-  int control(const std::vector<Pending> &b, const std::vector<uint32_t> &ue) {
+  int control(Slot &sl, const std::vector<Pending> &b, const std::vector<uint32_t> &ue) {
     const uint32_t nu = (uint32_t)ue.size();
-    for (uint32_t j = 0; j < nu; j++) h_sel[j] = ue[j];
-    RXQ_CHK(hipMemcpyAsync(d_sel, h_sel, sizeof(uint32_t) * nu, hipMemcpyHostToDevice, st));
+    for (uint32_t j = 0; j < nu; j++) sl.h_sel[j] = ue[j];
+    RXQ_CHK(hipMemcpyAsync(d_sel, sl.h_sel, sizeof(uint32_t) * nu, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_sf_noise, dim3((nu + 63) / 64), dim3(64), 0, st, d_noise, d_sel, (int)nu, (int)nrx,
                        (int)nports, d_uenoise);
     RXQ_CHK(hipGetLastError());
@@ -611,10 +679,9 @@ struct srsgpu_rxq {
       any = any || b[ue[j]].ue->feedback;
     }
     if (any && srsgpu_pdsch_feedback_dev(pdsch, fb_sf.data(), nu, d_ce, gsz, d_uenoise, d_fb)) return -1;
-    fb_any = any;
+    sl.fb_any = any;
     return 0;
   }
-  bool fb_any = false;
 
   // the grant of a found DCI as srslte_ue_dl_decode_rnti configures it (ue_dl.c:498-574): unpack,
   // redundancy versions, softbuffer resets, MIMO type of the format, srslte_pdsch_cfg_mimo's
@@ -697,13 +764,16 @@ struct srsgpu_rxq {
     return 1;
   }
 
-  // one batch: OFDM of the staged samples, channel estimation, the ue_dl items' control channel and
-  // grants, the PDSCH / DL-SCH of every subframe with a grant, one copy of the results back
   static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
-  double run_tm[8] = {}; // this batch's stage times, added to tm under the lock by run_loop
-  int run(std::vector<Pending> &b, const float *d_td) {
+  double run_tm[8] = {}; // the dispatcher's stage times of its last batch, added to tm under the lock
+
+  // one batch, enqueued as a whole: OFDM of the staged samples, channel estimation and measurements,
+  // the ue_dl items' control channel (its host round trips) and grants, the softbuffer resets, the
+  // PDSCH / DL-SCH of every subframe with a grant (TB bytes straight into registered caller buffers,
+  // the others into d_data), and the copies of the results into the slot's pinned buffers
+  int enqueue(Slot &sl, std::vector<Pending> &b, const float *d_td) {
     const uint32_t n = (uint32_t)b.size();
     for (double &v : run_tm) v = 0;
     double t0 = now_s(), t1;
@@ -727,8 +797,8 @@ struct srsgpu_rxq {
     }
     if (srsgpu_chest_estimate_meas_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise, d_meas)) return -1;
     if (ccfg.noise_alg != 0) { // PSS / EMPTY: carry the estimate across subframes in order
-      for (uint32_t i = 0; i < n; i++) h_est[i] = (uint8_t)(b[i].sf_idx() == 0 || b[i].sf_idx() == 5);
-      RXQ_CHK(hipMemcpyAsync(d_est, h_est, n, hipMemcpyHostToDevice, st));
+      for (uint32_t i = 0; i < n; i++) sl.h_est[i] = (uint8_t)(b[i].sf_idx() == 0 || b[i].sf_idx() == 5);
+      RXQ_CHK(hipMemcpyAsync(d_est, sl.h_est, n, hipMemcpyHostToDevice, st));
       // grids of one subframe's rx antennas are consecutive: n rows of nrx * nports columns
       hipLaunchKernelGGL(k_noise_carry, dim3(1), dim3(64), 0, st, d_noise, d_est, (int)n, (int)(nrx * nports),
                          d_noise_last);
@@ -738,10 +808,10 @@ struct srsgpu_rxq {
       int32_t src = -1;
       for (uint32_t i = 0; i < n; i++) {
         if (ccfg.cfo_estimate_enable && ((ccfg.cfo_estimate_sf_mask >> b[i].sf_idx()) & 1u)) src = (int32_t)i;
-        h_cfo_src[i] = src;
+        sl.h_cfo_src[i] = src;
       }
       const int cols = (int)(nrx * nports);
-      RXQ_CHK(hipMemcpyAsync(d_cfo_src, h_cfo_src, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+      RXQ_CHK(hipMemcpyAsync(d_cfo_src, sl.h_cfo_src, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_getters, dim3((n + 63) / 64), dim3(64), 0, st, d_noise, d_meas, d_cfo_src,
                          (int)ccfg.rsrp_neighbour, d_meas_last, (int)n, (int)nrx, (int)nports, (int)cell.nof_prb,
                          d_getters);
@@ -749,22 +819,22 @@ struct srsgpu_rxq {
       hipLaunchKernelGGL(k_meas_last, dim3(1), dim3(64), 0, st, d_meas, src, ccfg.rsrp_neighbour ? (int)n - 1 : -1,
                          cols, d_meas_last);
       RXQ_CHK(hipGetLastError());
-      RXQ_CHK(hipMemcpyAsync(h_getters, d_getters, sizeof(float) * 6 * n, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(hipMemcpyAsync(sl.h_getters, d_getters, sizeof(float) * 6 * n, hipMemcpyDeviceToHost, st));
     }
     srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(pdsch);
     std::vector<uint32_t> ue;
     for (uint32_t i = 0; i < n; i++)
       if (b[i].ue) ue.push_back(i);
-    fb_any = false;
+    sl.fb_any = false;
     lap(0);
-    if (!ue.empty() && control(b, ue)) return -1;
+    if (!ue.empty() && control(sl, b, ue)) return -1;
     lap(1);
-    if (fb_any)
-      RXQ_CHK(hipMemcpyAsync(h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
+    if (sl.fb_any)
+      RXQ_CHK(hipMemcpyAsync(sl.h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
     // grants: the grant items' own, the ue_dl items' from their DCI
     std::vector<srsgpu_pdsch_sf_t> sfs;
-    std::vector<uint32_t> who;       // batch index of each PDSCH subframe
-    std::vector<int> state(n, 1);    // ue_dl: 1 decode, 0 no PDSCH call, -1 error
+    sl.who.clear();
+    sl.ue_state.assign(n, 1);
     for (uint32_t i = 0, j = 0; i < n; i++) {
       srsgpu_pdsch_sf_t s;
       if (b[i].ue) {
@@ -797,11 +867,11 @@ struct srsgpu_rxq {
           if (!u->acks[t]) u->noi[t] = 0; // an acked TB keeps what it had (the reference's last noi)
         j++;
         if (res.found != 1) { // no DCI, or the search's error: srslte_ue_dl_decode_rnti returns 0
-          state[i] = 0;
+          sl.ue_state[i] = 0;
           continue;
         }
-        state[i] = grant_of(u, res, u->cfi, dl, s);
-        if (state[i] != 1) continue;
+        sl.ue_state[i] = grant_of(u, res, u->cfi, dl, s);
+        if (sl.ue_state[i] != 1) continue;
       } else {
         s = b[i].it->sf;
         const uint32_t ntb = sf_ntb(s);
@@ -812,58 +882,93 @@ struct srsgpu_rxq {
             rs_ncb.push_back(UINT32_MAX); // srslte_softbuffer_rx_reset: every block
           }
       }
-      const uint32_t k = (uint32_t)sfs.size();
       s.grid_offset = (uint64_t)i * nrx * gsz;
       s.ce_offset = (uint64_t)i * nrx * nports * gsz;
-      s.data_offset[0] = (uint64_t)(2 * k) * dlen;
-      s.data_offset[1] = (uint64_t)(2 * k + 1) * dlen;
       sfs.push_back(s);
-      who.push_back(i);
+      sl.who.push_back(i);
     }
     const uint32_t np = (uint32_t)sfs.size();
-    uint32_t ntbs = 0;
-    for (uint32_t k = 0; k < np; k++) ntbs += sf_ntb(sfs[k]);
     if (!rs_slot.empty() && srsgpu_dlsch_softbuffer_reset_list(dl, rs_slot.data(), rs_ncb.data(), (uint32_t)rs_slot.size()))
       return -1;
+    // each TB's output: the caller's buffer itself when it lies in registered memory (the decoder writes
+    // it over PCIe), else the next free bytes of d_data, copied back in one transfer and then into place
+    std::vector<uint8_t *> outp;
+    sl.ntb_of.clear();
+    sl.tbs_of.clear();
+    sl.stage_off.clear();
+    sl.staged_bytes = 0;
+    {
+      std::lock_guard<std::mutex> lk(m); // regions
+      for (uint32_t k = 0; k < np; k++) {
+        const Pending &p = b[sl.who[k]];
+        const uint32_t ntb = sf_ntb(sfs[k]);
+        sl.ntb_of.push_back(ntb);
+        for (uint32_t t = 0; t < ntb; t++) {
+          uint8_t *out = p.it ? p.it->data[t] : p.ue->data[t];
+          const size_t len = SRSGPU_DLSCH_DATA_LEN(sfs[k].tbs[t]);
+          const bool skip = (sfs[k].skip_tb >> t) & 1u;
+          const void *dv = (out && !skip) ? device_view(out, len, false) : nullptr;
+          sl.tbs_of.push_back(sfs[k].tbs[t]);
+          if (dv) {
+            outp.push_back((uint8_t *)dv);
+            sl.stage_off.push_back(-1);
+            zero_copy_tbs++;
+          } else {
+            outp.push_back(d_data + sl.staged_bytes);
+            sl.stage_off.push_back(skip || !out ? -2 : (int64_t)sl.staged_bytes);
+            if (!skip && out) {
+              sl.staged_bytes += (len + 15) & ~(size_t)15;
+              staged_tbs++;
+            }
+          }
+        }
+      }
+    }
     lap(2);
     if (np) {
       srsgpu_pdsch_set_noise_dev(pdsch, d_noise);
       // the PDSCH's per-subframe noise comes from d_noise at the subframe's position in the call:
       // compact the noise rows of the decoded subframes when some subframes have no PDSCH
       if (np != n) {
-        for (uint32_t k = 0; k < np; k++) h_who[k] = who[k];
+        for (uint32_t k = 0; k < np; k++) sl.h_who[k] = sl.who[k];
         const int cols = (int)(nrx * nports);
-        RXQ_CHK(hipMemcpyAsync(d_who, h_who, sizeof(uint32_t) * np, hipMemcpyHostToDevice, st));
+        RXQ_CHK(hipMemcpyAsync(d_who, sl.h_who, sizeof(uint32_t) * np, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_noise_gather, dim3((np * cols + 255) / 256), dim3(256), 0, st, d_noise, d_who,
                            (int)np, cols, d_pnoise);
         RXQ_CHK(hipGetLastError());
         srsgpu_pdsch_set_noise_dev(pdsch, d_pnoise);
       }
       // TB results come back in call order: (subframe, tb), CDD subframes holding two
-      if (srsgpu_pdsch_decode_dev(pdsch, sfs.data(), np, d_grid, d_ce, gsz, d_data, max_halfits, d_ret, d_noi))
+      if (srsgpu_pdsch_decode_out_dev(pdsch, sfs.data(), np, d_grid, d_ce, gsz, outp.data(), max_halfits, d_ret, d_noi))
         return -1;
-      RXQ_CHK(hipMemcpyAsync(h_data, d_data, dlen * 2 * np, hipMemcpyDeviceToHost, st));
-      RXQ_CHK(hipMemcpyAsync(h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
-      RXQ_CHK(hipMemcpyAsync(h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
+      const size_t ntbs = outp.size();
+      if (sl.staged_bytes)
+        RXQ_CHK(hipMemcpyAsync(sl.h_data, d_data, sl.staged_bytes, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(hipMemcpyAsync(sl.h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(hipMemcpyAsync(sl.h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
     }
-    RXQ_CHK(hipMemcpyAsync(h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(hipMemcpyAsync(sl.h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
     lap(3);
-    RXQ_CHK(hipStreamSynchronize(st));
-    lap(4);
-    for (uint32_t k = 0, t0 = 0; k < np; k++) {
-      const Pending &p = b[who[k]];
-      const uint32_t ntb = sf_ntb(sfs[k]);
-      for (uint32_t t = 0; t < ntb; t++, t0++) {
+    return 0;
+  }
+
+  // the results of a finished batch into its items (completer thread)
+  void complete(Slot &sl) {
+    const std::vector<Pending> &b = sl.items;
+    const uint32_t n = (uint32_t)b.size();
+    for (uint32_t k = 0, t0 = 0; k < (uint32_t)sl.who.size(); k++) {
+      const Pending &p = b[sl.who[k]];
+      for (uint32_t t = 0; t < sl.ntb_of[k]; t++, t0++) {
         uint8_t *out = p.it ? p.it->data[t] : p.ue->data[t];
         if (p.it) {
-          p.it->ret[t] = h_ret[t0];
-          p.it->noi[t] = h_noi[t0];
+          p.it->ret[t] = sl.h_ret[t0];
+          p.it->noi[t] = sl.h_noi[t0];
         } else {
           if (p.ue->acked_in[t]) continue; // skipped as srslte_pdsch_decode skips it: nothing written
-          p.ue->noi[t] = h_noi[t0];
-          p.ue->acks[t] = h_ret[t0] == 0;
+          p.ue->noi[t] = sl.h_noi[t0];
+          p.ue->acks[t] = sl.h_ret[t0] == 0;
         }
-        if (out) memcpy(out, h_data + (2 * k + t) * dlen, SRSGPU_DLSCH_DATA_LEN(sfs[k].tbs[t]));
+        if (out && sl.stage_off[t0] >= 0) memcpy(out, sl.h_data + sl.stage_off[t0], SRSGPU_DLSCH_DATA_LEN(sl.tbs_of[t0]));
       }
     }
     for (uint32_t i = 0, jf = 0; i < n; i++) {
@@ -871,11 +976,11 @@ struct srsgpu_rxq {
       float nn = 0.f;
       for (uint32_t a = 0; a < nrx; a++) {
         float acc = 0.f;
-        for (uint32_t p = 0; p < nports; p++) acc += h_noise[(i * nrx + a) * nports + p];
+        for (uint32_t p = 0; p < nports; p++) acc += sl.h_noise[(i * nrx + a) * nports + p];
         nn += acc / (float)nports;
       }
       nn /= (float)nrx;
-      const float *g = h_getters + (size_t)i * 6;
+      const float *g = sl.h_getters + (size_t)i * 6;
       const srsgpu_rxq_meas_t meas = {g[0], g[1], g[2], g[3], g[4], g[5]};
       if (b[i].it) {
         b[i].it->noise = nn;
@@ -885,9 +990,9 @@ struct srsgpu_rxq {
         u->noise = nn;
         u->meas = meas;
         // ue_dl.c:612-616: TB 0's size when a DCI was found and the PDSCH call succeeded
-        u->ret = state[i] < 0 ? -1 : (u->found == 1 ? u->grant.tbs[0] : 0);
-        if (u->feedback) {
-          u->fb = h_fb[jf];
+        u->ret = sl.ue_state[i] < 0 ? -1 : (u->found == 1 ? u->grant.tbs[0] : 0);
+        if (u->feedback && sl.fb_any) {
+          u->fb = sl.h_fb[jf];
         } else {
           memset(&u->fb, 0, sizeof(u->fb));
           u->fb.ret_cn = u->fb.ret_pmi = -1;
@@ -895,8 +1000,6 @@ struct srsgpu_rxq {
         jf++;
       }
     }
-    lap(5);
-    return 0;
   }
 };
 

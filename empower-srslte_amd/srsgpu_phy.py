@@ -419,6 +419,9 @@ _sig = {
     "srsgpu_chest_set_smooth_filter3_coeff": (None, [_vp, ctypes.c_float]),
     "srsgpu_chest_set_smooth_filter_gauss": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_float]),
     "srsgpu_chest_estimate_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp]),
+    "srsgpu_pdsch_decode_out_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_pdsch_sf_t), _u32, _vp, _vp, _sz,
+                                           ctypes.POINTER(_vp), _u32, _vp, _vp]),
+    "srsgpu_dlsch_decode_out_dev": (_i32, [_vp, _vp, _u32, _vp, ctypes.POINTER(_vp), _u32, _vp, _vp]),
     "srsgpu_pdsch_feedback_dev": (_i32, [_vp, ctypes.POINTER(srsgpu_feedback_sf_t), _u32, _vp, _sz, _vp, _vp]),
     "srsgpu_chest_estimate_meas_dev": (_i32, [_vp, _u32p, _u32, _vp, _sz, _vp, _vp, _vp]),
     "srsgpu_chest_set_cfg": (_i32, [_vp, _vp]),

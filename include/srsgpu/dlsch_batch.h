@@ -70,6 +70,13 @@ int srsgpu_dlsch_decode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint
                             const int16_t *d_e_bits, uint8_t *d_data, uint32_t max_halfits,
                             int32_t *d_ret, uint32_t *d_noi);
 
+/* As srsgpu_dlsch_decode_dev with each TB's output bytes at d_out[i] (data_offset ignored): device
+ * memory, or host memory the device can address (registered / mapped), which the decoder then writes
+ * over PCIe with no copy. */
+int srsgpu_dlsch_decode_out_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
+                                const int16_t *d_e_bits, uint8_t *const *d_out, uint32_t max_halfits,
+                                int32_t *d_ret, uint32_t *d_noi);
+
 /* Host pointers: e_bits[i] / data[i] per TB (offsets in tb[] ignored); synchronises. */
 int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
                         const int16_t *const *e_bits, uint8_t *const *data, uint32_t max_halfits,

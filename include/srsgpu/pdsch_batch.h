@@ -122,6 +122,12 @@ int srsgpu_pdsch_decode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint
                             const float *d_grid, const float *d_ce, size_t ant_stride,
                             uint8_t *d_data, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
 
+/* As srsgpu_pdsch_decode_dev with TB t of the call (subframe order, TB 0 then TB 1) written at d_out[t]
+ * (data_offset ignored): device memory or host memory the device can address (srsgpu_dlsch_decode_out_dev). */
+int srsgpu_pdsch_decode_out_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t nof_sf,
+                                const float *d_grid, const float *d_ce, size_t ant_stride,
+                                uint8_t *const *d_out, uint32_t max_halfits, int32_t *d_ret, uint32_t *d_noi);
+
 /* Transmit side, used to synthesise traffic on the device (srslte_pdsch_encode, pdsch.c:1048-1131,
  * single antenna port): per subframe, DL-SCH encoding of TB 0 (srsgpu_dlsch_encode_dev, rv from
  * sf[i].rv[0]), scrambling, modulation (modem/lte_tables.c), rho_a scaling and RE mapping into

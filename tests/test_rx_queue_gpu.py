@@ -115,6 +115,47 @@ def test_worker_threads_through_the_queue(oracle):
     q.close()
 
 
+def test_registered_outputs_written_in_place(oracle):
+    """TB outputs that lie in a registered host block are written by the decoder itself over PCIe
+    (no staging in the queue): the bytes, return codes and nof_iterations equal the direct batch API's;
+    outputs outside the block (every third item) take the staged copy-back in the same batches; several
+    batches in flight (three slots) keep every item's results its own"""
+    import torch
+    import srsgpu_phy as s
+    po, dl = PdschOracle(oracle), DlschOracle(oracle)
+    rng = np.random.default_rng(5)
+    nof_prb, cell_id, tbs = 25, 9, 18336  # 5 MHz, MCS 28
+    N = s.symbol_sz(nof_prb, True)
+    n = 30
+    xs, datas, sfs = [], [], []
+    for i in range(n):
+        sf_idx = [1, 2, 3, 4, 6, 7, 8, 9][i % 8]
+        x, data, idx = build_subframe(po, dl, rng, nof_prb, cell_id, N, sf_idx, tbs, 1234, 30.0 if i % 4 else 12.0,
+                                      rng.uniform(0, 6.28))
+        xs.append(x)
+        datas.append(data)
+        sfs.append((sf_idx, idx.size))
+    ret_d, noi_d, data_d, _ = _direct(s, torch, xs, sfs, nof_prb, cell_id, N, tbs)
+    q = s.RxQueue(nof_prb, cell_id, N, nof_softbuffers=n, max_batch=4, max_wait_us=2000)
+    dlen = tbs // 8 + 6
+    block = np.zeros((n, dlen + 3), np.uint8)  # rows at odd offsets: no alignment needed
+    q.register(block)
+    own = [np.zeros(dlen, np.uint8) for _ in range(n)]
+    outs = [own[i] if i % 3 == 0 else block[i, 3:3 + dlen] for i in range(n)]
+    items = [q.item([xs[i]], s.make_sf(sf_idx=sfs[i][0], lstart=1, nof_prb=nof_prb, mod=3, nof_re=sfs[i][1],
+                                        rnti=1234, tbs=tbs, softbuffer=i), [outs[i]]) for i in range(n)]
+    tickets = [q.submit(it) for it in items]
+    q.flush()
+    assert all(q.wait(t) == 0 for t in tickets)
+    nb = (tbs + 24) // 8
+    for i in range(n):
+        assert items[i].ret[0] == ret_d[i] and items[i].noi[0] == noi_d[i], i
+        assert (outs[i][:nb] == data_d[i][:nb]).all(), i
+    assert sum(int(items[i].ret[0] == 0) for i in range(n)) >= n // 2
+    q.unregister(block)
+    q.close()
+
+
 def test_empty_noise_carried_across_batches(oracle):
     """EMPTY noise (srsUE's snr_estim_alg=empty, phch_worker.cc:557-564): only subframes 0 and 5
     estimate the noise (chest_dl.c:628-637); every other subframe keeps the latest estimate of an
