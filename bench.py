@@ -698,6 +698,12 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
             "decoded_fraction": round(float(d_dec.float().mean().item()), 3)}
 
 
+# registered-sample ingest of the queue (srsgpu_rxq, rx_queue.hip stage()): DMA from the caller's
+# memory on the copy stream (default), the same split over 4 copy streams, or the ingest kernel
+# reading the samples over the bus
+INGEST_VARIANTS = {"dma": {}, "dma4": {"SRSGPU_RXQ_DMA_STREAMS": "4"}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
+
+
 def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0,
                  paced_streams=(32, 64, 128, 192, 256, 320, 384, 448, 512, 640, 768), ticks=300, depth=3,
                  budget_ms=3.0):
@@ -709,8 +715,10 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
     saturated: `producers` threads submit nsf subframes as fast as the queue takes them, per batch
     size and ingest mode — staged (each submission copies its samples into the queue's pinned
     staging, then one DMA per batch), zero-copy (the samples lie in a srsgpu_rxq_register'ed block:
-    the batch's ingest kernel reads them over PCIe in place) and zero-copy SC16 (the radio's int16
-    I/Q, half the bytes, converted on the GPU). ingest_GBps = sample bytes handed over / wall time.
+    DMA'd from there, one copy per run of address-contiguous subframes), zero-copy SC16 (the radio's
+    int16 I/Q, half the bytes, converted on the GPU) and zero-copy SC16 bus-read (the batch's ingest
+    kernel reads the registered samples over PCIe in place, SRSGPU_RXQ_INGEST=kernel).
+    ingest_GBps = sample bytes handed over / wall time.
 
     paced: N streams each hand over one subframe per 1 ms TTI (srsgpu_rxq_drive_paced, zero-copy
     SC16, batch = N, depth HARQ slots per stream) for `ticks` TTIs; latency = results written - TTI
@@ -748,11 +756,22 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             items.append(q.item([src[j]], sf, [outs[i % nsb]]))
         return items, outs
 
+    def queue(variant, *a, **kw):
+        """a queue under one registered-ingest variant (the env is read when the queue is created)"""
+        env = INGEST_VARIANTS[variant]
+        os.environ.update(env)
+        try:
+            return s.RxQueue(*a, **kw)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+
     for B in batches:
-        for mode in ("staged", "zero_copy", "zero_copy_sc16"):
-            q = s.RxQueue(C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
-            src = x_sc if mode.endswith("sc16") else x_cf
-            if mode.endswith("sc16"):
+        modes = [("staged", "dma"), ("zero_copy", "dma")] + [("zero_copy_sc16", v) for v in INGEST_VARIANTS]
+        for mode, variant in modes:
+            q = queue(variant, C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
+            src = x_sc if "sc16" in mode else x_cf
+            if "sc16" in mode:
                 q.set_input_format(q.SC16, scale)
             if mode != "staged":
                 q.register(src)
@@ -770,48 +789,53 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             acked = sum(1 for it in items[-min(nsf, 4 * B):] if it.ret[0] == 0)
             zc, st = q.ingest_stats()
             tmg = q.timing()
-            out["saturated"]["%s_b%d" % (mode, B)] = {
+            key = "%s_b%d" % (mode, B) if mode != "zero_copy_sc16" or variant == "dma" else \
+                "%s_%s_b%d" % (mode, variant, B)
+            out["saturated"][key] = {
                 "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
                 "subframes_per_s": round(nsf / el, 1),
-                "ingest_GBps": round(nsf * sf_bytes["sc16" if mode.endswith("sc16") else "cf32"] / el / 1e9, 2),
+                "ingest_GBps": round(nsf * sf_bytes["sc16" if "sc16" in mode else "cf32"] / el / 1e9, 2),
                 "latency_ms_p50": round(float(np.percentile(lat, 50)), 3),
                 "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
                 "mean_batch": round(done / max(nb, 1), 1), "failed": int((status != 0).sum()),
-                "zero_copy_rows": zc, "staged_rows": st,
+                "zero_copy_rows": zc, "staged_rows": st, "ingest": variant,
                 "acked_of_last": "%d/%d" % (acked, min(nsf, 4 * B))}
             q.close()
             del items, outs
-    # paced real-time streams
-    best = 0
-    for ns in paced_streams:
-        q = s.RxQueue(C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
-        q.set_input_format(q.SC16, scale)
-        q.register(x_sc)
-        items, outs = make_items(q, ns * depth, ns * depth, x_sc)
-        warm = [q.submit(items[i]) for i in range(ns)]
-        q.flush()
-        assert all(q.wait(t) == 0 for t in warm)
-        lat, status, acked, late = q.drive_paced(items, ns, depth, ticks, 1000, workers=min(8, ns))
-        nb, done = q.stats()
-        tmg = q.timing()
-        p99 = float(np.percentile(lat, 99))
-        rec = {"latency_ms_p50": round(float(np.percentile(lat, 50)), 3), "latency_ms_p99": round(p99, 3),
-               "latency_ms_max": round(float(lat.max()), 3), "acked": "%d/%d" % (acked, ns * ticks),
-               "failed": int((status != 0).sum()), "mean_batch": round(done / max(nb, 1), 1),
-               "producer_late_ms_max": round(late, 3), "subframes_per_s": round(ns * 1000.0, 1),
-               "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
-               "ingest_GBps": round(ns * 1000.0 * sf_bytes["sc16"] / 1e9, 2)}
-        out["paced"][str(ns)] = rec
-        q.close()
-        del items, outs
-        ok = p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks
-        if ok:
-            best = ns
-        else:
-            break
+    # paced real-time streams, per registered-ingest variant
+    best, best_variant = 0, None
+    for variant in INGEST_VARIANTS:
+        paced = out["paced"] if variant == "dma" else out.setdefault("paced_" + variant, {})
+        for ns in paced_streams:
+            q = queue(variant, C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
+            q.set_input_format(q.SC16, scale)
+            q.register(x_sc)
+            items, outs = make_items(q, ns * depth, ns * depth, x_sc)
+            warm = [q.submit(items[i]) for i in range(ns)]
+            q.flush()
+            assert all(q.wait(t) == 0 for t in warm)
+            lat, status, acked, late = q.drive_paced(items, ns, depth, ticks, 1000, workers=min(8, ns))
+            nb, done = q.stats()
+            tmg = q.timing()
+            p99 = float(np.percentile(lat, 99))
+            rec = {"latency_ms_p50": round(float(np.percentile(lat, 50)), 3), "latency_ms_p99": round(p99, 3),
+                   "latency_ms_max": round(float(lat.max()), 3), "acked": "%d/%d" % (acked, ns * ticks),
+                   "failed": int((status != 0).sum()), "mean_batch": round(done / max(nb, 1), 1),
+                   "producer_late_ms_max": round(late, 3), "subframes_per_s": round(ns * 1000.0, 1),
+                   "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
+                   "ingest_GBps": round(ns * 1000.0 * sf_bytes["sc16"] / 1e9, 2)}
+            paced[str(ns)] = rec
+            q.close()
+            del items, outs
+            if p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks:
+                if ns > best:
+                    best, best_variant = ns, variant
+            else:
+                break
     out["paced_cfg"] = {"ticks": ticks, "tti_us": 1000, "depth": depth, "input": "sc16 zero-copy",
                         "batch": "one TTI of all streams", "p99_budget_ms": budget_ms}
     out["real_time_streams"] = best
+    out["real_time_streams_ingest"] = best_variant
     return out
 
 
@@ -1328,8 +1352,11 @@ def compact_summary(result, detail_name, limit=6000):
     rq = result.get("rx_queue")
     if rq:
         sat = rq.get("saturated", {})
+        top = max(sat, key=lambda k: sat[k]["subframes_per_s"], default=None)
         legs["rx_queue"] = {"real_time_streams": rq.get("real_time_streams"),
-                            "saturated_max_sfps": max((v["subframes_per_s"] for v in sat.values()), default=None)}
+                            "real_time_ingest": rq.get("real_time_streams_ingest"),
+                            "saturated_max_sfps": sat[top]["subframes_per_s"] if top else None,
+                            "saturated_max_mode": top}
     hd = result.get("headline_detail") or {}
     if hd.get("gather_ms") is not None:
         legs["headline_gather_ms"] = hd["gather_ms"]

@@ -202,6 +202,13 @@ struct srsgpu_rxq {
   bool phich_dirty = false; // srsgpu_rxq_set_phich: the dispatcher rebuilds pdcch before its next use
   size_t td_len = 0, gsz = 0, dlen = 0; // complex samples per antenna / grid elements / TB bytes
   hipStream_t st = nullptr, cst = nullptr; // compute / copy streams
+  // ingest_dma: registered rows' copies spread over ndma streams (SRSGPU_RXQ_DMA_STREAMS, default 1:
+  // all on cst), runs cut into pieces of at most dma_piece bytes, joined back into cst
+  static constexpr int MAX_DMA = 4;
+  int ndma = 1;
+  size_t dma_piece = (size_t)64 << 20;
+  hipStream_t dst_[MAX_DMA] = {};
+  hipEvent_t dev_[MAX_DMA] = {}, dfork = nullptr;
   srsgpu_ofdm_t *ofdm = nullptr;
   srsgpu_chest_t *chest = nullptr;
   srsgpu_pdsch_t *pdsch = nullptr;
@@ -243,6 +250,8 @@ struct srsgpu_rxq {
     float *h_td = nullptr, *d_td = nullptr; // pinned staging (raw format) / device samples (cf32)
     float *d_raw = nullptr;                  // SC16: the staged raw samples before conversion
     const void **h_src = nullptr, **d_src = nullptr; // per row: registered host source (device view) or null
+    std::vector<const void *> h_host;                // per row: the registered host pointer itself
+    void *d_reg = nullptr;                           // registered rows' DMA target (ingest_dma)
     hipEvent_t staged = nullptr;
     std::vector<Pending> items;
     int state = FILLING;
@@ -282,7 +291,11 @@ struct srsgpu_rxq {
     const char *d; // device view of the same memory
   };
   std::vector<Region> regions; // guarded by m
-  uint64_t zero_copy_rows = 0, staged_rows = 0, zero_copy_tbs = 0, staged_tbs = 0;
+  uint64_t zero_copy_rows = 0, staged_rows = 0, zero_copy_tbs = 0, staged_tbs = 0, dma_copies = 0;
+  // registered rows: true (default) DMA them (one copy per run of address-contiguous rows) and convert
+  // on the device; false (SRSGPU_RXQ_INGEST=kernel) the ingest kernel reads them over the bus
+  bool ingest_dma = true;
+  std::vector<std::pair<const char *, uint32_t>> reg; // stage(): registered rows by host address
   // device view of a registered host pointer holding `bytes`, or null (caller holds m); aligned16: the
   // ingest kernel reads 16 B vectors (else the samples are staged)
   const void *device_view(const void *p, size_t bytes, bool aligned16 = true) const {
@@ -350,6 +363,8 @@ struct srsgpu_rxq {
       RXQ_CHK(hipHostMalloc(&s.h_td, sizeof(float) * 2 * td_len * mb * nrx));
       RXQ_CHK(hipHostMalloc(&s.h_src, sizeof(void *) * mb * nrx));
       RXQ_CHK(hipMalloc(&s.d_src, sizeof(void *) * mb * nrx));
+      s.h_host.assign((size_t)mb * nrx, nullptr);
+      RXQ_CHK(hipMalloc(&s.d_reg, sizeof(float) * 2 * td_len * mb * nrx));
       RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
       RXQ_CHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
       RXQ_CHK(hipHostMalloc(&s.h_est, mb));
@@ -392,6 +407,16 @@ struct srsgpu_rxq {
     RXQ_CHK(hipMalloc(&d_res_ul, sizeof(srsgpu_dci_result_t) * mb));
     RXQ_CHK(hipHostMalloc(&h_res_ul, sizeof(srsgpu_dci_result_t) * mb));
     srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
+    if (const char *e = getenv("SRSGPU_RXQ_INGEST")) ingest_dma = strcmp(e, "kernel") != 0;
+    if (const char *e = getenv("SRSGPU_RXQ_DMA_STREAMS")) ndma = std::max(1, std::min(MAX_DMA, atoi(e)));
+    if (ndma > 1) {
+      dma_piece = (size_t)8 << 20;
+      RXQ_CHK(hipEventCreateWithFlags(&dfork, hipEventDisableTiming));
+      for (int k = 0; k < ndma; k++) {
+        RXQ_CHK(hipStreamCreateWithFlags(&dst_[k], hipStreamNonBlocking));
+        RXQ_CHK(hipEventCreateWithFlags(&dev_[k], hipEventDisableTiming));
+      }
+    }
     closer = std::thread([this] { close_loop(); });
     worker = std::thread([this] { run_loop(); });
     completer = std::thread([this] { comp_loop(); });
@@ -422,7 +447,7 @@ struct srsgpu_rxq {
     if (pcfich) srsgpu_pcfich_destroy(pcfich);
     if (pdcch) srsgpu_pdcch_destroy(pdcch);
     for (Slot &s : slot) {
-      for (void *p : {(void *)s.d_td, (void *)s.d_raw, (void *)s.d_src})
+      for (void *p : {(void *)s.d_td, (void *)s.d_raw, (void *)s.d_src, (void *)s.d_reg})
         if (p) (void)hipFree(p);
       for (void *p : {(void *)s.h_td, (void *)s.h_src, (void *)s.h_est, (void *)s.h_cfo_src, (void *)s.h_sel,
                       (void *)s.h_who, (void *)s.h_noise, (void *)s.h_getters, (void *)s.h_ret, (void *)s.h_noi,
@@ -443,6 +468,11 @@ struct srsgpu_rxq {
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
+    for (int k = 0; k < MAX_DMA; k++) {
+      if (dst_[k]) (void)hipStreamDestroy(dst_[k]);
+      if (dev_[k]) (void)hipEventDestroy(dev_[k]);
+    }
+    if (dfork) (void)hipEventDestroy(dfork);
   }
 
   // ---------------------------------------------------------------- submission ----
@@ -472,6 +502,7 @@ struct srsgpu_rxq {
       for (uint32_t a = 0; a < nrx; a++) {
         dv[a] = device_view(td[a], row_bytes);
         slot[s].h_src[(size_t)idx * nrx + a] = dv[a]; // null: staged by the host copy below
+        slot[s].h_host[(size_t)idx * nrx + a] = dv[a] ? td[a] : nullptr;
       }
       slot[s].copying++;
     }
@@ -488,7 +519,10 @@ struct srsgpu_rxq {
   }
 
   // the closed slot's samples to the device: one DMA of the staged rows' region (up to the last staged
-  // row), then the ingest kernel for rows read from registered memory and for SC16 conversion
+  // row); registered rows either by DMA straight from the caller's memory into d_reg, one copy per run
+  // of rows contiguous there (ingest_dma), or read over the bus by the ingest kernel; the ingest kernel
+  // then converts SC16 rows and moves registered rows into place. The staged DMA may cover registered
+  // rows' places with stale staging bytes: the ingest kernel writes them after it on the same stream.
   bool stage(Slot &sl, size_t n) {
     const int sc16 = sl.sc16;
     const size_t rows = n * nrx, row_bytes = (sc16 ? 4 : 8) * td_len;
@@ -502,9 +536,56 @@ struct srsgpu_rxq {
     char *dst_raw = sc16 ? (char *)sl.d_raw : (char *)sl.d_td;
     if (last && hipMemcpyAsync(dst_raw, sl.h_td, last * row_bytes, hipMemcpyHostToDevice, cst) != hipSuccess)
       return false;
+    if (ingest_dma) {
+      // registered rows in host address order, runs of contiguous rows one DMA each into d_reg (a row
+      // handed over twice is copied once); the ingest kernel then reads them from d_reg
+      reg.clear();
+      for (size_t r = 0; r < rows; r++)
+        if (sl.h_src[r]) reg.push_back({(const char *)sl.h_host[r], (uint32_t)r});
+      std::sort(reg.begin(), reg.end());
+      size_t pos = 0, run0 = 0, i0 = 0;
+      int next = 0; // the copy stream of the next piece
+      if (ndma > 1) {
+        if (hipEventRecord(dfork, cst) != hipSuccess) return false;
+        for (int k = 0; k < ndma; k++)
+          if (hipStreamWaitEvent(dst_[k], dfork, 0) != hipSuccess) return false;
+      }
+      auto flush_run = [&](size_t i1) {
+        if (i1 == i0) return true;
+        const size_t bytes = (pos - run0) * row_bytes;
+        for (size_t o = 0; o < bytes; o += dma_piece) {
+          hipStream_t cs = ndma > 1 ? dst_[next] : cst;
+          next = (next + 1) % ndma;
+          dma_copies++;
+          if (hipMemcpyAsync((char *)sl.d_reg + run0 * row_bytes + o, reg[i0].first + o,
+                             std::min(dma_piece, bytes - o), hipMemcpyHostToDevice, cs) != hipSuccess)
+            return false;
+        }
+        return true;
+      };
+      for (size_t i = 0; i < reg.size(); i++) {
+        const char *h = reg[i].first;
+        if (i > i0 && h == reg[i - 1].first) { // the same samples again
+          sl.h_src[reg[i].second] = (const char *)sl.d_reg + (pos - 1) * row_bytes;
+          continue;
+        }
+        if (i > i0 && h != reg[i - 1].first + row_bytes) {
+          if (!flush_run(i)) return false;
+          i0 = i;
+          run0 = pos;
+        }
+        sl.h_src[reg[i].second] = (const char *)sl.d_reg + pos * row_bytes;
+        pos++;
+      }
+      if (!flush_run(reg.size())) return false;
+      if (ndma > 1)
+        for (int k = 0; k < ndma; k++)
+          if (hipEventRecord(dev_[k], dst_[k]) != hipSuccess || hipStreamWaitEvent(cst, dev_[k], 0) != hipSuccess)
+            return false;
+    }
     const bool kernel = sc16 || nst < rows;
     if (kernel) {
-      // staged SC16 rows convert from the raw device copy; staged cf32 rows are in place already
+      // staged rows: SC16 converts from the raw copy, cf32 is in place
       for (size_t r = 0; r < rows; r++)
         if (!sl.h_src[r]) sl.h_src[r] = sc16 ? (const void *)(dst_raw + r * row_bytes) : nullptr;
       if (hipMemcpyAsync(sl.d_src, sl.h_src, sizeof(void *) * rows, hipMemcpyHostToDevice, cst) != hipSuccess)

@@ -238,14 +238,17 @@ def _run_queue(s, q, xs, sfs, nof_prb, tbs):
     return [it.ret[0] for it in items], [it.noi[0] for it in items], [it.noise for it in items], outs
 
 
-def test_registered_and_sc16_ingest(oracle):
-    """Zero-copy ingest (srsgpu_rxq_register: the batch's ingest kernel reads the caller's pinned
-    samples in place) and SC16 input (int16 I/Q converted on the GPU): the same TBs, iterations and
-    noise estimates, bit for bit, as the staged complex-float path on the same sample values — with
-    registered and staged subframes mixed in one batch, and misaligned pointers falling back to
-    staging."""
+@pytest.mark.parametrize("ingest", ["dma", "kernel"])
+def test_registered_and_sc16_ingest(oracle, ingest, monkeypatch):
+    """Zero-copy ingest (srsgpu_rxq_register: registered samples are DMA'd straight from the caller's
+    pinned memory, runs of address-contiguous subframes one copy each — or, SRSGPU_RXQ_INGEST=kernel,
+    read in place by the batch's ingest kernel) and SC16 input (int16 I/Q converted on the GPU): the
+    same TBs, iterations and noise estimates, bit for bit, as the staged complex-float path on the same
+    sample values — with registered and staged subframes mixed in one batch, registered subframes out
+    of address order and handed over twice, and misaligned pointers falling back to staging."""
     import torch
     import srsgpu_phy as s
+    monkeypatch.setenv("SRSGPU_RXQ_INGEST", ingest)
     nof_prb, cell_id, tbs, N, xs, datas, sfs = _queue_case(oracle)
     n = len(xs)
     # the radio's int16 samples and their float values (what a staged cf32 caller would hand over)
@@ -285,6 +288,12 @@ def test_registered_and_sc16_ingest(oracle):
     got = _run_queue(s, q, list(blk16), sfs, nof_prb, tbs)
     assert got[:3] == want[:3] and all((a == b).all() for a, b in zip(got[3], want[3]))
     assert q.ingest_stats()[0] == z0 + n
+    # out of address order, one subframe twice in the batch
+    perm = [5, 0, 0, 11, 3, 2, 1, 4, 10, 9, 7, 6][:n]
+    got = _run_queue(s, q, [blk16[p] for p in perm], [sfs[p] for p in perm], nof_prb, tbs)
+    for i, p in enumerate(perm):
+        assert (got[0][i], got[1][i], got[2][i]) == (want[0][p], want[1][p], want[2][p]), i
+        assert (got[3][i] == want[3][p]).all(), i
     q.close()
     torch.cuda.synchronize()
 
