@@ -699,9 +699,8 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
 
 
 # registered-sample ingest of the queue (srsgpu_rxq, rx_queue.hip stage()): DMA from the caller's
-# memory on the copy stream (default), the same split over 4 copy streams, or the ingest kernel
-# reading the samples over the bus
-INGEST_VARIANTS = {"dma": {}, "dma4": {"SRSGPU_RXQ_DMA_STREAMS": "4"}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
+# memory on the copy stream (default), or the ingest kernel reading the samples over the bus
+INGEST_VARIANTS = {"dma": {}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
 
 
 def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0,
@@ -766,8 +765,10 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             for k in env:
                 os.environ.pop(k, None)
 
+    # BENCH_RXQ_VARIANTS=a,b: only these ingest variants (diagnosis runs)
+    variants = [v for v in os.environ.get("BENCH_RXQ_VARIANTS", ",".join(INGEST_VARIANTS)).split(",") if v]
     for B in batches:
-        modes = [("staged", "dma"), ("zero_copy", "dma")] + [("zero_copy_sc16", v) for v in INGEST_VARIANTS]
+        modes = [("staged", "dma"), ("zero_copy", "dma")] + [("zero_copy_sc16", v) for v in variants]
         for mode, variant in modes:
             q = queue(variant, C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
             src = x_sc if "sc16" in mode else x_cf
@@ -804,7 +805,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             del items, outs
     # paced real-time streams, per registered-ingest variant
     best, best_variant = 0, None
-    for variant in INGEST_VARIANTS:
+    for variant in variants:
         paced = out["paced"] if variant == "dma" else out.setdefault("paced_" + variant, {})
         for ns in paced_streams:
             q = queue(variant, C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)

@@ -202,13 +202,6 @@ struct srsgpu_rxq {
   bool phich_dirty = false; // srsgpu_rxq_set_phich: the dispatcher rebuilds pdcch before its next use
   size_t td_len = 0, gsz = 0, dlen = 0; // complex samples per antenna / grid elements / TB bytes
   hipStream_t st = nullptr, cst = nullptr; // compute / copy streams
-  // ingest_dma: registered rows' copies spread over ndma streams (SRSGPU_RXQ_DMA_STREAMS, default 1:
-  // all on cst), runs cut into pieces of at most dma_piece bytes, joined back into cst
-  static constexpr int MAX_DMA = 4;
-  int ndma = 1;
-  size_t dma_piece = (size_t)64 << 20;
-  hipStream_t dst_[MAX_DMA] = {};
-  hipEvent_t dev_[MAX_DMA] = {}, dfork = nullptr;
   srsgpu_ofdm_t *ofdm = nullptr;
   srsgpu_chest_t *chest = nullptr;
   srsgpu_pdsch_t *pdsch = nullptr;
@@ -408,15 +401,6 @@ struct srsgpu_rxq {
     RXQ_CHK(hipHostMalloc(&h_res_ul, sizeof(srsgpu_dci_result_t) * mb));
     srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
     if (const char *e = getenv("SRSGPU_RXQ_INGEST")) ingest_dma = strcmp(e, "kernel") != 0;
-    if (const char *e = getenv("SRSGPU_RXQ_DMA_STREAMS")) ndma = std::max(1, std::min(MAX_DMA, atoi(e)));
-    if (ndma > 1) {
-      dma_piece = (size_t)8 << 20;
-      RXQ_CHK(hipEventCreateWithFlags(&dfork, hipEventDisableTiming));
-      for (int k = 0; k < ndma; k++) {
-        RXQ_CHK(hipStreamCreateWithFlags(&dst_[k], hipStreamNonBlocking));
-        RXQ_CHK(hipEventCreateWithFlags(&dev_[k], hipEventDisableTiming));
-      }
-    }
     closer = std::thread([this] { close_loop(); });
     worker = std::thread([this] { run_loop(); });
     completer = std::thread([this] { comp_loop(); });
@@ -468,11 +452,6 @@ struct srsgpu_rxq {
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
-    for (int k = 0; k < MAX_DMA; k++) {
-      if (dst_[k]) (void)hipStreamDestroy(dst_[k]);
-      if (dev_[k]) (void)hipEventDestroy(dev_[k]);
-    }
-    if (dfork) (void)hipEventDestroy(dfork);
   }
 
   // ---------------------------------------------------------------- submission ----
@@ -544,24 +523,11 @@ struct srsgpu_rxq {
         if (sl.h_src[r]) reg.push_back({(const char *)sl.h_host[r], (uint32_t)r});
       std::sort(reg.begin(), reg.end());
       size_t pos = 0, run0 = 0, i0 = 0;
-      int next = 0; // the copy stream of the next piece
-      if (ndma > 1) {
-        if (hipEventRecord(dfork, cst) != hipSuccess) return false;
-        for (int k = 0; k < ndma; k++)
-          if (hipStreamWaitEvent(dst_[k], dfork, 0) != hipSuccess) return false;
-      }
       auto flush_run = [&](size_t i1) {
         if (i1 == i0) return true;
-        const size_t bytes = (pos - run0) * row_bytes;
-        for (size_t o = 0; o < bytes; o += dma_piece) {
-          hipStream_t cs = ndma > 1 ? dst_[next] : cst;
-          next = (next + 1) % ndma;
-          dma_copies++;
-          if (hipMemcpyAsync((char *)sl.d_reg + run0 * row_bytes + o, reg[i0].first + o,
-                             std::min(dma_piece, bytes - o), hipMemcpyHostToDevice, cs) != hipSuccess)
-            return false;
-        }
-        return true;
+        dma_copies++;
+        return hipMemcpyAsync((char *)sl.d_reg + run0 * row_bytes, reg[i0].first, (pos - run0) * row_bytes,
+                              hipMemcpyHostToDevice, cst) == hipSuccess;
       };
       for (size_t i = 0; i < reg.size(); i++) {
         const char *h = reg[i].first;
@@ -578,10 +544,6 @@ struct srsgpu_rxq {
         pos++;
       }
       if (!flush_run(reg.size())) return false;
-      if (ndma > 1)
-        for (int k = 0; k < ndma; k++)
-          if (hipEventRecord(dev_[k], dst_[k]) != hipSuccess || hipStreamWaitEvent(cst, dev_[k], 0) != hipSuccess)
-            return false;
     }
     const bool kernel = sc16 || nst < rows;
     if (kernel) {
@@ -628,7 +590,7 @@ struct srsgpu_rxq {
       const double te = now_s();
       l.lock();
       tm[6] += te - ts;
-      if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed\n");
+      if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed: %s\n", hipGetErrorString(hipGetLastError()));
       slot[s].state = STAGED;
       ready.push_back(ok ? s : -1 - s);
       cv_ready.notify_one();
@@ -654,6 +616,7 @@ struct srsgpu_rxq {
       if (!r) r = enqueue(sl, b, sl.d_td);
       if (!r) r = hipEventRecord(sl.done, st) == hipSuccess ? 0 : -1;
       // a failed batch may have left work in flight that reads its buffers: drain before reuse
+      if (r && tag >= 0) fprintf(stderr, "srsgpu rxq: dispatch failed: %s\n", hipGetErrorString(hipGetLastError()));
       if (r) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamSynchronize(cst);
@@ -679,7 +642,11 @@ struct srsgpu_rxq {
       double w = 0, c = 0;
       if (!sl.r) {
         const double t0 = now_s();
-        if (hipEventSynchronize(sl.done) != hipSuccess) sl.r = -1;
+        const hipError_t e = hipEventSynchronize(sl.done);
+        if (e != hipSuccess) {
+          sl.r = -1;
+          fprintf(stderr, "srsgpu rxq: batch wait: %s\n", hipGetErrorString(e));
+        }
         const double t1 = now_s();
         if (!sl.r) complete(sl);
         w = t1 - t0;
