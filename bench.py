@@ -424,7 +424,7 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedul
 
 
 def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None,
-                standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1):
+                standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1, tail=0):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
@@ -447,7 +447,10 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     rotate R > 1: successive steps cycle through R descriptor sets with different softbuffers
     (MixedCells rotate), so the PDSCH / DL-SCH repeat-call caches never hit and every step pays the
     per-code-block host work a receiver with changing grants pays. host_ms_per_step is the host
-    time spent inside the step calls (enqueue side; the GPU runs asynchronously)."""
+    time spent inside the step calls (enqueue side; the GPU runs asynchronously).
+    tail 1 / 2: each lane alternates between two DL-SCH engines whose early-stop tails run on a tail
+    stream (srsgpu_dlsch_set_tail_stream; 1: one tail stream shared by the lanes, 2: one per lane), so
+    a lane's next batch starts while the last one's straggling code blocks finish."""
     import srsgpu_shard as sh
     import srsgpu_traffic as tr
     rank = dist.get_rank() if dist else 0
@@ -469,9 +472,12 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     ms = []
     for li in range(lanes):
         st = (lane_stream(torch, dev, li) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
+        tk = {}
+        if tail:
+            tk = dict(engines=2, tail_stream=lane_stream(torch, dev, "tail" if tail == 1 else "tail%d" % li).cuda_stream)
         ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
                                 keep=mine[li::lanes], standard_rate=standard_rate, early_stop=early_stop,
-                                rotate=rotate, **kw))  # one plan: the same seed everywhere
+                                rotate=rotate, **tk, **kw))  # one plan: the same seed everywhere
     torch.cuda.synchronize()
 
     def step():
@@ -1498,6 +1504,14 @@ def main():
         # the worst-case processing rate on real codewords
         extra["fixed8"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
                                                   snr_db=HEADLINE_SNR_DB, dist=dist, early_stop=False))
+    if "tailab" in legs:
+        # the headline workload with the early-stop tails on tail streams (two engines per lane)
+        for t in (0, 1, 2, 0):
+            r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
+                            tail=t, lanes=args.lanes)
+            extra.setdefault("tailab", []).append({"tail": t, "ms_per_batch": r["ms_per_batch"],
+                                                   "decoded_mbps": r["decoded_mbps"], "acked_tbs": r["acked_tbs"],
+                                                   "tbs_bytes_ok": r["tbs_bytes_ok"]})
     if "uncached" in legs:
         # the headline workload with a different descriptor set every step (4 sets: other softbuffers),
         # so the PDSCH / DL-SCH repeat-call caches never hit: the host cost of changing grants
@@ -1600,6 +1614,8 @@ def main():
             result["c3_fft1536"] = extra["n1536"]
         if "uncached" in extra:
             result["c3_uncached"] = extra["uncached"]
+        if "tailab" in extra:
+            result["tail_ab"] = extra["tailab"]
         if pipe:
             result["config"]["subframes_per_s_random_symbols_fixed8"] = pipe["subframes_per_s"]
             result["pipeline"] = pipe

@@ -212,7 +212,9 @@ struct DlschEngine {
   }
 
   void destroy() {
+    if (tail_st) (void)hipStreamSynchronize(tail_st);
     if (st) (void)hipStreamSynchronize(st);
+    if (ev_tail) (void)hipEventDestroy(ev_tail);
     for (void *p : {(void *)soft, (void *)saved, (void *)cbcrc, (void *)fresh, (void *)d_items, (void *)d_tbs,
                     (void *)d_rows, (void *)d_cbmap, (void *)d_init, (void *)d_dec, (void *)d_ok,
                     (void *)d_noi, (void *)d_late, (void *)d_ret_stage, (void *)d_noi_stage, (void *)e_stage,
@@ -447,6 +449,19 @@ struct DlschEngine {
     memcpy(k.data() + n1 + 2 * n2, tail, sizeof(tail));
   }
 
+  // srsgpu_dlsch_set_tail_stream: the early-stop tail of a decode call runs on tail_st; the engine's
+  // next work on st waits for it (join_tail, at every entry point that enqueues work)
+  hipStream_t tail_st = nullptr;
+  hipEvent_t ev_tail = nullptr;
+  bool tail_pending = false;
+  int join_tail() {
+    if (tail_pending) {
+      HIPCHK(hipStreamWaitEvent(st, ev_tail, 0));
+      tail_pending = false;
+    }
+    return 0;
+  }
+
   int decode(const srsgpu_dlsch_tb_t *tb, uint32_t ntb, const int16_t *const *e_ptr,
              uint8_t *const *data_ptr, uint32_t maxh, int32_t *d_ret, uint32_t *d_noi_out) {
     if (ntb > cap) {
@@ -457,7 +472,9 @@ struct DlschEngine {
       fprintf(stderr, "srsgpu: max_halfits must be > 0\n");
       return -1;
     }
+    if (join_tail()) return -1;
     tdec.st = st;
+    tdec.split_st = tail_st;
     memo_key(memo_scratch, tb, ntb, e_ptr, data_ptr, maxh, d_ret, d_noi_out);
     if (memo.valid && memo_scratch == memo.key)
       return launch_decode(memo.ncb, memo.ndirect, memo.norder, memo.o_rows, memo.o_map, memo.o_tbs, memo.e_base,
@@ -663,14 +680,22 @@ struct DlschEngine {
         tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, norder, nullptr, 0,
                           d_rows_c, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed, ndirect ? &dc : nullptr))
       return -1;
+    // the epilogue on the stream the decoder job ended on (the tail stream when it split)
+    const hipStream_t es = tdec.st;
+    tdec.st = st;
     {
-      ProfScope ps("k_tb_finish", st);
-      HIPCHK(launch_tb_finish(d_tbs_c, (int)ntb, d_map_c, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, st,
+      ProfScope ps("k_tb_finish", es);
+      HIPCHK(launch_tb_finish(d_tbs_c, (int)ntb, d_map_c, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, es,
                               ndirect ? dc : DermCall{}, ndirect ? d_late : nullptr));
     }
     if (ndirect) { // rows of the direct blocks of failed TBs, for the retransmission
-      ProfScope ps("k_rows_late", st); // k_derm_late
-      HIPCHK(launch_derm_late(dc, (int)ncb, d_late, st));
+      ProfScope ps("k_rows_late", es); // k_derm_late
+      HIPCHK(launch_derm_late(dc, (int)ncb, d_late, es));
+    }
+    if (es != st) {
+      if (!ev_tail) HIPCHK(hipEventCreateWithFlags(&ev_tail, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(ev_tail, es));
+      tail_pending = true;
     }
     return 0;
   }
@@ -711,24 +736,32 @@ void srsgpu_dlsch_destroy(srsgpu_dlsch_t *q) {
 }
 
 void srsgpu_dlsch_set_stream(srsgpu_dlsch_t *q, void *s) {
-  if (q) q->e.st = (hipStream_t)s;
+  if (!q) return;
+  q->e.st = (hipStream_t)s;
+  (void)q->e.join_tail(); // a pending tail: the new stream waits for it
+}
+
+int srsgpu_dlsch_set_tail_stream(srsgpu_dlsch_t *q, void *s) {
+  if (!q || q->e.join_tail()) return -1;
+  q->e.tail_st = (hipStream_t)s;
+  return 0;
 }
 
 int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t slot) {
-  return q ? q->e.reset(slot, 1, q->e.max_cb) : -1;
+  return q && !q->e.join_tail() ? q->e.reset(slot, 1, q->e.max_cb) : -1;
 }
 
 int srsgpu_dlsch_softbuffer_reset_range(srsgpu_dlsch_t *q, uint32_t first, uint32_t count) {
-  return q ? q->e.reset(first, count, q->e.max_cb) : -1;
+  return q && !q->e.join_tail() ? q->e.reset(first, count, q->e.max_cb) : -1;
 }
 
 int srsgpu_dlsch_softbuffer_reset_list(srsgpu_dlsch_t *q, const uint32_t *slots, const uint32_t *ncb, uint32_t n) {
-  if (!q || (!slots && n)) return -1;
+  if (!q || (!slots && n) || q->e.join_tail()) return -1;
   return q->e.reset_list(slots, ncb, n);
 }
 
 int srsgpu_dlsch_softbuffer_reset_tbs(srsgpu_dlsch_t *q, uint32_t slot, uint32_t tbs) {
-  if (!q) return -1;
+  if (!q || q->e.join_tail()) return -1;
   const uint32_t n = (tbs + 24) / 6120 + 1; // softbuffer.c:113-116
   return q->e.reset(slot, 1, n < q->e.max_cb ? n : q->e.max_cb);
 }
@@ -766,7 +799,7 @@ int srsgpu_dlsch_decode_out_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, 
 static int ulsch_deinterleave(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, uint32_t ntb, const int16_t *d_q,
                               int16_t *d_g) {
   DlschEngine &E = q->e;
-  if (ntb > E.cap) return -1;
+  if (ntb > E.cap || E.join_tail()) return -1;
   for (uint32_t i = 0; i < ntb; i++) {
     const uint32_t Qm = tb[i].Qm, ns = tb[i].nof_symb;
     if ((Qm != 2 && Qm != 4 && Qm != 6) || ns == 0 || tb[i].nof_bits % (Qm * ns)) {
@@ -839,7 +872,7 @@ int srsgpu_ulsch_uci_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, 
   if (!q || (!tb && ntb) || (!uci && ntb) || !d_q || !d_c || !d_g || !d_data || !d_ret || !d_noi || !d_uci) return -1;
   if (ntb == 0) return 0;
   DlschEngine &E = q->e;
-  if (ntb > E.cap) return -1;
+  if (ntb > E.cap || E.join_tail()) return -1;
   std::vector<srsgpu::UlItem> it(ntb);
   uint32_t max_bits = 0;
   for (uint32_t i = 0; i < ntb; i++) {
@@ -937,7 +970,8 @@ int srsgpu_ulsch_uci_decode_dev(srsgpu_dlsch_t *q, const srsgpu_ulsch_tb_t *tb, 
   if (!E.d_uci_ret) HIPCHK(hipMalloc(&E.d_uci_ret, sizeof(int32_t) * 2 * E.cap));
   int32_t *r_tmp = E.d_uci_ret;
   uint32_t *n_tmp = (uint32_t *)(r_tmp + E.cap);
-  if (q->e.decode(dl.data(), (uint32_t)dl.size(), e.data(), d.data(), maxh, r_tmp, n_tmp)) return -1;
+  if (q->e.decode(dl.data(), (uint32_t)dl.size(), e.data(), d.data(), maxh, r_tmp, n_tmp) || E.join_tail())
+    return -1; // (the scatter below reads what the tail wrote)
   for (size_t k = 0; k < dl.size(); k++) {
     HIPCHK(hipMemcpyAsync(d_ret + idx[k], r_tmp + k, 4, hipMemcpyDeviceToDevice, E.st));
     HIPCHK(hipMemcpyAsync(d_noi + idx[k], n_tmp + k, 4, hipMemcpyDeviceToDevice, E.st));
@@ -951,7 +985,7 @@ int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t
   if (!q || (!tb && ntb) || !e_bits || !data || !ret || !noi) return -1;
   if (ntb == 0) return 0;
   DlschEngine &E = q->e;
-  if (ntb > E.cap) return -1;
+  if (ntb > E.cap || E.join_tail()) return -1;
   size_t elen = 0, dlen = 0;
   for (uint32_t i = 0; i < ntb; i++) {
     elen += tb[i].nof_e_bits;
@@ -982,7 +1016,8 @@ int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t
   }
   HIPCHK(hipMemsetAsync(E.data_stage, 0, dlen, E.st));
   if (srsgpu_dlsch_decode_dev(q, t.data(), ntb, E.e_stage, E.data_stage, maxh, E.d_ret_stage,
-                              E.d_noi_stage))
+                              E.d_noi_stage) ||
+      E.join_tail()) // the copies below read what the tail wrote
     return -1;
   for (uint32_t i = 0; i < ntb; i++)
     HIPCHK(hipMemcpyAsync(data[i], E.data_stage + t[i].data_offset, SRSGPU_DLSCH_DATA_LEN(tb[i].tbs),
@@ -996,6 +1031,7 @@ int srsgpu_dlsch_decode(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t
 int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t slot, int16_t *rows, uint8_t *cb_crc) {
   if (!q || slot >= q->e.nslots) return -1;
   DlschEngine &E = q->e;
+  if (E.join_tail()) return -1;
   std::vector<uint8_t> fr(E.max_cb);
   HIPCHK(hipMemcpyAsync(fr.data(), E.fresh + (size_t)slot * E.max_cb, E.max_cb, hipMemcpyDeviceToHost, E.st));
   if (rows)
@@ -1013,7 +1049,7 @@ int srsgpu_dlsch_softbuffer_read(srsgpu_dlsch_t *q, uint32_t slot, int16_t *rows
 
 int srsgpu_dlsch_encode_dev(srsgpu_dlsch_t *q, const srsgpu_dlsch_tb_t *tb, uint32_t nof_tb,
                             const uint8_t *d_data, uint8_t *d_e_bits) {
-  if (!q || (!tb && nof_tb) || !d_data || !d_e_bits) return -1;
+  if (!q || (!tb && nof_tb) || !d_data || !d_e_bits || q->e.join_tail()) return -1;
   return q->e.encode(tb, nof_tb, d_data, d_e_bits);
 }
 

@@ -100,6 +100,10 @@ struct TdecEngine {
   // second stream of the fused early stop: the SSE kind beside the window kinds
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // tail stream (srsgpu_dlsch_set_tail_stream): under the hybrid early-stop schedule, everything after
+  // the first half-iteration's k_decide moves to split_st (st is switched for the rest of the call)
+  hipStream_t split_st = nullptr;
+  hipEvent_t ev_split = nullptr;
   bool gev_pending = false;
   int kind_g0[TD_NKIND + 1] = {0};
   int kind_blocks[TD_NKIND] = {0};
@@ -165,7 +169,7 @@ struct TdecEngine {
     if (h_groups) (void)hipHostFree(h_groups);
     if (gev) (void)hipEventDestroy(gev);
     if (aux) (void)hipStreamSynchronize(aux);
-    for (hipEvent_t e : {ev_fork, ev_join})
+    for (hipEvent_t e : {ev_fork, ev_join, ev_split})
       if (e) (void)hipEventDestroy(e);
     if (aux) (void)hipStreamDestroy(aux);
     for (auto &kv : crc_tables) (void)hipFree(kv.second);
@@ -633,6 +637,14 @@ struct TdecEngine {
           HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
         }
         if (decide(0, d_out, out_stride, true, maxh)) return -1;
+        if (split_st && split_st != st) {
+          // the few blocks still running, their bytes and the caller's epilogue on the tail stream:
+          // the caller's stream goes on with its next work meanwhile
+          if (!ev_split) HIPCHK(hipEventCreateWithFlags(&ev_split, hipEventDisableTiming));
+          HIPCHK(hipEventRecord(ev_split, st));
+          HIPCHK(hipStreamWaitEvent(split_st, ev_split, 0));
+          st = split_st;
+        }
         es.n0 = 1;
         es.n1 = (int)maxh;
         for (int k = 0; k < TD_NKIND; k++) {

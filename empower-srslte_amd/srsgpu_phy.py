@@ -402,6 +402,7 @@ _sig = {
     "srsgpu_rxq_decode_rnti": (_i32, [_vp, _vp]),
     "srsgpu_rxq_set_phich": (_i32, [_vp, _u32, _u32]),
     "srsgpu_dlsch_set_early_stop": (None, [_vp, _i32]),
+    "srsgpu_dlsch_set_tail_stream": (_i32, [_vp, _vp]),
     "srsgpu_dlsch_set_llr_8bit": (None, [_vp, _i32]),
     "srsgpu_dlsch_set_direct_derm": (None, [_vp, _i32]),
     "srsgpu_rm_turbo_rx_8bit_dev": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32]),
@@ -632,6 +633,12 @@ class Dlsch:
     def set_early_stop(self, on):
         """srsgpu_dlsch_set_early_stop (off: every CB runs max_halfits, one CRC check at the end)"""
         _lib.srsgpu_dlsch_set_early_stop(self.q, int(bool(on)))
+
+    def set_tail_stream(self, stream):
+        """srsgpu_dlsch_set_tail_stream: the early-stop tail of each decode call on `stream` (a HIP
+        stream handle, 0 = off)"""
+        if _lib.srsgpu_dlsch_set_tail_stream(self.q, _vp(stream or None)) != 0:
+            raise RuntimeError("srsgpu_dlsch_set_tail_stream failed")
 
     def set_direct_derm(self, on):
         """srsgpu_dlsch_set_direct_derm (off: every softbuffer row written before the decode)"""

@@ -66,7 +66,7 @@ def tb_weights(table, sf_plan, max_halfits=8):
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
                  snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None, standard_rate=True,
-                 early_stop=True, ce_rows=True, rotate=1):
+                 early_stop=True, ce_rows=True, rotate=1, engines=1, tail_stream=None):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
         traffic). keep: the subframe indices this instance builds and receives (a rank's shard
@@ -78,7 +78,12 @@ class MixedCells:
         rotate R > 1: R descriptor sets that differ in their softbuffers (set r uses softbuffers
         r * ntb ..), used in turn by successive steps, so no two consecutive calls of the PDSCH and
         DL-SCH stages repeat their inputs and their repeat-call caches never hit, as for a receiver
-        whose grants change every subframe."""
+        whose grants change every subframe.
+        engines 2 with tail_stream (a HIP stream handle): two DL-SCH engines (each with its own LLR,
+        output and softbuffer sets) used by alternate steps, each decoding its early-stop tail on
+        tail_stream (srsgpu_dlsch_set_tail_stream): a step's front end and first half-iteration run
+        while the previous step's few straggling code blocks finish beside them. The attributes dlsch,
+        d_e, d_data, d_ret, d_noi name the engine of the last step."""
         self.torch, self.dev = torch, dev
         self.max_halfits = max_halfits
         sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
@@ -138,15 +143,21 @@ class MixedCells:
             for r in range(1, self.rotate)]
         self.ncb = sum(int(table["cbsegm_C_C1_K1_C2_K2_F"][str(t["tbs"])][0]) for t in tb_list)
         self.bits = sum(t["tbs"] for t in tb_list)
-        self.dlsch = s.Dlsch(max(self.ntb * self.rotate, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
-        self.dlsch.set_early_stop(early_stop)
+        self.nengine, self.eng = max(1, int(engines)), 0
         z = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
-        self.d_e = z(max(e_off, 1), torch.int16)
+        self._dl, self._de, self._dd, self._dr, self._dn = [], [], [], [], []
+        for _ in range(self.nengine):
+            dl = s.Dlsch(max(self.ntb * self.rotate, 1), max_cb=13, max_cbs_per_call=max(self.ncb, 1), stream=stream)
+            dl.set_early_stop(early_stop)
+            if tail_stream and self.nengine > 1:
+                dl.set_tail_stream(tail_stream)
+            self._dl.append(dl)
+            self._de.append(z(max(e_off, 1), torch.int16))
+            self._dd.append(z(max(d_off, 1), torch.uint8))
+            self._dr.append(z(self.ntb, torch.int32))
+            self._dn.append(z(self.ntb, torch.int32))
         self.d_data_tx = torch.randint(0, 256, (max(d_off, 1),), dtype=torch.uint8, device=dev,
                                        generator=torch.Generator(device=dev).manual_seed(seed))
-        self.d_data = z(max(d_off, 1), torch.uint8)
-        self.d_ret = z(self.ntb, torch.int32)
-        self.d_noi = z(self.ntb, torch.int32)
         for c in self.cells:
             n, gsz, N = c["n"], c["gsz"], c["N"]
             c["grid"] = z(n * gsz, torch.complex64)
@@ -155,6 +166,12 @@ class MixedCells:
             c["x"] = z(n * 15 * N, torch.complex64)
             c["pd"].set_noise_dev(c["noise"].data_ptr())
         self._transmit(snr_db, seed)
+
+    dlsch = property(lambda self: self._dl[self.eng])
+    d_e = property(lambda self: self._de[self.eng])
+    d_data = property(lambda self: self._dd[self.eng])
+    d_ret = property(lambda self: self._dr[self.eng])
+    d_noi = property(lambda self: self._dn[self.eng])
 
     def _transmit(self, snr_db, seed):
         torch = self.torch
@@ -192,6 +209,7 @@ class MixedCells:
         """one receive batch; host_s accumulates the host (enqueue) seconds of the front end and of the
         DL-SCH call"""
         self.cur = (self.cur + 1) % self.rotate
+        self.eng = (self.eng + 1) % self.nengine
         t0 = time.perf_counter()
         self.front_end()
         t1 = time.perf_counter()
@@ -235,8 +253,8 @@ class MixedCells:
         for c in self.cells:
             for k in ("ofdm", "chest", "pd"):
                 c[k].close()
-        self.dlsch.close()
-
+        for dl in self._dl:
+            dl.close()
 
 
 class MimoSubframes:

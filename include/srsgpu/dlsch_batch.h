@@ -115,6 +115,13 @@ void srsgpu_dlsch_set_llr_8bit(srsgpu_dlsch_t *q, int enable);
  * half-iterations and its CRC is checked once after the last (the fixed-iteration processing rate
  * on real codewords; nof_iterations then reports max_halfits). */
 void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable);
+/* Tail stream (no reference counterpart; NULL = off, the default): under early stop, each decode
+ * call's work after the first half-iteration and its CRC check (the few code blocks still running,
+ * their bytes, the TB CRC and the epilogue of sch.c:393-491) goes to `hip_stream`, and the call's
+ * results (TB bytes, d_ret, d_noi, softbuffers) are final when that stream reaches them. The engine's
+ * own stream is free for the caller's next work meanwhile (e.g. the next batch's front end into
+ * another engine); the next call into this engine makes its stream wait for the tail first. */
+int srsgpu_dlsch_set_tail_stream(srsgpu_dlsch_t *q, void *hip_stream);
 /* Direct de-rate-matching (default on). Code blocks of the window decoders (K > 400 under AUTO)
  * are de-rate-matched and HARQ-combined straight into the decoder's inputs, and their softbuffer
  * rows are written after the decode only when their TB failed (every block not decoded before
