@@ -1314,7 +1314,6 @@ LEG_SUMMARY = (
     ("c3_fft1536", "n1536", ("subframes_per_s", "decoded_mbps")),
     ("pipeline", "c3_random_fixed8", ("subframes_per_s",)),
     ("pipeline_tm3", "tm3_random_fixed8", ("subframes_per_s",)),
-    ("decoder_8bit", "decoder_8bit", ("mbps", "bit_errors")),
     ("pdcch", "pdcch", ("subframes_per_s",)),
     ("pcfich", "pcfich", ("subframes_per_s",)),
     ("pdcch_dci", "dci", ("candidates_per_s",)),
@@ -1504,6 +1503,19 @@ def main():
         # the worst-case processing rate on real codewords
         extra["fixed8"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
                                                   snr_db=HEADLINE_SNR_DB, dist=dist, early_stop=False))
+    if "envab" in legs:
+        # the headline workload with and without an environment setting (BENCH_AB_ENV="NAME=VALUE"), in
+        # turn in one process: A/B of a kernel variant the library reads from the environment per call
+        name, _, val = os.environ.get("BENCH_AB_ENV", "SRSGPU_LLR_GENERIC=1").partition("=")
+        for on in (0, 1, 0, 1, 0, 1):
+            if on:
+                os.environ[name] = val
+            r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
+                            lanes=args.lanes)
+            os.environ.pop(name, None)
+            extra.setdefault("envab", []).append({name: val if on else None, "ms_per_batch": r["ms_per_batch"],
+                                                  "stage_ms": r["stage_ms_per_batch"], "acked_tbs": r["acked_tbs"],
+                                                  "tbs_bytes_ok": r["tbs_bytes_ok"]})
     if "tailab" in legs:
         # the headline workload with the early-stop tails on tail streams (two engines per lane)
         for t in (0, 1, 2, 0):
@@ -1616,6 +1628,8 @@ def main():
             result["c3_uncached"] = extra["uncached"]
         if "tailab" in extra:
             result["tail_ab"] = extra["tailab"]
+        if "envab" in extra:
+            result["env_ab"] = extra["envab"]
         if pipe:
             result["config"]["subframes_per_s_random_symbols_fixed8"] = pipe["subframes_per_s"]
             result["pipeline"] = pipe

@@ -315,6 +315,7 @@ struct PdschEngine {
   bool memo_valid = false;
   uint32_t memo_k = 0, memo_mre = 0;
   int memo_ndual = 0;
+  int memo_p0 = 0; // nof_rx_ant when every item equalises port 0 alone (k_pdsch_llr_p0), else 0
 
   int llr(const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid, const float *d_ce,
           size_t ant_stride, int16_t *const *e_ptr) {
@@ -334,7 +335,7 @@ struct PdschEngine {
       if (memo_valid && memo_scratch == memo_key) {
         if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)memo_k * 4, st));
         ProfScope ps("k_pdsch_llr", st);
-        HIPCHK(launch_pdsch_llr(d_llr, (int)memo_k, memo_mre, csi, st, memo_ndual));
+        HIPCHK(launch_pdsch_llr(d_llr, (int)memo_k, memo_mre, csi, st, memo_ndual, memo_p0));
         return 0;
       }
       memo_valid = false;
@@ -342,6 +343,7 @@ struct PdschEngine {
     if (ring_take()) return -1;
     uint32_t mre = 0, k = 0;
     int n_dual = 0;
+    bool p0 = true;
     gold_slot.clear();
     ngold = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -384,6 +386,7 @@ struct PdschEngine {
           t.mux = nt == 2 ? 1 + (int)s.codebook_idx : -(1 + (int)s.codebook_idx);
         t.txdiv = s.mimo_type == SRSGPU_MIMO_TX_DIVERSITY ? (int)cell.nof_ports : 0;
         t.layer = (int)cw;
+        p0 = p0 && !t.cdd && !t.mux && !t.txdiv;
         t.csi_mode = csi ? 1 : 0;
         t.llr8 = llr8 ? 1 : 0;
         t.ce_rows = ce_rows;
@@ -412,11 +415,12 @@ struct PdschEngine {
       HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
     }
     ProfScope ps("k_pdsch_llr", st);
-    HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual));
+    HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual, p0 && cell.nof_rx_ant <= 2 ? (int)cell.nof_rx_ant : 0));
     memo_key.swap(memo_scratch);
     memo_k = k;
     memo_mre = mre;
     memo_ndual = n_dual;
+    memo_p0 = p0 && cell.nof_rx_ant <= 2 ? (int)cell.nof_rx_ant : 0;
     memo_valid = true;
     return 0;
   }

@@ -62,9 +62,12 @@ struct TxItem {
 
 hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const uint32_t *x1,
                        const uint32_t *x2b, uint32_t words, hipStream_t st);
-// n_dual: pairs of items with dual = 1 / 2 (both layers of a 2-layer MMSE subframe from one solve)
+// n_dual: pairs of items with dual = 1 / 2 (both layers of a 2-layer MMSE subframe from one solve);
+// p0 = nof_rx_ant (1 / 2) when every item equalises CRS port 0 alone (no transmit diversity, CDD or
+// spatial multiplexing), else 0: the kernel specialised for it, with the multi-port paths compiled
+// out and the antenna count fixed (fewer registers)
 hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st,
-                            int n_dual = 0);
+                            int n_dual = 0, int p0 = 0);
 // tables: 2 BPSK + 4 QPSK + 16 16QAM + 64 64QAM constellation points (lte_tables.c order)
 hipError_t launch_pdsch_tx(const TxItem *d_items, int n, uint32_t max_re, const float2 *tables,
                            hipStream_t st);

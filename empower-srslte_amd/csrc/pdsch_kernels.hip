@@ -20,6 +20,7 @@
 // since x2 is linear in its seed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "pdsch_kernels.h"
 #include "srsgpu/pdsch_batch.h"
@@ -110,11 +111,13 @@ __device__ __forceinline__ float2 ce_at(const LlrItem &t, const float2 *h, uint3
   return c;
 }
 
+// NRX: the receive antennas when known at compile time (0: t.nrx)
+template <int NRX = 0>
 __device__ __forceinline__ ReIn load_re(const LlrItem &t, uint32_t pos, bool two_ports) {
   ReIn in;
 #pragma unroll
   for (int a = 0; a < 2; a++) {
-    if (a == 1 && t.nrx < 2) break;
+    if (a == 1 && (NRX ? NRX : t.nrx) < 2) break;
     in.y[a] = gmem(t.y[a])[pos];
     in.h[0][a] = ce_at(t, t.h[0][a], pos);
     if (two_ports) in.h[1][a] = ce_at(t, t.h[1][a], pos);
@@ -122,7 +125,9 @@ __device__ __forceinline__ ReIn load_re(const LlrItem &t, uint32_t pos, bool two
   return in;
 }
 
+template <int NRX = 0>
 __device__ __forceinline__ Eq equalise(const LlrItem &t, const ReIn &in, uint32_t j) {
+  const int nrx = NRX ? NRX : t.nrx;
   Eq e;
   if (!t.csi_mode && (t.nof_re <= 32 || j >= 16 * (t.nof_re / 16))) { // AVX only above 32 (:330)
     // symbols after the last whole 16 take the reference's C path (precoding.c:231-240), whose
@@ -130,7 +135,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, const ReIn &in, uint32_
     // then r / ((hh + n0) * scaling)
     float hh = 0.f, rr = 0.f, ri = 0.f;
     for (int a = 0; a < 2; a++) {
-      if (a == 1 && t.nrx < 2) break;
+      if (a == 1 && nrx < 2) break;
       const float2 y = in.y[a], h = in.h[0][a];
       const double yr = y.x, yi = y.y, hr = h.x, hi = h.y;
       rr = (float)__dadd_rn((double)rr, __dsub_rn(__dmul_rn(yr, hr), __dmul_rn(yi, -hi)));
@@ -145,7 +150,7 @@ __device__ __forceinline__ Eq equalise(const LlrItem &t, const ReIn &in, uint32_
   }
   float hh = 0.f, rr = 0.f, ri = 0.f;
   for (int a = 0; a < 2; a++) {
-    if (a == 1 && t.nrx < 2) break;
+    if (a == 1 && nrx < 2) break;
     const float2 y = in.y[a], h = in.h[0][a];
     // |h|^2 as hadd(h*h) (precoding.c:179-187), antenna sums in order
     hh = __fadd_rn(hh, __fadd_rn(__fmul_rn(h.x, h.x), __fmul_rn(h.y, h.y)));
@@ -581,12 +586,14 @@ __device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &
 // two round trips per LLR_RES REs instead of per RE (one RE per thread left the kernel at ~1.5 TB/s,
 // bound by the dependent map -> grid load chain). TM2 pairs REs across the map and keeps the
 // one-RE loop.
+// P0: the call's items all equalise port 0 alone (k_pdsch_llr_p0): the other equalisers are not
+// compiled in, so the kernel's register budget is the single-port one.
 #define LLR_RES 4
-template <int MOD>
+template <int MOD, bool P0 = false, int NRX = 0>
 __device__ __forceinline__ void llr_body(const LlrItem &t) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
   const uint32_t stride = gridDim.x * 256;
-  if (t.txdiv) {
+  if (!P0 && t.txdiv) {
     for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += stride) {
       const uint32_t w = (j * Q) >> 5;
       llr_out<MOD>(t, j, t.txdiv == 4 ? equalise_txdiv4(t, j) : equalise_txdiv(t, j), gmem(t.c)[w],
@@ -594,7 +601,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     }
     return;
   }
-  const bool two_ports = t.cdd || t.mux != 0;
+  const bool two_ports = !P0 && (t.cdd || t.mux != 0);
   for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
     uint32_t pos[LLR_RES];
 #pragma unroll
@@ -608,7 +615,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     for (int r = 0; r < LLR_RES; r++) {
       const uint32_t j = j0 + r * stride;
       const uint32_t w = ((j < t.nof_re ? j : j0) * Q) >> 5;
-      in[r] = load_re(t, pos[r], two_ports);
+      in[r] = load_re<NRX>(t, pos[r], two_ports);
       c0[r] = gmem(t.c)[w];
       c1[r] = gmem(t.c)[w + 1];
     }
@@ -616,7 +623,8 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     for (int r = 0; r < LLR_RES; r++) {
       const uint32_t j = j0 + r * stride;
       if (j >= t.nof_re) break;
-      const Eq e = (t.cdd || t.mux > 0) ? equalise_cdd(t, in[r], j)
+      const Eq e = P0                   ? equalise<NRX>(t, in[r], j)
+                   : (t.cdd || t.mux > 0) ? equalise_cdd(t, in[r], j)
                    : t.mux < 0          ? equalise_mrc(t, in[r])
                                         : equalise(t, in[r], j);
       llr_out<MOD>(t, j, e, c0[r], c1[r]);
@@ -703,6 +711,22 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
   }
 }
 
+// the same for calls whose items all equalise port 0 alone (SISO / receive diversity on port 0),
+// NRX receive antennas
+template <int NRX>
+__global__ __launch_bounds__(256) void k_pdsch_llr_p0(const LlrItem *__restrict__ items, int nitems) {
+  const int it = blockIdx.y;
+  if (it >= nitems) return;
+  LlrItem t = items[it];
+  llr_item_fix(t);
+  switch (t.mod) {
+  case 0: llr_body<0, true, NRX>(t); break;
+  case 1: llr_body<1, true, NRX>(t); break;
+  case 2: llr_body<2, true, NRX>(t); break;
+  default: llr_body<3, true, NRX>(t); break;
+  }
+}
+
 // both TBs of a 2-layer MMSE subframe (item it with dual = 1 and item it + 1) from one solve per
 // RE; a kernel of its own, so the single-TB kernel keeps its smaller register budget
 __global__ __launch_bounds__(256) void k_pdsch_llr2(const LlrItem *__restrict__ items, int nitems) {
@@ -780,10 +804,16 @@ hipError_t launch_gold(const GoldItem *d_items, int n, uint32_t max_len, const u
 }
 
 hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool csi, hipStream_t st,
-                            int n_dual) {
+                            int n_dual, int p0) {
   if (n <= 0) return hipSuccess;
   const unsigned gx = std::min(cdiv(max_re, 256 * LLR_RES), 64u);
-  if (n > 2 * n_dual)
+  const bool generic = getenv("SRSGPU_LLR_GENERIC") != nullptr; // A/B: the general kernel only
+  if (p0 && !n_dual && !generic) {
+    if (p0 == 1)
+      hipLaunchKernelGGL(k_pdsch_llr_p0<1>, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+    else
+      hipLaunchKernelGGL(k_pdsch_llr_p0<2>, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+  } else if (n > 2 * n_dual)
     hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
   if (n_dual > 0)
     hipLaunchKernelGGL(k_pdsch_llr2, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
