@@ -998,8 +998,7 @@ ALG_BYTES_PER_SF = {
 }
 HEADLINE_SNR_DB = 20.0
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
-HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 1}, "per_halfit": {"es_fused": 0},
-               "fused_c1": {"es_fused": 1, "es_chunk": 1}, "fused_c2": {"es_fused": 1, "es_chunk": 2},
+HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 8}, "per_halfit": {"es_fused": 0},
                "fused_c8": {"es_fused": 1, "es_chunk": 8}, "hybrid": {"es_fused": 3, "es_chunk": 8}}
 
 

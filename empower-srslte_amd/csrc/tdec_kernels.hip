@@ -560,6 +560,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
 
   // ---- checkpoints in LDS: [slot][half][lane] x 16 B (conflict-free b128 accesses)
   auto ck_put = [&](int slot, const St8 &o) {
+#ifdef TD_EXP_HALFLDS
+    slot >>= 1; // timing experiment only (wrong results): half the checkpoint slots, aliased
+#endif
     s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
     p[0] = s4{o.s[0].x, o.s[0].y, o.s[1].x, o.s[1].y};
     p[1] = s4{o.s[2].x, o.s[2].y, o.s[3].x, o.s[3].y};
@@ -568,6 +571,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
     q[1] = s4{o.s[6].x, o.s[6].y, o.s[7].x, o.s[7].y};
   };
   auto ck_get = [&](int slot, St8 &o) {
+#ifdef TD_EXP_HALFLDS
+    slot >>= 1;
+#endif
     const s4 *p = &cks[((slot * 2) * 64 + lane) * 2];
     const s4 *q = &cks[((slot * 2 + 1) * 64 + lane) * 2];
     s4 a = p[0], b = p[1], c = q[0], e = q[1];
@@ -983,8 +989,11 @@ __device__ __forceinline__ WinRes win_res(const TdGroup &G, int K, int blk, int 
   return R;
 }
 
+#ifndef TD_BIDIR_WAVES
+#define TD_BIDIR_WAVES 1 // minimum waves per SIMD the windowed decoders are compiled for
+#endif
 template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
-__global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
+__global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                    const s2 *__restrict__ T, size_t plane,
@@ -1039,7 +1048,7 @@ __global__ __launch_bounds__(128) void k_win_bidir(const TdGroup *__restrict__ g
 // end-of-kernel skew go. Decisions only after the last half-iteration (early stop keeps the
 // per-half-iteration launches and k_decide between them). Arithmetic identical to k_win_bidir.
 template <int NB, int DIV, bool B8>
-__global__ __launch_bounds__(128) void k_win_bidir_run(const TdGroup *__restrict__ groups, int ngroups,
+__global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_run(const TdGroup *__restrict__ groups, int ngroups,
                                                        const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                        s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                        const s2 *__restrict__ T, size_t plane, int n0,
@@ -1224,7 +1233,7 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
 // Blocks done at entry (HARQ retransmissions whose CRC passed before, cb_done seeded) are
 // skipped; a partly finished workgroup decodes on, its finished blocks' results stay frozen.
 template <int NB, int DIV, bool B8>
-__global__ __launch_bounds__(128) void k_win_bidir_es(const TdGroup *__restrict__ groups, int ngroups,
+__global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGroup *__restrict__ groups, int ngroups,
                                                       const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                       s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                       const s2 *__restrict__ T, size_t plane, TdEs es) {
@@ -2465,6 +2474,9 @@ size_t seq_scratch_elems(int K, int npairs) { return (size_t)(K + 4) * 8 * npair
 
 
 size_t bidir_lds_bytes(int K, int nb) {
+#ifdef TD_EXP_HALFLDS
+  return (size_t)(((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) / 2 + 1) * 2 * 64 * 16;
+#endif
   return (size_t)((K / nb + TD_BIDIR_CW - 1) / TD_BIDIR_CW + 1) * 2 * 64 * 16;
 }
 

@@ -22,9 +22,13 @@ def _results(m):
     return ret, noi, data, crc
 
 
+@pytest.mark.parametrize("es_fused", [3])
 @pytest.mark.parametrize("snr_db", [14.0, 16.5, 20.0])
-def test_tail_stream_equals_single_stream(snr_db):
+def test_tail_stream_equals_single_stream(snr_db, es_fused):
+    """es_fused 3 (hybrid: first half-iteration, k_decide, the rest in one early-stop launch, as the
+    headline's batches run): the split comes after the first half-iteration's k_decide"""
     import torch
+    import srsgpu_phy as s
     import srsgpu_traffic as tr
     dev = torch.device("cuda:0")
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
@@ -34,9 +38,11 @@ def test_tail_stream_equals_single_stream(snr_db):
     ref = tr.MixedCells(table, 96, torch, dev, stream=main.cuda_stream, **kw)
     two = tr.MixedCells(table, 96, torch, dev, stream=main.cuda_stream, engines=2, tail_stream=tail.cuda_stream, **kw)
     torch.cuda.synchronize()
-    ref.step()
+    ref.step()  # default schedule (auto: this small job runs fused)
     torch.cuda.synchronize()
     want = _results(ref)
+    keep = s.get_schedule()
+    s.set_schedule(es_fused=es_fused, es_chunk=8)
     # 14 dB: every TB fails (the failed TBs' deferred rows, k_derm_late, run in the tail); 16.5 dB: mixed
     for k in range(4):  # both engines twice, back to back without a host wait between the steps
         two.step()
@@ -48,5 +54,6 @@ def test_tail_stream_equals_single_stream(snr_db):
                     assert (a == b).all(), (k, e)
             two.eng = 0
     torch.cuda.synchronize()
+    s.set_schedule(**keep)
     ref.close()
     two.close()
