@@ -589,12 +589,13 @@ __device__ __forceinline__ void llr_out(const LlrItem &t, uint32_t j, const Eq &
 // P0: the call's items all equalise port 0 alone (k_pdsch_llr_p0): the other equalisers are not
 // compiled in, so the kernel's register budget is the single-port one.
 #define LLR_RES 4
+// part / nparts: this workgroup's share of the item's REs (the RE loop strides over nparts x 256)
 template <int MOD, bool P0 = false, int NRX = 0>
-__device__ __forceinline__ void llr_body(const LlrItem &t) {
+__device__ __forceinline__ void llr_body(const LlrItem &t, uint32_t part, uint32_t nparts) {
   constexpr int Q = MOD == 0 ? 1 : MOD == 1 ? 2 : MOD == 2 ? 4 : 6;
-  const uint32_t stride = gridDim.x * 256;
+  const uint32_t stride = nparts * 256;
   if (!P0 && t.txdiv) {
-    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < t.nof_re; j += stride) {
+    for (uint32_t j = part * 256 + threadIdx.x; j < t.nof_re; j += stride) {
       const uint32_t w = (j * Q) >> 5;
       llr_out<MOD>(t, j, t.txdiv == 4 ? equalise_txdiv4(t, j) : equalise_txdiv(t, j), gmem(t.c)[w],
                    gmem(t.c)[w + 1]);
@@ -602,7 +603,7 @@ __device__ __forceinline__ void llr_body(const LlrItem &t) {
     return;
   }
   const bool two_ports = !P0 && (t.cdd || t.mux != 0);
-  for (uint32_t j0 = blockIdx.x * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
+  for (uint32_t j0 = part * 256 + threadIdx.x; j0 < t.nof_re; j0 += stride * LLR_RES) {
     uint32_t pos[LLR_RES];
 #pragma unroll
     for (int r = 0; r < LLR_RES; r++) {
@@ -704,26 +705,36 @@ __global__ __launch_bounds__(256) void k_pdsch_llr(const LlrItem *__restrict__ i
   if (t.dual) return;
   llr_item_fix(t);
   switch (t.mod) {
-  case 0: llr_body<0>(t); break;
-  case 1: llr_body<1>(t); break;
-  case 2: llr_body<2>(t); break;
-  default: llr_body<3>(t); break;
+  case 0: llr_body<0>(t, blockIdx.x, gridDim.x); break;
+  case 1: llr_body<1>(t, blockIdx.x, gridDim.x); break;
+  case 2: llr_body<2>(t, blockIdx.x, gridDim.x); break;
+  default: llr_body<3>(t, blockIdx.x, gridDim.x); break;
   }
 }
 
 // the same for calls whose items all equalise port 0 alone (SISO / receive diversity on port 0),
 // NRX receive antennas
+// XCD-aware: a 1-D grid in which an item's nparts workgroups all fall on one XCD (workgroups are dealt
+// round-robin over the 8 XCDs, so b and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"):
+// workgroup b serves item (b % 8) + 8 ((b / 8) / nparts), part (b / 8) % nparts. The item's estimate
+// rows, which every part re-reads for each OFDM symbol, then come from one XCD's L2 instead of up to
+// eight.
 template <int NRX>
-__global__ __launch_bounds__(256) void k_pdsch_llr_p0(const LlrItem *__restrict__ items, int nitems) {
-  const int it = blockIdx.y;
+// (xcd = 0: item b / nparts, part b % nparts, for the A/B)
+__global__ __launch_bounds__(256) void k_pdsch_llr_p0(const LlrItem *__restrict__ items, int nitems, int nparts,
+                                                      int xcd) {
+  const uint32_t b = blockIdx.x, idx = xcd ? b >> 3 : b;
+  const uint32_t per = idx / (uint32_t)nparts;
+  const int it = (int)(xcd ? (b & 7) + 8 * per : per);
   if (it >= nitems) return;
+  const uint32_t part = idx - per * (uint32_t)nparts;
   LlrItem t = items[it];
   llr_item_fix(t);
   switch (t.mod) {
-  case 0: llr_body<0, true, NRX>(t); break;
-  case 1: llr_body<1, true, NRX>(t); break;
-  case 2: llr_body<2, true, NRX>(t); break;
-  default: llr_body<3, true, NRX>(t); break;
+  case 0: llr_body<0, true, NRX>(t, part, nparts); break;
+  case 1: llr_body<1, true, NRX>(t, part, nparts); break;
+  case 2: llr_body<2, true, NRX>(t, part, nparts); break;
+  default: llr_body<3, true, NRX>(t, part, nparts); break;
   }
 }
 
@@ -809,10 +820,12 @@ hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool
   const unsigned gx = std::min(cdiv(max_re, 256 * LLR_RES), 64u);
   const bool generic = getenv("SRSGPU_LLR_GENERIC") != nullptr; // A/B: the general kernel only
   if (p0 && !n_dual && !generic) {
+    const int xcd = getenv("SRSGPU_LLR_NOXCD") ? 0 : 1; // A/B: the plain item-major mapping
+    const unsigned parts = gx ? gx : 1, nb = parts * ((unsigned)(n + 7) / 8) * 8; // items rounded up to 8
     if (p0 == 1)
-      hipLaunchKernelGGL(k_pdsch_llr_p0<1>, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+      hipLaunchKernelGGL(k_pdsch_llr_p0<1>, dim3(nb), dim3(256), 0, st, d_items, n, (int)parts, xcd);
     else
-      hipLaunchKernelGGL(k_pdsch_llr_p0<2>, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
+      hipLaunchKernelGGL(k_pdsch_llr_p0<2>, dim3(nb), dim3(256), 0, st, d_items, n, (int)parts, xcd);
   } else if (n > 2 * n_dual)
     hipLaunchKernelGGL(k_pdsch_llr, dim3(gx ? gx : 1, (unsigned)n), dim3(256), 0, st, d_items, n);
   if (n_dual > 0)
