@@ -15,6 +15,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <chrono>
@@ -815,6 +816,12 @@ struct srsgpu_rxq {
   static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
+  static double cpu_s() { // this thread's CPU time (SRSGPU_RXQ_TRACE: busy or waiting)
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+  }
+  const bool trace = getenv("SRSGPU_RXQ_TRACE") != nullptr;
   double run_tm[8] = {}; // the dispatcher's stage times of its last batch, added to tm under the lock
 
   // one batch, enqueued as a whole: OFDM of the staged samples, channel estimation and measurements,
@@ -987,8 +994,12 @@ struct srsgpu_rxq {
         srsgpu_pdsch_set_noise_dev(pdsch, d_pnoise);
       }
       // TB results come back in call order: (subframe, tb), CDD subframes holding two
+      const double pw = now_s(), pc = cpu_s();
       if (srsgpu_pdsch_decode_out_dev(pdsch, sfs.data(), np, d_grid, d_ce, gsz, outp.data(), max_halfits, d_ret, d_noi))
         return -1;
+      if (trace)
+        fprintf(stderr, "rxq trace: n %u pdsch_decode wall %.3f ms cpu %.3f ms\n", n, (now_s() - pw) * 1e3,
+                (cpu_s() - pc) * 1e3);
       const size_t ntbs = outp.size();
       if (sl.staged_bytes)
         RXQ_CHK(hipMemcpyAsync(sl.h_data, d_data, sl.staged_bytes, hipMemcpyDeviceToHost, st));
@@ -997,6 +1008,9 @@ struct srsgpu_rxq {
     }
     RXQ_CHK(hipMemcpyAsync(sl.h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
     lap(3);
+    if (trace)
+      fprintf(stderr, "rxq trace: n %u front %.3f control %.3f grants %.3f pdsch %.3f ms\n", n, run_tm[0] * 1e3,
+              run_tm[1] * 1e3, run_tm[2] * 1e3, run_tm[3] * 1e3);
     return 0;
   }
 

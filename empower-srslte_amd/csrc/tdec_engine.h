@@ -17,6 +17,7 @@
 #include "srsgpu/tdec_batch.h"
 #include "srslte/phy/fec/turbodecoder.h"
 #include "tdec_kernels.h"
+#include "host_ring.h"
 #include "dlsch_kernels.h"
 
 #define HIPCHK(x)                                                                               \
@@ -94,9 +95,13 @@ struct TdecEngine {
   std::map<std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>, std::pair<uint32_t *, uint32_t *>> wc_tables;
   // current job (one pass)
   std::vector<TdGroup> groups; // kind order
-  TdGroup *d_groups = nullptr, *h_groups = nullptr;
+  TdGroup *d_groups = nullptr;
+  // pinned staging of the group table: a ring, so a call does not wait for the previous call's upload
+  // (which sits on the stream behind that call's earlier kernels: the host would run in lockstep with
+  // the device); last_up is what d_groups holds after the last upload
+  HostRing gring;
+  std::vector<TdGroup> last_up;
   size_t groups_cap = 0, uploaded = 0;
-  hipEvent_t gev = nullptr;
   // second stream of the fused early stop: the SSE kind beside the window kinds
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -104,7 +109,6 @@ struct TdecEngine {
   // the first half-iteration's k_decide moves to split_st (st is switched for the rest of the call)
   hipStream_t split_st = nullptr;
   hipEvent_t ev_split = nullptr;
-  bool gev_pending = false;
   int kind_g0[TD_NKIND + 1] = {0};
   int kind_blocks[TD_NKIND] = {0};
   size_t kind_lds[TD_NKIND] = {0};
@@ -155,19 +159,16 @@ struct TdecEngine {
     HIPCHK(hipMalloc(&Dfz, cap_dw * 4));
     HIPCHK(hipMalloc(&cb_end, cap_cbs));
     HIPCHK(hipMemset(cb_end, 0, cap_cbs));
-    HIPCHK(hipEventCreateWithFlags(&gev, hipEventDisableTiming));
     return 0;
   }
 
   void destroy() {
-    if (gev_pending) (void)hipEventSynchronize(gev);
+    gring.destroy();
     for (void *p : {SP0, XP1, A, D, T, scratch, (void *)d_groups})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
                     (void *)out_stage, (void *)Dfz, (void *)cb_end})
       if (p) (void)hipFree(p);
-    if (h_groups) (void)hipHostFree(h_groups);
-    if (gev) (void)hipEventDestroy(gev);
     if (aux) (void)hipStreamSynchronize(aux);
     for (hipEvent_t e : {ev_fork, ev_join, ev_split})
       if (e) (void)hipEventDestroy(e);
@@ -377,21 +378,24 @@ struct TdecEngine {
   int upload_groups() {
     const size_t ng = groups.size();
     if (ng > groups_cap) {
-      if (gev_pending) HIPCHK(hipEventSynchronize(gev));
-      gev_pending = false;
-      if (d_groups) HIPCHK(hipFree(d_groups));
-      if (h_groups) HIPCHK(hipHostFree(h_groups));
+      gring.destroy(); // waits for the uploads still reading it
+      if (d_groups) {
+        HIPCHK(hipStreamSynchronize(st)); // kernels of earlier calls may still read the old table
+        HIPCHK(hipFree(d_groups));
+      }
       groups_cap = std::max<size_t>(ng, 64);
       HIPCHK(hipMalloc(&d_groups, groups_cap * sizeof(TdGroup)));
-      HIPCHK(hipHostMalloc(&h_groups, groups_cap * sizeof(TdGroup)));
+      HIPCHK(gring.create(groups_cap * sizeof(TdGroup)));
       uploaded = 0;
     }
-    if (uploaded == ng && memcmp(h_groups, groups.data(), ng * sizeof(TdGroup)) == 0) return 0;
-    if (gev_pending) HIPCHK(hipEventSynchronize(gev));
-    memcpy(h_groups, groups.data(), ng * sizeof(TdGroup));
-    HIPCHK(hipMemcpyAsync(d_groups, h_groups, ng * sizeof(TdGroup), hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(gev, st));
-    gev_pending = true;
+    if (uploaded == ng && memcmp(last_up.data(), groups.data(), ng * sizeof(TdGroup)) == 0) return 0;
+    hipError_t re;
+    TdGroup *h = (TdGroup *)gring.acquire(&re);
+    HIPCHK(re);
+    memcpy(h, groups.data(), ng * sizeof(TdGroup));
+    HIPCHK(hipMemcpyAsync(d_groups, h, ng * sizeof(TdGroup), hipMemcpyHostToDevice, st));
+    HIPCHK(gring.mark(st));
+    last_up.assign(groups.begin(), groups.end());
     uploaded = ng;
     return 0;
   }

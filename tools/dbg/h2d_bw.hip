@@ -20,11 +20,21 @@
     }                                                                                              \
   } while (0)
 
+// an HBM-streaming kernel on its own stream for `iters` passes over 1 GiB: the copies' competition
+__global__ void k_busy(float4 *a, size_t n, int iters) {
+  for (int it = 0; it < iters; it++)
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+      float4 v = a[i];
+      v.x += 1.f;
+      a[i] = v;
+    }
+}
+
 static int run(const char *name, const char *src, char *dst, size_t bytes, int nstreams, hipStream_t *st,
                hipEvent_t e0, hipEvent_t e1) {
   std::vector<float> ms;
   for (int rep = 0; rep < 6; rep++) {
-    CHK(hipDeviceSynchronize());
+    for (int k = 0; k < nstreams; k++) CHK(hipStreamSynchronize(st[k])); // not the device: see k_busy
     CHK(hipEventRecord(e0, st[0]));
     for (int k = 1; k < nstreams; k++) CHK(hipStreamWaitEvent(st[k], e0, 0));
     const size_t piece = bytes / nstreams;
@@ -67,6 +77,37 @@ int main(int argc, char **argv) {
     if (run("hipHostMalloc", pinned, dev, bytes, ns, st, e0, e1)) return 1;
     if (run("hipHostRegister(malloc)", reg, dev, bytes, ns, st, e0, e1)) return 1;
   }
+  // as the queue copies registered rows: runs of 20 rows of 122,880 bytes (SC16 20 MHz subframes) at
+  // row offsets inside the registered region, one hipMemcpyAsync per run
+  {
+    const size_t row = 122880, rows = bytes / row, runl = 20;
+    std::vector<float> ms;
+    for (int rep = 0; rep < 4; rep++) {
+      CHK(hipStreamSynchronize(st[0]));
+      CHK(hipEventRecord(e0, st[0]));
+      const double h0 = (double)clock() / CLOCKS_PER_SEC;
+      for (size_t r = 1; r + runl <= rows; r += runl + 1)
+        CHK(hipMemcpyAsync(dev + r * row, reg + r * row, runl * row, hipMemcpyHostToDevice, st[0]));
+      const double h1 = (double)clock() / CLOCKS_PER_SEC;
+      CHK(hipEventRecord(e1, st[0]));
+      CHK(hipEventSynchronize(e1));
+      float t = 0;
+      CHK(hipEventElapsedTime(&t, e0, e1));
+      if (rep) printf("registered runs of %zu rows at offsets: %.2f GB/s (%.3f ms), host %.3f ms to enqueue\n", runl,
+                      (double)(rows / (runl + 1)) * runl * row / (t * 1e-3) / 1e9, t, (h1 - h0) * 1e3);
+    }
+  }
+  // the same with an HBM-bound kernel running beside the copy (as the queue's decode does)
+  float4 *busy = nullptr;
+  const size_t bn = ((size_t)1 << 30) / 16;
+  CHK(hipMalloc(&busy, bn * 16));
+  hipStream_t bs;
+  CHK(hipStreamCreateWithFlags(&bs, hipStreamNonBlocking));
+  hipLaunchKernelGGL(k_busy, dim3(2048), dim3(256), 0, bs, busy, bn, 200);
+  if (run("pinned, HBM kernel beside", pinned, dev, bytes, 1, st, e0, e1)) return 1;
+  if (run("registered, HBM kernel beside", reg, dev, bytes, 1, st, e0, e1)) return 1;
+  CHK(hipStreamSynchronize(bs));
+  CHK(hipFree(busy));
   CHK(hipHostUnregister(reg));
   free(reg);
   CHK(hipHostFree(pinned));
