@@ -576,12 +576,9 @@ struct srsgpu_rxq {
       if (stop) return;
       flush = false;
       slot[s].state = CLOSED;
-      // the next slot takes submissions once its batch has been completed
-      const int nx = (s + 1) % NSLOT;
-      cv_slot.wait(l, [&] { return stop || slot[nx].state == FILLING; });
-      if (stop) return;
-      fill = nx;
-      cv_slot.notify_all();
+      // the closed slot's transfer starts at once (its buffers are its own), overlapping the batches
+      // ahead of it; only then does the closer wait for the next slot to be free for submissions
+      // (waiting first held every transfer back until the batch two ahead had completed)
       cv_close.wait(l, [&] { return stop || slot[s].copying == 0; });
       if (stop) return;
       const size_t n = slot[s].items.size();
@@ -595,6 +592,12 @@ struct srsgpu_rxq {
       slot[s].state = STAGED;
       ready.push_back(ok ? s : -1 - s);
       cv_ready.notify_one();
+      // the next slot takes submissions once its batch has been completed
+      const int nx = (s + 1) % NSLOT;
+      cv_slot.wait(l, [&] { return stop || slot[nx].state == FILLING; });
+      if (stop) return;
+      fill = nx;
+      cv_slot.notify_all();
     }
   }
 
