@@ -727,7 +727,8 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
 
     paced: N streams each hand over one subframe per 1 ms TTI (srsgpu_rxq_drive_paced, zero-copy
     SC16, batch = N, depth HARQ slots per stream) for `ticks` TTIs; latency = results written - TTI
-    start. real_time_streams = the largest N whose p99 latency is within budget_ms (srsUE must send
+    start. real_time_streams = the largest N whose p99 latency is within budget_ms (the sweep goes on
+    past one miss and stops at the second in a row, or at a queue that falls behind; srsUE must send
     the HARQ ACK in subframe n + 4: HARQ_DELAY_MS, lib/include/srslte/common/common.h:49, leaving
     ~3 ms for the decode)."""
     import srsgpu_traffic as tr
@@ -824,6 +825,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
     best, best_variant = 0, None
     for variant in variants:
         paced = out["paced"] if variant == "dma" else out.setdefault("paced_" + variant, {})
+        misses = 0
         for ns in paced_streams:
             q = queue(variant, C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
             q.set_input_format(q.SC16, scale)
@@ -845,11 +847,18 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             paced[str(ns)] = rec
             q.close()
             del items, outs
-            if p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks:
+            rec["within_budget"] = bool(p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks)
+            if rec["within_budget"]:
+                misses = 0
                 if ns > best:
                     best, best_variant = ns, variant
             else:
-                break
+                # one miss can be a host hiccup (a producer thread descheduled for a few ms puts every
+                # stream it serves past the budget for those TTIs): the sweep stops at the second miss
+                # in a row; real_time_streams is the largest N that met the budget
+                misses += 1
+                if misses >= 2 or rec["producer_late_ms_max"] > 50:
+                    break
     out["paced_cfg"] = {"ticks": ticks, "tti_us": 1000, "depth": depth, "input": "sc16 zero-copy",
                         "batch": "one TTI of all streams", "p99_budget_ms": budget_ms}
     out["real_time_streams"] = best
