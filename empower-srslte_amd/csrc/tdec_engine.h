@@ -611,7 +611,12 @@ struct TdecEngine {
     const int chunk = td_sched().es_chunk;
     bool seq = false, es_any = false;
     const TdArrays a = arrays();
-    TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end};
+    // the early-stop launches' wave priority, 0..3 (SRSGPU_ES_PRIO, read per call; default 3): the
+    // few workgroups still running after the heavy pass win their SIMDs' issue arbitration against
+    // other streams' throughput kernels (headline 0.871 -> 0.858 ms per batch, r05_s34 / r05_s35)
+    const char *pe = getenv("SRSGPU_ES_PRIO");
+    TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end,
+            pe && pe[0] ? std::min(std::max(atoi(pe), 0), 3) : 3};
     // es_fused 3 (hybrid): the first half-iteration of every kind as one launch per kind plus one
     // k_decide (the whole batch's heavy pass, with kernel boundaries that let other streams in), then
     // the blocks still running (a few at high SNR) through the remaining half-iterations in ONE

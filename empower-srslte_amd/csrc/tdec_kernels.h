@@ -102,6 +102,7 @@ struct TdEs {
   int n0, n1; // this launch runs half-iterations n0 .. n1-1 (0 <= n0 < n1 <= max_halfits)
   uint32_t *dfz;  // decision words of the blocks that ended (layout of D), for k_es_bytes
   uint8_t *cb_end; // per CB: 0, or 1 + parity of the half-iteration that ended it (kept zero between jobs)
+  int prio;        // 0..3: the early-stop waves' issue priority on their SIMD (s_setprio; 0 = default)
 };
 // the natural-order bytes of the blocks the fused launches ended (after the last of them)
 hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st);

@@ -1226,6 +1226,17 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
   return all;
 }
 
+// the early-stop tail runs a few workgroups beside other streams' throughput kernels; a raised
+// issue priority lets its waves win the SIMD's arbitration against those (es.prio, 0 = default)
+__device__ __forceinline__ void es_set_prio(int prio) {
+  switch (__builtin_amdgcn_readfirstlane(prio)) {
+  case 1: __builtin_amdgcn_s_setprio(1); break;
+  case 2: __builtin_amdgcn_s_setprio(2); break;
+  case 3: __builtin_amdgcn_s_setprio(3); break;
+  default: break;
+  }
+}
+
 // The early-stop form of k_win_bidir_run (the DL-SCH path: srslte_tdec_iteration + CRC check per
 // half-iteration, sch.c:361-391): up to max_halfits half-iterations in ONE launch; after each one
 // the workgroup checks the CRC of its own code blocks (es_check) and leaves once all of them are
@@ -1240,6 +1251,7 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
   extern __shared__ s4 cks[];
   __shared__ uint32_t red[(64 / NB) * 2 * 2];
   __shared__ int fin[(64 / NB) * 2];
+  es_set_prio(es.prio);
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
   const int K_ = G.K, npairs = G.npairs;
@@ -1879,6 +1891,7 @@ __global__ __launch_bounds__(128) void k_sse_es(const TdGroup *__restrict__ grou
                                                 s2 *__restrict__ scratch_base, TdEs es) {
   __shared__ uint32_t red[128];
   __shared__ int fin[128];
+  es_set_prio(es.prio);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
   const int p = (blockIdx.x - G.blk_half) * 64 + (threadIdx.x & 63);
   if (threadIdx.x < 64) {
