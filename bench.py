@@ -709,7 +709,7 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
 INGEST_VARIANTS = {"dma": {}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
 
 
-def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0,
+def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0, min_batches=16,
                  paced_streams=(32, 64, 128, 192, 256, 320, 384, 448, 512, 640, 768), ticks=300, depth=3,
                  budget_ms=3.0):
     """The real srsUE caller path: host threads hand single time-domain C3
@@ -717,7 +717,9 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
     once) to the subframe batch queue (include/srsgpu/rx_queue.h). The threads are native
     (srsgpu_rxq_drive / _drive_paced), as srsUE's PHY workers are.
 
-    saturated: `producers` threads submit nsf subframes as fast as the queue takes them, per batch
+    saturated: `producers` threads submit max(nsf, min_batches * B) subframes as fast as the queue
+    takes them (at least min_batches batches: the pipeline's first transfer and last decode do not
+    overlap anything, and over 4 batches of 1024 they were a quarter of the time), per batch
     size and ingest mode — staged (each submission copies its samples into the queue's pinned
     staging, then one DMA per batch), zero-copy (the samples lie in a srsgpu_rxq_register'ed block:
     DMA'd from there, one copy per run of address-contiguous subframes), zero-copy SC16 (the radio's
@@ -794,8 +796,9 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
                 q.set_input_format(q.SC16, scale)
             if mode != "staged":
                 q.register(src)
-            items, outs = make_items(q, nsf, 4 * B, src)
-            warm = [q.submit(items[i]) for i in range(min(B, nsf))]
+            count = max(nsf, min_batches * B)
+            items, outs = make_items(q, count, 4 * B, src)
+            warm = [q.submit(items[i]) for i in range(min(B, count))]
             q.flush()
             assert all(q.wait(t) == 0 for t in warm)
             nb0, done0 = q.stats()
@@ -805,20 +808,20 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             nb, done = q.stats()
             nb, done = nb - nb0, done - done0
             lat = (t_done - t_sub) * 1e3
-            acked = sum(1 for it in items[-min(nsf, 4 * B):] if it.ret[0] == 0)
+            acked = sum(1 for it in items[-min(count, 4 * B):] if it.ret[0] == 0)
             zc, st = q.ingest_stats()
             tmg = q.timing()
             key = "%s_b%d" % (mode, B) if mode != "zero_copy_sc16" or variant == "dma" else \
                 "%s_%s_b%d" % (mode, variant, B)
             out["saturated"][key] = {
                 "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
-                "subframes_per_s": round(nsf / el, 1),
-                "ingest_GBps": round(nsf * sf_bytes["sc16" if "sc16" in mode else "cf32"] / el / 1e9, 2),
+                "subframes": count, "subframes_per_s": round(count / el, 1),
+                "ingest_GBps": round(count * sf_bytes["sc16" if "sc16" in mode else "cf32"] / el / 1e9, 2),
                 "latency_ms_p50": round(float(np.percentile(lat, 50)), 3),
                 "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
                 "mean_batch": round(done / max(nb, 1), 1), "failed": int((status != 0).sum()),
                 "zero_copy_rows": zc, "staged_rows": st, "ingest": variant,
-                "acked_of_last": "%d/%d" % (acked, min(nsf, 4 * B))}
+                "acked_of_last": "%d/%d" % (acked, min(count, 4 * B))}
             q.close()
             del items, outs
     # paced real-time streams, per registered-ingest variant

@@ -14,6 +14,7 @@
 
 #include "dlsch_kernels.h"
 #include "uci_dev.h"
+#include "wave_prio.h"
 #include "srsgpu/dlsch_batch.h"
 
 #include <algorithm>
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint8_t *__restrict__ init_done,
                                                    const uint32_t *__restrict__ noi_in,
                                                    const uint32_t *__restrict__ crc_a, DermCall dc,
-                                                   uint32_t *__restrict__ late) {
+                                                   uint32_t *__restrict__ late, int prio) {
   __shared__ uint32_t red[4];
   __shared__ uint32_t crc_tab[256];
   __shared__ uint32_t c_ck0[TBF_MAXC + 1];
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
   __shared__ uint8_t c_init[TBF_MAXC], c_ok[TBF_MAXC];
   __shared__ int all_ok;
   __shared__ uint32_t noi_sum;
+  wave_prio(prio);
   const int b = blockIdx.x;
   if (b >= ntb) return;
   TbItem t = tbs_[b];
@@ -741,7 +743,7 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
                             const DermCall &dc, uint32_t *late) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late);
+                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late, env_prio("SRSGPU_TAIL_PRIO", 0));
   return hipGetLastError();
 }
 

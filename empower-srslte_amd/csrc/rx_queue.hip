@@ -462,6 +462,7 @@ struct srsgpu_rxq {
     size_t row_bytes;
     int s, idx;
     const void *dv[2] = {nullptr, nullptr};
+    bool need_copy = false, wake = false;
     {
       std::unique_lock<std::mutex> l(m);
       // the filling slot has room (else wait for the closer to switch to the other slot), and no
@@ -483,18 +484,24 @@ struct srsgpu_rxq {
         dv[a] = device_view(td[a], row_bytes);
         slot[s].h_src[(size_t)idx * nrx + a] = dv[a]; // null: staged by the host copy below
         slot[s].h_host[(size_t)idx * nrx + a] = dv[a] ? td[a] : nullptr;
+        need_copy = need_copy || !dv[a];
       }
-      slot[s].copying++;
+      if (need_copy) slot[s].copying++;
+      // the closer waits for a first item, then for a full slot (or its deadline): only those wake it
+      // (a wake per submission had the closer contend for the lock with every worker)
+      wake = idx == 0 || slot[s].items.size() >= max_batch;
     }
-    cv_close.notify_one();
+    if (wake) cv_close.notify_one();
+    if (!need_copy) return 0;
     // the worker stages its own unregistered samples (outside the lock: many workers copy at once)
     for (uint32_t a = 0; a < nrx; a++)
       if (!dv[a]) memcpy((char *)slot[s].h_td + ((size_t)idx * nrx + a) * row_bytes, td[a], row_bytes);
     {
       std::lock_guard<std::mutex> l(m);
-      slot[s].copying--;
+      // the closer, having closed the slot, waits for the last copy to finish
+      wake = --slot[s].copying == 0 && slot[s].state == CLOSED;
     }
-    cv_close.notify_one();
+    if (wake) cv_close.notify_one();
     return 0;
   }
 
@@ -583,9 +590,13 @@ struct srsgpu_rxq {
       if (stop) return;
       const size_t n = slot[s].items.size();
       l.unlock();
-      const double ts = now_s();
+      const double ts = now_s(), cs = trace ? cpu_s() : 0.0;
+      const uint64_t dc0 = dma_copies;
       const bool ok = stage(slot[s], n);
       const double te = now_s();
+      if (trace)
+        fprintf(stderr, "rxq trace: n %zu stage wall %.3f ms cpu %.3f ms, %llu copies\n", n, (te - ts) * 1e3,
+                (cpu_s() - cs) * 1e3, (unsigned long long)(dma_copies - dc0));
       l.lock();
       tm[6] += te - ts;
       if (!ok) fprintf(stderr, "srsgpu rxq: staging copy failed: %s\n", hipGetErrorString(hipGetLastError()));
@@ -1215,7 +1226,8 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
                      uint32_t reuse, double *t_sub, double *t_done, int32_t *status) {
   if (!q || !items || !workers || workers > 256 || !t_sub || !t_done || !status) return -1;
   std::mutex m;
-  std::condition_variable cv;
+  // the collector waits for submissions, producers for collected items: each side wakes only the other
+  std::condition_variable cv_col, cv_prod;
   std::vector<uint64_t> tickets(n, 0);
   std::vector<uint8_t> state(n, 0); // 1 submitted, 2 refused
   uint32_t ndone = 0, producing = workers;
@@ -1227,7 +1239,7 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
     for (uint32_t i = w; i < n; i += workers) {
       if (reuse && i >= reuse) { // the item's softbuffer / output slot: wait for its last user
         std::unique_lock<std::mutex> l(m);
-        cv.wait(l, [&] { return ndone > i - reuse || err; });
+        cv_prod.wait(l, [&] { return ndone > i - reuse || err; });
       }
       {
         std::lock_guard<std::mutex> l(m);
@@ -1242,13 +1254,14 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
         state[i] = r ? 2 : 1;
         if (r && !err) err = r;
       }
-      cv.notify_all();
+      cv_col.notify_one();
+      if (r) cv_prod.notify_all();
     }
     {
       std::lock_guard<std::mutex> l(m);
       producing--;
     }
-    cv.notify_all();
+    cv_col.notify_one();
   };
   std::thread collector([&] {
     for (uint32_t i = 0; i < n; i++) {
@@ -1256,7 +1269,7 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
       uint64_t t;
       {
         std::unique_lock<std::mutex> l(m);
-        cv.wait(l, [&] { return state[i] != 0 || producing == 0; });
+        cv_col.wait(l, [&] { return state[i] != 0 || producing == 0; });
         s = state[i];
         t = tickets[i];
       }
@@ -1266,7 +1279,7 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
         std::lock_guard<std::mutex> l(m);
         ndone = i + 1;
       }
-      cv.notify_all();
+      cv_prod.notify_all();
     }
   });
   std::vector<std::thread> pool;
@@ -1286,7 +1299,8 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
   using clk = std::chrono::steady_clock;
   const uint64_t n = (uint64_t)streams * ticks;
   std::mutex m;
-  std::condition_variable cv;
+  // the collector waits for submissions, producers for collected items: each side wakes only the other
+  std::condition_variable cv_col, cv_prod;
   std::vector<uint64_t> tickets(n, 0);
   std::vector<uint8_t> state(n, 0); // 1 submitted, 2 refused / skipped
   uint64_t ndone = 0;
@@ -1303,7 +1317,7 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
         const uint64_t i = t * streams + st;
         if (t >= depth) { // the item's softbuffer / output slot: its use depth ticks ago is collected
           std::unique_lock<std::mutex> l(m);
-          cv.wait(l, [&] { return ndone > i - (uint64_t)depth * streams || err; });
+          cv_prod.wait(l, [&] { return ndone > i - (uint64_t)depth * streams || err; });
         }
         int r = -1;
         uint64_t tk = 0;
@@ -1324,7 +1338,8 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
           state[i] = r ? 2 : 1;
           if (r && !err) err = -1;
         }
-        cv.notify_all();
+        cv_col.notify_one();
+        if (r) cv_prod.notify_all();
       }
     }
   };
@@ -1334,7 +1349,7 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
       uint64_t tk;
       {
         std::unique_lock<std::mutex> l(m);
-        cv.wait(l, [&] { return state[i] != 0; });
+        cv_col.wait(l, [&] { return state[i] != 0; });
         s = state[i];
         tk = tickets[i];
       }
@@ -1348,7 +1363,7 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
         if (!r && it->ret[0] == 0) nack++;
         ndone = i + 1;
       }
-      cv.notify_all();
+      cv_prod.notify_all();
     }
   });
   std::vector<std::thread> pool;

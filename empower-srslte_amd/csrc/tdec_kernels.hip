@@ -41,6 +41,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "wave_prio.h"
+
 #include <algorithm>
 
 #include "tdec_kernels.h"
@@ -1226,23 +1228,14 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
   return all;
 }
 
-// the early-stop tail runs a few workgroups beside other streams' throughput kernels; a raised
-// issue priority lets its waves win the SIMD's arbitration against those (es.prio, 0 = default)
-__device__ __forceinline__ void es_set_prio(int prio) {
-  switch (__builtin_amdgcn_readfirstlane(prio)) {
-  case 1: __builtin_amdgcn_s_setprio(1); break;
-  case 2: __builtin_amdgcn_s_setprio(2); break;
-  case 3: __builtin_amdgcn_s_setprio(3); break;
-  default: break;
-  }
-}
-
 // The early-stop form of k_win_bidir_run (the DL-SCH path: srslte_tdec_iteration + CRC check per
 // half-iteration, sch.c:361-391): up to max_halfits half-iterations in ONE launch; after each one
 // the workgroup checks the CRC of its own code blocks (es_check) and leaves once all of them are
 // done, so a batch at high SNR costs the half-iterations its blocks need and no decide launches.
 // Blocks done at entry (HARQ retransmissions whose CRC passed before, cb_done seeded) are
 // skipped; a partly finished workgroup decodes on, its finished blocks' results stay frozen.
+// es.prio raises its waves' issue priority (wave_prio.h): it runs a few workgroups beside other
+// streams' throughput kernels.
 template <int NB, int DIV, bool B8>
 __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGroup *__restrict__ groups, int ngroups,
                                                       const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
@@ -1251,7 +1244,7 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
   extern __shared__ s4 cks[];
   __shared__ uint32_t red[(64 / NB) * 2 * 2];
   __shared__ int fin[(64 / NB) * 2];
-  es_set_prio(es.prio);
+  wave_prio(es.prio);
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
   const int K_ = G.K, npairs = G.npairs;
@@ -1891,7 +1884,7 @@ __global__ __launch_bounds__(128) void k_sse_es(const TdGroup *__restrict__ grou
                                                 s2 *__restrict__ scratch_base, TdEs es) {
   __shared__ uint32_t red[128];
   __shared__ int fin[128];
-  es_set_prio(es.prio);
+  wave_prio(es.prio);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
   const int p = (blockIdx.x - G.blk_half) * 64 + (threadIdx.x & 63);
   if (threadIdx.x < 64) {
@@ -2255,10 +2248,11 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
                                                 uint8_t *__restrict__ outb, size_t out_stride,
                                                 int early, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
-                                                int max_halfits, uint8_t *__restrict__ pair_done) {
+                                                int max_halfits, uint8_t *__restrict__ pair_done, int prio) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ uint32_t red[2][4];
   __shared__ int fin[4]; // [0..1] CB done, [2..3] CB finished at this half-iteration
+  wave_prio(prio);
   const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, blockIdx.x)];
   const int K = G.K, NB = G.nb, ncb = G.ncb;
   const int pair = blockIdx.x - G.pair0;
@@ -2381,9 +2375,10 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
 __global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
                                                   const uint32_t *__restrict__ Dfz,
                                                   uint8_t *__restrict__ outb, size_t out_stride,
-                                                  uint8_t *__restrict__ cb_end) {
+                                                  uint8_t *__restrict__ cb_end, int prio) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ int todo[ESB_PAIRS], ntodo;
+  wave_prio(prio);
   // the workgroup's pairs' flags all at once (one thread per pair), then only the pairs that ended
   // (a pair-by-pair scan waited on two dependent loads per pair, ~45 us per launch)
   if (threadIdx.x == 0) ntodo = 0;
@@ -2727,7 +2722,8 @@ hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t
 hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_es_bytes, dim3(nblk(npairs, ESB_PAIRS)), dim3(256), 0, st, dg, ng, npairs,
-                     (const uint32_t *)es.dfz, es.outb, es.out_stride, es.cb_end);
+                     (const uint32_t *)es.dfz, es.outb, es.out_stride, es.cb_end,
+                     env_prio("SRSGPU_TAIL_PRIO", 0));
   return hipGetLastError();
 }
 
@@ -2738,7 +2734,7 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, dg, ng, (const uint32_t *)a.D, outb,
                      out_stride, early ? 1 : 0, cb_done, cb_ok, noi, max_halfits,
-                     early ? pair_done : nullptr);
+                     early ? pair_done : nullptr, env_prio("SRSGPU_TAIL_PRIO", 0));
   return hipGetLastError();
 }
 #endif // TD_PART == 0
