@@ -743,7 +743,7 @@ hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap,
                             const DermCall &dc, uint32_t *late) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late, env_prio("SRSGPU_TAIL_PRIO", 0));
+                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late, env_prio("SRSGPU_TAIL_PRIO", 3));
   return hipGetLastError();
 }
 

@@ -245,6 +245,7 @@ struct srsgpu_rxq {
     float *d_raw = nullptr;                  // SC16: the staged raw samples before conversion
     const void **h_src = nullptr, **d_src = nullptr; // per row: registered host source (device view) or null
     std::vector<const void *> h_host;                // per row: the registered host pointer itself
+    std::vector<const char *> h_rgn;                 // per row: the start of its registered region
     void *d_reg = nullptr;                           // registered rows' DMA target (ingest_dma)
     hipEvent_t staged = nullptr;
     std::vector<Pending> items;
@@ -290,14 +291,17 @@ struct srsgpu_rxq {
   // on the device; false (SRSGPU_RXQ_INGEST=kernel) the ingest kernel reads them over the bus
   bool ingest_dma = true;
   std::vector<std::pair<const char *, uint32_t>> reg; // stage(): registered rows by host address
+  static constexpr size_t kMaxGap = 512 * 1024;        // stage(): bytes between rows one span may bridge
   // device view of a registered host pointer holding `bytes`, or null (caller holds m); aligned16: the
   // ingest kernel reads 16 B vectors (else the samples are staged)
-  const void *device_view(const void *p, size_t bytes, bool aligned16 = true) const {
+  const void *device_view(const void *p, size_t bytes, bool aligned16 = true, const char **rgn = nullptr) const {
     const char *c = (const char *)p;
     for (const Region &r : regions)
       if (c >= r.h && c + bytes <= r.h + r.bytes) {
         const char *d = r.d + (c - r.h);
-        return (aligned16 && ((uintptr_t)d & 15)) ? nullptr : d;
+        if (aligned16 && ((uintptr_t)d & 15)) return nullptr;
+        if (rgn) *rgn = r.h;
+        return d;
       }
     return nullptr;
   }
@@ -358,6 +362,7 @@ struct srsgpu_rxq {
       RXQ_CHK(hipHostMalloc(&s.h_src, sizeof(void *) * mb * nrx));
       RXQ_CHK(hipMalloc(&s.d_src, sizeof(void *) * mb * nrx));
       s.h_host.assign((size_t)mb * nrx, nullptr);
+      s.h_rgn.assign((size_t)mb * nrx, nullptr);
       RXQ_CHK(hipMalloc(&s.d_reg, sizeof(float) * 2 * td_len * mb * nrx));
       RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
       RXQ_CHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
@@ -481,9 +486,11 @@ struct srsgpu_rxq {
       *ticket = next_ticket++;
       slot[s].items.push_back({it, ue, *ticket, std::chrono::steady_clock::now()});
       for (uint32_t a = 0; a < nrx; a++) {
-        dv[a] = device_view(td[a], row_bytes);
+        const char *rgn = nullptr;
+        dv[a] = device_view(td[a], row_bytes, true, &rgn);
         slot[s].h_src[(size_t)idx * nrx + a] = dv[a]; // null: staged by the host copy below
         slot[s].h_host[(size_t)idx * nrx + a] = dv[a] ? td[a] : nullptr;
+        slot[s].h_rgn[(size_t)idx * nrx + a] = rgn; // the region stays registered while the row is queued
         need_copy = need_copy || !dv[a];
       }
       if (need_copy) slot[s].copying++;
@@ -524,34 +531,43 @@ struct srsgpu_rxq {
     if (last && hipMemcpyAsync(dst_raw, sl.h_td, last * row_bytes, hipMemcpyHostToDevice, cst) != hipSuccess)
       return false;
     if (ingest_dma) {
-      // registered rows in host address order, runs of contiguous rows one DMA each into d_reg (a row
-      // handed over twice is copied once); the ingest kernel then reads them from d_reg
+      // registered rows in host address order, one DMA per span of the caller's memory into d_reg: rows
+      // that touch or overlap share a span (a row handed over twice is copied once), and so do rows a
+      // short gap apart in one registered region: the gap's bytes cost less than a copy's own overhead
+      // (~12 us per hipMemcpyAsync on the copy engine, r05_s37), as long as d_reg has room for them.
+      // The ingest kernel then reads every row from its place in d_reg.
       reg.clear();
       for (size_t r = 0; r < rows; r++)
         if (sl.h_src[r]) reg.push_back({(const char *)sl.h_host[r], (uint32_t)r});
       std::sort(reg.begin(), reg.end());
-      size_t pos = 0, run0 = 0, i0 = 0;
-      auto flush_run = [&](size_t i1) {
-        if (i1 == i0) return true;
+      const size_t cap = sizeof(float) * 2 * td_len * max_batch * nrx; // d_reg's bytes
+      const char *sp0 = nullptr, *sp1 = nullptr, *rg = nullptr;           // the open span, its region
+      size_t dpos = 0, d0 = 0; // bytes of d_reg used; the open span's place there
+      auto flush_span = [&]() {
+        if (!sp0) return true;
         dma_copies++;
-        return hipMemcpyAsync((char *)sl.d_reg + run0 * row_bytes, reg[i0].first, (pos - run0) * row_bytes,
-                              hipMemcpyHostToDevice, cst) == hipSuccess;
+        const bool ok = hipMemcpyAsync((char *)sl.d_reg + d0, sp0, (size_t)(sp1 - sp0), hipMemcpyHostToDevice,
+                                       cst) == hipSuccess;
+        dpos = d0 + (size_t)(sp1 - sp0);
+        sp0 = nullptr;
+        return ok;
       };
       for (size_t i = 0; i < reg.size(); i++) {
-        const char *h = reg[i].first;
-        if (i > i0 && h == reg[i - 1].first) { // the same samples again
-          sl.h_src[reg[i].second] = (const char *)sl.d_reg + (pos - 1) * row_bytes;
-          continue;
+        const char *h = reg[i].first, *rgn = sl.h_rgn[reg[i].second];
+        const size_t later = (reg.size() - 1 - i) * row_bytes; // what the rows after this one may need
+        const bool joins = sp0 && rgn == rg && h <= sp1 + kMaxGap &&
+                           d0 + (size_t)(std::max(sp1, h + row_bytes) - sp0) + later <= cap;
+        if (!joins) {
+          if (!flush_span()) return false;
+          sp0 = h;
+          sp1 = h;
+          rg = rgn;
+          d0 = dpos;
         }
-        if (i > i0 && h != reg[i - 1].first + row_bytes) {
-          if (!flush_run(i)) return false;
-          i0 = i;
-          run0 = pos;
-        }
-        sl.h_src[reg[i].second] = (const char *)sl.d_reg + pos * row_bytes;
-        pos++;
+        sp1 = std::max(sp1, h + row_bytes);
+        sl.h_src[reg[i].second] = (const char *)sl.d_reg + d0 + (size_t)(h - sp0);
       }
-      if (!flush_run(reg.size())) return false;
+      if (!flush_span()) return false;
     }
     const bool kernel = sc16 || nst < rows;
     if (kernel) {

@@ -131,9 +131,10 @@ int srsgpu_rxq_decode_rnti(srsgpu_rxq_t *q, srsgpu_rxq_ue_dl_t *item);
 int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_resources);
 /* Zero-copy ingest: pin caller memory that holds time-domain subframes (hipHostRegister, mapped).
  * Submissions whose td buffers lie inside a registered region skip the host copy into the queue's
- * staging: the batch DMAs them straight from the caller's memory, one copy per run of td buffers
- * that are contiguous there (SRSGPU_RXQ_INGEST=kernel: one kernel per batch reads them over PCIe
- * instead). Such a td buffer is read after srsgpu_rxq_submit returns: keep it unchanged until the
+ * staging: the batch DMAs them straight from the caller's memory, one copy per span of td buffers
+ * that are contiguous there or at most 512 KB apart in one region (the copy then also reads the
+ * registered bytes between them, and discards them; SRSGPU_RXQ_INGEST=kernel: one kernel per batch
+ * reads the td buffers over PCIe instead). Such a td buffer is read after srsgpu_rxq_submit returns: keep it unchanged until the
  * ticket is waited for (unregistered ones are copied before submit returns). td pointers must be
  * 16-byte aligned to be read in place (others are staged). The region must stay valid until
  * unregistered; unregister waits until nothing queued points into it. */

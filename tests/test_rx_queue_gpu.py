@@ -294,6 +294,33 @@ def test_registered_and_sc16_ingest(oracle, ingest, monkeypatch):
     for i, p in enumerate(perm):
         assert (got[0][i], got[1][i], got[2][i]) == (want[0][p], want[1][p], want[2][p]), i
         assert (got[3][i] == want[3][p]).all(), i
+
+    def same(got):
+        return got[:3] == want[:3] and all((a == b).all() for a, b in zip(got[3], want[3]))
+
+    # rows a short gap apart in one registered region share one DMA span, the gap's bytes (other
+    # samples) copied with them; rows alternating between two registered regions never share one
+    junk = np.random.default_rng(5).integers(-30000, 30000, size=blk16.shape, dtype=np.int16)
+    gap16 = np.empty((2 * n,) + blk16.shape[1:], np.int16)
+    gap16[0::2] = blk16
+    gap16[1::2] = junk
+    q.register(gap16)
+    assert same(_run_queue(s, q, list(gap16[0::2]), sfs, nof_prb, tbs))
+    blk16b = blk16.copy()
+    q.register(blk16b)
+    assert same(_run_queue(s, q, [blk16[i] if i % 2 else blk16b[i] for i in range(n)], sfs, nof_prb, tbs))
+    q.unregister(blk16b)
+    q.unregister(gap16)
+    q.unregister(blk16)
+    # cf32 rows a gap apart in a full batch: the queue's DMA target holds exactly max_batch rows, so a
+    # span bridges gaps only while the rows after it still fit
+    q.set_input_format(q.CF32)
+    gapf = np.empty((2 * n,) + xq[0].shape, np.complex64)
+    gapf[0::2] = np.stack(xq)
+    gapf[1::2] = np.random.default_rng(6).standard_normal((n, 2 * xq[0].size)).astype(np.float32).view(np.complex64)
+    q.register(gapf)
+    assert same(_run_queue(s, q, list(gapf[0::2]), sfs, nof_prb, tbs))
+    q.unregister(gapf)
     q.close()
     torch.cuda.synchronize()
 

@@ -97,6 +97,41 @@ int main(int argc, char **argv) {
                       (double)(rows / (runl + 1)) * runl * row / (t * 1e-3) / 1e9, t, (h1 - h0) * 1e3);
     }
   }
+  // single rows (one 20 MHz SC16 subframe each) at every other row offset: one hipMemcpyAsync per row
+  // against one hipMemcpyBatchAsync of the same copies (the per-copy overhead of the copy engine)
+  for (size_t runl : {(size_t)1, (size_t)20}) {
+    const size_t row = 122880, rows = bytes / row;
+    std::vector<void *> ds, ss;
+    std::vector<size_t> sz;
+    for (size_t r = 1; r + runl <= rows; r += runl + 1) {
+      ds.push_back(dev + r * row);
+      ss.push_back(reg + r * row);
+      sz.push_back(runl * row);
+    }
+    for (int mode = 0; mode < 2; mode++) {
+      std::vector<float> ms;
+      for (int rep = 0; rep < 4; rep++) {
+        CHK(hipStreamSynchronize(st[0]));
+        CHK(hipEventRecord(e0, st[0]));
+        if (mode == 0) {
+          for (size_t k = 0; k < ds.size(); k++)
+            CHK(hipMemcpyAsync(ds[k], ss[k], sz[k], hipMemcpyHostToDevice, st[0]));
+        } else {
+          size_t fail = 0;
+          CHK(hipMemcpyBatchAsync(ds.data(), ss.data(), sz.data(), ds.size(), nullptr, nullptr, 0, &fail, st[0]));
+        }
+        CHK(hipEventRecord(e1, st[0]));
+        CHK(hipEventSynchronize(e1));
+        float t = 0;
+        CHK(hipEventElapsedTime(&t, e0, e1));
+        if (rep) ms.push_back(t);
+      }
+      std::sort(ms.begin(), ms.end());
+      printf("%zu copies of %zu row(s), %s: %.2f GB/s (%.3f ms, %.1f us per copy)\n", ds.size(), runl,
+             mode ? "hipMemcpyBatchAsync" : "hipMemcpyAsync each", ds.size() * runl * row / (ms[1] * 1e-3) / 1e9,
+             ms[1], ms[1] * 1e3 / ds.size());
+    }
+  }
   // the same with an HBM-bound kernel running beside the copy (as the queue's decode does)
   float4 *busy = nullptr;
   const size_t bn = ((size_t)1 << 30) / 16;
