@@ -790,6 +790,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
     for B in batches:
         modes = [("staged", "dma"), ("zero_copy", "dma")] + [("zero_copy_sc16", v) for v in variants]
         for mode, variant in modes:
+            print("rx_queue: saturated %s %s b%d" % (mode, variant, B), file=sys.stderr, flush=True)
             q = queue(variant, C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
             src = x_sc if "sc16" in mode else x_cf
             if "sc16" in mode:
@@ -823,6 +824,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
                 "zero_copy_rows": zc, "staged_rows": st, "ingest": variant,
                 "acked_of_last": "%d/%d" % (acked, min(count, 4 * B))}
             q.close()
+            torch.cuda.synchronize()  # a fault of this queue's work is reported here, not by the next one
             del items, outs
     # paced real-time streams, per registered-ingest variant
     best, best_variant = 0, None
@@ -830,6 +832,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         paced = out["paced"] if variant == "dma" else out.setdefault("paced_" + variant, {})
         misses = 0
         for ns in paced_streams:
+            print("rx_queue: paced %s %d streams" % (variant, ns), file=sys.stderr, flush=True)
             q = queue(variant, C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
             q.set_input_format(q.SC16, scale)
             q.register(x_sc)
@@ -849,6 +852,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
                    "ingest_GBps": round(ns * 1000.0 * sf_bytes["sc16"] / 1e9, 2)}
             paced[str(ns)] = rec
             q.close()
+            torch.cuda.synchronize()
             del items, outs
             rec["within_budget"] = bool(p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks)
             if rec["within_budget"]:

@@ -239,7 +239,8 @@ struct srsgpu_rxq {
   // writes them into the items) before it takes submissions again. Three slots: one filling, one on
   // the GPU, one completing; the GPU gets the next batch while the host finishes the last.
   enum { FILLING = 0, CLOSED = 1, STAGED = 2, RUNNING = 3 };
-  static constexpr int NSLOT = 3;
+  static constexpr int NSLOT = 4;
+  int nslot = 3; // slots in use (SRSGPU_RXQ_SLOTS, 3 or 4)
   struct Slot {
     float *h_td = nullptr, *d_td = nullptr; // pinned staging (raw format) / device samples (cf32)
     float *d_raw = nullptr;                  // SC16: the staged raw samples before conversion
@@ -290,6 +291,7 @@ struct srsgpu_rxq {
   // registered rows: true (default) DMA them (one copy per run of address-contiguous rows) and convert
   // on the device; false (SRSGPU_RXQ_INGEST=kernel) the ingest kernel reads them over the bus
   bool ingest_dma = true;
+  bool wake_all = false; // SRSGPU_RXQ_WAKE_ALL=1: every submission wakes the closer (diagnosis)
   std::vector<std::pair<const char *, uint32_t>> reg; // stage(): registered rows by host address
   static constexpr size_t kMaxGap = 512 * 1024;        // stage(): bytes between rows one span may bridge
   // device view of a registered host pointer holding `bytes`, or null (caller holds m); aligned16: the
@@ -355,7 +357,9 @@ struct srsgpu_rxq {
     if (srsgpu_ofdm_set_cp(ofdm, cell.cp)) return -1;
     srsgpu_chest_set_stream(chest, st);
     srsgpu_pdsch_set_stream(pdsch, st);
-    for (Slot &s : slot) {
+    if (const char *e = getenv("SRSGPU_RXQ_SLOTS")) nslot = std::min(std::max(atoi(e), 3), NSLOT);
+    for (int k = 0; k < nslot; k++) {
+      Slot &s = slot[k];
       RXQ_CHK(hipMalloc(&s.d_td, sizeof(float) * 2 * td_len * mb * nrx));
       RXQ_CHK(hipMalloc(&s.d_raw, sizeof(float) * td_len * mb * nrx)); // SC16 rows: 4 B per sample
       RXQ_CHK(hipHostMalloc(&s.h_td, sizeof(float) * 2 * td_len * mb * nrx));
@@ -407,6 +411,7 @@ struct srsgpu_rxq {
     RXQ_CHK(hipHostMalloc(&h_res_ul, sizeof(srsgpu_dci_result_t) * mb));
     srsgpu_pcfich_set_noise_dev(pcfich, d_uenoise);
     if (const char *e = getenv("SRSGPU_RXQ_INGEST")) ingest_dma = strcmp(e, "kernel") != 0;
+    if (const char *e = getenv("SRSGPU_RXQ_WAKE_ALL")) wake_all = e[0] == '1';
     closer = std::thread([this] { close_loop(); });
     worker = std::thread([this] { run_loop(); });
     completer = std::thread([this] { comp_loop(); });
@@ -429,8 +434,12 @@ struct srsgpu_rxq {
     }
     cv_comp.notify_all();
     if (completer.joinable()) completer.join();
-    if (st) (void)hipStreamSynchronize(st);
-    if (cst) (void)hipStreamSynchronize(cst);
+    // a fault of the queue's last work shows here rather than in the caller's next HIP call
+    for (hipStream_t x : {st, cst})
+      if (x) {
+        const hipError_t e = hipStreamSynchronize(x);
+        if (e != hipSuccess) fprintf(stderr, "srsgpu rxq: teardown sync: %s\n", hipGetErrorString(e));
+      }
     if (ofdm) srsgpu_ofdm_rx_destroy(ofdm);
     if (chest) srsgpu_chest_destroy(chest);
     if (pdsch) srsgpu_pdsch_destroy(pdsch);
@@ -496,7 +505,7 @@ struct srsgpu_rxq {
       if (need_copy) slot[s].copying++;
       // the closer waits for a first item, then for a full slot (or its deadline): only those wake it
       // (a wake per submission had the closer contend for the lock with every worker)
-      wake = idx == 0 || slot[s].items.size() >= max_batch;
+      wake = wake_all || idx == 0 || slot[s].items.size() >= max_batch;
     }
     if (wake) cv_close.notify_one();
     if (!need_copy) return 0;
@@ -506,7 +515,7 @@ struct srsgpu_rxq {
     {
       std::lock_guard<std::mutex> l(m);
       // the closer, having closed the slot, waits for the last copy to finish
-      wake = --slot[s].copying == 0 && slot[s].state == CLOSED;
+      wake = --slot[s].copying == 0 && (wake_all || slot[s].state == CLOSED);
     }
     if (wake) cv_close.notify_one();
     return 0;
@@ -620,7 +629,7 @@ struct srsgpu_rxq {
       ready.push_back(ok ? s : -1 - s);
       cv_ready.notify_one();
       // the next slot takes submissions once its batch has been completed
-      const int nx = (s + 1) % NSLOT;
+      const int nx = (s + 1) % nslot;
       cv_slot.wait(l, [&] { return stop || slot[nx].state == FILLING; });
       if (stop) return;
       fill = nx;
