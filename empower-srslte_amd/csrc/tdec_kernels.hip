@@ -2734,7 +2734,7 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, dg, ng, (const uint32_t *)a.D, outb,
                      out_stride, early ? 1 : 0, cb_done, cb_ok, noi, max_halfits,
-                     early ? pair_done : nullptr, env_prio("SRSGPU_TAIL_PRIO", 3));
+                     early ? pair_done : nullptr, env_prio("SRSGPU_DECIDE_PRIO", env_prio("SRSGPU_TAIL_PRIO", 3)));
   return hipGetLastError();
 }
 #endif // TD_PART == 0
