@@ -999,10 +999,11 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir(const TdGroup
                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                    const s2 *__restrict__ T, size_t plane,
-                                                   const uint8_t *__restrict__ pair_done) {
+                                                   const uint8_t *__restrict__ pair_done, int prio) {
   // checkpoint slots in (dynamic) LDS, [slot][half][lane] x 16 B (conflict-free b128 accesses);
   // nc + 1 slots of 2 KiB: 50 KiB at K = 6144 with 16 sub-blocks
   extern __shared__ s4 cks[];
+  wave_prio(prio);
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
   TD_T(0);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
@@ -2561,7 +2562,8 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
     allow_big_lds((const void *)(k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>));                 \
     hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>), dim3(nblocks), dim3(128), \
                        lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
-                       (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done);                     \
+                       (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done,                      \
+                       env_prio("SRSGPU_H0_PRIO", 0));                                              \
   } while (0)
 #define BIDIR(nb, div, b8)                                                                         \
   do {                                                                                             \
