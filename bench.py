@@ -750,6 +750,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         out[...] = a
         return out
 
+    registered_keep = []  # registered host blocks, freed only when the leg returns (see make_items)
     x_cf = page_aligned(c["x"].cpu().numpy().reshape(n_src, 15 * N))
     base = c["sfs"]
     m.close()
@@ -762,9 +763,14 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
 
     def make_items(q, count, nsb, src):
         """outputs in one registered block (srsgpu_rxq_register): the decoder writes the TB bytes into
-        them over PCIe, with no copy-back through the queue"""
+        them over PCIe, with no copy-back through the queue. The block outlives its queue (kept in
+        `registered_keep`): twice (r05_s39, r05_s46) the next queue's creation faulted in a plain
+        pageable hipMemcpy right after an unregistered output block was freed, consistent with the
+        runtime reusing a stale registration of those addresses; keeping every registered block
+        alive until the leg ends keeps their addresses from being reused."""
         dl = (C3_TBS // 8 + 6 + 63) // 64 * 64
         block = page_aligned(np.zeros((nsb, dl), np.uint8))
+        registered_keep.append(block)
         q.register(block)
         outs = [block[k, :C3_TBS // 8 + 6] for k in range(nsb)]
         items = []
