@@ -709,6 +709,11 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
 INGEST_VARIANTS = {"dma": {}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
 
 
+# host blocks the queue leg registered (srsgpu_rxq_register), kept until the process ends: see
+# rx_queue_leg's make_items
+REGISTERED_KEEP = []
+
+
 def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0, min_batches=16,
                  paced_streams=(32, 64, 128, 192, 256, 320, 384, 448, 512, 640, 768), ticks=300, depth=3,
                  budget_ms=3.0):
@@ -750,13 +755,14 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         out[...] = a
         return out
 
-    registered_keep = []  # registered host blocks, freed only when the leg returns (see make_items)
+    registered_keep = REGISTERED_KEEP  # registered host blocks, never freed (see make_items)
     x_cf = page_aligned(c["x"].cpu().numpy().reshape(n_src, 15 * N))
     base = c["sfs"]
     m.close()
     torch.cuda.synchronize()
     scale = float(np.abs(x_cf.view(np.float32)).max()) / 32000.0
     x_sc = page_aligned(np.round(x_cf.view(np.float32) / scale).astype(np.int16))  # [n_src][15 N * 2]
+    registered_keep += [x_cf, x_sc]
     sf_bytes = {"cf32": 8 * 15 * N, "sc16": 4 * 15 * N}
     out = {"workload": "c3_coded_queue_20MHz_64QAM_tbs%d" % C3_TBS, "snr_db": snr_db,
            "producers": producers, "saturated": {}, "paced": {}}
@@ -767,7 +773,7 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         `registered_keep`): twice (r05_s39, r05_s46) the next queue's creation faulted in a plain
         pageable hipMemcpy right after an unregistered output block was freed, consistent with the
         runtime reusing a stale registration of those addresses; keeping every registered block
-        alive until the leg ends keeps their addresses from being reused."""
+        alive (REGISTERED_KEEP) keeps their addresses from being reused."""
         dl = (C3_TBS // 8 + 6 + 63) // 64 * 64
         block = page_aligned(np.zeros((nsb, dl), np.uint8))
         registered_keep.append(block)
