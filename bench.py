@@ -423,6 +423,12 @@ def run_pipeline(s, torch, dev, steps, warmup, tm=1, lanes=2, dist=None, schedul
                     "not decoded Mbps; see c3_coded_sweep for SURVEY 8(d)'s decoded Mbps)"}
 
 
+def cb_sizes(table, tbs):
+    """K of each code block of a TB (cbsegm.c order: C2 blocks of K2, then K1)"""
+    C, _c1, K1, C2, K2, _f = table["cbsegm_C_C1_K1_C2_K2_F"][str(tbs)]
+    return [K2 if i < C2 else K1 for i in range(C)]
+
+
 def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None,
                 standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1, tail=0):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
@@ -505,6 +511,18 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
     ab = schedule_ab(s, torch, step, steps, schedules)
     chk = [m.check() for m in ms]
+    # decoder work of the last batch: the half-iterations each code block ran (srsgpu_dlsch_cb_halfits)
+    # weighted by its K, for the VALU roofline of the whole decoder (first + early-stop launches)
+    # (one block size only: the decoder's block order groups blocks by K, not by TB)
+    halfit_bits = 0
+    for m in ms:
+        h = m.dlsch.cb_halfits()
+        ks_cb = [k for t in m.tb_list for k in cb_sizes(table, t["tbs"])]
+        assert len(ks_cb) == h.size, (len(ks_cb), h.size)
+        if halfit_bits is None or len(set(ks_cb)) != 1:
+            halfit_bits = None
+            continue
+        halfit_bits += int(h.astype(np.int64).sum()) * ks_cb[0]
     acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
     noi = float(np.mean([c[2] for c in chk]))
     tbl = [t for m in ms for t in m.tb_list]
@@ -544,6 +562,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
            "result_bytes_per_rank": int(local.numel()), "schedule_ab": ab,
            "symbol_size": ms[0].cells[0]["N"], "early_stop": early_stop,
            "host_ms_per_step": round(host / steps * 1e3, 3), "descriptor_sets": rotate,
+           "halfit_bits_per_batch": halfit_bits,
            "host_ms_front_end": round(host_split[0] / steps * 1e3, 3),
            "host_ms_dlsch": round(host_split[1] / steps * 1e3, 3),
            "kernels_per_batch": {k: {"ms": round(v[0], 4), "launches": v[1]} for k, v in ktab.items()},
@@ -599,6 +618,18 @@ def run_tm3_coded(s, torch, dev, steps, warmup, snr_db=30.0, lanes=2, dist=None)
     gc.enable()
     stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
     chk = [m.check() for m in ms]
+    # decoder work of the last batch: the half-iterations each code block ran (srsgpu_dlsch_cb_halfits)
+    # weighted by its K, for the VALU roofline of the whole decoder (first + early-stop launches)
+    # (one block size only: the decoder's block order groups blocks by K, not by TB)
+    halfit_bits = 0
+    for m in ms:
+        h = m.dlsch.cb_halfits()
+        ks_cb = [k for t in m.tb_list for k in cb_sizes(table, t["tbs"])]
+        assert len(ks_cb) == h.size, (len(ks_cb), h.size)
+        if halfit_bits is None or len(set(ks_cb)) != 1:
+            halfit_bits = None
+            continue
+        halfit_bits += int(h.astype(np.int64).sum()) * ks_cb[0]
     acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
     noi = float(np.mean([c[2] for c in chk]))
     cb_bits = sum(m.decoded_bits(table) for m in ms)
@@ -709,115 +740,171 @@ def dci_blind_decode(s, torch, steps, nsf=1024, per_sf=44):
 INGEST_VARIANTS = {"dma": {}, "busread": {"SRSGPU_RXQ_INGEST": "kernel"}}
 
 
-# host blocks the queue leg registered (srsgpu_rxq_register), kept until the process ends: see
-# rx_queue_leg's make_items
-REGISTERED_KEEP = []
+def cpu_probe():
+    """(wall s, this process's CPU s, cgroup throttled usec, cgroup nr_throttled): the GPU box gives a
+    command a CFS quota (/sys/fs/cgroup/cpu.max, 16 CPUs over 256 visible cores), so a process that
+    burns more than its quota in a 100 ms period stalls every thread until the next one"""
+    import resource
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    thr = nr = None
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k == "throttled_usec":
+                thr = int(v)
+            elif k == "nr_throttled":
+                nr = int(v)
+    except OSError:
+        pass
+    return time.perf_counter(), r.ru_utime + r.ru_stime, thr, nr
+
+
+def cpu_delta(a, b):
+    """CPU use between two cpu_probe() samples: cores busy on average, ms of quota throttling"""
+    out = {"cpu_cores_busy": round((b[1] - a[1]) / max(b[0] - a[0], 1e-9), 2)}
+    if a[2] is not None and b[2] is not None:
+        out["cgroup_throttled_ms"] = round((b[2] - a[2]) / 1e3, 1)
+        out["cgroup_nr_throttled"] = b[3] - a[3]
+    return out
+
+
+def cpu_quota():
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def paced_record(lat, slat, status, acked, late, ns, ticks, nb, done, tmg, budget_ms, sf_bytes):
+    """one paced point: latency from the tick (what the HARQ budget sees) and from the actual submission
+    (the queue's own latency, without the producer threads' lateness behind the tick)"""
+    ok = slat >= 0
+    p99 = float(np.percentile(lat, 99))
+    rec = {"latency_ms_p50": round(float(np.percentile(lat, 50)), 3), "latency_ms_p99": round(p99, 3),
+           "latency_ms_max": round(float(lat.max()), 3),
+           "submit_latency_ms_p50": round(float(np.percentile(slat[ok], 50)), 3) if ok.any() else None,
+           "submit_latency_ms_p99": round(float(np.percentile(slat[ok], 99)), 3) if ok.any() else None,
+           "producer_late_ms_max": round(late, 3),
+           "producer_late_ms_p99": round(float(np.percentile(lat[ok] - slat[ok], 99)), 3) if ok.any() else None,
+           "acked": "%d/%d" % (acked, ns * ticks), "failed": int((status != 0).sum()),
+           "mean_batch": round(done / max(nb, 1), 1), "subframes_per_s": round(ns * 1000.0, 1),
+           "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
+           "ingest_GBps": round(ns * 1000.0 * sf_bytes / 1e9, 2)}
+    rec["within_budget"] = bool(p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks)
+    return rec
 
 
 def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_db=30.0, min_batches=16,
-                 paced_streams=(32, 64, 128, 192, 256, 320, 384, 448, 512, 640, 768), ticks=300, depth=3,
-                 budget_ms=3.0):
+                 paced_streams=(32, 64, 128, 192, 256, 320, 384, 448, 512, 640), ticks=300, depth=3,
+                 budget_ms=3.0, paced_fft=(2048, 1536), paced_workers=4):
     """The real srsUE caller path: host threads hand single time-domain C3
     subframes (20 MHz, MCS 28 codewords from the GPU transmitter at snr_db, copied to host memory
     once) to the subframe batch queue (include/srsgpu/rx_queue.h). The threads are native
-    (srsgpu_rxq_drive / _drive_paced), as srsUE's PHY workers are.
+    (srsgpu_rxq_drive / _drive_paced_ex), as srsUE's PHY workers are.
+
+    Host memory: the samples a queue reads in place and the TB outputs the decoder writes in place lie
+    in queue-owned blocks (srsgpu_rxq_alloc_host), filled from the caller's arrays and freed by the
+    queue; the caller's own memory is never pinned (the r05_s39 / r05_s46 fault followed
+    the free of caller memory the queue had pinned).
 
     saturated: `producers` threads submit max(nsf, min_batches * B) subframes as fast as the queue
     takes them (at least min_batches batches: the pipeline's first transfer and last decode do not
-    overlap anything, and over 4 batches of 1024 they were a quarter of the time), per batch
-    size and ingest mode — staged (each submission copies its samples into the queue's pinned
-    staging, then one DMA per batch), zero-copy (the samples lie in a srsgpu_rxq_register'ed block:
-    DMA'd from there, one copy per run of address-contiguous subframes), zero-copy SC16 (the radio's
-    int16 I/Q, half the bytes, converted on the GPU) and zero-copy SC16 bus-read (the batch's ingest
-    kernel reads the registered samples over PCIe in place, SRSGPU_RXQ_INGEST=kernel).
+    overlap anything), per batch size and ingest mode — staged (each submission copies its samples
+    into the queue's pinned staging, then one DMA per batch), zero-copy (the samples lie in a
+    queue-owned block: DMA'd from there, one copy per run of address-contiguous subframes), zero-copy
+    SC16 (the radio's int16 I/Q, half the bytes, converted on the GPU) and zero-copy SC16 bus-read
+    (the batch's ingest kernel reads the samples over PCIe in place, SRSGPU_RXQ_INGEST=kernel).
     ingest_GBps = sample bytes handed over / wall time.
 
-    paced: N streams each hand over one subframe per 1 ms TTI (srsgpu_rxq_drive_paced, zero-copy
-    SC16, batch = N, depth HARQ slots per stream) for `ticks` TTIs; latency = results written - TTI
-    start. real_time_streams = the largest N whose p99 latency is within budget_ms (the sweep goes on
-    past one miss and stops at the second in a row, or at a queue that falls behind; srsUE must send
-    the HARQ ACK in subframe n + 4: HARQ_DELAY_MS, lib/include/srslte/common/common.h:49, leaving
-    ~3 ms for the decode)."""
+    paced: N streams each hand over one SC16 subframe per 1 ms TTI (srsgpu_rxq_drive_paced_ex,
+    zero-copy, batch = N, depth HARQ slots per stream) for `ticks` TTIs, at the 3GPP 2048-point rate
+    and at srsLTE's default 1536-point rate (phy_common.c:37-41, 25 % fewer bytes). The queue's three
+    threads, the collector and `paced_workers` producers are pinned to distinct physical cores.
+    latency = results written - TTI start (the HARQ budget's view) and - actual submission (the
+    queue's own); real_time_streams = the largest N whose p99 latency from the tick is within
+    budget_ms with every TB acked (the sweep stops at the second miss in a row; srsUE must send the
+    HARQ ACK in subframe n + 4: HARQ_DELAY_MS, lib/include/srslte/common/common.h:49, leaving ~3 ms
+    for the decode). The first miss is kept whole in `first_miss`."""
     import srsgpu_traffic as tr
     table = json.load(open(os.path.join(REPO, "tests", "golden", "c5_traffic.json")))
-    m = tr.MixedCells(table, 1024, torch, dev, seed=22, snr_db=snr_db, prbs=(100,), mcs=28, full_band=True)
-    c = m.cells[0]
-    N = c["N"]
-    n_src = c["n"]
-    def page_aligned(a):
-        """a copy of `a` in page-aligned host memory (hipHostRegister of a region that does not start on
-        a page boundary DMAs at about half the rate, r05_s22 / r05_s23)"""
-        if os.environ.get("BENCH_RXQ_UNALIGNED"):
-            return np.ascontiguousarray(a)
-        raw = np.empty(a.nbytes + 4096, np.uint8)
-        off = (-raw.ctypes.data) % 4096
-        out = raw[off:off + a.nbytes].view(a.dtype).reshape(a.shape)
-        out[...] = a
-        return out
-
-    registered_keep = REGISTERED_KEEP  # registered host blocks, never freed (see make_items)
-    x_cf = page_aligned(c["x"].cpu().numpy().reshape(n_src, 15 * N))
-    base = c["sfs"]
-    m.close()
-    torch.cuda.synchronize()
-    scale = float(np.abs(x_cf.view(np.float32)).max()) / 32000.0
-    x_sc = page_aligned(np.round(x_cf.view(np.float32) / scale).astype(np.int16))  # [n_src][15 N * 2]
-    registered_keep += [x_cf, x_sc]
-    sf_bytes = {"cf32": 8 * 15 * N, "sc16": 4 * 15 * N}
+    srcs = {}
+    for fft in sorted(set((2048,) + tuple(paced_fft))):
+        m = tr.MixedCells(table, 1024, torch, dev, seed=22, snr_db=snr_db, prbs=(100,), mcs=28, full_band=True,
+                          standard_rate=(fft == 2048))
+        c = m.cells[0]
+        assert c["N"] == fft, (c["N"], fft)
+        x_cf = c["x"].cpu().numpy().reshape(c["n"], 15 * fft)
+        base = c["sfs"]
+        m.close()
+        torch.cuda.synchronize()
+        scale = float(np.abs(x_cf.view(np.float32)).max()) / 32000.0
+        x_sc = np.round(x_cf.view(np.float32) / scale).astype(np.int16)  # [n_src][15 N * 2]
+        srcs[fft] = {"cf": x_cf, "sc": x_sc, "scale": scale, "sfs": base, "n": c["n"]}
+    cpus = physical_cpus()
+    # the queue's closer / dispatcher / completer, then the collector and the producers (paced)
+    q_cpus, d_cpus = cpus[:3], cpus[3:4 + paced_workers] or cpus[:1]
     out = {"workload": "c3_coded_queue_20MHz_64QAM_tbs%d" % C3_TBS, "snr_db": snr_db,
-           "producers": producers, "saturated": {}, "paced": {}}
+           "producers": producers, "saturated": {}, "paced": {},
+           "host_memory": "queue-owned (srsgpu_rxq_alloc_host)",
+           "cpus": {"available": len(os.sched_getaffinity(0)), "physical": len(cpus), "quota": cpu_quota(),
+                    "queue_threads": q_cpus, "paced_threads": d_cpus}}
 
-    def make_items(q, count, nsb, src):
-        """outputs in one registered block (srsgpu_rxq_register): the decoder writes the TB bytes into
-        them over PCIe, with no copy-back through the queue. The block outlives its queue (kept in
-        `registered_keep`): twice (r05_s39, r05_s46) the next queue's creation faulted in a plain
-        pageable hipMemcpy right after an unregistered output block was freed, consistent with the
-        runtime reusing a stale registration of those addresses; keeping every registered block
-        alive (REGISTERED_KEEP) keeps their addresses from being reused."""
+    def owned(q, x):
+        """the caller's sample ring in queue-owned device-visible memory"""
+        a = q.alloc_host(x.shape, x.dtype)
+        a[...] = x
+        return a
+
+    def make_items(q, count, nsb, src, sfs, n_src):
+        """TB outputs in one queue-owned block: the decoder writes the TB bytes into it over PCIe"""
         dl = (C3_TBS // 8 + 6 + 63) // 64 * 64
-        block = page_aligned(np.zeros((nsb, dl), np.uint8))
-        registered_keep.append(block)
-        q.register(block)
+        block = q.alloc_host((nsb, dl), np.uint8)
         outs = [block[k, :C3_TBS // 8 + 6] for k in range(nsb)]
         items = []
         for i in range(count):
             j = i % n_src
-            sf = base[j]
+            sf = sfs[j]
             sf.softbuffer[0] = i % nsb
             items.append(q.item([src[j]], sf, [outs[i % nsb]]))
-        return items, outs
+        return items, outs, block
 
     def queue(variant, *a, **kw):
         """a queue under one registered-ingest variant (the env is read when the queue is created)"""
         env = INGEST_VARIANTS[variant]
         os.environ.update(env)
         try:
-            return s.RxQueue(*a, **kw)
+            q = s.RxQueue(*a, **kw)
         finally:
             for k in env:
                 os.environ.pop(k, None)
+        q.set_affinity(q_cpus)
+        return q
 
     # BENCH_RXQ_VARIANTS=a,b: only these ingest variants (diagnosis runs)
     variants = [v for v in os.environ.get("BENCH_RXQ_VARIANTS", ",".join(INGEST_VARIANTS)).split(",") if v]
+    sf_bytes = {"cf32": 8 * 15 * 2048, "sc16": 4 * 15 * 2048}
+    S = srcs[2048]
     for B in batches:
         modes = [("staged", "dma"), ("zero_copy", "dma")] + [("zero_copy_sc16", v) for v in variants]
         for mode, variant in modes:
             print("rx_queue: saturated %s %s b%d" % (mode, variant, B), file=sys.stderr, flush=True)
-            q = queue(variant, C3_PRB, 1, N, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
-            src = x_sc if "sc16" in mode else x_cf
+            q = queue(variant, C3_PRB, 1, 2048, nof_softbuffers=4 * B, max_batch=B, max_wait_us=2000)
+            x = S["sc"] if "sc16" in mode else S["cf"]
             if "sc16" in mode:
-                q.set_input_format(q.SC16, scale)
-            if mode != "staged":
-                q.register(src)
+                q.set_input_format(q.SC16, S["scale"])
+            src = x if mode == "staged" else owned(q, x)
             count = max(nsf, min_batches * B)
-            items, outs = make_items(q, count, 4 * B, src)
+            items, outs, block = make_items(q, count, 4 * B, src, S["sfs"], S["n"])
             warm = [q.submit(items[i]) for i in range(min(B, count))]
             q.flush()
             assert all(q.wait(t) == 0 for t in warm)
             nb0, done0 = q.stats()
+            c0 = cpu_probe()
             t0 = time.perf_counter()
             t_sub, t_done, status = q.drive(items, producers, reuse=4 * B)
             el = time.perf_counter() - t0
+            c1 = cpu_probe()
             nb, done = q.stats()
             nb, done = nb - nb0, done - done0
             lat = (t_done - t_sub) * 1e3
@@ -834,54 +921,73 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
                 "latency_ms_p99": round(float(np.percentile(lat, 99)), 3),
                 "mean_batch": round(done / max(nb, 1), 1), "failed": int((status != 0).sum()),
                 "zero_copy_rows": zc, "staged_rows": st, "ingest": variant,
-                "acked_of_last": "%d/%d" % (acked, min(count, 4 * B))}
+                "acked_of_last": "%d/%d" % (acked, min(count, 4 * B)), **cpu_delta(c0, c1)}
+            del items, outs, block, src  # views of the queue's blocks: gone before the queue frees them
             q.close()
             torch.cuda.synchronize()  # a fault of this queue's work is reported here, not by the next one
-            del items, outs
-    # paced real-time streams, per registered-ingest variant
-    best, best_variant = 0, None
-    for variant in variants:
-        paced = out["paced"] if variant == "dma" else out.setdefault("paced_" + variant, {})
-        misses = 0
-        for ns in paced_streams:
-            print("rx_queue: paced %s %d streams" % (variant, ns), file=sys.stderr, flush=True)
-            q = queue(variant, C3_PRB, 1, N, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
-            q.set_input_format(q.SC16, scale)
-            q.register(x_sc)
-            items, outs = make_items(q, ns * depth, ns * depth, x_sc)
+    # paced real-time streams (zero-copy SC16 by DMA), per FFT size
+    for fft in paced_fft:
+        S = srcs[fft]
+        key = "paced" if fft == 2048 else "paced_%d" % fft
+        paced = out.setdefault(key, {})
+        best, best_q, misses, first_miss = 0, 0, 0, None
+
+        def point(ns):
+            q = queue("dma", C3_PRB, 1, fft, nof_softbuffers=ns * depth, max_batch=ns, max_wait_us=800)
+            q.set_input_format(q.SC16, S["scale"])
+            src = owned(q, S["sc"])
+            items, outs, block = make_items(q, ns * depth, ns * depth, src, S["sfs"], S["n"])
             warm = [q.submit(items[i]) for i in range(ns)]
             q.flush()
             assert all(q.wait(t) == 0 for t in warm)
-            lat, status, acked, late = q.drive_paced(items, ns, depth, ticks, 1000, workers=min(8, ns))
+            nb0, done0 = q.stats()
+            c0 = cpu_probe()
+            lat, slat, status, acked, late = q.drive_paced_ex(items, ns, depth, ticks, 1000,
+                                                              workers=min(paced_workers, ns), cpus=d_cpus)
+            c1 = cpu_probe()
             nb, done = q.stats()
-            tmg = q.timing()
-            p99 = float(np.percentile(lat, 99))
-            rec = {"latency_ms_p50": round(float(np.percentile(lat, 50)), 3), "latency_ms_p99": round(p99, 3),
-                   "latency_ms_max": round(float(lat.max()), 3), "acked": "%d/%d" % (acked, ns * ticks),
-                   "failed": int((status != 0).sum()), "mean_batch": round(done / max(nb, 1), 1),
-                   "producer_late_ms_max": round(late, 3), "subframes_per_s": round(ns * 1000.0, 1),
-                   "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
-                   "ingest_GBps": round(ns * 1000.0 * sf_bytes["sc16"] / 1e9, 2)}
-            paced[str(ns)] = rec
+            rec = paced_record(lat, slat, status, acked, late, ns, ticks, nb - nb0, done - done0, q.timing(),
+                               budget_ms, 4 * 15 * fft)
+            rec.update(cpu_delta(c0, c1))
+            del items, outs, block, src
             q.close()
             torch.cuda.synchronize()
-            del items, outs
-            rec["within_budget"] = bool(p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks)
+            return rec
+
+        for ns in paced_streams:
+            print("rx_queue: paced N=%d %d streams" % (fft, ns), file=sys.stderr, flush=True)
+            rec = point(ns)
+            if not rec["within_budget"] and (rec["producer_late_ms_p99"] or 0) > 1.0 and \
+                    (rec["submit_latency_ms_p99"] or 1e9) <= budget_ms:
+                # the load generator itself fell behind its ticks (host scheduling of the producer threads:
+                # the queue's own latency was within budget): measured once more, both records kept
+                again = point(ns)
+                again["first_attempt"] = {k: rec[k] for k in ("latency_ms_p99", "submit_latency_ms_p99",
+                                                              "producer_late_ms_max", "producer_late_ms_p99")}
+                rec = again
+            paced[str(ns)] = rec
+            if rec["failed"] == 0 and rec["acked"] == "%d/%d" % (ns * ticks, ns * ticks) and \
+                    (rec["submit_latency_ms_p99"] or 1e9) <= budget_ms:
+                best_q = max(best_q, ns)
             if rec["within_budget"]:
                 misses = 0
-                if ns > best:
-                    best, best_variant = ns, variant
+                best = max(best, ns)
             else:
                 # one miss can be a host hiccup (a producer thread descheduled for a few ms puts every
                 # stream it serves past the budget for those TTIs): the sweep stops at the second miss
                 # in a row; real_time_streams is the largest N that met the budget
                 misses += 1
+                if first_miss is None:
+                    first_miss = dict(rec, streams=ns)
                 if misses >= 2 or rec["producer_late_ms_max"] > 50:
                     break
-    out["paced_cfg"] = {"ticks": ticks, "tti_us": 1000, "depth": depth, "input": "sc16 zero-copy",
-                        "batch": "one TTI of all streams", "p99_budget_ms": budget_ms}
-    out["real_time_streams"] = best
-    out["real_time_streams_ingest"] = best_variant
+        out["real_time_streams" if fft == 2048 else "real_time_streams_%d" % fft] = best
+        # the queue's own capacity: latency from each subframe's actual submission within the budget
+        out["queue_streams" if fft == 2048 else "queue_streams_%d" % fft] = best_q
+        out["first_miss" if fft == 2048 else "first_miss_%d" % fft] = first_miss
+    out["paced_cfg"] = {"ticks": ticks, "tti_us": 1000, "depth": depth, "input": "sc16 zero-copy (DMA)",
+                        "batch": "one TTI of all streams", "p99_budget_ms": budget_ms, "producers": paced_workers,
+                        "fft": list(paced_fft)}
     return out
 
 
@@ -1036,9 +1142,40 @@ ALG_BYTES_PER_SF = {
     "k_tb_finish": lambda N: sum(k // 8 for k in C3_KS) + C3_TBS // 8,
 }
 HEADLINE_SNR_DB = 20.0
+# descriptor sets the headline cycles through (a new grant every step: no repeat-call cache hits)
+HEADLINE_DESCRIPTOR_SETS = 4
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
 HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 8}, "per_halfit": {"es_fused": 0},
                "fused_c8": {"es_fused": 1, "es_chunk": 8}, "hybrid": {"es_fused": 3, "es_chunk": 8}}
+
+
+def decoder_valu_roofline(leg):
+    """VALU roofline of the WHOLE turbo decoder of a coded leg: SURVEY 8(d)'s 90 int16 ops per info
+    bit per half-iteration, over every half-iteration every code block ran in the batch (the first,
+    k_win_bidir_h0, for all blocks; the early-stop continuation, k_win_bidir_es, for the blocks
+    still running; srsgpu_dlsch_cb_halfits), divided by the device time of all decoder launches of
+    the batch (HIP events on the lane streams). The per-launch-class split stays in `launches`."""
+    kt = leg["kernels_per_batch"]
+    h0, es = kt.get("k_win_bidir_h0"), kt.get("k_win_bidir_es")
+    bits = leg.get("halfit_bits_per_batch")
+    if not (h0 and h0["launches"]) or not bits:
+        return None
+    first_bits = sum(C3_KS) * C3_SF
+    ms = h0["ms"] + (es["ms"] if es else 0.0)
+    ops = ALG_OPS_PER_BIT_HALFIT * bits
+    rate = ops / (ms / 1e3) / 1e12
+    split = {"k_win_bidir_h0": {"ms_per_batch": h0["ms"], "launches": h0["launches"],
+                                "ops": ALG_OPS_PER_BIT_HALFIT * first_bits,
+                                "T_ops": round(ALG_OPS_PER_BIT_HALFIT * first_bits / (h0["ms"] / 1e3) / 1e12, 2)}}
+    if es and es["launches"]:
+        rest = ALG_OPS_PER_BIT_HALFIT * max(bits - first_bits, 0)
+        split["k_win_bidir_es"] = {"ms_per_batch": es["ms"], "launches": es["launches"], "ops": rest,
+                                   "T_ops": round(rest / (es["ms"] / 1e3) / 1e12, 3)}
+    return {"bound": "valu (packed int16)", "kernel": "turbo decoder, all launches (k_win_bidir_h0 + k_win_bidir_es)",
+            "achieved": round(rate, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
+            "frac": round(rate / VALU_INT16_PEAK_T, 4), "alg_ops_per_batch": int(ops),
+            "halfits_per_cb_mean": round(bits / first_bits, 4), "decoder_ms_per_batch": round(ms, 4),
+            "avg_launch_ms": round(ms / (h0["launches"] + (es["launches"] if es else 0)), 4), "launches": split}
 
 
 def pipeline_roofline(leg, nsf_per_batch):
@@ -1344,8 +1481,7 @@ def dist_check(dist, torch, rank, nranks):
 # keys of a leg's result reported in the compact summary line (one or two numbers per leg)
 LEG_SUMMARY = (
     ("c3_fixed8_codewords", "fixed8", ("subframes_per_s", "decoded_mbps", "ms_per_batch")),
-    ("c3_uncached", "uncached", ("subframes_per_s", "decoded_mbps", "host_ms_per_step", "host_ms_front_end",
-                                 "host_ms_dlsch")),
+    ("c3_cached", "cached", ("subframes_per_s", "decoded_mbps", "ms_per_batch", "host_ms_per_step")),
     ("pipeline_tm3_coded", "tm3_coded", ("subframes_per_s", "decoded_mbps")),
     ("pipeline_c5", "c5", ("subframes_per_s", "decoded_mbps")),
     ("pipeline_coded", "coded30", ("subframes_per_s", "decoded_mbps")),
@@ -1370,7 +1506,7 @@ def compact_summary(result, detail_name, limit=6000):
     cfg = result.get("config", {})
     out["config"] = {k: cfg[k] for k in ("workload", "baseline_config", "subframes_per_batch_per_gpu", "nof_prb",
                                          "fft_size", "mcs", "tbs", "code_blocks_per_subframe", "K", "snr_db",
-                                         "early_stop_max_halfits", "subframes_per_s", "nof_iterations_mean",
+                                         "early_stop_max_halfits", "descriptor_sets", "subframes_per_s", "nof_iterations_mean",
                                          "acked_tbs", "tbs_bytes_ok", "parallelism") if k in cfg}
     for key, fields in (("roofline", ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
                                       "traffic_over_alg", "traffic_source", "alg_bytes_per_launch", "avg_launch_ms",
@@ -1397,10 +1533,19 @@ def compact_summary(result, detail_name, limit=6000):
     if rq:
         sat = rq.get("saturated", {})
         top = max(sat, key=lambda k: sat[k]["subframes_per_s"], default=None)
+        def miss(fm):
+            return None if not fm else {k: fm.get(k) for k in (
+                "streams", "latency_ms_p99", "submit_latency_ms_p99", "producer_late_ms_max", "producer_late_ms_p99",
+                "failed", "acked", "mean_batch", "cpu_cores_busy", "cgroup_throttled_ms")}
+
         legs["rx_queue"] = {"real_time_streams": rq.get("real_time_streams"),
-                            "real_time_ingest": rq.get("real_time_streams_ingest"),
+                            "real_time_streams_1536": rq.get("real_time_streams_1536"),
+                            "queue_streams": rq.get("queue_streams"),
+                            "queue_streams_1536": rq.get("queue_streams_1536"),
+                            "first_miss": miss(rq.get("first_miss")),
+                            "first_miss_1536": miss(rq.get("first_miss_1536")),
                             "saturated_max_sfps": sat[top]["subframes_per_s"] if top else None,
-                            "saturated_max_mode": top}
+                            "saturated_max_mode": top, "cpu_quota": (rq.get("cpus") or {}).get("quota")}
     hd = result.get("headline_detail") or {}
     if hd.get("gather_ms") is not None:
         legs["headline_gather_ms"] = hd["gather_ms"]
@@ -1430,7 +1575,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=2, help="HIP streams per rank for the headline leg")
     ap.add_argument("--ab-headline", action="store_true",
                     help="A/B the decoder's early-stop launch schedules on the headline workload")
-    ap.add_argument("--legs", default="c2,fixed8,uncached,c3,tm3,tm3c,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
+    ap.add_argument("--legs", default="c2,fixed8,cached,c3,tm3,tm3c,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
                     help="legs after the headline (profiling aid); 'distcheck' alone rehearses the multi-rank "
                          "partition and gather on the CPU (gloo), without a GPU")
     ap.add_argument("--detail", default=os.path.join(REPO, "bench_detail.json"),
@@ -1493,25 +1638,19 @@ def main():
     # transmitter at 20 dB, time domain -> TB bytes: OFDM FFT, CRS channel estimation, PDSCH (RE
     # extraction, MMSE, 64QAM demap, descramble), DL-SCH (de-RM, turbo decoding with CRC early stop up
     # to 8 half-iterations as srsUE runs it, TB CRC). One step = one 1024-subframe batch.
+    # The descriptors change every step (four sets with different softbuffers in turn, rotate=4), as a
+    # receiver's grants do (pdsch.c:868-1007 is called with a fresh cfg per subframe): the PDSCH / DL-SCH
+    # repeat-call caches never hit, every step pays its per-code-block host work
     head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
                                    dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0, lanes=args.lanes,
-                                   warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None))
+                                   warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None,
+                                   rotate=HEADLINE_DESCRIPTOR_SETS))
     cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
     result = None
     if rank == 0:
         roof, ktable = pipeline_roofline(head, C3_SF)
         head["kernel_table"] = ktable
-        h0 = head["kernels_per_batch"].get("k_win_bidir_h0")
-        valu = None
-        if h0 and h0["launches"]:
-            # the first half-iteration of every code block: SURVEY 8(d)'s 90 int16 ops per info bit
-            avg = h0["ms"] / h0["launches"]
-            ops = ALG_OPS_PER_BIT_HALFIT * sum(C3_KS) * C3_SF / h0["launches"]
-            rate = ops / (avg / 1e3) / 1e12
-            valu = {"bound": "valu (packed int16)", "kernel": "k_win_bidir (first half-iteration, early-stop job)",
-                    "achieved": round(rate, 2), "peak": VALU_INT16_PEAK_T, "unit": "T int16-ops/s",
-                    "frac": round(rate / VALU_INT16_PEAK_T, 4), "alg_ops_per_launch": int(ops),
-                    "avg_launch_ms": round(avg, 4)}
+        valu = decoder_valu_roofline(head)
         result = {
             "metric": METRIC, "value": head["decoded_mbps"], "unit": "Mbps", "n_gpus": nranks, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": head["ms_per_batch"], "higher_is_better": True, "scaling": "weak",
@@ -1521,7 +1660,8 @@ def main():
                        "baseline_config": "BASELINE configs[2]", "subframes_per_batch_per_gpu": C3_SF,
                        "nof_prb": C3_PRB, "fft_size": head["symbol_size"], "mcs": 28, "tbs": C3_TBS,
                        "code_blocks_per_subframe": 13, "K": 5824, "snr_db": HEADLINE_SNR_DB,
-                       "early_stop_max_halfits": 8, "subframes_per_s": head["subframes_per_s"],
+                       "early_stop_max_halfits": 8, "descriptor_sets": HEADLINE_DESCRIPTOR_SETS,
+                       "subframes_per_s": head["subframes_per_s"],
                        "nof_iterations_mean": head["nof_iterations_mean"], "acked_tbs": head["acked_tbs"],
                        "tbs_bytes_ok": head["tbs_bytes_ok"], "parallelism": "dp%d" % nranks},
             "value_def": "decoded Mbps = sum of K over CRC-passing code blocks per second (SURVEY 8(d)), whole "
@@ -1543,14 +1683,16 @@ def main():
                                                   snr_db=HEADLINE_SNR_DB, dist=dist, early_stop=False))
     if "envab" in legs:
         # the headline workload with and without an environment setting (BENCH_AB_ENV="NAME=VALUE"), in
-        # turn in one process: A/B of a kernel variant the library reads from the environment per call
+        # turn in one process: A/B of a launch knob (wave_prio.h; srsgpu_knobs_reload after each change)
         name, _, val = os.environ.get("BENCH_AB_ENV", "SRSGPU_LLR_GENERIC=1").partition("=")
         for on in (0, 1, 0, 1, 0, 1):
             if on:
                 os.environ[name] = val
+            s.knobs_reload()
             r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
                             lanes=args.lanes)
             os.environ.pop(name, None)
+            s.knobs_reload()
             extra.setdefault("envab", []).append({name: val if on else None, "ms_per_batch": r["ms_per_batch"],
                                                   "stage_ms": r["stage_ms_per_batch"], "acked_tbs": r["acked_tbs"],
                                                   "tbs_bytes_ok": r["tbs_bytes_ok"]})
@@ -1562,11 +1704,12 @@ def main():
             extra.setdefault("tailab", []).append({"tail": t, "ms_per_batch": r["ms_per_batch"],
                                                    "decoded_mbps": r["decoded_mbps"], "acked_tbs": r["acked_tbs"],
                                                    "tbs_bytes_ok": r["tbs_bytes_ok"]})
-    if "uncached" in legs:
-        # the headline workload with a different descriptor set every step (4 sets: other softbuffers),
-        # so the PDSCH / DL-SCH repeat-call caches never hit: the host cost of changing grants
-        extra["uncached"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
-                                                    snr_db=HEADLINE_SNR_DB, dist=dist, rotate=4))
+    if "cached" in legs:
+        # the headline workload with ONE descriptor set repeated every step, so the PDSCH / DL-SCH
+        # repeat-call caches hit (no per-code-block host work): what a receiver never sees, kept as the
+        # upper bound beside the headline, whose descriptors change every step
+        extra["cached"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
+                                                  snr_db=HEADLINE_SNR_DB, dist=dist, rotate=1))
     if "n1536" in legs:
         # srsLTE's reduced 20 MHz sampling (1536-point FFT, SURVEY 8(d) "N=1536")
         extra["n1536"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
@@ -1662,8 +1805,8 @@ def main():
             result["config"]["subframes_per_s_fixed8"] = extra["fixed8"]["subframes_per_s"]
         if "n1536" in extra:
             result["c3_fft1536"] = extra["n1536"]
-        if "uncached" in extra:
-            result["c3_uncached"] = extra["uncached"]
+        if "cached" in extra:
+            result["c3_cached"] = extra["cached"]
         if "tailab" in extra:
             result["tail_ab"] = extra["tailab"]
         if "envab" in extra:

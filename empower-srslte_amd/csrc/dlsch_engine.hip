@@ -149,6 +149,10 @@ struct DlschEngine {
   // decoder inputs (k_load_derm) and their softbuffer rows written after the decode, only for TBs
   // that failed (the only rows the reference reads again)
   bool direct_derm = true;
+  // the epilogue (k_tb_finish) also makes the bytes of the blocks the fused early stop ended and the
+  // rows of failed TBs: two launches fewer per call (SRSGPU_EPILOGUE=split: the separate k_es_bytes
+  // and k_derm_late, for A/B; read at create)
+  bool fused_epilogue = true;
   std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint16_t *> tables, inv_tables, inv_t4_tables;
   TdecEngine tdec;
   // transmit side: per-CB encode descriptors (lazily allocated) and the long CRC24A table
@@ -167,6 +171,7 @@ struct DlschEngine {
     nslots = slots;
     max_cb = mcb;
     cap = cap_cbs;
+    if (const char *e = getenv("SRSGPU_EPILOGUE")) fused_epilogue = strcmp(e, "split") != 0;
     const size_t rows = (size_t)slots * mcb;
     HIPCHK(hipMalloc(&soft, rows * SRSGPU_SOFTBUFFER_SIZE * 2));
     HIPCHK(hipMemset(soft, 0, rows * SRSGPU_SOFTBUFFER_SIZE * 2));
@@ -451,6 +456,7 @@ struct DlschEngine {
 
   // srsgpu_dlsch_set_tail_stream: the early-stop tail of a decode call runs on tail_st; the engine's
   // next work on st waits for it (join_tail, at every entry point that enqueues work)
+  uint32_t last_ncb = 0; // code blocks of the last decode call (d_noi holds their half-iterations)
   hipStream_t tail_st = nullptr;
   hipEvent_t ev_tail = nullptr;
   bool tail_pending = false;
@@ -667,6 +673,7 @@ struct DlschEngine {
                     const int16_t *e_base, const std::vector<TdSpec> &specs, uint32_t ntb, uint32_t maxh,
                     int32_t *d_ret, uint32_t derm_max_ne) {
     tdec.derm_max_ne = derm_max_ne;
+    last_ncb = ncb;
     const TbItem *d_tbs_c = reinterpret_cast<const TbItem *>(d_blk + o_tbs);
     const uint32_t *d_map_c = reinterpret_cast<const uint32_t *>(d_blk + o_map);
     const int16_t *const *d_rows_c = reinterpret_cast<const int16_t *const *>(d_blk + o_rows);
@@ -676,6 +683,11 @@ struct DlschEngine {
       ProfScope ps("k_derm", st);
       HIPCHK(launch_derm(dc, (int)ncb, d_init, st));
     }
+    // the epilogue makes the bytes of the blocks the fused early stop ended (no k_es_bytes) and the
+    // rows of failed TBs (no k_derm_late) itself, unless SRSGPU_EPILOGUE=split (A/B) or a TB may hold
+    // more blocks than it has LDS slots for
+    tdec.defer_bytes = fused_epilogue && max_cb <= 32;
+    tdec.bytes_deferred = false;
     if (!specs.empty() &&
         tdec.decode_multi(llr8 ? SRSGPU_TDEC_AUTO_8BIT : SRSLTE_TDEC_AUTO, 1, specs, norder, nullptr, 0,
                           d_rows_c, 16, d_init, maxh, d_dec, 768, d_ok, d_noi, fixed, ndirect ? &dc : nullptr))
@@ -683,12 +695,15 @@ struct DlschEngine {
     // the epilogue on the stream the decoder job ended on (the tail stream when it split)
     const hipStream_t es = tdec.st;
     tdec.st = st;
+    FzSrc fz;
+    if (tdec.bytes_deferred) fz = FzSrc{tdec.d_groups, (int)tdec.groups.size(), tdec.Dfz, tdec.cb_end};
+    const bool inline_rows = ndirect && fused_epilogue;
     {
       ProfScope ps("k_tb_finish", es);
       HIPCHK(launch_tb_finish(d_tbs_c, (int)ntb, d_map_c, d_dec, 768, d_ok, d_init, d_noi, d_crc_a, es,
-                              ndirect ? dc : DermCall{}, ndirect ? d_late : nullptr));
+                              ndirect ? dc : DermCall{}, ndirect && !inline_rows ? d_late : nullptr, fz, inline_rows));
     }
-    if (ndirect) { // rows of the direct blocks of failed TBs, for the retransmission
+    if (ndirect && !inline_rows) { // rows of the direct blocks of failed TBs, for the retransmission
       ProfScope ps("k_rows_late", es); // k_derm_late
       HIPCHK(launch_derm_late(dc, (int)ncb, d_late, es));
     }
@@ -745,6 +760,17 @@ int srsgpu_dlsch_set_tail_stream(srsgpu_dlsch_t *q, void *s) {
   if (!q || q->e.join_tail()) return -1;
   q->e.tail_st = (hipStream_t)s;
   return 0;
+}
+
+int srsgpu_dlsch_join_tail(srsgpu_dlsch_t *q) { return q ? q->e.join_tail() : -1; }
+
+int srsgpu_dlsch_cb_halfits(srsgpu_dlsch_t *q, uint32_t *out, uint32_t n) {
+  if (!q || (!out && n) || q->e.join_tail()) return -1;
+  const uint32_t m = std::min(n, q->e.last_ncb);
+  if (m && (hipMemcpyAsync(out, q->e.d_noi, sizeof(uint32_t) * m, hipMemcpyDeviceToHost, q->e.st) != hipSuccess ||
+            hipStreamSynchronize(q->e.st) != hipSuccess))
+    return -1;
+  return (int)q->e.last_ncb;
 }
 
 int srsgpu_dlsch_softbuffer_reset(srsgpu_dlsch_t *q, uint32_t slot) {

@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "tdec_kernels.h"
+
 namespace srsgpu {
 
 // one code block to de-rate-match into its softbuffer row
@@ -96,10 +98,22 @@ hipError_t launch_sb_reset(uint8_t *fresh, uint8_t *cbcrc, uint32_t count, uint3
 // crc_a[d] = x^(d+24) mod P_24A for d < the largest TBS + 24
 // dc.rec / late (both or neither): a failed TB appends its direct blocks not decoded before the
 // call to late (launch_derm_late)
+// The decision words of the blocks a fused early-stop launch ended (the decoder job's Dfz / cb_end and
+// its group table, tdec_kernels.h TdEs): with groups set, k_tb_finish turns those blocks' words into
+// their natural-order bytes itself (k_es_bytes' work, no launch of its own) and clears cb_end.
+struct FzSrc {
+  const TdGroup *groups = nullptr;
+  int ngroups = 0;
+  const uint32_t *dfz = nullptr;
+  uint8_t *cb_end = nullptr;
+};
+// inline_rows (with dc.rec, late null): a failed TB's workgroup writes the rows of its direct blocks
+// not decoded before the call itself (k_derm_late's work, no launch of its own)
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
                             const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
-                            const DermCall &dc = DermCall{}, uint32_t *late = nullptr);
+                            const DermCall &dc = DermCall{}, uint32_t *late = nullptr,
+                            const FzSrc &fz = FzSrc{}, bool inline_rows = false);
 // crc_a: x^(d+24) mod CRC24A for d < tbs; crc_b: the same for CRC24B, d < 6144
 hipError_t launch_dlsch_encode(const EncItem *d_items, int n, const uint32_t *crc_a,
                                const uint32_t *crc_b, hipStream_t st);
@@ -124,7 +138,6 @@ hipError_t launch_uci_cqi(const UlItem *d_items, int n, const int16_t *q, const 
                           int32_t *ret, uint32_t *noi, hipStream_t st);
 } // namespace srsgpu
 
-#include "tdec_kernels.h"
 namespace srsgpu {
 // Direct de-rate-matching for the window decoders: the decoder inputs SP0 / P1 / T of groups
 // [0, ng) of dg (sub-block rows, nb a multiple of 8) computed from each code block's LLRs and its

@@ -474,6 +474,52 @@ __device__ __forceinline__ uint32_t wg_xor(uint32_t v, uint32_t *red) {
 // the CRC weights are fetched eight bytes per thread and round: the TB's dependent loads are a few
 // round trips, not one chain per CB (the CB-serial form spent ~60 us per 512-TB launch waiting).
 #define TBF_MAXC 64 // > SRSLTE_MAX_CODEBLOCKS (phy_common.h:57)
+#define TBF_FZ 32   // code blocks of one TB whose bytes the workgroup makes from decision words (FzSrc)
+
+// Natural-order bytes of decoder block g from its frozen decision words (es_check / sse_es_check:
+// Dfz, cb_end = 1 + parity of the half-iteration that ended it), exactly as k_es_bytes writes them
+// (turbodecoder.c:353-360 + decision_byte, MSB first), into `out` (LDS) by the whole workgroup.
+__device__ void fz_bytes(const FzSrc &fz, int gi, int g, int end, uint32_t *dw, uint8_t *out) {
+  const TdGroup &G = fz.groups[gi];
+  const int K = G.K, NB = G.nb, c = g - G.cb0, pair = c >> 1, h = c & 1;
+  const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
+  const gp_t<const uint32_t> src = glob(fz.dfz + G.dw0 + (size_t)pair * nw);
+  for (int q = threadIdx.x; q < nw; q += blockDim.x) dw[q] = src[q];
+  __syncthreads();
+  const gp_t<const uint16_t> dmap = glob(G.dmap);
+  const bool dec2 = end == 2;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float invL = 1.0f / (float)L;
+  const int gap = 16 * G16 - L;
+  constexpr int PMAX = 6144 / 256;
+  int ci[PMAX];
+#pragma unroll
+  for (int u = 0; u < PMAX; u++) { // every map load issued before the first use
+    const int p = wv * 64 + u * 256 + lane;
+    int cc = 0;
+    if (p < K) {
+      if (dec2) {
+        cc = (int)dmap[p];
+      } else {
+        const int d = (int)(((float)p + 0.5f) * invL); // exact: see k_decide
+        cc = p + d * gap;
+      }
+    }
+    ci[u] = cc;
+  }
+#pragma unroll
+  for (int u = 0; u < PMAX; u++) {
+    const int p0 = wv * 64 + u * 256;
+    if (p0 >= K) break;
+    const int p = p0 + lane;
+    const uint32_t bit = p < K ? (dw[ci[u] >> 4] >> ((ci[u] & 15) + 16 * h)) & 1u : 0u;
+    const uint64_t m = __ballot(bit);
+    if (lane < 8 && p0 + 8 * lane < K)
+      out[(p0 >> 3) + lane] = (uint8_t)(__builtin_bitreverse32((uint32_t)((m >> (8 * lane)) & 0xffu)) >> 24);
+  }
+  __syncthreads(); // dw is reused by the next block
+}
+
 __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tbs_, int ntb,
                                                    const uint32_t *__restrict__ cbmap,
                                                    const uint8_t *__restrict__ dec, size_t dec_stride,
@@ -481,12 +527,20 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
                                                    const uint8_t *__restrict__ init_done,
                                                    const uint32_t *__restrict__ noi_in,
                                                    const uint32_t *__restrict__ crc_a, DermCall dc,
-                                                   uint32_t *__restrict__ late, int prio) {
+                                                   uint32_t *__restrict__ late, int prio, FzSrc fz,
+                                                   int inline_rows) {
   __shared__ uint32_t red[4];
   __shared__ uint32_t crc_tab[256];
   __shared__ uint32_t c_ck0[TBF_MAXC + 1];
   __shared__ uint32_t c_g[TBF_MAXC], c_dst[TBF_MAXC], c_nb[TBF_MAXC], c_rb[TBF_MAXC];
   __shared__ uint8_t c_init[TBF_MAXC], c_ok[TBF_MAXC];
+  __shared__ int8_t c_fz[TBF_MAXC];    // slot of the block's bytes in fzb, -1: in dec / saved
+  __shared__ uint8_t c_end[TBF_MAXC];  // cb_end of the block (FzSrc)
+  __shared__ int16_t c_grp[TBF_MAXC];  // its decoder group
+  __shared__ uint32_t fz_dw[6144 / 16 + 16];
+  // the bytes made here (TBF_FZ blocks x 768), later the LLR staging of the inline rows (DERM_LDS)
+  __shared__ __attribute__((aligned(16))) uint32_t fz_lds[(TBF_FZ * 768 > DERM_LDS * 2 ? TBF_FZ * 768 : DERM_LDS * 2) / 4];
+  uint8_t *fzb = reinterpret_cast<uint8_t *>(fz_lds);
   __shared__ int all_ok;
   __shared__ uint32_t noi_sum;
   wave_prio(prio);
@@ -540,8 +594,42 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       all_ok = ok;
       noi_sum = s;
     }
+    // blocks a fused early-stop launch ended: their bytes are made here from the decision words
+    c_fz[i] = -1;
+    if (fz.groups && i < C && !c_init[i]) {
+      const int g = (int)c_g[i];
+      const uint8_t end = glob(fz.cb_end)[g];
+      c_end[i] = end;
+      if (end) {
+        int gi = 0;
+        while (gi + 1 < fz.ngroups && !(fz.groups[gi].cb0 <= g && g < fz.groups[gi].cb0 + fz.groups[gi].ncb)) gi++;
+        c_grp[i] = (int16_t)gi;
+      }
+    } else if (i < C) {
+      c_end[i] = 0;
+    }
   }
   __syncthreads();
+  if (fz.groups) {
+    int slot = 0;
+    for (uint32_t i = 0; i < C; i++) {
+      if (!c_end[i]) continue;
+      if (slot < TBF_FZ) {
+        fz_bytes(fz, c_grp[i], (int)c_g[i], c_end[i], fz_dw, fzb + 768 * slot);
+        if (threadIdx.x == 0) {
+          c_fz[i] = (int8_t)slot;
+          glob(fz.cb_end)[c_g[i]] = 0;
+        }
+        slot++;
+      }
+    }
+    __syncthreads();
+  }
+  // where CB i's bytes are: made here (LDS), saved from an earlier transmission, or its decision row
+  auto cb_src = [&](uint32_t i) -> const uint8_t * {
+    if (c_fz[i] >= 0) return fzb + 768 * c_fz[i];
+    return c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride;
+  };
   // 2. TB bytes, CBs in order (a later CB's bytes win where the regions meet, as the reference's
   //    sequential copies): the (CB, byte) pairs of the TB spread over all threads
   //    Eight CBs at a time: their bytes (at most 768 = 3 x 256 per CB) are all loaded before any
@@ -552,7 +640,7 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
     for (int u = 0; u < 8; u++) {
       const uint32_t i = i0 + u;
       if (i >= C) break;
-      const uint8_t *src = c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride;
+      const uint8_t *src = cb_src(i);
 #pragma unroll
       for (int r = 0; r < 3; r++) {
         const uint32_t j = threadIdx.x + r * 256;
@@ -584,6 +672,12 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       const uint8_t *src = t.data + c_dst[i];
       uint8_t *dst = t.saved + (size_t)i * 768;
       for (uint32_t j = threadIdx.x; j < c_rb[i]; j += blockDim.x) dst[j] = src[j];
+    }
+    if (inline_rows && dc.rec) {
+      // the rows themselves (k_derm_late's work): the bytes in fzb are consumed, its LDS stages the LLRs
+      __syncthreads();
+      for (uint32_t i = 0; i < C; i++)
+        if (!c_init[i] && dc.rec[c_g[i]].direct) derm_item(derm_get(dc, c_g[i]), fz_lds);
     }
   }
   // 3. TB CRC24A over tbs bits vs the 24 bits that follow (sch.c:475-491). crc.c:144-155 (MSB
@@ -618,8 +712,16 @@ __global__ __launch_bounds__(256) void k_tb_finish(const TbItem *__restrict__ tb
       while (c_ck0[i + 1] <= q) i++;
       const uint32_t off = 32 * (q - c_ck0[i]);
       const uint32_t len = min(c_rb[i], nbytes - c_dst[i]), n = min(32u, len - off);
-      const uint8_t *src = (c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride) + off;
-      const u4v w0 = *glob(reinterpret_cast<const u4v *>(src)), w1 = *glob(reinterpret_cast<const u4v *>(src + 16));
+      u4v w0, w1;
+      if (c_fz[i] >= 0) {
+        const u4v *src = reinterpret_cast<const u4v *>(fzb + 768 * c_fz[i] + off);
+        w0 = src[0];
+        w1 = src[1];
+      } else {
+        const uint8_t *src = (c_init[i] ? t.saved + (size_t)i * 768 : glob_g(dec) + (size_t)c_g[i] * dec_stride) + off;
+        w0 = *glob(reinterpret_cast<const u4v *>(src));
+        w1 = *glob(reinterpret_cast<const u4v *>(src + 16));
+      }
       const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       const uint32_t after = nbytes - (c_dst[i] + off + n); // bytes after the chunk
       const uint32_t shift = after == 0 ? 1u : 8 * after < 24 ? (1u << (8 * after)) : crc_a[8 * after - 24];
@@ -740,10 +842,11 @@ hipError_t launch_derm_rmw(const DermItem *d_item, uint32_t n, hipStream_t st) {
 hipError_t launch_tb_finish(const TbItem *d_tbs, int ntb, const uint32_t *cbmap, const uint8_t *dec,
                             size_t dec_stride, const uint8_t *cb_ok, const uint8_t *init_done,
                             const uint32_t *noi, const uint32_t *crc_a, hipStream_t st,
-                            const DermCall &dc, uint32_t *late) {
+                            const DermCall &dc, uint32_t *late, const FzSrc &fz, bool inline_rows) {
   if (ntb <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_tb_finish, dim3((unsigned)ntb), dim3(256), 0, st, d_tbs, ntb, cbmap, dec,
-                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late, env_prio("SRSGPU_TAIL_PRIO", 3));
+                     dec_stride, cb_ok, init_done, noi, crc_a, dc, late, knobs().tail_prio, fz,
+                     inline_rows ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -106,19 +106,59 @@ struct PdschEngine {
   // one scrambling sequence per distinct seed of a call (a UE's TBs use at most 10 subframe seeds per
   // codeword): the TBs that share a seed read the same words
   std::unordered_map<uint32_t, uint32_t> gold_slot;
-  uint32_t ngold = 0;
+  uint32_t ngold = 0, nper = 0;
+  // Sequences kept across calls: a receiver sees a handful of seeds (RNTI x codeword x subframe; the
+  // reference pre-generates them per user, pdsch.c:436-440), so the first GCACHE distinct seeds get a
+  // full-length sequence generated once and reused by every later call (no k_gold launch and no item
+  // upload when a call's seeds are all known). A seed first met in a call is generated by that call's
+  // k_gold and becomes usable by later calls once the launch is enqueued (gold_commit); the cache is
+  // cleared when the stream changes (the entries were made in another stream's order).
+  static constexpr uint32_t GCACHE = 64;
+  uint32_t *d_gcache = nullptr;
+  std::unordered_map<uint32_t, uint32_t> gcache; // seed -> slot of d_gcache
+  std::vector<std::pair<uint32_t, uint32_t>> gcache_new; // this call's additions (seed, slot)
   const uint32_t *gold(uint32_t seed, uint32_t len) {
+    auto hit = gcache.find(seed);
+    if (hit != gcache.end()) return d_gcache + (size_t)hit->second * cwords;
     auto it = gold_slot.find(seed);
     if (it == gold_slot.end()) {
       GoldItem &g = h_gold[ngold];
       g.seed = seed;
-      g.len = len;
-      g.c = d_c + (size_t)ngold * cwords;
+      const uint32_t slot = (uint32_t)(gcache.size() + gcache_new.size());
+      if (d_gcache && slot < GCACHE) {
+        g.len = max_bits;
+        g.c = d_gcache + (size_t)slot * cwords;
+        gcache_new.push_back({seed, slot});
+      } else {
+        g.len = len;
+        g.c = d_c + (size_t)nper++ * cwords;
+      }
       it = gold_slot.emplace(seed, ngold++).first;
     } else if (h_gold[it->second].len < len) {
       h_gold[it->second].len = len; // the sequence's prefix does not depend on its length
     }
     return h_gold[it->second].c;
+  }
+  void gold_reset() {
+    gold_slot.clear();
+    gcache_new.clear();
+    ngold = nper = 0;
+  }
+  // after the call's k_gold is enqueued: its new full-length sequences serve later calls
+  void gold_commit() {
+    for (const auto &kv : gcache_new) gcache.emplace(kv.first, kv.second);
+    gcache_new.clear();
+  }
+  // the call's generation (only sequences not already on the device)
+  int gold_launch() {
+    if (!ngold) return 0;
+    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
+    {
+      ProfScope ps("k_gold", st);
+      HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
+    }
+    gold_commit();
+    return 0;
   }
   uint32_t gold_bits() const {
     uint32_t m = 0;
@@ -189,6 +229,7 @@ struct PdschEngine {
     HIPCHK(hipMalloc(&d_csi, (size_t)mtb * max_re * 4));
     HIPCHK(hipMalloc(&d_csimax, (size_t)mtb * 4));
     HIPCHK(hipMalloc(&d_e, (size_t)mtb * max_bits * 2));
+    HIPCHK(hipMalloc(&d_gcache, (size_t)GCACHE * cwords * 4));
     return 0;
   }
 
@@ -196,7 +237,7 @@ struct PdschEngine {
     if (st) (void)hipStreamSynchronize(st);
     for (void *p : {(void *)d_x1, (void *)d_x2b, (void *)d_gold, (void *)d_llr, (void *)d_c,
                     (void *)d_csi, (void *)d_csimax, (void *)d_e, (void *)d_tx, (void *)d_ebits,
-                    (void *)d_mod, (void *)d_fb})
+                    (void *)d_mod, (void *)d_fb, (void *)d_gcache})
       if (p) (void)hipFree(p);
     ring.destroy();
     for (void *p : {(void *)h_tb, (void *)h_fb})
@@ -344,8 +385,7 @@ struct PdschEngine {
     uint32_t mre = 0, k = 0;
     int n_dual = 0;
     bool p0 = true;
-    gold_slot.clear();
-    ngold = 0;
+    gold_reset();
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
@@ -406,14 +446,10 @@ struct PdschEngine {
         mre = std::max(mre, nre);
       }
     }
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
+    if (gold_launch()) return -1;
     HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * k, hipMemcpyHostToDevice, st));
     HIPCHK(ring.mark(st));
     if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)k * 4, st));
-    {
-      ProfScope ps("k_gold", st);
-      HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
-    }
     ProfScope ps("k_pdsch_llr", st);
     HIPCHK(launch_pdsch_llr(d_llr, (int)k, mre, csi, st, n_dual, p0 && cell.nof_rx_ant <= 2 ? (int)cell.nof_rx_ant : 0));
     memo_key.swap(memo_scratch);
@@ -461,8 +497,7 @@ struct PdschEngine {
     if (ring_take()) return -1;
     memo_valid = false; // the sequences and items below overwrite the ones llr() keeps
     uint32_t mre = 0, k = 0;
-    gold_slot.clear();
-    ngold = 0;
+    gold_reset();
     for (uint32_t i = 0; i < n; i++) {
       const srsgpu_pdsch_sf_t &s = sf[i];
       if (check(s, i)) return -1;
@@ -522,10 +557,9 @@ struct PdschEngine {
       mre = std::max(mre, nre);
     }
     if (srsgpu_dlsch_encode_dev(dl, h_tb, k, d_data, d_ebits)) return -1;
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
+    if (gold_launch()) return -1;
     HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
     HIPCHK(ring.mark(st));
-    HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
     ProfScope ps("k_pdsch_tx", st);
     HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));
     return 0;
@@ -611,6 +645,7 @@ void srsgpu_pdsch_destroy(srsgpu_pdsch_t *q) {
 
 void srsgpu_pdsch_set_stream(srsgpu_pdsch_t *q, void *s) {
   if (!q) return;
+  if (q->e.st != (hipStream_t)s) q->e.gcache.clear(); // kept sequences were made in the old stream's order
   q->e.st = (hipStream_t)s;
   srsgpu_dlsch_set_stream(q->e.dl, s);
 }
@@ -649,6 +684,7 @@ int srsgpu_pdsch_nof_re(const srsgpu_cell_t *cell, const srsgpu_pdsch_sf_t *sf) 
 int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const float *d_grid,
                          const float *d_ce, size_t ant_stride, int16_t *d_e, const uint64_t *e_offset) {
   if (!q || (!sf && n) || !d_grid || !d_ce || !d_e || !e_offset) return -1;
+  if (srsgpu_dlsch_join_tail(q->e.dl)) return -1; // the previous call's tail may read its LLRs
   const uint32_t k = q->e.count_tb(sf, n);
   std::vector<int16_t *> e(k);
   for (uint32_t i = 0; i < k; i++) e[i] = d_e + e_offset[i];
@@ -657,19 +693,19 @@ int srsgpu_pdsch_llr_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_
 
 int srsgpu_pdsch_encode_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n,
                             const uint8_t *d_data, float *d_grid) {
-  if (!q || (!sf && n) || !d_data || !d_grid) return -1;
+  if (!q || (!sf && n) || !d_data || !d_grid || srsgpu_dlsch_join_tail(q->e.dl)) return -1;
   return q->e.encode(sf, n, d_data, d_grid, 0);
 }
 
 int srsgpu_pdsch_encode_ports_dev(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t n, const uint8_t *d_data,
                                   float *d_grid, size_t port_stride) {
-  if (!q || (!sf && n) || !d_data || !d_grid) return -1;
+  if (!q || (!sf && n) || !d_data || !d_grid || srsgpu_dlsch_join_tail(q->e.dl)) return -1;
   return q->e.encode(sf, n, d_data, d_grid, (uint64_t)port_stride);
 }
 
 int srsgpu_pdsch_feedback_dev(srsgpu_pdsch_t *q, const srsgpu_feedback_sf_t *sf, uint32_t n, const float *d_ce,
                               size_t ant_stride, const float *d_noise, srsgpu_feedback_t *d_out) {
-  if (!q || (!sf && n) || !d_ce || !d_out) return -1;
+  if (!q || (!sf && n) || !d_ce || !d_out || srsgpu_dlsch_join_tail(q->e.dl)) return -1;
   return q->e.feedback(sf, n, d_ce, ant_stride, d_noise, d_out);
 }
 
@@ -696,6 +732,9 @@ static int pdsch_decode(srsgpu_pdsch_t *q, const srsgpu_pdsch_sf_t *sf, uint32_t
                         int32_t *d_ret, uint32_t *d_noi) {
   if (!q || (!sf && n) || !d_grid || !d_ce || !d_ret || !d_noi) return -1;
   PdschEngine &E = q->e;
+  // a tail of the previous call (srsgpu_dlsch_set_tail_stream on srsgpu_pdsch_get_dlsch) still reads
+  // E.d_e, which llr() rewrites on st: the stream waits for it first
+  if (srsgpu_dlsch_join_tail(E.dl)) return -1;
   const uint32_t k = E.count_tb(sf, n);
   std::vector<int16_t *> e(k);
   for (uint32_t i = 0; i < k; i++) e[i] = E.d_e + (size_t)i * E.max_bits;

@@ -25,6 +25,7 @@
 #include "pdsch_kernels.h"
 #include "srsgpu/pdsch_batch.h"
 #include "gmem.h"
+#include "wave_prio.h"
 
 // The equaliser must round like the reference's separate SSE/AVX multiplies and adds: no FMA
 // contraction anywhere in this file (HIP's __fmul_rn is a plain '*').
@@ -818,9 +819,9 @@ hipError_t launch_pdsch_llr(const LlrItem *d_items, int n, uint32_t max_re, bool
                             int n_dual, int p0) {
   if (n <= 0) return hipSuccess;
   const unsigned gx = std::min(cdiv(max_re, 256 * LLR_RES), 64u);
-  const bool generic = getenv("SRSGPU_LLR_GENERIC") != nullptr; // A/B: the general kernel only
+  const bool generic = knobs().llr_generic; // A/B: the general kernel only
   if (p0 && !n_dual && !generic) {
-    const int xcd = getenv("SRSGPU_LLR_NOXCD") ? 0 : 1; // A/B: the plain item-major mapping
+    const int xcd = knobs().llr_noxcd ? 0 : 1; // A/B: the plain item-major mapping
     const unsigned parts = gx ? gx : 1, nb = parts * ((unsigned)(n + 7) / 8) * 8; // items rounded up to 8
     if (p0 == 1)
       hipLaunchKernelGGL(k_pdsch_llr_p0<1>, dim3(nb), dim3(256), 0, st, d_items, n, (int)parts, xcd);

@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <pthread.h>
+#include <sched.h>
 #include <string.h>
 #include <time.h>
 
@@ -285,6 +287,7 @@ struct srsgpu_rxq {
     const char *h;
     size_t bytes;
     const char *d; // device view of the same memory
+    bool owned;    // srsgpu_rxq_alloc_host (hipHostMalloc'd here), else the caller's (hipHostRegister'd)
   };
   std::vector<Region> regions; // guarded by m
   uint64_t zero_copy_rows = 0, staged_rows = 0, zero_copy_tbs = 0, staged_tbs = 0, dma_copies = 0;
@@ -292,6 +295,12 @@ struct srsgpu_rxq {
   // on the device; false (SRSGPU_RXQ_INGEST=kernel) the ingest kernel reads them over the bus
   bool ingest_dma = true;
   bool wake_all = false; // SRSGPU_RXQ_WAKE_ALL=1: every submission wakes the closer (diagnosis)
+  // The queue's waits on the GPU (a batch's results, the control channel's round trips) block on the
+  // completion interrupt instead of spinning a core (hipEventBlockingSync): a PHY host shares its cores
+  // with the radio and the stack, and a container's CPU quota counts a spinning waiter in full (the GPU
+  // box: 16 CPUs of quota over 256 visible cores). SRSGPU_RXQ_SPIN=1 spins (A/B).
+  bool spin_wait = false;
+  hipEvent_t ev_ctl = nullptr; // control(): the CFI / DCI results are on the host
   std::vector<std::pair<const char *, uint32_t>> reg; // stage(): registered rows by host address
   static constexpr size_t kMaxGap = 512 * 1024;        // stage(): bytes between rows one span may bridge
   // device view of a registered host pointer holding `bytes`, or null (caller holds m); aligned16: the
@@ -358,6 +367,8 @@ struct srsgpu_rxq {
     srsgpu_chest_set_stream(chest, st);
     srsgpu_pdsch_set_stream(pdsch, st);
     if (const char *e = getenv("SRSGPU_RXQ_SLOTS")) nslot = std::min(std::max(atoi(e), 3), NSLOT);
+    if (const char *e = getenv("SRSGPU_RXQ_SPIN")) spin_wait = e[0] == '1';
+    RXQ_CHK(hipEventCreateWithFlags(&ev_ctl, hipEventDisableTiming | (spin_wait ? 0u : hipEventBlockingSync)));
     for (int k = 0; k < nslot; k++) {
       Slot &s = slot[k];
       RXQ_CHK(hipMalloc(&s.d_td, sizeof(float) * 2 * td_len * mb * nrx));
@@ -369,7 +380,7 @@ struct srsgpu_rxq {
       s.h_rgn.assign((size_t)mb * nrx, nullptr);
       RXQ_CHK(hipMalloc(&s.d_reg, sizeof(float) * 2 * td_len * mb * nrx));
       RXQ_CHK(hipEventCreateWithFlags(&s.staged, hipEventDisableTiming));
-      RXQ_CHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+      RXQ_CHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming | (spin_wait ? 0u : hipEventBlockingSync)));
       RXQ_CHK(hipHostMalloc(&s.h_est, mb));
       RXQ_CHK(hipHostMalloc(&s.h_cfo_src, sizeof(int32_t) * mb));
       RXQ_CHK(hipHostMalloc(&s.h_sel, sizeof(uint32_t) * mb));
@@ -455,7 +466,7 @@ struct srsgpu_rxq {
       if (s.staged) (void)hipEventDestroy(s.staged);
       if (s.done) (void)hipEventDestroy(s.done);
     }
-    for (const Region &r : regions) (void)hipHostUnregister((void *)r.h);
+    for (const Region &r : regions) (void)(r.owned ? hipHostFree((void *)r.h) : hipHostUnregister((void *)r.h));
     regions.clear();
     for (void *p : {(void *)d_grid, (void *)d_ce, (void *)d_noise, (void *)d_data, (void *)d_ret,
                     (void *)d_noi, (void *)d_noise_last, (void *)d_est, (void *)d_sel, (void *)d_uenoise,
@@ -465,6 +476,7 @@ struct srsgpu_rxq {
       if (p) (void)hipFree(p);
     for (void *p : {(void *)h_cfi, (void *)h_corr, (void *)h_res, (void *)h_res_ul})
       if (p) (void)hipHostFree(p);
+    if (ev_ctl) (void)hipEventDestroy(ev_ctl);
     if (st) (void)hipStreamDestroy(st);
     if (cst) (void)hipStreamDestroy(cst);
   }
@@ -726,7 +738,8 @@ struct srsgpu_rxq {
     if (srsgpu_pcfich_decode_dev(pcfich, pc.data(), nu, d_grid, d_ce, gsz, d_cfi, d_corr, st)) return -1;
     RXQ_CHK(hipMemcpyAsync(h_cfi, d_cfi, sizeof(uint32_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipMemcpyAsync(h_corr, d_corr, sizeof(float) * nu, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipStreamSynchronize(st));
+    RXQ_CHK(hipEventRecord(ev_ctl, st));
+    RXQ_CHK(hipEventSynchronize(ev_ctl));
     uint32_t plen, pres;
     bool rebuild;
     {
@@ -757,7 +770,8 @@ struct srsgpu_rxq {
       return -1;
     RXQ_CHK(hipMemcpyAsync(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipMemcpyAsync(h_res_ul, d_res_ul, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipStreamSynchronize(st));
+    RXQ_CHK(hipEventRecord(ev_ctl, st));
+    RXQ_CHK(hipEventSynchronize(ev_ctl));
     // the workers' TM3 / TM4 feedback on the same estimates (phch_worker.cc:522-540); its results come
     // back with the batch's other results
     bool any = false;
@@ -1191,21 +1205,54 @@ int srsgpu_rxq_register(srsgpu_rxq_t *q, void *host, size_t bytes) {
     return -1;
   }
   std::lock_guard<std::mutex> l(q->m);
-  q->regions.push_back({(const char *)host, bytes, (const char *)d});
+  q->regions.push_back({(const char *)host, bytes, (const char *)d, false});
+  return 0;
+}
+
+// remove a region of the given kind once nothing queued or in flight points into it: 0, -1 if there
+// is no such region, -2 if it is of the other kind (then kept)
+static int rxq_drop_region(srsgpu_rxq_t *q, void *host, bool owned) {
+  std::unique_lock<std::mutex> l(q->m);
+  q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; });
+  auto it = std::find_if(q->regions.begin(), q->regions.end(), [&](const srsgpu_rxq::Region &r) { return r.h == host; });
+  if (it == q->regions.end()) return -1;
+  if (it->owned != owned) {
+    fprintf(stderr, owned ? "srsgpu rxq: free_host of a registered region (use srsgpu_rxq_unregister)\n"
+                          : "srsgpu rxq: unregister of a queue-owned block (use srsgpu_rxq_free_host)\n");
+    return -2;
+  }
+  q->regions.erase(it);
   return 0;
 }
 
 int srsgpu_rxq_unregister(srsgpu_rxq_t *q, void *host) {
   if (!q || !host) return -1;
-  {
-    std::unique_lock<std::mutex> l(q->m);
-    // nothing queued or in flight may still point into it
-    q->cv_done.wait(l, [&] { return q->done_upto + 1 >= q->next_ticket; });
-    auto it = std::find_if(q->regions.begin(), q->regions.end(), [&](const srsgpu_rxq::Region &r) { return r.h == host; });
-    if (it == q->regions.end()) return -1;
-    q->regions.erase(it);
-  }
+  // every batch that read or wrote the region has completed (its done event synchronised), and the
+  // copy stream's spans from it with them: no device view of it outlives this call
+  if (rxq_drop_region(q, host, false)) return -1;
   return hipHostUnregister(host) == hipSuccess ? 0 : -1;
+}
+
+void *srsgpu_rxq_alloc_host(srsgpu_rxq_t *q, size_t bytes) {
+  if (!q || !bytes) return nullptr;
+  void *h = nullptr, *d = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped) != hipSuccess || !h) {
+    fprintf(stderr, "srsgpu rxq: hipHostMalloc of %zu bytes failed\n", bytes);
+    return nullptr;
+  }
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> l(q->m);
+  q->regions.push_back({(const char *)h, bytes, (const char *)d, true});
+  return h;
+}
+
+int srsgpu_rxq_free_host(srsgpu_rxq_t *q, void *host) {
+  if (!q || !host) return -1;
+  if (rxq_drop_region(q, host, true)) return -1;
+  return hipHostFree(host) == hipSuccess ? 0 : -1;
 }
 
 int srsgpu_rxq_set_input_format(srsgpu_rxq_t *q, uint32_t format, float scale) {
@@ -1315,11 +1362,37 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
   return err ? -1 : 0;
 }
 
+// pin a std::thread to one CPU (no-op for cpu < 0); 0 or the pthread error
+static int pin_thread(std::thread &t, int cpu) {
+  if (cpu < 0) return 0;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpu, &set);
+  return pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);
+}
+
+int srsgpu_rxq_set_affinity(srsgpu_rxq_t *q, const int32_t *cpus, uint32_t n) {
+  if (!q || (!cpus && n)) return -1;
+  std::thread *th[3] = {&q->closer, &q->worker, &q->completer};
+  int r = 0;
+  for (int k = 0; k < 3; k++)
+    if (n && pin_thread(*th[k], cpus[k % n])) r = -1;
+  return r;
+}
+
 int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
                            uint32_t ticks, uint32_t period_us, uint32_t workers, float *latency_ms, int32_t *status,
                            uint32_t *acked, double *late_ms) {
+  return srsgpu_rxq_drive_paced_ex(q, items, streams, depth, ticks, period_us, workers, nullptr, 0, latency_ms,
+                                   nullptr, status, acked, late_ms);
+}
+
+int srsgpu_rxq_drive_paced_ex(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
+                              uint32_t ticks, uint32_t period_us, uint32_t workers, const int32_t *cpus,
+                              uint32_t ncpus, float *latency_ms, float *submit_latency_ms, int32_t *status,
+                              uint32_t *acked, double *late_ms) {
   if (!q || !items || !streams || !depth || !ticks || !period_us || !workers || workers > 256 || !latency_ms ||
-      !status)
+      !status || (!cpus && ncpus))
     return -1;
   using clk = std::chrono::steady_clock;
   const uint64_t n = (uint64_t)streams * ticks;
@@ -1328,6 +1401,7 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
   std::condition_variable cv_col, cv_prod;
   std::vector<uint64_t> tickets(n, 0);
   std::vector<uint8_t> state(n, 0); // 1 submitted, 2 refused / skipped
+  std::vector<clk::time_point> t_sub(n);
   uint64_t ndone = 0;
   uint32_t producing = std::min(workers, streams), nack = 0;
   int err = 0;
@@ -1352,9 +1426,11 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
           skip = err != 0;
         }
         if (!skip) {
-          const double late = std::chrono::duration<double, std::milli>(clk::now() - tick_time(t)).count();
+          const clk::time_point ts = clk::now();
+          const double late = std::chrono::duration<double, std::milli>(ts - tick_time(t)).count();
           r = srsgpu_rxq_submit(q, items[(t % depth) * streams + st], &tk);
           std::lock_guard<std::mutex> l(m);
+          t_sub[i] = ts;
           if (late > worst_late) worst_late = late;
         }
         {
@@ -1372,16 +1448,20 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
     for (uint64_t i = 0; i < n; i++) {
       uint8_t s;
       uint64_t tk;
+      clk::time_point ts;
       {
         std::unique_lock<std::mutex> l(m);
         cv_col.wait(l, [&] { return state[i] != 0; });
         s = state[i];
         tk = tickets[i];
+        ts = t_sub[i];
       }
       const int r = s == 1 ? srsgpu_rxq_wait(q, tk) : -1;
       const clk::time_point done = clk::now();
       status[i] = r;
       latency_ms[i] = (float)std::chrono::duration<double, std::milli>(done - tick_time(i / streams)).count();
+      if (submit_latency_ms)
+        submit_latency_ms[i] = s == 1 ? (float)std::chrono::duration<double, std::milli>(done - ts).count() : -1.f;
       const srsgpu_rxq_item_t *it = items[((i / streams) % depth) * streams + i % streams];
       {
         std::lock_guard<std::mutex> l(m);
@@ -1391,8 +1471,13 @@ int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uin
       cv_prod.notify_all();
     }
   });
+  // CPUs: the collector on cpus[0], producer w on cpus[(1 + w) % ncpus]
+  if (ncpus) (void)pin_thread(collector, cpus[0]);
   std::vector<std::thread> pool;
-  for (uint32_t w = 0; w < producing; w++) pool.emplace_back(produce, w);
+  for (uint32_t w = 0; w < producing; w++) {
+    pool.emplace_back(produce, w);
+    if (ncpus) (void)pin_thread(pool.back(), cpus[(1 + w) % ncpus]);
+  }
   for (auto &t : pool) t.join();
   srsgpu_rxq_flush(q);
   collector.join();

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "srsgpu/qpp_table.h"
+#include "wave_prio.h"
 #include "srsgpu/tdec_batch.h"
 #include "srslte/phy/fec/turbodecoder.h"
 #include "tdec_kernels.h"
@@ -82,6 +83,9 @@ struct TdecEngine {
   void *SP0 = nullptr, *XP1 = nullptr, *A = nullptr, *T = nullptr, *D = nullptr, *scratch = nullptr;
   uint32_t *Dfz = nullptr; // frozen decision words of the fused early stop (TdEs::dfz)
   uint8_t *cb_end = nullptr; // TdEs::cb_end, zero between jobs
+  // the hybrid schedule's list of pairs still running after the first half-iteration (TdEs::run_list;
+  // run_cnt per group at its pair0, zeroed by k_pair_done). SRSGPU_ES_COMPACT=0: every pair (A/B)
+  uint32_t *run_list = nullptr, *run_cnt = nullptr;
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
   uint32_t *noi = nullptr;
   int16_t *in_stage = nullptr; // host-pointer API staging
@@ -109,6 +113,11 @@ struct TdecEngine {
   // the first half-iteration's k_decide moves to split_st (st is switched for the rest of the call)
   hipStream_t split_st = nullptr;
   hipEvent_t ev_split = nullptr;
+  // defer_bytes (the DL-SCH engine's request): the natural-order bytes of the blocks a fused early-stop
+  // launch ended are left in Dfz / cb_end for the caller's epilogue (k_tb_finish, FzSrc) instead of a
+  // k_es_bytes launch; only for a job decoded in one pass (the group table and Dfz stay as they are).
+  // bytes_deferred tells the caller, after decode_multi, that it did so.
+  bool defer_bytes = false, defer_now = false, bytes_deferred = false;
   int kind_g0[TD_NKIND + 1] = {0};
   int kind_blocks[TD_NKIND] = {0};
   size_t kind_lds[TD_NKIND] = {0};
@@ -159,6 +168,9 @@ struct TdecEngine {
     HIPCHK(hipMalloc(&Dfz, cap_dw * 4));
     HIPCHK(hipMalloc(&cb_end, cap_cbs));
     HIPCHK(hipMemset(cb_end, 0, cap_cbs));
+    HIPCHK(hipMalloc(&run_list, cap_pairs * 4));
+    HIPCHK(hipMalloc(&run_cnt, cap_pairs * 4));
+    HIPCHK(hipMemset(run_cnt, 0, cap_pairs * 4));
     return 0;
   }
 
@@ -167,7 +179,7 @@ struct TdecEngine {
     for (void *p : {SP0, XP1, A, D, T, scratch, (void *)d_groups})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
-                    (void *)out_stage, (void *)Dfz, (void *)cb_end})
+                    (void *)out_stage, (void *)Dfz, (void *)cb_end, (void *)run_list, (void *)run_cnt})
       if (p) (void)hipFree(p);
     if (aux) (void)hipStreamSynchronize(aux);
     for (hipEvent_t e : {ev_fork, ev_join, ev_split})
@@ -461,7 +473,7 @@ struct TdecEngine {
     // several passes seeds each pass's blocks before its decode)
     (void)first;
     (void)total_cbs;
-    HIPCHK(launch_pair_done(d_groups, (int)ng, total_pairs, init_done, cb_done, cb_ok, noi, pair_done, st));
+    HIPCHK(launch_pair_done(d_groups, (int)ng, total_pairs, init_done, cb_done, cb_ok, noi, pair_done, st, run_cnt));
     return 0;
   }
 
@@ -541,10 +553,11 @@ struct TdecEngine {
     return 0;
   }
 
-  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t maxh = 0) {
+  int decide(int n, uint8_t *d_out, size_t out_stride, bool early, uint32_t maxh = 0, bool list = false) {
     ProfScope ps("k_decide", st);
     HIPCHK(launch_decide(n, d_groups, (int)groups.size(), total_pairs, arrays(), d_out, out_stride,
-                         early, cb_done, cb_ok, noi, (int)maxh, pair_done, st));
+                         early, cb_done, cb_ok, noi, (int)maxh, pair_done, st, list ? run_list : nullptr,
+                         list ? run_cnt : nullptr));
     return 0;
   }
 
@@ -611,12 +624,10 @@ struct TdecEngine {
     const int chunk = td_sched().es_chunk;
     bool seq = false, es_any = false;
     const TdArrays a = arrays();
-    // the early-stop launches' wave priority, 0..3 (SRSGPU_ES_PRIO, read per call; default 3): the
-    // few workgroups still running after the heavy pass win their SIMDs' issue arbitration against
-    // other streams' throughput kernels (headline 0.871 -> 0.858 ms per batch, r05_s34 / r05_s35)
-    const char *pe = getenv("SRSGPU_ES_PRIO");
-    TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end,
-            pe && pe[0] ? std::min(std::max(atoi(pe), 0), 3) : 3};
+    // the early-stop launches' wave priority, 0..3 (SRSGPU_ES_PRIO from the knob snapshot, wave_prio.h;
+    // default 3): the few workgroups still running after the heavy pass win their SIMDs' issue
+    // arbitration against other streams' throughput kernels (headline 0.871 -> 0.858 ms, r05_s34 / s35)
+    TdEs es{d_out, out_stride, cb_done, cb_ok, noi, (int)maxh, 0, 0, Dfz, cb_end, knobs().es_prio};
     // es_fused 3 (hybrid): the first half-iteration of every kind as one launch per kind plus one
     // k_decide (the whole batch's heavy pass, with kernel boundaries that let other streams in), then
     // the blocks still running (a few at high SNR) through the remaining half-iterations in ONE
@@ -645,7 +656,10 @@ struct TdecEngine {
           ProfScope ps(names0[k], st);
           HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
         }
-        if (decide(0, d_out, out_stride, true, maxh)) return -1;
+        // windowed kinds: the pairs still running are listed by k_decide and packed by the early-stop
+        // launch (TdEs::run_list); the SSE kind keeps its own mapping
+        const bool compact = knobs().es_compact;
+        if (decide(0, d_out, out_stride, true, maxh, compact)) return -1;
         if (split_st && split_st != st) {
           // the few blocks still running, their bytes and the caller's epilogue on the tail stream:
           // the caller's stream goes on with its next work meanwhile
@@ -659,10 +673,17 @@ struct TdecEngine {
         for (int k = 0; k < TD_NKIND; k++) {
           const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
           if (g1 <= g0) continue;
+          TdEs ek = es;
+          if (compact && k != TD_KIND_SSE) {
+            ek.run_list = run_list;
+            ek.run_cnt = run_cnt;
+          }
           ProfScope ps(k == TD_KIND_SSE ? "k_sse_es" : "k_win_bidir_es", st);
-          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, es, st));
+          HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, ek, st));
         }
-        {
+        if (defer_now) {
+          bytes_deferred = true;
+        } else {
           ProfScope ps("k_es_bytes", st);
           HIPCHK(launch_es_bytes(d_groups, (int)groups.size(), total_pairs, es, st));
         }
@@ -706,7 +727,9 @@ struct TdecEngine {
       HIPCHK(hipEventRecord(ev_join, aux));
       HIPCHK(hipStreamWaitEvent(st, ev_join, 0));
     }
-    if (es_any) {
+    if (es_any && defer_now) {
+      bytes_deferred = true;
+    } else if (es_any) {
       ProfScope ps("k_es_bytes", st);
       HIPCHK(launch_es_bytes(d_groups, (int)groups.size(), total_pairs, es, st));
     }
@@ -763,6 +786,7 @@ struct TdecEngine {
     } swap{*this, cb_ok, noi};
     if (d_ok) cb_ok = d_ok;
     if (d_noi) noi = d_noi;
+    bytes_deferred = false;
     bool first = true;
     for (size_t s0 = 0; s0 < specs.size();) {
       size_t s1 = specs.size();
@@ -774,6 +798,7 @@ struct TdecEngine {
         return -1;
       }
       if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs, true, derm)) return -1;
+      defer_now = defer_bytes && s0 == 0 && s1 == specs.size(); // one pass: Dfz / groups stay for the caller
       if (fixed) { // all maxh half-iterations, then one CRC check (no early stop: measurement mode)
         if (halfits_fixed((int)maxh) || decide((int)maxh - 1, d_out, out_stride, true, maxh)) return -1;
       } else if (decode_planned(maxh, d_out, out_stride)) {

@@ -159,6 +159,8 @@ struct srsgpu_tdec_batch {
 
 extern "C" {
 
+void srsgpu_knobs_reload(void) { srsgpu::knobs_slot().store(srsgpu::knobs_from_env(), std::memory_order_release); }
+
 uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t K) {
   const int sb = sb_layout && sb_input_for(impl, resolve_impl(impl, K));
   return sb ? 3 * (K + 32) + 12 : 3 * K + 12;

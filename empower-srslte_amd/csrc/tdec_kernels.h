@@ -103,6 +103,9 @@ struct TdEs {
   uint32_t *dfz;  // decision words of the blocks that ended (layout of D), for k_es_bytes
   uint8_t *cb_end; // per CB: 0, or 1 + parity of the half-iteration that ended it (kept zero between jobs)
   int prio;        // 0..3: the early-stop waves' issue priority on their SIMD (s_setprio; 0 = default)
+  // windowed kinds after a k_decide that listed the pairs still running (hybrid schedule): per group,
+  // run_cnt[pair0] of them at run_list[pair0 ..] (group-local pair numbers, any order); null: every pair
+  const uint32_t *run_list = nullptr, *run_cnt = nullptr;
 };
 // the natural-order bytes of the blocks the fused launches ended (after the last of them)
 hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st);
@@ -113,13 +116,16 @@ hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, s
                              const TdArrays &a, const TdEs &es, hipStream_t st);
 // hard decision after half-iteration n for every pair of the job (npairs in total); early: also
 // the CRC, cb_done / cb_ok / noi and pair_done (turbodecoder.c:353-360, sch.c:361-391)
+// run_list / run_cnt (early, optional): every pair not done after half-iteration n is appended to its
+// group's list (TdEs::run_list; run_cnt zeroed by launch_pair_done)
 hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,
                          uint8_t *outb, size_t out_stride, bool early, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int max_halfits, uint8_t *pair_done,
-                         hipStream_t st);
+                         hipStream_t st, uint32_t *run_list = nullptr, uint32_t *run_cnt = nullptr);
 // the early-stop flags of the job's code blocks: cb_done = init_done (0 without), cb_ok = noi = 0,
 // pair_done[p] = both code blocks of pair p done
 hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *init_done, uint8_t *cb_done,
-                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st);
+                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st,
+                            uint32_t *run_cnt = nullptr);
 } // namespace srsgpu
 #endif

@@ -1138,11 +1138,10 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_run(const TdG
 // that end at this half-iteration (via Dfz / cb_end and k_es_bytes). Returns (uniformly) whether
 // every block of the workgroup is done.
 template <int NB>
-__device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const uint32_t *__restrict__ Darr,
+__device__ __noinline__ bool es_check(const TdGroup &G, const int *wpair, int n, const uint32_t *__restrict__ Darr,
                                       const TdEs &es, uint32_t *red, int *fin) {
-  constexpr int NP = 64 / NB; // pairs per workgroup
+  constexpr int NP = 64 / NB; // pairs per workgroup (wpair[lp]: their group-local pair numbers)
   const int K = G.K;
-  const int pw = (blk * 64) / NB;
   const int L = K / NB, G16 = (L + 15) / 16, nw = NB * G16;
   const bool dec2 = n & 1;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1158,7 +1157,7 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
   for (int lp = 0; lp < NP; lp++) {
     uint32_t c0 = 0, c1 = 0;
     if (!(skip[lp][0] && skip[lp][1])) {
-      const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
+      const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)wpair[lp] * nw);
       for (int q = t; q < nw; q += 128) {
         const uint32_t w = dw[q];
         if (w == 0u) continue;
@@ -1193,7 +1192,7 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
     const int lp = t >> 1, h = t & 1;
     int done = 1, now = 0;
     if (!skip[lp][h]) {
-      const int cb = G.cb0 + 2 * (pw + lp) + h;
+      const int cb = G.cb0 + 2 * wpair[lp] + h;
       const uint32_t crc = red[t * 2] ^ red[t * 2 + 1];
       es.noi[cb] = (uint32_t)(n + 1);
       if (crc == 0u) {
@@ -1221,10 +1220,10 @@ __device__ __noinline__ bool es_check(const TdGroup &G, int blk, int n, const ui
     all = all && (f0 & 1) && (f1 & 1);
     const uint32_t mask = ((f0 & 2) ? 0xffffu : 0u) | ((f1 & 2) ? 0xffff0000u : 0u);
     if (!mask) continue;
-    const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)(pw + lp) * nw);
-    const gmut_t<uint32_t> fz = gmut<uint32_t>(es.dfz + G.dw0 + (size_t)(pw + lp) * nw);
+    const gptr_t<uint32_t> dw = gptr(Darr + G.dw0 + (size_t)wpair[lp] * nw);
+    const gmut_t<uint32_t> fz = gmut<uint32_t>(es.dfz + G.dw0 + (size_t)wpair[lp] * nw);
     for (int q = t; q < nw; q += 128) fz[q] = (fz[q] & ~mask) | (dw[q] & mask);
-    if (t < 2 && (fin[lp * 2 + t] & 2)) es.cb_end[G.cb0 + 2 * (pw + lp) + t] = (uint8_t)(1 + (n & 1));
+    if (t < 2 && (fin[lp * 2 + t] & 2)) es.cb_end[G.cb0 + 2 * wpair[lp] + t] = (uint8_t)(1 + (n & 1));
   }
   return all;
 }
@@ -1243,31 +1242,53 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
                                                       s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                       const s2 *__restrict__ T, size_t plane, TdEs es) {
   extern __shared__ s4 cks[];
-  __shared__ uint32_t red[(64 / NB) * 2 * 2];
-  __shared__ int fin[(64 / NB) * 2];
+  constexpr int NP = 64 / NB; // pairs per workgroup
+  __shared__ uint32_t red[NP * 2 * 2];
+  __shared__ int fin[NP * 2];
+  __shared__ int wpair[NP];
   wave_prio(es.prio);
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
   const int K_ = G.K, npairs = G.npairs;
   const int blk = blockIdx.x - G.blk_half;
+  // The workgroup's pairs: NP consecutive ones, or with es.run_list (the hybrid schedule, after the
+  // first half-iteration's k_decide) entries NP blk .. of the group's list of pairs still running
+  // (run_cnt[pair0] of them): the few stragglers are packed into few workgroups, and the rest of the
+  // launch's workgroups leave at once instead of holding a CU's SIMDs each for one running block.
+  // A list slot past the count repeats the workgroup's first pair, marked done (never checked).
+  const int nrun = es.run_list ? (int)es.run_cnt[G.pair0] : 0;
+  if (es.run_list && NP * blk >= nrun) return;
+  if (threadIdx.x < NP) {
+    const int lp = threadIdx.x;
+    int p;
+    if (es.run_list) {
+      const int j = NP * blk + lp;
+      p = (int)es.run_list[G.pair0 + (j < nrun ? j : NP * blk)];
+      if (j >= nrun) p = -1 - p;
+    } else {
+      p = NP * blk + lp;
+      if (p >= npairs) p = -1 - (npairs - 1);
+    }
+    wpair[lp] = p;
+  }
+  __syncthreads();
   // fin[2 lp + h]: bit 0 = CB h of the workgroup's pair lp is done (seeded from cb_done: HARQ
   // blocks that passed earlier; absent blocks count as done), bit 1 = it ended at this check
-  if (threadIdx.x < 2 * (64 / NB)) {
-    const int p = (blk * 64) / NB + (threadIdx.x >> 1), h = threadIdx.x & 1;
-    fin[threadIdx.x] = (p >= npairs || 2 * p + h >= G.ncb || es.cb_done[G.cb0 + 2 * p + h]) ? 1 : 0;
+  if (threadIdx.x < 2 * NP) {
+    const int p = wpair[threadIdx.x >> 1], h = threadIdx.x & 1;
+    fin[threadIdx.x] = (p < 0 || 2 * p + h >= G.ncb || es.cb_done[G.cb0 + 2 * p + h]) ? 1 : 0;
   }
   __syncthreads();
   {
     bool all_done = true;
-    for (int i = 0; i < 2 * (64 / NB); i++) all_done = all_done && (fin[i] & 1);
+    for (int i = 0; i < 2 * NP; i++) all_done = all_done && (fin[i] & 1);
     if (all_done) return;
   }
+  if (threadIdx.x < NP && wpair[threadIdx.x] < 0) wpair[threadIdx.x] = -1 - wpair[threadIdx.x]; // a real pair
+  __syncthreads();
   const int lane_ = threadIdx.x & 63;
-  const int gl = blk * 64 + lane_;
-  const int nlanes = npairs * NB;
-  const int g = gl < nlanes ? gl : nlanes - 1;
-  const int pair = g / NB;
-  const int d_ = g % NB;
+  const int pair = wpair[lane_ / NB]; // lanes of a repeated slot redo that pair: same values, same addresses
+  const int d_ = lane_ % NB;
   const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K_, NB);
   const s4 *sp0_ = SP0 + base;
   s2 *xp1_ = XP1 + base;
@@ -1275,7 +1296,8 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
   s2 *A_ = Aarr + base;
   uint32_t *D_ = Darr + G.dw0 + (size_t)pair * dec_words(K_, NB);
   const s2 *tl_ = T + (size_t)(G.pair0 + pair) * 12;
-  const int pe = t4_pair_elems(K_, NB), pw = (blk * 64) / NB;
+  // wave bases at the group's first pair, each lane's pair by its offset (any pair of the group)
+  const int pe = t4_pair_elems(K_, NB), pw = 0;
   const size_t wb = (size_t)G.elem0 + (size_t)pw * pe;
   const s4 *wsp0_ = SP0 + wb;
   s2 *wx2_ = XP1 + wb, *wa_ = Aarr + wb;
@@ -1315,7 +1337,7 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
     else
       win_bidir_body<NB, DIV, 0, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
     __syncthreads(); // the half-iteration's decision words of both waves are written
-    if (es_check<NB>(G, blk, n, Darr, es, red, fin)) break;
+    if (es_check<NB>(G, wpair, n, Darr, es, red, fin)) break;
   }
 }
 
@@ -2249,7 +2271,8 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
                                                 uint8_t *__restrict__ outb, size_t out_stride,
                                                 int early, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
-                                                int max_halfits, uint8_t *__restrict__ pair_done, int prio) {
+                                                int max_halfits, uint8_t *__restrict__ pair_done, int prio,
+                                                uint32_t *__restrict__ run_list, uint32_t *__restrict__ run_cnt) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ uint32_t red[2][4];
   __shared__ int fin[4]; // [0..1] CB done, [2..3] CB finished at this half-iteration
@@ -2324,6 +2347,8 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
     }
     __syncthreads();
     if (threadIdx.x == 0 && pair_done) pair_done[blockIdx.x] = (uint8_t)(fin[0] && fin[1]);
+    if (threadIdx.x == 0 && run_list && !(fin[0] && fin[1])) // still running: into the group's list
+      run_list[G.pair0 + atomicAdd(&run_cnt[G.pair0], 1u)] = (uint32_t)pair;
     // the bytes of a block matter once, at the half-iteration that ends it (sch.c:361-391: the
     // data of the last iteration run stays)
     out[0] = fin[2] != 0;
@@ -2457,9 +2482,10 @@ __global__ __launch_bounds__(256) void k_es_bytes(const TdGroup *__restrict__ gr
 __global__ void k_pair_done(const TdGroup *__restrict__ groups, int ngroups, int npairs_total,
                             const uint8_t *__restrict__ init_done, uint8_t *__restrict__ cb_done,
                             uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
-                            uint8_t *__restrict__ pair_done) {
+                            uint8_t *__restrict__ pair_done, uint32_t *__restrict__ run_cnt) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npairs_total) return;
+  if (run_cnt) run_cnt[p] = 0; // the groups' running-pair counts (at their pair0)
   const TdGroup &G = groups[grp_find<GF_PAIR>(groups, ngroups, p)];
   const int lp = p - G.pair0;
   const int c0 = G.cb0 + 2 * lp, c1 = 2 * lp + 1 < G.ncb ? c0 + 1 : c0;
@@ -2563,7 +2589,7 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
     hipLaunchKernelGGL((k_win_bidir<nb, div, m, TD_BIDIR_CW, dout, b8>), dim3(nblocks), dim3(128), \
                        lds, st, dg, ng, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A,               \
                        (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done,                      \
-                       env_prio("SRSGPU_H0_PRIO", 0));                                              \
+                       knobs().h0_prio);                                              \
   } while (0)
 #define BIDIR(nb, div, b8)                                                                         \
   do {                                                                                             \
@@ -2714,10 +2740,11 @@ hipError_t launch_halfits_es(int kind, const TdGroup *dg, int ng, int nblocks, s
 }
 
 hipError_t launch_pair_done(const TdGroup *dg, int ng, int npairs, const uint8_t *init_done, uint8_t *cb_done,
-                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st) {
+                            uint8_t *cb_ok, uint32_t *noi, uint8_t *pair_done, hipStream_t st,
+                            uint32_t *run_cnt) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pair_done, dim3(nblk(npairs, 256)), dim3(256), 0, st, dg, ng, npairs, init_done,
-                     cb_done, cb_ok, noi, pair_done);
+                     cb_done, cb_ok, noi, pair_done, run_cnt);
   return hipGetLastError();
 }
 
@@ -2725,18 +2752,19 @@ hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_es_bytes, dim3(nblk(npairs, ESB_PAIRS)), dim3(256), 0, st, dg, ng, npairs,
                      (const uint32_t *)es.dfz, es.outb, es.out_stride, es.cb_end,
-                     env_prio("SRSGPU_TAIL_PRIO", 3));
+                     knobs().tail_prio);
   return hipGetLastError();
 }
 
 hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdArrays &a,
                          uint8_t *outb, size_t out_stride, bool early, uint8_t *cb_done,
                          uint8_t *cb_ok, uint32_t *noi, int max_halfits, uint8_t *pair_done,
-                         hipStream_t st) {
+                         hipStream_t st, uint32_t *run_list, uint32_t *run_cnt) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, dg, ng, (const uint32_t *)a.D, outb,
                      out_stride, early ? 1 : 0, cb_done, cb_ok, noi, max_halfits,
-                     early ? pair_done : nullptr, env_prio("SRSGPU_DECIDE_PRIO", env_prio("SRSGPU_TAIL_PRIO", 3)));
+                     early ? pair_done : nullptr, knobs().decide_prio, early ? run_list : nullptr,
+                     early ? run_cnt : nullptr);
   return hipGetLastError();
 }
 #endif // TD_PART == 0

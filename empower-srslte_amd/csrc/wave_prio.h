@@ -1,8 +1,13 @@
 // Wave issue priority for latency-critical launches that run beside other streams' throughput
 // kernels: s_setprio raises the wave's priority in its SIMD's instruction arbitration (0 = default).
+// Plus the process-wide tuning knobs those launches read: a snapshot of the environment taken once
+// (first use) and replaced only by srsgpu_knobs_reload(), so no launch calls getenv (a getenv on a
+// queue's dispatcher thread racing a setenv elsewhere is undefined behaviour in glibc).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+
+#include <atomic>
 
 namespace srsgpu {
 __device__ __forceinline__ void wave_prio(int prio) {
@@ -13,11 +18,51 @@ __device__ __forceinline__ void wave_prio(int prio) {
   default: break;
   }
 }
-// the priority of a launch class from the environment (read per call, clamped to 0..3)
+
+struct Knobs {
+  int es_prio;     // SRSGPU_ES_PRIO (0..3, default 3): the early-stop decoder launches
+  int tail_prio;   // SRSGPU_TAIL_PRIO (default 3): k_es_bytes, k_tb_finish
+  int decide_prio; // SRSGPU_DECIDE_PRIO (default: tail_prio): k_decide
+  int h0_prio;     // SRSGPU_H0_PRIO (default 0): the first half-iteration
+  bool llr_generic; // SRSGPU_LLR_GENERIC (A/B): the general PDSCH LLR kernel only
+  bool llr_noxcd;   // SRSGPU_LLR_NOXCD (A/B): the plain item-major workgroup mapping
+  bool es_compact;  // SRSGPU_ES_COMPACT (default 1): the hybrid early-stop launch packs the running pairs
+};
+
 inline int env_prio(const char *name, int dflt) {
   const char *e = getenv(name);
   if (!e || !e[0]) return dflt;
   const int v = atoi(e);
   return v < 0 ? 0 : (v > 3 ? 3 : v);
+}
+
+inline const Knobs *knobs_from_env() {
+  Knobs *k = new Knobs;
+  k->es_prio = env_prio("SRSGPU_ES_PRIO", 3);
+  k->tail_prio = env_prio("SRSGPU_TAIL_PRIO", 3);
+  k->decide_prio = env_prio("SRSGPU_DECIDE_PRIO", k->tail_prio);
+  k->h0_prio = env_prio("SRSGPU_H0_PRIO", 0);
+  k->llr_generic = getenv("SRSGPU_LLR_GENERIC") != nullptr;
+  k->llr_noxcd = getenv("SRSGPU_LLR_NOXCD") != nullptr;
+  {
+    const char *e = getenv("SRSGPU_ES_COMPACT");
+    k->es_compact = !(e && e[0] == '0');
+  }
+  return k;
+}
+
+inline std::atomic<const Knobs *> &knobs_slot() {
+  static std::atomic<const Knobs *> p{nullptr};
+  return p;
+}
+
+// the current snapshot (a replaced one is never freed: a launch on another thread may still read it)
+inline const Knobs &knobs() {
+  const Knobs *k = knobs_slot().load(std::memory_order_acquire);
+  if (k) return *k;
+  const Knobs *n = knobs_from_env();
+  if (knobs_slot().compare_exchange_strong(k, n, std::memory_order_acq_rel)) return *n;
+  delete n;
+  return *k;
 }
 } // namespace srsgpu

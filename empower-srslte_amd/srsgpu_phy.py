@@ -388,12 +388,21 @@ _sig = {
     "srsgpu_dlsch_softbuffer_reset_list": (_i32, [_vp, _u32p, _u32p, _u32]),
     "srsgpu_tdec_set_schedule": (ctypes.c_int, [ctypes.c_int] * 4),
     "srsgpu_tdec_get_schedule": (None, [ctypes.POINTER(ctypes.c_int)] * 4),
+    "srsgpu_knobs_reload": (None, []),
     "srsgpu_rxq_drive": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint32, _vp, _vp, _vp]),
     "srsgpu_rxq_drive_paced": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)] + [ctypes.c_uint32] * 5 +
                                [_vp, _vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double)]),
     "srsgpu_rxq_register": (_i32, [_vp, _vp, ctypes.c_size_t]),
     "srsgpu_rxq_unregister": (_i32, [_vp, _vp]),
+    "srsgpu_rxq_alloc_host": (_vp, [_vp, ctypes.c_size_t]),
+    "srsgpu_rxq_drive_paced_ex": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)] + [ctypes.c_uint32] * 5 +
+                                  [_vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_uint32),
+                                   ctypes.POINTER(ctypes.c_double)]),
+    "srsgpu_rxq_set_affinity": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32]),
+    "srsgpu_rxq_free_host": (_i32, [_vp, _vp]),
+    "srsgpu_dlsch_join_tail": (_i32, [_vp]),
+    "srsgpu_dlsch_cb_halfits": (_i32, [_vp, _vp, _u32]),
     "srsgpu_rxq_set_input_format": (_i32, [_vp, _u32, ctypes.c_float]),
     "srsgpu_rxq_ingest_stats": (None, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "srsgpu_rxq_get_chest": (_vp, [_vp]),
@@ -698,6 +707,14 @@ class Dlsch:
         if _lib.srsgpu_dlsch_softbuffer_read(self.q, slot, None, _u8(crc)) != 0:
             raise RuntimeError("softbuffer read failed")
         return crc
+
+    def cb_halfits(self, max_cbs=1 << 16):
+        """srsgpu_dlsch_cb_halfits: the half-iterations of every code block of the last decode call"""
+        out = np.zeros(max_cbs, np.uint32)
+        n = _lib.srsgpu_dlsch_cb_halfits(self.q, out.ctypes.data, max_cbs)
+        if n < 0:
+            raise RuntimeError("srsgpu_dlsch_cb_halfits failed")
+        return out[:min(n, max_cbs)]
 
     def read_softbuffer(self, slot):
         rows = np.zeros((self.max_cb, SOFTBUFFER_SIZE), np.int16)
@@ -1174,6 +1191,12 @@ def set_schedule(fused=-1, es_fused=-1, es_chunk=-1, sse_bidir=-1):
         raise ValueError("invalid decoder schedule")
 
 
+def knobs_reload():
+    """srsgpu_knobs_reload: re-read the launch knobs (SRSGPU_*_PRIO, SRSGPU_LLR_*) after os.environ
+    changed them; the library reads them once otherwise"""
+    _lib.srsgpu_knobs_reload()
+
+
 def get_schedule():
     v = [ctypes.c_int(0) for _ in range(4)]
     _lib.srsgpu_tdec_get_schedule(*[ctypes.byref(x) for x in v])
@@ -1300,6 +1323,31 @@ class RxQueue:
             raise RuntimeError("srsgpu_rxq_drive_paced: a submission was refused")
         return lat, status, acked.value, late.value
 
+    def drive_paced_ex(self, items, streams, depth, ticks, period_us=1000, workers=8, cpus=()):
+        """srsgpu_rxq_drive_paced_ex: drive_paced with the collector / producers pinned to `cpus` and the
+        latency from the actual submission beside the latency from the tick; returns (latency_ms,
+        submit_latency_ms, status, acked, late_ms)"""
+        import numpy as np
+        assert len(items) == streams * depth
+        ptrs = (ctypes.c_void_p * len(items))(*[ctypes.addressof(it) for it in items])
+        lat = np.zeros(streams * ticks, np.float32)
+        slat = np.zeros(streams * ticks, np.float32)
+        status = np.zeros(streams * ticks, np.int32)
+        acked, late = ctypes.c_uint32(0), ctypes.c_double(0)
+        cp = np.asarray(list(cpus), np.int32)
+        if _lib.srsgpu_rxq_drive_paced_ex(self.q, ptrs, streams, depth, ticks, period_us, workers,
+                                          cp.ctypes.data if cp.size else None, int(cp.size), lat.ctypes.data,
+                                          slat.ctypes.data, status.ctypes.data, ctypes.byref(acked),
+                                          ctypes.byref(late)) != 0:
+            raise RuntimeError("srsgpu_rxq_drive_paced_ex: a submission was refused")
+        return lat, slat, status, acked.value, late.value
+
+    def set_affinity(self, cpus):
+        """srsgpu_rxq_set_affinity: the queue's closer / dispatcher / completer threads onto `cpus`"""
+        cp = np.asarray(list(cpus), np.int32)
+        if _lib.srsgpu_rxq_set_affinity(self.q, cp.ctypes.data if cp.size else None, int(cp.size)) != 0:
+            raise RuntimeError("srsgpu_rxq_set_affinity failed")
+
     def register(self, arr):
         """srsgpu_rxq_register: the GPU reads submissions whose samples lie in arr in place"""
         if _lib.srsgpu_rxq_register(self.q, arr.ctypes.data, arr.nbytes) != 0:
@@ -1310,6 +1358,26 @@ class RxQueue:
         if _lib.srsgpu_rxq_unregister(self.q, arr.ctypes.data) != 0:
             raise RuntimeError("srsgpu_rxq_unregister failed")
         self._registered = [a for a in self._registered if a is not arr]
+
+    def alloc_host(self, shape, dtype):
+        """srsgpu_rxq_alloc_host: a numpy array over queue-owned device-visible host memory (a zero-copy
+        region of this queue, like a registered one). The array is invalid after free_host(arr) or
+        close(): drop every reference to it (and its views) before either."""
+        dt = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dt.itemsize
+        p = _lib.srsgpu_rxq_alloc_host(self.q, max(nbytes, 1))
+        if not p:
+            raise RuntimeError("srsgpu_rxq_alloc_host failed")
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(p))[:nbytes].view(dt).reshape(shape)
+        self._owned = getattr(self, "_owned", {})
+        self._owned[p] = nbytes
+        return arr
+
+    def free_host(self, arr):
+        p = arr.ctypes.data
+        if _lib.srsgpu_rxq_free_host(self.q, p) != 0:
+            raise RuntimeError("srsgpu_rxq_free_host failed")
+        self._owned.pop(p, None)
 
     SC16, CF32 = 1, 0
 

@@ -120,8 +120,20 @@ void srsgpu_dlsch_set_early_stop(srsgpu_dlsch_t *q, int enable);
  * their bytes, the TB CRC and the epilogue of sch.c:393-491) goes to `hip_stream`, and the call's
  * results (TB bytes, d_ret, d_noi, softbuffers) are final when that stream reaches them. The engine's
  * own stream is free for the caller's next work meanwhile (e.g. the next batch's front end into
- * another engine); the next call into this engine makes its stream wait for the tail first. */
+ * another engine); the next call into this engine makes its stream wait for the tail first.
+ * The tail also READS the call's inputs: the e-bits LLRs (the rows of failed TBs are written from
+ * them after the decode) stay unchanged until the tail stream has reached the end of the call. A
+ * caller that rewrites its LLR buffer on the engine's stream before calling the engine again joins
+ * the tail first (srsgpu_dlsch_join_tail). srsgpu_pdsch_* do so at every entry point that enqueues
+ * work, so an engine taken from srsgpu_pdsch_get_dlsch() is safe with the PDSCH's own LLR buffer. */
 int srsgpu_dlsch_set_tail_stream(srsgpu_dlsch_t *q, void *hip_stream);
+/* Make the engine's stream wait for a pending tail (a no-op without one). 0, or -1 on a HIP error. */
+int srsgpu_dlsch_join_tail(srsgpu_dlsch_t *q);
+/* Half-iterations each code block of the last decode call ran (sch.c:361-391's cb_noi; every block
+ * when early stop is off: max_halfits), in the decoder's block order: waits for the call, copies
+ * min(n, blocks) values and returns the call's block count, or -1. A measurement aid (bench.py's
+ * decoder work per batch). */
+int srsgpu_dlsch_cb_halfits(srsgpu_dlsch_t *q, uint32_t *out, uint32_t n);
 /* Direct de-rate-matching (default on). Code blocks of the window decoders (K > 400 under AUTO)
  * are de-rate-matched and HARQ-combined straight into the decoder's inputs, and their softbuffer
  * rows are written after the decode only when their TB failed (every block not decoded before

@@ -140,6 +140,15 @@ int srsgpu_rxq_set_phich(srsgpu_rxq_t *q, uint32_t phich_length, uint32_t phich_
  * unregistered; unregister waits until nothing queued points into it. */
 int srsgpu_rxq_register(srsgpu_rxq_t *q, void *host, size_t bytes);
 int srsgpu_rxq_unregister(srsgpu_rxq_t *q, void *host);
+/* Queue-owned device-visible host memory (hipHostMalloc, mapped): the recommended home of the
+ * caller's sample rings and TB output buffers. A block from here is a zero-copy region of this queue
+ * exactly as a registered one (td buffers DMA'd from it, TB bytes written into it by the decoder),
+ * but its memory is never the caller's own: the caller never frees pinned pages itself, so no later
+ * allocation of the caller's can land on pages the runtime still tracks as pinned. Returns the block
+ * (16-byte aligned) or NULL. srsgpu_rxq_free_host waits until nothing queued points into it, then
+ * frees it; blocks not freed are freed by srsgpu_rxq_destroy. */
+void *srsgpu_rxq_alloc_host(srsgpu_rxq_t *q, size_t bytes);
+int srsgpu_rxq_free_host(srsgpu_rxq_t *q, void *host);
 /* Sample format of every td buffer: complex float (default; srslte_ofdm_rx_sf's input) or the radio's
  * int16 I/Q pairs (4 bytes per sample, half the PCIe bytes), converted on the GPU as value * scale
  * (0: 1 / 32768, UHD's sc16 -> fc32). Waits until nothing is queued. */
@@ -183,6 +192,17 @@ int srsgpu_rxq_drive(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t 
 int srsgpu_rxq_drive_paced(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
                            uint32_t ticks, uint32_t period_us, uint32_t workers, float *latency_ms, int32_t *status,
                            uint32_t *acked, double *late_ms);
+/* srsgpu_rxq_drive_paced with thread placement and a second latency: cpus[0..ncpus) (NULL / 0:
+ * unpinned) take the collector (cpus[0]) and producer w (cpus[(1 + w) % ncpus]);
+ * submit_latency_ms[i] (optional) = results written - the moment submission i actually went out,
+ * i.e. the queue's own latency without the producer's lateness behind its tick (-1: not submitted). */
+int srsgpu_rxq_drive_paced_ex(srsgpu_rxq_t *q, srsgpu_rxq_item_t *const *items, uint32_t streams, uint32_t depth,
+                              uint32_t ticks, uint32_t period_us, uint32_t workers, const int32_t *cpus,
+                              uint32_t ncpus, float *latency_ms, float *submit_latency_ms, int32_t *status,
+                              uint32_t *acked, double *late_ms);
+/* Pin the queue's own threads (closer, dispatcher, completer) to cpus[0], cpus[1 % n], cpus[2 % n]
+ * (e.g. cores apart from the PHY workers that submit). 0, or -1 if a pin failed. */
+int srsgpu_rxq_set_affinity(srsgpu_rxq_t *q, const int32_t *cpus, uint32_t n);
 
 #ifdef __cplusplus
 }

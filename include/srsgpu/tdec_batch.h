@@ -100,6 +100,11 @@ uint32_t srsgpu_tdec_input_len(int impl, int sb_layout, uint32_t long_cb);
  * Change it only while no decode is being issued. Returns 0, or -1 for es_chunk == 0 or es_fused > 3. */
 int srsgpu_tdec_set_schedule(int fused, int es_fused, int es_chunk, int sse_bidir);
 void srsgpu_tdec_get_schedule(int *fused, int *es_fused, int *es_chunk, int *sse_bidir);
+/* Re-read the launch tuning knobs from the environment (SRSGPU_ES_PRIO, SRSGPU_TAIL_PRIO,
+ * SRSGPU_DECIDE_PRIO, SRSGPU_H0_PRIO, SRSGPU_LLR_GENERIC, SRSGPU_LLR_NOXCD). They are read once, at
+ * the first launch that needs them, and kept; a process that changes one of them afterwards calls
+ * this (no launch reads the environment itself). */
+void srsgpu_knobs_reload(void);
 
 /* Live kernel timing with HIP events on the batch stream (for bench.py's roofline). */
 void srsgpu_prof_enable(int on);
