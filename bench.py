@@ -94,6 +94,34 @@ def physical_cpus():
     return out
 
 
+def ref8_sample(d_in8, d_out, expect, stride, nsample=64):
+    """The reference's own 8-bit decoder (srslte_tdec_iteration_8bit, AUTO -> AVX8, oracle/_ref) on
+    `nsample` of the 8-bit leg's code blocks (the same int8 LLRs): its bit errors against the
+    transmitted bits beside the GPU's on the same blocks, and whether every decision is equal"""
+    ref = os.path.join(REPO, "oracle", "_ref", "libsrsref.so")
+    if not os.path.exists(ref):
+        return None
+    lib = ctypes.CDLL(ref)
+    fn = lib.ref_tdec8_run
+    i8p, u8p = ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_uint8)
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, i8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, u8p]
+    ins = d_in8.cpu().numpy().reshape(-1, stride)
+    outs = d_out.cpu().numpy()
+    idx = np.linspace(0, ins.shape[0] - 1, nsample).astype(int)
+    e_ref = e_gpu = same = 0
+    for i in idx:
+        x = np.ascontiguousarray(ins[i, :3 * K + 12].astype(np.int8))
+        dec = np.zeros((NHALF, K // 8), np.uint8)
+        if fn(0, 0, x.ctypes.data_as(i8p), x.size, K, NHALF, dec.ctypes.data_as(u8p)) != 0:
+            return None
+        e_ref += int(np.unpackbits(dec[-1] ^ expect[i]).sum())
+        e_gpu += int(np.unpackbits(outs[i] ^ expect[i]).sum())
+        same += int((dec[-1] == outs[i]).all())
+    return {"code_blocks": int(idx.size), "reference_bit_errors": e_ref, "gpu_bit_errors": e_gpu,
+            "identical_decisions": "%d/%d" % (same, idx.size),
+            "reference": "oracle/_ref srslte_tdec_iteration_8bit (AUTO -> AVX8), same int8 LLRs"}
+
+
 def cpu_baseline(llr, nthreads=None):
     """Reference AVX2 AUTO decoder (oracle/_ref, compiled from the reference's own sources) on
     the host cores: one srslte_tdec_t per thread, each thread pinned to its own physical core
@@ -225,13 +253,15 @@ KERNELS = ("k_ofdm_rx", "k_chest", "k_gold", "k_pdsch_llr", "k_derm", "k_load", 
 _LANE_STREAMS = {}
 
 
-def lane_stream(torch, dev, li):
+def lane_stream(torch, dev, li, priority=0):
     """lane li's HIP stream, created once and shared by every leg: each leg then runs on the same
     streams (and so the same hardware queues) as the headline. Fresh streams per leg land on other
-    hardware queues of the process (4 on the box), and two lanes on one queue run one after the other."""
-    if li not in _LANE_STREAMS:
-        _LANE_STREAMS[li] = torch.cuda.Stream(dev)
-    return _LANE_STREAMS[li]
+    hardware queues of the process (4 on the box), and two lanes on one queue run one after the other.
+    priority < 0: a high-priority stream (its hardware queue's dispatches go first)."""
+    key = (li, priority)
+    if key not in _LANE_STREAMS:
+        _LANE_STREAMS[key] = torch.cuda.Stream(dev, priority=priority) if priority else torch.cuda.Stream(dev)
+    return _LANE_STREAMS[key]
 
 
 def stage_profile(s, torch, step, steps, kernels=None):
@@ -430,7 +460,8 @@ def cb_sizes(table, tbs):
 
 
 def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None,
-                standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1, tail=0):
+                standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1, tail=0,
+                tail_prio=True):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
@@ -456,7 +487,8 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     time spent inside the step calls (enqueue side; the GPU runs asynchronously).
     tail 1 / 2: each lane alternates between two DL-SCH engines whose early-stop tails run on a tail
     stream (srsgpu_dlsch_set_tail_stream; 1: one tail stream shared by the lanes, 2: one per lane), so
-    a lane's next batch starts while the last one's straggling code blocks finish."""
+    a lane's next batch starts while the last one's straggling code blocks finish; tail_prio: the tail
+    streams are high-priority streams."""
     import srsgpu_shard as sh
     import srsgpu_traffic as tr
     rank = dist.get_rank() if dist else 0
@@ -480,7 +512,10 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
         st = (lane_stream(torch, dev, li) if lanes > 1 else torch.cuda.current_stream(dev)).cuda_stream
         tk = {}
         if tail:
-            tk = dict(engines=2, tail_stream=lane_stream(torch, dev, "tail" if tail == 1 else "tail%d" % li).cuda_stream)
+            # tail_prio: the tail streams at high priority (their straggler workgroups dispatched first)
+            tp = -1 if tail_prio else 0
+            tk = dict(engines=2, tail_stream=lane_stream(torch, dev, "tail" if tail == 1 else "tail%d" % li,
+                                                         priority=tp).cuda_stream)
         ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
                                 keep=mine[li::lanes], standard_rate=standard_rate, early_stop=early_stop,
                                 rotate=rotate, **tk, **kw))  # one plan: the same seed everywhere
@@ -618,18 +653,6 @@ def run_tm3_coded(s, torch, dev, steps, warmup, snr_db=30.0, lanes=2, dist=None)
     gc.enable()
     stages, ktab = stage_profile(s, torch, step, steps, KERNELS)
     chk = [m.check() for m in ms]
-    # decoder work of the last batch: the half-iterations each code block ran (srsgpu_dlsch_cb_halfits)
-    # weighted by its K, for the VALU roofline of the whole decoder (first + early-stop launches)
-    # (one block size only: the decoder's block order groups blocks by K, not by TB)
-    halfit_bits = 0
-    for m in ms:
-        h = m.dlsch.cb_halfits()
-        ks_cb = [k for t in m.tb_list for k in cb_sizes(table, t["tbs"])]
-        assert len(ks_cb) == h.size, (len(ks_cb), h.size)
-        if halfit_bits is None or len(set(ks_cb)) != 1:
-            halfit_bits = None
-            continue
-        halfit_bits += int(h.astype(np.int64).sum()) * ks_cb[0]
     acks, good = sum(c[0] for c in chk), sum(c[1] for c in chk)
     noi = float(np.mean([c[2] for c in chk]))
     cb_bits = sum(m.decoded_bits(table) for m in ms)
@@ -1144,6 +1167,7 @@ ALG_BYTES_PER_SF = {
 HEADLINE_SNR_DB = 20.0
 # descriptor sets the headline cycles through (a new grant every step: no repeat-call cache hits)
 HEADLINE_DESCRIPTOR_SETS = 4
+HEADLINE_TAIL = 0
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
 HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 8}, "per_halfit": {"es_fused": 0},
                "fused_c8": {"es_fused": 1, "es_chunk": 8}, "hybrid": {"es_fused": 3, "es_chunk": 8}}
@@ -1573,6 +1597,8 @@ def main():
     ap.add_argument("--coded-snr", type=float, default=None,
                     help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
     ap.add_argument("--lanes", type=int, default=2, help="HIP streams per rank for the headline leg")
+    ap.add_argument("--tail", type=int, default=HEADLINE_TAIL,
+                    help="headline early-stop tails: 0 on the lane's stream, 1 on one high-priority tail stream")
     ap.add_argument("--ab-headline", action="store_true",
                     help="A/B the decoder's early-stop launch schedules on the headline workload")
     ap.add_argument("--legs", default="c2,fixed8,cached,c3,tm3,tm3c,coded,sweep,n1536,c5,d8,dropin,dci,pcfich,pdcch,rxq",
@@ -1644,7 +1670,7 @@ def main():
     head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
                                    dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0, lanes=args.lanes,
                                    warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None,
-                                   rotate=HEADLINE_DESCRIPTOR_SETS))
+                                   rotate=HEADLINE_DESCRIPTOR_SETS, tail=args.tail))
     cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
     result = None
     if rank == 0:
@@ -1661,6 +1687,7 @@ def main():
                        "nof_prb": C3_PRB, "fft_size": head["symbol_size"], "mcs": 28, "tbs": C3_TBS,
                        "code_blocks_per_subframe": 13, "K": 5824, "snr_db": HEADLINE_SNR_DB,
                        "early_stop_max_halfits": 8, "descriptor_sets": HEADLINE_DESCRIPTOR_SETS,
+                       "tail_stream": args.tail,
                        "subframes_per_s": head["subframes_per_s"],
                        "nof_iterations_mean": head["nof_iterations_mean"], "acked_tbs": head["acked_tbs"],
                        "tbs_bytes_ok": head["tbs_bytes_ok"], "parallelism": "dp%d" % nranks},
@@ -1690,7 +1717,7 @@ def main():
                 os.environ[name] = val
             s.knobs_reload()
             r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
-                            lanes=args.lanes)
+                            lanes=args.lanes, rotate=int(os.environ.get("BENCH_AB_ROTATE", "1")))
             os.environ.pop(name, None)
             s.knobs_reload()
             extra.setdefault("envab", []).append({name: val if on else None, "ms_per_batch": r["ms_per_batch"],
@@ -1698,9 +1725,11 @@ def main():
                                                   "tbs_bytes_ok": r["tbs_bytes_ok"]})
     if "tailab" in legs:
         # the headline workload with the early-stop tails on tail streams (two engines per lane)
-        for t in (0, 1, 2, 0):
+        # (BENCH_AB_ROTATE descriptor sets, BENCH_TAIL_PRIO=0: tail streams at normal priority)
+        for t in (0, 1, 0, 1, 0, 1):
             r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
-                            tail=t, lanes=args.lanes)
+                            tail=t, lanes=args.lanes, rotate=int(os.environ.get("BENCH_AB_ROTATE", "1")),
+                            tail_prio=os.environ.get("BENCH_TAIL_PRIO", "1") == "1")
             extra.setdefault("tailab", []).append({"tail": t, "ms_per_batch": r["ms_per_batch"],
                                                    "decoded_mbps": r["decoded_mbps"], "acked_tbs": r["acked_tbs"],
                                                    "tbs_bytes_ok": r["tbs_bytes_ok"]})
@@ -1778,6 +1807,8 @@ def main():
         dec8 = {"decoder": "AUTO 8-bit (int8 AVX8 window, 32 sub-blocks)",
                 "mbps": round(decoded_mbps(nranks, NCB, K, args.steps, el8), 1),
                 "ms_per_step": round(el8 / args.steps * 1e3, 3), "bit_errors": err8}
+        if rank == 0:
+            dec8["reference_sample"] = ref8_sample(d_in8, d_out, expect, stride)
     dci = pcf = pdc = rxq = dropin = None
     if "dci" in legs and rank == 0:
         dci = dci_blind_decode(s, torch, max(4, args.steps // 4))

@@ -135,7 +135,7 @@ struct ChestEngine {
         t.pad = 0;
       }
     }
-    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
+    HIPCHK(ring.upload(d_items, h_items, sizeof(ChestItem) * n * np, st));
     HIPCHK(ring.mark(st));
     // chest_dl.c:620-621: no smoothing for an empty filter or a 3-tap one with w == 0
     ChestCfg kc;
@@ -178,7 +178,7 @@ struct ChestEngine {
         t.port = p;
       }
     }
-    HIPCHK(hipMemcpyAsync(d_items, h_items, sizeof(ChestItem) * n * np, hipMemcpyHostToDevice, st));
+    HIPCHK(ring.upload(d_items, h_items, sizeof(ChestItem) * n * np, st));
     HIPCHK(ring.mark(st));
     HIPCHK(launch_crs_put(d_items, (int)(n * np), (int)cell.nof_prb, (int)cell.id, cell.cp == 1 ? 6 : 7, d_crs, st));
     return 0;

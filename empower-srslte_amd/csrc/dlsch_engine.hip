@@ -402,7 +402,7 @@ struct DlschEngine {
         h[2 * i] = slots[i0 + i];
         h[2 * i + 1] = ncb ? std::min(ncb[i0 + i], max_cb) : max_cb;
       }
-      HIPCHK(hipMemcpyAsync(d_list, h, sizeof(uint32_t) * 2 * m, hipMemcpyHostToDevice, st));
+      HIPCHK(list_ring.upload(d_list, h, sizeof(uint32_t) * 2 * m, st));
       HIPCHK(list_ring.mark(st));
       HIPCHK(launch_sb_reset_list(fresh, cbcrc, d_list, m, max_cb, st));
     }
@@ -640,7 +640,7 @@ struct DlschEngine {
     }
     memcpy(h_blk + o_tbs, h_tbs, sizeof(TbItem) * ntb);
     // ---- device ----
-    HIPCHK(hipMemcpyAsync(d_blk, h_blk, o_end, hipMemcpyHostToDevice, st));
+    HIPCHK(blk_ring.upload(d_blk, h_blk, o_end, st));
     HIPCHK(blk_ring.mark(st));
     // one decoder job over all (K, CRC) groups: one launch per decoder variant and half-iteration
     std::vector<TdSpec> specs;

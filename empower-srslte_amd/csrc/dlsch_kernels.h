@@ -144,7 +144,10 @@ namespace srsgpu {
 // softbuffer row (skipped when fresh) as k_derm + k_load_sbt would, without writing the row.
 // c.rec is indexed by decoder position (TdGroup::cb0 numbering); one workgroup per pair.
 // max_ne: the largest E among the items (sizes the LDS staging of the LLRs)
+// mode 0: SP0 / P1 / T; 1: SP0 / T (P1 deferred); 2: P1 of the listed pairs only (list / cnt as
+// TdEs::run_list / run_cnt; nblocks as for mode 0)
 hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCall &c,
-                            const TdArrays &a, uint32_t max_ne, hipStream_t st);
+                            const TdArrays &a, uint32_t max_ne, hipStream_t st, int mode = 0,
+                            const uint32_t *list = nullptr, const uint32_t *cnt = nullptr);
 } // namespace srsgpu
 #endif

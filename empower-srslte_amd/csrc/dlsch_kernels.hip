@@ -219,8 +219,14 @@ __global__ __launch_bounds__(256) void k_derm_flags(DermCall dc, int n, uint8_t 
 // traffic per code block: its E LLRs in and the 12 B per info bit of SP0 / P1 out (the separate
 // passes also wrote and re-read the 3(K+32)+12 row entries).
 #define LDR_THREADS 256
+// mode 0: SP0, P1 and T of every pair; 1: SP0 and T only (P1 deferred: the first half-iteration does
+// not read it, and at high SNR few blocks reach the second); 2: P1 only, for the pairs k_decide listed
+// as still running after the first half-iteration (TdEs::run_list / run_cnt per group at pair0:
+// workgroup j of a group takes its list entry j)
 __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
-                                                           DermCall dc, TdArrays arr, uint32_t stage) {
+                                                           DermCall dc, TdArrays arr, uint32_t stage, int mode,
+                                                           const uint32_t *__restrict__ list,
+                                                           const uint32_t *__restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
   uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
   int gi = 0;
@@ -237,8 +243,12 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   }
   const TdGroup &G = groups[gi];
   const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
-  const int pair = blockIdx.x - G.blk_load;
+  int pair = blockIdx.x - G.blk_load;
   if (pair >= npairs) return;
+  if (mode == 2) {
+    if (pair >= (int)cnt[G.pair0]) return;
+    pair = (int)list[G.pair0 + pair];
+  }
   const int L = K / nb, G4 = (L + 3) >> 2, ne = nb * 4 * G4;
   const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
   struct Blk {
@@ -280,7 +290,7 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   const gp_t<const uint32_t> tb = glob(reinterpret_cast<const uint32_t *>(bb.t4));
   // SP0: vector v holds T4 elements 2v, 2v + 1 as (sys a, sys b, p0 a, p0 b) each
 #pragma unroll 4
-  for (int v = threadIdx.x; v < ne / 2; v += LDR_THREADS) {
+  for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
     const uint32_t sa = ta[v], pa = ta[ne / 2 + v], sb = tb[v], pb = tb[ne / 2 + v];
     const int el = 2 * v;
     SP0[v] = u4v{value(ba, l0, 0, el, sa & 0xFFFFu) | (value(bb, l1, 0, el, sb & 0xFFFFu) << 16),
@@ -293,7 +303,7 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   const gp_t<const u2v> qa = glob(reinterpret_cast<const u2v *>(ba.t4 + 2 * ne));
   const gp_t<const u2v> qb = glob(reinterpret_cast<const u2v *>(bb.t4 + 2 * ne));
 #pragma unroll 4
-  for (int v = threadIdx.x; v < ne / 4; v += LDR_THREADS) {
+  for (int v = threadIdx.x; v < (mode == 1 ? 0 : ne / 4); v += LDR_THREADS) {
     const u2v ma = qa[v], mb = qb[v];
     const int el = 4 * v;
     P1[v] = u4v{value(ba, l0, 2, el, ma.x & 0xFFFFu) | (value(bb, l1, 2, el, mb.x & 0xFFFFu) << 16),
@@ -301,7 +311,7 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
                 value(ba, l0, 2, el + 2, ma.y & 0xFFFFu) | (value(bb, l1, 2, el + 2, mb.y & 0xFFFFu) << 16),
                 value(ba, l0, 2, el + 3, ma.y >> 16) | (value(bb, l1, 2, el + 3, mb.y >> 16) << 16)};
   }
-  if (threadIdx.x < 12) { // the tails: row positions 3(K+32) .. +11, table entries 3 ne + t
+  if (threadIdx.x < 12 && mode != 2) { // the tails: row positions 3(K+32) .. +11, table entries 3 ne + t
     const int t = threadIdx.x;
     auto tail = [&](const Blk &b, const uint16_t *lds) -> uint32_t {
       const uint32_t m = glob(b.t4)[3 * ne + t];
@@ -814,7 +824,8 @@ hipError_t launch_derm_flags(const DermCall &c, int nitems, uint8_t *init_done, 
 }
 
 hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCall &c,
-                            const TdArrays &a, uint32_t max_ne, hipStream_t st) {
+                            const TdArrays &a, uint32_t max_ne, hipStream_t st, int mode,
+                            const uint32_t *list, const uint32_t *cnt) {
   if (ng <= 0 || nblocks <= 0) return hipSuccess;
   // LLRs staged per block: the largest E of the call, rounded to 8, at most 8192 (16 KB); blocks
   // with more (or with repetition, E > 3K+12) gather theirs from HBM
@@ -824,12 +835,13 @@ hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCa
     const char *e = getenv("SRSGPU_LDERM");
     return e && e[0] == 't';
   }();
-  if (tile) {
+  if (tile && mode == 0) {
     hipLaunchKernelGGL(k_load_derm_tile, dim3((unsigned)nblocks), dim3(LDT_THREADS), lds + 6 * LDT_TILE * 2, st, dg,
                        ng, c, a, stage);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, c, a, stage);
+  hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, c, a, stage, mode,
+                     list, cnt);
   return hipGetLastError();
 }
 

@@ -152,7 +152,7 @@ struct PdschEngine {
   // the call's generation (only sequences not already on the device)
   int gold_launch() {
     if (!ngold) return 0;
-    HIPCHK(hipMemcpyAsync(d_gold, h_gold, sizeof(GoldItem) * ngold, hipMemcpyHostToDevice, st));
+    HIPCHK(ring.upload(d_gold, h_gold, sizeof(GoldItem) * ngold, st));
     {
       ProfScope ps("k_gold", st);
       HIPCHK(launch_gold(d_gold, (int)ngold, gold_bits(), d_x1, d_x2b, gold_words, st));
@@ -447,7 +447,7 @@ struct PdschEngine {
       }
     }
     if (gold_launch()) return -1;
-    HIPCHK(hipMemcpyAsync(d_llr, h_llr, sizeof(LlrItem) * k, hipMemcpyHostToDevice, st));
+    HIPCHK(ring.upload(d_llr, h_llr, sizeof(LlrItem) * k, st));
     HIPCHK(ring.mark(st));
     if (csi) HIPCHK(hipMemsetAsync(d_csimax, 0, (size_t)k * 4, st));
     ProfScope ps("k_pdsch_llr", st);
@@ -558,7 +558,7 @@ struct PdschEngine {
     }
     if (srsgpu_dlsch_encode_dev(dl, h_tb, k, d_data, d_ebits)) return -1;
     if (gold_launch()) return -1;
-    HIPCHK(hipMemcpyAsync(d_tx, h_tx, sizeof(TxItem) * n, hipMemcpyHostToDevice, st));
+    HIPCHK(ring.upload(d_tx, h_tx, sizeof(TxItem) * n, st));
     HIPCHK(ring.mark(st));
     ProfScope ps("k_pdsch_tx", st);
     HIPCHK(launch_pdsch_tx(d_tx, (int)n, mre, d_mod, st));

@@ -36,6 +36,7 @@
 #include "srsgpu/pdcch_batch.h"
 #include "srsgpu/pdsch_batch.h"
 #include "srsgpu/rx_queue.h"
+#include "host_ring.h"
 
 namespace {
 
@@ -595,7 +596,7 @@ struct srsgpu_rxq {
       // staged rows: SC16 converts from the raw copy, cf32 is in place
       for (size_t r = 0; r < rows; r++)
         if (!sl.h_src[r]) sl.h_src[r] = sc16 ? (const void *)(dst_raw + r * row_bytes) : nullptr;
-      if (hipMemcpyAsync(sl.d_src, sl.h_src, sizeof(void *) * rows, hipMemcpyHostToDevice, cst) != hipSuccess)
+      if (xfer(sl.d_src, sl.h_src, sizeof(void *) * rows, hipMemcpyHostToDevice, cst) != hipSuccess)
         return false;
       const unsigned gx = (unsigned)std::min<size_t>(64, (td_len / 2 + 255) / 256);
       hipLaunchKernelGGL(k_ingest, dim3(gx, (unsigned)rows), dim3(256), 0, cst, (const void *const *)sl.d_src,
@@ -728,7 +729,7 @@ struct srsgpu_rxq {
   int control(Slot &sl, const std::vector<Pending> &b, const std::vector<uint32_t> &ue) {
     const uint32_t nu = (uint32_t)ue.size();
     for (uint32_t j = 0; j < nu; j++) sl.h_sel[j] = ue[j];
-    RXQ_CHK(hipMemcpyAsync(d_sel, sl.h_sel, sizeof(uint32_t) * nu, hipMemcpyHostToDevice, st));
+    RXQ_CHK(xfer(d_sel, sl.h_sel, sizeof(uint32_t) * nu, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_sf_noise, dim3((nu + 63) / 64), dim3(64), 0, st, d_noise, d_sel, (int)nu, (int)nrx,
                        (int)nports, d_uenoise);
     RXQ_CHK(hipGetLastError());
@@ -736,8 +737,8 @@ struct srsgpu_rxq {
     for (uint32_t j = 0; j < nu; j++)
       pc[j] = {(uint64_t)ue[j] * nrx * gsz, (uint64_t)ue[j] * nrx * nports * gsz, b[ue[j]].sf_idx(), 0.f};
     if (srsgpu_pcfich_decode_dev(pcfich, pc.data(), nu, d_grid, d_ce, gsz, d_cfi, d_corr, st)) return -1;
-    RXQ_CHK(hipMemcpyAsync(h_cfi, d_cfi, sizeof(uint32_t) * nu, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipMemcpyAsync(h_corr, d_corr, sizeof(float) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(xfer(h_cfi, d_cfi, sizeof(uint32_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(xfer(h_corr, d_corr, sizeof(float) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipEventRecord(ev_ctl, st));
     RXQ_CHK(hipEventSynchronize(ev_ctl));
     uint32_t plen, pres;
@@ -768,8 +769,8 @@ struct srsgpu_rxq {
     if (srsgpu_pdcch_extract_llr_dev(pdcch, ps.data(), nu, d_grid, d_ce, gsz, d_llr, st) ||
         srsgpu_pdcch_find_dci_dev(pdcch, se.data(), nu, d_llr, d_res, d_res_ul, st))
       return -1;
-    RXQ_CHK(hipMemcpyAsync(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
-    RXQ_CHK(hipMemcpyAsync(h_res_ul, d_res_ul, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(xfer(h_res, d_res, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(xfer(h_res_ul, d_res_ul, sizeof(srsgpu_dci_result_t) * nu, hipMemcpyDeviceToHost, st));
     RXQ_CHK(hipEventRecord(ev_ctl, st));
     RXQ_CHK(hipEventSynchronize(ev_ctl));
     // the workers' TM3 / TM4 feedback on the same estimates (phch_worker.cc:522-540); its results come
@@ -875,6 +876,24 @@ struct srsgpu_rxq {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
   }
   const bool trace = getenv("SRSGPU_RXQ_TRACE") != nullptr;
+  // The batch's small copies between device buffers and the slot's pinned host buffers run as kernels
+  // in the stream's order (launch_h2d through the pinned buffer's device view): an SDMA copy between
+  // two kernels of a stream left it idle ~30 us each in the headline's trace (r06_s5), and a batch
+  // makes five to ten of them. SRSGPU_RXQ_COPY=dma restores hipMemcpyAsync (A/B).
+  const bool kcopy = [] {
+    const char *e = getenv("SRSGPU_RXQ_COPY");
+    return !(e && strcmp(e, "dma") == 0);
+  }();
+  hipError_t xfer(void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (kcopy) {
+      void *v = nullptr;
+      void *host = k == hipMemcpyHostToDevice ? const_cast<void *>(src) : dst;
+      if (hipHostGetDevicePointer(&v, host, 0) == hipSuccess && v)
+        return k == hipMemcpyHostToDevice ? srsgpu::launch_h2d(dst, v, n, s) : srsgpu::launch_h2d(v, src, n, s);
+    }
+    return hipMemcpyAsync(dst, src, n, k, s);
+  }
   double run_tm[8] = {}; // the dispatcher's stage times of its last batch, added to tm under the lock
 
   // one batch, enqueued as a whole: OFDM of the staged samples, channel estimation and measurements,
@@ -906,7 +925,7 @@ struct srsgpu_rxq {
     if (srsgpu_chest_estimate_meas_dev(chest, sfi.data(), n * nrx, d_grid, gsz, d_ce, d_noise, d_meas)) return -1;
     if (ccfg.noise_alg != 0) { // PSS / EMPTY: carry the estimate across subframes in order
       for (uint32_t i = 0; i < n; i++) sl.h_est[i] = (uint8_t)(b[i].sf_idx() == 0 || b[i].sf_idx() == 5);
-      RXQ_CHK(hipMemcpyAsync(d_est, sl.h_est, n, hipMemcpyHostToDevice, st));
+      RXQ_CHK(xfer(d_est, sl.h_est, n, hipMemcpyHostToDevice, st));
       // grids of one subframe's rx antennas are consecutive: n rows of nrx * nports columns
       hipLaunchKernelGGL(k_noise_carry, dim3(1), dim3(64), 0, st, d_noise, d_est, (int)n, (int)(nrx * nports),
                          d_noise_last);
@@ -919,7 +938,7 @@ struct srsgpu_rxq {
         sl.h_cfo_src[i] = src;
       }
       const int cols = (int)(nrx * nports);
-      RXQ_CHK(hipMemcpyAsync(d_cfo_src, sl.h_cfo_src, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
+      RXQ_CHK(xfer(d_cfo_src, sl.h_cfo_src, sizeof(int32_t) * n, hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_getters, dim3((n + 63) / 64), dim3(64), 0, st, d_noise, d_meas, d_cfo_src,
                          (int)ccfg.rsrp_neighbour, d_meas_last, (int)n, (int)nrx, (int)nports, (int)cell.nof_prb,
                          d_getters);
@@ -927,7 +946,7 @@ struct srsgpu_rxq {
       hipLaunchKernelGGL(k_meas_last, dim3(1), dim3(64), 0, st, d_meas, src, ccfg.rsrp_neighbour ? (int)n - 1 : -1,
                          cols, d_meas_last);
       RXQ_CHK(hipGetLastError());
-      RXQ_CHK(hipMemcpyAsync(sl.h_getters, d_getters, sizeof(float) * 6 * n, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(xfer(sl.h_getters, d_getters, sizeof(float) * 6 * n, hipMemcpyDeviceToHost, st));
     }
     srsgpu_dlsch_t *dl = srsgpu_pdsch_get_dlsch(pdsch);
     std::vector<uint32_t> ue;
@@ -938,7 +957,7 @@ struct srsgpu_rxq {
     if (!ue.empty() && control(sl, b, ue)) return -1;
     lap(1);
     if (sl.fb_any)
-      RXQ_CHK(hipMemcpyAsync(sl.h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
+      RXQ_CHK(xfer(sl.h_fb, d_fb, sizeof(srsgpu_feedback_t) * ue.size(), hipMemcpyDeviceToHost, st));
     // grants: the grant items' own, the ue_dl items' from their DCI
     std::vector<srsgpu_pdsch_sf_t> sfs;
     sl.who.clear();
@@ -1040,7 +1059,7 @@ struct srsgpu_rxq {
       if (np != n) {
         for (uint32_t k = 0; k < np; k++) sl.h_who[k] = sl.who[k];
         const int cols = (int)(nrx * nports);
-        RXQ_CHK(hipMemcpyAsync(d_who, sl.h_who, sizeof(uint32_t) * np, hipMemcpyHostToDevice, st));
+        RXQ_CHK(xfer(d_who, sl.h_who, sizeof(uint32_t) * np, hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_noise_gather, dim3((np * cols + 255) / 256), dim3(256), 0, st, d_noise, d_who,
                            (int)np, cols, d_pnoise);
         RXQ_CHK(hipGetLastError());
@@ -1055,11 +1074,11 @@ struct srsgpu_rxq {
                 (cpu_s() - pc) * 1e3);
       const size_t ntbs = outp.size();
       if (sl.staged_bytes)
-        RXQ_CHK(hipMemcpyAsync(sl.h_data, d_data, sl.staged_bytes, hipMemcpyDeviceToHost, st));
-      RXQ_CHK(hipMemcpyAsync(sl.h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
-      RXQ_CHK(hipMemcpyAsync(sl.h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
+        RXQ_CHK(xfer(sl.h_data, d_data, sl.staged_bytes, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(xfer(sl.h_ret, d_ret, sizeof(int32_t) * ntbs, hipMemcpyDeviceToHost, st));
+      RXQ_CHK(xfer(sl.h_noi, d_noi, sizeof(uint32_t) * ntbs, hipMemcpyDeviceToHost, st));
     }
-    RXQ_CHK(hipMemcpyAsync(sl.h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
+    RXQ_CHK(xfer(sl.h_noise, d_noise, sizeof(float) * n * nrx * nports, hipMemcpyDeviceToHost, st));
     lap(3);
     if (trace)
       fprintf(stderr, "rxq trace: n %u front %.3f control %.3f grants %.3f pdsch %.3f ms\n", n, run_tm[0] * 1e3,

@@ -405,7 +405,7 @@ struct TdecEngine {
     TdGroup *h = (TdGroup *)gring.acquire(&re);
     HIPCHK(re);
     memcpy(h, groups.data(), ng * sizeof(TdGroup));
-    HIPCHK(hipMemcpyAsync(d_groups, h, ng * sizeof(TdGroup), hipMemcpyHostToDevice, st));
+    HIPCHK(gring.upload(d_groups, h, ng * sizeof(TdGroup), st));
     HIPCHK(gring.mark(st));
     last_up.assign(groups.begin(), groups.end());
     uploaded = ng;
@@ -422,9 +422,20 @@ struct TdecEngine {
   static bool derm_direct(const TdGroup &g, int rows_aligned) {
     return g.sb_input && rows_aligned >= 16 && g.nb % 8 == 0;
   }
+  // P1 deferral (defer_p1, the hybrid early-stop schedule with packed stragglers): the first
+  // half-iteration (DEC1) does not read P1, so k_load_derm leaves it out and the pairs k_decide lists
+  // as still running get theirs just before the early-stop launch (at 20 dB 3 % of them): a quarter
+  // of the loader's writes. p1_runs / p1_dc: the direct loads of this pass, for that late launch.
+  struct P1Run {
+    size_t g0, g1;
+    int blocks;
+  };
+  std::vector<P1Run> p1_runs;
+  DermCall p1_dc{};
+  bool p1_deferred = false;
   int load_planned(const int16_t *d_in, size_t in_stride, const int16_t *const *rows,
                    int rows_aligned, const uint8_t *init_done, bool first, uint32_t total_cbs,
-                   bool flags = true, const DermCall *derm = nullptr) {
+                   bool flags = true, const DermCall *derm = nullptr, bool defer_p1 = false) {
     // load launches: runs of groups with the same loader (nb, sb_input); rows_aligned is the
     // byte alignment every row is guaranteed to have (0: none)
     const size_t ng = groups.size();
@@ -457,11 +468,19 @@ struct TdecEngine {
     }
     if (upload_groups()) return -1;
     const TdArrays a = arrays();
+    p1_runs.clear();
+    p1_deferred = false;
     for (const Run &r : runs) {
       const TdGroup &f = groups[r.g0];
       if (r.direct) {
         ProfScope ps("k_ldderm", st); // k_load_derm (a name no other scope contains: srsgpu_prof_get matches substrings)
-        HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, *derm, a, derm_max_ne, st));
+        HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, *derm, a, derm_max_ne, st,
+                                defer_p1 ? 1 : 0));
+        if (defer_p1) {
+          p1_runs.push_back(P1Run{r.g0, r.g1, r.blocks});
+          p1_dc = *derm;
+          p1_deferred = true;
+        }
         continue;
       }
       ProfScope ps("k_load", st);
@@ -606,6 +625,20 @@ struct TdecEngine {
   // one launch each (k_win_bidir_es, k_sse_es); GENERIC one launch per half-iteration plus a decide
   // launch, which skips the pairs the fused launches finished.
   // SRSGPU_TDEC_FUSED=0 selects the per-half-iteration launches everywhere (A/B measurements).
+  // the hybrid early-stop schedule (decode_planned): es_fused 3, or 2 when a kind's workgroups do not
+  // fit on the chip at once; every kind fusable. A plan() must have run.
+  bool hybrid_planned(uint32_t maxh) const {
+    const int es_mode = td_sched().es_fused;
+    if (!((es_mode == 3 || es_mode == 2) && maxh > 1)) return false;
+    bool all_es = true, any_big = false;
+    for (int k = 0; k < TD_NKIND; k++)
+      if (kind_g0[k + 1] > kind_g0[k]) {
+        if (!halfits_es_fusable(k)) all_es = false;
+        const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, 160 * 1024 / (kind_lds[k] + 2048)));
+        if ((size_t)kind_blocks[k] > (size_t)num_cus() * per_cu) any_big = true;
+      }
+    return all_es && (es_mode == 3 || any_big);
+  }
   int decode_planned(uint32_t maxh, uint8_t *d_out, size_t out_stride) {
     // td_sched().es_chunk: half-iterations per early-stop launch. One launch per half-iteration
     // (with the CRC check inside, no decide launch) lets the kernels of other streams in between;
@@ -634,18 +667,12 @@ struct TdecEngine {
     // early-stop launch per kind, where they loop without a launch and a k_decide per half-iteration
     // es_fused 2 (auto) takes this form too when a kind's workgroups do not fit on the chip at once
     // (a fused launch would leave its last round of workgroups to run every half-iteration alone)
-    auto fits = [&](int k) {
-      const size_t per_cu = std::max<size_t>(1, std::min<size_t>(8, 160 * 1024 / (kind_lds[k] + 2048)));
-      return (size_t)kind_blocks[k] <= (size_t)num_cus() * per_cu;
-    };
-    if ((es_mode == 3 || es_mode == 2) && maxh > 1) {
-      bool all_es = true, any_big = false;
-      for (int k = 0; k < TD_NKIND; k++)
-        if (kind_g0[k + 1] > kind_g0[k]) {
-          if (!halfits_es_fusable(k)) all_es = false;
-          if (!fits(k)) any_big = true;
-        }
-      if (all_es && (es_mode == 3 || any_big)) {
+    if (p1_deferred && !hybrid_planned(maxh)) {
+      fprintf(stderr, "srsgpu: internal: P1 deferred without the hybrid schedule\n");
+      return -1;
+    }
+    {
+      if (hybrid_planned(maxh)) {
         // "_h0": the first half-iteration's own scope name (a subset of "k_win_bidir" for
         // srsgpu_prof_get, which matches substrings)
         static const char *const names0[TD_NKIND] = {"k_win_bidir_h0", "k_win_bidir_h0", "k_sse_halfit",
@@ -658,8 +685,16 @@ struct TdecEngine {
         }
         // windowed kinds: the pairs still running are listed by k_decide and packed by the early-stop
         // launch (TdEs::run_list); the SSE kind keeps its own mapping
-        const bool compact = knobs().es_compact;
+        const bool compact = knobs().es_compact || p1_deferred;
         if (decide(0, d_out, out_stride, true, maxh, compact)) return -1;
+        if (p1_deferred) { // P1 of the pairs still running (k_load_derm mode 2), before their DEC2
+          const TdArrays a1 = arrays();
+          for (const P1Run &r : p1_runs) {
+            ProfScope ps("k_ldderm", st);
+            HIPCHK(launch_load_derm(d_groups + r.g0, (int)(r.g1 - r.g0), r.blocks, p1_dc, a1, derm_max_ne, st, 2,
+                                    run_list, run_cnt));
+          }
+        }
         if (split_st && split_st != st) {
           // the few blocks still running, their bytes and the caller's epilogue on the tail stream:
           // the caller's stream goes on with its next work meanwhile
@@ -797,7 +832,10 @@ struct TdecEngine {
         if (r > 0) fprintf(stderr, "srsgpu: code block group exceeds the decoder capacity\n");
         return -1;
       }
-      if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs, true, derm)) return -1;
+      // P1 deferral needs the hybrid schedule's k_decide list (and the early stop)
+      const bool defer_p1 = derm && !fixed && knobs().defer_p1 && hybrid_planned(maxh);
+      if (load_planned(d_in, in_stride, rows, rows_aligned, init_done, first, total_cbs, true, derm, defer_p1))
+        return -1;
       defer_now = defer_bytes && s0 == 0 && s1 == specs.size(); // one pass: Dfz / groups stay for the caller
       if (fixed) { // all maxh half-iterations, then one CRC check (no early stop: measurement mode)
         if (halfits_fixed((int)maxh) || decide((int)maxh - 1, d_out, out_stride, true, maxh)) return -1;

@@ -27,6 +27,7 @@ struct Knobs {
   bool llr_generic; // SRSGPU_LLR_GENERIC (A/B): the general PDSCH LLR kernel only
   bool llr_noxcd;   // SRSGPU_LLR_NOXCD (A/B): the plain item-major workgroup mapping
   bool es_compact;  // SRSGPU_ES_COMPACT (default 1): the hybrid early-stop launch packs the running pairs
+  bool defer_p1;    // SRSGPU_DEFER_P1 (default 1): k_load_derm leaves P1 to the pairs still running
 };
 
 inline int env_prio(const char *name, int dflt) {
@@ -47,6 +48,8 @@ inline const Knobs *knobs_from_env() {
   {
     const char *e = getenv("SRSGPU_ES_COMPACT");
     k->es_compact = !(e && e[0] == '0');
+    const char *f = getenv("SRSGPU_DEFER_P1");
+    k->defer_p1 = !(f && f[0] == '0');
   }
   return k;
 }
