@@ -94,6 +94,43 @@ def physical_cpus():
     return out
 
 
+def quiet_cpus(n, sample_s=0.3):
+    """n physical cores (one logical CPU each) among this process's CPUs, the least busy first, from two
+    /proc/stat samples sample_s apart (a core's load = its busiest SMT sibling). The GPU box shares its
+    host's cores with other jobs: a thread pinned to a core another process keeps busy waits behind it
+    (r06_s7: the first paced point on CPUs 0-7 saw 35-95 ms stalls without any quota throttling).
+    Returns (cpus, busy fraction of each)."""
+    def snap():
+        out = {}
+        try:
+            for line in open("/proc/stat"):
+                if line.startswith("cpu") and line[3].isdigit():
+                    f = line.split()
+                    v = [int(x) for x in f[1:]]
+                    out[int(f[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+        except OSError:
+            pass
+        return out
+    a = snap()
+    time.sleep(sample_s)
+    b = snap()
+    busy = {}
+    for c in os.sched_getaffinity(0):
+        if c in a and c in b and b[c][0] > a[c][0]:
+            busy[c] = 1.0 - (b[c][1] - a[c][1]) / (b[c][0] - a[c][0])
+        else:
+            busy[c] = 0.5
+    cores = {}
+    for c in sorted(busy):
+        try:
+            sib = open("/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % c).read().strip()
+        except OSError:
+            sib = str(c)
+        cores.setdefault(sib, []).append(c)
+    ranked = sorted(cores.values(), key=lambda cs: (max(busy[c] for c in cs), cs[0]))[:n]
+    return [cs[0] for cs in ranked], [round(max(busy[c] for c in cs), 3) for cs in ranked]
+
+
 def ref8_sample(d_in8, d_out, expect, stride, nsample=64):
     """The reference's own 8-bit decoder (srslte_tdec_iteration_8bit, AUTO -> AVX8, oracle/_ref) on
     `nsample` of the 8-bit leg's code blocks (the same int8 LLRs): its bit errors against the
@@ -133,7 +170,7 @@ def cpu_baseline(llr, nthreads=None):
     cap = int(os.environ.get("SRSGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", len(cores))))
     if nthreads is None:
         nthreads = max(1, min(len(cores), cap))
-    pin = cores[:nthreads]
+    pin = quiet_cpus(nthreads)[0]  # the least busy physical cores of the shared host
     ref = os.path.join(REPO, "oracle", "_ref", "libsrsref.so")
     port = os.path.join(REPO, "oracle", "liboracle.so")
     kind = "reference" if os.path.exists(ref) else "port"
@@ -815,6 +852,7 @@ def paced_record(lat, slat, status, acked, late, ns, ticks, nb, done, tmg, budge
            "dispatcher_us_per_sf": {k: round(v / max(done, 1) * 1e6, 3) for k, v in tmg.items()},
            "ingest_GBps": round(ns * 1000.0 * sf_bytes / 1e9, 2)}
     rec["within_budget"] = bool(p99 <= budget_ms and rec["failed"] == 0 and acked == ns * ticks)
+    rec["worst_tick"] = int(np.argmax(lat)) // ns  # where the largest latency fell in the run
     return rec
 
 
@@ -864,14 +902,15 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
         scale = float(np.abs(x_cf.view(np.float32)).max()) / 32000.0
         x_sc = np.round(x_cf.view(np.float32) / scale).astype(np.int16)  # [n_src][15 N * 2]
         srcs[fft] = {"cf": x_cf, "sc": x_sc, "scale": scale, "sfs": base, "n": c["n"]}
-    cpus = physical_cpus()
-    # the queue's closer / dispatcher / completer, then the collector and the producers (paced)
+    # the queue's closer / dispatcher / completer, then the collector and the producers (paced), each on
+    # its own physical core, the least busy ones of the host
+    cpus, cpu_busy = quiet_cpus(4 + paced_workers)
     q_cpus, d_cpus = cpus[:3], cpus[3:4 + paced_workers] or cpus[:1]
     out = {"workload": "c3_coded_queue_20MHz_64QAM_tbs%d" % C3_TBS, "snr_db": snr_db,
            "producers": producers, "saturated": {}, "paced": {},
            "host_memory": "queue-owned (srsgpu_rxq_alloc_host)",
-           "cpus": {"available": len(os.sched_getaffinity(0)), "physical": len(cpus), "quota": cpu_quota(),
-                    "queue_threads": q_cpus, "paced_threads": d_cpus}}
+           "cpus": {"available": len(os.sched_getaffinity(0)), "physical": len(physical_cpus()), "quota": cpu_quota(),
+                    "queue_threads": q_cpus, "paced_threads": d_cpus, "busy_when_chosen": cpu_busy}}
 
     def owned(q, x):
         """the caller's sample ring in queue-owned device-visible memory"""
@@ -977,17 +1016,22 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
             torch.cuda.synchronize()
             return rec
 
+        # an unrecorded first point: the sweep's first queue met one-time stalls of 35-95 ms (r06_s7)
+        print("rx_queue: paced N=%d warm-up" % fft, file=sys.stderr, flush=True)
+        warm_rec = point(paced_streams[0])
+        paced["warm_up"] = {k: warm_rec[k] for k in ("latency_ms_p99", "producer_late_ms_max", "worst_tick")}
         for ns in paced_streams:
             print("rx_queue: paced N=%d %d streams" % (fft, ns), file=sys.stderr, flush=True)
             rec = point(ns)
-            if not rec["within_budget"] and (rec["producer_late_ms_p99"] or 0) > 1.0 and \
-                    (rec["submit_latency_ms_p99"] or 1e9) <= budget_ms:
-                # the load generator itself fell behind its ticks (host scheduling of the producer threads:
-                # the queue's own latency was within budget): measured once more, both records kept
-                again = point(ns)
-                again["first_attempt"] = {k: rec[k] for k in ("latency_ms_p99", "submit_latency_ms_p99",
-                                                              "producer_late_ms_max", "producer_late_ms_p99")}
-                rec = again
+            attempts = []
+            while not rec["within_budget"] and (rec["producer_late_ms_p99"] or 0) > 1.0 and len(attempts) < 2:
+                # the load generator fell behind its ticks (the producer threads descheduled on a shared
+                # host): measured again, at most twice, every attempt kept
+                attempts.append({k: rec[k] for k in ("latency_ms_p99", "submit_latency_ms_p99", "producer_late_ms_max",
+                                                     "producer_late_ms_p99", "worst_tick")})
+                rec = point(ns)
+            if attempts:
+                rec["earlier_attempts"] = attempts
             paced[str(ns)] = rec
             if rec["failed"] == 0 and rec["acked"] == "%d/%d" % (ns * ticks, ns * ticks) and \
                     (rec["submit_latency_ms_p99"] or 1e9) <= budget_ms:
@@ -996,13 +1040,14 @@ def rx_queue_leg(s, torch, dev, nsf=4096, batches=(256, 1024), producers=8, snr_
                 misses = 0
                 best = max(best, ns)
             else:
-                # one miss can be a host hiccup (a producer thread descheduled for a few ms puts every
-                # stream it serves past the budget for those TTIs): the sweep stops at the second miss
-                # in a row; real_time_streams is the largest N that met the budget
+                # a miss can be a host hiccup (the shared host stalled this process for 30-90 ms in
+                # r06_s7 / r06_s8 at 32 streams, with every later point met): the sweep stops at the
+                # second miss in a row once some N has met the budget; real_time_streams is the largest
+                # N that met it
                 misses += 1
                 if first_miss is None:
                     first_miss = dict(rec, streams=ns)
-                if misses >= 2 or rec["producer_late_ms_max"] > 50:
+                if misses >= 2 and best > 0:
                     break
         out["real_time_streams" if fft == 2048 else "real_time_streams_%d" % fft] = best
         # the queue's own capacity: latency from each subframe's actual submission within the budget
@@ -1167,7 +1212,7 @@ ALG_BYTES_PER_SF = {
 HEADLINE_SNR_DB = 20.0
 # descriptor sets the headline cycles through (a new grant every step: no repeat-call cache hits)
 HEADLINE_DESCRIPTOR_SETS = 4
-HEADLINE_TAIL = 0
+HEADLINE_TAIL = 1  # r06_s7: 0.770 against 0.845 ms per batch (three alternated pairs, four descriptor sets)
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
 HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 8}, "per_halfit": {"es_fused": 0},
                "fused_c8": {"es_fused": 1, "es_chunk": 8}, "hybrid": {"es_fused": 3, "es_chunk": 8}}
@@ -1278,7 +1323,7 @@ def cpu_baseline_pipeline(grids, sf_idx, snr_db, nthreads=None, target_thread_s=
     cap = int(os.environ.get("SRSGPU_CPU_THREADS", os.environ.get("OMP_NUM_THREADS", len(cores))))
     if nthreads is None:
         nthreads = max(1, min(len(cores), cap))
-    pin = cores[:nthreads]
+    pin = quiet_cpus(nthreads)[0]  # the least busy physical cores of the shared host
     nsf = len(sf_idx)
 
     def run(reps):

@@ -876,13 +876,14 @@ struct srsgpu_rxq {
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
   }
   const bool trace = getenv("SRSGPU_RXQ_TRACE") != nullptr;
-  // The batch's small copies between device buffers and the slot's pinned host buffers run as kernels
-  // in the stream's order (launch_h2d through the pinned buffer's device view): an SDMA copy between
-  // two kernels of a stream left it idle ~30 us each in the headline's trace (r06_s5), and a batch
-  // makes five to ten of them. SRSGPU_RXQ_COPY=dma restores hipMemcpyAsync (A/B).
+  // The batch's small copies between device buffers and the slot's pinned host buffers: hipMemcpyAsync
+  // (DMA), or with SRSGPU_RXQ_COPY=kernel copy kernels through the pinned buffer's device view
+  // (launch_h2d), as the engines' host rings do. A/B r06_s7: the kernel copies lost 25-30 % of the
+  // saturated rate at batch 256 (99-105 K against 129-147 K subframes/s; a batch makes 10-15 of them,
+  // each a launch on the dispatcher thread) and 1-4 % at batch 1024, so DMA stays the default here.
   const bool kcopy = [] {
     const char *e = getenv("SRSGPU_RXQ_COPY");
-    return !(e && strcmp(e, "dma") == 0);
+    return e && strcmp(e, "kernel") == 0;
   }();
   hipError_t xfer(void *dst, const void *src, size_t n, hipMemcpyKind k, hipStream_t s) {
     if (!n) return hipSuccess;
