@@ -745,7 +745,7 @@ def load_profile_json(workload, tag="pmc_traffic"):
                 except Exception:
                     continue
                 if d.get("workload") == workload:
-                    best = d
+                    best = dict(d, source="profiles/" + f)  # the committed file the figures come from
     return best
 
 
@@ -1446,6 +1446,11 @@ def decoder_leg(s, torch, dev, args, dist, rank, nranks):
                         "traffic": traffic, "traffic_over_compulsory": round(traffic / alg_bytes, 2) if traffic else None,
                         "traffic_source": pmc.get("source") if pmc else None, "alg_bytes_per_launch": int(alg_bytes),
                         "alg_bytes_def": "SURVEY 8(d): (3(K+32)+12)*2 + K/8 = %d B per CB per decode" % COMPULSORY_BYTES_PER_CB,
+                        # what an iterative decoder must stream every half-iteration (its state does not fit
+                        # the caches: 4096 x K=6144 x 10 B = 252 MB): DEC1 reads SP0 + A (6 B per CB and info
+                        # bit) and writes X2 (2 B), DEC2 reads X2 + P1 (4 B) and writes A (2 B)
+                        "working_set_bytes_per_launch": int(7 * NCB * K * halfits_per_launch),
+                        "traffic_over_working_set": round(traffic / (7 * NCB * K * halfits_per_launch), 2) if traffic else None,
                         "avg_launch_ms": round(avg_launch_ms, 4), "launches": kern_n,
                         "halfits_per_launch": halfits_per_launch, "avg_halfit_ms": round(avg_launch_ms / halfits_per_launch, 4)}}
     if kern_n:
@@ -1762,7 +1767,8 @@ def main():
                 os.environ[name] = val
             s.knobs_reload()
             r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
-                            lanes=args.lanes, rotate=int(os.environ.get("BENCH_AB_ROTATE", "1")))
+                            lanes=args.lanes, rotate=int(os.environ.get("BENCH_AB_ROTATE", str(HEADLINE_DESCRIPTOR_SETS))),
+                            tail=args.tail)
             os.environ.pop(name, None)
             s.knobs_reload()
             extra.setdefault("envab", []).append({name: val if on else None, "ms_per_batch": r["ms_per_batch"],
@@ -1778,12 +1784,20 @@ def main():
             extra.setdefault("tailab", []).append({"tail": t, "ms_per_batch": r["ms_per_batch"],
                                                    "decoded_mbps": r["decoded_mbps"], "acked_tbs": r["acked_tbs"],
                                                    "tbs_bytes_ok": r["tbs_bytes_ok"]})
+    if "laneab" in legs:
+        # the headline workload on one and on two lane streams, in turn (with the tail stream)
+        for ln in (1, 2, 1, 2, 1, 2):
+            r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
+                            lanes=ln, rotate=HEADLINE_DESCRIPTOR_SETS, tail=args.tail)
+            extra.setdefault("laneab", []).append({"lanes": ln, "ms_per_batch": r["ms_per_batch"],
+                                                   "stage_ms": r["stage_ms_per_batch"], "acked_tbs": r["acked_tbs"],
+                                                   "tbs_bytes_ok": r["tbs_bytes_ok"]})
     if "cached" in legs:
         # the headline workload with ONE descriptor set repeated every step, so the PDSCH / DL-SCH
         # repeat-call caches hit (no per-code-block host work): what a receiver never sees, kept as the
         # upper bound beside the headline, whose descriptors change every step
         extra["cached"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
-                                                  snr_db=HEADLINE_SNR_DB, dist=dist, rotate=1))
+                                                  snr_db=HEADLINE_SNR_DB, dist=dist, rotate=1, tail=args.tail))
     if "n1536" in legs:
         # srsLTE's reduced 20 MHz sampling (1536-point FFT, SURVEY 8(d) "N=1536")
         extra["n1536"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
@@ -1885,6 +1899,8 @@ def main():
             result["c3_cached"] = extra["cached"]
         if "tailab" in extra:
             result["tail_ab"] = extra["tailab"]
+        if "laneab" in extra:
+            result["lane_ab"] = extra["laneab"]
         if "envab" in extra:
             result["env_ab"] = extra["envab"]
         if pipe:

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void k_derm_flags(DermCall dc, int n, uint8_t 
 __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
                                                            DermCall dc, TdArrays arr, uint32_t stage, int mode,
                                                            const uint32_t *__restrict__ list,
-                                                           const uint32_t *__restrict__ cnt) {
+                                                           const uint32_t *__restrict__ cnt, int fast) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
   uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
   int gi = 0;
@@ -288,6 +288,32 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
   const gp_t<const uint32_t> ta = glob(reinterpret_cast<const uint32_t *>(ba.t4));
   const gp_t<const uint32_t> tb = glob(reinterpret_cast<const uint32_t *>(bb.t4));
+  if (fast && ba.fresh && bb.fresh && ba.staged && bb.staged && ba.t4 == bb.t4 && !w8) {
+    // the usual first transmission: both rows fresh, both blocks' LLRs staged, one table (same K and
+    // rv), 16-bit: an output element is the staged LLR its table entry m names (0 past E), the same m
+    // for both blocks — two table words per 16-byte SP0 vector, no per-element branches
+    const uint32_t na = ba.ne, nbk = bb.ne;
+    auto pk = [&](uint32_t m) -> uint32_t {
+      return (m < na ? (uint32_t)l0[m] : 0u) | ((m < nbk ? (uint32_t)l1[m] : 0u) << 16);
+    };
+#pragma unroll 4
+    for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
+      const uint32_t sa = ta[v], pa = ta[ne / 2 + v];
+      SP0[v] = u4v{pk(sa & 0xFFFFu), pk(pa & 0xFFFFu), pk(sa >> 16), pk(pa >> 16)};
+    }
+    typedef uint32_t u2f __attribute__((ext_vector_type(2)));
+    const gp_t<const u2f> qa = glob(reinterpret_cast<const u2f *>(ba.t4 + 2 * ne));
+#pragma unroll 4
+    for (int v = threadIdx.x; v < (mode == 1 ? 0 : ne / 4); v += LDR_THREADS) {
+      const u2f ma = qa[v];
+      P1[v] = u4v{pk(ma.x & 0xFFFFu), pk(ma.x >> 16), pk(ma.y & 0xFFFFu), pk(ma.y >> 16)};
+    }
+    if (threadIdx.x < 12 && mode != 2) {
+      const int t = threadIdx.x;
+      glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = pk(glob(ba.t4)[3 * ne + t]);
+    }
+    return;
+  }
   // SP0: vector v holds T4 elements 2v, 2v + 1 as (sys a, sys b, p0 a, p0 b) each
 #pragma unroll 4
   for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
@@ -841,7 +867,7 @@ hipError_t launch_load_derm(const TdGroup *dg, int ng, int nblocks, const DermCa
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_load_derm, dim3((unsigned)nblocks), dim3(LDR_THREADS), lds, st, dg, ng, c, a, stage, mode,
-                     list, cnt);
+                     list, cnt, knobs().ldderm_fast ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -677,16 +677,35 @@ struct TdecEngine {
         // srsgpu_prof_get, which matches substrings)
         static const char *const names0[TD_NKIND] = {"k_win_bidir_h0", "k_win_bidir_h0", "k_sse_halfit",
                                                       "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
+        // windowed kinds: the pairs still running are listed after the first half-iteration and packed
+        // by the early-stop launch (TdEs::run_list); the SSE kind keeps its own mapping
+        const bool compact = knobs().es_compact || p1_deferred;
+        // only 16-bit window kinds: the first half-iteration as an early-stop launch of one half-iteration
+        // per kind, whose workgroups check their own blocks' CRC, write the bytes of those that end and
+        // list the pairs still running (no k_decide launch, no decision-word round trip)
+        bool h0_fused = knobs().h0_decide;
+        for (int k = 0; k < TD_NKIND; k++)
+          if (kind_g0[k + 1] > kind_g0[k] && k != TD_KIND_W16 && k != TD_KIND_W8) h0_fused = false;
         for (int k = 0; k < TD_NKIND; k++) {
           const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
           if (g1 <= g0) continue;
           ProfScope ps(names0[k], st);
-          HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
+          if (h0_fused) {
+            TdEs e0 = es;
+            e0.n0 = 0;
+            e0.n1 = 1;
+            e0.prio = knobs().h0_prio;
+            e0.bytes_direct = 1;
+            if (compact) {
+              e0.list_out = run_list;
+              e0.cnt_out = run_cnt;
+            }
+            HIPCHK(launch_halfits_es(k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], a, e0, st));
+          } else {
+            HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
+          }
         }
-        // windowed kinds: the pairs still running are listed by k_decide and packed by the early-stop
-        // launch (TdEs::run_list); the SSE kind keeps its own mapping
-        const bool compact = knobs().es_compact || p1_deferred;
-        if (decide(0, d_out, out_stride, true, maxh, compact)) return -1;
+        if (!h0_fused && decide(0, d_out, out_stride, true, maxh, compact)) return -1;
         if (p1_deferred) { // P1 of the pairs still running (k_load_derm mode 2), before their DEC2
           const TdArrays a1 = arrays();
           for (const P1Run &r : p1_runs) {

@@ -106,6 +106,12 @@ struct TdEs {
   // windowed kinds after a k_decide that listed the pairs still running (hybrid schedule): per group,
   // run_cnt[pair0] of them at run_list[pair0 ..] (group-local pair numbers, any order); null: every pair
   const uint32_t *run_list = nullptr, *run_cnt = nullptr;
+  // bytes_direct with n0 = 0, n1 = 1: the hybrid schedule's first half-iteration with the decide of its
+  // own blocks fused in (k_win_bidir_h0c): the blocks that pass get their natural-order bytes written at
+  // once, and with list_out / cnt_out the pairs still running are appended to their group's list there
+  // (the run_list / run_cnt of the early-stop launch that follows; cnt_out zeroed by launch_pair_done)
+  int bytes_direct = 0;
+  uint32_t *list_out = nullptr, *cnt_out = nullptr;
 };
 // the natural-order bytes of the blocks the fused launches ended (after the last of them)
 hipError_t launch_es_bytes(const TdGroup *dg, int ng, int npairs, const TdEs &es, hipStream_t st);

@@ -1341,6 +1341,183 @@ __global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_es(const TdGr
   }
 }
 
+// ------------------------------------------------------------------ first half-iteration + check ----
+// The hybrid schedule's first half-iteration (DEC1, n = 0) with the decide of its own blocks fused in
+// (TdEs::bytes_direct, SRSGPU_H0_DECIDE): k_win_bidir's body, then the workgroup stages its pairs'
+// decision words in the checkpoint LDS (free after the body) and does what k_decide does for them —
+// the CRC of each block (the chain-major weights TdGroup::wc, crc.c:144-155 is linear), done / ok /
+// noi (sch.c:361-391), the natural-order bytes of the blocks that pass (turbodecoder.c:353-360 +
+// decision_byte, MSB first), and the pairs still running appended to their group's list for the
+// early-stop launch (TdEs::list_out / cnt_out).
+// Bytes from the staged words: natural position p = d L + k is step k of chain d, bit (c & 15) + 16 h
+// of word c >> 4 with c = p + d (16 G16 - L); the threads take 32-bit output words, a byte inside one
+// chain is 8 consecutive bits of it (two 16-bit halves funnelled), a byte across a chain boundary
+// goes bit by bit.
+__device__ __forceinline__ uint32_t h0_byte(const uint32_t *dw, int nw, int L, int gap, float invL, int h, int p) {
+  const int d = (int)(((float)p + 0.5f) * invL); // exact: see k_decide
+  const int k0 = p - d * L;
+  uint32_t v;
+  if (k0 + 7 < L) {
+    const int c = p + d * gap, q = c >> 4;
+    const uint32_t lo = (dw[q] >> (16 * h)) & 0xffffu;
+    const uint32_t hi = q + 1 < nw ? (dw[q + 1] >> (16 * h)) & 0xffffu : 0u;
+    v = ((lo | (hi << 16)) >> (c & 15)) & 0xffu;
+  } else {
+    v = 0;
+    for (int i = 0; i < 8; i++) {
+      const int pi = p + i;
+      const int di = (int)(((float)pi + 0.5f) * invL);
+      const int c = pi + di * gap;
+      v |= ((dw[c >> 4] >> ((c & 15) + 16 * h)) & 1u) << i;
+    }
+  }
+  return __builtin_bitreverse32(v) >> 24;
+}
+
+template <int NB>
+__device__ __noinline__ void h0_check(const TdGroup &G, const int *wpair, const uint32_t *__restrict__ Darr,
+                                      const TdEs &es, uint32_t *red, int *fin, uint32_t *sdw) {
+  constexpr int NP = 64 / NB;
+  const int K = G.K, L = K / NB, G16 = (L + 15) / 16, nw = NB * G16, gap = 16 * G16 - L;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // the pairs' decision words into LDS (coalesced, all loads up front)
+  for (int i = t; i < NP * nw; i += 128) {
+    const int lp = i / nw, q = i - lp * nw;
+    sdw[i] = Darr[G.dw0 + (size_t)wpair[lp] * nw + q];
+  }
+  __syncthreads();
+  const gptr_t<uint32_t> wc = gptr(G.wc[0]);
+#pragma unroll
+  for (int lp = 0; lp < NP; lp++) {
+    uint32_t c0 = 0, c1 = 0;
+    if (!((fin[2 * lp] & 1) && (fin[2 * lp + 1] & 1))) {
+      for (int q = t; q < nw; q += 128) {
+        const uint32_t w = sdw[lp * nw + q];
+        if (w == 0u) continue;
+        const gptr_t<u4> wq = (gptr_t<u4>)(wc + (size_t)q * 16);
+        uint32_t wt[16];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const u4 v = wq[i];
+          wt[4 * i] = v[0];
+          wt[4 * i + 1] = v[1];
+          wt[4 * i + 2] = v[2];
+          wt[4 * i + 3] = v[3];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          c0 ^= ((w >> j) & 1u) ? wt[j] : 0u;
+          c1 ^= ((w >> (16 + j)) & 1u) ? wt[j] : 0u;
+        }
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      c0 ^= __shfl_xor(c0, o);
+      c1 ^= __shfl_xor(c1, o);
+    }
+    if (lane == 0) {
+      red[(lp * 2 + 0) * 2 + wv] = c0;
+      red[(lp * 2 + 1) * 2 + wv] = c1;
+    }
+  }
+  __syncthreads();
+  if (t < 2 * NP) {
+    const int lp = t >> 1, h = t & 1;
+    int done = 1, now = 0;
+    if (!(fin[t] & 1)) {
+      const int cb = G.cb0 + 2 * wpair[lp] + h;
+      const uint32_t crc = red[t * 2] ^ red[t * 2 + 1];
+      es.noi[cb] = 1u;
+      if (crc == 0u) {
+        es.cb_ok[cb] = 1;
+        es.cb_done[cb] = 1;
+        now = 1;
+      } else if (1 >= es.max_halfits) {
+        es.cb_done[cb] = 1;
+        now = 1;
+      } else {
+        done = 0;
+      }
+    }
+    fin[t] = done | (now << 1);
+  }
+  __syncthreads();
+  if (es.list_out && t < NP && !((fin[2 * t] & 1) && (fin[2 * t + 1] & 1)))
+    es.list_out[G.pair0 + atomicAdd(&es.cnt_out[G.pair0], 1u)] = (uint32_t)wpair[t];
+  // bytes of the blocks that ended now, 32-bit words (rows are 4-byte aligned when outb and the
+  // stride are; otherwise bytes)
+  const float invL = 1.0f / (float)L;
+  const int nbytes = K / 8, nwd = nbytes / 4;
+  const bool w32 = ((uintptr_t)es.outb & 3u) == 0 && (es.out_stride & 3u) == 0;
+#pragma unroll
+  for (int lp = 0; lp < NP; lp++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (!(fin[2 * lp + h] & 2)) continue;
+      const uint32_t *dw = sdw + lp * nw;
+      uint8_t *row = es.outb + (size_t)(G.cb0 + 2 * wpair[lp] + h) * es.out_stride;
+      if (w32) {
+        for (int w = t; w < nwd; w += 128) {
+          const int p = 32 * w;
+          gmut<uint32_t>(row)[w] = h0_byte(dw, nw, L, gap, invL, h, p) | (h0_byte(dw, nw, L, gap, invL, h, p + 8) << 8) |
+                                   (h0_byte(dw, nw, L, gap, invL, h, p + 16) << 16) |
+                                   (h0_byte(dw, nw, L, gap, invL, h, p + 24) << 24);
+        }
+        for (int b = 4 * nwd + t; b < nbytes; b += 128) gmut<uint8_t>(row)[b] = (uint8_t)h0_byte(dw, nw, L, gap, invL, h, 8 * b);
+      } else {
+        for (int b = t; b < nbytes; b += 128) gmut<uint8_t>(row)[b] = (uint8_t)h0_byte(dw, nw, L, gap, invL, h, 8 * b);
+      }
+    }
+  }
+}
+
+template <int NB, int DIV, bool B8>
+__global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir_h0c(const TdGroup *__restrict__ groups, int ngroups,
+                                                       const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                       s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                       const s2 *__restrict__ T, size_t plane, TdEs es) {
+  extern __shared__ s4 cks[];
+  constexpr int NP = 64 / NB;
+  __shared__ uint32_t red[NP * 2 * 2];
+  __shared__ int fin[NP * 2];
+  __shared__ int wpair[NP];
+  wave_prio(es.prio);
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // 0: alpha, 1: beta
+  const TdGroup &G = groups[grp_find<GF_HALF>(groups, ngroups, blockIdx.x)];
+  const int K = G.K, npairs = G.npairs;
+  const int blk = blockIdx.x - G.blk_half;
+  const int lane = threadIdx.x & 63;
+  // k_win_bidir's mapping: NP consecutive pairs, lanes past the group's chains repeat its last pair
+  // (their slots count as done: never checked, never listed)
+  if (threadIdx.x < 2 * NP) {
+    const int p = NP * blk + (threadIdx.x >> 1), h = threadIdx.x & 1;
+    fin[threadIdx.x] = (p >= npairs || 2 * p + h >= G.ncb || es.cb_done[G.cb0 + 2 * p + h]) ? 1 : 0;
+    if (h == 0) wpair[threadIdx.x >> 1] = p < npairs ? p : npairs - 1;
+  }
+  __syncthreads();
+  {
+    bool all_done = true;
+    for (int i = 0; i < 2 * NP; i++) all_done = all_done && (fin[i] & 1);
+    if (all_done) return; // HARQ blocks that passed before: both waves leave before the barriers
+  }
+  const int gl = blk * 64 + lane;
+  const int nlanes = npairs * NB;
+  const int g = gl < nlanes ? gl : nlanes - 1;
+  const int pair = g / NB;
+  const int d = g % NB;
+  const size_t base = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, NB);
+  const s4 *sp0 = SP0 + base;
+  s2 *xp1 = XP1 + base;
+  const s2 *p1 = XP1 + plane + base;
+  s2 *A = Aarr + base;
+  uint32_t *D = Darr + G.dw0 + (size_t)pair * dec_words(K, NB);
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const WinRes R = win_res<NB>(G, K, blk, pair, SP0, XP1, Aarr, plane, G.rev);
+  win_bidir_body<NB, DIV, 2, true, B8>(sp0, xp1, p1, A, D, tl, R, cks, K, d, role, lane);
+  __syncthreads(); // both waves' decision words are written; the checkpoint LDS is free
+  h0_check<NB>(G, wpair, Darr, es, red, fin, reinterpret_cast<uint32_t *>(cks));
+}
+
 // ------------------------------------------------------------------ SSE non-window ----
 #define TD_SP 8 // steps per prefetch group of the sequential decoders: must divide 8 (every LTE K is a multiple of 8, not of 16)
 // turbodecoder_sse.c:97-407, one lane per CB pair, natural index (NB = 1). Branch metrics from
@@ -2272,7 +2449,8 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
                                                 int early, uint8_t *__restrict__ cb_done,
                                                 uint8_t *__restrict__ cb_ok, uint32_t *__restrict__ noi,
                                                 int max_halfits, uint8_t *__restrict__ pair_done, int prio,
-                                                uint32_t *__restrict__ run_list, uint32_t *__restrict__ run_cnt) {
+                                                uint32_t *__restrict__ run_list, uint32_t *__restrict__ run_cnt,
+                                                int knobs_dev_word_bytes) {
   __shared__ uint32_t dw[6144 / 16 + 16];
   __shared__ uint32_t red[2][4];
   __shared__ int fin[4]; // [0..1] CB done, [2..3] CB finished at this half-iteration
@@ -2360,6 +2538,29 @@ __global__ __launch_bounds__(256) void k_decide(int n, const TdGroup *__restrict
   // fraction of (p + 0.5) / L stays >= 1 / (2 L) away from an integer)
   const float invL = 1.0f / (float)L;
   const int gap = 16 * G16 - L;
+  if (!dec2 && knobs_dev_word_bytes) {
+    // after DEC1 a byte inside one chain is 8 consecutive bits of its chain: each thread forms whole
+    // 32-bit output words from the staged words (h0_byte), one store per word
+    const int nbytes = K / 8, nwd = nbytes / 4;
+    const bool w32 = ((uintptr_t)outb & 3u) == 0 && (out_stride & 3u) == 0;
+    for (int h = 0; h < 2; h++) {
+      if (!out[h]) continue;
+      uint8_t *row = outb + (size_t)cbs[h] * out_stride;
+      if (w32) {
+        for (int w = threadIdx.x; w < nwd; w += blockDim.x) {
+          const int p = 32 * w;
+          reinterpret_cast<uint32_t *>(row)[w] =
+              h0_byte(dw, nw, L, gap, invL, h, p) | (h0_byte(dw, nw, L, gap, invL, h, p + 8) << 8) |
+              (h0_byte(dw, nw, L, gap, invL, h, p + 16) << 16) | (h0_byte(dw, nw, L, gap, invL, h, p + 24) << 24);
+        }
+        for (int b = 4 * nwd + (int)threadIdx.x; b < nbytes; b += blockDim.x)
+          row[b] = (uint8_t)h0_byte(dw, nw, L, gap, invL, h, 8 * b);
+      } else {
+        for (int b = threadIdx.x; b < nbytes; b += blockDim.x) row[b] = (uint8_t)h0_byte(dw, nw, L, gap, invL, h, 8 * b);
+      }
+    }
+    return;
+  }
   auto chain_index = [&](int p) -> int {
     if (dec2) return (int)dmap[p];
     const int d = (int)(((float)p + 0.5f) * invL);
@@ -2619,6 +2820,13 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
   } while (0)
 #define RUNES(nb, div, b8)                                                                         \
   do {                                                                                             \
+    if (es.bytes_direct && es.n0 == 0 && es.n1 == 1) { /* first half-iteration + its check */      \
+      allow_big_lds((const void *)(k_win_bidir_h0c<nb, div, b8>), 1024);                           \
+      hipLaunchKernelGGL((k_win_bidir_h0c<nb, div, b8>), dim3(nblocks), dim3(128), lds, st, dg, ng, \
+                         (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,               \
+                         (const s2 *)a.T, a.plane, es);                                            \
+      break;                                                                                       \
+    }                                                                                              \
     allow_big_lds((const void *)(k_win_bidir_es<nb, div, b8>), 1024); /* + its static LDS */       \
     hipLaunchKernelGGL((k_win_bidir_es<nb, div, b8>), dim3(nblocks), dim3(128), lds, st, dg, ng,   \
                        (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,                 \
@@ -2764,7 +2972,7 @@ hipError_t launch_decide(int n, const TdGroup *dg, int ng, int npairs, const TdA
   hipLaunchKernelGGL(k_decide, dim3(npairs), dim3(256), 0, st, n, dg, ng, (const uint32_t *)a.D, outb,
                      out_stride, early ? 1 : 0, cb_done, cb_ok, noi, max_halfits,
                      early ? pair_done : nullptr, knobs().decide_prio, early ? run_list : nullptr,
-                     early ? run_cnt : nullptr);
+                     early ? run_cnt : nullptr, knobs().decide_words ? 1 : 0);
   return hipGetLastError();
 }
 #endif // TD_PART == 0

@@ -28,6 +28,13 @@ struct Knobs {
   bool llr_noxcd;   // SRSGPU_LLR_NOXCD (A/B): the plain item-major workgroup mapping
   bool es_compact;  // SRSGPU_ES_COMPACT (default 1): the hybrid early-stop launch packs the running pairs
   bool defer_p1;    // SRSGPU_DEFER_P1 (default 1): k_load_derm leaves P1 to the pairs still running
+  bool h0_decide;   // SRSGPU_H0_DECIDE=1 (A/B, default 0): the hybrid schedule's first half-iteration
+                    // checks its own blocks (k_win_bidir_h0c: bytes written at once), no k_decide launch;
+                    // slower (r06_s10: 0.799 against 0.770 ms per batch: the check lengthens every
+                    // decoder workgroup's life on its CU, where k_decide's 3,328 small ones overlap)
+  bool ldderm_fast; // SRSGPU_LDERM_FAST (default 1): k_load_derm's branch-free form for fresh, staged,
+                    // same-table 16-bit pairs
+  bool decide_words; // SRSGPU_DECIDE_WORDS (default 1): k_decide writes DEC1 bytes as 32-bit words
 };
 
 inline int env_prio(const char *name, int dflt) {
@@ -50,6 +57,12 @@ inline const Knobs *knobs_from_env() {
     k->es_compact = !(e && e[0] == '0');
     const char *f = getenv("SRSGPU_DEFER_P1");
     k->defer_p1 = !(f && f[0] == '0');
+    const char *h = getenv("SRSGPU_H0_DECIDE");
+    k->h0_decide = h && h[0] == '1';
+    const char *l = getenv("SRSGPU_LDERM_FAST");
+    k->ldderm_fast = !(l && l[0] == '0');
+    const char *w = getenv("SRSGPU_DECIDE_WORDS");
+    k->decide_words = !(w && w[0] == '0');
   }
   return k;
 }
