@@ -1646,7 +1646,9 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true", help="headline and configs[1] decoder only")
     ap.add_argument("--coded-snr", type=float, default=None,
                     help="SNR of the coded C3 leg (default 30 dB; profiling aid)")
-    ap.add_argument("--lanes", type=int, default=2, help="HIP streams per rank for the headline leg")
+    # one lane: with the early-stop tails on the tail stream, a second lane no longer pays
+    # (r06_s12: 0.743 against 0.754 ms per batch, three alternated pairs)
+    ap.add_argument("--lanes", type=int, default=1, help="HIP streams per rank for the headline leg")
     ap.add_argument("--tail", type=int, default=HEADLINE_TAIL,
                     help="headline early-stop tails: 0 on the lane's stream, 1 on one high-priority tail stream")
     ap.add_argument("--ab-headline", action="store_true",
@@ -1737,7 +1739,7 @@ def main():
                        "nof_prb": C3_PRB, "fft_size": head["symbol_size"], "mcs": 28, "tbs": C3_TBS,
                        "code_blocks_per_subframe": 13, "K": 5824, "snr_db": HEADLINE_SNR_DB,
                        "early_stop_max_halfits": 8, "descriptor_sets": HEADLINE_DESCRIPTOR_SETS,
-                       "tail_stream": args.tail,
+                       "tail_stream": args.tail, "lanes": args.lanes,
                        "subframes_per_s": head["subframes_per_s"],
                        "nof_iterations_mean": head["nof_iterations_mean"], "acked_tbs": head["acked_tbs"],
                        "tbs_bytes_ok": head["tbs_bytes_ok"], "parallelism": "dp%d" % nranks},
@@ -1797,11 +1799,13 @@ def main():
         # repeat-call caches hit (no per-code-block host work): what a receiver never sees, kept as the
         # upper bound beside the headline, whose descriptors change every step
         extra["cached"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
-                                                  snr_db=HEADLINE_SNR_DB, dist=dist, rotate=1, tail=args.tail))
+                                                  snr_db=HEADLINE_SNR_DB, dist=dist, rotate=1, tail=args.tail,
+                                                  lanes=args.lanes))
     if "n1536" in legs:
         # srsLTE's reduced 20 MHz sampling (1536-point FFT, SURVEY 8(d) "N=1536")
         extra["n1536"] = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps), 2, "c3_coded",
-                                                 snr_db=HEADLINE_SNR_DB, dist=dist, standard_rate=False))
+                                                 snr_db=HEADLINE_SNR_DB, dist=dist, standard_rate=False,
+                                                 lanes=args.lanes, tail=args.tail, rotate=HEADLINE_DESCRIPTOR_SETS))
     pipe = None
     if "c3" in legs:
         pipe = run_pipeline(s, torch, dev, max(2, args.steps // 2), 2, dist=dist)
@@ -1829,7 +1833,8 @@ def main():
         # (14-16 dB: 2..8 half-iterations, failing TBs) and up to 30 dB
         sweep = []
         for snr in (14.0, 15.0, 16.0, 18.0, 20.0, 25.0, 30.0):
-            r = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps // 2), 2, "c3_coded", snr_db=snr, dist=dist))
+            r = scale_ranks(run_traffic(s, torch, dev, max(8, args.steps // 2), 2, "c3_coded", snr_db=snr, dist=dist,
+                                        lanes=args.lanes, tail=args.tail, rotate=HEADLINE_DESCRIPTOR_SETS))
             sweep.append({k: r[k] for k in ("snr_db", "decoded_mbps", "acked_tb_mbps", "offered_tb_mbps",
                                              "subframes_per_s", "ms_per_batch", "nof_iterations_mean",
                                              "acked_tbs", "tbs")})

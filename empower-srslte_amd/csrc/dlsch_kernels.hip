@@ -223,53 +223,52 @@ __global__ __launch_bounds__(256) void k_derm_flags(DermCall dc, int n, uint8_t 
 // not read it, and at high SNR few blocks reach the second); 2: P1 only, for the pairs k_decide listed
 // as still running after the first half-iteration (TdEs::run_list / run_cnt per group at pair0:
 // workgroup j of a group takes its list entry j)
-__global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
-                                                           DermCall dc, TdArrays arr, uint32_t stage, int mode,
-                                                           const uint32_t *__restrict__ list,
-                                                           const uint32_t *__restrict__ cnt, int fast) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
-  uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
-  int gi = 0;
-  { // the last group whose first workgroup is <= blockIdx.x
-    int lo = 0, hi = ngroups - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (groups[mid].blk_load <= (int)blockIdx.x)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    gi = lo;
-  }
-  const TdGroup &G = groups[gi];
-  const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
-  int pair = blockIdx.x - G.blk_load;
-  if (pair >= npairs) return;
-  if (mode == 2) {
-    if (pair >= (int)cnt[G.pair0]) return;
-    pair = (int)list[G.pair0 + pair];
-  }
-  const int L = K / nb, G4 = (L + 3) >> 2, ne = nb * 4 * G4;
-  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
-  struct Blk {
-    const int16_t *e, *row;
-    const uint16_t *t4;
-    uint32_t ne, N;
-    bool fresh, staged;
+struct LdrBlk {
+  const int16_t *e, *row;
+  const uint16_t *t4;
+  uint32_t ne, N;
+  bool fresh, staged;
+};
+__device__ __forceinline__ LdrBlk ldr_blk(const DermCall &dc, int c, uint32_t stage) {
+  const DermItem it = derm_get(dc, c);
+  return LdrBlk{it.e, it.row, it.inv_t4, it.ne, it.N, it.fresh && *glob(it.fresh), it.ne <= it.N && it.ne <= stage};
+}
+// the usual first transmission: both rows fresh, both blocks' LLRs staged, one table (same K and rv),
+// 16-bit: an output element is the staged LLR its table entry m names (0 past E), the same m for both
+// blocks — two table words per 16-byte SP0 vector, no per-element branches
+__device__ __forceinline__ bool ldr_fast_ok(const LdrBlk &a, const LdrBlk &b, bool w8) {
+  return a.fresh && b.fresh && a.staged && b.staged && a.t4 == b.t4 && !w8;
+}
+// tw: the table's stream-0/1 words (entries 2v, 2v+1 of stream st at word st ne/2 + v), in LDS or HBM
+template <typename TW>
+__device__ __forceinline__ void ldr_fast(TW tw, const LdrBlk &ba, const LdrBlk &bb, const uint16_t *l0,
+                                         const uint16_t *l1, int ne, int mode, gp_t<u4v> SP0, gp_t<u4v> P1,
+                                         uint32_t *T12) {
+  const uint32_t na = ba.ne, nbk = bb.ne;
+  auto pk = [&](uint32_t m) -> uint32_t {
+    return (m < na ? (uint32_t)l0[m] : 0u) | ((m < nbk ? (uint32_t)l1[m] : 0u) << 16);
   };
-  auto blk = [&](int c) {
-    const DermItem it = derm_get(dc, c);
-    return Blk{it.e, it.row, it.inv_t4, it.ne, it.N, it.fresh && *glob(it.fresh),
-               it.ne <= it.N && it.ne <= stage};
-  };
-  const Blk ba = blk(c0), bb = blk(c1);
-  const bool w8 = dc.rec[c0].w8 != 0; // one LLR width per call
-  if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
-  if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
-  __syncthreads();
-  const uint16_t *l0 = reinterpret_cast<const uint16_t *>(llr0), *l1 = reinterpret_cast<const uint16_t *>(llr1);
+#pragma unroll 4
+  for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
+    const uint32_t sa = tw[v], pa = tw[ne / 2 + v];
+    SP0[v] = u4v{pk(sa & 0xFFFFu), pk(pa & 0xFFFFu), pk(sa >> 16), pk(pa >> 16)};
+  }
+  typedef uint32_t u2f __attribute__((ext_vector_type(2)));
+  const gp_t<const u2f> qa = glob(reinterpret_cast<const u2f *>(ba.t4 + 2 * ne));
+#pragma unroll 4
+  for (int v = threadIdx.x; v < (mode == 1 ? 0 : ne / 4); v += LDR_THREADS) {
+    const u2f ma = qa[v];
+    P1[v] = u4v{pk(ma.x & 0xFFFFu), pk(ma.x >> 16), pk(ma.y & 0xFFFFu), pk(ma.y >> 16)};
+  }
+  if (threadIdx.x < 12 && mode != 2) glob(T12)[threadIdx.x] = pk(glob(ba.t4)[3 * ne + threadIdx.x]);
+}
+// every other case (HARQ combining with the row's old entries, unstaged LLRs, two tables, 8-bit)
+__device__ __forceinline__ void ldr_generic(const LdrBlk &ba, const LdrBlk &bb, const uint16_t *l0, const uint16_t *l1,
+                                            bool w8, int K, int nb, int ne, int mode, gp_t<u4v> SP0, gp_t<u4v> P1,
+                                            uint32_t *T12) {
+  const int L = K / nb;
   // value of T4 element el of stream st of block b, given its table entry m
-  auto value = [&](const Blk &b, const uint16_t *lds, int st, int el, uint32_t m) -> uint32_t {
+  auto value = [&](const LdrBlk &b, const uint16_t *lds, int st, int el, uint32_t m) -> uint32_t {
     uint32_t acc = 0;
     if (!b.fresh) { // the row's old entry at its row position (padded steps: step L - 1's)
       const int k = min(4 * (el / (4 * nb)) + (el & 3), L - 1), d = (el >> 2) % nb;
@@ -283,37 +282,8 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
     }
     return derm_fold(acc, w8) & 0xFFFFu;
   };
-  const size_t pbase = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
-  const gp_t<u4v> SP0 = glob(reinterpret_cast<u4v *>((int16_t *)arr.SP0 + 4 * pbase));
-  const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
   const gp_t<const uint32_t> ta = glob(reinterpret_cast<const uint32_t *>(ba.t4));
   const gp_t<const uint32_t> tb = glob(reinterpret_cast<const uint32_t *>(bb.t4));
-  if (fast && ba.fresh && bb.fresh && ba.staged && bb.staged && ba.t4 == bb.t4 && !w8) {
-    // the usual first transmission: both rows fresh, both blocks' LLRs staged, one table (same K and
-    // rv), 16-bit: an output element is the staged LLR its table entry m names (0 past E), the same m
-    // for both blocks — two table words per 16-byte SP0 vector, no per-element branches
-    const uint32_t na = ba.ne, nbk = bb.ne;
-    auto pk = [&](uint32_t m) -> uint32_t {
-      return (m < na ? (uint32_t)l0[m] : 0u) | ((m < nbk ? (uint32_t)l1[m] : 0u) << 16);
-    };
-#pragma unroll 4
-    for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
-      const uint32_t sa = ta[v], pa = ta[ne / 2 + v];
-      SP0[v] = u4v{pk(sa & 0xFFFFu), pk(pa & 0xFFFFu), pk(sa >> 16), pk(pa >> 16)};
-    }
-    typedef uint32_t u2f __attribute__((ext_vector_type(2)));
-    const gp_t<const u2f> qa = glob(reinterpret_cast<const u2f *>(ba.t4 + 2 * ne));
-#pragma unroll 4
-    for (int v = threadIdx.x; v < (mode == 1 ? 0 : ne / 4); v += LDR_THREADS) {
-      const u2f ma = qa[v];
-      P1[v] = u4v{pk(ma.x & 0xFFFFu), pk(ma.x >> 16), pk(ma.y & 0xFFFFu), pk(ma.y >> 16)};
-    }
-    if (threadIdx.x < 12 && mode != 2) {
-      const int t = threadIdx.x;
-      glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = pk(glob(ba.t4)[3 * ne + t]);
-    }
-    return;
-  }
   // SP0: vector v holds T4 elements 2v, 2v + 1 as (sys a, sys b, p0 a, p0 b) each
 #pragma unroll 4
   for (int v = threadIdx.x; v < (mode == 2 ? 0 : ne / 2); v += LDR_THREADS) {
@@ -339,7 +309,7 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
   }
   if (threadIdx.x < 12 && mode != 2) { // the tails: row positions 3(K+32) .. +11, table entries 3 ne + t
     const int t = threadIdx.x;
-    auto tail = [&](const Blk &b, const uint16_t *lds) -> uint32_t {
+    auto tail = [&](const LdrBlk &b, const uint16_t *lds) -> uint32_t {
       const uint32_t m = glob(b.t4)[3 * ne + t];
       uint32_t acc = b.fresh ? 0u : (uint16_t)glob(b.row)[3 * (K + 32) + t];
       if (b.staged) {
@@ -351,8 +321,53 @@ __global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__rest
       return derm_fold(acc, w8) & 0xFFFFu;
     };
     const uint32_t va = tail(ba, l0), vb = tail(bb, l1);
-    glob(reinterpret_cast<uint32_t *>(arr.T))[(size_t)(G.pair0 + pair) * 12 + t] = va | (vb << 16);
+    glob(T12)[t] = va | (vb << 16);
   }
+}
+
+// the last group whose first load workgroup is <= w
+__device__ __forceinline__ int ldr_group(const TdGroup *__restrict__ groups, int ngroups, int w) {
+  int lo = 0, hi = ngroups - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (groups[mid].blk_load <= w)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(LDR_THREADS) void k_load_derm(const TdGroup *__restrict__ groups, int ngroups,
+                                                           DermCall dc, TdArrays arr, uint32_t stage, int mode,
+                                                           const uint32_t *__restrict__ list,
+                                                           const uint32_t *__restrict__ cnt, int fast) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t ldr_lds[];
+  uint32_t *llr0 = ldr_lds, *llr1 = ldr_lds + stage / 2;
+  const TdGroup &G = groups[ldr_group(groups, ngroups, (int)blockIdx.x)];
+  const int K = G.K, ncb = G.ncb, npairs = G.npairs, nb = G.nb;
+  int pair = blockIdx.x - G.blk_load;
+  if (pair >= npairs) return;
+  if (mode == 2) {
+    if (pair >= (int)cnt[G.pair0]) return;
+    pair = (int)list[G.pair0 + pair];
+  }
+  const int L = K / nb, G4 = (L + 3) >> 2, ne = nb * 4 * G4;
+  const int c0 = G.cb0 + 2 * pair, c1 = 2 * pair + 1 < ncb ? c0 + 1 : c0;
+  const LdrBlk ba = ldr_blk(dc, c0, stage), bb = ldr_blk(dc, c1, stage);
+  const bool w8 = dc.rec[c0].w8 != 0; // one LLR width per call
+  if (ba.staged) stage_llrs(llr0, ba.e, ba.ne);
+  if (bb.staged) stage_llrs(llr1, bb.e, bb.ne);
+  __syncthreads();
+  const uint16_t *l0 = reinterpret_cast<const uint16_t *>(llr0), *l1 = reinterpret_cast<const uint16_t *>(llr1);
+  const size_t pbase = (size_t)G.elem0 + (size_t)pair * t4_pair_elems(K, nb);
+  const gp_t<u4v> SP0 = glob(reinterpret_cast<u4v *>((int16_t *)arr.SP0 + 4 * pbase));
+  const gp_t<u4v> P1 = glob(reinterpret_cast<u4v *>((int16_t *)arr.XP1 + 2 * (arr.plane + pbase)));
+  uint32_t *T12 = reinterpret_cast<uint32_t *>(arr.T) + (size_t)(G.pair0 + pair) * 12;
+  if (fast && ldr_fast_ok(ba, bb, w8))
+    ldr_fast(glob(reinterpret_cast<const uint32_t *>(ba.t4)), ba, bb, l0, l1, ne, mode, SP0, P1, T12);
+  else
+    ldr_generic(ba, bb, l0, l1, w8, K, nb, ne, mode, SP0, P1, T12);
 }
 
 // The previous form of k_load_derm, kept for A/B measurements (SRSGPU_LDERM=tile): row-order

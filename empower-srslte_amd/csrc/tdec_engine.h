@@ -110,7 +110,7 @@ struct TdecEngine {
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // tail stream (srsgpu_dlsch_set_tail_stream): under the hybrid early-stop schedule, everything after
-  // the first half-iteration's k_decide moves to split_st (st is switched for the rest of the call)
+  // the first half-iteration moves to split_st (st is switched for the rest of the call)
   hipStream_t split_st = nullptr;
   hipEvent_t ev_split = nullptr;
   // defer_bytes (the DL-SCH engine's request): the natural-order bytes of the blocks a fused early-stop
@@ -705,6 +705,21 @@ struct TdecEngine {
             HIPCHK(launch_halfit(0, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, pair_done, st));
           }
         }
+        auto split = [&]() -> int {
+          if (split_st && split_st != st) {
+            // the few blocks still running, their bytes and the caller's epilogue on the tail stream:
+            // the caller's stream goes on with its next work meanwhile
+            if (!ev_split) HIPCHK(hipEventCreateWithFlags(&ev_split, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ev_split, st));
+            HIPCHK(hipStreamWaitEvent(split_st, ev_split, 0));
+            st = split_st;
+          }
+          return 0;
+        };
+        // the tail stream takes over right after the first half-iteration (the first check and the P1
+        // loads too), so the caller's stream moves on to its next work two launches earlier
+        // (SRSGPU_SPLIT_EARLY=0: after them)
+        if (knobs().split_early && split()) return -1;
         if (!h0_fused && decide(0, d_out, out_stride, true, maxh, compact)) return -1;
         if (p1_deferred) { // P1 of the pairs still running (k_load_derm mode 2), before their DEC2
           const TdArrays a1 = arrays();
@@ -714,14 +729,7 @@ struct TdecEngine {
                                     run_list, run_cnt));
           }
         }
-        if (split_st && split_st != st) {
-          // the few blocks still running, their bytes and the caller's epilogue on the tail stream:
-          // the caller's stream goes on with its next work meanwhile
-          if (!ev_split) HIPCHK(hipEventCreateWithFlags(&ev_split, hipEventDisableTiming));
-          HIPCHK(hipEventRecord(ev_split, st));
-          HIPCHK(hipStreamWaitEvent(split_st, ev_split, 0));
-          st = split_st;
-        }
+        if (split()) return -1;
         es.n0 = 1;
         es.n1 = (int)maxh;
         for (int k = 0; k < TD_NKIND; k++) {

@@ -649,6 +649,11 @@ class Dlsch:
         if _lib.srsgpu_dlsch_set_tail_stream(self.q, _vp(stream or None)) != 0:
             raise RuntimeError("srsgpu_dlsch_set_tail_stream failed")
 
+    def join_tail(self):
+        """srsgpu_dlsch_join_tail: the engine's stream waits for its last call's tail (tail stream)"""
+        if _lib.srsgpu_dlsch_join_tail(self.q) != 0:
+            raise RuntimeError("srsgpu_dlsch_join_tail failed")
+
     def set_direct_derm(self, on):
         """srsgpu_dlsch_set_direct_derm (off: every softbuffer row written before the decode)"""
         _lib.srsgpu_dlsch_set_direct_derm(self.q, int(bool(on)))

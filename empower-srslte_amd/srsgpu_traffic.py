@@ -211,6 +211,10 @@ class MixedCells:
         self.cur = (self.cur + 1) % self.rotate
         self.eng = (self.eng + 1) % self.nengine
         t0 = time.perf_counter()
+        if self.nengine > 1:
+            # the engine's previous call may still read its LLR buffer on the tail stream (the P1 loads,
+            # the rows of failed TBs): the front end rewrites that buffer only after it
+            self.dlsch.join_tail()
         self.front_end()
         t1 = time.perf_counter()
         self.decode()
