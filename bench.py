@@ -498,7 +498,7 @@ def cb_sizes(table, tbs):
 
 def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=None, schedules=None,
                 standard_rate=True, early_stop=True, cpu_sample=0, warm_seconds=0.25, rotate=1, tail=0,
-                tail_prio=True):
+                tail_prio=True, fe_split=False):
     """Coded traffic made on the GPU by the transmit chain (srsgpu_traffic.MixedCells), received
     with CRC early stop (max 8 half-iterations, srsUE's default):
     kind "c5" — BASELINE configs[4] per-GPU shard: 1024 subframes per GPU interleaved over cells of
@@ -525,7 +525,7 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
     tail 1 / 2: each lane alternates between two DL-SCH engines whose early-stop tails run on a tail
     stream (srsgpu_dlsch_set_tail_stream; 1: one tail stream shared by the lanes, 2: one per lane), so
     a lane's next batch starts while the last one's straggling code blocks finish; tail_prio: the tail
-    streams are high-priority streams."""
+    streams are high-priority streams; fe_split: each lane's front end on a stream of its own."""
     import srsgpu_shard as sh
     import srsgpu_traffic as tr
     rank = dist.get_rank() if dist else 0
@@ -553,6 +553,8 @@ def run_traffic(s, torch, dev, steps, warmup, kind, lanes=2, snr_db=None, dist=N
             tp = -1 if tail_prio else 0
             tk = dict(engines=2, tail_stream=lane_stream(torch, dev, "tail" if tail == 1 else "tail%d" % li,
                                                          priority=tp).cuda_stream)
+            if fe_split:  # the front end on a stream of its own (MixedCells fe_stream)
+                tk["fe_stream"] = lane_stream(torch, dev, "fe%d" % li).cuda_stream
         ms.append(tr.MixedCells(table, n_global, torch, dev, seed=seed, stream=st, snr_db=snr,
                                 keep=mine[li::lanes], standard_rate=standard_rate, early_stop=early_stop,
                                 rotate=rotate, **tk, **kw))  # one plan: the same seed everywhere
@@ -1212,6 +1214,7 @@ ALG_BYTES_PER_SF = {
 HEADLINE_SNR_DB = 20.0
 # descriptor sets the headline cycles through (a new grant every step: no repeat-call cache hits)
 HEADLINE_DESCRIPTOR_SETS = 4
+HEADLINE_FE_STREAM = 1  # r06_s16: 0.695 against 0.712 ms per batch (three alternated pairs)
 HEADLINE_TAIL = 1  # r06_s7: 0.770 against 0.845 ms per batch (three alternated pairs, four descriptor sets)
 # decoder early-stop launch schedules (srsgpu_tdec_set_schedule) compared by --ab-headline
 HEADLINE_AB = {"auto": {"es_fused": 2, "es_chunk": 8}, "per_halfit": {"es_fused": 0},
@@ -1649,6 +1652,8 @@ def main():
     # one lane: with the early-stop tails on the tail stream, a second lane no longer pays
     # (r06_s12: 0.743 against 0.754 ms per batch, three alternated pairs)
     ap.add_argument("--lanes", type=int, default=1, help="HIP streams per rank for the headline leg")
+    ap.add_argument("--fe-stream", type=int, default=HEADLINE_FE_STREAM,
+                    help="1: the headline's front end on a stream of its own, beside the previous batch's decoder")
     ap.add_argument("--tail", type=int, default=HEADLINE_TAIL,
                     help="headline early-stop tails: 0 on the lane's stream, 1 on one high-priority tail stream")
     ap.add_argument("--ab-headline", action="store_true",
@@ -1722,7 +1727,7 @@ def main():
     head = scale_ranks(run_traffic(s, torch, dev, args.steps, args.warmup, "c3_coded", snr_db=HEADLINE_SNR_DB,
                                    dist=dist, cpu_sample=64 if (rank == 0 and nranks == 1) else 0, lanes=args.lanes,
                                    warm_seconds=1.0, schedules=HEADLINE_AB if args.ab_headline else None,
-                                   rotate=HEADLINE_DESCRIPTOR_SETS, tail=args.tail))
+                                   rotate=HEADLINE_DESCRIPTOR_SETS, tail=args.tail, fe_split=bool(args.fe_stream)))
     cpu_grids, cpu_sf = head.pop("_cpu_grids", None), head.pop("_cpu_sf_idx", None)
     result = None
     if rank == 0:
@@ -1739,7 +1744,7 @@ def main():
                        "nof_prb": C3_PRB, "fft_size": head["symbol_size"], "mcs": 28, "tbs": C3_TBS,
                        "code_blocks_per_subframe": 13, "K": 5824, "snr_db": HEADLINE_SNR_DB,
                        "early_stop_max_halfits": 8, "descriptor_sets": HEADLINE_DESCRIPTOR_SETS,
-                       "tail_stream": args.tail, "lanes": args.lanes,
+                       "tail_stream": args.tail, "lanes": args.lanes, "fe_stream": args.fe_stream,
                        "subframes_per_s": head["subframes_per_s"],
                        "nof_iterations_mean": head["nof_iterations_mean"], "acked_tbs": head["acked_tbs"],
                        "tbs_bytes_ok": head["tbs_bytes_ok"], "parallelism": "dp%d" % nranks},
@@ -1786,6 +1791,14 @@ def main():
             extra.setdefault("tailab", []).append({"tail": t, "ms_per_batch": r["ms_per_batch"],
                                                    "decoded_mbps": r["decoded_mbps"], "acked_tbs": r["acked_tbs"],
                                                    "tbs_bytes_ok": r["tbs_bytes_ok"]})
+    if "feab" in legs:
+        # the headline with and without a front-end stream of its own, in turn
+        for fe in (0, 1, 0, 1, 0, 1):
+            r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
+                            lanes=args.lanes, rotate=HEADLINE_DESCRIPTOR_SETS, tail=args.tail, fe_split=bool(fe))
+            extra.setdefault("feab", []).append({"fe_stream": fe, "ms_per_batch": r["ms_per_batch"],
+                                                 "stage_ms": r["stage_ms_per_batch"], "acked_tbs": r["acked_tbs"],
+                                                 "tbs_bytes_ok": r["tbs_bytes_ok"]})
     if "laneab" in legs:
         # the headline workload on one and on two lane streams, in turn (with the tail stream)
         for ln in (1, 2, 1, 2, 1, 2):
@@ -1906,6 +1919,8 @@ def main():
             result["tail_ab"] = extra["tailab"]
         if "laneab" in extra:
             result["lane_ab"] = extra["laneab"]
+        if "feab" in extra:
+            result["fe_ab"] = extra["feab"]
         if "envab" in extra:
             result["env_ab"] = extra["envab"]
         if pipe:

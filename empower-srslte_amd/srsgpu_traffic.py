@@ -66,7 +66,7 @@ def tb_weights(table, sf_plan, max_halfits=8):
 class MixedCells:
     def __init__(self, table, n_sf, torch, dev, prbs=(6, 25, 50, 100), seed=5, stream=None,
                  snr_db=30.0, max_halfits=8, mcs=None, full_band=False, keep=None, standard_rate=True,
-                 early_stop=True, ce_rows=True, rotate=1, engines=1, tail_stream=None):
+                 early_stop=True, ce_rows=True, rotate=1, engines=1, tail_stream=None, fe_stream=None):
         """n_sf subframes round-robin over the cells of `prbs`; mcs / full_band pin the MCS and
         the allocation (e.g. prbs=(100,), mcs=28, full_band=True is the C3 subframe as coded
         traffic). keep: the subframe indices this instance builds and receives (a rank's shard
@@ -83,8 +83,20 @@ class MixedCells:
         output and softbuffer sets) used by alternate steps, each decoding its early-stop tail on
         tail_stream (srsgpu_dlsch_set_tail_stream): a step's front end and first half-iteration run
         while the previous step's few straggling code blocks finish beside them. The attributes dlsch,
-        d_e, d_data, d_ret, d_noi name the engine of the last step."""
+        d_e, d_data, d_ret, d_noi name the engine of the last step.
+        fe_stream (with engines 2 and tail_stream): the front end (OFDM, estimator, PDSCH LLRs) on a
+        stream of its own, so a batch's front end runs beside the previous batch's decoder; it starts
+        once the LLR buffer it writes is free (the tail of that engine's previous call, an event on the
+        tail stream) and the DL-SCH call waits for it (an event on fe_stream)."""
         self.torch, self.dev = torch, dev
+        self._split = bool(fe_stream) and bool(tail_stream) and int(engines) > 1
+        if self._split:
+            self._fe = torch.cuda.ExternalStream(fe_stream, device=dev)
+            self._ln = torch.cuda.ExternalStream(stream, device=dev) if stream else torch.cuda.current_stream(dev)
+            self._tl = torch.cuda.ExternalStream(tail_stream, device=dev)
+            self._ev_fe = torch.cuda.Event()
+            self._ev_tail = [None, None]
+        fe_st = fe_stream if self._split else stream
         self.max_halfits = max_halfits
         sf_plan = plan(table, n_sf, prbs, seed, mcs, full_band)
         keep = set(range(n_sf)) if keep is None else set(int(k) for k in keep)
@@ -104,9 +116,9 @@ class MixedCells:
             gsz = 14 * 12 * prb
             c = {"prb": prb, "N": N, "gsz": gsz, "n": n, "id": 1 + ci,
                  "lstart": 2 if prb <= 10 else 1}
-            c["ofdm"] = s.OfdmRx(prb, N, stream=stream)
-            c["chest"] = s.Chest(prb, c["id"], max_grids=n, stream=stream)
-            c["pd"] = s.Pdsch(prb, c["id"], nof_softbuffers=1, max_cb=13, max_sf=n, stream=stream)
+            c["ofdm"] = s.OfdmRx(prb, N, stream=fe_st)
+            c["chest"] = s.Chest(prb, c["id"], max_grids=n, stream=fe_st)
+            c["pd"] = s.Pdsch(prb, c["id"], nof_softbuffers=1, max_cb=13, max_sf=n, stream=fe_st)
             c["chest"].set_ce_rows(ce_rows)
             c["pd"].set_ce_rows(4 if ce_rows else 0)
             sfs, e_offs, sf_idx = [], [], []
@@ -211,6 +223,21 @@ class MixedCells:
         self.cur = (self.cur + 1) % self.rotate
         self.eng = (self.eng + 1) % self.nengine
         t0 = time.perf_counter()
+        if self._split:
+            ev = self._ev_tail[self.eng]
+            if ev is not None:
+                self._fe.wait_event(ev)  # the engine's previous tail has read its LLR buffer
+            self.front_end()
+            self._ev_fe.record(self._fe)
+            self._ln.wait_event(self._ev_fe)
+            t1 = time.perf_counter()
+            self.decode()
+            ev = self._ev_tail[self.eng] or self.torch.cuda.Event()
+            ev.record(self._tl)  # everything of this call on the tail stream
+            self._ev_tail[self.eng] = ev
+            self.host_s[0] += t1 - t0
+            self.host_s[1] += time.perf_counter() - t1
+            return
         if self.nengine > 1:
             # the engine's previous call may still read its LLR buffer on the tail stream (the P1 loads,
             # the rows of failed TBs): the front end rewrites that buffer only after it

@@ -35,7 +35,7 @@ if [ "$PMC" = pmc ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 180 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc_$c -o pmc -- python3 bench.py --no-cpu-baseline --legs none --steps 3 --warmup 1 --detail $O/pmc_detail.json > $O/pmc_$c.log 2>&1 || { tail -5 $O/pmc_$c.log; exit 1; }
   done
-  python3 tools/pmc_pipeline.py $(find $O/pmc_FETCH_SIZE -name 'pmc_counter_collection.csv' | head -1) $(find $O/pmc_WRITE_SIZE -name 'pmc_counter_collection.csv' | head -1) $O/pmc_pipeline.json
+  python3 tools/pmc_pipeline.py $(find $O/pmc_FETCH_SIZE -name 'pmc_counter_collection.csv' | head -1) $(find $O/pmc_WRITE_SIZE -name 'pmc_counter_collection.csv' | head -1) $O/pmc_pipeline.json ${PMC_SF:-1024}
 fi
 if [ "$C2PMC" = c2pmc ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
