@@ -1775,7 +1775,7 @@ def main():
             s.knobs_reload()
             r = run_traffic(s, torch, dev, max(10, args.steps), 3, "c3_coded", snr_db=HEADLINE_SNR_DB, dist=dist,
                             lanes=args.lanes, rotate=int(os.environ.get("BENCH_AB_ROTATE", str(HEADLINE_DESCRIPTOR_SETS))),
-                            tail=args.tail)
+                            tail=args.tail, fe_split=bool(args.fe_stream))
             os.environ.pop(name, None)
             s.knobs_reload()
             extra.setdefault("envab", []).append({name: val if on else None, "ms_per_batch": r["ms_per_batch"],

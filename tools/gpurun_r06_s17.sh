@@ -1,0 +1,5 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r06_s17; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 &&
+BENCH_AB_ENV=SRSGPU_TBF_WAVES4=0 timeout -k 10 300 python -u bench.py --legs envab --steps 20 --warmup 5 --no-cpu-baseline --detail $O/ab_tbf.json > $O/ab_tbf.log 2> $O/ab_tbf.err
