@@ -994,8 +994,11 @@ __device__ __forceinline__ WinRes win_res(const TdGroup &G, int K, int blk, int 
 #ifndef TD_BIDIR_WAVES
 #define TD_BIDIR_WAVES 1 // minimum waves per SIMD the windowed decoders are compiled for
 #endif
+#ifndef TD_H0_WAVES
+#define TD_H0_WAVES TD_BIDIR_WAVES // the same for the first half-iteration (MODE 2) alone
+#endif
 template <int NB, int DIV, int MODE, int CW, bool DOUT, bool B8>
-__global__ __launch_bounds__(128, TD_BIDIR_WAVES) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
+__global__ __launch_bounds__(128, MODE == 2 ? TD_H0_WAVES : TD_BIDIR_WAVES) void k_win_bidir(const TdGroup *__restrict__ groups, int ngroups,
                                                    const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                    s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                    const s2 *__restrict__ T, size_t plane,

@@ -2,7 +2,9 @@
 the first, the bytes, the TB CRC) on a second stream, two engines alternating per batch, must give
 exactly what the single-stream decode gives — return codes, TB bytes, nof_iterations and cb_crc —
 on coded C3 subframes at SNRs where code blocks need one, two or more extra half-iterations, and
-where TBs fail (their softbuffer rows are written in the tail)."""
+where TBs fail (their softbuffer rows are written in the tail). With fe_stream the front end runs on a
+third stream, ordered against the DL-SCH call and the engine's previous tail by events (the headline's
+form: bench.py --fe-stream 1), and must give the same again."""
 import json
 import os
 
@@ -22,11 +24,12 @@ def _results(m):
     return ret, noi, data, crc
 
 
+@pytest.mark.parametrize("fe", [0, 1])
 @pytest.mark.parametrize("es_fused", [3])
 @pytest.mark.parametrize("snr_db", [14.0, 16.5, 20.0])
-def test_tail_stream_equals_single_stream(snr_db, es_fused):
+def test_tail_stream_equals_single_stream(snr_db, es_fused, fe):
     """es_fused 3 (hybrid: first half-iteration, k_decide, the rest in one early-stop launch, as the
-    headline's batches run): the split comes after the first half-iteration's k_decide"""
+    headline's batches run): the split comes right after the first half-iteration (SRSGPU_SPLIT_EARLY)"""
     import torch
     import srsgpu_phy as s
     import srsgpu_traffic as tr
@@ -36,7 +39,9 @@ def test_tail_stream_equals_single_stream(snr_db, es_fused):
     main = torch.cuda.Stream(dev)
     tail = torch.cuda.Stream(dev)
     ref = tr.MixedCells(table, 96, torch, dev, stream=main.cuda_stream, **kw)
-    two = tr.MixedCells(table, 96, torch, dev, stream=main.cuda_stream, engines=2, tail_stream=tail.cuda_stream, **kw)
+    fes = torch.cuda.Stream(dev) if fe else None
+    two = tr.MixedCells(table, 96, torch, dev, stream=main.cuda_stream, engines=2, tail_stream=tail.cuda_stream,
+                        fe_stream=fes.cuda_stream if fe else None, **kw)
     torch.cuda.synchronize()
     ref.step()  # default schedule (auto: this small job runs fused)
     torch.cuda.synchronize()
