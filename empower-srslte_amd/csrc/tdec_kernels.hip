@@ -700,6 +700,9 @@ __device__ __forceinline__ void win_bidir_body(const s4 *__restrict__ sp0, s2 *_
           } else {
             out = wsub(v, e); // store_out: DEC1 E' = L - A into app2, DEC2 L - app2 into A
           }
+#ifdef TD_EXP_NOX2
+          if (MODE != 2) // timing experiment only (wrong results): the first DEC1 stores no X2
+#endif
           bst32(__builtin_bit_cast(uint32_t, out), MODE == 1 ? R.a : R.x2, R.po + 4u * (uint32_t)t);
         }
         if (DOUT) dacc |= dec_bits(v) << j;
