@@ -1583,7 +1583,8 @@ def compact_summary(result, detail_name, limit=6000):
     cfg = result.get("config", {})
     out["config"] = {k: cfg[k] for k in ("workload", "baseline_config", "subframes_per_batch_per_gpu", "nof_prb",
                                          "fft_size", "mcs", "tbs", "code_blocks_per_subframe", "K", "snr_db",
-                                         "early_stop_max_halfits", "descriptor_sets", "subframes_per_s", "nof_iterations_mean",
+                                         "early_stop_max_halfits", "descriptor_sets", "lanes", "fe_stream", "tail_stream",
+                                         "subframes_per_s", "nof_iterations_mean",
                                          "acked_tbs", "tbs_bytes_ok", "parallelism") if k in cfg}
     for key, fields in (("roofline", ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
                                       "traffic_over_alg", "traffic_source", "alg_bytes_per_launch", "avg_launch_ms",
