@@ -522,6 +522,14 @@ struct TdecEngine {
   // dec: leave hard decisions in D (needed by the decide() that follows this half-iteration)
   int last_n = -1; // the last half-iteration launched (read_state)
 
+  // kind k of the planned job is one group of a few pairs that k_win_spread can take (latency form)
+  bool use_spread(int k) const {
+    const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
+    if (g1 - g0 != 1 || !knobs().spread) return false;
+    const TdGroup &f = groups[g0];
+    return f.npairs <= spread_max_pairs() && spread_ok(k, f.K, f.nb);
+  }
+
   int halfit(int n, bool early, bool dec = true) {
     last_n = n;
     const uint8_t *pd = early ? pair_done : nullptr;
@@ -531,6 +539,12 @@ struct TdecEngine {
       if (g1 <= g0) continue;
       static const char *const names[TD_NKIND] = {"k_win_bidir", "k_win_bidir", "k_sse_halfit",
                                                    "k_gen_halfit", "k_win8_bidir", "k_win8_bidir"};
+      if (use_spread(k)) {
+        ProfScope ps("k_win_spread", st);
+        const TdGroup &f = groups[g0];
+        HIPCHK(launch_halfit_spread(n, k, d_groups + g0, f.npairs, f.K, f.nb, dec, a, pd, st));
+        continue;
+      }
       ProfScope ps(names[k], st);
       HIPCHK(launch_halfit(n, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], dec, a, pd, st));
     }
@@ -606,7 +620,13 @@ struct TdecEngine {
     for (int k = 0; k < TD_NKIND; k++) {
       const int g0 = kind_g0[k], g1 = kind_g0[k + 1];
       if (g1 <= g0) continue;
-      if (halfits_fusable(k)) {
+      if (use_spread(k)) { // a few pairs: per-half-iteration latency launches beat one long one
+        const TdGroup &f = groups[g0];
+        for (int h = 0; h < nh; h++) {
+          ProfScope ps("k_win_spread", st);
+          HIPCHK(launch_halfit_spread(h, k, d_groups + g0, f.npairs, f.K, f.nb, h + 1 == nh, a, nullptr, st));
+        }
+      } else if (halfits_fusable(k)) {
         ProfScope ps("k_win_bidir_run", st);
         HIPCHK(launch_halfits(0, nh, k, d_groups + g0, g1 - g0, kind_blocks[k], kind_lds[k], true, a, st));
       } else {

@@ -80,6 +80,12 @@ int dec_words_host(int K, int nb);
 // one half-iteration n (DEC1 for even n, DEC2 for odd n) of every group of one kind
 hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks, size_t lds,
                          bool dec, const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
+// the same for ONE group of at most spread_max_pairs() pairs as k_win_spread (latency form), when
+// spread_ok(kind, K, nb): a windowed kind with K / nb a multiple of 16 and at least 48
+int spread_max_pairs();
+bool spread_ok(int kind, int K, int nb);
+hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
+                                const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
 // half-iterations n0 .. n0+nh-1 of every group of one windowed kind in one launch (fixed-iteration
 // jobs: no early stop in between); dec: decisions after the last one
 bool halfits_fusable(int kind);

@@ -1047,6 +1047,310 @@ __global__ __launch_bounds__(128, MODE == 2 ? TD_H0_WAVES : TD_BIDIR_WAVES) void
   TD_T(4);
 }
 
+// ------------------------------------------------------------------ windowed, spread (latency) ----
+// One half-iteration of a FEW pairs (the drop-in srslte_tdec_iteration: one code block per call),
+// where k_win_bidir leaves the chip idle and its serial chain (the prepass, then half the chunks of
+// one recursion, then the other half with the LLR, ~100 packed ops a step) is the call's latency.
+// Here a workgroup of TD_SPREAD_THREADS holds ONE pair:
+//   phase A  wave 0 runs the whole alpha recursion (prepass + chunks 0..nc-1) and checkpoints the
+//            state entering every chunk, wave 1 the whole beta recursion (prepass, tail, chunks
+//            nc-1..1) and checkpoints beta at every chunk boundary (the value before
+//            normalisation, as k_win_bidir's backward wave does); ~24 ops a step
+//   phase B  every (chain d, chunk q) is an independent task (K / 16 of them): betas recomputed
+//            from the checkpoint above the chunk, the alpha recursion with the LLR from the one
+//            below it — the pieces k_win_bidir's phase 2 runs, spread over every lane of the
+//            workgroup instead of one lane per chain.
+// The serial chain becomes L + 40 steps of one recursion plus two chunk tasks. Same steps, same
+// normalisation schedule and same checkpoint values as k_win_bidir, so the output is identical
+// (tests: every batch of one pair goes through here, larger ones through k_win_bidir).
+// Needs L = K / NB a multiple of 16 (no partial chunk) and nc >= 3 (spread_ok).
+#define TD_SPREAD_THREADS 512
+#define TD_SPREAD_MAX_PAIRS 16 // at most this many pairs per job: k_win_bidir beyond
+
+template <int NB, int DIV, int MODE, bool DOUT, bool B8>
+__global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup *__restrict__ groups,
+                                                                const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
+                                                                s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
+                                                                const s2 *__restrict__ T, size_t plane,
+                                                                const uint8_t *__restrict__ pair_done) {
+  constexpr int CW = 16;
+  extern __shared__ s4 spk[]; // checkpoints [slot][chain] x 32 B: alpha 0..nc-1, beta nc..2nc
+  const TdGroup &G = groups[0];
+  const int K = G.K, pair = blockIdx.x;
+  if (pair_done && pair_done[G.pair0 + pair]) return; // uniform over the workgroup
+  const int L = K / NB, nc = L / CW;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int pe = t4_pair_elems(K, NB);
+  const size_t base = (size_t)G.elem0 + (size_t)pair * pe;
+  WinRes R;
+  R.sp0 = mk_rsrc(SP0 + base);
+  R.x2 = mk_rsrc(XP1 + base);
+  R.p1 = mk_rsrc(XP1 + plane + base);
+  R.a = mk_rsrc(Aarr + base);
+  R.tb = mk_rsrc(MODE == 1 ? G.fwd : G.rev);
+  R.po = 0;
+  uint32_t *D = DOUT ? Darr + G.dw0 + (size_t)pair * dec_words(K, NB) : nullptr;
+  const s2 *tl = T + (size_t)(G.pair0 + pair) * 12;
+  const int K32 = K & ~31;
+
+  auto astep = [&](St8 &o, s2 x, s2 y) {
+    if (B8) {
+      s2 mb[8], nw[8];
+      b_alpha_branches(o, x, y, mb, nw);
+#pragma unroll
+      for (int i = 0; i < 8; i++) o.s[i] = bmask(smax(mb[i], nw[i]));
+    } else {
+      win_alpha_step(o, x, y);
+    }
+  };
+  auto bstep = [&](St8 &o, s2 x, s2 y) {
+    if (B8)
+      b_beta_step(o, x, y);
+    else
+      win_beta_step(o, x, y);
+  };
+  auto norm0 = [&](St8 &o) {
+    const s2 z = o.s[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++) o.s[i] = ssub(o.s[i], z);
+    o.s[0] = splat(0);
+  };
+  auto nrm_fwd = [&](St8 &o, int q, int j) { // as win_bidir_body's
+    if (B8) {
+      if (!(q == 0 && j == 0)) b_norm_max(o);
+    } else if ((j & 1) == 0) {
+      if (j != 0 || q != 0) norm0(o);
+    }
+  };
+  auto nrm_k = [&](St8 &o, bool even) {
+    if (B8)
+      b_norm_max(o);
+    else if (even)
+      norm0(o);
+  };
+  auto pnorm = [&](int k, St8 &o) {
+    if (B8)
+      b_norm(k, o);
+    else
+      win_norm(k, o);
+  };
+  auto ck_put = [&](int slot, int d, const St8 &o) {
+    s4 *p = &spk[(slot * NB + d) * 4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) p[i] = s4{o.s[2 * i].x, o.s[2 * i].y, o.s[2 * i + 1].x, o.s[2 * i + 1].y};
+  };
+  auto ck_get = [&](int slot, int d, St8 &o) {
+    const s4 *p = &spk[(slot * NB + d) * 4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const s4 v = p[i];
+      o.s[2 * i] = lo2(v);
+      o.s[2 * i + 1] = hi2(v);
+    }
+  };
+  // group g of chain dd; `lo` = per-lane byte offset added to the wave-uniform step offset (phase B:
+  // the lane's chunk), as in win_bidir_body's loads
+  auto ld_sb4 = [&](rsrc_t r, int g, int dd, uint32_t lo) {
+    const uint32_t vo = 4u * (uint32_t)dd + lo, so = 16u * NB * (uint32_t)g;
+    return u4{bld32(r, vo, so), bld32(r, vo, so + 4 * NB), bld32(r, vo, so + 8 * NB),
+              bld32(r, vo, so + 12 * NB)};
+  };
+  auto ld_grp = [&](Grp<MODE> &r, int g, int dd, uint32_t lo) {
+    if (MODE == 1) {
+      r.s0 = ld_sb4(R.x2, g, dd, lo);
+      r.s1 = bld128(R.p1, 16u * (uint32_t)dd + lo, 16u * NB * (uint32_t)g);
+    } else {
+      const uint32_t vo = 32u * (uint32_t)dd + 2u * lo, so = 32u * NB * (uint32_t)g;
+      r.s0 = bld128(R.sp0, vo, so);
+      r.s1 = bld128(R.sp0, vo, so + 16);
+      if (MODE == 0) r.a = ld_sb4(R.a, g, dd, lo);
+    }
+  };
+  auto ld_chunk = [&](Chunk<MODE> &c, int q, int dd) { // phase A: q wave-uniform
+#pragma unroll
+    for (int u = 0; u < 4; u++) ld_grp(c.g[u], 4 * q + u, dd, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto cstep = [&](const Chunk<MODE> &c, int j, s2 &x, s2 &y, s2 &e) {
+    grp_step<MODE, B8>(c.g[j >> 2], j & 3, x, y, e);
+  };
+
+  if (wave == 0) {
+    // ---- phase A, alpha: win.h:501-506,512-584 prepass over the last 40 steps of chain d-1, then
+    // every chunk, the entering state checkpointed
+    const int d = lane % NB, dp = d > 0 ? d - 1 : 0;
+    St8 o;
+    st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
+    Chunk<MODE> c0, c1, c2;
+    {
+      Grp<MODE> pg[10];
+      const int gp = (L - TD_OVERLAP) >> 2;
+#pragma unroll
+      for (int u = 0; u < 10; u++) ld_grp(pg[u], gp + u, dp, 0);
+      ld_chunk(c0, 0, d);
+      ld_chunk(c1, 1, d);
+#pragma unroll
+      for (int k = 0; k < TD_OVERLAP; k++) {
+        s2 x, y, e;
+        grp_step<MODE, B8>(pg[k >> 2], k & 3, x, y, e);
+        astep(o, x, y);
+        pnorm(k, o);
+      }
+    }
+    if (d == 0) st_fill(o, 0, B8 ? 0 : -TD_INF);
+    auto fwd_chunk = [&](const Chunk<MODE> &c, int q) {
+      ck_put(q, d, o);
+#pragma unroll
+      for (int j = 0; j < CW; j++) {
+        s2 x, y, e;
+        cstep(c, j, x, y, e);
+        astep(o, x, y);
+        nrm_fwd(o, q, j);
+      }
+    };
+    int q = 0;
+    for (; q + 2 < nc; q += 3) {
+      ld_chunk(c2, q + 2, d);
+      fwd_chunk(c0, q);
+      ld_chunk(c0, min(q + 3, nc - 1), d);
+      fwd_chunk(c1, q + 1);
+      ld_chunk(c1, min(q + 4, nc - 1), d);
+      fwd_chunk(c2, q + 2);
+    }
+    if (q < nc) fwd_chunk(c0, q);
+    if (q + 1 < nc) fwd_chunk(c1, q + 1);
+  } else if (wave == 1) {
+    // ---- phase A, beta: win.h:376-384,386-433 prepass over the first 40 steps of chain d+1 (the
+    // last chain from the tail trellis, :350-355), beta[L] and beta[16 q] for q = nc-1..1
+    const int d = lane % NB, dn = d + 1 < NB ? d + 1 : d;
+    St8 o;
+    st_fill(o, B8 ? 0 : -TD_INF, B8 ? 0 : -TD_INF);
+    Chunk<MODE> c0, c1, c2;
+    {
+      Grp<MODE> pg[10];
+#pragma unroll
+      for (int u = 0; u < 10; u++) ld_grp(pg[u], u, dn, 0);
+      s2 tv[6];
+#pragma unroll
+      for (int u = 0; u < 6; u++) tv[u] = tl[(MODE == 1 ? 6 : 0) + u];
+      ld_chunk(c0, nc - 1, d);
+      ld_chunk(c1, nc - 2, d);
+#pragma unroll
+      for (int k = TD_OVERLAP - 1; k >= 0; k--) {
+        s2 x, y, e;
+        grp_step<MODE, B8>(pg[k >> 2], k & 3, x, y, e);
+        bstep(o, x, y);
+        pnorm(k, o);
+      }
+      St8 t;
+      if (B8)
+        b_tail_trellis(tv, 0, t);
+      else
+        win_tail_trellis(tv, 0, t);
+      if (d == NB - 1) o = t;
+    }
+    ck_put(2 * nc, d, o); // beta[L]
+    auto bwd_chunk = [&](const Chunk<MODE> &c, int q) { // q >= 1
+#pragma unroll
+      for (int j = CW - 1; j >= 0; j--) {
+        s2 x, y, e;
+        cstep(c, j, x, y, e);
+        bstep(o, x, y);
+        if (j == 0) ck_put(nc + q, d, o);
+        nrm_k(o, (j & 1) == 0);
+      }
+    };
+    int q = nc - 1;
+    for (; q - 2 >= 1; q -= 3) {
+      ld_chunk(c2, q - 2, d);
+      bwd_chunk(c0, q);
+      ld_chunk(c0, max(q - 3, 1), d);
+      bwd_chunk(c1, q - 1);
+      ld_chunk(c1, max(q - 4, 1), d);
+      bwd_chunk(c2, q - 2);
+    }
+    if (q >= 1) bwd_chunk(c0, q);
+    if (q - 1 >= 1) bwd_chunk(c1, q - 1);
+  }
+  __syncthreads();
+
+  // ---- phase B: task t = (chunk q, chain d), chains of one chunk on consecutive lanes (coalesced
+  // T4 loads and table reads; the scatter stores of one step land on NB consecutive elements)
+  for (int t = tid; t < NB * nc; t += TD_SPREAD_THREADS) {
+    const int q = t / NB, d = t % NB;
+    Chunk<MODE> c;
+    {
+      const uint32_t lo = 16u * NB * 4u * (uint32_t)q; // 4 T4 groups per chunk, 16 B per group and chain
+#pragma unroll
+      for (int u = 0; u < 4; u++) ld_grp(c.g[u], u, d, lo);
+      const uint32_t vo = 32u * (uint32_t)d + 32u * NB * (uint32_t)q;
+      c.t[0] = bld128(R.tb, vo, 0);
+      c.t[1] = bld128(R.tb, vo, 16);
+    }
+    // betas of the chunk (win_bidir_body's `betas` with n = CW): bst[j] = beta[16 q + 1 + j]
+    St8 run, bst[CW];
+    ck_get(nc + q + 1, d, run); // beta[16 (q + 1)] before normalisation (beta[L] for the top chunk)
+    bst[CW - 1] = run;
+    if (q + 1 < nc) nrm_k(run, true);
+#pragma unroll
+    for (int j = CW - 2; j >= 0; j--) {
+      s2 x, y, e;
+      cstep(c, j + 1, x, y, e);
+      bstep(run, x, y);
+      bst[j] = run;
+      nrm_k(run, ((j + 1) & 1) == 0);
+    }
+    // alpha with the LLR (win_bidir_body's `alpha_llr`, n = CW)
+    St8 o;
+    ck_get(q, d, o);
+    const int s0 = CW * q;
+    uint32_t dacc = 0;
+#pragma unroll
+    for (int j = 0; j < CW; j++) {
+      s2 x, y, e;
+      cstep(c, j, x, y, e);
+      s2 mb[8], nw[8];
+      if (B8)
+        b_alpha_branches(o, x, y, mb, nw);
+      else
+        win_alpha_branches(o, x, y, mb, nw);
+      const St8 &be = bst[j];
+      s2 t0[8], t1[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        t0[i] = sadd(be.s[i], mb[i]);
+        t1[i] = sadd(be.s[i], nw[i]);
+      }
+#pragma unroll
+      for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; i++) {
+          t0[i] = smax(t0[i], t0[i + w]);
+          t1[i] = smax(t1[i], t1[i + w]);
+        }
+      s2 v = B8 ? bsub(bmask(t1[0]), bmask(t0[0])) : ssub(t1[0], t0[0]);
+      if (B8)
+        v = bmask(v >> 1);
+      else if (DIV)
+        v = v >> 1;
+      const int tt = chunk_t(c, j);
+      s2 out;
+      if (B8) {
+        const bool sat = (MODE == 1 ? tt : (s0 + j) * NB + d) < K32;
+        out = MODE == 2 ? v : (sat ? bsub(v, e) : wsub(v, e));
+      } else {
+        out = wsub(v, e);
+      }
+      bst32(__builtin_bit_cast(uint32_t, out), MODE == 1 ? R.a : R.x2, 4u * (uint32_t)tt);
+      if (DOUT) dacc |= dec_bits(v) << j;
+#pragma unroll
+      for (int i = 0; i < 8; i++) o.s[i] = B8 ? bmask(smax(mb[i], nw[i])) : smax(mb[i], nw[i]);
+      nrm_fwd(o, q, j);
+    }
+    if (DOUT) D[d * nc + q] = dacc;
+  }
+}
+
 // Half-iterations n0 .. n0+nh-1 of a fixed-iteration job in ONE launch (turbodecoder.c:510-533,
 // srslte_tdec_run_all's loop). A pair's 16 / 8 / 32 chains all sit in one workgroup, and the
 // interleaver permutes within a code block, so half-iteration n+1 of a pair reads only what this
@@ -2859,6 +3163,39 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
     return hipGetLastError();                                                                      \
   }
 
+// k_win_spread launchers, one per windowed kind (in the part that holds the kind)
+template <int KIND>
+hipError_t spread_part(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec, const TdArrays &a,
+                       const uint8_t *pair_done, hipStream_t st);
+#define SPREAD1(nb, div, m, dout, b8)                                                              \
+  hipLaunchKernelGGL((k_win_spread<nb, div, m, dout, b8>), dim3(npairs), dim3(TD_SPREAD_THREADS), lds, \
+                     st, dg, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,          \
+                     (const s2 *)a.T, a.plane, pair_done)
+#define SPREAD(KIND, nb, div, b8)                                                                  \
+  template <>                                                                                      \
+  hipError_t spread_part<KIND>(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec,      \
+                               const TdArrays &a, const uint8_t *pair_done, hipStream_t st) {      \
+    if (mode == 1) {                                                                               \
+      if (dec) SPREAD1(nb, div, 1, true, b8); else SPREAD1(nb, div, 1, false, b8);                 \
+    } else if (mode == 2) {                                                                        \
+      if (dec) SPREAD1(nb, div, 2, true, b8); else SPREAD1(nb, div, 2, false, b8);                 \
+    } else {                                                                                       \
+      if (dec) SPREAD1(nb, div, 0, true, b8); else SPREAD1(nb, div, 0, false, b8);                 \
+    }                                                                                              \
+    return hipGetLastError();                                                                      \
+  }
+#if TD_PART == 1
+SPREAD(TD_KIND_W16, 16, 0, false)
+#elif TD_PART == 2
+SPREAD(TD_KIND_W8, 8, 1, false)
+#elif TD_PART == 3
+SPREAD(TD_KIND_B16, 16, 1, true)
+#elif TD_PART == 4
+SPREAD(TD_KIND_B32, 32, 1, true)
+#endif
+#undef SPREAD
+#undef SPREAD1
+
 #define NO_ES (void)dg; (void)ng; (void)nblocks; (void)lds; (void)a; (void)es; (void)st; return hipErrorInvalidValue
 #if TD_PART == 1
 PART_FUNCS(TD_KIND_W16, BIDIR(16, 0, false), RUN1(16, 0, false), RUNES(16, 0, false))
@@ -2900,6 +3237,30 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
   case TD_KIND_GEN: return halfit_part<TD_KIND_GEN>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
   case TD_KIND_B16: return halfit_part<TD_KIND_B16>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
   case TD_KIND_B32: return halfit_part<TD_KIND_B32>(mode, dg, ng, nblocks, lds, dec, a, pair_done, st);
+  default: return hipErrorInvalidValue;
+  }
+}
+
+int spread_max_pairs() { return TD_SPREAD_MAX_PAIRS; }
+
+bool spread_ok(int kind, int K, int nb) {
+  const bool win = kind == TD_KIND_W16 || kind == TD_KIND_W8 || kind == TD_KIND_B16 || kind == TD_KIND_B32;
+  return win && nb > 1 && K % nb == 0 && (K / nb) % TD_BIDIR_CW == 0 && K / nb >= 48;
+}
+
+hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
+                                const TdArrays &arr, const uint8_t *pair_done, hipStream_t st) {
+  if (npairs <= 0) return hipSuccess;
+  if (!spread_ok(kind, K, nb) || npairs > TD_SPREAD_MAX_PAIRS) return hipErrorInvalidValue;
+  const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
+  TdArrays a = arr;
+  if (!dec) a.D = nullptr;
+  const size_t lds = (size_t)(2 * (K / nb / TD_BIDIR_CW) + 1) * nb * 32;
+  switch (kind) {
+  case TD_KIND_W16: return spread_part<TD_KIND_W16>(mode, dg, npairs, lds, dec, a, pair_done, st);
+  case TD_KIND_W8: return spread_part<TD_KIND_W8>(mode, dg, npairs, lds, dec, a, pair_done, st);
+  case TD_KIND_B16: return spread_part<TD_KIND_B16>(mode, dg, npairs, lds, dec, a, pair_done, st);
+  case TD_KIND_B32: return spread_part<TD_KIND_B32>(mode, dg, npairs, lds, dec, a, pair_done, st);
   default: return hipErrorInvalidValue;
   }
 }

@@ -37,6 +37,9 @@ struct Knobs {
   bool decide_words; // SRSGPU_DECIDE_WORDS (default 1): k_decide writes DEC1 bytes as 32-bit words
   bool split_early;  // SRSGPU_SPLIT_EARLY (default 1): a tail stream takes over right after the first
                      // half-iteration (r06_s14, one lane: 0.721 against 0.764 ms per batch)
+  bool spread;       // SRSGPU_SPREAD (default 1): per-half-iteration launches of a few pairs run as
+                     // k_win_spread (one pair per workgroup, both recursions whole, then every chunk
+                     // in parallel): the drop-in srslte_tdec_iteration's latency
 };
 
 inline int env_prio(const char *name, int dflt) {
@@ -67,6 +70,8 @@ inline const Knobs *knobs_from_env() {
     k->decide_words = !(w && w[0] == '0');
     const char *se = getenv("SRSGPU_SPLIT_EARLY");
     k->split_early = !(se && se[0] == '0');
+    const char *sp = getenv("SRSGPU_SPREAD");
+    k->spread = !(sp && sp[0] == '0');
   }
   return k;
 }
