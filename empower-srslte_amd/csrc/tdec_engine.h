@@ -530,6 +530,20 @@ struct TdecEngine {
     return f.npairs <= spread_max_pairs() && spread_ok(k, f.K, f.nb);
   }
 
+  // half-iteration n of a one-group job that k_win_spread takes, with the decision bytes of its
+  // blocks written to outb by the same launch (the drop-in's one launch per call); 1: not this job
+  int halfit_bytes(int n, uint8_t *outb, size_t out_stride) {
+    if (groups.size() != 1) return 1;
+    int k = 0;
+    while (k < TD_NKIND && kind_g0[k + 1] - kind_g0[k] != 1) k++;
+    if (k == TD_NKIND || !use_spread(k)) return 1;
+    last_n = n;
+    const TdGroup &f = groups[0];
+    ProfScope ps("k_win_spread", st);
+    HIPCHK(launch_halfit_spread(n, k, d_groups, f.npairs, f.K, f.nb, true, arrays(), nullptr, st, outb, out_stride));
+    return 0;
+  }
+
   int halfit(int n, bool early, bool dec = true) {
     last_n = n;
     const uint8_t *pd = early ? pair_done : nullptr;

@@ -315,6 +315,9 @@ struct TdecGpu {
   int16_t *d_in = nullptr;
   uint8_t *d_out = nullptr;
   size_t in_len = 0;
+  // decision bytes written by the half-iteration's own launch (k_win_spread) into mapped, coherent
+  // host memory: no k_decide launch and no copy per srslte_tdec_iteration call (null: not available)
+  uint8_t *h_out = nullptr, *dh_out = nullptr;
 };
 
 int srslte_tdec_init(srslte_tdec_t *h, uint32_t max_long_cb) {
@@ -347,6 +350,11 @@ int srslte_tdec_init_manual(srslte_tdec_t *h, uint32_t max_long_cb, srslte_tdec_
     delete g;
     return -1;
   }
+  if (hipHostMalloc((void **)&g->h_out, max_long_cb / 8 + 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void **)&g->dh_out, g->h_out, 0) != hipSuccess) {
+    if (g->h_out) (void)hipHostFree(g->h_out);
+    g->h_out = g->dh_out = nullptr; // the k_decide + copy path
+  }
   h->gpu = g;
   h->max_long_cb = max_long_cb;
   h->dec_type = dec_type;
@@ -361,6 +369,7 @@ void srslte_tdec_free(srslte_tdec_t *h) {
     (void)hipStreamSynchronize(g->e.st);
     if (g->d_in) (void)hipFree(g->d_in);
     if (g->d_out) (void)hipFree(g->d_out);
+    if (g->h_out) (void)hipHostFree(g->h_out);
     g->e.destroy();
     if (g->e.st) (void)hipStreamDestroy(g->e.st);
     delete g;
@@ -394,8 +403,8 @@ uint32_t srslte_tdec_autoimp_get_subblocks(uint32_t long_cb) { return auto_subbl
 // turbodecoder.c:392-406 (AVX2 build)
 uint32_t srslte_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb) { return srsgpu::auto_subblocks_8bit(long_cb); }
 
-// one half-iteration; at the first one the (int16) input of decoder `impl` is uploaded and loaded
-static int tdec_gpu_halfit(srslte_tdec_t *h, const int16_t *input, int impl) {
+// at the first half-iteration of a code block the (int16) input of decoder `impl` is uploaded and loaded
+static int tdec_gpu_upload(srslte_tdec_t *h, const int16_t *input, int impl) {
   auto *g = (TdecGpu *)h->gpu;
   Engine &e = g->e;
   const uint32_t K = h->current_long_cb;
@@ -405,7 +414,13 @@ static int tdec_gpu_halfit(srslte_tdec_t *h, const int16_t *input, int impl) {
     HIPCHK(hipMemcpyAsync(g->d_in, input, len * 2, hipMemcpyHostToDevice, e.st));
     if (e.load(impl, sb, g->d_in, len, K, 1)) return -1;
   }
-  if (e.halfit(h->n_iter, false)) return -1;
+  return 0;
+}
+
+// one half-iteration
+static int tdec_gpu_halfit(srslte_tdec_t *h, const int16_t *input, int impl) {
+  if (tdec_gpu_upload(h, input, impl)) return -1;
+  if (((TdecGpu *)h->gpu)->e.halfit(h->n_iter, false)) return -1;
   h->n_iter++;
   return 0;
 }
@@ -417,6 +432,27 @@ static int tdec_gpu_decide(srslte_tdec_t *h, uint8_t *output) {
   if (e.decide(h->n_iter - 1, g->d_out, K / 8, false)) return -1;
   HIPCHK(hipMemcpyAsync(output, g->d_out, K / 8, hipMemcpyDeviceToHost, e.st));
   HIPCHK(hipStreamSynchronize(e.st));
+  return 0;
+}
+
+// one half-iteration and its decision bytes (the srslte_tdec_iteration protocol): one k_win_spread
+// launch that also writes the bytes into the handle's mapped host buffer when the block allows it
+// (windowed kind, K / nb a multiple of 16), else the half-iteration, k_decide and a copy
+static int tdec_gpu_step(srslte_tdec_t *h, const int16_t *input, int impl, uint8_t *output) {
+  auto *g = (TdecGpu *)h->gpu;
+  Engine &e = g->e;
+  const uint32_t K = h->current_long_cb;
+  if (tdec_gpu_upload(h, input, impl)) return -1;
+  const int r = g->dh_out ? e.halfit_bytes(h->n_iter, g->dh_out, K / 8) : 1;
+  if (r < 0) return -1;
+  if (r == 1) {
+    if (e.halfit(h->n_iter, false)) return -1;
+    h->n_iter++;
+    return tdec_gpu_decide(h, output);
+  }
+  h->n_iter++;
+  HIPCHK(hipStreamSynchronize(e.st));
+  memcpy(output, g->h_out, K / 8);
   return 0;
 }
 
@@ -457,7 +493,7 @@ void srslte_tdec_iteration(srslte_tdec_t *h, int16_t *input, uint8_t *output) {
   if (h && h->gpu && h->current_cbidx >= 0) {
     const int16_t *in = h->n_iter == 0 ? tdec_input16(h, input) : input;
     if (!in) return;
-    if (tdec_gpu_halfit(h, in, h->dec_type) == 0) (void)tdec_gpu_decide(h, output);
+    (void)tdec_gpu_step(h, in, h->dec_type, output);
   }
 }
 
@@ -477,7 +513,7 @@ void srslte_tdec_iteration_8bit(srslte_tdec_t *h, int8_t *input, uint8_t *output
   if (h && h->gpu && h->current_cbidx >= 0) {
     int impl = 0;
     const int16_t *in = tdec_input8(h, input, &impl);
-    if (tdec_gpu_halfit(h, in, impl) == 0) (void)tdec_gpu_decide(h, output);
+    (void)tdec_gpu_step(h, in, impl, output);
   }
 }
 

@@ -84,8 +84,11 @@ hipError_t launch_halfit(int n, int kind, const TdGroup *dg, int ng, int nblocks
 // spread_ok(kind, K, nb): a windowed kind with K / nb a multiple of 16 and at least 48
 int spread_max_pairs();
 bool spread_ok(int kind, int K, int nb);
+// outb (dec only): the decision bytes of every block of the group also written by the same launch,
+// row cb0 + c at outb + (cb0 + c) * out_stride (k_decide's fixed-iteration output)
 hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
-                                const TdArrays &a, const uint8_t *pair_done, hipStream_t st);
+                                const TdArrays &a, const uint8_t *pair_done, hipStream_t st,
+                                uint8_t *outb = nullptr, size_t out_stride = 0);
 // half-iterations n0 .. n0+nh-1 of every group of one windowed kind in one launch (fixed-iteration
 // jobs: no early stop in between); dec: decisions after the last one
 bool halfits_fusable(int kind);

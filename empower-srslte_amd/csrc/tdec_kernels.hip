@@ -1064,6 +1064,10 @@ __global__ __launch_bounds__(128, MODE == 2 ? TD_H0_WAVES : TD_BIDIR_WAVES) void
 // normalisation schedule and same checkpoint values as k_win_bidir, so the output is identical
 // (tests: every batch of one pair goes through here, larger ones through k_win_bidir).
 // Needs L = K / NB a multiple of 16 (no partial chunk) and nc >= 3 (spread_ok).
+// quad_perm DPP move (within each group of 4 lanes)
+template <int CTRL> __device__ __forceinline__ uint32_t dppq(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
 #define TD_SPREAD_THREADS 512
 #define TD_SPREAD_MAX_PAIRS 16 // at most this many pairs per job: k_win_bidir beyond
 
@@ -1072,9 +1076,11 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
                                                                 const s4 *__restrict__ SP0, s2 *__restrict__ XP1,
                                                                 s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                                 const s2 *__restrict__ T, size_t plane,
-                                                                const uint8_t *__restrict__ pair_done) {
+                                                                const uint8_t *__restrict__ pair_done,
+                                                                uint8_t *__restrict__ outb, size_t out_stride) {
   constexpr int CW = 16;
   extern __shared__ s4 spk[]; // checkpoints [slot][chain] x 32 B: alpha 0..nc-1, beta nc..2nc
+  __shared__ uint32_t sdw[6144 / 16]; // the decision words again, for the fused bytes (outb)
   const TdGroup &G = groups[0];
   const int K = G.K, pair = blockIdx.x;
   if (pair_done && pair_done[G.pair0 + pair]) return; // uniform over the workgroup
@@ -1175,7 +1181,149 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
     grp_step<MODE, B8>(c.g[j >> 2], j & 3, x, y, e);
   };
 
-  if (wave == 0) {
+  if (!B8 && wave < 4) {
+    // ---- phase A, 16-bit windows, state-parallel: a quad of lanes per chain and block (wave 0 / 2:
+    // alpha of the pair's block 0 / 1, wave 1 / 3: beta), each lane two states in one packed
+    // register. The trellis is four butterflies: alpha lane r holds (a[2r], a[2r+1]) and forms
+    // (a'[r], a'[r+4]); beta lane r holds (b[r], b[r+4]) and forms (b'[2r], b'[2r+1]). A step is one
+    // add on the lane's pair, one on the swapped pair, one max, and two quad permutes (DPP) plus a
+    // byte permute to bring the next step's pair in — the same saturating sums and maxima as
+    // win_alpha_step / win_beta_step, state by state, so every metric is the reference's.
+    const int role = wave & 1, h = wave >> 1;
+    const int d = (lane >> 2) % NB, r = lane & 3;
+    // per-lane branch metrics: g = (gP, gQ): lane 0 (0, xy), 1 (x, y), 2 (y, x), 3 (xy, 0), the
+    // same table for both recursions (gP added to the lane's pair, gQ to the swapped pair)
+    const uint32_t MX = ((r == 1 || r == 3) ? 0xffffu : 0u) | ((r == 0 || r == 2) ? 0xffff0000u : 0u);
+    const uint32_t MY = ((r == 2 || r == 3) ? 0xffffu : 0u) | ((r == 0 || r == 1) ? 0xffff0000u : 0u);
+    const uint32_t hsel = h ? 0x03020302u : 0x01000100u; // splat of block h's half
+    const uint32_t asel = r < 2 ? 0x05040100u : 0x07060302u, bsel = (r & 1) ? 0x07060302u : 0x05040100u;
+    auto bits = [](s2 v) { return __builtin_bit_cast(uint32_t, v); };
+    auto bfly = [&](uint32_t v, s2 x, s2 y) -> uint32_t { // (P, Q) maxima of the lane's butterfly
+      const uint32_t xx = __builtin_amdgcn_perm(bits(x), bits(x), hsel);
+      const uint32_t yy = __builtin_amdgcn_perm(bits(y), bits(y), hsel);
+      const s2 g = sadd(as_s2(xx & MX), as_s2(yy & MY));
+      const s2 vv = as_s2(v);
+      return bits(smax(sadd(vv, s2{g.x, g.x}), sadd(s2{vv.y, vv.x}, s2{g.y, g.y})));
+    };
+    auto qa = [&](uint32_t &v, s2 x, s2 y) { // alpha: (a'[r], a'[r+4]) -> (a'[2r], a'[2r+1])
+      const uint32_t w = bfly(v, x, y);
+      v = __builtin_amdgcn_perm(dppq<0xDD>(w), dppq<0x88>(w), asel); // quad_perm [1,3,1,3], [0,2,0,2]
+    };
+    auto qb = [&](uint32_t &u, s2 x, s2 y) { // beta: (b'[2r], b'[2r+1]) -> (b'[r], b'[r+4])
+      const uint32_t w = bfly(u, x, y);
+      u = __builtin_amdgcn_perm(dppq<0xFA>(w), dppq<0x50>(w), bsel); // quad_perm [2,2,3,3], [0,0,1,1]
+    };
+    auto qnorm = [&](uint32_t &v) { // win.h:255-258: minus state 0 (lane 0's low half in both layouts)
+      const uint32_t z = __builtin_amdgcn_perm(0u, dppq<0x00>(v), 0x01000100u);
+      v = bits(ssub(as_s2(v), as_s2(z)));
+    };
+    short *ck16 = reinterpret_cast<short *>(spk);
+    auto ck_at = [&](int slot, int s) -> short & { // state s of block h in slot `slot`, chain d
+      return ck16[(slot * NB + d) * 16 + 4 * (s >> 1) + 2 * (s & 1) + h];
+    };
+    const uint32_t NEG = 0xffffu & (uint32_t)(uint16_t)(short)-TD_INF;
+    uint32_t v = NEG | (NEG << 16);
+    Chunk<MODE> c0, c1, c2;
+    if (role == 0) {
+      const int dp = d > 0 ? d - 1 : 0;
+      {
+        Grp<MODE> pg[10];
+        const int gp = (L - TD_OVERLAP) >> 2;
+#pragma unroll
+        for (int u = 0; u < 10; u++) ld_grp(pg[u], gp + u, dp, 0);
+        ld_chunk(c0, 0, d);
+        ld_chunk(c1, 1, d);
+#pragma unroll
+        for (int k = 0; k < TD_OVERLAP; k++) {
+          s2 x, y, e;
+          grp_step<MODE, false>(pg[k >> 2], k & 3, x, y, e);
+          qa(v, x, y);
+          if ((k & 1) == 0 && k != 0) qnorm(v);
+        }
+      }
+      if (d == 0) v = r == 0 ? (NEG << 16) : (NEG | (NEG << 16)); // state 0 = 0 (win.h:496-500)
+      auto fwd_chunk = [&](const Chunk<MODE> &c, int q) {
+        ck_at(q, 2 * r) = (short)(v & 0xffffu);
+        ck_at(q, 2 * r + 1) = (short)(v >> 16);
+#pragma unroll
+        for (int j = 0; j < CW; j++) {
+          s2 x, y, e;
+          cstep(c, j, x, y, e);
+          qa(v, x, y);
+          if ((j & 1) == 0 && (j != 0 || q != 0)) qnorm(v);
+        }
+      };
+      int q = 0;
+      for (; q + 2 < nc; q += 3) {
+        ld_chunk(c2, q + 2, d);
+        fwd_chunk(c0, q);
+        ld_chunk(c0, min(q + 3, nc - 1), d);
+        fwd_chunk(c1, q + 1);
+        ld_chunk(c1, min(q + 4, nc - 1), d);
+        fwd_chunk(c2, q + 2);
+      }
+      if (q < nc) fwd_chunk(c0, q);
+      if (q + 1 < nc) fwd_chunk(c1, q + 1);
+    } else {
+      const int dn = d + 1 < NB ? d + 1 : d;
+      {
+        Grp<MODE> pg[10];
+#pragma unroll
+        for (int u = 0; u < 10; u++) ld_grp(pg[u], u, dn, 0);
+        s2 tv[6];
+#pragma unroll
+        for (int u = 0; u < 6; u++) tv[u] = tl[(MODE == 1 ? 6 : 0) + u];
+        ld_chunk(c0, nc - 1, d);
+        ld_chunk(c1, nc - 2, d);
+#pragma unroll
+        for (int k = TD_OVERLAP - 1; k >= 0; k--) {
+          s2 x, y, e;
+          grp_step<MODE, false>(pg[k >> 2], k & 3, x, y, e);
+          qb(v, x, y);
+          if ((k & 1) == 0 && k != 0) qnorm(v);
+        }
+        if (d == NB - 1) { // the last chain starts from the tail trellis (win.h:350-355)
+          St8 t;
+          win_tail_trellis(tv, 0, t);
+          s2 lo = t.s[0], hi = t.s[4];
+#pragma unroll
+          for (int i = 1; i < 4; i++)
+            if (r == i) {
+              lo = t.s[i];
+              hi = t.s[i + 4];
+            }
+          v = h ? ((uint32_t)(uint16_t)lo.y | ((uint32_t)(uint16_t)hi.y << 16))
+                : ((uint32_t)(uint16_t)lo.x | ((uint32_t)(uint16_t)hi.x << 16));
+        }
+      }
+      auto put_b = [&](int slot) {
+        ck_at(slot, r) = (short)(v & 0xffffu);
+        ck_at(slot, r + 4) = (short)(v >> 16);
+      };
+      put_b(2 * nc); // beta[L]
+      auto bwd_chunk = [&](const Chunk<MODE> &c, int q) { // q >= 1
+#pragma unroll
+        for (int j = CW - 1; j >= 0; j--) {
+          s2 x, y, e;
+          cstep(c, j, x, y, e);
+          qb(v, x, y);
+          if (j == 0) put_b(nc + q);
+          if ((j & 1) == 0) qnorm(v);
+        }
+      };
+      int q = nc - 1;
+      for (; q - 2 >= 1; q -= 3) {
+        ld_chunk(c2, q - 2, d);
+        bwd_chunk(c0, q);
+        ld_chunk(c0, max(q - 3, 1), d);
+        bwd_chunk(c1, q - 1);
+        ld_chunk(c1, max(q - 4, 1), d);
+        bwd_chunk(c2, q - 2);
+      }
+      if (q >= 1) bwd_chunk(c0, q);
+      if (q - 1 >= 1) bwd_chunk(c1, q - 1);
+    }
+  } else if (B8 && wave == 0) {
     // ---- phase A, alpha: win.h:501-506,512-584 prepass over the last 40 steps of chain d-1, then
     // every chunk, the entering state checkpointed
     const int d = lane % NB, dp = d > 0 ? d - 1 : 0;
@@ -1219,7 +1367,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
     }
     if (q < nc) fwd_chunk(c0, q);
     if (q + 1 < nc) fwd_chunk(c1, q + 1);
-  } else if (wave == 1) {
+  } else if (B8 && wave == 1) {
     // ---- phase A, beta: win.h:376-384,386-433 prepass over the first 40 steps of chain d+1 (the
     // last chain from the tail trellis, :350-355), beta[L] and beta[16 q] for q = nc-1..1
     const int d = lane % NB, dn = d + 1 < NB ? d + 1 : d;
@@ -1347,7 +1495,46 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
       for (int i = 0; i < 8; i++) o.s[i] = B8 ? bmask(smax(mb[i], nw[i])) : smax(mb[i], nw[i]);
       nrm_fwd(o, q, j);
     }
-    if (DOUT) D[d * nc + q] = dacc;
+    if (DOUT) {
+      D[d * nc + q] = dacc;
+      sdw[d * nc + q] = dacc;
+    }
+  }
+  // ---- the decision bytes of the pair's blocks (k_decide's fixed-iteration output, fused: the drop-in
+  // srslte_tdec_iteration's one launch per call), MSB first (turbodecoder.c:353-360). With L a multiple
+  // of 16 the chain-major index of natural position p after DEC1 is p itself; after DEC2 dmap[p].
+  if (DOUT && outb) {
+    __syncthreads();
+    const int nwd = K / 32; // K is a multiple of 16 NB >= 128: whole 32-bit words
+    const gptr_t<uint16_t> dmap = gptr(G.dmap);
+    const bool w32 = ((uintptr_t)outb & 3u) == 0 && (out_stride & 3u) == 0;
+    for (int i = tid; i < 2 * nwd; i += TD_SPREAD_THREADS) {
+      const int h = i >= nwd, w = i - h * nwd, cb = 2 * pair + h;
+      if (cb >= G.ncb) continue;
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int p = 32 * w + 8 * j;
+        uint32_t v = 0;
+        if (MODE != 1) {
+          v = (sdw[p >> 4] >> (16 * h + (p & 15))) & 0xffu;
+        } else {
+#pragma unroll
+          for (int b = 0; b < 8; b++) {
+            const int c = dmap[p + b];
+            v |= ((sdw[c >> 4] >> ((c & 15) + 16 * h)) & 1u) << b;
+          }
+        }
+        word |= (__builtin_bitreverse32(v) >> 24) << (8 * j);
+      }
+      uint8_t *row = outb + (size_t)(G.cb0 + cb) * out_stride;
+      if (w32) {
+        reinterpret_cast<uint32_t *>(row)[w] = word;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) row[4 * w + j] = (uint8_t)(word >> (8 * j));
+      }
+    }
   }
 }
 
@@ -3166,15 +3353,16 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
 // k_win_spread launchers, one per windowed kind (in the part that holds the kind)
 template <int KIND>
 hipError_t spread_part(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec, const TdArrays &a,
-                       const uint8_t *pair_done, hipStream_t st);
+                       const uint8_t *pair_done, uint8_t *outb, size_t out_stride, hipStream_t st);
 #define SPREAD1(nb, div, m, dout, b8)                                                              \
   hipLaunchKernelGGL((k_win_spread<nb, div, m, dout, b8>), dim3(npairs), dim3(TD_SPREAD_THREADS), lds, \
                      st, dg, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,          \
-                     (const s2 *)a.T, a.plane, pair_done)
+                     (const s2 *)a.T, a.plane, pair_done, outb, out_stride)
 #define SPREAD(KIND, nb, div, b8)                                                                  \
   template <>                                                                                      \
   hipError_t spread_part<KIND>(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec,      \
-                               const TdArrays &a, const uint8_t *pair_done, hipStream_t st) {      \
+                               const TdArrays &a, const uint8_t *pair_done, uint8_t *outb,         \
+                               size_t out_stride, hipStream_t st) {                               \
     if (mode == 1) {                                                                               \
       if (dec) SPREAD1(nb, div, 1, true, b8); else SPREAD1(nb, div, 1, false, b8);                 \
     } else if (mode == 2) {                                                                        \
@@ -3249,18 +3437,20 @@ bool spread_ok(int kind, int K, int nb) {
 }
 
 hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
-                                const TdArrays &arr, const uint8_t *pair_done, hipStream_t st) {
+                                const TdArrays &arr, const uint8_t *pair_done, hipStream_t st,
+                                uint8_t *outb, size_t out_stride) {
   if (npairs <= 0) return hipSuccess;
-  if (!spread_ok(kind, K, nb) || npairs > TD_SPREAD_MAX_PAIRS) return hipErrorInvalidValue;
+  if (!spread_ok(kind, K, nb) || npairs > TD_SPREAD_MAX_PAIRS || K > 6144 || (outb && !dec))
+    return hipErrorInvalidValue;
   const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
   TdArrays a = arr;
   if (!dec) a.D = nullptr;
   const size_t lds = (size_t)(2 * (K / nb / TD_BIDIR_CW) + 1) * nb * 32;
   switch (kind) {
-  case TD_KIND_W16: return spread_part<TD_KIND_W16>(mode, dg, npairs, lds, dec, a, pair_done, st);
-  case TD_KIND_W8: return spread_part<TD_KIND_W8>(mode, dg, npairs, lds, dec, a, pair_done, st);
-  case TD_KIND_B16: return spread_part<TD_KIND_B16>(mode, dg, npairs, lds, dec, a, pair_done, st);
-  case TD_KIND_B32: return spread_part<TD_KIND_B32>(mode, dg, npairs, lds, dec, a, pair_done, st);
+  case TD_KIND_W16: return spread_part<TD_KIND_W16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
+  case TD_KIND_W8: return spread_part<TD_KIND_W8>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
+  case TD_KIND_B16: return spread_part<TD_KIND_B16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
+  case TD_KIND_B32: return spread_part<TD_KIND_B32>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
   default: return hipErrorInvalidValue;
   }
 }
