@@ -86,6 +86,7 @@ struct TdecEngine {
   // the hybrid schedule's list of pairs still running after the first half-iteration (TdEs::run_list;
   // run_cnt per group at its pair0, zeroed by k_pair_done). SRSGPU_ES_COMPACT=0: every pair (A/B)
   uint32_t *run_list = nullptr, *run_cnt = nullptr;
+  uint32_t *spread_cnt = nullptr; // k_win_spread's per-pair workgroup arrival counters (zero between launches)
   uint8_t *cb_done = nullptr, *pair_done = nullptr, *cb_ok = nullptr;
   uint32_t *noi = nullptr;
   int16_t *in_stage = nullptr; // host-pointer API staging
@@ -171,6 +172,8 @@ struct TdecEngine {
     HIPCHK(hipMalloc(&run_list, cap_pairs * 4));
     HIPCHK(hipMalloc(&run_cnt, cap_pairs * 4));
     HIPCHK(hipMemset(run_cnt, 0, cap_pairs * 4));
+    HIPCHK(hipMalloc(&spread_cnt, (size_t)spread_max_pairs() * 4));
+    HIPCHK(hipMemset(spread_cnt, 0, (size_t)spread_max_pairs() * 4));
     return 0;
   }
 
@@ -179,7 +182,8 @@ struct TdecEngine {
     for (void *p : {SP0, XP1, A, D, T, scratch, (void *)d_groups})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)cb_done, (void *)cb_ok, (void *)pair_done, (void *)noi, (void *)in_stage,
-                    (void *)out_stage, (void *)Dfz, (void *)cb_end, (void *)run_list, (void *)run_cnt})
+                    (void *)out_stage, (void *)Dfz, (void *)cb_end, (void *)run_list, (void *)run_cnt,
+                    (void *)spread_cnt})
       if (p) (void)hipFree(p);
     if (aux) (void)hipStreamSynchronize(aux);
     for (hipEvent_t e : {ev_fork, ev_join, ev_split})
@@ -532,7 +536,8 @@ struct TdecEngine {
 
   // half-iteration n of a one-group job that k_win_spread takes, with the decision bytes of its
   // blocks written to outb by the same launch (the drop-in's one launch per call); 1: not this job
-  int halfit_bytes(int n, uint8_t *outb, size_t out_stride) {
+  // flag (optional, host-mapped): seq stored there by the launch once the bytes are written
+  int halfit_bytes(int n, uint8_t *outb, size_t out_stride, uint32_t *flag = nullptr, uint32_t seq = 0) {
     if (groups.size() != 1) return 1;
     int k = 0;
     while (k < TD_NKIND && kind_g0[k + 1] - kind_g0[k] != 1) k++;
@@ -540,7 +545,11 @@ struct TdecEngine {
     last_n = n;
     const TdGroup &f = groups[0];
     ProfScope ps("k_win_spread", st);
-    HIPCHK(launch_halfit_spread(n, k, d_groups, f.npairs, f.K, f.nb, true, arrays(), nullptr, st, outb, out_stride));
+    SpreadOut so;
+    so.cnt = spread_cnt;
+    so.flag = flag;
+    so.seq = seq;
+    HIPCHK(launch_halfit_spread(n, k, d_groups, f.npairs, f.K, f.nb, true, arrays(), nullptr, st, outb, out_stride, so));
     return 0;
   }
 

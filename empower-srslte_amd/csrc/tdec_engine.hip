@@ -8,6 +8,7 @@
 //   decide(n)     hard decision after half-iteration n (+ CRC and early-stop flags when asked,
 //                 sch.c:361-391)
 #include <hip/hip_runtime.h>
+#include <chrono>
 
 #include <map>
 #include <mutex>
@@ -318,6 +319,8 @@ struct TdecGpu {
   // decision bytes written by the half-iteration's own launch (k_win_spread) into mapped, coherent
   // host memory: no k_decide launch and no copy per srslte_tdec_iteration call (null: not available)
   uint8_t *h_out = nullptr, *dh_out = nullptr;
+  size_t flag_off = 0; // the launch's completion word in the same buffer (polled, SRSGPU_SPREAD_POLL)
+  uint32_t seq = 0;
 };
 
 int srslte_tdec_init(srslte_tdec_t *h, uint32_t max_long_cb) {
@@ -350,7 +353,8 @@ int srslte_tdec_init_manual(srslte_tdec_t *h, uint32_t max_long_cb, srslte_tdec_
     delete g;
     return -1;
   }
-  if (hipHostMalloc((void **)&g->h_out, max_long_cb / 8 + 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  g->flag_off = (max_long_cb / 8 + 15) & ~(size_t)15;
+  if (hipHostMalloc((void **)&g->h_out, g->flag_off + 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&g->dh_out, g->h_out, 0) != hipSuccess) {
     if (g->h_out) (void)hipHostFree(g->h_out);
     g->h_out = g->dh_out = nullptr; // the k_decide + copy path
@@ -443,7 +447,12 @@ static int tdec_gpu_step(srslte_tdec_t *h, const int16_t *input, int impl, uint8
   Engine &e = g->e;
   const uint32_t K = h->current_long_cb;
   if (tdec_gpu_upload(h, input, impl)) return -1;
-  const int r = g->dh_out ? e.halfit_bytes(h->n_iter, g->dh_out, K / 8) : 1;
+  const bool poll = srsgpu::knobs().spread_poll;
+  const uint32_t seq = ++g->seq ? g->seq : ++g->seq; // never 0
+  volatile uint32_t *hflag = (volatile uint32_t *)(g->h_out + g->flag_off);
+  const int r = g->dh_out ? e.halfit_bytes(h->n_iter, g->dh_out, K / 8,
+                                           poll ? (uint32_t *)(g->dh_out + g->flag_off) : nullptr, seq)
+                          : 1;
   if (r < 0) return -1;
   if (r == 1) {
     if (e.halfit(h->n_iter, false)) return -1;
@@ -451,7 +460,14 @@ static int tdec_gpu_step(srslte_tdec_t *h, const int16_t *input, int impl, uint8
     return tdec_gpu_decide(h, output);
   }
   h->n_iter++;
-  HIPCHK(hipStreamSynchronize(e.st));
+  bool seen = false;
+  if (poll) { // the launch stores seq after the bytes (system-scope release); bounded spin, then the stream
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!(seen = __atomic_load_n(hflag, __ATOMIC_ACQUIRE) == seq) &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20)) {
+    }
+  }
+  if (!seen) HIPCHK(hipStreamSynchronize(e.st));
   memcpy(output, g->h_out, K / 8);
   return 0;
 }

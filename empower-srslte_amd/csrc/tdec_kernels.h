@@ -86,9 +86,15 @@ int spread_max_pairs();
 bool spread_ok(int kind, int K, int nb);
 // outb (dec only): the decision bytes of every block of the group also written by the same launch,
 // row cb0 + c at outb + (cb0 + c) * out_stride (k_decide's fixed-iteration output)
+// cnt: per-pair arrival counters of the pair's workgroups (zeroed, left zeroed; needed with outb);
+// flag (optional, host-mapped): seq is stored there once the bytes are written
+struct SpreadOut {
+  uint32_t *cnt = nullptr, *flag = nullptr;
+  uint32_t seq = 0;
+};
 hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
                                 const TdArrays &a, const uint8_t *pair_done, hipStream_t st,
-                                uint8_t *outb = nullptr, size_t out_stride = 0);
+                                uint8_t *outb = nullptr, size_t out_stride = 0, const SpreadOut &so = SpreadOut{});
 // half-iterations n0 .. n0+nh-1 of every group of one windowed kind in one launch (fixed-iteration
 // jobs: no early stop in between); dec: decisions after the last one
 bool halfits_fusable(int kind);

@@ -1068,7 +1068,20 @@ __global__ __launch_bounds__(128, MODE == 2 ? TD_H0_WAVES : TD_BIDIR_WAVES) void
 template <int CTRL> __device__ __forceinline__ uint32_t dppq(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
+#ifdef TD_TIMING
+#define SP_T(k)                                                                                    \
+  do {                                                                                             \
+    if (lane == 0 && blockIdx.x < 1024) td_times[blockIdx.x * 8 + (k)] = clock64();                \
+  } while (0)
+#else
+#define SP_T(k)
+#endif
 #define TD_SPREAD_THREADS 512
+#ifndef TD_SPREAD_SPLIT
+#define TD_SPREAD_SPLIT 1 // workgroups per pair: phase A on each, phase B's tasks shared (r06_s30: 2 was
+                          // slower: the arrival counter, fences and decision-word reload before the bytes
+                          // cost more than the halved phase B)
+#endif
 #define TD_SPREAD_MAX_PAIRS 16 // at most this many pairs per job: k_win_bidir beyond
 
 template <int NB, int DIV, int MODE, bool DOUT, bool B8>
@@ -1077,15 +1090,18 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
                                                                 s2 *__restrict__ Aarr, uint32_t *__restrict__ Darr,
                                                                 const s2 *__restrict__ T, size_t plane,
                                                                 const uint8_t *__restrict__ pair_done,
-                                                                uint8_t *__restrict__ outb, size_t out_stride) {
+                                                                uint8_t *__restrict__ outb, size_t out_stride,
+                                                                uint32_t *__restrict__ cnt, uint32_t *__restrict__ flag,
+                                                                uint32_t seq) {
   constexpr int CW = 16;
   extern __shared__ s4 spk[]; // checkpoints [slot][chain] x 32 B: alpha 0..nc-1, beta nc..2nc
   __shared__ uint32_t sdw[6144 / 16]; // the decision words again, for the fused bytes (outb)
   const TdGroup &G = groups[0];
-  const int K = G.K, pair = blockIdx.x;
+  const int K = G.K, pair = blockIdx.x / TD_SPREAD_SPLIT, part = blockIdx.x % TD_SPREAD_SPLIT;
   if (pair_done && pair_done[G.pair0 + pair]) return; // uniform over the workgroup
   const int L = K / NB, nc = L / CW;
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if (wave == 0) SP_T(0);
   const int pe = t4_pair_elems(K, NB);
   const size_t base = (size_t)G.elem0 + (size_t)pair * pe;
   WinRes R;
@@ -1173,6 +1189,9 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
     }
   };
   auto ld_chunk = [&](Chunk<MODE> &c, int q, int dd) { // phase A: q wave-uniform
+#ifdef TD_EXP_SPREAD_L2
+    q &= 1; // timing experiment only (wrong results): phase A's chunk loads from two cache-resident chunks
+#endif
 #pragma unroll
     for (int u = 0; u < 4; u++) ld_grp(c.g[u], 4 * q + u, dd, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1193,15 +1212,15 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
     const int d = (lane >> 2) % NB, r = lane & 3;
     // per-lane branch metrics: g = (gP, gQ): lane 0 (0, xy), 1 (x, y), 2 (y, x), 3 (xy, 0), the
     // same table for both recursions (gP added to the lane's pair, gQ to the swapped pair)
-    const uint32_t MX = ((r == 1 || r == 3) ? 0xffffu : 0u) | ((r == 0 || r == 2) ? 0xffff0000u : 0u);
-    const uint32_t MY = ((r == 2 || r == 3) ? 0xffffu : 0u) | ((r == 0 || r == 1) ? 0xffff0000u : 0u);
-    const uint32_t hsel = h ? 0x03020302u : 0x01000100u; // splat of block h's half
+    // as byte selections of block h's x / y (or zero: selector 0x0C) into the two halves
+    const uint32_t hb = h ? 0x0302u : 0x0100u, zb = 0x0C0Cu;
+    const uint32_t SX = ((r == 1 || r == 3) ? hb : zb) | (((r == 0 || r == 2) ? hb : zb) << 16);
+    const uint32_t SY = ((r == 2 || r == 3) ? hb : zb) | (((r == 0 || r == 1) ? hb : zb) << 16);
     const uint32_t asel = r < 2 ? 0x05040100u : 0x07060302u, bsel = (r & 1) ? 0x07060302u : 0x05040100u;
     auto bits = [](s2 v) { return __builtin_bit_cast(uint32_t, v); };
     auto bfly = [&](uint32_t v, s2 x, s2 y) -> uint32_t { // (P, Q) maxima of the lane's butterfly
-      const uint32_t xx = __builtin_amdgcn_perm(bits(x), bits(x), hsel);
-      const uint32_t yy = __builtin_amdgcn_perm(bits(y), bits(y), hsel);
-      const s2 g = sadd(as_s2(xx & MX), as_s2(yy & MY));
+      const s2 g = sadd(as_s2(__builtin_amdgcn_perm(bits(x), bits(x), SX)),
+                        as_s2(__builtin_amdgcn_perm(bits(y), bits(y), SY)));
       const s2 vv = as_s2(v);
       return bits(smax(sadd(vv, s2{g.x, g.x}), sadd(s2{vv.y, vv.x}, s2{g.y, g.y})));
     };
@@ -1214,8 +1233,8 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
       u = __builtin_amdgcn_perm(dppq<0xFA>(w), dppq<0x50>(w), bsel); // quad_perm [2,2,3,3], [0,0,1,1]
     };
     auto qnorm = [&](uint32_t &v) { // win.h:255-258: minus state 0 (lane 0's low half in both layouts)
-      const uint32_t z = __builtin_amdgcn_perm(0u, dppq<0x00>(v), 0x01000100u);
-      v = bits(ssub(as_s2(v), as_s2(z)));
+      const s2 z = as_s2(dppq<0x00>(v));
+      v = bits(ssub(as_s2(v), s2{z.x, z.x}));
     };
     short *ck16 = reinterpret_cast<short *>(spk);
     auto ck_at = [&](int slot, int s) -> short & { // state s of block h in slot `slot`, chain d
@@ -1241,6 +1260,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
           if ((k & 1) == 0 && k != 0) qnorm(v);
         }
       }
+      if (wave == 0) SP_T(1);
       if (d == 0) v = r == 0 ? (NEG << 16) : (NEG | (NEG << 16)); // state 0 = 0 (win.h:496-500)
       auto fwd_chunk = [&](const Chunk<MODE> &c, int q) {
         ck_at(q, 2 * r) = (short)(v & 0xffffu);
@@ -1264,6 +1284,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
       }
       if (q < nc) fwd_chunk(c0, q);
       if (q + 1 < nc) fwd_chunk(c1, q + 1);
+      if (wave == 0) SP_T(2);
     } else {
       const int dn = d + 1 < NB ? d + 1 : d;
       {
@@ -1322,6 +1343,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
       }
       if (q >= 1) bwd_chunk(c0, q);
       if (q - 1 >= 1) bwd_chunk(c1, q - 1);
+      if (wave == 1) SP_T(3);
     }
   } else if (B8 && wave == 0) {
     // ---- phase A, alpha: win.h:501-506,512-584 prepass over the last 40 steps of chain d-1, then
@@ -1420,21 +1442,34 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
     if (q >= 1) bwd_chunk(c0, q);
     if (q - 1 >= 1) bwd_chunk(c1, q - 1);
   }
-  __syncthreads();
-
-  // ---- phase B: task t = (chunk q, chain d), chains of one chunk on consecutive lanes (coalesced
-  // T4 loads and table reads; the scatter stores of one step land on NB consecutive elements)
-  for (int t = tid; t < NB * nc; t += TD_SPREAD_THREADS) {
-    const int q = t / NB, d = t % NB;
-    Chunk<MODE> c;
-    {
-      const uint32_t lo = 16u * NB * 4u * (uint32_t)q; // 4 T4 groups per chunk, 16 B per group and chain
+  // ---- phase B's inputs, loaded before the barrier: waves 4.. (idle in phase A) load theirs while
+  // phase A runs. The pair's TD_SPREAD_SPLIT workgroups (on as many CUs) each ran phase A and take
+  // their share of the tasks, at most one per thread (launch_halfit_spread checks K / 16).
+  const int t_lo = part * NB * nc / TD_SPREAD_SPLIT, t_hi = (part + 1) * NB * nc / TD_SPREAD_SPLIT;
+  const int t = t_lo + tid, q = t / NB, d = t % NB;
+  const bool has = t < t_hi;
+  Chunk<MODE> c;
+  if (has) {
+    const uint32_t lo = 16u * NB * 4u * (uint32_t)q; // 4 T4 groups per chunk, 16 B per group and chain
 #pragma unroll
-      for (int u = 0; u < 4; u++) ld_grp(c.g[u], u, d, lo);
-      const uint32_t vo = 32u * (uint32_t)d + 32u * NB * (uint32_t)q;
-      c.t[0] = bld128(R.tb, vo, 0);
-      c.t[1] = bld128(R.tb, vo, 16);
-    }
+    for (int u = 0; u < 4; u++) ld_grp(c.g[u], u, d, lo);
+    const uint32_t vo = 32u * (uint32_t)d + 32u * NB * (uint32_t)q;
+    c.t[0] = bld128(R.tb, vo, 0);
+    c.t[1] = bld128(R.tb, vo, 16);
+  }
+  __shared__ uint16_t sdm[6144]; // dmap, for the fused bytes after DEC2 (staged by the idle waves)
+  if (MODE == 1 && DOUT && outb && wave >= 4) {
+    const gptr_t<uint32_t> dm32 = gptr((const uint32_t *)G.dmap);
+    for (int i = tid - 256; i < K / 2; i += TD_SPREAD_THREADS - 256)
+      reinterpret_cast<uint32_t *>(sdm)[i] = dm32[i];
+  }
+  __syncthreads();
+  if (wave == 0) SP_T(4);
+#ifdef TD_EXP_SPREAD_AONLY
+  if (K > 0) return; // timing experiment only (wrong results): phase A alone
+#endif
+
+  if (has) {
     // betas of the chunk (win_bidir_body's `betas` with n = CW): bst[j] = beta[16 q + 1 + j]
     St8 run, bst[CW];
     ck_get(nc + q + 1, d, run); // beta[16 (q + 1)] before normalisation (beta[L] for the top chunk)
@@ -1503,10 +1538,22 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
   // ---- the decision bytes of the pair's blocks (k_decide's fixed-iteration output, fused: the drop-in
   // srslte_tdec_iteration's one launch per call), MSB first (turbodecoder.c:353-360). With L a multiple
   // of 16 the chain-major index of natural position p after DEC1 is p itself; after DEC2 dmap[p].
+  if (wave == 0) SP_T(5);
   if (DOUT && outb) {
+    if (TD_SPREAD_SPLIT > 1) { // the last of the pair's workgroups to finish writes the bytes
+      __shared__ int last;
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) last = atomicAdd(&cnt[pair], 1u) == TD_SPREAD_SPLIT - 1;
+      __syncthreads();
+      if (!last) return;
+      if (tid == 0) cnt[pair] = 0; // for the next launch
+      __threadfence();
+      for (int i = tid; i < NB * nc; i += TD_SPREAD_THREADS)
+        sdw[i] = __hip_atomic_load(&D[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __syncthreads();
     const int nwd = K / 32; // K is a multiple of 16 NB >= 128: whole 32-bit words
-    const gptr_t<uint16_t> dmap = gptr(G.dmap);
     const bool w32 = ((uintptr_t)outb & 3u) == 0 && (out_stride & 3u) == 0;
     for (int i = tid; i < 2 * nwd; i += TD_SPREAD_THREADS) {
       const int h = i >= nwd, w = i - h * nwd, cb = 2 * pair + h;
@@ -1521,7 +1568,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         } else {
 #pragma unroll
           for (int b = 0; b < 8; b++) {
-            const int c = dmap[p + b];
+            const int c = sdm[p + b];
             v |= ((sdw[c >> 4] >> ((c & 15) + 16 * h)) & 1u) << b;
           }
         }
@@ -1535,6 +1582,12 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         for (int j = 0; j < 4; j++) row[4 * w + j] = (uint8_t)(word >> (8 * j));
       }
     }
+    if (flag) { // host-mapped completion word: the caller polls it instead of synchronising the stream
+      __threadfence_system();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (wave == 0) SP_T(6);
   }
 }
 
@@ -3353,16 +3406,18 @@ hipError_t halfits_es_part(const TdGroup *dg, int ng, int nblocks, size_t lds, c
 // k_win_spread launchers, one per windowed kind (in the part that holds the kind)
 template <int KIND>
 hipError_t spread_part(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec, const TdArrays &a,
-                       const uint8_t *pair_done, uint8_t *outb, size_t out_stride, hipStream_t st);
+                       const uint8_t *pair_done, uint8_t *outb, size_t out_stride, const SpreadOut &so,
+                       hipStream_t st);
 #define SPREAD1(nb, div, m, dout, b8)                                                              \
-  hipLaunchKernelGGL((k_win_spread<nb, div, m, dout, b8>), dim3(npairs), dim3(TD_SPREAD_THREADS), lds, \
-                     st, dg, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, (uint32_t *)a.D,          \
-                     (const s2 *)a.T, a.plane, pair_done, outb, out_stride)
+  hipLaunchKernelGGL((k_win_spread<nb, div, m, dout, b8>), dim3(npairs * TD_SPREAD_SPLIT),           \
+                     dim3(TD_SPREAD_THREADS), lds, st, dg, (const s4 *)a.SP0, (s2 *)a.XP1, (s2 *)a.A, \
+                     (uint32_t *)a.D, (const s2 *)a.T, a.plane, pair_done, outb, out_stride, so.cnt, \
+                     so.flag, so.seq)
 #define SPREAD(KIND, nb, div, b8)                                                                  \
   template <>                                                                                      \
   hipError_t spread_part<KIND>(int mode, const TdGroup *dg, int npairs, size_t lds, bool dec,      \
                                const TdArrays &a, const uint8_t *pair_done, uint8_t *outb,         \
-                               size_t out_stride, hipStream_t st) {                               \
+                               size_t out_stride, const SpreadOut &so, hipStream_t st) {          \
     if (mode == 1) {                                                                               \
       if (dec) SPREAD1(nb, div, 1, true, b8); else SPREAD1(nb, div, 1, false, b8);                 \
     } else if (mode == 2) {                                                                        \
@@ -3438,19 +3493,20 @@ bool spread_ok(int kind, int K, int nb) {
 
 hipError_t launch_halfit_spread(int n, int kind, const TdGroup *dg, int npairs, int K, int nb, bool dec,
                                 const TdArrays &arr, const uint8_t *pair_done, hipStream_t st,
-                                uint8_t *outb, size_t out_stride) {
+                                uint8_t *outb, size_t out_stride, const SpreadOut &so) {
   if (npairs <= 0) return hipSuccess;
-  if (!spread_ok(kind, K, nb) || npairs > TD_SPREAD_MAX_PAIRS || K > 6144 || (outb && !dec))
+  if (!spread_ok(kind, K, nb) || npairs > TD_SPREAD_MAX_PAIRS || K > 6144 ||
+      K / TD_BIDIR_CW > TD_SPREAD_THREADS * TD_SPREAD_SPLIT || (outb && (!dec || !so.cnt)))
     return hipErrorInvalidValue;
   const int mode = (n & 1) ? 1 : (n == 0 ? 2 : 0);
   TdArrays a = arr;
   if (!dec) a.D = nullptr;
   const size_t lds = (size_t)(2 * (K / nb / TD_BIDIR_CW) + 1) * nb * 32;
   switch (kind) {
-  case TD_KIND_W16: return spread_part<TD_KIND_W16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
-  case TD_KIND_W8: return spread_part<TD_KIND_W8>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
-  case TD_KIND_B16: return spread_part<TD_KIND_B16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
-  case TD_KIND_B32: return spread_part<TD_KIND_B32>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, st);
+  case TD_KIND_W16: return spread_part<TD_KIND_W16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, so, st);
+  case TD_KIND_W8: return spread_part<TD_KIND_W8>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, so, st);
+  case TD_KIND_B16: return spread_part<TD_KIND_B16>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, so, st);
+  case TD_KIND_B32: return spread_part<TD_KIND_B32>(mode, dg, npairs, lds, dec, a, pair_done, outb, out_stride, so, st);
   default: return hipErrorInvalidValue;
   }
 }

@@ -40,6 +40,8 @@ struct Knobs {
   bool spread;       // SRSGPU_SPREAD (default 1): per-half-iteration launches of a few pairs run as
                      // k_win_spread (one pair per workgroup, both recursions whole, then every chunk
                      // in parallel): the drop-in srslte_tdec_iteration's latency
+  bool spread_poll;  // SRSGPU_SPREAD_POLL (default 1): the drop-in waits for k_win_spread's host-mapped
+                     // completion word instead of synchronising the stream
 };
 
 inline int env_prio(const char *name, int dflt) {
@@ -72,6 +74,8 @@ inline const Knobs *knobs_from_env() {
     k->split_early = !(se && se[0] == '0');
     const char *sp = getenv("SRSGPU_SPREAD");
     k->spread = !(sp && sp[0] == '0');
+    const char *spp = getenv("SRSGPU_SPREAD_POLL");
+    k->spread_poll = !(spp && spp[0] == '0');
   }
   return k;
 }

@@ -69,24 +69,28 @@ def test_spread_equals_bidir(s, oracle, impl, K, sb, n):
                 assert (st[i][0] == rst[i][0]).all() and (st[i][1] == rst[i][1]).all(), (impl, K, nh, i)
 
 
-def test_spread_dropin_matches(s, oracle):
-    """the drop-in protocol (one srslte_tdec_iteration per half-iteration, k_win_spread each) against
-    the oracle's decisions after every half-iteration, with SRSGPU_SPREAD on and off"""
-    K = 6144
-    _, llr = make_cb(K, 1.0, 4242, oracle)
-    ref = oracle.tdec_run(AUTO, 0, llr, K, 8)[0]
-    for spread in (True, False):
-        os.environ["SRSGPU_SPREAD"] = "1" if spread else "0"
-        s.knobs_reload()
-        try:
-            d = s.Tdec(K)
-            d.force_not_sb()
+@pytest.mark.parametrize("spread,poll", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_spread_dropin_matches(s, oracle, spread, poll):
+    """the drop-in protocol (one srslte_tdec_iteration per half-iteration: one k_win_spread launch
+    that also writes the decision bytes, its two workgroups per pair meeting on an arrival counter,
+    and the host polling the launch's completion word) against the oracle's decisions after every
+    half-iteration, several code blocks in a row on one handle; SRSGPU_SPREAD_POLL=0 synchronises the
+    stream instead, SRSGPU_SPREAD=0 takes k_win_bidir + k_decide"""
+    os.environ["SRSGPU_SPREAD"], os.environ["SRSGPU_SPREAD_POLL"] = spread, poll
+    s.knobs_reload()
+    try:
+        d = s.Tdec(6144)
+        d.force_not_sb()
+        for i, K in enumerate((6144, 4096, 6144, 1024)):
+            _, llr = make_cb(K, 1.0 + 0.3 * i, 4242 + i, oracle)
+            ref = oracle.tdec_run(AUTO, 0, llr, K, 8)[0]
             assert d.new_cb(K) == 0
             out = np.zeros(K // 8, np.uint8)
             for h in range(8):
                 d.iteration(llr, out)
-                assert (out == ref[h]).all(), (spread, h)
-            d.free()
-        finally:
-            os.environ.pop("SRSGPU_SPREAD", None)
-            s.knobs_reload()
+                assert (out == ref[h]).all(), (spread, poll, K, h)
+        d.free()
+    finally:
+        os.environ.pop("SRSGPU_SPREAD", None)
+        os.environ.pop("SRSGPU_SPREAD_POLL", None)
+        s.knobs_reload()
