@@ -1224,17 +1224,19 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
       const s2 vv = as_s2(v);
       return bits(smax(sadd(vv, s2{g.x, g.x}), sadd(s2{vv.y, vv.x}, s2{g.y, g.y})));
     };
-    auto qa = [&](uint32_t &v, s2 x, s2 y) { // alpha: (a'[r], a'[r+4]) -> (a'[2r], a'[2r+1])
+    // nrm: the step's normalisation (win.h:255-258: minus the new state 0, which is lane 0's low
+    // half of the butterfly output in both layouts), its broadcast beside the redistribution
+    auto qa = [&](uint32_t &v, s2 x, s2 y, bool nrm) { // alpha: (a'[r], a'[r+4]) -> (a'[2r], a'[2r+1])
       const uint32_t w = bfly(v, x, y);
+      const s2 z = as_s2(dppq<0x00>(w));
       v = __builtin_amdgcn_perm(dppq<0xDD>(w), dppq<0x88>(w), asel); // quad_perm [1,3,1,3], [0,2,0,2]
+      if (nrm) v = bits(ssub(as_s2(v), s2{z.x, z.x}));
     };
-    auto qb = [&](uint32_t &u, s2 x, s2 y) { // beta: (b'[2r], b'[2r+1]) -> (b'[r], b'[r+4])
+    auto qb = [&](uint32_t &u, s2 x, s2 y, bool nrm) { // beta: (b'[2r], b'[2r+1]) -> (b'[r], b'[r+4])
       const uint32_t w = bfly(u, x, y);
+      const s2 z = as_s2(dppq<0x00>(w));
       u = __builtin_amdgcn_perm(dppq<0xFA>(w), dppq<0x50>(w), bsel); // quad_perm [2,2,3,3], [0,0,1,1]
-    };
-    auto qnorm = [&](uint32_t &v) { // win.h:255-258: minus state 0 (lane 0's low half in both layouts)
-      const s2 z = as_s2(dppq<0x00>(v));
-      v = bits(ssub(as_s2(v), s2{z.x, z.x}));
+      if (nrm) u = bits(ssub(as_s2(u), s2{z.x, z.x}));
     };
     short *ck16 = reinterpret_cast<short *>(spk);
     auto ck_at = [&](int slot, int s) -> short & { // state s of block h in slot `slot`, chain d
@@ -1256,8 +1258,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         for (int k = 0; k < TD_OVERLAP; k++) {
           s2 x, y, e;
           grp_step<MODE, false>(pg[k >> 2], k & 3, x, y, e);
-          qa(v, x, y);
-          if ((k & 1) == 0 && k != 0) qnorm(v);
+          qa(v, x, y, (k & 1) == 0 && k != 0);
         }
       }
       if (wave == 0) SP_T(1);
@@ -1269,8 +1270,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         for (int j = 0; j < CW; j++) {
           s2 x, y, e;
           cstep(c, j, x, y, e);
-          qa(v, x, y);
-          if ((j & 1) == 0 && (j != 0 || q != 0)) qnorm(v);
+          qa(v, x, y, (j & 1) == 0 && (j != 0 || q != 0));
         }
       };
       int q = 0;
@@ -1300,8 +1300,7 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         for (int k = TD_OVERLAP - 1; k >= 0; k--) {
           s2 x, y, e;
           grp_step<MODE, false>(pg[k >> 2], k & 3, x, y, e);
-          qb(v, x, y);
-          if ((k & 1) == 0 && k != 0) qnorm(v);
+          qb(v, x, y, (k & 1) == 0 && k != 0);
         }
         if (d == NB - 1) { // the last chain starts from the tail trellis (win.h:350-355)
           St8 t;
@@ -1327,9 +1326,13 @@ __global__ __launch_bounds__(TD_SPREAD_THREADS) void k_win_spread(const TdGroup 
         for (int j = CW - 1; j >= 0; j--) {
           s2 x, y, e;
           cstep(c, j, x, y, e);
-          qb(v, x, y);
-          if (j == 0) put_b(nc + q);
-          if ((j & 1) == 0) qnorm(v);
+          if (j == 0) { // the checkpoint is beta[16 q] before its normalisation
+            qb(v, x, y, false);
+            put_b(nc + q);
+            v = bits(ssub(as_s2(v), s2{as_s2(dppq<0x00>(v)).x, as_s2(dppq<0x00>(v)).x}));
+          } else {
+            qb(v, x, y, (j & 1) == 0);
+          }
         }
       };
       int q = nc - 1;
